@@ -1,0 +1,118 @@
+"""ctypes binding of include/cad/cad.h (libcad_hip.so, built in-tree for gfx950).
+
+This is the ONLY way the Python host reaches device code: there is no CPU fallback.  If the shared
+library is missing the import fails loudly (run `make -C <package dir>` or __graft_entry__.build()).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libcad_hip.so")
+HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "cad", "cad.h")
+
+P = C.c_void_p
+F = C.c_float
+I = C.c_int
+I64 = C.c_int64
+FP = C.POINTER(C.c_float)
+I64P = C.POINTER(C.c_int64)
+
+
+class UnetDesc(C.Structure):
+    _fields_ = [("in_channels", I), ("init_features", I), ("max_depth", F), ("max_batch", I),
+                ("height", I), ("width", I)]
+
+
+class AdamOpts(C.Structure):
+    _fields_ = [("lr", F), ("beta1", F), ("beta2", F), ("eps", F), ("weight_decay", F)]
+
+
+# name: (restype, argtypes)
+SIGNATURES = {
+    "cad_abi_version": (I, []),
+    "cad_last_error": (C.c_char_p, []),
+    "cad_device_count": (I, [C.POINTER(I)]),
+    "cad_set_device": (I, [I]),
+    "cad_stream_synchronize": (I, [P]),
+    "cad_unet_create": (I, [C.POINTER(UnetDesc), I, C.POINTER(P)]),
+    "cad_unet_destroy": (None, [P]),
+    "cad_unet_count_parameters": (I64, [P]),
+    "cad_unet_num_params": (I, [P]),
+    "cad_unet_num_buffers": (I, [P]),
+    "cad_unet_tensor_info": (I, [P, I, I, C.POINTER(C.c_char_p), C.POINTER(I), I64P]),
+    "cad_unet_set_tensor": (I, [P, I, I, FP, I64]),
+    "cad_unet_get_tensor": (I, [P, I, I, FP, I64]),
+    "cad_unet_get_grad": (I, [P, I, FP, I64]),
+    "cad_unet_train": (I, [P, I]),
+    "cad_unet_flat": (I, [P, C.POINTER(P), C.POINTER(P), I64P]),
+    "cad_unet_use_external_slabs": (I, [P, P, P]),
+    "cad_unet_forward": (I, [P, P, P, I, P]),
+    "cad_unet_backward": (I, [P, P, P]),
+    "cad_unet_num_stages": (I, [P]),
+    "cad_unet_backward_stage": (I, [P, I, P, P]),
+    "cad_unet_stage_grad_range": (I, [P, I, I64P, I64P]),
+    "cad_clip_grad_norm": (I, [P, F, F, P]),
+    "cad_unet_last_grad_norm": (I, [P, FP, P]),
+    "cad_adam_create": (I, [P, C.POINTER(AdamOpts), C.POINTER(P)]),
+    "cad_adam_destroy": (None, [P]),
+    "cad_adam_step": (I, [P, P]),
+    "cad_adam_set_lr": (I, [P, F]),
+    "cad_adam_step_count": (I64, [P]),
+    "cad_loss_create": (I, [F, F, F, F, I, I, I, I, C.POINTER(P)]),
+    "cad_loss_destroy": (None, [P]),
+    "cad_loss_forward_backward": (I, [P, P, P, P, P, I, P, P, P]),
+    "cad_loss_get_components": (I, [P, FP, P]),
+    "cad_depth_metrics": (I, [P, P, I, I, I, FP, P]),
+    "cad_ray_directions": (I, [P, I, I, I, P, P]),
+    "cad_profile_enable": (I, [I]),
+    "cad_profile_reset": (I, []),
+    "cad_profile_report": (I, [C.c_char_p, I]),
+    "cad_op_conv3x3_fwd": (I, [P, I64, I, I, P, I, P, I64, I, I, I, I, P]),
+    "cad_op_conv3x3_dgrad": (I, [P, I, P, I, P, I64, I, I, I, P]),
+    "cad_op_conv3x3_wgrad": (I, [P, I, P, I64, I, I, P, I, I, I, P]),
+    "cad_op_convT_fwd": (I, [P, I, P, P, I, P, I64, I, I, I, I, P]),
+    "cad_op_convT_dgrad": (I, [P, I64, I, I, P, I, P, I, I, I, P]),
+    "cad_op_convT_wgrad": (I, [P, I, P, I64, I, I, P, I, I, I, P]),
+    "cad_op_maxpool_fwd": (I, [P, I64, I, I, I, I, P, P, P]),
+}
+
+
+class CadError(RuntimeError):
+    pass
+
+
+def header_functions(path: str = HEADER):
+    """Every function name declared in include/cad/cad.h."""
+    with open(path) as fh:
+        text = fh.read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(cad_[A-Za-z0-9_]+)\s*\(", text)))
+
+
+_lib = None
+
+
+def load():
+    """Load libcad_hip.so (fails loudly if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libcad_hip.so not built at {LIB_PATH}: run `make -C {PKG_DIR}` "
+                          "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(status: int, what: str = ""):
+    if status != 0:
+        msg = load().cad_last_error().decode(errors="replace")
+        raise CadError(f"{what} failed (status {status}): {msg}")

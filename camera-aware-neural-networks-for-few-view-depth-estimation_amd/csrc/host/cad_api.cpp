@@ -1,0 +1,927 @@
+// libcad_hip.so — host runtime behind include/cad/cad.h.
+//
+// Owns the U-Net's device state (flat parameter/gradient slabs, BN buffers, activation arena sized
+// at create time — no allocation inside a step, so a step is hipGraph-capturable) and sequences the
+// HIP kernels of csrc/kernels for BaselineUNetImpl::forward (baseline_unet.h:174-195), its
+// backward, CombinedDepthLoss (depth_loss.h:366-433), clip_grad_norm_ and Adam
+// (tensorboard_trainer_enhanced.h:287-304).
+//
+// Activation layout per level l (H_l = H >> l, C_l = f << l), NHWC fp32:
+//   enc/bottleneck: y1, a1, y2 [M_l][C_l]; output written straight into cat_l[:, 0:C_l]
+//   cat_l [M_l][2 C_l] = decoder concat buffer {skip | up} (baseline_unet.h:98, skip first) — the
+//         encoder writes the skip half, the ConvTranspose epilogue writes the up half: no cat/pad.
+//   pool_l [M_l][C_{l-1}] + uint8 argmax; dec: y1d, a1d, y2d, d_l [M_l][C_l].
+// Backward scratch: S_a, S_b [M_0][C_0], S_c [M_1][C_0]; dcat_l [M_l][2 C_l].
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../../include/cad/cad.h"
+#include "../kernels/kernels.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+struct CadError : std::runtime_error {
+    cad_status st;
+    CadError(cad_status s, const std::string& m) : std::runtime_error(m), st(s) {}
+};
+
+#define HIPCHK(expr)                                                                            \
+    do {                                                                                        \
+        hipError_t e_ = (expr);                                                                 \
+        if (e_ != hipSuccess)                                                                   \
+            throw CadError(e_ == hipErrorOutOfMemory ? CAD_ERR_OOM : CAD_ERR_HIP,               \
+                           std::string(#expr) + ": " + hipGetErrorString(e_));                 \
+    } while (0)
+
+void require(bool c, const std::string& m, cad_status s = CAD_ERR_INVALID) {
+    if (!c) throw CadError(s, m);
+}
+
+template <class F>
+cad_status guard(F&& f) {
+    try {
+        f();
+        return CAD_OK;
+    } catch (const CadError& e) {
+        g_err = e.what();
+        return e.st;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return CAD_ERR_INVALID;
+    }
+}
+
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// bump allocator over one hipMalloc; run once with base == nullptr to size it
+struct Arena {
+    char* base = nullptr;
+    size_t off = 0;
+    void* take(size_t bytes) {
+        off = (off + 255) & ~size_t(255);
+        void* p = base ? base + off : nullptr;
+        off += bytes;
+        return p;
+    }
+    float* f(int64_t n) { return static_cast<float*>(take(sizeof(float) * (size_t)std::max<int64_t>(n, 1))); }
+    double* d(int64_t n) { return static_cast<double*>(take(sizeof(double) * (size_t)std::max<int64_t>(n, 1))); }
+    uint8_t* u8(int64_t n) { return static_cast<uint8_t*>(take((size_t)std::max<int64_t>(n, 1))); }
+};
+
+enum PKind { P_CONV3, P_BNW, P_BNB, P_CONVT_W, P_CONVT_B, P_HEAD_W, P_HEAD_B };
+
+struct PInfo {
+    std::string name;
+    int ndim;
+    int64_t shape[4];
+    PKind kind;
+    int64_t off;      // offset in the flat slab (floats)
+    int64_t n_int;    // internal element count
+    int64_t n_ref;    // reference element count
+    int cin_ref = 0, cin_int = 0, cout = 0;
+};
+
+struct BufInfo {
+    std::string name;
+    int64_t C;
+    float* ptr;
+};
+
+struct BN {
+    int C = 0, widx = -1, bidx = -1;
+    float *rm = nullptr, *rv = nullptr;
+    float *mean = nullptr, *invstd = nullptr, *scale = nullptr, *shift = nullptr, *coef = nullptr;
+};
+struct Conv {
+    int pidx = -1, cin = 0, cout = 0;
+    float* wd = nullptr;   // dgrad repack
+};
+struct DoubleConv {
+    Conv c1, c2;
+    BN b1, b2;
+    int level = 0;
+    float *y1 = nullptr, *a1 = nullptr, *y2 = nullptr;
+    int first_param = 0, last_param = 0;   // [first, last] indices in named_parameters()
+};
+struct Up {
+    int widx = -1, bidx = -1, cin = 0, cout = 0;
+    float* wf = nullptr;   // forward repack [q][co][ci]
+};
+
+}  // namespace
+
+struct cad_unet {
+    int device = 0;
+    int in_ch = 3, f = 64, Bmax = 1, H = 0, W = 0;
+    float max_depth = 10.f;
+    bool train = true;
+    bool have_fwd = false;
+    int fwd_B = 0;
+    std::vector<PInfo> params;
+    std::vector<BufInfo> bufs;
+    int64_t n_flat = 0;
+    float *flat_p = nullptr, *flat_g = nullptr;
+    float* norm_coef = nullptr;   // [norm, coef]
+    void* arena_base = nullptr;
+    // model structure
+    DoubleConv enc[5];   // enc1..enc4 = levels 0..3, bottleneck = level 4
+    DoubleConv dec[4];   // dec1..dec4 at levels 0..3 (index = level)
+    Up up[4];            // dec_l.up: level l+1 -> l
+    int head_w = -1, head_b = -1;
+    // activations
+    float* x0 = nullptr;
+    float* cat[4] = {};
+    float* pool[5] = {};
+    uint8_t* pidx[5] = {};
+    float* a2_bott = nullptr;
+    float* dout[4] = {};   // decoder outputs d_l
+    float* sig = nullptr;
+    // backward
+    float* dcat[4] = {};
+    float *Sa = nullptr, *Sb = nullptr, *Sc = nullptr;
+    float* stats = nullptr;    // conv-epilogue BN partials
+    double* dscr = nullptr;    // column-reduction scratch
+    float* slab = nullptr;
+    int64_t slab_cap = 0;
+    // stage grad ranges
+    std::vector<std::pair<int64_t, int64_t>> stage_range;
+
+    int Hl(int l) const { return H >> l; }
+    int Wl(int l) const { return W >> l; }
+    int Cl(int l) const { return f << l; }
+    int64_t Ml(int l, int B) const { return (int64_t)B * Hl(l) * Wl(l); }
+    float* P(int i) const { return flat_p + params[i].off; }
+    float* G(int i) const { return flat_g + params[i].off; }
+};
+
+struct cad_loss {
+    int device = 0, Bmax = 0, H = 0, W = 0;
+    float w[4];
+    cad::LossWorkspace ws{};
+    float* out5 = nullptr;
+    void* base = nullptr;
+};
+
+struct cad_adam {
+    cad_unet* model = nullptr;
+    cad_adam_opts o{};
+    float *m = nullptr, *v = nullptr;
+    int64_t step = 0;
+};
+
+namespace {
+
+// ------------------------------------------------------------------------------------------
+// model construction: parameter table in named_parameters() order (baseline_unet.h:147-165)
+// ------------------------------------------------------------------------------------------
+void add_param(cad_unet* h, const std::string& name, std::vector<int64_t> shape, PKind kind, int cin_ref = 0,
+               int cin_int = 0, int cout = 0) {
+    PInfo p;
+    p.name = name;
+    p.ndim = (int)shape.size();
+    p.n_ref = 1;
+    for (int i = 0; i < 4; ++i) p.shape[i] = i < p.ndim ? shape[i] : 1;
+    for (int i = 0; i < p.ndim; ++i) p.n_ref *= shape[i];
+    p.kind = kind;
+    p.cin_ref = cin_ref; p.cin_int = cin_int; p.cout = cout;
+    p.n_int = kind == P_CONV3 ? (int64_t)cout * 9 * cin_int : p.n_ref;
+    h->n_flat = (h->n_flat + 63) & ~int64_t(63);
+    p.off = h->n_flat;
+    h->n_flat += p.n_int;
+    h->params.push_back(p);
+}
+
+void add_double_conv(cad_unet* h, DoubleConv& dc, const std::string& pre, int cin_ref, int cin_int, int cout, int level) {
+    dc.level = level;
+    dc.first_param = (int)h->params.size();
+    add_param(h, pre + "conv1.weight", {cout, cin_ref, 3, 3}, P_CONV3, cin_ref, cin_int, cout);
+    dc.c1 = Conv{(int)h->params.size() - 1, cin_int, cout, nullptr};
+    add_param(h, pre + "bn1.weight", {cout}, P_BNW);
+    add_param(h, pre + "bn1.bias", {cout}, P_BNB);
+    dc.b1.C = cout; dc.b1.widx = (int)h->params.size() - 2; dc.b1.bidx = (int)h->params.size() - 1;
+    add_param(h, pre + "conv2.weight", {cout, cout, 3, 3}, P_CONV3, cout, cout, cout);
+    dc.c2 = Conv{(int)h->params.size() - 1, cout, cout, nullptr};
+    add_param(h, pre + "bn2.weight", {cout}, P_BNW);
+    add_param(h, pre + "bn2.bias", {cout}, P_BNB);
+    dc.b2.C = cout; dc.b2.widx = (int)h->params.size() - 2; dc.b2.bidx = (int)h->params.size() - 1;
+    dc.last_param = (int)h->params.size() - 1;
+}
+
+void build_tables(cad_unet* h) {
+    const int f = h->f;
+    add_double_conv(h, h->enc[0], "enc1.", h->in_ch, 4, f, 0);
+    const char* enames[4] = {"enc2", "enc3", "enc4", "bottleneck"};
+    for (int i = 0; i < 4; ++i)
+        add_double_conv(h, h->enc[i + 1], std::string(enames[i]) + ".conv.", f << i, f << i, f << (i + 1), i + 1);
+    for (int k = 0; k < 4; ++k) {   // dec4 .. dec1
+        const int l = 3 - k;        // decoder level
+        const int cin = f << (l + 1), cout = f << l;
+        const std::string pre = "dec" + std::to_string(l + 1) + ".";
+        add_param(h, pre + "up.weight", {cin, cout, 2, 2}, P_CONVT_W);
+        add_param(h, pre + "up.bias", {cout}, P_CONVT_B);
+        h->up[l] = Up{(int)h->params.size() - 2, (int)h->params.size() - 1, cin, cout, nullptr};
+        add_double_conv(h, h->dec[l], pre + "conv.", cin, cin, cout, l);
+        h->dec[l].first_param = h->up[l].widx;
+    }
+    add_param(h, "out_conv.weight", {1, f, 1, 1}, P_HEAD_W);
+    add_param(h, "out_conv.bias", {1}, P_HEAD_B);
+    h->head_w = (int)h->params.size() - 2;
+    h->head_b = (int)h->params.size() - 1;
+    h->n_flat = (h->n_flat + 63) & ~int64_t(63);
+}
+
+void bn_alloc(Arena& a, BN& b) {
+    b.rm = a.f(b.C); b.rv = a.f(b.C);
+    b.mean = a.f(b.C); b.invstd = a.f(b.C); b.scale = a.f(b.C); b.shift = a.f(b.C); b.coef = a.f(3 * b.C);
+}
+
+void layout(cad_unet* h, Arena& a) {
+    const int B = h->Bmax;
+    h->flat_p = a.f(h->n_flat);
+    h->flat_g = a.f(h->n_flat);
+    h->norm_coef = a.f(4);
+    for (int l = 0; l < 5; ++l) {
+        DoubleConv& e = h->enc[l];
+        bn_alloc(a, e.b1); bn_alloc(a, e.b2);
+        const int64_t MC = h->Ml(l, B) * h->Cl(l);
+        e.y1 = a.f(MC); e.a1 = a.f(MC); e.y2 = a.f(MC);
+        if (l > 0) e.c1.wd = a.f((int64_t)e.c1.cout * 9 * e.c1.cin);
+        e.c2.wd = a.f((int64_t)e.c2.cout * 9 * e.c2.cin);
+        if (l < 4) h->cat[l] = a.f(2 * MC);
+        if (l > 0) {
+            h->pool[l] = a.f(h->Ml(l, B) * h->Cl(l - 1));
+            h->pidx[l] = a.u8(h->Ml(l, B) * h->Cl(l - 1));
+        }
+    }
+    h->a2_bott = a.f(h->Ml(4, B) * h->Cl(4));
+    for (int l = 0; l < 4; ++l) {
+        DoubleConv& d = h->dec[l];
+        bn_alloc(a, d.b1); bn_alloc(a, d.b2);
+        const int64_t MC = h->Ml(l, B) * h->Cl(l);
+        d.y1 = a.f(MC); d.a1 = a.f(MC); d.y2 = a.f(MC);
+        h->dout[l] = a.f(MC);
+        d.c1.wd = a.f((int64_t)d.c1.cout * 9 * d.c1.cin);
+        d.c2.wd = a.f((int64_t)d.c2.cout * 9 * d.c2.cin);
+        h->up[l].wf = a.f((int64_t)4 * h->up[l].cout * h->up[l].cin);
+        h->dcat[l] = a.f(2 * MC);
+    }
+    h->x0 = a.f(h->Ml(0, B) * 4);
+    h->sig = a.f(h->Ml(0, B));
+    const int64_t M0C0 = h->Ml(0, B) * h->Cl(0);
+    h->Sa = a.f(M0C0);
+    h->Sb = a.f(M0C0);
+    h->Sc = a.f(h->Ml(1, B) * h->Cl(0));
+    // BN tile partials: rows x 2C, max over layers
+    int64_t st = 0, colmax = 0;
+    for (int l = 0; l < 5; ++l) {
+        const int64_t r = cad::conv3x3_stats_rows(B, h->Hl(l), h->Wl(l), h->Cl(l));
+        st = std::max<int64_t>(st, r * 2 * h->Cl(l));
+        colmax = std::max<int64_t>(colmax, h->Cl(l));
+    }
+    h->stats = a.f(st);
+    h->dscr = a.d((int64_t)(cad::colsum_slices(h->Ml(0, B)) + 2) * 4 * colmax + 4 * colmax + 8192);
+    // wgrad split-K slab: enough for the largest-benefit layers, capped at 64M floats (256 MB)
+    int64_t sl = 0;
+    for (int l = 0; l < 5; ++l) {
+        const int64_t Kp = h->Ml(l, B);
+        sl = std::max(sl, cad::wgrad_slab_floats(h->Cl(l), 9 * h->Cl(l) * 2, (int)std::min<int64_t>(Kp, INT32_MAX)));
+    }
+    h->slab_cap = std::min<int64_t>(sl, (int64_t)64 << 20);
+    h->slab = a.f(h->slab_cap);
+    // buffers table (running stats), named_buffers() order (parameter order of the BNs)
+    h->bufs.clear();
+    auto add_bn_bufs = [&](const std::string& pre, BN& b) {
+        h->bufs.push_back({pre + ".running_mean", b.C, b.rm});
+        h->bufs.push_back({pre + ".running_var", b.C, b.rv});
+    };
+    const char* en[5] = {"enc1.", "enc2.conv.", "enc3.conv.", "enc4.conv.", "bottleneck.conv."};
+    for (int l = 0; l < 5; ++l) { add_bn_bufs(std::string(en[l]) + "bn1", h->enc[l].b1); add_bn_bufs(std::string(en[l]) + "bn2", h->enc[l].b2); }
+    for (int k = 0; k < 4; ++k) {
+        const int l = 3 - k;
+        const std::string pre = "dec" + std::to_string(l + 1) + ".conv.";
+        add_bn_bufs(pre + "bn1", h->dec[l].b1);
+        add_bn_bufs(pre + "bn2", h->dec[l].b2);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------------------
+void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin, int B, float* out, int64_t ldo,
+                     int ocoff, hipStream_t st) {
+    const int l = dc.level, Hh = h->Hl(l), Ww = h->Wl(l), C = dc.c1.cout;
+    const int64_t M = h->Ml(l, B);
+    const bool tr = h->train;
+    const int rows = cad::conv3x3_stats_rows(B, Hh, Ww, C);
+    auto bn = [&](BN& b) {
+        if (tr)
+            cad::bn_fwd_finalize(h->stats, rows, C, M, h->P(b.widx), h->P(b.bidx), b.rm, b.rv, 0.1f, 1e-5f, h->dscr,
+                                 b.mean, b.invstd, b.scale, b.shift, st);
+        else
+            cad::bn_eval_coeffs(h->P(b.widx), h->P(b.bidx), b.rm, b.rv, C, 1e-5f, b.mean, b.invstd, b.scale, b.shift, st);
+    };
+    cad::conv3x3_fwd(in, ldin, 0, dc.c1.cin, h->P(dc.c1.pidx), C, dc.y1, C, 0, B, Hh, Ww, tr ? h->stats : nullptr, st);
+    bn(dc.b1);
+    cad::bn_relu_fwd(dc.y1, C, dc.b1.scale, dc.b1.shift, dc.a1, C, 0, M, st);
+    cad::conv3x3_fwd(dc.a1, C, 0, C, h->P(dc.c2.pidx), C, dc.y2, C, 0, B, Hh, Ww, tr ? h->stats : nullptr, st);
+    bn(dc.b2);
+    cad::bn_relu_fwd(dc.y2, C, dc.b2.scale, dc.b2.shift, out, ldo, ocoff, M, st);
+}
+
+void unet_forward(cad_unet* h, const float* rgb, float* depth, int B, hipStream_t st) {
+    const int f = h->f;
+    for (int l = 0; l < 4; ++l)
+        cad::repack_convT_fwd(h->P(h->up[l].widx), h->up[l].wf, h->up[l].cin, h->up[l].cout, st);
+    cad::rgb_to_nhwc4(rgb, h->x0, B, h->H, h->W, st);
+    double_conv_fwd(h, h->enc[0], h->x0, 4, B, h->cat[0], 2 * f, 0, st);
+    for (int l = 1; l <= 4; ++l) {
+        const int Cp = h->Cl(l - 1);
+        cad::maxpool_fwd(h->cat[l - 1], 2 * Cp, Cp, B, h->Hl(l - 1), h->Wl(l - 1), h->pool[l], h->pidx[l], st);
+        if (l < 4)
+            double_conv_fwd(h, h->enc[l], h->pool[l], Cp, B, h->cat[l], 2 * h->Cl(l), 0, st);
+        else
+            double_conv_fwd(h, h->enc[4], h->pool[4], Cp, B, h->a2_bott, h->Cl(4), 0, st);
+    }
+    for (int l = 3; l >= 0; --l) {
+        const float* upin = l == 3 ? h->a2_bott : h->dout[l + 1];
+        const Up& u = h->up[l];
+        cad::convT_fwd(upin, u.cin, u.cin, u.wf, h->P(u.bidx), u.cout, h->cat[l], 2 * h->Cl(l), h->Cl(l), B,
+                       h->Hl(l + 1), h->Wl(l + 1), st);
+        double_conv_fwd(h, h->dec[l], h->cat[l], 2 * h->Cl(l), B, h->dout[l], h->Cl(l), 0, st);
+    }
+    cad::head_fwd(h->dout[0], f, h->P(h->head_w), h->P(h->head_b), h->max_depth, h->sig, depth, h->Ml(0, B), st);
+}
+
+// ------------------------------------------------------------------------------------------
+// backward
+// ------------------------------------------------------------------------------------------
+// g: grad wrt the DoubleConv output (ld ldg, channel offset gcoff); in: the block input (ld ldin,
+// cin channels); din: where conv1's dgrad goes (nullptr = not needed), ld lddin.
+void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, int gcoff, const float* in,
+                     int64_t ldin, int B, float* din, int64_t lddin, hipStream_t st) {
+    const int l = dc.level, Hh = h->Hl(l), Ww = h->Wl(l), C = dc.c1.cout;
+    const int64_t M = h->Ml(l, B);
+    float* dY = h->Sb;
+    float* dA1 = h->Sa;
+    // bn2 + relu
+    cad::bn_relu_bwd(g, ldg, gcoff, dc.y2, C, dc.b2.mean, dc.b2.invstd, dc.b2.scale, dc.b2.shift, h->P(dc.b2.widx), M,
+                     h->dscr, dc.b2.coef, h->G(dc.b2.widx), h->G(dc.b2.bidx), dY, st);
+    // conv2
+    cad::conv3x3_wgrad(dY, C, dc.a1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
+    cad::conv3x3_dgrad(dY, C, dc.c2.wd, C, dA1, C, B, Hh, Ww, st);
+    // bn1 + relu
+    cad::bn_relu_bwd(dA1, C, 0, dc.y1, C, dc.b1.mean, dc.b1.invstd, dc.b1.scale, dc.b1.shift, h->P(dc.b1.widx), M,
+                     h->dscr, dc.b1.coef, h->G(dc.b1.widx), h->G(dc.b1.bidx), dY, st);
+    // conv1
+    cad::conv3x3_wgrad(dY, C, in, ldin, 0, dc.c1.cin, h->G(dc.c1.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
+    if (din) cad::conv3x3_dgrad(dY, C, dc.c1.wd, dc.c1.cin, din, lddin, B, Hh, Ww, st);
+}
+
+void repack_dgrad_weights(cad_unet* h, hipStream_t st) {
+    auto rp = [&](DoubleConv& dc, bool first) {
+        if (!first) cad::repack_conv_dgrad(h->P(dc.c1.pidx), dc.c1.wd, dc.c1.cout, dc.c1.cin, st);
+        cad::repack_conv_dgrad(h->P(dc.c2.pidx), dc.c2.wd, dc.c2.cout, dc.c2.cin, st);
+    };
+    for (int l = 0; l < 5; ++l) rp(h->enc[l], l == 0);
+    for (int l = 0; l < 4; ++l) rp(h->dec[l], false);
+}
+
+// stages: 0 head, 1..4 dec1..dec4, 5 bottleneck, 6..9 enc4..enc1
+constexpr int kStages = 10;
+
+void backward_stage(cad_unet* h, int stage, const float* dpred, hipStream_t st) {
+    const int B = h->fwd_B;
+    const int f = h->f;
+    if (stage == 0) {
+        repack_dgrad_weights(h, st);
+        cad::head_bwd(h->dout[0], f, h->P(h->head_w), dpred, h->sig, h->max_depth, h->Sa, h->Ml(0, B), h->dscr,
+                      h->G(h->head_w), h->G(h->head_b), st);
+        return;
+    }
+    if (stage <= 4) {   // decoder level l = stage-1; grad of its output is in Sa
+        const int l = stage - 1;
+        const int C = h->Cl(l);
+        double_conv_bwd(h, h->dec[l], h->Sa, C, 0, h->cat[l], 2 * C, B, h->dcat[l], 2 * C, st);
+        const Up& u = h->up[l];
+        const float* upin = l == 3 ? h->a2_bott : h->dout[l + 1];
+        // up (ConvTranspose2d) backward: grad of its output = dcat[:, C:2C]
+        cad::convT_wgrad(upin, u.cin, h->dcat[l], 2 * C, C, u.cout, h->G(u.widx), B, h->Hl(l + 1), h->Wl(l + 1),
+                         h->slab, h->slab_cap, st);
+        cad::colsum(h->dcat[l], 2 * C, C, h->Ml(l, B), C, h->dscr, st);
+        cad::colsum_finalize(h->dscr, cad::colsum_slices(h->Ml(l, B)), C, h->G(u.bidx), 1.f, st);
+        cad::convT_dgrad(h->dcat[l], 2 * C, C, u.cout, h->P(u.widx), u.cin, h->Sa, B, h->Hl(l + 1), h->Wl(l + 1), st);
+        return;
+    }
+    // encoder side: stage 5 = bottleneck (level 4), 6..9 = enc4..enc1 (levels 3..0)
+    const int l = 4 - (stage - 5);
+    DoubleConv& e = h->enc[l];
+    const int C = h->Cl(l);
+    const float* g = l == 4 ? h->Sa : h->dcat[l];
+    const int64_t ldg = l == 4 ? C : 2 * C;
+    if (l == 0) {
+        double_conv_bwd(h, e, g, ldg, 0, h->x0, 4, B, nullptr, 0, st);
+        return;
+    }
+    const int Cp = h->Cl(l - 1);
+    double_conv_bwd(h, e, g, ldg, 0, h->pool[l], Cp, B, h->Sc, Cp, st);
+    cad::maxpool_bwd(h->Sc, h->pidx[l], Cp, B, h->Hl(l - 1), h->Wl(l - 1), h->dcat[l - 1], 2 * Cp, st);
+}
+
+void compute_stage_ranges(cad_unet* h) {
+    auto rng = [&](int first, int last) {
+        const int64_t a = h->params[first].off;
+        const int64_t b = h->params[last].off + h->params[last].n_int;
+        return std::make_pair(a, b - a);
+    };
+    h->stage_range.clear();
+    h->stage_range.push_back(rng(h->head_w, h->head_b));
+    for (int l = 0; l < 4; ++l) h->stage_range.push_back(rng(h->dec[l].first_param, h->dec[l].last_param));
+    for (int l = 4; l >= 0; --l) h->stage_range.push_back(rng(h->enc[l].first_param, h->enc[l].last_param));
+}
+
+// reference layout <-> internal layout
+void ref_to_int(const PInfo& p, const float* src, std::vector<float>& dst) {
+    dst.assign(p.n_int, 0.f);
+    if (p.kind == P_CONV3) {   // (co, ci, ky, kx) -> [co][ky*3+kx][ci_pad]
+        for (int co = 0; co < p.cout; ++co)
+            for (int ci = 0; ci < p.cin_ref; ++ci)
+                for (int t = 0; t < 9; ++t)
+                    dst[((int64_t)co * 9 + t) * p.cin_int + ci] = src[((int64_t)co * p.cin_ref + ci) * 9 + t];
+    } else if (p.kind == P_CONVT_W) {   // (ci, co, dy, dx) -> [ci][q][co]
+        const int64_t ci_n = p.shape[0], co_n = p.shape[1];
+        for (int64_t ci = 0; ci < ci_n; ++ci)
+            for (int64_t co = 0; co < co_n; ++co)
+                for (int q = 0; q < 4; ++q) dst[(ci * 4 + q) * co_n + co] = src[(ci * co_n + co) * 4 + q];
+    } else {
+        std::memcpy(dst.data(), src, sizeof(float) * p.n_ref);
+    }
+}
+void int_to_ref(const PInfo& p, const float* src, float* dst) {
+    if (p.kind == P_CONV3) {
+        for (int co = 0; co < p.cout; ++co)
+            for (int ci = 0; ci < p.cin_ref; ++ci)
+                for (int t = 0; t < 9; ++t)
+                    dst[((int64_t)co * p.cin_ref + ci) * 9 + t] = src[((int64_t)co * 9 + t) * p.cin_int + ci];
+    } else if (p.kind == P_CONVT_W) {
+        const int64_t ci_n = p.shape[0], co_n = p.shape[1];
+        for (int64_t ci = 0; ci < ci_n; ++ci)
+            for (int64_t co = 0; co < co_n; ++co)
+                for (int q = 0; q < 4; ++q) dst[(ci * co_n + co) * 4 + q] = src[(ci * 4 + q) * co_n + co];
+    } else {
+        std::memcpy(dst, src, sizeof(float) * p.n_ref);
+    }
+}
+
+// default init: reference module defaults (kaiming_uniform(a=sqrt5) => U(+-1/sqrt(fan_in)) weights and
+// biases, BN weight 1 bias 0, running mean 0 var 1); deterministic host LCG stream (seed 42)
+void default_init(cad_unet* h) {
+    uint64_t s = 0x2545F4914F6CDD1Dull ^ 42;
+    auto rnd = [&]() {
+        s ^= s << 13; s ^= s >> 7; s ^= s << 17;
+        return (float)((s >> 40) * (1.0 / 16777216.0));
+    };
+    std::vector<float> ref, inter;
+    for (const PInfo& p : h->params) {
+        ref.assign(p.n_ref, 0.f);
+        if (p.kind == P_BNW) std::fill(ref.begin(), ref.end(), 1.f);
+        else if (p.kind == P_BNB) { /* zeros */ }
+        else {
+            int64_t fan_in;
+            if (p.kind == P_CONV3) fan_in = (int64_t)p.cin_ref * 9;
+            else if (p.kind == P_CONVT_W || p.kind == P_CONVT_B) {
+                const PInfo& w = p.kind == P_CONVT_W ? p : h->params[&p - &h->params[0] - 1];
+                fan_in = w.shape[1] * 4;
+            } else fan_in = h->f;
+            const float bound = 1.f / std::sqrt((float)fan_in);
+            for (auto& x : ref) x = (rnd() * 2.f - 1.f) * bound;
+        }
+        ref_to_int(p, ref.data(), inter);
+        HIPCHK(hipMemcpy(h->flat_p + p.off, inter.data(), sizeof(float) * p.n_int, hipMemcpyHostToDevice));
+    }
+    for (const BufInfo& b : h->bufs) {
+        std::vector<float> v(b.C, b.name.find("running_var") != std::string::npos ? 1.f : 0.f);
+        HIPCHK(hipMemcpy(b.ptr, v.data(), sizeof(float) * b.C, hipMemcpyHostToDevice));
+    }
+}
+
+}  // namespace
+
+// ============================================================================================
+// C ABI
+// ============================================================================================
+extern "C" {
+
+int cad_abi_version(void) { return CAD_ABI_VERSION; }
+const char* cad_last_error(void) { return g_err.c_str(); }
+
+cad_status cad_device_count(int* n) {
+    return guard([&] { HIPCHK(hipGetDeviceCount(n)); });
+}
+cad_status cad_set_device(int device) {
+    return guard([&] { HIPCHK(hipSetDevice(device)); });
+}
+cad_status cad_stream_synchronize(void* stream) {
+    return guard([&] { HIPCHK(hipStreamSynchronize(S(stream))); });
+}
+
+cad_status cad_unet_create(const cad_unet_desc* d, int device, cad_unet** out) {
+    return guard([&] {
+        require(d && out, "null argument");
+        require(d->in_channels == 3, "in_channels must be 3 (rgb)");
+        require(d->init_features >= 4 && d->init_features % 4 == 0, "init_features must be a multiple of 4");
+        require(d->height > 0 && d->width > 0 && d->height % 16 == 0 && d->width % 16 == 0,
+                "height/width must be positive multiples of 16");
+        require(d->max_batch >= 1, "max_batch must be >= 1");
+        HIPCHK(hipSetDevice(device));
+        auto h = std::make_unique<cad_unet>();
+        h->device = device;
+        h->in_ch = d->in_channels;
+        h->f = d->init_features;
+        h->max_depth = d->max_depth;
+        h->Bmax = d->max_batch;
+        h->H = d->height;
+        h->W = d->width;
+        build_tables(h.get());
+        Arena sz;
+        layout(h.get(), sz);
+        void* base = nullptr;
+        HIPCHK(hipMalloc(&base, sz.off + 4096));
+        HIPCHK(hipMemset(base, 0, sz.off + 4096));
+        h->arena_base = base;
+        Arena real;
+        real.base = static_cast<char*>(base);
+        layout(h.get(), real);
+        compute_stage_ranges(h.get());
+        default_init(h.get());
+        HIPCHK(hipDeviceSynchronize());
+        *out = h.release();
+    });
+}
+
+void cad_unet_destroy(cad_unet* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    (void)hipFree(h->arena_base);
+    delete h;
+}
+
+int64_t cad_unet_count_parameters(const cad_unet* h) {
+    int64_t n = 0;
+    for (const auto& p : h->params) n += p.n_ref;
+    return n;
+}
+int cad_unet_num_params(const cad_unet* h) { return (int)h->params.size(); }
+int cad_unet_num_buffers(const cad_unet* h) { return (int)h->bufs.size(); }
+
+cad_status cad_unet_tensor_info(const cad_unet* h, int kind, int idx, const char** name, int* ndim, int64_t shape[4]) {
+    return guard([&] {
+        if (kind == 0) {
+            require(idx >= 0 && idx < (int)h->params.size(), "param index out of range");
+            const PInfo& p = h->params[idx];
+            if (name) *name = p.name.c_str();
+            if (ndim) *ndim = p.ndim;
+            if (shape) for (int i = 0; i < 4; ++i) shape[i] = p.shape[i];
+        } else {
+            require(idx >= 0 && idx < (int)h->bufs.size(), "buffer index out of range");
+            const BufInfo& b = h->bufs[idx];
+            if (name) *name = b.name.c_str();
+            if (ndim) *ndim = 1;
+            if (shape) { shape[0] = b.C; shape[1] = shape[2] = shape[3] = 1; }
+        }
+    });
+}
+
+cad_status cad_unet_set_tensor(cad_unet* h, int kind, int idx, const float* host, int64_t numel) {
+    return guard([&] {
+        HIPCHK(hipSetDevice(h->device));
+        if (kind == 0) {
+            require(idx >= 0 && idx < (int)h->params.size(), "param index out of range");
+            const PInfo& p = h->params[idx];
+            require(numel == p.n_ref, "numel mismatch for " + p.name);
+            std::vector<float> inter;
+            ref_to_int(p, host, inter);
+            HIPCHK(hipMemcpy(h->flat_p + p.off, inter.data(), sizeof(float) * p.n_int, hipMemcpyHostToDevice));
+        } else {
+            require(idx >= 0 && idx < (int)h->bufs.size(), "buffer index out of range");
+            require(numel == h->bufs[idx].C, "numel mismatch for " + h->bufs[idx].name);
+            HIPCHK(hipMemcpy(h->bufs[idx].ptr, host, sizeof(float) * numel, hipMemcpyHostToDevice));
+        }
+    });
+}
+
+static void get_slab_tensor(const cad_unet* h, const float* slab, int idx, float* host, int64_t numel) {
+    require(idx >= 0 && idx < (int)h->params.size(), "param index out of range");
+    const PInfo& p = h->params[idx];
+    require(numel == p.n_ref, "numel mismatch for " + p.name);
+    std::vector<float> inter(p.n_int);
+    HIPCHK(hipMemcpy(inter.data(), slab + p.off, sizeof(float) * p.n_int, hipMemcpyDeviceToHost));
+    int_to_ref(p, inter.data(), host);
+}
+
+cad_status cad_unet_get_tensor(const cad_unet* h, int kind, int idx, float* host, int64_t numel) {
+    return guard([&] {
+        HIPCHK(hipSetDevice(h->device));
+        HIPCHK(hipDeviceSynchronize());
+        if (kind == 0) {
+            get_slab_tensor(h, h->flat_p, idx, host, numel);
+        } else {
+            require(idx >= 0 && idx < (int)h->bufs.size(), "buffer index out of range");
+            require(numel == h->bufs[idx].C, "numel mismatch");
+            HIPCHK(hipMemcpy(host, h->bufs[idx].ptr, sizeof(float) * numel, hipMemcpyDeviceToHost));
+        }
+    });
+}
+
+cad_status cad_unet_get_grad(const cad_unet* h, int idx, float* host, int64_t numel) {
+    return guard([&] {
+        HIPCHK(hipSetDevice(h->device));
+        HIPCHK(hipDeviceSynchronize());
+        get_slab_tensor(h, h->flat_g, idx, host, numel);
+    });
+}
+
+cad_status cad_unet_train(cad_unet* h, int train) {
+    return guard([&] { h->train = train != 0; });
+}
+
+cad_status cad_unet_flat(cad_unet* h, float** params, float** grads, int64_t* n) {
+    return guard([&] {
+        if (params) *params = h->flat_p;
+        if (grads) *grads = h->flat_g;
+        if (n) *n = h->n_flat;
+    });
+}
+
+cad_status cad_unet_use_external_slabs(cad_unet* h, float* params, float* grads) {
+    return guard([&] {
+        require(params && grads, "null slab");
+        HIPCHK(hipSetDevice(h->device));
+        HIPCHK(hipDeviceSynchronize());
+        HIPCHK(hipMemcpy(params, h->flat_p, sizeof(float) * h->n_flat, hipMemcpyDeviceToDevice));
+        HIPCHK(hipMemcpy(grads, h->flat_g, sizeof(float) * h->n_flat, hipMemcpyDeviceToDevice));
+        h->flat_p = params;
+        h->flat_g = grads;
+    });
+}
+
+cad_status cad_unet_forward(cad_unet* h, const float* rgb, float* depth, int B, void* stream) {
+    return guard([&] {
+        require(rgb && depth, "null tensor");
+        require(B >= 1 && B <= h->Bmax, "batch exceeds max_batch");
+        HIPCHK(hipSetDevice(h->device));
+        unet_forward(h, rgb, depth, B, S(stream));
+        HIPCHK(hipGetLastError());
+        h->have_fwd = h->train;
+        h->fwd_B = B;
+    });
+}
+
+int cad_unet_num_stages(const cad_unet*) { return kStages; }
+
+cad_status cad_unet_backward_stage(cad_unet* h, int stage, const float* ddepth, void* stream) {
+    return guard([&] {
+        require(h->have_fwd, "backward needs a preceding train-mode forward", CAD_ERR_STATE);
+        require(stage >= 0 && stage < kStages, "stage out of range");
+        require(stage != 0 || ddepth, "null ddepth");
+        HIPCHK(hipSetDevice(h->device));
+        backward_stage(h, stage, ddepth, S(stream));
+        HIPCHK(hipGetLastError());
+    });
+}
+
+cad_status cad_unet_backward(cad_unet* h, const float* ddepth, void* stream) {
+    return guard([&] {
+        require(h->have_fwd, "backward needs a preceding train-mode forward", CAD_ERR_STATE);
+        require(ddepth, "null ddepth");
+        HIPCHK(hipSetDevice(h->device));
+        for (int s = 0; s < kStages; ++s) backward_stage(h, s, ddepth, S(stream));
+        HIPCHK(hipGetLastError());
+    });
+}
+
+cad_status cad_unet_stage_grad_range(const cad_unet* h, int stage, int64_t* offset, int64_t* count) {
+    return guard([&] {
+        require(stage >= 0 && stage < kStages, "stage out of range");
+        if (offset) *offset = h->stage_range[stage].first;
+        if (count) *count = h->stage_range[stage].second;
+    });
+}
+
+cad_status cad_clip_grad_norm(cad_unet* h, float max_norm, float prescale, void* stream) {
+    return guard([&] {
+        HIPCHK(hipSetDevice(h->device));
+        cad::grad_norm_clip(h->flat_g, h->n_flat, max_norm, prescale, h->dscr, h->norm_coef, S(stream));
+        HIPCHK(hipGetLastError());
+    });
+}
+
+cad_status cad_unet_last_grad_norm(cad_unet* h, float* total_norm, void* stream) {
+    return guard([&] {
+        float v[2];
+        HIPCHK(hipMemcpyAsync(v, h->norm_coef, sizeof(v), hipMemcpyDeviceToHost, S(stream)));
+        HIPCHK(hipStreamSynchronize(S(stream)));
+        *total_norm = v[0];
+    });
+}
+
+cad_status cad_adam_create(cad_unet* model, const cad_adam_opts* o, cad_adam** out) {
+    return guard([&] {
+        require(model && o && out, "null argument");
+        HIPCHK(hipSetDevice(model->device));
+        auto a = std::make_unique<cad_adam>();
+        a->model = model;
+        a->o = *o;
+        HIPCHK(hipMalloc(&a->m, sizeof(float) * model->n_flat));
+        HIPCHK(hipMalloc(&a->v, sizeof(float) * model->n_flat));
+        HIPCHK(hipMemset(a->m, 0, sizeof(float) * model->n_flat));
+        HIPCHK(hipMemset(a->v, 0, sizeof(float) * model->n_flat));
+        *out = a.release();
+    });
+}
+void cad_adam_destroy(cad_adam* a) {
+    if (!a) return;
+    (void)hipFree(a->m);
+    (void)hipFree(a->v);
+    delete a;
+}
+cad_status cad_adam_step(cad_adam* a, void* stream) {
+    return guard([&] {
+        cad_unet* h = a->model;
+        HIPCHK(hipSetDevice(h->device));
+        a->step += 1;
+        cad::adam_step(h->flat_p, h->flat_g, a->m, a->v, h->n_flat, h->norm_coef, a->o.lr, a->o.beta1, a->o.beta2,
+                       a->o.eps, a->o.weight_decay, (int)a->step, S(stream));
+        HIPCHK(hipGetLastError());
+    });
+}
+cad_status cad_adam_set_lr(cad_adam* a, float lr) {
+    return guard([&] { a->o.lr = lr; });
+}
+int64_t cad_adam_step_count(const cad_adam* a) { return a->step; }
+
+cad_status cad_loss_create(float si, float gr, float sm, float rp, int max_batch, int height, int width, int device,
+                           cad_loss** out) {
+    return guard([&] {
+        require(out && max_batch >= 1 && height >= 2 && width >= 2, "bad loss arguments");
+        HIPCHK(hipSetDevice(device));
+        auto l = std::make_unique<cad_loss>();
+        l->device = device; l->Bmax = max_batch; l->H = height; l->W = width;
+        l->w[0] = si; l->w[1] = gr; l->w[2] = sm; l->w[3] = rp;
+        const int64_t nf = cad::loss_workspace_floats(max_batch, height, width);
+        const int64_t nd = cad::loss_part_doubles(max_batch, height, width);
+        size_t bytes = ((sizeof(double) * nd + 255) & ~size_t(255)) + sizeof(float) * (nf + 64);
+        HIPCHK(hipMalloc(&l->base, bytes));
+        HIPCHK(hipMemset(l->base, 0, bytes));
+        l->ws.part = static_cast<double*>(l->base);
+        l->ws.part_cap = nd;
+        l->ws.pyr = reinterpret_cast<float*>(static_cast<char*>(l->base) + ((sizeof(double) * nd + 255) & ~size_t(255)));
+        l->out5 = l->ws.pyr + nf;
+        *out = l.release();
+    });
+}
+void cad_loss_destroy(cad_loss* l) {
+    if (!l) return;
+    (void)hipFree(l->base);
+    delete l;
+}
+cad_status cad_loss_forward_backward(cad_loss* l, const float* pred, const float* gt, const float* rgb, const float* K,
+                                     int B, float* loss5, float* dpred, void* stream) {
+    return guard([&] {
+        require(pred && gt && rgb && K && dpred, "null tensor");
+        require(B >= 1 && B <= l->Bmax, "batch exceeds max_batch");
+        HIPCHK(hipSetDevice(l->device));
+        cad::loss_fwd_bwd(pred, gt, rgb, K, B, l->H, l->W, l->w, loss5 ? loss5 : l->out5, dpred, l->ws, S(stream));
+        if (loss5) HIPCHK(hipMemcpyAsync(l->out5, loss5, 5 * sizeof(float), hipMemcpyDeviceToDevice, S(stream)));
+        HIPCHK(hipGetLastError());
+    });
+}
+cad_status cad_loss_get_components(cad_loss* l, float out5[5], void* stream) {
+    return guard([&] {
+        HIPCHK(hipMemcpyAsync(out5, l->out5, 5 * sizeof(float), hipMemcpyDeviceToHost, S(stream)));
+        HIPCHK(hipStreamSynchronize(S(stream)));
+    });
+}
+
+cad_status cad_depth_metrics(const float* pred, const float* gt, int B, int H, int W, float out7[7], void* stream) {
+    return guard([&] {
+        require(pred && gt && out7 && B > 0, "bad arguments");
+        double* part = nullptr;
+        const int nb = cad::metrics_blocks((int64_t)H * W);
+        HIPCHK(hipMalloc((void**)&part, sizeof(double) * (size_t)B * nb * 8));
+        cad::depth_metrics_partials(pred, gt, B, (int64_t)H * W, part, nb, S(stream));
+        std::vector<double> hp((size_t)B * nb * 8);
+        HIPCHK(hipMemcpyAsync(hp.data(), part, sizeof(double) * hp.size(), hipMemcpyDeviceToHost, S(stream)));
+        HIPCHK(hipStreamSynchronize(S(stream)));
+        HIPCHK(hipFree(part));
+        // computeDepthMetrics per sample (enhanced.h:400-439), averaged over samples (:383-391)
+        double acc[7] = {0, 0, 0, 0, 0, 0, 0};
+        for (int b = 0; b < B; ++b) {
+            double t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            for (int i = 0; i < nb; ++i)
+                for (int q = 0; q < 8; ++q) t[q] += hp[((size_t)b * nb + i) * 8 + q];
+            if (t[0] <= 0) continue;   // no valid pixel: the reference returns zeros for the sample
+            acc[0] += t[1] / t[0];
+            acc[1] += t[2] / t[0];
+            acc[2] += std::sqrt(t[3] / t[0]);
+            acc[3] += std::sqrt(t[4] / t[0]);
+            acc[4] += t[5] / t[0];
+            acc[5] += t[6] / t[0];
+            acc[6] += t[7] / t[0];
+        }
+        for (int q = 0; q < 7; ++q) out7[q] = (float)(acc[q] / B);
+    });
+}
+
+cad_status cad_ray_directions(const float* K, int B, int H, int W, float* rays, void* stream) {
+    return guard([&] {
+        require(K && rays && B > 0 && H > 0 && W > 0, "bad arguments");
+        cad::ray_directions(K, B, H, W, rays, S(stream));
+        HIPCHK(hipGetLastError());
+    });
+}
+
+// ---------------- operator-level entry points ----------------
+cad_status cad_op_conv3x3_fwd(const float* x, int64_t ldx, int xcoff, int cin, const float* w, int cout, float* y,
+                              int64_t ldy, int ycoff, int B, int H, int W, void* stream) {
+    return guard([&] {
+        require(cin % 4 == 0 && cout % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && xcoff % 4 == 0 && ycoff % 4 == 0,
+                "channels / strides must be multiples of 4");
+        cad::conv3x3_fwd(x, ldx, xcoff, cin, w, cout, y, ldy, ycoff, B, H, W, nullptr, S(stream));
+        HIPCHK(hipGetLastError());
+    });
+}
+cad_status cad_op_conv3x3_dgrad(const float* dz, int cout, const float* w, int cin, float* dx, int64_t lddx, int B,
+                                int H, int W, void* stream) {
+    return guard([&] {
+        require(cin % 4 == 0 && cout % 4 == 0, "channels must be multiples of 4");
+        float* wd = nullptr;
+        HIPCHK(hipMallocAsync((void**)&wd, sizeof(float) * (size_t)cout * 9 * cin, S(stream)));
+        cad::repack_conv_dgrad(w, wd, cout, cin, S(stream));
+        cad::conv3x3_dgrad(dz, cout, wd, cin, dx, lddx, B, H, W, S(stream));
+        HIPCHK(hipFreeAsync(wd, S(stream)));
+        HIPCHK(hipGetLastError());
+    });
+}
+cad_status cad_op_conv3x3_wgrad(const float* dz, int cout, const float* x, int64_t ldx, int xcoff, int cin, float* dw,
+                                int B, int H, int W, void* stream) {
+    return guard([&] {
+        require(cin % 4 == 0 && cout % 4 == 0, "channels must be multiples of 4");
+        const int64_t cap = cad::wgrad_slab_floats(cout, 9 * cin, B * H * W);
+        float* slab = nullptr;
+        HIPCHK(hipMallocAsync((void**)&slab, sizeof(float) * (size_t)std::max<int64_t>(cap, 4), S(stream)));
+        cad::conv3x3_wgrad(dz, cout, x, ldx, xcoff, cin, dw, B, H, W, slab, cap, S(stream));
+        HIPCHK(hipFreeAsync(slab, S(stream)));
+        HIPCHK(hipGetLastError());
+    });
+}
+cad_status cad_op_convT_fwd(const float* x, int cin, const float* w, const float* bias, int cout, float* y,
+                            int64_t ldy, int ycoff, int B, int H, int W, void* stream) {
+    return guard([&] {
+        require(cin % 4 == 0 && cout % 4 == 0, "channels must be multiples of 4");
+        float* wf = nullptr;
+        HIPCHK(hipMallocAsync((void**)&wf, sizeof(float) * (size_t)cout * 4 * cin, S(stream)));
+        cad::repack_convT_fwd(w, wf, cin, cout, S(stream));
+        cad::convT_fwd(x, cin, cin, wf, bias, cout, y, ldy, ycoff, B, H, W, S(stream));
+        HIPCHK(hipFreeAsync(wf, S(stream)));
+        HIPCHK(hipGetLastError());
+    });
+}
+cad_status cad_op_convT_dgrad(const float* g, int64_t ldg, int gcoff, int cout, const float* w, int cin, float* dx,
+                              int B, int H, int W, void* stream) {
+    return guard([&] {
+        require(cin % 4 == 0 && cout % 4 == 0, "channels must be multiples of 4");
+        cad::convT_dgrad(g, ldg, gcoff, cout, w, cin, dx, B, H, W, S(stream));
+        HIPCHK(hipGetLastError());
+    });
+}
+cad_status cad_op_convT_wgrad(const float* x, int cin, const float* g, int64_t ldg, int gcoff, int cout, float* dw,
+                              int B, int H, int W, void* stream) {
+    return guard([&] {
+        require(cin % 4 == 0 && cout % 4 == 0, "channels must be multiples of 4");
+        const int64_t cap = cad::wgrad_slab_floats(cin, 4 * cout, B * H * W);
+        float* slab = nullptr;
+        HIPCHK(hipMallocAsync((void**)&slab, sizeof(float) * (size_t)std::max<int64_t>(cap, 4), S(stream)));
+        cad::convT_wgrad(x, cin, g, ldg, gcoff, cout, dw, B, H, W, slab, cap, S(stream));
+        HIPCHK(hipFreeAsync(slab, S(stream)));
+        HIPCHK(hipGetLastError());
+    });
+}
+cad_status cad_op_maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float* out, uint8_t* idx,
+                              void* stream) {
+    return guard([&] {
+        require(C % 4 == 0, "channels must be multiples of 4");
+        cad::maxpool_fwd(x, ldx, C, B, H, W, out, idx, S(stream));
+        HIPCHK(hipGetLastError());
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,278 @@
+// Convolution / transposed-convolution kernels on the fp32 MFMA engine (gemm_mfma.hpp) and their
+// host launchers.  Reference ops replaced: torch::nn::Conv2d(k3,p1,no bias) and
+// ConvTranspose2d(k2,s2,bias) of src/models/baseline_unet.h:20-30,85 (forward) and their autograd
+// backward (dgrad + wgrad), see SURVEY.md §8(a) a1, a3, a5.
+#include <algorithm>
+#include <cstdio>
+
+#include "gemm_mfma.hpp"
+#include "kernels.hpp"
+
+namespace cad {
+
+struct EpiStore {
+    static constexpr bool STATS = false;
+    __device__ void operator()(const GemmArgs& a, int m, int n, float v) const {
+        a.C[(int64_t)m * a.ldc + a.c_coff + n] = v;
+    }
+};
+struct EpiStoreStats : EpiStore {
+    static constexpr bool STATS = true;
+};
+// ConvTranspose2d(k2,s2) pixel shuffle: n = (q=(dy,dx), co) -> high-res pixel (2y+dy, 2x+dx)
+struct EpiConvT {
+    static constexpr bool STATS = false;
+    __device__ void operator()(const GemmArgs& a, int m, int n, float v) const {
+        const int cout = a.N >> 2;
+        const int q = n / cout, co = n - q * cout;
+        const int x = m % a.W, t = m / a.W, y = t % a.H, b = t / a.H;
+        const int64_t hp = ((int64_t)b * (2 * a.H) + 2 * y + (q >> 1)) * (2 * a.W) + 2 * x + (q & 1);
+        a.C[hp * a.ldc + a.c_coff + co] = v + a.bias[co];
+    }
+};
+struct EpiSlab {   // split-K partial: slab z holds C[m][n] of K-slice z
+    static constexpr bool STATS = false;
+    __device__ void operator()(const GemmArgs& a, int m, int n, float v) const {
+        a.C[blockIdx.z * a.slab_stride + (int64_t)m * a.ldc + n] = v;
+    }
+};
+
+template <int WM, int WN, class Epi>
+__global__ __launch_bounds__(256) void k_conv3x3_fwd(GemmArgs a) {
+    using LA = KcIm2col3x3<64 * WM>;
+    using LB = KcDense<64 * WN>;
+    gemm_body<WM, WN, LA, true, LB, true>(
+        a,
+        [&](LA& l, int r0, int t) { l.init(a.A, a.lda, a.a_coff, a.a_cin, a.B, a.H, a.W, r0, t); },
+        [&](LB& l, int r0, int t) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t); }, Epi{});
+}
+
+template <int WM, int WN>
+__global__ __launch_bounds__(256) void k_convT_fwd(GemmArgs a) {
+    using LA = KcDense<64 * WM>;
+    using LB = KcDense<64 * WN>;
+    gemm_body<WM, WN, LA, true, LB, true>(
+        a, [&](LA& l, int r0, int t) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t); },
+        [&](LB& l, int r0, int t) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t); }, EpiConvT{});
+}
+
+template <int WM, int WN>
+__global__ __launch_bounds__(256) void k_convT_dgrad(GemmArgs a) {
+    using LA = KcUpGather<64 * WM>;
+    using LB = KcDense<64 * WN>;
+    gemm_body<WM, WN, LA, true, LB, true>(
+        a, [&](LA& l, int r0, int t) { l.init(a.A, a.lda, a.a_coff, a.a_cin, a.B, a.H, a.W, r0, t); },
+        [&](LB& l, int r0, int t) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t); }, EpiStore{});
+}
+
+template <int WM, int WN>
+__global__ __launch_bounds__(256) void k_conv3x3_wgrad(GemmArgs a) {
+    using LA = MNcDense<64 * WM>;
+    using LB = MNcIm2col3x3<64 * WN>;
+    gemm_body<WM, WN, LA, false, LB, false>(
+        a, [&](LA& l, int r0, int t) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t); },
+        [&](LB& l, int r0, int t) { l.init(a.Bm, a.ldb, a.b_coff, a.b_cin, a.B, a.H, a.W, r0, t); },
+        EpiSlab{});
+}
+
+template <int WM, int WN>
+__global__ __launch_bounds__(256) void k_convT_wgrad(GemmArgs a) {
+    using LA = MNcDense<64 * WM>;
+    using LB = MNcUpGather<64 * WN>;
+    gemm_body<WM, WN, LA, false, LB, false>(
+        a, [&](LA& l, int r0, int t) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t); },
+        [&](LB& l, int r0, int t) { l.init(a.Bm, a.ldb, a.b_coff, a.b_cin, a.B, a.H, a.W, r0, t); },
+        EpiSlab{});
+}
+
+// deterministic split-K reduction: dst[e] = sum_z slab[z][e]
+__global__ void k_slab_reduce(const float* __restrict__ slab, int nsplit, int64_t stride,
+                              float* __restrict__ dst, int64_t n) {
+    int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (i >= n) return;
+    float4 s = *reinterpret_cast<const float4*>(slab + i);
+    for (int z = 1; z < nsplit; ++z) {
+        float4 t = *reinterpret_cast<const float4*>(slab + z * stride + i);
+        s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+    }
+    *reinterpret_cast<float4*>(dst + i) = s;
+}
+
+// ------------------------------------------------------------------------------------------
+// host launchers
+// ------------------------------------------------------------------------------------------
+namespace {
+inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+// tile shape by output width: narrow N -> tall tiles
+enum Cfg { C41, C22, C14 };
+Cfg pick_cfg(int M, int N) {
+    if (N <= 64) return C41;
+    if (M <= 64) return C14;
+    return C22;
+}
+
+template <template <int, int> class KT, int WM, int WN>
+void launch_one(const GemmArgs& a, int splits, hipStream_t st) {
+    const dim3 grid(cdiv(a.M, 64 * WM), cdiv(a.N, 64 * WN), splits);
+    if (prof_enabled()) {
+        char name[160];
+        snprintf(name, sizeof(name), KT<WM, WN>::fmt, WM, WN);
+        prof_push(name, 2.0 * a.M * a.N * (double)a.K, st);
+        hipLaunchKernelGGL((KT<WM, WN>::fn), grid, dim3(256), 0, st, a);
+        prof_pop(st);
+    } else {
+        hipLaunchKernelGGL((KT<WM, WN>::fn), grid, dim3(256), 0, st, a);
+    }
+}
+template <template <int, int> class KT>
+void launch_cfg(Cfg c, const GemmArgs& a, int splits, hipStream_t st) {
+    switch (c) {
+        case C41: launch_one<KT, 4, 1>(a, splits, st); break;
+        case C22: launch_one<KT, 2, 2>(a, splits, st); break;
+        case C14: launch_one<KT, 1, 4>(a, splits, st); break;
+    }
+}
+// fmt = the symbol as rocprofv3 demangles it
+template <int WM, int WN> struct KConvFwd {
+    static constexpr auto fn = k_conv3x3_fwd<WM, WN, EpiStore>;
+    static constexpr const char* fmt = "void cad::k_conv3x3_fwd<%d, %d, cad::EpiStore>(cad::GemmArgs)";
+};
+template <int WM, int WN> struct KConvFwdS {
+    static constexpr auto fn = k_conv3x3_fwd<WM, WN, EpiStoreStats>;
+    static constexpr const char* fmt = "void cad::k_conv3x3_fwd<%d, %d, cad::EpiStoreStats>(cad::GemmArgs)";
+};
+template <int WM, int WN> struct KConvTFwd {
+    static constexpr auto fn = k_convT_fwd<WM, WN>;
+    static constexpr const char* fmt = "void cad::k_convT_fwd<%d, %d>(cad::GemmArgs)";
+};
+template <int WM, int WN> struct KConvTDgrad {
+    static constexpr auto fn = k_convT_dgrad<WM, WN>;
+    static constexpr const char* fmt = "void cad::k_convT_dgrad<%d, %d>(cad::GemmArgs)";
+};
+template <int WM, int WN> struct KConvWgrad {
+    static constexpr auto fn = k_conv3x3_wgrad<WM, WN>;
+    static constexpr const char* fmt = "void cad::k_conv3x3_wgrad<%d, %d>(cad::GemmArgs)";
+};
+template <int WM, int WN> struct KConvTWgrad {
+    static constexpr auto fn = k_convT_wgrad<WM, WN>;
+    static constexpr const char* fmt = "void cad::k_convT_wgrad<%d, %d>(cad::GemmArgs)";
+};
+
+int tile_m(Cfg c) { return c == C41 ? 256 : c == C22 ? 128 : 64; }
+int tile_n(Cfg c) { return c == C41 ? 64 : c == C22 ? 128 : 256; }
+
+// split-K planning for the weight-gradient GEMMs: aim for >= ~2048 workgroups, >= 32 K-stages each
+int plan_splits(const GemmArgs& a, Cfg c, int64_t slab_cap_floats) {
+    const int tiles = cdiv(a.M, tile_m(c)) * cdiv(a.N, tile_n(c));
+    const int nk = cdiv(a.K, BK);
+    int s = std::max(1, std::min(cdiv(2048, tiles), nk / 32));
+    const int64_t per = (int64_t)a.M * a.N;
+    if (slab_cap_floats > 0) s = (int)std::max<int64_t>(1, std::min<int64_t>(s, slab_cap_floats / per));
+    return s;
+}
+}  // namespace
+
+void conv3x3_fwd(const float* x, int64_t ldx, int xcoff, int cin, const float* w, int cout, float* y,
+                 int64_t ldy, int ycoff, int B, int H, int W, float* stats, hipStream_t st) {
+    GemmArgs a{};
+    a.M = B * H * W; a.N = cout; a.K = 9 * cin;
+    a.B = B; a.H = H; a.W = W;
+    a.A = x; a.lda = ldx; a.a_coff = xcoff; a.a_cin = cin;
+    a.Bm = w; a.ldb = 9 * cin; a.b_coff = 0;
+    a.C = y; a.ldc = ldy; a.c_coff = ycoff;
+    a.stats = stats;
+    a.kstages_per_split = cdiv(a.K, BK);
+    Cfg c = pick_cfg(a.M, a.N);
+    if (stats) launch_cfg<KConvFwdS>(c, a, 1, st); else launch_cfg<KConvFwd>(c, a, 1, st);
+}
+
+int conv3x3_stats_rows(int B, int H, int W, int cout) {
+    Cfg c = pick_cfg(B * H * W, cout);
+    return cdiv((int64_t)B * H * W, tile_m(c));
+}
+
+void convT_fwd(const float* x, int64_t ldx, int cin, const float* wf, const float* bias, int cout,
+               float* y, int64_t ldy, int ycoff, int B, int H, int W, hipStream_t st) {
+    GemmArgs a{};
+    a.M = B * H * W; a.N = 4 * cout; a.K = cin;
+    a.B = B; a.H = H; a.W = W;
+    a.A = x; a.lda = ldx; a.a_coff = 0;
+    a.Bm = wf; a.ldb = cin;
+    a.C = y; a.ldc = ldy; a.c_coff = ycoff; a.bias = bias;
+    a.kstages_per_split = cdiv(a.K, BK);
+    launch_cfg<KConvTFwd>(pick_cfg(a.M, a.N), a, 1, st);
+}
+
+void conv3x3_dgrad(const float* dz, int cout, const float* wd, int cin, float* dx, int64_t lddx,
+                   int B, int H, int W, hipStream_t st) {
+    GemmArgs a{};
+    a.M = B * H * W; a.N = cin; a.K = 9 * cout;
+    a.B = B; a.H = H; a.W = W;
+    a.A = dz; a.lda = cout; a.a_coff = 0; a.a_cin = cout;
+    a.Bm = wd; a.ldb = 9 * cout;
+    a.C = dx; a.ldc = lddx; a.c_coff = 0;
+    a.kstages_per_split = cdiv(a.K, BK);
+    launch_cfg<KConvFwd>(pick_cfg(a.M, a.N), a, 1, st);
+}
+
+void convT_dgrad(const float* g, int64_t ldg, int gcoff, int cout, const float* wm, int cin, float* dx,
+                 int B, int H, int W, hipStream_t st) {
+    GemmArgs a{};
+    a.M = B * H * W; a.N = cin; a.K = 4 * cout;
+    a.B = B; a.H = H; a.W = W;
+    a.A = g; a.lda = ldg; a.a_coff = gcoff; a.a_cin = cout;
+    a.Bm = wm; a.ldb = 4 * cout;
+    a.C = dx; a.ldc = cin; a.c_coff = 0;
+    a.kstages_per_split = cdiv(a.K, BK);
+    launch_cfg<KConvTDgrad>(pick_cfg(a.M, a.N), a, 1, st);
+}
+
+int64_t wgrad_slab_floats(int M, int N, int Kpix) {
+    GemmArgs a{};
+    a.M = M; a.N = N; a.K = Kpix;
+    Cfg c = pick_cfg(M, N);
+    return (int64_t)plan_splits(a, c, 0) * M * N;
+}
+
+static void finish_slabs(float* slab, int splits, int64_t per, float* dw, hipStream_t st) {
+    hipLaunchKernelGGL(k_slab_reduce, dim3(cdiv(per / 4, 256)), dim3(256), 0, st, slab, splits, per, dw, per);
+}
+
+void conv3x3_wgrad(const float* dz, int cout, const float* x, int64_t ldx, int xcoff, int cin, float* dw,
+                   int B, int H, int W, float* slab, int64_t slab_cap, hipStream_t st) {
+    GemmArgs a{};
+    a.M = cout; a.N = 9 * cin; a.K = B * H * W;
+    a.B = B; a.H = H; a.W = W;
+    a.A = dz; a.lda = cout; a.a_coff = 0;
+    a.Bm = x; a.ldb = ldx; a.b_coff = xcoff; a.b_cin = cin;
+    Cfg c = pick_cfg(a.M, a.N);
+    int s = plan_splits(a, c, slab_cap);
+    a.kstages_per_split = cdiv(cdiv(a.K, BK), s);
+    s = cdiv(cdiv(a.K, BK), a.kstages_per_split);
+    const int64_t per = (int64_t)a.M * a.N;
+    a.ldc = a.N; a.slab_stride = per;
+    a.C = s == 1 ? dw : slab;
+    launch_cfg<KConvWgrad>(c, a, s, st);
+    if (s > 1) finish_slabs(slab, s, per, dw, st);
+}
+
+void convT_wgrad(const float* x, int cin, const float* g, int64_t ldg, int gcoff, int cout, float* dw,
+                 int B, int H, int W, float* slab, int64_t slab_cap, hipStream_t st) {
+    GemmArgs a{};
+    a.M = cin; a.N = 4 * cout; a.K = B * H * W;
+    a.B = B; a.H = H; a.W = W;
+    a.A = x; a.lda = cin; a.a_coff = 0;
+    a.Bm = g; a.ldb = ldg; a.b_coff = gcoff; a.b_cin = cout;
+    Cfg c = pick_cfg(a.M, a.N);
+    int s = plan_splits(a, c, slab_cap);
+    a.kstages_per_split = cdiv(cdiv(a.K, BK), s);
+    s = cdiv(cdiv(a.K, BK), a.kstages_per_split);
+    const int64_t per = (int64_t)a.M * a.N;
+    a.ldc = a.N; a.slab_stride = per;
+    a.C = s == 1 ? dw : slab;
+    launch_cfg<KConvTWgrad>(c, a, s, st);
+    if (s > 1) finish_slabs(slab, s, per, dw, st);
+}
+
+}  // namespace cad

@@ -1,0 +1,97 @@
+// Internal (C++) launch API of the HIP kernels.  All activations are NHWC fp32; "ld" is the row
+// stride in floats between consecutive pixels, "coff" the channel offset inside a row (so the
+// decoder concat buffer [pix][skip | up] is read and written in place).  Every launcher is
+// asynchronous on the given stream and allocates nothing (graph-capture safe).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cad {
+
+// ---------------- launch profiler (host/profiler.cpp) ----------------
+bool prof_enabled();
+void prof_push(const char* name, double flops, hipStream_t st);
+void prof_pop(hipStream_t st);
+
+// ---------------- convolutions (conv_kernels.hip) ----------------
+// y = conv3x3(x) (+ per-tile BN partials [rows][2][cout] when stats != nullptr)
+void conv3x3_fwd(const float* x, int64_t ldx, int xcoff, int cin, const float* w, int cout, float* y,
+                 int64_t ldy, int ycoff, int B, int H, int W, float* stats, hipStream_t st);
+int conv3x3_stats_rows(int B, int H, int W, int cout);
+// dx[pix][ci] = conv3x3(dz, wd) with wd = repacked [ci][tap'][co]
+void conv3x3_dgrad(const float* dz, int cout, const float* wd, int cin, float* dx, int64_t lddx,
+                   int B, int H, int W, hipStream_t st);
+// dw[co][tap][ci] = sum_pix dz[pix][co] * im2col(x)[pix][tap,ci]
+void conv3x3_wgrad(const float* dz, int cout, const float* x, int64_t ldx, int xcoff, int cin, float* dw,
+                   int B, int H, int W, float* slab, int64_t slab_cap, hipStream_t st);
+// ConvTranspose2d(k2,s2): (B,H,W,cin) -> (B,2H,2W,cout) written at channel offset ycoff of rows ldy
+void convT_fwd(const float* x, int64_t ldx, int cin, const float* wf, const float* bias, int cout,
+               float* y, int64_t ldy, int ycoff, int B, int H, int W, hipStream_t st);
+void convT_dgrad(const float* g, int64_t ldg, int gcoff, int cout, const float* wm, int cin, float* dx,
+                 int B, int H, int W, hipStream_t st);
+void convT_wgrad(const float* x, int cin, const float* g, int64_t ldg, int gcoff, int cout, float* dw,
+                 int B, int H, int W, float* slab, int64_t slab_cap, hipStream_t st);
+int64_t wgrad_slab_floats(int M, int N, int Kpix);
+
+// ---------------- NN elementwise / reductions (nn_kernels.hip) ----------------
+// column partial sums: part[s][c] (double) over row slices; returns number of slices
+int colsum_slices(int64_t R);
+void colsum(const float* x, int64_t ld, int coff, int64_t R, int C, double* part, hipStream_t st);
+void colsum_finalize(const double* part, int S, int C, float* dst, float scale, hipStream_t st);
+// BatchNorm2d (train mode) from conv-epilogue partials [rows][2][C]
+void bn_fwd_finalize(const float* tile_part, int rows, int C, int64_t count, const float* gamma,
+                     const float* beta, float* run_mean, float* run_var, float momentum, float eps,
+                     double* scratch, float* mean, float* invstd, float* scale, float* shift,
+                     hipStream_t st);
+// eval-mode BN coefficients from running statistics
+void bn_eval_coeffs(const float* gamma, const float* beta, const float* run_mean, const float* run_var,
+                    int C, float eps, float* mean, float* invstd, float* scale, float* shift, hipStream_t st);
+void bn_relu_fwd(const float* y, int C, const float* scale, const float* shift, float* out, int64_t ldo,
+                 int ocoff, int64_t M, hipStream_t st);
+// BN+ReLU backward: dy = k1*dz - k2 - k3*xhat, dz = g*[y*scale+shift > 0];
+// writes dgamma/dbeta (grad buffer) and dy (dense [M][C])
+void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, const float* mean,
+                 const float* invstd, const float* scale, const float* shift, const float* gamma,
+                 int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
+                 hipStream_t st);
+void maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float* out, uint8_t* idx,
+                 hipStream_t st);
+void maxpool_bwd(const float* dout, const uint8_t* idx, int C, int B, int H, int W, float* dx,
+                 int64_t lddx, hipStream_t st);
+void rgb_to_nhwc4(const float* rgb, float* out, int B, int H, int W, hipStream_t st);
+void head_fwd(const float* a, int C, const float* w, const float* b, float max_depth, float* sig,
+              float* pred, int64_t M, hipStream_t st);
+void head_bwd(const float* a, int C, const float* w, const float* dpred, const float* sig,
+              float max_depth, float* da, int64_t M, double* scratch, float* dw, float* db,
+              hipStream_t st);
+// computeDepthMetrics partial sums per (sample, block): {n, |d|/g, d^2/g, d^2, dlog^2, a1, a2, a3}
+int metrics_blocks(int64_t HW);
+void depth_metrics_partials(const float* pred, const float* gt, int B, int64_t HW, double* part, int nb,
+                            hipStream_t st);
+void repack_conv_dgrad(const float* w, float* wd, int cout, int cin, hipStream_t st);
+void repack_convT_fwd(const float* wm, float* wf, int cin, int cout, hipStream_t st);
+
+// ---------------- losses (loss_kernels.hip) ----------------
+struct LossWorkspace {
+    double* part;        // partial sums
+    float* scal;         // scalars: see loss_kernels.hip
+    float* pyr;          // log-pooled pyramid (pred, gt) for scales 1..3
+    int64_t part_cap;
+};
+int64_t loss_workspace_floats(int B, int H, int W);
+int64_t loss_part_doubles(int B, int H, int W);
+// total/components -> out[5] = {total, si, grad, smooth, reproj}; dpred = dL/dpred
+void loss_fwd_bwd(const float* pred, const float* gt, const float* rgb, const float* K, int B, int H,
+                  int W, const float w[4], float* out5, float* dpred, LossWorkspace ws, hipStream_t st);
+
+// ---------------- optimizer (optim_kernels.hip) ----------------
+int sumsq_blocks(int64_t n);
+void grad_norm_clip(const float* g, int64_t n, float max_norm, float prescale, double* scratch,
+                    float* norm_coef, hipStream_t st);
+void adam_step(float* p, float* g, float* m, float* v, int64_t n, const float* norm_coef, float lr,
+               float b1, float b2, float eps, float wd, int step, hipStream_t st);
+
+// ---------------- conditioning (cond_kernels.hip) ----------------
+void ray_directions(const float* K, int B, int H, int W, float* rays_nchw, hipStream_t st);
+
+}  // namespace cad

@@ -1,0 +1,455 @@
+// Memory-bound NN kernels of the U-Net step: BatchNorm2d (train/eval),
+// ReLU, MaxPool2d(2), ConvTranspose bias grad, the 1x1 depth head with sigmoid*max_depth, layout
+// conversion of the NCHW rgb batch, weight repacks.  All NHWC fp32, float4-vectorised, and every
+// reduction is deterministic (fixed-order partial slabs reduced in fp64; no atomics).
+//
+// Reference semantics:
+//   BatchNorm2d: torch/nn/options/batchnorm.h:20-34 defaults (eps 1e-5, momentum 0.1, affine),
+//     batch statistics for normalisation (biased var), unbiased var for running_var.
+//   MaxPool2d(2): first maximum in kernel scan order wins (strict >), NaN propagates.
+//   head: baseline_unet.h:191-192  x = out_conv(x); x = sigmoid(x) * max_depth
+#include <algorithm>
+
+#include "kernels.hpp"
+
+namespace cad {
+namespace {
+inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+inline int ew_blocks(int64_t n) { return (int)std::min<int64_t>(std::max<int64_t>(1, cdiv(n, 256)), 8192); }
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// generic deterministic column reduction: part[s][o][c] = sum_{rows r in slice s} op(r, c)[o]
+// ------------------------------------------------------------------------------------------
+template <int NOUT, class Op>
+__global__ void k_colreduce(Op op, int64_t R, int C, int64_t rows_per_slice, double* part) {
+    const int CX = blockDim.x, RY = blockDim.y;
+    const int C4 = C >> 2;
+    const int c4 = blockIdx.x * CX + threadIdx.x;
+    const int64_t r0 = (int64_t)blockIdx.y * rows_per_slice;
+    const int64_t r1 = min(R, r0 + rows_per_slice);
+    double acc[NOUT][4];
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[o][e] = 0.0;
+    if (c4 < C4)
+        for (int64_t r = r0 + threadIdx.y; r < r1; r += RY) op(r, c4, acc);
+    extern __shared__ double red[];   // [RY][CX][NOUT*4]
+    double* mine = red + ((int64_t)threadIdx.y * CX + threadIdx.x) * NOUT * 4;
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) mine[o * 4 + e] = acc[o][e];
+    __syncthreads();
+    if (threadIdx.y == 0 && c4 < C4) {
+        for (int y = 1; y < RY; ++y) {
+            const double* o2 = red + ((int64_t)y * CX + threadIdx.x) * NOUT * 4;
+#pragma unroll
+            for (int o = 0; o < NOUT; ++o)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[o][e] += o2[o * 4 + e];
+        }
+#pragma unroll
+        for (int o = 0; o < NOUT; ++o)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                part[((int64_t)blockIdx.y * NOUT + o) * C + c4 * 4 + e] = acc[o][e];
+    }
+}
+
+// tot[n] = sum_s part[s][n] (fixed order), optional float copy dst[n] = scale * tot[n]
+__global__ void k_colfinal(const double* part, int S, int N, double* tot, float* dst, float scale) {
+    const int n = blockIdx.x * 64 + threadIdx.x;
+    const int sy = threadIdx.y;   // 4 slice lanes
+    double s = 0.0;
+    if (n < N)
+        for (int i = sy; i < S; i += 4) s += part[(int64_t)i * N + n];
+    __shared__ double red[4][64];
+    red[sy][threadIdx.x] = s;
+    __syncthreads();
+    if (sy == 0 && n < N) {
+        s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+        if (tot) tot[n] = s;
+        if (dst) dst[n] = (float)(s * scale);
+    }
+}
+
+namespace {
+struct OpSum {
+    const float* x; int64_t ld; int coff;
+    __device__ void operator()(int64_t r, int c4, double (&acc)[1][4]) const {
+        float4 v = *reinterpret_cast<const float4*>(x + r * ld + coff + c4 * 4);
+        acc[0][0] += v.x; acc[0][1] += v.y; acc[0][2] += v.z; acc[0][3] += v.w;
+    }
+};
+struct OpBnBwd {
+    const float *g, *y, *mean, *invstd, *scale, *shift;
+    int64_t ldg; int gcoff, C;
+    __device__ void operator()(int64_t r, int c4, double (&acc)[2][4]) const {
+        float4 gv = *reinterpret_cast<const float4*>(g + r * ldg + gcoff + c4 * 4);
+        float4 yv = *reinterpret_cast<const float4*>(y + r * C + c4 * 4);
+        const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, ya[4] = {yv.x, yv.y, yv.z, yv.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int c = c4 * 4 + e;
+            const float z = ya[e] * scale[c] + shift[c];
+            const float dz = z > 0.f ? ga[e] : 0.f;
+            const float xh = (ya[e] - mean[c]) * invstd[c];
+            acc[0][e] += dz;
+            acc[1][e] += (double)dz * xh;
+        }
+    }
+};
+struct OpHeadBwd {
+    const float *a, *dpred, *sig; float md; int C;
+    __device__ void operator()(int64_t r, int c4, double (&acc)[2][4]) const {
+        const float s = sig[r];
+        const float dp = dpred[r] * md * ((1.f - s) * s);
+        float4 v = *reinterpret_cast<const float4*>(a + r * C + c4 * 4);
+        acc[0][0] += (double)dp * v.x; acc[0][1] += (double)dp * v.y;
+        acc[0][2] += (double)dp * v.z; acc[0][3] += (double)dp * v.w;
+        if (c4 == 0) acc[1][0] += dp;
+    }
+};
+
+template <int NOUT, class Op>
+int launch_colreduce(const Op& op, int64_t R, int C, double* part, hipStream_t st) {
+    const int C4 = C >> 2;
+    const int CX = std::min(C4, 64);
+    const int RY = std::max(1, 256 / CX);
+    const int S = colsum_slices(R);
+    const int64_t rps = (R + S - 1) / S;
+    const size_t shm = (size_t)RY * CX * NOUT * 4 * sizeof(double);
+    hipLaunchKernelGGL((k_colreduce<NOUT, Op>), dim3(cdiv(C4, CX), S), dim3(CX, RY), shm, st, op, R, C, rps, part);
+    return S;
+}
+void launch_colfinal(const double* part, int S, int N, double* tot, float* dst, float scale, hipStream_t st) {
+    hipLaunchKernelGGL(k_colfinal, dim3(cdiv(N, 64)), dim3(64, 4), 0, st, part, S, N, tot, dst, scale);
+}
+}  // namespace
+
+int colsum_slices(int64_t R) { return (int)std::max<int64_t>(1, std::min<int64_t>(512, R / 1024)); }
+
+void colsum(const float* x, int64_t ld, int coff, int64_t R, int C, double* part, hipStream_t st) {
+    launch_colreduce<1>(OpSum{x, ld, coff}, R, C, part, st);
+}
+void colsum_finalize(const double* part, int S, int C, float* dst, float scale, hipStream_t st) {
+    launch_colfinal(part, S, C, nullptr, dst, scale, st);
+}
+
+// ------------------------------------------------------------------------------------------
+// BatchNorm forward
+// ------------------------------------------------------------------------------------------
+__global__ void k_bn_stats(const double* tot, int C, int64_t count, const float* gamma, const float* beta,
+                           float* rmean, float* rvar, float momentum, float eps, float* mean,
+                           float* invstd, float* scale, float* shift) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const double mu = tot[c] / (double)count;
+    double var = tot[C + c] / (double)count - mu * mu;
+    if (var < 0.0) var = 0.0;
+    const float is = (float)(1.0 / sqrt(var + (double)eps));
+    mean[c] = (float)mu;
+    invstd[c] = is;
+    const float sc = gamma[c] * is;
+    scale[c] = sc;
+    shift[c] = beta[c] - (float)mu * sc;
+    if (rmean) {
+        const double unb = count > 1 ? var * (double)count / (double)(count - 1) : var;
+        rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mu;
+        rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
+    }
+}
+
+void bn_fwd_finalize(const float* tile_part, int rows, int C, int64_t count, const float* gamma,
+                     const float* beta, float* run_mean, float* run_var, float momentum, float eps,
+                     double* scratch, float* mean, float* invstd, float* scale, float* shift,
+                     hipStream_t st) {
+    double* tot = scratch;
+    double* part = scratch + 2 * C;
+    const int S = launch_colreduce<1>(OpSum{tile_part, 2 * C, 0}, rows, 2 * C, part, st);
+    launch_colfinal(part, S, 2 * C, tot, nullptr, 1.f, st);
+    hipLaunchKernelGGL(k_bn_stats, dim3(cdiv(C, 64)), dim3(64), 0, st, tot, C, count, gamma, beta,
+                       run_mean, run_var, momentum, eps, mean, invstd, scale, shift);
+}
+
+__global__ void k_bn_eval(const float* gamma, const float* beta, const float* rm, const float* rv, int C,
+                          float eps, float* mean, float* invstd, float* scale, float* shift) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const float is = 1.f / sqrtf(rv[c] + eps);
+    mean[c] = rm[c];
+    invstd[c] = is;
+    scale[c] = gamma[c] * is;
+    shift[c] = beta[c] - rm[c] * gamma[c] * is;
+}
+void bn_eval_coeffs(const float* gamma, const float* beta, const float* run_mean, const float* run_var,
+                    int C, float eps, float* mean, float* invstd, float* scale, float* shift, hipStream_t st) {
+    hipLaunchKernelGGL(k_bn_eval, dim3(cdiv(C, 64)), dim3(64), 0, st, gamma, beta, run_mean, run_var, C, eps,
+                       mean, invstd, scale, shift);
+}
+
+__global__ void k_bn_relu_fwd(const float* __restrict__ y, int C, const float* __restrict__ scale,
+                              const float* __restrict__ shift, float* __restrict__ out, int64_t ldo,
+                              int ocoff, int64_t n4) {
+    const int C4 = C >> 2;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / C4;
+        const int c = (int)(i - r * C4) * 4;
+        float4 v = *reinterpret_cast<const float4*>(y + i * 4);
+        float4 s = *reinterpret_cast<const float4*>(scale + c);
+        float4 t = *reinterpret_cast<const float4*>(shift + c);
+        float4 o;
+        o.x = fmaxf(v.x * s.x + t.x, 0.f);
+        o.y = fmaxf(v.y * s.y + t.y, 0.f);
+        o.z = fmaxf(v.z * s.z + t.z, 0.f);
+        o.w = fmaxf(v.w * s.w + t.w, 0.f);
+        *reinterpret_cast<float4*>(out + r * ldo + ocoff + c) = o;
+    }
+}
+void bn_relu_fwd(const float* y, int C, const float* scale, const float* shift, float* out, int64_t ldo,
+                 int ocoff, int64_t M, hipStream_t st) {
+    const int64_t n4 = M * C / 4;
+    hipLaunchKernelGGL(k_bn_relu_fwd, dim3(ew_blocks(n4)), dim3(256), 0, st, y, C, scale, shift, out, ldo, ocoff, n4);
+}
+
+// ------------------------------------------------------------------------------------------
+// BatchNorm + ReLU backward
+// ------------------------------------------------------------------------------------------
+__global__ void k_bn_bwd_coef(const double* tot, int C, int64_t M, const float* gamma, const float* invstd,
+                              float* coef, float* dgamma, float* dbeta) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const double sdz = tot[c], sdzx = tot[C + c];
+    dgamma[c] = (float)sdzx;
+    dbeta[c] = (float)sdz;
+    const float k1 = gamma[c] * invstd[c];
+    coef[c] = k1;
+    coef[C + c] = (float)(k1 * sdz / (double)M);
+    coef[2 * C + c] = (float)(k1 * sdzx / (double)M);
+}
+__global__ void k_bn_relu_bwd(const float* __restrict__ g, int64_t ldg, int gcoff, const float* __restrict__ y,
+                              int C, const float* __restrict__ mean, const float* __restrict__ invstd,
+                              const float* __restrict__ scale, const float* __restrict__ shift,
+                              const float* __restrict__ coef, float* __restrict__ dy, int64_t n4) {
+    const int C4 = C >> 2;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / C4;
+        const int c0 = (int)(i - r * C4) * 4;
+        float4 gv = *reinterpret_cast<const float4*>(g + r * ldg + gcoff + c0);
+        float4 yv = *reinterpret_cast<const float4*>(y + i * 4);
+        const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, ya[4] = {yv.x, yv.y, yv.z, yv.w};
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int c = c0 + e;
+            const float z = ya[e] * scale[c] + shift[c];
+            const float dz = z > 0.f ? ga[e] : 0.f;
+            const float xh = (ya[e] - mean[c]) * invstd[c];
+            o[e] = coef[c] * dz - coef[C + c] - coef[2 * C + c] * xh;
+        }
+        *reinterpret_cast<float4*>(dy + i * 4) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+}
+void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, const float* mean,
+                 const float* invstd, const float* scale, const float* shift, const float* gamma,
+                 int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
+                 hipStream_t st) {
+    double* tot = scratch;
+    double* part = scratch + 2 * C;
+    OpBnBwd op{g, y, mean, invstd, scale, shift, ldg, gcoff, C};
+    const int S = launch_colreduce<2>(op, M, C, part, st);
+    launch_colfinal(part, S, 2 * C, tot, nullptr, 1.f, st);
+    hipLaunchKernelGGL(k_bn_bwd_coef, dim3(cdiv(C, 64)), dim3(64), 0, st, tot, C, M, gamma, invstd, coef, dgamma, dbeta);
+    const int64_t n4 = M * C / 4;
+    hipLaunchKernelGGL(k_bn_relu_bwd, dim3(ew_blocks(n4)), dim3(256), 0, st, g, ldg, gcoff, y, C, mean, invstd,
+                       scale, shift, coef, dy, n4);
+}
+
+// ------------------------------------------------------------------------------------------
+// MaxPool2d(2) (baseline_unet.h:55 / :62), argmax kept as uint8 in scan order 0..3
+// ------------------------------------------------------------------------------------------
+__global__ void k_maxpool_fwd(const float* __restrict__ x, int64_t ldx, int C, int B, int H, int W,
+                              float* __restrict__ out, uint8_t* __restrict__ idx, int64_t n4) {
+    const int C4 = C >> 2, Ho = H >> 1, Wo = W >> 1;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t op = i / C4;
+        const int c = (int)(i - op * C4) * 4;
+        const int xo = (int)(op % Wo);
+        const int64_t t = op / Wo;
+        const int yo = (int)(t % Ho);
+        const int b = (int)(t / Ho);
+        const int64_t p00 = ((int64_t)b * H + 2 * yo) * W + 2 * xo;
+        const int64_t pp[4] = {p00, p00 + 1, p00 + W, p00 + W + 1};
+        float best[4];
+        uint8_t arg[4] = {0, 0, 0, 0};
+        {
+            float4 v = *reinterpret_cast<const float4*>(x + pp[0] * ldx + c);
+            best[0] = v.x; best[1] = v.y; best[2] = v.z; best[3] = v.w;
+        }
+#pragma unroll
+        for (int k = 1; k < 4; ++k) {
+            float4 v = *reinterpret_cast<const float4*>(x + pp[k] * ldx + c);
+            const float va[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (va[e] > best[e] || isnan(va[e])) { best[e] = va[e]; arg[e] = (uint8_t)k; }
+        }
+        *reinterpret_cast<float4*>(out + op * C + c) = make_float4(best[0], best[1], best[2], best[3]);
+        *reinterpret_cast<uchar4*>(idx + op * C + c) = make_uchar4(arg[0], arg[1], arg[2], arg[3]);
+    }
+}
+void maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float* out, uint8_t* idx,
+                 hipStream_t st) {
+    const int64_t n4 = (int64_t)B * (H / 2) * (W / 2) * C / 4;
+    hipLaunchKernelGGL(k_maxpool_fwd, dim3(ew_blocks(n4)), dim3(256), 0, st, x, ldx, C, B, H, W, out, idx, n4);
+}
+// dx[argmax] += dout  (in place on the skip half of the decoder concat gradient)
+__global__ void k_maxpool_bwd(const float* __restrict__ dout, const uint8_t* __restrict__ idx, int C, int B,
+                              int H, int W, float* __restrict__ dx, int64_t lddx, int64_t n4) {
+    const int C4 = C >> 2, Ho = H >> 1, Wo = W >> 1;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t op = i / C4;
+        const int c = (int)(i - op * C4) * 4;
+        const int xo = (int)(op % Wo);
+        const int64_t t = op / Wo;
+        const int yo = (int)(t % Ho);
+        const int b = (int)(t / Ho);
+        const int64_t p00 = ((int64_t)b * H + 2 * yo) * W + 2 * xo;
+        float4 d = *reinterpret_cast<const float4*>(dout + op * C + c);
+        uchar4 a = *reinterpret_cast<const uchar4*>(idx + op * C + c);
+        const float da[4] = {d.x, d.y, d.z, d.w};
+        const uint8_t aa[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int64_t p = p00 + (aa[e] >> 1) * W + (aa[e] & 1);
+            dx[p * lddx + c + e] += da[e];
+        }
+    }
+}
+void maxpool_bwd(const float* dout, const uint8_t* idx, int C, int B, int H, int W, float* dx,
+                 int64_t lddx, hipStream_t st) {
+    const int64_t n4 = (int64_t)B * (H / 2) * (W / 2) * C / 4;
+    hipLaunchKernelGGL(k_maxpool_bwd, dim3(ew_blocks(n4)), dim3(256), 0, st, dout, idx, C, B, H, W, dx, lddx, n4);
+}
+
+// ------------------------------------------------------------------------------------------
+// layout, head, repacks
+// ------------------------------------------------------------------------------------------
+__global__ void k_rgb_to_nhwc4(const float* __restrict__ rgb, float* __restrict__ out, int64_t HW, int64_t n) {
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = p / HW, yx = p - b * HW;
+        const float* s = rgb + b * 3 * HW + yx;
+        *reinterpret_cast<float4*>(out + p * 4) = make_float4(s[0], s[HW], s[2 * HW], 0.f);
+    }
+}
+void rgb_to_nhwc4(const float* rgb, float* out, int B, int H, int W, hipStream_t st) {
+    const int64_t n = (int64_t)B * H * W;
+    hipLaunchKernelGGL(k_rgb_to_nhwc4, dim3(ew_blocks(n)), dim3(256), 0, st, rgb, out, (int64_t)H * W, n);
+}
+
+__global__ void k_head_fwd(const float* __restrict__ a, int C, const float* __restrict__ w,
+                           const float* __restrict__ b, float md, float* __restrict__ sig,
+                           float* __restrict__ pred, int64_t M) {
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < M; p += (int64_t)gridDim.x * blockDim.x) {
+        const float* row = a + p * C;
+        float z = 0.f;
+        for (int c = 0; c < C; c += 4) {
+            float4 v = *reinterpret_cast<const float4*>(row + c);
+            z += v.x * w[c] + v.y * w[c + 1] + v.z * w[c + 2] + v.w * w[c + 3];
+        }
+        z += b[0];
+        const float s = 1.f / (1.f + expf(-z));
+        sig[p] = s;
+        pred[p] = s * md;
+    }
+}
+void head_fwd(const float* a, int C, const float* w, const float* b, float max_depth, float* sig,
+              float* pred, int64_t M, hipStream_t st) {
+    hipLaunchKernelGGL(k_head_fwd, dim3(ew_blocks(M)), dim3(256), 0, st, a, C, w, b, max_depth, sig, pred, M);
+}
+
+__global__ void k_head_da(const float* __restrict__ w, int C, const float* __restrict__ dpred,
+                          const float* __restrict__ sig, float md, float* __restrict__ da, int64_t n4) {
+    const int C4 = C >> 2;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / C4;
+        const int c = (int)(i - r * C4) * 4;
+        const float s = sig[r];
+        const float dp = dpred[r] * md * ((1.f - s) * s);
+        *reinterpret_cast<float4*>(da + i * 4) = make_float4(dp * w[c], dp * w[c + 1], dp * w[c + 2], dp * w[c + 3]);
+    }
+}
+void head_bwd(const float* a, int C, const float* w, const float* dpred, const float* sig,
+              float max_depth, float* da, int64_t M, double* scratch, float* dw, float* db,
+              hipStream_t st) {
+    const int64_t n4 = M * C / 4;
+    hipLaunchKernelGGL(k_head_da, dim3(ew_blocks(n4)), dim3(256), 0, st, w, C, dpred, sig, max_depth, da, n4);
+    double* part = scratch + 2 * C;
+    const int S = launch_colreduce<2>(OpHeadBwd{a, dpred, sig, max_depth, C}, M, C, part, st);
+    // part[s][0][c] -> dw ; part[s][1][0] -> db
+    launch_colfinal(part, S, 2 * C, scratch, nullptr, 1.f, st);
+    hipLaunchKernelGGL(k_colfinal, dim3(1), dim3(64, 4), 0, st, scratch, 1, C, nullptr, dw, 1.f);
+    hipLaunchKernelGGL(k_colfinal, dim3(1), dim3(64, 4), 0, st, scratch + C, 1, 1, nullptr, db, 1.f);
+}
+
+// computeDepthMetrics (tensorboard_trainer_enhanced.h:400-439): mask gt > 0
+__global__ __launch_bounds__(256) void k_metrics(const float* __restrict__ pred, const float* __restrict__ gt,
+                                                 int64_t HW, double* part, int nb) {
+    const int b = blockIdx.y;
+    double v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < HW; i += (int64_t)nb * 256) {
+        const float p = pred[b * HW + i], g = gt[b * HW + i];
+        if (!(g > 0.f)) continue;
+        const float ad = fabsf(p - g);
+        const float ld = fabsf(logf(p + 1e-8f) - logf(g + 1e-8f));
+        const float r = fmaxf(p / g, g / p);
+        v[0] += 1.0; v[1] += ad / g; v[2] += (ad * ad) / g; v[3] += ad * ad; v[4] += ld * ld;
+        v[5] += r < 1.25f; v[6] += r < 1.5625f; v[7] += r < 1.953125f;
+    }
+    __shared__ double red[4][8];
+    for (int q = 0; q < 8; ++q) {
+        double x = v[q];
+        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][q] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x < 8)
+        part[((int64_t)b * nb + blockIdx.x) * 8 + threadIdx.x] =
+            red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+int metrics_blocks(int64_t HW) { return std::max(1, std::min(64, cdiv(HW, 256))); }
+void depth_metrics_partials(const float* pred, const float* gt, int B, int64_t HW, double* part, int nb,
+                            hipStream_t st) {
+    hipLaunchKernelGGL(k_metrics, dim3(nb, B), dim3(256), 0, st, pred, gt, HW, part, nb);
+}
+
+// conv3x3 dgrad weights: wd[ci][t][co] = w[co][8-t][ci]
+__global__ void k_repack_conv_dgrad(const float* __restrict__ w, float* __restrict__ wd, int cout, int cin) {
+    const int64_t n = (int64_t)cout * 9 * cin;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int co = (int)(i % cout);
+        const int64_t t2 = i / cout;
+        const int t = (int)(t2 % 9);
+        const int ci = (int)(t2 / 9);
+        wd[i] = w[((int64_t)co * 9 + (8 - t)) * cin + ci];
+    }
+}
+void repack_conv_dgrad(const float* w, float* wd, int cout, int cin, hipStream_t st) {
+    hipLaunchKernelGGL(k_repack_conv_dgrad, dim3(ew_blocks((int64_t)cout * 9 * cin)), dim3(256), 0, st, w, wd, cout, cin);
+}
+// convT forward weights: wf[q][co][ci] = wm[ci][q][co]
+__global__ void k_repack_convT_fwd(const float* __restrict__ wm, float* __restrict__ wf, int cin, int cout) {
+    const int64_t n = (int64_t)4 * cout * cin;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int ci = (int)(i % cin);
+        const int64_t qc = i / cin;   // q*cout + co
+        wf[i] = wm[(int64_t)ci * 4 * cout + qc];
+    }
+}
+void repack_convT_fwd(const float* wm, float* wf, int cin, int cout, hipStream_t st) {
+    hipLaunchKernelGGL(k_repack_convT_fwd, dim3(ew_blocks((int64_t)4 * cout * cin)), dim3(256), 0, st, wm, wf, cin, cout);
+}
+
+}  // namespace cad

@@ -1,0 +1,338 @@
+"""Python host mirror of the reference's hot-path operator API, on libcad_hip.so.
+
+Class and method names follow the reference so that a caller (and the parity tests) read like
+the reference's own code:
+
+  BaselineUNet            BaselineUNetImpl           src/models/baseline_unet.h:122-208
+  CombinedDepthLoss       CombinedDepthLoss          src/loss/depth_loss.h:366-479
+  Adam                    torch::optim::Adam         (options built at tensorboard_trainer_enhanced.h:97-101)
+  clip_grad_norm_         torch::nn::utils::clip_grad_norm_ (enhanced.h:300-302)
+  Trainer.train_step      TensorBoardTrainerEnhanced::trainEpoch body, enhanced.h:287-304
+
+torch is used only as device-memory / stream / torch.distributed plumbing: every computation on the
+path runs in the HIP kernels behind the C ABI.  Tensors are torch CUDA (HIP) tensors in the
+reference's NCHW fp32 layout.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from . import _abi
+from ._abi import check
+
+
+def _stream(device=None):
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _ptr(t: torch.Tensor):
+    assert t.is_cuda and t.is_contiguous() and t.dtype == torch.float32, "expected contiguous fp32 device tensor"
+    return C.c_void_p(t.data_ptr())
+
+
+class BaselineUNet:
+    """BaselineUNetImpl(in_channels, init_features, max_depth) on MI355X.
+
+    Extra keyword-only arguments size the device workspace (the reference allocates per call)."""
+
+    def __init__(self, in_channels=3, init_features=64, max_depth=10.0, *, batch, height, width, device=0):
+        self.lib = _abi.load()
+        self.device = torch.device("cuda", device)
+        self.in_channels, self.init_features, self.max_depth = in_channels, init_features, max_depth
+        self.batch, self.height, self.width = batch, height, width
+        desc = _abi.UnetDesc(in_channels, init_features, max_depth, batch, height, width)
+        h = C.c_void_p()
+        check(self.lib.cad_unet_create(C.byref(desc), device, C.byref(h)), "cad_unet_create")
+        self.h = h
+        self._param_info = [self._info(0, i) for i in range(self.lib.cad_unet_num_params(h))]
+        self._buffer_info = [self._info(1, i) for i in range(self.lib.cad_unet_num_buffers(h))]
+        n = C.c_int64()
+        check(self.lib.cad_unet_flat(h, None, None, C.byref(n)), "cad_unet_flat")
+        self.n_flat = n.value
+        # flat slabs owned by torch so torch.distributed (RCCL) can all-reduce them in place
+        self.flat_params = torch.zeros(self.n_flat, dtype=torch.float32, device=self.device)
+        self.flat_grads = torch.zeros(self.n_flat, dtype=torch.float32, device=self.device)
+        check(self.lib.cad_unet_use_external_slabs(h, _ptr(self.flat_params), _ptr(self.flat_grads)),
+              "cad_unet_use_external_slabs")
+        self.num_stages = self.lib.cad_unet_num_stages(h)
+        self.stage_ranges = []
+        for s in range(self.num_stages):
+            off, cnt = C.c_int64(), C.c_int64()
+            check(self.lib.cad_unet_stage_grad_range(h, s, C.byref(off), C.byref(cnt)), "stage range")
+            self.stage_ranges.append((off.value, cnt.value))
+        self.training = True
+        self._out = None
+
+    def _info(self, kind, idx):
+        name = C.c_char_p()
+        nd = C.c_int()
+        shape = (C.c_int64 * 4)()
+        check(self.lib.cad_unet_tensor_info(self.h, kind, idx, C.byref(name), C.byref(nd), shape), "tensor_info")
+        return name.value.decode(), tuple(shape[i] for i in range(nd.value))
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            self.lib.cad_unet_destroy(h)
+            self.h = None
+
+    # ---- torch::nn::Module surface used by the trainer ----
+    def train(self, mode=True):
+        self.training = bool(mode)
+        check(self.lib.cad_unet_train(self.h, int(mode)), "cad_unet_train")
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+    def count_parameters(self) -> int:
+        return int(self.lib.cad_unet_count_parameters(self.h))
+
+    def _get(self, kind, idx, shape):
+        out = np.empty(int(np.prod(shape)) if shape else 1, np.float32)
+        check(self.lib.cad_unet_get_tensor(self.h, kind, idx, out.ctypes.data_as(_abi.FP), out.size), "get_tensor")
+        return torch.from_numpy(out.reshape(shape))
+
+    def named_parameters(self):
+        torch.cuda.synchronize(self.device)
+        return OrderedDict((n, self._get(0, i, s)) for i, (n, s) in enumerate(self._param_info))
+
+    def named_buffers(self):
+        torch.cuda.synchronize(self.device)
+        return OrderedDict((n, self._get(1, i, s)) for i, (n, s) in enumerate(self._buffer_info))
+
+    def state_dict(self):
+        d = self.named_parameters()
+        d.update(self.named_buffers())
+        return d
+
+    def load_state_dict(self, state, strict=True):
+        torch.cuda.synchronize(self.device)
+        names = {n: (0, i, s) for i, (n, s) in enumerate(self._param_info)}
+        names.update({n: (1, i, s) for i, (n, s) in enumerate(self._buffer_info)})
+        missing = [n for n in names if n not in state]
+        if strict and missing:
+            raise KeyError(f"missing keys: {missing[:5]}")
+        for n, (kind, i, s) in names.items():
+            if n not in state:
+                continue
+            v = np.ascontiguousarray(torch.as_tensor(state[n]).detach().cpu().float().numpy())
+            assert tuple(v.shape) == tuple(s), f"{n}: shape {v.shape} != {s}"
+            check(self.lib.cad_unet_set_tensor(self.h, kind, i, v.ctypes.data_as(_abi.FP), v.size), f"set {n}")
+
+    def grads(self):
+        torch.cuda.synchronize(self.device)
+        out = OrderedDict()
+        for i, (n, s) in enumerate(self._param_info):
+            g = np.empty(int(np.prod(s)), np.float32)
+            check(self.lib.cad_unet_get_grad(self.h, i, g.ctypes.data_as(_abi.FP), g.size), "get_grad")
+            out[n] = torch.from_numpy(g.reshape(s))
+        return out
+
+    # ---- forward / backward ----
+    def forward(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        B, Cc, H, W = x.shape
+        assert Cc == self.in_channels and H == self.height and W == self.width, "input shape mismatch"
+        if out is None:
+            out = torch.empty((B, 1, H, W), dtype=torch.float32, device=self.device)
+        check(self.lib.cad_unet_forward(self.h, _ptr(x), _ptr(out), B, _stream(self.device)), "cad_unet_forward")
+        return out
+
+    __call__ = forward
+
+    def backward(self, ddepth: torch.Tensor, on_stage=None):
+        """Backward of the last train-mode forward. on_stage(stage, offset, count) is called after
+        each stage is enqueued (gradients of flat_grads[offset:offset+count] are then final on the
+        stream) — the hook the data-parallel trainer uses to overlap RCCL all-reduce."""
+        st = _stream(self.device)
+        if on_stage is None:
+            check(self.lib.cad_unet_backward(self.h, _ptr(ddepth), st), "cad_unet_backward")
+            return
+        for s in range(self.num_stages):
+            check(self.lib.cad_unet_backward_stage(self.h, s, _ptr(ddepth), st), f"backward stage {s}")
+            on_stage(s, *self.stage_ranges[s])
+
+    def last_grad_norm(self) -> float:
+        v = C.c_float()
+        check(self.lib.cad_unet_last_grad_norm(self.h, C.byref(v), _stream(self.device)), "last_grad_norm")
+        return float(v.value)
+
+
+def clip_grad_norm_(model: BaselineUNet, max_norm: float, prescale: float = 1.0):
+    """torch::nn::utils::clip_grad_norm_ over all parameters (device-resident total norm)."""
+    check(model.lib.cad_clip_grad_norm(model.h, float(max_norm), float(prescale), _stream(model.device)), "clip")
+
+
+class Adam:
+    """torch::optim::Adam(params, AdamOptions(lr).betas(b).eps(eps).weight_decay(wd)) — coupled L2."""
+
+    def __init__(self, model: BaselineUNet, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        self.model = model
+        self.lib = model.lib
+        o = _abi.AdamOpts(lr, betas[0], betas[1], eps, weight_decay)
+        h = C.c_void_p()
+        check(self.lib.cad_adam_create(model.h, C.byref(o), C.byref(h)), "cad_adam_create")
+        self.h = h
+
+    def step(self):
+        check(self.lib.cad_adam_step(self.h, _stream(self.model.device)), "cad_adam_step")
+
+    def zero_grad(self):
+        """No-op: every backward overwrites the whole gradient slab (set_to_none semantics)."""
+
+    def set_lr(self, lr):
+        check(self.lib.cad_adam_set_lr(self.h, float(lr)), "set_lr")
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            self.lib.cad_adam_destroy(h)
+            self.h = None
+
+
+class CombinedDepthLoss:
+    """CombinedDepthLoss(si_weight, grad_weight, smooth_weight, reproj_weight) with its backward."""
+
+    def __init__(self, si_weight=1.0, grad_weight=0.1, smooth_weight=0.001, reproj_weight=0.01, *, batch, height,
+                 width, device=0):
+        self.lib = _abi.load()
+        self.device = torch.device("cuda", device)
+        self.weights = (si_weight, grad_weight, smooth_weight, reproj_weight)
+        self.height, self.width = height, width
+        h = C.c_void_p()
+        check(self.lib.cad_loss_create(si_weight, grad_weight, smooth_weight, reproj_weight, batch, height, width,
+                                       device, C.byref(h)), "cad_loss_create")
+        self.h = h
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            self.lib.cad_loss_destroy(h)
+            self.h = None
+
+    def forward_with_intrinsics(self, pred, gt, image, intrinsics, loss5=None, dpred=None):
+        """forwardWithIntrinsics + backward. Returns (loss5, dpred): loss5 = device tensor
+        [total, si, grad, smooth, reproj]; dpred = dL/dpred (B,1,H,W)."""
+        B = pred.shape[0]
+        assert pred.shape[2] == self.height and pred.shape[3] == self.width
+        K = intrinsics.reshape(B, 3, 3).contiguous()
+        if loss5 is None:
+            loss5 = torch.empty(5, dtype=torch.float32, device=self.device)
+        if dpred is None:
+            dpred = torch.empty_like(pred)
+        check(self.lib.cad_loss_forward_backward(self.h, _ptr(pred), _ptr(gt), _ptr(image), _ptr(K), B, _ptr(loss5),
+                                                 _ptr(dpred), _stream(self.device)), "cad_loss_forward_backward")
+        return loss5, dpred
+
+    forwardWithIntrinsics = forward_with_intrinsics
+
+    def get_components_with_intrinsics(self, pred, gt, image, intrinsics):
+        loss5, _ = self.forward_with_intrinsics(pred, gt, image, intrinsics)
+        v = loss5.cpu().tolist()
+        return {"si_loss": v[1], "grad_loss": v[2], "smooth_loss": v[3], "reproj_loss": v[4]}
+
+    getComponentsWithIntrinsics = get_components_with_intrinsics
+
+
+def depth_metrics(pred: torch.Tensor, gt: torch.Tensor) -> dict:
+    """computeDepthMetrics (enhanced.h:400-439) per sample, averaged over the batch."""
+    lib = _abi.load()
+    B, _, H, W = pred.shape
+    out = (C.c_float * 7)()
+    check(lib.cad_depth_metrics(_ptr(pred), _ptr(gt), B, H, W, out, _stream(pred.device)), "cad_depth_metrics")
+    keys = ["abs_rel", "sq_rel", "rmse", "rmse_log", "a1", "a2", "a3"]
+    return {k: float(out[i]) for i, k in enumerate(keys)}
+
+
+def ray_directions(K: torch.Tensor, height: int, width: int) -> torch.Tensor:
+    """RayDirectionComputer::computeRayDirections for a batch of K (B,3,3) -> (B,3,H,W)."""
+    lib = _abi.load()
+    B = K.shape[0]
+    out = torch.empty((B, 3, height, width), dtype=torch.float32, device=K.device)
+    check(lib.cad_ray_directions(_ptr(K.contiguous()), B, height, width, _ptr(out), _stream(K.device)), "rays")
+    return out
+
+
+class GradBucketer:
+    """Decoder-first gradient buckets for the data-parallel all-reduce.
+
+    Backward stages finish in decreasing flat-slab offset order (head, dec1..dec4, bottleneck,
+    enc4..enc1), so consecutive stages form contiguous slices.  A slice is launched (async, RCCL over
+    xGMI via torch.distributed) as soon as it holds >= bucket_elems floats or the last stage ends;
+    the launch records an event on the current stream, so the collective overlaps the remaining
+    backward kernels.  Every element is reduced exactly once (SUM; the 1/world mean is folded into
+    clip + Adam)."""
+
+    def __init__(self, flat: torch.Tensor, num_stages: int, bucket_elems: int, process_group=None):
+        self.flat, self.num_stages, self.bucket_elems, self.pg = flat, num_stages, bucket_elems, process_group
+        self.pending = []
+        self.lo = self.hi = None
+        self.buckets = []
+
+    def on_stage(self, stage, off, cnt):
+        lo, hi = off, off + cnt
+        self.lo = lo if self.lo is None else min(self.lo, lo)
+        self.hi = hi if self.hi is None else max(self.hi, hi)
+        if self.hi - self.lo >= self.bucket_elems or stage == self.num_stages - 1:
+            self.flush()
+
+    def flush(self):
+        import torch.distributed as dist
+        if self.lo is None:
+            return
+        self.buckets.append((self.lo, self.hi))
+        self.pending.append(dist.all_reduce(self.flat[self.lo:self.hi], group=self.pg, async_op=True))
+        self.lo = self.hi = None
+
+    def wait(self):
+        for w in self.pending:
+            w.wait()
+        self.pending = []
+
+
+class Trainer:
+    """One optimisation step of TensorBoardTrainerEnhanced::trainEpoch (enhanced.h:287-304):
+    zero_grad, forward, forwardWithIntrinsics, backward, clip_grad_norm_(max 1.0), Adam.step.
+
+    Data-parallel: with `process_group` set, gradient buckets are all-reduced
+    (RCCL over xGMI via torch.distributed) as soon as their backward stage is enqueued, overlapping
+    the rest of the backward; the mean (1/world) is folded into clip + Adam.  BN statistics and
+    loss masks stay per replica (DDP semantics, no SyncBN)."""
+
+    def __init__(self, model: BaselineUNet, loss_fn: CombinedDepthLoss, lr=1e-4, weight_decay=1e-5,
+                 grad_clip=1.0, use_grad_clip=True, process_group=None, bucket_mb=25.0):
+        self.model, self.loss_fn = model, loss_fn
+        self.optimizer = Adam(model, lr=lr, weight_decay=weight_decay)
+        self.grad_clip = grad_clip if use_grad_clip else float("inf")
+        self.pg = process_group
+        self.world = 1
+        if process_group is not None:
+            import torch.distributed as dist
+            self.world = dist.get_world_size(process_group)
+        self.bucket_elems = int(bucket_mb * (1 << 20) / 4)
+        self.pred = None
+        self.loss5 = torch.zeros(5, dtype=torch.float32, device=model.device)
+
+    def train_step(self, rgb, gt, K):
+        m = self.model
+        m.train()
+        self.optimizer.zero_grad()
+        if self.pred is None or self.pred.shape[0] != rgb.shape[0]:
+            self.pred = torch.empty((rgb.shape[0], 1, m.height, m.width), dtype=torch.float32, device=m.device)
+            self.dpred = torch.empty_like(self.pred)
+        m.forward(rgb, out=self.pred)
+        self.loss_fn.forward_with_intrinsics(self.pred, gt, rgb, K, loss5=self.loss5, dpred=self.dpred)
+        if self.world > 1:
+            bk = GradBucketer(m.flat_grads, m.num_stages, self.bucket_elems, self.pg)
+            m.backward(self.dpred, on_stage=bk.on_stage)
+            bk.wait()
+            clip_grad_norm_(m, self.grad_clip, prescale=1.0 / self.world)
+        else:
+            m.backward(self.dpred)
+            clip_grad_norm_(m, self.grad_clip)
+        self.optimizer.step()
+        return self.loss5

@@ -1,0 +1,174 @@
+/*
+ * cad.h — C ABI of libcad_hip.so, the MI355X (gfx950) implementation of the camera-aware depth
+ * training step of RyoK3N/Camera-Aware-Neural-Networks-for-Few-View-Depth-Estimation.
+ *
+ * Boundary.  Each entry point replaces one reference interface on the hot path
+ * (paths relative to the reference checkout):
+ *   cad_unet_create / destroy       BaselineUNetImpl(in_channels, init_features, max_depth)
+ *                                   src/models/baseline_unet.h:144-166 (+ TORCH_MODULE holder :208)
+ *   cad_unet_count_parameters       BaselineUNetImpl::count_parameters        baseline_unet.h:200-206
+ *   cad_unet_tensor_info/get/set    torch::nn::Module::named_parameters()/named_buffers() order and
+ *                                   shapes (registration order, baseline_unet.h:20-30,53-56,79-81,
+ *                                   147-165); used by torch::save / load and the trainer
+ *   cad_unet_train                  Module::train()/eval()  (enhanced.h:259, :341)
+ *   cad_unet_forward                BaselineUNetImpl::forward                 baseline_unet.h:174-195
+ *   cad_loss_create/forward_backward CombinedDepthLoss(si,grad,smooth,reproj) + forwardWithIntrinsics
+ *                                   + the autograd backward of the loss       src/loss/depth_loss.h:366-433
+ *   cad_loss_get_components         getComponentsWithIntrinsics               depth_loss.h:454-467
+ *   cad_unet_backward[_stage]       loss.backward() through the U-Net         enhanced.h:297
+ *   cad_clip_grad_norm              torch::nn::utils::clip_grad_norm_         enhanced.h:300-302
+ *   cad_adam_create/step            torch::optim::Adam(AdamOptions(lr).weight_decay(wd)) / step()
+ *                                   enhanced.h:97-101, :304
+ *   cad_unet_flat                   flat gradient slab for the data-parallel RCCL all-reduce (new:
+ *                                   the reference is single-device)
+ *   cad_depth_metrics               computeDepthMetrics (abs_rel ...)          enhanced.h:400-439
+ *   cad_ray_directions              RayDirectionComputer::computeRayDirections
+ *                                   src/preprocessing/ray_direction_computer.cpp:17-62
+ *   cad_op_*                        single operators of the step (conv, convT, BN, pool, ...), the
+ *                                   ATen calls the reference dispatches
+ *
+ * Conventions: all tensor pointers are DEVICE pointers owned by the caller unless a handle owns
+ * them; tensors crossing the boundary use the reference's NCHW fp32 layout (rgb (B,3,H,W), depth
+ * (B,1,H,W), K (B,3,3) row-major).  Every call that launches work takes an explicit stream
+ * (a hipStream_t passed as void*; NULL = default stream) and is asynchronous unless documented.
+ * Status codes replace exceptions; cad_last_error() returns the thread-local message of the last
+ * failing call.  Handles are not thread-safe: one handle per device per host thread.
+ */
+#ifndef CAD_CAD_H
+#define CAD_CAD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CAD_ABI_VERSION 1
+
+typedef enum {
+    CAD_OK = 0,
+    CAD_ERR_INVALID = 1, /* bad argument / shape */
+    CAD_ERR_HIP = 2,     /* HIP runtime error */
+    CAD_ERR_OOM = 3,     /* device allocation failed */
+    CAD_ERR_STATE = 4    /* call out of order (e.g. backward before a train-mode forward) */
+} cad_status;
+
+typedef struct cad_unet cad_unet;
+typedef struct cad_loss cad_loss;
+typedef struct cad_adam cad_adam;
+
+typedef struct {
+    int in_channels;   /* 3 */
+    int init_features; /* f (64 default, 96 in train_config_production.yaml) */
+    float max_depth;   /* 10.0 */
+    int max_batch;     /* activation workspace is sized for this batch */
+    int height;        /* H, W: must be divisible by 16 (the reference's pad branch is then a no-op) */
+    int width;
+} cad_unet_desc;
+
+typedef struct {
+    float lr;           /* optimization.learning_rate (1e-4) */
+    float beta1, beta2; /* 0.9, 0.999 */
+    float eps;          /* 1e-8 */
+    float weight_decay; /* coupled L2 (torch::optim::Adam), 1e-5 */
+} cad_adam_opts;
+
+/* ---- library ---- */
+int cad_abi_version(void);
+const char* cad_last_error(void);
+cad_status cad_device_count(int* n);
+cad_status cad_set_device(int device);
+cad_status cad_stream_synchronize(void* stream);
+
+/* ---- model: BaselineUNetImpl ---- */
+cad_status cad_unet_create(const cad_unet_desc* desc, int device, cad_unet** out);
+void cad_unet_destroy(cad_unet* h);
+int64_t cad_unet_count_parameters(const cad_unet* h);
+int cad_unet_num_params(const cad_unet* h);  /* tensors in named_parameters() */
+int cad_unet_num_buffers(const cad_unet* h); /* float tensors in named_buffers() */
+/* kind: 0 = parameter, 1 = buffer.  shape has up to 4 entries (reference layout). */
+cad_status cad_unet_tensor_info(const cad_unet* h, int kind, int idx, const char** name, int* ndim,
+                                int64_t shape[4]);
+/* host <-> device copies in the REFERENCE layout (OIHW conv, (Cin,Cout,2,2) convT); synchronous */
+cad_status cad_unet_set_tensor(cad_unet* h, int kind, int idx, const float* host, int64_t numel);
+cad_status cad_unet_get_tensor(const cad_unet* h, int kind, int idx, float* host, int64_t numel);
+cad_status cad_unet_get_grad(const cad_unet* h, int idx, float* host, int64_t numel);
+cad_status cad_unet_train(cad_unet* h, int train); /* 1 = train(), 0 = eval() */
+/* flat parameter / gradient slabs (internal packed layout; n = elements incl. alignment padding) */
+cad_status cad_unet_flat(cad_unet* h, float** params, float** grads, int64_t* n);
+/* switch the flat slabs to caller-owned device memory of cad_unet_flat()'s n floats each (e.g.
+ * buffers a collective library registers); current parameter values are copied over.  The caller
+ * keeps them alive for the handle's lifetime. */
+cad_status cad_unet_use_external_slabs(cad_unet* h, float* params, float* grads);
+
+/* forward: rgb (B,3,H,W) -> depth (B,1,H,W) in (0, max_depth).  B <= max_batch. */
+cad_status cad_unet_forward(cad_unet* h, const float* rgb, float* depth, int B, void* stream);
+
+/* backward of the last train-mode forward given dL/ddepth; writes every parameter gradient.
+ * Stage form (stage 0 .. cad_unet_num_stages()-1, in order) lets a caller overlap the gradient
+ * all-reduce of finished stages with the rest of the backward. */
+cad_status cad_unet_backward(cad_unet* h, const float* ddepth, void* stream);
+int cad_unet_num_stages(const cad_unet* h);
+cad_status cad_unet_backward_stage(cad_unet* h, int stage, const float* ddepth, void* stream);
+/* [offset, offset+count) of the flat gradient slab completed by `stage` */
+cad_status cad_unet_stage_grad_range(const cad_unet* h, int stage, int64_t* offset, int64_t* count);
+
+/* clip_grad_norm_: total = ||prescale * g||_2; g *= prescale * min(1, max_norm / (total + 1e-6))
+ * (the scaling is applied inside cad_adam_step; prescale = 1/world after a SUM all-reduce).
+ * The total norm stays on device; cad_unet_last_grad_norm() fetches it (synchronises). */
+cad_status cad_clip_grad_norm(cad_unet* h, float max_norm, float prescale, void* stream);
+cad_status cad_unet_last_grad_norm(cad_unet* h, float* total_norm, void* stream);
+
+/* ---- optimizer: torch::optim::Adam (coupled L2) over the model's flat slab ---- */
+cad_status cad_adam_create(cad_unet* model, const cad_adam_opts* opts, cad_adam** out);
+void cad_adam_destroy(cad_adam* a);
+cad_status cad_adam_step(cad_adam* a, void* stream); /* consumes the clip coefficient */
+cad_status cad_adam_set_lr(cad_adam* a, float lr);
+int64_t cad_adam_step_count(const cad_adam* a);
+
+/* ---- loss: CombinedDepthLoss ---- */
+cad_status cad_loss_create(float si_weight, float grad_weight, float smooth_weight, float reproj_weight,
+                           int max_batch, int height, int width, int device, cad_loss** out);
+void cad_loss_destroy(cad_loss* l);
+/* forwardWithIntrinsics + backward: loss5 (device, 5 floats) = {total, si, grad, smooth, reproj};
+ * dpred (device, B*H*W) = dL/dpred.  K (B,3,3) row-major. */
+cad_status cad_loss_forward_backward(cad_loss* l, const float* pred, const float* gt, const float* rgb,
+                                     const float* K, int B, float* loss5, float* dpred, void* stream);
+/* getComponentsWithIntrinsics: host copy of {total, si, grad, smooth, reproj} of the last call */
+cad_status cad_loss_get_components(cad_loss* l, float out5[5], void* stream);
+
+/* ---- metrics (computeDepthMetrics) on host-visible results: abs_rel etc. per sample, averaged */
+cad_status cad_depth_metrics(const float* pred, const float* gt, int B, int H, int W, float out7[7],
+                             void* stream);
+
+/* ---- conditioning: per-pixel unit ray directions (B,3,H,W) from K (B,3,3) ---- */
+cad_status cad_ray_directions(const float* K, int B, int H, int W, float* rays, void* stream);
+
+/* ---- launch profiler: HIP events around every MFMA GEMM launch on its own stream ---- */
+cad_status cad_profile_enable(int on);
+cad_status cad_profile_reset(void);
+/* writes a JSON array [{"name","launches","ms","gflop"}...] into buf (synchronises); returns the
+ * length needed including the terminator */
+int cad_profile_report(char* buf, int cap);
+
+/* ---- operator-level entry points (NHWC fp32; ld = floats between pixels, coff = channel offset) */
+cad_status cad_op_conv3x3_fwd(const float* x, int64_t ldx, int xcoff, int cin, const float* w_ohwi,
+                              int cout, float* y, int64_t ldy, int ycoff, int B, int H, int W,
+                              void* stream);
+cad_status cad_op_conv3x3_dgrad(const float* dz, int cout, const float* w_ohwi, int cin, float* dx,
+                                int64_t lddx, int B, int H, int W, void* stream);
+cad_status cad_op_conv3x3_wgrad(const float* dz, int cout, const float* x, int64_t ldx, int xcoff, int cin,
+                                float* dw_ohwi, int B, int H, int W, void* stream);
+cad_status cad_op_convT_fwd(const float* x, int cin, const float* w_iqo, const float* bias, int cout,
+                            float* y, int64_t ldy, int ycoff, int B, int H, int W, void* stream);
+cad_status cad_op_convT_dgrad(const float* g, int64_t ldg, int gcoff, int cout, const float* w_iqo, int cin,
+                              float* dx, int B, int H, int W, void* stream);
+cad_status cad_op_convT_wgrad(const float* x, int cin, const float* g, int64_t ldg, int gcoff, int cout,
+                              float* dw_iqo, int B, int H, int W, void* stream);
+cad_status cad_op_maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float* out,
+                              uint8_t* idx, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CAD_CAD_H */

@@ -1,0 +1,394 @@
+"""ORACLE / TEST INFRASTRUCTURE ONLY.
+
+CPU restatement (PyTorch CPU, fp32, autograd) of the reference training step that the MI355X path
+replaces.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this
+module, and only as the CHECKER: the product path (libcad_hip.so and its bindings) never calls it.
+
+Every function cites the reference file:line it restates (paths relative to /root/reference):
+
+  * BaselineUNetImpl            src/models/baseline_unet.h:14-208
+  * ScaleInvariantLoss          src/loss/depth_loss.h:20-69
+  * GradientMatchingLoss        src/loss/depth_loss.h:82-167
+  * SmoothnessLoss              src/loss/depth_loss.h:178-238
+  * ReprojectionLoss            src/loss/depth_loss.h:255-355
+  * CombinedDepthLoss           src/loss/depth_loss.h:366-479
+  * train step                  src/training/tensorboard_trainer_enhanced.h:287-304
+  * clip_grad_norm_             torch/csrc/api/include/torch/nn/utils/clip_grad.h:22-85 (LibTorch)
+  * Adam (coupled L2)           torch::optim::Adam, options built at enhanced.h:97-101
+  * computeDepthMetrics (a20)   src/training/tensorboard_trainer_enhanced.h:400-439
+
+Parity pin: tests/test_oracle_golden.py checks this restatement against fixtures produced by the
+REFERENCE itself (oracle/ref_harness.cpp compiled in place against /root/reference/src by
+oracle/Makefile, fixtures committed under tests/golden/ by oracle/gen_golden.py).
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+EPS = 1e-6
+
+# --------------------------------------------------------------------------------------------
+# Synthetic SUN-RGB-D-shaped batches; byte-identical to ref_harness.cpp.
+# --------------------------------------------------------------------------------------------
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def splitmix64(seed: int, idx: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + (idx.astype(np.uint64) + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def u01(seed: int, idx: np.ndarray) -> np.ndarray:
+    u = (splitmix64(seed, idx) >> np.uint64(32)).astype(np.uint32)
+    return (u >> np.uint32(8)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+
+
+def intrinsics_for(B: int, H: int, W: int) -> np.ndarray:
+    """Per-sample K (B,3,3): NYU/kv1 and Xtion calibrations scaled like sunrgbd_loader.cpp:480-488."""
+    K = np.zeros((B, 3, 3), np.float32)
+    sx, sy = np.float32(W / 640.0), np.float32(H / 480.0)
+    for b in range(B):
+        if b % 2 == 0:
+            fx, fy, cx, cy = 518.858, 519.470, 325.582, 253.736
+        else:
+            fx, fy, cx, cy = 570.342, 570.342, 320.0, 240.0
+        K[b, 0, 0] = np.float32(fx) * sx
+        K[b, 0, 2] = np.float32(cx) * sx
+        K[b, 1, 1] = np.float32(fy) * sy
+        K[b, 1, 2] = np.float32(cy) * sy
+        K[b, 2, 2] = 1.0
+    return K
+
+
+def synth_batch(B: int, H: int, W: int, rgb_seed: int = 0xC0FFEE, hole_seed: int = 0xD3E7):
+    """rgb (B,3,H,W) U[0,1); gt (B,1,H,W) smooth field with holes; K (B,3,3). numpy float32."""
+    rgb = u01(rgb_seed, np.arange(B * 3 * H * W, dtype=np.uint64)).reshape(B, 3, H, W)
+    b = np.arange(B, dtype=np.float64)[:, None, None]
+    v = np.arange(H, dtype=np.float64)[None, :, None]
+    u = np.arange(W, dtype=np.float64)[None, None, :]
+    ph = 2.0 * math.pi * (u / W * 1.3 + v / H * 0.7 + 0.1 * b)
+    d = np.clip(0.5 + 9.0 * (0.5 + 0.5 * np.sin(ph)), 0.5, 9.5)
+    holes = u01(hole_seed, np.arange(B * H * W, dtype=np.uint64)).reshape(B, H, W) < np.float32(0.15)
+    holes |= (np.arange(H)[None, :, None] < H // 16)
+    gt = np.where(holes, 0.0, d).astype(np.float32).reshape(B, 1, H, W)
+    return rgb, gt, intrinsics_for(B, H, W)
+
+
+# --------------------------------------------------------------------------------------------
+# Model: BaselineUNetImpl (baseline_unet.h:122-208) as named parameter/buffer dictionaries.
+# --------------------------------------------------------------------------------------------
+def _double_conv_spec(prefix, cin, cout):
+    # DoubleConvImpl ctor (baseline_unet.h:20-30): conv1 (no bias), bn1, conv2 (no bias), bn2
+    return [(prefix + "conv1.weight", (cout, cin, 3, 3)),
+            (prefix + "bn1.weight", (cout,)), (prefix + "bn1.bias", (cout,)),
+            (prefix + "conv2.weight", (cout, cout, 3, 3)),
+            (prefix + "bn2.weight", (cout,)), (prefix + "bn2.bias", (cout,))]
+
+
+def param_spec(f: int = 64, in_ch: int = 3):
+    """named_parameters() order of BaselineUNetImpl(in_ch, f) (registration order, :144-166)."""
+    spec = _double_conv_spec("enc1.", in_ch, f)
+    for i, name in enumerate(["enc2", "enc3", "enc4", "bottleneck"]):
+        spec += _double_conv_spec(f"{name}.conv.", f << i, f << (i + 1))
+    for i, name in enumerate(["dec4", "dec3", "dec2", "dec1"]):
+        cin = f << (4 - i)
+        spec += [(f"{name}.up.weight", (cin, cin // 2, 2, 2)), (f"{name}.up.bias", (cin // 2,))]
+        spec += _double_conv_spec(f"{name}.conv.", cin, cin // 2)
+    spec += [("out_conv.weight", (1, f, 1, 1)), ("out_conv.bias", (1,))]
+    return spec
+
+
+def buffer_spec(f: int = 64, in_ch: int = 3):
+    """Float BatchNorm buffers (running_mean/var) in named_buffers() order."""
+    out = []
+    for name, shape in param_spec(f, in_ch):
+        if name.endswith(".bias") and ".bn" in name:
+            base = name[: -len(".bias")]
+            out += [(base + ".running_mean", shape), (base + ".running_var", shape)]
+    return out
+
+
+def num_params(f: int = 64, in_ch: int = 3) -> int:
+    return int(sum(np.prod(s) for _, s in param_spec(f, in_ch)))
+
+
+def init_params(f: int = 64, seed: int = 42, in_ch: int = 3):
+    """torch.nn default init (kaiming_uniform(a=sqrt 5) weights, U(-1/sqrt(fan_in),..) biases,
+    BN weight 1 / bias 0) — same distributions as the LibTorch modules; not bitwise the C++ stream."""
+    g = torch.Generator().manual_seed(seed)
+    params = OrderedDict()
+    for name, shape in param_spec(f, in_ch):
+        if ".bn" in name:
+            params[name] = torch.ones(shape) if name.endswith("weight") else torch.zeros(shape)
+            continue
+        if name.endswith("weight"):
+            fan_in = shape[1] * int(np.prod(shape[2:])) if "up." not in name else shape[1] * 4
+            bound = 1.0 / math.sqrt(fan_in)  # kaiming_uniform_(a=sqrt(5)) => gain sqrt(2/6)*sqrt(3/fan)
+            params[name] = (torch.rand(shape, generator=g) * 2 - 1) * bound
+        else:
+            wshape = dict(param_spec(f, in_ch))[name[: -len("bias")] + "weight"]
+            fan_in = wshape[1] * int(np.prod(wshape[2:])) if "up." not in name else wshape[1] * 4
+            bound = 1.0 / math.sqrt(fan_in)
+            params[name] = (torch.rand(shape, generator=g) * 2 - 1) * bound
+    return params
+
+
+def init_buffers(f: int = 64, in_ch: int = 3):
+    return OrderedDict((n, torch.zeros(s) if n.endswith("mean") else torch.ones(s))
+                       for n, s in buffer_spec(f, in_ch))
+
+
+def _bn(x, p, bufs, prefix, train):
+    # torch::nn::BatchNorm2d defaults (eps 1e-5, momentum 0.1, affine, track_running_stats)
+    return F.batch_norm(x, bufs[prefix + ".running_mean"], bufs[prefix + ".running_var"],
+                        p[prefix + ".weight"], p[prefix + ".bias"], train, 0.1, 1e-5)
+
+
+def _double_conv(x, p, bufs, pre, train):
+    # DoubleConvImpl::forward (baseline_unet.h:32-43)
+    x = F.conv2d(x, p[pre + "conv1.weight"], None, 1, 1)
+    x = F.relu(_bn(x, p, bufs, pre + "bn1", train))
+    x = F.conv2d(x, p[pre + "conv2.weight"], None, 1, 1)
+    return F.relu(_bn(x, p, bufs, pre + "bn2", train))
+
+
+def _decoder(x, skip, p, bufs, pre, train):
+    # DecoderBlockImpl::forward (baseline_unet.h:83-102): up, pad-if-needed, cat({skip, up}), conv
+    x = F.conv_transpose2d(x, p[pre + "up.weight"], p[pre + "up.bias"], stride=2)
+    dh, dw = skip.shape[2] - x.shape[2], skip.shape[3] - x.shape[3]
+    if dh > 0 or dw > 0:
+        x = F.pad(x, (dw // 2, dw - dw // 2, dh // 2, dh - dh // 2))
+    return _double_conv(torch.cat([skip, x], 1), p, bufs, pre + "conv.", train)
+
+
+def unet_forward(x, p, bufs, train=True, max_depth=10.0):
+    """BaselineUNetImpl::forward (baseline_unet.h:174-195)."""
+    s1 = _double_conv(x, p, bufs, "enc1.", train)
+    s2 = _double_conv(F.max_pool2d(s1, 2), p, bufs, "enc2.conv.", train)
+    s3 = _double_conv(F.max_pool2d(s2, 2), p, bufs, "enc3.conv.", train)
+    s4 = _double_conv(F.max_pool2d(s3, 2), p, bufs, "enc4.conv.", train)
+    xb = _double_conv(F.max_pool2d(s4, 2), p, bufs, "bottleneck.conv.", train)
+    x = _decoder(xb, s4, p, bufs, "dec4.", train)
+    x = _decoder(x, s3, p, bufs, "dec3.", train)
+    x = _decoder(x, s2, p, bufs, "dec2.", train)
+    x = _decoder(x, s1, p, bufs, "dec1.", train)
+    x = F.conv2d(x, p["out_conv.weight"], p["out_conv.bias"])
+    return torch.sigmoid(x) * max_depth
+
+
+# --------------------------------------------------------------------------------------------
+# Losses (depth_loss.h)
+# --------------------------------------------------------------------------------------------
+def si_loss(pred, gt, lam=0.5, eps=EPS):
+    """ScaleInvariantLoss::forward (depth_loss.h:33-64): 0-dim result, zeros(1) when n == 0."""
+    mask = gt > eps
+    pred = torch.clamp(pred, eps, 1000.0)
+    gt = torch.clamp(gt, eps, 1000.0)
+    d = (torch.log(pred) - torch.log(gt)).masked_select(mask)
+    n = d.numel()
+    if n == 0:
+        return torch.zeros(1, dtype=pred.dtype)
+    return torch.pow(d, 2).sum() / n - lam * torch.pow(d.sum(), 2) / (n * n)
+
+
+def _grad_scale(pred, gt):
+    # GradientMatchingLoss::computeGradientLoss (depth_loss.h:135-166); the mask is unused (:137)
+    px = pred[..., 1:] - pred[..., :-1]
+    gx = gt[..., 1:] - gt[..., :-1]
+    py = pred[..., 1:, :] - pred[..., :-1, :]
+    gy = gt[..., 1:, :] - gt[..., :-1, :]
+    return torch.abs(px - gx).mean() + torch.abs(py - gy).mean()
+
+
+def grad_loss(pred, gt, num_scales=4, eps=EPS):
+    """GradientMatchingLoss::forward (depth_loss.h:95-124): shape-[1] result."""
+    total = torch.zeros(1, dtype=pred.dtype)
+    for s in range(num_scales):
+        ps, gs = pred, gt
+        if s > 0:
+            k = 2 ** s
+            ps = F.avg_pool2d(pred, k, k)
+            gs = F.avg_pool2d(gt, k, k)
+        ps = torch.log(torch.clamp(ps, eps, 1000.0))
+        gs = torch.log(torch.clamp(gs, eps, 1000.0))
+        total = total + _grad_scale(ps, gs)
+    return total / num_scales
+
+
+def smooth_loss(pred, image, eps=EPS):
+    """SmoothnessLoss::forward (depth_loss.h:189-234)."""
+    m = pred.mean((2, 3), keepdim=True)
+    n = pred / (m + eps)
+    dx = torch.abs(n[..., 1:] - n[..., :-1])
+    dy = torch.abs(n[..., 1:, :] - n[..., :-1, :])
+    ix = torch.abs(image[..., 1:] - image[..., :-1]).mean(1, keepdim=True)
+    iy = torch.abs(image[..., 1:, :] - image[..., :-1, :]).mean(1, keepdim=True)
+    return (dx * torch.exp(-ix)).mean() + (dy * torch.exp(-iy)).mean()
+
+
+def reproj_loss(pred, gt, K, eps=EPS):
+    """ReprojectionLoss::forward (depth_loss.h:268-331)."""
+    B, _, H, W = pred.shape
+    if K.dim() == 2:
+        K = K.unsqueeze(0).expand(B, 3, 3)
+    gy = torch.arange(0, H, dtype=pred.dtype).view(1, H, 1).expand(1, H, W)
+    gx = torch.arange(0, W, dtype=pred.dtype).view(1, 1, W).expand(1, H, W)
+    fx = K[:, 0, 0].view(B, 1, 1, 1)
+    fy = K[:, 1, 1].view(B, 1, 1, 1)
+    cx = K[:, 0, 2].view(B, 1, 1, 1)
+    cy = K[:, 1, 2].view(B, 1, 1, 1)
+    pX = (gx - cx) * pred / (fx + eps)
+    pY = (gy - cy) * pred / (fy + eps)
+    tX = (gx - cx) * gt / (fx + eps)
+    tY = (gy - cy) * gt / (fy + eps)
+    dX, dY, dZ = pX - tX, pY - tY, pred - gt
+    err = torch.sqrt(dX * dX + dY * dY + dZ * dZ + eps)
+    e = err.masked_select(gt > eps)
+    if e.numel() == 0:
+        return torch.zeros(1, dtype=pred.dtype)
+    return e.mean()
+
+
+def combined_loss(pred, gt, image, K, weights=(1.0, 0.1, 0.001, 0.01)):
+    """CombinedDepthLoss::forwardWithIntrinsics (depth_loss.h:416-433). Returns (total, comps)."""
+    si = si_loss(pred, gt)
+    gr = grad_loss(pred, gt)
+    sm = smooth_loss(pred, image)
+    rp = reproj_loss(pred, gt, K)
+    w = [torch.tensor(float(x), dtype=torch.float32).item() for x in weights]
+    total = w[0] * si + w[1] * gr + w[2] * sm + w[3] * rp
+    comps = {"si_loss": float(si.detach()), "grad_loss": float(gr.detach()), "smooth_loss": float(sm.detach()),
+             "reproj_loss": float(rp.detach())}
+    return total, comps
+
+
+def loss_and_dpred(pred, gt, image, K, weights=(1.0, 0.1, 0.001, 0.01)):
+    """Fused-loss reference: (total, comps, dL/dpred) for the GPU loss kernels' parity tests."""
+    p = pred.detach().clone().requires_grad_(True)
+    total, comps = combined_loss(p, gt, image, K, weights)
+    total.sum().backward()
+    return float(total), comps, p.grad.detach()
+
+
+# --------------------------------------------------------------------------------------------
+# Optimizer: clip_grad_norm_ (LibTorch clip_grad.h) + torch::optim::Adam (coupled L2)
+# --------------------------------------------------------------------------------------------
+def clip_grad_norm_(grads, max_norm=1.0):
+    norms = torch.stack([g.norm(2) for g in grads])
+    total = norms.norm(2) if len(grads) > 1 else norms[0]
+    coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
+    for g in grads:
+        g.mul_(coef)
+    return float(total)
+
+
+class Adam:
+    """torch::optim::Adam with coupled L2 weight decay (AdamOptions(lr).weight_decay(wd))."""
+
+    def __init__(self, params, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5):
+        self.params = params
+        self.lr, self.b1, self.b2, self.eps, self.wd = lr, betas[0], betas[1], eps, weight_decay
+        self.m = OrderedDict((k, torch.zeros_like(v)) for k, v in params.items())
+        self.v = OrderedDict((k, torch.zeros_like(v)) for k, v in params.items())
+        self.t = 0
+
+    @torch.no_grad()
+    def step(self, grads):
+        self.t += 1
+        bc1 = 1 - self.b1 ** self.t
+        bc2 = 1 - self.b2 ** self.t
+        for (k, p), g in zip(self.params.items(), grads):
+            if self.wd != 0:
+                g = g.add(p, alpha=self.wd)
+            self.m[k].mul_(self.b1).add_(g, alpha=1 - self.b1)
+            self.v[k].mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
+            denom = (self.v[k].sqrt() / math.sqrt(bc2)).add_(self.eps)
+            p.addcdiv_(self.m[k], denom, value=-(self.lr / bc1))
+
+
+class Trainer:
+    """One replica of TensorBoardTrainerEnhanced's step (enhanced.h:287-304) on host cores."""
+
+    def __init__(self, params, buffers, weights=(1.0, 0.1, 0.001, 0.01), lr=1e-4, wd=1e-5,
+                 clip=1.0, max_depth=10.0, dtype=torch.float32):
+        # dtype=float64 gives the exact-arithmetic yardstick the fp32 paths are both measured against
+        self.dtype = dtype
+        self.p = OrderedDict((k, v.clone().to(dtype)) for k, v in params.items())
+        self.bufs = OrderedDict((k, v.clone().to(dtype)) for k, v in buffers.items())
+        self.weights, self.clip, self.max_depth = weights, clip, max_depth
+        self.opt = Adam(self.p, lr=lr, weight_decay=wd)
+
+    def forward_backward(self, rgb, gt, K):
+        rgb, gt, K = rgb.to(self.dtype), gt.to(self.dtype), K.to(self.dtype)
+        for v in self.p.values():
+            v.requires_grad_(True)
+            v.grad = None
+        pred = unet_forward(rgb, self.p, self.bufs, True, self.max_depth)
+        pred.retain_grad()
+        loss, comps = combined_loss(pred, gt, rgb, K, self.weights)
+        loss.sum().backward()
+        grads = [v.grad.detach().clone() for v in self.p.values()]
+        for v in self.p.values():
+            v.requires_grad_(False)
+        return pred.detach(), pred.grad.detach(), float(loss), comps, grads
+
+    def apply(self, grads):
+        total = clip_grad_norm_(grads, self.clip)
+        self.opt.step(grads)
+        return total
+
+    def step(self, rgb, gt, K):
+        pred, dpred, loss, comps, grads = self.forward_backward(rgb, gt, K)
+        pre_clip = [g.clone() for g in grads]
+        total = self.apply(grads)
+        return dict(pred=pred, dpred=dpred, loss=loss, comps=comps, grads=pre_clip, norm=total)
+
+    @torch.no_grad()
+    def predict_eval(self, rgb):
+        return unet_forward(rgb, self.p, self.bufs, False, self.max_depth)
+
+
+def depth_metrics(pred, gt):
+    """computeDepthMetrics (enhanced.h:400-439) on flattened tensors."""
+    p, g = pred.reshape(-1), gt.reshape(-1)
+    m = g > 0
+    p, g = p[m], g[m]
+    if p.numel() == 0:
+        return {}
+    ad = (p - g).abs()
+    ld = (torch.log(p + 1e-8) - torch.log(g + 1e-8)).abs()
+    ratio = torch.maximum(p / g, g / p)
+    return {"abs_rel": float((ad / g).mean()), "sq_rel": float((ad * ad / g).mean()),
+            "rmse": float(torch.sqrt((ad * ad).mean())), "rmse_log": float(torch.sqrt((ld * ld).mean())),
+            "a1": float((ratio < 1.25).float().mean()), "a2": float((ratio < 1.5625).float().mean()),
+            "a3": float((ratio < 1.953125).float().mean())}
+
+
+def abs_rel_per_sample(pred, gt):
+    vals = [depth_metrics(pred[b], gt[b]).get("abs_rel") for b in range(pred.shape[0])]
+    vals = [v for v in vals if v is not None]
+    return sum(vals) / pred.shape[0]
+
+
+# --------------------------------------------------------------------------------------------
+# Golden fixture I/O (written by oracle/ref_harness.cpp)
+# --------------------------------------------------------------------------------------------
+def load_fixture(path):
+    import json
+    import os
+    with open(os.path.join(path, "manifest.json")) as fh:
+        man = json.load(fh)
+    raw = np.fromfile(os.path.join(path, "tensors.bin"), dtype="<f4")
+    out = OrderedDict()
+    for t in man["tensors"]:
+        n = int(np.prod(t["shape"])) if t["shape"] else 1
+        out[t["name"]] = torch.from_numpy(raw[t["offset"]: t["offset"] + n].reshape(t["shape"]).copy())
+    return out, man["meta"]

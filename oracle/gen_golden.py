@@ -1,0 +1,40 @@
+"""ORACLE / TEST INFRASTRUCTURE ONLY — regenerates tests/golden/ from the compiled reference.
+
+Runs oracle/_ref/ref_harness (built by `make -C oracle` from /root/reference/src headers, in this
+container only) and writes the fixtures the test-suite pins the oracle and the HIP path against.
+Run:  make -C oracle && python oracle/gen_golden.py
+All fixtures are generated single-threaded (torch::set_num_threads(1)) with manual_seed(42).
+"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+FIXTURES = {
+    # whole train step(s), default 4-term weights (train_config.yaml:89-92), f=4, 64x64
+    "train_f4_b2_64x64": ["--mode", "golden", "--f", "4", "--B", "2", "--H", "64", "--W", "64",
+                          "--steps", "3"],
+    # config-2 semantics: SI-only weights, non-square 96x128, batch 3 (odd: mixed K per sample)
+    "train_f4_b3_96x128_si": ["--mode", "golden", "--f", "4", "--B", "3", "--H", "96", "--W", "128",
+                              "--steps", "2", "--weights", "1,0,0,0"],
+    # loss-only goldens (depth_loss.h) incl. a size whose pyramid floors (50x70 -> 6x8 at k=8)
+    "loss_b2_120x160": ["--mode", "loss", "--B", "2", "--H", "120", "--W", "160"],
+    "loss_b3_50x70": ["--mode", "loss", "--B", "3", "--H", "50", "--W", "70"],
+    "loss_b2_32x48_allholes": ["--mode", "loss", "--B", "2", "--H", "32", "--W", "48", "--holes-all", "1"],
+}
+
+
+def main():
+    if not os.path.exists(HARNESS):
+        sys.exit("build the harness first: make -C oracle")
+    for name, args in FIXTURES.items():
+        out = os.path.join(GOLDEN, name)
+        os.makedirs(out, exist_ok=True)
+        subprocess.run([HARNESS, "--threads", "1", "--out", out] + args, check=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,160 @@
+"""Operator-level parity of the HIP kernels (through the C ABI's cad_op_* entry points) against
+the oracle's ATen CPU ops in fp64 — the contractions of SURVEY.md §8(a) a1-a5 at real channel
+counts on small spatial sizes, including masked tails (M, N not multiples of the tile) and the
+strided/offset views the U-Net uses for its concat buffer.  Tolerance: normalised max error
+<= 1e-5 (fp32 MFMA accumulation vs fp64)."""
+import ctypes as C
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import max_rel_err
+
+pytestmark = pytest.mark.gpu
+
+TOL = 2e-5
+
+
+def _p(t):
+    return C.c_void_p(t.data_ptr())
+
+
+def _s():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def nchw(x):
+    return x.permute(0, 3, 1, 2).contiguous()
+
+
+CONV_SHAPES = [  # B, H, W, cin, cout
+    (2, 16, 24, 4, 64), (2, 16, 16, 64, 64), (1, 8, 12, 128, 256), (2, 6, 8, 1024, 512), (3, 10, 14, 32, 16),
+    (2, 4, 4, 8, 4), (1, 30, 40, 256, 128),
+]
+
+
+@pytest.mark.parametrize("B,H,W,cin,cout", CONV_SHAPES)
+def test_conv3x3_fwd_dgrad_wgrad(cad, dev, B, H, W, cin, cout):
+    lib = cad.load_library()
+    g = torch.Generator().manual_seed(B * 1000 + cin + cout)
+    x = torch.randn(B, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)
+    dy = torch.randn(B, cout, H, W, generator=g)
+    xd, wd, dyd = x.double().requires_grad_(), w.double().requires_grad_(), dy.double()
+    y_ref = F.conv2d(xd, wd, None, 1, 1)
+    y_ref.backward(dyd)
+    # forward, written at channel offset 4 of a wider row (concat-buffer view)
+    ld = cout + 8
+    ybuf = torch.zeros(B, H, W, ld, device=dev)
+    xg, wg = nhwc(x).to(dev), w.permute(0, 2, 3, 1).contiguous().to(dev)
+    assert lib.cad_op_conv3x3_fwd(_p(xg), cin, 0, cin, _p(wg), cout, _p(ybuf), ld, 4, B, H, W, _s()) == 0
+    torch.cuda.synchronize()
+    assert max_rel_err(nchw(ybuf[..., 4:4 + cout].cpu()), y_ref.detach()) < TOL
+    assert ybuf[..., :4].abs().max().item() == 0 and ybuf[..., 4 + cout:].abs().max().item() == 0
+    # dgrad
+    dx = torch.zeros(B, H, W, cin, device=dev)
+    dyg = nhwc(dy).to(dev)
+    assert lib.cad_op_conv3x3_dgrad(_p(dyg), cout, _p(wg), cin, _p(dx), cin, B, H, W, _s()) == 0
+    torch.cuda.synchronize()
+    assert max_rel_err(nchw(dx.cpu()), xd.grad) < TOL
+    # wgrad
+    dw = torch.zeros(cout, 3, 3, cin, device=dev)
+    assert lib.cad_op_conv3x3_wgrad(_p(dyg), cout, _p(xg), cin, 0, cin, _p(dw), B, H, W, _s()) == 0
+    torch.cuda.synchronize()
+    assert max_rel_err(dw.cpu().permute(0, 3, 1, 2), wd.grad) < TOL
+
+
+def test_conv3x3_wgrad_strided_input(cad, dev):
+    """wgrad reading its input from the skip half of a concat-style buffer (ld = 2C, coff = C)."""
+    lib = cad.load_library()
+    B, H, W, cin, cout = 2, 12, 20, 32, 64
+    g = torch.Generator().manual_seed(7)
+    big = torch.randn(B, H, W, 2 * cin, generator=g)
+    x = nchw(big[..., cin:].contiguous())
+    dy = torch.randn(B, cout, H, W, generator=g)
+    xd = x.double().requires_grad_()
+    wd = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, requires_grad=True)
+    F.conv2d(xd, wd, None, 1, 1).backward(dy.double())
+    dw = torch.zeros(cout, 3, 3, cin, device=dev)
+    bg = big.to(dev)
+    assert lib.cad_op_conv3x3_wgrad(_p(nhwc(dy).to(dev)), cout, _p(bg), 2 * cin, cin, cin, _p(dw), B, H, W, _s()) == 0
+    torch.cuda.synchronize()
+    assert max_rel_err(dw.cpu().permute(0, 3, 1, 2), wd.grad) < TOL
+
+
+CONVT_SHAPES = [(2, 8, 12, 128, 64), (1, 4, 5, 1024, 512), (3, 6, 6, 32, 16), (2, 3, 4, 8, 4)]
+
+
+@pytest.mark.parametrize("B,H,W,cin,cout", CONVT_SHAPES)
+def test_convT(cad, dev, B, H, W, cin, cout):
+    lib = cad.load_library()
+    g = torch.Generator().manual_seed(cin * 7 + cout)
+    x = torch.randn(B, cin, H, W, generator=g)
+    w = torch.randn(cin, cout, 2, 2, generator=g) / cin ** 0.5
+    b = torch.randn(cout, generator=g)
+    dy = torch.randn(B, cout, 2 * H, 2 * W, generator=g)
+    xd, wdd, bd = x.double().requires_grad_(), w.double().requires_grad_(), b.double().requires_grad_()
+    y_ref = F.conv_transpose2d(xd, wdd, bd, stride=2)
+    y_ref.backward(dy.double())
+    wg = w.permute(0, 2, 3, 1).contiguous().to(dev)   # [ci][dy][dx][co]
+    # forward into the "up" half of a concat buffer
+    ybuf = torch.zeros(B, 2 * H, 2 * W, 2 * cout, device=dev)
+    xg = nhwc(x).to(dev)
+    assert lib.cad_op_convT_fwd(_p(xg), cin, _p(wg), _p(b.to(dev)), cout, _p(ybuf), 2 * cout, cout, B, H, W, _s()) == 0
+    torch.cuda.synchronize()
+    assert max_rel_err(nchw(ybuf[..., cout:].cpu()), y_ref.detach()) < TOL
+    # dgrad from the up half of a concat-gradient buffer
+    gbuf = torch.zeros(B, 2 * H, 2 * W, 2 * cout)
+    gbuf[..., cout:] = nhwc(dy)
+    gg = gbuf.to(dev)
+    dx = torch.zeros(B, H, W, cin, device=dev)
+    assert lib.cad_op_convT_dgrad(_p(gg), 2 * cout, cout, cout, _p(wg), cin, _p(dx), B, H, W, _s()) == 0
+    torch.cuda.synchronize()
+    assert max_rel_err(nchw(dx.cpu()), xd.grad) < TOL
+    dw = torch.zeros(cin, 2, 2, cout, device=dev)
+    assert lib.cad_op_convT_wgrad(_p(xg), cin, _p(gg), 2 * cout, cout, cout, _p(dw), B, H, W, _s()) == 0
+    torch.cuda.synchronize()
+    assert max_rel_err(dw.cpu().permute(0, 3, 1, 2), wdd.grad) < TOL
+
+
+def test_maxpool(cad, dev):
+    lib = cad.load_library()
+    B, H, W, Cc = 2, 10, 14, 16
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(B, Cc, H, W, generator=g)
+    x[0, 0, 0, :2] = 5.0   # tie: first in scan order must win
+    ref, ridx = F.max_pool2d(x, 2, return_indices=True)
+    buf = torch.zeros(B, H, W, 2 * Cc)
+    buf[..., :Cc] = nhwc(x)
+    bg = buf.to(dev)
+    out = torch.zeros(B, H // 2, W // 2, Cc, device=dev)
+    idx = torch.zeros(B, H // 2, W // 2, Cc, dtype=torch.uint8, device=dev)
+    assert lib.cad_op_maxpool_fwd(_p(bg), 2 * Cc, Cc, B, H, W, _p(out), _p(idx), _s()) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(nchw(out.cpu()), ref)
+    # argmax code k = 2*dy + dx must point at the same element as torch's flat index
+    k = nchw(idx.cpu()).long()
+    yo = torch.arange(H // 2).view(1, 1, -1, 1)
+    xo = torch.arange(W // 2).view(1, 1, 1, -1)
+    flat = (2 * yo + k // 2) * W + 2 * xo + k % 2
+    assert torch.equal(flat, ridx)
+
+
+def test_ray_directions(cad, dev, oracle):
+    B, H, W = 3, 24, 32
+    _, _, K = oracle.synth_batch(B, H, W)
+    rays = cad.ray_directions(torch.from_numpy(K).to(dev), H, W).cpu()
+    Kt = torch.from_numpy(K).double()
+    u = torch.arange(W, dtype=torch.float64).view(1, 1, W)
+    v = torch.arange(H, dtype=torch.float64).view(1, H, 1)
+    x = (u - Kt[:, 0, 2].view(B, 1, 1)) / Kt[:, 0, 0].view(B, 1, 1)
+    y = (v - Kt[:, 1, 2].view(B, 1, 1)) / Kt[:, 1, 1].view(B, 1, 1)
+    n = torch.sqrt(x * x + y * y + 1)
+    ref = torch.stack([x / n, y / n, (1 / n).expand(B, H, W)], 1)
+    assert (rays.double() - ref).abs().max().item() < 1e-6
+    assert torch.allclose(rays.double().norm(dim=1), torch.ones(B, H, W, dtype=torch.float64), atol=1e-6)
