@@ -67,6 +67,7 @@ SIGNATURES = {
     "cad_loss_get_components": (I, [P, FP, P]),
     "cad_depth_metrics": (I, [P, P, I, I, I, FP, P]),
     "cad_ray_directions": (I, [P, I, I, I, P, P]),
+    "cad_unet_debug_buffer": (I64, [P, C.c_char_p, FP, I64]),
     "cad_profile_enable": (I, [I]),
     "cad_profile_reset": (I, []),
     "cad_profile_report": (I, [C.c_char_p, I]),

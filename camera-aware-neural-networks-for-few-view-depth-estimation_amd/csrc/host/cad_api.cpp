@@ -661,6 +661,39 @@ cad_status cad_unet_flat(cad_unet* h, float** params, float** grads, int64_t* n)
     });
 }
 
+int64_t cad_unet_debug_buffer(cad_unet* h, const char* name, float* host, int64_t numel) {
+    const int B = h->fwd_B > 0 ? h->fwd_B : h->Bmax;
+    std::string n(name ? name : "");
+    const float* p = nullptr;
+    int64_t cnt = -1;
+    auto lvl = [&](const std::string& pre) -> int {
+        if (n.compare(0, pre.size(), pre) != 0 || n.size() < pre.size() + 1) return -1;
+        return n[pre.size()] - '0';
+    };
+    int l;
+    if (n == "x0") { p = h->x0; cnt = h->Ml(0, B) * 4; }
+    else if (n == "Sa" || n == "Sb") { p = n == "Sa" ? h->Sa : h->Sb; cnt = h->Ml(0, B) * h->Cl(0); }
+    else if (n == "Sc") { p = h->Sc; cnt = h->Ml(1, B) * h->Cl(0); }
+    else if (n == "bott") { p = h->a2_bott; cnt = h->Ml(4, B) * h->Cl(4); }
+    else if ((l = lvl("dcat")) >= 0 && l < 4) { p = h->dcat[l]; cnt = h->Ml(l, B) * 2 * h->Cl(l); }
+    else if ((l = lvl("cat")) >= 0 && l < 4) { p = h->cat[l]; cnt = h->Ml(l, B) * 2 * h->Cl(l); }
+    else if ((l = lvl("pool")) >= 1 && l <= 4) { p = h->pool[l]; cnt = h->Ml(l, B) * h->Cl(l - 1); }
+    else if ((l = lvl("dout")) >= 0 && l < 4) { p = h->dout[l]; cnt = h->Ml(l, B) * h->Cl(l); }
+    else if (((l = lvl("enc")) >= 0 && l < 5) || ((l = lvl("dec")) >= 0 && l < 4)) {
+        DoubleConv& dc = n[0] == 'e' ? h->enc[l] : h->dec[l];
+        const std::string t = n.size() > 5 ? n.substr(5) : "";
+        p = t == "y1" ? dc.y1 : t == "a1" ? dc.a1 : t == "y2" ? dc.y2 : nullptr;
+        cnt = p ? h->Ml(l, B) * h->Cl(l) : -1;
+    }
+    if (!p || cnt < 0) return -1;
+    if (host) {
+        if (numel < cnt) return -1;
+        if (hipDeviceSynchronize() != hipSuccess) return -1;
+        if (hipMemcpy(host, p, sizeof(float) * cnt, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    }
+    return cnt;
+}
+
 cad_status cad_unet_use_external_slabs(cad_unet* h, float* params, float* grads) {
     return guard([&] {
         require(params && grads, "null slab");

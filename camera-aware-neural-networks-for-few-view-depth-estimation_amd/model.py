@@ -156,6 +156,15 @@ class BaselineUNet:
             check(self.lib.cad_unet_backward_stage(self.h, s, _ptr(ddepth), st), f"backward stage {s}")
             on_stage(s, *self.stage_ranges[s])
 
+    def debug_buffer(self, name: str) -> torch.Tensor:
+        """Host copy of an internal NHWC buffer (flat) — debugging / layer-level parity only."""
+        n = self.lib.cad_unet_debug_buffer(self.h, name.encode(), None, 0)
+        if n < 0:
+            raise KeyError(name)
+        out = np.empty(n, np.float32)
+        assert self.lib.cad_unet_debug_buffer(self.h, name.encode(), out.ctypes.data_as(_abi.FP), n) == n
+        return torch.from_numpy(out)
+
     def last_grad_norm(self) -> float:
         v = C.c_float()
         check(self.lib.cad_unet_last_grad_norm(self.h, C.byref(v), _stream(self.device)), "last_grad_norm")

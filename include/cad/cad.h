@@ -144,6 +144,12 @@ cad_status cad_depth_metrics(const float* pred, const float* gt, int B, int H, i
 /* ---- conditioning: per-pixel unit ray directions (B,3,H,W) from K (B,3,3) ---- */
 cad_status cad_ray_directions(const float* K, int B, int H, int W, float* rays, void* stream);
 
+/* ---- debugging: synchronous host copy of an internal NHWC activation buffer by name
+ * ("x0", "cat<l>", "dcat<l>", "pool<l>", "dout<l>", "bott", "Sa", "Sb", "Sc",
+ *  "enc<l>.y1|a1|y2", "dec<l>.y1|a1|y2"); numel = rows*channels of the last forward's batch.
+ * Returns the element count (host may be NULL to query), or -1 for an unknown name. */
+int64_t cad_unet_debug_buffer(cad_unet* h, const char* name, float* host, int64_t numel);
+
 /* ---- launch profiler: HIP events around every MFMA GEMM launch on its own stream ---- */
 cad_status cad_profile_enable(int on);
 cad_status cad_profile_reset(void);

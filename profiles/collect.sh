@@ -1,0 +1,20 @@
+#!/bin/bash
+# Reproduce the committed profiles on a GPU box:  bash profiles/collect.sh <round-tag>
+#   1. rocprofv3 --kernel-trace --stats of bench.py (same command line as the bench leg, short)
+#   2. two SEPARATE --pmc passes (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass on gfx950)
+#   3. profiles/summarize.py -> profiles/<tag>_kernel_stats.md, profiles/pmc_traffic.json
+set -euo pipefail
+TAG=${1:-r01}
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+OUT=$ROOT/gpurun_out/prof_$TAG
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+cd "$ROOT"
+ARGS="--steps 3 --warmup 1 --no-cpu-baseline"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
+    python3 bench.py $ARGS > "$OUT/trace.json" 2> "$OUT/trace.err"
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- \
+    python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/fetch.json" 2> "$OUT/fetch.err"
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- \
+    python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/write.json" 2> "$OUT/write.err"
+python3 profiles/summarize.py "$OUT" "$TAG"

@@ -35,6 +35,8 @@ def nchw(x):
 CONV_SHAPES = [  # B, H, W, cin, cout
     (2, 16, 24, 4, 64), (2, 16, 16, 64, 64), (1, 8, 12, 128, 256), (2, 6, 8, 1024, 512), (3, 10, 14, 32, 16),
     (2, 4, 4, 8, 4), (1, 30, 40, 256, 128),
+    # M <= 64 with N > 64: the 64x256 tile (bottleneck at small images)
+    (1, 4, 4, 512, 1024), (1, 8, 8, 256, 512), (2, 3, 4, 64, 128),
 ]
 
 
