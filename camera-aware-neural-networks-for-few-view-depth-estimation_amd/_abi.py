@@ -37,6 +37,11 @@ SIGNATURES = {
     "cad_device_count": (I, [C.POINTER(I)]),
     "cad_set_device": (I, [I]),
     "cad_stream_synchronize": (I, [P]),
+    "cad_malloc": (I, [I, I64, C.POINTER(P)]),
+    "cad_free": (None, [P]),
+    "cad_memcpy": (I, [P, P, I64, I, P]),
+    "cad_adam_state": (I, [P, C.POINTER(P), C.POINTER(P)]),
+    "cad_adam_set_step_count": (I, [P, I64]),
     "cad_unet_create": (I, [C.POINTER(UnetDesc), I, C.POINTER(P)]),
     "cad_unet_destroy": (None, [P]),
     "cad_unet_count_parameters": (I64, [P]),

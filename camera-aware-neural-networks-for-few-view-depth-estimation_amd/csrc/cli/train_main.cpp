@@ -1,0 +1,390 @@
+// build/train — drop-in for the reference's `./build/train --config <yaml>` entry point
+// (src/training/train_main.cpp:279-507 driving TensorBoardTrainerEnhanced, enhanced.h:142-334),
+// on libcad_hip.so through the C++ drop-in classes of include/cad/cad.hpp.
+//
+//   build/train -c configs/train_config.yaml [-e baseline_unet] [-g 0] [-d] [--tensorboard true]
+//               [-r checkpoint.cadckpt]
+//
+// Same flags and defaults (train_main.cpp:38-45), same YAML keys (loadConfig :60-167, main :297-430),
+// same per-batch step (enhanced.h:287-304), sample-weighted epoch loss (:308,333), validation every
+// val_interval with computeDepthMetrics averaged per sample (:339-439), metrics.csv with the
+// reference's header (:104-115), checkpoints every save_interval (:218-220).  Exit 0 on success;
+// any exception prints "Error: <what>" and exits 1 (:503-506).
+// Deliberate differences: the model lives on the GPU (the reference never moves it,
+// SURVEY §0 fact 2); --resume really resumes (params + BN buffers + Adam state; the reference parses
+// and ignores it); TensorBoard events are written as a CSV of scalars (no Python tensorboard here);
+// the dataset is data.dataset_name: "synthetic" (SUN-RGB-D-shaped counter-based samples) — decoding
+// the real SUN RGB-D JPEG/PNG files needs OpenCV, absent on this image.
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <filesystem>
+#include <fstream>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "../../../include/cad/cad.hpp"
+#include "../host/yaml_lite.hpp"
+
+namespace fs = std::filesystem;
+using namespace camera_aware_depth;
+
+namespace {
+
+struct Args {
+    std::string config = "configs/train_config.yaml", experiment = "baseline_unet", resume;
+    int gpu = 0;
+    bool debug = false, tensorboard = true;
+};
+
+void usage() {
+    std::cout << "train - Train depth estimation models (MI355X)\n"
+                 "  -c, --config arg      Path to config file (default: configs/train_config.yaml)\n"
+                 "  -e, --experiment arg  Experiment name (default: baseline_unet)\n"
+                 "  -r, --resume arg      Resume from checkpoint (.cadckpt)\n"
+                 "  -g, --gpu arg         GPU ID (default: 0)\n"
+                 "  -d, --debug           Enable debug mode\n"
+                 "      --tensorboard arg Enable TensorBoard-style scalar logging (default: true)\n"
+                 "  -h, --help            Print help\n";
+}
+
+Args parse_args(int argc, char** argv) {
+    Args a;
+    for (int i = 1; i < argc; ++i) {
+        std::string k = argv[i], v;
+        auto eq = k.find('=');
+        if (eq != std::string::npos) { v = k.substr(eq + 1); k = k.substr(0, eq); }
+        auto next = [&]() -> std::string {
+            if (!v.empty()) return v;
+            if (i + 1 >= argc) throw std::runtime_error("missing value for " + k);
+            return argv[++i];
+        };
+        if (k == "-h" || k == "--help") { usage(); std::exit(0); }
+        else if (k == "-c" || k == "--config") a.config = next();
+        else if (k == "-e" || k == "--experiment") a.experiment = next();
+        else if (k == "-r" || k == "--resume") a.resume = next();
+        else if (k == "-g" || k == "--gpu") a.gpu = std::stoi(next());
+        else if (k == "-d" || k == "--debug") a.debug = v.empty() ? true : (v == "true" || v == "1");
+        else if (k == "--tensorboard") {
+            std::string t = (!v.empty() || (i + 1 < argc && argv[i + 1][0] != '-')) ? next() : "true";
+            a.tensorboard = t == "true" || t == "1";
+        } else throw std::runtime_error("unknown option " + k);
+    }
+    return a;
+}
+
+struct Config {   // the TrainingConfig fields the step uses (trainer.h:24-92)
+    int num_epochs = 50, batch_size = 8, log_interval = 10, val_interval = 1, save_interval = 5;
+    float learning_rate = 1e-4f, weight_decay = 1e-5f, grad_clip_value = 1.0f;
+    bool use_grad_clip = true;
+    float si = 1.0f, grad = 0.1f, smooth = 0.001f, reproj = 0.01f, max_depth = 10.0f;
+    int init_features = 64, height = 240, width = 320, seed = 42;
+    std::string checkpoint_dir = "./checkpoints", log_dir = "./logs", experiment_name = "baseline_unet";
+    std::string dataset = "sunrgbd";
+    int n_train = 64, n_val = 16;
+};
+
+Config load_config(const yaml_lite::Node& y, const std::string& experiment) {   // train_main.cpp:60-167
+    Config c;
+    c.experiment_name = experiment;
+    if (auto& o = y["optimization"]) {
+        c.learning_rate = o["learning_rate"].as<float>(1e-4f);
+        c.weight_decay = o["weight_decay"].as<float>(1e-5f);
+        if (o["gradient_clip"]) {
+            c.use_grad_clip = o["gradient_clip"].as<bool>(true);
+            c.grad_clip_value = o["gradient_clip_value"].as<float>(1.0f);
+        }
+    }
+    if (auto& t = y["training"]) {
+        c.num_epochs = t["num_epochs"].as<int>(50);
+        c.batch_size = t["batch_size"].as<int>(8);
+        c.log_interval = t["log_interval"].as<int>(10);
+        c.val_interval = t["val_interval"].as<int>(1);
+    }
+    if (auto& l = y["loss"]) {
+        c.si = l["si_weight"].as<float>(1.0f);
+        c.grad = l["grad_weight"].as<float>(0.1f);
+        c.smooth = l["smooth_weight"].as<float>(0.001f);
+        c.reproj = l["reproj_weight"].as<float>(0.01f);
+    }
+    if (auto& k = y["checkpointing"]) {
+        c.checkpoint_dir = k["checkpoint_dir"].as<std::string>("./checkpoints");
+        c.save_interval = k["save_interval"].as<int>(5);
+    }
+    if (auto& l = y["logging"]) c.log_dir = l["log_dir"].as<std::string>("./logs");
+    if (auto& e = y["experiment"]) {
+        c.experiment_name = e["name"].as<std::string>(experiment);
+        c.seed = e["seed"].as<int>(42);
+    }
+    if (y["experiments"] && y["experiments"][experiment]) {   // :150-160
+        auto& ex = y["experiments"][experiment];
+        if (ex["training"] && ex["training"]["batch_size"]) c.batch_size = ex["training"]["batch_size"].as<int>();
+        if (ex["experiment"] && ex["experiment"]["name"]) c.experiment_name = ex["experiment"]["name"].as<std::string>();
+    }
+    if (auto& m = y["model"]) {   // :325-333 (architecture key ignored, like the reference)
+        c.init_features = m["init_features"].as<int>(64);
+        c.max_depth = m["max_depth"].as<float>(10.0f);
+    }
+    if (auto& d = y["data"]) {
+        c.height = d["input_height"].as<int>(240);
+        c.width = d["input_width"].as<int>(320);
+        c.dataset = d["dataset_name"].as<std::string>("sunrgbd");
+        c.n_train = d["num_train_samples"].as<int>(64);
+        c.n_val = d["num_val_samples"].as<int>(16);
+    }
+    c.checkpoint_dir += "/" + c.experiment_name;   // :163-164
+    c.log_dir += "/" + c.experiment_name;
+    return c;
+}
+
+// ---- synthetic SUN-RGB-D-shaped samples (same generator as synthetic.py / SURVEY §8d) ----
+uint64_t splitmix64(uint64_t seed, uint64_t idx) {
+    uint64_t z = seed + (idx + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+float u01(uint64_t seed, uint64_t idx) { return (float)((uint32_t)(splitmix64(seed, idx) >> 32) >> 8) * (1.0f / 16777216.0f); }
+
+struct HostBatch {
+    std::vector<float> rgb, gt, K;
+};
+// sample s of a split = sample s of one virtual batch (split offsets keep train/val disjoint)
+void make_sample(int64_t s, int H, int W, float* rgb, float* gt, float* K) {
+    const int64_t HW = (int64_t)H * W;
+    for (int64_t i = 0; i < 3 * HW; ++i) rgb[i] = u01(0xC0FFEE, s * 3 * HW + i);
+    for (int v = 0; v < H; ++v)
+        for (int u = 0; u < W; ++u) {
+            const int64_t idx = s * HW + (int64_t)v * W + u;
+            double d = 0.5 + 9.0 * (0.5 + 0.5 * std::sin(2.0 * M_PI * ((double)u / W * 1.3 + (double)v / H * 0.7 + 0.1 * s)));
+            d = std::min(9.5, std::max(0.5, d));
+            if (u01(0xD3E7, idx) < 0.15f || v < H / 16) d = 0.0;
+            gt[(int64_t)v * W + u] = (float)d;
+        }
+    const bool even = s % 2 == 0;
+    const float sx = (float)W / 640.f, sy = (float)H / 480.f;
+    std::fill(K, K + 9, 0.f);
+    K[0] = (even ? 518.858f : 570.342f) * sx;
+    K[2] = (even ? 325.582f : 320.0f) * sx;
+    K[4] = (even ? 519.470f : 570.342f) * sy;
+    K[5] = (even ? 253.736f : 240.0f) * sy;
+    K[8] = 1.f;
+}
+
+// ---- checkpoint (.cadckpt): named tensors in reference layout + Adam state ----
+void save_checkpoint(const std::string& path, BaselineUNetImpl& m, optim::Adam& opt) {
+    std::ofstream f(path, std::ios::binary);
+    if (!f) throw std::runtime_error("cannot write checkpoint " + path);
+    auto ps = m.named_parameters();
+    auto bs = m.named_buffers();
+    ps.insert(ps.end(), bs.begin(), bs.end());
+    f.write("CADCKPT1", 8);
+    int32_t n = (int32_t)ps.size();
+    f.write((const char*)&n, 4);
+    for (auto& t : ps) {
+        int32_t ln = (int32_t)t.name.size(), nd = (int32_t)t.shape.size();
+        f.write((const char*)&ln, 4);
+        f.write(t.name.data(), ln);
+        f.write((const char*)&nd, 4);
+        f.write((const char*)t.shape.data(), 8 * nd);
+        f.write((const char*)t.value.data(), 4 * (int64_t)t.value.size());
+    }
+    float *mp, *vp, *pp;
+    int64_t nflat;
+    cad::check(cad_unet_flat(m.handle(), &pp, nullptr, &nflat), "flat");
+    cad::check(cad_adam_state(opt.handle(), &mp, &vp), "adam_state");
+    std::vector<float> buf((size_t)nflat);
+    int64_t step = opt.step_count();
+    f.write("ADAM", 4);
+    f.write((const char*)&step, 8);
+    f.write((const char*)&nflat, 8);
+    for (float* src : {mp, vp}) {
+        cad::check(cad_memcpy(buf.data(), src, 4 * nflat, 1, nullptr), "d2h");
+        f.write((const char*)buf.data(), 4 * nflat);
+    }
+}
+
+void load_checkpoint(const std::string& path, BaselineUNetImpl& m, optim::Adam& opt) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) throw std::runtime_error("Cannot open checkpoint: " + path);
+    char magic[8];
+    f.read(magic, 8);
+    if (std::memcmp(magic, "CADCKPT1", 8) != 0) throw std::runtime_error("not a .cadckpt file: " + path);
+    int32_t n;
+    f.read((char*)&n, 4);
+    std::vector<NamedTensor> ts((size_t)n);
+    for (auto& t : ts) {
+        int32_t ln, nd;
+        f.read((char*)&ln, 4);
+        t.name.resize((size_t)ln);
+        f.read(&t.name[0], ln);
+        f.read((char*)&nd, 4);
+        t.shape.resize((size_t)nd);
+        f.read((char*)t.shape.data(), 8 * nd);
+        int64_t cnt = 1;
+        for (auto s : t.shape) cnt *= s;
+        t.value.resize((size_t)cnt);
+        f.read((char*)t.value.data(), 4 * cnt);
+    }
+    if (m.load(ts) != n) throw std::runtime_error("checkpoint does not match the model: " + path);
+    char tag[4];
+    if (f.read(tag, 4) && std::memcmp(tag, "ADAM", 4) == 0) {
+        int64_t step, nflat, mine;
+        f.read((char*)&step, 8);
+        f.read((char*)&nflat, 8);
+        float *mp, *vp;
+        cad::check(cad_unet_flat(m.handle(), nullptr, nullptr, &mine), "flat");
+        if (nflat != mine) throw std::runtime_error("optimizer state size mismatch in " + path);
+        cad::check(cad_adam_state(opt.handle(), &mp, &vp), "adam_state");
+        std::vector<float> buf((size_t)nflat);
+        for (float* dst : {mp, vp}) {
+            f.read((char*)buf.data(), 4 * nflat);
+            cad::check(cad_memcpy(dst, buf.data(), 4 * nflat, 0, nullptr), "h2d");
+        }
+        cad::check(cad_adam_set_step_count(opt.handle(), step), "set_step");
+    }
+}
+
+int run(const Args& args) {
+    std::cout << "Loading configuration from: " << args.config << "\n";
+    yaml_lite::Node y = yaml_lite::load_file(args.config);
+    Config c = load_config(y, args.experiment);
+    if (args.debug || (y["debug"] && y["debug"]["enabled"].as<bool>(false))) {   // :297-301
+        std::cout << "Debug mode enabled - using reduced dataset\n";
+        c.num_epochs = y["debug"]["num_epochs"].as<int>(2);
+        c.log_interval = y["debug"]["log_interval"].as<int>(1);
+    }
+    if (c.dataset != "synthetic")
+        throw std::runtime_error("dataset '" + c.dataset + "': SUN RGB-D JPEG/PNG decoding needs OpenCV, which this "
+                                 "build does not include; set data.dataset_name: \"synthetic\"");
+    int ndev = 0;
+    cad::check(cad_device_count(&ndev), "device query");
+    if (args.gpu < 0 || args.gpu >= ndev) throw std::runtime_error("GPU " + std::to_string(args.gpu) + " not available");
+    cad::check(cad_set_device(args.gpu), "set device");
+    fs::create_directories(c.checkpoint_dir);
+    fs::create_directories(c.log_dir);
+
+    const int B = c.batch_size, H = c.height, W = c.width;
+    cad::Workspace ws{B, H, W, args.gpu};
+    BaselineUNetImpl model(3, c.init_features, c.max_depth, ws);
+    CombinedDepthLoss loss_fn(c.si, c.grad, c.smooth, c.reproj, ws);
+    optim::Adam opt(model, c.learning_rate, c.weight_decay);
+    std::cout << "Model: baseline_unet (f=" << c.init_features << "), parameters: " << model.count_parameters() << "\n"
+              << "Using MI355X device " << args.gpu << "\n"
+              << "Training samples: " << c.n_train << " (synthetic), validation samples: " << c.n_val << "\n";
+    if (!args.resume.empty()) {
+        load_checkpoint(args.resume, model, opt);
+        std::cout << "Resumed from " << args.resume << " (optimizer step " << opt.step_count() << ")\n";
+    }
+
+    std::ofstream train_log(c.log_dir + "/training.log", std::ios::app);
+    std::ofstream metrics_csv(c.log_dir + "/metrics.csv", std::ios::app);
+    if (metrics_csv.tellp() == 0)
+        metrics_csv << "epoch,step,train_loss,val_loss,abs_rel,sq_rel,rmse,rmse_log,a1,a2,a3,learning_rate,time_elapsed\n";
+    std::ofstream tb;
+    if (args.tensorboard) {
+        tb.open(c.log_dir + "/tensorboard_scalars.csv", std::ios::app);
+        if (tb.tellp() == 0) tb << "tag,step,value\n";
+    }
+
+    const int64_t HW = (int64_t)H * W;
+    HostBatch hb;
+    hb.rgb.resize((size_t)(B * 3 * HW));
+    hb.gt.resize((size_t)(B * HW));
+    hb.K.resize((size_t)B * 9);
+    DeviceTensor rgb = DeviceTensor::empty({B, 3, H, W}, args.gpu), gt = DeviceTensor::empty({B, 1, H, W}, args.gpu),
+                 K = DeviceTensor::empty({B, 3, 3}, args.gpu), pred = DeviceTensor::empty({B, 1, H, W}, args.gpu);
+    auto upload = [&](int64_t first, int n, int64_t split_offset) {
+        for (int i = 0; i < n; ++i)
+            make_sample(split_offset + first + i, H, W, hb.rgb.data() + i * 3 * HW, hb.gt.data() + i * HW, hb.K.data() + i * 9);
+        cad::check(cad_memcpy(rgb.data, hb.rgb.data(), 4 * n * 3 * HW, 0, nullptr), "h2d");
+        cad::check(cad_memcpy(gt.data, hb.gt.data(), 4 * n * HW, 0, nullptr), "h2d");
+        cad::check(cad_memcpy(K.data, hb.K.data(), 4 * n * 9, 0, nullptr), "h2d");
+        rgb.shape[0] = gt.shape[0] = K.shape[0] = pred.shape[0] = n;
+    };
+    const auto t0 = std::chrono::steady_clock::now();
+    int64_t global_step = opt.step_count();
+    const int start_epoch = 1 + (int)(global_step / std::max(1, (c.n_train + B - 1) / B));
+    for (int epoch = start_epoch; epoch <= c.num_epochs; ++epoch) {
+        model.train();
+        double total = 0.0;
+        int seen = 0;
+        const int nb = (c.n_train + B - 1) / B;
+        for (int bi = 0; bi < nb; ++bi) {   // enhanced.h:266-329
+            const int n = std::min(B, c.n_train - bi * B);   // last partial batch (:269-270)
+            upload((int64_t)bi * B, n, 0);
+            opt.zero_grad();
+            model.forward_into(rgb, pred);
+            DeviceTensor l = loss_fn.forwardWithIntrinsics(pred, gt, rgb, K);
+            model.backward(loss_fn.dpred());
+            double gnorm = c.use_grad_clip ? clip_grad_norm_(model, c.grad_clip_value) : 0.0;
+            if (!c.use_grad_clip) cad::check(cad_clip_grad_norm(model.handle(), INFINITY, 1.f, nullptr), "noclip");
+            opt.step();
+            const float lv = l.to_host()[0];   // loss.item<float>() (:307)
+            if (!std::isfinite(lv)) throw std::runtime_error("non-finite loss at step " + std::to_string(global_step));
+            total += (double)lv * n;
+            seen += n;
+            ++global_step;
+            if ((bi + 1) % c.log_interval == 0 || bi == nb - 1) {
+                std::cout << "\r  [" << (100 * (bi + 1) / nb) << "%] Batch " << (bi + 1) << "/" << nb
+                          << " | Loss: " << lv << std::flush;
+                if (tb) tb << "batch_loss/train," << global_step << "," << lv << "\ntraining/gradient_norm,"
+                           << global_step << "," << gnorm << "\n";
+            }
+        }
+        std::cout << "\n";
+        const float train_loss = (float)(total / std::max(1, seen));
+        float val_loss = 0.f;
+        DepthMetrics vm{};
+        if (c.val_interval > 0 && epoch % c.val_interval == 0 && c.n_val > 0) {   // validateEpoch :339-395
+            model.eval();
+            double vl = 0.0;
+            int vn = 0;
+            for (int64_t s = 0; s < c.n_val; s += B) {
+                const int n = (int)std::min<int64_t>(B, c.n_val - s);
+                upload(s, n, 1 << 20);
+                model.forward_into(rgb, pred);
+                DeviceTensor l = loss_fn.forwardWithIntrinsics(pred, gt, rgb, K);
+                // the reference evaluates sample by sample (batch 1); loss over a batch of n equals the
+                // per-sample mean only for n == 1, so report the batch loss weighted by n
+                vl += (double)l.to_host()[0] * n;
+                DepthMetrics m = computeDepthMetrics(pred, gt);
+                vm.abs_rel += m.abs_rel * n; vm.sq_rel += m.sq_rel * n; vm.rmse += m.rmse * n;
+                vm.rmse_log += m.rmse_log * n; vm.a1 += m.a1 * n; vm.a2 += m.a2 * n; vm.a3 += m.a3 * n;
+                vn += n;
+            }
+            val_loss = (float)(vl / vn);
+            for (float* p : {&vm.abs_rel, &vm.sq_rel, &vm.rmse, &vm.rmse_log, &vm.a1, &vm.a2, &vm.a3}) *p /= vn;
+        }
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        metrics_csv << epoch << "," << global_step << "," << train_loss << "," << val_loss << "," << vm.abs_rel << ","
+                    << vm.sq_rel << "," << vm.rmse << "," << vm.rmse_log << "," << vm.a1 << "," << vm.a2 << "," << vm.a3
+                    << "," << c.learning_rate << "," << el << "\n";
+        metrics_csv.flush();
+        train_log << "Epoch " << epoch << " train_loss " << train_loss << " val_loss " << val_loss << " abs_rel "
+                  << vm.abs_rel << "\n";
+        if (tb) tb << "loss/train," << epoch << "," << train_loss << "\nloss/val," << epoch << "," << val_loss
+                   << "\nmetrics/abs_rel," << epoch << "," << vm.abs_rel << "\n";
+        std::cout << "Epoch " << epoch << "/" << c.num_epochs << " | train " << train_loss << " | val " << val_loss
+                  << " | abs_rel " << vm.abs_rel << " | " << el << " s\n";
+        if (c.save_interval > 0 && epoch % c.save_interval == 0)
+            save_checkpoint(c.checkpoint_dir + "/" + c.experiment_name + "_epoch_" + std::to_string(epoch) + ".cadckpt",
+                            model, opt);
+    }
+    save_checkpoint(c.checkpoint_dir + "/final_model.cadckpt", model, opt);
+    std::cout << "Training complete.\n";
+    return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    try {
+        return run(parse_args(argc, argv));
+    } catch (const std::exception& e) {
+        std::cerr << "Error: " << e.what() << std::endl;   // train_main.cpp:503-506
+        return 1;
+    }
+}

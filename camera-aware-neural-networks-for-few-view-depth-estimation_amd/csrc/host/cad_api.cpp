@@ -533,6 +533,26 @@ cad_status cad_stream_synchronize(void* stream) {
     return guard([&] { HIPCHK(hipStreamSynchronize(S(stream))); });
 }
 
+cad_status cad_malloc(int device, int64_t bytes, void** out) {
+    return guard([&] {
+        require(out && bytes >= 0, "bad arguments");
+        HIPCHK(hipSetDevice(device));
+        HIPCHK(hipMalloc(out, (size_t)std::max<int64_t>(bytes, 1)));
+    });
+}
+void cad_free(void* p) {
+    if (p) (void)hipFree(p);
+}
+cad_status cad_memcpy(void* dst, const void* src, int64_t bytes, int kind, void* stream) {
+    return guard([&] {
+        require(kind >= 0 && kind <= 2 && bytes >= 0, "bad memcpy arguments");
+        const hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost
+                                                                              : hipMemcpyDeviceToDevice;
+        if (stream) HIPCHK(hipMemcpyAsync(dst, src, (size_t)bytes, k, S(stream)));
+        else HIPCHK(hipMemcpy(dst, src, (size_t)bytes, k));
+    });
+}
+
 cad_status cad_unet_create(const cad_unet_desc* d, int device, cad_unet** out) {
     return guard([&] {
         require(d && out, "null argument");
@@ -800,6 +820,18 @@ cad_status cad_adam_set_lr(cad_adam* a, float lr) {
     return guard([&] { a->o.lr = lr; });
 }
 int64_t cad_adam_step_count(const cad_adam* a) { return a->step; }
+cad_status cad_adam_state(cad_adam* a, float** m, float** v) {
+    return guard([&] {
+        if (m) *m = a->m;
+        if (v) *v = a->v;
+    });
+}
+cad_status cad_adam_set_step_count(cad_adam* a, int64_t step) {
+    return guard([&] {
+        require(step >= 0, "negative step");
+        a->step = step;
+    });
+}
 
 cad_status cad_loss_create(float si, float gr, float sm, float rp, int max_batch, int height, int width, int device,
                            cad_loss** out) {

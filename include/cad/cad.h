@@ -79,6 +79,11 @@ const char* cad_last_error(void);
 cad_status cad_device_count(int* n);
 cad_status cad_set_device(int device);
 cad_status cad_stream_synchronize(void* stream);
+/* device memory for callers without HIP headers (the C++ drop-in, the train CLI) */
+cad_status cad_malloc(int device, int64_t bytes, void** out);
+void cad_free(void* p);
+/* kind: 0 host->device, 1 device->host, 2 device->device; synchronous when stream is NULL */
+cad_status cad_memcpy(void* dst, const void* src, int64_t bytes, int kind, void* stream);
 
 /* ---- model: BaselineUNetImpl ---- */
 cad_status cad_unet_create(const cad_unet_desc* desc, int device, cad_unet** out);
@@ -125,6 +130,10 @@ void cad_adam_destroy(cad_adam* a);
 cad_status cad_adam_step(cad_adam* a, void* stream); /* consumes the clip coefficient */
 cad_status cad_adam_set_lr(cad_adam* a, float lr);
 int64_t cad_adam_step_count(const cad_adam* a);
+/* optimizer state for checkpoint / resume: device pointers to the m and v slabs (cad_unet_flat's n
+ * floats each, same packed layout as the parameters) and the step counter */
+cad_status cad_adam_state(cad_adam* a, float** m, float** v);
+cad_status cad_adam_set_step_count(cad_adam* a, int64_t step);
 
 /* ---- loss: CombinedDepthLoss ---- */
 cad_status cad_loss_create(float si_weight, float grad_weight, float smooth_weight, float reproj_weight,

@@ -1,0 +1,269 @@
+// cad.hpp — header-only C++ drop-in for the reference's hot-path classes, over the C ABI (cad.h).
+//
+// Same namespace, class names and argument meaning as the reference; device tensors (cad::DeviceTensor,
+// NCHW fp32) replace torch::Tensor at the API edge.  Errors throw std::runtime_error, like the
+// reference's LibTorch / std::runtime_error paths (train_main.cpp:503-506 prints "Error: <what>").
+//
+//   camera_aware_depth::BaselineUNetImpl   src/models/baseline_unet.h:122-208
+//   camera_aware_depth::CombinedDepthLoss  src/loss/depth_loss.h:366-479
+//   camera_aware_depth::optim::Adam        torch::optim::Adam (tensorboard_trainer_enhanced.h:97-101)
+//   camera_aware_depth::clip_grad_norm_    torch::nn::utils::clip_grad_norm_ (enhanced.h:300-302)
+#ifndef CAD_CAD_HPP
+#define CAD_CAD_HPP
+
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <numeric>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "cad.h"
+
+namespace cad {
+
+inline void check(cad_status s, const char* what) {
+    if (s != CAD_OK) throw std::runtime_error(std::string(what) + ": " + cad_last_error());
+}
+
+// owning (or borrowed) device tensor view, NCHW fp32
+struct DeviceTensor {
+    float* data = nullptr;
+    std::vector<int64_t> shape;
+    int device = 0;
+    std::shared_ptr<void> owner;
+
+    int dim() const { return (int)shape.size(); }
+    int64_t size(int d) const { return shape.at(d < 0 ? d + dim() : d); }
+    int64_t numel() const {
+        return std::accumulate(shape.begin(), shape.end(), int64_t(1), std::multiplies<int64_t>());
+    }
+    static DeviceTensor empty(std::vector<int64_t> shape, int device = 0) {
+        DeviceTensor t;
+        t.shape = std::move(shape);
+        t.device = device;
+        void* p = nullptr;
+        check(cad_malloc(device, t.numel() * (int64_t)sizeof(float), &p), "cad_malloc");
+        t.data = static_cast<float*>(p);
+        t.owner = std::shared_ptr<void>(p, [](void* q) { cad_free(q); });
+        return t;
+    }
+    static DeviceTensor from_host(const float* host, std::vector<int64_t> shape, int device = 0) {
+        DeviceTensor t = empty(std::move(shape), device);
+        check(cad_memcpy(t.data, host, t.numel() * (int64_t)sizeof(float), 0, nullptr), "cad_memcpy h2d");
+        return t;
+    }
+    std::vector<float> to_host() const {
+        std::vector<float> h((size_t)numel());
+        check(cad_memcpy(h.data(), data, numel() * (int64_t)sizeof(float), 1, nullptr), "cad_memcpy d2h");
+        return h;
+    }
+};
+
+struct Workspace {   // device workspace sizing (the reference allocates per call)
+    int batch = 1, height = 480, width = 640, device = 0;
+};
+
+}  // namespace cad
+
+namespace camera_aware_depth {
+
+using cad::DeviceTensor;
+
+struct NamedTensor {
+    std::string name;
+    std::vector<int64_t> shape;
+    std::vector<float> value;   // reference layout (OIHW conv, (Cin,Cout,2,2) ConvTranspose)
+};
+
+class BaselineUNetImpl {
+public:
+    explicit BaselineUNetImpl(int in_channels = 3, int init_features = 64, float max_depth_value = 10.0f,
+                              cad::Workspace ws = {})
+        : max_depth(max_depth_value), ws_(ws) {
+        cad_unet_desc d{in_channels, init_features, max_depth_value, ws.batch, ws.height, ws.width};
+        cad::check(cad_unet_create(&d, ws.device, &h_), "BaselineUNetImpl");
+    }
+    ~BaselineUNetImpl() { cad_unet_destroy(h_); }
+    BaselineUNetImpl(const BaselineUNetImpl&) = delete;
+    BaselineUNetImpl& operator=(const BaselineUNetImpl&) = delete;
+
+    // forward(x): (B,3,H,W) in [0,1] -> depth (B,1,H,W) in (0, max_depth)   (baseline_unet.h:174-195)
+    DeviceTensor forward(const DeviceTensor& x, void* stream = nullptr) {
+        if (x.dim() != 4 || x.size(1) != 3) throw std::runtime_error("forward: expected (B,3,H,W)");
+        DeviceTensor out = DeviceTensor::empty({x.size(0), 1, x.size(2), x.size(3)}, ws_.device);
+        cad::check(cad_unet_forward(h_, x.data, out.data, (int)x.size(0), stream), "forward");
+        return out;
+    }
+    DeviceTensor operator()(const DeviceTensor& x) { return forward(x); }
+    void forward_into(const DeviceTensor& x, DeviceTensor& out, void* stream = nullptr) {
+        cad::check(cad_unet_forward(h_, x.data, out.data, (int)x.size(0), stream), "forward");
+    }
+    // loss.backward() through the network (enhanced.h:297), given dL/ddepth
+    void backward(const DeviceTensor& ddepth, void* stream = nullptr) {
+        cad::check(cad_unet_backward(h_, ddepth.data, stream), "backward");
+    }
+    int64_t count_parameters() const { return cad_unet_count_parameters(h_); }
+    void train(bool on = true) { cad::check(cad_unet_train(h_, on ? 1 : 0), "train"); }
+    void eval() { train(false); }
+
+    std::vector<NamedTensor> named_parameters() const { return fetch(0); }
+    std::vector<NamedTensor> named_buffers() const { return fetch(1); }
+    std::vector<NamedTensor> named_grads() const {
+        auto v = fetch(0);
+        for (size_t i = 0; i < v.size(); ++i)
+            cad::check(cad_unet_get_grad(h_, (int)i, v[i].value.data(), (int64_t)v[i].value.size()), "get_grad");
+        return v;
+    }
+    // load by name (parameters and buffers); returns the number of tensors loaded
+    int load(const std::vector<NamedTensor>& ts) {
+        int n = 0;
+        for (int kind = 0; kind < 2; ++kind) {
+            const int cnt = kind == 0 ? cad_unet_num_params(h_) : cad_unet_num_buffers(h_);
+            for (int i = 0; i < cnt; ++i) {
+                const char* name;
+                cad::check(cad_unet_tensor_info(h_, kind, i, &name, nullptr, nullptr), "tensor_info");
+                for (const auto& t : ts)
+                    if (t.name == name) {
+                        cad::check(cad_unet_set_tensor(h_, kind, i, t.value.data(), (int64_t)t.value.size()), name);
+                        ++n;
+                    }
+            }
+        }
+        return n;
+    }
+    cad_unet* handle() const { return h_; }
+    const cad::Workspace& workspace() const { return ws_; }
+
+    float max_depth;
+
+private:
+    std::vector<NamedTensor> fetch(int kind) const {
+        const int cnt = kind == 0 ? cad_unet_num_params(h_) : cad_unet_num_buffers(h_);
+        std::vector<NamedTensor> out;
+        for (int i = 0; i < cnt; ++i) {
+            const char* name;
+            int nd;
+            int64_t shp[4];
+            cad::check(cad_unet_tensor_info(h_, kind, i, &name, &nd, shp), "tensor_info");
+            NamedTensor t;
+            t.name = name;
+            t.shape.assign(shp, shp + nd);
+            int64_t n = 1;
+            for (int k = 0; k < nd; ++k) n *= shp[k];
+            t.value.resize((size_t)n);
+            cad::check(cad_unet_get_tensor(h_, kind, i, t.value.data(), n), "get_tensor");
+            out.push_back(std::move(t));
+        }
+        return out;
+    }
+    cad::Workspace ws_;
+    cad_unet* h_ = nullptr;
+};
+
+class CombinedDepthLoss {
+public:
+    explicit CombinedDepthLoss(float si_weight = 1.0f, float grad_weight = 0.1f, float smooth_weight = 0.001f,
+                               float reproj_weight = 0.01f, cad::Workspace ws = {})
+        : w_{si_weight, grad_weight, smooth_weight, reproj_weight}, ws_(ws) {}
+    ~CombinedDepthLoss() {
+        cad_loss_destroy(with_);
+        cad_loss_destroy(without_);
+    }
+    CombinedDepthLoss(const CombinedDepthLoss&) = delete;
+    CombinedDepthLoss& operator=(const CombinedDepthLoss&) = delete;
+
+    // forwardWithIntrinsics (depth_loss.h:416-433): returns the 5-float device tensor
+    // {total, si, grad, smooth, reproj}; dL/dpred is left in dpred()
+    DeviceTensor forwardWithIntrinsics(const DeviceTensor& pred, const DeviceTensor& gt, const DeviceTensor& image,
+                                       const DeviceTensor& intrinsics, void* stream = nullptr) {
+        return run(get(true), pred, gt, image, intrinsics, stream);
+    }
+    // forward (depth_loss.h:390-404): SI + grad + smooth (no reprojection term)
+    DeviceTensor forward(const DeviceTensor& pred, const DeviceTensor& gt, const DeviceTensor& image,
+                         const DeviceTensor& intrinsics, void* stream = nullptr) {
+        return run(get(false), pred, gt, image, intrinsics, stream);
+    }
+    std::map<std::string, float> getComponentsWithIntrinsics(const DeviceTensor& pred, const DeviceTensor& gt,
+                                                             const DeviceTensor& image, const DeviceTensor& K) {
+        DeviceTensor l = forwardWithIntrinsics(pred, gt, image, K);
+        auto v = l.to_host();
+        return {{"si_loss", v[1]}, {"grad_loss", v[2]}, {"smooth_loss", v[3]}, {"reproj_loss", v[4]}};
+    }
+    std::map<std::string, float> getComponents(const DeviceTensor& pred, const DeviceTensor& gt,
+                                               const DeviceTensor& image, const DeviceTensor& K) {
+        DeviceTensor l = forward(pred, gt, image, K);
+        auto v = l.to_host();
+        return {{"si_loss", v[1]}, {"grad_loss", v[2]}, {"smooth_loss", v[3]}};
+    }
+    const DeviceTensor& dpred() const { return dpred_; }
+
+private:
+    cad_loss* get(bool with_reproj) {
+        cad_loss*& h = with_reproj ? with_ : without_;
+        if (!h)
+            cad::check(cad_loss_create(w_[0], w_[1], w_[2], with_reproj ? w_[3] : 0.f, ws_.batch, ws_.height,
+                                       ws_.width, ws_.device, &h), "CombinedDepthLoss");
+        return h;
+    }
+    DeviceTensor run(cad_loss* h, const DeviceTensor& pred, const DeviceTensor& gt, const DeviceTensor& image,
+                     const DeviceTensor& K, void* stream) {
+        if (dpred_.numel() != pred.numel()) dpred_ = DeviceTensor::empty(pred.shape, ws_.device);
+        DeviceTensor l = DeviceTensor::empty({5}, ws_.device);
+        cad::check(cad_loss_forward_backward(h, pred.data, gt.data, image.data, K.data, (int)pred.size(0), l.data,
+                                             dpred_.data, stream), "forwardWithIntrinsics");
+        return l;
+    }
+    float w_[4];
+    cad::Workspace ws_;
+    cad_loss* with_ = nullptr;
+    cad_loss* without_ = nullptr;
+    DeviceTensor dpred_;
+};
+
+namespace optim {
+class Adam {   // torch::optim::Adam(params, AdamOptions(lr).weight_decay(wd)) — coupled L2
+public:
+    Adam(BaselineUNetImpl& model, float lr = 1e-3f, float weight_decay = 0.f, float beta1 = 0.9f,
+         float beta2 = 0.999f, float eps = 1e-8f) {
+        cad_adam_opts o{lr, beta1, beta2, eps, weight_decay};
+        cad::check(cad_adam_create(model.handle(), &o, &h_), "Adam");
+    }
+    ~Adam() { cad_adam_destroy(h_); }
+    Adam(const Adam&) = delete;
+    Adam& operator=(const Adam&) = delete;
+    void zero_grad() {}   // every backward overwrites the gradient slab
+    void step(void* stream = nullptr) { cad::check(cad_adam_step(h_, stream), "Adam::step"); }
+    void set_lr(float lr) { cad::check(cad_adam_set_lr(h_, lr), "set_lr"); }
+    int64_t step_count() const { return cad_adam_step_count(h_); }
+    cad_adam* handle() const { return h_; }
+
+private:
+    cad_adam* h_ = nullptr;
+};
+}  // namespace optim
+
+// torch::nn::utils::clip_grad_norm_(model->parameters(), max_norm) -> total norm (synchronises)
+inline double clip_grad_norm_(BaselineUNetImpl& model, double max_norm, void* stream = nullptr) {
+    cad::check(cad_clip_grad_norm(model.handle(), (float)max_norm, 1.0f, stream), "clip_grad_norm_");
+    float n = 0.f;
+    cad::check(cad_unet_last_grad_norm(model.handle(), &n, stream), "clip_grad_norm_");
+    return n;
+}
+
+// computeDepthMetrics (tensorboard_trainer_enhanced.h:400-439), averaged over the batch
+struct DepthMetrics {
+    float abs_rel = 0, sq_rel = 0, rmse = 0, rmse_log = 0, a1 = 0, a2 = 0, a3 = 0;
+};
+inline DepthMetrics computeDepthMetrics(const DeviceTensor& pred, const DeviceTensor& gt, void* stream = nullptr) {
+    float o[7];
+    cad::check(cad_depth_metrics(pred.data, gt.data, (int)pred.size(0), (int)pred.size(2), (int)pred.size(3), o, stream),
+               "computeDepthMetrics");
+    return {o[0], o[1], o[2], o[3], o[4], o[5], o[6]};
+}
+
+}  // namespace camera_aware_depth
+
+#endif  // CAD_CAD_HPP

@@ -353,7 +353,7 @@ class Trainer:
 
     @torch.no_grad()
     def predict_eval(self, rgb):
-        return unet_forward(rgb, self.p, self.bufs, False, self.max_depth)
+        return unet_forward(rgb.to(self.dtype), self.p, self.bufs, False, self.max_depth)
 
 
 def depth_metrics(pred, gt):
