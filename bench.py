@@ -97,6 +97,24 @@ def pmc_traffic(kernel_name):
         return None
 
 
+def parity_evidence():
+    """The committed GPU-vs-CPU-reference parity report (tests/parity_report.py), newest round."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "parity_r*.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as fh:
+            d = json.load(fh)
+        c0, rf = d["config0_vs_cpu_ref"], d["reference_fixture"]
+        return {"source": os.path.relpath(files[-1], ROOT), "abs_rel_gpu": round(c0["abs_rel_gpu"], 6),
+                "abs_rel_cpu_ref": round(c0["abs_rel_cpu_ref"], 6), "abs_rel_delta": c0["abs_rel_delta"],
+                "eval_pred_max_rel_err_vs_cpu": c0["eval_pred_max_rel_err_vs_cpu"], "shape": c0["shape"],
+                "reference_fixture_pred_max_rel_err": rf["pred_max_rel_err"]}
+    except Exception:
+        return None
+
+
 def main():
     args = parse()
     import torch
@@ -158,6 +176,9 @@ def main():
     prof = json.loads(buf.value.decode())
 
     if rank == 0:
+        for r in sorted(prof, key=lambda r: -r["ms"]):
+            log(f"  {r['ms'] / args.steps:8.2f} ms/step  {r['gflop'] / r['ms']:7.2f} TF/s  "
+                f"x{r['launches'] // args.steps:<3d} {r['name']}")
         images = B * world * args.steps
         value = images / elapsed
         ms_per_step = 1e3 * elapsed / args.steps
@@ -193,6 +214,7 @@ def main():
             "last_loss": last_loss,
             "roofline": roof,
             "cpu_baseline": cpu,
+            "parity": parity_evidence(),
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -10,7 +10,8 @@ import os
 import re
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libcad_hip.so")
+# CAD_LIB selects an A/B variant build (make VARIANT=... -> libcad_hip_<variant>.so) for tuning runs
+LIB_PATH = os.path.join(PKG_DIR, os.environ.get("CAD_LIB", "libcad_hip.so"))
 HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "cad", "cad.h")
 
 P = C.c_void_p

@@ -7,7 +7,8 @@
 // (tensorboard_trainer_enhanced.h:287-304).
 //
 // Activation layout per level l (H_l = H >> l, C_l = f << l), NHWC fp32:
-//   enc/bottleneck: y1, a1, y2 [M_l][C_l]; output written straight into cat_l[:, 0:C_l]
+//   enc/bottleneck: y1, y2 [M_l][C_l] (conv outputs pre-BN; a1 = relu(bn1(y1)) is applied inside
+//         conv2's operand loaders and never stored); output written straight into cat_l[:, 0:C_l]
 //   cat_l [M_l][2 C_l] = decoder concat buffer {skip | up} (baseline_unet.h:98, skip first) — the
 //         encoder writes the skip half, the ConvTranspose epilogue writes the up half: no cat/pad.
 //   pool_l [M_l][C_{l-1}] + uint8 argmax; dec: y1d, a1d, y2d, d_l [M_l][C_l].
@@ -253,7 +254,7 @@ void layout(cad_unet* h, Arena& a) {
         DoubleConv& e = h->enc[l];
         bn_alloc(a, e.b1); bn_alloc(a, e.b2);
         const int64_t MC = h->Ml(l, B) * h->Cl(l);
-        e.y1 = a.f(MC); e.a1 = a.f(MC); e.y2 = a.f(MC);
+        e.y1 = a.f(MC); e.y2 = a.f(MC);   // a1 is fused into conv2's loaders
         if (l > 0) e.c1.wd = a.f((int64_t)e.c1.cout * 9 * e.c1.cin);
         e.c2.wd = a.f((int64_t)e.c2.cout * 9 * e.c2.cin);
         if (l < 4) h->cat[l] = a.f(2 * MC);
@@ -267,7 +268,7 @@ void layout(cad_unet* h, Arena& a) {
         DoubleConv& d = h->dec[l];
         bn_alloc(a, d.b1); bn_alloc(a, d.b2);
         const int64_t MC = h->Ml(l, B) * h->Cl(l);
-        d.y1 = a.f(MC); d.a1 = a.f(MC); d.y2 = a.f(MC);
+        d.y1 = a.f(MC); d.y2 = a.f(MC);
         h->dout[l] = a.f(MC);
         d.c1.wd = a.f((int64_t)d.c1.cout * 9 * d.c1.cin);
         d.c2.wd = a.f((int64_t)d.c2.cout * 9 * d.c2.cin);
@@ -331,8 +332,9 @@ void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin,
     };
     cad::conv3x3_fwd(in, ldin, 0, dc.c1.cin, h->P(dc.c1.pidx), C, dc.y1, C, 0, B, Hh, Ww, tr ? h->stats : nullptr, st);
     bn(dc.b1);
-    cad::bn_relu_fwd(dc.y1, C, dc.b1.scale, dc.b1.shift, dc.a1, C, 0, M, st);
-    cad::conv3x3_fwd(dc.a1, C, 0, C, h->P(dc.c2.pidx), C, dc.y2, C, 0, B, Hh, Ww, tr ? h->stats : nullptr, st);
+    // a1 = relu(bn1(y1)) is never materialised: conv2's loader applies it (and so does conv2's wgrad)
+    cad::conv3x3_fwd(dc.y1, C, 0, C, h->P(dc.c2.pidx), C, dc.y2, C, 0, B, Hh, Ww, tr ? h->stats : nullptr, st,
+                     dc.b1.scale, dc.b1.shift);
     bn(dc.b2);
     cad::bn_relu_fwd(dc.y2, C, dc.b2.scale, dc.b2.shift, out, ldo, ocoff, M, st);
 }
@@ -376,7 +378,8 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     cad::bn_relu_bwd(g, ldg, gcoff, dc.y2, C, dc.b2.mean, dc.b2.invstd, dc.b2.scale, dc.b2.shift, h->P(dc.b2.widx), M,
                      h->dscr, dc.b2.coef, h->G(dc.b2.widx), h->G(dc.b2.bidx), dY, st);
     // conv2
-    cad::conv3x3_wgrad(dY, C, dc.a1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
+    cad::conv3x3_wgrad(dY, C, dc.y1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st,
+                       dc.b1.scale, dc.b1.shift);
     cad::conv3x3_dgrad(dY, C, dc.c2.wd, C, dA1, C, B, Hh, Ww, st);
     // bn1 + relu
     cad::bn_relu_bwd(dA1, C, 0, dc.y1, C, dc.b1.mean, dc.b1.invstd, dc.b1.scale, dc.b1.shift, h->P(dc.b1.widx), M,

@@ -12,39 +12,64 @@ namespace cad {
 
 struct EpiStore {
     static constexpr bool STATS = false;
-    __device__ void operator()(const GemmArgs& a, int m, int n, float v) const {
+    __device__ void operator()(const GemmArgs& a, int m, int n, float v, int) const {
         a.C[(int64_t)m * a.ldc + a.c_coff + n] = v;
     }
 };
 struct EpiStoreStats : EpiStore {
     static constexpr bool STATS = true;
 };
-// ConvTranspose2d(k2,s2) pixel shuffle: n = (q=(dy,dx), co) -> high-res pixel (2y+dy, 2x+dx)
+// ConvTranspose2d(k2,s2) pixel shuffle: n = (q=(dy,dx), co) -> high-res pixel (2y+dy, 2x+dx).
+// The column (q, co) is fixed per lane and sub-block, and rows advance in small steps, so the
+// epilogue carries (x, y, b) incrementally instead of dividing per element (STRUCTURED epilogue).
 struct EpiConvT {
     static constexpr bool STATS = false;
-    __device__ void operator()(const GemmArgs& a, int m, int n, float v) const {
+    static constexpr bool STRUCTURED = true;
+    __device__ void operator()(const GemmArgs& a, int m, int n, float v, int) const {
         const int cout = a.N >> 2;
         const int q = n / cout, co = n - q * cout;
         const int x = m % a.W, t = m / a.W, y = t % a.H, b = t / a.H;
         const int64_t hp = ((int64_t)b * (2 * a.H) + 2 * y + (q >> 1)) * (2 * a.W) + 2 * x + (q & 1);
         a.C[hp * a.ldc + a.c_coff + co] = v + a.bias[co];
     }
+    // one lane's 16 accumulator rows of a 32x32 sub-block: rows mbase + (r&3) + 8(r>>2), column n
+    __device__ void block(const GemmArgs& a, int mbase, int n, const floatx16& acc) const {
+        if (n >= a.N) return;
+        const int cout = a.N >> 2;
+        const int q = n / cout, co = n - q * cout;
+        const float bias = a.bias[co];
+        float* dst = a.C + a.c_coff + co;
+        const int64_t W2 = 2 * a.W;
+        int x = mbase % a.W, t = mbase / a.W, y = t % a.H, b = t / a.H;
+        int cur = 0;   // row offset that (x, y, b) currently describe
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int off = (r & 3) + 8 * (r >> 2);
+            x += off - cur;
+            cur = off;
+            while (x >= a.W) { x -= a.W; if (++y == a.H) { y = 0; ++b; } }
+            if (mbase + off < a.M) {
+                const int64_t hp = ((int64_t)b * (2 * a.H) + 2 * y + (q >> 1)) * W2 + 2 * x + (q & 1);
+                dst[hp * a.ldc] = acc[r] + bias;
+            }
+        }
+    }
 };
 struct EpiSlab {   // split-K partial: slab z holds C[m][n] of K-slice z
     static constexpr bool STATS = false;
-    __device__ void operator()(const GemmArgs& a, int m, int n, float v) const {
-        a.C[blockIdx.z * a.slab_stride + (int64_t)m * a.ldc + n] = v;
+    __device__ void operator()(const GemmArgs& a, int m, int n, float v, int z) const {
+        a.C[z * a.slab_stride + (int64_t)m * a.ldc + n] = v;
     }
 };
 
-template <int WM, int WN, class Epi>
+template <int WM, int WN, class Epi, bool BNA = false>
 __global__ __launch_bounds__(256) void k_conv3x3_fwd(GemmArgs a) {
-    using LA = KcIm2col3x3<64 * WM>;
+    using LA = KcIm2col3x3<64 * WM, BNA>;
     using LB = KcDense<64 * WN>;
     gemm_body<WM, WN, LA, true, LB, true>(
         a,
-        [&](LA& l, int r0, int t) { l.init(a.A, a.lda, a.a_coff, a.a_cin, a.B, a.H, a.W, r0, t); },
-        [&](LB& l, int r0, int t) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t); }, Epi{});
+        [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.a_cin, a.B, a.H, a.W, r0, t, kb, a.a_sc, a.a_sh); },
+        [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, Epi{});
 }
 
 template <int WM, int WN>
@@ -52,8 +77,8 @@ __global__ __launch_bounds__(256) void k_convT_fwd(GemmArgs a) {
     using LA = KcDense<64 * WM>;
     using LB = KcDense<64 * WN>;
     gemm_body<WM, WN, LA, true, LB, true>(
-        a, [&](LA& l, int r0, int t) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t); },
-        [&](LB& l, int r0, int t) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t); }, EpiConvT{});
+        a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t, kb); },
+        [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, EpiConvT{});
 }
 
 template <int WM, int WN>
@@ -61,17 +86,17 @@ __global__ __launch_bounds__(256) void k_convT_dgrad(GemmArgs a) {
     using LA = KcUpGather<64 * WM>;
     using LB = KcDense<64 * WN>;
     gemm_body<WM, WN, LA, true, LB, true>(
-        a, [&](LA& l, int r0, int t) { l.init(a.A, a.lda, a.a_coff, a.a_cin, a.B, a.H, a.W, r0, t); },
-        [&](LB& l, int r0, int t) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t); }, EpiStore{});
+        a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.a_cin, a.B, a.H, a.W, r0, t, kb); },
+        [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, EpiStore{});
 }
 
-template <int WM, int WN>
+template <int WM, int WN, bool BNB = false>
 __global__ __launch_bounds__(256) void k_conv3x3_wgrad(GemmArgs a) {
     using LA = MNcDense<64 * WM>;
-    using LB = MNcIm2col3x3<64 * WN>;
+    using LB = MNcIm2col3x3<64 * WN, BNB>;
     gemm_body<WM, WN, LA, false, LB, false>(
-        a, [&](LA& l, int r0, int t) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t); },
-        [&](LB& l, int r0, int t) { l.init(a.Bm, a.ldb, a.b_coff, a.b_cin, a.B, a.H, a.W, r0, t); },
+        a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t, kb); },
+        [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.b_cin, a.B, a.H, a.W, r0, t, kb, a.b_sc, a.b_sh); },
         EpiSlab{});
 }
 
@@ -80,8 +105,8 @@ __global__ __launch_bounds__(256) void k_convT_wgrad(GemmArgs a) {
     using LA = MNcDense<64 * WM>;
     using LB = MNcUpGather<64 * WN>;
     gemm_body<WM, WN, LA, false, LB, false>(
-        a, [&](LA& l, int r0, int t) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t); },
-        [&](LB& l, int r0, int t) { l.init(a.Bm, a.ldb, a.b_coff, a.b_cin, a.B, a.H, a.W, r0, t); },
+        a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t, kb); },
+        [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.b_cin, a.B, a.H, a.W, r0, t, kb); },
         EpiSlab{});
 }
 
@@ -142,6 +167,18 @@ template <int WM, int WN> struct KConvFwdS {
     static constexpr auto fn = k_conv3x3_fwd<WM, WN, EpiStoreStats>;
     static constexpr const char* fmt = "void cad::k_conv3x3_fwd<%d, %d, cad::EpiStoreStats>(cad::GemmArgs)";
 };
+template <int WM, int WN> struct KConvFwdBN {
+    static constexpr auto fn = k_conv3x3_fwd<WM, WN, EpiStore, true>;
+    static constexpr const char* fmt = "void cad::k_conv3x3_fwd<%d, %d, cad::EpiStore, true>(cad::GemmArgs)";
+};
+template <int WM, int WN> struct KConvFwdSBN {
+    static constexpr auto fn = k_conv3x3_fwd<WM, WN, EpiStoreStats, true>;
+    static constexpr const char* fmt = "void cad::k_conv3x3_fwd<%d, %d, cad::EpiStoreStats, true>(cad::GemmArgs)";
+};
+template <int WM, int WN> struct KConvWgradBN {
+    static constexpr auto fn = k_conv3x3_wgrad<WM, WN, true>;
+    static constexpr const char* fmt = "void cad::k_conv3x3_wgrad<%d, %d, true>(cad::GemmArgs)";
+};
 template <int WM, int WN> struct KConvTFwd {
     static constexpr auto fn = k_convT_fwd<WM, WN>;
     static constexpr const char* fmt = "void cad::k_convT_fwd<%d, %d>(cad::GemmArgs)";
@@ -174,7 +211,8 @@ int plan_splits(const GemmArgs& a, Cfg c, int64_t slab_cap_floats) {
 }  // namespace
 
 void conv3x3_fwd(const float* x, int64_t ldx, int xcoff, int cin, const float* w, int cout, float* y,
-                 int64_t ldy, int ycoff, int B, int H, int W, float* stats, hipStream_t st) {
+                 int64_t ldy, int ycoff, int B, int H, int W, float* stats, hipStream_t st,
+                 const float* in_scale, const float* in_shift) {
     GemmArgs a{};
     a.M = B * H * W; a.N = cout; a.K = 9 * cin;
     a.B = B; a.H = H; a.W = W;
@@ -182,9 +220,14 @@ void conv3x3_fwd(const float* x, int64_t ldx, int xcoff, int cin, const float* w
     a.Bm = w; a.ldb = 9 * cin; a.b_coff = 0;
     a.C = y; a.ldc = ldy; a.c_coff = ycoff;
     a.stats = stats;
+    a.a_sc = in_scale; a.a_sh = in_shift;
     a.kstages_per_split = cdiv(a.K, BK);
     Cfg c = pick_cfg(a.M, a.N);
-    if (stats) launch_cfg<KConvFwdS>(c, a, 1, st); else launch_cfg<KConvFwd>(c, a, 1, st);
+    if (in_scale) {
+        if (stats) launch_cfg<KConvFwdSBN>(c, a, 1, st); else launch_cfg<KConvFwdBN>(c, a, 1, st);
+    } else {
+        if (stats) launch_cfg<KConvFwdS>(c, a, 1, st); else launch_cfg<KConvFwd>(c, a, 1, st);
+    }
 }
 
 int conv3x3_stats_rows(int B, int H, int W, int cout) {
@@ -240,12 +283,14 @@ static void finish_slabs(float* slab, int splits, int64_t per, float* dw, hipStr
 }
 
 void conv3x3_wgrad(const float* dz, int cout, const float* x, int64_t ldx, int xcoff, int cin, float* dw,
-                   int B, int H, int W, float* slab, int64_t slab_cap, hipStream_t st) {
+                   int B, int H, int W, float* slab, int64_t slab_cap, hipStream_t st,
+                   const float* x_scale, const float* x_shift) {
     GemmArgs a{};
     a.M = cout; a.N = 9 * cin; a.K = B * H * W;
     a.B = B; a.H = H; a.W = W;
     a.A = dz; a.lda = cout; a.a_coff = 0;
     a.Bm = x; a.ldb = ldx; a.b_coff = xcoff; a.b_cin = cin;
+    a.b_sc = x_scale; a.b_sh = x_shift;
     Cfg c = pick_cfg(a.M, a.N);
     int s = plan_splits(a, c, slab_cap);
     a.kstages_per_split = cdiv(cdiv(a.K, BK), s);
@@ -253,7 +298,7 @@ void conv3x3_wgrad(const float* dz, int cout, const float* x, int64_t ldx, int x
     const int64_t per = (int64_t)a.M * a.N;
     a.ldc = a.N; a.slab_stride = per;
     a.C = s == 1 ? dw : slab;
-    launch_cfg<KConvWgrad>(c, a, s, st);
+    if (x_scale) launch_cfg<KConvWgradBN>(c, a, s, st); else launch_cfg<KConvWgrad>(c, a, s, st);
     if (s > 1) finish_slabs(slab, s, per, dw, st);
 }
 

@@ -23,12 +23,26 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace cad {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-constexpr int BK = 16;
-constexpr int LDK = BK + 4;   // Kc LDS row stride (floats)
+#ifndef CAD_BK
+#define CAD_BK 16
+#endif
+#ifndef CAD_XCD_SWIZZLE
+#define CAD_XCD_SWIZZLE 0
+#endif
+#ifndef CAD_PREFETCH2
+#define CAD_PREFETCH2 0
+#endif
+constexpr int BK = CAD_BK;            // K-stage depth (16 or 32)
+constexpr int LDK = BK + 4;           // Kc LDS row stride (floats): 80 B / 144 B rows, conflict-free b128
+constexpr int KC_TPR = BK / 4;        // threads per Kc row (one float4 each)
+constexpr int KC_RPP = 256 / KC_TPR;  // Kc rows staged per pass of the workgroup
+constexpr int HK = BK / 2;            // MFMA steps per stage = k values per lane half
 
 struct GemmArgs {
     int M, N, K;          // GEMM extents
@@ -42,11 +56,17 @@ struct GemmArgs {
     float* C; int64_t ldc; int c_coff;
     const float* bias;
     float* stats;         // BN partials [gridDim.x][2][N]  (sum, sumsq) or nullptr
+    // fused BatchNorm-apply + ReLU on a gathered operand: x -> max(0, x*sc[c] + sh[c]) (in-image only)
+    const float *a_sc, *a_sh, *b_sc, *b_sh;
     int kstages_per_split;
     int64_t slab_stride;  // elements between split-K slabs
 };
 
 __device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+__device__ __forceinline__ float4 bn_relu4(float4 v, float4 s, float4 h) {
+    return make_float4(fmaxf(v.x * s.x + h.x, 0.f), fmaxf(v.y * s.y + h.y, 0.f), fmaxf(v.z * s.z + h.z, 0.f),
+                       fmaxf(v.w * s.w + h.w, 0.f));
+}
 
 // --------------------------------------------------------------------------------------------
 // Kc loaders: operand(row r, k) with k contiguous in memory.  Thread t owns rows t/4 + 64j and
@@ -54,49 +74,62 @@ __device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0
 // --------------------------------------------------------------------------------------------
 template <int ROWS>
 struct KcDense {   // op(r,k) = P[r*ld + coff + k], r < nrows, k < K
-    static constexpr int NV = ROWS / 64;
+    static constexpr int NV = ROWS / KC_RPP;
     const float* p[NV];
     bool ok[NV];
-    int K;
-    __device__ void init(const float* P, int64_t ld, int coff, int nrows, int K_, int row0, int tid) {
+    int K, k;
+    __device__ void init(const float* P, int64_t ld, int coff, int nrows, int K_, int row0, int tid, int kbeg) {
         K = K_;
+        k = kbeg * BK;
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
-            int r = row0 + tid / 4 + 64 * j;
+            int r = row0 + tid / KC_TPR + KC_RPP * j;
             ok[j] = r < nrows;
-            p[j] = P + (int64_t)(ok[j] ? r : 0) * ld + coff + (tid & 3) * 4;
+            p[j] = P + (int64_t)(ok[j] ? r : 0) * ld + coff + (tid % KC_TPR) * 4;
         }
     }
-    __device__ void load(int kt, float4 (&v)[NV]) const {
-        int k = kt * BK;
-        bool kin = (k + ((threadIdx.x & 3) * 4)) < K;
+    __device__ void load(float4 (&v)[NV]) {
+        bool kin = (k + ((threadIdx.x % KC_TPR) * 4)) < K;
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             bool g = ok[j] && kin;
             float4 t = *reinterpret_cast<const float4*>(g ? p[j] + k : p[j]);
             v[j] = g ? t : f4zero();
         }
+        k += BK;
     }
 };
 
+// (tap, ci) of a thread's float4 column, carried incrementally across K-stages of BK
+__device__ __forceinline__ void tapci_advance(int& tap, int& ci, int cin) {
+    ci += BK;
+    while (ci >= cin) { ci -= cin; ++tap; }
+}
+
 // op(pix, k=(tap,ci)) = X[(b, y+ky-1, x+kx-1)*ld + coff + ci], zero outside the image.
-template <int ROWS>
+// BNR: X is a pre-BatchNorm conv output; apply relu(x*sc[ci] + sh[ci]) to in-image elements.
+template <int ROWS, bool BNR = false>
 struct KcIm2col3x3 {
-    static constexpr int NV = ROWS / 64;
+    static constexpr int NV = ROWS / KC_RPP;
     const float* base;
+    const float *sc, *sh;
     int64_t ld;
     int y[NV], x[NV];
     int64_t pix[NV];
     bool ok[NV];
-    int H, W, cin, K;
+    int H, W, cin, tap, ci;
     __device__ void init(const float* P, int64_t ld_, int coff, int cin_, int B, int H_, int W_,
-                         int row0, int tid) {
-        H = H_; W = W_; cin = cin_; ld = ld_; K = 9 * cin_;
-        base = P + coff;   // the float4 column (tid&3)*4 is folded into ci by load()
+                         int row0, int tid, int kbeg, const float* sc_ = nullptr, const float* sh_ = nullptr) {
+        H = H_; W = W_; cin = cin_; ld = ld_;
+        sc = sc_; sh = sh_;
+        base = P + coff;   // the float4 column (tid&3)*4 is folded into ci
+        const int k = kbeg * BK + (tid % KC_TPR) * 4;
+        tap = k / cin;
+        ci = k - tap * cin;
         int M = B * H * W;
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
-            int r = row0 + tid / 4 + 64 * j;
+            int r = row0 + tid / KC_TPR + KC_RPP * j;
             ok[j] = r < M;
             int rr = ok[j] ? r : 0;
             x[j] = rr % W;
@@ -104,53 +137,59 @@ struct KcIm2col3x3 {
             pix[j] = rr;
         }
     }
-    __device__ void load(int kt, float4 (&v)[NV]) const {
-        int k = kt * BK + (threadIdx.x & 3) * 4;
-        bool kin = k < K;
-        int tap = kin ? k / cin : 0;
-        int ci = k - tap * cin;
-        int dy = tap / 3 - 1, dx = tap % 3 - 1;
-        int64_t off = (int64_t)(dy * W + dx) * ld + ci;
+    __device__ void load(float4 (&v)[NV]) {
+        const bool kin = tap < 9;
+        const int t = kin ? tap : 0;
+        const int dy = t / 3 - 1, dx = t - 3 * (t / 3) - 1;
+        const int64_t off = (int64_t)(dy * W + dx) * ld + ci;
+        float4 s4, h4;
+        if constexpr (BNR) {
+            s4 = *reinterpret_cast<const float4*>(sc + ci);
+            h4 = *reinterpret_cast<const float4*>(sh + ci);
+        }
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             int yy = y[j] + dy, xx = x[j] + dx;
             bool g = ok[j] && kin && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
             const float* q = base + pix[j] * ld + (g ? off : 0);
-            float4 t = *reinterpret_cast<const float4*>(q);
-            v[j] = g ? t : f4zero();
+            float4 tv = *reinterpret_cast<const float4*>(q);
+            if constexpr (BNR) tv = bn_relu4(tv, s4, h4);
+            v[j] = g ? tv : f4zero();
         }
+        tapci_advance(tap, ci, cin);
     }
 };
 
 // op(lowres pix (b,y,x), k=(q=(dy,dx), co)) = G[(b, 2y+dy, 2x+dx)*ld + coff + co]
 template <int ROWS>
 struct KcUpGather {
-    static constexpr int NV = ROWS / 64;
+    static constexpr int NV = ROWS / KC_RPP;
     const float* base;
     int64_t ld;
     int64_t hrpix[NV];   // high-res pixel index of (2y, 2x)
     bool ok[NV];
-    int W2, cout, K;
+    int W2, cout, q, co;
     __device__ void init(const float* P, int64_t ld_, int coff, int cout_, int B, int H, int W,
-                         int row0, int tid) {
-        ld = ld_; cout = cout_; K = 4 * cout_; W2 = 2 * W;
-        base = P + coff;   // the float4 column (tid&3)*4 is folded into ci by load()
+                         int row0, int tid, int kbeg) {
+        ld = ld_; cout = cout_; W2 = 2 * W;
+        base = P + coff;   // the float4 column (tid&3)*4 is folded into co
+        const int k = kbeg * BK + (tid % KC_TPR) * 4;
+        q = k / cout;
+        co = k - q * cout;
         int M = B * H * W;
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
-            int r = row0 + tid / 4 + 64 * j;
+            int r = row0 + tid / KC_TPR + KC_RPP * j;
             ok[j] = r < M;
             int rr = ok[j] ? r : 0;
             int xx = rr % W, t = rr / W, yy = t % H, b = t / H;
             hrpix[j] = ((int64_t)b * (2 * H) + 2 * yy) * W2 + 2 * xx;
         }
     }
-    __device__ void load(int kt, float4 (&v)[NV]) const {
-        int k = kt * BK + (threadIdx.x & 3) * 4;
-        bool kin = k < K;
-        int q = kin ? k / cout : 0;
-        int co = k - q * cout;
-        int64_t off = (int64_t)((q >> 1) * W2 + (q & 1)) * ld + co;
+    __device__ void load(float4 (&v)[NV]) {
+        const bool kin = q < 4;
+        const int qq = kin ? q : 0;
+        const int64_t off = (int64_t)((qq >> 1) * W2 + (qq & 1)) * ld + co;
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             bool g = ok[j] && kin;
@@ -158,6 +197,7 @@ struct KcUpGather {
             float4 t = *reinterpret_cast<const float4*>(p);
             v[j] = g ? t : f4zero();
         }
+        tapci_advance(q, co, cout);
     }
 };
 
@@ -172,42 +212,56 @@ struct MNcBase {
     static constexpr int NV = BK / KSTEP;
 };
 
+// The MNc loaders walk pixels: each thread's k-rows advance by BK pixels per stage, so (x, y) is
+// carried incrementally (one compare-subtract per stage for W >= BK) instead of dividing per stage.
+__device__ __forceinline__ void px_advance(int& x, int& y, int& b, int W, int H) {
+    x += BK;
+    while (x >= W) {
+        x -= W;
+        if (++y == H) { y = 0; ++b; }
+    }
+}
+
 template <int ROWS>
 struct MNcDense : MNcBase<ROWS> {   // op(r, k) = P[k*ld + coff + r], r < nrows, k < Kp
     using Base = MNcBase<ROWS>;
     static constexpr int NV = Base::NV;
     const float* p;
     int64_t ld;
-    int Kp;
+    int Kp, k0;
     bool rok;
-    __device__ void init(const float* P, int64_t ld_, int coff, int nrows, int Kp_, int row0, int tid) {
+    __device__ void init(const float* P, int64_t ld_, int coff, int nrows, int Kp_, int row0, int tid, int kbeg) {
         ld = ld_; Kp = Kp_;
         int r = row0 + (tid % Base::TPR) * 4;
         rok = r < nrows;   // nrows % 4 == 0 is required
         p = P + coff + (rok ? r : 0);
+        k0 = kbeg * BK + tid / Base::TPR;
     }
-    __device__ void load(int kt, float4 (&v)[NV]) const {
+    __device__ void load(float4 (&v)[NV]) {
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
-            int k = kt * BK + threadIdx.x / Base::TPR + Base::KSTEP * j;
+            int k = k0 + Base::KSTEP * j;
             bool g = rok && k < Kp;
             float4 t = *reinterpret_cast<const float4*>(p + (int64_t)(g ? k : 0) * ld);
             v[j] = g ? t : f4zero();
         }
+        k0 += BK;
     }
 };
 
-// op(j=(tap,ci), k=pix) = X[(b,y+ky-1,x+kx-1)*ld + coff + ci]
-template <int ROWS>
+// op(j=(tap,ci), k=pix) = X[(b,y+ky-1,x+kx-1)*ld + coff + ci]   (BNR: relu(x*sc+sh) in-image)
+template <int ROWS, bool BNR = false>
 struct MNcIm2col3x3 : MNcBase<ROWS> {
     using Base = MNcBase<ROWS>;
     static constexpr int NV = Base::NV;
     const float* p;
+    float4 s4, h4;
     int64_t ld;
     int H, W, Kp, dy, dx;
+    int k[NV], x[NV], y[NV];
     bool rok;
     __device__ void init(const float* P, int64_t ld_, int coff, int cin, int B, int H_, int W_,
-                         int row0, int tid) {
+                         int row0, int tid, int kbeg, const float* sc = nullptr, const float* sh = nullptr) {
         ld = ld_; H = H_; W = W_; Kp = B * H_ * W_;
         int j = row0 + (tid % Base::TPR) * 4;
         rok = j < 9 * cin;
@@ -215,18 +269,30 @@ struct MNcIm2col3x3 : MNcBase<ROWS> {
         int tap = jj / cin, ci = jj - tap * cin;
         dy = tap / 3 - 1; dx = tap % 3 - 1;
         p = P + coff + ci;
+        if constexpr (BNR) {
+            s4 = *reinterpret_cast<const float4*>(sc + ci);
+            h4 = *reinterpret_cast<const float4*>(sh + ci);
+        }
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            k[i] = kbeg * BK + tid / Base::TPR + Base::KSTEP * i;
+            int kk = k[i] < Kp ? k[i] : 0;
+            x[i] = kk % W;
+            y[i] = (kk / W) % H;
+        }
     }
-    __device__ void load(int kt, float4 (&v)[NV]) const {
+    __device__ void load(float4 (&v)[NV]) {
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
-            int k = kt * BK + threadIdx.x / Base::TPR + Base::KSTEP * j;
-            int kk = k < Kp ? k : 0;
-            int x = kk % W, y = (kk / W) % H;
-            int yy = y + dy, xx = x + dx;
-            bool g = rok && k < Kp && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
-            int64_t q = g ? (int64_t)kk + dy * W + dx : 0;
+            const int yy = y[j] + dy, xx = x[j] + dx;
+            const bool g = rok && k[j] < Kp && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+            const int64_t q = g ? (int64_t)k[j] + dy * W + dx : 0;
             float4 t = *reinterpret_cast<const float4*>(p + q * ld);
+            if constexpr (BNR) t = bn_relu4(t, s4, h4);
             v[j] = g ? t : f4zero();
+            int b = 0;
+            px_advance(x[j], y[j], b, W, H);
+            k[j] += BK;
         }
     }
 };
@@ -239,9 +305,10 @@ struct MNcUpGather : MNcBase<ROWS> {
     const float* p;
     int64_t ld;
     int H, W, Kp, qy, qx;
+    int k[NV], x[NV], y[NV], b[NV];
     bool rok;
     __device__ void init(const float* P, int64_t ld_, int coff, int cout, int B, int H_, int W_,
-                         int row0, int tid) {
+                         int row0, int tid, int kbeg) {
         ld = ld_; H = H_; W = W_; Kp = B * H_ * W_;
         int j = row0 + (tid % Base::TPR) * 4;
         rok = j < 4 * cout;
@@ -249,17 +316,25 @@ struct MNcUpGather : MNcBase<ROWS> {
         int q = jj / cout, co = jj - q * cout;
         qy = q >> 1; qx = q & 1;
         p = P + coff + co;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            k[i] = kbeg * BK + tid / Base::TPR + Base::KSTEP * i;
+            int kk = k[i] < Kp ? k[i] : 0;
+            x[i] = kk % W;
+            int t = kk / W;
+            y[i] = t % H;
+            b[i] = t / H;
+        }
     }
-    __device__ void load(int kt, float4 (&v)[NV]) const {
+    __device__ void load(float4 (&v)[NV]) {
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
-            int k = kt * BK + threadIdx.x / Base::TPR + Base::KSTEP * j;
-            bool g = rok && k < Kp;
-            int kk = g ? k : 0;
-            int x = kk % W, t = kk / W, y = t % H, b = t / H;
-            int64_t hp = ((int64_t)b * (2 * H) + 2 * y + qy) * (2 * W) + 2 * x + qx;
+            const bool g = rok && k[j] < Kp;
+            const int64_t hp = g ? ((int64_t)b[j] * (2 * H) + 2 * y[j] + qy) * (2 * W) + 2 * x[j] + qx : 0;
             float4 t4 = *reinterpret_cast<const float4*>(p + hp * ld);
             v[j] = g ? t4 : f4zero();
+            px_advance(x[j], y[j], b[j], W, H);
+            k[j] += BK;
         }
     }
 };
@@ -272,7 +347,7 @@ __device__ __forceinline__ void kc_store(float* s, const float4 (&v)[NV]) {
     const int t = threadIdx.x;
 #pragma unroll
     for (int j = 0; j < NV; ++j)
-        *reinterpret_cast<float4*>(s + (t / 4 + 64 * j) * LDK + (t & 3) * 4) = v[j];
+        *reinterpret_cast<float4*>(s + (t / KC_TPR + KC_RPP * j) * LDK + (t % KC_TPR) * 4) = v[j];
 }
 template <int ROWS, int NV>
 __device__ __forceinline__ void mnc_store(float* s, const float4 (&v)[NV]) {
@@ -282,21 +357,22 @@ __device__ __forceinline__ void mnc_store(float* s, const float4 (&v)[NV]) {
     for (int j = 0; j < NV; ++j)
         *reinterpret_cast<float4*>(s + (t / TPR + KSTEP * j) * ROWS + (t % TPR) * 4) = v[j];
 }
-// fragment: 8 consecutive chunk-k values of row (rb + lane&31), half h = lane>>5
-__device__ __forceinline__ void kc_frag(const float* s, int rb, float (&f)[8]) {
+// fragment: HK consecutive chunk-k values of row (rb + lane&31), half h = lane>>5
+__device__ __forceinline__ void kc_frag(const float* s, int rb, float (&f)[HK]) {
     const int lane = threadIdx.x & 63;
-    const float* q = s + (rb + (lane & 31)) * LDK + (lane >> 5) * 8;
-    float4 a = *reinterpret_cast<const float4*>(q);
-    float4 b = *reinterpret_cast<const float4*>(q + 4);
-    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
-    f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+    const float* q = s + (rb + (lane & 31)) * LDK + (lane >> 5) * HK;
+#pragma unroll
+    for (int i = 0; i < HK; i += 4) {
+        float4 a = *reinterpret_cast<const float4*>(q + i);
+        f[i] = a.x; f[i + 1] = a.y; f[i + 2] = a.z; f[i + 3] = a.w;
+    }
 }
 template <int ROWS>
-__device__ __forceinline__ void mnc_frag(const float* s, int rb, float (&f)[8]) {
+__device__ __forceinline__ void mnc_frag(const float* s, int rb, float (&f)[HK]) {
     const int lane = threadIdx.x & 63;
-    const float* q = s + (lane >> 5) * 8 * ROWS + rb + (lane & 31);
+    const float* q = s + (lane >> 5) * HK * ROWS + rb + (lane & 31);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) f[i] = q[i * ROWS];
+    for (int i = 0; i < HK; ++i) f[i] = q[i * ROWS];
 }
 
 template <bool KC, int ROWS>
@@ -310,6 +386,34 @@ struct OpLds {
 // plus static constexpr bool STATS (per-column BN partial sums written to a.stats).
 // blockIdx.x -> M tile, blockIdx.y -> N tile, blockIdx.z -> split-K slice.
 // --------------------------------------------------------------------------------------------
+template <class E, class = void>
+struct is_structured : std::false_type {};
+template <class E>
+struct is_structured<E, std::void_t<decltype(E::STRUCTURED)>> : std::integral_constant<bool, E::STRUCTURED> {};
+
+// XCD-aware tile order (cdna_hip_programming.md T1, bijective form): the dispatcher deals linear
+// block ids round-robin over the 8 XCDs, so consecutive ids land on different private L2s.  Remap so
+// that each XCD walks a contiguous range of logical tiles (x fastest): neighbouring M-tiles, which
+// share im2col halo rows, then hit the same L2.  Speed only: any placement gives the same result.
+struct TileId {
+    int x, y, z;
+};
+__device__ __forceinline__ TileId xcd_tile() {
+    const int nx = gridDim.x, ny = gridDim.y;
+    const int nwg = nx * ny * gridDim.z;
+    const int L = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+    int logical = L;
+    if (CAD_XCD_SWIZZLE && nwg > 8) {
+        const int q = nwg / 8, r = nwg % 8, xcd = L % 8;
+        logical = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
+    }
+    TileId t;
+    t.x = logical % nx;
+    t.y = (logical / nx) % ny;
+    t.z = logical / (nx * ny);
+    return t;
+}
+
 template <int WM, int WN, class LA, bool KCA, class LB, bool KCB, class Epi, class InitA, class InitB>
 __device__ __forceinline__ void gemm_body(const GemmArgs& a, InitA init_a, InitB init_b, Epi epi) {
     constexpr int BM = 64 * WM, BN = 64 * WN;
@@ -319,15 +423,16 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, InitA init_a, InitB
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
     const int wm = wave / WN, wn = wave % WN;
-    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-
-    LA la; LB lb;
-    init_a(la, m0, tid);
-    init_b(lb, n0, tid);
+    const TileId tile = xcd_tile();
+    const int m0 = tile.x * BM, n0 = tile.y * BN;
 
     const int nk_total = (a.K + BK - 1) / BK;
-    const int kbeg = blockIdx.z * a.kstages_per_split;
+    const int kbeg = tile.z * a.kstages_per_split;
     const int kend = min(nk_total, kbeg + a.kstages_per_split);
+
+    LA la; LB lb;
+    init_a(la, m0, tid, kbeg);
+    init_b(lb, n0, tid, kbeg);
 
     floatx16 acc[2][2];
 #pragma unroll
@@ -337,41 +442,70 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, InitA init_a, InitB
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    float4 ra[LA::NV], rb[LB::NV];
-    if (kbeg < kend) {
-        la.load(kbeg, ra);
-        lb.load(kbeg, rb);
-        if constexpr (KCA) kc_store<BM>(lds, ra); else mnc_store<BM>(lds, ra);
-        if constexpr (KCB) kc_store<BN>(lds + SA, rb); else mnc_store<BN>(lds + SA, rb);
-    }
-    __syncthreads();
-    int cur = 0;
-    for (int kt = kbeg; kt < kend; ++kt) {
-        const bool more = kt + 1 < kend;
-        if (more) { la.load(kt + 1, ra); lb.load(kt + 1, rb); }
-        const float* sa = lds + cur * (SA + SB);
+    auto stage_store = [&](int buf, const float4 (&xa)[LA::NV], const float4 (&xb)[LB::NV]) {
+        float* da = lds + buf * (SA + SB);
+        if constexpr (KCA) kc_store<BM>(da, xa); else mnc_store<BM>(da, xa);
+        if constexpr (KCB) kc_store<BN>(da + SA, xb); else mnc_store<BN>(da + SA, xb);
+    };
+    auto stage_compute = [&](int buf) {
+        const float* sa = lds + buf * (SA + SB);
         const float* sb = sa + SA;
-        float fa[2][8], fb[2][8];
+        float fa[2][HK], fb[2][HK];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             if constexpr (KCA) kc_frag(sa, wm * 64 + i * 32, fa[i]); else mnc_frag<BM>(sa, wm * 64 + i * 32, fa[i]);
             if constexpr (KCB) kc_frag(sb, wn * 64 + i * 32, fb[i]); else mnc_frag<BN>(sb, wn * 64 + i * 32, fb[i]);
         }
 #pragma unroll
-        for (int s = 0; s < 8; ++s)
+        for (int s = 0; s < HK; ++s)
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
-        if (more) {
-            float* da = lds + (cur ^ 1) * (SA + SB);
-            if constexpr (KCA) kc_store<BM>(da, ra); else mnc_store<BM>(da, ra);
-            if constexpr (KCB) kc_store<BN>(da + SA, rb); else mnc_store<BN>(da + SA, rb);
-        }
+    };
+
+#if CAD_PREFETCH2
+    // Global loads run two K-stages ahead of the MFMAs (two register sets, loop unrolled x2 so every
+    // register index is static): a stage's operands have two stage-times to arrive before the LDS write.
+    float4 ra0[LA::NV], rb0[LB::NV], ra1[LA::NV], rb1[LB::NV];
+    if (kbeg < kend) {
+        la.load(ra0);
+        lb.load(rb0);
+        stage_store(0, ra0, rb0);
+    }
+    if (kbeg + 1 < kend) { la.load(ra0); lb.load(rb0); }
+    __syncthreads();
+    for (int kt = kbeg; kt < kend;) {
+        if (kt + 2 < kend) { la.load(ra1); lb.load(rb1); }
+        stage_compute(0);
+        if (kt + 1 < kend) stage_store(1, ra0, rb0);
+        __syncthreads();
+        if (++kt >= kend) break;
+        if (kt + 2 < kend) { la.load(ra0); lb.load(rb0); }
+        stage_compute(1);
+        if (kt + 1 < kend) stage_store(0, ra1, rb1);
+        __syncthreads();
+        ++kt;
+    }
+#else
+    float4 ra[LA::NV], rb[LB::NV];
+    if (kbeg < kend) {
+        la.load(ra);
+        lb.load(rb);
+        stage_store(0, ra, rb);
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int kt = kbeg; kt < kend; ++kt) {
+        const bool more = kt + 1 < kend;
+        if (more) { la.load(ra); lb.load(rb); }
+        stage_compute(cur);
+        if (more) stage_store(cur ^ 1, ra, rb);
         __syncthreads();
         cur ^= 1;
     }
+#endif
 
     // epilogue: element (m, n) of sub-block (i, j), register r
     const int h = lane >> 5, col = lane & 31;
@@ -380,10 +514,14 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, InitA init_a, InitB
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int n = n0 + wn * 64 + j * 32 + col;
+            if constexpr (is_structured<Epi>::value) {
+                epi.block(a, m0 + wm * 64 + i * 32 + 4 * h, n, acc[i][j]);
+            } else {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (m < a.M && n < a.N) epi(a, m, n, acc[i][j][r]);
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    if (m < a.M && n < a.N) epi(a, m, n, acc[i][j][r], tile.z);
+                }
             }
         }
 
@@ -418,8 +556,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, InitA init_a, InitB
             for (int w = 0; w < WM; ++w) { s += red[(w * BN + c) * 2]; q += red[(w * BN + c) * 2 + 1]; }
             const int n = n0 + c;
             if (n < a.N) {
-                a.stats[(int64_t)blockIdx.x * 2 * a.N + n] = s;
-                a.stats[(int64_t)blockIdx.x * 2 * a.N + a.N + n] = q;
+                a.stats[(int64_t)tile.x * 2 * a.N + n] = s;
+                a.stats[(int64_t)tile.x * 2 * a.N + a.N + n] = q;
             }
         }
     }

@@ -15,15 +15,19 @@ void prof_pop(hipStream_t st);
 
 // ---------------- convolutions (conv_kernels.hip) ----------------
 // y = conv3x3(x) (+ per-tile BN partials [rows][2][cout] when stats != nullptr)
+// in_scale/in_shift != nullptr: x is a pre-BN conv output and the loader applies
+// relu(x*scale[c] + shift[c]) on the fly (BN-apply + ReLU fused into the consumer)
 void conv3x3_fwd(const float* x, int64_t ldx, int xcoff, int cin, const float* w, int cout, float* y,
-                 int64_t ldy, int ycoff, int B, int H, int W, float* stats, hipStream_t st);
+                 int64_t ldy, int ycoff, int B, int H, int W, float* stats, hipStream_t st,
+                 const float* in_scale = nullptr, const float* in_shift = nullptr);
 int conv3x3_stats_rows(int B, int H, int W, int cout);
 // dx[pix][ci] = conv3x3(dz, wd) with wd = repacked [ci][tap'][co]
 void conv3x3_dgrad(const float* dz, int cout, const float* wd, int cin, float* dx, int64_t lddx,
                    int B, int H, int W, hipStream_t st);
 // dw[co][tap][ci] = sum_pix dz[pix][co] * im2col(x)[pix][tap,ci]
 void conv3x3_wgrad(const float* dz, int cout, const float* x, int64_t ldx, int xcoff, int cin, float* dw,
-                   int B, int H, int W, float* slab, int64_t slab_cap, hipStream_t st);
+                   int B, int H, int W, float* slab, int64_t slab_cap, hipStream_t st,
+                   const float* x_scale = nullptr, const float* x_shift = nullptr);
 // ConvTranspose2d(k2,s2): (B,H,W,cin) -> (B,2H,2W,cout) written at channel offset ycoff of rows ldy
 void convT_fwd(const float* x, int64_t ldx, int cin, const float* wf, const float* bias, int cout,
                float* y, int64_t ldy, int ycoff, int B, int H, int W, hipStream_t st);

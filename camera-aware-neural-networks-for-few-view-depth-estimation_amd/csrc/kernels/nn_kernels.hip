@@ -328,10 +328,36 @@ __global__ void k_maxpool_bwd(const float* __restrict__ dout, const uint8_t* __r
         }
     }
 }
+// gather form: one thread per (INPUT pixel, 4 channels) inside the pooled region, coalesced float4
+// read-modify-write of dx; adds dout[parent] where this pixel is the recorded argmax
+__global__ void k_maxpool_bwd_gather(const float* __restrict__ dout, const uint8_t* __restrict__ idx, int C, int B,
+                                     int H, int W, float* __restrict__ dx, int64_t lddx, int64_t n4) {
+    const int C4 = C >> 2, Ho = H >> 1, Wo = W >> 1, He = 2 * Ho, We = 2 * Wo;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t p = i / C4;          // pixel in the (2Ho x 2Wo) pooled region
+        const int c = (int)(i - p * C4) * 4;
+        const int x = (int)(p % We);
+        const int64_t t = p / We;
+        const int y = (int)(t % He);
+        const int b = (int)(t / He);
+        const int code = ((y & 1) << 1) | (x & 1);
+        const int64_t op = ((int64_t)b * Ho + (y >> 1)) * Wo + (x >> 1);
+        const uchar4 a = *reinterpret_cast<const uchar4*>(idx + op * C + c);
+        if (a.x != code && a.y != code && a.z != code && a.w != code) continue;
+        const float4 d = *reinterpret_cast<const float4*>(dout + op * C + c);
+        float* q = dx + (((int64_t)b * H + y) * W + x) * lddx + c;
+        float4 v = *reinterpret_cast<float4*>(q);
+        if (a.x == code) v.x += d.x;
+        if (a.y == code) v.y += d.y;
+        if (a.z == code) v.z += d.z;
+        if (a.w == code) v.w += d.w;
+        *reinterpret_cast<float4*>(q) = v;
+    }
+}
 void maxpool_bwd(const float* dout, const uint8_t* idx, int C, int B, int H, int W, float* dx,
                  int64_t lddx, hipStream_t st) {
-    const int64_t n4 = (int64_t)B * (H / 2) * (W / 2) * C / 4;
-    hipLaunchKernelGGL(k_maxpool_bwd, dim3(ew_blocks(n4)), dim3(256), 0, st, dout, idx, C, B, H, W, dx, lddx, n4);
+    const int64_t n4 = (int64_t)B * (H / 2 * 2) * (W / 2 * 2) * C / 4;
+    hipLaunchKernelGGL(k_maxpool_bwd_gather, dim3(ew_blocks(n4)), dim3(256), 0, st, dout, idx, C, B, H, W, dx, lddx, n4);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -365,9 +391,38 @@ __global__ void k_head_fwd(const float* __restrict__ a, int C, const float* __re
         pred[p] = s * md;
     }
 }
+// coalesced form: TPP = C/4 lanes share one pixel row (one float4 each), shuffle-reduced
+template <int TPP>
+__global__ __launch_bounds__(256) void k_head_fwd_coop(const float* __restrict__ a, int C, const float* __restrict__ w,
+                                                       const float* __restrict__ b, float md, float* __restrict__ sig,
+                                                       float* __restrict__ pred, int64_t M) {
+    const int sub = threadIdx.x % TPP;
+    const float4 wv = *reinterpret_cast<const float4*>(w + sub * 4);
+    for (int64_t p = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / TPP; p < M;
+         p += (int64_t)gridDim.x * blockDim.x / TPP) {
+        float4 v = *reinterpret_cast<const float4*>(a + p * C + sub * 4);
+        float z = v.x * wv.x + v.y * wv.y + v.z * wv.z + v.w * wv.w;
+#pragma unroll
+        for (int o = TPP / 2; o > 0; o >>= 1) z += __shfl_xor(z, o);
+        if (sub == 0) {
+            z += b[0];
+            const float s = 1.f / (1.f + expf(-z));
+            sig[p] = s;
+            pred[p] = s * md;
+        }
+    }
+}
 void head_fwd(const float* a, int C, const float* w, const float* b, float max_depth, float* sig,
               float* pred, int64_t M, hipStream_t st) {
-    hipLaunchKernelGGL(k_head_fwd, dim3(ew_blocks(M)), dim3(256), 0, st, a, C, w, b, max_depth, sig, pred, M);
+    const int blocks = std::max(1, std::min(8192, cdiv(M * (C / 4), 256)));
+    switch (C / 4) {
+        case 16: hipLaunchKernelGGL(k_head_fwd_coop<16>, dim3(blocks), dim3(256), 0, st, a, C, w, b, max_depth, sig, pred, M); return;
+        case 32: hipLaunchKernelGGL(k_head_fwd_coop<32>, dim3(blocks), dim3(256), 0, st, a, C, w, b, max_depth, sig, pred, M); return;
+        case 8: hipLaunchKernelGGL(k_head_fwd_coop<8>, dim3(blocks), dim3(256), 0, st, a, C, w, b, max_depth, sig, pred, M); return;
+        case 4: hipLaunchKernelGGL(k_head_fwd_coop<4>, dim3(blocks), dim3(256), 0, st, a, C, w, b, max_depth, sig, pred, M); return;
+        default:
+            hipLaunchKernelGGL(k_head_fwd, dim3(ew_blocks(M)), dim3(256), 0, st, a, C, w, b, max_depth, sig, pred, M);
+    }
 }
 
 __global__ void k_head_da(const float* __restrict__ w, int C, const float* __restrict__ dpred,
