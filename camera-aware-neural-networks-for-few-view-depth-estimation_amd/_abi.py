@@ -44,6 +44,10 @@ SIGNATURES = {
     "cad_adam_state": (I, [P, C.POINTER(P), C.POINTER(P)]),
     "cad_adam_set_step_count": (I, [P, I64]),
     "cad_unet_create": (I, [C.POINTER(UnetDesc), I, C.POINTER(P)]),
+    "cad_unet_create_model": (I, [C.POINTER(UnetDesc), I, I, C.POINTER(P)]),
+    "cad_unet_model": (I, [P]),
+    "cad_unet_forward_cam": (I, [P, P, P, P, I, P]),
+    "cad_camera_from_K": (I, [P, I, P, P]),
     "cad_unet_destroy": (None, [P]),
     "cad_unet_count_parameters": (I64, [P]),
     "cad_unet_num_params": (I, [P]),

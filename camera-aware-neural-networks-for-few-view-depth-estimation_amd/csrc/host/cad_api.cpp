@@ -13,6 +13,11 @@
 //         encoder writes the skip half, the ConvTranspose epilogue writes the up half: no cat/pad.
 //   pool_l [M_l][C_{l-1}] + uint8 argmax; dec: y1d, a1d, y2d, d_l [M_l][C_l].
 // Backward scratch: S_a, S_b [M_0][C_0], S_c [M_1][C_0]; dcat_l [M_l][2 C_l].
+//
+// Config-3 models (cad_unet_create_model): every DoubleConv also owns a FiLMLayer (film_layer.h);
+// its a1 = FiLM(relu(bn1(y1))) is materialised [M_l][C_l] (conv2 reads it, conv2's wgrad too), and
+// the FiLM MLPs of all nine blocks run at the start of the forward (they only see the camera).
+// RAY_FILM's enc1 reads NHWC8 [rgb | rays | 0 0] built on device from the intrinsics.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -78,7 +83,11 @@ struct Arena {
     uint8_t* u8(int64_t n) { return static_cast<uint8_t*>(take((size_t)std::max<int64_t>(n, 1))); }
 };
 
-enum PKind { P_CONV3, P_BNW, P_BNB, P_CONVT_W, P_CONVT_B, P_HEAD_W, P_HEAD_B };
+enum PKind {
+    P_CONV3, P_BNW, P_BNB, P_CONVT_W, P_CONVT_B, P_HEAD_W, P_HEAD_B,
+    P_FC_W, P_FC_B,                                  // FiLM fc1 / fc2 (torch::nn::Linear defaults)
+    P_FILM_HEAD_W, P_FILM_GAMMA_B, P_FILM_BETA_B     // fc_gamma / fc_beta (film_layer.h:68-71)
+};
 
 struct PInfo {
     std::string name;
@@ -106,12 +115,19 @@ struct Conv {
     int pidx = -1, cin = 0, cout = 0;
     float* wd = nullptr;   // dgrad repack
 };
+struct Film {
+    int p0 = -1;   // index of film.fc1.weight; the 12 FiLM parameters follow in registration order
+    float *rm1, *rv1, *rm2, *rv2;
+    float *xh1, *h1, *xh2, *h2, *is1, *is2, *gam, *bet, *dgam, *dbet, *dh2, *dh1;
+};
 struct DoubleConv {
     Conv c1, c2;
     BN b1, b2;
+    Film film;     // film.p0 < 0: plain DoubleConv
     int level = 0;
     float *y1 = nullptr, *a1 = nullptr, *y2 = nullptr;
     int first_param = 0, last_param = 0;   // [first, last] indices in named_parameters()
+    bool has_film() const { return film.p0 >= 0; }
 };
 struct Up {
     int widx = -1, bidx = -1, cin = 0, cout = 0;
@@ -122,7 +138,10 @@ struct Up {
 
 struct cad_unet {
     int device = 0;
+    int model = CAD_MODEL_BASELINE;
     int in_ch = 3, f = 64, Bmax = 1, H = 0, W = 0;
+    int x0_ld = 4;               // NHWC4 rgb (baseline, film) or NHWC8 rgb+rays (ray_film)
+    float* camn = nullptr;       // normalised intrinsics (Bmax x 4) of the last forward
     float max_depth = 10.f;
     bool train = true;
     bool have_fwd = false;
@@ -201,6 +220,24 @@ void add_param(cad_unet* h, const std::string& name, std::vector<int64_t> shape,
     h->params.push_back(p);
 }
 
+void add_film(cad_unet* h, DoubleConv& dc, const std::string& pre, int C) {
+    // FiLMLayerImpl ctor registration order (film_layer.h:55-66): fc1, fc2, fc_gamma, fc_beta, bn1, bn2
+    const int H1 = cad::kFilmH1, H2 = cad::kFilmH2;
+    dc.film.p0 = (int)h->params.size();
+    add_param(h, pre + "fc1.weight", {H1, 4}, P_FC_W);
+    add_param(h, pre + "fc1.bias", {H1}, P_FC_B);
+    add_param(h, pre + "fc2.weight", {H2, H1}, P_FC_W);
+    add_param(h, pre + "fc2.bias", {H2}, P_FC_B);
+    add_param(h, pre + "fc_gamma.weight", {C, H2}, P_FILM_HEAD_W);
+    add_param(h, pre + "fc_gamma.bias", {C}, P_FILM_GAMMA_B);
+    add_param(h, pre + "fc_beta.weight", {C, H2}, P_FILM_HEAD_W);
+    add_param(h, pre + "fc_beta.bias", {C}, P_FILM_BETA_B);
+    add_param(h, pre + "bn1.weight", {H1}, P_BNW);
+    add_param(h, pre + "bn1.bias", {H1}, P_BNB);
+    add_param(h, pre + "bn2.weight", {H2}, P_BNW);
+    add_param(h, pre + "bn2.bias", {H2}, P_BNB);
+}
+
 void add_double_conv(cad_unet* h, DoubleConv& dc, const std::string& pre, int cin_ref, int cin_int, int cout, int level) {
     dc.level = level;
     dc.first_param = (int)h->params.size();
@@ -214,12 +251,16 @@ void add_double_conv(cad_unet* h, DoubleConv& dc, const std::string& pre, int ci
     add_param(h, pre + "bn2.weight", {cout}, P_BNW);
     add_param(h, pre + "bn2.bias", {cout}, P_BNB);
     dc.b2.C = cout; dc.b2.widx = (int)h->params.size() - 2; dc.b2.bidx = (int)h->params.size() - 1;
+    if (h->model != CAD_MODEL_BASELINE) add_film(h, dc, pre + "film.", cout);   // intrinsics_unet.h:34
     dc.last_param = (int)h->params.size() - 1;
 }
 
 void build_tables(cad_unet* h) {
     const int f = h->f;
-    add_double_conv(h, h->enc[0], "enc1.", h->in_ch, 4, f, 0);
+    if (h->model == CAD_MODEL_RAY_FILM)   // RayEnhancedConv(3, f, 4, true): conv1 sees rgb + rays
+        add_double_conv(h, h->enc[0], "enc1.", h->in_ch + 3, 8, f, 0);
+    else
+        add_double_conv(h, h->enc[0], "enc1.", h->in_ch, 4, f, 0);
     const char* enames[4] = {"enc2", "enc3", "enc4", "bottleneck"};
     for (int i = 0; i < 4; ++i)
         add_double_conv(h, h->enc[i + 1], std::string(enames[i]) + ".conv.", f << i, f << i, f << (i + 1), i + 1);
@@ -245,16 +286,32 @@ void bn_alloc(Arena& a, BN& b) {
     b.mean = a.f(b.C); b.invstd = a.f(b.C); b.scale = a.f(b.C); b.shift = a.f(b.C); b.coef = a.f(3 * b.C);
 }
 
+void film_alloc(Arena& a, DoubleConv& dc, int B) {
+    if (!dc.has_film()) return;
+    Film& F = dc.film;
+    const int H1 = cad::kFilmH1, H2 = cad::kFilmH2, C = dc.c1.cout;
+    F.rm1 = a.f(H1); F.rv1 = a.f(H1); F.rm2 = a.f(H2); F.rv2 = a.f(H2);
+    F.xh1 = a.f((int64_t)B * H1); F.h1 = a.f((int64_t)B * H1); F.dh1 = a.f((int64_t)B * H1);
+    F.xh2 = a.f((int64_t)B * H2); F.h2 = a.f((int64_t)B * H2); F.dh2 = a.f((int64_t)B * H2);
+    F.is1 = a.f(H1); F.is2 = a.f(H2);
+    F.gam = a.f((int64_t)B * C); F.bet = a.f((int64_t)B * C);
+    F.dgam = a.f((int64_t)B * C); F.dbet = a.f((int64_t)B * C);
+}
+
 void layout(cad_unet* h, Arena& a) {
     const int B = h->Bmax;
+    const bool film = h->model != CAD_MODEL_BASELINE;
     h->flat_p = a.f(h->n_flat);
     h->flat_g = a.f(h->n_flat);
     h->norm_coef = a.f(4);
+    h->camn = a.f((int64_t)B * 4);
     for (int l = 0; l < 5; ++l) {
         DoubleConv& e = h->enc[l];
         bn_alloc(a, e.b1); bn_alloc(a, e.b2);
         const int64_t MC = h->Ml(l, B) * h->Cl(l);
-        e.y1 = a.f(MC); e.y2 = a.f(MC);   // a1 is fused into conv2's loaders
+        e.y1 = a.f(MC); e.y2 = a.f(MC);   // a1 is fused into conv2's loaders (baseline)
+        if (film) e.a1 = a.f(MC);          // FiLM output feeding conv2
+        film_alloc(a, e, B);
         if (l > 0) e.c1.wd = a.f((int64_t)e.c1.cout * 9 * e.c1.cin);
         e.c2.wd = a.f((int64_t)e.c2.cout * 9 * e.c2.cin);
         if (l < 4) h->cat[l] = a.f(2 * MC);
@@ -269,13 +326,15 @@ void layout(cad_unet* h, Arena& a) {
         bn_alloc(a, d.b1); bn_alloc(a, d.b2);
         const int64_t MC = h->Ml(l, B) * h->Cl(l);
         d.y1 = a.f(MC); d.y2 = a.f(MC);
+        if (film) d.a1 = a.f(MC);
+        film_alloc(a, d, B);
         h->dout[l] = a.f(MC);
         d.c1.wd = a.f((int64_t)d.c1.cout * 9 * d.c1.cin);
         d.c2.wd = a.f((int64_t)d.c2.cout * 9 * d.c2.cin);
         h->up[l].wf = a.f((int64_t)4 * h->up[l].cout * h->up[l].cin);
         h->dcat[l] = a.f(2 * MC);
     }
-    h->x0 = a.f(h->Ml(0, B) * 4);
+    h->x0 = a.f(h->Ml(0, B) * h->x0_ld);
     h->sig = a.f(h->Ml(0, B));
     const int64_t M0C0 = h->Ml(0, B) * h->Cl(0);
     h->Sa = a.f(M0C0);
@@ -289,7 +348,10 @@ void layout(cad_unet* h, Arena& a) {
         colmax = std::max<int64_t>(colmax, h->Cl(l));
     }
     h->stats = a.f(st);
-    h->dscr = a.d((int64_t)(cad::colsum_slices(h->Ml(0, B)) + 2) * 4 * colmax + 4 * colmax + 8192);
+    int64_t dscr = (int64_t)(cad::colsum_slices(h->Ml(0, B)) + 2) * 4 * colmax + 4 * colmax + 8192;
+    for (int l = 0; l < 5 && film; ++l)
+        dscr = std::max(dscr, cad::film_reduce_doubles(B, (int64_t)h->Hl(l) * h->Wl(l), h->Cl(l)) + 8192);
+    h->dscr = a.d(dscr);
     // wgrad split-K slab: enough for the largest-benefit layers, capped at 64M floats (256 MB)
     int64_t sl = 0;
     for (int l = 0; l < 5; ++l) {
@@ -304,19 +366,45 @@ void layout(cad_unet* h, Arena& a) {
         h->bufs.push_back({pre + ".running_mean", b.C, b.rm});
         h->bufs.push_back({pre + ".running_var", b.C, b.rv});
     };
+    auto add_block = [&](const std::string& pre, DoubleConv& dc) {
+        add_bn_bufs(pre + "bn1", dc.b1);
+        add_bn_bufs(pre + "bn2", dc.b2);
+        if (!dc.has_film()) return;
+        h->bufs.push_back({pre + "film.bn1.running_mean", cad::kFilmH1, dc.film.rm1});
+        h->bufs.push_back({pre + "film.bn1.running_var", cad::kFilmH1, dc.film.rv1});
+        h->bufs.push_back({pre + "film.bn2.running_mean", cad::kFilmH2, dc.film.rm2});
+        h->bufs.push_back({pre + "film.bn2.running_var", cad::kFilmH2, dc.film.rv2});
+    };
     const char* en[5] = {"enc1.", "enc2.conv.", "enc3.conv.", "enc4.conv.", "bottleneck.conv."};
-    for (int l = 0; l < 5; ++l) { add_bn_bufs(std::string(en[l]) + "bn1", h->enc[l].b1); add_bn_bufs(std::string(en[l]) + "bn2", h->enc[l].b2); }
+    for (int l = 0; l < 5; ++l) add_block(en[l], h->enc[l]);
     for (int k = 0; k < 4; ++k) {
         const int l = 3 - k;
-        const std::string pre = "dec" + std::to_string(l + 1) + ".conv.";
-        add_bn_bufs(pre + "bn1", h->dec[l].b1);
-        add_bn_bufs(pre + "bn2", h->dec[l].b2);
+        add_block("dec" + std::to_string(l + 1) + ".conv.", h->dec[l]);
     }
 }
 
 // ------------------------------------------------------------------------------------------
 // forward
 // ------------------------------------------------------------------------------------------
+// the FilmLayer view of a block (pointers into the current slabs: rebuilt per use because the slabs
+// can move, cad_unet_use_external_slabs)
+cad::FilmLayer film_view(const cad_unet* h, const DoubleConv& dc) {
+    const Film& F = dc.film;
+    const int i = F.p0;
+    cad::FilmLayer L;
+    L.C = dc.c1.cout;
+    L.w1 = h->P(i); L.b1 = h->P(i + 1); L.w2 = h->P(i + 2); L.b2 = h->P(i + 3);
+    L.wg = h->P(i + 4); L.bg = h->P(i + 5); L.wb = h->P(i + 6); L.bb = h->P(i + 7);
+    L.g1 = h->P(i + 8); L.be1 = h->P(i + 9); L.g2 = h->P(i + 10); L.be2 = h->P(i + 11);
+    L.rm1 = F.rm1; L.rv1 = F.rv1; L.rm2 = F.rm2; L.rv2 = F.rv2;
+    L.xh1 = F.xh1; L.h1 = F.h1; L.xh2 = F.xh2; L.h2 = F.h2; L.is1 = F.is1; L.is2 = F.is2;
+    L.gam = F.gam; L.bet = F.bet; L.dgam = F.dgam; L.dbet = F.dbet; L.dh2 = F.dh2; L.dh1 = F.dh1;
+    L.gw1 = h->G(i); L.gb1 = h->G(i + 1); L.gw2 = h->G(i + 2); L.gb2 = h->G(i + 3);
+    L.gwg = h->G(i + 4); L.gbg = h->G(i + 5); L.gwb = h->G(i + 6); L.gbb = h->G(i + 7);
+    L.gg1 = h->G(i + 8); L.gbe1 = h->G(i + 9); L.gg2 = h->G(i + 10); L.gbe2 = h->G(i + 11);
+    return L;
+}
+
 void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin, int B, float* out, int64_t ldo,
                      int ocoff, hipStream_t st) {
     const int l = dc.level, Hh = h->Hl(l), Ww = h->Wl(l), C = dc.c1.cout;
@@ -332,19 +420,33 @@ void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin,
     };
     cad::conv3x3_fwd(in, ldin, 0, dc.c1.cin, h->P(dc.c1.pidx), C, dc.y1, C, 0, B, Hh, Ww, tr ? h->stats : nullptr, st);
     bn(dc.b1);
-    // a1 = relu(bn1(y1)) is never materialised: conv2's loader applies it (and so does conv2's wgrad)
-    cad::conv3x3_fwd(dc.y1, C, 0, C, h->P(dc.c2.pidx), C, dc.y2, C, 0, B, Hh, Ww, tr ? h->stats : nullptr, st,
-                     dc.b1.scale, dc.b1.shift);
+    if (dc.has_film()) {   // FiLMDoubleConvImpl::forward (intrinsics_unet.h:38-52)
+        cad::film_apply(dc.y1, C, dc.b1.scale, dc.b1.shift, dc.film.gam, dc.film.bet, B, (int64_t)Hh * Ww, dc.a1, st);
+        cad::conv3x3_fwd(dc.a1, C, 0, C, h->P(dc.c2.pidx), C, dc.y2, C, 0, B, Hh, Ww, tr ? h->stats : nullptr, st);
+    } else {
+        // a1 = relu(bn1(y1)) is never materialised: conv2's loader applies it (and so does conv2's wgrad)
+        cad::conv3x3_fwd(dc.y1, C, 0, C, h->P(dc.c2.pidx), C, dc.y2, C, 0, B, Hh, Ww, tr ? h->stats : nullptr, st,
+                         dc.b1.scale, dc.b1.shift);
+    }
     bn(dc.b2);
     cad::bn_relu_fwd(dc.y2, C, dc.b2.scale, dc.b2.shift, out, ldo, ocoff, M, st);
 }
 
-void unet_forward(cad_unet* h, const float* rgb, float* depth, int B, hipStream_t st) {
+void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth, int B, hipStream_t st) {
     const int f = h->f;
     for (int l = 0; l < 4; ++l)
         cad::repack_convT_fwd(h->P(h->up[l].widx), h->up[l].wf, h->up[l].cin, h->up[l].cout, st);
-    cad::rgb_to_nhwc4(rgb, h->x0, B, h->H, h->W, st);
-    double_conv_fwd(h, h->enc[0], h->x0, 4, B, h->cat[0], 2 * f, 0, st);
+    if (h->model != CAD_MODEL_BASELINE) {
+        // a14 normalisation, then every block's FiLM MLP (gamma/beta depend on the camera only)
+        cad::camera_normalize(cam4, B, h->H, h->W, h->camn, st);
+        for (int l = 0; l < 5; ++l) cad::film_mlp_fwd(film_view(h, h->enc[l]), h->camn, B, h->train, st);
+        for (int l = 3; l >= 0; --l) cad::film_mlp_fwd(film_view(h, h->dec[l]), h->camn, B, h->train, st);
+    }
+    if (h->model == CAD_MODEL_RAY_FILM)
+        cad::rgb_rays_to_nhwc8(rgb, cam4, B, h->H, h->W, h->x0, st);
+    else
+        cad::rgb_to_nhwc4(rgb, h->x0, B, h->H, h->W, st);
+    double_conv_fwd(h, h->enc[0], h->x0, h->x0_ld, B, h->cat[0], 2 * f, 0, st);
     for (int l = 1; l <= 4; ++l) {
         const int Cp = h->Cl(l - 1);
         cad::maxpool_fwd(h->cat[l - 1], 2 * Cp, Cp, B, h->Hl(l - 1), h->Wl(l - 1), h->pool[l], h->pidx[l], st);
@@ -378,12 +480,21 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     cad::bn_relu_bwd(g, ldg, gcoff, dc.y2, C, dc.b2.mean, dc.b2.invstd, dc.b2.scale, dc.b2.shift, h->P(dc.b2.widx), M,
                      h->dscr, dc.b2.coef, h->G(dc.b2.widx), h->G(dc.b2.bidx), dY, st);
     // conv2
-    cad::conv3x3_wgrad(dY, C, dc.y1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st,
-                       dc.b1.scale, dc.b1.shift);
+    if (dc.has_film())
+        cad::conv3x3_wgrad(dY, C, dc.a1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
+    else
+        cad::conv3x3_wgrad(dY, C, dc.y1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st,
+                           dc.b1.scale, dc.b1.shift);
     cad::conv3x3_dgrad(dY, C, dc.c2.wd, C, dA1, C, B, Hh, Ww, st);
+    // FiLM: dgamma/dbeta per (sample, channel); the ReLU sees dA1 * gamma (folded into bn_relu_bwd)
+    const int64_t HW = (int64_t)Hh * Ww;
+    if (dc.has_film())
+        cad::film_affine_bwd(dA1, dc.y1, C, dc.b1.scale, dc.b1.shift, B, HW, h->dscr, dc.film.dgam, dc.film.dbet, st);
     // bn1 + relu
     cad::bn_relu_bwd(dA1, C, 0, dc.y1, C, dc.b1.mean, dc.b1.invstd, dc.b1.scale, dc.b1.shift, h->P(dc.b1.widx), M,
-                     h->dscr, dc.b1.coef, h->G(dc.b1.widx), h->G(dc.b1.bidx), dY, st);
+                     h->dscr, dc.b1.coef, h->G(dc.b1.widx), h->G(dc.b1.bidx), dY, st,
+                     dc.has_film() ? dc.film.gam : nullptr, HW);
+    if (dc.has_film()) cad::film_mlp_bwd(film_view(h, dc), h->camn, B, st);
     // conv1
     cad::conv3x3_wgrad(dY, C, in, ldin, 0, dc.c1.cin, h->G(dc.c1.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
     if (din) cad::conv3x3_dgrad(dY, C, dc.c1.wd, dc.c1.cin, din, lddin, B, Hh, Ww, st);
@@ -431,7 +542,7 @@ void backward_stage(cad_unet* h, int stage, const float* dpred, hipStream_t st) 
     const float* g = l == 4 ? h->Sa : h->dcat[l];
     const int64_t ldg = l == 4 ? C : 2 * C;
     if (l == 0) {
-        double_conv_bwd(h, e, g, ldg, 0, h->x0, 4, B, nullptr, 0, st);
+        double_conv_bwd(h, e, g, ldg, 0, h->x0, h->x0_ld, B, nullptr, 0, st);
         return;
     }
     const int Cp = h->Cl(l - 1);
@@ -492,12 +603,21 @@ void default_init(cad_unet* h) {
         s ^= s << 13; s ^= s >> 7; s ^= s << 17;
         return (float)((s >> 40) * (1.0 / 16777216.0));
     };
+    auto normal = [&]() {   // Box-Muller
+        const float u1 = std::max(rnd(), 1e-7f), u2 = rnd();
+        return std::sqrt(-2.f * std::log(u1)) * std::cos(6.2831853f * u2);
+    };
     std::vector<float> ref, inter;
     for (const PInfo& p : h->params) {
         ref.assign(p.n_ref, 0.f);
-        if (p.kind == P_BNW) std::fill(ref.begin(), ref.end(), 1.f);
-        else if (p.kind == P_BNB) { /* zeros */ }
-        else {
+        if (p.kind == P_BNW || p.kind == P_FILM_GAMMA_B) std::fill(ref.begin(), ref.end(), 1.f);
+        else if (p.kind == P_BNB || p.kind == P_FILM_BETA_B) { /* zeros */ }
+        else if (p.kind == P_FILM_HEAD_W) { for (auto& x : ref) x = 0.01f * normal(); }   // N(0, 0.01)
+        else if (p.kind == P_FC_W || p.kind == P_FC_B) {
+            const PInfo& w = p.kind == P_FC_W ? p : h->params[&p - &h->params[0] - 1];
+            const float bound = 1.f / std::sqrt((float)w.shape[1]);
+            for (auto& x : ref) x = (rnd() * 2.f - 1.f) * bound;
+        } else {
             int64_t fan_in;
             if (p.kind == P_CONV3) fan_in = (int64_t)p.cin_ref * 9;
             else if (p.kind == P_CONVT_W || p.kind == P_CONVT_B) {
@@ -557,8 +677,14 @@ cad_status cad_memcpy(void* dst, const void* src, int64_t bytes, int kind, void*
 }
 
 cad_status cad_unet_create(const cad_unet_desc* d, int device, cad_unet** out) {
+    return cad_unet_create_model(d, CAD_MODEL_BASELINE, device, out);
+}
+
+cad_status cad_unet_create_model(const cad_unet_desc* d, int model, int device, cad_unet** out) {
     return guard([&] {
         require(d && out, "null argument");
+        require(model == CAD_MODEL_BASELINE || model == CAD_MODEL_INTRINSICS_FILM || model == CAD_MODEL_RAY_FILM,
+                "unknown model kind");
         require(d->in_channels == 3, "in_channels must be 3 (rgb)");
         require(d->init_features >= 4 && d->init_features % 4 == 0, "init_features must be a multiple of 4");
         require(d->height > 0 && d->width > 0 && d->height % 16 == 0 && d->width % 16 == 0,
@@ -567,6 +693,8 @@ cad_status cad_unet_create(const cad_unet_desc* d, int device, cad_unet** out) {
         HIPCHK(hipSetDevice(device));
         auto h = std::make_unique<cad_unet>();
         h->device = device;
+        h->model = model;
+        h->x0_ld = model == CAD_MODEL_RAY_FILM ? 8 : 4;
         h->in_ch = d->in_channels;
         h->f = d->init_features;
         h->max_depth = d->max_depth;
@@ -603,6 +731,7 @@ int64_t cad_unet_count_parameters(const cad_unet* h) {
     return n;
 }
 int cad_unet_num_params(const cad_unet* h) { return (int)h->params.size(); }
+int cad_unet_model(const cad_unet* h) { return h->model; }
 int cad_unet_num_buffers(const cad_unet* h) { return (int)h->bufs.size(); }
 
 cad_status cad_unet_tensor_info(const cad_unet* h, int kind, int idx, const char** name, int* ndim, int64_t shape[4]) {
@@ -694,7 +823,7 @@ int64_t cad_unet_debug_buffer(cad_unet* h, const char* name, float* host, int64_
         return n[pre.size()] - '0';
     };
     int l;
-    if (n == "x0") { p = h->x0; cnt = h->Ml(0, B) * 4; }
+    if (n == "x0") { p = h->x0; cnt = h->Ml(0, B) * h->x0_ld; }
     else if (n == "Sa" || n == "Sb") { p = n == "Sa" ? h->Sa : h->Sb; cnt = h->Ml(0, B) * h->Cl(0); }
     else if (n == "Sc") { p = h->Sc; cnt = h->Ml(1, B) * h->Cl(0); }
     else if (n == "bott") { p = h->a2_bott; cnt = h->Ml(4, B) * h->Cl(4); }
@@ -707,7 +836,12 @@ int64_t cad_unet_debug_buffer(cad_unet* h, const char* name, float* host, int64_
         const std::string t = n.size() > 5 ? n.substr(5) : "";
         p = t == "y1" ? dc.y1 : t == "a1" ? dc.a1 : t == "y2" ? dc.y2 : nullptr;
         cnt = p ? h->Ml(l, B) * h->Cl(l) : -1;
+        if (dc.has_film() && (t == "gamma" || t == "beta")) {
+            p = t == "gamma" ? dc.film.gam : dc.film.bet;
+            cnt = (int64_t)B * h->Cl(l);
+        }
     }
+    else if (n == "camn") { p = h->camn; cnt = (int64_t)B * 4; }
     if (!p || cnt < 0) return -1;
     if (host) {
         if (numel < cnt) return -1;
@@ -730,11 +864,16 @@ cad_status cad_unet_use_external_slabs(cad_unet* h, float* params, float* grads)
 }
 
 cad_status cad_unet_forward(cad_unet* h, const float* rgb, float* depth, int B, void* stream) {
+    return cad_unet_forward_cam(h, rgb, nullptr, depth, B, stream);
+}
+
+cad_status cad_unet_forward_cam(cad_unet* h, const float* rgb, const float* cam4, float* depth, int B, void* stream) {
     return guard([&] {
         require(rgb && depth, "null tensor");
         require(B >= 1 && B <= h->Bmax, "batch exceeds max_batch");
+        require(h->model == CAD_MODEL_BASELINE || cam4, "this model is conditioned on camera intrinsics: pass cam4");
         HIPCHK(hipSetDevice(h->device));
-        unet_forward(h, rgb, depth, B, S(stream));
+        unet_forward(h, rgb, cam4, depth, B, S(stream));
         HIPCHK(hipGetLastError());
         h->have_fwd = h->train;
         h->fwd_B = B;
@@ -906,6 +1045,14 @@ cad_status cad_depth_metrics(const float* pred, const float* gt, int B, int H, i
             acc[6] += t[7] / t[0];
         }
         for (int q = 0; q < 7; ++q) out7[q] = (float)(acc[q] / B);
+    });
+}
+
+cad_status cad_camera_from_K(const float* K, int B, float* cam4, void* stream) {
+    return guard([&] {
+        require(K && cam4 && B > 0, "bad arguments");
+        cad::camera_from_K(K, B, cam4, S(stream));
+        HIPCHK(hipGetLastError());
     });
 }
 

@@ -1,0 +1,375 @@
+// Camera conditioning of the config-3 models.
+//
+//   a14 normalizeCameraIntrinsics (intrinsics_unet.h:252-268): [fx/W, fy/H, 2cx/W - 1, 2cy/H - 1]
+//   a15 (no reference code): cam4 = [K00, K11, K02, K12]
+//   a16 FiLMLayerImpl::forward (film_layer.h:82-108):
+//         h1 = relu(BN1d(fc1(c))) [128], h2 = relu(BN1d(fc2(h1))) [256]  (BN1d only when B > 1)
+//         gamma = fc_gamma(h2), beta = fc_beta(h2) [C];   out = gamma * F + beta  (per sample, channel)
+//   a17 FiLMDoubleConv: conv1 -> BN -> ReLU -> FiLM -> conv2 -> BN -> ReLU (intrinsics_unet.h:38-52)
+//   a19 RayEnhancedConv enc1: cat(rgb, rays) -> the same block (geometry_aware_network.h:47-64)
+//
+// The FiLM MLP is a few hundred kFLOP per sample: each piece is a small deterministic kernel
+// (no atomics; batch statistics reduced in a fixed order, fp64).  The per-pixel affine is a
+// memory-bound elementwise pass; its backward reduces Σ dA·r and Σ dA per (sample, channel) with
+// the same two-level slice scheme as the BN reductions.
+#include <algorithm>
+
+#include "kernels.hpp"
+
+namespace cad {
+namespace {
+inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+inline int ew_blocks(int64_t n) { return (int)std::min<int64_t>(std::max<int64_t>(1, cdiv(n, 256)), 8192); }
+constexpr int H1 = kFilmH1, H2 = kFilmH2;
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// a15 + a14
+// ------------------------------------------------------------------------------------------
+__global__ void k_cam_from_K(const float* __restrict__ K, int B, float* __restrict__ cam4) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const float* k = K + b * 9;
+    cam4[b * 4 + 0] = k[0];
+    cam4[b * 4 + 1] = k[4];
+    cam4[b * 4 + 2] = k[2];
+    cam4[b * 4 + 3] = k[5];
+}
+void camera_from_K(const float* K, int B, float* cam4, hipStream_t st) {
+    hipLaunchKernelGGL(k_cam_from_K, dim3(cdiv(B, 64)), dim3(64), 0, st, K, B, cam4);
+}
+
+__global__ void k_cam_normalize(const float* __restrict__ cam4, int B, int H, int W, float* __restrict__ camn) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const float w = (float)W, h = (float)H;
+    camn[b * 4 + 0] = cam4[b * 4 + 0] / w;
+    camn[b * 4 + 1] = cam4[b * 4 + 1] / h;
+    camn[b * 4 + 2] = (cam4[b * 4 + 2] / w) * 2.0f - 1.0f;
+    camn[b * 4 + 3] = (cam4[b * 4 + 3] / h) * 2.0f - 1.0f;
+}
+void camera_normalize(const float* cam4, int B, int H, int W, float* camn, hipStream_t st) {
+    hipLaunchKernelGGL(k_cam_normalize, dim3(cdiv(B, 64)), dim3(64), 0, st, cam4, B, H, W, camn);
+}
+
+// ------------------------------------------------------------------------------------------
+// a19 input: NHWC8 [r, g, b, ray_x, ray_y, ray_z, 0, 0], rays computed in place from cam4 (a18
+// formula of ray_direction_computer.cpp:47-55), so the (B,3,H,W) ray tensor is never materialised.
+// ------------------------------------------------------------------------------------------
+__global__ void k_rgb_rays_to_nhwc8(const float* __restrict__ rgb, const float* __restrict__ cam4, int H, int W,
+                                    float* __restrict__ out, int64_t n) {
+    const int64_t HW = (int64_t)H * W;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = p / HW, yx = p - b * HW;
+        const int u = (int)(yx % W), v = (int)(yx / W);
+        const float* c = cam4 + b * 4;
+        const float fx_inv = 1.0f / c[0], fy_inv = 1.0f / c[1];
+        const float x = ((float)u - c[2]) * fx_inv;
+        const float y = ((float)v - c[3]) * fy_inv;
+        const float z = 1.0f;
+        const float nrm = sqrtf(x * x + y * y + z * z);
+        const float* s = rgb + b * 3 * HW + yx;
+        float4* o = reinterpret_cast<float4*>(out + p * 8);
+        o[0] = make_float4(s[0], s[HW], s[2 * HW], x / nrm);
+        o[1] = make_float4(y / nrm, z / nrm, 0.f, 0.f);
+    }
+}
+void rgb_rays_to_nhwc8(const float* rgb, const float* cam4, int B, int H, int W, float* out, hipStream_t st) {
+    const int64_t n = (int64_t)B * H * W;
+    hipLaunchKernelGGL(k_rgb_rays_to_nhwc8, dim3(ew_blocks(n)), dim3(256), 0, st, rgb, cam4, H, W, out, n);
+}
+
+// ------------------------------------------------------------------------------------------
+// a16 FiLM MLP forward
+// ------------------------------------------------------------------------------------------
+// one BatchNorm1d(+ReLU) feature column j over the batch, z[b] given in `zx` (overwritten by xhat)
+__device__ void bn1d_relu_col(float* zx, float* h, int ldz, int j, int B, bool bn, bool train, const float* g,
+                              const float* be, float* rm, float* rv, float* is_out) {
+    if (!bn) {   // film_layer.h:85,91: BatchNorm1d skipped when the batch has one sample
+        for (int b = 0; b < B; ++b) {
+            const float z = zx[b * ldz + j];
+            zx[b * ldz + j] = z;
+            h[b * ldz + j] = fmaxf(z, 0.f);
+        }
+        is_out[j] = 1.f;
+        return;
+    }
+    float mean, is;
+    if (train) {
+        double s = 0.0, s2 = 0.0;
+        for (int b = 0; b < B; ++b) {
+            const double z = zx[b * ldz + j];
+            s += z;
+            s2 += z * z;
+        }
+        const double mu = s / B;
+        double var = s2 / B - mu * mu;
+        if (var < 0.0) var = 0.0;
+        mean = (float)mu;
+        is = (float)(1.0 / sqrt(var + 1e-5));
+        rm[j] = 0.9f * rm[j] + 0.1f * mean;
+        rv[j] = 0.9f * rv[j] + 0.1f * (float)(var * B / (B - 1));
+    } else {
+        mean = rm[j];
+        is = 1.f / sqrtf(rv[j] + 1e-5f);
+    }
+    is_out[j] = is;
+    for (int b = 0; b < B; ++b) {
+        const float xh = (zx[b * ldz + j] - mean) * is;
+        zx[b * ldz + j] = xh;
+        h[b * ldz + j] = fmaxf(xh * g[j] + be[j], 0.f);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_film_hidden_fwd(FilmLayer L, const float* __restrict__ camn, int B,
+                                                         int train) {
+    const int j = threadIdx.x;
+    const bool bn = B > 1;
+    if (j < H1) {
+        for (int b = 0; b < B; ++b) {
+            float z = L.b1[j];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) z += camn[b * 4 + k] * L.w1[j * 4 + k];
+            L.xh1[b * H1 + j] = z;
+        }
+        bn1d_relu_col(L.xh1, L.h1, H1, j, B, bn, train, L.g1, L.be1, L.rm1, L.rv1, L.is1);
+    }
+    __syncthreads();
+    for (int b = 0; b < B; ++b) {
+        float z = L.b2[j];
+        const float* hr = L.h1 + b * H1;
+        const float* wr = L.w2 + j * H1;
+        for (int k = 0; k < H1; ++k) z += hr[k] * wr[k];
+        L.xh2[b * H2 + j] = z;
+    }
+    bn1d_relu_col(L.xh2, L.h2, H2, j, B, bn, train, L.g2, L.be2, L.rm2, L.rv2, L.is2);
+}
+
+// gamma / beta: column o in [0, 2C): o < C -> gamma[:, o], else beta[:, o - C]
+__global__ __launch_bounds__(256) void k_film_head_fwd(FilmLayer L, int B) {
+    const int o = blockIdx.x * blockDim.x + threadIdx.x;
+    const int C = L.C;
+    if (o >= 2 * C) return;
+    const bool isg = o < C;
+    const int c = isg ? o : o - C;
+    const float* w = (isg ? L.wg : L.wb) + (int64_t)c * H2;
+    const float bias = (isg ? L.bg : L.bb)[c];
+    float* dst = isg ? L.gam : L.bet;
+    for (int b = 0; b < B; ++b) {
+        const float* hr = L.h2 + b * H2;
+        float z = bias;
+        for (int k = 0; k < H2; ++k) z += hr[k] * w[k];
+        dst[b * C + c] = z;
+    }
+}
+
+void film_mlp_fwd(const FilmLayer& L, const float* camn, int B, bool train, hipStream_t st) {
+    hipLaunchKernelGGL(k_film_hidden_fwd, dim3(1), dim3(H2), 0, st, L, camn, B, (int)train);
+    hipLaunchKernelGGL(k_film_head_fwd, dim3(cdiv(2 * L.C, 256)), dim3(256), 0, st, L, B);
+}
+
+// ------------------------------------------------------------------------------------------
+// a16/a17 affine: a1 = gamma[b,c] * relu(y1 * scale[c] + shift[c]) + beta[b,c]
+// ------------------------------------------------------------------------------------------
+__global__ void k_film_apply(const float* __restrict__ y, int C, const float* __restrict__ scale,
+                             const float* __restrict__ shift, const float* __restrict__ gam,
+                             const float* __restrict__ bet, int64_t HW, float* __restrict__ out, int64_t n4) {
+    const int C4 = C >> 2;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / C4;
+        const int c = (int)(i - r * C4) * 4;
+        const int64_t bc = (r / HW) * C + c;
+        const float4 v = *reinterpret_cast<const float4*>(y + i * 4);
+        const float4 s = *reinterpret_cast<const float4*>(scale + c);
+        const float4 t = *reinterpret_cast<const float4*>(shift + c);
+        const float4 g = *reinterpret_cast<const float4*>(gam + bc);
+        const float4 b = *reinterpret_cast<const float4*>(bet + bc);
+        float4 o;
+        o.x = g.x * fmaxf(v.x * s.x + t.x, 0.f) + b.x;
+        o.y = g.y * fmaxf(v.y * s.y + t.y, 0.f) + b.y;
+        o.z = g.z * fmaxf(v.z * s.z + t.z, 0.f) + b.z;
+        o.w = g.w * fmaxf(v.w * s.w + t.w, 0.f) + b.w;
+        *reinterpret_cast<float4*>(out + i * 4) = o;
+    }
+}
+void film_apply(const float* y, int C, const float* scale, const float* shift, const float* gam, const float* bet,
+                int B, int64_t HW, float* out, hipStream_t st) {
+    const int64_t n4 = (int64_t)B * HW * C / 4;
+    hipLaunchKernelGGL(k_film_apply, dim3(ew_blocks(n4)), dim3(256), 0, st, y, C, scale, shift, gam, bet, HW, out, n4);
+}
+
+// ------------------------------------------------------------------------------------------
+// affine backward reductions: dgam[b,c] = Σ_hw dA·relu(y·sc+sh), dbet[b,c] = Σ_hw dA
+// part[b][s][2][C] (double), slices of each sample's HW rows; then a fixed-order sum over s.
+// ------------------------------------------------------------------------------------------
+int film_reduce_slices(int64_t HW) { return (int)std::max<int64_t>(1, std::min<int64_t>(64, HW / 1024)); }
+
+__global__ __launch_bounds__(256) void k_film_reduce(const float* __restrict__ dA, const float* __restrict__ y,
+                                                     int C, const float* __restrict__ scale,
+                                                     const float* __restrict__ shift, int64_t HW, int64_t rps,
+                                                     double* __restrict__ part) {
+    const int CX = blockDim.x, RY = blockDim.y;
+    const int C4 = C >> 2;
+    const int c4 = blockIdx.x * CX + threadIdx.x;
+    const int S = gridDim.y;
+    const int b = blockIdx.z;
+    const int64_t r0 = (int64_t)blockIdx.y * rps, r1 = min(HW, r0 + rps);
+    double ag[4] = {0, 0, 0, 0}, ab[4] = {0, 0, 0, 0};
+    if (c4 < C4) {
+        const float4 s = *reinterpret_cast<const float4*>(scale + c4 * 4);
+        const float4 t = *reinterpret_cast<const float4*>(shift + c4 * 4);
+        for (int64_t r = r0 + threadIdx.y; r < r1; r += RY) {
+            const int64_t off = ((int64_t)b * HW + r) * C + c4 * 4;
+            const float4 d = *reinterpret_cast<const float4*>(dA + off);
+            const float4 v = *reinterpret_cast<const float4*>(y + off);
+            ag[0] += (double)d.x * fmaxf(v.x * s.x + t.x, 0.f);
+            ag[1] += (double)d.y * fmaxf(v.y * s.y + t.y, 0.f);
+            ag[2] += (double)d.z * fmaxf(v.z * s.z + t.z, 0.f);
+            ag[3] += (double)d.w * fmaxf(v.w * s.w + t.w, 0.f);
+            ab[0] += d.x; ab[1] += d.y; ab[2] += d.z; ab[3] += d.w;
+        }
+    }
+    extern __shared__ double red[];   // [RY][CX][8]
+    double* mine = red + ((int64_t)threadIdx.y * CX + threadIdx.x) * 8;
+    for (int e = 0; e < 4; ++e) { mine[e] = ag[e]; mine[4 + e] = ab[e]; }
+    __syncthreads();
+    if (threadIdx.y == 0 && c4 < C4) {
+        for (int yy = 1; yy < RY; ++yy) {
+            const double* o = red + ((int64_t)yy * CX + threadIdx.x) * 8;
+            for (int e = 0; e < 4; ++e) { ag[e] += o[e]; ab[e] += o[4 + e]; }
+        }
+        double* p = part + (((int64_t)b * S + blockIdx.y) * 2) * C + c4 * 4;
+        for (int e = 0; e < 4; ++e) { p[e] = ag[e]; p[C + e] = ab[e]; }
+    }
+}
+__global__ void k_film_reduce_final(const double* __restrict__ part, int S, int C, int B, float* __restrict__ dgam,
+                                    float* __restrict__ dbet) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B * C) return;
+    const int b = i / C, c = i - b * C;
+    double g = 0.0, be = 0.0;
+    for (int s = 0; s < S; ++s) {
+        const double* p = part + (((int64_t)b * S + s) * 2) * C;
+        g += p[c];
+        be += p[C + c];
+    }
+    dgam[i] = (float)g;
+    dbet[i] = (float)be;
+}
+void film_affine_bwd(const float* dA, const float* y, int C, const float* scale, const float* shift, int B, int64_t HW,
+                     double* scratch, float* dgam, float* dbet, hipStream_t st) {
+    const int C4 = C >> 2;
+    const int CX = std::min(C4, 64);
+    const int RY = std::max(1, 256 / CX);
+    const int S = film_reduce_slices(HW);
+    const int64_t rps = (HW + S - 1) / S;
+    const size_t shm = (size_t)RY * CX * 8 * sizeof(double);
+    hipLaunchKernelGGL(k_film_reduce, dim3(cdiv(C4, CX), S, B), dim3(CX, RY), shm, st, dA, y, C, scale, shift, HW, rps,
+                       scratch);
+    hipLaunchKernelGGL(k_film_reduce_final, dim3(cdiv((int64_t)B * C, 256)), dim3(256), 0, st, scratch, S, C, B, dgam,
+                       dbet);
+}
+int64_t film_reduce_doubles(int B, int64_t HW, int C) { return (int64_t)B * film_reduce_slices(HW) * 2 * C; }
+
+// ------------------------------------------------------------------------------------------
+// a16 FiLM MLP backward (train mode)
+// ------------------------------------------------------------------------------------------
+// heads: dW[o][k] = Σ_b d[b][o] h2[b][k], db[o] = Σ_b d[b][o]; column k == H2 is the bias
+__global__ __launch_bounds__(256) void k_film_head_bwd_w(FilmLayer L, int B) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int C = L.C;
+    if (t >= (int64_t)2 * C * (H2 + 1)) return;
+    const int o = (int)(t / (H2 + 1)), k = (int)(t - (int64_t)o * (H2 + 1));
+    const bool isg = o < C;
+    const int c = isg ? o : o - C;
+    const float* d = isg ? L.dgam : L.dbet;
+    float acc = 0.f;
+    if (k < H2)
+        for (int b = 0; b < B; ++b) acc += d[b * C + c] * L.h2[b * H2 + k];
+    else
+        for (int b = 0; b < B; ++b) acc += d[b * C + c];
+    if (k < H2) (isg ? L.gwg : L.gwb)[(int64_t)c * H2 + k] = acc;
+    else (isg ? L.gbg : L.gbb)[c] = acc;
+}
+// dh2[b][k] = Σ_c dgam[b][c] Wg[c][k] + dbet[b][c] Wb[c][k]
+__global__ __launch_bounds__(256) void k_film_dh2(FilmLayer L, int B) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= B * H2) return;
+    const int b = t / H2, k = t - b * H2;
+    const int C = L.C;
+    float acc = 0.f;
+    for (int c = 0; c < C; ++c) acc += L.dgam[b * C + c] * L.wg[(int64_t)c * H2 + k];
+    for (int c = 0; c < C; ++c) acc += L.dbet[b * C + c] * L.wb[(int64_t)c * H2 + k];
+    L.dh2[t] = acc;
+}
+
+// BatchNorm1d(+ReLU) backward for feature column j: in: dh (grad of h = relu(n)), out: dz (grad of
+// the Linear output) into dh's slot; writes the BN affine grads
+__device__ void bn1d_relu_bwd_col(float* dh, const float* h, const float* xh, int ldz, int j, int B, bool bn,
+                                  const float* g, const float* is, float* dg, float* dbe) {
+    if (!bn) {
+        for (int b = 0; b < B; ++b) dh[b * ldz + j] = h[b * ldz + j] > 0.f ? dh[b * ldz + j] : 0.f;
+        dg[j] = 0.f;
+        dbe[j] = 0.f;
+        return;
+    }
+    double s = 0.0, sx = 0.0;
+    for (int b = 0; b < B; ++b) {
+        const float dn = h[b * ldz + j] > 0.f ? dh[b * ldz + j] : 0.f;
+        dh[b * ldz + j] = dn;
+        s += dn;
+        sx += (double)dn * xh[b * ldz + j];
+    }
+    dg[j] = (float)sx;
+    dbe[j] = (float)s;
+    const float k1 = g[j] * is[j];
+    const float k2 = (float)(k1 * s / B), k3 = (float)(k1 * sx / B);
+    for (int b = 0; b < B; ++b) dh[b * ldz + j] = k1 * dh[b * ldz + j] - k2 - k3 * xh[b * ldz + j];
+}
+
+__global__ __launch_bounds__(256) void k_film_hidden_bwd(FilmLayer L, const float* __restrict__ camn, int B) {
+    const int j = threadIdx.x;
+    const bool bn = B > 1;
+    // layer 2: dh2 -> dz2 (in place), fc2 grads
+    bn1d_relu_bwd_col(L.dh2, L.h2, L.xh2, H2, j, B, bn, L.g2, L.is2, L.gg2, L.gbe2);
+    {
+        float db = 0.f;
+        for (int b = 0; b < B; ++b) db += L.dh2[b * H2 + j];
+        L.gb2[j] = db;
+        for (int k = 0; k < H1; ++k) {
+            float acc = 0.f;
+            for (int b = 0; b < B; ++b) acc += L.dh2[b * H2 + j] * L.h1[b * H1 + k];
+            L.gw2[j * H1 + k] = acc;
+        }
+    }
+    __syncthreads();
+    // layer 1: dh1[b][k] = Σ_j dz2[b][j] W2[j][k] -> dz1, fc1 grads
+    if (j < H1) {
+        for (int b = 0; b < B; ++b) {
+            float acc = 0.f;
+            for (int jj = 0; jj < H2; ++jj) acc += L.dh2[b * H2 + jj] * L.w2[jj * H1 + j];
+            L.dh1[b * H1 + j] = acc;
+        }
+        bn1d_relu_bwd_col(L.dh1, L.h1, L.xh1, H1, j, B, bn, L.g1, L.is1, L.gg1, L.gbe1);
+        float db = 0.f;
+        float dw[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int b = 0; b < B; ++b) {
+            const float d = L.dh1[b * H1 + j];
+            db += d;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) dw[k] += d * camn[b * 4 + k];
+        }
+        L.gb1[j] = db;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) L.gw1[j * 4 + k] = dw[k];
+    }
+}
+
+void film_mlp_bwd(const FilmLayer& L, const float* camn, int B, hipStream_t st) {
+    const int64_t nw = (int64_t)2 * L.C * (H2 + 1);
+    hipLaunchKernelGGL(k_film_head_bwd_w, dim3(cdiv(nw, 256)), dim3(256), 0, st, L, B);
+    hipLaunchKernelGGL(k_film_dh2, dim3(cdiv((int64_t)B * H2, 256)), dim3(256), 0, st, L, B);
+    hipLaunchKernelGGL(k_film_hidden_bwd, dim3(1), dim3(H2), 0, st, L, camn, B);
+}
+
+}  // namespace cad

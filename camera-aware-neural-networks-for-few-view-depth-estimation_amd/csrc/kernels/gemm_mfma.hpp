@@ -98,6 +98,7 @@ struct KcDense {   // op(r,k) = P[r*ld + coff + k], r < nrows, k < K
         }
         k += BK;
     }
+    __device__ void finish(float4 (&)[NV]) {}
 };
 
 // (tap, ci) of a thread's float4 column, carried incrementally across K-stages of BK
@@ -107,12 +108,19 @@ __device__ __forceinline__ void tapci_advance(int& tap, int& ci, int cin) {
 }
 
 // op(pix, k=(tap,ci)) = X[(b, y+ky-1, x+kx-1)*ld + coff + ci], zero outside the image.
-// BNR: X is a pre-BatchNorm conv output; apply relu(x*sc[ci] + sh[ci]) to in-image elements.
+// BNR: X is a pre-BatchNorm conv output; relu(x*sc[ci] + sh[ci]) is applied to in-image elements
+// in finish(), i.e. when the stage is written to LDS after the MFMAs of the previous stage, so the
+// transform never stalls on the global loads it depends on.
+//
+// Loader protocol: load(v) issues the next stage's global loads into registers; finish(v) (called
+// right before the LDS store) completes any register-side transform.
 template <int ROWS, bool BNR = false>
 struct KcIm2col3x3 {
     static constexpr int NV = ROWS / KC_RPP;
     const float* base;
     const float *sc, *sh;
+    float4 s4, h4;     // BNR: coefficients of the loaded stage
+    bool gm[NV];       // BNR: in-image mask of the loaded stage
     int64_t ld;
     int y[NV], x[NV];
     int64_t pix[NV];
@@ -142,7 +150,6 @@ struct KcIm2col3x3 {
         const int t = kin ? tap : 0;
         const int dy = t / 3 - 1, dx = t - 3 * (t / 3) - 1;
         const int64_t off = (int64_t)(dy * W + dx) * ld + ci;
-        float4 s4, h4;
         if constexpr (BNR) {
             s4 = *reinterpret_cast<const float4*>(sc + ci);
             h4 = *reinterpret_cast<const float4*>(sh + ci);
@@ -153,10 +160,16 @@ struct KcIm2col3x3 {
             bool g = ok[j] && kin && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
             const float* q = base + pix[j] * ld + (g ? off : 0);
             float4 tv = *reinterpret_cast<const float4*>(q);
-            if constexpr (BNR) tv = bn_relu4(tv, s4, h4);
+            if constexpr (BNR) gm[j] = g;
             v[j] = g ? tv : f4zero();
         }
         tapci_advance(tap, ci, cin);
+    }
+    __device__ void finish(float4 (&v)[NV]) {
+        if constexpr (BNR) {
+#pragma unroll
+            for (int j = 0; j < NV; ++j) v[j] = gm[j] ? bn_relu4(v[j], s4, h4) : f4zero();
+        }
     }
 };
 
@@ -199,6 +212,7 @@ struct KcUpGather {
         }
         tapci_advance(q, co, cout);
     }
+    __device__ void finish(float4 (&)[NV]) {}
 };
 
 // --------------------------------------------------------------------------------------------
@@ -247,6 +261,7 @@ struct MNcDense : MNcBase<ROWS> {   // op(r, k) = P[k*ld + coff + r], r < nrows,
         }
         k0 += BK;
     }
+    __device__ void finish(float4 (&)[NV]) {}
 };
 
 // op(j=(tap,ci), k=pix) = X[(b,y+ky-1,x+kx-1)*ld + coff + ci]   (BNR: relu(x*sc+sh) in-image)
@@ -256,6 +271,7 @@ struct MNcIm2col3x3 : MNcBase<ROWS> {
     static constexpr int NV = Base::NV;
     const float* p;
     float4 s4, h4;
+    bool gm[NV];       // BNR: in-image mask of the loaded stage (transform deferred to finish())
     int64_t ld;
     int H, W, Kp, dy, dx;
     int k[NV], x[NV], y[NV];
@@ -288,11 +304,17 @@ struct MNcIm2col3x3 : MNcBase<ROWS> {
             const bool g = rok && k[j] < Kp && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
             const int64_t q = g ? (int64_t)k[j] + dy * W + dx : 0;
             float4 t = *reinterpret_cast<const float4*>(p + q * ld);
-            if constexpr (BNR) t = bn_relu4(t, s4, h4);
+            if constexpr (BNR) gm[j] = g;
             v[j] = g ? t : f4zero();
             int b = 0;
             px_advance(x[j], y[j], b, W, H);
             k[j] += BK;
+        }
+    }
+    __device__ void finish(float4 (&v)[NV]) {
+        if constexpr (BNR) {
+#pragma unroll
+            for (int j = 0; j < NV; ++j) v[j] = gm[j] ? bn_relu4(v[j], s4, h4) : f4zero();
         }
     }
 };
@@ -337,6 +359,7 @@ struct MNcUpGather : MNcBase<ROWS> {
             k[j] += BK;
         }
     }
+    __device__ void finish(float4 (&)[NV]) {}
 };
 
 // --------------------------------------------------------------------------------------------
@@ -442,7 +465,9 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, InitA init_a, InitB
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    auto stage_store = [&](int buf, const float4 (&xa)[LA::NV], const float4 (&xb)[LB::NV]) {
+    auto stage_store = [&](int buf, float4 (&xa)[LA::NV], float4 (&xb)[LB::NV]) {
+        la.finish(xa);
+        lb.finish(xb);
         float* da = lds + buf * (SA + SB);
         if constexpr (KCA) kc_store<BM>(da, xa); else mnc_store<BM>(da, xa);
         if constexpr (KCB) kc_store<BN>(da + SA, xb); else mnc_store<BN>(da + SA, xb);
@@ -507,42 +532,44 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, InitA init_a, InitB
     }
 #endif
 
-    // epilogue: element (m, n) of sub-block (i, j), register r
+    // epilogue: element (m, n) of sub-block (i, j), register r.  With STATS the per-column BN
+    // partials are accumulated in the same pass (each accumulator is read once: keeping them live
+    // for a second pass costs 64 VGPRs and an occupancy step).
     const int h = lane >> 5, col = lane & 31;
+    float ssum[2] = {0.f, 0.f}, ssq[2] = {0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int n = n0 + wn * 64 + j * 32 + col;
             if constexpr (is_structured<Epi>::value) {
+                static_assert(!Epi::STATS, "structured epilogues carry no BN partials");
                 epi.block(a, m0 + wm * 64 + i * 32 + 4 * h, n, acc[i][j]);
             } else {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    if (m < a.M && n < a.N) epi(a, m, n, acc[i][j][r], tile.z);
+                    const float v = acc[i][j][r];
+                    if (m < a.M && n < a.N) epi(a, m, n, v, tile.z);
+                    if constexpr (Epi::STATS) {
+                        const float vm = m < a.M ? v : 0.f;
+                        ssum[j] += vm;
+                        ssq[j] += vm * vm;
+                    }
                 }
+                // keep the scheduler from hoisting all 64 accumulator reads ahead of the stores
+                if constexpr (Epi::STATS) __builtin_amdgcn_sched_barrier(0);
             }
         }
 
     if constexpr (Epi::STATS) {
-        // per-column partial sum / sum of squares over this block's BM rows -> a.stats[bx][2][N]
-        float* red = lds;   // reuse: [WM][BN][2]
-        __syncthreads();
+        // per-column partial sum / sum of squares over this block's BM rows -> a.stats[bx][2][N];
+        // the main loop ended on a barrier, so the LDS operand buffers are free for the reduction
+        float* red = lds;   // [WM][BN][2]
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            float s = 0.f, q = 0.f;
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    const float v = m < a.M ? acc[i][j][r] : 0.f;
-                    s += v;
-                    q += v * v;
-                }
-            s += __shfl_xor(s, 32);
-            q += __shfl_xor(q, 32);
+            const float s = ssum[j] + __shfl_xor(ssum[j], 32);
+            const float q = ssq[j] + __shfl_xor(ssq[j], 32);
             if (h == 0) {
                 const int cl = wn * 64 + j * 32 + col;
                 red[(wm * BN + cl) * 2 + 0] = s;

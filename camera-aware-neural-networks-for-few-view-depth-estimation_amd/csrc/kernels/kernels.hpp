@@ -53,11 +53,12 @@ void bn_eval_coeffs(const float* gamma, const float* beta, const float* run_mean
 void bn_relu_fwd(const float* y, int C, const float* scale, const float* shift, float* out, int64_t ldo,
                  int ocoff, int64_t M, hipStream_t st);
 // BN+ReLU backward: dy = k1*dz - k2 - k3*xhat, dz = g*[y*scale+shift > 0];
-// writes dgamma/dbeta (grad buffer) and dy (dense [M][C])
+// writes dgamma/dbeta (grad buffer) and dy (dense [M][C]).  gmul != nullptr: g is first multiplied
+// by gmul[sample][c] (sample = row / HW) — the FiLM gamma sitting between this ReLU and the consumer
 void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, const float* mean,
                  const float* invstd, const float* scale, const float* shift, const float* gamma,
                  int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
-                 hipStream_t st);
+                 hipStream_t st, const float* gmul = nullptr, int64_t HW = 1);
 void maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float* out, uint8_t* idx,
                  hipStream_t st);
 void maxpool_bwd(const float* dout, const uint8_t* idx, int C, int B, int H, int W, float* dx,
@@ -95,7 +96,32 @@ void grad_norm_clip(const float* g, int64_t n, float max_norm, float prescale, d
 void adam_step(float* p, float* g, float* m, float* v, int64_t n, const float* norm_coef, float lr,
                float b1, float b2, float eps, float wd, int step, hipStream_t st);
 
-// ---------------- conditioning (cond_kernels.hip) ----------------
+// ---------------- conditioning (cond_kernels.hip, film_kernels.hip) ----------------
 void ray_directions(const float* K, int B, int H, int W, float* rays_nchw, hipStream_t st);
+void camera_from_K(const float* K, int B, float* cam4, hipStream_t st);            // a15
+void camera_normalize(const float* cam4, int B, int H, int W, float* camn, hipStream_t st);   // a14
+// a19 input: NHWC8 [r, g, b, ray_x, ray_y, ray_z, 0, 0] with rays from cam4 (a18)
+void rgb_rays_to_nhwc8(const float* rgb, const float* cam4, int B, int H, int W, float* out, hipStream_t st);
+
+// One FiLMLayerImpl (film_layer.h:26-108): parameters, running stats, saved activations, grads.
+constexpr int kFilmH1 = 128, kFilmH2 = 256;
+struct FilmLayer {
+    int C = 0;
+    const float *w1, *b1, *w2, *b2, *wg, *bg, *wb, *bb, *g1, *be1, *g2, *be2;   // parameters
+    float *rm1, *rv1, *rm2, *rv2;                                              // BatchNorm1d buffers
+    float *xh1, *h1, *xh2, *h2, *is1, *is2;   // [B][128] / [B][256] xhat + relu outputs, invstd
+    float *gam, *bet;                         // [B][C]
+    float *dgam, *dbet, *dh2, *dh1;           // backward scratch
+    float *gw1, *gb1, *gw2, *gb2, *gwg, *gbg, *gwb, *gbb, *gg1, *gbe1, *gg2, *gbe2;   // gradients
+};
+void film_mlp_fwd(const FilmLayer& L, const float* camn, int B, bool train, hipStream_t st);
+void film_mlp_bwd(const FilmLayer& L, const float* camn, int B, hipStream_t st);
+// a1 = gam[b,c] * relu(y*scale[c] + shift[c]) + bet[b,c]   (NHWC [B*HW][C])
+void film_apply(const float* y, int C, const float* scale, const float* shift, const float* gam, const float* bet,
+                int B, int64_t HW, float* out, hipStream_t st);
+// dgam[b,c] = sum_hw dA * relu(y*scale+shift), dbet[b,c] = sum_hw dA
+void film_affine_bwd(const float* dA, const float* y, int C, const float* scale, const float* shift, int B, int64_t HW,
+                     double* scratch, float* dgam, float* dbet, hipStream_t st);
+int64_t film_reduce_doubles(int B, int64_t HW, int C);
 
 }  // namespace cad

@@ -84,10 +84,14 @@ struct OpSum {
     }
 };
 struct OpBnBwd {
-    const float *g, *y, *mean, *invstd, *scale, *shift;
-    int64_t ldg; int gcoff, C;
+    const float *g, *y, *mean, *invstd, *scale, *shift, *gmul;
+    int64_t ldg; int gcoff, C; int64_t HW;
     __device__ void operator()(int64_t r, int c4, double (&acc)[2][4]) const {
         float4 gv = *reinterpret_cast<const float4*>(g + r * ldg + gcoff + c4 * 4);
+        if (gmul) {
+            const float4 m = *reinterpret_cast<const float4*>(gmul + (r / HW) * C + c4 * 4);
+            gv.x *= m.x; gv.y *= m.y; gv.z *= m.z; gv.w *= m.w;
+        }
         float4 yv = *reinterpret_cast<const float4*>(y + r * C + c4 * 4);
         const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, ya[4] = {yv.x, yv.y, yv.z, yv.w};
 #pragma unroll
@@ -232,12 +236,17 @@ __global__ void k_bn_bwd_coef(const double* tot, int C, int64_t M, const float* 
 __global__ void k_bn_relu_bwd(const float* __restrict__ g, int64_t ldg, int gcoff, const float* __restrict__ y,
                               int C, const float* __restrict__ mean, const float* __restrict__ invstd,
                               const float* __restrict__ scale, const float* __restrict__ shift,
-                              const float* __restrict__ coef, float* __restrict__ dy, int64_t n4) {
+                              const float* __restrict__ coef, float* __restrict__ dy, int64_t n4,
+                              const float* __restrict__ gmul, int64_t HW) {
     const int C4 = C >> 2;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = i / C4;
         const int c0 = (int)(i - r * C4) * 4;
         float4 gv = *reinterpret_cast<const float4*>(g + r * ldg + gcoff + c0);
+        if (gmul) {
+            const float4 m = *reinterpret_cast<const float4*>(gmul + (r / HW) * C + c0);
+            gv.x *= m.x; gv.y *= m.y; gv.z *= m.z; gv.w *= m.w;
+        }
         float4 yv = *reinterpret_cast<const float4*>(y + i * 4);
         const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, ya[4] = {yv.x, yv.y, yv.z, yv.w};
         float o[4];
@@ -255,16 +264,16 @@ __global__ void k_bn_relu_bwd(const float* __restrict__ g, int64_t ldg, int gcof
 void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, const float* mean,
                  const float* invstd, const float* scale, const float* shift, const float* gamma,
                  int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
-                 hipStream_t st) {
+                 hipStream_t st, const float* gmul, int64_t HW) {
     double* tot = scratch;
     double* part = scratch + 2 * C;
-    OpBnBwd op{g, y, mean, invstd, scale, shift, ldg, gcoff, C};
+    OpBnBwd op{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW};
     const int S = launch_colreduce<2>(op, M, C, part, st);
     launch_colfinal(part, S, 2 * C, tot, nullptr, 1.f, st);
     hipLaunchKernelGGL(k_bn_bwd_coef, dim3(cdiv(C, 64)), dim3(64), 0, st, tot, C, M, gamma, invstd, coef, dgamma, dbeta);
     const int64_t n4 = M * C / 4;
     hipLaunchKernelGGL(k_bn_relu_bwd, dim3(ew_blocks(n4)), dim3(256), 0, st, g, ldg, gcoff, y, C, mean, invstd,
-                       scale, shift, coef, dy, n4);
+                       scale, shift, coef, dy, n4, gmul, HW);
 }
 
 // ------------------------------------------------------------------------------------------

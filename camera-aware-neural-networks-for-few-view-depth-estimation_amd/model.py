@@ -4,6 +4,9 @@ Class and method names follow the reference so that a caller (and the parity tes
 the reference's own code:
 
   BaselineUNet            BaselineUNetImpl           src/models/baseline_unet.h:122-208
+  IntrinsicsConditionedUNet IntrinsicsConditionedUNetImpl src/models/intrinsics_unet.h:137-270
+  RayConditionedUNet      config-3 composite: enc1 = RayEnhancedConv (geometry_aware_network.h:17-65),
+                          FiLM blocks after (intrinsics_unet.h:16-113)
   CombinedDepthLoss       CombinedDepthLoss          src/loss/depth_loss.h:366-479
   Adam                    torch::optim::Adam         (options built at tensorboard_trainer_enhanced.h:97-101)
   clip_grad_norm_         torch::nn::utils::clip_grad_norm_ (enhanced.h:300-302)
@@ -34,10 +37,15 @@ def _ptr(t: torch.Tensor):
     return C.c_void_p(t.data_ptr())
 
 
+MODEL_BASELINE, MODEL_INTRINSICS_FILM, MODEL_RAY_FILM = 0, 1, 2   # CAD_MODEL_* of cad.h
+
+
 class BaselineUNet:
     """BaselineUNetImpl(in_channels, init_features, max_depth) on MI355X.
 
     Extra keyword-only arguments size the device workspace (the reference allocates per call)."""
+
+    MODEL = MODEL_BASELINE
 
     def __init__(self, in_channels=3, init_features=64, max_depth=10.0, *, batch, height, width, device=0):
         self.lib = _abi.load()
@@ -46,7 +54,7 @@ class BaselineUNet:
         self.batch, self.height, self.width = batch, height, width
         desc = _abi.UnetDesc(in_channels, init_features, max_depth, batch, height, width)
         h = C.c_void_p()
-        check(self.lib.cad_unet_create(C.byref(desc), device, C.byref(h)), "cad_unet_create")
+        check(self.lib.cad_unet_create_model(C.byref(desc), self.MODEL, device, C.byref(h)), "cad_unet_create_model")
         self.h = h
         self._param_info = [self._info(0, i) for i in range(self.lib.cad_unet_num_params(h))]
         self._buffer_info = [self._info(1, i) for i in range(self.lib.cad_unet_num_buffers(h))]
@@ -134,6 +142,10 @@ class BaselineUNet:
         return out
 
     # ---- forward / backward ----
+    @property
+    def conditioned(self) -> bool:
+        return self.MODEL != MODEL_BASELINE
+
     def forward(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
         B, Cc, H, W = x.shape
         assert Cc == self.in_channels and H == self.height and W == self.width, "input shape mismatch"
@@ -142,7 +154,19 @@ class BaselineUNet:
         check(self.lib.cad_unet_forward(self.h, _ptr(x), _ptr(out), B, _stream(self.device)), "cad_unet_forward")
         return out
 
-    __call__ = forward
+    def forward_cam(self, x: torch.Tensor, intrinsics: torch.Tensor, out: torch.Tensor | None = None):
+        """forward(x, camera_intrinsics (B,4) [fx, fy, cx, cy]) of the camera-conditioned models."""
+        B, Cc, H, W = x.shape
+        assert Cc == self.in_channels and H == self.height and W == self.width, "input shape mismatch"
+        assert tuple(intrinsics.shape) == (B, 4), "intrinsics must be (B, 4) [fx, fy, cx, cy]"
+        if out is None:
+            out = torch.empty((B, 1, H, W), dtype=torch.float32, device=self.device)
+        check(self.lib.cad_unet_forward_cam(self.h, _ptr(x), _ptr(intrinsics.contiguous()), _ptr(out), B,
+                                            _stream(self.device)), "cad_unet_forward_cam")
+        return out
+
+    def __call__(self, x, *args, **kw):
+        return self.forward_cam(x, *args, **kw) if self.conditioned else self.forward(x, *args, **kw)
 
     def backward(self, ddepth: torch.Tensor, on_stage=None):
         """Backward of the last train-mode forward. on_stage(stage, offset, count) is called after
@@ -169,6 +193,39 @@ class BaselineUNet:
         v = C.c_float()
         check(self.lib.cad_unet_last_grad_norm(self.h, C.byref(v), _stream(self.device)), "last_grad_norm")
         return float(v.value)
+
+
+class IntrinsicsConditionedUNet(BaselineUNet):
+    """IntrinsicsConditionedUNetImpl(in_channels, init_features, camera_dim=4, max_depth) on MI355X:
+    a FiLMLayerImpl(4, C) after the first BN-ReLU of every DoubleConv, fed the normalised (B,4)
+    intrinsics (intrinsics_unet.h:137-270).  forward(x, intrinsics) takes [fx, fy, cx, cy]."""
+
+    MODEL = MODEL_INTRINSICS_FILM
+
+    def __init__(self, in_channels=3, init_features=64, camera_dim=4, max_depth=10.0, *, batch, height, width,
+                 device=0):
+        assert camera_dim == 4, "camera_dim 4 ([fx, fy, cx, cy]) is the configuration on the hot path"
+        super().__init__(in_channels, init_features, max_depth, batch=batch, height=height, width=width,
+                         device=device)
+
+    def forward(self, x, intrinsics, out=None):   # noqa: D401 (reference signature)
+        return self.forward_cam(x, intrinsics, out)
+
+
+class RayConditionedUNet(IntrinsicsConditionedUNet):
+    """Config-3 model (SURVEY §8 "Recommended config-3 model"): enc1 = RayEnhancedConv(3, f, 4,
+    use_rays=true) fed cat(rgb, per-pixel rays from the intrinsics), FiLM blocks after."""
+
+    MODEL = MODEL_RAY_FILM
+
+
+def camera_from_K(K: torch.Tensor) -> torch.Tensor:
+    """(B,3,3) intrinsics -> (B,4) [fx, fy, cx, cy] on device."""
+    B = K.shape[0]
+    lib = _abi.load()
+    out = torch.empty((B, 4), dtype=torch.float32, device=K.device)
+    check(lib.cad_camera_from_K(_ptr(K.reshape(B, 9).contiguous()), B, _ptr(out), _stream(K.device)), "camera_from_K")
+    return out
 
 
 def clip_grad_norm_(model: BaselineUNet, max_norm: float, prescale: float = 1.0):
@@ -330,10 +387,17 @@ class Trainer:
         m = self.model
         m.train()
         self.optimizer.zero_grad()
-        if self.pred is None or self.pred.shape[0] != rgb.shape[0]:
-            self.pred = torch.empty((rgb.shape[0], 1, m.height, m.width), dtype=torch.float32, device=m.device)
+        B = rgb.shape[0]
+        if self.pred is None or self.pred.shape[0] != B:
+            self.pred = torch.empty((B, 1, m.height, m.width), dtype=torch.float32, device=m.device)
             self.dpred = torch.empty_like(self.pred)
-        m.forward(rgb, out=self.pred)
+            self.cam4 = torch.empty((B, 4), dtype=torch.float32, device=m.device)
+        if m.conditioned:   # camera vector from the batch intrinsics (a15), then the FiLM forward
+            check(m.lib.cad_camera_from_K(_ptr(K.reshape(B, 9).contiguous()), B, _ptr(self.cam4),
+                                          _stream(m.device)), "camera_from_K")
+            m.forward_cam(rgb, self.cam4, out=self.pred)
+        else:
+            m.forward(rgb, out=self.pred)
         self.loss_fn.forward_with_intrinsics(self.pred, gt, rgb, K, loss5=self.loss5, dpred=self.dpred)
         if self.world > 1:
             bk = GradBucketer(m.flat_grads, m.num_stages, self.bucket_elems, self.pg)

@@ -12,6 +12,16 @@
  *                                   147-165); used by torch::save / load and the trainer
  *   cad_unet_train                  Module::train()/eval()  (enhanced.h:259, :341)
  *   cad_unet_forward                BaselineUNetImpl::forward                 baseline_unet.h:174-195
+ *   cad_unet_create_model           IntrinsicsConditionedUNetImpl(in, f, 4, max_depth)
+ *                                   src/models/intrinsics_unet.h:137-200 (FiLMLayerImpl(4, C) per
+ *                                   DoubleConv, src/layers/film_layer.h:47-72); CAD_MODEL_RAY_FILM =
+ *                                   the config-3 composite with enc1 = RayEnhancedConv(3, f, 4, true)
+ *                                   (src/models/geometry_aware_network.h:17-65)
+ *   cad_unet_forward_cam            IntrinsicsConditionedUNetImpl::forward(x, intrinsics (B,4))
+ *                                   intrinsics_unet.h:204-228 (+ RayEnhancedConvImpl::forward's
+ *                                   cat(x, rays), geometry_aware_network.h:47-52)
+ *   cad_camera_from_K               K (B,3,3) -> (B,4) [fx, fy, cx, cy] (the reference
+ *                                   has no such code; train_main never builds camera vectors)
  *   cad_loss_create/forward_backward CombinedDepthLoss(si,grad,smooth,reproj) + forwardWithIntrinsics
  *                                   + the autograd backward of the loss       src/loss/depth_loss.h:366-433
  *   cad_loss_get_components         getComponentsWithIntrinsics               depth_loss.h:454-467
@@ -57,6 +67,11 @@ typedef struct cad_unet cad_unet;
 typedef struct cad_loss cad_loss;
 typedef struct cad_adam cad_adam;
 
+/* model families (cad_unet_create_model) */
+#define CAD_MODEL_BASELINE 0        /* BaselineUNetImpl */
+#define CAD_MODEL_INTRINSICS_FILM 1 /* IntrinsicsConditionedUNetImpl (camera_dim 4) */
+#define CAD_MODEL_RAY_FILM 2        /* enc1 = RayEnhancedConv(3, f, 4, use_rays), FiLM blocks after */
+
 typedef struct {
     int in_channels;   /* 3 */
     int init_features; /* f (64 default, 96 in train_config_production.yaml) */
@@ -86,7 +101,9 @@ void cad_free(void* p);
 cad_status cad_memcpy(void* dst, const void* src, int64_t bytes, int kind, void* stream);
 
 /* ---- model: BaselineUNetImpl ---- */
-cad_status cad_unet_create(const cad_unet_desc* desc, int device, cad_unet** out);
+cad_status cad_unet_create(const cad_unet_desc* desc, int device, cad_unet** out); /* baseline */
+cad_status cad_unet_create_model(const cad_unet_desc* desc, int model, int device, cad_unet** out);
+int cad_unet_model(const cad_unet* h);
 void cad_unet_destroy(cad_unet* h);
 int64_t cad_unet_count_parameters(const cad_unet* h);
 int cad_unet_num_params(const cad_unet* h);  /* tensors in named_parameters() */
@@ -106,8 +123,16 @@ cad_status cad_unet_flat(cad_unet* h, float** params, float** grads, int64_t* n)
  * keeps them alive for the handle's lifetime. */
 cad_status cad_unet_use_external_slabs(cad_unet* h, float* params, float* grads);
 
-/* forward: rgb (B,3,H,W) -> depth (B,1,H,W) in (0, max_depth).  B <= max_batch. */
+/* forward: rgb (B,3,H,W) -> depth (B,1,H,W) in (0, max_depth).  B <= max_batch.
+ * cad_unet_forward serves CAD_MODEL_BASELINE; the camera-conditioned models take cam4 (B,4)
+ * [fx, fy, cx, cy] in pixels of the H x W input (normalised on device, intrinsics_unet.h:252-268;
+ * RAY_FILM also derives the per-pixel rays from it).  Note FiLM's BatchNorm1d runs only for B > 1
+ * (film_layer.h:85,91), in train and eval mode alike. */
 cad_status cad_unet_forward(cad_unet* h, const float* rgb, float* depth, int B, void* stream);
+cad_status cad_unet_forward_cam(cad_unet* h, const float* rgb, const float* cam4, float* depth, int B,
+                                void* stream);
+/* K (B,3,3) row-major -> cam4 (B,4) = [K00, K11, K02, K12] */
+cad_status cad_camera_from_K(const float* K, int B, float* cam4, void* stream);
 
 /* backward of the last train-mode forward given dL/ddepth; writes every parameter gradient.
  * Stage form (stage 0 .. cad_unet_num_stages()-1, in order) lets a caller overlap the gradient

@@ -7,6 +7,11 @@ module, and only as the CHECKER: the product path (libcad_hip.so and its binding
 Every function cites the reference file:line it restates (paths relative to /root/reference):
 
   * BaselineUNetImpl            src/models/baseline_unet.h:14-208
+  * FiLMLayerImpl               src/layers/film_layer.h:26-108
+  * FiLMDoubleConv / FiLMEncoderBlock / FiLMDecoderBlock / IntrinsicsConditionedUNetImpl
+                                src/models/intrinsics_unet.h:16-270
+  * RayEnhancedConvImpl         src/models/geometry_aware_network.h:17-65
+  * computeRayDirections (a18)  src/preprocessing/ray_direction_computer.cpp:17-62
   * ScaleInvariantLoss          src/loss/depth_loss.h:20-69
   * GradientMatchingLoss        src/loss/depth_loss.h:82-167
   * SmoothnessLoss              src/loss/depth_loss.h:178-238
@@ -85,65 +90,146 @@ def synth_batch(B: int, H: int, W: int, rgb_seed: int = 0xC0FFEE, hole_seed: int
 # --------------------------------------------------------------------------------------------
 # Model: BaselineUNetImpl (baseline_unet.h:122-208) as named parameter/buffer dictionaries.
 # --------------------------------------------------------------------------------------------
-def _double_conv_spec(prefix, cin, cout):
-    # DoubleConvImpl ctor (baseline_unet.h:20-30): conv1 (no bias), bn1, conv2 (no bias), bn2
-    return [(prefix + "conv1.weight", (cout, cin, 3, 3)),
+MODELS = ("baseline", "film", "rayfilm")
+FILM_CAMERA_DIM, FILM_H1, FILM_HIDDEN = 4, 128, 256   # FiLMLayerImpl(4, C) defaults (film_layer.h:47-66)
+
+
+def _film_spec(prefix, C):
+    # FiLMLayerImpl ctor (film_layer.h:47-72): registration order fc1, fc2, fc_gamma, fc_beta, bn1, bn2
+    return [(prefix + "fc1.weight", (FILM_H1, FILM_CAMERA_DIM)), (prefix + "fc1.bias", (FILM_H1,)),
+            (prefix + "fc2.weight", (FILM_HIDDEN, FILM_H1)), (prefix + "fc2.bias", (FILM_HIDDEN,)),
+            (prefix + "fc_gamma.weight", (C, FILM_HIDDEN)), (prefix + "fc_gamma.bias", (C,)),
+            (prefix + "fc_beta.weight", (C, FILM_HIDDEN)), (prefix + "fc_beta.bias", (C,)),
+            (prefix + "bn1.weight", (FILM_H1,)), (prefix + "bn1.bias", (FILM_H1,)),
+            (prefix + "bn2.weight", (FILM_HIDDEN,)), (prefix + "bn2.bias", (FILM_HIDDEN,))]
+
+
+def _double_conv_spec(prefix, cin, cout, film=False):
+    # DoubleConvImpl ctor (baseline_unet.h:20-30): conv1 (no bias), bn1, conv2 (no bias), bn2;
+    # FiLMDoubleConvImpl / RayEnhancedConvImpl (intrinsics_unet.h:23-36, geometry_aware_network.h:25-45)
+    # register the same four modules, then `film`
+    spec = [(prefix + "conv1.weight", (cout, cin, 3, 3)),
             (prefix + "bn1.weight", (cout,)), (prefix + "bn1.bias", (cout,)),
             (prefix + "conv2.weight", (cout, cout, 3, 3)),
             (prefix + "bn2.weight", (cout,)), (prefix + "bn2.bias", (cout,))]
+    return spec + (_film_spec(prefix + "film.", cout) if film else [])
 
 
-def param_spec(f: int = 64, in_ch: int = 3):
-    """named_parameters() order of BaselineUNetImpl(in_ch, f) (registration order, :144-166)."""
-    spec = _double_conv_spec("enc1.", in_ch, f)
+def param_spec(f: int = 64, in_ch: int = 3, model: str = "baseline"):
+    """named_parameters() order of BaselineUNetImpl(in_ch, f) (registration order, :144-166),
+    IntrinsicsConditionedUNetImpl(in_ch, f, 4) (intrinsics_unet.h:168-195), or the config-3
+    composite "rayfilm" (enc1 = RayEnhancedConv(in_ch, f, 4, use_rays) with in_ch + 3 inputs)."""
+    assert model in MODELS, model
+    film = model != "baseline"
+    spec = _double_conv_spec("enc1.", in_ch + (3 if model == "rayfilm" else 0), f, film)
     for i, name in enumerate(["enc2", "enc3", "enc4", "bottleneck"]):
-        spec += _double_conv_spec(f"{name}.conv.", f << i, f << (i + 1))
+        spec += _double_conv_spec(f"{name}.conv.", f << i, f << (i + 1), film)
     for i, name in enumerate(["dec4", "dec3", "dec2", "dec1"]):
         cin = f << (4 - i)
         spec += [(f"{name}.up.weight", (cin, cin // 2, 2, 2)), (f"{name}.up.bias", (cin // 2,))]
-        spec += _double_conv_spec(f"{name}.conv.", cin, cin // 2)
+        spec += _double_conv_spec(f"{name}.conv.", cin, cin // 2, film)
     spec += [("out_conv.weight", (1, f, 1, 1)), ("out_conv.bias", (1,))]
     return spec
 
 
-def buffer_spec(f: int = 64, in_ch: int = 3):
+def buffer_spec(f: int = 64, in_ch: int = 3, model: str = "baseline"):
     """Float BatchNorm buffers (running_mean/var) in named_buffers() order."""
     out = []
-    for name, shape in param_spec(f, in_ch):
+    for name, shape in param_spec(f, in_ch, model):
         if name.endswith(".bias") and ".bn" in name:
             base = name[: -len(".bias")]
             out += [(base + ".running_mean", shape), (base + ".running_var", shape)]
     return out
 
 
-def num_params(f: int = 64, in_ch: int = 3) -> int:
-    return int(sum(np.prod(s) for _, s in param_spec(f, in_ch)))
+def num_params(f: int = 64, in_ch: int = 3, model: str = "baseline") -> int:
+    return int(sum(np.prod(s) for _, s in param_spec(f, in_ch, model)))
 
 
-def init_params(f: int = 64, seed: int = 42, in_ch: int = 3):
+def init_params(f: int = 64, seed: int = 42, in_ch: int = 3, model: str = "baseline"):
     """torch.nn default init (kaiming_uniform(a=sqrt 5) weights, U(-1/sqrt(fan_in),..) biases,
-    BN weight 1 / bias 0) — same distributions as the LibTorch modules; not bitwise the C++ stream."""
+    BN weight 1 / bias 0) — same distributions as the LibTorch modules; not bitwise the C++ stream.
+    FiLM heads: fc_gamma/fc_beta weights N(0, 0.01), biases 1 / 0 (film_layer.h:68-71)."""
     g = torch.Generator().manual_seed(seed)
     params = OrderedDict()
-    for name, shape in param_spec(f, in_ch):
+    spec = dict(param_spec(f, in_ch, model))
+    for name, shape in param_spec(f, in_ch, model):
         if ".bn" in name:
             params[name] = torch.ones(shape) if name.endswith("weight") else torch.zeros(shape)
+            continue
+        if ".fc_gamma." in name or ".fc_beta." in name:
+            if name.endswith("weight"):
+                params[name] = torch.randn(shape, generator=g) * 0.01
+            else:
+                params[name] = torch.full(shape, 1.0 if ".fc_gamma." in name else 0.0)
             continue
         if name.endswith("weight"):
             fan_in = shape[1] * int(np.prod(shape[2:])) if "up." not in name else shape[1] * 4
             bound = 1.0 / math.sqrt(fan_in)  # kaiming_uniform_(a=sqrt(5)) => gain sqrt(2/6)*sqrt(3/fan)
             params[name] = (torch.rand(shape, generator=g) * 2 - 1) * bound
         else:
-            wshape = dict(param_spec(f, in_ch))[name[: -len("bias")] + "weight"]
+            wshape = spec[name[: -len("bias")] + "weight"]
             fan_in = wshape[1] * int(np.prod(wshape[2:])) if "up." not in name else wshape[1] * 4
             bound = 1.0 / math.sqrt(fan_in)
             params[name] = (torch.rand(shape, generator=g) * 2 - 1) * bound
     return params
 
 
-def init_buffers(f: int = 64, in_ch: int = 3):
+def init_buffers(f: int = 64, in_ch: int = 3, model: str = "baseline"):
     return OrderedDict((n, torch.zeros(s) if n.endswith("mean") else torch.ones(s))
-                       for n, s in buffer_spec(f, in_ch))
+                       for n, s in buffer_spec(f, in_ch, model))
+
+
+def synth_init(f: int = 64, in_ch: int = 3, model: str = "baseline"):
+    """Counter-stream initial weights of ref_harness.cpp `--init synth` (bit-identical): u = u01(0x1A17,
+    running offset); >=2-D: (2u-1)/sqrt(numel/size(0)); 1-D *.weight and *.fc_gamma.bias:
+    1 + 0.1(2u-1); other 1-D: 0.1(2u-1)."""
+    params = OrderedDict()
+    off = 0
+    one, two, tenth = np.float32(1.0), np.float32(2.0), np.float32(0.1)
+    for name, shape in param_spec(f, in_ch, model):
+        n = int(np.prod(shape))
+        u = u01(0x1A17, np.arange(off, off + n, dtype=np.uint64))
+        if len(shape) >= 2:
+            bound = one / np.sqrt(np.float32(n // shape[0]))
+            v = (two * u - one) * bound
+        elif name.endswith(".weight") or name.endswith(".fc_gamma.bias"):
+            v = one + tenth * (two * u - one)
+        else:
+            v = tenth * (two * u - one)
+        params[name] = torch.from_numpy(v.astype(np.float32).reshape(shape))
+        off += n
+    return params
+
+
+def cam_from_K(K):
+    """a15 (no reference code): (B,3,3) -> (B,4) [fx, fy, cx, cy] = [K00, K11, K02, K12]."""
+    return torch.stack([K[:, 0, 0], K[:, 1, 1], K[:, 0, 2], K[:, 1, 2]], 1).contiguous()
+
+
+def normalize_cam(c, width, height):
+    """IntrinsicsConditionedUNetImpl::normalizeCameraIntrinsics (intrinsics_unet.h:252-268)."""
+    n = c.clone()
+    n[:, 0] = c[:, 0] / width
+    n[:, 1] = c[:, 1] / height
+    n[:, 2] = (c[:, 2] / width) * 2.0 - 1.0
+    n[:, 3] = (c[:, 3] / height) * 2.0 - 1.0
+    return n
+
+
+def rays_from_K(K, H, W):
+    """a18: computeRayDirections (ray_direction_computer.cpp:17-62) per sample, laid out (B,3,H,W)
+    (sunrgbd_loader.cpp:346-347), float32 like the reference: x = (u - cx) * (1/fx), ..., r / |r|."""
+    K = K.to(torch.float32)
+    fxi = (1.0 / K[:, 0, 0]).view(-1, 1, 1)
+    fyi = (1.0 / K[:, 1, 1]).view(-1, 1, 1)
+    cx, cy = K[:, 0, 2].view(-1, 1, 1), K[:, 1, 2].view(-1, 1, 1)
+    u = torch.arange(W, dtype=torch.float32).view(1, 1, W)
+    v = torch.arange(H, dtype=torch.float32).view(1, H, 1)
+    x = ((u - cx) * fxi).expand(-1, H, W)
+    y = ((v - cy) * fyi).expand(-1, H, W)
+    n = torch.sqrt(x * x + y * y + 1.0)
+    return torch.stack([x / n, y / n, 1.0 / n], 1).contiguous()
 
 
 def _bn(x, p, bufs, prefix, train):
@@ -152,34 +238,59 @@ def _bn(x, p, bufs, prefix, train):
                         p[prefix + ".weight"], p[prefix + ".bias"], train, 0.1, 1e-5)
 
 
-def _double_conv(x, p, bufs, pre, train):
-    # DoubleConvImpl::forward (baseline_unet.h:32-43)
+def _film(x, c, p, bufs, pre, train):
+    # FiLMLayerImpl::forward (film_layer.h:82-108): BatchNorm1d only when the batch has > 1 sample
+    def bn1d(h, name):
+        if h.shape[0] <= 1:
+            return h
+        return F.batch_norm(h, bufs[pre + name + ".running_mean"], bufs[pre + name + ".running_var"],
+                            p[pre + name + ".weight"], p[pre + name + ".bias"], train, 0.1, 1e-5)
+    h = F.relu(bn1d(F.linear(c, p[pre + "fc1.weight"], p[pre + "fc1.bias"]), "bn1"))
+    h = F.relu(bn1d(F.linear(h, p[pre + "fc2.weight"], p[pre + "fc2.bias"]), "bn2"))
+    gamma = F.linear(h, p[pre + "fc_gamma.weight"], p[pre + "fc_gamma.bias"])
+    beta = F.linear(h, p[pre + "fc_beta.weight"], p[pre + "fc_beta.bias"])
+    return gamma[:, :, None, None] * x + beta[:, :, None, None]
+
+
+def _double_conv(x, p, bufs, pre, train, cam=None):
+    # DoubleConvImpl::forward (baseline_unet.h:32-43); with `cam`: FiLMDoubleConvImpl::forward
+    # (intrinsics_unet.h:38-52) = RayEnhancedConvImpl::forward after its cat (geometry_aware_network.h:47-64)
     x = F.conv2d(x, p[pre + "conv1.weight"], None, 1, 1)
     x = F.relu(_bn(x, p, bufs, pre + "bn1", train))
+    if cam is not None:
+        x = _film(x, cam, p, bufs, pre + "film.", train)
     x = F.conv2d(x, p[pre + "conv2.weight"], None, 1, 1)
     return F.relu(_bn(x, p, bufs, pre + "bn2", train))
 
 
-def _decoder(x, skip, p, bufs, pre, train):
+def _decoder(x, skip, p, bufs, pre, train, cam=None):
     # DecoderBlockImpl::forward (baseline_unet.h:83-102): up, pad-if-needed, cat({skip, up}), conv
+    # (FiLMDecoderBlockImpl::forward, intrinsics_unet.h:91-110, is the same with a FiLM conv)
     x = F.conv_transpose2d(x, p[pre + "up.weight"], p[pre + "up.bias"], stride=2)
     dh, dw = skip.shape[2] - x.shape[2], skip.shape[3] - x.shape[3]
     if dh > 0 or dw > 0:
         x = F.pad(x, (dw // 2, dw - dw // 2, dh // 2, dh - dh // 2))
-    return _double_conv(torch.cat([skip, x], 1), p, bufs, pre + "conv.", train)
+    return _double_conv(torch.cat([skip, x], 1), p, bufs, pre + "conv.", train, cam)
 
 
-def unet_forward(x, p, bufs, train=True, max_depth=10.0):
-    """BaselineUNetImpl::forward (baseline_unet.h:174-195)."""
-    s1 = _double_conv(x, p, bufs, "enc1.", train)
-    s2 = _double_conv(F.max_pool2d(s1, 2), p, bufs, "enc2.conv.", train)
-    s3 = _double_conv(F.max_pool2d(s2, 2), p, bufs, "enc3.conv.", train)
-    s4 = _double_conv(F.max_pool2d(s3, 2), p, bufs, "enc4.conv.", train)
-    xb = _double_conv(F.max_pool2d(s4, 2), p, bufs, "bottleneck.conv.", train)
-    x = _decoder(xb, s4, p, bufs, "dec4.", train)
-    x = _decoder(x, s3, p, bufs, "dec3.", train)
-    x = _decoder(x, s2, p, bufs, "dec2.", train)
-    x = _decoder(x, s1, p, bufs, "dec1.", train)
+def unet_forward(x, p, bufs, train=True, max_depth=10.0, model="baseline", K=None):
+    """BaselineUNetImpl::forward (baseline_unet.h:174-195); model "film":
+    IntrinsicsConditionedUNetImpl::forward(x, cam_from_K(K)) (intrinsics_unet.h:204-228); "rayfilm":
+    the same wiring with enc1 fed cat(x, rays_from_K(K))."""
+    cam = None
+    if model != "baseline":
+        cam = normalize_cam(cam_from_K(K.to(x.dtype)), x.shape[3], x.shape[2])
+        if model == "rayfilm":
+            x = torch.cat([x, rays_from_K(K, x.shape[2], x.shape[3]).to(x.dtype)], 1)
+    s1 = _double_conv(x, p, bufs, "enc1.", train, cam)
+    s2 = _double_conv(F.max_pool2d(s1, 2), p, bufs, "enc2.conv.", train, cam)
+    s3 = _double_conv(F.max_pool2d(s2, 2), p, bufs, "enc3.conv.", train, cam)
+    s4 = _double_conv(F.max_pool2d(s3, 2), p, bufs, "enc4.conv.", train, cam)
+    xb = _double_conv(F.max_pool2d(s4, 2), p, bufs, "bottleneck.conv.", train, cam)
+    x = _decoder(xb, s4, p, bufs, "dec4.", train, cam)
+    x = _decoder(x, s3, p, bufs, "dec3.", train, cam)
+    x = _decoder(x, s2, p, bufs, "dec2.", train, cam)
+    x = _decoder(x, s1, p, bufs, "dec1.", train, cam)
     x = F.conv2d(x, p["out_conv.weight"], p["out_conv.bias"])
     return torch.sigmoid(x) * max_depth
 
@@ -282,6 +393,8 @@ def loss_and_dpred(pred, gt, image, K, weights=(1.0, 0.1, 0.001, 0.01)):
 # Optimizer: clip_grad_norm_ (LibTorch clip_grad.h) + torch::optim::Adam (coupled L2)
 # --------------------------------------------------------------------------------------------
 def clip_grad_norm_(grads, max_norm=1.0):
+    # parameters without a gradient (None: e.g. FiLM BatchNorm1d at batch 1) are skipped (clip_grad.h:29-35)
+    grads = [g for g in grads if g is not None]
     norms = torch.stack([g.norm(2) for g in grads])
     total = norms.norm(2) if len(grads) > 1 else norms[0]
     coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
@@ -298,14 +411,18 @@ class Adam:
         self.lr, self.b1, self.b2, self.eps, self.wd = lr, betas[0], betas[1], eps, weight_decay
         self.m = OrderedDict((k, torch.zeros_like(v)) for k, v in params.items())
         self.v = OrderedDict((k, torch.zeros_like(v)) for k, v in params.items())
-        self.t = 0
+        self.t = OrderedDict((k, 0) for k in params)   # per-parameter step (torch Adam state "step")
+        self.t_global = 0
 
     @torch.no_grad()
     def step(self, grads):
-        self.t += 1
-        bc1 = 1 - self.b1 ** self.t
-        bc2 = 1 - self.b2 ** self.t
+        self.t_global += 1
         for (k, p), g in zip(self.params.items(), grads):
+            if g is None:   # no gradient: the parameter and its state are left untouched (adam.cpp)
+                continue
+            self.t[k] += 1
+            bc1 = 1 - self.b1 ** self.t[k]
+            bc2 = 1 - self.b2 ** self.t[k]
             if self.wd != 0:
                 g = g.add(p, alpha=self.wd)
             self.m[k].mul_(self.b1).add_(g, alpha=1 - self.b1)
@@ -318,9 +435,10 @@ class Trainer:
     """One replica of TensorBoardTrainerEnhanced's step (enhanced.h:287-304) on host cores."""
 
     def __init__(self, params, buffers, weights=(1.0, 0.1, 0.001, 0.01), lr=1e-4, wd=1e-5,
-                 clip=1.0, max_depth=10.0, dtype=torch.float32):
+                 clip=1.0, max_depth=10.0, dtype=torch.float32, model="baseline"):
         # dtype=float64 gives the exact-arithmetic yardstick the fp32 paths are both measured against
         self.dtype = dtype
+        self.model = model
         self.p = OrderedDict((k, v.clone().to(dtype)) for k, v in params.items())
         self.bufs = OrderedDict((k, v.clone().to(dtype)) for k, v in buffers.items())
         self.weights, self.clip, self.max_depth = weights, clip, max_depth
@@ -331,11 +449,11 @@ class Trainer:
         for v in self.p.values():
             v.requires_grad_(True)
             v.grad = None
-        pred = unet_forward(rgb, self.p, self.bufs, True, self.max_depth)
+        pred = unet_forward(rgb, self.p, self.bufs, True, self.max_depth, self.model, K)
         pred.retain_grad()
         loss, comps = combined_loss(pred, gt, rgb, K, self.weights)
         loss.sum().backward()
-        grads = [v.grad.detach().clone() for v in self.p.values()]
+        grads = [v.grad.detach().clone() if v.grad is not None else None for v in self.p.values()]
         for v in self.p.values():
             v.requires_grad_(False)
         return pred.detach(), pred.grad.detach(), float(loss), comps, grads
@@ -347,13 +465,14 @@ class Trainer:
 
     def step(self, rgb, gt, K):
         pred, dpred, loss, comps, grads = self.forward_backward(rgb, gt, K)
-        pre_clip = [g.clone() for g in grads]
+        pre_clip = [g.clone() if g is not None else None for g in grads]
         total = self.apply(grads)
         return dict(pred=pred, dpred=dpred, loss=loss, comps=comps, grads=pre_clip, norm=total)
 
     @torch.no_grad()
-    def predict_eval(self, rgb):
-        return unet_forward(rgb.to(self.dtype), self.p, self.bufs, False, self.max_depth)
+    def predict_eval(self, rgb, K=None):
+        Kd = K.to(self.dtype) if K is not None else None
+        return unet_forward(rgb.to(self.dtype), self.p, self.bufs, False, self.max_depth, self.model, Kd)
 
 
 def depth_metrics(pred, gt):

@@ -20,6 +20,12 @@ FIXTURES = {
     # config-2 semantics: SI-only weights, non-square 96x128, batch 3 (odd: mixed K per sample)
     "train_f4_b3_96x128_si": ["--mode", "golden", "--f", "4", "--B", "3", "--H", "96", "--W", "128",
                               "--steps", "2", "--weights", "1,0,0,0"],
+    # config-3 model families: FiLM-conditioned U-Net on (B,4) intrinsics, and
+    # the RayEnhancedConv + FiLM composite fed cat(rgb, rays); full 4-term loss
+    "train_film_f4_b2_64x64": ["--mode", "golden", "--model", "film", "--init", "synth", "--f", "4", "--B", "2", "--H", "64",
+                               "--W", "64", "--steps", "3"],
+    "train_rayfilm_f4_b3_64x96": ["--mode", "golden", "--model", "rayfilm", "--init", "synth", "--f", "4", "--B", "3", "--H", "64",
+                                  "--W", "96", "--steps", "2"],
     # loss-only goldens (depth_loss.h) incl. a size whose pyramid floors (50x70 -> 6x8 at k=8)
     "loss_b2_120x160": ["--mode", "loss", "--B", "2", "--H", "120", "--W", "160"],
     "loss_b3_50x70": ["--mode", "loss", "--B", "3", "--H", "50", "--W", "70"],
@@ -30,7 +36,10 @@ FIXTURES = {
 def main():
     if not os.path.exists(HARNESS):
         sys.exit("build the harness first: make -C oracle")
+    only = set(sys.argv[1:])
     for name, args in FIXTURES.items():
+        if only and name not in only:
+            continue
         out = os.path.join(GOLDEN, name)
         os.makedirs(out, exist_ok=True)
         subprocess.run([HARNESS, "--threads", "1", "--out", out] + args, check=True)

@@ -9,6 +9,14 @@
 // and dumps golden fixtures (mode "golden") or times the step on the host cores (mode "time",
 // used by bench.py's cpu_baseline leg with kind="reference").
 //
+// --model selects the network:
+//   baseline  BaselineUNetImpl(3, f, 10)                       models/baseline_unet.h:144-206
+//   film      IntrinsicsConditionedUNetImpl(3, f, 4, 10)        models/intrinsics_unet.h:137-270
+//             fed (B,4) [fx, fy, cx, cy] = [K00, K11, K02, K12] (a15: no reference code exists)
+//   rayfilm   the config-3 composite of SURVEY §8 "Recommended config-3 model": enc1 =
+//             RayEnhancedConv(3, f, 4, true) (geometry_aware_network.h:17-65) fed cat(rgb, rays),
+//             enc2..dec1 = FiLMEncoderBlock / FiLMDecoderBlock (intrinsics_unet.h:59-113).
+//
 // Inputs are the synthetic SUN-RGB-D-shaped batches of SURVEY.md §8(d): a counter-based
 // splitmix64 stream so that every consumer (this harness, oracle/cad_oracle.py, bench.py) can
 // regenerate identical bytes.  Outputs: <out>/manifest.json + <out>/tensors.bin (raw f32 LE).
@@ -19,12 +27,15 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <functional>
 #include <map>
 #include <sstream>
 #include <string>
 #include <vector>
 
 #include "models/baseline_unet.h"
+#include "models/geometry_aware_network.h"
+#include "models/intrinsics_unet.h"
 #include "loss/depth_loss.h"
 
 using namespace camera_aware_depth;
@@ -42,7 +53,7 @@ float u01(uint64_t seed, uint64_t idx) {
     return (float)(u >> 8) * (1.0f / 16777216.0f);
 }
 
-struct Batch { torch::Tensor rgb, gt, K; };
+struct Batch { torch::Tensor rgb, gt, K, cam4, rays; };
 
 // SURVEY.md §8(d) synthetic batch (rgb U[0,1), smooth depth with Kinect-style holes, per-sample K).
 Batch make_batch(int B, int H, int W, uint64_t rgb_seed = 0xC0FFEE, uint64_t hole_seed = 0xD3E7) {
@@ -72,7 +83,137 @@ Batch make_batch(int B, int H, int W, uint64_t rgb_seed = 0xC0FFEE, uint64_t hol
         float* kk = k + bb * 9;
         kk[0] = fx * sx; kk[2] = cx * sx; kk[4] = fy * sy; kk[5] = cy * sy; kk[8] = 1.0f;
     }
+    // a15: (B,3,3) -> (B,4) [fx, fy, cx, cy]
+    b.cam4 = torch::stack({b.K.select(1, 0).select(1, 0), b.K.select(1, 1).select(1, 1),
+                           b.K.select(1, 0).select(1, 2), b.K.select(1, 1).select(1, 2)}, 1).contiguous();
+    // a18: RayDirectionComputer::computeRayDirections (ray_direction_computer.cpp:17-62) restated
+    // (that .cpp needs Eigen, absent here), laid out (B,3,H,W) as the loader reshapes it
+    // (sunrgbd_loader.cpp:346-347), computed directly at the working resolution from the scaled K.
+    b.rays = torch::empty({B, 3, H, W});
+    float* ry = b.rays.data_ptr<float>();
+    for (int bb = 0; bb < B; ++bb) {
+        const float* kk = k + bb * 9;
+        const float fx_inv = 1.0f / kk[0], fy_inv = 1.0f / kk[4], cx = kk[2], cy = kk[5];
+        for (int v = 0; v < H; ++v)
+            for (int u = 0; u < W; ++u) {
+                const float x = ((float)u - cx) * fx_inv, y = ((float)v - cy) * fy_inv, z = 1.0f;
+                const float n = std::sqrt(x * x + y * y + z * z);
+                const int64_t o = (int64_t)v * W + u, hw = (int64_t)H * W;
+                ry[((int64_t)bb * 3 + 0) * hw + o] = x / n;
+                ry[((int64_t)bb * 3 + 1) * hw + o] = y / n;
+                ry[((int64_t)bb * 3 + 2) * hw + o] = z / n;
+            }
+    }
     return b;
+}
+
+// IntrinsicsConditionedUNetImpl::normalizeCameraIntrinsics (intrinsics_unet.h:252-268) is private;
+// the composite below needs the same (B,4) normalisation (a14), so it is restated with the same ops.
+torch::Tensor normalize_cam(torch::Tensor in, int width, int height) {
+    using torch::indexing::Slice;
+    auto n = in.clone();
+    n.index_put_({Slice(), 0}, in.index({Slice(), 0}) / width);
+    n.index_put_({Slice(), 1}, in.index({Slice(), 1}) / height);
+    n.index_put_({Slice(), 2}, (in.index({Slice(), 2}) / width) * 2.0f - 1.0f);
+    n.index_put_({Slice(), 3}, (in.index({Slice(), 3}) / height) * 2.0f - 1.0f);
+    return n;
+}
+
+// Config-3 composite from reference classes only (no new math): module registration order equals
+// IntrinsicsConditionedUNetImpl's, so parameter names match it (enc1.* is a RayEnhancedConv whose
+// conv1 takes 3 + 3 ray channels).  32,862,465 parameters at f = 64.
+struct RayFiLMUNetImpl : torch::nn::Module {
+    RayEnhancedConv enc1{nullptr};
+    FiLMEncoderBlock enc2{nullptr}, enc3{nullptr}, enc4{nullptr}, bottleneck{nullptr};
+    FiLMDecoderBlock dec4{nullptr}, dec3{nullptr}, dec2{nullptr}, dec1{nullptr};
+    torch::nn::Conv2d out_conv{nullptr};
+    float max_depth;
+    RayFiLMUNetImpl(int f, float md) : max_depth(md) {
+        enc1 = register_module("enc1", RayEnhancedConv(3, f, 4, true));
+        enc2 = register_module("enc2", FiLMEncoderBlock(f, f * 2, 4));
+        enc3 = register_module("enc3", FiLMEncoderBlock(f * 2, f * 4, 4));
+        enc4 = register_module("enc4", FiLMEncoderBlock(f * 4, f * 8, 4));
+        bottleneck = register_module("bottleneck", FiLMEncoderBlock(f * 8, f * 16, 4));
+        dec4 = register_module("dec4", FiLMDecoderBlock(f * 16, f * 8, 4));
+        dec3 = register_module("dec3", FiLMDecoderBlock(f * 8, f * 4, 4));
+        dec2 = register_module("dec2", FiLMDecoderBlock(f * 4, f * 2, 4));
+        dec1 = register_module("dec1", FiLMDecoderBlock(f * 2, f, 4));
+        out_conv = register_module("out_conv", torch::nn::Conv2d(torch::nn::Conv2dOptions(f, 1, 1)));
+    }
+    torch::Tensor forward(torch::Tensor x, torch::Tensor cam4, torch::Tensor rays) {
+        auto c = normalize_cam(cam4, x.size(3), x.size(2));
+        auto s1 = enc1(x, c, rays);
+        auto s2 = enc2(s1, c);
+        auto s3 = enc3(s2, c);
+        auto s4 = enc4(s3, c);
+        auto y = bottleneck(s4, c);
+        y = dec4(y, s4, c);
+        y = dec3(y, s3, c);
+        y = dec2(y, s2, c);
+        y = dec1(y, s1, c);
+        return torch::sigmoid(out_conv(y)) * max_depth;
+    }
+};
+TORCH_MODULE(RayFiLMUNet);
+
+// --init synth: every parameter (named_parameters() order, running element offset `off`) is set from
+// the counter stream so fixtures need not store initial weights (tests regenerate them with
+// oracle/cad_oracle.py:synth_init, bit-identically):
+//   u = u01(0x1A17, off + i);  dim >= 2: (2u - 1) / sqrt(numel / size(0))
+//   1-D *.weight (BN affine) and *.fc_gamma.bias: 1 + 0.1 (2u - 1);  other 1-D: 0.1 (2u - 1)
+void synth_init(torch::nn::Module& m) {
+    torch::NoGradGuard ng;
+    int64_t off = 0;
+    for (auto& kv : m.named_parameters()) {
+        auto t = kv.value();
+        const std::string& n = kv.key();
+        auto ends = [&](const std::string& suf) {
+            return n.size() >= suf.size() && n.compare(n.size() - suf.size(), suf.size(), suf) == 0;
+        };
+        auto c = torch::empty_like(t).contiguous();
+        float* p = c.data_ptr<float>();
+        const int64_t N = c.numel();
+        const float bound = t.dim() >= 2 ? 1.0f / std::sqrt((float)(N / t.size(0))) : 0.f;
+        const bool one = t.dim() == 1 && (ends(".weight") || ends(".fc_gamma.bias"));
+        for (int64_t i = 0; i < N; ++i) {
+            const float u = u01(0x1A17, off + i);
+            p[i] = t.dim() >= 2 ? (2.0f * u - 1.0f) * bound : one ? 1.0f + 0.1f * (2.0f * u - 1.0f) : 0.1f * (2.0f * u - 1.0f);
+        }
+        t.copy_(c);
+        off += N;
+    }
+}
+
+// one network of --model behind a common face
+struct Net {
+    std::shared_ptr<torch::nn::Module> mod;
+    std::function<torch::Tensor(const Batch&)> fwd;
+    int64_t count() const {
+        int64_t n = 0;
+        for (auto& p : mod->parameters()) n += p.numel();
+        return n;
+    }
+};
+
+Net make_net(const std::string& kind, int f) {
+    Net n;
+    if (kind == "baseline") {
+        auto m = std::make_shared<BaselineUNetImpl>(3, f, 10.0f);   // train_main.cpp:325-333
+        n.mod = m;
+        n.fwd = [m](const Batch& b) { return m->forward(b.rgb); };
+    } else if (kind == "film") {
+        auto m = std::make_shared<IntrinsicsConditionedUNetImpl>(3, f, 4, 10.0f);
+        n.mod = m;
+        n.fwd = [m](const Batch& b) { return m->forward(b.rgb, b.cam4); };
+    } else if (kind == "rayfilm") {
+        auto m = std::make_shared<RayFiLMUNetImpl>(f, 10.0f);
+        n.mod = m;
+        n.fwd = [m](const Batch& b) { return m->forward(b.rgb, b.cam4, b.rays); };
+    } else {
+        fprintf(stderr, "unknown --model %s\n", kind.c_str());
+        exit(2);
+    }
+    return n;
 }
 
 struct Dumper {
@@ -116,7 +257,7 @@ double abs_rel_per_sample(torch::Tensor pred, torch::Tensor gt) {
 }
 
 struct Args {
-    std::string mode = "golden", out = ".";
+    std::string mode = "golden", out = ".", model = "baseline", init = "default";
     int f = 8, B = 2, H = 64, W = 64, steps = 3, threads = 1, warmup = 1, holes_all = 0;
     float w[4] = {1.0f, 0.1f, 0.001f, 0.01f};
     float lr = 1e-4f, wd = 1e-5f, clip = 1.0f;
@@ -128,6 +269,8 @@ Args parse(int argc, char** argv) {
         std::string k = argv[i], v = argv[i + 1];
         if (k == "--mode") a.mode = v;
         else if (k == "--out") a.out = v;
+        else if (k == "--model") a.model = v;
+        else if (k == "--init") a.init = v;
         else if (k == "--f") a.f = std::stoi(v);
         else if (k == "--B") a.B = std::stoi(v);
         else if (k == "--H") a.H = std::stoi(v);
@@ -151,7 +294,10 @@ int main(int argc, char** argv) {
     torch::set_num_threads(a.threads);
     torch::manual_seed(42);   // train_main.cpp:318 -> setupSeeds(42)
 
-    auto model = std::make_shared<BaselineUNetImpl>(3, a.f, 10.0f);   // train_main.cpp:325-333
+    Net net = make_net(a.model, a.f);
+    auto& model = net.mod;
+    const bool synth = a.init == "synth";
+    if (synth) synth_init(*model);
     CombinedDepthLoss loss_fn(a.w[0], a.w[1], a.w[2], a.w[3]);        // train_main.cpp:352-357
     torch::optim::Adam opt(model->parameters(),
                            torch::optim::AdamOptions(a.lr).weight_decay(a.wd));   // enhanced.h:97-101
@@ -161,7 +307,7 @@ int main(int argc, char** argv) {
                     std::vector<torch::Tensor>* grads_pre_clip) -> float {
         model->train();
         opt.zero_grad();
-        auto pred = model->forward(batch.rgb);
+        auto pred = net.fwd(batch);
         if (dpred_out) pred.retain_grad();
         auto loss = loss_fn.forwardWithIntrinsics(pred, batch.gt, batch.rgb, batch.K);
         loss.backward();
@@ -182,8 +328,8 @@ int main(int argc, char** argv) {
         for (int i = 0; i < a.steps; ++i) last = step(nullptr, nullptr, nullptr, nullptr);
         double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         printf("{\"images_per_s\": %.6f, \"seconds\": %.3f, \"steps\": %d, \"batch\": %d, \"H\": %d, "
-               "\"W\": %d, \"f\": %d, \"threads\": %d, \"last_loss\": %.6f}\n",
-               a.steps * a.B / s, s, a.steps, a.B, a.H, a.W, a.f, a.threads, last);
+               "\"W\": %d, \"f\": %d, \"threads\": %d, \"last_loss\": %.6f, \"model\": \"%s\"}\n",
+               a.steps * a.B / s, s, a.steps, a.B, a.H, a.W, a.f, a.threads, last, a.model.c_str());
         return 0;
     }
 
@@ -221,9 +367,13 @@ int main(int argc, char** argv) {
     d.add("input.rgb", batch.rgb);
     d.add("input.gt", batch.gt);
     d.add("input.K", batch.K);
-    for (auto& kv : model->named_parameters()) d.add("init." + kv.key(), kv.value());
-    for (auto& kv : model->named_buffers())
-        if (kv.value().is_floating_point()) d.add("init." + kv.key(), kv.value());
+    if (a.model != "baseline") d.add("input.cam4", batch.cam4);
+    if (a.model == "rayfilm") d.add("input.rays", batch.rays);
+    if (!synth) {   // synth init: regenerated by the tests, buffers are the module defaults
+        for (auto& kv : model->named_parameters()) d.add("init." + kv.key(), kv.value());
+        for (auto& kv : model->named_buffers())
+            if (kv.value().is_floating_point()) d.add("init." + kv.key(), kv.value());
+    }
 
     torch::Tensor pred1, dpred1;
     double norm1 = 0;
@@ -241,7 +391,8 @@ int main(int argc, char** argv) {
         auto names = model->named_parameters();
         int i = 0;
         for (auto& kv : names) d.add("step1.grad." + kv.key(), g1[i++]);
-        for (auto& kv : names) d.add("step1.param." + kv.key(), kv.value());
+        if (!synth)
+            for (auto& kv : names) d.add("step1.param." + kv.key(), kv.value());
         for (auto& kv : model->named_buffers())
             if (kv.value().is_floating_point()) d.add("step1." + kv.key(), kv.value());
     }
@@ -254,18 +405,18 @@ int main(int argc, char** argv) {
     {
         torch::NoGradGuard ng;
         model->eval();
-        pred_eval = model->forward(batch.rgb);
+        pred_eval = net.fwd(batch);
     }
     d.add("final.pred_eval", pred_eval);
     double absrel = abs_rel_per_sample(pred_eval, batch.gt);
 
     std::ostringstream meta;
     meta.precision(9);
-    meta << "{\"f\": " << a.f << ", \"B\": " << a.B << ", \"H\": " << a.H << ", \"W\": " << a.W
+    meta << "{\"model\": \"" << a.model << "\", \"init\": \"" << a.init << "\", \"f\": " << a.f << ", \"B\": " << a.B << ", \"H\": " << a.H << ", \"W\": " << a.W
          << ", \"steps\": " << a.steps << ", \"threads\": " << a.threads
          << ", \"weights\": [" << a.w[0] << ", " << a.w[1] << ", " << a.w[2] << ", " << a.w[3] << "]"
          << ", \"lr\": " << a.lr << ", \"wd\": " << a.wd << ", \"clip\": " << a.clip
-         << ", \"num_params\": " << model->count_parameters()
+         << ", \"num_params\": " << net.count()
          << ", \"step1_total_norm\": " << norm1 << ", \"losses\": [";
     for (size_t i = 0; i < losses.size(); ++i) meta << (i ? ", " : "") << losses[i];
     meta << "], \"step1_components\": {";
@@ -273,6 +424,6 @@ int main(int argc, char** argv) {
     for (auto& kv : comps1) { meta << (first ? "" : ", ") << "\"" << kv.first << "\": " << kv.second; first = false; }
     meta << "}, \"final_abs_rel_eval\": " << absrel << "}";
     d.finish(meta.str());
-    printf("wrote %s (num_params=%lld, loss1=%.6f)\n", a.out.c_str(), (long long)model->count_parameters(), losses[0]);
+    printf("wrote %s (num_params=%lld, loss1=%.6f)\n", a.out.c_str(), (long long)net.count(), losses[0]);
     return 0;
 }

@@ -1,0 +1,194 @@
+"""Config-3 model families on MI355X: IntrinsicsConditionedUNet (FiLM after
+every DoubleConv's first BN-ReLU) and the RayEnhancedConv + FiLM composite, through libcad_hip.so.
+
+Pinned to the REFERENCE by tests/golden/train_{film,rayfilm}_* (reference headers intrinsics_unet.h,
+geometry_aware_network.h, film_layer.h compiled against LibTorch by oracle/ref_harness.cpp) and to the
+oracle restatement (fp32 and the fp64 yardstick) at wider configurations."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, max_rel_err
+
+pytestmark = pytest.mark.gpu
+
+FILM = ["train_film_f4_b2_64x64", "train_rayfilm_f4_b3_64x96"]
+
+
+def _cls(cad, model):
+    return {"film": cad.IntrinsicsConditionedUNet, "rayfilm": cad.RayConditionedUNet}[model]
+
+
+def _build(cad, model, f, B, H, W, weights, state):
+    net = _cls(cad, model)(3, f, 4, 10.0, batch=B, height=H, width=W)
+    net.load_state_dict(state)
+    loss = cad.CombinedDepthLoss(*weights, batch=B, height=H, width=W)
+    tr = cad.Trainer(net, loss, lr=1e-4, weight_decay=1e-5, grad_clip=1.0)
+    return net, loss, tr
+
+
+def _zero_grad_bias(name, B):
+    # Linear bias feeding a train-mode BatchNorm1d: exactly-zero true gradient (rounding noise only)
+    return B > 1 and (name.endswith("film.fc1.bias") or name.endswith("film.fc2.bias"))
+
+
+@pytest.mark.parametrize("name", FILM)
+def test_film_train_steps_vs_reference_fixture(cad, dev, oracle, name):
+    fx, meta = oracle.load_fixture(os.path.join(GOLDEN, name))
+    model, f, B, H, W = meta["model"], meta["f"], meta["B"], meta["H"], meta["W"]
+    state = dict(oracle.synth_init(f, model=model))
+    state.update(oracle.init_buffers(f, model=model))
+    net, loss, tr = _build(cad, model, f, B, H, W, meta["weights"], state)
+    assert net.count_parameters() == meta["num_params"]
+    assert [n for n, _ in net._param_info] == [n for n, _ in oracle.param_spec(f, model=model)]
+    assert [n for n, _ in net._buffer_info] == [n for n, _ in oracle.buffer_spec(f, model=model)]
+    rgb, gt, K = fx["input.rgb"].to(dev), fx["input.gt"].to(dev), fx["input.K"].to(dev)
+    cam = cad.camera_from_K(K)
+    assert torch.equal(cam.cpu(), fx["input.cam4"])
+
+    net.train()
+    pred = net.forward_cam(rgb, cam)
+    loss5, dpred = loss.forward_with_intrinsics(pred, gt, rgb, K)
+    net.backward(dpred)
+    torch.cuda.synchronize()
+    assert max_rel_err(pred.cpu(), fx["step1.pred"]) < 1e-4
+    assert abs(loss5[0].item() - meta["losses"][0]) <= 1e-4 * abs(meta["losses"][0])
+    assert max_rel_err(dpred.cpu(), fx["step1.dpred"]) < 1e-3
+    grads = net.grads()
+    for n, g in grads.items():
+        ref = fx["step1.grad." + n]
+        if _zero_grad_bias(n, B):
+            scale = fx["step1.grad." + n[: -len("bias")] + "weight"].abs().max().item()
+            err = (g - ref).abs().max().item() / scale
+        else:
+            err = max_rel_err(g, ref)
+        # FiLM MLP gradients run through a BatchNorm1d over 2-3 samples (cancellation-dominated)
+        assert err < (3e-3 if ".film." in n else 1e-3), (n, err)
+    cad.clip_grad_norm_(net, 1.0)
+    tr.optimizer.step()
+    assert abs(net.last_grad_norm() - meta["step1_total_norm"]) <= 1e-4 * meta["step1_total_norm"]
+
+    losses = [loss5[0].item()]
+    for _ in range(1, meta["steps"]):
+        losses.append(tr.train_step(rgb, gt, K)[0].item())
+    np.testing.assert_allclose(losses, meta["losses"], rtol=2e-4)
+    lr = meta["lr"]
+    for n, p in net.named_parameters().items():
+        d = (p - fx["final.param." + n]).abs()
+        assert d.max().item() <= 2 * lr * meta["steps"] + 1e-6, n
+        assert (d < 1e-5).float().mean().item() > (0.5 if _zero_grad_bias(n, B) else 0.9), n
+    for n, b in net.named_buffers().items():
+        ref = fx["final." + n]
+        tol = 0.1 * 2 * lr * meta["steps"] if ".film.bn" in n and n.endswith("mean") else 0.0
+        assert (b - ref).abs().max().item() <= 1e-4 * ref.abs().max().item() + tol, n
+    net.eval()
+    pe = net.forward_cam(rgb, cam)
+    assert max_rel_err(pe.cpu(), fx["final.pred_eval"]) < 1e-3
+    a = cad.depth_metrics(pe, gt)["abs_rel"]
+    assert abs(a - meta["final_abs_rel_eval"]) <= 1e-3 * meta["final_abs_rel_eval"]
+
+
+def test_rayfilm_input_pack(cad, dev, oracle):
+    """a18/a19: enc1's NHWC8 input = [rgb | rays(K) | 0 0], rays from the on-device camera vector."""
+    B, H, W = 3, 32, 48
+    rgb, _, K = [torch.from_numpy(a) for a in oracle.synth_batch(B, H, W)]
+    net = cad.RayConditionedUNet(3, 4, 4, 10.0, batch=B, height=H, width=W)
+    net.eval()
+    Kd = K.to(dev)
+    net.forward_cam(rgb.to(dev), cad.camera_from_K(Kd))
+    x0 = net.debug_buffer("x0").view(B, H, W, 8).permute(0, 3, 1, 2)
+    assert torch.equal(x0[:, :3], rgb)
+    rays = oracle.rays_from_K(K, H, W)
+    assert (x0[:, 3:6] - rays).abs().max().item() < 2e-7
+    assert torch.equal(x0[:, 6:], torch.zeros_like(x0[:, 6:]))
+    camn = net.debug_buffer("camn").view(B, 4)
+    ref = oracle.normalize_cam(oracle.cam_from_K(K), W, H)
+    assert torch.equal(camn, ref)
+
+
+@pytest.mark.parametrize("model,f,B,H,W", [("film", 16, 2, 64, 96), ("rayfilm", 32, 4, 48, 64)])
+def test_film_train_step_vs_oracle(cad, dev, oracle, model, f, B, H, W):
+    """Wider FiLM nets against the oracle; same fp64-yardstick criteria as the baseline test
+    (test_gpu_model.py::test_train_step_vs_oracle)."""
+    params = oracle.init_params(f, seed=f, model=model)
+    bufs = oracle.init_buffers(f, model=model)
+    rgb, gt, K = [torch.from_numpy(a) for a in oracle.synth_batch(B, H, W)]
+    ref = oracle.Trainer(params, bufs, model=model)
+    r = ref.step(rgb, gt, K)
+    r64 = oracle.Trainer(params, bufs, dtype=torch.float64, model=model).step(rgb, gt, K)
+    state = dict(params)
+    state.update(bufs)
+    net, loss, tr = _build(cad, model, f, B, H, W, (1.0, 0.1, 0.001, 0.01), state)
+    rg, gg, kg = rgb.to(dev), gt.to(dev), K.to(dev)
+    pred = net.forward_cam(rg, cad.camera_from_K(kg))
+    loss5, dpred = loss.forward_with_intrinsics(pred, gg, rg, kg)
+    net.backward(dpred)
+    torch.cuda.synchronize()
+    assert max_rel_err(pred.cpu(), r["pred"]) < 1e-4
+    assert abs(loss5[0].item() - r["loss"]) <= 1e-4 * abs(r["loss"])
+    grads = net.grads()
+    for (n, _), g32, g64 in zip(oracle.param_spec(f, model=model), r["grads"], r64["grads"]):
+        if _zero_grad_bias(n, B):   # true gradient is 0: noise well below the weight-gradient scale
+            w = grads[n[: -len("bias")] + "weight"]
+            assert grads[n].abs().max().item() <= 1e-2 * w.abs().max().item() + 1e-12, n
+            continue
+        ours, ref32 = max_rel_err(grads[n], g64), max_rel_err(g32, g64)
+        cos = torch.nn.functional.cosine_similarity(grads[n].double().reshape(1, -1), g64.reshape(1, -1)).item()
+        assert cos > 0.9999 and ours < max(0.25, 3 * ref32), (n, cos, ours, ref32)
+    ref64 = oracle.Trainer(params, bufs, dtype=torch.float64, model=model)
+    ref64.step(rgb, gt, K)
+    cad.clip_grad_norm_(net, 1.0)
+    tr.optimizer.step()
+    for _ in range(2):
+        ref.step(rgb, gt, K)
+        ref64.step(rgb, gt, K)
+        tr.train_step(rg, gg, kg)
+    p_ref = ref.step(rgb, gt, K)["pred"]
+    p64 = ref64.step(rgb, gt, K)["pred"]
+    tr.train_step(rg, gg, kg)
+    torch.cuda.synchronize()
+    assert max_rel_err(tr.pred.cpu(), p64) < max(1e-3, 3 * max_rel_err(p_ref, p64))
+    net.eval()
+    pe = net.forward_cam(rg, cad.camera_from_K(kg))
+    pe_ref, pe64 = ref.predict_eval(rgb, K), ref64.predict_eval(rgb, K)
+    assert max_rel_err(pe.cpu(), pe64) < max(1e-3, 3 * max_rel_err(pe_ref, pe64))
+
+
+def test_film_batch_one_skips_batchnorm1d(cad, dev, oracle):
+    """film_layer.h:85,91: with one sample the FiLM MLP has no BatchNorm1d (train and eval)."""
+    f, H, W = 8, 32, 32
+    params = oracle.synth_init(f, model="film")
+    bufs = oracle.init_buffers(f, model="film")
+    rgb, gt, K = [torch.from_numpy(a) for a in oracle.synth_batch(1, H, W)]
+    state = dict(params)
+    state.update(bufs)
+    net, loss, tr = _build(cad, "film", f, 1, H, W, (1.0, 0.1, 0.001, 0.01), state)
+    cam = cad.camera_from_K(K.to(dev))
+    for train in (True, False):
+        net.train(train)
+        ref = oracle.unet_forward(rgb, {k: v.clone() for k, v in params.items()},
+                                  {k: v.clone() for k, v in bufs.items()}, train, 10.0, "film", K)
+        pred = net.forward_cam(rgb.to(dev), cam)
+        assert max_rel_err(pred.cpu(), ref) < 1e-4, train
+    # running stats of the FiLM BatchNorm1d are untouched by a batch-1 train forward
+    for n, b in net.named_buffers().items():
+        if ".film.bn" in n:
+            assert torch.equal(b, bufs[n]), n
+
+
+def test_film_bench_shape_smoke(cad, dev):
+    """Config-3 shape (bs2 slice of it): 480x640 f=64 ray+FiLM model, 32,862,465 parameters."""
+    B, H, W = 2, 480, 640
+    from cad_amd import synthetic
+    rgb, gt, K = synthetic.device_batch(B, H, W, dev)
+    net = cad.RayConditionedUNet(3, 64, 4, 10.0, batch=B, height=H, width=W)
+    assert net.count_parameters() == 32862465
+    loss = cad.CombinedDepthLoss(batch=B, height=H, width=W)
+    tr = cad.Trainer(net, loss)
+    l0 = tr.train_step(rgb, gt, K)[0].item()
+    l1 = tr.train_step(rgb, gt, K)[0].item()
+    assert np.isfinite(l0) and np.isfinite(l1)
+    assert tr.pred.min().item() > 0 and tr.pred.max().item() < 10
+    assert 0 < net.last_grad_norm() < 1e4

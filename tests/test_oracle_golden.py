@@ -104,3 +104,82 @@ def test_all_holes_fixture_semantics(oracle):
     assert meta["components"]["si_loss"] == 0.0 and meta["components"]["reproj_loss"] == 0.0
     assert meta["components"]["grad_loss"] > 0 and meta["components"]["smooth_loss"] > 0
     assert meta["total_dim"] == 1   # CombinedDepthLoss returns shape [1]
+
+
+# ---------------- config-3 model families ----------------
+FILM = ["train_film_f4_b2_64x64", "train_rayfilm_f4_b3_64x96"]
+
+
+def test_film_param_count_known_answers(oracle):
+    # IntrinsicsConditionedUNet(3, 64, 4): 32,860,737; config-3 composite: 32,862,465
+    assert oracle.num_params(64, model="film") == 32860737
+    assert oracle.num_params(64, model="rayfilm") == 32862465
+    # one FiLMLayer(4, 64): 67,328 parameters
+    assert sum(int(np.prod(s)) for _, s in oracle._film_spec("x.", 64)) == 67328
+
+
+@pytest.mark.parametrize("name", FILM)
+def test_film_fixture_layout_and_inputs(oracle, name):
+    fx, meta = oracle.load_fixture(os.path.join(GOLDEN, name))
+    model, f = meta["model"], meta["f"]
+    assert meta["init"] == "synth"
+    names = [k[len("step1.grad."):] for k in fx if k.startswith("step1.grad.")]
+    assert names == [n for n, _ in oracle.param_spec(f, model=model)]
+    assert meta["num_params"] == oracle.num_params(f, model=model)
+    bnames = [k[len("final."):] for k in fx if k.startswith("final.") and "running" in k]
+    assert bnames == [n for n, _ in oracle.buffer_spec(f, model=model)]
+    _, _, K = oracle.synth_batch(meta["B"], meta["H"], meta["W"])
+    K = torch.from_numpy(K)
+    assert torch.equal(oracle.cam_from_K(K), fx["input.cam4"])
+    if model == "rayfilm":
+        r = oracle.rays_from_K(K, meta["H"], meta["W"])
+        assert (r - fx["input.rays"]).abs().max().item() < 2e-7
+
+
+def film_zero_grad_bias(name, B):
+    return B > 1 and (name.endswith("film.fc1.bias") or name.endswith("film.fc2.bias"))
+
+
+def film_grad_err(name, g, fx, B):
+    """Relative error of a gradient; a Linear bias feeding a train-mode BatchNorm1d (FiLM fc1/fc2 at
+    B > 1) has an exactly-zero true gradient, so both sides hold rounding noise: measure it against
+    the scale of the matching weight's gradient instead."""
+    ref = fx["step1.grad." + name]
+    if film_zero_grad_bias(name, B):
+        scale = fx["step1.grad." + name[: -len("bias")] + "weight"].abs().max().item()
+        return (g - ref).abs().max().item() / max(scale, 1e-30)
+    return max_rel_err(g, ref)
+
+
+@pytest.mark.parametrize("name", FILM)
+def test_oracle_film_train_steps_vs_reference(oracle, name):
+    fx, meta = oracle.load_fixture(os.path.join(GOLDEN, name))
+    model, f = meta["model"], meta["f"]
+    params = oracle.synth_init(f, model=model)
+    bufs = oracle.init_buffers(f, model=model)
+    tr = oracle.Trainer(params, bufs, weights=meta["weights"], model=model)
+    rgb, gt, K = fx["input.rgb"], fx["input.gt"], fx["input.K"]
+    r = tr.step(rgb, gt, K)
+    assert max_rel_err(r["pred"], fx["step1.pred"]) < 1e-5
+    assert max_rel_err(r["dpred"], fx["step1.dpred"]) < 1e-4
+    assert abs(r["loss"] - meta["losses"][0]) <= 1e-6 * abs(meta["losses"][0])
+    assert abs(r["norm"] - meta["step1_total_norm"]) <= 1e-5 * meta["step1_total_norm"]
+    for (n, _), g in zip(oracle.param_spec(f, model=model), r["grads"]):
+        # FiLM MLP gradients pass a BatchNorm1d over only B = 2-3 samples (cancellation-dominated)
+        assert film_grad_err(n, g, fx, meta["B"]) < (1e-3 if ".film." in n else 1e-4), n
+    losses = [r["loss"]] + [tr.step(rgb, gt, K)["loss"] for _ in range(meta["steps"] - 1)]
+    np.testing.assert_allclose(losses, meta["losses"], rtol=1e-5)
+    for n, _ in oracle.param_spec(f, model=model):
+        # Adam maps a gradient's sign to a +-lr step: where a FiLM-MLP gradient is rounding noise (the
+        # zero-gradient biases, near-zero weight entries) the step sign is arbitrary, so bound the
+        # drift by the steps taken and require most entries to agree tightly
+        d = (tr.p[n] - fx["final.param." + n]).abs()
+        assert d.max().item() < 2 * meta["lr"] * meta["steps"], n
+        assert (d < 1e-5).float().mean().item() > (0.5 if film_zero_grad_bias(n, meta["B"]) else 0.9), n
+    for n, _ in oracle.buffer_spec(f, model=model):
+        # running_mean of a FiLM BatchNorm1d follows those biases (momentum 0.1)
+        tol = 0.1 * 2 * meta["lr"] * meta["steps"] if ".film.bn" in n and n.endswith("mean") else 0.0
+        assert (tr.bufs[n] - fx["final." + n]).abs().max().item() <= 1e-5 * fx["final." + n].abs().max().item() + tol, n
+    pe = tr.predict_eval(rgb, K)
+    assert max_rel_err(pe, fx["final.pred_eval"]) < 1e-5
+    assert abs(oracle.abs_rel_per_sample(pe, gt) - meta["final_abs_rel_eval"]) < 1e-5
