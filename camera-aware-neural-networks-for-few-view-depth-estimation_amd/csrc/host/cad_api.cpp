@@ -22,6 +22,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
@@ -141,6 +142,10 @@ struct cad_unet {
     int model = CAD_MODEL_BASELINE;
     int in_ch = 3, f = 64, Bmax = 1, H = 0, W = 0;
     int x0_ld = 4;               // NHWC4 rgb (baseline, film) or NHWC8 rgb+rays (ray_film)
+    // BN1-apply + ReLU fused into conv2's operand loaders instead of a materialised a1 (env
+    // CAD_FUSE_BN=1; measured slower on gfx950 — the extra per-stage coefficient loads cost the
+    // GEMMs more than the elementwise pass they remove — so off by default)
+    bool fuse_bn = false;
     float* camn = nullptr;       // normalised intrinsics (Bmax x 4) of the last forward
     float max_depth = 10.f;
     bool train = true;
@@ -309,8 +314,8 @@ void layout(cad_unet* h, Arena& a) {
         DoubleConv& e = h->enc[l];
         bn_alloc(a, e.b1); bn_alloc(a, e.b2);
         const int64_t MC = h->Ml(l, B) * h->Cl(l);
-        e.y1 = a.f(MC); e.y2 = a.f(MC);   // a1 is fused into conv2's loaders (baseline)
-        if (film) e.a1 = a.f(MC);          // FiLM output feeding conv2
+        e.y1 = a.f(MC); e.y2 = a.f(MC);
+        if (film || !h->fuse_bn) e.a1 = a.f(MC);   // relu(bn1(y1)) (FiLM'd) feeding conv2
         film_alloc(a, e, B);
         if (l > 0) e.c1.wd = a.f((int64_t)e.c1.cout * 9 * e.c1.cin);
         e.c2.wd = a.f((int64_t)e.c2.cout * 9 * e.c2.cin);
@@ -326,7 +331,7 @@ void layout(cad_unet* h, Arena& a) {
         bn_alloc(a, d.b1); bn_alloc(a, d.b2);
         const int64_t MC = h->Ml(l, B) * h->Cl(l);
         d.y1 = a.f(MC); d.y2 = a.f(MC);
-        if (film) d.a1 = a.f(MC);
+        if (film || !h->fuse_bn) d.a1 = a.f(MC);
         film_alloc(a, d, B);
         h->dout[l] = a.f(MC);
         d.c1.wd = a.f((int64_t)d.c1.cout * 9 * d.c1.cin);
@@ -423,6 +428,9 @@ void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin,
     if (dc.has_film()) {   // FiLMDoubleConvImpl::forward (intrinsics_unet.h:38-52)
         cad::film_apply(dc.y1, C, dc.b1.scale, dc.b1.shift, dc.film.gam, dc.film.bet, B, (int64_t)Hh * Ww, dc.a1, st);
         cad::conv3x3_fwd(dc.a1, C, 0, C, h->P(dc.c2.pidx), C, dc.y2, C, 0, B, Hh, Ww, tr ? h->stats : nullptr, st);
+    } else if (!h->fuse_bn) {
+        cad::bn_relu_fwd(dc.y1, C, dc.b1.scale, dc.b1.shift, dc.a1, C, 0, M, st);
+        cad::conv3x3_fwd(dc.a1, C, 0, C, h->P(dc.c2.pidx), C, dc.y2, C, 0, B, Hh, Ww, tr ? h->stats : nullptr, st);
     } else {
         // a1 = relu(bn1(y1)) is never materialised: conv2's loader applies it (and so does conv2's wgrad)
         cad::conv3x3_fwd(dc.y1, C, 0, C, h->P(dc.c2.pidx), C, dc.y2, C, 0, B, Hh, Ww, tr ? h->stats : nullptr, st,
@@ -480,7 +488,7 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     cad::bn_relu_bwd(g, ldg, gcoff, dc.y2, C, dc.b2.mean, dc.b2.invstd, dc.b2.scale, dc.b2.shift, h->P(dc.b2.widx), M,
                      h->dscr, dc.b2.coef, h->G(dc.b2.widx), h->G(dc.b2.bidx), dY, st);
     // conv2
-    if (dc.has_film())
+    if (dc.a1)
         cad::conv3x3_wgrad(dY, C, dc.a1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
     else
         cad::conv3x3_wgrad(dY, C, dc.y1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st,
@@ -695,6 +703,8 @@ cad_status cad_unet_create_model(const cad_unet_desc* d, int model, int device, 
         h->device = device;
         h->model = model;
         h->x0_ld = model == CAD_MODEL_RAY_FILM ? 8 : 4;
+        const char* fb = std::getenv("CAD_FUSE_BN");
+        h->fuse_bn = fb && fb[0] == '1';
         h->in_ch = d->in_channels;
         h->f = d->init_features;
         h->max_depth = d->max_depth;

@@ -4,6 +4,7 @@
 // backward (dgrad + wgrad), see SURVEY.md §8(a) a1, a3, a5.
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 
 #include "gemm_mfma.hpp"
 #include "kernels.hpp"
@@ -62,49 +63,49 @@ struct EpiSlab {   // split-K partial: slab z holds C[m][n] of K-slice z
     }
 };
 
-template <int WM, int WN, class Epi, bool BNA = false>
+template <int WM, int WN, int KB, class Epi, bool BNA>
 __global__ __launch_bounds__(256) void k_conv3x3_fwd(GemmArgs a) {
-    using LA = KcIm2col3x3<64 * WM, BNA>;
-    using LB = KcDense<64 * WN>;
-    gemm_body<WM, WN, LA, true, LB, true>(
+    using LA = KcIm2col3x3<64 * WM, KB, BNA>;
+    using LB = KcDense<64 * WN, KB>;
+    gemm_body<WM, WN, KB, LA, true, LB, true>(
         a,
         [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.a_cin, a.B, a.H, a.W, r0, t, kb, a.a_sc, a.a_sh); },
         [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, Epi{});
 }
 
-template <int WM, int WN>
+template <int WM, int WN, int KB>
 __global__ __launch_bounds__(256) void k_convT_fwd(GemmArgs a) {
-    using LA = KcDense<64 * WM>;
-    using LB = KcDense<64 * WN>;
-    gemm_body<WM, WN, LA, true, LB, true>(
+    using LA = KcDense<64 * WM, KB>;
+    using LB = KcDense<64 * WN, KB>;
+    gemm_body<WM, WN, KB, LA, true, LB, true>(
         a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t, kb); },
         [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, EpiConvT{});
 }
 
-template <int WM, int WN>
+template <int WM, int WN, int KB>
 __global__ __launch_bounds__(256) void k_convT_dgrad(GemmArgs a) {
-    using LA = KcUpGather<64 * WM>;
-    using LB = KcDense<64 * WN>;
-    gemm_body<WM, WN, LA, true, LB, true>(
+    using LA = KcUpGather<64 * WM, KB>;
+    using LB = KcDense<64 * WN, KB>;
+    gemm_body<WM, WN, KB, LA, true, LB, true>(
         a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.a_cin, a.B, a.H, a.W, r0, t, kb); },
         [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, EpiStore{});
 }
 
-template <int WM, int WN, bool BNB = false>
+template <int WM, int WN, int KB, bool BNB>
 __global__ __launch_bounds__(256) void k_conv3x3_wgrad(GemmArgs a) {
-    using LA = MNcDense<64 * WM>;
-    using LB = MNcIm2col3x3<64 * WN, BNB>;
-    gemm_body<WM, WN, LA, false, LB, false>(
+    using LA = MNcDense<64 * WM, KB>;
+    using LB = MNcIm2col3x3<64 * WN, KB, BNB>;
+    gemm_body<WM, WN, KB, LA, false, LB, false>(
         a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t, kb); },
         [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.b_cin, a.B, a.H, a.W, r0, t, kb, a.b_sc, a.b_sh); },
         EpiSlab{});
 }
 
-template <int WM, int WN>
+template <int WM, int WN, int KB>
 __global__ __launch_bounds__(256) void k_convT_wgrad(GemmArgs a) {
-    using LA = MNcDense<64 * WM>;
-    using LB = MNcUpGather<64 * WN>;
-    gemm_body<WM, WN, LA, false, LB, false>(
+    using LA = MNcDense<64 * WM, KB>;
+    using LB = MNcUpGather<64 * WN, KB>;
+    gemm_body<WM, WN, KB, LA, false, LB, false>(
         a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t, kb); },
         [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.b_cin, a.B, a.H, a.W, r0, t, kb); },
         EpiSlab{});
@@ -129,80 +130,91 @@ __global__ void k_slab_reduce(const float* __restrict__ slab, int nsplit, int64_
 namespace {
 inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
-// tile shape by output width: narrow N -> tall tiles
+// tile shape by output width: narrow N -> tall tiles.  K-stage depth per (kernel kind, tile shape),
+// measured on MI355X at the bench shapes (bs32 480x640 f=64): 32 pays for the conv3x3 forward/dgrad
+// on the square tile (+1% plain, +8% with the BN-stats epilogue), 16 everywhere else (the wgrad and
+// ConvT GEMMs lose 2-6% at 32, the tall/wide tiles ~10%).  CAD_KB_<KIND>_<CFG>=16|32 overrides,
+// e.g. CAD_KB_WGRAD_C22=32.
 enum Cfg { C41, C22, C14 };
+enum Kind { K_FWD, K_FWDS, K_WGRAD, K_TFWD, K_TDGRAD, K_TWGRAD, K_NKIND };
 Cfg pick_cfg(int M, int N) {
     if (N <= 64) return C41;
     if (M <= 64) return C14;
     return C22;
 }
+int kb_for(Kind k, Cfg c) {
+    static int kb[K_NKIND][3];
+    static bool init = false;
+    if (!init) {
+        const char* kn[K_NKIND] = {"FWD", "FWDS", "WGRAD", "TFWD", "TDGRAD", "TWGRAD"};
+        const char* cn[3] = {"C41", "C22", "C14"};
+        for (int i = 0; i < K_NKIND; ++i)
+            for (int j = 0; j < 3; ++j) {
+                int v = (j == C22 && (i == K_FWD || i == K_FWDS)) ? 32 : 16;
+                char name[40];
+                snprintf(name, sizeof(name), "CAD_KB_%s_%s", kn[i], cn[j]);
+                if (const char* e = std::getenv(name)) v = std::atoi(e);
+                kb[i][j] = v == 32 ? 32 : 16;
+            }
+        init = true;
+    }
+    return kb[k][c];
+}
 
-template <template <int, int> class KT, int WM, int WN>
+template <template <int, int, int> class KT, int WM, int WN, int KB>
 void launch_one(const GemmArgs& a, int splits, hipStream_t st) {
     const dim3 grid(cdiv(a.M, 64 * WM), cdiv(a.N, 64 * WN), splits);
     if (prof_enabled()) {
         char name[160];
-        snprintf(name, sizeof(name), KT<WM, WN>::fmt, WM, WN);
+        snprintf(name, sizeof(name), KT<WM, WN, KB>::fmt, WM, WN, KB);
         prof_push(name, 2.0 * a.M * a.N * (double)a.K, st);
-        hipLaunchKernelGGL((KT<WM, WN>::fn), grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL((KT<WM, WN, KB>::fn), grid, dim3(256), 0, st, a);
         prof_pop(st);
     } else {
-        hipLaunchKernelGGL((KT<WM, WN>::fn), grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL((KT<WM, WN, KB>::fn), grid, dim3(256), 0, st, a);
     }
 }
-template <template <int, int> class KT>
-void launch_cfg(Cfg c, const GemmArgs& a, int splits, hipStream_t st) {
+template <template <int, int, int> class KT, int WM, int WN>
+void launch_kb(int kb, const GemmArgs& a, int splits, hipStream_t st) {
+    if (kb == 32) launch_one<KT, WM, WN, 32>(a, splits, st);
+    else launch_one<KT, WM, WN, 16>(a, splits, st);
+}
+template <template <int, int, int> class KT>
+void launch_cfg(Cfg c, int kb, const GemmArgs& a, int splits, hipStream_t st) {
     switch (c) {
-        case C41: launch_one<KT, 4, 1>(a, splits, st); break;
-        case C22: launch_one<KT, 2, 2>(a, splits, st); break;
-        case C14: launch_one<KT, 1, 4>(a, splits, st); break;
+        case C41: launch_kb<KT, 4, 1>(kb, a, splits, st); break;
+        case C22: launch_kb<KT, 2, 2>(kb, a, splits, st); break;
+        case C14: launch_kb<KT, 1, 4>(kb, a, splits, st); break;
     }
 }
 // fmt = the symbol as rocprofv3 demangles it
-template <int WM, int WN> struct KConvFwd {
-    static constexpr auto fn = k_conv3x3_fwd<WM, WN, EpiStore>;
-    static constexpr const char* fmt = "void cad::k_conv3x3_fwd<%d, %d, cad::EpiStore>(cad::GemmArgs)";
-};
-template <int WM, int WN> struct KConvFwdS {
-    static constexpr auto fn = k_conv3x3_fwd<WM, WN, EpiStoreStats>;
-    static constexpr const char* fmt = "void cad::k_conv3x3_fwd<%d, %d, cad::EpiStoreStats>(cad::GemmArgs)";
-};
-template <int WM, int WN> struct KConvFwdBN {
-    static constexpr auto fn = k_conv3x3_fwd<WM, WN, EpiStore, true>;
-    static constexpr const char* fmt = "void cad::k_conv3x3_fwd<%d, %d, cad::EpiStore, true>(cad::GemmArgs)";
-};
-template <int WM, int WN> struct KConvFwdSBN {
-    static constexpr auto fn = k_conv3x3_fwd<WM, WN, EpiStoreStats, true>;
-    static constexpr const char* fmt = "void cad::k_conv3x3_fwd<%d, %d, cad::EpiStoreStats, true>(cad::GemmArgs)";
-};
-template <int WM, int WN> struct KConvWgradBN {
-    static constexpr auto fn = k_conv3x3_wgrad<WM, WN, true>;
-    static constexpr const char* fmt = "void cad::k_conv3x3_wgrad<%d, %d, true>(cad::GemmArgs)";
-};
-template <int WM, int WN> struct KConvTFwd {
-    static constexpr auto fn = k_convT_fwd<WM, WN>;
-    static constexpr const char* fmt = "void cad::k_convT_fwd<%d, %d>(cad::GemmArgs)";
-};
-template <int WM, int WN> struct KConvTDgrad {
-    static constexpr auto fn = k_convT_dgrad<WM, WN>;
-    static constexpr const char* fmt = "void cad::k_convT_dgrad<%d, %d>(cad::GemmArgs)";
-};
-template <int WM, int WN> struct KConvWgrad {
-    static constexpr auto fn = k_conv3x3_wgrad<WM, WN>;
-    static constexpr const char* fmt = "void cad::k_conv3x3_wgrad<%d, %d>(cad::GemmArgs)";
-};
-template <int WM, int WN> struct KConvTWgrad {
-    static constexpr auto fn = k_convT_wgrad<WM, WN>;
-    static constexpr const char* fmt = "void cad::k_convT_wgrad<%d, %d>(cad::GemmArgs)";
-};
+#define CAD_KT(NAME, EXPR, FMT)                                                  \
+    template <int WM, int WN, int KB> struct NAME {                              \
+        static constexpr auto fn = EXPR;                                         \
+        static constexpr const char* fmt = FMT;                                  \
+    };
+CAD_KT(KConvFwd, (k_conv3x3_fwd<WM, WN, KB, EpiStore, false>),
+       "void cad::k_conv3x3_fwd<%d, %d, %d, cad::EpiStore, false>(cad::GemmArgs)")
+CAD_KT(KConvFwdS, (k_conv3x3_fwd<WM, WN, KB, EpiStoreStats, false>),
+       "void cad::k_conv3x3_fwd<%d, %d, %d, cad::EpiStoreStats, false>(cad::GemmArgs)")
+CAD_KT(KConvFwdBN, (k_conv3x3_fwd<WM, WN, KB, EpiStore, true>),
+       "void cad::k_conv3x3_fwd<%d, %d, %d, cad::EpiStore, true>(cad::GemmArgs)")
+CAD_KT(KConvFwdSBN, (k_conv3x3_fwd<WM, WN, KB, EpiStoreStats, true>),
+       "void cad::k_conv3x3_fwd<%d, %d, %d, cad::EpiStoreStats, true>(cad::GemmArgs)")
+CAD_KT(KConvWgrad, (k_conv3x3_wgrad<WM, WN, KB, false>), "void cad::k_conv3x3_wgrad<%d, %d, %d, false>(cad::GemmArgs)")
+CAD_KT(KConvWgradBN, (k_conv3x3_wgrad<WM, WN, KB, true>), "void cad::k_conv3x3_wgrad<%d, %d, %d, true>(cad::GemmArgs)")
+CAD_KT(KConvTFwd, (k_convT_fwd<WM, WN, KB>), "void cad::k_convT_fwd<%d, %d, %d>(cad::GemmArgs)")
+CAD_KT(KConvTDgrad, (k_convT_dgrad<WM, WN, KB>), "void cad::k_convT_dgrad<%d, %d, %d>(cad::GemmArgs)")
+CAD_KT(KConvTWgrad, (k_convT_wgrad<WM, WN, KB>), "void cad::k_convT_wgrad<%d, %d, %d>(cad::GemmArgs)")
+#undef CAD_KT
 
 int tile_m(Cfg c) { return c == C41 ? 256 : c == C22 ? 128 : 64; }
 int tile_n(Cfg c) { return c == C41 ? 64 : c == C22 ? 128 : 256; }
 
 // split-K planning for the weight-gradient GEMMs: aim for >= ~2048 workgroups, >= 32 K-stages each
-int plan_splits(const GemmArgs& a, Cfg c, int64_t slab_cap_floats) {
+int plan_splits(const GemmArgs& a, Cfg c, int kb, int64_t slab_cap_floats) {
     const int tiles = cdiv(a.M, tile_m(c)) * cdiv(a.N, tile_n(c));
-    const int nk = cdiv(a.K, BK);
+    const int nk = cdiv(a.K, kb);
     int s = std::max(1, std::min(cdiv(2048, tiles), nk / 32));
     const int64_t per = (int64_t)a.M * a.N;
     if (slab_cap_floats > 0) s = (int)std::max<int64_t>(1, std::min<int64_t>(s, slab_cap_floats / per));
@@ -221,12 +233,13 @@ void conv3x3_fwd(const float* x, int64_t ldx, int xcoff, int cin, const float* w
     a.C = y; a.ldc = ldy; a.c_coff = ycoff;
     a.stats = stats;
     a.a_sc = in_scale; a.a_sh = in_shift;
-    a.kstages_per_split = cdiv(a.K, BK);
-    Cfg c = pick_cfg(a.M, a.N);
+    const Cfg c = pick_cfg(a.M, a.N);
+    const int kb = kb_for(stats ? K_FWDS : K_FWD, c);
+    a.kstages_per_split = cdiv(a.K, kb);
     if (in_scale) {
-        if (stats) launch_cfg<KConvFwdSBN>(c, a, 1, st); else launch_cfg<KConvFwdBN>(c, a, 1, st);
+        if (stats) launch_cfg<KConvFwdSBN>(c, kb, a, 1, st); else launch_cfg<KConvFwdBN>(c, kb, a, 1, st);
     } else {
-        if (stats) launch_cfg<KConvFwdS>(c, a, 1, st); else launch_cfg<KConvFwd>(c, a, 1, st);
+        if (stats) launch_cfg<KConvFwdS>(c, kb, a, 1, st); else launch_cfg<KConvFwd>(c, kb, a, 1, st);
     }
 }
 
@@ -243,8 +256,10 @@ void convT_fwd(const float* x, int64_t ldx, int cin, const float* wf, const floa
     a.A = x; a.lda = ldx; a.a_coff = 0;
     a.Bm = wf; a.ldb = cin;
     a.C = y; a.ldc = ldy; a.c_coff = ycoff; a.bias = bias;
-    a.kstages_per_split = cdiv(a.K, BK);
-    launch_cfg<KConvTFwd>(pick_cfg(a.M, a.N), a, 1, st);
+    const Cfg c = pick_cfg(a.M, a.N);
+    const int kb = kb_for(K_TFWD, c);
+    a.kstages_per_split = cdiv(a.K, kb);
+    launch_cfg<KConvTFwd>(c, kb, a, 1, st);
 }
 
 void conv3x3_dgrad(const float* dz, int cout, const float* wd, int cin, float* dx, int64_t lddx,
@@ -255,8 +270,10 @@ void conv3x3_dgrad(const float* dz, int cout, const float* wd, int cin, float* d
     a.A = dz; a.lda = cout; a.a_coff = 0; a.a_cin = cout;
     a.Bm = wd; a.ldb = 9 * cout;
     a.C = dx; a.ldc = lddx; a.c_coff = 0;
-    a.kstages_per_split = cdiv(a.K, BK);
-    launch_cfg<KConvFwd>(pick_cfg(a.M, a.N), a, 1, st);
+    const Cfg c = pick_cfg(a.M, a.N);
+    const int kb = kb_for(K_FWD, c);
+    a.kstages_per_split = cdiv(a.K, kb);
+    launch_cfg<KConvFwd>(c, kb, a, 1, st);
 }
 
 void convT_dgrad(const float* g, int64_t ldg, int gcoff, int cout, const float* wm, int cin, float* dx,
@@ -267,15 +284,17 @@ void convT_dgrad(const float* g, int64_t ldg, int gcoff, int cout, const float* 
     a.A = g; a.lda = ldg; a.a_coff = gcoff; a.a_cin = cout;
     a.Bm = wm; a.ldb = 4 * cout;
     a.C = dx; a.ldc = cin; a.c_coff = 0;
-    a.kstages_per_split = cdiv(a.K, BK);
-    launch_cfg<KConvTDgrad>(pick_cfg(a.M, a.N), a, 1, st);
+    const Cfg c = pick_cfg(a.M, a.N);
+    const int kb = kb_for(K_TDGRAD, c);
+    a.kstages_per_split = cdiv(a.K, kb);
+    launch_cfg<KConvTDgrad>(c, kb, a, 1, st);
 }
 
 int64_t wgrad_slab_floats(int M, int N, int Kpix) {
     GemmArgs a{};
     a.M = M; a.N = N; a.K = Kpix;
-    Cfg c = pick_cfg(M, N);
-    return (int64_t)plan_splits(a, c, 0) * M * N;
+    const Cfg c = pick_cfg(M, N);
+    return (int64_t)plan_splits(a, c, 16, 0) * M * N;   // kb 16: the larger split count
 }
 
 static void finish_slabs(float* slab, int splits, int64_t per, float* dw, hipStream_t st) {
@@ -291,14 +310,15 @@ void conv3x3_wgrad(const float* dz, int cout, const float* x, int64_t ldx, int x
     a.A = dz; a.lda = cout; a.a_coff = 0;
     a.Bm = x; a.ldb = ldx; a.b_coff = xcoff; a.b_cin = cin;
     a.b_sc = x_scale; a.b_sh = x_shift;
-    Cfg c = pick_cfg(a.M, a.N);
-    int s = plan_splits(a, c, slab_cap);
-    a.kstages_per_split = cdiv(cdiv(a.K, BK), s);
-    s = cdiv(cdiv(a.K, BK), a.kstages_per_split);
+    const Cfg c = pick_cfg(a.M, a.N);
+    const int kb = kb_for(K_WGRAD, c);
+    int s = plan_splits(a, c, kb, slab_cap);
+    a.kstages_per_split = cdiv(cdiv(a.K, kb), s);
+    s = cdiv(cdiv(a.K, kb), a.kstages_per_split);
     const int64_t per = (int64_t)a.M * a.N;
     a.ldc = a.N; a.slab_stride = per;
     a.C = s == 1 ? dw : slab;
-    if (x_scale) launch_cfg<KConvWgradBN>(c, a, s, st); else launch_cfg<KConvWgrad>(c, a, s, st);
+    if (x_scale) launch_cfg<KConvWgradBN>(c, kb, a, s, st); else launch_cfg<KConvWgrad>(c, kb, a, s, st);
     if (s > 1) finish_slabs(slab, s, per, dw, st);
 }
 
@@ -309,14 +329,15 @@ void convT_wgrad(const float* x, int cin, const float* g, int64_t ldg, int gcoff
     a.B = B; a.H = H; a.W = W;
     a.A = x; a.lda = cin; a.a_coff = 0;
     a.Bm = g; a.ldb = ldg; a.b_coff = gcoff; a.b_cin = cout;
-    Cfg c = pick_cfg(a.M, a.N);
-    int s = plan_splits(a, c, slab_cap);
-    a.kstages_per_split = cdiv(cdiv(a.K, BK), s);
-    s = cdiv(cdiv(a.K, BK), a.kstages_per_split);
+    const Cfg c = pick_cfg(a.M, a.N);
+    const int kb = kb_for(K_TWGRAD, c);
+    int s = plan_splits(a, c, kb, slab_cap);
+    a.kstages_per_split = cdiv(cdiv(a.K, kb), s);
+    s = cdiv(cdiv(a.K, kb), a.kstages_per_split);
     const int64_t per = (int64_t)a.M * a.N;
     a.ldc = a.N; a.slab_stride = per;
     a.C = s == 1 ? dw : slab;
-    launch_cfg<KConvTWgrad>(c, a, s, st);
+    launch_cfg<KConvTWgrad>(c, kb, a, s, st);
     if (s > 1) finish_slabs(slab, s, per, dw, st);
 }
 

@@ -11,14 +11,15 @@
 // row stride/channel offset so the decoder concat buffer is written/read in place).
 //
 // Tile: 4 waves (256 threads) = WM x WN waves, each wave owns 64x64 = 2x2 blocks of
-// v_mfma_f32_32x32x2_f32 (exact fp32 fmaf chains, 64 FLOP/clk/SIMD = the fp32 peak). BK = 16.
+// v_mfma_f32_32x32x2_f32 (exact fp32 fmaf chains, 64 FLOP/clk/SIMD = the fp32 peak). The K-stage
+// depth KB (16 or 32) is a template parameter chosen per tile shape by the host launchers.
 // Operand staging is register-staged double-buffered LDS, one barrier per K-stage.
-//   "Kc"  operands (global rows are contiguous along k): LDS image [rows][BK+4] (row stride 80 B:
-//         16 consecutive rows hit 16 distinct 16-B bank slots -> conflict-free ds_read_b128).
+//   "Kc"  operands (global rows are contiguous along k): LDS image [rows][KB+4] (row stride 80 B /
+//         144 B: consecutive rows hit distinct 16-B bank slots -> conflict-free ds_read_b128).
 //   "MNc" operands (global rows are contiguous along m/n, k = pixel is strided): LDS image
-//         [BK][rows] read with one ds_read_b32 per MFMA step (32 consecutive lanes, no conflict).
+//         [KB][rows] read with one ds_read_b32 per MFMA step (32 consecutive lanes, no conflict).
 // K order inside a stage is permuted so a lane's 8 k-values are contiguous: MFMA step s, lane half h
-// consumes chunk-k = 8h + s (both operands use the same map, so the sum is unchanged).
+// consumes chunk-k = (KB/2)h + s (both operands use the same map, so the sum is unchanged).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -29,20 +30,19 @@ namespace cad {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-#ifndef CAD_BK
-#define CAD_BK 16
-#endif
 #ifndef CAD_XCD_SWIZZLE
 #define CAD_XCD_SWIZZLE 0
 #endif
-#ifndef CAD_PREFETCH2
-#define CAD_PREFETCH2 0
-#endif
-constexpr int BK = CAD_BK;            // K-stage depth (16 or 32)
-constexpr int LDK = BK + 4;           // Kc LDS row stride (floats): 80 B / 144 B rows, conflict-free b128
-constexpr int KC_TPR = BK / 4;        // threads per Kc row (one float4 each)
-constexpr int KC_RPP = 256 / KC_TPR;  // Kc rows staged per pass of the workgroup
-constexpr int HK = BK / 2;            // MFMA steps per stage = k values per lane half
+// K-stage geometry for stage depth KB (16 or 32)
+template <int KB>
+struct KS {
+    static_assert(KB == 16 || KB == 32, "K-stage depth");
+    static constexpr int BK = KB;
+    static constexpr int LDK = KB + 4;        // Kc LDS row stride (floats), conflict-free b128
+    static constexpr int TPR = KB / 4;        // threads per Kc row (one float4 each)
+    static constexpr int RPP = 256 / TPR;     // Kc rows staged per pass of the workgroup
+    static constexpr int HK = KB / 2;         // MFMA steps per stage = k values per lane half
+};
 
 struct GemmArgs {
     int M, N, K;          // GEMM extents
@@ -72,38 +72,40 @@ __device__ __forceinline__ float4 bn_relu4(float4 v, float4 s, float4 h) {
 // Kc loaders: operand(row r, k) with k contiguous in memory.  Thread t owns rows t/4 + 64j and
 // the float4 column group (t&3)*4 of every stage.
 // --------------------------------------------------------------------------------------------
-template <int ROWS>
+template <int ROWS, int KB>
 struct KcDense {   // op(r,k) = P[r*ld + coff + k], r < nrows, k < K
-    static constexpr int NV = ROWS / KC_RPP;
+    using G = KS<KB>;
+    static constexpr int NV = ROWS / G::RPP;
     const float* p[NV];
     bool ok[NV];
     int K, k;
     __device__ void init(const float* P, int64_t ld, int coff, int nrows, int K_, int row0, int tid, int kbeg) {
         K = K_;
-        k = kbeg * BK;
+        k = kbeg * KB;
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
-            int r = row0 + tid / KC_TPR + KC_RPP * j;
+            int r = row0 + tid / G::TPR + G::RPP * j;
             ok[j] = r < nrows;
-            p[j] = P + (int64_t)(ok[j] ? r : 0) * ld + coff + (tid % KC_TPR) * 4;
+            p[j] = P + (int64_t)(ok[j] ? r : 0) * ld + coff + (tid % G::TPR) * 4;
         }
     }
     __device__ void load(float4 (&v)[NV]) {
-        bool kin = (k + ((threadIdx.x % KC_TPR) * 4)) < K;
+        bool kin = (k + ((threadIdx.x % G::TPR) * 4)) < K;
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             bool g = ok[j] && kin;
             float4 t = *reinterpret_cast<const float4*>(g ? p[j] + k : p[j]);
             v[j] = g ? t : f4zero();
         }
-        k += BK;
+        k += KB;
     }
     __device__ void finish(float4 (&)[NV]) {}
 };
 
-// (tap, ci) of a thread's float4 column, carried incrementally across K-stages of BK
+// (tap, ci) of a thread's float4 column, carried incrementally across K-stages of KB
+template <int KB>
 __device__ __forceinline__ void tapci_advance(int& tap, int& ci, int cin) {
-    ci += BK;
+    ci += KB;
     while (ci >= cin) { ci -= cin; ++tap; }
 }
 
@@ -114,9 +116,10 @@ __device__ __forceinline__ void tapci_advance(int& tap, int& ci, int cin) {
 //
 // Loader protocol: load(v) issues the next stage's global loads into registers; finish(v) (called
 // right before the LDS store) completes any register-side transform.
-template <int ROWS, bool BNR = false>
+template <int ROWS, int KB, bool BNR = false>
 struct KcIm2col3x3 {
-    static constexpr int NV = ROWS / KC_RPP;
+    using G = KS<KB>;
+    static constexpr int NV = ROWS / G::RPP;
     const float* base;
     const float *sc, *sh;
     float4 s4, h4;     // BNR: coefficients of the loaded stage
@@ -130,14 +133,14 @@ struct KcIm2col3x3 {
                          int row0, int tid, int kbeg, const float* sc_ = nullptr, const float* sh_ = nullptr) {
         H = H_; W = W_; cin = cin_; ld = ld_;
         sc = sc_; sh = sh_;
-        base = P + coff;   // the float4 column (tid&3)*4 is folded into ci
-        const int k = kbeg * BK + (tid % KC_TPR) * 4;
+        base = P + coff;   // the thread's float4 column is folded into ci
+        const int k = kbeg * KB + (tid % G::TPR) * 4;
         tap = k / cin;
         ci = k - tap * cin;
         int M = B * H * W;
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
-            int r = row0 + tid / KC_TPR + KC_RPP * j;
+            int r = row0 + tid / G::TPR + G::RPP * j;
             ok[j] = r < M;
             int rr = ok[j] ? r : 0;
             x[j] = rr % W;
@@ -163,7 +166,7 @@ struct KcIm2col3x3 {
             if constexpr (BNR) gm[j] = g;
             v[j] = g ? tv : f4zero();
         }
-        tapci_advance(tap, ci, cin);
+        tapci_advance<KB>(tap, ci, cin);
     }
     __device__ void finish(float4 (&v)[NV]) {
         if constexpr (BNR) {
@@ -174,9 +177,10 @@ struct KcIm2col3x3 {
 };
 
 // op(lowres pix (b,y,x), k=(q=(dy,dx), co)) = G[(b, 2y+dy, 2x+dx)*ld + coff + co]
-template <int ROWS>
+template <int ROWS, int KB>
 struct KcUpGather {
-    static constexpr int NV = ROWS / KC_RPP;
+    using G = KS<KB>;
+    static constexpr int NV = ROWS / G::RPP;
     const float* base;
     int64_t ld;
     int64_t hrpix[NV];   // high-res pixel index of (2y, 2x)
@@ -185,14 +189,14 @@ struct KcUpGather {
     __device__ void init(const float* P, int64_t ld_, int coff, int cout_, int B, int H, int W,
                          int row0, int tid, int kbeg) {
         ld = ld_; cout = cout_; W2 = 2 * W;
-        base = P + coff;   // the float4 column (tid&3)*4 is folded into co
-        const int k = kbeg * BK + (tid % KC_TPR) * 4;
+        base = P + coff;   // the thread's float4 column is folded into co
+        const int k = kbeg * KB + (tid % G::TPR) * 4;
         q = k / cout;
         co = k - q * cout;
         int M = B * H * W;
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
-            int r = row0 + tid / KC_TPR + KC_RPP * j;
+            int r = row0 + tid / G::TPR + G::RPP * j;
             ok[j] = r < M;
             int rr = ok[j] ? r : 0;
             int xx = rr % W, t = rr / W, yy = t % H, b = t / H;
@@ -210,7 +214,7 @@ struct KcUpGather {
             float4 t = *reinterpret_cast<const float4*>(p);
             v[j] = g ? t : f4zero();
         }
-        tapci_advance(q, co, cout);
+        tapci_advance<KB>(q, co, cout);
     }
     __device__ void finish(float4 (&)[NV]) {}
 };
@@ -219,26 +223,27 @@ struct KcUpGather {
 // MNc loaders: operand(row r, k=pixel); memory rows are pixels, contiguous along r.
 // Thread t owns row group cg = t % (ROWS/4) (4 rows) and k-rows t/(ROWS/4) + KSTEP*j.
 // --------------------------------------------------------------------------------------------
-template <int ROWS>
+template <int ROWS, int KB>
 struct MNcBase {
     static constexpr int TPR = ROWS / 4;          // threads per k-row
     static constexpr int KSTEP = 256 / TPR;       // k-rows per pass
-    static constexpr int NV = BK / KSTEP;
+    static constexpr int NV = KB / KSTEP;
 };
 
-// The MNc loaders walk pixels: each thread's k-rows advance by BK pixels per stage, so (x, y) is
-// carried incrementally (one compare-subtract per stage for W >= BK) instead of dividing per stage.
+// The MNc loaders walk pixels: each thread's k-rows advance by KB pixels per stage, so (x, y) is
+// carried incrementally (one compare-subtract per stage for W >= KB) instead of dividing per stage.
+template <int KB>
 __device__ __forceinline__ void px_advance(int& x, int& y, int& b, int W, int H) {
-    x += BK;
+    x += KB;
     while (x >= W) {
         x -= W;
         if (++y == H) { y = 0; ++b; }
     }
 }
 
-template <int ROWS>
-struct MNcDense : MNcBase<ROWS> {   // op(r, k) = P[k*ld + coff + r], r < nrows, k < Kp
-    using Base = MNcBase<ROWS>;
+template <int ROWS, int KB>
+struct MNcDense : MNcBase<ROWS, KB> {   // op(r, k) = P[k*ld + coff + r], r < nrows, k < Kp
+    using Base = MNcBase<ROWS, KB>;
     static constexpr int NV = Base::NV;
     const float* p;
     int64_t ld;
@@ -249,7 +254,7 @@ struct MNcDense : MNcBase<ROWS> {   // op(r, k) = P[k*ld + coff + r], r < nrows,
         int r = row0 + (tid % Base::TPR) * 4;
         rok = r < nrows;   // nrows % 4 == 0 is required
         p = P + coff + (rok ? r : 0);
-        k0 = kbeg * BK + tid / Base::TPR;
+        k0 = kbeg * KB + tid / Base::TPR;
     }
     __device__ void load(float4 (&v)[NV]) {
 #pragma unroll
@@ -259,15 +264,15 @@ struct MNcDense : MNcBase<ROWS> {   // op(r, k) = P[k*ld + coff + r], r < nrows,
             float4 t = *reinterpret_cast<const float4*>(p + (int64_t)(g ? k : 0) * ld);
             v[j] = g ? t : f4zero();
         }
-        k0 += BK;
+        k0 += KB;
     }
     __device__ void finish(float4 (&)[NV]) {}
 };
 
 // op(j=(tap,ci), k=pix) = X[(b,y+ky-1,x+kx-1)*ld + coff + ci]   (BNR: relu(x*sc+sh) in-image)
-template <int ROWS, bool BNR = false>
-struct MNcIm2col3x3 : MNcBase<ROWS> {
-    using Base = MNcBase<ROWS>;
+template <int ROWS, int KB, bool BNR = false>
+struct MNcIm2col3x3 : MNcBase<ROWS, KB> {
+    using Base = MNcBase<ROWS, KB>;
     static constexpr int NV = Base::NV;
     const float* p;
     float4 s4, h4;
@@ -291,7 +296,7 @@ struct MNcIm2col3x3 : MNcBase<ROWS> {
         }
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
-            k[i] = kbeg * BK + tid / Base::TPR + Base::KSTEP * i;
+            k[i] = kbeg * KB + tid / Base::TPR + Base::KSTEP * i;
             int kk = k[i] < Kp ? k[i] : 0;
             x[i] = kk % W;
             y[i] = (kk / W) % H;
@@ -307,8 +312,8 @@ struct MNcIm2col3x3 : MNcBase<ROWS> {
             if constexpr (BNR) gm[j] = g;
             v[j] = g ? t : f4zero();
             int b = 0;
-            px_advance(x[j], y[j], b, W, H);
-            k[j] += BK;
+            px_advance<KB>(x[j], y[j], b, W, H);
+            k[j] += KB;
         }
     }
     __device__ void finish(float4 (&v)[NV]) {
@@ -320,9 +325,9 @@ struct MNcIm2col3x3 : MNcBase<ROWS> {
 };
 
 // op(j=(q,co), k=lowres pix (b,y,x)) = G[(b,2y+dy,2x+dx)*ld + coff + co]
-template <int ROWS>
-struct MNcUpGather : MNcBase<ROWS> {
-    using Base = MNcBase<ROWS>;
+template <int ROWS, int KB>
+struct MNcUpGather : MNcBase<ROWS, KB> {
+    using Base = MNcBase<ROWS, KB>;
     static constexpr int NV = Base::NV;
     const float* p;
     int64_t ld;
@@ -340,7 +345,7 @@ struct MNcUpGather : MNcBase<ROWS> {
         p = P + coff + co;
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
-            k[i] = kbeg * BK + tid / Base::TPR + Base::KSTEP * i;
+            k[i] = kbeg * KB + tid / Base::TPR + Base::KSTEP * i;
             int kk = k[i] < Kp ? k[i] : 0;
             x[i] = kk % W;
             int t = kk / W;
@@ -355,8 +360,8 @@ struct MNcUpGather : MNcBase<ROWS> {
             const int64_t hp = g ? ((int64_t)b[j] * (2 * H) + 2 * y[j] + qy) * (2 * W) + 2 * x[j] + qx : 0;
             float4 t4 = *reinterpret_cast<const float4*>(p + hp * ld);
             v[j] = g ? t4 : f4zero();
-            px_advance(x[j], y[j], b[j], W, H);
-            k[j] += BK;
+            px_advance<KB>(x[j], y[j], b[j], W, H);
+            k[j] += KB;
         }
     }
     __device__ void finish(float4 (&)[NV]) {}
@@ -365,15 +370,16 @@ struct MNcUpGather : MNcBase<ROWS> {
 // --------------------------------------------------------------------------------------------
 // LDS staging + fragment reads
 // --------------------------------------------------------------------------------------------
-template <int ROWS, int NV>
+template <int ROWS, int KB, int NV>
 __device__ __forceinline__ void kc_store(float* s, const float4 (&v)[NV]) {
+    using G = KS<KB>;
     const int t = threadIdx.x;
 #pragma unroll
     for (int j = 0; j < NV; ++j)
-        *reinterpret_cast<float4*>(s + (t / KC_TPR + KC_RPP * j) * LDK + (t % KC_TPR) * 4) = v[j];
+        *reinterpret_cast<float4*>(s + (t / G::TPR + G::RPP * j) * G::LDK + (t % G::TPR) * 4) = v[j];
 }
-template <int ROWS, int NV>
-__device__ __forceinline__ void mnc_store(float* s, const float4 (&v)[NV]) {
+template <int ROWS, int KB, int NV>
+__device__ __forceinline__ void mnc_store(float* s, const float4 (&v)[NV]) {   // KB: same signature as kc_store
     constexpr int TPR = ROWS / 4, KSTEP = 256 / TPR;
     const int t = threadIdx.x;
 #pragma unroll
@@ -381,26 +387,29 @@ __device__ __forceinline__ void mnc_store(float* s, const float4 (&v)[NV]) {
         *reinterpret_cast<float4*>(s + (t / TPR + KSTEP * j) * ROWS + (t % TPR) * 4) = v[j];
 }
 // fragment: HK consecutive chunk-k values of row (rb + lane&31), half h = lane>>5
-__device__ __forceinline__ void kc_frag(const float* s, int rb, float (&f)[HK]) {
+template <int KB>
+__device__ __forceinline__ void kc_frag(const float* s, int rb, float (&f)[KS<KB>::HK]) {
+    using G = KS<KB>;
     const int lane = threadIdx.x & 63;
-    const float* q = s + (rb + (lane & 31)) * LDK + (lane >> 5) * HK;
+    const float* q = s + (rb + (lane & 31)) * G::LDK + (lane >> 5) * G::HK;
 #pragma unroll
-    for (int i = 0; i < HK; i += 4) {
+    for (int i = 0; i < G::HK; i += 4) {
         float4 a = *reinterpret_cast<const float4*>(q + i);
         f[i] = a.x; f[i + 1] = a.y; f[i + 2] = a.z; f[i + 3] = a.w;
     }
 }
-template <int ROWS>
-__device__ __forceinline__ void mnc_frag(const float* s, int rb, float (&f)[HK]) {
+template <int ROWS, int KB>
+__device__ __forceinline__ void mnc_frag(const float* s, int rb, float (&f)[KS<KB>::HK]) {
+    using G = KS<KB>;
     const int lane = threadIdx.x & 63;
-    const float* q = s + (lane >> 5) * HK * ROWS + rb + (lane & 31);
+    const float* q = s + (lane >> 5) * G::HK * ROWS + rb + (lane & 31);
 #pragma unroll
-    for (int i = 0; i < HK; ++i) f[i] = q[i * ROWS];
+    for (int i = 0; i < G::HK; ++i) f[i] = q[i * ROWS];
 }
 
-template <bool KC, int ROWS>
+template <bool KC, int ROWS, int KB>
 struct OpLds {
-    static constexpr int FLOATS = KC ? ROWS * LDK : BK * ROWS;
+    static constexpr int FLOATS = KC ? ROWS * KS<KB>::LDK : KB * ROWS;
 };
 
 // --------------------------------------------------------------------------------------------
@@ -437,10 +446,11 @@ __device__ __forceinline__ TileId xcd_tile() {
     return t;
 }
 
-template <int WM, int WN, class LA, bool KCA, class LB, bool KCB, class Epi, class InitA, class InitB>
+template <int WM, int WN, int KB, class LA, bool KCA, class LB, bool KCB, class Epi, class InitA, class InitB>
 __device__ __forceinline__ void gemm_body(const GemmArgs& a, InitA init_a, InitB init_b, Epi epi) {
+    using G = KS<KB>;
     constexpr int BM = 64 * WM, BN = 64 * WN;
-    constexpr int SA = OpLds<KCA, BM>::FLOATS, SB = OpLds<KCB, BN>::FLOATS;
+    constexpr int SA = OpLds<KCA, BM, KB>::FLOATS, SB = OpLds<KCB, BN, KB>::FLOATS;
     __shared__ __attribute__((aligned(16))) float lds[2 * (SA + SB)];
 
     const int tid = threadIdx.x;
@@ -449,7 +459,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, InitA init_a, InitB
     const TileId tile = xcd_tile();
     const int m0 = tile.x * BM, n0 = tile.y * BN;
 
-    const int nk_total = (a.K + BK - 1) / BK;
+    const int nk_total = (a.K + KB - 1) / KB;
     const int kbeg = tile.z * a.kstages_per_split;
     const int kend = min(nk_total, kbeg + a.kstages_per_split);
 
@@ -469,20 +479,20 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, InitA init_a, InitB
         la.finish(xa);
         lb.finish(xb);
         float* da = lds + buf * (SA + SB);
-        if constexpr (KCA) kc_store<BM>(da, xa); else mnc_store<BM>(da, xa);
-        if constexpr (KCB) kc_store<BN>(da + SA, xb); else mnc_store<BN>(da + SA, xb);
+        if constexpr (KCA) kc_store<BM, KB>(da, xa); else mnc_store<BM, KB>(da, xa);
+        if constexpr (KCB) kc_store<BN, KB>(da + SA, xb); else mnc_store<BN, KB>(da + SA, xb);
     };
     auto stage_compute = [&](int buf) {
         const float* sa = lds + buf * (SA + SB);
         const float* sb = sa + SA;
-        float fa[2][HK], fb[2][HK];
+        float fa[2][G::HK], fb[2][G::HK];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            if constexpr (KCA) kc_frag(sa, wm * 64 + i * 32, fa[i]); else mnc_frag<BM>(sa, wm * 64 + i * 32, fa[i]);
-            if constexpr (KCB) kc_frag(sb, wn * 64 + i * 32, fb[i]); else mnc_frag<BN>(sb, wn * 64 + i * 32, fb[i]);
+            if constexpr (KCA) kc_frag<KB>(sa, wm * 64 + i * 32, fa[i]); else mnc_frag<BM, KB>(sa, wm * 64 + i * 32, fa[i]);
+            if constexpr (KCB) kc_frag<KB>(sb, wn * 64 + i * 32, fb[i]); else mnc_frag<BN, KB>(sb, wn * 64 + i * 32, fb[i]);
         }
 #pragma unroll
-        for (int s = 0; s < HK; ++s)
+        for (int s = 0; s < G::HK; ++s)
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -490,30 +500,6 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, InitA init_a, InitB
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
     };
 
-#if CAD_PREFETCH2
-    // Global loads run two K-stages ahead of the MFMAs (two register sets, loop unrolled x2 so every
-    // register index is static): a stage's operands have two stage-times to arrive before the LDS write.
-    float4 ra0[LA::NV], rb0[LB::NV], ra1[LA::NV], rb1[LB::NV];
-    if (kbeg < kend) {
-        la.load(ra0);
-        lb.load(rb0);
-        stage_store(0, ra0, rb0);
-    }
-    if (kbeg + 1 < kend) { la.load(ra0); lb.load(rb0); }
-    __syncthreads();
-    for (int kt = kbeg; kt < kend;) {
-        if (kt + 2 < kend) { la.load(ra1); lb.load(rb1); }
-        stage_compute(0);
-        if (kt + 1 < kend) stage_store(1, ra0, rb0);
-        __syncthreads();
-        if (++kt >= kend) break;
-        if (kt + 2 < kend) { la.load(ra0); lb.load(rb0); }
-        stage_compute(1);
-        if (kt + 1 < kend) stage_store(0, ra1, rb1);
-        __syncthreads();
-        ++kt;
-    }
-#else
     float4 ra[LA::NV], rb[LB::NV];
     if (kbeg < kend) {
         la.load(ra);
@@ -530,7 +516,6 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, InitA init_a, InitB
         __syncthreads();
         cur ^= 1;
     }
-#endif
 
     // epilogue: element (m, n) of sub-block (i, j), register r.  With STATS the per-column BN
     // partials are accumulated in the same pass (each accumulator is read once: keeping them live

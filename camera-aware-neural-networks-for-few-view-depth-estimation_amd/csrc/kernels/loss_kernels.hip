@@ -199,15 +199,18 @@ __device__ __forceinline__ float edge_wy(const float* img, int64_t HW, int64_t i
     return expf(-((d0 + d1 + d2) / 3.f));
 }
 
-// dL_smooth/dn at pixel i of sample plane (pp = pred plane, img = rgb of the sample)
+// dL_smooth/dn at pixel i of sample plane (pp = pred plane, img = rgb of the sample).  n = p / denom
+// by true division, as the reference computes it (depth_loss.h:193): the sign of a difference of
+// neighbouring n must come out as the reference's, and a rounded reciprocal can merge neighbours
+// that differ by an ulp (sign 0 instead of +-1).
 __device__ __forceinline__ float smooth_gn(const float* pp, const float* img, int64_t HW, int W, int H,
-                                           int x, int y, int64_t i, float inv_m, const SmoothCtx& c) {
-    const float n0 = pp[i] * inv_m;
+                                           int x, int y, int64_t i, float denom, const SmoothCtx& c) {
+    const float n0 = pp[i] / denom;
     float gx = 0.f, gy = 0.f;
-    if (x > 0) gx += sgnf(n0 - pp[i - 1] * inv_m) * edge_wx(img, HW, i - 1);
-    if (x + 1 < W) gx -= sgnf(pp[i + 1] * inv_m - n0) * edge_wx(img, HW, i);
-    if (y > 0) gy += sgnf(n0 - pp[i - W] * inv_m) * edge_wy(img, HW, i - W, W);
-    if (y + 1 < H) gy -= sgnf(pp[i + W] * inv_m - n0) * edge_wy(img, HW, i, W);
+    if (x > 0) gx += sgnf(n0 - pp[i - 1] / denom) * edge_wx(img, HW, i - 1);
+    if (x + 1 < W) gx -= sgnf(pp[i + 1] / denom - n0) * edge_wx(img, HW, i);
+    if (y > 0) gy += sgnf(n0 - pp[i - W] / denom) * edge_wy(img, HW, i - W, W);
+    if (y + 1 < H) gy -= sgnf(pp[i + W] / denom - n0) * edge_wy(img, HW, i, W);
     return gx * c.inv_nx + gy * c.inv_ny;
 }
 
@@ -227,7 +230,7 @@ __global__ __launch_bounds__(kTPB) void k_smooth(const float* __restrict__ pred,
         const float n0 = pp[i] / denom;
         if (x + 1 < g.W) v[0] += fabsf(pp[i + 1] / denom - n0) * edge_wx(img, HW, i);
         if (y + 1 < g.H) v[1] += fabsf(pp[i + g.W] / denom - n0) * edge_wy(img, HW, i, g.W);
-        v[2] += (double)smooth_gn(pp, img, HW, g.W, g.H, x, y, i, 1.f / denom, c) * pp[i];
+        v[2] += (double)smooth_gn(pp, img, HW, g.W, g.H, x, y, i, denom, c) * pp[i];
     }
     block_sum<3>(v, red);
     if (threadIdx.x == 0)
@@ -332,7 +335,7 @@ __global__ void k_dpred(const float* __restrict__ pred, const float* __restrict_
             const float mean = (float)(dsc[S_PB + b] / (double)HW);
             const float denom = mean + kEps;
             const float gn = smooth_gn(pred + (int64_t)b * HW, rgb + (int64_t)b * 3 * HW, HW, g.W, g.H, x, y, pi,
-                                       1.f / denom, c);
+                                       denom, c);
             const float Sb = (float)dsc[S_PB + g.B + b];
             grad += w2 * (gn / denom - Sb / (denom * denom * (float)HW));
         }
