@@ -5,6 +5,10 @@
                                    passes, corrected as MI355X_MICROARCH.md §HBM prescribes:
                                    FETCH_SIZE (KB) reads half the bytes of 16-B/lane streaming loads
                                    on gfx950 -> x2; WRITE_SIZE (KB) exact for 16-B stores.
+  profiles/<tag>_sq_counters.md    per-kernel clock under load (GRBM_GUI_ACTIVE / 8 XCDs / duration),
+                                   MFMA busy fraction (SQ_VALU_MFMA_BUSY_CYCLES over 1024 SIMDs x
+                                   active cycles) and the wave-cycle breakdown (SQ_WAIT_ANY parked,
+                                   SQ_WAIT_INST_ANY issue-stalled, SQ_ACTIVE_INST_ANY issuing).
 """
 import csv
 import glob
@@ -31,14 +35,58 @@ def pmc(d, counter):
     return vals
 
 
+def durations(d):
+    """Kernel_Name -> list of durations (ns) from a pass's kernel trace, if it wrote one."""
+    path = find(d, "*kernel_trace.csv")
+    out = defaultdict(list)
+    if not path:
+        return out
+    with open(path) as fh:
+        for row in csv.DictReader(fh):
+            out[row["Kernel_Name"]].append(float(row["End_Timestamp"]) - float(row["Start_Timestamp"]))
+    return out
+
+
+def sq_table(d, tag, here, avg_ns):
+    names = ["SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
+             "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_LDS", "SQ_WAIT_INST_LDS", "GRBM_GUI_ACTIVE", "GRBM_COUNT"]
+    c = {n: pmc(d, n) for n in names}
+    ks = set(c["GRBM_GUI_ACTIVE"])
+    if not ks:
+        return
+    rows = []
+    for k in ks:
+        avg = {n: (sum(v) / len(v) if v else 0.0) for n, v in ((n, c[n].get(k, [])) for n in names)}
+        dur = avg_ns.get(k)
+        clk = avg["GRBM_GUI_ACTIVE"] / 8.0 / dur if dur else float("nan")   # GHz (cycles per ns)
+        active = avg["GRBM_GUI_ACTIVE"] / 8.0
+        mfma = avg["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * active) if active else 0.0
+        wc = avg["SQ_WAVE_CYCLES"] or 1.0
+        rows.append((dur or 0.0, k, clk, mfma, avg["SQ_WAIT_ANY"] / wc, avg["SQ_WAIT_INST_ANY"] / wc,
+                     avg["SQ_ACTIVE_INST_ANY"] / wc, avg["SQ_WAIT_INST_LDS"] / wc))
+    rows.sort(key=lambda r: -r[0])
+    lines = [f"# rocprofv3 SQ/GRBM pass: bench.py --steps 1 --warmup 0 ({tag})\n",
+             "clock = GRBM_GUI_ACTIVE / 8 / avg duration (kernel-trace pass); MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES /",
+             "(1024 SIMDs x GRBM_GUI_ACTIVE/8); wave-cycle shares: parked (SQ_WAIT_ANY), issue-stalled",
+             "(SQ_WAIT_INST_ANY, of which LDS SQ_WAIT_INST_LDS), issuing (SQ_ACTIVE_INST_ANY).\n",
+             "| kernel | avg us | clock GHz | MFMA busy | parked | stalled | issuing | LDS-stall |",
+             "|---|---|---|---|---|---|---|---|"]
+    for dur, k, clk, mfma, wa, wi, ac, wl in rows[:30]:
+        lines.append(f"| `{k[:100]}` | {dur / 1e3:.1f} | {clk:.2f} | {mfma:.3f} | {wa:.2f} | {wi:.2f} | {ac:.2f} | {wl:.2f} |")
+    with open(os.path.join(here, f"{tag}_sq_counters.md"), "w") as fh:
+        fh.write("\n".join(lines) + "\n")
+
+
 def main():
     out, tag = sys.argv[1], sys.argv[2]
     here = os.path.dirname(os.path.abspath(__file__))
     stats = find(os.path.join(out, "trace"), "*kernel_stats.csv")
     lines = []
+    avg_ns = {}
     if stats:
         with open(stats) as fh:
             rows = list(csv.DictReader(fh))
+        avg_ns = {r["Name"]: float(r["AverageNs"]) for r in rows}
         rows.sort(key=lambda r: -float(r["TotalDurationNs"]))
         tot = sum(float(r["TotalDurationNs"]) for r in rows)
         lines.append(f"# rocprofv3 --kernel-trace --stats: bench.py --steps 3 --warmup 1 ({tag})\n")
@@ -49,7 +97,8 @@ def main():
                          f"{float(r['AverageNs']) / 1e3:.1f} | {100 * float(r['TotalDurationNs']) / tot:.1f} |")
         with open(os.path.join(here, f"{tag}_kernel_stats.md"), "w") as fh:
             fh.write("\n".join(lines) + "\n")
-    for name in ("trace", "fetch", "write"):
+    sq_table(os.path.join(out, "sq"), tag, here, avg_ns)
+    for name in ("trace", "fetch", "write", "sq"):
         p = os.path.join(out, f"{name}.json")
         if os.path.exists(p) and os.path.getsize(p):
             with open(p) as fh:
