@@ -29,6 +29,11 @@ sys.path.insert(0, ROOT)
 
 METRIC = "images/sec (640×480 bs32) at 1/2/4/8 MI355X; abs_rel vs CPU ref"
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 = fp32 vector peak
+# S3 engine (gemm_s3.hpp): each fp32 multiply-add costs 6 bf16 products on v_mfma_f32_32x32x16_bf16
+# (1024 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz = 2516.6 TFLOP/s dense bf16), so its fp32-equivalent
+# ceiling is 2516.6 / 6.
+BF16_MFMA_PEAK_TFLOPS = 2516.6
+S3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6.0
 HBM_PEAK_GBS = 8000.0
 FLOP_PER_IMAGE_480x640_F64 = 1.353646e12   # fwd + dgrad + wgrad
 
@@ -186,8 +191,13 @@ def main():
         roof = None
         if dom:
             achieved = dom["gflop"] / dom["ms"]   # GFLOP/ms == TFLOP/s
-            roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": pmc_traffic(dom["name"]),
+            s3 = "_s3<" in dom["name"]
+            peak = S3_PEAK_TFLOPS if s3 else FP32_MFMA_PEAK_TFLOPS
+            roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": round(peak, 1), "unit": "TFLOP/s",
+                    "frac": round(achieved / peak, 4), "traffic": pmc_traffic(dom["name"]),
+                    "arith": ("fp32 via exact 3-way bf16 split, 6 bf16 MFMA products per fp32 MAC: peak = dense "
+                              "bf16 MFMA 2516.6 / 6; achieved counts algorithmic fp32 FLOPs") if s3 else
+                             "fp32 MFMA (v_mfma_f32_32x32x2_f32)",
                     "kernel": dom["name"], "launches_per_step": dom["launches"] // args.steps,
                     "avg_launch_ms": round(dom["ms"] / dom["launches"], 4),
                     "gflop_per_launch": round(dom["gflop"] / dom["launches"], 3)}

@@ -43,6 +43,8 @@ SIGNATURES = {
     "cad_memcpy": (I, [P, P, I64, I, P]),
     "cad_adam_state": (I, [P, C.POINTER(P), C.POINTER(P)]),
     "cad_adam_set_step_count": (I, [P, I64]),
+    "cad_set_gemm_engine": (I, [I]),
+    "cad_get_gemm_engine": (I, []),
     "cad_unet_create": (I, [C.POINTER(UnetDesc), I, C.POINTER(P)]),
     "cad_unet_create_model": (I, [C.POINTER(UnetDesc), I, I, C.POINTER(P)]),
     "cad_unet_model": (I, [P]),

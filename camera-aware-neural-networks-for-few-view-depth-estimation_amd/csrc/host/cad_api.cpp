@@ -652,6 +652,13 @@ void default_init(cad_unet* h) {
 extern "C" {
 
 int cad_abi_version(void) { return CAD_ABI_VERSION; }
+cad_status cad_set_gemm_engine(int engine) {
+    return guard([&] {
+        require(engine == CAD_GEMM_F32 || engine == CAD_GEMM_S3, "unknown GEMM engine");
+        cad::set_gemm_engine(engine);
+    });
+}
+int cad_get_gemm_engine(void) { return cad::gemm_engine(); }
 const char* cad_last_error(void) { return g_err.c_str(); }
 
 cad_status cad_device_count(int* n) {

@@ -7,6 +7,7 @@
 #include <cstdlib>
 
 #include "gemm_mfma.hpp"
+#include "gemm_s3.hpp"
 #include "kernels.hpp"
 
 namespace cad {
@@ -111,6 +112,52 @@ __global__ __launch_bounds__(256) void k_convT_wgrad(GemmArgs a) {
         EpiSlab{});
 }
 
+// ---- S3 engine (gemm_s3.hpp): fp32 operands split exactly into 3 bf16 terms ----
+template <int WM, int WN, int KB, class Epi>
+__global__ __launch_bounds__(256) void k_conv3x3_fwd_s3(GemmArgs a) {
+    using LA = KcIm2col3x3<64 * WM, KB, false>;
+    using LB = KcDense<64 * WN, KB>;
+    gemm_body_s3<WM, WN, KB, LA, LB>(
+        a,
+        [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.a_cin, a.B, a.H, a.W, r0, t, kb); },
+        [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, Epi{});
+}
+template <int WM, int WN, int KB>
+__global__ __launch_bounds__(256) void k_convT_fwd_s3(GemmArgs a) {
+    using LA = KcDense<64 * WM, KB>;
+    using LB = KcDense<64 * WN, KB>;
+    gemm_body_s3<WM, WN, KB, LA, LB>(
+        a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t, kb); },
+        [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, EpiConvT{});
+}
+template <int WM, int WN, int KB>
+__global__ __launch_bounds__(256) void k_convT_dgrad_s3(GemmArgs a) {
+    using LA = KcUpGather<64 * WM, KB>;
+    using LB = KcDense<64 * WN, KB>;
+    gemm_body_s3<WM, WN, KB, LA, LB>(
+        a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.a_cin, a.B, a.H, a.W, r0, t, kb); },
+        [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, EpiStore{});
+}
+
+template <int WM, int WN, int KB>
+__global__ __launch_bounds__(256) void k_conv3x3_wgrad_s3(GemmArgs a) {
+    using LA = MNcDense<64 * WM, KB>;
+    using LB = MNcIm2col3x3<64 * WN, KB, false>;
+    gemm_body_s3m<WM, WN, KB, LA, LB>(
+        a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t, kb); },
+        [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.b_cin, a.B, a.H, a.W, r0, t, kb); },
+        EpiSlab{});
+}
+template <int WM, int WN, int KB>
+__global__ __launch_bounds__(256) void k_convT_wgrad_s3(GemmArgs a) {
+    using LA = MNcDense<64 * WM, KB>;
+    using LB = MNcUpGather<64 * WN, KB>;
+    gemm_body_s3m<WM, WN, KB, LA, LB>(
+        a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t, kb); },
+        [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.b_cin, a.B, a.H, a.W, r0, t, kb); },
+        EpiSlab{});
+}
+
 // deterministic split-K reduction: dst[e] = sum_z slab[z][e]
 __global__ void k_slab_reduce(const float* __restrict__ slab, int nsplit, int64_t stride,
                               float* __restrict__ dst, int64_t n) {
@@ -187,6 +234,14 @@ void launch_cfg(Cfg c, int kb, const GemmArgs& a, int splits, hipStream_t st) {
         case C14: launch_kb<KT, 1, 4>(kb, a, splits, st); break;
     }
 }
+template <template <int, int, int> class KT, int KB>
+void launch_cfg_kb(Cfg c, const GemmArgs& a, int splits, hipStream_t st) {
+    switch (c) {
+        case C41: launch_one<KT, 4, 1, KB>(a, splits, st); break;
+        case C22: launch_one<KT, 2, 2, KB>(a, splits, st); break;
+        case C14: launch_one<KT, 1, 4, KB>(a, splits, st); break;
+    }
+}
 // fmt = the symbol as rocprofv3 demangles it
 #define CAD_KT(NAME, EXPR, FMT)                                                  \
     template <int WM, int WN, int KB> struct NAME {                              \
@@ -206,7 +261,28 @@ CAD_KT(KConvWgradBN, (k_conv3x3_wgrad<WM, WN, KB, true>), "void cad::k_conv3x3_w
 CAD_KT(KConvTFwd, (k_convT_fwd<WM, WN, KB>), "void cad::k_convT_fwd<%d, %d, %d>(cad::GemmArgs)")
 CAD_KT(KConvTDgrad, (k_convT_dgrad<WM, WN, KB>), "void cad::k_convT_dgrad<%d, %d, %d>(cad::GemmArgs)")
 CAD_KT(KConvTWgrad, (k_convT_wgrad<WM, WN, KB>), "void cad::k_convT_wgrad<%d, %d, %d>(cad::GemmArgs)")
+CAD_KT(KConvFwd3, (k_conv3x3_fwd_s3<WM, WN, KB, EpiStore>), "void cad::k_conv3x3_fwd_s3<%d, %d, %d, cad::EpiStore>(cad::GemmArgs)")
+CAD_KT(KConvFwdS3, (k_conv3x3_fwd_s3<WM, WN, KB, EpiStoreStats>),
+       "void cad::k_conv3x3_fwd_s3<%d, %d, %d, cad::EpiStoreStats>(cad::GemmArgs)")
+CAD_KT(KConvTFwd3, (k_convT_fwd_s3<WM, WN, KB>), "void cad::k_convT_fwd_s3<%d, %d, %d>(cad::GemmArgs)")
+CAD_KT(KConvTDgrad3, (k_convT_dgrad_s3<WM, WN, KB>), "void cad::k_convT_dgrad_s3<%d, %d, %d>(cad::GemmArgs)")
+CAD_KT(KConvWgrad3, (k_conv3x3_wgrad_s3<WM, WN, KB>), "void cad::k_conv3x3_wgrad_s3<%d, %d, %d>(cad::GemmArgs)")
+CAD_KT(KConvTWgrad3, (k_convT_wgrad_s3<WM, WN, KB>), "void cad::k_convT_wgrad_s3<%d, %d, %d>(cad::GemmArgs)")
 #undef CAD_KT
+
+// GEMM engine for the k-contiguous (forward / dgrad) contractions: 0 = exact f32 MFMA,
+// 1 = S3 (bf16 matrix cores, exact 3-term split; gemm_s3.hpp) — the default: fp32 accuracy
+// (tests/test_gpu_ops.py) at 1.35-1.4x the f32 engine's speed on MI355X.  Process-wide;
+// CAD_GEMM=f32|s3 sets the initial value.
+int g_engine = -1;
+int engine() {
+    if (g_engine < 0) {
+        const char* e = std::getenv("CAD_GEMM");
+        g_engine = (e && e[0] == 'f') ? 0 : 1;
+    }
+    return g_engine;
+}
+constexpr int kS3KB = 16;   // S3 stage depth (LDS: 3 bf16 planes per operand)
 
 int tile_m(Cfg c) { return c == C41 ? 256 : c == C22 ? 128 : 64; }
 int tile_n(Cfg c) { return c == C41 ? 64 : c == C22 ? 128 : 256; }
@@ -234,6 +310,11 @@ void conv3x3_fwd(const float* x, int64_t ldx, int xcoff, int cin, const float* w
     a.stats = stats;
     a.a_sc = in_scale; a.a_sh = in_shift;
     const Cfg c = pick_cfg(a.M, a.N);
+    if (engine() == 1 && !in_scale) {
+        a.kstages_per_split = cdiv(a.K, kS3KB);
+        if (stats) launch_cfg_kb<KConvFwdS3, kS3KB>(c, a, 1, st); else launch_cfg_kb<KConvFwd3, kS3KB>(c, a, 1, st);
+        return;
+    }
     const int kb = kb_for(stats ? K_FWDS : K_FWD, c);
     a.kstages_per_split = cdiv(a.K, kb);
     if (in_scale) {
@@ -242,6 +323,9 @@ void conv3x3_fwd(const float* x, int64_t ldx, int xcoff, int cin, const float* w
         if (stats) launch_cfg<KConvFwdS>(c, kb, a, 1, st); else launch_cfg<KConvFwd>(c, kb, a, 1, st);
     }
 }
+
+void set_gemm_engine(int e) { g_engine = e == 1 ? 1 : 0; }
+int gemm_engine() { return engine(); }
 
 int conv3x3_stats_rows(int B, int H, int W, int cout) {
     Cfg c = pick_cfg(B * H * W, cout);
@@ -257,6 +341,11 @@ void convT_fwd(const float* x, int64_t ldx, int cin, const float* wf, const floa
     a.Bm = wf; a.ldb = cin;
     a.C = y; a.ldc = ldy; a.c_coff = ycoff; a.bias = bias;
     const Cfg c = pick_cfg(a.M, a.N);
+    if (engine() == 1) {
+        a.kstages_per_split = cdiv(a.K, kS3KB);
+        launch_cfg_kb<KConvTFwd3, kS3KB>(c, a, 1, st);
+        return;
+    }
     const int kb = kb_for(K_TFWD, c);
     a.kstages_per_split = cdiv(a.K, kb);
     launch_cfg<KConvTFwd>(c, kb, a, 1, st);
@@ -271,6 +360,11 @@ void conv3x3_dgrad(const float* dz, int cout, const float* wd, int cin, float* d
     a.Bm = wd; a.ldb = 9 * cout;
     a.C = dx; a.ldc = lddx; a.c_coff = 0;
     const Cfg c = pick_cfg(a.M, a.N);
+    if (engine() == 1) {
+        a.kstages_per_split = cdiv(a.K, kS3KB);
+        launch_cfg_kb<KConvFwd3, kS3KB>(c, a, 1, st);
+        return;
+    }
     const int kb = kb_for(K_FWD, c);
     a.kstages_per_split = cdiv(a.K, kb);
     launch_cfg<KConvFwd>(c, kb, a, 1, st);
@@ -285,6 +379,11 @@ void convT_dgrad(const float* g, int64_t ldg, int gcoff, int cout, const float* 
     a.Bm = wm; a.ldb = 4 * cout;
     a.C = dx; a.ldc = cin; a.c_coff = 0;
     const Cfg c = pick_cfg(a.M, a.N);
+    if (engine() == 1) {
+        a.kstages_per_split = cdiv(a.K, kS3KB);
+        launch_cfg_kb<KConvTDgrad3, kS3KB>(c, a, 1, st);
+        return;
+    }
     const int kb = kb_for(K_TDGRAD, c);
     a.kstages_per_split = cdiv(a.K, kb);
     launch_cfg<KConvTDgrad>(c, kb, a, 1, st);
@@ -311,14 +410,17 @@ void conv3x3_wgrad(const float* dz, int cout, const float* x, int64_t ldx, int x
     a.Bm = x; a.ldb = ldx; a.b_coff = xcoff; a.b_cin = cin;
     a.b_sc = x_scale; a.b_sh = x_shift;
     const Cfg c = pick_cfg(a.M, a.N);
-    const int kb = kb_for(K_WGRAD, c);
+    const bool s3 = engine() == 1 && !x_scale;
+    const int kb = s3 ? kS3KB : kb_for(K_WGRAD, c);
     int s = plan_splits(a, c, kb, slab_cap);
     a.kstages_per_split = cdiv(cdiv(a.K, kb), s);
     s = cdiv(cdiv(a.K, kb), a.kstages_per_split);
     const int64_t per = (int64_t)a.M * a.N;
     a.ldc = a.N; a.slab_stride = per;
     a.C = s == 1 ? dw : slab;
-    if (x_scale) launch_cfg<KConvWgradBN>(c, kb, a, s, st); else launch_cfg<KConvWgrad>(c, kb, a, s, st);
+    if (s3) launch_cfg_kb<KConvWgrad3, kS3KB>(c, a, s, st);
+    else if (x_scale) launch_cfg<KConvWgradBN>(c, kb, a, s, st);
+    else launch_cfg<KConvWgrad>(c, kb, a, s, st);
     if (s > 1) finish_slabs(slab, s, per, dw, st);
 }
 
@@ -330,14 +432,16 @@ void convT_wgrad(const float* x, int cin, const float* g, int64_t ldg, int gcoff
     a.A = x; a.lda = cin; a.a_coff = 0;
     a.Bm = g; a.ldb = ldg; a.b_coff = gcoff; a.b_cin = cout;
     const Cfg c = pick_cfg(a.M, a.N);
-    const int kb = kb_for(K_TWGRAD, c);
+    const bool s3 = engine() == 1;
+    const int kb = s3 ? kS3KB : kb_for(K_TWGRAD, c);
     int s = plan_splits(a, c, kb, slab_cap);
     a.kstages_per_split = cdiv(cdiv(a.K, kb), s);
     s = cdiv(cdiv(a.K, kb), a.kstages_per_split);
     const int64_t per = (int64_t)a.M * a.N;
     a.ldc = a.N; a.slab_stride = per;
     a.C = s == 1 ? dw : slab;
-    launch_cfg<KConvTWgrad>(c, kb, a, s, st);
+    if (s3) launch_cfg_kb<KConvTWgrad3, kS3KB>(c, a, s, st);
+    else launch_cfg<KConvTWgrad>(c, kb, a, s, st);
     if (s > 1) finish_slabs(slab, s, per, dw, st);
 }
 

@@ -446,6 +446,73 @@ __device__ __forceinline__ TileId xcd_tile() {
     return t;
 }
 
+// Epilogue shared by the engines: element (m, n) of sub-block (i, j), register r of the 32x32 C/D
+// layout (dtype-independent on gfx950).  `lds` is free scratch (the main loop ended on a barrier).
+template <int WM, int WN, class Epi>
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, floatx16 (&acc)[2][2], const TileId& tile,
+                                              float* lds, Epi epi) {
+    constexpr int BN = 64 * WN;
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int wm = wave / WN, wn = wave % WN;
+    const int m0 = tile.x * 64 * WM, n0 = tile.y * BN;
+    // With STATS the per-column BN partials are accumulated in the same pass (each accumulator is read once: keeping them live
+    // for a second pass costs 64 VGPRs and an occupancy step).
+    const int h = lane >> 5, col = lane & 31;
+    float ssum[2] = {0.f, 0.f}, ssq[2] = {0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int n = n0 + wn * 64 + j * 32 + col;
+            if constexpr (is_structured<Epi>::value) {
+                static_assert(!Epi::STATS, "structured epilogues carry no BN partials");
+                epi.block(a, m0 + wm * 64 + i * 32 + 4 * h, n, acc[i][j]);
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const float v = acc[i][j][r];
+                    if (m < a.M && n < a.N) epi(a, m, n, v, tile.z);
+                    if constexpr (Epi::STATS) {
+                        const float vm = m < a.M ? v : 0.f;
+                        ssum[j] += vm;
+                        ssq[j] += vm * vm;
+                    }
+                }
+                // keep the scheduler from hoisting all 64 accumulator reads ahead of the stores
+                if constexpr (Epi::STATS) __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+
+    if constexpr (Epi::STATS) {
+        // per-column partial sum / sum of squares over this block's BM rows -> a.stats[bx][2][N];
+        // the main loop ended on a barrier, so the LDS operand buffers are free for the reduction
+        float* red = lds;   // [WM][BN][2]
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const float s = ssum[j] + __shfl_xor(ssum[j], 32);
+            const float q = ssq[j] + __shfl_xor(ssq[j], 32);
+            if (h == 0) {
+                const int cl = wn * 64 + j * 32 + col;
+                red[(wm * BN + cl) * 2 + 0] = s;
+                red[(wm * BN + cl) * 2 + 1] = q;
+            }
+        }
+        __syncthreads();
+        for (int c = tid; c < BN; c += 256) {
+            float s = 0.f, q = 0.f;
+#pragma unroll
+            for (int w = 0; w < WM; ++w) { s += red[(w * BN + c) * 2]; q += red[(w * BN + c) * 2 + 1]; }
+            const int n = n0 + c;
+            if (n < a.N) {
+                a.stats[(int64_t)tile.x * 2 * a.N + n] = s;
+                a.stats[(int64_t)tile.x * 2 * a.N + a.N + n] = q;
+            }
+        }
+    }
+}
+
 template <int WM, int WN, int KB, class LA, bool KCA, class LB, bool KCB, class Epi, class InitA, class InitB>
 __device__ __forceinline__ void gemm_body(const GemmArgs& a, InitA init_a, InitB init_b, Epi epi) {
     using G = KS<KB>;
@@ -454,7 +521,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, InitA init_a, InitB
     __shared__ __attribute__((aligned(16))) float lds[2 * (SA + SB)];
 
     const int tid = threadIdx.x;
-    const int wave = tid >> 6, lane = tid & 63;
+    const int wave = tid >> 6;
     const int wm = wave / WN, wn = wave % WN;
     const TileId tile = xcd_tile();
     const int m0 = tile.x * BM, n0 = tile.y * BN;
@@ -517,62 +584,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, InitA init_a, InitB
         cur ^= 1;
     }
 
-    // epilogue: element (m, n) of sub-block (i, j), register r.  With STATS the per-column BN
-    // partials are accumulated in the same pass (each accumulator is read once: keeping them live
-    // for a second pass costs 64 VGPRs and an occupancy step).
-    const int h = lane >> 5, col = lane & 31;
-    float ssum[2] = {0.f, 0.f}, ssq[2] = {0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int n = n0 + wn * 64 + j * 32 + col;
-            if constexpr (is_structured<Epi>::value) {
-                static_assert(!Epi::STATS, "structured epilogues carry no BN partials");
-                epi.block(a, m0 + wm * 64 + i * 32 + 4 * h, n, acc[i][j]);
-            } else {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    const float v = acc[i][j][r];
-                    if (m < a.M && n < a.N) epi(a, m, n, v, tile.z);
-                    if constexpr (Epi::STATS) {
-                        const float vm = m < a.M ? v : 0.f;
-                        ssum[j] += vm;
-                        ssq[j] += vm * vm;
-                    }
-                }
-                // keep the scheduler from hoisting all 64 accumulator reads ahead of the stores
-                if constexpr (Epi::STATS) __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-
-    if constexpr (Epi::STATS) {
-        // per-column partial sum / sum of squares over this block's BM rows -> a.stats[bx][2][N];
-        // the main loop ended on a barrier, so the LDS operand buffers are free for the reduction
-        float* red = lds;   // [WM][BN][2]
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const float s = ssum[j] + __shfl_xor(ssum[j], 32);
-            const float q = ssq[j] + __shfl_xor(ssq[j], 32);
-            if (h == 0) {
-                const int cl = wn * 64 + j * 32 + col;
-                red[(wm * BN + cl) * 2 + 0] = s;
-                red[(wm * BN + cl) * 2 + 1] = q;
-            }
-        }
-        __syncthreads();
-        for (int c = tid; c < BN; c += 256) {
-            float s = 0.f, q = 0.f;
-#pragma unroll
-            for (int w = 0; w < WM; ++w) { s += red[(w * BN + c) * 2]; q += red[(w * BN + c) * 2 + 1]; }
-            const int n = n0 + c;
-            if (n < a.N) {
-                a.stats[(int64_t)tile.x * 2 * a.N + n] = s;
-                a.stats[(int64_t)tile.x * 2 * a.N + a.N + n] = q;
-            }
-        }
-    }
+    gemm_epilogue<WM, WN>(a, acc, tile, lds, epi);
 }
 
 }  // namespace cad

@@ -1,0 +1,325 @@
+// fp32 GEMM on the bf16 matrix cores by exact operand splitting ("S3" engine).
+//
+// Every fp32 operand x is split EXACTLY into three bf16 terms, x = x0 + x1 + x2:
+//   x0 = x with the low 16 bits cleared (8 significant bits), r = x - x0 (exact, <= 16 bits),
+//   x1 = r with the low 16 bits cleared, x2 = r - x1 (exact, <= 8 bits: a bf16 with zero low half).
+// A product is then a*b = sum_{p,q} a_p b_q with |a_p b_q| <= 2^-8(p+q) |a b|; the six terms with
+// p + q <= 2 are issued to v_mfma_f32_32x32x16_bf16 (bf16 x bf16 products are exact in fp32) and
+// accumulated in fp32, smallest first.  The dropped terms a1b2 + a2b1 + a2b2 are < 2^-23 |a b|, i.e.
+// the same order as one fp32 rounding, so the result carries fp32 accuracy (measured against fp64
+// in tests/test_gpu_ops.py next to the exact-fp32 MFMA engine).  Cost: 6 bf16 MFMAs of 32 cycles
+// per 16-deep k step instead of 8 f32 MFMAs of 64 cycles: 2.67x fewer matrix-core cycles.
+// Inf/NaN operands give NaN (the split of an infinity is inf - inf); the hot path never carries them.
+//
+// Staging: the Kc loaders of gemm_mfma.hpp (k-contiguous global rows, float4 per thread) fill
+// registers; the stage store splits each float4 into three bf16x4 and writes three LDS planes
+// [rows][KB + 8] (row stride 48 B at KB = 16: 16 consecutive rows hit distinct 16-B bank slots, so
+// the ds_read_b128 fragment reads are conflict-free).  Fragment of a 32x32x16 MFMA: lane l holds
+// A[row l&31][k = 8(l>>5) + j], j < 8 (one ds_read_b128 per plane); B likewise by column.
+#pragma once
+#include "gemm_mfma.hpp"
+
+namespace cad {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// three packed bf16x4 planes (as 2 x u32 each) of one float4
+struct Split4 {
+    uint2 p[3];
+};
+__device__ __forceinline__ Split4 split3(float4 v) {
+    const float x[4] = {v.x, v.y, v.z, v.w};
+    uint32_t h[4], m[4], l[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const uint32_t u = __float_as_uint(x[e]);
+        const uint32_t uh = u & 0xFFFF0000u;
+        const float r = x[e] - __uint_as_float(uh);
+        const uint32_t ur = __float_as_uint(r) & 0xFFFF0000u;
+        const float r2 = r - __uint_as_float(ur);
+        h[e] = uh >> 16;
+        m[e] = ur >> 16;
+        l[e] = __float_as_uint(r2) >> 16;
+    }
+    Split4 s;
+    s.p[0] = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+    s.p[1] = make_uint2(m[0] | (m[1] << 16), m[2] | (m[3] << 16));
+    s.p[2] = make_uint2(l[0] | (l[1] << 16), l[2] | (l[3] << 16));
+    return s;
+}
+
+template <int KB>
+struct S3 {
+    static_assert(KB % 16 == 0, "S3 stage depth is a multiple of the bf16 MFMA k (16)");
+    static constexpr int LDK = KB + 8;          // bf16 elements per plane row (16-B pad)
+    static constexpr int KSTEPS = KB / 16;      // MFMA k16 steps per stage
+};
+
+// LDS bytes of one operand image: 3 planes x ROWS x LDK bf16
+template <int ROWS, int KB>
+struct S3Lds {
+    static constexpr int ELEMS = 3 * ROWS * S3<KB>::LDK;   // bf16 elements
+};
+
+// store the loader's float4s (Kc mapping of KS<KB>) as three bf16 planes
+template <int ROWS, int KB, int NV>
+__device__ __forceinline__ void s3_store(uint16_t* s, const float4 (&v)[NV]) {
+    using G = KS<KB>;
+    constexpr int PL = ROWS * S3<KB>::LDK;   // elements per plane
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const Split4 sp = split3(v[j]);
+        const int off = (t / G::TPR + G::RPP * j) * S3<KB>::LDK + (t % G::TPR) * 4;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(s + p * PL + off) = sp.p[p];
+    }
+}
+
+// fp32 Kc image in natural k order ([rows][KB+4] floats; kc_store of gemm_mfma.hpp writes the
+// same addresses — the f32 engine's k permutation lives only in its fragment reads)
+template <int ROWS, int KB, int NV>
+__device__ __forceinline__ void kc_store_nat(float* s, const float4 (&v)[NV]) {
+    kc_store<ROWS, KB>(s, v);
+}
+
+// fragments of the three planes for 32-row block rb, k16 step q
+template <int ROWS, int KB>
+__device__ __forceinline__ void s3_frag(const uint16_t* s, int rb, int q, bf16x8 (&f)[3]) {
+    constexpr int PL = ROWS * S3<KB>::LDK;
+    const int lane = threadIdx.x & 63;
+    const uint16_t* base = s + (rb + (lane & 31)) * S3<KB>::LDK + q * 16 + (lane >> 5) * 8;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const bf16x8*>(base + p * PL);
+}
+
+// A operand kept fp32 in LDS ([rows][KB+4] floats, the Kc image of gemm_mfma.hpp in natural k
+// order) and split after the fragment read: used when every A row is read by ONE wave (WN == 1), so
+// splitting at read costs no more VALU than splitting at store, and the fp32 image is 2/3 the bytes
+// (the 256x64 tile then fits two workgroups per CU).
+template <int ROWS, int KB>
+__device__ __forceinline__ void s3_frag_f32(const float* s, int rb, int q, bf16x8 (&f)[3]) {
+    const int lane = threadIdx.x & 63;
+    const float* base = s + (rb + (lane & 31)) * KS<KB>::LDK + q * 16 + (lane >> 5) * 8;
+    const float4 v0 = *reinterpret_cast<const float4*>(base);
+    const float4 v1 = *reinterpret_cast<const float4*>(base + 4);
+    const Split4 s0 = split3(v0), s1 = split3(v1);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+        const uint4 u = make_uint4(s0.p[p].x, s0.p[p].y, s1.p[p].x, s1.p[p].y);
+        f[p] = __builtin_bit_cast(bf16x8, u);
+    }
+}
+
+// The S3 engine for Kc x Kc operands (conv3x3 fwd/dgrad, ConvT fwd/dgrad).  Same tiling, loaders,
+// pipeline and epilogue as gemm_body (gemm_mfma.hpp); only the LDS image and the MFMA differ.
+// AF32: A staged fp32 and split at fragment read (see s3_frag_f32); requires WN == 1.
+template <int WM, int WN, int KB, class LA, class LB, class Epi, class InitA, class InitB>
+__device__ __forceinline__ void gemm_body_s3(const GemmArgs& a, InitA init_a, InitB init_b, Epi epi) {
+    constexpr bool AF32 = WN == 1;
+    constexpr int BM = 64 * WM, BN = 64 * WN;
+    // LDS element counts in bf16 units (an fp32 A image counts 2 per float)
+    constexpr int SA = AF32 ? 2 * BM * KS<KB>::LDK : S3Lds<BM, KB>::ELEMS;
+    constexpr int SB = S3Lds<BN, KB>::ELEMS;
+    __shared__ __attribute__((aligned(16))) uint16_t lds[2 * (SA + SB)];
+
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const TileId tile = xcd_tile();
+    const int m0 = tile.x * BM, n0 = tile.y * BN;
+
+    const int nk_total = (a.K + KB - 1) / KB;
+    const int kbeg = tile.z * a.kstages_per_split;
+    const int kend = min(nk_total, kbeg + a.kstages_per_split);
+
+    LA la; LB lb;
+    init_a(la, m0, tid, kbeg);
+    init_b(lb, n0, tid, kbeg);
+
+    floatx16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    auto stage_store = [&](int buf, float4 (&xa)[LA::NV], float4 (&xb)[LB::NV]) {
+        la.finish(xa);
+        lb.finish(xb);
+        uint16_t* da = lds + buf * (SA + SB);
+        if constexpr (AF32) kc_store_nat<BM, KB>(reinterpret_cast<float*>(da), xa);
+        else s3_store<BM, KB>(da, xa);
+        s3_store<BN, KB>(da + SA, xb);
+    };
+    auto stage_compute = [&](int buf) {
+        const uint16_t* sa = lds + buf * (SA + SB);
+        const uint16_t* sb = sa + SA;
+#pragma unroll
+        for (int q = 0; q < S3<KB>::KSTEPS; ++q) {
+            bf16x8 fa[2][3], fb[2][3];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                if constexpr (AF32) s3_frag_f32<BM, KB>(reinterpret_cast<const float*>(sa), wm * 64 + i * 32, q, fa[i]);
+                else s3_frag<BM, KB>(sa, wm * 64 + i * 32, q, fa[i]);
+                s3_frag<BN, KB>(sb, wn * 64 + i * 32, q, fb[i]);
+            }
+            // smallest terms first: (2,0) (1,1) (0,2) (1,0) (0,1) (0,0)
+            constexpr int P[6] = {2, 1, 0, 1, 0, 0};
+            constexpr int Q[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+            for (int t = 0; t < 6; ++t)
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][P[t]], fb[j][Q[t]], acc[i][j], 0, 0, 0);
+        }
+    };
+
+    float4 ra[LA::NV], rb[LB::NV];
+    if (kbeg < kend) {
+        la.load(ra);
+        lb.load(rb);
+        stage_store(0, ra, rb);
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int kt = kbeg; kt < kend; ++kt) {
+        const bool more = kt + 1 < kend;
+        if (more) { la.load(ra); lb.load(rb); }
+        stage_compute(cur);
+        if (more) stage_store(cur ^ 1, ra, rb);
+        __syncthreads();
+        cur ^= 1;
+    }
+    gemm_epilogue<WM, WN>(a, acc, tile, reinterpret_cast<float*>(lds), epi);
+}
+
+// ------------------------------------------------------------------------------------------
+// S3 engine for MNc x MNc operands (the weight-gradient GEMMs: k = pixel is the strided index).
+// LDS planes are [KB k-rows][ROWS] bf16 with a 64-B pad per k-row (row stride 192 / 320 / 576 B
+// for 64 / 128 / 256 rows: the four k-rows a transposed read gathers then land on disjoint bank
+// quarters).  The MNc loader's float4 (4 consecutive rows at one k) is split and stored with one
+// ds_write_b64 per plane; fragments are read with ds_read_b64_tr_b16, which hands lane i of each
+// 16-lane group column i of 4 consecutive k-rows: two such reads give a lane its 8 consecutive k of
+// one row — exactly the 32x32x16 operand map — with no register transpose.
+// ------------------------------------------------------------------------------------------
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+
+template <int ROWS>
+struct S3M {
+    static constexpr int STRIDE = ROWS * 2 + 64;    // bytes per k-row of a plane
+};
+
+template <int ROWS, int KB, int NV>
+__device__ __forceinline__ void s3m_store(char* s, const float4 (&v)[NV]) {
+    using Base = MNcBase<ROWS, KB>;
+    constexpr int PL = KB * S3M<ROWS>::STRIDE;   // bytes per plane
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const Split4 sp = split3(v[j]);
+        const int off = (t / Base::TPR + Base::KSTEP * j) * S3M<ROWS>::STRIDE + (t % Base::TPR) * 8;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(s + p * PL + off) = sp.p[p];
+    }
+}
+
+template <int ROWS, int KB>
+__device__ __forceinline__ void s3m_frag(const char* s, int rb, int q, bf16x8 (&f)[3]) {
+    constexpr int PL = KB * S3M<ROWS>::STRIDE;
+    const int lane = threadIdx.x & 63;
+    const int g = (lane >> 4) & 1, h = lane >> 5, i = lane & 15;
+    const int krow = q * 16 + 8 * h + (i >> 2);
+    const int col = rb + 16 * g + 4 * (i & 3);
+    const char* base = s + krow * S3M<ROWS>::STRIDE + col * 2;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+        typedef __attribute__((address_space(3))) v4i16 lds_v4;
+        const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(base + p * PL));
+        const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(base + p * PL + 4 * S3M<ROWS>::STRIDE));
+        const uint2 ul = __builtin_bit_cast(uint2, lo), uh = __builtin_bit_cast(uint2, hi);
+        f[p] = __builtin_bit_cast(bf16x8, make_uint4(ul.x, ul.y, uh.x, uh.y));
+    }
+}
+
+template <int WM, int WN, int KB, class LA, class LB, class Epi, class InitA, class InitB>
+__device__ __forceinline__ void gemm_body_s3m(const GemmArgs& a, InitA init_a, InitB init_b, Epi epi) {
+    constexpr int BM = 64 * WM, BN = 64 * WN;
+    constexpr int SA = 3 * KB * S3M<BM>::STRIDE, SB = 3 * KB * S3M<BN>::STRIDE;   // bytes
+    __shared__ __attribute__((aligned(16))) char lds[2 * (SA + SB)];
+
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const TileId tile = xcd_tile();
+    const int m0 = tile.x * BM, n0 = tile.y * BN;
+
+    const int nk_total = (a.K + KB - 1) / KB;
+    const int kbeg = tile.z * a.kstages_per_split;
+    const int kend = min(nk_total, kbeg + a.kstages_per_split);
+
+    LA la; LB lb;
+    init_a(la, m0, tid, kbeg);
+    init_b(lb, n0, tid, kbeg);
+
+    floatx16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    auto stage_store = [&](int buf, float4 (&xa)[LA::NV], float4 (&xb)[LB::NV]) {
+        la.finish(xa);
+        lb.finish(xb);
+        char* da = lds + buf * (SA + SB);
+        s3m_store<BM, KB>(da, xa);
+        s3m_store<BN, KB>(da + SA, xb);
+    };
+    auto stage_compute = [&](int buf) {
+        const char* sa = lds + buf * (SA + SB);
+        const char* sb = sa + SA;
+#pragma unroll
+        for (int q = 0; q < S3<KB>::KSTEPS; ++q) {
+            bf16x8 fa[2][3], fb[2][3];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                s3m_frag<BM, KB>(sa, wm * 64 + i * 32, q, fa[i]);
+                s3m_frag<BN, KB>(sb, wn * 64 + i * 32, q, fb[i]);
+            }
+            constexpr int P[6] = {2, 1, 0, 1, 0, 0};
+            constexpr int Q[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+            for (int t = 0; t < 6; ++t)
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][P[t]], fb[j][Q[t]], acc[i][j], 0, 0, 0);
+        }
+    };
+
+    float4 ra[LA::NV], rb[LB::NV];
+    if (kbeg < kend) {
+        la.load(ra);
+        lb.load(rb);
+        stage_store(0, ra, rb);
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int kt = kbeg; kt < kend; ++kt) {
+        const bool more = kt + 1 < kend;
+        if (more) { la.load(ra); lb.load(rb); }
+        stage_compute(cur);
+        if (more) stage_store(cur ^ 1, ra, rb);
+        __syncthreads();
+        cur ^= 1;
+    }
+    gemm_epilogue<WM, WN>(a, acc, tile, reinterpret_cast<float*>(lds), epi);
+}
+
+}  // namespace cad

@@ -14,6 +14,10 @@ void prof_push(const char* name, double flops, hipStream_t st);
 void prof_pop(hipStream_t st);
 
 // ---------------- convolutions (conv_kernels.hip) ----------------
+// GEMM engine of the forward / dgrad contractions: 0 = exact fp32 MFMA (v_mfma_f32_32x32x2_f32),
+// 1 = S3: fp32 operands split exactly into three bf16 terms on the bf16 matrix cores (gemm_s3.hpp)
+void set_gemm_engine(int e);
+int gemm_engine();
 // y = conv3x3(x) (+ per-tile BN partials [rows][2][cout] when stats != nullptr)
 // in_scale/in_shift != nullptr: x is a pre-BN conv output and the loader applies
 // relu(x*scale[c] + shift[c]) on the fly (BN-apply + ReLU fused into the consumer)

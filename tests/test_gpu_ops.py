@@ -16,6 +16,17 @@ pytestmark = pytest.mark.gpu
 TOL = 2e-5
 
 
+@pytest.fixture(params=["f32", "s3"])
+def engine(request, cad):
+    """The forward/dgrad contractions run on either GEMM engine (cad.h CAD_GEMM_*): exact fp32 MFMA,
+    or S3 (exact 3-way bf16 split on the bf16 matrix cores); both must meet the same tolerance."""
+    lib = cad.load_library()
+    prev = lib.cad_get_gemm_engine()
+    assert lib.cad_set_gemm_engine(0 if request.param == "f32" else 1) == 0
+    yield request.param
+    lib.cad_set_gemm_engine(prev)
+
+
 def _p(t):
     return C.c_void_p(t.data_ptr())
 
@@ -41,7 +52,7 @@ CONV_SHAPES = [  # B, H, W, cin, cout
 
 
 @pytest.mark.parametrize("B,H,W,cin,cout", CONV_SHAPES)
-def test_conv3x3_fwd_dgrad_wgrad(cad, dev, B, H, W, cin, cout):
+def test_conv3x3_fwd_dgrad_wgrad(cad, dev, engine, B, H, W, cin, cout):
     lib = cad.load_library()
     g = torch.Generator().manual_seed(B * 1000 + cin + cout)
     x = torch.randn(B, cin, H, W, generator=g)
@@ -93,7 +104,7 @@ CONVT_SHAPES = [(2, 8, 12, 128, 64), (1, 4, 5, 1024, 512), (3, 6, 6, 32, 16), (2
 
 
 @pytest.mark.parametrize("B,H,W,cin,cout", CONVT_SHAPES)
-def test_convT(cad, dev, B, H, W, cin, cout):
+def test_convT(cad, dev, engine, B, H, W, cin, cout):
     lib = cad.load_library()
     g = torch.Generator().manual_seed(cin * 7 + cout)
     x = torch.randn(B, cin, H, W, generator=g)
@@ -160,3 +171,26 @@ def test_ray_directions(cad, dev, oracle):
     ref = torch.stack([x / n, y / n, (1 / n).expand(B, H, W)], 1)
     assert (rays.double() - ref).abs().max().item() < 1e-6
     assert torch.allclose(rays.double().norm(dim=1), torch.ones(B, H, W, dtype=torch.float64), atol=1e-6)
+
+
+@pytest.mark.parametrize("cin,cout,H,W", [(64, 64, 48, 64), (512, 512, 12, 16), (1024, 512, 8, 10)])
+def test_s3_engine_accuracy_matches_fp32(cad, dev, cin, cout, H, W):
+    """S3 (bf16 split) vs exact-fp32 MFMA, both against fp64, at the U-Net's K = 9*Cin: the S3
+    error must stay within the fp32 engine's own (fp32 accumulation) error band."""
+    lib = cad.load_library()
+    prev = lib.cad_get_gemm_engine()
+    B = 2
+    g = torch.Generator().manual_seed(cin + H)
+    x = torch.randn(B, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)
+    ref = F.conv2d(x.double(), w.double(), None, 1, 1)
+    xg, wg = nhwc(x).to(dev), w.permute(0, 2, 3, 1).contiguous().to(dev)
+    errs = {}
+    for eng in (0, 1):
+        assert lib.cad_set_gemm_engine(eng) == 0
+        y = torch.zeros(B, H, W, cout, device=dev)
+        assert lib.cad_op_conv3x3_fwd(_p(xg), cin, 0, cin, _p(wg), cout, _p(y), cout, 0, B, H, W, _s()) == 0
+        torch.cuda.synchronize()
+        errs[eng] = max_rel_err(nchw(y.cpu()), ref)
+    lib.cad_set_gemm_engine(prev)
+    assert errs[1] < max(2.0 * errs[0], 2e-6), errs
