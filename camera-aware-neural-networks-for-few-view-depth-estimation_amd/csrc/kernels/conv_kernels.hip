@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <stdexcept>
 
 #include "gemm_mfma.hpp"
 #include "gemm_s3.hpp"
@@ -287,13 +288,21 @@ constexpr int kS3KB = 16;   // S3 stage depth (LDS: 3 bf16 planes per operand)
 int tile_m(Cfg c) { return c == C41 ? 256 : c == C22 ? 128 : 64; }
 int tile_n(Cfg c) { return c == C41 ? 64 : c == C22 ? 128 : 256; }
 
-// split-K planning for the weight-gradient GEMMs: aim for >= ~2048 workgroups, >= 32 K-stages each
-int plan_splits(const GemmArgs& a, Cfg c, int kb, int64_t slab_cap_floats) {
+// split-K planning for the weight-gradient GEMMs: aim for >= ~2048 workgroups, >= 32 K-stages each.
+// A K-slice is also a loader's buffer window (gemm_mfma.hpp: 32-bit offsets from the slice's first
+// pixel): `kbytes` = bytes one K step spans in the widest operand; slices stay below 1 GB.
+int plan_splits(const GemmArgs& a, Cfg c, int kb, int64_t slab_cap_floats, int64_t kbytes) {
     const int tiles = cdiv(a.M, tile_m(c)) * cdiv(a.N, tile_n(c));
     const int nk = cdiv(a.K, kb);
     int s = std::max(1, std::min(cdiv(2048, tiles), nk / 32));
     const int64_t per = (int64_t)a.M * a.N;
     if (slab_cap_floats > 0) s = (int)std::max<int64_t>(1, std::min<int64_t>(s, slab_cap_floats / per));
+    const int64_t need = (int64_t)cdiv((int64_t)a.K * kbytes, (int64_t)1 << 30);
+    if (need > s) {
+        if (slab_cap_floats > 0 && need * per > slab_cap_floats)
+            throw std::runtime_error("weight-gradient K-slice exceeds the 1 GB loader window and the split-K slab");
+        s = (int)need;
+    }
     return s;
 }
 }  // namespace
@@ -393,7 +402,7 @@ int64_t wgrad_slab_floats(int M, int N, int Kpix) {
     GemmArgs a{};
     a.M = M; a.N = N; a.K = Kpix;
     const Cfg c = pick_cfg(M, N);
-    return (int64_t)plan_splits(a, c, 16, 0) * M * N;   // kb 16: the larger split count
+    return (int64_t)plan_splits(a, c, 16, 0, 0) * M * N;   // kb 16: the larger split count
 }
 
 static void finish_slabs(float* slab, int splits, int64_t per, float* dw, hipStream_t st) {
@@ -412,7 +421,7 @@ void conv3x3_wgrad(const float* dz, int cout, const float* x, int64_t ldx, int x
     const Cfg c = pick_cfg(a.M, a.N);
     const bool s3 = engine() == 1 && !x_scale;
     const int kb = s3 ? kS3KB : kb_for(K_WGRAD, c);
-    int s = plan_splits(a, c, kb, slab_cap);
+    int s = plan_splits(a, c, kb, slab_cap, 4 * std::max<int64_t>(a.lda, ldx));
     a.kstages_per_split = cdiv(cdiv(a.K, kb), s);
     s = cdiv(cdiv(a.K, kb), a.kstages_per_split);
     const int64_t per = (int64_t)a.M * a.N;
@@ -434,7 +443,7 @@ void convT_wgrad(const float* x, int cin, const float* g, int64_t ldg, int gcoff
     const Cfg c = pick_cfg(a.M, a.N);
     const bool s3 = engine() == 1;
     const int kb = s3 ? kS3KB : kb_for(K_TWGRAD, c);
-    int s = plan_splits(a, c, kb, slab_cap);
+    int s = plan_splits(a, c, kb, slab_cap, 4 * std::max<int64_t>(a.lda, 4 * ldg));
     a.kstages_per_split = cdiv(cdiv(a.K, kb), s);
     s = cdiv(cdiv(a.K, kb), a.kstages_per_split);
     const int64_t per = (int64_t)a.M * a.N;

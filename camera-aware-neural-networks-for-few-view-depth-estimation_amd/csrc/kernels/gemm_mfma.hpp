@@ -69,34 +69,58 @@ __device__ __forceinline__ float4 bn_relu4(float4 v, float4 s, float4 h) {
 }
 
 // --------------------------------------------------------------------------------------------
-// Kc loaders: operand(row r, k) with k contiguous in memory.  Thread t owns rows t/4 + 64j and
-// the float4 column group (t&3)*4 of every stage.
+// Operand fetch: buffer loads against a per-workgroup base.  Every loader builds ONE buffer
+// descriptor from wave-uniform values (kernel arguments and the tile's block-derived origin), so the
+// per-lane part of an address is a 32-bit byte offset from that base.  An element that lies outside
+// the operand (image border of the 3x3 gather, M/N/K tails) gets the offset kOOB: the hardware range
+// check returns zeros for it, so the loaders have no branches and no selects around their loads.
+// A block's window (its rows plus the 3x3 halo, or its K-slice of pixels) is far below 2 GB; the
+// host launchers keep it so (conv_kernels.hip: plan_splits).
+// --------------------------------------------------------------------------------------------
+constexpr uint32_t kOOB = 0x80000000u;
+constexpr uint32_t kRecords = 0x7FFFFFF0u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* base) {
+    // readfirstlane: make the uniformity of the descriptor provable to the compiler
+    const uint64_t a = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    void* p = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(p, 0, kRecords, 0x00020000);
+}
+__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+// --------------------------------------------------------------------------------------------
+// Kc loaders: operand(row r, k) with k contiguous in memory.  Thread t owns rows t/TPR + RPP*j and
+// the float4 column group (t%TPR)*4 of every stage.
+//
+// Loader protocol: init(..., kbeg) positions the loader at K-stage kbeg; load(v) issues the next
+// stage's global loads into registers; finish(v) (called right before the LDS store) completes any
+// register-side transform.
 // --------------------------------------------------------------------------------------------
 template <int ROWS, int KB>
 struct KcDense {   // op(r,k) = P[r*ld + coff + k], r < nrows, k < K
     using G = KS<KB>;
     static constexpr int NV = ROWS / G::RPP;
-    const float* p[NV];
-    bool ok[NV];
+    __amdgpu_buffer_rsrc_t rs;
+    uint32_t roff[NV];   // byte offset of the thread's row from the block base (kOOB: row out of range)
     int K, k;
     __device__ void init(const float* P, int64_t ld, int coff, int nrows, int K_, int row0, int tid, int kbeg) {
         K = K_;
-        k = kbeg * KB;
+        k = kbeg * KB + (tid % G::TPR) * 4;
+        rs = make_rsrc(P + (int64_t)row0 * ld + coff);
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
-            int r = row0 + tid / G::TPR + G::RPP * j;
-            ok[j] = r < nrows;
-            p[j] = P + (int64_t)(ok[j] ? r : 0) * ld + coff + (tid % G::TPR) * 4;
+            const int rr = tid / G::TPR + G::RPP * j;
+            roff[j] = row0 + rr < nrows ? (uint32_t)(rr * ld * 4) : kOOB;
         }
     }
     __device__ void load(float4 (&v)[NV]) {
-        bool kin = (k + ((threadIdx.x % G::TPR) * 4)) < K;
+        const bool kin = k < K;
 #pragma unroll
-        for (int j = 0; j < NV; ++j) {
-            bool g = ok[j] && kin;
-            float4 t = *reinterpret_cast<const float4*>(g ? p[j] + k : p[j]);
-            v[j] = g ? t : f4zero();
-        }
+        for (int j = 0; j < NV; ++j) v[j] = bload4(rs, kin ? roff[j] + (uint32_t)k * 4 : kOOB);
         k += KB;
     }
     __device__ void finish(float4 (&)[NV]) {}
@@ -106,65 +130,67 @@ struct KcDense {   // op(r,k) = P[r*ld + coff + k], r < nrows, k < K
 template <int KB>
 __device__ __forceinline__ void tapci_advance(int& tap, int& ci, int cin) {
     ci += KB;
-    while (ci >= cin) { ci -= cin; ++tap; }
+    if (cin >= KB) {   // uniform: at most one wrap per stage, branch-free
+        const bool w = ci >= cin;
+        ci -= w ? cin : 0;
+        tap += w;
+    } else {
+        while (ci >= cin) { ci -= cin; ++tap; }
+    }
 }
 
 // op(pix, k=(tap,ci)) = X[(b, y+ky-1, x+kx-1)*ld + coff + ci], zero outside the image.
 // BNR: X is a pre-BatchNorm conv output; relu(x*sc[ci] + sh[ci]) is applied to in-image elements
 // in finish(), i.e. when the stage is written to LDS after the MFMAs of the previous stage, so the
 // transform never stalls on the global loads it depends on.
-//
-// Loader protocol: load(v) issues the next stage's global loads into registers; finish(v) (called
-// right before the LDS store) completes any register-side transform.
 template <int ROWS, int KB, bool BNR = false>
 struct KcIm2col3x3 {
     using G = KS<KB>;
     static constexpr int NV = ROWS / G::RPP;
-    const float* base;
+    __amdgpu_buffer_rsrc_t rs;
     const float *sc, *sh;
     float4 s4, h4;     // BNR: coefficients of the loaded stage
     bool gm[NV];       // BNR: in-image mask of the loaded stage
-    int64_t ld;
+    int ld4;           // row stride in bytes
+    uint32_t poff[NV]; // byte offset of the thread's pixel from the block base
     int y[NV], x[NV];
-    int64_t pix[NV];
     bool ok[NV];
     int H, W, cin, tap, ci;
     __device__ void init(const float* P, int64_t ld_, int coff, int cin_, int B, int H_, int W_,
                          int row0, int tid, int kbeg, const float* sc_ = nullptr, const float* sh_ = nullptr) {
-        H = H_; W = W_; cin = cin_; ld = ld_;
+        H = H_; W = W_; cin = cin_; ld4 = (int)ld_ * 4;
         sc = sc_; sh = sh_;
-        base = P + coff;   // the thread's float4 column is folded into ci
+        const int pb = max(row0 - W_ - 1, 0);   // first pixel of the block's halo window
+        rs = make_rsrc(P + (int64_t)pb * ld_ + coff);
         const int k = kbeg * KB + (tid % G::TPR) * 4;
         tap = k / cin;
         ci = k - tap * cin;
-        int M = B * H * W;
+        const int M = B * H * W;
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
-            int r = row0 + tid / G::TPR + G::RPP * j;
+            const int r = row0 + tid / G::TPR + G::RPP * j;
             ok[j] = r < M;
-            int rr = ok[j] ? r : 0;
+            const int rr = ok[j] ? r : 0;
             x[j] = rr % W;
             y[j] = (rr / W) % H;
-            pix[j] = rr;
+            poff[j] = (uint32_t)((rr - pb) * ld4);
         }
     }
     __device__ void load(float4 (&v)[NV]) {
         const bool kin = tap < 9;
         const int t = kin ? tap : 0;
         const int dy = t / 3 - 1, dx = t - 3 * (t / 3) - 1;
-        const int64_t off = (int64_t)(dy * W + dx) * ld + ci;
+        const int off = (dy * W + dx) * ld4 + ci * 4;
         if constexpr (BNR) {
             s4 = *reinterpret_cast<const float4*>(sc + ci);
             h4 = *reinterpret_cast<const float4*>(sh + ci);
         }
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
-            int yy = y[j] + dy, xx = x[j] + dx;
-            bool g = ok[j] && kin && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
-            const float* q = base + pix[j] * ld + (g ? off : 0);
-            float4 tv = *reinterpret_cast<const float4*>(q);
+            const int yy = y[j] + dy, xx = x[j] + dx;
+            const bool g = ok[j] && kin && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
             if constexpr (BNR) gm[j] = g;
-            v[j] = g ? tv : f4zero();
+            v[j] = bload4(rs, g ? poff[j] + (uint32_t)off : kOOB);
         }
         tapci_advance<KB>(tap, ci, cin);
     }
@@ -181,39 +207,35 @@ template <int ROWS, int KB>
 struct KcUpGather {
     using G = KS<KB>;
     static constexpr int NV = ROWS / G::RPP;
-    const float* base;
-    int64_t ld;
-    int64_t hrpix[NV];   // high-res pixel index of (2y, 2x)
-    bool ok[NV];
+    __amdgpu_buffer_rsrc_t rs;
+    int ld4;
+    uint32_t hoff[NV];   // byte offset of high-res pixel (2y, 2x) from the block base (kOOB: row out of range)
     int W2, cout, q, co;
     __device__ void init(const float* P, int64_t ld_, int coff, int cout_, int B, int H, int W,
                          int row0, int tid, int kbeg) {
-        ld = ld_; cout = cout_; W2 = 2 * W;
-        base = P + coff;   // the thread's float4 column is folded into co
+        ld4 = (int)ld_ * 4; cout = cout_; W2 = 2 * W;
         const int k = kbeg * KB + (tid % G::TPR) * 4;
         q = k / cout;
         co = k - q * cout;
-        int M = B * H * W;
+        const int M = B * H * W;
+        auto hr = [&](int r) {
+            const int xx = r % W, t = r / W, yy = t % H, b = t / H;
+            return ((int64_t)b * (2 * H) + 2 * yy) * W2 + 2 * xx;
+        };
+        const int64_t hb = hr(min(row0, M - 1));
+        rs = make_rsrc(P + hb * ld_ + coff);
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
-            int r = row0 + tid / G::TPR + G::RPP * j;
-            ok[j] = r < M;
-            int rr = ok[j] ? r : 0;
-            int xx = rr % W, t = rr / W, yy = t % H, b = t / H;
-            hrpix[j] = ((int64_t)b * (2 * H) + 2 * yy) * W2 + 2 * xx;
+            const int r = row0 + tid / G::TPR + G::RPP * j;
+            hoff[j] = r < M ? (uint32_t)((hr(r) - hb) * ld4) : kOOB;
         }
     }
     __device__ void load(float4 (&v)[NV]) {
         const bool kin = q < 4;
         const int qq = kin ? q : 0;
-        const int64_t off = (int64_t)((qq >> 1) * W2 + (qq & 1)) * ld + co;
+        const uint32_t off = (uint32_t)(((qq >> 1) * W2 + (qq & 1)) * ld4 + co * 4);
 #pragma unroll
-        for (int j = 0; j < NV; ++j) {
-            bool g = ok[j] && kin;
-            const float* p = base + hrpix[j] * ld + (g ? off : 0);
-            float4 t = *reinterpret_cast<const float4*>(p);
-            v[j] = g ? t : f4zero();
-        }
+        for (int j = 0; j < NV; ++j) v[j] = bload4(rs, kin && hoff[j] != kOOB ? hoff[j] + off : kOOB);
         tapci_advance<KB>(q, co, cout);
     }
     __device__ void finish(float4 (&)[NV]) {}
@@ -221,7 +243,8 @@ struct KcUpGather {
 
 // --------------------------------------------------------------------------------------------
 // MNc loaders: operand(row r, k=pixel); memory rows are pixels, contiguous along r.
-// Thread t owns row group cg = t % (ROWS/4) (4 rows) and k-rows t/(ROWS/4) + KSTEP*j.
+// Thread t owns row group cg = t % (ROWS/4) (4 rows) and k-rows t/(ROWS/4) + KSTEP*j.  The block's
+// base is the first pixel of its K-slice (minus the 3x3 halo for the gather).
 // --------------------------------------------------------------------------------------------
 template <int ROWS, int KB>
 struct MNcBase {
@@ -245,26 +268,27 @@ template <int ROWS, int KB>
 struct MNcDense : MNcBase<ROWS, KB> {   // op(r, k) = P[k*ld + coff + r], r < nrows, k < Kp
     using Base = MNcBase<ROWS, KB>;
     static constexpr int NV = Base::NV;
-    const float* p;
-    int64_t ld;
-    int Kp, k0;
+    __amdgpu_buffer_rsrc_t rs;
+    uint32_t koff;   // byte offset of the thread's k-row 0 (advances KB rows per stage)
+    int ld4, Kp, k0;
     bool rok;
     __device__ void init(const float* P, int64_t ld_, int coff, int nrows, int Kp_, int row0, int tid, int kbeg) {
-        ld = ld_; Kp = Kp_;
-        int r = row0 + (tid % Base::TPR) * 4;
+        ld4 = (int)ld_ * 4; Kp = Kp_;
+        const int r = row0 + (tid % Base::TPR) * 4;
         rok = r < nrows;   // nrows % 4 == 0 is required
-        p = P + coff + (rok ? r : 0);
-        k0 = kbeg * KB + tid / Base::TPR;
+        const int kb0 = kbeg * KB;
+        rs = make_rsrc(P + (int64_t)kb0 * ld_ + coff + row0);
+        k0 = kb0 + tid / Base::TPR;
+        koff = (uint32_t)((tid / Base::TPR) * ld4 + (tid % Base::TPR) * 16);
     }
     __device__ void load(float4 (&v)[NV]) {
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
-            int k = k0 + Base::KSTEP * j;
-            bool g = rok && k < Kp;
-            float4 t = *reinterpret_cast<const float4*>(p + (int64_t)(g ? k : 0) * ld);
-            v[j] = g ? t : f4zero();
+            const int k = k0 + Base::KSTEP * j;
+            v[j] = bload4(rs, rok && k < Kp ? koff + (uint32_t)(Base::KSTEP * j * ld4) : kOOB);
         }
         k0 += KB;
+        koff += (uint32_t)(KB * ld4);
     }
     __device__ void finish(float4 (&)[NV]) {}
 };
@@ -274,22 +298,24 @@ template <int ROWS, int KB, bool BNR = false>
 struct MNcIm2col3x3 : MNcBase<ROWS, KB> {
     using Base = MNcBase<ROWS, KB>;
     static constexpr int NV = Base::NV;
-    const float* p;
+    __amdgpu_buffer_rsrc_t rs;
     float4 s4, h4;
     bool gm[NV];       // BNR: in-image mask of the loaded stage (transform deferred to finish())
-    int64_t ld;
-    int H, W, Kp, dy, dx;
+    int ld4, H, W, Kp, dy, dx, pb;
+    int tapoff;        // byte offset of the thread's (tap, ci) relative to its pixel
     int k[NV], x[NV], y[NV];
     bool rok;
     __device__ void init(const float* P, int64_t ld_, int coff, int cin, int B, int H_, int W_,
                          int row0, int tid, int kbeg, const float* sc = nullptr, const float* sh = nullptr) {
-        ld = ld_; H = H_; W = W_; Kp = B * H_ * W_;
-        int j = row0 + (tid % Base::TPR) * 4;
+        ld4 = (int)ld_ * 4; H = H_; W = W_; Kp = B * H_ * W_;
+        const int j = row0 + (tid % Base::TPR) * 4;
         rok = j < 9 * cin;
-        int jj = rok ? j : 0;
-        int tap = jj / cin, ci = jj - tap * cin;
+        const int jj = rok ? j : 0;
+        const int tap = jj / cin, ci = jj - tap * cin;
         dy = tap / 3 - 1; dx = tap % 3 - 1;
-        p = P + coff + ci;
+        pb = max(kbeg * KB - W_ - 1, 0);
+        rs = make_rsrc(P + (int64_t)pb * ld_ + coff);
+        tapoff = (dy * W + dx) * ld4 + ci * 4;
         if constexpr (BNR) {
             s4 = *reinterpret_cast<const float4*>(sc + ci);
             h4 = *reinterpret_cast<const float4*>(sh + ci);
@@ -297,7 +323,7 @@ struct MNcIm2col3x3 : MNcBase<ROWS, KB> {
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
             k[i] = kbeg * KB + tid / Base::TPR + Base::KSTEP * i;
-            int kk = k[i] < Kp ? k[i] : 0;
+            const int kk = k[i] < Kp ? k[i] : 0;
             x[i] = kk % W;
             y[i] = (kk / W) % H;
         }
@@ -307,10 +333,8 @@ struct MNcIm2col3x3 : MNcBase<ROWS, KB> {
         for (int j = 0; j < NV; ++j) {
             const int yy = y[j] + dy, xx = x[j] + dx;
             const bool g = rok && k[j] < Kp && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
-            const int64_t q = g ? (int64_t)k[j] + dy * W + dx : 0;
-            float4 t = *reinterpret_cast<const float4*>(p + q * ld);
             if constexpr (BNR) gm[j] = g;
-            v[j] = g ? t : f4zero();
+            v[j] = bload4(rs, g ? (uint32_t)((k[j] - pb) * ld4 + tapoff) : kOOB);
             int b = 0;
             px_advance<KB>(x[j], y[j], b, W, H);
             k[j] += KB;
@@ -329,26 +353,32 @@ template <int ROWS, int KB>
 struct MNcUpGather : MNcBase<ROWS, KB> {
     using Base = MNcBase<ROWS, KB>;
     static constexpr int NV = Base::NV;
-    const float* p;
-    int64_t ld;
-    int H, W, Kp, qy, qx;
+    __amdgpu_buffer_rsrc_t rs;
+    int64_t hb;          // high-res pixel of the block base
+    int ld4, H, W, Kp, qy, qx, cooff;
     int k[NV], x[NV], y[NV], b[NV];
     bool rok;
     __device__ void init(const float* P, int64_t ld_, int coff, int cout, int B, int H_, int W_,
                          int row0, int tid, int kbeg) {
-        ld = ld_; H = H_; W = W_; Kp = B * H_ * W_;
-        int j = row0 + (tid % Base::TPR) * 4;
+        ld4 = (int)ld_ * 4; H = H_; W = W_; Kp = B * H_ * W_;
+        const int j = row0 + (tid % Base::TPR) * 4;
         rok = j < 4 * cout;
-        int jj = rok ? j : 0;
-        int q = jj / cout, co = jj - q * cout;
+        const int jj = rok ? j : 0;
+        const int q = jj / cout, co = jj - q * cout;
         qy = q >> 1; qx = q & 1;
-        p = P + coff + co;
+        cooff = co * 4;
+        {   // block base: high-res pixel (2y, 2x) of the slice's first low-res pixel
+            const int kk = min(kbeg * KB, Kp - 1);
+            const int xx = kk % W, t = kk / W, yy = t % H, bb = t / H;
+            hb = ((int64_t)bb * (2 * H) + 2 * yy) * (2 * W) + 2 * xx;
+        }
+        rs = make_rsrc(P + hb * ld_ + coff);
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
             k[i] = kbeg * KB + tid / Base::TPR + Base::KSTEP * i;
-            int kk = k[i] < Kp ? k[i] : 0;
+            const int kk = k[i] < Kp ? k[i] : 0;
             x[i] = kk % W;
-            int t = kk / W;
+            const int t = kk / W;
             y[i] = t % H;
             b[i] = t / H;
         }
@@ -357,9 +387,8 @@ struct MNcUpGather : MNcBase<ROWS, KB> {
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             const bool g = rok && k[j] < Kp;
-            const int64_t hp = g ? ((int64_t)b[j] * (2 * H) + 2 * y[j] + qy) * (2 * W) + 2 * x[j] + qx : 0;
-            float4 t4 = *reinterpret_cast<const float4*>(p + hp * ld);
-            v[j] = g ? t4 : f4zero();
+            const int64_t hp = ((int64_t)b[j] * (2 * H) + 2 * y[j] + qy) * (2 * W) + 2 * x[j] + qx;
+            v[j] = bload4(rs, g ? (uint32_t)((hp - hb) * ld4 + cooff) : kOOB);
             px_advance<KB>(x[j], y[j], b[j], W, H);
             k[j] += KB;
         }
