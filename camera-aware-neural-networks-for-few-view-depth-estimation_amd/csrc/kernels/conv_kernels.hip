@@ -284,6 +284,31 @@ int engine() {
     return g_engine;
 }
 constexpr int kS3KB = 16;   // S3 stage depth (LDS: 3 bf16 planes per operand)
+// S3 stage depth: one bf16 k16 step per LDS stage (32 measured 12-13% slower: the LDS footprint
+// costs a workgroup per CU); kept as a function for the launch sites
+int s3_kb(Kind, Cfg) { return kS3KB; }
+[[maybe_unused]] int s3_kb_env(Kind k, Cfg c) {
+    static int kb[K_NKIND][3];
+    static bool init = false;
+    if (!init) {
+        const char* kn[K_NKIND] = {"FWD", "FWDS", "WGRAD", "TFWD", "TDGRAD", "TWGRAD"};
+        const char* cn[3] = {"C41", "C22", "C14"};
+        for (int i = 0; i < K_NKIND; ++i)
+            for (int j = 0; j < 3; ++j) {
+                int v = kS3KB;
+                char name[40];
+                snprintf(name, sizeof(name), "CAD_S3KB_%s_%s", kn[i], cn[j]);
+                if (const char* e = std::getenv(name)) v = std::atoi(e);
+                kb[i][j] = v == 32 ? 32 : 16;
+            }
+        init = true;
+    }
+    return kb[k][c];
+}
+template <template <int, int, int> class KT>
+void launch_s3(Cfg c, int, const GemmArgs& a, int splits, hipStream_t st) {
+    launch_cfg_kb<KT, 16>(c, a, splits, st);
+}
 
 int tile_m(Cfg c) { return c == C41 ? 256 : c == C22 ? 128 : 64; }
 int tile_n(Cfg c) { return c == C41 ? 64 : c == C22 ? 128 : 256; }
@@ -320,8 +345,9 @@ void conv3x3_fwd(const float* x, int64_t ldx, int xcoff, int cin, const float* w
     a.a_sc = in_scale; a.a_sh = in_shift;
     const Cfg c = pick_cfg(a.M, a.N);
     if (engine() == 1 && !in_scale) {
-        a.kstages_per_split = cdiv(a.K, kS3KB);
-        if (stats) launch_cfg_kb<KConvFwdS3, kS3KB>(c, a, 1, st); else launch_cfg_kb<KConvFwd3, kS3KB>(c, a, 1, st);
+        const int kb = s3_kb(stats ? K_FWDS : K_FWD, c);
+        a.kstages_per_split = cdiv(a.K, kb);
+        if (stats) launch_s3<KConvFwdS3>(c, kb, a, 1, st); else launch_s3<KConvFwd3>(c, kb, a, 1, st);
         return;
     }
     const int kb = kb_for(stats ? K_FWDS : K_FWD, c);
@@ -351,8 +377,9 @@ void convT_fwd(const float* x, int64_t ldx, int cin, const float* wf, const floa
     a.C = y; a.ldc = ldy; a.c_coff = ycoff; a.bias = bias;
     const Cfg c = pick_cfg(a.M, a.N);
     if (engine() == 1) {
-        a.kstages_per_split = cdiv(a.K, kS3KB);
-        launch_cfg_kb<KConvTFwd3, kS3KB>(c, a, 1, st);
+        const int kb = s3_kb(K_TFWD, c);
+        a.kstages_per_split = cdiv(a.K, kb);
+        launch_s3<KConvTFwd3>(c, kb, a, 1, st);
         return;
     }
     const int kb = kb_for(K_TFWD, c);
@@ -370,8 +397,9 @@ void conv3x3_dgrad(const float* dz, int cout, const float* wd, int cin, float* d
     a.C = dx; a.ldc = lddx; a.c_coff = 0;
     const Cfg c = pick_cfg(a.M, a.N);
     if (engine() == 1) {
-        a.kstages_per_split = cdiv(a.K, kS3KB);
-        launch_cfg_kb<KConvFwd3, kS3KB>(c, a, 1, st);
+        const int kb = s3_kb(K_FWD, c);
+        a.kstages_per_split = cdiv(a.K, kb);
+        launch_s3<KConvFwd3>(c, kb, a, 1, st);
         return;
     }
     const int kb = kb_for(K_FWD, c);
@@ -389,8 +417,9 @@ void convT_dgrad(const float* g, int64_t ldg, int gcoff, int cout, const float* 
     a.C = dx; a.ldc = cin; a.c_coff = 0;
     const Cfg c = pick_cfg(a.M, a.N);
     if (engine() == 1) {
-        a.kstages_per_split = cdiv(a.K, kS3KB);
-        launch_cfg_kb<KConvTDgrad3, kS3KB>(c, a, 1, st);
+        const int kb = s3_kb(K_TDGRAD, c);
+        a.kstages_per_split = cdiv(a.K, kb);
+        launch_s3<KConvTDgrad3>(c, kb, a, 1, st);
         return;
     }
     const int kb = kb_for(K_TDGRAD, c);
@@ -420,14 +449,14 @@ void conv3x3_wgrad(const float* dz, int cout, const float* x, int64_t ldx, int x
     a.b_sc = x_scale; a.b_sh = x_shift;
     const Cfg c = pick_cfg(a.M, a.N);
     const bool s3 = engine() == 1 && !x_scale;
-    const int kb = s3 ? kS3KB : kb_for(K_WGRAD, c);
+    const int kb = s3 ? s3_kb(K_WGRAD, c) : kb_for(K_WGRAD, c);
     int s = plan_splits(a, c, kb, slab_cap, 4 * std::max<int64_t>(a.lda, ldx));
     a.kstages_per_split = cdiv(cdiv(a.K, kb), s);
     s = cdiv(cdiv(a.K, kb), a.kstages_per_split);
     const int64_t per = (int64_t)a.M * a.N;
     a.ldc = a.N; a.slab_stride = per;
     a.C = s == 1 ? dw : slab;
-    if (s3) launch_cfg_kb<KConvWgrad3, kS3KB>(c, a, s, st);
+    if (s3) launch_s3<KConvWgrad3>(c, kb, a, s, st);
     else if (x_scale) launch_cfg<KConvWgradBN>(c, kb, a, s, st);
     else launch_cfg<KConvWgrad>(c, kb, a, s, st);
     if (s > 1) finish_slabs(slab, s, per, dw, st);
@@ -442,14 +471,14 @@ void convT_wgrad(const float* x, int cin, const float* g, int64_t ldg, int gcoff
     a.Bm = g; a.ldb = ldg; a.b_coff = gcoff; a.b_cin = cout;
     const Cfg c = pick_cfg(a.M, a.N);
     const bool s3 = engine() == 1;
-    const int kb = s3 ? kS3KB : kb_for(K_TWGRAD, c);
+    const int kb = s3 ? s3_kb(K_TWGRAD, c) : kb_for(K_TWGRAD, c);
     int s = plan_splits(a, c, kb, slab_cap, 4 * std::max<int64_t>(a.lda, 4 * ldg));
     a.kstages_per_split = cdiv(cdiv(a.K, kb), s);
     s = cdiv(cdiv(a.K, kb), a.kstages_per_split);
     const int64_t per = (int64_t)a.M * a.N;
     a.ldc = a.N; a.slab_stride = per;
     a.C = s == 1 ? dw : slab;
-    if (s3) launch_cfg_kb<KConvTWgrad3, kS3KB>(c, a, s, st);
+    if (s3) launch_s3<KConvTWgrad3>(c, kb, a, s, st);
     else launch_cfg<KConvTWgrad>(c, kb, a, s, st);
     if (s > 1) finish_slabs(slab, s, per, dw, st);
 }

@@ -13,8 +13,10 @@
 //
 // Staging: the Kc loaders of gemm_mfma.hpp (k-contiguous global rows, float4 per thread) fill
 // registers; the stage store splits each float4 into three bf16x4 and writes three LDS planes
-// [rows][KB + 8] (row stride 48 B at KB = 16: 16 consecutive rows hit distinct 16-B bank slots, so
-// the ds_read_b128 fragment reads are conflict-free).  Fragment of a 32x32x16 MFMA: lane l holds
+// [rows][16] (32-B rows, no padding: the 16-B half h of row r is stored at half h ^ ((r >> 3) & 1),
+// which makes the ds_read_b128 fragment reads conflict-free in all four lane groups of the
+// instruction, MI355X_MICROARCH.md §LDS).  Unpadded planes keep a 128x128 tile at 48 KB of LDS
+// (double-buffered), three workgroups per CU.  Fragment of a 32x32x16 MFMA: lane l holds
 // A[row l&31][k = 8(l>>5) + j], j < 8 (one ds_read_b128 per plane); B likewise by column.
 #pragma once
 #include "gemm_mfma.hpp"
@@ -50,16 +52,18 @@ __device__ __forceinline__ Split4 split3(float4 v) {
 
 template <int KB>
 struct S3 {
-    static_assert(KB % 16 == 0, "S3 stage depth is a multiple of the bf16 MFMA k (16)");
-    static constexpr int LDK = KB + 8;          // bf16 elements per plane row (16-B pad)
-    static constexpr int KSTEPS = KB / 16;      // MFMA k16 steps per stage
+    static_assert(KB == 16, "S3 stage depth: one bf16 MFMA k step (16) per LDS stage");
+    static constexpr int LDK = 16;              // bf16 elements per plane row (32 B, swizzled)
+    static constexpr int KSTEPS = 1;
 };
 
-// LDS bytes of one operand image: 3 planes x ROWS x LDK bf16
+// LDS bytes of one operand image: 3 planes x ROWS x 16 bf16
 template <int ROWS, int KB>
 struct S3Lds {
     static constexpr int ELEMS = 3 * ROWS * S3<KB>::LDK;   // bf16 elements
 };
+// element offset of (row r, k) in a swizzled plane
+__device__ __forceinline__ int s3_off(int r, int k) { return r * 16 + (((k >> 3) ^ ((r >> 3) & 1)) << 3) + (k & 7); }
 
 // store the loader's float4s (Kc mapping of KS<KB>) as three bf16 planes
 template <int ROWS, int KB, int NV>
@@ -70,7 +74,7 @@ __device__ __forceinline__ void s3_store(uint16_t* s, const float4 (&v)[NV]) {
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
         const Split4 sp = split3(v[j]);
-        const int off = (t / G::TPR + G::RPP * j) * S3<KB>::LDK + (t % G::TPR) * 4;
+        const int off = s3_off(t / G::TPR + G::RPP * j, (t % G::TPR) * 4);
 #pragma unroll
         for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(s + p * PL + off) = sp.p[p];
     }
@@ -88,7 +92,7 @@ template <int ROWS, int KB>
 __device__ __forceinline__ void s3_frag(const uint16_t* s, int rb, int q, bf16x8 (&f)[3]) {
     constexpr int PL = ROWS * S3<KB>::LDK;
     const int lane = threadIdx.x & 63;
-    const uint16_t* base = s + (rb + (lane & 31)) * S3<KB>::LDK + q * 16 + (lane >> 5) * 8;
+    const uint16_t* base = s + s3_off(rb + (lane & 31), q * 16 + (lane >> 5) * 8);
 #pragma unroll
     for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const bf16x8*>(base + p * PL);
 }
@@ -208,9 +212,18 @@ __device__ __forceinline__ void gemm_body_s3(const GemmArgs& a, InitA init_a, In
 // ------------------------------------------------------------------------------------------
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 
+// k-row stride: 128+ rows are unpadded with the 16-B chunks of k-row kr XORed by 4(kr & 3), which
+// moves the four k-rows of a transposed read to disjoint bank quarters; 64-row planes (too narrow
+// for that XOR) keep a 64-B pad instead.
 template <int ROWS>
 struct S3M {
-    static constexpr int STRIDE = ROWS * 2 + 64;    // bytes per k-row of a plane
+    static constexpr bool SWZ = ROWS >= 128;
+    static constexpr int STRIDE = SWZ ? ROWS * 2 : ROWS * 2 + 64;    // bytes per k-row of a plane
+    // byte offset of (k-row kr, column c), c a multiple of 4
+    __device__ static __forceinline__ int off(int kr, int c) {
+        if constexpr (SWZ) return kr * STRIDE + ((((c >> 3) ^ ((kr & 3) << 2))) << 4) + (c & 7) * 2;
+        else return kr * STRIDE + c * 2;
+    }
 };
 
 template <int ROWS, int KB, int NV>
@@ -221,7 +234,7 @@ __device__ __forceinline__ void s3m_store(char* s, const float4 (&v)[NV]) {
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
         const Split4 sp = split3(v[j]);
-        const int off = (t / Base::TPR + Base::KSTEP * j) * S3M<ROWS>::STRIDE + (t % Base::TPR) * 8;
+        const int off = S3M<ROWS>::off(t / Base::TPR + Base::KSTEP * j, (t % Base::TPR) * 4);
 #pragma unroll
         for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(s + p * PL + off) = sp.p[p];
     }
@@ -234,12 +247,13 @@ __device__ __forceinline__ void s3m_frag(const char* s, int rb, int q, bf16x8 (&
     const int g = (lane >> 4) & 1, h = lane >> 5, i = lane & 15;
     const int krow = q * 16 + 8 * h + (i >> 2);
     const int col = rb + 16 * g + 4 * (i & 3);
-    const char* base = s + krow * S3M<ROWS>::STRIDE + col * 2;
+    const char* b0 = s + S3M<ROWS>::off(krow, col);       // k-rows 8h + 0..3
+    const char* b1 = s + S3M<ROWS>::off(krow + 4, col);   // k-rows 8h + 4..7
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
         typedef __attribute__((address_space(3))) v4i16 lds_v4;
-        const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(base + p * PL));
-        const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(base + p * PL + 4 * S3M<ROWS>::STRIDE));
+        const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(b0 + p * PL));
+        const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(b1 + p * PL));
         const uint2 ul = __builtin_bit_cast(uint2, lo), uh = __builtin_bit_cast(uint2, hi);
         f[p] = __builtin_bit_cast(bf16x8, make_uint4(ul.x, ul.y, uh.x, uh.y));
     }
