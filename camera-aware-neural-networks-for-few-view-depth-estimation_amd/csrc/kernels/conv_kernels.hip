@@ -13,10 +13,12 @@
 
 namespace cad {
 
+// Row-major epilogues: C[m][c_coff + n] with row stride ldc; the engine stores through a buffer
+// descriptor based at row_base (gemm_mfma.hpp gemm_epilogue).
 struct EpiStore {
     static constexpr bool STATS = false;
-    __device__ void operator()(const GemmArgs& a, int m, int n, float v, int) const {
-        a.C[(int64_t)m * a.ldc + a.c_coff + n] = v;
+    __device__ static const float* row_base(const GemmArgs& a, int m0, int) {
+        return a.C + (int64_t)m0 * a.ldc + a.c_coff;
     }
 };
 struct EpiStoreStats : EpiStore {
@@ -60,8 +62,8 @@ struct EpiConvT {
 };
 struct EpiSlab {   // split-K partial: slab z holds C[m][n] of K-slice z
     static constexpr bool STATS = false;
-    __device__ void operator()(const GemmArgs& a, int m, int n, float v, int z) const {
-        a.C[z * a.slab_stride + (int64_t)m * a.ldc + n] = v;
+    __device__ static const float* row_base(const GemmArgs& a, int m0, int z) {
+        return a.C + (int64_t)z * a.slab_stride + (int64_t)m0 * a.ldc;
     }
 };
 

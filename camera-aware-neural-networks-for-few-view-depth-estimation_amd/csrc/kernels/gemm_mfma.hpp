@@ -80,13 +80,13 @@ __device__ __forceinline__ float4 bn_relu4(float4 v, float4 s, float4 h) {
 constexpr uint32_t kOOB = 0x80000000u;
 constexpr uint32_t kRecords = 0x7FFFFFF0u;
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* base) {
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* base, uint32_t records = kRecords) {
     // readfirstlane: make the uniformity of the descriptor provable to the compiler
     const uint64_t a = reinterpret_cast<uint64_t>(base);
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
     void* p = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
-    return __builtin_amdgcn_make_buffer_rsrc(p, 0, kRecords, 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc(p, 0, __builtin_amdgcn_readfirstlane(records), 0x00020000);
 }
 __device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
@@ -475,6 +475,12 @@ __device__ __forceinline__ TileId xcd_tile() {
     return t;
 }
 
+template <class Epi>
+__device__ __forceinline__ const float* epi_row_base(const GemmArgs& a, int m0, int z) {
+    if constexpr (is_structured<Epi>::value) return a.C;   // unused by structured epilogues
+    else return Epi::row_base(a, m0, z);
+}
+
 // Epilogue shared by the engines: element (m, n) of sub-block (i, j), register r of the 32x32 C/D
 // layout (dtype-independent on gfx950).  `lds` is free scratch (the main loop ended on a barrier).
 template <int WM, int WN, class Epi>
@@ -489,6 +495,13 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, floatx16 (&acc)
     // for a second pass costs 64 VGPRs and an occupancy step).
     const int h = lane >> 5, col = lane & 31;
     float ssum[2] = {0.f, 0.f}, ssq[2] = {0.f, 0.f};
+    // Row-major epilogues (EpiStore, EpiSlab) store through a buffer descriptor based at the tile's
+    // first output row whose range ends at row M: rows past M are dropped by the range check and
+    // columns past N get an out-of-range offset, so each store is one 32-bit offset add.
+    const int64_t ldc4 = a.ldc * 4;
+    const int64_t bytes = (int64_t)(a.M - m0) * ldc4;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(epi_row_base<Epi>(a, m0, tile.z),
+                                                (uint32_t)(bytes < (int64_t)kRecords ? bytes : kRecords));
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -498,19 +511,20 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, floatx16 (&acc)
                 static_assert(!Epi::STATS, "structured epilogues carry no BN partials");
                 epi.block(a, m0 + wm * 64 + i * 32 + 4 * h, n, acc[i][j]);
             } else {
+                const int mr = wm * 64 + i * 32 + 4 * h;   // tile-relative row of register 0
+                const uint32_t lo = n < a.N ? (uint32_t)(mr * ldc4 + (int64_t)n * 4) : kOOB;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const int dr = (r & 3) + 8 * (r >> 2);
                     const float v = acc[i][j][r];
-                    if (m < a.M && n < a.N) epi(a, m, n, v, tile.z);
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rs,
+                                                          lo + (uint32_t)(dr * ldc4), 0, 0);
                     if constexpr (Epi::STATS) {
-                        const float vm = m < a.M ? v : 0.f;
+                        const float vm = m0 + mr + dr < a.M ? v : 0.f;
                         ssum[j] += vm;
                         ssq[j] += vm * vm;
                     }
                 }
-                // keep the scheduler from hoisting all 64 accumulator reads ahead of the stores
-                if constexpr (Epi::STATS) __builtin_amdgcn_sched_barrier(0);
             }
         }
 

@@ -94,7 +94,10 @@ def test_film_train_steps_vs_reference_fixture(cad, dev, oracle, name):
     for n, b in net.named_buffers().items():
         b64 = t64.bufs[n]
         ours, theirs = (b.double() - b64).abs().max().item(), (fx["final." + n].double() - b64).abs().max().item()
-        assert ours <= max(1e-4 * b64.abs().max().item(), 3 * theirs), (n, ours, theirs)
+        # a FiLM BatchNorm1d running mean follows its Linear bias, whose (exactly zero) gradient is
+        # rounding noise that Adam turns into +-lr steps: momentum 0.1 of that walk on top
+        walk = 0.1 * 2 * lr * meta["steps"] if ".film.bn" in n and n.endswith("mean") else 0.0
+        assert ours <= max(1e-4 * b64.abs().max().item(), 3 * theirs) + walk, (n, ours, theirs)
     net.eval()
     pe = net.forward_cam(rgb, cam)
     pe64 = t64.predict_eval(fx["input.rgb"], fx["input.K"])
