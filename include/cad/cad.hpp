@@ -82,10 +82,7 @@ class BaselineUNetImpl {
 public:
     explicit BaselineUNetImpl(int in_channels = 3, int init_features = 64, float max_depth_value = 10.0f,
                               cad::Workspace ws = {})
-        : max_depth(max_depth_value), ws_(ws) {
-        cad_unet_desc d{in_channels, init_features, max_depth_value, ws.batch, ws.height, ws.width};
-        cad::check(cad_unet_create(&d, ws.device, &h_), "BaselineUNetImpl");
-    }
+        : BaselineUNetImpl(CAD_MODEL_BASELINE, in_channels, init_features, max_depth_value, ws) {}
     ~BaselineUNetImpl() { cad_unet_destroy(h_); }
     BaselineUNetImpl(const BaselineUNetImpl&) = delete;
     BaselineUNetImpl& operator=(const BaselineUNetImpl&) = delete;
@@ -139,6 +136,13 @@ public:
 
     float max_depth;
 
+protected:
+    BaselineUNetImpl(int model, int in_channels, int init_features, float max_depth_value, cad::Workspace ws)
+        : max_depth(max_depth_value), ws_(ws) {
+        cad_unet_desc d{in_channels, init_features, max_depth_value, ws.batch, ws.height, ws.width};
+        cad::check(cad_unet_create_model(&d, model, ws.device, &h_), "cad_unet_create_model");
+    }
+
 private:
     std::vector<NamedTensor> fetch(int kind) const {
         const int cnt = kind == 0 ? cad_unet_num_params(h_) : cad_unet_num_buffers(h_);
@@ -161,6 +165,39 @@ private:
     }
     cad::Workspace ws_;
     cad_unet* h_ = nullptr;
+};
+
+// IntrinsicsConditionedUNetImpl(in, f, camera_dim = 4, max_depth)   (intrinsics_unet.h:137-270):
+// FiLMLayer(4, C) after every DoubleConv's first BN-ReLU; forward(x, camera_intrinsics (B,4)).
+class IntrinsicsConditionedUNetImpl : public BaselineUNetImpl {
+public:
+    explicit IntrinsicsConditionedUNetImpl(int in_channels = 3, int init_features = 64, int camera_dim = 4,
+                                           float max_depth_value = 10.0f, cad::Workspace ws = {},
+                                           int model = CAD_MODEL_INTRINSICS_FILM)
+        : BaselineUNetImpl(model, in_channels, init_features, max_depth_value, ws) {
+        if (camera_dim != 4) throw std::runtime_error("camera_dim must be 4 ([fx, fy, cx, cy])");
+    }
+    // intrinsics: (B,4) [fx, fy, cx, cy] in pixels of the input (normalised on device, :252-268)
+    DeviceTensor forward(const DeviceTensor& x, const DeviceTensor& intrinsics, void* stream = nullptr) {
+        if (x.dim() != 4 || x.size(1) != 3) throw std::runtime_error("forward: expected (B,3,H,W)");
+        if (intrinsics.dim() != 2 || intrinsics.size(0) != x.size(0) || intrinsics.size(1) != 4)
+            throw std::runtime_error("forward: expected intrinsics (B,4)");
+        DeviceTensor out = DeviceTensor::empty({x.size(0), 1, x.size(2), x.size(3)}, workspace().device);
+        cad::check(cad_unet_forward_cam(handle(), x.data, intrinsics.data, out.data, (int)x.size(0), stream),
+                   "forward");
+        return out;
+    }
+    DeviceTensor operator()(const DeviceTensor& x, const DeviceTensor& intrinsics) { return forward(x, intrinsics); }
+};
+
+// Config-3 composite: enc1 = RayEnhancedConv(3, f, 4, use_rays) fed cat(x, rays(K)) (geometry_aware_network.h:17-65),
+// FiLM blocks after; same forward(x, intrinsics) (rays derived on device from the intrinsics).
+class RayConditionedUNetImpl : public IntrinsicsConditionedUNetImpl {
+public:
+    explicit RayConditionedUNetImpl(int in_channels = 3, int init_features = 64, int camera_dim = 4,
+                                    float max_depth_value = 10.0f, cad::Workspace ws = {})
+        : IntrinsicsConditionedUNetImpl(in_channels, init_features, camera_dim, max_depth_value, ws,
+                                        CAD_MODEL_RAY_FILM) {}
 };
 
 class CombinedDepthLoss {
