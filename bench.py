@@ -7,7 +7,9 @@ evaluates all four terms, and so do we).  One step = TensorBoardTrainerEnhanced:
 (enhanced.h:287-304): forward, loss + dL/dpred, backward, clip_grad_norm_(1.0), Adam — all in
 libcad_hip.so.  Synthetic SUN-RGB-D-shaped batches resident in HBM (data loading excluded).
 
-  python bench.py [--gpus N --steps K --warmup W]
+  python bench.py [--gpus N --steps K --warmup W]      # configs[1] (the headline line)
+  python bench.py --config 3                            # ray+FiLM model, bf16 GEMMs, full loss
+  python bench.py --config 4                            # baseline_unet, bf16 GEMMs, full loss
   N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N  (one rank per GPU,
   RCCL gradient all-reduce overlapped with backward, weak scaling: bs32 per GPU).
 
@@ -36,6 +38,10 @@ BF16_MFMA_PEAK_TFLOPS = 2516.6
 S3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6.0
 HBM_PEAK_GBS = 8000.0
 FLOP_PER_IMAGE_480x640_F64 = 1.353646e12   # fwd + dgrad + wgrad
+WORKLOADS = {2: "baseline_unet train step, configs[1]: bs32/GPU 480x640 fp32 SI-only loss",
+             3: "ray+FiLM conditioned U-Net train step, configs[2]: bs32/GPU 480x640 bf16 GEMMs, full loss",
+             4: "baseline_unet train step, configs[3]: bs32/GPU 480x640 bf16 GEMMs, full loss, DP over RCCL"}
+PRESETS = {2: ("baseline", "fp32"), 3: ("rayfilm", "bf16"), 4: ("baseline", "bf16")}
 
 
 def log(*a):
@@ -51,23 +57,36 @@ def parse():
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--features", type=int, default=64)
-    ap.add_argument("--weights", default="1,0,0,0", help="si,grad,smooth,reproj (configs[1]: SI only)")
+    ap.add_argument("--weights", default=None, help="si,grad,smooth,reproj (configs[1]: SI only 1,0,0,0)")
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4),
+                    help="BASELINE.json configs[i-1]: 2 = baseline_unet fp32 SI-only (default); 3 = ray+FiLM "
+                         "conditioned U-Net, bf16, full loss; 4 = baseline_unet bf16 full loss (DP over --gpus)")
+    ap.add_argument("--model", default=None, choices=("baseline", "film", "rayfilm"))
+    ap.add_argument("--dtype", default=None, choices=("fp32", "bf16"),
+                    help="GEMM arithmetic: fp32 (S3 engine, fp32-accurate) or bf16 operands / fp32 accumulation")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-batch", type=int, default=2)
     ap.add_argument("--cpu-sample-steps", type=int, default=2)
-    return ap.parse_args()
+    a = ap.parse_args()
+    preset = {2: ("baseline", "fp32", "1,0,0,0"), 3: ("rayfilm", "bf16", "1,0.1,0.001,0.01"),
+              4: ("baseline", "bf16", "1,0.1,0.001,0.01")}[a.config]
+    a.model = a.model or preset[0]
+    a.dtype = a.dtype or preset[1]
+    a.weights = a.weights or preset[2]
+    return a
 
 
 def cpu_baseline(args):
     """Reference LibTorch CPU path on a bounded sample of the same workload (host cores)."""
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     B, H, W, f = args.cpu_sample_batch, args.height, args.width, args.features
-    sample = f"bs{B} {H}x{W} f={f} weights {args.weights}, 1 warm-up + {args.cpu_sample_steps} timed train steps"
+    sample = (f"{args.model} bs{B} {H}x{W} f={f} weights {args.weights}, fp32 (the reference's only precision), "
+              f"1 warm-up + {args.cpu_sample_steps} timed train steps")
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
     if os.path.exists(harness):
         cmd = [harness, "--mode", "time", "--f", str(f), "--B", str(B), "--H", str(H), "--W", str(W),
                "--steps", str(args.cpu_sample_steps), "--warmup", "1", "--threads", str(threads),
-               "--weights", args.weights]
+               "--weights", args.weights, "--model", args.model]
         try:
             out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, check=True).stdout
             r = json.loads(out.strip().splitlines()[-1])
@@ -142,7 +161,11 @@ def main():
     from cad_amd import synthetic
     B, H, W, f = args.batch, args.height, args.width, args.features
     w = tuple(float(x) for x in args.weights.split(","))
-    model = cad.BaselineUNet(3, f, 10.0, batch=B, height=H, width=W, device=local)
+    lib = cad.load_library()
+    assert lib.cad_set_gemm_engine(2 if args.dtype == "bf16" else 1) == 0   # CAD_GEMM_BF16 / CAD_GEMM_S3
+    cls = {"baseline": cad.BaselineUNet, "film": cad.IntrinsicsConditionedUNet,
+           "rayfilm": cad.RayConditionedUNet}[args.model]
+    model = cls(3, f, max_depth=10.0, batch=B, height=H, width=W, device=local)
     if world > 1:
         dist.broadcast(model.flat_params, 0)   # identical replicas (DDP semantics)
     loss = cad.CombinedDepthLoss(*w, batch=B, height=H, width=W, device=local)
@@ -156,7 +179,6 @@ def main():
     for i in range(args.warmup):
         trainer.train_step(rgb, gt, K)
     torch.cuda.synchronize(dev)
-    lib = cad.load_library()
     lib.cad_profile_reset()
     lib.cad_profile_enable(1)
     if world > 1:
@@ -191,13 +213,14 @@ def main():
         roof = None
         if dom:
             achieved = dom["gflop"] / dom["ms"]   # GFLOP/ms == TFLOP/s
-            s3 = "_s3<" in dom["name"]
-            peak = S3_PEAK_TFLOPS if s3 else FP32_MFMA_PEAK_TFLOPS
+            s3, b1 = "_s3<" in dom["name"], "_bf16<" in dom["name"]
+            peak = S3_PEAK_TFLOPS if s3 else BF16_MFMA_PEAK_TFLOPS if b1 else FP32_MFMA_PEAK_TFLOPS
             roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": round(peak, 1), "unit": "TFLOP/s",
                     "frac": round(achieved / peak, 4), "traffic": pmc_traffic(dom["name"]),
                     "arith": ("fp32 via exact 3-way bf16 split, 6 bf16 MFMA products per fp32 MAC: peak = dense "
                               "bf16 MFMA 2516.6 / 6; achieved counts algorithmic fp32 FLOPs") if s3 else
-                             "fp32 MFMA (v_mfma_f32_32x32x2_f32)",
+                             ("bf16 operands, fp32 accumulation (v_mfma_f32_32x32x16_bf16): peak = dense bf16 MFMA")
+                             if b1 else "fp32 MFMA (v_mfma_f32_32x32x2_f32)",
                     "kernel": dom["name"], "launches_per_step": dom["launches"] // args.steps,
                     "avg_launch_ms": round(dom["ms"] / dom["launches"], 4),
                     "gflop_per_launch": round(dom["gflop"] / dom["launches"], 3)}
@@ -205,7 +228,8 @@ def main():
             tot_gf = sum(r["gflop"] for r in prof)
             roof["all_gemm_kernels"] = {"tflops": round(tot_gf / tot_ms, 3), "ms_per_step": round(tot_ms / args.steps, 3),
                                         "share_of_step": round(tot_ms / args.steps / ms_per_step, 4)}
-        step_tflops = FLOP_PER_IMAGE_480x640_F64 * value / 1e12 if (H, W, f) == (480, 640, 64) else None
+        step_tflops = (FLOP_PER_IMAGE_480x640_F64 * value / 1e12
+                       if (H, W, f, args.model) == (480, 640, 64, "baseline") else None)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
@@ -215,8 +239,10 @@ def main():
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "fp32", "data": "synthetic (SUN-RGB-D-shaped, HBM-resident)",
-            "config": {"workload": "baseline_unet train step, configs[1]: bs32/GPU 480x640 fp32 SI-only loss",
+            "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (SUN-RGB-D-shaped, HBM-resident)",
+            "config": {"workload": WORKLOADS[args.config] if (args.model, args.dtype) == PRESETS[args.config] else
+                       f"{args.model} train step, {args.dtype} GEMMs, bs{B}/GPU {H}x{W}, loss weights {args.weights}",
+                       "model": args.model,
                        "global_batch": B * world, "height": H, "width": W, "init_features": f,
                        "params": model.count_parameters(), "loss_weights": list(w),
                        "parallelism": f"dp{world}", "optimizer": "adam(lr1e-4,wd1e-5)+clip1.0"},

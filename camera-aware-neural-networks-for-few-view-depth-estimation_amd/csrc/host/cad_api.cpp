@@ -654,7 +654,7 @@ extern "C" {
 int cad_abi_version(void) { return CAD_ABI_VERSION; }
 cad_status cad_set_gemm_engine(int engine) {
     return guard([&] {
-        require(engine == CAD_GEMM_F32 || engine == CAD_GEMM_S3, "unknown GEMM engine");
+        require(engine == CAD_GEMM_F32 || engine == CAD_GEMM_S3 || engine == CAD_GEMM_BF16, "unknown GEMM engine");
         cad::set_gemm_engine(engine);
     });
 }

@@ -115,51 +115,73 @@ __global__ __launch_bounds__(256) void k_convT_wgrad(GemmArgs a) {
         EpiSlab{});
 }
 
-// ---- S3 engine (gemm_s3.hpp): fp32 operands split exactly into 3 bf16 terms ----
-template <int WM, int WN, int KB, class Epi>
-__global__ __launch_bounds__(256) void k_conv3x3_fwd_s3(GemmArgs a) {
+// ---- S3 / B1 engines (gemm_s3.hpp): NP = 3 exact bf16 planes (fp32 accuracy) or 1 rounded plane
+// (bf16 operands).  The __global__ wrappers carry distinct names per engine (rocprof symbols). ----
+template <int NP, int WM, int WN, int KB, class Epi>
+__device__ __forceinline__ void conv3x3_fwd_np(const GemmArgs& a) {
     using LA = KcIm2col3x3<64 * WM, KB, false>;
     using LB = KcDense<64 * WN, KB>;
-    gemm_body_s3<WM, WN, KB, LA, LB>(
+    gemm_body_s3<NP, WM, WN, KB, LA, LB>(
         a,
         [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.a_cin, a.B, a.H, a.W, r0, t, kb); },
         [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, Epi{});
 }
-template <int WM, int WN, int KB>
-__global__ __launch_bounds__(256) void k_convT_fwd_s3(GemmArgs a) {
+template <int NP, int WM, int WN, int KB>
+__device__ __forceinline__ void convT_fwd_np(const GemmArgs& a) {
     using LA = KcDense<64 * WM, KB>;
     using LB = KcDense<64 * WN, KB>;
-    gemm_body_s3<WM, WN, KB, LA, LB>(
+    gemm_body_s3<NP, WM, WN, KB, LA, LB>(
         a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t, kb); },
         [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, EpiConvT{});
 }
-template <int WM, int WN, int KB>
-__global__ __launch_bounds__(256) void k_convT_dgrad_s3(GemmArgs a) {
+template <int NP, int WM, int WN, int KB>
+__device__ __forceinline__ void convT_dgrad_np(const GemmArgs& a) {
     using LA = KcUpGather<64 * WM, KB>;
     using LB = KcDense<64 * WN, KB>;
-    gemm_body_s3<WM, WN, KB, LA, LB>(
+    gemm_body_s3<NP, WM, WN, KB, LA, LB>(
         a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.a_cin, a.B, a.H, a.W, r0, t, kb); },
         [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, EpiStore{});
 }
-
-template <int WM, int WN, int KB>
-__global__ __launch_bounds__(256) void k_conv3x3_wgrad_s3(GemmArgs a) {
+template <int NP, int WM, int WN, int KB>
+__device__ __forceinline__ void conv3x3_wgrad_np(const GemmArgs& a) {
     using LA = MNcDense<64 * WM, KB>;
     using LB = MNcIm2col3x3<64 * WN, KB, false>;
-    gemm_body_s3m<WM, WN, KB, LA, LB>(
+    gemm_body_s3m<NP, WM, WN, KB, LA, LB>(
         a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t, kb); },
         [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.b_cin, a.B, a.H, a.W, r0, t, kb); },
         EpiSlab{});
 }
-template <int WM, int WN, int KB>
-__global__ __launch_bounds__(256) void k_convT_wgrad_s3(GemmArgs a) {
+template <int NP, int WM, int WN, int KB>
+__device__ __forceinline__ void convT_wgrad_np(const GemmArgs& a) {
     using LA = MNcDense<64 * WM, KB>;
     using LB = MNcUpGather<64 * WN, KB>;
-    gemm_body_s3m<WM, WN, KB, LA, LB>(
+    gemm_body_s3m<NP, WM, WN, KB, LA, LB>(
         a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t, kb); },
         [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.b_cin, a.B, a.H, a.W, r0, t, kb); },
         EpiSlab{});
 }
+
+template <int WM, int WN, int KB, class Epi>
+__global__ __launch_bounds__(256) void k_conv3x3_fwd_s3(GemmArgs a) { conv3x3_fwd_np<3, WM, WN, KB, Epi>(a); }
+template <int WM, int WN, int KB>
+__global__ __launch_bounds__(256) void k_convT_fwd_s3(GemmArgs a) { convT_fwd_np<3, WM, WN, KB>(a); }
+template <int WM, int WN, int KB>
+__global__ __launch_bounds__(256) void k_convT_dgrad_s3(GemmArgs a) { convT_dgrad_np<3, WM, WN, KB>(a); }
+template <int WM, int WN, int KB>
+__global__ __launch_bounds__(256) void k_conv3x3_wgrad_s3(GemmArgs a) { conv3x3_wgrad_np<3, WM, WN, KB>(a); }
+template <int WM, int WN, int KB>
+__global__ __launch_bounds__(256) void k_convT_wgrad_s3(GemmArgs a) { convT_wgrad_np<3, WM, WN, KB>(a); }
+
+template <int WM, int WN, int KB, class Epi>
+__global__ __launch_bounds__(256) void k_conv3x3_fwd_bf16(GemmArgs a) { conv3x3_fwd_np<1, WM, WN, KB, Epi>(a); }
+template <int WM, int WN, int KB>
+__global__ __launch_bounds__(256) void k_convT_fwd_bf16(GemmArgs a) { convT_fwd_np<1, WM, WN, KB>(a); }
+template <int WM, int WN, int KB>
+__global__ __launch_bounds__(256) void k_convT_dgrad_bf16(GemmArgs a) { convT_dgrad_np<1, WM, WN, KB>(a); }
+template <int WM, int WN, int KB>
+__global__ __launch_bounds__(256) void k_conv3x3_wgrad_bf16(GemmArgs a) { conv3x3_wgrad_np<1, WM, WN, KB>(a); }
+template <int WM, int WN, int KB>
+__global__ __launch_bounds__(256) void k_convT_wgrad_bf16(GemmArgs a) { convT_wgrad_np<1, WM, WN, KB>(a); }
 
 // deterministic split-K reduction: dst[e] = sum_z slab[z][e]
 __global__ void k_slab_reduce(const float* __restrict__ slab, int nsplit, int64_t stride,
@@ -271,19 +293,40 @@ CAD_KT(KConvTFwd3, (k_convT_fwd_s3<WM, WN, KB>), "void cad::k_convT_fwd_s3<%d, %
 CAD_KT(KConvTDgrad3, (k_convT_dgrad_s3<WM, WN, KB>), "void cad::k_convT_dgrad_s3<%d, %d, %d>(cad::GemmArgs)")
 CAD_KT(KConvWgrad3, (k_conv3x3_wgrad_s3<WM, WN, KB>), "void cad::k_conv3x3_wgrad_s3<%d, %d, %d>(cad::GemmArgs)")
 CAD_KT(KConvTWgrad3, (k_convT_wgrad_s3<WM, WN, KB>), "void cad::k_convT_wgrad_s3<%d, %d, %d>(cad::GemmArgs)")
+CAD_KT(KConvFwdB, (k_conv3x3_fwd_bf16<WM, WN, KB, EpiStore>), "void cad::k_conv3x3_fwd_bf16<%d, %d, %d, cad::EpiStore>(cad::GemmArgs)")
+CAD_KT(KConvFwdSB, (k_conv3x3_fwd_bf16<WM, WN, KB, EpiStoreStats>),
+       "void cad::k_conv3x3_fwd_bf16<%d, %d, %d, cad::EpiStoreStats>(cad::GemmArgs)")
+CAD_KT(KConvTFwdB, (k_convT_fwd_bf16<WM, WN, KB>), "void cad::k_convT_fwd_bf16<%d, %d, %d>(cad::GemmArgs)")
+CAD_KT(KConvTDgradB, (k_convT_dgrad_bf16<WM, WN, KB>), "void cad::k_convT_dgrad_bf16<%d, %d, %d>(cad::GemmArgs)")
+CAD_KT(KConvWgradB, (k_conv3x3_wgrad_bf16<WM, WN, KB>), "void cad::k_conv3x3_wgrad_bf16<%d, %d, %d>(cad::GemmArgs)")
+CAD_KT(KConvTWgradB, (k_convT_wgrad_bf16<WM, WN, KB>), "void cad::k_convT_wgrad_bf16<%d, %d, %d>(cad::GemmArgs)")
 #undef CAD_KT
 
-// GEMM engine for the k-contiguous (forward / dgrad) contractions: 0 = exact f32 MFMA,
-// 1 = S3 (bf16 matrix cores, exact 3-term split; gemm_s3.hpp) — the default: fp32 accuracy
-// (tests/test_gpu_ops.py) at 1.35-1.4x the f32 engine's speed on MI355X.  Process-wide;
-// CAD_GEMM=f32|s3 sets the initial value.
+// GEMM engine of every conv / ConvT contraction: 0 = exact f32 MFMA, 1 = S3 (bf16 matrix cores,
+// exact 3-term split; gemm_s3.hpp) — the default: fp32 accuracy (tests/test_gpu_ops.py) at
+// 1.35-1.4x the f32 engine's speed on MI355X; 2 = B1 (operands rounded to bf16, one product, fp32
+// accumulation: the bf16 configs 3-5).  Process-wide; CAD_GEMM=f32|s3|bf16 sets the initial value.
 int g_engine = -1;
 int engine() {
     if (g_engine < 0) {
         const char* e = std::getenv("CAD_GEMM");
-        g_engine = (e && e[0] == 'f') ? 0 : 1;
+        g_engine = (e && e[0] == 'f') ? 0 : (e && e[0] == 'b') ? 2 : 1;
     }
     return g_engine;
+}
+// B1 stage depth (two k16 steps per LDS stage by default; CAD_BF16_KB=16|32)
+int bf16_kb() {
+    static int kb = 0;
+    if (!kb) {
+        const char* e = std::getenv("CAD_BF16_KB");
+        kb = (e && std::atoi(e) == 16) ? 16 : 32;
+    }
+    return kb;
+}
+template <template <int, int, int> class KT>
+void launch_b1(Cfg c, const GemmArgs& a, int splits, hipStream_t st) {
+    if (bf16_kb() == 16) launch_cfg_kb<KT, 16>(c, a, splits, st);
+    else launch_cfg_kb<KT, 32>(c, a, splits, st);
 }
 constexpr int kS3KB = 16;   // S3 stage depth (LDS: 3 bf16 planes per operand)
 // S3 stage depth: one bf16 k16 step per LDS stage (32 measured 12-13% slower: the LDS footprint
@@ -346,6 +389,11 @@ void conv3x3_fwd(const float* x, int64_t ldx, int xcoff, int cin, const float* w
     a.stats = stats;
     a.a_sc = in_scale; a.a_sh = in_shift;
     const Cfg c = pick_cfg(a.M, a.N);
+    if (engine() == 2 && !in_scale) {
+        a.kstages_per_split = cdiv(a.K, bf16_kb());
+        if (stats) launch_b1<KConvFwdSB>(c, a, 1, st); else launch_b1<KConvFwdB>(c, a, 1, st);
+        return;
+    }
     if (engine() == 1 && !in_scale) {
         const int kb = s3_kb(stats ? K_FWDS : K_FWD, c);
         a.kstages_per_split = cdiv(a.K, kb);
@@ -361,7 +409,7 @@ void conv3x3_fwd(const float* x, int64_t ldx, int xcoff, int cin, const float* w
     }
 }
 
-void set_gemm_engine(int e) { g_engine = e == 1 ? 1 : 0; }
+void set_gemm_engine(int e) { g_engine = (e == 1 || e == 2) ? e : 0; }
 int gemm_engine() { return engine(); }
 
 int conv3x3_stats_rows(int B, int H, int W, int cout) {
@@ -378,6 +426,11 @@ void convT_fwd(const float* x, int64_t ldx, int cin, const float* wf, const floa
     a.Bm = wf; a.ldb = cin;
     a.C = y; a.ldc = ldy; a.c_coff = ycoff; a.bias = bias;
     const Cfg c = pick_cfg(a.M, a.N);
+    if (engine() == 2) {
+        a.kstages_per_split = cdiv(a.K, bf16_kb());
+        launch_b1<KConvTFwdB>(c, a, 1, st);
+        return;
+    }
     if (engine() == 1) {
         const int kb = s3_kb(K_TFWD, c);
         a.kstages_per_split = cdiv(a.K, kb);
@@ -398,6 +451,11 @@ void conv3x3_dgrad(const float* dz, int cout, const float* wd, int cin, float* d
     a.Bm = wd; a.ldb = 9 * cout;
     a.C = dx; a.ldc = lddx; a.c_coff = 0;
     const Cfg c = pick_cfg(a.M, a.N);
+    if (engine() == 2) {
+        a.kstages_per_split = cdiv(a.K, bf16_kb());
+        launch_b1<KConvFwdB>(c, a, 1, st);
+        return;
+    }
     if (engine() == 1) {
         const int kb = s3_kb(K_FWD, c);
         a.kstages_per_split = cdiv(a.K, kb);
@@ -418,6 +476,11 @@ void convT_dgrad(const float* g, int64_t ldg, int gcoff, int cout, const float* 
     a.Bm = wm; a.ldb = 4 * cout;
     a.C = dx; a.ldc = cin; a.c_coff = 0;
     const Cfg c = pick_cfg(a.M, a.N);
+    if (engine() == 2) {
+        a.kstages_per_split = cdiv(a.K, bf16_kb());
+        launch_b1<KConvTDgradB>(c, a, 1, st);
+        return;
+    }
     if (engine() == 1) {
         const int kb = s3_kb(K_TDGRAD, c);
         a.kstages_per_split = cdiv(a.K, kb);
@@ -450,15 +513,16 @@ void conv3x3_wgrad(const float* dz, int cout, const float* x, int64_t ldx, int x
     a.Bm = x; a.ldb = ldx; a.b_coff = xcoff; a.b_cin = cin;
     a.b_sc = x_scale; a.b_sh = x_shift;
     const Cfg c = pick_cfg(a.M, a.N);
-    const bool s3 = engine() == 1 && !x_scale;
-    const int kb = s3 ? s3_kb(K_WGRAD, c) : kb_for(K_WGRAD, c);
+    const bool s3 = engine() == 1 && !x_scale, b1 = engine() == 2 && !x_scale;
+    const int kb = b1 ? bf16_kb() : s3 ? s3_kb(K_WGRAD, c) : kb_for(K_WGRAD, c);
     int s = plan_splits(a, c, kb, slab_cap, 4 * std::max<int64_t>(a.lda, ldx));
     a.kstages_per_split = cdiv(cdiv(a.K, kb), s);
     s = cdiv(cdiv(a.K, kb), a.kstages_per_split);
     const int64_t per = (int64_t)a.M * a.N;
     a.ldc = a.N; a.slab_stride = per;
     a.C = s == 1 ? dw : slab;
-    if (s3) launch_s3<KConvWgrad3>(c, kb, a, s, st);
+    if (b1) launch_b1<KConvWgradB>(c, a, s, st);
+    else if (s3) launch_s3<KConvWgrad3>(c, kb, a, s, st);
     else if (x_scale) launch_cfg<KConvWgradBN>(c, kb, a, s, st);
     else launch_cfg<KConvWgrad>(c, kb, a, s, st);
     if (s > 1) finish_slabs(slab, s, per, dw, st);
@@ -472,15 +536,16 @@ void convT_wgrad(const float* x, int cin, const float* g, int64_t ldg, int gcoff
     a.A = x; a.lda = cin; a.a_coff = 0;
     a.Bm = g; a.ldb = ldg; a.b_coff = gcoff; a.b_cin = cout;
     const Cfg c = pick_cfg(a.M, a.N);
-    const bool s3 = engine() == 1;
-    const int kb = s3 ? s3_kb(K_TWGRAD, c) : kb_for(K_TWGRAD, c);
+    const bool s3 = engine() == 1, b1 = engine() == 2;
+    const int kb = b1 ? bf16_kb() : s3 ? s3_kb(K_TWGRAD, c) : kb_for(K_TWGRAD, c);
     int s = plan_splits(a, c, kb, slab_cap, 4 * std::max<int64_t>(a.lda, 4 * ldg));
     a.kstages_per_split = cdiv(cdiv(a.K, kb), s);
     s = cdiv(cdiv(a.K, kb), a.kstages_per_split);
     const int64_t per = (int64_t)a.M * a.N;
     a.ldc = a.N; a.slab_stride = per;
     a.C = s == 1 ? dw : slab;
-    if (s3) launch_s3<KConvTWgrad3>(c, kb, a, s, st);
+    if (b1) launch_b1<KConvTWgradB>(c, a, s, st);
+    else if (s3) launch_s3<KConvTWgrad3>(c, kb, a, s, st);
     else launch_cfg<KConvTWgrad>(c, kb, a, s, st);
     if (s > 1) finish_slabs(slab, s, per, dw, st);
 }

@@ -1,4 +1,5 @@
-// fp32 GEMM on the bf16 matrix cores by exact operand splitting ("S3" engine).
+// fp32 GEMM on the bf16 matrix cores by exact operand splitting ("S3" engine), and the plain bf16
+// engine ("B1") that shares its staging.
 //
 // Every fp32 operand x is split EXACTLY into three bf16 terms, x = x0 + x1 + x2:
 //   x0 = x with the low 16 bits cleared (8 significant bits), r = x - x0 (exact, <= 16 bits),
@@ -11,13 +12,20 @@
 // per 16-deep k step instead of 8 f32 MFMAs of 64 cycles: 2.67x fewer matrix-core cycles.
 // Inf/NaN operands give NaN (the split of an infinity is inf - inf); the hot path never carries them.
 //
+// B1 (NP = 1 plane): each fp32 operand is rounded to the nearest bf16 (v_cvt_pk_bf16_f32) and one
+// product per k is issued — bf16 operands, fp32 accumulation: the arithmetic of BASELINE configs
+// 3-5 ("bf16").  Its result equals the fp64 contraction of the bf16-rounded operands up to fp32
+// accumulation error (tests/test_gpu_ops.py).
+//
 // Staging: the Kc loaders of gemm_mfma.hpp (k-contiguous global rows, float4 per thread) fill
-// registers; the stage store splits each float4 into three bf16x4 and writes three LDS planes
-// [rows][16] (32-B rows, no padding: the 16-B half h of row r is stored at half h ^ ((r >> 3) & 1),
-// which makes the ds_read_b128 fragment reads conflict-free in all four lane groups of the
-// instruction, MI355X_MICROARCH.md §LDS).  Unpadded planes keep a 128x128 tile at 48 KB of LDS
-// (double-buffered), three workgroups per CU.  Fragment of a 32x32x16 MFMA: lane l holds
-// A[row l&31][k = 8(l>>5) + j], j < 8 (one ds_read_b128 per plane); B likewise by column.
+// registers; the stage store converts each float4 into NP bf16x4 and writes NP LDS planes.
+// KB = 16 (one k16 step per stage): 32-B rows, no padding, the 16-B half h of row r is stored at
+// half h ^ ((r >> 3) & 1), which makes the ds_read_b128 fragment reads conflict-free in all four
+// lane groups of the instruction (MI355X_MICROARCH.md §LDS).  Unpadded planes keep a 128x128 S3
+// tile at 48 KB of LDS (double-buffered), three workgroups per CU.  KB = 32 (two k16 steps, B1):
+// rows padded to 40 bf16 = 80 B, the conflict-free b128 stride of the f32 engine's Kc image.
+// Fragment of a 32x32x16 MFMA: lane l holds A[row l&31][k = 8(l>>5) + j], j < 8 (one
+// ds_read_b128 per plane); B likewise by column.
 #pragma once
 #include "gemm_mfma.hpp"
 
@@ -50,33 +58,59 @@ __device__ __forceinline__ Split4 split3(float4 v) {
     return s;
 }
 
+// one round-to-nearest-even bf16x4 plane of one float4 (B1)
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+struct Split1 {
+    uint2 p[1];
+};
+__device__ __forceinline__ Split1 split1(float4 v) {
+    const bf16x2_t lo = __builtin_convertvector((f32x2_t){v.x, v.y}, bf16x2_t);
+    const bf16x2_t hi = __builtin_convertvector((f32x2_t){v.z, v.w}, bf16x2_t);
+    Split1 s;
+    s.p[0] = make_uint2(__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi));
+    return s;
+}
+template <int NP>
+__device__ __forceinline__ auto split_np(float4 v) {
+    static_assert(NP == 3 || NP == 1, "planes");
+    if constexpr (NP == 3) return split3(v);
+    else return split1(v);
+}
+
+// Stage geometry: KB k per LDS stage = KB/16 bf16 MFMA k-steps.
 template <int KB>
 struct S3 {
-    static_assert(KB == 16, "S3 stage depth: one bf16 MFMA k step (16) per LDS stage");
-    static constexpr int LDK = 16;              // bf16 elements per plane row (32 B, swizzled)
-    static constexpr int KSTEPS = 1;
+    static_assert(KB == 16 || KB == 32, "S3/B1 stage depth");
+    static constexpr bool SWZ = KB == 16;
+    static constexpr int LDK = SWZ ? 16 : KB + 8;   // bf16 elements per plane row
+    static constexpr int KSTEPS = KB / 16;
 };
 
-// LDS bytes of one operand image: 3 planes x ROWS x 16 bf16
-template <int ROWS, int KB>
+// LDS bf16 elements of one operand image: NP planes x ROWS x LDK
+template <int ROWS, int KB, int NP = 3>
 struct S3Lds {
-    static constexpr int ELEMS = 3 * ROWS * S3<KB>::LDK;   // bf16 elements
+    static constexpr int ELEMS = NP * ROWS * S3<KB>::LDK;
 };
-// element offset of (row r, k) in a swizzled plane
-__device__ __forceinline__ int s3_off(int r, int k) { return r * 16 + (((k >> 3) ^ ((r >> 3) & 1)) << 3) + (k & 7); }
+// element offset of (row r, k) in a plane
+template <int KB>
+__device__ __forceinline__ int s3_off(int r, int k) {
+    if constexpr (S3<KB>::SWZ) return r * 16 + (((k >> 3) ^ ((r >> 3) & 1)) << 3) + (k & 7);
+    else return r * S3<KB>::LDK + k;
+}
 
-// store the loader's float4s (Kc mapping of KS<KB>) as three bf16 planes
-template <int ROWS, int KB, int NV>
+// store the loader's float4s (Kc mapping of KS<KB>) as NP bf16 planes
+template <int ROWS, int KB, int NP, int NV>
 __device__ __forceinline__ void s3_store(uint16_t* s, const float4 (&v)[NV]) {
     using G = KS<KB>;
     constexpr int PL = ROWS * S3<KB>::LDK;   // elements per plane
     const int t = threadIdx.x;
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
-        const Split4 sp = split3(v[j]);
-        const int off = s3_off(t / G::TPR + G::RPP * j, (t % G::TPR) * 4);
+        const auto sp = split_np<NP>(v[j]);
+        const int off = s3_off<KB>(t / G::TPR + G::RPP * j, (t % G::TPR) * 4);
 #pragma unroll
-        for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(s + p * PL + off) = sp.p[p];
+        for (int p = 0; p < NP; ++p) *reinterpret_cast<uint2*>(s + p * PL + off) = sp.p[p];
     }
 }
 
@@ -87,20 +121,20 @@ __device__ __forceinline__ void kc_store_nat(float* s, const float4 (&v)[NV]) {
     kc_store<ROWS, KB>(s, v);
 }
 
-// fragments of the three planes for 32-row block rb, k16 step q
-template <int ROWS, int KB>
-__device__ __forceinline__ void s3_frag(const uint16_t* s, int rb, int q, bf16x8 (&f)[3]) {
+// fragments of the NP planes for 32-row block rb, k16 step q
+template <int ROWS, int KB, int NP>
+__device__ __forceinline__ void s3_frag(const uint16_t* s, int rb, int q, bf16x8 (&f)[NP]) {
     constexpr int PL = ROWS * S3<KB>::LDK;
     const int lane = threadIdx.x & 63;
-    const uint16_t* base = s + s3_off(rb + (lane & 31), q * 16 + (lane >> 5) * 8);
+    const uint16_t* base = s + s3_off<KB>(rb + (lane & 31), q * 16 + (lane >> 5) * 8);
 #pragma unroll
-    for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const bf16x8*>(base + p * PL);
+    for (int p = 0; p < NP; ++p) f[p] = *reinterpret_cast<const bf16x8*>(base + p * PL);
 }
 
 // A operand kept fp32 in LDS ([rows][KB+4] floats, the Kc image of gemm_mfma.hpp in natural k
-// order) and split after the fragment read: used when every A row is read by ONE wave (WN == 1), so
-// splitting at read costs no more VALU than splitting at store, and the fp32 image is 2/3 the bytes
-// (the 256x64 tile then fits two workgroups per CU).
+// order) and split after the fragment read: used by S3 when every A row is read by ONE wave
+// (WN == 1), so splitting at read costs no more VALU than splitting at store, and the fp32 image is
+// 2/3 the bytes (the 256x64 tile then fits two workgroups per CU).
 template <int ROWS, int KB>
 __device__ __forceinline__ void s3_frag_f32(const float* s, int rb, int q, bf16x8 (&f)[3]) {
     const int lane = threadIdx.x & 63;
@@ -115,16 +149,39 @@ __device__ __forceinline__ void s3_frag_f32(const float* s, int rb, int q, bf16x
     }
 }
 
-// The S3 engine for Kc x Kc operands (conv3x3 fwd/dgrad, ConvT fwd/dgrad).  Same tiling, loaders,
-// pipeline and epilogue as gemm_body (gemm_mfma.hpp); only the LDS image and the MFMA differ.
-// AF32: A staged fp32 and split at fragment read (see s3_frag_f32); requires WN == 1.
-template <int WM, int WN, int KB, class LA, class LB, class Epi, class InitA, class InitB>
+// the MFMAs of one k16 step on NP-plane fragments: S3 issues the six products with p + q <= 2,
+// smallest terms first ((2,0) (1,1) (0,2) (1,0) (0,1) (0,0)); B1 the single bf16 product
+template <int NP>
+__device__ __forceinline__ void s3_mfma(floatx16 (&acc)[2][2], const bf16x8 (&fa)[2][NP], const bf16x8 (&fb)[2][NP]) {
+    if constexpr (NP == 3) {
+        constexpr int P[6] = {2, 1, 0, 1, 0, 0};
+        constexpr int Q[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+        for (int t = 0; t < 6; ++t)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][P[t]], fb[j][Q[t]], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], acc[i][j], 0, 0, 0);
+    }
+}
+
+// The S3/B1 engine for Kc x Kc operands (conv3x3 fwd/dgrad, ConvT fwd/dgrad).  Same tiling,
+// loaders, pipeline and epilogue as gemm_body (gemm_mfma.hpp); only the LDS image and the MFMA
+// differ.  AF32: A staged fp32 and split at fragment read (see s3_frag_f32); S3 with WN == 1 only.
+template <int NP, int WM, int WN, int KB, class LA, class LB, class Epi, class InitA, class InitB>
 __device__ __forceinline__ void gemm_body_s3(const GemmArgs& a, InitA init_a, InitB init_b, Epi epi) {
-    constexpr bool AF32 = WN == 1;
+    constexpr bool AF32 = NP == 3 && WN == 1;
     constexpr int BM = 64 * WM, BN = 64 * WN;
     // LDS element counts in bf16 units (an fp32 A image counts 2 per float)
-    constexpr int SA = AF32 ? 2 * BM * KS<KB>::LDK : S3Lds<BM, KB>::ELEMS;
-    constexpr int SB = S3Lds<BN, KB>::ELEMS;
+    constexpr int SA = AF32 ? 2 * BM * KS<KB>::LDK : S3Lds<BM, KB, NP>::ELEMS;
+    constexpr int SB = S3Lds<BN, KB, NP>::ELEMS;
     __shared__ __attribute__((aligned(16))) uint16_t lds[2 * (SA + SB)];
 
     const int tid = threadIdx.x;
@@ -154,31 +211,22 @@ __device__ __forceinline__ void gemm_body_s3(const GemmArgs& a, InitA init_a, In
         lb.finish(xb);
         uint16_t* da = lds + buf * (SA + SB);
         if constexpr (AF32) kc_store_nat<BM, KB>(reinterpret_cast<float*>(da), xa);
-        else s3_store<BM, KB>(da, xa);
-        s3_store<BN, KB>(da + SA, xb);
+        else s3_store<BM, KB, NP>(da, xa);
+        s3_store<BN, KB, NP>(da + SA, xb);
     };
     auto stage_compute = [&](int buf) {
         const uint16_t* sa = lds + buf * (SA + SB);
         const uint16_t* sb = sa + SA;
 #pragma unroll
         for (int q = 0; q < S3<KB>::KSTEPS; ++q) {
-            bf16x8 fa[2][3], fb[2][3];
+            bf16x8 fa[2][NP], fb[2][NP];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 if constexpr (AF32) s3_frag_f32<BM, KB>(reinterpret_cast<const float*>(sa), wm * 64 + i * 32, q, fa[i]);
-                else s3_frag<BM, KB>(sa, wm * 64 + i * 32, q, fa[i]);
-                s3_frag<BN, KB>(sb, wn * 64 + i * 32, q, fb[i]);
+                else s3_frag<BM, KB, NP>(sa, wm * 64 + i * 32, q, fa[i]);
+                s3_frag<BN, KB, NP>(sb, wn * 64 + i * 32, q, fb[i]);
             }
-            // smallest terms first: (2,0) (1,1) (0,2) (1,0) (0,1) (0,0)
-            constexpr int P[6] = {2, 1, 0, 1, 0, 0};
-            constexpr int Q[6] = {0, 1, 2, 0, 1, 0};
-#pragma unroll
-            for (int t = 0; t < 6; ++t)
-#pragma unroll
-                for (int i = 0; i < 2; ++i)
-#pragma unroll
-                    for (int j = 0; j < 2; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][P[t]], fb[j][Q[t]], acc[i][j], 0, 0, 0);
+            s3_mfma<NP>(acc, fa, fb);
         }
     };
 
@@ -202,13 +250,12 @@ __device__ __forceinline__ void gemm_body_s3(const GemmArgs& a, InitA init_a, In
 }
 
 // ------------------------------------------------------------------------------------------
-// S3 engine for MNc x MNc operands (the weight-gradient GEMMs: k = pixel is the strided index).
-// LDS planes are [KB k-rows][ROWS] bf16 with a 64-B pad per k-row (row stride 192 / 320 / 576 B
-// for 64 / 128 / 256 rows: the four k-rows a transposed read gathers then land on disjoint bank
-// quarters).  The MNc loader's float4 (4 consecutive rows at one k) is split and stored with one
-// ds_write_b64 per plane; fragments are read with ds_read_b64_tr_b16, which hands lane i of each
-// 16-lane group column i of 4 consecutive k-rows: two such reads give a lane its 8 consecutive k of
-// one row — exactly the 32x32x16 operand map — with no register transpose.
+// S3/B1 engine for MNc x MNc operands (the weight-gradient GEMMs: k = pixel is the strided index).
+// LDS planes are [KB k-rows][ROWS] bf16 (see S3M for the row stride / swizzle).  The MNc loader's
+// float4 (4 consecutive rows at one k) is converted and stored with one ds_write_b64 per plane;
+// fragments are read with ds_read_b64_tr_b16, which hands lane i of each 16-lane group column i of
+// 4 consecutive k-rows: two such reads give a lane its 8 consecutive k of one row — exactly the
+// 32x32x16 operand map — with no register transpose.
 // ------------------------------------------------------------------------------------------
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 
@@ -226,22 +273,22 @@ struct S3M {
     }
 };
 
-template <int ROWS, int KB, int NV>
+template <int ROWS, int KB, int NP, int NV>
 __device__ __forceinline__ void s3m_store(char* s, const float4 (&v)[NV]) {
     using Base = MNcBase<ROWS, KB>;
     constexpr int PL = KB * S3M<ROWS>::STRIDE;   // bytes per plane
     const int t = threadIdx.x;
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
-        const Split4 sp = split3(v[j]);
+        const auto sp = split_np<NP>(v[j]);
         const int off = S3M<ROWS>::off(t / Base::TPR + Base::KSTEP * j, (t % Base::TPR) * 4);
 #pragma unroll
-        for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(s + p * PL + off) = sp.p[p];
+        for (int p = 0; p < NP; ++p) *reinterpret_cast<uint2*>(s + p * PL + off) = sp.p[p];
     }
 }
 
-template <int ROWS, int KB>
-__device__ __forceinline__ void s3m_frag(const char* s, int rb, int q, bf16x8 (&f)[3]) {
+template <int ROWS, int KB, int NP>
+__device__ __forceinline__ void s3m_frag(const char* s, int rb, int q, bf16x8 (&f)[NP]) {
     constexpr int PL = KB * S3M<ROWS>::STRIDE;
     const int lane = threadIdx.x & 63;
     const int g = (lane >> 4) & 1, h = lane >> 5, i = lane & 15;
@@ -250,7 +297,7 @@ __device__ __forceinline__ void s3m_frag(const char* s, int rb, int q, bf16x8 (&
     const char* b0 = s + S3M<ROWS>::off(krow, col);       // k-rows 8h + 0..3
     const char* b1 = s + S3M<ROWS>::off(krow + 4, col);   // k-rows 8h + 4..7
 #pragma unroll
-    for (int p = 0; p < 3; ++p) {
+    for (int p = 0; p < NP; ++p) {
         typedef __attribute__((address_space(3))) v4i16 lds_v4;
         const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(b0 + p * PL));
         const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(b1 + p * PL));
@@ -259,10 +306,10 @@ __device__ __forceinline__ void s3m_frag(const char* s, int rb, int q, bf16x8 (&
     }
 }
 
-template <int WM, int WN, int KB, class LA, class LB, class Epi, class InitA, class InitB>
+template <int NP, int WM, int WN, int KB, class LA, class LB, class Epi, class InitA, class InitB>
 __device__ __forceinline__ void gemm_body_s3m(const GemmArgs& a, InitA init_a, InitB init_b, Epi epi) {
     constexpr int BM = 64 * WM, BN = 64 * WN;
-    constexpr int SA = 3 * KB * S3M<BM>::STRIDE, SB = 3 * KB * S3M<BN>::STRIDE;   // bytes
+    constexpr int SA = NP * KB * S3M<BM>::STRIDE, SB = NP * KB * S3M<BN>::STRIDE;   // bytes
     __shared__ __attribute__((aligned(16))) char lds[2 * (SA + SB)];
 
     const int tid = threadIdx.x;
@@ -291,29 +338,21 @@ __device__ __forceinline__ void gemm_body_s3m(const GemmArgs& a, InitA init_a, I
         la.finish(xa);
         lb.finish(xb);
         char* da = lds + buf * (SA + SB);
-        s3m_store<BM, KB>(da, xa);
-        s3m_store<BN, KB>(da + SA, xb);
+        s3m_store<BM, KB, NP>(da, xa);
+        s3m_store<BN, KB, NP>(da + SA, xb);
     };
     auto stage_compute = [&](int buf) {
         const char* sa = lds + buf * (SA + SB);
         const char* sb = sa + SA;
 #pragma unroll
         for (int q = 0; q < S3<KB>::KSTEPS; ++q) {
-            bf16x8 fa[2][3], fb[2][3];
+            bf16x8 fa[2][NP], fb[2][NP];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                s3m_frag<BM, KB>(sa, wm * 64 + i * 32, q, fa[i]);
-                s3m_frag<BN, KB>(sb, wn * 64 + i * 32, q, fb[i]);
+                s3m_frag<BM, KB, NP>(sa, wm * 64 + i * 32, q, fa[i]);
+                s3m_frag<BN, KB, NP>(sb, wn * 64 + i * 32, q, fb[i]);
             }
-            constexpr int P[6] = {2, 1, 0, 1, 0, 0};
-            constexpr int Q[6] = {0, 1, 2, 0, 1, 0};
-#pragma unroll
-            for (int t = 0; t < 6; ++t)
-#pragma unroll
-                for (int i = 0; i < 2; ++i)
-#pragma unroll
-                    for (int j = 0; j < 2; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][P[t]], fb[j][Q[t]], acc[i][j], 0, 0, 0);
+            s3_mfma<NP>(acc, fa, fb);
         }
     };
 

@@ -90,13 +90,16 @@ typedef struct {
 
 /* ---- library ---- */
 int cad_abi_version(void);
-/* GEMM engine of the k-contiguous contractions (conv3x3 forward/dgrad, ConvTranspose forward/dgrad):
+/* GEMM engine of the conv3x3 / ConvTranspose contractions (forward, dgrad, wgrad):
  * CAD_GEMM_F32 = v_mfma_f32_32x32x2_f32 (exact fp32 fmaf chains); CAD_GEMM_S3 = fp32 operands split
  * exactly into three bf16 terms on the bf16 matrix cores, six products accumulated in fp32 (error
- * < 2^-23 |a b| per product: fp32 accuracy).  Process-wide, default CAD_GEMM_S3; the env var
- * CAD_GEMM=f32|s3 sets the initial value. */
+ * < 2^-23 |a b| per product: fp32 accuracy); CAD_GEMM_BF16 = operands rounded to bf16 (nearest
+ * even), one product, fp32 accumulation — the bf16 arithmetic of BASELINE configs 3-5 (activations,
+ * BatchNorm, loss and optimizer stay fp32).  Process-wide, default CAD_GEMM_S3; the env var
+ * CAD_GEMM=f32|s3|bf16 sets the initial value. */
 #define CAD_GEMM_F32 0
 #define CAD_GEMM_S3 1
+#define CAD_GEMM_BF16 2
 cad_status cad_set_gemm_engine(int engine);
 int cad_get_gemm_engine(void);
 const char* cad_last_error(void);

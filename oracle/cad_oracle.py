@@ -232,6 +232,52 @@ def rays_from_K(K, H, W):
     return torch.stack([x / n, y / n, 1.0 / n], 1).contiguous()
 
 
+# GEMM operand precision of the conv / ConvT contractions.  "exact": the reference's fp32 (or the
+# fp64 yardstick).  "bf16": the bf16 configs' arithmetic (BASELINE configs 3-5, cad.h CAD_GEMM_BF16):
+# every contraction multiplies bf16-rounded operands — forward (x, w), dgrad (dy, w) and wgrad
+# (dy, x) — and accumulates in the working dtype; BN, FiLM, the 1x1 head, the loss and the
+# optimizer stay in the working dtype.  Not a reference behaviour (the reference has no bf16 path):
+# the yardstick the GPU bf16 engine is checked against.
+_GEMM = {"operands": "exact"}
+
+
+class _RoundOperand(torch.autograd.Function):
+    """bf16 rounding of a GEMM input in the forward; straight-through gradient."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
+class _RoundGradOperand(torch.autograd.Function):
+    """Identity forward; bf16 rounding of the incoming gradient (the dy operand of dgrad/wgrad)."""
+
+    @staticmethod
+    def forward(ctx, y):
+        return y.view_as(y)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).to(g.dtype)
+
+
+def _conv3x3(x, w):
+    if _GEMM["operands"] == "bf16":
+        return _RoundGradOperand.apply(F.conv2d(_RoundOperand.apply(x), _RoundOperand.apply(w), None, 1, 1))
+    return F.conv2d(x, w, None, 1, 1)
+
+
+def _convT2x2(x, w, b):
+    if _GEMM["operands"] == "bf16":
+        y = _RoundGradOperand.apply(F.conv_transpose2d(_RoundOperand.apply(x), _RoundOperand.apply(w), None, stride=2))
+        return y + b.view(1, -1, 1, 1)
+    return F.conv_transpose2d(x, w, b, stride=2)
+
+
 def _bn(x, p, bufs, prefix, train):
     # torch::nn::BatchNorm2d defaults (eps 1e-5, momentum 0.1, affine, track_running_stats)
     return F.batch_norm(x, bufs[prefix + ".running_mean"], bufs[prefix + ".running_var"],
@@ -255,18 +301,18 @@ def _film(x, c, p, bufs, pre, train):
 def _double_conv(x, p, bufs, pre, train, cam=None):
     # DoubleConvImpl::forward (baseline_unet.h:32-43); with `cam`: FiLMDoubleConvImpl::forward
     # (intrinsics_unet.h:38-52) = RayEnhancedConvImpl::forward after its cat (geometry_aware_network.h:47-64)
-    x = F.conv2d(x, p[pre + "conv1.weight"], None, 1, 1)
+    x = _conv3x3(x, p[pre + "conv1.weight"])
     x = F.relu(_bn(x, p, bufs, pre + "bn1", train))
     if cam is not None:
         x = _film(x, cam, p, bufs, pre + "film.", train)
-    x = F.conv2d(x, p[pre + "conv2.weight"], None, 1, 1)
+    x = _conv3x3(x, p[pre + "conv2.weight"])
     return F.relu(_bn(x, p, bufs, pre + "bn2", train))
 
 
 def _decoder(x, skip, p, bufs, pre, train, cam=None):
     # DecoderBlockImpl::forward (baseline_unet.h:83-102): up, pad-if-needed, cat({skip, up}), conv
     # (FiLMDecoderBlockImpl::forward, intrinsics_unet.h:91-110, is the same with a FiLM conv)
-    x = F.conv_transpose2d(x, p[pre + "up.weight"], p[pre + "up.bias"], stride=2)
+    x = _convT2x2(x, p[pre + "up.weight"], p[pre + "up.bias"])
     dh, dw = skip.shape[2] - x.shape[2], skip.shape[3] - x.shape[3]
     if dh > 0 or dw > 0:
         x = F.pad(x, (dw // 2, dw - dw // 2, dh // 2, dh - dh // 2))
@@ -435,9 +481,11 @@ class Trainer:
     """One replica of TensorBoardTrainerEnhanced's step (enhanced.h:287-304) on host cores."""
 
     def __init__(self, params, buffers, weights=(1.0, 0.1, 0.001, 0.01), lr=1e-4, wd=1e-5,
-                 clip=1.0, max_depth=10.0, dtype=torch.float32, model="baseline"):
-        # dtype=float64 gives the exact-arithmetic yardstick the fp32 paths are both measured against
+                 clip=1.0, max_depth=10.0, dtype=torch.float32, model="baseline", gemm_operands="exact"):
+        # dtype=float64 gives the exact-arithmetic yardstick the fp32 paths are both measured against;
+        # gemm_operands="bf16" the bf16 configs' contraction arithmetic (see _GEMM)
         self.dtype = dtype
+        self.gemm_operands = gemm_operands
         self.model = model
         self.p = OrderedDict((k, v.clone().to(dtype)) for k, v in params.items())
         self.bufs = OrderedDict((k, v.clone().to(dtype)) for k, v in buffers.items())
@@ -449,10 +497,14 @@ class Trainer:
         for v in self.p.values():
             v.requires_grad_(True)
             v.grad = None
-        pred = unet_forward(rgb, self.p, self.bufs, True, self.max_depth, self.model, K)
-        pred.retain_grad()
-        loss, comps = combined_loss(pred, gt, rgb, K, self.weights)
-        loss.sum().backward()
+        prev, _GEMM["operands"] = _GEMM["operands"], self.gemm_operands
+        try:
+            pred = unet_forward(rgb, self.p, self.bufs, True, self.max_depth, self.model, K)
+            pred.retain_grad()
+            loss, comps = combined_loss(pred, gt, rgb, K, self.weights)
+            loss.sum().backward()
+        finally:
+            _GEMM["operands"] = prev
         grads = [v.grad.detach().clone() if v.grad is not None else None for v in self.p.values()]
         for v in self.p.values():
             v.requires_grad_(False)
@@ -472,7 +524,11 @@ class Trainer:
     @torch.no_grad()
     def predict_eval(self, rgb, K=None):
         Kd = K.to(self.dtype) if K is not None else None
-        return unet_forward(rgb.to(self.dtype), self.p, self.bufs, False, self.max_depth, self.model, Kd)
+        prev, _GEMM["operands"] = _GEMM["operands"], self.gemm_operands
+        try:
+            return unet_forward(rgb.to(self.dtype), self.p, self.bufs, False, self.max_depth, self.model, Kd)
+        finally:
+            _GEMM["operands"] = prev
 
 
 def depth_metrics(pred, gt):

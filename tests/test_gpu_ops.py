@@ -16,15 +16,25 @@ pytestmark = pytest.mark.gpu
 TOL = 2e-5
 
 
-@pytest.fixture(params=["f32", "s3"])
+ENGINES = {"f32": 0, "s3": 1, "bf16": 2}
+
+
+@pytest.fixture(params=list(ENGINES))
 def engine(request, cad):
-    """The forward/dgrad contractions run on either GEMM engine (cad.h CAD_GEMM_*): exact fp32 MFMA,
-    or S3 (exact 3-way bf16 split on the bf16 matrix cores); both must meet the same tolerance."""
+    """The contractions run on any GEMM engine (cad.h CAD_GEMM_*): exact fp32 MFMA, S3 (exact 3-way
+    bf16 split on the bf16 matrix cores) or bf16 (operands rounded to bf16, fp32 accumulation).  All
+    meet the same tolerance — for bf16 against the fp64 contraction of the bf16-ROUNDED operands
+    (see q()), i.e. the only admitted error is fp32 accumulation."""
     lib = cad.load_library()
     prev = lib.cad_get_gemm_engine()
-    assert lib.cad_set_gemm_engine(0 if request.param == "f32" else 1) == 0
+    assert lib.cad_set_gemm_engine(ENGINES[request.param]) == 0
     yield request.param
     lib.cad_set_gemm_engine(prev)
+
+
+def q(t, engine):
+    """The operand values the engine multiplies: bf16 round-to-nearest-even for the bf16 engine."""
+    return t.bfloat16().float() if engine == "bf16" else t
 
 
 def _p(t):
@@ -58,7 +68,7 @@ def test_conv3x3_fwd_dgrad_wgrad(cad, dev, engine, B, H, W, cin, cout):
     x = torch.randn(B, cin, H, W, generator=g)
     w = torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)
     dy = torch.randn(B, cout, H, W, generator=g)
-    xd, wd, dyd = x.double().requires_grad_(), w.double().requires_grad_(), dy.double()
+    xd, wd, dyd = q(x, engine).double().requires_grad_(), q(w, engine).double().requires_grad_(), q(dy, engine).double()
     y_ref = F.conv2d(xd, wd, None, 1, 1)
     y_ref.backward(dyd)
     # forward, written at channel offset 4 of a wider row (concat-buffer view)
@@ -111,9 +121,9 @@ def test_convT(cad, dev, engine, B, H, W, cin, cout):
     w = torch.randn(cin, cout, 2, 2, generator=g) / cin ** 0.5
     b = torch.randn(cout, generator=g)
     dy = torch.randn(B, cout, 2 * H, 2 * W, generator=g)
-    xd, wdd, bd = x.double().requires_grad_(), w.double().requires_grad_(), b.double().requires_grad_()
+    xd, wdd, bd = q(x, engine).double().requires_grad_(), q(w, engine).double().requires_grad_(), b.double().requires_grad_()
     y_ref = F.conv_transpose2d(xd, wdd, bd, stride=2)
-    y_ref.backward(dy.double())
+    y_ref.backward(q(dy, engine).double())
     wg = w.permute(0, 2, 3, 1).contiguous().to(dev)   # [ci][dy][dx][co]
     # forward into the "up" half of a concat buffer
     ybuf = torch.zeros(B, 2 * H, 2 * W, 2 * cout, device=dev)
