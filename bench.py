@@ -149,11 +149,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    # CAD_BENCH_DEVICE / CAD_DIST_BACKEND: rehearsal of the N>1 path on a 1-GPU box (every rank on
+    # one device, gloo) — never set for the driver's runs (one rank per GPU over RCCL)
+    local = int(os.environ.get("CAD_BENCH_DEVICE", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pg = None
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("CAD_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
         pg = dist.group.WORLD
 
     import cad_pkg

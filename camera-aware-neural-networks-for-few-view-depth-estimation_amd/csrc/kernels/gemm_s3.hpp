@@ -38,6 +38,16 @@ struct Split4 {
     uint2 p[3];
 };
 __device__ __forceinline__ Split4 split3(float4 v) {
+#ifdef CAD_S3_FAKESPLIT   // timing experiment only: WRONG numerics, near-zero split VALU
+    {
+        const uint32_t a = __float_as_uint(v.x), b = __float_as_uint(v.y), c = __float_as_uint(v.z), d = __float_as_uint(v.w);
+        Split4 s;
+        s.p[0] = make_uint2(__builtin_amdgcn_perm(b, a, 0x07060302u), __builtin_amdgcn_perm(d, c, 0x07060302u));
+        s.p[1] = make_uint2(__builtin_amdgcn_perm(b, a, 0x05040100u), __builtin_amdgcn_perm(d, c, 0x05040100u));
+        s.p[2] = s.p[1];
+        return s;
+    }
+#endif
     const float x[4] = {v.x, v.y, v.z, v.w};
     uint32_t h[4], m[4], l[4];
 #pragma unroll
