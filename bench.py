@@ -220,7 +220,9 @@ def main():
         roof = None
         if dom:
             achieved = dom["gflop"] / dom["ms"]   # GFLOP/ms == TFLOP/s
-            s3, b1 = "_s3<" in dom["name"], "_bf16<" in dom["name"]
+            kname = dom["name"].split("<")[0]   # k_<op>_<engine>[p][L]: p = pre-split operands, L = large tile
+            s3 = kname.endswith(("_s3", "_s3p", "_s3L", "_s3pL"))
+            b1 = kname.endswith(("_bf16", "_bf16p", "_bf16L", "_bf16pL"))
             peak = S3_PEAK_TFLOPS if s3 else BF16_MFMA_PEAK_TFLOPS if b1 else FP32_MFMA_PEAK_TFLOPS
             roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": round(peak, 1), "unit": "TFLOP/s",
                     "frac": round(achieved / peak, 4), "traffic": pmc_traffic(dom["name"]),

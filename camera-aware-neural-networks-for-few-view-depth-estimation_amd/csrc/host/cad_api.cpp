@@ -115,6 +115,7 @@ struct BN {
 struct Conv {
     int pidx = -1, cin = 0, cout = 0;
     float* wd = nullptr;   // dgrad repack
+    void *ws = nullptr, *wds = nullptr;   // pre-split weights / dgrad repack (cin % 8 == 0 only)
 };
 struct Film {
     int p0 = -1;   // index of film.fc1.weight; the 12 FiLM parameters follow in registration order
@@ -127,12 +128,14 @@ struct DoubleConv {
     Film film;     // film.p0 < 0: plain DoubleConv
     int level = 0;
     float *y1 = nullptr, *a1 = nullptr, *y2 = nullptr;
+    void* a1s = nullptr;   // pre-split a1 (gemm_ps.hpp)
     int first_param = 0, last_param = 0;   // [first, last] indices in named_parameters()
     bool has_film() const { return film.p0 >= 0; }
 };
 struct Up {
     int widx = -1, bidx = -1, cin = 0, cout = 0;
     float* wf = nullptr;   // forward repack [q][co][ci]
+    void *wfs = nullptr, *wms = nullptr;   // pre-split forward repack / weights [ci][q][co]
 };
 
 }  // namespace
@@ -170,6 +173,16 @@ struct cad_unet {
     float* a2_bott = nullptr;
     float* dout[4] = {};   // decoder outputs d_l
     float* sig = nullptr;
+    // pre-split operand twins (gemm_ps.hpp; sized for 3 planes): written after their producer when
+    // the GEMM engine splits (S3, B1), read by the pre-split GEMMs; fwd_np = planes of the last forward
+    void* x0s = nullptr;          // RAY_FILM's NHWC8 input (8 channels)
+    void* cats[4] = {};
+    void* pools[5] = {};
+    void* botts = nullptr;
+    void* douts[4] = {};          // l = 1..3 (dout[0] feeds only the head)
+    void* dcats[4] = {};          // up half of dcat, [M_l][C_l]
+    void* dYs = nullptr;          // split dL/dz scratch (largest level)
+    int fwd_np = 0;
     // backward
     float* dcat[4] = {};
     float *Sa = nullptr, *Sb = nullptr, *Sc = nullptr;
@@ -306,6 +319,14 @@ void film_alloc(Arena& a, DoubleConv& dc, int B) {
 void layout(cad_unet* h, Arena& a) {
     const int B = h->Bmax;
     const bool film = h->model != CAD_MODEL_BASELINE;
+    // pre-split twin of `elems` fp32 values (3 bf16 planes: the S3 layout; B1 uses a third of it)
+    auto sp = [&](int64_t elems) -> void* { return a.take((size_t)elems * 2 * cad::kMaxPlanes); };
+    auto conv_split_alloc = [&](Conv& c, bool dgrad) {
+        if (c.cin % 8) return;   // enc1.conv1 of the 3-channel models: in-loader split
+        const int64_t n = (int64_t)c.cout * 9 * c.cin;
+        c.ws = sp(n);
+        if (dgrad) c.wds = sp(n);
+    };
     h->flat_p = a.f(h->n_flat);
     h->flat_g = a.f(h->n_flat);
     h->norm_coef = a.f(4);
@@ -316,30 +337,44 @@ void layout(cad_unet* h, Arena& a) {
         const int64_t MC = h->Ml(l, B) * h->Cl(l);
         e.y1 = a.f(MC); e.y2 = a.f(MC);
         if (film || !h->fuse_bn) e.a1 = a.f(MC);   // relu(bn1(y1)) (FiLM'd) feeding conv2
+        if (film || !h->fuse_bn) e.a1s = sp(MC);   // (not `if (e.a1)`: the sizing pass has null pointers)
         film_alloc(a, e, B);
         if (l > 0) e.c1.wd = a.f((int64_t)e.c1.cout * 9 * e.c1.cin);
         e.c2.wd = a.f((int64_t)e.c2.cout * 9 * e.c2.cin);
-        if (l < 4) h->cat[l] = a.f(2 * MC);
+        conv_split_alloc(e.c1, l > 0);
+        conv_split_alloc(e.c2, true);
+        if (l < 4) { h->cat[l] = a.f(2 * MC); h->cats[l] = sp(2 * MC); }
         if (l > 0) {
             h->pool[l] = a.f(h->Ml(l, B) * h->Cl(l - 1));
+            h->pools[l] = sp(h->Ml(l, B) * h->Cl(l - 1));
             h->pidx[l] = a.u8(h->Ml(l, B) * h->Cl(l - 1));
         }
     }
     h->a2_bott = a.f(h->Ml(4, B) * h->Cl(4));
+    h->botts = sp(h->Ml(4, B) * h->Cl(4));
     for (int l = 0; l < 4; ++l) {
         DoubleConv& d = h->dec[l];
         bn_alloc(a, d.b1); bn_alloc(a, d.b2);
         const int64_t MC = h->Ml(l, B) * h->Cl(l);
         d.y1 = a.f(MC); d.y2 = a.f(MC);
         if (film || !h->fuse_bn) d.a1 = a.f(MC);
+        if (film || !h->fuse_bn) d.a1s = sp(MC);   // (not `if (d.a1)`: the sizing pass has null pointers)
         film_alloc(a, d, B);
         h->dout[l] = a.f(MC);
+        if (l > 0) h->douts[l] = sp(MC);
         d.c1.wd = a.f((int64_t)d.c1.cout * 9 * d.c1.cin);
         d.c2.wd = a.f((int64_t)d.c2.cout * 9 * d.c2.cin);
+        conv_split_alloc(d.c1, true);
+        conv_split_alloc(d.c2, true);
         h->up[l].wf = a.f((int64_t)4 * h->up[l].cout * h->up[l].cin);
+        h->up[l].wfs = sp((int64_t)4 * h->up[l].cout * h->up[l].cin);
+        h->up[l].wms = sp((int64_t)4 * h->up[l].cout * h->up[l].cin);
         h->dcat[l] = a.f(2 * MC);
+        h->dcats[l] = sp(MC);
     }
     h->x0 = a.f(h->Ml(0, B) * h->x0_ld);
+    if (h->x0_ld % 8 == 0) h->x0s = sp(h->Ml(0, B) * h->x0_ld);
+    h->dYs = sp(h->Ml(0, B) * h->Cl(0));
     h->sig = a.f(h->Ml(0, B));
     const int64_t M0C0 = h->Ml(0, B) * h->Cl(0);
     h->Sa = a.f(M0C0);
@@ -348,7 +383,7 @@ void layout(cad_unet* h, Arena& a) {
     // BN tile partials: rows x 2C, max over layers
     int64_t st = 0, colmax = 0;
     for (int l = 0; l < 5; ++l) {
-        const int64_t r = cad::conv3x3_stats_rows(B, h->Hl(l), h->Wl(l), h->Cl(l));
+        const int64_t r = (h->Ml(l, B) + 63) / 64;   // any tile height: the engine may change at run time
         st = std::max<int64_t>(st, r * 2 * h->Cl(l));
         colmax = std::max<int64_t>(colmax, h->Cl(l));
     }
@@ -410,11 +445,37 @@ cad::FilmLayer film_view(const cad_unet* h, const DoubleConv& dc) {
     return L;
 }
 
-void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin, int B, float* out, int64_t ldo,
-                     int ocoff, hipStream_t st) {
+// pre-split operands (gemm_ps.hpp) are used when the engine splits (S3 / B1) and the operand's
+// channel count is a multiple of 8; the fp32 tensors are still written (BN, pooling, the head and
+// the loss read them), the split twin is written right after by split_rows
+cad::Split sv(const void* p, int64_t ld, int coff = 0) {
+    cad::Split v;
+    v.p = p; v.ld = ld; v.coff = coff;
+    return v;
+}
+void split_into(const float* x, int64_t ldx, int xcoff, int C, int64_t M, void* out, int64_t ldo, int ocoff,
+                hipStream_t st) {
+    if (out) cad::split_rows(x, ldx, xcoff, C, M, out, ldo, ocoff, st);
+}
+void split_weights(const cad_unet* h, hipStream_t st) {   // forward weights, every forward (they change per step)
+    auto sw = [&](const Conv& c) {
+        if (c.ws) cad::split_rows(h->P(c.pidx), 9 * c.cin, 0, 9 * c.cin, c.cout, c.ws, 9 * c.cin, 0, st);
+    };
+    for (int l = 0; l < 5; ++l) { sw(h->enc[l].c1); sw(h->enc[l].c2); }
+    for (int l = 0; l < 4; ++l) {
+        sw(h->dec[l].c1); sw(h->dec[l].c2);
+        const Up& u = h->up[l];   // forward repack [q][co][ci]: rows 4*cout, K = cin
+        cad::split_rows(u.wf, u.cin, 0, u.cin, 4 * u.cout, u.wfs, u.cin, 0, st);
+    }
+}
+
+// in_s / out_s: split twins of the block input / output (p == nullptr: none)
+void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin, cad::Split in_s, int B, float* out,
+                     int64_t ldo, int ocoff, cad::Split out_s, hipStream_t st) {
     const int l = dc.level, Hh = h->Hl(l), Ww = h->Wl(l), C = dc.c1.cout;
     const int64_t M = h->Ml(l, B);
     const bool tr = h->train;
+    const bool ps = h->fwd_np > 0;
     const int rows = cad::conv3x3_stats_rows(B, Hh, Ww, C);
     auto bn = [&](BN& b) {
         if (tr)
@@ -423,27 +484,51 @@ void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin,
         else
             cad::bn_eval_coeffs(h->P(b.widx), h->P(b.bidx), b.rm, b.rv, C, 1e-5f, b.mean, b.invstd, b.scale, b.shift, st);
     };
-    cad::conv3x3_fwd(in, ldin, 0, dc.c1.cin, h->P(dc.c1.pidx), C, dc.y1, C, 0, B, Hh, Ww, tr ? h->stats : nullptr, st);
+    float* stats = tr ? h->stats : nullptr;
+    if (ps && in_s.p && dc.c1.ws)
+        cad::conv3x3_fwd_ps(in_s, dc.c1.cin, sv(dc.c1.ws, 9 * dc.c1.cin), C, dc.y1, C, 0, B, Hh, Ww, stats, st);
+    else
+        cad::conv3x3_fwd(in, ldin, 0, dc.c1.cin, h->P(dc.c1.pidx), C, dc.y1, C, 0, B, Hh, Ww, stats, st);
     bn(dc.b1);
-    if (dc.has_film()) {   // FiLMDoubleConvImpl::forward (intrinsics_unet.h:38-52)
-        cad::film_apply(dc.y1, C, dc.b1.scale, dc.b1.shift, dc.film.gam, dc.film.bet, B, (int64_t)Hh * Ww, dc.a1, st);
-        cad::conv3x3_fwd(dc.a1, C, 0, C, h->P(dc.c2.pidx), C, dc.y2, C, 0, B, Hh, Ww, tr ? h->stats : nullptr, st);
-    } else if (!h->fuse_bn) {
-        cad::bn_relu_fwd(dc.y1, C, dc.b1.scale, dc.b1.shift, dc.a1, C, 0, M, st);
-        cad::conv3x3_fwd(dc.a1, C, 0, C, h->P(dc.c2.pidx), C, dc.y2, C, 0, B, Hh, Ww, tr ? h->stats : nullptr, st);
+    if (dc.has_film() || !h->fuse_bn) {
+        if (dc.has_film()) {   // FiLMDoubleConvImpl::forward (intrinsics_unet.h:38-52)
+            cad::film_apply(dc.y1, C, dc.b1.scale, dc.b1.shift, dc.film.gam, dc.film.bet, B, (int64_t)Hh * Ww, dc.a1, st);
+            if (ps) cad::split_rows(dc.a1, C, 0, C, M, dc.a1s, C, 0, st);
+        } else {
+            cad::bn_relu_fwd(dc.y1, C, dc.b1.scale, dc.b1.shift, dc.a1, C, 0, M, st, ps ? dc.a1s : nullptr, C, 0);
+        }
+        if (ps) {
+            cad::conv3x3_fwd_ps(sv(dc.a1s, C), C, sv(dc.c2.ws, 9 * C), C, dc.y2, C, 0, B, Hh, Ww, stats, st);
+        } else {
+            cad::conv3x3_fwd(dc.a1, C, 0, C, h->P(dc.c2.pidx), C, dc.y2, C, 0, B, Hh, Ww, stats, st);
+        }
     } else {
         // a1 = relu(bn1(y1)) is never materialised: conv2's loader applies it (and so does conv2's wgrad)
-        cad::conv3x3_fwd(dc.y1, C, 0, C, h->P(dc.c2.pidx), C, dc.y2, C, 0, B, Hh, Ww, tr ? h->stats : nullptr, st,
-                         dc.b1.scale, dc.b1.shift);
+        cad::conv3x3_fwd(dc.y1, C, 0, C, h->P(dc.c2.pidx), C, dc.y2, C, 0, B, Hh, Ww, stats, st, dc.b1.scale,
+                         dc.b1.shift);
     }
     bn(dc.b2);
-    cad::bn_relu_fwd(dc.y2, C, dc.b2.scale, dc.b2.shift, out, ldo, ocoff, M, st);
+    cad::bn_relu_fwd(dc.y2, C, dc.b2.scale, dc.b2.shift, out, ldo, ocoff, M, st, ps ? const_cast<void*>(out_s.p) : nullptr,
+                     out_s.ld, out_s.coff);
 }
 
 void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth, int B, hipStream_t st) {
     const int f = h->f;
+    // pre-split operands need every block's channel count (f * 2^l) to be a multiple of 8
+    // Pre-split operands by default on the bf16 engine only (measured on MI355X at bs32 480x640:
+    // B1 198 -> 277 img/s; S3 112 -> 101 img/s — its 6-byte split operands make the 128x128 GEMMs
+    // operand-bandwidth-bound at the rate the in-loader split reaches).  CAD_PS=0|1 overrides.
+    static const int ps_env = [] {
+        const char* e = std::getenv("CAD_PS");
+        return e ? std::atoi(e) : -1;
+    }();
+    const int np = cad::split_planes();
+    const bool ps_on = ps_env < 0 ? np == 1 : ps_env != 0;
+    h->fwd_np = (!ps_on || h->f % 8 || (h->fuse_bn && h->model == CAD_MODEL_BASELINE)) ? 0 : np;
+    const bool ps = h->fwd_np > 0;
     for (int l = 0; l < 4; ++l)
         cad::repack_convT_fwd(h->P(h->up[l].widx), h->up[l].wf, h->up[l].cin, h->up[l].cout, st);
+    if (ps) split_weights(h, st);
     if (h->model != CAD_MODEL_BASELINE) {
         // a14 normalisation, then every block's FiLM MLP (gamma/beta depend on the camera only)
         cad::camera_normalize(cam4, B, h->H, h->W, h->camn, st);
@@ -454,21 +539,39 @@ void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth
         cad::rgb_rays_to_nhwc8(rgb, cam4, B, h->H, h->W, h->x0, st);
     else
         cad::rgb_to_nhwc4(rgb, h->x0, B, h->H, h->W, st);
-    double_conv_fwd(h, h->enc[0], h->x0, h->x0_ld, B, h->cat[0], 2 * f, 0, st);
+    const cad::Split none{};
+    cad::Split x0s = none;
+    if (ps && h->x0s) {
+        cad::split_rows(h->x0, h->x0_ld, 0, h->x0_ld, h->Ml(0, B), h->x0s, h->x0_ld, 0, st);
+        x0s = sv(h->x0s, h->x0_ld);
+    }
+    double_conv_fwd(h, h->enc[0], h->x0, h->x0_ld, x0s, B, h->cat[0], 2 * f, 0, sv(h->cats[0], 2 * f), st);
     for (int l = 1; l <= 4; ++l) {
         const int Cp = h->Cl(l - 1);
         cad::maxpool_fwd(h->cat[l - 1], 2 * Cp, Cp, B, h->Hl(l - 1), h->Wl(l - 1), h->pool[l], h->pidx[l], st);
+        if (ps) split_into(h->pool[l], Cp, 0, Cp, h->Ml(l, B), h->pools[l], Cp, 0, st);
+        const cad::Split pin = sv(h->pools[l], Cp);
         if (l < 4)
-            double_conv_fwd(h, h->enc[l], h->pool[l], Cp, B, h->cat[l], 2 * h->Cl(l), 0, st);
+            double_conv_fwd(h, h->enc[l], h->pool[l], Cp, pin, B, h->cat[l], 2 * h->Cl(l), 0,
+                            sv(h->cats[l], 2 * h->Cl(l)), st);
         else
-            double_conv_fwd(h, h->enc[4], h->pool[4], Cp, B, h->a2_bott, h->Cl(4), 0, st);
+            double_conv_fwd(h, h->enc[4], h->pool[4], Cp, pin, B, h->a2_bott, h->Cl(4), 0, sv(h->botts, h->Cl(4)), st);
     }
     for (int l = 3; l >= 0; --l) {
         const float* upin = l == 3 ? h->a2_bott : h->dout[l + 1];
+        const void* upins = l == 3 ? h->botts : h->douts[l + 1];
         const Up& u = h->up[l];
-        cad::convT_fwd(upin, u.cin, u.cin, u.wf, h->P(u.bidx), u.cout, h->cat[l], 2 * h->Cl(l), h->Cl(l), B,
-                       h->Hl(l + 1), h->Wl(l + 1), st);
-        double_conv_fwd(h, h->dec[l], h->cat[l], 2 * h->Cl(l), B, h->dout[l], h->Cl(l), 0, st);
+        const int C = h->Cl(l);
+        if (ps) {
+            cad::convT_fwd_ps(sv(upins, u.cin), u.cin, sv(u.wfs, u.cin), h->P(u.bidx), u.cout, h->cat[l], 2 * C, C, B,
+                              h->Hl(l + 1), h->Wl(l + 1), st);
+            cad::split_rows(h->cat[l], 2 * C, C, C, h->Ml(l, B), h->cats[l], 2 * C, C, st);
+        } else {
+            cad::convT_fwd(upin, u.cin, u.cin, u.wf, h->P(u.bidx), u.cout, h->cat[l], 2 * C, C, B, h->Hl(l + 1),
+                           h->Wl(l + 1), st);
+        }
+        double_conv_fwd(h, h->dec[l], h->cat[l], 2 * C, sv(h->cats[l], 2 * C), B, h->dout[l], C, 0,
+                        l > 0 ? sv(h->douts[l], C) : none, st);
     }
     cad::head_fwd(h->dout[0], f, h->P(h->head_w), h->P(h->head_b), h->max_depth, h->sig, depth, h->Ml(0, B), st);
 }
@@ -477,23 +580,29 @@ void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth
 // backward
 // ------------------------------------------------------------------------------------------
 // g: grad wrt the DoubleConv output (ld ldg, channel offset gcoff); in: the block input (ld ldin,
-// cin channels); din: where conv1's dgrad goes (nullptr = not needed), ld lddin.
+// cin channels; in_s its split twin); din: where conv1's dgrad goes (nullptr = not needed), ld lddin.
 void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, int gcoff, const float* in,
-                     int64_t ldin, int B, float* din, int64_t lddin, hipStream_t st) {
+                     int64_t ldin, cad::Split in_s, int B, float* din, int64_t lddin, hipStream_t st) {
     const int l = dc.level, Hh = h->Hl(l), Ww = h->Wl(l), C = dc.c1.cout;
     const int64_t M = h->Ml(l, B);
+    const bool ps = h->fwd_np > 0 && h->fwd_np == cad::split_planes();
     float* dY = h->Sb;
     float* dA1 = h->Sa;
     // bn2 + relu
     cad::bn_relu_bwd(g, ldg, gcoff, dc.y2, C, dc.b2.mean, dc.b2.invstd, dc.b2.scale, dc.b2.shift, h->P(dc.b2.widx), M,
-                     h->dscr, dc.b2.coef, h->G(dc.b2.widx), h->G(dc.b2.bidx), dY, st);
+                     h->dscr, dc.b2.coef, h->G(dc.b2.widx), h->G(dc.b2.bidx), dY, st, nullptr, 1, ps ? h->dYs : nullptr);
     // conv2
-    if (dc.a1)
-        cad::conv3x3_wgrad(dY, C, dc.a1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
-    else
-        cad::conv3x3_wgrad(dY, C, dc.y1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st,
-                           dc.b1.scale, dc.b1.shift);
-    cad::conv3x3_dgrad(dY, C, dc.c2.wd, C, dA1, C, B, Hh, Ww, st);
+    if (ps) {
+        cad::conv3x3_wgrad_ps(sv(h->dYs, C), C, sv(dc.a1s, C), C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
+        cad::conv3x3_dgrad_ps(sv(h->dYs, C), C, sv(dc.c2.wds, 9 * C), C, dA1, C, B, Hh, Ww, st);
+    } else {
+        if (dc.a1)
+            cad::conv3x3_wgrad(dY, C, dc.a1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
+        else
+            cad::conv3x3_wgrad(dY, C, dc.y1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st,
+                               dc.b1.scale, dc.b1.shift);
+        cad::conv3x3_dgrad(dY, C, dc.c2.wd, C, dA1, C, B, Hh, Ww, st);
+    }
     // FiLM: dgamma/dbeta per (sample, channel); the ReLU sees dA1 * gamma (folded into bn_relu_bwd)
     const int64_t HW = (int64_t)Hh * Ww;
     if (dc.has_film())
@@ -501,20 +610,38 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     // bn1 + relu
     cad::bn_relu_bwd(dA1, C, 0, dc.y1, C, dc.b1.mean, dc.b1.invstd, dc.b1.scale, dc.b1.shift, h->P(dc.b1.widx), M,
                      h->dscr, dc.b1.coef, h->G(dc.b1.widx), h->G(dc.b1.bidx), dY, st,
-                     dc.has_film() ? dc.film.gam : nullptr, HW);
+                     dc.has_film() ? dc.film.gam : nullptr, HW, ps ? h->dYs : nullptr);
     if (dc.has_film()) cad::film_mlp_bwd(film_view(h, dc), h->camn, B, st);
     // conv1
-    cad::conv3x3_wgrad(dY, C, in, ldin, 0, dc.c1.cin, h->G(dc.c1.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
-    if (din) cad::conv3x3_dgrad(dY, C, dc.c1.wd, dc.c1.cin, din, lddin, B, Hh, Ww, st);
+    const bool ps1 = ps && in_s.p && dc.c1.ws;
+    if (ps1)
+        cad::conv3x3_wgrad_ps(sv(h->dYs, C), C, in_s, dc.c1.cin, h->G(dc.c1.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
+    else
+        cad::conv3x3_wgrad(dY, C, in, ldin, 0, dc.c1.cin, h->G(dc.c1.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
+    if (din) {
+        if (ps && dc.c1.wds)
+            cad::conv3x3_dgrad_ps(sv(h->dYs, C), C, sv(dc.c1.wds, 9 * C), dc.c1.cin, din, lddin, B, Hh, Ww, st);
+        else
+            cad::conv3x3_dgrad(dY, C, dc.c1.wd, dc.c1.cin, din, lddin, B, Hh, Ww, st);
+    }
 }
 
 void repack_dgrad_weights(cad_unet* h, hipStream_t st) {
-    auto rp = [&](DoubleConv& dc, bool first) {
-        if (!first) cad::repack_conv_dgrad(h->P(dc.c1.pidx), dc.c1.wd, dc.c1.cout, dc.c1.cin, st);
-        cad::repack_conv_dgrad(h->P(dc.c2.pidx), dc.c2.wd, dc.c2.cout, dc.c2.cin, st);
+    const bool ps = h->fwd_np > 0 && h->fwd_np == cad::split_planes();
+    auto rp = [&](Conv& c) {   // dgrad repack [ci][tap][co]: rows cin, K = 9*cout
+        cad::repack_conv_dgrad(h->P(c.pidx), c.wd, c.cout, c.cin, st);
+        if (ps && c.wds) cad::split_rows(c.wd, 9 * c.cout, 0, 9 * c.cout, c.cin, c.wds, 9 * c.cout, 0, st);
     };
-    for (int l = 0; l < 5; ++l) rp(h->enc[l], l == 0);
-    for (int l = 0; l < 4; ++l) rp(h->dec[l], false);
+    for (int l = 0; l < 5; ++l) {
+        if (l > 0) rp(h->enc[l].c1);
+        rp(h->enc[l].c2);
+    }
+    for (int l = 0; l < 4; ++l) {
+        rp(h->dec[l].c1);
+        rp(h->dec[l].c2);
+        const Up& u = h->up[l];   // ConvT weights [ci][q][co]: rows cin, K = 4*cout
+        if (ps) cad::split_rows(h->P(u.widx), 4 * u.cout, 0, 4 * u.cout, u.cin, u.wms, 4 * u.cout, 0, st);
+    }
 }
 
 // stages: 0 head, 1..4 dec1..dec4, 5 bottleneck, 6..9 enc4..enc1
@@ -523,6 +650,7 @@ constexpr int kStages = 10;
 void backward_stage(cad_unet* h, int stage, const float* dpred, hipStream_t st) {
     const int B = h->fwd_B;
     const int f = h->f;
+    const bool ps = h->fwd_np > 0 && h->fwd_np == cad::split_planes();
     if (stage == 0) {
         repack_dgrad_weights(h, st);
         cad::head_bwd(h->dout[0], f, h->P(h->head_w), dpred, h->sig, h->max_depth, h->Sa, h->Ml(0, B), h->dscr,
@@ -532,15 +660,26 @@ void backward_stage(cad_unet* h, int stage, const float* dpred, hipStream_t st) 
     if (stage <= 4) {   // decoder level l = stage-1; grad of its output is in Sa
         const int l = stage - 1;
         const int C = h->Cl(l);
-        double_conv_bwd(h, h->dec[l], h->Sa, C, 0, h->cat[l], 2 * C, B, h->dcat[l], 2 * C, st);
+        double_conv_bwd(h, h->dec[l], h->Sa, C, 0, h->cat[l], 2 * C, sv(h->cats[l], 2 * C), B, h->dcat[l], 2 * C, st);
         const Up& u = h->up[l];
         const float* upin = l == 3 ? h->a2_bott : h->dout[l + 1];
+        const void* upins = l == 3 ? h->botts : h->douts[l + 1];
         // up (ConvTranspose2d) backward: grad of its output = dcat[:, C:2C]
-        cad::convT_wgrad(upin, u.cin, h->dcat[l], 2 * C, C, u.cout, h->G(u.widx), B, h->Hl(l + 1), h->Wl(l + 1),
-                         h->slab, h->slab_cap, st);
+        if (ps) {
+            cad::split_rows(h->dcat[l], 2 * C, C, C, h->Ml(l, B), h->dcats[l], C, 0, st);
+            cad::convT_wgrad_ps(sv(upins, u.cin), u.cin, sv(h->dcats[l], C), u.cout, h->G(u.widx), B, h->Hl(l + 1),
+                                h->Wl(l + 1), h->slab, h->slab_cap, st);
+        } else {
+            cad::convT_wgrad(upin, u.cin, h->dcat[l], 2 * C, C, u.cout, h->G(u.widx), B, h->Hl(l + 1), h->Wl(l + 1),
+                             h->slab, h->slab_cap, st);
+        }
         cad::colsum(h->dcat[l], 2 * C, C, h->Ml(l, B), C, h->dscr, st);
         cad::colsum_finalize(h->dscr, cad::colsum_slices(h->Ml(l, B)), C, h->G(u.bidx), 1.f, st);
-        cad::convT_dgrad(h->dcat[l], 2 * C, C, u.cout, h->P(u.widx), u.cin, h->Sa, B, h->Hl(l + 1), h->Wl(l + 1), st);
+        if (ps)
+            cad::convT_dgrad_ps(sv(h->dcats[l], C), u.cout, sv(u.wms, 4 * u.cout), u.cin, h->Sa, B, h->Hl(l + 1),
+                                h->Wl(l + 1), st);
+        else
+            cad::convT_dgrad(h->dcat[l], 2 * C, C, u.cout, h->P(u.widx), u.cin, h->Sa, B, h->Hl(l + 1), h->Wl(l + 1), st);
         return;
     }
     // encoder side: stage 5 = bottleneck (level 4), 6..9 = enc4..enc1 (levels 3..0)
@@ -550,11 +689,11 @@ void backward_stage(cad_unet* h, int stage, const float* dpred, hipStream_t st) 
     const float* g = l == 4 ? h->Sa : h->dcat[l];
     const int64_t ldg = l == 4 ? C : 2 * C;
     if (l == 0) {
-        double_conv_bwd(h, e, g, ldg, 0, h->x0, h->x0_ld, B, nullptr, 0, st);
+        double_conv_bwd(h, e, g, ldg, 0, h->x0, h->x0_ld, sv(h->x0s, h->x0_ld), B, nullptr, 0, st);
         return;
     }
     const int Cp = h->Cl(l - 1);
-    double_conv_bwd(h, e, g, ldg, 0, h->pool[l], Cp, B, h->Sc, Cp, st);
+    double_conv_bwd(h, e, g, ldg, 0, h->pool[l], Cp, sv(h->pools[l], Cp), B, h->Sc, Cp, st);
     cad::maxpool_bwd(h->Sc, h->pidx[l], Cp, B, h->Hl(l - 1), h->Wl(l - 1), h->dcat[l - 1], 2 * Cp, st);
 }
 
@@ -728,6 +867,7 @@ cad_status cad_unet_create_model(const cad_unet_desc* d, int model, int device, 
         Arena real;
         real.base = static_cast<char*>(base);
         layout(h.get(), real);
+        require(real.off == sz.off, "internal: arena layout differs between the sizing and the real pass", CAD_ERR_STATE);
         compute_stage_ranges(h.get());
         default_init(h.get());
         HIPCHK(hipDeviceSynchronize());

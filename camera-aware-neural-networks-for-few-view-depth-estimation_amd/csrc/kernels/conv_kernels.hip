@@ -9,6 +9,7 @@
 
 #include "gemm_mfma.hpp"
 #include "gemm_s3.hpp"
+#include "gemm_ps.hpp"
 #include "kernels.hpp"
 
 namespace cad {
@@ -117,71 +118,166 @@ __global__ __launch_bounds__(256) void k_convT_wgrad(GemmArgs a) {
 
 // ---- S3 / B1 engines (gemm_s3.hpp): NP = 3 exact bf16 planes (fp32 accuracy) or 1 rounded plane
 // (bf16 operands).  The __global__ wrappers carry distinct names per engine (rocprof symbols). ----
-template <int NP, int WM, int WN, int KB, class Epi>
+template <int NP, int WM, int WN, int MI, int NJ, int KB, class Epi>
 __device__ __forceinline__ void conv3x3_fwd_np(const GemmArgs& a) {
-    using LA = KcIm2col3x3<64 * WM, KB, false>;
-    using LB = KcDense<64 * WN, KB>;
-    gemm_body_s3<NP, WM, WN, KB, LA, LB>(
+    using LA = KcIm2col3x3<32 * MI * WM, KB, false>;
+    using LB = KcDense<32 * NJ * WN, KB>;
+    gemm_body_s3<NP, WM, WN, MI, NJ, KB, LA, LB>(
         a,
         [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.a_cin, a.B, a.H, a.W, r0, t, kb); },
         [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, Epi{});
 }
-template <int NP, int WM, int WN, int KB>
+template <int NP, int WM, int WN, int MI, int NJ, int KB>
 __device__ __forceinline__ void convT_fwd_np(const GemmArgs& a) {
-    using LA = KcDense<64 * WM, KB>;
-    using LB = KcDense<64 * WN, KB>;
-    gemm_body_s3<NP, WM, WN, KB, LA, LB>(
+    using LA = KcDense<32 * MI * WM, KB>;
+    using LB = KcDense<32 * NJ * WN, KB>;
+    gemm_body_s3<NP, WM, WN, MI, NJ, KB, LA, LB>(
         a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t, kb); },
         [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, EpiConvT{});
 }
-template <int NP, int WM, int WN, int KB>
+template <int NP, int WM, int WN, int MI, int NJ, int KB>
 __device__ __forceinline__ void convT_dgrad_np(const GemmArgs& a) {
-    using LA = KcUpGather<64 * WM, KB>;
-    using LB = KcDense<64 * WN, KB>;
-    gemm_body_s3<NP, WM, WN, KB, LA, LB>(
+    using LA = KcUpGather<32 * MI * WM, KB>;
+    using LB = KcDense<32 * NJ * WN, KB>;
+    gemm_body_s3<NP, WM, WN, MI, NJ, KB, LA, LB>(
         a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.a_cin, a.B, a.H, a.W, r0, t, kb); },
         [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, EpiStore{});
 }
-template <int NP, int WM, int WN, int KB>
+template <int NP, int WM, int WN, int MI, int NJ, int KB>
 __device__ __forceinline__ void conv3x3_wgrad_np(const GemmArgs& a) {
-    using LA = MNcDense<64 * WM, KB>;
-    using LB = MNcIm2col3x3<64 * WN, KB, false>;
-    gemm_body_s3m<NP, WM, WN, KB, LA, LB>(
+    using LA = MNcDense<32 * MI * WM, KB>;
+    using LB = MNcIm2col3x3<32 * NJ * WN, KB, false>;
+    gemm_body_s3m<NP, WM, WN, MI, NJ, KB, LA, LB>(
         a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t, kb); },
         [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.b_cin, a.B, a.H, a.W, r0, t, kb); },
         EpiSlab{});
 }
-template <int NP, int WM, int WN, int KB>
+template <int NP, int WM, int WN, int MI, int NJ, int KB>
 __device__ __forceinline__ void convT_wgrad_np(const GemmArgs& a) {
-    using LA = MNcDense<64 * WM, KB>;
-    using LB = MNcUpGather<64 * WN, KB>;
-    gemm_body_s3m<NP, WM, WN, KB, LA, LB>(
+    using LA = MNcDense<32 * MI * WM, KB>;
+    using LB = MNcUpGather<32 * NJ * WN, KB>;
+    gemm_body_s3m<NP, WM, WN, MI, NJ, KB, LA, LB>(
         a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t, kb); },
         [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.b_cin, a.B, a.H, a.W, r0, t, kb); },
         EpiSlab{});
 }
 
 template <int WM, int WN, int KB, class Epi>
-__global__ __launch_bounds__(256) void k_conv3x3_fwd_s3(GemmArgs a) { conv3x3_fwd_np<3, WM, WN, KB, Epi>(a); }
+__global__ __launch_bounds__(256) void k_conv3x3_fwd_s3(GemmArgs a) { conv3x3_fwd_np<3, WM, WN, 2, 2, KB, Epi>(a); }
 template <int WM, int WN, int KB>
-__global__ __launch_bounds__(256) void k_convT_fwd_s3(GemmArgs a) { convT_fwd_np<3, WM, WN, KB>(a); }
+__global__ __launch_bounds__(256) void k_convT_fwd_s3(GemmArgs a) { convT_fwd_np<3, WM, WN, 2, 2, KB>(a); }
 template <int WM, int WN, int KB>
-__global__ __launch_bounds__(256) void k_convT_dgrad_s3(GemmArgs a) { convT_dgrad_np<3, WM, WN, KB>(a); }
+__global__ __launch_bounds__(256) void k_convT_dgrad_s3(GemmArgs a) { convT_dgrad_np<3, WM, WN, 2, 2, KB>(a); }
 template <int WM, int WN, int KB>
-__global__ __launch_bounds__(256) void k_conv3x3_wgrad_s3(GemmArgs a) { conv3x3_wgrad_np<3, WM, WN, KB>(a); }
+__global__ __launch_bounds__(256) void k_conv3x3_wgrad_s3(GemmArgs a) { conv3x3_wgrad_np<3, WM, WN, 2, 2, KB>(a); }
 template <int WM, int WN, int KB>
-__global__ __launch_bounds__(256) void k_convT_wgrad_s3(GemmArgs a) { convT_wgrad_np<3, WM, WN, KB>(a); }
+__global__ __launch_bounds__(256) void k_convT_wgrad_s3(GemmArgs a) { convT_wgrad_np<3, WM, WN, 2, 2, KB>(a); }
 
 template <int WM, int WN, int KB, class Epi>
-__global__ __launch_bounds__(256) void k_conv3x3_fwd_bf16(GemmArgs a) { conv3x3_fwd_np<1, WM, WN, KB, Epi>(a); }
+__global__ __launch_bounds__(256) void k_conv3x3_fwd_bf16(GemmArgs a) { conv3x3_fwd_np<1, WM, WN, 2, 2, KB, Epi>(a); }
 template <int WM, int WN, int KB>
-__global__ __launch_bounds__(256) void k_convT_fwd_bf16(GemmArgs a) { convT_fwd_np<1, WM, WN, KB>(a); }
+__global__ __launch_bounds__(256) void k_convT_fwd_bf16(GemmArgs a) { convT_fwd_np<1, WM, WN, 2, 2, KB>(a); }
 template <int WM, int WN, int KB>
-__global__ __launch_bounds__(256) void k_convT_dgrad_bf16(GemmArgs a) { convT_dgrad_np<1, WM, WN, KB>(a); }
+__global__ __launch_bounds__(256) void k_convT_dgrad_bf16(GemmArgs a) { convT_dgrad_np<1, WM, WN, 2, 2, KB>(a); }
 template <int WM, int WN, int KB>
-__global__ __launch_bounds__(256) void k_conv3x3_wgrad_bf16(GemmArgs a) { conv3x3_wgrad_np<1, WM, WN, KB>(a); }
+__global__ __launch_bounds__(256) void k_conv3x3_wgrad_bf16(GemmArgs a) { conv3x3_wgrad_np<1, WM, WN, 2, 2, KB>(a); }
 template <int WM, int WN, int KB>
-__global__ __launch_bounds__(256) void k_convT_wgrad_bf16(GemmArgs a) { convT_wgrad_np<1, WM, WN, KB>(a); }
+__global__ __launch_bounds__(256) void k_convT_wgrad_bf16(GemmArgs a) { convT_wgrad_np<1, WM, WN, 2, 2, KB>(a); }
+#define CAD_NP_LKERNELS(SUF, NP)                                                                             \
+    template <int WM, int WN, int KB, class Epi>                                                             \
+    __global__ __launch_bounds__(256, 2) void k_conv3x3_fwd_##SUF(GemmArgs a) { conv3x3_fwd_np<NP, WM, WN, 4, 2, KB, Epi>(a); } \
+    template <int WM, int WN, int KB>                                                                        \
+    __global__ __launch_bounds__(256, 2) void k_convT_fwd_##SUF(GemmArgs a) { convT_fwd_np<NP, WM, WN, 4, 2, KB>(a); }     \
+    template <int WM, int WN, int KB>                                                                        \
+    __global__ __launch_bounds__(256, 2) void k_convT_dgrad_##SUF(GemmArgs a) { convT_dgrad_np<NP, WM, WN, 4, 2, KB>(a); } \
+    template <int WM, int WN, int KB>                                                                        \
+    __global__ __launch_bounds__(256, 2) void k_conv3x3_wgrad_##SUF(GemmArgs a) { conv3x3_wgrad_np<NP, WM, WN, 2, 4, KB>(a); } \
+    template <int WM, int WN, int KB>                                                                        \
+    __global__ __launch_bounds__(256, 2) void k_convT_wgrad_##SUF(GemmArgs a) { convT_wgrad_np<NP, WM, WN, 2, 4, KB>(a); }
+CAD_NP_LKERNELS(s3L, 3)
+CAD_NP_LKERNELS(bf16L, 1)
+#undef CAD_NP_LKERNELS
+
+// ---- pre-split operand kernels (gemm_ps.hpp): A/B pointers are split tensors (kernels.hpp Split),
+// lda/ldb their row length in channels, a_coff/b_coff channel offsets ----
+template <int NP, int WM, int WN, int MI, int NJ, int KB, class Epi>
+__device__ __forceinline__ void conv3x3_fwd_psb(const GemmArgs& a) {
+    using LA = PsKcIm2col3x3<32 * MI * WM, KB, NP>;
+    using LB = PsKcDense<32 * NJ * WN, KB, NP>;
+    gemm_body_ps<NP, WM, WN, MI, NJ, KB, LA, LB>(
+        a,
+        [&](LA& l, int r0, int t, int kb) {
+            l.init(a.A, a.lda, a.a_coff, a.a_cin, a.B, a.H, a.W, r0, t, kb, a.cimajor);
+        },
+        [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb, a.cimajor, a.a_cin); },
+        Epi{});
+}
+template <int NP, int WM, int WN, int MI, int NJ, int KB>
+__device__ __forceinline__ void convT_fwd_psb(const GemmArgs& a) {
+    using LA = PsKcDense<32 * MI * WM, KB, NP>;
+    using LB = PsKcDense<32 * NJ * WN, KB, NP>;
+    gemm_body_ps<NP, WM, WN, MI, NJ, KB, LA, LB>(
+        a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t, kb); },
+        [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, EpiConvT{});
+}
+template <int NP, int WM, int WN, int MI, int NJ, int KB>
+__device__ __forceinline__ void convT_dgrad_psb(const GemmArgs& a) {
+    using LA = PsKcUpGather<32 * MI * WM, KB, NP>;
+    using LB = PsKcDense<32 * NJ * WN, KB, NP>;
+    gemm_body_ps<NP, WM, WN, MI, NJ, KB, LA, LB>(
+        a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.a_cin, a.B, a.H, a.W, r0, t, kb); },
+        [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, EpiStore{});
+}
+template <int NP, int WM, int WN, int MI, int NJ, int KB>
+__device__ __forceinline__ void conv3x3_wgrad_psb(const GemmArgs& a) {
+    using LA = PsMNcDense<32 * MI * WM, KB, NP>;
+    using LB = PsMNcIm2col3x3<32 * NJ * WN, KB, NP>;
+    gemm_body_psm<NP, WM, WN, MI, NJ, KB, LA, LB>(
+        a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t, kb); },
+        [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.b_cin, a.B, a.H, a.W, r0, t, kb); },
+        EpiSlab{});
+}
+template <int NP, int WM, int WN, int MI, int NJ, int KB>
+__device__ __forceinline__ void convT_wgrad_psb(const GemmArgs& a) {
+    using LA = PsMNcDense<32 * MI * WM, KB, NP>;
+    using LB = PsMNcUpGather<32 * NJ * WN, KB, NP>;
+    gemm_body_psm<NP, WM, WN, MI, NJ, KB, LA, LB>(
+        a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t, kb); },
+        [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.b_cin, a.B, a.H, a.W, r0, t, kb); },
+        EpiSlab{});
+}
+#define CAD_PS_KERNELS(SUF, NP, MI_, NJ_, NJW_, WPE)                                                               \
+    template <int WM, int WN, int KB, class Epi>                                                             \
+    __global__ __launch_bounds__(256, WPE) void k_conv3x3_fwd_##SUF(GemmArgs a) { conv3x3_fwd_psb<NP, WM, WN, MI_, NJ_, KB, Epi>(a); } \
+    template <int WM, int WN, int KB>                                                                        \
+    __global__ __launch_bounds__(256, WPE) void k_convT_fwd_##SUF(GemmArgs a) { convT_fwd_psb<NP, WM, WN, MI_, NJ_, KB>(a); }     \
+    template <int WM, int WN, int KB>                                                                        \
+    __global__ __launch_bounds__(256, WPE) void k_convT_dgrad_##SUF(GemmArgs a) { convT_dgrad_psb<NP, WM, WN, MI_, NJ_, KB>(a); } \
+    template <int WM, int WN, int KB>                                                                        \
+    __global__ __launch_bounds__(256, WPE) void k_conv3x3_wgrad_##SUF(GemmArgs a) { conv3x3_wgrad_psb<NP, WM, WN, 2, NJW_, KB>(a); } \
+    template <int WM, int WN, int KB>                                                                        \
+    __global__ __launch_bounds__(256, WPE) void k_convT_wgrad_##SUF(GemmArgs a) { convT_wgrad_psb<NP, WM, WN, 2, NJW_, KB>(a); }
+CAD_PS_KERNELS(s3p, 3, 2, 2, 2, 1)
+CAD_PS_KERNELS(bf16p, 1, 2, 2, 2, 1)
+// large tiles: 256x128 (conv / ConvT forward, dgrad: 2x2 waves of 128x64) and 128x256 (weight
+// gradients: 2x2 waves of 64x128) — 0.75x the operand bytes per MAC of the 128x128 tile
+CAD_PS_KERNELS(s3pL, 3, 4, 2, 4, 2)   // (256, 2): at most 256 VGPRs, two waves per SIMD
+CAD_PS_KERNELS(bf16pL, 1, 4, 2, 4, 2)
+#undef CAD_PS_KERNELS
+
+// split pass: one thread per (row, 8-channel group)
+template <int NP>
+__global__ void k_split_rows(const float* __restrict__ x, int64_t ldx, int xcoff, int G, int64_t n,
+                             char* __restrict__ out, int64_t ldo, int ocoff) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t row = i / G;
+    const int g = (int)(i - row * G);
+    const float* s = x + row * ldx + xcoff + 8 * g;
+    const float4 a = *reinterpret_cast<const float4*>(s);
+    const float4 b = *reinterpret_cast<const float4*>(s + 4);
+    split8_store<NP>(out + row * ldo * 2 * NP + (int64_t)((ocoff >> 3) + g) * 16 * NP, a, b);
+}
 
 // deterministic split-K reduction: dst[e] = sum_z slab[z][e]
 __global__ void k_slab_reduce(const float* __restrict__ slab, int nsplit, int64_t stride,
@@ -207,11 +303,29 @@ inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 // on the square tile (+1% plain, +8% with the BN-stats epilogue), 16 everywhere else (the wgrad and
 // ConvT GEMMs lose 2-6% at 32, the tall/wide tiles ~10%).  CAD_KB_<KIND>_<CFG>=16|32 overrides,
 // e.g. CAD_KB_WGRAD_C22=32.
-enum Cfg { C41, C22, C14 };
+// C22L / C22W (S3, B1 and pre-split engines): 256x128 / 128x256 tiles of 2x2 waves with 128x64 /
+// 64x128 per wave — 0.75x the operand bytes and LDS traffic per MAC of C22, half the barriers per
+// MFMA; for the pixel-major (forward, dgrad) and the weight-gradient contractions.  Off by default
+// (CAD_BIGTILE=1 enables): measured on MI355X they tie C22 on S3 (189 vs 188 TFLOP/s) and B1
+// (676 vs 693) at two waves per SIMD instead of three.
+enum Cfg { C41, C22, C14, C22L, C22W };
 enum Kind { K_FWD, K_FWDS, K_WGRAD, K_TFWD, K_TDGRAD, K_TWGRAD, K_NKIND };
-Cfg pick_cfg(int M, int N) {
+int engine();
+bool big_tiles() {
+    static int on = -1;
+    if (on < 0) {
+        const char* e = std::getenv("CAD_BIGTILE");
+        on = (e && e[0] == '1') ? 1 : 0;
+    }
+    return on && engine() != 0;
+}
+Cfg pick_cfg(int M, int N, bool wgrad = false) {
     if (N <= 64) return C41;
     if (M <= 64) return C14;
+    if (big_tiles()) {
+        if (!wgrad && M >= 4096) return C22L;
+        if (wgrad && N >= 256) return C22W;
+    }
     return C22;
 }
 int kb_for(Kind k, Cfg c) {
@@ -234,16 +348,20 @@ int kb_for(Kind k, Cfg c) {
 }
 
 template <template <int, int, int> class KT, int WM, int WN, int KB>
-void launch_one(const GemmArgs& a, int splits, hipStream_t st) {
-    const dim3 grid(cdiv(a.M, 64 * WM), cdiv(a.N, 64 * WN), splits);
+void launch_one(const GemmArgs& a, int splits, hipStream_t st, bool large = false) {
+    using K = KT<WM, WN, KB>;
+    if (large && !K::HASL) throw std::runtime_error("large tile requested for a kernel without one");
+    const int mi = large ? K::LMI : 2, nj = large ? K::LNJ : 2;
+    const dim3 grid(cdiv(a.M, 32 * mi * WM), cdiv(a.N, 32 * nj * WN), splits);
+    auto fn = large ? K::fnL : K::fn;
     if (prof_enabled()) {
         char name[160];
-        snprintf(name, sizeof(name), KT<WM, WN, KB>::fmt, WM, WN, KB);
+        snprintf(name, sizeof(name), large ? K::fmtL : K::fmt, WM, WN, KB);
         prof_push(name, 2.0 * a.M * a.N * (double)a.K, st);
-        hipLaunchKernelGGL((KT<WM, WN, KB>::fn), grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL(fn, grid, dim3(256), 0, st, a);
         prof_pop(st);
     } else {
-        hipLaunchKernelGGL((KT<WM, WN, KB>::fn), grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL(fn, grid, dim3(256), 0, st, a);
     }
 }
 template <template <int, int, int> class KT, int WM, int WN>
@@ -257,6 +375,7 @@ void launch_cfg(Cfg c, int kb, const GemmArgs& a, int splits, hipStream_t st) {
         case C41: launch_kb<KT, 4, 1>(kb, a, splits, st); break;
         case C22: launch_kb<KT, 2, 2>(kb, a, splits, st); break;
         case C14: launch_kb<KT, 1, 4>(kb, a, splits, st); break;
+        default: throw std::runtime_error("tile configuration not available on this engine");
     }
 }
 template <template <int, int, int> class KT, int KB>
@@ -265,6 +384,8 @@ void launch_cfg_kb(Cfg c, const GemmArgs& a, int splits, hipStream_t st) {
         case C41: launch_one<KT, 4, 1, KB>(a, splits, st); break;
         case C22: launch_one<KT, 2, 2, KB>(a, splits, st); break;
         case C14: launch_one<KT, 1, 4, KB>(a, splits, st); break;
+        case C22L:
+        case C22W: launch_one<KT, 2, 2, KB>(a, splits, st, true); break;
     }
 }
 // fmt = the symbol as rocprofv3 demangles it
@@ -272,6 +393,20 @@ void launch_cfg_kb(Cfg c, const GemmArgs& a, int splits, hipStream_t st) {
     template <int WM, int WN, int KB> struct NAME {                              \
         static constexpr auto fn = EXPR;                                         \
         static constexpr const char* fmt = FMT;                                  \
+        static constexpr bool HASL = false;                                      \
+        static constexpr auto fnL = EXPR;                                        \
+        static constexpr const char* fmtL = FMT;                                 \
+        static constexpr int LMI = 2, LNJ = 2;                                   \
+    };
+// with a large-tile variant (launched for C22L / C22W): LMI x LNJ 32x32 blocks per wave
+#define CAD_KTL(NAME, EXPR, FMT, EXPRL, FMTL, LMI_, LNJ_)                        \
+    template <int WM, int WN, int KB> struct NAME {                              \
+        static constexpr auto fn = EXPR;                                         \
+        static constexpr const char* fmt = FMT;                                  \
+        static constexpr bool HASL = true;                                       \
+        static constexpr auto fnL = EXPRL;                                       \
+        static constexpr const char* fmtL = FMTL;                                \
+        static constexpr int LMI = LMI_, LNJ = LNJ_;                             \
     };
 CAD_KT(KConvFwd, (k_conv3x3_fwd<WM, WN, KB, EpiStore, false>),
        "void cad::k_conv3x3_fwd<%d, %d, %d, cad::EpiStore, false>(cad::GemmArgs)")
@@ -286,20 +421,32 @@ CAD_KT(KConvWgradBN, (k_conv3x3_wgrad<WM, WN, KB, true>), "void cad::k_conv3x3_w
 CAD_KT(KConvTFwd, (k_convT_fwd<WM, WN, KB>), "void cad::k_convT_fwd<%d, %d, %d>(cad::GemmArgs)")
 CAD_KT(KConvTDgrad, (k_convT_dgrad<WM, WN, KB>), "void cad::k_convT_dgrad<%d, %d, %d>(cad::GemmArgs)")
 CAD_KT(KConvTWgrad, (k_convT_wgrad<WM, WN, KB>), "void cad::k_convT_wgrad<%d, %d, %d>(cad::GemmArgs)")
-CAD_KT(KConvFwd3, (k_conv3x3_fwd_s3<WM, WN, KB, EpiStore>), "void cad::k_conv3x3_fwd_s3<%d, %d, %d, cad::EpiStore>(cad::GemmArgs)")
-CAD_KT(KConvFwdS3, (k_conv3x3_fwd_s3<WM, WN, KB, EpiStoreStats>),
-       "void cad::k_conv3x3_fwd_s3<%d, %d, %d, cad::EpiStoreStats>(cad::GemmArgs)")
-CAD_KT(KConvTFwd3, (k_convT_fwd_s3<WM, WN, KB>), "void cad::k_convT_fwd_s3<%d, %d, %d>(cad::GemmArgs)")
-CAD_KT(KConvTDgrad3, (k_convT_dgrad_s3<WM, WN, KB>), "void cad::k_convT_dgrad_s3<%d, %d, %d>(cad::GemmArgs)")
-CAD_KT(KConvWgrad3, (k_conv3x3_wgrad_s3<WM, WN, KB>), "void cad::k_conv3x3_wgrad_s3<%d, %d, %d>(cad::GemmArgs)")
-CAD_KT(KConvTWgrad3, (k_convT_wgrad_s3<WM, WN, KB>), "void cad::k_convT_wgrad_s3<%d, %d, %d>(cad::GemmArgs)")
-CAD_KT(KConvFwdB, (k_conv3x3_fwd_bf16<WM, WN, KB, EpiStore>), "void cad::k_conv3x3_fwd_bf16<%d, %d, %d, cad::EpiStore>(cad::GemmArgs)")
-CAD_KT(KConvFwdSB, (k_conv3x3_fwd_bf16<WM, WN, KB, EpiStoreStats>),
-       "void cad::k_conv3x3_fwd_bf16<%d, %d, %d, cad::EpiStoreStats>(cad::GemmArgs)")
-CAD_KT(KConvTFwdB, (k_convT_fwd_bf16<WM, WN, KB>), "void cad::k_convT_fwd_bf16<%d, %d, %d>(cad::GemmArgs)")
-CAD_KT(KConvTDgradB, (k_convT_dgrad_bf16<WM, WN, KB>), "void cad::k_convT_dgrad_bf16<%d, %d, %d>(cad::GemmArgs)")
-CAD_KT(KConvWgradB, (k_conv3x3_wgrad_bf16<WM, WN, KB>), "void cad::k_conv3x3_wgrad_bf16<%d, %d, %d>(cad::GemmArgs)")
-CAD_KT(KConvTWgradB, (k_convT_wgrad_bf16<WM, WN, KB>), "void cad::k_convT_wgrad_bf16<%d, %d, %d>(cad::GemmArgs)")
+#define CAD_NP_KT(SUF, T)                                                                                      \
+    CAD_KTL(KConvFwd##T, (k_conv3x3_fwd_##SUF<WM, WN, KB, EpiStore>),                                          \
+            "void cad::k_conv3x3_fwd_" #SUF "<%d, %d, %d, cad::EpiStore>(cad::GemmArgs)",                      \
+            (k_conv3x3_fwd_##SUF##L<WM, WN, KB, EpiStore>),                                                   \
+            "void cad::k_conv3x3_fwd_" #SUF "L<%d, %d, %d, cad::EpiStore>(cad::GemmArgs)", 4, 2)               \
+    CAD_KTL(KConvFwdS##T, (k_conv3x3_fwd_##SUF<WM, WN, KB, EpiStoreStats>),                                    \
+            "void cad::k_conv3x3_fwd_" #SUF "<%d, %d, %d, cad::EpiStoreStats>(cad::GemmArgs)",                 \
+            (k_conv3x3_fwd_##SUF##L<WM, WN, KB, EpiStoreStats>),                                              \
+            "void cad::k_conv3x3_fwd_" #SUF "L<%d, %d, %d, cad::EpiStoreStats>(cad::GemmArgs)", 4, 2)          \
+    CAD_KTL(KConvTFwd##T, (k_convT_fwd_##SUF<WM, WN, KB>), "void cad::k_convT_fwd_" #SUF "<%d, %d, %d>(cad::GemmArgs)", \
+            (k_convT_fwd_##SUF##L<WM, WN, KB>), "void cad::k_convT_fwd_" #SUF "L<%d, %d, %d>(cad::GemmArgs)", 4, 2) \
+    CAD_KTL(KConvTDgrad##T, (k_convT_dgrad_##SUF<WM, WN, KB>),                                                 \
+            "void cad::k_convT_dgrad_" #SUF "<%d, %d, %d>(cad::GemmArgs)",                                     \
+            (k_convT_dgrad_##SUF##L<WM, WN, KB>), "void cad::k_convT_dgrad_" #SUF "L<%d, %d, %d>(cad::GemmArgs)", 4, 2) \
+    CAD_KTL(KConvWgrad##T, (k_conv3x3_wgrad_##SUF<WM, WN, KB>),                                                \
+            "void cad::k_conv3x3_wgrad_" #SUF "<%d, %d, %d>(cad::GemmArgs)",                                   \
+            (k_conv3x3_wgrad_##SUF##L<WM, WN, KB>), "void cad::k_conv3x3_wgrad_" #SUF "L<%d, %d, %d>(cad::GemmArgs)", 2, 4) \
+    CAD_KTL(KConvTWgrad##T, (k_convT_wgrad_##SUF<WM, WN, KB>),                                                 \
+            "void cad::k_convT_wgrad_" #SUF "<%d, %d, %d>(cad::GemmArgs)",                                     \
+            (k_convT_wgrad_##SUF##L<WM, WN, KB>), "void cad::k_convT_wgrad_" #SUF "L<%d, %d, %d>(cad::GemmArgs)", 2, 4)
+// in-loader split engines: KConvFwd3 ... (S3), KConvFwdB ... (B1); pre-split: KConvFwdP3 ..., KConvFwdP1 ...
+CAD_NP_KT(s3, 3)
+CAD_NP_KT(bf16, B)
+CAD_NP_KT(s3p, P3)
+CAD_NP_KT(bf16p, P1)
+#undef CAD_NP_KT
 #undef CAD_KT
 
 // GEMM engine of every conv / ConvT contraction: 0 = exact f32 MFMA, 1 = S3 (bf16 matrix cores,
@@ -328,6 +475,14 @@ void launch_b1(Cfg c, const GemmArgs& a, int splits, hipStream_t st) {
     if (bf16_kb() == 16) launch_cfg_kb<KT, 16>(c, a, splits, st);
     else launch_cfg_kb<KT, 32>(c, a, splits, st);
 }
+int ps_planes() { return engine() == 1 ? 3 : engine() == 2 ? 1 : 0; }
+int ps_kb() { return engine() == 1 ? 16 : bf16_kb(); }
+template <template <int, int, int> class KT3, template <int, int, int> class KT1>
+void launch_ps(Cfg c, const GemmArgs& a, int splits, hipStream_t st) {
+    if (engine() == 1) launch_cfg_kb<KT3, 16>(c, a, splits, st);
+    else if (engine() == 2) launch_b1<KT1>(c, a, splits, st);
+    else throw std::runtime_error("pre-split GEMM launched on the f32 engine");
+}
 constexpr int kS3KB = 16;   // S3 stage depth (LDS: 3 bf16 planes per operand)
 // S3 stage depth: one bf16 k16 step per LDS stage (32 measured 12-13% slower: the LDS footprint
 // costs a workgroup per CU); kept as a function for the launch sites
@@ -355,8 +510,8 @@ void launch_s3(Cfg c, int, const GemmArgs& a, int splits, hipStream_t st) {
     launch_cfg_kb<KT, 16>(c, a, splits, st);
 }
 
-int tile_m(Cfg c) { return c == C41 ? 256 : c == C22 ? 128 : 64; }
-int tile_n(Cfg c) { return c == C41 ? 64 : c == C22 ? 128 : 256; }
+int tile_m(Cfg c) { return c == C41 || c == C22L ? 256 : c == C22 || c == C22W ? 128 : 64; }
+int tile_n(Cfg c) { return c == C41 ? 64 : c == C22 || c == C22L ? 128 : 256; }
 
 // split-K planning for the weight-gradient GEMMs: aim for >= ~2048 workgroups, >= 32 K-stages each.
 // A K-slice is also a loader's buffer window (gemm_mfma.hpp: 32-bit offsets from the slice's first
@@ -495,7 +650,7 @@ void convT_dgrad(const float* g, int64_t ldg, int gcoff, int cout, const float* 
 int64_t wgrad_slab_floats(int M, int N, int Kpix) {
     GemmArgs a{};
     a.M = M; a.N = N; a.K = Kpix;
-    const Cfg c = pick_cfg(M, N);
+    const Cfg c = pick_cfg(M, N, true);
     return (int64_t)plan_splits(a, c, 16, 0, 0) * M * N;   // kb 16: the larger split count
 }
 
@@ -512,7 +667,7 @@ void conv3x3_wgrad(const float* dz, int cout, const float* x, int64_t ldx, int x
     a.A = dz; a.lda = cout; a.a_coff = 0;
     a.Bm = x; a.ldb = ldx; a.b_coff = xcoff; a.b_cin = cin;
     a.b_sc = x_scale; a.b_sh = x_shift;
-    const Cfg c = pick_cfg(a.M, a.N);
+    const Cfg c = pick_cfg(a.M, a.N, true);
     const bool s3 = engine() == 1 && !x_scale, b1 = engine() == 2 && !x_scale;
     const int kb = b1 ? bf16_kb() : s3 ? s3_kb(K_WGRAD, c) : kb_for(K_WGRAD, c);
     int s = plan_splits(a, c, kb, slab_cap, 4 * std::max<int64_t>(a.lda, ldx));
@@ -535,7 +690,7 @@ void convT_wgrad(const float* x, int cin, const float* g, int64_t ldg, int gcoff
     a.B = B; a.H = H; a.W = W;
     a.A = x; a.lda = cin; a.a_coff = 0;
     a.Bm = g; a.ldb = ldg; a.b_coff = gcoff; a.b_cin = cout;
-    const Cfg c = pick_cfg(a.M, a.N);
+    const Cfg c = pick_cfg(a.M, a.N, true);
     const bool s3 = engine() == 1, b1 = engine() == 2;
     const int kb = b1 ? bf16_kb() : s3 ? s3_kb(K_TWGRAD, c) : kb_for(K_TWGRAD, c);
     int s = plan_splits(a, c, kb, slab_cap, 4 * std::max<int64_t>(a.lda, 4 * ldg));
@@ -547,6 +702,146 @@ void convT_wgrad(const float* x, int cin, const float* g, int64_t ldg, int gcoff
     if (b1) launch_b1<KConvTWgradB>(c, a, s, st);
     else if (s3) launch_s3<KConvTWgrad3>(c, kb, a, s, st);
     else launch_cfg<KConvTWgrad>(c, kb, a, s, st);
+    if (s > 1) finish_slabs(slab, s, per, dw, st);
+}
+
+// ------------------------------------------------------------------------------------------
+// pre-split launchers
+// ------------------------------------------------------------------------------------------
+int split_planes() { return ps_planes(); }
+
+void split_rows(const float* x, int64_t ldx, int xcoff, int C, int64_t M, void* out, int64_t ldo, int ocoff,
+                hipStream_t st) {
+    if (C % 8 || xcoff % 4 || ldx % 4 || ocoff % 8 || ldo % 8) throw std::runtime_error("split_rows: alignment");
+    const int G = C / 8;
+    const int64_t n = M * G;
+    if (n == 0) return;
+    const dim3 grid((unsigned)((n + 255) / 256));
+    if (ps_planes() == 3)
+        hipLaunchKernelGGL(k_split_rows<3>, grid, dim3(256), 0, st, x, ldx, xcoff, G, n, (char*)out, ldo, ocoff);
+    else if (ps_planes() == 1)
+        hipLaunchKernelGGL(k_split_rows<1>, grid, dim3(256), 0, st, x, ldx, xcoff, G, n, (char*)out, ldo, ocoff);
+    else
+        throw std::runtime_error("split_rows on the f32 engine");
+}
+
+namespace {
+// channel-major K order for the pre-split conv3x3 forward/dgrad (GemmArgs::cimajor); CAD_CIMAJOR=0 disables
+int cimajor_ok(int cin) {
+    static int on = -1;
+    if (on < 0) {
+        const char* e = std::getenv("CAD_CIMAJOR");
+        on = (e && e[0] == '0') ? 0 : 1;
+    }
+    return on && cin % ps_kb() == 0 ? 1 : 0;
+}
+void ps_check(const Split& s, int channels, const char* what) {
+    if (!s.p || s.ld % 8 || s.coff % 8 || channels % 8) throw std::runtime_error(std::string("pre-split operand: ") + what);
+}
+}  // namespace
+
+void conv3x3_fwd_ps(Split x, int cin, Split w, int cout, float* y, int64_t ldy, int ycoff, int B, int H, int W,
+                    float* stats, hipStream_t st) {
+    ps_check(x, cin, "conv3x3_fwd x");
+    ps_check(w, 9 * cin, "conv3x3_fwd w");
+    GemmArgs a{};
+    a.M = B * H * W; a.N = cout; a.K = 9 * cin;
+    a.B = B; a.H = H; a.W = W;
+    a.A = (const float*)x.p; a.lda = x.ld; a.a_coff = x.coff; a.a_cin = cin;
+    a.Bm = (const float*)w.p; a.ldb = w.ld; a.b_coff = w.coff;
+    a.C = y; a.ldc = ldy; a.c_coff = ycoff;
+    a.stats = stats;
+    const Cfg c = pick_cfg(a.M, a.N);
+    a.kstages_per_split = cdiv(a.K, ps_kb());
+    a.cimajor = cimajor_ok(cin);
+    if (stats) launch_ps<KConvFwdSP3, KConvFwdSP1>(c, a, 1, st);
+    else launch_ps<KConvFwdP3, KConvFwdP1>(c, a, 1, st);
+}
+
+void conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t lddx, int B, int H, int W,
+                      hipStream_t st) {
+    ps_check(dz, cout, "conv3x3_dgrad dz");
+    ps_check(wd, 9 * cout, "conv3x3_dgrad w");
+    GemmArgs a{};
+    a.M = B * H * W; a.N = cin; a.K = 9 * cout;
+    a.B = B; a.H = H; a.W = W;
+    a.A = (const float*)dz.p; a.lda = dz.ld; a.a_coff = dz.coff; a.a_cin = cout;
+    a.Bm = (const float*)wd.p; a.ldb = wd.ld; a.b_coff = wd.coff;
+    a.C = dx; a.ldc = lddx; a.c_coff = 0;
+    const Cfg c = pick_cfg(a.M, a.N);
+    a.kstages_per_split = cdiv(a.K, ps_kb());
+    a.cimajor = cimajor_ok(cout);
+    launch_ps<KConvFwdP3, KConvFwdP1>(c, a, 1, st);
+}
+
+void conv3x3_wgrad_ps(Split dz, int cout, Split x, int cin, float* dw, int B, int H, int W, float* slab,
+                      int64_t slab_cap, hipStream_t st) {
+    ps_check(dz, cout, "conv3x3_wgrad dz");
+    ps_check(x, cin, "conv3x3_wgrad x");
+    GemmArgs a{};
+    a.M = cout; a.N = 9 * cin; a.K = B * H * W;
+    a.B = B; a.H = H; a.W = W;
+    a.A = (const float*)dz.p; a.lda = dz.ld; a.a_coff = dz.coff;
+    a.Bm = (const float*)x.p; a.ldb = x.ld; a.b_coff = x.coff; a.b_cin = cin;
+    const Cfg c = pick_cfg(a.M, a.N, true);
+    const int kb = ps_kb();
+    int s = plan_splits(a, c, kb, slab_cap, 2 * kMaxPlanes * std::max<int64_t>(dz.ld, x.ld));
+    a.kstages_per_split = cdiv(cdiv(a.K, kb), s);
+    s = cdiv(cdiv(a.K, kb), a.kstages_per_split);
+    const int64_t per = (int64_t)a.M * a.N;
+    a.ldc = a.N; a.slab_stride = per;
+    a.C = s == 1 ? dw : slab;
+    launch_ps<KConvWgradP3, KConvWgradP1>(c, a, s, st);
+    if (s > 1) finish_slabs(slab, s, per, dw, st);
+}
+
+void convT_fwd_ps(Split x, int cin, Split wf, const float* bias, int cout, float* y, int64_t ldy, int ycoff, int B,
+                  int H, int W, hipStream_t st) {
+    ps_check(x, cin, "convT_fwd x");
+    ps_check(wf, cin, "convT_fwd w");
+    GemmArgs a{};
+    a.M = B * H * W; a.N = 4 * cout; a.K = cin;
+    a.B = B; a.H = H; a.W = W;
+    a.A = (const float*)x.p; a.lda = x.ld; a.a_coff = x.coff;
+    a.Bm = (const float*)wf.p; a.ldb = wf.ld; a.b_coff = wf.coff;
+    a.C = y; a.ldc = ldy; a.c_coff = ycoff; a.bias = bias;
+    const Cfg c = pick_cfg(a.M, a.N);
+    a.kstages_per_split = cdiv(a.K, ps_kb());
+    launch_ps<KConvTFwdP3, KConvTFwdP1>(c, a, 1, st);
+}
+
+void convT_dgrad_ps(Split g, int cout, Split wm, int cin, float* dx, int B, int H, int W, hipStream_t st) {
+    ps_check(g, cout, "convT_dgrad g");
+    ps_check(wm, 4 * cout, "convT_dgrad w");
+    GemmArgs a{};
+    a.M = B * H * W; a.N = cin; a.K = 4 * cout;
+    a.B = B; a.H = H; a.W = W;
+    a.A = (const float*)g.p; a.lda = g.ld; a.a_coff = g.coff; a.a_cin = cout;
+    a.Bm = (const float*)wm.p; a.ldb = wm.ld; a.b_coff = wm.coff;
+    a.C = dx; a.ldc = cin; a.c_coff = 0;
+    const Cfg c = pick_cfg(a.M, a.N);
+    a.kstages_per_split = cdiv(a.K, ps_kb());
+    launch_ps<KConvTDgradP3, KConvTDgradP1>(c, a, 1, st);
+}
+
+void convT_wgrad_ps(Split x, int cin, Split g, int cout, float* dw, int B, int H, int W, float* slab,
+                    int64_t slab_cap, hipStream_t st) {
+    ps_check(x, cin, "convT_wgrad x");
+    ps_check(g, cout, "convT_wgrad g");
+    GemmArgs a{};
+    a.M = cin; a.N = 4 * cout; a.K = B * H * W;
+    a.B = B; a.H = H; a.W = W;
+    a.A = (const float*)x.p; a.lda = x.ld; a.a_coff = x.coff;
+    a.Bm = (const float*)g.p; a.ldb = g.ld; a.b_coff = g.coff; a.b_cin = cout;
+    const Cfg c = pick_cfg(a.M, a.N, true);
+    const int kb = ps_kb();
+    int s = plan_splits(a, c, kb, slab_cap, 2 * kMaxPlanes * std::max<int64_t>(x.ld, 4 * g.ld));
+    a.kstages_per_split = cdiv(cdiv(a.K, kb), s);
+    s = cdiv(cdiv(a.K, kb), a.kstages_per_split);
+    const int64_t per = (int64_t)a.M * a.N;
+    a.ldc = a.N; a.slab_stride = per;
+    a.C = s == 1 ? dw : slab;
+    launch_ps<KConvTWgradP3, KConvTWgradP1>(c, a, s, st);
     if (s > 1) finish_slabs(slab, s, per, dw, st);
 }
 

@@ -60,6 +60,11 @@ struct GemmArgs {
     const float *a_sc, *a_sh, *b_sc, *b_sh;
     int kstages_per_split;
     int64_t slab_stride;  // elements between split-K slabs
+    // conv3x3 forward/dgrad on pre-split operands: K stages in channel-major order (stage s = tap
+    // s % 9 of channel block s / 9, KB channels per block) instead of tap-major, so the nine taps of
+    // a channel block re-read the same input rows back to back (L2 hits) — needs cin % KB == 0
+    int cimajor;
+    int conv_cin;         // cin of that contraction (the B loader walks the same (tap, ci) order)
 };
 
 __device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
@@ -483,18 +488,21 @@ __device__ __forceinline__ const float* epi_row_base(const GemmArgs& a, int m0, 
 
 // Epilogue shared by the engines: element (m, n) of sub-block (i, j), register r of the 32x32 C/D
 // layout (dtype-independent on gfx950).  `lds` is free scratch (the main loop ended on a barrier).
-template <int WM, int WN, class Epi>
-__device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, floatx16 (&acc)[2][2], const TileId& tile,
-                                              float* lds, Epi epi) {
-    constexpr int BN = 64 * WN;
+// Each wave owns MI x NJ blocks of 32x32: a (32 MI) x (32 NJ) sub-tile; the tile is WM x WN waves.
+template <int WM, int WN, int MI, int NJ, class Epi>
+__device__ __forceinline__ void gemm_epilogue_t(const GemmArgs& a, floatx16 (&acc)[MI][NJ], const TileId& tile,
+                                                float* lds, Epi epi) {
+    constexpr int BM = 32 * MI * WM, BN = 32 * NJ * WN;
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
     const int wm = wave / WN, wn = wave % WN;
-    const int m0 = tile.x * 64 * WM, n0 = tile.y * BN;
+    const int m0 = tile.x * BM, n0 = tile.y * BN;
     // With STATS the per-column BN partials are accumulated in the same pass (each accumulator is read once: keeping them live
     // for a second pass costs 64 VGPRs and an occupancy step).
     const int h = lane >> 5, col = lane & 31;
-    float ssum[2] = {0.f, 0.f}, ssq[2] = {0.f, 0.f};
+    float ssum[NJ], ssq[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) ssum[j] = ssq[j] = 0.f;
     // Row-major epilogues (EpiStore, EpiSlab) store through a buffer descriptor based at the tile's
     // first output row whose range ends at row M: rows past M are dropped by the range check and
     // columns past N get an out-of-range offset, so each store is one 32-bit offset add.
@@ -503,15 +511,15 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, floatx16 (&acc)
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(epi_row_base<Epi>(a, m0, tile.z),
                                                 (uint32_t)(bytes < (int64_t)kRecords ? bytes : kRecords));
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int n = n0 + wn * 64 + j * 32 + col;
+        for (int j = 0; j < NJ; ++j) {
+            const int n = n0 + wn * 32 * NJ + j * 32 + col;
             if constexpr (is_structured<Epi>::value) {
                 static_assert(!Epi::STATS, "structured epilogues carry no BN partials");
-                epi.block(a, m0 + wm * 64 + i * 32 + 4 * h, n, acc[i][j]);
+                epi.block(a, m0 + wm * 32 * MI + i * 32 + 4 * h, n, acc[i][j]);
             } else {
-                const int mr = wm * 64 + i * 32 + 4 * h;   // tile-relative row of register 0
+                const int mr = wm * 32 * MI + i * 32 + 4 * h;   // tile-relative row of register 0
                 const uint32_t lo = n < a.N ? (uint32_t)(mr * ldc4 + (int64_t)n * 4) : kOOB;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
@@ -533,11 +541,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, floatx16 (&acc)
         // the main loop ended on a barrier, so the LDS operand buffers are free for the reduction
         float* red = lds;   // [WM][BN][2]
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < NJ; ++j) {
             const float s = ssum[j] + __shfl_xor(ssum[j], 32);
             const float q = ssq[j] + __shfl_xor(ssq[j], 32);
             if (h == 0) {
-                const int cl = wn * 64 + j * 32 + col;
+                const int cl = wn * 32 * NJ + j * 32 + col;
                 red[(wm * BN + cl) * 2 + 0] = s;
                 red[(wm * BN + cl) * 2 + 1] = q;
             }
@@ -554,6 +562,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, floatx16 (&acc)
             }
         }
     }
+}
+template <int WM, int WN, class Epi>
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, floatx16 (&acc)[2][2], const TileId& tile,
+                                              float* lds, Epi epi) {
+    gemm_epilogue_t<WM, WN, 2, 2>(a, acc, tile, lds, epi);
 }
 
 template <int WM, int WN, int KB, class LA, bool KCA, class LB, bool KCB, class Epi, class InitA, class InitB>

@@ -161,23 +161,23 @@ __device__ __forceinline__ void s3_frag_f32(const float* s, int rb, int q, bf16x
 
 // the MFMAs of one k16 step on NP-plane fragments: S3 issues the six products with p + q <= 2,
 // smallest terms first ((2,0) (1,1) (0,2) (1,0) (0,1) (0,0)); B1 the single bf16 product
-template <int NP>
-__device__ __forceinline__ void s3_mfma(floatx16 (&acc)[2][2], const bf16x8 (&fa)[2][NP], const bf16x8 (&fb)[2][NP]) {
+template <int NP, int MI, int NJ>
+__device__ __forceinline__ void s3_mfma(floatx16 (&acc)[MI][NJ], const bf16x8 (&fa)[MI][NP], const bf16x8 (&fb)[NJ][NP]) {
     if constexpr (NP == 3) {
         constexpr int P[6] = {2, 1, 0, 1, 0, 0};
         constexpr int Q[6] = {0, 1, 2, 0, 1, 0};
 #pragma unroll
         for (int t = 0; t < 6; ++t)
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int i = 0; i < MI; ++i)
 #pragma unroll
-                for (int j = 0; j < 2; ++j)
+                for (int j = 0; j < NJ; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][P[t]], fb[j][Q[t]], acc[i][j], 0, 0, 0);
     } else {
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
+            for (int j = 0; j < NJ; ++j)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], acc[i][j], 0, 0, 0);
     }
 }
@@ -185,10 +185,10 @@ __device__ __forceinline__ void s3_mfma(floatx16 (&acc)[2][2], const bf16x8 (&fa
 // The S3/B1 engine for Kc x Kc operands (conv3x3 fwd/dgrad, ConvT fwd/dgrad).  Same tiling,
 // loaders, pipeline and epilogue as gemm_body (gemm_mfma.hpp); only the LDS image and the MFMA
 // differ.  AF32: A staged fp32 and split at fragment read (see s3_frag_f32); S3 with WN == 1 only.
-template <int NP, int WM, int WN, int KB, class LA, class LB, class Epi, class InitA, class InitB>
+template <int NP, int WM, int WN, int MI, int NJ, int KB, class LA, class LB, class Epi, class InitA, class InitB>
 __device__ __forceinline__ void gemm_body_s3(const GemmArgs& a, InitA init_a, InitB init_b, Epi epi) {
     constexpr bool AF32 = NP == 3 && WN == 1;
-    constexpr int BM = 64 * WM, BN = 64 * WN;
+    constexpr int BM = 32 * MI * WM, BN = 32 * NJ * WN;
     // LDS element counts in bf16 units (an fp32 A image counts 2 per float)
     constexpr int SA = AF32 ? 2 * BM * KS<KB>::LDK : S3Lds<BM, KB, NP>::ELEMS;
     constexpr int SB = S3Lds<BN, KB, NP>::ELEMS;
@@ -208,11 +208,11 @@ __device__ __forceinline__ void gemm_body_s3(const GemmArgs& a, InitA init_a, In
     init_a(la, m0, tid, kbeg);
     init_b(lb, n0, tid, kbeg);
 
-    floatx16 acc[2][2];
+    floatx16 acc[MI][NJ];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < NJ; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
@@ -229,12 +229,13 @@ __device__ __forceinline__ void gemm_body_s3(const GemmArgs& a, InitA init_a, In
         const uint16_t* sb = sa + SA;
 #pragma unroll
         for (int q = 0; q < S3<KB>::KSTEPS; ++q) {
-            bf16x8 fa[2][NP], fb[2][NP];
+            bf16x8 fa[MI][NP], fb[NJ][NP];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                if constexpr (AF32) s3_frag_f32<BM, KB>(reinterpret_cast<const float*>(sa), wm * 64 + i * 32, q, fa[i]);
-                else s3_frag<BM, KB, NP>(sa, wm * 64 + i * 32, q, fa[i]);
-                s3_frag<BN, KB, NP>(sb, wn * 64 + i * 32, q, fb[i]);
+            for (int j = 0; j < NJ; ++j) s3_frag<BN, KB, NP>(sb, wn * 32 * NJ + j * 32, q, fb[j]);
+#pragma unroll
+            for (int i = 0; i < MI; ++i) {
+                if constexpr (AF32) s3_frag_f32<BM, KB>(reinterpret_cast<const float*>(sa), wm * 32 * MI + i * 32, q, fa[i]);
+                else s3_frag<BM, KB, NP>(sa, wm * 32 * MI + i * 32, q, fa[i]);
             }
             s3_mfma<NP>(acc, fa, fb);
         }
@@ -256,7 +257,7 @@ __device__ __forceinline__ void gemm_body_s3(const GemmArgs& a, InitA init_a, In
         __syncthreads();
         cur ^= 1;
     }
-    gemm_epilogue<WM, WN>(a, acc, tile, reinterpret_cast<float*>(lds), epi);
+    gemm_epilogue_t<WM, WN, MI, NJ>(a, acc, tile, reinterpret_cast<float*>(lds), epi);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -316,9 +317,9 @@ __device__ __forceinline__ void s3m_frag(const char* s, int rb, int q, bf16x8 (&
     }
 }
 
-template <int NP, int WM, int WN, int KB, class LA, class LB, class Epi, class InitA, class InitB>
+template <int NP, int WM, int WN, int MI, int NJ, int KB, class LA, class LB, class Epi, class InitA, class InitB>
 __device__ __forceinline__ void gemm_body_s3m(const GemmArgs& a, InitA init_a, InitB init_b, Epi epi) {
-    constexpr int BM = 64 * WM, BN = 64 * WN;
+    constexpr int BM = 32 * MI * WM, BN = 32 * NJ * WN;
     constexpr int SA = NP * KB * S3M<BM>::STRIDE, SB = NP * KB * S3M<BN>::STRIDE;   // bytes
     __shared__ __attribute__((aligned(16))) char lds[2 * (SA + SB)];
 
@@ -336,11 +337,11 @@ __device__ __forceinline__ void gemm_body_s3m(const GemmArgs& a, InitA init_a, I
     init_a(la, m0, tid, kbeg);
     init_b(lb, n0, tid, kbeg);
 
-    floatx16 acc[2][2];
+    floatx16 acc[MI][NJ];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < NJ; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
@@ -356,12 +357,11 @@ __device__ __forceinline__ void gemm_body_s3m(const GemmArgs& a, InitA init_a, I
         const char* sb = sa + SA;
 #pragma unroll
         for (int q = 0; q < S3<KB>::KSTEPS; ++q) {
-            bf16x8 fa[2][NP], fb[2][NP];
+            bf16x8 fa[MI][NP], fb[NJ][NP];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                s3m_frag<BM, KB, NP>(sa, wm * 64 + i * 32, q, fa[i]);
-                s3m_frag<BN, KB, NP>(sb, wn * 64 + i * 32, q, fb[i]);
-            }
+            for (int j = 0; j < NJ; ++j) s3m_frag<BN, KB, NP>(sb, wn * 32 * NJ + j * 32, q, fb[j]);
+#pragma unroll
+            for (int i = 0; i < MI; ++i) s3m_frag<BM, KB, NP>(sa, wm * 32 * MI + i * 32, q, fa[i]);
             s3_mfma<NP>(acc, fa, fb);
         }
     };
@@ -382,7 +382,7 @@ __device__ __forceinline__ void gemm_body_s3m(const GemmArgs& a, InitA init_a, I
         __syncthreads();
         cur ^= 1;
     }
-    gemm_epilogue<WM, WN>(a, acc, tile, reinterpret_cast<float*>(lds), epi);
+    gemm_epilogue_t<WM, WN, MI, NJ>(a, acc, tile, reinterpret_cast<float*>(lds), epi);
 }
 
 }  // namespace cad

@@ -41,6 +41,32 @@ void convT_wgrad(const float* x, int cin, const float* g, int64_t ldg, int gcoff
                  int B, int H, int W, float* slab, int64_t slab_cap, hipStream_t st);
 int64_t wgrad_slab_floats(int M, int N, int Kpix);
 
+// ---- pre-split operands (gemm_ps.hpp): tensors split into bf16 planes once, by a split pass after
+// their producer, and read by the S3 (NP = 3) / B1 (NP = 1) GEMMs without per-fetch conversion.
+// A view: p = split rows of `ld` channels (ld, coff, channel counts multiples of 8).
+struct Split {
+    const void* p = nullptr;
+    int64_t ld = 0;
+    int coff = 0;
+};
+int split_planes();                    // NP of the current engine: 3 (S3), 1 (B1), 0 (f32: no split)
+inline bool ps_ok(int channels) { return split_planes() > 0 && channels % 8 == 0; }
+constexpr int kMaxPlanes = 3;          // buffers are sized for NP = 3 (bytes = elems * 2 * 3)
+// out[row][ocoff + c] (split, ld ldo) = split(x[row][xcoff + c]), c < C, rows < M
+void split_rows(const float* x, int64_t ldx, int xcoff, int C, int64_t M, void* out, int64_t ldo, int ocoff,
+                hipStream_t st);
+void conv3x3_fwd_ps(Split x, int cin, Split w, int cout, float* y, int64_t ldy, int ycoff, int B, int H, int W,
+                    float* stats, hipStream_t st);
+void conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t lddx, int B, int H, int W,
+                      hipStream_t st);
+void conv3x3_wgrad_ps(Split dz, int cout, Split x, int cin, float* dw, int B, int H, int W, float* slab,
+                      int64_t slab_cap, hipStream_t st);
+void convT_fwd_ps(Split x, int cin, Split wf, const float* bias, int cout, float* y, int64_t ldy, int ycoff, int B,
+                  int H, int W, hipStream_t st);
+void convT_dgrad_ps(Split g, int cout, Split wm, int cin, float* dx, int B, int H, int W, hipStream_t st);
+void convT_wgrad_ps(Split x, int cin, Split g, int cout, float* dw, int B, int H, int W, float* slab,
+                    int64_t slab_cap, hipStream_t st);
+
 // ---------------- NN elementwise / reductions (nn_kernels.hip) ----------------
 // column partial sums: part[s][c] (double) over row slices; returns number of slices
 int colsum_slices(int64_t R);
@@ -54,15 +80,18 @@ void bn_fwd_finalize(const float* tile_part, int rows, int C, int64_t count, con
 // eval-mode BN coefficients from running statistics
 void bn_eval_coeffs(const float* gamma, const float* beta, const float* run_mean, const float* run_var,
                     int C, float eps, float* mean, float* invstd, float* scale, float* shift, hipStream_t st);
+// os != nullptr: also writes the output's pre-split twin (split rows of ldos channels at channel
+// offset oscoff, split_planes() planes; see Split below)
 void bn_relu_fwd(const float* y, int C, const float* scale, const float* shift, float* out, int64_t ldo,
-                 int ocoff, int64_t M, hipStream_t st);
+                 int ocoff, int64_t M, hipStream_t st, void* os = nullptr, int64_t ldos = 0, int oscoff = 0);
 // BN+ReLU backward: dy = k1*dz - k2 - k3*xhat, dz = g*[y*scale+shift > 0];
 // writes dgamma/dbeta (grad buffer) and dy (dense [M][C]).  gmul != nullptr: g is first multiplied
-// by gmul[sample][c] (sample = row / HW) — the FiLM gamma sitting between this ReLU and the consumer
+// by gmul[sample][c] (sample = row / HW) — the FiLM gamma sitting between this ReLU and the consumer.
+// dy_split != nullptr: also the pre-split twin of dy (dense, ld C)
 void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, const float* mean,
                  const float* invstd, const float* scale, const float* shift, const float* gamma,
                  int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
-                 hipStream_t st, const float* gmul = nullptr, int64_t HW = 1);
+                 hipStream_t st, const float* gmul = nullptr, int64_t HW = 1, void* dy_split = nullptr);
 void maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float* out, uint8_t* idx,
                  hipStream_t st);
 void maxpool_bwd(const float* dout, const uint8_t* idx, int C, int B, int H, int W, float* dx,

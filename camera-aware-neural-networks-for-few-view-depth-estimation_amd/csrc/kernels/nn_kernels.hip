@@ -10,6 +10,7 @@
 //   head: baseline_unet.h:191-192  x = out_conv(x); x = sigmoid(x) * max_depth
 #include <algorithm>
 
+#include "gemm_s3.hpp"   // split_np (pre-split twins written by the elementwise passes)
 #include "kernels.hpp"
 
 namespace cad {
@@ -194,9 +195,20 @@ void bn_eval_coeffs(const float* gamma, const float* beta, const float* run_mean
                        mean, invstd, scale, shift);
 }
 
+// split-twin store of 4 channels [c, c+4) of row r (gemm_ps.hpp layout; c % 4 == 0): NP x 8 B
+template <int NP>
+__device__ __forceinline__ void split4_store(char* os, int64_t ldos, int oscoff, int64_t r, int c, float4 v) {
+    const auto sp = split_np<NP>(v);
+    const int cc = oscoff + c;
+    char* d = os + r * ldos * 2 * NP + (int64_t)(cc >> 3) * 16 * NP + (cc & 7) * 2;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) *reinterpret_cast<uint2*>(d + p * 16) = sp.p[p];
+}
+
+template <int NP>
 __global__ void k_bn_relu_fwd(const float* __restrict__ y, int C, const float* __restrict__ scale,
                               const float* __restrict__ shift, float* __restrict__ out, int64_t ldo,
-                              int ocoff, int64_t n4) {
+                              int ocoff, int64_t n4, char* __restrict__ os, int64_t ldos, int oscoff) {
     const int C4 = C >> 2;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = i / C4;
@@ -210,12 +222,23 @@ __global__ void k_bn_relu_fwd(const float* __restrict__ y, int C, const float* _
         o.z = fmaxf(v.z * s.z + t.z, 0.f);
         o.w = fmaxf(v.w * s.w + t.w, 0.f);
         *reinterpret_cast<float4*>(out + r * ldo + ocoff + c) = o;
+        if constexpr (NP > 0) split4_store<NP>(os, ldos, oscoff, r, c, o);
     }
 }
 void bn_relu_fwd(const float* y, int C, const float* scale, const float* shift, float* out, int64_t ldo,
-                 int ocoff, int64_t M, hipStream_t st) {
+                 int ocoff, int64_t M, hipStream_t st, void* os, int64_t ldos, int oscoff) {
     const int64_t n4 = M * C / 4;
-    hipLaunchKernelGGL(k_bn_relu_fwd, dim3(ew_blocks(n4)), dim3(256), 0, st, y, C, scale, shift, out, ldo, ocoff, n4);
+    const int np = os ? split_planes() : 0;
+    char* o = static_cast<char*>(os);
+    if (np == 3)
+        hipLaunchKernelGGL(k_bn_relu_fwd<3>, dim3(ew_blocks(n4)), dim3(256), 0, st, y, C, scale, shift, out, ldo, ocoff,
+                           n4, o, ldos, oscoff);
+    else if (np == 1)
+        hipLaunchKernelGGL(k_bn_relu_fwd<1>, dim3(ew_blocks(n4)), dim3(256), 0, st, y, C, scale, shift, out, ldo, ocoff,
+                           n4, o, ldos, oscoff);
+    else
+        hipLaunchKernelGGL(k_bn_relu_fwd<0>, dim3(ew_blocks(n4)), dim3(256), 0, st, y, C, scale, shift, out, ldo, ocoff,
+                           n4, o, ldos, oscoff);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -233,11 +256,12 @@ __global__ void k_bn_bwd_coef(const double* tot, int C, int64_t M, const float* 
     coef[C + c] = (float)(k1 * sdz / (double)M);
     coef[2 * C + c] = (float)(k1 * sdzx / (double)M);
 }
+template <int NP>
 __global__ void k_bn_relu_bwd(const float* __restrict__ g, int64_t ldg, int gcoff, const float* __restrict__ y,
                               int C, const float* __restrict__ mean, const float* __restrict__ invstd,
                               const float* __restrict__ scale, const float* __restrict__ shift,
                               const float* __restrict__ coef, float* __restrict__ dy, int64_t n4,
-                              const float* __restrict__ gmul, int64_t HW) {
+                              const float* __restrict__ gmul, int64_t HW, char* __restrict__ os) {
     const int C4 = C >> 2;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = i / C4;
@@ -258,13 +282,15 @@ __global__ void k_bn_relu_bwd(const float* __restrict__ g, int64_t ldg, int gcof
             const float xh = (ya[e] - mean[c]) * invstd[c];
             o[e] = coef[c] * dz - coef[C + c] - coef[2 * C + c] * xh;
         }
-        *reinterpret_cast<float4*>(dy + i * 4) = make_float4(o[0], o[1], o[2], o[3]);
+        const float4 ov = make_float4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<float4*>(dy + i * 4) = ov;
+        if constexpr (NP > 0) split4_store<NP>(os, C, 0, r, c0, ov);
     }
 }
 void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, const float* mean,
                  const float* invstd, const float* scale, const float* shift, const float* gamma,
                  int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
-                 hipStream_t st, const float* gmul, int64_t HW) {
+                 hipStream_t st, const float* gmul, int64_t HW, void* dy_split) {
     double* tot = scratch;
     double* part = scratch + 2 * C;
     OpBnBwd op{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW};
@@ -272,8 +298,17 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
     launch_colfinal(part, S, 2 * C, tot, nullptr, 1.f, st);
     hipLaunchKernelGGL(k_bn_bwd_coef, dim3(cdiv(C, 64)), dim3(64), 0, st, tot, C, M, gamma, invstd, coef, dgamma, dbeta);
     const int64_t n4 = M * C / 4;
-    hipLaunchKernelGGL(k_bn_relu_bwd, dim3(ew_blocks(n4)), dim3(256), 0, st, g, ldg, gcoff, y, C, mean, invstd,
-                       scale, shift, coef, dy, n4, gmul, HW);
+    const int np = dy_split ? split_planes() : 0;
+    char* os = static_cast<char*>(dy_split);
+    if (np == 3)
+        hipLaunchKernelGGL(k_bn_relu_bwd<3>, dim3(ew_blocks(n4)), dim3(256), 0, st, g, ldg, gcoff, y, C, mean, invstd,
+                           scale, shift, coef, dy, n4, gmul, HW, os);
+    else if (np == 1)
+        hipLaunchKernelGGL(k_bn_relu_bwd<1>, dim3(ew_blocks(n4)), dim3(256), 0, st, g, ldg, gcoff, y, C, mean, invstd,
+                           scale, shift, coef, dy, n4, gmul, HW, os);
+    else
+        hipLaunchKernelGGL(k_bn_relu_bwd<0>, dim3(ew_blocks(n4)), dim3(256), 0, st, g, ldg, gcoff, y, C, mean, invstd,
+                           scale, shift, coef, dy, n4, gmul, HW, os);
 }
 
 // ------------------------------------------------------------------------------------------
