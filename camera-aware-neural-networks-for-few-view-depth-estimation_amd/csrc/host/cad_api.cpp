@@ -183,6 +183,7 @@ struct cad_unet {
     void* dcats[4] = {};          // up half of dcat, [M_l][C_l]
     void* dYs = nullptr;          // split dL/dz scratch (largest level)
     int fwd_np = 0;
+    bool wsplit = false;          // S3 without pre-split activations: weights still pre-split (s3w kernels)
     // backward
     float* dcat[4] = {};
     float *Sa = nullptr, *Sb = nullptr, *Sc = nullptr;
@@ -488,7 +489,8 @@ void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin,
     if (ps && in_s.p && dc.c1.ws)
         cad::conv3x3_fwd_ps(in_s, dc.c1.cin, sv(dc.c1.ws, 9 * dc.c1.cin), C, dc.y1, C, 0, B, Hh, Ww, stats, st);
     else
-        cad::conv3x3_fwd(in, ldin, 0, dc.c1.cin, h->P(dc.c1.pidx), C, dc.y1, C, 0, B, Hh, Ww, stats, st);
+        cad::conv3x3_fwd(in, ldin, 0, dc.c1.cin, h->P(dc.c1.pidx), C, dc.y1, C, 0, B, Hh, Ww, stats, st, nullptr,
+                         nullptr, h->wsplit ? dc.c1.ws : nullptr);
     bn(dc.b1);
     if (dc.has_film() || !h->fuse_bn) {
         if (dc.has_film()) {   // FiLMDoubleConvImpl::forward (intrinsics_unet.h:38-52)
@@ -500,7 +502,8 @@ void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin,
         if (ps) {
             cad::conv3x3_fwd_ps(sv(dc.a1s, C), C, sv(dc.c2.ws, 9 * C), C, dc.y2, C, 0, B, Hh, Ww, stats, st);
         } else {
-            cad::conv3x3_fwd(dc.a1, C, 0, C, h->P(dc.c2.pidx), C, dc.y2, C, 0, B, Hh, Ww, stats, st);
+            cad::conv3x3_fwd(dc.a1, C, 0, C, h->P(dc.c2.pidx), C, dc.y2, C, 0, B, Hh, Ww, stats, st, nullptr, nullptr,
+                             h->wsplit ? dc.c2.ws : nullptr);
         }
     } else {
         // a1 = relu(bn1(y1)) is never materialised: conv2's loader applies it (and so does conv2's wgrad)
@@ -525,10 +528,18 @@ void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth
     const int np = cad::split_planes();
     const bool ps_on = ps_env < 0 ? np == 1 : ps_env != 0;
     h->fwd_np = (!ps_on || h->f % 8 || (h->fuse_bn && h->model == CAD_MODEL_BASELINE)) ? 0 : np;
+    // CAD_WSPLIT=1: the S3 engine stages pre-split weights (s3w kernels) and splits only the
+    // activations in its loaders — measured neutral on MI355X (180 vs 180 TFLOP/s: the S3 GEMMs run
+    // at ~1.6 GHz with the matrix pipe 68% busy, not bound by the split), so off by default
+    static const bool ws_env = [] {
+        const char* e = std::getenv("CAD_WSPLIT");
+        return e && e[0] == '1';
+    }();
+    h->wsplit = ws_env && h->fwd_np == 0 && np == 3 && h->f % 8 == 0;
     const bool ps = h->fwd_np > 0;
     for (int l = 0; l < 4; ++l)
         cad::repack_convT_fwd(h->P(h->up[l].widx), h->up[l].wf, h->up[l].cin, h->up[l].cout, st);
-    if (ps) split_weights(h, st);
+    if (ps || h->wsplit) split_weights(h, st);
     if (h->model != CAD_MODEL_BASELINE) {
         // a14 normalisation, then every block's FiLM MLP (gamma/beta depend on the camera only)
         cad::camera_normalize(cam4, B, h->H, h->W, h->camn, st);
@@ -568,7 +579,7 @@ void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth
             cad::split_rows(h->cat[l], 2 * C, C, C, h->Ml(l, B), h->cats[l], 2 * C, C, st);
         } else {
             cad::convT_fwd(upin, u.cin, u.cin, u.wf, h->P(u.bidx), u.cout, h->cat[l], 2 * C, C, B, h->Hl(l + 1),
-                           h->Wl(l + 1), st);
+                           h->Wl(l + 1), st, h->wsplit ? u.wfs : nullptr);
         }
         double_conv_fwd(h, h->dec[l], h->cat[l], 2 * C, sv(h->cats[l], 2 * C), B, h->dout[l], C, 0,
                         l > 0 ? sv(h->douts[l], C) : none, st);
@@ -601,7 +612,7 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
         else
             cad::conv3x3_wgrad(dY, C, dc.y1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st,
                                dc.b1.scale, dc.b1.shift);
-        cad::conv3x3_dgrad(dY, C, dc.c2.wd, C, dA1, C, B, Hh, Ww, st);
+        cad::conv3x3_dgrad(dY, C, dc.c2.wd, C, dA1, C, B, Hh, Ww, st, h->wsplit ? dc.c2.wds : nullptr);
     }
     // FiLM: dgamma/dbeta per (sample, channel); the ReLU sees dA1 * gamma (folded into bn_relu_bwd)
     const int64_t HW = (int64_t)Hh * Ww;
@@ -622,7 +633,7 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
         if (ps && dc.c1.wds)
             cad::conv3x3_dgrad_ps(sv(h->dYs, C), C, sv(dc.c1.wds, 9 * C), dc.c1.cin, din, lddin, B, Hh, Ww, st);
         else
-            cad::conv3x3_dgrad(dY, C, dc.c1.wd, dc.c1.cin, din, lddin, B, Hh, Ww, st);
+            cad::conv3x3_dgrad(dY, C, dc.c1.wd, dc.c1.cin, din, lddin, B, Hh, Ww, st, h->wsplit ? dc.c1.wds : nullptr);
     }
 }
 
@@ -630,7 +641,7 @@ void repack_dgrad_weights(cad_unet* h, hipStream_t st) {
     const bool ps = h->fwd_np > 0 && h->fwd_np == cad::split_planes();
     auto rp = [&](Conv& c) {   // dgrad repack [ci][tap][co]: rows cin, K = 9*cout
         cad::repack_conv_dgrad(h->P(c.pidx), c.wd, c.cout, c.cin, st);
-        if (ps && c.wds) cad::split_rows(c.wd, 9 * c.cout, 0, 9 * c.cout, c.cin, c.wds, 9 * c.cout, 0, st);
+        if ((ps || h->wsplit) && c.wds) cad::split_rows(c.wd, 9 * c.cout, 0, 9 * c.cout, c.cin, c.wds, 9 * c.cout, 0, st);
     };
     for (int l = 0; l < 5; ++l) {
         if (l > 0) rp(h->enc[l].c1);
@@ -640,7 +651,7 @@ void repack_dgrad_weights(cad_unet* h, hipStream_t st) {
         rp(h->dec[l].c1);
         rp(h->dec[l].c2);
         const Up& u = h->up[l];   // ConvT weights [ci][q][co]: rows cin, K = 4*cout
-        if (ps) cad::split_rows(h->P(u.widx), 4 * u.cout, 0, 4 * u.cout, u.cin, u.wms, 4 * u.cout, 0, st);
+        if (ps || h->wsplit) cad::split_rows(h->P(u.widx), 4 * u.cout, 0, 4 * u.cout, u.cin, u.wms, 4 * u.cout, 0, st);
     }
 }
 
@@ -679,7 +690,8 @@ void backward_stage(cad_unet* h, int stage, const float* dpred, hipStream_t st) 
             cad::convT_dgrad_ps(sv(h->dcats[l], C), u.cout, sv(u.wms, 4 * u.cout), u.cin, h->Sa, B, h->Hl(l + 1),
                                 h->Wl(l + 1), st);
         else
-            cad::convT_dgrad(h->dcat[l], 2 * C, C, u.cout, h->P(u.widx), u.cin, h->Sa, B, h->Hl(l + 1), h->Wl(l + 1), st);
+            cad::convT_dgrad(h->dcat[l], 2 * C, C, u.cout, h->P(u.widx), u.cin, h->Sa, B, h->Hl(l + 1), h->Wl(l + 1), st,
+                             h->wsplit ? u.wms : nullptr);
         return;
     }
     // encoder side: stage 5 = bottleneck (level 4), 6..9 = enc4..enc1 (levels 3..0)

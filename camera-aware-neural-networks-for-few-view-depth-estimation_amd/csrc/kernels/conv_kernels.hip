@@ -198,6 +198,35 @@ CAD_NP_LKERNELS(s3L, 3)
 CAD_NP_LKERNELS(bf16L, 1)
 #undef CAD_NP_LKERNELS
 
+// ---- S3 with pre-split weights ("s3w"): the activation operand A is split in the loader, the
+// weight operand B (split once per step) is staged without conversion — half the main-loop split
+// work of s3 at 1.25x its operand bytes ----
+template <int WM, int WN, int KB, class Epi>
+__global__ __launch_bounds__(256) void k_conv3x3_fwd_s3w(GemmArgs a) {
+    using LA = KcIm2col3x3<64 * WM, KB, false>;
+    using LB = PsKcDense<64 * WN, KB, 3>;
+    gemm_body_s3<3, WM, WN, 2, 2, KB, LA, LB>(
+        a,
+        [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.a_cin, a.B, a.H, a.W, r0, t, kb); },
+        [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, Epi{});
+}
+template <int WM, int WN, int KB>
+__global__ __launch_bounds__(256) void k_convT_fwd_s3w(GemmArgs a) {
+    using LA = KcDense<64 * WM, KB>;
+    using LB = PsKcDense<64 * WN, KB, 3>;
+    gemm_body_s3<3, WM, WN, 2, 2, KB, LA, LB>(
+        a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t, kb); },
+        [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, EpiConvT{});
+}
+template <int WM, int WN, int KB>
+__global__ __launch_bounds__(256) void k_convT_dgrad_s3w(GemmArgs a) {
+    using LA = KcUpGather<64 * WM, KB>;
+    using LB = PsKcDense<64 * WN, KB, 3>;
+    gemm_body_s3<3, WM, WN, 2, 2, KB, LA, LB>(
+        a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.a_cin, a.B, a.H, a.W, r0, t, kb); },
+        [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, EpiStore{});
+}
+
 // ---- pre-split operand kernels (gemm_ps.hpp): A/B pointers are split tensors (kernels.hpp Split),
 // lda/ldb their row length in channels, a_coff/b_coff channel offsets ----
 template <int NP, int WM, int WN, int MI, int NJ, int KB, class Epi>
@@ -441,6 +470,11 @@ CAD_KT(KConvTWgrad, (k_convT_wgrad<WM, WN, KB>), "void cad::k_convT_wgrad<%d, %d
     CAD_KTL(KConvTWgrad##T, (k_convT_wgrad_##SUF<WM, WN, KB>),                                                 \
             "void cad::k_convT_wgrad_" #SUF "<%d, %d, %d>(cad::GemmArgs)",                                     \
             (k_convT_wgrad_##SUF##L<WM, WN, KB>), "void cad::k_convT_wgrad_" #SUF "L<%d, %d, %d>(cad::GemmArgs)", 2, 4)
+CAD_KT(KConvFwdW3, (k_conv3x3_fwd_s3w<WM, WN, KB, EpiStore>), "void cad::k_conv3x3_fwd_s3w<%d, %d, %d, cad::EpiStore>(cad::GemmArgs)")
+CAD_KT(KConvFwdSW3, (k_conv3x3_fwd_s3w<WM, WN, KB, EpiStoreStats>),
+       "void cad::k_conv3x3_fwd_s3w<%d, %d, %d, cad::EpiStoreStats>(cad::GemmArgs)")
+CAD_KT(KConvTFwdW3, (k_convT_fwd_s3w<WM, WN, KB>), "void cad::k_convT_fwd_s3w<%d, %d, %d>(cad::GemmArgs)")
+CAD_KT(KConvTDgradW3, (k_convT_dgrad_s3w<WM, WN, KB>), "void cad::k_convT_dgrad_s3w<%d, %d, %d>(cad::GemmArgs)")
 // in-loader split engines: KConvFwd3 ... (S3), KConvFwdB ... (B1); pre-split: KConvFwdP3 ..., KConvFwdP1 ...
 CAD_NP_KT(s3, 3)
 CAD_NP_KT(bf16, B)
@@ -534,7 +568,7 @@ int plan_splits(const GemmArgs& a, Cfg c, int kb, int64_t slab_cap_floats, int64
 
 void conv3x3_fwd(const float* x, int64_t ldx, int xcoff, int cin, const float* w, int cout, float* y,
                  int64_t ldy, int ycoff, int B, int H, int W, float* stats, hipStream_t st,
-                 const float* in_scale, const float* in_shift) {
+                 const float* in_scale, const float* in_shift, const void* w_split) {
     GemmArgs a{};
     a.M = B * H * W; a.N = cout; a.K = 9 * cin;
     a.B = B; a.H = H; a.W = W;
@@ -552,6 +586,11 @@ void conv3x3_fwd(const float* x, int64_t ldx, int xcoff, int cin, const float* w
     if (engine() == 1 && !in_scale) {
         const int kb = s3_kb(stats ? K_FWDS : K_FWD, c);
         a.kstages_per_split = cdiv(a.K, kb);
+        if (w_split && a.K % 8 == 0) {   // pre-split weights: rows cout of K = 9 cin
+            a.Bm = static_cast<const float*>(w_split); a.ldb = a.K; a.b_coff = 0;
+            if (stats) launch_s3<KConvFwdSW3>(c, kb, a, 1, st); else launch_s3<KConvFwdW3>(c, kb, a, 1, st);
+            return;
+        }
         if (stats) launch_s3<KConvFwdS3>(c, kb, a, 1, st); else launch_s3<KConvFwd3>(c, kb, a, 1, st);
         return;
     }
@@ -573,7 +612,7 @@ int conv3x3_stats_rows(int B, int H, int W, int cout) {
 }
 
 void convT_fwd(const float* x, int64_t ldx, int cin, const float* wf, const float* bias, int cout,
-               float* y, int64_t ldy, int ycoff, int B, int H, int W, hipStream_t st) {
+               float* y, int64_t ldy, int ycoff, int B, int H, int W, hipStream_t st, const void* wf_split) {
     GemmArgs a{};
     a.M = B * H * W; a.N = 4 * cout; a.K = cin;
     a.B = B; a.H = H; a.W = W;
@@ -589,6 +628,11 @@ void convT_fwd(const float* x, int64_t ldx, int cin, const float* wf, const floa
     if (engine() == 1) {
         const int kb = s3_kb(K_TFWD, c);
         a.kstages_per_split = cdiv(a.K, kb);
+        if (wf_split && a.K % 8 == 0) {   // rows 4 cout of K = cin
+            a.Bm = static_cast<const float*>(wf_split);
+            launch_s3<KConvTFwdW3>(c, kb, a, 1, st);
+            return;
+        }
         launch_s3<KConvTFwd3>(c, kb, a, 1, st);
         return;
     }
@@ -598,7 +642,7 @@ void convT_fwd(const float* x, int64_t ldx, int cin, const float* wf, const floa
 }
 
 void conv3x3_dgrad(const float* dz, int cout, const float* wd, int cin, float* dx, int64_t lddx,
-                   int B, int H, int W, hipStream_t st) {
+                   int B, int H, int W, hipStream_t st, const void* wd_split) {
     GemmArgs a{};
     a.M = B * H * W; a.N = cin; a.K = 9 * cout;
     a.B = B; a.H = H; a.W = W;
@@ -614,6 +658,11 @@ void conv3x3_dgrad(const float* dz, int cout, const float* wd, int cin, float* d
     if (engine() == 1) {
         const int kb = s3_kb(K_FWD, c);
         a.kstages_per_split = cdiv(a.K, kb);
+        if (wd_split && a.K % 8 == 0) {   // rows cin of K = 9 cout
+            a.Bm = static_cast<const float*>(wd_split);
+            launch_s3<KConvFwdW3>(c, kb, a, 1, st);
+            return;
+        }
         launch_s3<KConvFwd3>(c, kb, a, 1, st);
         return;
     }
@@ -623,7 +672,7 @@ void conv3x3_dgrad(const float* dz, int cout, const float* wd, int cin, float* d
 }
 
 void convT_dgrad(const float* g, int64_t ldg, int gcoff, int cout, const float* wm, int cin, float* dx,
-                 int B, int H, int W, hipStream_t st) {
+                 int B, int H, int W, hipStream_t st, const void* wm_split) {
     GemmArgs a{};
     a.M = B * H * W; a.N = cin; a.K = 4 * cout;
     a.B = B; a.H = H; a.W = W;
@@ -639,6 +688,11 @@ void convT_dgrad(const float* g, int64_t ldg, int gcoff, int cout, const float* 
     if (engine() == 1) {
         const int kb = s3_kb(K_TDGRAD, c);
         a.kstages_per_split = cdiv(a.K, kb);
+        if (wm_split && a.K % 8 == 0) {   // rows cin of K = 4 cout
+            a.Bm = static_cast<const float*>(wm_split);
+            launch_s3<KConvTDgradW3>(c, kb, a, 1, st);
+            return;
+        }
         launch_s3<KConvTDgrad3>(c, kb, a, 1, st);
         return;
     }

@@ -44,6 +44,7 @@ struct PKc {
 
 template <int ROWS, int KB, int NP>
 struct PsKcBase {
+    static constexpr bool PRESPLIT = true;
     using G = PKc<ROWS, KB, NP>;
     static constexpr int NV = G::NV;
     uint4 v[NV];

@@ -159,6 +159,12 @@ __device__ __forceinline__ void s3_frag_f32(const float* s, int rb, int q, bf16x
     }
 }
 
+// loaders of pre-split operands (gemm_ps.hpp) declare PRESPLIT
+template <class L, class = void>
+struct is_presplit : std::false_type {};
+template <class L>
+struct is_presplit<L, std::void_t<decltype(L::PRESPLIT)>> : std::integral_constant<bool, L::PRESPLIT> {};
+
 // the MFMAs of one k16 step on NP-plane fragments: S3 issues the six products with p + q <= 2,
 // smallest terms first ((2,0) (1,1) (0,2) (1,0) (0,1) (0,0)); B1 the single bf16 product
 template <int NP, int MI, int NJ>
@@ -216,13 +222,26 @@ __device__ __forceinline__ void gemm_body_s3(const GemmArgs& a, InitA init_a, In
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    auto stage_store = [&](int buf, float4 (&xa)[LA::NV], float4 (&xb)[LB::NV]) {
-        la.finish(xa);
-        lb.finish(xb);
+    // B may come pre-split (gemm_ps.hpp loaders: the weights, split once per step): its loader then
+    // keeps its own staged registers and writes the planes without conversion
+    constexpr bool BPS = is_presplit<LB>::value;
+    float4 ra[LA::NV];
+    float4 rb[BPS ? 1 : LB::NV];
+    auto load_ab = [&]() {
+        la.load(ra);
+        if constexpr (BPS) lb.load(); else lb.load(rb);
+    };
+    auto stage_store = [&](int buf) {
+        la.finish(ra);
         uint16_t* da = lds + buf * (SA + SB);
-        if constexpr (AF32) kc_store_nat<BM, KB>(reinterpret_cast<float*>(da), xa);
-        else s3_store<BM, KB, NP>(da, xa);
-        s3_store<BN, KB, NP>(da + SA, xb);
+        if constexpr (AF32) kc_store_nat<BM, KB>(reinterpret_cast<float*>(da), ra);
+        else s3_store<BM, KB, NP>(da, ra);
+        if constexpr (BPS) {
+            lb.store(da + SA);
+        } else {
+            lb.finish(rb);
+            s3_store<BN, KB, NP>(da + SA, rb);
+        }
     };
     auto stage_compute = [&](int buf) {
         const uint16_t* sa = lds + buf * (SA + SB);
@@ -241,19 +260,17 @@ __device__ __forceinline__ void gemm_body_s3(const GemmArgs& a, InitA init_a, In
         }
     };
 
-    float4 ra[LA::NV], rb[LB::NV];
     if (kbeg < kend) {
-        la.load(ra);
-        lb.load(rb);
-        stage_store(0, ra, rb);
+        load_ab();
+        stage_store(0);
     }
     __syncthreads();
     int cur = 0;
     for (int kt = kbeg; kt < kend; ++kt) {
         const bool more = kt + 1 < kend;
-        if (more) { la.load(ra); lb.load(rb); }
+        if (more) load_ab();
         stage_compute(cur);
-        if (more) stage_store(cur ^ 1, ra, rb);
+        if (more) stage_store(cur ^ 1);
         __syncthreads();
         cur ^= 1;
     }

@@ -21,22 +21,24 @@ int gemm_engine();
 // y = conv3x3(x) (+ per-tile BN partials [rows][2][cout] when stats != nullptr)
 // in_scale/in_shift != nullptr: x is a pre-BN conv output and the loader applies
 // relu(x*scale[c] + shift[c]) on the fly (BN-apply + ReLU fused into the consumer)
+// w_split etc. (optional): the same weights pre-split (3 planes, gemm_ps.hpp layout) for the S3
+// engine, which then stages them without conversion
 void conv3x3_fwd(const float* x, int64_t ldx, int xcoff, int cin, const float* w, int cout, float* y,
                  int64_t ldy, int ycoff, int B, int H, int W, float* stats, hipStream_t st,
-                 const float* in_scale = nullptr, const float* in_shift = nullptr);
+                 const float* in_scale = nullptr, const float* in_shift = nullptr, const void* w_split = nullptr);
 int conv3x3_stats_rows(int B, int H, int W, int cout);
 // dx[pix][ci] = conv3x3(dz, wd) with wd = repacked [ci][tap'][co]
 void conv3x3_dgrad(const float* dz, int cout, const float* wd, int cin, float* dx, int64_t lddx,
-                   int B, int H, int W, hipStream_t st);
+                   int B, int H, int W, hipStream_t st, const void* wd_split = nullptr);
 // dw[co][tap][ci] = sum_pix dz[pix][co] * im2col(x)[pix][tap,ci]
 void conv3x3_wgrad(const float* dz, int cout, const float* x, int64_t ldx, int xcoff, int cin, float* dw,
                    int B, int H, int W, float* slab, int64_t slab_cap, hipStream_t st,
                    const float* x_scale = nullptr, const float* x_shift = nullptr);
 // ConvTranspose2d(k2,s2): (B,H,W,cin) -> (B,2H,2W,cout) written at channel offset ycoff of rows ldy
 void convT_fwd(const float* x, int64_t ldx, int cin, const float* wf, const float* bias, int cout,
-               float* y, int64_t ldy, int ycoff, int B, int H, int W, hipStream_t st);
+               float* y, int64_t ldy, int ycoff, int B, int H, int W, hipStream_t st, const void* wf_split = nullptr);
 void convT_dgrad(const float* g, int64_t ldg, int gcoff, int cout, const float* wm, int cin, float* dx,
-                 int B, int H, int W, hipStream_t st);
+                 int B, int H, int W, hipStream_t st, const void* wm_split = nullptr);
 void convT_wgrad(const float* x, int cin, const float* g, int64_t ldg, int gcoff, int cout, float* dw,
                  int B, int H, int W, float* slab, int64_t slab_cap, hipStream_t st);
 int64_t wgrad_slab_floats(int M, int N, int Kpix);

@@ -117,9 +117,15 @@ def main():
         fa, wa = sum(f) / len(f), sum(w) / len(w)
         traffic[k] = {"launches": len(f), "fetch_kb_avg": fa, "write_kb_avg": wa,
                       "hbm_bytes_per_launch": round((2 * fa + wa) * 1024)}
-    if traffic:
-        with open(os.path.join(here, "pmc_traffic.json"), "w") as fh:
-            json.dump(traffic, fh, indent=1, sort_keys=True)
+    if traffic:   # merged: kernel names differ per engine, so several configs share the file
+        path = os.path.join(here, "pmc_traffic.json")
+        merged = {}
+        if os.path.exists(path):
+            with open(path) as fh:
+                merged = json.load(fh)
+        merged.update(traffic)
+        with open(path, "w") as fh:
+            json.dump(merged, fh, indent=1, sort_keys=True)
     print(f"stats rows: {len(lines)}; pmc kernels: {len(traffic)}")
 
 
