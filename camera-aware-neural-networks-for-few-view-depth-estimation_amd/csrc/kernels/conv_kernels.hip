@@ -379,10 +379,13 @@ int kb_for(Kind k, Cfg c) {
 template <template <int, int, int> class KT, int WM, int WN, int KB>
 void launch_one(const GemmArgs& a, int splits, hipStream_t st, bool large = false) {
     using K = KT<WM, WN, KB>;
-    if (large && !K::HASL) throw std::runtime_error("large tile requested for a kernel without one");
+    auto fn = K::fn();
+    if (large) {   // large tiles exist as 2x2-wave launches only (pick_cfg)
+        if constexpr (WM == 2 && WN == 2 && K::HASL) fn = K::fnL();
+        else throw std::runtime_error("large tile requested for a kernel without one");
+    }
     const int mi = large ? K::LMI : 2, nj = large ? K::LNJ : 2;
     const dim3 grid(cdiv(a.M, 32 * mi * WM), cdiv(a.N, 32 * nj * WN), splits);
-    auto fn = large ? K::fnL : K::fn;
     if (prof_enabled()) {
         char name[160];
         snprintf(name, sizeof(name), large ? K::fmtL : K::fmt, WM, WN, KB);
@@ -418,22 +421,23 @@ void launch_cfg_kb(Cfg c, const GemmArgs& a, int splits, hipStream_t st) {
     }
 }
 // fmt = the symbol as rocprofv3 demangles it
+// (kernel pointers behind functions: a specialization is instantiated only when launched)
 #define CAD_KT(NAME, EXPR, FMT)                                                  \
     template <int WM, int WN, int KB> struct NAME {                              \
-        static constexpr auto fn = EXPR;                                         \
+        static auto fn() { return EXPR; }                                        \
         static constexpr const char* fmt = FMT;                                  \
         static constexpr bool HASL = false;                                      \
-        static constexpr auto fnL = EXPR;                                        \
+        static auto fnL() { return EXPR; }                                       \
         static constexpr const char* fmtL = FMT;                                 \
         static constexpr int LMI = 2, LNJ = 2;                                   \
     };
 // with a large-tile variant (launched for C22L / C22W): LMI x LNJ 32x32 blocks per wave
 #define CAD_KTL(NAME, EXPR, FMT, EXPRL, FMTL, LMI_, LNJ_)                        \
     template <int WM, int WN, int KB> struct NAME {                              \
-        static constexpr auto fn = EXPR;                                         \
+        static auto fn() { return EXPR; }                                        \
         static constexpr const char* fmt = FMT;                                  \
         static constexpr bool HASL = true;                                       \
-        static constexpr auto fnL = EXPRL;                                       \
+        static auto fnL() { return EXPRL; }                                      \
         static constexpr const char* fmtL = FMTL;                                \
         static constexpr int LMI = LMI_, LNJ = LNJ_;                             \
     };
@@ -496,25 +500,45 @@ int engine() {
     return g_engine;
 }
 // B1 stage depth (two k16 steps per LDS stage by default; CAD_BF16_KB=16|32)
-int bf16_kb() {
-    static int kb = 0;
-    if (!kb) {
+// B1 stage depth override (CAD_BF16_KB=16|32|64; 0 = per-kernel defaults below)
+int bf16_kb_env() {
+    static int kb = -1;
+    if (kb < 0) {
         const char* e = std::getenv("CAD_BF16_KB");
-        kb = (e && std::atoi(e) == 16) ? 16 : 32;
+        const int v = e ? std::atoi(e) : 0;
+        kb = (v == 16 || v == 32 || v == 64) ? v : 0;
     }
     return kb;
+}
+int ps_bf16_kb() { return bf16_kb_env() ? bf16_kb_env() : 32; }
+int bf16_kb() {   // in-loader B1 kernels (KS<KB> staging: 16 or 32)
+    return std::min(ps_bf16_kb(), 32);
 }
 template <template <int, int, int> class KT>
 void launch_b1(Cfg c, const GemmArgs& a, int splits, hipStream_t st) {
     if (bf16_kb() == 16) launch_cfg_kb<KT, 16>(c, a, splits, st);
     else launch_cfg_kb<KT, 32>(c, a, splits, st);
 }
+// pre-split B1 kernels may also stage 64 k per stage (four k16 steps between barriers)
+template <template <int, int, int> class KT>
+void launch_b1p(Cfg c, int kb, const GemmArgs& a, int splits, hipStream_t st) {
+    if (kb == 16) launch_cfg_kb<KT, 16>(c, a, splits, st);
+    else if (kb == 64) launch_cfg_kb<KT, 64>(c, a, splits, st);
+    else launch_cfg_kb<KT, 32>(c, a, splits, st);
+}
 int ps_planes() { return engine() == 1 ? 3 : engine() == 2 ? 1 : 0; }
-int ps_kb() { return engine() == 1 ? 16 : bf16_kb(); }
+// stage depth of a pre-split GEMM: S3 16 (three planes); B1 per kernel kind — 64 for the
+// conv3x3 forward/dgrad on 128x128 tiles (measured on MI355X: 708 -> 790 TFLOP/s), 32 elsewhere
+// (64 costs the weight-gradient and the tall/wide tiles 7-20%)
+int ps_kb(bool fwd_kind = false, Cfg c = C41) {
+    if (engine() == 1) return 16;
+    if (bf16_kb_env()) return bf16_kb_env();
+    return fwd_kind && c == C22 ? 64 : 32;
+}
 template <template <int, int, int> class KT3, template <int, int, int> class KT1>
-void launch_ps(Cfg c, const GemmArgs& a, int splits, hipStream_t st) {
+void launch_ps(Cfg c, int kb, const GemmArgs& a, int splits, hipStream_t st) {
     if (engine() == 1) launch_cfg_kb<KT3, 16>(c, a, splits, st);
-    else if (engine() == 2) launch_b1<KT1>(c, a, splits, st);
+    else if (engine() == 2) launch_b1p<KT1>(c, kb, a, splits, st);
     else throw std::runtime_error("pre-split GEMM launched on the f32 engine");
 }
 constexpr int kS3KB = 16;   // S3 stage depth (LDS: 3 bf16 planes per operand)
@@ -781,13 +805,13 @@ void split_rows(const float* x, int64_t ldx, int xcoff, int C, int64_t M, void* 
 
 namespace {
 // channel-major K order for the pre-split conv3x3 forward/dgrad (GemmArgs::cimajor); CAD_CIMAJOR=0 disables
-int cimajor_ok(int cin) {
+int cimajor_ok(int cin, int kb) {
     static int on = -1;
     if (on < 0) {
         const char* e = std::getenv("CAD_CIMAJOR");
         on = (e && e[0] == '0') ? 0 : 1;
     }
-    return on && cin % ps_kb() == 0 ? 1 : 0;
+    return on && cin % kb == 0 ? 1 : 0;
 }
 void ps_check(const Split& s, int channels, const char* what) {
     if (!s.p || s.ld % 8 || s.coff % 8 || channels % 8) throw std::runtime_error(std::string("pre-split operand: ") + what);
@@ -806,10 +830,11 @@ void conv3x3_fwd_ps(Split x, int cin, Split w, int cout, float* y, int64_t ldy, 
     a.C = y; a.ldc = ldy; a.c_coff = ycoff;
     a.stats = stats;
     const Cfg c = pick_cfg(a.M, a.N);
-    a.kstages_per_split = cdiv(a.K, ps_kb());
-    a.cimajor = cimajor_ok(cin);
-    if (stats) launch_ps<KConvFwdSP3, KConvFwdSP1>(c, a, 1, st);
-    else launch_ps<KConvFwdP3, KConvFwdP1>(c, a, 1, st);
+    const int kb = ps_kb(true, c);
+    a.kstages_per_split = cdiv(a.K, kb);
+    a.cimajor = cimajor_ok(cin, kb);
+    if (stats) launch_ps<KConvFwdSP3, KConvFwdSP1>(c, kb, a, 1, st);
+    else launch_ps<KConvFwdP3, KConvFwdP1>(c, kb, a, 1, st);
 }
 
 void conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t lddx, int B, int H, int W,
@@ -823,9 +848,10 @@ void conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t 
     a.Bm = (const float*)wd.p; a.ldb = wd.ld; a.b_coff = wd.coff;
     a.C = dx; a.ldc = lddx; a.c_coff = 0;
     const Cfg c = pick_cfg(a.M, a.N);
-    a.kstages_per_split = cdiv(a.K, ps_kb());
-    a.cimajor = cimajor_ok(cout);
-    launch_ps<KConvFwdP3, KConvFwdP1>(c, a, 1, st);
+    const int kb = ps_kb(true, c);
+    a.kstages_per_split = cdiv(a.K, kb);
+    a.cimajor = cimajor_ok(cout, kb);
+    launch_ps<KConvFwdP3, KConvFwdP1>(c, kb, a, 1, st);
 }
 
 void conv3x3_wgrad_ps(Split dz, int cout, Split x, int cin, float* dw, int B, int H, int W, float* slab,
@@ -845,7 +871,7 @@ void conv3x3_wgrad_ps(Split dz, int cout, Split x, int cin, float* dw, int B, in
     const int64_t per = (int64_t)a.M * a.N;
     a.ldc = a.N; a.slab_stride = per;
     a.C = s == 1 ? dw : slab;
-    launch_ps<KConvWgradP3, KConvWgradP1>(c, a, s, st);
+    launch_ps<KConvWgradP3, KConvWgradP1>(c, kb, a, s, st);
     if (s > 1) finish_slabs(slab, s, per, dw, st);
 }
 
@@ -860,8 +886,9 @@ void convT_fwd_ps(Split x, int cin, Split wf, const float* bias, int cout, float
     a.Bm = (const float*)wf.p; a.ldb = wf.ld; a.b_coff = wf.coff;
     a.C = y; a.ldc = ldy; a.c_coff = ycoff; a.bias = bias;
     const Cfg c = pick_cfg(a.M, a.N);
-    a.kstages_per_split = cdiv(a.K, ps_kb());
-    launch_ps<KConvTFwdP3, KConvTFwdP1>(c, a, 1, st);
+    const int kb = ps_kb();
+    a.kstages_per_split = cdiv(a.K, kb);
+    launch_ps<KConvTFwdP3, KConvTFwdP1>(c, kb, a, 1, st);
 }
 
 void convT_dgrad_ps(Split g, int cout, Split wm, int cin, float* dx, int B, int H, int W, hipStream_t st) {
@@ -874,8 +901,9 @@ void convT_dgrad_ps(Split g, int cout, Split wm, int cin, float* dx, int B, int 
     a.Bm = (const float*)wm.p; a.ldb = wm.ld; a.b_coff = wm.coff;
     a.C = dx; a.ldc = cin; a.c_coff = 0;
     const Cfg c = pick_cfg(a.M, a.N);
-    a.kstages_per_split = cdiv(a.K, ps_kb());
-    launch_ps<KConvTDgradP3, KConvTDgradP1>(c, a, 1, st);
+    const int kb = ps_kb();
+    a.kstages_per_split = cdiv(a.K, kb);
+    launch_ps<KConvTDgradP3, KConvTDgradP1>(c, kb, a, 1, st);
 }
 
 void convT_wgrad_ps(Split x, int cin, Split g, int cout, float* dw, int B, int H, int W, float* slab,
@@ -895,7 +923,7 @@ void convT_wgrad_ps(Split x, int cin, Split g, int cout, float* dw, int B, int H
     const int64_t per = (int64_t)a.M * a.N;
     a.ldc = a.N; a.slab_stride = per;
     a.C = s == 1 ? dw : slab;
-    launch_ps<KConvTWgradP3, KConvTWgradP1>(c, a, s, st);
+    launch_ps<KConvTWgradP3, KConvTWgradP1>(c, kb, a, s, st);
     if (s > 1) finish_slabs(slab, s, per, dw, st);
 }
 

@@ -13,8 +13,9 @@
 // Channel offsets and channel counts must be multiples of 8 (every U-Net conv except enc1.conv1's
 // 3/4-channel input, which keeps the in-loader split).  For NP = 1 this is plain NHWC bf16.
 //
-// Loaders own their staged registers (uint4 v[NV][NP], one 8-element chunk of one row per slot)
-// and write them to the LDS images of gemm_s3.hpp unchanged (planes [rows][LDK] for k-contiguous
+// Loaders fill caller-owned register sets (Regs: uint4 per 16-B piece; the bodies keep two, so a
+// stage's loads are in flight across two compute phases) and write them to the LDS images of
+// gemm_s3.hpp unchanged (planes [rows][LDK] for k-contiguous
 // operands, [k-rows][rows] for the weight-gradient operands), so fragment reads and MFMAs are shared.
 #pragma once
 #include "gemm_s3.hpp"
@@ -47,7 +48,7 @@ struct PsKcBase {
     static constexpr bool PRESPLIT = true;
     using G = PKc<ROWS, KB, NP>;
     static constexpr int NV = G::NV;
-    uint4 v[NV];
+    using Regs = uint4[NV];
     int lofs[NV];   // element offset in the operand image (plane * PL + swizzled (row, 8g))
     int grp[NV];    // the piece's 8-k group in the stage
     int prow[NV];   // the piece's tile row
@@ -67,7 +68,7 @@ struct PsKcBase {
     }
     // byte offset of the piece inside its row-stage: (g * NP + p) * 16
     __device__ uint32_t piece_off(int tid, int j) const { return (uint32_t)((tid + 256 * j) % G::PPR) * 16; }
-    __device__ void store(uint16_t* s) const {   // s: the operand image (plane 0)
+    __device__ void store(const Regs& v, uint16_t* s) const {   // s: the operand image (plane 0)
 #pragma unroll
         for (int j = 0; j < NV; ++j)
             if (act(j)) *reinterpret_cast<uint4*>(s + lofs[j]) = v[j];
@@ -97,18 +98,18 @@ struct PsKcDense : PsKcBase<ROWS, KB, NP> {
             roff[j] = (this->act(j) && row0 + this->prow[j] < nrows)
                           ? (uint32_t)(this->prow[j] * rowB) + this->piece_off(tid, j) : kOOB;
     }
-    __device__ void load() {
+    __device__ void load(typename Base::Regs& v) {
         if (cim) {   // every stage is whole (K = 9 cin, cin % KB == 0)
             const uint32_t ko = (uint32_t)((tap * cin + ci) >> 3) * 16 * NP;
 #pragma unroll
-            for (int j = 0; j < G::NV; ++j) this->v[j] = bload16(rs, roff[j] != kOOB ? roff[j] + ko : kOOB);
+            for (int j = 0; j < G::NV; ++j) v[j] = bload16(rs, roff[j] != kOOB ? roff[j] + ko : kOOB);
             if (++tap == 9) { tap = 0; ci += KB; }
             return;
         }
         const uint32_t ko = (uint32_t)(k0 >> 3) * 16 * NP;
 #pragma unroll
         for (int j = 0; j < G::NV; ++j)
-            this->v[j] = bload16(rs, (k0 + 8 * this->grp[j] < K && roff[j] != kOOB) ? roff[j] + ko : kOOB);
+            v[j] = bload16(rs, (k0 + 8 * this->grp[j] < K && roff[j] != kOOB) ? roff[j] + ko : kOOB);
         k0 += KB;
     }
 };
@@ -166,7 +167,7 @@ struct PsKcIm2col3x3 : PsKcBase<ROWS, KB, NP> {
             poff[j] = (uint32_t)((rr - pb) * rowB) + this->piece_off(tid, j) - (uint32_t)(this->grp[j] * NP * 16);
         }
     }
-    __device__ void load() {
+    __device__ void load(typename Base::Regs& v) {
         if (cim) {   // one tap per stage, groups = consecutive channels
             const int dy = tap / 3 - 1, dx = tap - 3 * (tap / 3) - 1;
             const int off = (dy * W + dx) * rowB + (ci >> 3) * 16 * NP;
@@ -174,7 +175,7 @@ struct PsKcIm2col3x3 : PsKcBase<ROWS, KB, NP> {
             for (int j = 0; j < G::NV; ++j) {
                 const int yy = y[j] + dy, xx = x[j] + dx;
                 const bool g = ok[j] && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
-                this->v[j] = bload16(rs, g ? poff[j] + (uint32_t)(off + this->grp[j] * 16 * NP) : kOOB);
+                v[j] = bload16(rs, g ? poff[j] + (uint32_t)(off + this->grp[j] * 16 * NP) : kOOB);
             }
             if (++tap == 9) { tap = 0; ci += KB; }
             return;
@@ -193,7 +194,7 @@ struct PsKcIm2col3x3 : PsKcBase<ROWS, KB, NP> {
             const int yy = y[j] + dy, xx = x[j] + dx;
             const bool g = ok[j] && kin && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
             const int off = (dy * W + dx) * rowB + (c >> 3) * 16 * NP;
-            this->v[j] = bload16(rs, g ? poff[j] + (uint32_t)off : kOOB);
+            v[j] = bload16(rs, g ? poff[j] + (uint32_t)off : kOOB);
         }
         tapci_advance<KB>(tap, ci, cin);
     }
@@ -230,7 +231,7 @@ struct PsKcUpGather : PsKcBase<ROWS, KB, NP> {
                           : kOOB;
         }
     }
-    __device__ void load() {
+    __device__ void load(typename Base::Regs& v) {
         GroupTaps<G::NG> gt;
         gt.from(q, co, cout);
 #pragma unroll
@@ -242,7 +243,7 @@ struct PsKcUpGather : PsKcBase<ROWS, KB, NP> {
             const bool kin = t < 4;
             const int qq = kin ? t : 0;
             const uint32_t off = (uint32_t)(((qq >> 1) * W2 + (qq & 1)) * rowB + (c >> 3) * 16 * NP);
-            this->v[j] = bload16(rs, kin && hoff[j] != kOOB ? hoff[j] + off : kOOB);
+            v[j] = bload16(rs, kin && hoff[j] != kOOB ? hoff[j] + off : kOOB);
         }
         tapci_advance<KB>(q, co, cout);
     }
@@ -265,7 +266,7 @@ template <int ROWS, int KB, int NP>
 struct PsMNcBase {
     using G = PMNc<ROWS, KB>;
     static constexpr int NV = G::NV;
-    uint4 v[NV][NP];
+    using Regs = uint4[NV][NP];
     int lofs[NV];   // byte offset of the chunk in a plane (gemm_s3.hpp S3M)
     bool act;
     __device__ void init_lds(int tid) {
@@ -273,7 +274,7 @@ struct PsMNcBase {
 #pragma unroll
         for (int j = 0; j < NV; ++j) lofs[j] = S3M<ROWS>::off(tid / G::TPR + G::KSTEP * j, (tid % G::TPR) * 8);
     }
-    __device__ void store(char* s) const {   // s: plane 0 of the operand image
+    __device__ void store(const Regs& v, char* s) const {   // s: plane 0 of the operand image
         constexpr int PL = KB * S3M<ROWS>::STRIDE;
         if (!act) return;
 #pragma unroll
@@ -302,14 +303,14 @@ struct PsMNcDense : PsMNcBase<ROWS, KB, NP> {
         k0 = kb0 + tid / G::TPR;
         koff = (uint32_t)((tid / G::TPR) * rowB + (tid % G::TPR) * 16 * NP);
     }
-    __device__ void load() {
+    __device__ void load(typename Base::Regs& v) {
 #pragma unroll
         for (int j = 0; j < G::NV; ++j) {
             const int k = k0 + G::KSTEP * j;
             const bool g = rok && k < Kp;
 #pragma unroll
             for (int p = 0; p < NP; ++p)
-                this->v[j][p] = bload16(rs, g ? koff + (uint32_t)(G::KSTEP * j * rowB) + p * 16 : kOOB);
+                v[j][p] = bload16(rs, g ? koff + (uint32_t)(G::KSTEP * j * rowB) + p * 16 : kOOB);
         }
         k0 += KB;
         koff += (uint32_t)(KB * rowB);
@@ -346,14 +347,14 @@ struct PsMNcIm2col3x3 : PsMNcBase<ROWS, KB, NP> {
             y[i] = (kk / W) % H;
         }
     }
-    __device__ void load() {
+    __device__ void load(typename Base::Regs& v) {
 #pragma unroll
         for (int j = 0; j < G::NV; ++j) {
             const int yy = y[j] + dy, xx = x[j] + dx;
             const bool g = rok && k[j] < Kp && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
             const uint32_t off = (uint32_t)((k[j] - pb) * rowB + tapoff);
 #pragma unroll
-            for (int p = 0; p < NP; ++p) this->v[j][p] = bload16(rs, g ? off + p * 16 : kOOB);
+            for (int p = 0; p < NP; ++p) v[j][p] = bload16(rs, g ? off + p * 16 : kOOB);
             int b = 0;
             px_advance<KB>(x[j], y[j], b, W, H);
             k[j] += KB;
@@ -397,14 +398,14 @@ struct PsMNcUpGather : PsMNcBase<ROWS, KB, NP> {
             b[i] = t / H;
         }
     }
-    __device__ void load() {
+    __device__ void load(typename Base::Regs& v) {
 #pragma unroll
         for (int j = 0; j < G::NV; ++j) {
             const bool g = rok && k[j] < Kp;
             const int64_t hp = ((int64_t)b[j] * (2 * H) + 2 * y[j] + qy) * (2 * W) + 2 * x[j] + qx;
             const uint32_t off = (uint32_t)((hp - hb) * rowB + cooff);
 #pragma unroll
-            for (int p = 0; p < NP; ++p) this->v[j][p] = bload16(rs, g ? off + p * 16 : kOOB);
+            for (int p = 0; p < NP; ++p) v[j][p] = bload16(rs, g ? off + p * 16 : kOOB);
             px_advance<KB>(x[j], y[j], b[j], W, H);
             k[j] += KB;
         }
@@ -412,9 +413,32 @@ struct PsMNcUpGather : PsMNcBase<ROWS, KB, NP> {
 };
 
 // --------------------------------------------------------------------------------------------
-// engine bodies: the S3/B1 pipeline of gemm_s3.hpp (register-staged, double-buffered LDS, one
-// barrier per stage) with the split moved out of the loop
+// engine bodies: double-buffered LDS, one barrier per stage, one register set per operand (the
+// loads of stage k+1 are in flight while stage k is computed).  A two-set variant (loads two
+// compute phases ahead) measured slower on MI355X: the second set costs ~50 VGPRs and a wave per
+// SIMD (B1 128x128 GEMMs 700 -> 544 TFLOP/s), more than the deeper prefetch returns.
 // --------------------------------------------------------------------------------------------
+template <class LA, class LB, class Compute, class StoreAB>
+__device__ __forceinline__ void ps_pipeline(LA& la, LB& lb, int kbeg, int kend, Compute compute, StoreAB store_ab) {
+    typename LA::Regs ra;
+    typename LB::Regs rb;
+    if (kbeg < kend) {
+        la.load(ra);
+        lb.load(rb);
+        store_ab(0, ra, rb);
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int kt = kbeg; kt < kend; ++kt) {
+        const bool more = kt + 1 < kend;
+        if (more) { la.load(ra); lb.load(rb); }
+        compute(cur);
+        if (more) store_ab(cur ^ 1, ra, rb);
+        __syncthreads();
+        cur ^= 1;
+    }
+}
+
 template <int NP, int WM, int WN, int MI, int NJ, int KB, class LA, class LB, class Epi, class InitA, class InitB>
 __device__ __forceinline__ void gemm_body_ps(const GemmArgs& a, InitA init_a, InitB init_b, Epi epi) {
     constexpr int BM = 32 * MI * WM, BN = 32 * NJ * WN;
@@ -443,12 +467,12 @@ __device__ __forceinline__ void gemm_body_ps(const GemmArgs& a, InitA init_a, In
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    auto stage_store = [&](int buf) {
+    auto store_ab = [&](int buf, const typename LA::Regs& xa, const typename LB::Regs& xb) {
         uint16_t* da = lds + buf * (SA + SB);
-        la.store(da);
-        lb.store(da + SA);
+        la.store(xa, da);
+        lb.store(xb, da + SA);
     };
-    auto stage_compute = [&](int buf) {
+    auto compute = [&](int buf) {
         const uint16_t* sa = lds + buf * (SA + SB);
         const uint16_t* sb = sa + SA;
 #pragma unroll
@@ -461,22 +485,7 @@ __device__ __forceinline__ void gemm_body_ps(const GemmArgs& a, InitA init_a, In
             s3_mfma<NP>(acc, fa, fb);
         }
     };
-
-    if (kbeg < kend) {
-        la.load();
-        lb.load();
-        stage_store(0);
-    }
-    __syncthreads();
-    int cur = 0;
-    for (int kt = kbeg; kt < kend; ++kt) {
-        const bool more = kt + 1 < kend;
-        if (more) { la.load(); lb.load(); }
-        stage_compute(cur);
-        if (more) stage_store(cur ^ 1);
-        __syncthreads();
-        cur ^= 1;
-    }
+    ps_pipeline(la, lb, kbeg, kend, compute, store_ab);
     gemm_epilogue_t<WM, WN, MI, NJ>(a, acc, tile, reinterpret_cast<float*>(lds), epi);
 }
 
@@ -508,12 +517,12 @@ __device__ __forceinline__ void gemm_body_psm(const GemmArgs& a, InitA init_a, I
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    auto stage_store = [&](int buf) {
+    auto store_ab = [&](int buf, const typename LA::Regs& xa, const typename LB::Regs& xb) {
         char* da = lds + buf * (SA + SB);
-        la.store(da);
-        lb.store(da + SA);
+        la.store(xa, da);
+        lb.store(xb, da + SA);
     };
-    auto stage_compute = [&](int buf) {
+    auto compute = [&](int buf) {
         const char* sa = lds + buf * (SA + SB);
         const char* sb = sa + SA;
 #pragma unroll
@@ -526,22 +535,7 @@ __device__ __forceinline__ void gemm_body_psm(const GemmArgs& a, InitA init_a, I
             s3_mfma<NP>(acc, fa, fb);
         }
     };
-
-    if (kbeg < kend) {
-        la.load();
-        lb.load();
-        stage_store(0);
-    }
-    __syncthreads();
-    int cur = 0;
-    for (int kt = kbeg; kt < kend; ++kt) {
-        const bool more = kt + 1 < kend;
-        if (more) { la.load(); lb.load(); }
-        stage_compute(cur);
-        if (more) stage_store(cur ^ 1);
-        __syncthreads();
-        cur ^= 1;
-    }
+    ps_pipeline(la, lb, kbeg, kend, compute, store_ab);
     gemm_epilogue_t<WM, WN, MI, NJ>(a, acc, tile, reinterpret_cast<float*>(lds), epi);
 }
 

@@ -91,9 +91,9 @@ __device__ __forceinline__ auto split_np(float4 v) {
 // Stage geometry: KB k per LDS stage = KB/16 bf16 MFMA k-steps.
 template <int KB>
 struct S3 {
-    static_assert(KB == 16 || KB == 32, "S3/B1 stage depth");
+    static_assert(KB == 16 || KB == 32 || KB == 64, "S3/B1 stage depth (64: pre-split B1 only)");
     static constexpr bool SWZ = KB == 16;
-    static constexpr int LDK = SWZ ? 16 : KB + 8;   // bf16 elements per plane row
+    static constexpr int LDK = SWZ ? 16 : KB + 8;   // bf16 elements per plane row (80 / 144 B: conflict-free b128)
     static constexpr int KSTEPS = KB / 16;
 };
 
@@ -227,9 +227,10 @@ __device__ __forceinline__ void gemm_body_s3(const GemmArgs& a, InitA init_a, In
     constexpr bool BPS = is_presplit<LB>::value;
     float4 ra[LA::NV];
     float4 rb[BPS ? 1 : LB::NV];
+    uint4 rbp[BPS ? LB::NV : 1];   // pre-split B pieces (gemm_ps.hpp PsKcBase::Regs)
     auto load_ab = [&]() {
         la.load(ra);
-        if constexpr (BPS) lb.load(); else lb.load(rb);
+        if constexpr (BPS) lb.load(rbp); else lb.load(rb);
     };
     auto stage_store = [&](int buf) {
         la.finish(ra);
@@ -237,7 +238,7 @@ __device__ __forceinline__ void gemm_body_s3(const GemmArgs& a, InitA init_a, In
         if constexpr (AF32) kc_store_nat<BM, KB>(reinterpret_cast<float*>(da), ra);
         else s3_store<BM, KB, NP>(da, ra);
         if constexpr (BPS) {
-            lb.store(da + SA);
+            lb.store(rbp, da + SA);
         } else {
             lb.finish(rb);
             s3_store<BN, KB, NP>(da + SA, rb);
