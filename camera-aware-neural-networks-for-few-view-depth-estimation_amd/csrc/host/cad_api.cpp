@@ -187,6 +187,13 @@ struct cad_unet {
     // backward
     float* dcat[4] = {};
     float *Sa = nullptr, *Sb = nullptr, *Sc = nullptr;
+    float* Sd = nullptr;           // bn1's dL/dz while the side stream still reads bn2's (Sb)
+    void* dYs1 = nullptr;          // its split twin
+    // CAD_OVERLAP=1: weight-gradient GEMMs run on a second stream, overlapping the dgrad GEMMs and
+    // the HBM-bound BN / pooling backward passes of the same stage (joined at the end of every
+    // backward stage)
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     float* stats = nullptr;    // conv-epilogue BN partials
     double* dscr = nullptr;    // column-reduction scratch
     float* slab = nullptr;
@@ -381,6 +388,8 @@ void layout(cad_unet* h, Arena& a) {
     h->Sa = a.f(M0C0);
     h->Sb = a.f(M0C0);
     h->Sc = a.f(h->Ml(1, B) * h->Cl(0));
+    h->Sd = a.f(M0C0);
+    h->dYs1 = sp(M0C0);
     // BN tile partials: rows x 2C, max over layers
     int64_t st = 0, colmax = 0;
     for (int l = 0; l < 5; ++l) {
@@ -592,27 +601,44 @@ void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth
 // ------------------------------------------------------------------------------------------
 // g: grad wrt the DoubleConv output (ld ldg, channel offset gcoff); in: the block input (ld ldin,
 // cin channels; in_s its split twin); din: where conv1's dgrad goes (nullptr = not needed), ld lddin.
+// side-stream fork / join (no-ops without a side stream)
+void fork_side(cad_unet* h, hipStream_t st) {
+    if (!h->side) return;
+    HIPCHK(hipEventRecord(h->ev_fork, st));
+    HIPCHK(hipStreamWaitEvent(h->side, h->ev_fork, 0));
+}
+void join_side(cad_unet* h, hipStream_t st) {
+    if (!h->side) return;
+    HIPCHK(hipEventRecord(h->ev_join, h->side));
+    HIPCHK(hipStreamWaitEvent(st, h->ev_join, 0));
+}
+
 void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, int gcoff, const float* in,
                      int64_t ldin, cad::Split in_s, int B, float* din, int64_t lddin, hipStream_t st) {
     const int l = dc.level, Hh = h->Hl(l), Ww = h->Wl(l), C = dc.c1.cout;
     const int64_t M = h->Ml(l, B);
     const bool ps = h->fwd_np > 0 && h->fwd_np == cad::split_planes();
-    float* dY = h->Sb;
+    const hipStream_t ws = h->side ? h->side : st;   // weight-gradient stream
+    float* dY2 = h->Sb;
+    float* dY1 = h->side ? h->Sd : h->Sb;
+    void* dYs2 = h->dYs;
+    void* dYs1 = h->side ? h->dYs1 : h->dYs;
     float* dA1 = h->Sa;
     // bn2 + relu
     cad::bn_relu_bwd(g, ldg, gcoff, dc.y2, C, dc.b2.mean, dc.b2.invstd, dc.b2.scale, dc.b2.shift, h->P(dc.b2.widx), M,
-                     h->dscr, dc.b2.coef, h->G(dc.b2.widx), h->G(dc.b2.bidx), dY, st, nullptr, 1, ps ? h->dYs : nullptr);
-    // conv2
+                     h->dscr, dc.b2.coef, h->G(dc.b2.widx), h->G(dc.b2.bidx), dY2, st, nullptr, 1, ps ? dYs2 : nullptr);
+    fork_side(h, st);
+    // conv2: wgrad (side) || dgrad (caller's stream)
     if (ps) {
-        cad::conv3x3_wgrad_ps(sv(h->dYs, C), C, sv(dc.a1s, C), C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
-        cad::conv3x3_dgrad_ps(sv(h->dYs, C), C, sv(dc.c2.wds, 9 * C), C, dA1, C, B, Hh, Ww, st);
+        cad::conv3x3_wgrad_ps(sv(dYs2, C), C, sv(dc.a1s, C), C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, ws);
+        cad::conv3x3_dgrad_ps(sv(dYs2, C), C, sv(dc.c2.wds, 9 * C), C, dA1, C, B, Hh, Ww, st);
     } else {
         if (dc.a1)
-            cad::conv3x3_wgrad(dY, C, dc.a1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
+            cad::conv3x3_wgrad(dY2, C, dc.a1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, ws);
         else
-            cad::conv3x3_wgrad(dY, C, dc.y1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st,
+            cad::conv3x3_wgrad(dY2, C, dc.y1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, ws,
                                dc.b1.scale, dc.b1.shift);
-        cad::conv3x3_dgrad(dY, C, dc.c2.wd, C, dA1, C, B, Hh, Ww, st, h->wsplit ? dc.c2.wds : nullptr);
+        cad::conv3x3_dgrad(dY2, C, dc.c2.wd, C, dA1, C, B, Hh, Ww, st, h->wsplit ? dc.c2.wds : nullptr);
     }
     // FiLM: dgamma/dbeta per (sample, channel); the ReLU sees dA1 * gamma (folded into bn_relu_bwd)
     const int64_t HW = (int64_t)Hh * Ww;
@@ -620,20 +646,21 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
         cad::film_affine_bwd(dA1, dc.y1, C, dc.b1.scale, dc.b1.shift, B, HW, h->dscr, dc.film.dgam, dc.film.dbet, st);
     // bn1 + relu
     cad::bn_relu_bwd(dA1, C, 0, dc.y1, C, dc.b1.mean, dc.b1.invstd, dc.b1.scale, dc.b1.shift, h->P(dc.b1.widx), M,
-                     h->dscr, dc.b1.coef, h->G(dc.b1.widx), h->G(dc.b1.bidx), dY, st,
-                     dc.has_film() ? dc.film.gam : nullptr, HW, ps ? h->dYs : nullptr);
+                     h->dscr, dc.b1.coef, h->G(dc.b1.widx), h->G(dc.b1.bidx), dY1, st,
+                     dc.has_film() ? dc.film.gam : nullptr, HW, ps ? dYs1 : nullptr);
     if (dc.has_film()) cad::film_mlp_bwd(film_view(h, dc), h->camn, B, st);
-    // conv1
+    fork_side(h, st);
+    // conv1: wgrad (side) || dgrad (caller's stream)
     const bool ps1 = ps && in_s.p && dc.c1.ws;
     if (ps1)
-        cad::conv3x3_wgrad_ps(sv(h->dYs, C), C, in_s, dc.c1.cin, h->G(dc.c1.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
+        cad::conv3x3_wgrad_ps(sv(dYs1, C), C, in_s, dc.c1.cin, h->G(dc.c1.pidx), B, Hh, Ww, h->slab, h->slab_cap, ws);
     else
-        cad::conv3x3_wgrad(dY, C, in, ldin, 0, dc.c1.cin, h->G(dc.c1.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
+        cad::conv3x3_wgrad(dY1, C, in, ldin, 0, dc.c1.cin, h->G(dc.c1.pidx), B, Hh, Ww, h->slab, h->slab_cap, ws);
     if (din) {
         if (ps && dc.c1.wds)
-            cad::conv3x3_dgrad_ps(sv(h->dYs, C), C, sv(dc.c1.wds, 9 * C), dc.c1.cin, din, lddin, B, Hh, Ww, st);
+            cad::conv3x3_dgrad_ps(sv(dYs1, C), C, sv(dc.c1.wds, 9 * C), dc.c1.cin, din, lddin, B, Hh, Ww, st);
         else
-            cad::conv3x3_dgrad(dY, C, dc.c1.wd, dc.c1.cin, din, lddin, B, Hh, Ww, st, h->wsplit ? dc.c1.wds : nullptr);
+            cad::conv3x3_dgrad(dY1, C, dc.c1.wd, dc.c1.cin, din, lddin, B, Hh, Ww, st, h->wsplit ? dc.c1.wds : nullptr);
     }
 }
 
@@ -675,14 +702,16 @@ void backward_stage(cad_unet* h, int stage, const float* dpred, hipStream_t st) 
         const Up& u = h->up[l];
         const float* upin = l == 3 ? h->a2_bott : h->dout[l + 1];
         const void* upins = l == 3 ? h->botts : h->douts[l + 1];
-        // up (ConvTranspose2d) backward: grad of its output = dcat[:, C:2C]
+        const hipStream_t ws = h->side ? h->side : st;
+        // up (ConvTranspose2d) backward: grad of its output = dcat[:, C:2C]; wgrad on the side stream
+        if (ps) cad::split_rows(h->dcat[l], 2 * C, C, C, h->Ml(l, B), h->dcats[l], C, 0, st);
+        fork_side(h, st);
         if (ps) {
-            cad::split_rows(h->dcat[l], 2 * C, C, C, h->Ml(l, B), h->dcats[l], C, 0, st);
             cad::convT_wgrad_ps(sv(upins, u.cin), u.cin, sv(h->dcats[l], C), u.cout, h->G(u.widx), B, h->Hl(l + 1),
-                                h->Wl(l + 1), h->slab, h->slab_cap, st);
+                                h->Wl(l + 1), h->slab, h->slab_cap, ws);
         } else {
             cad::convT_wgrad(upin, u.cin, h->dcat[l], 2 * C, C, u.cout, h->G(u.widx), B, h->Hl(l + 1), h->Wl(l + 1),
-                             h->slab, h->slab_cap, st);
+                             h->slab, h->slab_cap, ws);
         }
         cad::colsum(h->dcat[l], 2 * C, C, h->Ml(l, B), C, h->dscr, st);
         cad::colsum_finalize(h->dscr, cad::colsum_slices(h->Ml(l, B)), C, h->G(u.bidx), 1.f, st);
@@ -692,6 +721,7 @@ void backward_stage(cad_unet* h, int stage, const float* dpred, hipStream_t st) 
         else
             cad::convT_dgrad(h->dcat[l], 2 * C, C, u.cout, h->P(u.widx), u.cin, h->Sa, B, h->Hl(l + 1), h->Wl(l + 1), st,
                              h->wsplit ? u.wms : nullptr);
+        join_side(h, st);   // the stage's gradients are complete on the caller's stream
         return;
     }
     // encoder side: stage 5 = bottleneck (level 4), 6..9 = enc4..enc1 (levels 3..0)
@@ -702,11 +732,13 @@ void backward_stage(cad_unet* h, int stage, const float* dpred, hipStream_t st) 
     const int64_t ldg = l == 4 ? C : 2 * C;
     if (l == 0) {
         double_conv_bwd(h, e, g, ldg, 0, h->x0, h->x0_ld, sv(h->x0s, h->x0_ld), B, nullptr, 0, st);
+        join_side(h, st);
         return;
     }
     const int Cp = h->Cl(l - 1);
     double_conv_bwd(h, e, g, ldg, 0, h->pool[l], Cp, sv(h->pools[l], Cp), B, h->Sc, Cp, st);
     cad::maxpool_bwd(h->Sc, h->pidx[l], Cp, B, h->Hl(l - 1), h->Wl(l - 1), h->dcat[l - 1], 2 * Cp, st);
+    join_side(h, st);
 }
 
 void compute_stage_ranges(cad_unet* h) {
@@ -880,6 +912,15 @@ cad_status cad_unet_create_model(const cad_unet_desc* d, int model, int device, 
         real.base = static_cast<char*>(base);
         layout(h.get(), real);
         require(real.off == sz.off, "internal: arena layout differs between the sizing and the real pass", CAD_ERR_STATE);
+        // off by default: measured +1 % on MI355X (the S3 GEMMs hold the chip at its power limit,
+        // the B1 ones at its memory latency), and concurrent kernels blur the per-launch HIP-event
+        // timing bench.py reports as roofline.achieved
+        const char* ov = std::getenv("CAD_OVERLAP");
+        if (ov && ov[0] == '1') {
+            HIPCHK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+            HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+        }
         compute_stage_ranges(h.get());
         default_init(h.get());
         HIPCHK(hipDeviceSynchronize());
@@ -890,6 +931,12 @@ cad_status cad_unet_create_model(const cad_unet_desc* d, int model, int device, 
 void cad_unet_destroy(cad_unet* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
+    if (h->side) {
+        (void)hipStreamSynchronize(h->side);
+        (void)hipStreamDestroy(h->side);
+        (void)hipEventDestroy(h->ev_fork);
+        (void)hipEventDestroy(h->ev_join);
+    }
     (void)hipFree(h->arena_base);
     delete h;
 }
