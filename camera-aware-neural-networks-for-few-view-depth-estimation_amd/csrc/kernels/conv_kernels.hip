@@ -60,6 +60,24 @@ struct EpiConvT {
             }
         }
     }
+    // 4 consecutive rows m..m+3 at column n (the 16x16 MFMA layout's quads)
+    __device__ void quad(const GemmArgs& a, int m, int n, const float (&v)[4]) const {
+        if (n >= a.N) return;
+        const int cout = a.N >> 2;
+        const int q = n / cout, co = n - q * cout;
+        const float bias = a.bias[co];
+        float* dst = a.C + a.c_coff + co;
+        const int64_t W2 = 2 * a.W;
+        int x = m % a.W, t = m / a.W, y = t % a.H, b = t / a.H;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            if (m + r < a.M) {
+                const int64_t hp = ((int64_t)b * (2 * a.H) + 2 * y + (q >> 1)) * W2 + 2 * x + (q & 1);
+                dst[hp * a.ldc] = v[r] + bias;
+            }
+            if (++x == a.W) { x = 0; if (++y == a.H) { y = 0; ++b; } }
+        }
+    }
 };
 struct EpiSlab {   // split-K partial: slab z holds C[m][n] of K-slice z
     static constexpr bool STATS = false;

@@ -29,6 +29,7 @@
 namespace cad {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 #ifndef CAD_XCD_SWIZZLE
 #define CAD_XCD_SWIZZLE 0
@@ -486,23 +487,39 @@ __device__ __forceinline__ const float* epi_row_base(const GemmArgs& a, int m0, 
     else return Epi::row_base(a, m0, z);
 }
 
-// Epilogue shared by the engines: element (m, n) of sub-block (i, j), register r of the 32x32 C/D
-// layout (dtype-independent on gfx950).  `lds` is free scratch (the main loop ended on a barrier).
-// Each wave owns MI x NJ blocks of 32x32: a (32 MI) x (32 NJ) sub-tile; the tile is WM x WN waves.
-template <int WM, int WN, int MI, int NJ, class Epi>
-__device__ __forceinline__ void gemm_epilogue_t(const GemmArgs& a, floatx16 (&acc)[MI][NJ], const TileId& tile,
-                                                float* lds, Epi epi) {
+// Epilogue shared by the engines.  Each wave owns MI x NJ blocks of 32x32: a (32 MI) x (32 NJ)
+// sub-tile; the tile is WM x WN waves.  A block's 16 accumulator values per lane are visited as four
+// "quads" of 4 consecutive rows at one column:
+//   32x32 MFMA layout (acc: floatx16 [MI][NJ]): quad g = registers 4g..4g+3, rows 4(lane>>5) + 8g,
+//     column lane & 31;
+//   16x16 MFMA layout (acc: floatx4 [2MI][2NJ], the four 16x16 sub-blocks s = (s>>1, s&1) of a
+//     block): quad s = sub-block s, rows 16(s>>1) + 4(lane>>4), column 16(s&1) + (lane&15).
+// `lds` is free scratch (the main loop ended on a barrier).
+template <int MI, int NJ>
+__device__ __forceinline__ void epi_quad(const floatx16 (&acc)[MI][NJ], int i, int j, int g, float (&v)[4]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = acc[i][j][4 * g + r];
+}
+template <int MI, int NJ>
+__device__ __forceinline__ void epi_quad(const floatx4 (&acc)[2 * MI][2 * NJ], int i, int j, int g, float (&v)[4]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = acc[2 * i + (g >> 1)][2 * j + (g & 1)][r];
+}
+
+template <int WM, int WN, int MI, int NJ, class Epi, class Acc>
+__device__ __forceinline__ void gemm_epilogue_t(const GemmArgs& a, const Acc& acc, const TileId& tile, float* lds,
+                                                Epi epi) {
+    constexpr bool S16 = std::is_same<std::remove_cv_t<std::remove_all_extents_t<Acc>>, floatx4>::value;
     constexpr int BM = 32 * MI * WM, BN = 32 * NJ * WN;
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
     const int wm = wave / WN, wn = wave % WN;
     const int m0 = tile.x * BM, n0 = tile.y * BN;
     // With STATS the per-column BN partials are accumulated in the same pass (each accumulator is read once: keeping them live
-    // for a second pass costs 64 VGPRs and an occupancy step).
-    const int h = lane >> 5, col = lane & 31;
-    float ssum[NJ], ssq[NJ];
+    // for a second pass costs 64 VGPRs and an occupancy step).  ssum[j][slot]: the lane's column(s) of block column j.
+    float ssum[NJ][2], ssq[NJ][2];
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) ssum[j] = ssq[j] = 0.f;
+    for (int j = 0; j < NJ; ++j) ssum[j][0] = ssq[j][0] = ssum[j][1] = ssq[j][1] = 0.f;
     // Row-major epilogues (EpiStore, EpiSlab) store through a buffer descriptor based at the tile's
     // first output row whose range ends at row M: rows past M are dropped by the range check and
     // columns past N get an out-of-range offset, so each store is one 32-bit offset add.
@@ -514,23 +531,35 @@ __device__ __forceinline__ void gemm_epilogue_t(const GemmArgs& a, floatx16 (&ac
     for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-            const int n = n0 + wn * 32 * NJ + j * 32 + col;
-            if constexpr (is_structured<Epi>::value) {
+            if constexpr (is_structured<Epi>::value && !S16) {
                 static_assert(!Epi::STATS, "structured epilogues carry no BN partials");
-                epi.block(a, m0 + wm * 32 * MI + i * 32 + 4 * h, n, acc[i][j]);
-            } else {
-                const int mr = wm * 32 * MI + i * 32 + 4 * h;   // tile-relative row of register 0
-                const uint32_t lo = n < a.N ? (uint32_t)(mr * ldc4 + (int64_t)n * 4) : kOOB;
+                epi.block(a, m0 + wm * 32 * MI + i * 32 + 4 * (lane >> 5), n0 + wn * 32 * NJ + j * 32 + (lane & 31),
+                          acc[i][j]);
+                continue;
+            }
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int dr = (r & 3) + 8 * (r >> 2);
-                    const float v = acc[i][j][r];
-                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rs,
-                                                          lo + (uint32_t)(dr * ldc4), 0, 0);
-                    if constexpr (Epi::STATS) {
-                        const float vm = m0 + mr + dr < a.M ? v : 0.f;
-                        ssum[j] += vm;
-                        ssq[j] += vm * vm;
+            for (int g = 0; g < 4; ++g) {
+                const int slot = S16 ? (g & 1) : 0;
+                const int cw = S16 ? j * 32 + 16 * (g & 1) + (lane & 15) : j * 32 + (lane & 31);
+                const int rw = S16 ? i * 32 + 16 * (g >> 1) + 4 * (lane >> 4) : i * 32 + 4 * (lane >> 5) + 8 * g;
+                const int n = n0 + wn * 32 * NJ + cw;
+                const int mr = wm * 32 * MI + rw;   // tile-relative row of the quad's first register
+                float v[4];
+                epi_quad<MI, NJ>(acc, i, j, g, v);
+                if constexpr (is_structured<Epi>::value) {
+                    static_assert(!Epi::STATS, "structured epilogues carry no BN partials");
+                    epi.quad(a, m0 + mr, n, v);
+                } else {
+                    const uint32_t lo = n < a.N ? (uint32_t)(mr * ldc4 + (int64_t)n * 4) : kOOB;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[r]), rs,
+                                                              lo + (uint32_t)(r * ldc4), 0, 0);
+                        if constexpr (Epi::STATS) {
+                            const float vm = m0 + mr + r < a.M ? v[r] : 0.f;
+                            ssum[j][slot] += vm;
+                            ssq[j][slot] += vm * vm;
+                        }
                     }
                 }
             }
@@ -541,15 +570,22 @@ __device__ __forceinline__ void gemm_epilogue_t(const GemmArgs& a, floatx16 (&ac
         // the main loop ended on a barrier, so the LDS operand buffers are free for the reduction
         float* red = lds;   // [WM][BN][2]
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const float s = ssum[j] + __shfl_xor(ssum[j], 32);
-            const float q = ssq[j] + __shfl_xor(ssq[j], 32);
-            if (h == 0) {
-                const int cl = wn * 32 * NJ + j * 32 + col;
-                red[(wm * BN + cl) * 2 + 0] = s;
-                red[(wm * BN + cl) * 2 + 1] = q;
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int slot = 0; slot < (S16 ? 2 : 1); ++slot) {
+                float s = ssum[j][slot], q = ssq[j][slot];
+                if constexpr (S16) {   // lanes sharing a column: lane & 15 equal
+                    s += __shfl_xor(s, 16);
+                    q += __shfl_xor(q, 16);
+                }
+                s += __shfl_xor(s, 32);
+                q += __shfl_xor(q, 32);
+                if (S16 ? lane < 16 : lane < 32) {
+                    const int cl = wn * 32 * NJ + j * 32 + (S16 ? 16 * slot + lane : lane);
+                    red[(wm * BN + cl) * 2 + 0] = s;
+                    red[(wm * BN + cl) * 2 + 1] = q;
+                }
             }
-        }
         __syncthreads();
         for (int c = tid; c < BN; c += 256) {
             float s = 0.f, q = 0.f;

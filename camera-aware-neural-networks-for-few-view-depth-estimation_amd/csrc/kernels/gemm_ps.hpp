@@ -459,13 +459,9 @@ __device__ __forceinline__ void gemm_body_ps(const GemmArgs& a, InitA init_a, In
     init_a(la, m0, tid, kbeg);
     init_b(lb, n0, tid, kbeg);
 
-    floatx16 acc[MI][NJ];
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    constexpr bool S16 = Mma16<NP, KB>::ON;
+    WaveAcc<MI, NJ, S16> acc;
+    acc.zero();
 
     auto store_ab = [&](int buf, const typename LA::Regs& xa, const typename LB::Regs& xb) {
         uint16_t* da = lds + buf * (SA + SB);
@@ -475,18 +471,22 @@ __device__ __forceinline__ void gemm_body_ps(const GemmArgs& a, InitA init_a, In
     auto compute = [&](int buf) {
         const uint16_t* sa = lds + buf * (SA + SB);
         const uint16_t* sb = sa + SA;
+        if constexpr (S16) {
+            stage16_kc<NP, KB, BM, BN, MI, NJ, false>(acc.v, sa, sb, wm * 32 * MI, wn * 32 * NJ);
+        } else {
 #pragma unroll
-        for (int q = 0; q < S3<KB>::KSTEPS; ++q) {
-            bf16x8 fa[MI][NP], fb[NJ][NP];
+            for (int q = 0; q < S3<KB>::KSTEPS; ++q) {
+                bf16x8 fa[MI][NP], fb[NJ][NP];
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) s3_frag<BN, KB, NP>(sb, wn * 32 * NJ + j * 32, q, fb[j]);
+                for (int j = 0; j < NJ; ++j) s3_frag<BN, KB, NP>(sb, wn * 32 * NJ + j * 32, q, fb[j]);
 #pragma unroll
-            for (int i = 0; i < MI; ++i) s3_frag<BM, KB, NP>(sa, wm * 32 * MI + i * 32, q, fa[i]);
-            s3_mfma<NP>(acc, fa, fb);
+                for (int i = 0; i < MI; ++i) s3_frag<BM, KB, NP>(sa, wm * 32 * MI + i * 32, q, fa[i]);
+                s3_mfma<NP>(acc.v, fa, fb);
+            }
         }
     };
     ps_pipeline(la, lb, kbeg, kend, compute, store_ab);
-    gemm_epilogue_t<WM, WN, MI, NJ>(a, acc, tile, reinterpret_cast<float*>(lds), epi);
+    gemm_epilogue_t<WM, WN, MI, NJ>(a, acc.v, tile, reinterpret_cast<float*>(lds), epi);
 }
 
 template <int NP, int WM, int WN, int MI, int NJ, int KB, class LA, class LB, class Epi, class InitA, class InitB>
@@ -509,13 +509,9 @@ __device__ __forceinline__ void gemm_body_psm(const GemmArgs& a, InitA init_a, I
     init_a(la, m0, tid, kbeg);
     init_b(lb, n0, tid, kbeg);
 
-    floatx16 acc[MI][NJ];
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    constexpr bool S16 = Mma16<NP, KB>::ON;
+    WaveAcc<MI, NJ, S16> acc;
+    acc.zero();
 
     auto store_ab = [&](int buf, const typename LA::Regs& xa, const typename LB::Regs& xb) {
         char* da = lds + buf * (SA + SB);
@@ -525,18 +521,22 @@ __device__ __forceinline__ void gemm_body_psm(const GemmArgs& a, InitA init_a, I
     auto compute = [&](int buf) {
         const char* sa = lds + buf * (SA + SB);
         const char* sb = sa + SA;
+        if constexpr (S16) {
+            stage16_mn<NP, KB, BM, BN, MI, NJ>(acc.v, sa, sb, wm * 32 * MI, wn * 32 * NJ);
+        } else {
 #pragma unroll
-        for (int q = 0; q < S3<KB>::KSTEPS; ++q) {
-            bf16x8 fa[MI][NP], fb[NJ][NP];
+            for (int q = 0; q < S3<KB>::KSTEPS; ++q) {
+                bf16x8 fa[MI][NP], fb[NJ][NP];
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) s3m_frag<BN, KB, NP>(sb, wn * 32 * NJ + j * 32, q, fb[j]);
+                for (int j = 0; j < NJ; ++j) s3m_frag<BN, KB, NP>(sb, wn * 32 * NJ + j * 32, q, fb[j]);
 #pragma unroll
-            for (int i = 0; i < MI; ++i) s3m_frag<BM, KB, NP>(sa, wm * 32 * MI + i * 32, q, fa[i]);
-            s3_mfma<NP>(acc, fa, fb);
+                for (int i = 0; i < MI; ++i) s3m_frag<BM, KB, NP>(sa, wm * 32 * MI + i * 32, q, fa[i]);
+                s3_mfma<NP>(acc.v, fa, fb);
+            }
         }
     };
     ps_pipeline(la, lb, kbeg, kend, compute, store_ab);
-    gemm_epilogue_t<WM, WN, MI, NJ>(a, acc, tile, reinterpret_cast<float*>(lds), epi);
+    gemm_epilogue_t<WM, WN, MI, NJ>(a, acc.v, tile, reinterpret_cast<float*>(lds), epi);
 }
 
 // --------------------------------------------------------------------------------------------

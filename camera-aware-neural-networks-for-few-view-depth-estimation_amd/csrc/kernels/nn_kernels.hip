@@ -60,17 +60,19 @@ __global__ void k_colreduce(Op op, int64_t R, int C, int64_t rows_per_slice, dou
 }
 
 // tot[n] = sum_s part[s][n] (fixed order), optional float copy dst[n] = scale * tot[n]
+constexpr int kFinalLanes = 16;   // slice lanes of k_colfinal (block 64 x 16)
 __global__ void k_colfinal(const double* part, int S, int N, double* tot, float* dst, float scale) {
     const int n = blockIdx.x * 64 + threadIdx.x;
-    const int sy = threadIdx.y;   // 4 slice lanes
+    const int sy = threadIdx.y;
     double s = 0.0;
     if (n < N)
-        for (int i = sy; i < S; i += 4) s += part[(int64_t)i * N + n];
-    __shared__ double red[4][64];
+        for (int i = sy; i < S; i += kFinalLanes) s += part[(int64_t)i * N + n];
+    __shared__ double red[kFinalLanes][64];
     red[sy][threadIdx.x] = s;
     __syncthreads();
     if (sy == 0 && n < N) {
-        s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+        s = 0.0;
+        for (int y = 0; y < kFinalLanes; ++y) s += red[y][threadIdx.x];
         if (tot) tot[n] = s;
         if (dst) dst[n] = (float)(s * scale);
     }
@@ -130,11 +132,13 @@ int launch_colreduce(const Op& op, int64_t R, int C, double* part, hipStream_t s
     return S;
 }
 void launch_colfinal(const double* part, int S, int N, double* tot, float* dst, float scale, hipStream_t st) {
-    hipLaunchKernelGGL(k_colfinal, dim3(cdiv(N, 64)), dim3(64, 4), 0, st, part, S, N, tot, dst, scale);
+    hipLaunchKernelGGL(k_colfinal, dim3(cdiv(N, 64)), dim3(64, kFinalLanes), 0, st, part, S, N, tot, dst, scale);
 }
 }  // namespace
 
-int colsum_slices(int64_t R) { return (int)std::max<int64_t>(1, std::min<int64_t>(512, R / 1024)); }
+// >= 128 rows per slice, at most 512 slices (monotone in R: scratch is sized at the largest R).  The
+// narrow reductions (GEMM tile partials: M/128 rows) then still spread over 512 workgroups.
+int colsum_slices(int64_t R) { return (int)std::max<int64_t>(1, std::min<int64_t>(512, R / 128)); }
 
 void colsum(const float* x, int64_t ld, int coff, int64_t R, int C, double* part, hipStream_t st) {
     launch_colreduce<1>(OpSum{x, ld, coff}, R, C, part, st);
@@ -489,8 +493,8 @@ void head_bwd(const float* a, int C, const float* w, const float* dpred, const f
     const int S = launch_colreduce<2>(OpHeadBwd{a, dpred, sig, max_depth, C}, M, C, part, st);
     // part[s][0][c] -> dw ; part[s][1][0] -> db
     launch_colfinal(part, S, 2 * C, scratch, nullptr, 1.f, st);
-    hipLaunchKernelGGL(k_colfinal, dim3(1), dim3(64, 4), 0, st, scratch, 1, C, nullptr, dw, 1.f);
-    hipLaunchKernelGGL(k_colfinal, dim3(1), dim3(64, 4), 0, st, scratch + C, 1, 1, nullptr, db, 1.f);
+    hipLaunchKernelGGL(k_colfinal, dim3(1), dim3(64, kFinalLanes), 0, st, scratch, 1, C, nullptr, dw, 1.f);
+    hipLaunchKernelGGL(k_colfinal, dim3(1), dim3(64, kFinalLanes), 0, st, scratch + C, 1, 1, nullptr, db, 1.f);
 }
 
 // computeDepthMetrics (tensorboard_trainer_enhanced.h:400-439): mask gt > 0
