@@ -481,6 +481,17 @@ __device__ __forceinline__ TileId xcd_tile() {
     return t;
 }
 
+// A wave whose sub-tile lies entirely past M or N (in the tail tile of a dimension that is not a
+// multiple of the tile: e.g. the 576 = 2.25 x 256 columns of a 64-channel weight gradient) skips its
+// MFMAs, leaving the SIMD to co-resident waves; it still stages operands and joins every barrier.
+#ifndef CAD_WAVE_SKIP
+#define CAD_WAVE_SKIP 1
+#endif
+__device__ __forceinline__ bool wave_live(const GemmArgs& a, int m0, int n0, int wrows, int wcols) {
+    if constexpr (!CAD_WAVE_SKIP) return true;
+    return m0 + wrows < a.M && n0 + wcols < a.N;
+}
+
 template <class Epi>
 __device__ __forceinline__ const float* epi_row_base(const GemmArgs& a, int m0, int z) {
     if constexpr (is_structured<Epi>::value) return a.C;   // unused by structured epilogues

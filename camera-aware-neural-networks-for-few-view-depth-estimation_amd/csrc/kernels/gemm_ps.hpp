@@ -13,9 +13,8 @@
 // Channel offsets and channel counts must be multiples of 8 (every U-Net conv except enc1.conv1's
 // 3/4-channel input, which keeps the in-loader split).  For NP = 1 this is plain NHWC bf16.
 //
-// Loaders fill caller-owned register sets (Regs: uint4 per 16-B piece; the bodies keep two, so a
-// stage's loads are in flight across two compute phases) and write them to the LDS images of
-// gemm_s3.hpp unchanged (planes [rows][LDK] for k-contiguous
+// Loaders fill caller-owned register sets (Regs: uint4 per 16-B piece; the bodies keep one, loaded
+// one compute phase ahead — see ps_pipeline) and write them to the LDS images of gemm_s3.hpp unchanged (planes [rows][LDK] for k-contiguous
 // operands, [k-rows][rows] for the weight-gradient operands), so fragment reads and MFMAs are shared.
 #pragma once
 #include "gemm_s3.hpp"
@@ -518,7 +517,9 @@ __device__ __forceinline__ void gemm_body_psm(const GemmArgs& a, InitA init_a, I
         la.store(xa, da);
         lb.store(xb, da + SA);
     };
+    const bool live = wave_live(a, m0, n0, wm * 32 * MI, wn * 32 * NJ);
     auto compute = [&](int buf) {
+        if (!live) return;
         const char* sa = lds + buf * (SA + SB);
         const char* sb = sa + SA;
         if constexpr (S16) {

@@ -526,7 +526,9 @@ __device__ __forceinline__ void gemm_body_s3m(const GemmArgs& a, InitA init_a, I
         s3m_store<BM, KB, NP>(da, xa);
         s3m_store<BN, KB, NP>(da + SA, xb);
     };
+    const bool live = wave_live(a, m0, n0, wm * 32 * MI, wn * 32 * NJ);
     auto stage_compute = [&](int buf) {
+        if (!live) return;
         const char* sa = lds + buf * (SA + SB);
         const char* sb = sa + SA;
         if constexpr (S16) {
