@@ -17,4 +17,7 @@ def __getattr__(name):
                 "Trainer", "clip_grad_norm_", "depth_metrics", "ray_directions", "camera_from_K"):
         from . import model
         return getattr(model, name)
+    if name in ("BatchAssembler", "AugSampler"):
+        from . import batch
+        return getattr(batch, name)
     raise AttributeError(name)

@@ -90,7 +90,33 @@ SIGNATURES = {
     "cad_op_convT_dgrad": (I, [P, I64, I, I, P, I, P, I, I, I, P]),
     "cad_op_convT_wgrad": (I, [P, I, P, I64, I, I, P, I, I, I, P]),
     "cad_op_maxpool_fwd": (I, [P, I64, I, I, I, I, P, P, P]),
+    "cad_batcher_create": (I, [I, I, I, I, C.POINTER(P)]),
+    "cad_batcher_destroy": (None, [P]),
+    "cad_batcher_assemble": (I, [P, C.c_void_p, I, P, P, P, P]),
+    "cad_aug_sampler_create": (I, [C.c_void_p, C.c_uint32, C.POINTER(P)]),
+    "cad_aug_sampler_destroy": (None, [P]),
+    "cad_aug_sampler_draw": (I, [P, I, I, C.c_void_p]),
 }
+
+
+class Sample(C.Structure):
+    """cad_sample (cad.h): one decoded sample and its augmentation parameters."""
+    _fields_ = [("rgb", P), ("depth", P), ("h0", I), ("w0", I), ("bgr", I), ("depth_scale", F),
+                ("K", F * 9), ("aug", I), ("crop", I), ("crop_scale", F), ("crop_x", I), ("crop_y", I),
+                ("flip", I), ("jitter", I), ("brightness", F), ("contrast", F)]
+
+
+class AugConfig(C.Structure):
+    """cad_aug_config = AugmentationConfig (sunrgbd_loader.h:30-42), defaults as there."""
+    _fields_ = [("enable_random_crop", I), ("crop_scale_min", F), ("crop_scale_max", F),
+                ("enable_horizontal_flip", I), ("horizontal_flip_prob", F), ("enable_color_jitter", I),
+                ("brightness_delta", F), ("contrast_delta", F)]
+
+    def __init__(self, **kw):
+        d = dict(enable_random_crop=1, crop_scale_min=0.7, crop_scale_max=1.0, enable_horizontal_flip=1,
+                 horizontal_flip_prob=0.5, enable_color_jitter=1, brightness_delta=0.2, contrast_delta=0.2)
+        d.update(kw)
+        super().__init__(**d)
 
 
 class CadError(RuntimeError):

@@ -25,6 +25,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <random>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -1277,6 +1278,147 @@ cad_status cad_ray_directions(const float* K, int B, int H, int W, float* rays, 
         require(K && rays && B > 0 && H > 0 && W > 0, "bad arguments");
         cad::ray_directions(K, B, H, W, rays, S(stream));
         HIPCHK(hipGetLastError());
+    });
+}
+
+// ---------------- batch assembly (SunRGBDLoader::getSample resize + augmentation, on device) -------
+struct cad_batcher {
+    int device = 0, Bmax = 0, H = 0, W = 0;
+    cad::BatchSample* dev = nullptr;    // [Bmax] launch parameters
+    float* tmp = nullptr;               // stage-1 planes of augmented samples: [Bmax][3][H][W] + [Bmax][H][W]
+    cad::BatchSample* host = nullptr;   // pinned staging: Bmax samples, then Bmax x 9 floats of K
+    hipEvent_t staged = nullptr;        // the last upload from the staging buffer
+};
+
+cad_status cad_batcher_create(int max_batch, int height, int width, int device, cad_batcher** out) {
+    return guard([&] {
+        require(out && max_batch >= 1 && height >= 1 && width >= 1, "bad batcher arguments");
+        HIPCHK(hipSetDevice(device));
+        auto b = std::make_unique<cad_batcher>();
+        b->device = device; b->Bmax = max_batch; b->H = height; b->W = width;
+        HIPCHK(hipMalloc((void**)&b->dev, sizeof(cad::BatchSample) * max_batch));
+        HIPCHK(hipMalloc((void**)&b->tmp, sizeof(float) * 4 * (size_t)max_batch * height * width));
+        HIPCHK(hipHostMalloc((void**)&b->host, (sizeof(cad::BatchSample) + 9 * sizeof(float)) * max_batch));
+        HIPCHK(hipEventCreateWithFlags(&b->staged, hipEventDisableTiming));
+        *out = b.release();
+    });
+}
+void cad_batcher_destroy(cad_batcher* b) {
+    if (!b) return;
+    (void)hipSetDevice(b->device);
+    (void)hipEventSynchronize(b->staged);
+    (void)hipEventDestroy(b->staged);
+    (void)hipFree(b->dev);
+    (void)hipFree(b->tmp);
+    (void)hipHostFree(b->host);
+    delete b;
+}
+
+cad_status cad_batcher_assemble(cad_batcher* b, const cad_sample* samples, int B, float* rgb, float* depth, float* K,
+                                void* stream) {
+    return guard([&] {
+        require(b && samples && rgb && depth && K, "null argument");
+        require(B >= 1 && B <= b->Bmax, "batch exceeds max_batch");
+        HIPCHK(hipSetDevice(b->device));
+        HIPCHK(hipEventSynchronize(b->staged));   // the staging buffer is free again
+        const int H = b->H, W = b->W;
+        float* Kh = reinterpret_cast<float*>(b->host + b->Bmax);
+        bool any_aug = false;
+        for (int i = 0; i < B; ++i) {
+            const cad_sample& s = samples[i];
+            require(s.rgb && s.depth && s.h0 >= 1 && s.w0 >= 1, "sample " + std::to_string(i) + ": no image");
+            cad::BatchSample& d = b->host[i];
+            d = cad::BatchSample{};
+            d.rgb = s.rgb; d.depth = s.depth; d.h0 = s.h0; d.w0 = s.w0; d.bgr = s.bgr;
+            d.depth_scale = s.depth_scale;
+            // intrinsics with the reference's float operations
+            float* k = Kh + 9 * i;
+            for (int e = 0; e < 9; ++e) k[e] = s.K[e];
+            if (s.h0 != H || s.w0 != W) {   // resizeSample :480-488
+                const float sx = static_cast<float>(W) / s.w0, sy = static_cast<float>(H) / s.h0;
+                k[0] = k[0] * sx; k[4] = k[4] * sy; k[2] = k[2] * sx; k[5] = k[5] * sy;
+            }
+            if (!s.aug) continue;
+            any_aug = true;
+            d.aug = 1;
+            d.cy = 0; d.cx = 0; d.ch = H; d.cw = W;
+            if (s.crop) {   // applyCrop :389-414 (torch Slice clamps the window to the image)
+                const int chn = static_cast<int>(H * s.crop_scale), cwn = static_cast<int>(W * s.crop_scale);
+                require(s.crop_x >= 0 && s.crop_y >= 0 && s.crop_x < W && s.crop_y < H && chn >= 1 && cwn >= 1,
+                        "sample " + std::to_string(i) + ": crop window outside the image");
+                d.cy = s.crop_y; d.cx = s.crop_x;
+                d.ch = std::min(s.crop_y + chn, H) - s.crop_y;
+                d.cw = std::min(s.crop_x + cwn, W) - s.crop_x;
+                k[2] = k[2] - s.crop_x;
+                k[5] = k[5] - s.crop_y;
+            }
+            if (s.flip) {   // applyHorizontalFlip :416-430
+                d.flip = 1;
+                k[2] = d.cw - k[2] - 1;
+            }
+            if (s.jitter) {   // applyColorJitter :432-443
+                d.jitter = 1; d.contrast = s.contrast; d.brightness = s.brightness;
+            }
+            if (d.ch != H || d.cw != W) {   // the second resizeSample (getSample :165)
+                const float sx = static_cast<float>(W) / d.cw, sy = static_cast<float>(H) / d.ch;
+                k[0] = k[0] * sx; k[4] = k[4] * sy; k[2] = k[2] * sx; k[5] = k[5] * sy;
+            }
+        }
+        HIPCHK(hipMemcpyAsync(b->dev, b->host, sizeof(cad::BatchSample) * B, hipMemcpyHostToDevice, S(stream)));
+        HIPCHK(hipMemcpyAsync(K, Kh, sizeof(float) * 9 * B, hipMemcpyHostToDevice, S(stream)));
+        HIPCHK(hipEventRecord(b->staged, S(stream)));
+        float* rgb_tmp = b->tmp;
+        float* depth_tmp = b->tmp + 3 * (size_t)b->Bmax * H * W;
+        cad::batch_assemble(b->dev, B, H, W, any_aug, rgb, depth, rgb_tmp, depth_tmp, S(stream));
+        HIPCHK(hipGetLastError());
+    });
+}
+
+// augmentSample's draws (sunrgbd_loader.cpp:352-443): std::mt19937, same distributions, same order
+struct cad_aug_sampler {
+    cad_aug_config cfg;
+    std::mt19937 rng;
+};
+cad_status cad_aug_sampler_create(const cad_aug_config* cfg, uint32_t seed, cad_aug_sampler** out) {
+    return guard([&] {
+        require(cfg && out, "null argument");
+        require(cfg->crop_scale_min > 0.f && cfg->crop_scale_min <= cfg->crop_scale_max && cfg->crop_scale_max <= 1.f,
+                "crop scale range must satisfy 0 < min <= max <= 1");
+        auto s = std::make_unique<cad_aug_sampler>();
+        s->cfg = *cfg;
+        s->rng.seed(seed);
+        *out = s.release();
+    });
+}
+void cad_aug_sampler_destroy(cad_aug_sampler* s) { delete s; }
+cad_status cad_aug_sampler_draw(cad_aug_sampler* s, int height, int width, cad_sample* smp) {
+    return guard([&] {
+        require(s && smp && height >= 1 && width >= 1, "bad arguments");
+        const cad_aug_config& c = s->cfg;
+        smp->aug = 1;
+        smp->crop = c.enable_random_crop;
+        if (c.enable_random_crop) {
+            std::uniform_real_distribution<float> scale_dist(c.crop_scale_min, c.crop_scale_max);
+            const float scale = scale_dist(s->rng);
+            const int crop_h = static_cast<int>(height * scale), crop_w = static_cast<int>(width * scale);
+            std::uniform_int_distribution<int> x_dist(0, std::max(1, width - crop_w));
+            std::uniform_int_distribution<int> y_dist(0, std::max(1, height - crop_h));
+            smp->crop_scale = scale;
+            smp->crop_x = x_dist(s->rng);
+            smp->crop_y = y_dist(s->rng);
+        }
+        smp->flip = 0;
+        if (c.enable_horizontal_flip) {
+            std::uniform_real_distribution<float> flip_dist(0.0f, 1.0f);
+            smp->flip = flip_dist(s->rng) < c.horizontal_flip_prob;
+        }
+        smp->jitter = c.enable_color_jitter;
+        if (c.enable_color_jitter) {
+            std::uniform_real_distribution<float> bd(1.0f - c.brightness_delta, 1.0f + c.brightness_delta);
+            std::uniform_real_distribution<float> cd(1.0f - c.contrast_delta, 1.0f + c.contrast_delta);
+            smp->brightness = bd(s->rng);
+            smp->contrast = cd(s->rng);
+        }
     });
 }
 

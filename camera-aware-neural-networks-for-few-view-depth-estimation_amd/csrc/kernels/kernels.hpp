@@ -131,6 +131,22 @@ void grad_norm_clip(const float* g, int64_t n, float max_norm, float prescale, d
 void adam_step(float* p, float* g, float* m, float* v, int64_t n, const float* norm_coef, float lr,
                float b1, float b2, float eps, float wd, int step, hipStream_t st);
 
+// ---------------- batch assembly (batch_kernels.hip) ----------------
+// One decoded sample and what the loader does to it (sunrgbd_loader.cpp resizeSample / augmentSample);
+// an array of these lives in device memory for the launch.
+struct BatchSample {
+    const uint8_t* rgb;      // HWC u8, h0 x w0 x 3 (bgr = 1: OpenCV channel order)
+    const uint16_t* depth;   // HW u16
+    int h0, w0, bgr;
+    float depth_scale;       // metres per depth unit (1/1000)
+    int aug;                 // 0: output = stage 1 (resize); 1: crop / flip / jitter / resize of stage 1
+    int cy, cx, ch, cw;      // crop window of the H x W stage-1 image (already clamped to it)
+    int flip, jitter;
+    float contrast, brightness;
+};
+void batch_assemble(const BatchSample* samples_dev, int B, int H, int W, bool any_aug, float* rgb, float* depth,
+                    float* rgb_tmp, float* depth_tmp, hipStream_t st);
+
 // ---------------- conditioning (cond_kernels.hip, film_kernels.hip) ----------------
 void ray_directions(const float* K, int B, int H, int W, float* rays_nchw, hipStream_t st);
 void camera_from_K(const float* K, int B, float* cam4, hipStream_t st);            // a15

@@ -34,6 +34,11 @@
  *   cad_depth_metrics               computeDepthMetrics (abs_rel ...)          enhanced.h:400-439
  *   cad_ray_directions              RayDirectionComputer::computeRayDirections
  *                                   src/preprocessing/ray_direction_computer.cpp:17-62
+ *   cad_batcher_create/assemble     SunRGBDLoader::getSample's resizeSample + augmentSample
+ *                                   (src/data/sunrgbd_loader.cpp:158-166, 352-489) and the trainer's
+ *                                   batch torch::stack + .to(device) (enhanced.h:277-289), on device
+ *   cad_aug_sampler_create/draw     augmentSample's random draws (sunrgbd_loader.cpp:352-443;
+ *                                   AugmentationConfig sunrgbd_loader.h:30-42, rng_ seed :185)
  *   cad_op_*                        single operators of the step (conv, convT, BN, pool, ...), the
  *                                   ATen calls the reference dispatches
  *
@@ -189,6 +194,49 @@ cad_status cad_depth_metrics(const float* pred, const float* gt, int B, int H, i
 
 /* ---- conditioning: per-pixel unit ray directions (B,3,H,W) from K (B,3,3) ---- */
 cad_status cad_ray_directions(const float* K, int B, int H, int W, float* rays, void* stream);
+
+/* ---- batch assembly on device: decoded samples -> the step's (B,3,H,W) rgb, (B,1,H,W) depth,
+ * (B,3,3) K.  Per sample: rgb = u8/255, depth = u16 * depth_scale, resized to H x W (rgb bilinear,
+ * align_corners = false; depth nearest; K scaled), then — when aug is set — crop (window clamped to
+ * the image like a torch Slice, K's principal point shifted), horizontal flip (cx = W - cx - 1),
+ * colour jitter clamp(rgb * contrast + brightness - 1, 0, 1), and the resize back to H x W. */
+typedef struct {
+    const uint8_t* rgb;     /* device: decoded image, HWC u8, h0 x w0 x 3 */
+    const uint16_t* depth;  /* device: decoded depth, HW u16 */
+    int h0, w0;
+    int bgr;                /* 1: rgb is in OpenCV BGR order (loadRGB's cvtColor happens here) */
+    float depth_scale;      /* metres per unit: 1/1000 (loadDepth) */
+    float K[9];             /* host: the sample's intrinsics, 3x3 row-major */
+    int aug;                /* 0: resize only (validation / augmentation off) */
+    int crop;               /* applyCrop with crop_scale, crop_x, crop_y (on the resized image) */
+    float crop_scale;
+    int crop_x, crop_y;
+    int flip;               /* applyHorizontalFlip */
+    int jitter;             /* applyColorJitter with brightness, contrast */
+    float brightness, contrast;
+} cad_sample;
+typedef struct cad_batcher cad_batcher;
+cad_status cad_batcher_create(int max_batch, int height, int width, int device, cad_batcher** out);
+void cad_batcher_destroy(cad_batcher* b);
+/* asynchronous on `stream`; samples[] is read before the call returns */
+cad_status cad_batcher_assemble(cad_batcher* b, const cad_sample* samples, int B, float* rgb, float* depth,
+                                float* K, void* stream);
+
+typedef struct { /* AugmentationConfig (sunrgbd_loader.h:30-42) */
+    int enable_random_crop;
+    float crop_scale_min, crop_scale_max; /* 0.7, 1.0 */
+    int enable_horizontal_flip;
+    float horizontal_flip_prob; /* 0.5 */
+    int enable_color_jitter;
+    float brightness_delta, contrast_delta; /* 0.2, 0.2 */
+} cad_aug_config;
+typedef struct cad_aug_sampler cad_aug_sampler;
+/* std::mt19937 seeded like the loader's rng_ (config.random_seed) */
+cad_status cad_aug_sampler_create(const cad_aug_config* cfg, uint32_t seed, cad_aug_sampler** out);
+void cad_aug_sampler_destroy(cad_aug_sampler* s);
+/* fills sample->aug/crop/flip/jitter fields with augmentSample's draws, in its order, for an image
+ * already resized to height x width */
+cad_status cad_aug_sampler_draw(cad_aug_sampler* s, int height, int width, cad_sample* sample);
 
 /* ---- debugging: synchronous host copy of an internal NHWC activation buffer by name
  * ("x0", "cat<l>", "dcat<l>", "pool<l>", "dout<l>", "bott", "Sa", "Sb", "Sc",

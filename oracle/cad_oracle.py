@@ -21,6 +21,8 @@ Every function cites the reference file:line it restates (paths relative to /roo
   * clip_grad_norm_             torch/csrc/api/include/torch/nn/utils/clip_grad.h:22-85 (LibTorch)
   * Adam (coupled L2)           torch::optim::Adam, options built at enhanced.h:97-101
   * computeDepthMetrics (a20)   src/training/tensorboard_trainer_enhanced.h:400-439
+  * SunRGBDLoader::getSample    src/data/sunrgbd_loader.cpp:105-169 (load :221-259, augment
+                                :352-443, resize :445-489), decode excluded
 
 Parity pin: tests/test_oracle_golden.py checks this restatement against fixtures produced by the
 REFERENCE itself (oracle/ref_harness.cpp compiled in place against /root/reference/src by
@@ -551,6 +553,117 @@ def abs_rel_per_sample(pred, gt):
     vals = [depth_metrics(pred[b], gt[b]).get("abs_rel") for b in range(pred.shape[0])]
     vals = [v for v in vals if v is not None]
     return sum(vals) / pred.shape[0]
+
+
+# --------------------------------------------------------------------------------------------
+# Batch assembly: SunRGBDLoader::getSample (src/data/sunrgbd_loader.cpp), decode excluded
+# --------------------------------------------------------------------------------------------
+def load_sample(rgb_u8_hwc, depth_u16, K, bgr=False, depth_scale=1.0 / 1000.0):
+    """loadRGB :221-233 (cv::COLOR_BGR2RGB, matToTensor HWC->CHW, / 255.0f) and loadDepth :235-259
+    (CV_16UC1 convertTo CV_32F with scale 1/1000: one single-precision product per pixel)."""
+    rgb = torch.from_numpy(np.ascontiguousarray(rgb_u8_hwc)).float()
+    if bgr:
+        rgb = rgb.flip(2)
+    rgb = rgb.permute(2, 0, 1).contiguous() / 255.0
+    d = torch.from_numpy(depth_u16.astype(np.float32) * np.float32(depth_scale))[None]
+    return rgb, d, torch.as_tensor(np.asarray(K, dtype=np.float32).reshape(3, 3)).clone()
+
+
+def resize_sample(rgb, depth, K, H, W):
+    """resizeSample :445-489: rgb bilinear (align_corners false), depth nearest, K scaled (float32)."""
+    h, w = rgb.shape[1], rgb.shape[2]
+    if (h, w) == (H, W):
+        return rgb, depth, K
+    rgb = F.interpolate(rgb[None], size=(H, W), mode="bilinear", align_corners=False)[0]
+    depth = F.interpolate(depth[None], size=(H, W), mode="nearest")[0]
+    sx, sy = np.float32(W) / np.float32(w), np.float32(H) / np.float32(h)
+    K = K.clone()
+    K[0, 0] = K[0, 0] * sx
+    K[1, 1] = K[1, 1] * sy
+    K[0, 2] = K[0, 2] * sx
+    K[1, 2] = K[1, 2] * sy
+    return rgb, depth, K
+
+
+def augment_sample(rgb, depth, K, aug):
+    """augmentSample :352-387 with the draws given: applyCrop :389-414 (slices clamp like torch's),
+    applyHorizontalFlip :416-430, applyColorJitter :432-443."""
+    K = K.clone()
+    if aug.get("crop"):
+        H, W = rgb.shape[1], rgb.shape[2]
+        s = np.float32(aug["crop_scale"])
+        ch, cw = int(np.float32(H) * s), int(np.float32(W) * s)
+        cx, cy = int(aug["crop_x"]), int(aug["crop_y"])
+        rgb = rgb[:, cy:cy + ch, cx:cx + cw]
+        depth = depth[:, cy:cy + ch, cx:cx + cw]
+        K[0, 2] = K[0, 2] - cx
+        K[1, 2] = K[1, 2] - cy
+    if aug.get("flip"):
+        rgb, depth = torch.flip(rgb, [2]), torch.flip(depth, [2])
+        K[0, 2] = rgb.shape[2] - K[0, 2] - 1
+    if aug.get("jitter"):
+        rgb = torch.clamp(rgb * np.float32(aug["contrast"]) + np.float32(aug["brightness"]) - 1.0, 0.0, 1.0)
+    return rgb, depth, K
+
+
+def get_sample(rgb_u8_hwc, depth_u16, K, H, W, aug=None, bgr=False, depth_scale=1.0 / 1000.0):
+    """getSample :105-169: load, resize, then (train + augmentation) augment and resize again."""
+    rgb, depth, K = load_sample(rgb_u8_hwc, depth_u16, K, bgr, depth_scale)
+    rgb, depth, K = resize_sample(rgb, depth, K, H, W)
+    if aug and aug.get("aug"):
+        rgb, depth, K = augment_sample(rgb, depth, K, aug)
+        rgb, depth, K = resize_sample(rgb, depth, K, H, W)
+    return rgb, depth, K
+
+
+class StdMt19937Draws:
+    """augmentSample's draws as libstdc++ makes them: std::mt19937 (== numpy RandomState's legacy
+    init_genrand seeding and 32-bit outputs), uniform_real_distribution<float> via
+    generate_canonical<float, 24> (one 32-bit draw, sum / 2^32 in float, nudged below 1), and
+    uniform_int_distribution<int> by Lemire's nearly-divisionless downscaling (libstdc++ 11,
+    bits/uniform_int_dist.h _S_nd for 32-bit engines)."""
+
+    def __init__(self, seed, cfg):
+        self.rs = np.random.RandomState(seed)
+        self.cfg = cfg
+
+    def _u32(self):
+        return int(self.rs.randint(0, 2 ** 32, dtype=np.uint64))
+
+    def _real(self, a, b):
+        a, b = np.float32(a), np.float32(b)
+        r = np.float32(self._u32()) / np.float32(2.0 ** 32)
+        if r >= np.float32(1.0):
+            r = np.nextafter(np.float32(1.0), np.float32(0.0))
+        return np.float32(r * (b - a) + a)
+
+    def _int(self, a, b):
+        rng = (b - a) + 1
+        prod = self._u32() * rng
+        low = prod & 0xFFFFFFFF
+        if low < rng:
+            thr = (2 ** 32 - rng) % rng
+            while low < thr:
+                prod = self._u32() * rng
+                low = prod & 0xFFFFFFFF
+        return a + (prod >> 32)
+
+    def draw(self, H, W):
+        c = self.cfg
+        out = {"aug": 1, "crop": int(c["enable_random_crop"]), "flip": 0, "jitter": int(c["enable_color_jitter"])}
+        if c["enable_random_crop"]:
+            s = self._real(c["crop_scale_min"], c["crop_scale_max"])
+            ch, cw = int(np.float32(H) * s), int(np.float32(W) * s)
+            out["crop_scale"] = float(s)
+            out["crop_x"] = self._int(0, max(1, W - cw))
+            out["crop_y"] = self._int(0, max(1, H - ch))
+        if c["enable_horizontal_flip"]:
+            out["flip"] = int(self._real(0.0, 1.0) < np.float32(c["horizontal_flip_prob"]))
+        if c["enable_color_jitter"]:
+            one, bd, cd = np.float32(1.0), np.float32(c["brightness_delta"]), np.float32(c["contrast_delta"])
+            out["brightness"] = float(self._real(one - bd, one + bd))
+            out["contrast"] = float(self._real(one - cd, one + cd))
+        return out
 
 
 # --------------------------------------------------------------------------------------------
