@@ -629,17 +629,26 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     cad::bn_relu_bwd(g, ldg, gcoff, dc.y2, C, dc.b2.mean, dc.b2.invstd, dc.b2.scale, dc.b2.shift, h->P(dc.b2.widx), M,
                      h->dscr, dc.b2.coef, h->G(dc.b2.widx), h->G(dc.b2.bidx), dY2, st, nullptr, 1, ps ? dYs2 : nullptr);
     fork_side(h, st);
+    // CAD_BNB=1: bn1's (Σ dz, Σ dz·x̂) come out of conv2's dgrad epilogue as tile partials (no FiLM
+    // between the ReLU and conv2; not on the in-loader S3 pre-split-weight kernels).  Off by default:
+    // measured on MI355X the epilogue's extra y reads cost the dgrad GEMMs more (+4 ms fp32, +7 ms bf16
+    // per step) than the skipped reduction pass saves (~3.8 ms)
+    static const bool bnb_on = std::getenv("CAD_BNB") && std::getenv("CAD_BNB")[0] == '1';
+    const bool bnb = bnb_on && !dc.has_film() && (ps || !h->wsplit);
+    const cad::BnBwdEpi bn1{dc.y1, dc.b1.mean, dc.b1.invstd, dc.b1.scale, dc.b1.shift, h->stats};
+    const int bn_rows = cad::conv3x3_stats_rows(B, Hh, Ww, C);
     // conv2: wgrad (side) || dgrad (caller's stream)
     if (ps) {
         cad::conv3x3_wgrad_ps(sv(dYs2, C), C, sv(dc.a1s, C), C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, ws);
-        cad::conv3x3_dgrad_ps(sv(dYs2, C), C, sv(dc.c2.wds, 9 * C), C, dA1, C, B, Hh, Ww, st);
+        cad::conv3x3_dgrad_ps(sv(dYs2, C), C, sv(dc.c2.wds, 9 * C), C, dA1, C, B, Hh, Ww, st, bnb ? &bn1 : nullptr);
     } else {
         if (dc.a1)
             cad::conv3x3_wgrad(dY2, C, dc.a1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, ws);
         else
             cad::conv3x3_wgrad(dY2, C, dc.y1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, ws,
                                dc.b1.scale, dc.b1.shift);
-        cad::conv3x3_dgrad(dY2, C, dc.c2.wd, C, dA1, C, B, Hh, Ww, st, h->wsplit ? dc.c2.wds : nullptr);
+        cad::conv3x3_dgrad(dY2, C, dc.c2.wd, C, dA1, C, B, Hh, Ww, st, h->wsplit ? dc.c2.wds : nullptr,
+                           bnb ? &bn1 : nullptr);
     }
     // FiLM: dgamma/dbeta per (sample, channel); the ReLU sees dA1 * gamma (folded into bn_relu_bwd)
     const int64_t HW = (int64_t)Hh * Ww;
@@ -648,7 +657,8 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     // bn1 + relu
     cad::bn_relu_bwd(dA1, C, 0, dc.y1, C, dc.b1.mean, dc.b1.invstd, dc.b1.scale, dc.b1.shift, h->P(dc.b1.widx), M,
                      h->dscr, dc.b1.coef, h->G(dc.b1.widx), h->G(dc.b1.bidx), dY1, st,
-                     dc.has_film() ? dc.film.gam : nullptr, HW, ps ? dYs1 : nullptr);
+                     dc.has_film() ? dc.film.gam : nullptr, HW, ps ? dYs1 : nullptr, bnb ? h->stats : nullptr,
+                     bn_rows);
     if (dc.has_film()) cad::film_mlp_bwd(film_view(h, dc), h->camn, B, st);
     fork_side(h, st);
     // conv1: wgrad (side) || dgrad (caller's stream)

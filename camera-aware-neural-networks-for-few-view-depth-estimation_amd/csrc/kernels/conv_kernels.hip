@@ -25,6 +25,12 @@ struct EpiStore {
 struct EpiStoreStats : EpiStore {
     static constexpr bool STATS = true;
 };
+// conv3x3 dgrad whose output feeds a ReLU(BatchNorm) backward: per-tile (Σ dz, Σ dz·x̂) partials
+// (GemmArgs e_*), so the BN backward skips its reduction pass over (g, y)
+struct EpiStoreBnBwd : EpiStore {
+    static constexpr bool STATS = true;
+    static constexpr bool BNBWD = true;
+};
 // ConvTranspose2d(k2,s2) pixel shuffle: n = (q=(dy,dx), co) -> high-res pixel (2y+dy, 2x+dx).
 // The column (q, co) is fixed per lane and sub-block, and rows advance in small steps, so the
 // epilogue carries (x, y, b) incrementally instead of dividing per element (STRUCTURED epilogue).
@@ -463,6 +469,8 @@ CAD_KT(KConvFwd, (k_conv3x3_fwd<WM, WN, KB, EpiStore, false>),
        "void cad::k_conv3x3_fwd<%d, %d, %d, cad::EpiStore, false>(cad::GemmArgs)")
 CAD_KT(KConvFwdS, (k_conv3x3_fwd<WM, WN, KB, EpiStoreStats, false>),
        "void cad::k_conv3x3_fwd<%d, %d, %d, cad::EpiStoreStats, false>(cad::GemmArgs)")
+CAD_KT(KConvFwdX, (k_conv3x3_fwd<WM, WN, KB, EpiStoreBnBwd, false>),
+       "void cad::k_conv3x3_fwd<%d, %d, %d, cad::EpiStoreBnBwd, false>(cad::GemmArgs)")
 CAD_KT(KConvFwdBN, (k_conv3x3_fwd<WM, WN, KB, EpiStore, true>),
        "void cad::k_conv3x3_fwd<%d, %d, %d, cad::EpiStore, true>(cad::GemmArgs)")
 CAD_KT(KConvFwdSBN, (k_conv3x3_fwd<WM, WN, KB, EpiStoreStats, true>),
@@ -481,6 +489,10 @@ CAD_KT(KConvTWgrad, (k_convT_wgrad<WM, WN, KB>), "void cad::k_convT_wgrad<%d, %d
             "void cad::k_conv3x3_fwd_" #SUF "<%d, %d, %d, cad::EpiStoreStats>(cad::GemmArgs)",                 \
             (k_conv3x3_fwd_##SUF##L<WM, WN, KB, EpiStoreStats>),                                              \
             "void cad::k_conv3x3_fwd_" #SUF "L<%d, %d, %d, cad::EpiStoreStats>(cad::GemmArgs)", 4, 2)          \
+    CAD_KTL(KConvFwdX##T, (k_conv3x3_fwd_##SUF<WM, WN, KB, EpiStoreBnBwd>),                                    \
+            "void cad::k_conv3x3_fwd_" #SUF "<%d, %d, %d, cad::EpiStoreBnBwd>(cad::GemmArgs)",                 \
+            (k_conv3x3_fwd_##SUF##L<WM, WN, KB, EpiStoreBnBwd>),                                              \
+            "void cad::k_conv3x3_fwd_" #SUF "L<%d, %d, %d, cad::EpiStoreBnBwd>(cad::GemmArgs)", 4, 2)          \
     CAD_KTL(KConvTFwd##T, (k_convT_fwd_##SUF<WM, WN, KB>), "void cad::k_convT_fwd_" #SUF "<%d, %d, %d>(cad::GemmArgs)", \
             (k_convT_fwd_##SUF##L<WM, WN, KB>), "void cad::k_convT_fwd_" #SUF "L<%d, %d, %d>(cad::GemmArgs)", 4, 2) \
     CAD_KTL(KConvTDgrad##T, (k_convT_dgrad_##SUF<WM, WN, KB>),                                                 \
@@ -683,18 +695,28 @@ void convT_fwd(const float* x, int64_t ldx, int cin, const float* wf, const floa
     launch_cfg<KConvTFwd>(c, kb, a, 1, st);
 }
 
+static void set_bnbwd(GemmArgs& a, const BnBwdEpi* bn) {
+    a.stats = bn->stats;
+    a.e_y = bn->y; a.e_mean = bn->mean; a.e_invstd = bn->invstd; a.e_scale = bn->scale; a.e_shift = bn->shift;
+}
+
 void conv3x3_dgrad(const float* dz, int cout, const float* wd, int cin, float* dx, int64_t lddx,
-                   int B, int H, int W, hipStream_t st, const void* wd_split) {
+                   int B, int H, int W, hipStream_t st, const void* wd_split, const BnBwdEpi* bn) {
     GemmArgs a{};
     a.M = B * H * W; a.N = cin; a.K = 9 * cout;
     a.B = B; a.H = H; a.W = W;
     a.A = dz; a.lda = cout; a.a_coff = 0; a.a_cin = cout;
     a.Bm = wd; a.ldb = 9 * cout;
     a.C = dx; a.ldc = lddx; a.c_coff = 0;
+    if (bn) {
+        if (lddx != cin || (engine() == 1 && wd_split))
+            throw std::runtime_error("BN-backward dgrad epilogue: dense output, no pre-split-weight kernel");
+        set_bnbwd(a, bn);
+    }
     const Cfg c = pick_cfg(a.M, a.N);
     if (engine() == 2) {
         a.kstages_per_split = cdiv(a.K, bf16_kb());
-        launch_b1<KConvFwdB>(c, a, 1, st);
+        if (bn) launch_b1<KConvFwdXB>(c, a, 1, st); else launch_b1<KConvFwdB>(c, a, 1, st);
         return;
     }
     if (engine() == 1) {
@@ -705,12 +727,12 @@ void conv3x3_dgrad(const float* dz, int cout, const float* wd, int cin, float* d
             launch_s3<KConvFwdW3>(c, kb, a, 1, st);
             return;
         }
-        launch_s3<KConvFwd3>(c, kb, a, 1, st);
+        if (bn) launch_s3<KConvFwdX3>(c, kb, a, 1, st); else launch_s3<KConvFwd3>(c, kb, a, 1, st);
         return;
     }
     const int kb = kb_for(K_FWD, c);
     a.kstages_per_split = cdiv(a.K, kb);
-    launch_cfg<KConvFwd>(c, kb, a, 1, st);
+    if (bn) launch_cfg<KConvFwdX>(c, kb, a, 1, st); else launch_cfg<KConvFwd>(c, kb, a, 1, st);
 }
 
 void convT_dgrad(const float* g, int64_t ldg, int gcoff, int cout, const float* wm, int cin, float* dx,
@@ -856,7 +878,7 @@ void conv3x3_fwd_ps(Split x, int cin, Split w, int cout, float* y, int64_t ldy, 
 }
 
 void conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t lddx, int B, int H, int W,
-                      hipStream_t st) {
+                      hipStream_t st, const BnBwdEpi* bn) {
     ps_check(dz, cout, "conv3x3_dgrad dz");
     ps_check(wd, 9 * cout, "conv3x3_dgrad w");
     GemmArgs a{};
@@ -869,7 +891,13 @@ void conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t 
     const int kb = ps_kb(true, c);
     a.kstages_per_split = cdiv(a.K, kb);
     a.cimajor = cimajor_ok(cout, kb);
-    launch_ps<KConvFwdP3, KConvFwdP1>(c, kb, a, 1, st);
+    if (bn) {
+        if (lddx != cin) throw std::runtime_error("BN-backward dgrad epilogue: dense output only");
+        set_bnbwd(a, bn);
+        launch_ps<KConvFwdXP3, KConvFwdXP1>(c, kb, a, 1, st);
+    } else {
+        launch_ps<KConvFwdP3, KConvFwdP1>(c, kb, a, 1, st);
+    }
 }
 
 void conv3x3_wgrad_ps(Split dz, int cout, Split x, int cin, float* dw, int B, int H, int W, float* slab,

@@ -66,6 +66,9 @@ struct GemmArgs {
     // a channel block re-read the same input rows back to back (L2 hits) — needs cin % KB == 0
     int cimajor;
     int conv_cin;         // cin of that contraction (the B loader walks the same (tap, ci) order)
+    // BN-backward partials in a dgrad epilogue (EpiStoreBnBwd): the pre-BN activation y [M][N] and
+    // the BatchNorm's per-channel mean, invstd, scale, shift of the ReLU(BN(y)) this output feeds
+    const float *e_y, *e_mean, *e_invstd, *e_scale, *e_shift;
 };
 
 __device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
@@ -453,6 +456,11 @@ struct OpLds {
 // plus static constexpr bool STATS (per-column BN partial sums written to a.stats).
 // blockIdx.x -> M tile, blockIdx.y -> N tile, blockIdx.z -> split-K slice.
 // --------------------------------------------------------------------------------------------
+// epilogues declaring BNBWD accumulate BN-backward partials (Σ dz, Σ dz·x̂) instead of (Σ v, Σ v²)
+template <class E, class = void>
+struct is_bnbwd : std::false_type {};
+template <class E>
+struct is_bnbwd<E, std::void_t<decltype(E::BNBWD)>> : std::integral_constant<bool, E::BNBWD> {};
 template <class E, class = void>
 struct is_structured : std::false_type {};
 template <class E>
@@ -566,10 +574,27 @@ __device__ __forceinline__ void gemm_epilogue_t(const GemmArgs& a, const Acc& ac
                     for (int r = 0; r < 4; ++r) {
                         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[r]), rs,
                                                               lo + (uint32_t)(r * ldc4), 0, 0);
-                        if constexpr (Epi::STATS) {
+                        if constexpr (Epi::STATS && !is_bnbwd<Epi>::value) {
                             const float vm = m0 + mr + r < a.M ? v[r] : 0.f;
                             ssum[j][slot] += vm;
                             ssq[j][slot] += vm * vm;
+                        }
+                    }
+                    if constexpr (is_bnbwd<Epi>::value) {
+                        // v = dL/d relu(bn(y)): Σ dz and Σ dz·x̂ with dz = v·[y·scale + shift > 0]
+                        // (the same test and x̂ as k_bn_relu_bwd), x̂ = (y − mean)·invstd
+                        if (n < a.N) {
+                            const float sc = a.e_scale[n], sh = a.e_shift[n], mu = a.e_mean[n], is = a.e_invstd[n];
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                const int m = m0 + mr + r;
+                                if (m < a.M) {
+                                    const float y = a.e_y[(int64_t)m * a.N + n];
+                                    const float dz = y * sc + sh > 0.f ? v[r] : 0.f;
+                                    ssum[j][slot] += dz;
+                                    ssq[j][slot] += dz * ((y - mu) * is);
+                                }
+                            }
                         }
                     }
                 }

@@ -27,9 +27,16 @@ void conv3x3_fwd(const float* x, int64_t ldx, int xcoff, int cin, const float* w
                  int64_t ldy, int ycoff, int B, int H, int W, float* stats, hipStream_t st,
                  const float* in_scale = nullptr, const float* in_shift = nullptr, const void* w_split = nullptr);
 int conv3x3_stats_rows(int B, int H, int W, int cout);
+// BN-backward partials from a conv3x3 dgrad epilogue (EpiStoreBnBwd) whose output g feeds
+// relu(bn(y)): y [M][cin] and that BatchNorm's coefficients; writes stats [tiles][2][cin] =
+// per-tile (Σ dz, Σ dz·x̂), tiles = conv3x3_stats_rows(B, H, W, cin)
+struct BnBwdEpi {
+    const float *y, *mean, *invstd, *scale, *shift;
+    float* stats;
+};
 // dx[pix][ci] = conv3x3(dz, wd) with wd = repacked [ci][tap'][co]
 void conv3x3_dgrad(const float* dz, int cout, const float* wd, int cin, float* dx, int64_t lddx,
-                   int B, int H, int W, hipStream_t st, const void* wd_split = nullptr);
+                   int B, int H, int W, hipStream_t st, const void* wd_split = nullptr, const BnBwdEpi* bn = nullptr);
 // dw[co][tap][ci] = sum_pix dz[pix][co] * im2col(x)[pix][tap,ci]
 void conv3x3_wgrad(const float* dz, int cout, const float* x, int64_t ldx, int xcoff, int cin, float* dw,
                    int B, int H, int W, float* slab, int64_t slab_cap, hipStream_t st,
@@ -60,7 +67,7 @@ void split_rows(const float* x, int64_t ldx, int xcoff, int C, int64_t M, void* 
 void conv3x3_fwd_ps(Split x, int cin, Split w, int cout, float* y, int64_t ldy, int ycoff, int B, int H, int W,
                     float* stats, hipStream_t st);
 void conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t lddx, int B, int H, int W,
-                      hipStream_t st);
+                      hipStream_t st, const BnBwdEpi* bn = nullptr);
 void conv3x3_wgrad_ps(Split dz, int cout, Split x, int cin, float* dw, int B, int H, int W, float* slab,
                       int64_t slab_cap, hipStream_t st);
 void convT_fwd_ps(Split x, int cin, Split wf, const float* bias, int cout, float* y, int64_t ldy, int ycoff, int B,
@@ -90,10 +97,13 @@ void bn_relu_fwd(const float* y, int C, const float* scale, const float* shift, 
 // writes dgamma/dbeta (grad buffer) and dy (dense [M][C]).  gmul != nullptr: g is first multiplied
 // by gmul[sample][c] (sample = row / HW) — the FiLM gamma sitting between this ReLU and the consumer.
 // dy_split != nullptr: also the pre-split twin of dy (dense, ld C)
+// tile_part != nullptr: (Σ dz, Σ dz·x̂) already reduced per GEMM tile by the producing dgrad
+// (BnBwdEpi, [tile_rows][2][C]); only those partials are summed (no pass over g and y)
 void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, const float* mean,
                  const float* invstd, const float* scale, const float* shift, const float* gamma,
                  int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
-                 hipStream_t st, const float* gmul = nullptr, int64_t HW = 1, void* dy_split = nullptr);
+                 hipStream_t st, const float* gmul = nullptr, int64_t HW = 1, void* dy_split = nullptr,
+                 const float* tile_part = nullptr, int tile_rows = 0);
 void maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float* out, uint8_t* idx,
                  hipStream_t st);
 void maxpool_bwd(const float* dout, const uint8_t* idx, int C, int B, int H, int W, float* dx,

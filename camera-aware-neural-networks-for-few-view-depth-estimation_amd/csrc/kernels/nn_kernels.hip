@@ -294,11 +294,17 @@ __global__ void k_bn_relu_bwd(const float* __restrict__ g, int64_t ldg, int gcof
 void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, const float* mean,
                  const float* invstd, const float* scale, const float* shift, const float* gamma,
                  int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
-                 hipStream_t st, const float* gmul, int64_t HW, void* dy_split) {
+                 hipStream_t st, const float* gmul, int64_t HW, void* dy_split, const float* tile_part,
+                 int tile_rows) {
     double* tot = scratch;
     double* part = scratch + 2 * C;
-    OpBnBwd op{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW};
-    const int S = launch_colreduce<2>(op, M, C, part, st);
+    int S;
+    if (tile_part) {   // [rows][2][C] partials -> part[s][2C] (the layout OpBnBwd's slices have)
+        S = launch_colreduce<1>(OpSum{tile_part, 2 * C, 0}, tile_rows, 2 * C, part, st);
+    } else {
+        OpBnBwd op{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW};
+        S = launch_colreduce<2>(op, M, C, part, st);
+    }
     launch_colfinal(part, S, 2 * C, tot, nullptr, 1.f, st);
     hipLaunchKernelGGL(k_bn_bwd_coef, dim3(cdiv(C, 64)), dim3(64), 0, st, tot, C, M, gamma, invstd, coef, dgamma, dbeta);
     const int64_t n4 = M * C / 4;
