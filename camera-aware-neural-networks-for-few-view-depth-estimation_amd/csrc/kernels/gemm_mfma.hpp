@@ -32,7 +32,7 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 #ifndef CAD_XCD_SWIZZLE
-#define CAD_XCD_SWIZZLE 0
+#define CAD_XCD_SWIZZLE 1
 #endif
 // K-stage geometry for stage depth KB (16 or 32)
 template <int KB>
