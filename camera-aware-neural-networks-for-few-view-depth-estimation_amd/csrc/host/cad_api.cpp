@@ -507,7 +507,9 @@ void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin,
             cad::film_apply(dc.y1, C, dc.b1.scale, dc.b1.shift, dc.film.gam, dc.film.bet, B, (int64_t)Hh * Ww, dc.a1, st);
             if (ps) cad::split_rows(dc.a1, C, 0, C, M, dc.a1s, C, 0, st);
         } else {
-            cad::bn_relu_fwd(dc.y1, C, dc.b1.scale, dc.b1.shift, dc.a1, C, 0, M, st, ps ? dc.a1s : nullptr, C, 0);
+            // pre-split GEMMs read only a1's twin (conv2 and its weight gradient): the fp32 a1 is not written
+            cad::bn_relu_fwd(dc.y1, C, dc.b1.scale, dc.b1.shift, ps ? nullptr : dc.a1, C, 0, M, st, ps ? dc.a1s : nullptr,
+                             C, 0);
         }
         if (ps) {
             cad::conv3x3_fwd_ps(sv(dc.a1s, C), C, sv(dc.c2.ws, 9 * C), C, dc.y2, C, 0, B, Hh, Ww, stats, st);
@@ -626,8 +628,10 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     void* dYs1 = h->side ? h->dYs1 : h->dYs;
     float* dA1 = h->Sa;
     // bn2 + relu
+    // with pre-split GEMMs both consumers of dY2 read its twin: the fp32 dY2 is not written
     cad::bn_relu_bwd(g, ldg, gcoff, dc.y2, C, dc.b2.mean, dc.b2.invstd, dc.b2.scale, dc.b2.shift, h->P(dc.b2.widx), M,
-                     h->dscr, dc.b2.coef, h->G(dc.b2.widx), h->G(dc.b2.bidx), dY2, st, nullptr, 1, ps ? dYs2 : nullptr);
+                     h->dscr, dc.b2.coef, h->G(dc.b2.widx), h->G(dc.b2.bidx), ps ? nullptr : dY2, st, nullptr, 1,
+                     ps ? dYs2 : nullptr);
     fork_side(h, st);
     // CAD_BNB=1: bn1's (Σ dz, Σ dz·x̂) come out of conv2's dgrad epilogue as tile partials (no FiLM
     // between the ReLU and conv2; not on the in-loader S3 pre-split-weight kernels).  Off by default:
@@ -654,15 +658,17 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     const int64_t HW = (int64_t)Hh * Ww;
     if (dc.has_film())
         cad::film_affine_bwd(dA1, dc.y1, C, dc.b1.scale, dc.b1.shift, B, HW, h->dscr, dc.film.dgam, dc.film.dbet, st);
-    // bn1 + relu
+    // bn1 + relu; the fp32 dY1 only when a conv1 GEMM below reads it (enc1's 4-channel input keeps the
+    // in-loader weight gradient)
+    const bool ps1 = ps && in_s.p && dc.c1.ws;
+    const bool dy1_f32 = !ps1 || (din && !(ps && dc.c1.wds));
     cad::bn_relu_bwd(dA1, C, 0, dc.y1, C, dc.b1.mean, dc.b1.invstd, dc.b1.scale, dc.b1.shift, h->P(dc.b1.widx), M,
-                     h->dscr, dc.b1.coef, h->G(dc.b1.widx), h->G(dc.b1.bidx), dY1, st,
+                     h->dscr, dc.b1.coef, h->G(dc.b1.widx), h->G(dc.b1.bidx), dy1_f32 ? dY1 : nullptr, st,
                      dc.has_film() ? dc.film.gam : nullptr, HW, ps ? dYs1 : nullptr, bnb ? h->stats : nullptr,
                      bn_rows);
     if (dc.has_film()) cad::film_mlp_bwd(film_view(h, dc), h->camn, B, st);
     fork_side(h, st);
     // conv1: wgrad (side) || dgrad (caller's stream)
-    const bool ps1 = ps && in_s.p && dc.c1.ws;
     if (ps1)
         cad::conv3x3_wgrad_ps(sv(dYs1, C), C, in_s, dc.c1.cin, h->G(dc.c1.pidx), B, Hh, Ww, h->slab, h->slab_cap, ws);
     else
@@ -1112,6 +1118,9 @@ int cad_unet_num_stages(const cad_unet*) { return kStages; }
 cad_status cad_unet_backward_stage(cad_unet* h, int stage, const float* ddepth, void* stream) {
     return guard([&] {
         require(h->have_fwd, "backward needs a preceding train-mode forward", CAD_ERR_STATE);
+        // the forward kept only the split twins of some operands (a1) for the pre-split backward
+        require(h->fwd_np == 0 || h->fwd_np == cad::split_planes(),
+                "GEMM engine changed between forward and backward", CAD_ERR_STATE);
         require(stage >= 0 && stage < kStages, "stage out of range");
         require(stage != 0 || ddepth, "null ddepth");
         HIPCHK(hipSetDevice(h->device));
@@ -1123,6 +1132,9 @@ cad_status cad_unet_backward_stage(cad_unet* h, int stage, const float* ddepth, 
 cad_status cad_unet_backward(cad_unet* h, const float* ddepth, void* stream) {
     return guard([&] {
         require(h->have_fwd, "backward needs a preceding train-mode forward", CAD_ERR_STATE);
+        // the forward kept only the split twins of some operands (a1) for the pre-split backward
+        require(h->fwd_np == 0 || h->fwd_np == cad::split_planes(),
+                "GEMM engine changed between forward and backward", CAD_ERR_STATE);
         require(ddepth, "null ddepth");
         HIPCHK(hipSetDevice(h->device));
         for (int s = 0; s < kStages; ++s) backward_stage(h, s, ddepth, S(stream));

@@ -225,7 +225,7 @@ __global__ void k_bn_relu_fwd(const float* __restrict__ y, int C, const float* _
         o.y = fmaxf(v.y * s.y + t.y, 0.f);
         o.z = fmaxf(v.z * s.z + t.z, 0.f);
         o.w = fmaxf(v.w * s.w + t.w, 0.f);
-        *reinterpret_cast<float4*>(out + r * ldo + ocoff + c) = o;
+        if (out) *reinterpret_cast<float4*>(out + r * ldo + ocoff + c) = o;   // nullptr: only the twin is read
         if constexpr (NP > 0) split4_store<NP>(os, ldos, oscoff, r, c, o);
     }
 }
@@ -287,7 +287,7 @@ __global__ void k_bn_relu_bwd(const float* __restrict__ g, int64_t ldg, int gcof
             o[e] = coef[c] * dz - coef[C + c] - coef[2 * C + c] * xh;
         }
         const float4 ov = make_float4(o[0], o[1], o[2], o[3]);
-        *reinterpret_cast<float4*>(dy + i * 4) = ov;
+        if (dy) *reinterpret_cast<float4*>(dy + i * 4) = ov;   // nullptr: only the twin is read
         if constexpr (NP > 0) split4_store<NP>(os, C, 0, r, c0, ov);
     }
 }
