@@ -481,8 +481,10 @@ void split_weights(const cad_unet* h, hipStream_t st) {   // forward weights, ev
 }
 
 // in_s / out_s: split twins of the block input / output (p == nullptr: none)
+// out_f32 = false: with pre-split GEMMs downstream only the output's twin is read (decoder outputs
+// above level 0, the bottleneck), so the fp32 output is not written
 void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin, cad::Split in_s, int B, float* out,
-                     int64_t ldo, int ocoff, cad::Split out_s, hipStream_t st) {
+                     int64_t ldo, int ocoff, cad::Split out_s, hipStream_t st, bool out_f32 = true) {
     const int l = dc.level, Hh = h->Hl(l), Ww = h->Wl(l), C = dc.c1.cout;
     const int64_t M = h->Ml(l, B);
     const bool tr = h->train;
@@ -523,8 +525,9 @@ void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin,
                          dc.b1.shift);
     }
     bn(dc.b2);
-    cad::bn_relu_fwd(dc.y2, C, dc.b2.scale, dc.b2.shift, out, ldo, ocoff, M, st, ps ? const_cast<void*>(out_s.p) : nullptr,
-                     out_s.ld, out_s.coff);
+    const bool twin = ps && out_s.p;
+    cad::bn_relu_fwd(dc.y2, C, dc.b2.scale, dc.b2.shift, (out_f32 || !twin) ? out : nullptr, ldo, ocoff, M, st,
+                     twin ? const_cast<void*>(out_s.p) : nullptr, out_s.ld, out_s.coff);
 }
 
 void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth, int B, hipStream_t st) {
@@ -571,14 +574,17 @@ void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth
     double_conv_fwd(h, h->enc[0], h->x0, h->x0_ld, x0s, B, h->cat[0], 2 * f, 0, sv(h->cats[0], 2 * f), st);
     for (int l = 1; l <= 4; ++l) {
         const int Cp = h->Cl(l - 1);
-        cad::maxpool_fwd(h->cat[l - 1], 2 * Cp, Cp, B, h->Hl(l - 1), h->Wl(l - 1), h->pool[l], h->pidx[l], st);
-        if (ps) split_into(h->pool[l], Cp, 0, Cp, h->Ml(l, B), h->pools[l], Cp, 0, st);
+        // pre-split GEMMs read only the pooled twin (enc conv1 and its weight gradient)
+        const bool ptwin = ps && h->pools[l];
+        cad::maxpool_fwd(h->cat[l - 1], 2 * Cp, Cp, B, h->Hl(l - 1), h->Wl(l - 1), ptwin ? nullptr : h->pool[l],
+                         h->pidx[l], st, ptwin ? h->pools[l] : nullptr);
         const cad::Split pin = sv(h->pools[l], Cp);
         if (l < 4)
             double_conv_fwd(h, h->enc[l], h->pool[l], Cp, pin, B, h->cat[l], 2 * h->Cl(l), 0,
                             sv(h->cats[l], 2 * h->Cl(l)), st);
         else
-            double_conv_fwd(h, h->enc[4], h->pool[4], Cp, pin, B, h->a2_bott, h->Cl(4), 0, sv(h->botts, h->Cl(4)), st);
+            double_conv_fwd(h, h->enc[4], h->pool[4], Cp, pin, B, h->a2_bott, h->Cl(4), 0, sv(h->botts, h->Cl(4)), st,
+                            false);
     }
     for (int l = 3; l >= 0; --l) {
         const float* upin = l == 3 ? h->a2_bott : h->dout[l + 1];
@@ -594,7 +600,7 @@ void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth
                            h->Wl(l + 1), st, h->wsplit ? u.wfs : nullptr);
         }
         double_conv_fwd(h, h->dec[l], h->cat[l], 2 * C, sv(h->cats[l], 2 * C), B, h->dout[l], C, 0,
-                        l > 0 ? sv(h->douts[l], C) : none, st);
+                        l > 0 ? sv(h->douts[l], C) : none, st, l == 0);
     }
     cad::head_fwd(h->dout[0], f, h->P(h->head_w), h->P(h->head_b), h->max_depth, h->sig, depth, h->Ml(0, B), st);
 }

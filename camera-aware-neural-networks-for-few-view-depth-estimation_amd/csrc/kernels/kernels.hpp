@@ -104,8 +104,9 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
                  int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
                  hipStream_t st, const float* gmul = nullptr, int64_t HW = 1, void* dy_split = nullptr,
                  const float* tile_part = nullptr, int tile_rows = 0);
+// out_split != nullptr: also the pooled output's split twin (dense, ld C); out may then be nullptr
 void maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float* out, uint8_t* idx,
-                 hipStream_t st);
+                 hipStream_t st, void* out_split = nullptr);
 void maxpool_bwd(const float* dout, const uint8_t* idx, int C, int B, int H, int W, float* dx,
                  int64_t lddx, hipStream_t st);
 void rgb_to_nhwc4(const float* rgb, float* out, int B, int H, int W, hipStream_t st);

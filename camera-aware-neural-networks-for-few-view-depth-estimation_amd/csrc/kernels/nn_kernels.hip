@@ -324,8 +324,9 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
 // ------------------------------------------------------------------------------------------
 // MaxPool2d(2) (baseline_unet.h:55 / :62), argmax kept as uint8 in scan order 0..3
 // ------------------------------------------------------------------------------------------
+template <int NP>
 __global__ void k_maxpool_fwd(const float* __restrict__ x, int64_t ldx, int C, int B, int H, int W,
-                              float* __restrict__ out, uint8_t* __restrict__ idx, int64_t n4) {
+                              float* __restrict__ out, uint8_t* __restrict__ idx, int64_t n4, char* __restrict__ os) {
     const int C4 = C >> 2, Ho = H >> 1, Wo = W >> 1;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t op = i / C4;
@@ -350,14 +351,23 @@ __global__ void k_maxpool_fwd(const float* __restrict__ x, int64_t ldx, int C, i
             for (int e = 0; e < 4; ++e)
                 if (va[e] > best[e] || isnan(va[e])) { best[e] = va[e]; arg[e] = (uint8_t)k; }
         }
-        *reinterpret_cast<float4*>(out + op * C + c) = make_float4(best[0], best[1], best[2], best[3]);
+        const float4 o = make_float4(best[0], best[1], best[2], best[3]);
+        if (out) *reinterpret_cast<float4*>(out + op * C + c) = o;   // nullptr: only the twin is read
+        if constexpr (NP > 0) split4_store<NP>(os, C, 0, op, c, o);
         *reinterpret_cast<uchar4*>(idx + op * C + c) = make_uchar4(arg[0], arg[1], arg[2], arg[3]);
     }
 }
 void maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float* out, uint8_t* idx,
-                 hipStream_t st) {
+                 hipStream_t st, void* out_split) {
     const int64_t n4 = (int64_t)B * (H / 2) * (W / 2) * C / 4;
-    hipLaunchKernelGGL(k_maxpool_fwd, dim3(ew_blocks(n4)), dim3(256), 0, st, x, ldx, C, B, H, W, out, idx, n4);
+    const int np = out_split ? split_planes() : 0;
+    char* os = static_cast<char*>(out_split);
+    if (np == 3)
+        hipLaunchKernelGGL(k_maxpool_fwd<3>, dim3(ew_blocks(n4)), dim3(256), 0, st, x, ldx, C, B, H, W, out, idx, n4, os);
+    else if (np == 1)
+        hipLaunchKernelGGL(k_maxpool_fwd<1>, dim3(ew_blocks(n4)), dim3(256), 0, st, x, ldx, C, B, H, W, out, idx, n4, os);
+    else
+        hipLaunchKernelGGL(k_maxpool_fwd<0>, dim3(ew_blocks(n4)), dim3(256), 0, st, x, ldx, C, B, H, W, out, idx, n4, os);
 }
 // dx[argmax] += dout  (in place on the skip half of the decoder concat gradient)
 __global__ void k_maxpool_bwd(const float* __restrict__ dout, const uint8_t* __restrict__ idx, int C, int B,
