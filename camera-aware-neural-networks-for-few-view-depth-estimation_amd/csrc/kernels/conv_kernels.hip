@@ -332,17 +332,22 @@ __global__ void k_split_rows(const float* __restrict__ x, int64_t ldx, int xcoff
     split8_store<NP>(out + row * ldo * 2 * NP + (int64_t)((ocoff >> 3) + g) * 16 * NP, a, b);
 }
 
-// deterministic split-K reduction: dst[e] = sum_z slab[z][e]
-__global__ void k_slab_reduce(const float* __restrict__ slab, int nsplit, int64_t stride,
+// deterministic split-K reduction: dst[e] = sum_z slab[z * zstep][e] for z < nsplit (fixed order).
+// Two levels when there are many slabs (the 64-channel weight gradients: ~680 slices of a small
+// M x N): level 1 sums each group of G consecutive slabs into the group's first slab (blockIdx.y =
+// group), level 2 sums the group heads — a few dozen dependent loads per thread instead of ~680.
+__global__ void k_slab_reduce(float* __restrict__ slab, int nsplit, int64_t stride, int zstep,
                               float* __restrict__ dst, int64_t n) {
     int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
     if (i >= n) return;
-    float4 s = *reinterpret_cast<const float4*>(slab + i);
+    const int z0 = blockIdx.y * nsplit;   // level 1: this group's slabs; level 2: gridDim.y == 1
+    float4 s = *reinterpret_cast<const float4*>(slab + (int64_t)z0 * zstep * stride + i);
     for (int z = 1; z < nsplit; ++z) {
-        float4 t = *reinterpret_cast<const float4*>(slab + z * stride + i);
+        float4 t = *reinterpret_cast<const float4*>(slab + (int64_t)(z0 + z) * zstep * stride + i);
         s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
     }
-    *reinterpret_cast<float4*>(dst + i) = s;
+    float* out = dst ? dst + i : slab + (int64_t)z0 * zstep * stride + i;
+    *reinterpret_cast<float4*>(out) = s;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -773,7 +778,26 @@ int64_t wgrad_slab_floats(int M, int N, int Kpix) {
 }
 
 static void finish_slabs(float* slab, int splits, int64_t per, float* dw, hipStream_t st) {
-    hipLaunchKernelGGL(k_slab_reduce, dim3(cdiv(per / 4, 256)), dim3(256), 0, st, slab, splits, per, dw, per);
+    const unsigned bx = (unsigned)cdiv(per / 4, 256);
+    constexpr int G = 24;   // slabs per level-1 group
+    static const bool two_level = !(std::getenv("CAD_SLAB2") && std::getenv("CAD_SLAB2")[0] == '0');
+    if (two_level && splits >= 2 * G && bx < 512) {
+        const int groups = splits / G;   // whole groups; the remainder slabs join level 2 one by one
+        hipLaunchKernelGGL(k_slab_reduce, dim3(bx, groups), dim3(256), 0, st, slab, G, per, 1, (float*)nullptr, per);
+        // level 2: group heads z = 0, G, 2G, ... then the remainder slabs groups*G .. splits-1
+        hipLaunchKernelGGL(k_slab_reduce, dim3(bx, 1), dim3(256), 0, st, slab, groups, per, G, (float*)nullptr, per);
+        const int rem = splits - groups * G;
+        if (rem == 0) {
+            hipLaunchKernelGGL(k_slab_reduce, dim3(bx, 1), dim3(256), 0, st, slab, 1, per, 1, dw, per);
+        } else {
+            // move the level-2 total next to the remainder and sum those (fixed order)
+            float* tail = slab + (int64_t)(groups * G - 1) * per;
+            hipLaunchKernelGGL(k_slab_reduce, dim3(bx, 1), dim3(256), 0, st, slab, 1, per, 1, tail, per);
+            hipLaunchKernelGGL(k_slab_reduce, dim3(bx, 1), dim3(256), 0, st, tail, rem + 1, per, 1, dw, per);
+        }
+        return;
+    }
+    hipLaunchKernelGGL(k_slab_reduce, dim3(bx, 1), dim3(256), 0, st, slab, splits, per, 1, dw, per);
 }
 
 void conv3x3_wgrad(const float* dz, int cout, const float* x, int64_t ldx, int xcoff, int cin, float* dw,
