@@ -622,8 +622,10 @@ void join_side(cad_unet* h, hipStream_t st) {
     HIPCHK(hipStreamWaitEvent(st, h->ev_join, 0));
 }
 
+// pool: the max-pool gradient of the next level, still to be routed into g (folded into bn2's backward)
 void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, int gcoff, const float* in,
-                     int64_t ldin, cad::Split in_s, int B, float* din, int64_t lddin, hipStream_t st) {
+                     int64_t ldin, cad::Split in_s, int B, float* din, int64_t lddin, hipStream_t st,
+                     cad::PoolGrad pool = cad::PoolGrad{}) {
     const int l = dc.level, Hh = h->Hl(l), Ww = h->Wl(l), C = dc.c1.cout;
     const int64_t M = h->Ml(l, B);
     const bool ps = h->fwd_np > 0 && h->fwd_np == cad::split_planes();
@@ -637,7 +639,7 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     // with pre-split GEMMs both consumers of dY2 read its twin: the fp32 dY2 is not written
     cad::bn_relu_bwd(g, ldg, gcoff, dc.y2, C, dc.b2.mean, dc.b2.invstd, dc.b2.scale, dc.b2.shift, h->P(dc.b2.widx), M,
                      h->dscr, dc.b2.coef, h->G(dc.b2.widx), h->G(dc.b2.bidx), ps ? nullptr : dY2, st, nullptr, 1,
-                     ps ? dYs2 : nullptr);
+                     ps ? dYs2 : nullptr, nullptr, 0, pool);
     fork_side(h, st);
     // CAD_BNB=1: bn1's (Σ dz, Σ dz·x̂) come out of conv2's dgrad epilogue as tile partials (no FiLM
     // between the ReLU and conv2; not on the in-loader S3 pre-split-weight kernels).  Off by default:
@@ -753,14 +755,21 @@ void backward_stage(cad_unet* h, int stage, const float* dpred, hipStream_t st) 
     const int C = h->Cl(l);
     const float* g = l == 4 ? h->Sa : h->dcat[l];
     const int64_t ldg = l == 4 ? C : 2 * C;
+    // CAD_POOLFOLD=1: the max-pool backward of level l+1 (its gradient in Sc) is folded into this
+    // block's bn2 backward passes instead of a read-modify-write pass over dcat's skip half.  Off by
+    // default: measured on MI355X the gather in both BN-backward passes costs 0.3-0.6 % more than the
+    // pass it removes
+    static const bool fold = std::getenv("CAD_POOLFOLD") && std::getenv("CAD_POOLFOLD")[0] == '1';
+    const cad::PoolGrad pool =
+        fold && l < 4 ? cad::PoolGrad{h->Sc, h->pidx[l + 1], h->Hl(l), h->Wl(l)} : cad::PoolGrad{};
     if (l == 0) {
-        double_conv_bwd(h, e, g, ldg, 0, h->x0, h->x0_ld, sv(h->x0s, h->x0_ld), B, nullptr, 0, st);
+        double_conv_bwd(h, e, g, ldg, 0, h->x0, h->x0_ld, sv(h->x0s, h->x0_ld), B, nullptr, 0, st, pool);
         join_side(h, st);
         return;
     }
     const int Cp = h->Cl(l - 1);
-    double_conv_bwd(h, e, g, ldg, 0, h->pool[l], Cp, sv(h->pools[l], Cp), B, h->Sc, Cp, st);
-    cad::maxpool_bwd(h->Sc, h->pidx[l], Cp, B, h->Hl(l - 1), h->Wl(l - 1), h->dcat[l - 1], 2 * Cp, st);
+    double_conv_bwd(h, e, g, ldg, 0, h->pool[l], Cp, sv(h->pools[l], Cp), B, h->Sc, Cp, st, pool);
+    if (!fold) cad::maxpool_bwd(h->Sc, h->pidx[l], Cp, B, h->Hl(l - 1), h->Wl(l - 1), h->dcat[l - 1], 2 * Cp, st);
     join_side(h, st);
 }
 

@@ -93,6 +93,13 @@ void bn_eval_coeffs(const float* gamma, const float* beta, const float* run_mean
 // offset oscoff, split_planes() planes; see Split below)
 void bn_relu_fwd(const float* y, int C, const float* scale, const float* shift, float* out, int64_t ldo,
                  int ocoff, int64_t M, hipStream_t st, void* os = nullptr, int64_t ldos = 0, int oscoff = 0);
+// MaxPool2d(2) backward folded into a consumer of its gradient: g[pixel] += dpool[parent] where the
+// pixel is the parent's recorded argmax (H, W: the pooled-from grid); g = nullptr: none
+struct PoolGrad {
+    const float* g = nullptr;
+    const uint8_t* idx = nullptr;
+    int H = 0, W = 0;
+};
 // BN+ReLU backward: dy = k1*dz - k2 - k3*xhat, dz = g*[y*scale+shift > 0];
 // writes dgamma/dbeta (grad buffer) and dy (dense [M][C]).  gmul != nullptr: g is first multiplied
 // by gmul[sample][c] (sample = row / HW) — the FiLM gamma sitting between this ReLU and the consumer.
@@ -103,7 +110,7 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
                  const float* invstd, const float* scale, const float* shift, const float* gamma,
                  int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
                  hipStream_t st, const float* gmul = nullptr, int64_t HW = 1, void* dy_split = nullptr,
-                 const float* tile_part = nullptr, int tile_rows = 0);
+                 const float* tile_part = nullptr, int tile_rows = 0, PoolGrad pool = PoolGrad{});
 // out_split != nullptr: also the pooled output's split twin (dense, ld C); out may then be nullptr
 void maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float* out, uint8_t* idx,
                  hipStream_t st, void* out_split = nullptr);
