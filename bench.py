@@ -14,15 +14,16 @@ libcad_hip.so.  Synthetic SUN-RGB-D-shaped batches resident in HBM (data loading
   RCCL gradient all-reduce overlapped with backward, weak scaling: bs32 per GPU).
 
 Rank 0 prints ONE JSON line.  roofline: the dominant MFMA kernel (largest total time in the timed
-region, timed live with HIP events on its launch stream) against the fp32 MFMA peak.  cpu_baseline:
-the REFERENCE itself (oracle/_ref/ref_harness, the reference headers compiled against LibTorch) on a
-bounded sample on the host cores, or the oracle restatement if that binary is absent.
+region, timed live with HIP events on its launch stream) against its engine's MFMA ceiling.
+cpu_baseline: the oracle restatement (LibTorch CPU, the reference's ATen kernels) on a bounded
+sample of the workload on this host's cores; parity: the same sampled steps on the GPU compared live
+with it (prediction, losses, eval-mode abs_rel).  bf16_workloads: bounded runs of the other BASELINE
+workloads (configs[2], configs[3]'s per-GPU step) in the same process.
 """
 import argparse
 import ctypes as C
 import json
 import os
-import subprocess
 import sys
 import time
 
@@ -65,8 +66,9 @@ def parse():
     ap.add_argument("--dtype", default=None, choices=("fp32", "bf16"),
                     help="GEMM arithmetic: fp32 (S3 engine, fp32-accurate) or bf16 operands / fp32 accumulation")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-batch", type=int, default=2)
-    ap.add_argument("--cpu-sample-steps", type=int, default=2)
+    ap.add_argument("--no-extra", action="store_true", help="skip the bf16 workload legs and the data path")
+    ap.add_argument("--cpu-sample-batch", type=int, default=8)
+    ap.add_argument("--cpu-sample-steps", type=int, default=3)
     a = ap.parse_args()
     preset = {2: ("baseline", "fp32", "1,0,0,0"), 3: ("rayfilm", "bf16", "1,0.1,0.001,0.01"),
               4: ("baseline", "bf16", "1,0.1,0.001,0.01")}[a.config]
@@ -76,38 +78,138 @@ def parse():
     return a
 
 
-def cpu_baseline(args):
-    """Reference LibTorch CPU path on a bounded sample of the same workload (host cores)."""
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    B, H, W, f = args.cpu_sample_batch, args.height, args.width, args.features
-    sample = (f"{args.model} bs{B} {H}x{W} f={f} weights {args.weights}, fp32 (the reference's only precision), "
-              f"1 warm-up + {args.cpu_sample_steps} timed train steps")
-    harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
-    if os.path.exists(harness):
-        cmd = [harness, "--mode", "time", "--f", str(f), "--B", str(B), "--H", str(H), "--W", str(W),
-               "--steps", str(args.cpu_sample_steps), "--warmup", "1", "--threads", str(threads),
-               "--weights", args.weights, "--model", args.model]
-        try:
-            out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, check=True).stdout
-            r = json.loads(out.strip().splitlines()[-1])
-            return {"value": round(r["images_per_s"], 4), "unit": "images/s", "cores": threads, "kind": "reference",
-                    "sample": sample + " (reference headers compiled against LibTorch CPU: oracle/_ref/ref_harness)"}
-        except Exception as e:   # fall through to the restatement
-            log(f"reference harness failed ({e}); timing the oracle restatement instead")
+def host_cpu():
+    """CPU model, physical core / logical CPU counts of this host, and the CPUs this process may use."""
+    model, pairs, logical, phys_id = None, set(), 0, "0"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "processor":
+                    logical += 1
+                elif k == "model name" and model is None:
+                    model = v
+                elif k == "physical id":
+                    phys_id = v
+                elif k == "core id":
+                    pairs.add((phys_id, v))
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = os.cpu_count()
+    return {"cpu_model": model, "physical_cores": len(pairs) or None, "logical_cpus": logical or os.cpu_count(),
+            "usable_cpus": usable}
+
+
+def cpu_baseline_and_parity(args, cad, dev, lib):
+    """cpu_baseline leg: the oracle restatement (oracle/cad_oracle.py: LibTorch CPU, the ATen kernels
+    the reference dispatches; the reference source and its compiled harness stay in the build
+    container) timed on this host on a bounded sample of the workload — bs`cpu_sample_batch` at the
+    benchmark resolution, 1 warm-up + `cpu_sample_steps` timed train steps from the same initial
+    weights and batch.  The same steps also run on the GPU (same engine as the headline) and are
+    compared live: step-1 prediction, every step's loss, and after the last step the eval-mode
+    prediction and abs_rel (computeDepthMetrics) on a held-out synthetic batch."""
     import torch
-    torch.set_num_threads(threads)
     from oracle import cad_oracle as O
-    params, bufs = O.init_params(f), O.init_buffers(f)
-    rgb, gt, K = [torch.from_numpy(a) for a in O.synth_batch(B, H, W)]
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    B, H, W, f = args.cpu_sample_batch, args.height, args.width, args.features
     w = tuple(float(x) for x in args.weights.split(","))
-    tr = O.Trainer(params, bufs, weights=w)
-    tr.step(rgb, gt, K)
+    params = O.init_params(f, seed=42, model=args.model)
+    bufs = O.init_buffers(f, model=args.model)
+    rgb, gt, K = [torch.from_numpy(a) for a in O.synth_batch(B, H, W)]
+    hr, hg, hk = [torch.from_numpy(a) for a in O.synth_batch(2, H, W, rgb_seed=0xBEEF, hole_seed=0xF00D)]
+
+    # GPU replica of the sampled steps
+    cls = {"baseline": cad.BaselineUNet, "film": cad.IntrinsicsConditionedUNet,
+           "rayfilm": cad.RayConditionedUNet}[args.model]
+    model = cls(3, f, max_depth=10.0, batch=B, height=H, width=W, device=dev.index)
+    st = dict(params)
+    st.update(bufs)
+    model.load_state_dict(st)
+    loss = cad.CombinedDepthLoss(*w, batch=B, height=H, width=W, device=dev.index)
+    tr = cad.Trainer(model, loss, lr=1e-4, weight_decay=1e-5, grad_clip=1.0)
+    rg, gg, kg = rgb.to(dev), gt.to(dev), K.to(dev)
+    g_losses, g_pred1 = [], None
+    for i in range(1 + args.cpu_sample_steps):
+        g_losses.append(tr.train_step(rg, gg, kg)[0].item())
+        if i == 0:
+            g_pred1 = tr.pred.cpu()
+    model.eval()
+    hrg, hgg = hr.to(dev), hg.to(dev)
+    g_eval = model(hrg, cad.camera_from_K(hk.to(dev))) if model.conditioned else model(hrg)
+    g_eval = g_eval.cpu()
+    g_absrel = cad.depth_metrics(g_eval.to(dev), hgg)["abs_rel"]
+    del model, loss, tr
+    torch.cuda.empty_cache()
+
+    # the CPU reference path (fp32: the reference's only precision)
+    ref = O.Trainer(params, bufs, weights=w, model=args.model)
+    r1 = ref.step(rgb, gt, K)                      # warm-up (and parity step 1)
+    c_losses = [r1["loss"]]
     t0 = time.perf_counter()
     for _ in range(args.cpu_sample_steps):
-        tr.step(rgb, gt, K)
+        c_losses.append(ref.step(rgb, gt, K)["loss"])
     dt = time.perf_counter() - t0
-    return {"value": round(B * args.cpu_sample_steps / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": sample + " (oracle/cad_oracle.py restatement on LibTorch CPU)"}
+    c_eval = ref.predict_eval(hr, hk if args.model != "baseline" else None)
+    c_absrel = O.abs_rel_per_sample(c_eval, hg)
+
+    def mre(a, b):
+        den = b.abs().max().item()
+        return (a.double() - b.double()).abs().max().item() / (den if den > 0 else 1.0)
+    host = host_cpu()
+    cpu = {"value": round(B * args.cpu_sample_steps / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
+           "sample": (f"{args.model} bs{B} {H}x{W} f={f} loss weights {args.weights}, fp32 (the reference's only "
+                      f"precision), 1 warm-up + {args.cpu_sample_steps} timed train steps of the oracle restatement "
+                      f"(oracle/cad_oracle.py on LibTorch CPU, {threads} threads; BN statistics over bs{B}, not bs32)"),
+           "seconds": round(dt, 2), "host": host}
+    parity = {"what": (f"the cpu_baseline sample's {1 + args.cpu_sample_steps} train steps on the GPU "
+                       f"({args.dtype} engine) vs the CPU reference path from identical weights and batch, then "
+                       f"eval-mode forward + computeDepthMetrics on a held-out bs2 batch"),
+              "step1_pred_max_rel_err": mre(g_pred1, r1["pred"]),
+              "loss_max_rel_err": max(abs(a - b) / abs(b) for a, b in zip(g_losses, c_losses)),
+              "eval_pred_max_rel_err": mre(g_eval, c_eval),
+              "abs_rel_gpu": round(g_absrel, 6), "abs_rel_cpu_ref": round(c_absrel, 6),
+              "abs_rel_delta": abs(g_absrel - c_absrel)}
+    return cpu, parity
+
+
+def extra_leg(cad, lib, dev, config, steps=5, warmup=2, B=32, H=480, W=640, f=64):
+    """A bounded measurement of another BASELINE workload in the same run (driver-observed):
+    configs[2] (ray+FiLM U-Net, bf16 GEMMs, full loss) or configs[3]'s per-GPU step (baseline_unet,
+    bf16 GEMMs, full loss)."""
+    import torch
+    from cad_amd import synthetic
+    model_name, dtype = PRESETS[config]
+    prev = lib.cad_get_gemm_engine()
+    assert lib.cad_set_gemm_engine(2 if dtype == "bf16" else 1) == 0
+    cls = {"baseline": cad.BaselineUNet, "rayfilm": cad.RayConditionedUNet}[model_name]
+    model = cls(3, f, max_depth=10.0, batch=B, height=H, width=W, device=dev.index)
+    loss = cad.CombinedDepthLoss(1.0, 0.1, 0.001, 0.01, batch=B, height=H, width=W, device=dev.index)
+    tr = cad.Trainer(model, loss, lr=1e-4, weight_decay=1e-5, grad_clip=1.0)
+    rgb, gt, K = (t.to(dev) for t in synthetic.device_batch(B, H, W, "cpu"))
+    for _ in range(warmup):
+        tr.train_step(rgb, gt, K)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tr.train_step(rgb, gt, K)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    last = tr.loss5[0].item()
+    del tr, loss, model
+    torch.cuda.empty_cache()
+    lib.cad_set_gemm_engine(prev)
+    value = B * steps / dt
+    out = {"workload": WORKLOADS[config], "value": round(value, 3), "unit": "images/s",
+           "ms_per_step": round(1e3 * dt / steps, 3), "steps": steps, "warmup": warmup, "dtype": dtype,
+           "last_loss": last}
+    if model_name == "baseline":
+        out["mfma_frac_dense_bf16"] = round(FLOP_PER_IMAGE_480x640_F64 * value / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4)
+    return out
 
 
 def pmc_traffic(kernel_name):
@@ -117,24 +219,6 @@ def pmc_traffic(kernel_name):
         with open(path) as fh:
             d = json.load(fh)
         return d.get(kernel_name, {}).get("hbm_bytes_per_launch")
-    except Exception:
-        return None
-
-
-def parity_evidence():
-    """The committed GPU-vs-CPU-reference parity report (tests/parity_report.py), newest round."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "parity_r*.json")))
-    if not files:
-        return None
-    try:
-        with open(files[-1]) as fh:
-            d = json.load(fh)
-        c0, rf = d["config0_vs_cpu_ref"], d["reference_fixture"]
-        return {"source": os.path.relpath(files[-1], ROOT), "abs_rel_gpu": round(c0["abs_rel_gpu"], 6),
-                "abs_rel_cpu_ref": round(c0["abs_rel_cpu_ref"], 6), "abs_rel_delta": c0["abs_rel_delta"],
-                "eval_pred_max_rel_err_vs_cpu": c0["eval_pred_max_rel_err_vs_cpu"], "shape": c0["shape"],
-                "reference_fixture_pred_max_rel_err": rf["pred_max_rel_err"]}
     except Exception:
         return None
 
@@ -205,7 +289,9 @@ def main():
     assert lib.cad_set_gemm_engine(2 if args.dtype == "bf16" else 1) == 0   # CAD_GEMM_BF16 / CAD_GEMM_S3
     cls = {"baseline": cad.BaselineUNet, "film": cad.IntrinsicsConditionedUNet,
            "rayfilm": cad.RayConditionedUNet}[args.model]
+    params_count = None
     model = cls(3, f, max_depth=10.0, batch=B, height=H, width=W, device=local)
+    params_count = model.count_parameters()
     if world > 1:
         dist.broadcast(model.flat_params, 0)   # identical replicas (DDP semantics)
     loss = cad.CombinedDepthLoss(*w, batch=B, height=H, width=W, device=local)
@@ -249,13 +335,14 @@ def main():
         images = B * world * args.steps
         value = images / elapsed
         ms_per_step = 1e3 * elapsed / args.steps
-        dom = max(prof, key=lambda r: r["ms"]) if prof else None
+        gemm = [r for r in prof if r["gflop"] > 0]   # (split-K reductions are profiled at 0 FLOP)
+        dom = max(gemm, key=lambda r: r["ms"]) if gemm else None
         roof = None
         if dom:
             achieved = dom["gflop"] / dom["ms"]   # GFLOP/ms == TFLOP/s
-            kname = dom["name"].split("<")[0]   # k_<op>_<engine>[p][L]: p = pre-split operands, L = large tile
-            s3 = kname.endswith(("_s3", "_s3p", "_s3L", "_s3pL"))
-            b1 = kname.endswith(("_bf16", "_bf16p", "_bf16L", "_bf16pL"))
+            kname = dom["name"].split("<")[0]   # k_<op>_<engine>[p]: p = pre-split operands
+            s3 = kname.endswith("_s3")
+            b1 = kname.endswith(("_bf16", "_bf16p"))
             peak = S3_PEAK_TFLOPS if s3 else BF16_MFMA_PEAK_TFLOPS if b1 else FP32_MFMA_PEAK_TFLOPS
             roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": round(peak, 1), "unit": "TFLOP/s",
                     "frac": round(achieved / peak, 4), "traffic": pmc_traffic(dom["name"]),
@@ -266,21 +353,32 @@ def main():
                     "kernel": dom["name"], "launches_per_step": dom["launches"] // args.steps,
                     "avg_launch_ms": round(dom["ms"] / dom["launches"], 4),
                     "gflop_per_launch": round(dom["gflop"] / dom["launches"], 3)}
-            tot_ms = sum(r["ms"] for r in prof)
-            tot_gf = sum(r["gflop"] for r in prof)
+            tot_ms = sum(r["ms"] for r in gemm)
+            tot_gf = sum(r["gflop"] for r in gemm)
             roof["all_gemm_kernels"] = {"tflops": round(tot_gf / tot_ms, 3), "ms_per_step": round(tot_ms / args.steps, 3),
                                         "share_of_step": round(tot_ms / args.steps / ms_per_step, 4)}
         step_tflops = (FLOP_PER_IMAGE_480x640_F64 * value / 1e12
                        if (H, W, f, args.model) == (480, 640, 64, "baseline") else None)
-        dp = None
-        try:
-            dp = data_path(cad, dev, B, H, W)
-        except Exception as e:
-            log(f"data-path measurement failed: {e}")
-        cpu = None
+        dp, extra, cpu, parity = None, None, None, None
+        del trainer, loss, model
+        torch.cuda.empty_cache()
+        if world == 1 and not args.no_extra:
+            extra = {}
+            for cfg in (3, 4):
+                if cfg == args.config:
+                    continue
+                try:
+                    extra[f"config{cfg}"] = extra_leg(cad, lib, dev, cfg)
+                    log(f"extra leg config {cfg}: {extra[f'config{cfg}']}")
+                except Exception as e:
+                    log(f"extra leg config {cfg} failed: {e}")
+            try:
+                dp = data_path(cad, dev, B, H, W)
+            except Exception as e:
+                log(f"data-path measurement failed: {e}")
         if world == 1 and not args.no_cpu_baseline:
             try:
-                cpu = cpu_baseline(args)
+                cpu, parity = cpu_baseline_and_parity(args, cad, dev, lib)
             except Exception as e:
                 log(f"cpu baseline failed: {e}")
         out = {
@@ -291,14 +389,15 @@ def main():
                        f"{args.model} train step, {args.dtype} GEMMs, bs{B}/GPU {H}x{W}, loss weights {args.weights}",
                        "model": args.model,
                        "global_batch": B * world, "height": H, "width": W, "init_features": f,
-                       "params": model.count_parameters(), "loss_weights": list(w),
+                       "params": params_count, "loss_weights": list(w),
                        "parallelism": f"dp{world}", "optimizer": "adam(lr1e-4,wd1e-5)+clip1.0"},
             "step_tflops_algorithmic": round(step_tflops, 3) if step_tflops else None,
             "last_loss": last_loss,
             "roofline": roof,
             "cpu_baseline": cpu,
+            "parity": parity,
+            "bf16_workloads": extra,
             "data_path": dp,
-            "parity": parity_evidence(),
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -7,8 +7,8 @@
 // (tensorboard_trainer_enhanced.h:287-304).
 //
 // Activation layout per level l (H_l = H >> l, C_l = f << l), NHWC fp32:
-//   enc/bottleneck: y1, y2 [M_l][C_l] (conv outputs pre-BN; a1 = relu(bn1(y1)) is applied inside
-//         conv2's operand loaders and never stored); output written straight into cat_l[:, 0:C_l]
+//   enc/bottleneck: y1, a1, y2 [M_l][C_l] (conv outputs pre-BN and a1 = relu(bn1(y1)) feeding
+//         conv2); output written straight into cat_l[:, 0:C_l]
 //   cat_l [M_l][2 C_l] = decoder concat buffer {skip | up} (baseline_unet.h:98, skip first) — the
 //         encoder writes the skip half, the ConvTranspose epilogue writes the up half: no cat/pad.
 //   pool_l [M_l][C_{l-1}] + uint8 argmax; dec: y1d, a1d, y2d, d_l [M_l][C_l].
@@ -146,10 +146,6 @@ struct cad_unet {
     int model = CAD_MODEL_BASELINE;
     int in_ch = 3, f = 64, Bmax = 1, H = 0, W = 0;
     int x0_ld = 4;               // NHWC4 rgb (baseline, film) or NHWC8 rgb+rays (ray_film)
-    // BN1-apply + ReLU fused into conv2's operand loaders instead of a materialised a1 (env
-    // CAD_FUSE_BN=1; measured slower on gfx950 — the extra per-stage coefficient loads cost the
-    // GEMMs more than the elementwise pass they remove — so off by default)
-    bool fuse_bn = false;
     float* camn = nullptr;       // normalised intrinsics (Bmax x 4) of the last forward
     float max_depth = 10.f;
     bool train = true;
@@ -174,8 +170,8 @@ struct cad_unet {
     float* a2_bott = nullptr;
     float* dout[4] = {};   // decoder outputs d_l
     float* sig = nullptr;
-    // pre-split operand twins (gemm_ps.hpp; sized for 3 planes): written after their producer when
-    // the GEMM engine splits (S3, B1), read by the pre-split GEMMs; fwd_np = planes of the last forward
+    // pre-split operand twins (gemm_ps.hpp, bf16): written by their producer on the B1 engine, read by
+    // the pre-split GEMMs; fwd_np = planes of the last forward (0: fp32 operands only)
     void* x0s = nullptr;          // RAY_FILM's NHWC8 input (8 channels)
     void* cats[4] = {};
     void* pools[5] = {};
@@ -184,17 +180,9 @@ struct cad_unet {
     void* dcats[4] = {};          // up half of dcat, [M_l][C_l]
     void* dYs = nullptr;          // split dL/dz scratch (largest level)
     int fwd_np = 0;
-    bool wsplit = false;          // S3 without pre-split activations: weights still pre-split (s3w kernels)
     // backward
     float* dcat[4] = {};
     float *Sa = nullptr, *Sb = nullptr, *Sc = nullptr;
-    float* Sd = nullptr;           // bn1's dL/dz while the side stream still reads bn2's (Sb)
-    void* dYs1 = nullptr;          // its split twin
-    // CAD_OVERLAP=1: weight-gradient GEMMs run on a second stream, overlapping the dgrad GEMMs and
-    // the HBM-bound BN / pooling backward passes of the same stage (joined at the end of every
-    // backward stage)
-    hipStream_t side = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     float* stats = nullptr;    // conv-epilogue BN partials
     double* dscr = nullptr;    // column-reduction scratch
     float* slab = nullptr;
@@ -328,7 +316,7 @@ void film_alloc(Arena& a, DoubleConv& dc, int B) {
 void layout(cad_unet* h, Arena& a) {
     const int B = h->Bmax;
     const bool film = h->model != CAD_MODEL_BASELINE;
-    // pre-split twin of `elems` fp32 values (3 bf16 planes: the S3 layout; B1 uses a third of it)
+    // pre-split (bf16) twin of `elems` fp32 values
     auto sp = [&](int64_t elems) -> void* { return a.take((size_t)elems * 2 * cad::kMaxPlanes); };
     auto conv_split_alloc = [&](Conv& c, bool dgrad) {
         if (c.cin % 8) return;   // enc1.conv1 of the 3-channel models: in-loader split
@@ -345,8 +333,8 @@ void layout(cad_unet* h, Arena& a) {
         bn_alloc(a, e.b1); bn_alloc(a, e.b2);
         const int64_t MC = h->Ml(l, B) * h->Cl(l);
         e.y1 = a.f(MC); e.y2 = a.f(MC);
-        if (film || !h->fuse_bn) e.a1 = a.f(MC);   // relu(bn1(y1)) (FiLM'd) feeding conv2
-        if (film || !h->fuse_bn) e.a1s = sp(MC);   // (not `if (e.a1)`: the sizing pass has null pointers)
+        e.a1 = a.f(MC);   // relu(bn1(y1)) (FiLM'd) feeding conv2
+        e.a1s = sp(MC);
         film_alloc(a, e, B);
         if (l > 0) e.c1.wd = a.f((int64_t)e.c1.cout * 9 * e.c1.cin);
         e.c2.wd = a.f((int64_t)e.c2.cout * 9 * e.c2.cin);
@@ -366,8 +354,8 @@ void layout(cad_unet* h, Arena& a) {
         bn_alloc(a, d.b1); bn_alloc(a, d.b2);
         const int64_t MC = h->Ml(l, B) * h->Cl(l);
         d.y1 = a.f(MC); d.y2 = a.f(MC);
-        if (film || !h->fuse_bn) d.a1 = a.f(MC);
-        if (film || !h->fuse_bn) d.a1s = sp(MC);   // (not `if (d.a1)`: the sizing pass has null pointers)
+        d.a1 = a.f(MC);
+        d.a1s = sp(MC);
         film_alloc(a, d, B);
         h->dout[l] = a.f(MC);
         if (l > 0) h->douts[l] = sp(MC);
@@ -389,8 +377,6 @@ void layout(cad_unet* h, Arena& a) {
     h->Sa = a.f(M0C0);
     h->Sb = a.f(M0C0);
     h->Sc = a.f(h->Ml(1, B) * h->Cl(0));
-    h->Sd = a.f(M0C0);
-    h->dYs1 = sp(M0C0);
     // BN tile partials: rows x 2C, max over layers
     int64_t st = 0, colmax = 0;
     for (int l = 0; l < 5; ++l) {
@@ -501,29 +487,20 @@ void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin,
     if (ps && in_s.p && dc.c1.ws)
         cad::conv3x3_fwd_ps(in_s, dc.c1.cin, sv(dc.c1.ws, 9 * dc.c1.cin), C, dc.y1, C, 0, B, Hh, Ww, stats, st);
     else
-        cad::conv3x3_fwd(in, ldin, 0, dc.c1.cin, h->P(dc.c1.pidx), C, dc.y1, C, 0, B, Hh, Ww, stats, st, nullptr,
-                         nullptr, h->wsplit ? dc.c1.ws : nullptr);
+        cad::conv3x3_fwd(in, ldin, 0, dc.c1.cin, h->P(dc.c1.pidx), C, dc.y1, C, 0, B, Hh, Ww, stats, st);
     bn(dc.b1);
-    if (dc.has_film() || !h->fuse_bn) {
-        if (dc.has_film()) {   // FiLMDoubleConvImpl::forward (intrinsics_unet.h:38-52)
-            cad::film_apply(dc.y1, C, dc.b1.scale, dc.b1.shift, dc.film.gam, dc.film.bet, B, (int64_t)Hh * Ww, dc.a1, st);
-            if (ps) cad::split_rows(dc.a1, C, 0, C, M, dc.a1s, C, 0, st);
-        } else {
-            // pre-split GEMMs read only a1's twin (conv2 and its weight gradient): the fp32 a1 is not written
-            cad::bn_relu_fwd(dc.y1, C, dc.b1.scale, dc.b1.shift, ps ? nullptr : dc.a1, C, 0, M, st, ps ? dc.a1s : nullptr,
-                             C, 0);
-        }
-        if (ps) {
-            cad::conv3x3_fwd_ps(sv(dc.a1s, C), C, sv(dc.c2.ws, 9 * C), C, dc.y2, C, 0, B, Hh, Ww, stats, st);
-        } else {
-            cad::conv3x3_fwd(dc.a1, C, 0, C, h->P(dc.c2.pidx), C, dc.y2, C, 0, B, Hh, Ww, stats, st, nullptr, nullptr,
-                             h->wsplit ? dc.c2.ws : nullptr);
-        }
+    if (dc.has_film()) {   // FiLMDoubleConvImpl::forward (intrinsics_unet.h:38-52)
+        cad::film_apply(dc.y1, C, dc.b1.scale, dc.b1.shift, dc.film.gam, dc.film.bet, B, (int64_t)Hh * Ww, dc.a1, st);
+        if (ps) cad::split_rows(dc.a1, C, 0, C, M, dc.a1s, C, 0, st);
     } else {
-        // a1 = relu(bn1(y1)) is never materialised: conv2's loader applies it (and so does conv2's wgrad)
-        cad::conv3x3_fwd(dc.y1, C, 0, C, h->P(dc.c2.pidx), C, dc.y2, C, 0, B, Hh, Ww, stats, st, dc.b1.scale,
-                         dc.b1.shift);
+        // pre-split GEMMs read only a1's twin (conv2 and its weight gradient): the fp32 a1 is not written
+        cad::bn_relu_fwd(dc.y1, C, dc.b1.scale, dc.b1.shift, ps ? nullptr : dc.a1, C, 0, M, st, ps ? dc.a1s : nullptr,
+                         C, 0);
     }
+    if (ps)
+        cad::conv3x3_fwd_ps(sv(dc.a1s, C), C, sv(dc.c2.ws, 9 * C), C, dc.y2, C, 0, B, Hh, Ww, stats, st);
+    else
+        cad::conv3x3_fwd(dc.a1, C, 0, C, h->P(dc.c2.pidx), C, dc.y2, C, 0, B, Hh, Ww, stats, st);
     bn(dc.b2);
     const bool twin = ps && out_s.p;
     cad::bn_relu_fwd(dc.y2, C, dc.b2.scale, dc.b2.shift, (out_f32 || !twin) ? out : nullptr, ldo, ocoff, M, st,
@@ -532,29 +509,14 @@ void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin,
 
 void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth, int B, hipStream_t st) {
     const int f = h->f;
-    // pre-split operands need every block's channel count (f * 2^l) to be a multiple of 8
-    // Pre-split operands by default on the bf16 engine only (measured on MI355X at bs32 480x640:
-    // B1 198 -> 277 img/s; S3 112 -> 101 img/s — its 6-byte split operands make the 128x128 GEMMs
-    // operand-bandwidth-bound at the rate the in-loader split reaches).  CAD_PS=0|1 overrides.
-    static const int ps_env = [] {
-        const char* e = std::getenv("CAD_PS");
-        return e ? std::atoi(e) : -1;
-    }();
-    const int np = cad::split_planes();
-    const bool ps_on = ps_env < 0 ? np == 1 : ps_env != 0;
-    h->fwd_np = (!ps_on || h->f % 8 || (h->fuse_bn && h->model == CAD_MODEL_BASELINE)) ? 0 : np;
-    // CAD_WSPLIT=1: the S3 engine stages pre-split weights (s3w kernels) and splits only the
-    // activations in its loaders — measured neutral on MI355X (180 vs 180 TFLOP/s: the S3 GEMMs run
-    // at ~1.6 GHz with the matrix pipe 68% busy, not bound by the split), so off by default
-    static const bool ws_env = [] {
-        const char* e = std::getenv("CAD_WSPLIT");
-        return e && e[0] == '1';
-    }();
-    h->wsplit = ws_env && h->fwd_np == 0 && np == 3 && h->f % 8 == 0;
+    // Pre-split operands on the bf16 engine (measured on MI355X at bs32 480x640: B1 198 -> 277
+    // img/s); every block's channel count (f * 2^l) must be a multiple of 8.  The S3 engine splits in
+    // its loaders (pre-split S3 operands are 6 bytes per element: measured 112 -> 101 img/s).
+    h->fwd_np = h->f % 8 ? 0 : cad::split_planes();
     const bool ps = h->fwd_np > 0;
     for (int l = 0; l < 4; ++l)
         cad::repack_convT_fwd(h->P(h->up[l].widx), h->up[l].wf, h->up[l].cin, h->up[l].cout, st);
-    if (ps || h->wsplit) split_weights(h, st);
+    if (ps) split_weights(h, st);
     if (h->model != CAD_MODEL_BASELINE) {
         // a14 normalisation, then every block's FiLM MLP (gamma/beta depend on the camera only)
         cad::camera_normalize(cam4, B, h->H, h->W, h->camn, st);
@@ -597,7 +559,7 @@ void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth
             cad::split_rows(h->cat[l], 2 * C, C, C, h->Ml(l, B), h->cats[l], 2 * C, C, st);
         } else {
             cad::convT_fwd(upin, u.cin, u.cin, u.wf, h->P(u.bidx), u.cout, h->cat[l], 2 * C, C, B, h->Hl(l + 1),
-                           h->Wl(l + 1), st, h->wsplit ? u.wfs : nullptr);
+                           h->Wl(l + 1), st);
         }
         double_conv_fwd(h, h->dec[l], h->cat[l], 2 * C, sv(h->cats[l], 2 * C), B, h->dout[l], C, 0,
                         l > 0 ? sv(h->douts[l], C) : none, st, l == 0);
@@ -610,57 +572,26 @@ void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth
 // ------------------------------------------------------------------------------------------
 // g: grad wrt the DoubleConv output (ld ldg, channel offset gcoff); in: the block input (ld ldin,
 // cin channels; in_s its split twin); din: where conv1's dgrad goes (nullptr = not needed), ld lddin.
-// side-stream fork / join (no-ops without a side stream)
-void fork_side(cad_unet* h, hipStream_t st) {
-    if (!h->side) return;
-    HIPCHK(hipEventRecord(h->ev_fork, st));
-    HIPCHK(hipStreamWaitEvent(h->side, h->ev_fork, 0));
-}
-void join_side(cad_unet* h, hipStream_t st) {
-    if (!h->side) return;
-    HIPCHK(hipEventRecord(h->ev_join, h->side));
-    HIPCHK(hipStreamWaitEvent(st, h->ev_join, 0));
-}
-
-// pool: the max-pool gradient of the next level, still to be routed into g (folded into bn2's backward)
 void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, int gcoff, const float* in,
-                     int64_t ldin, cad::Split in_s, int B, float* din, int64_t lddin, hipStream_t st,
-                     cad::PoolGrad pool = cad::PoolGrad{}) {
+                     int64_t ldin, cad::Split in_s, int B, float* din, int64_t lddin, hipStream_t st) {
     const int l = dc.level, Hh = h->Hl(l), Ww = h->Wl(l), C = dc.c1.cout;
     const int64_t M = h->Ml(l, B);
     const bool ps = h->fwd_np > 0 && h->fwd_np == cad::split_planes();
-    const hipStream_t ws = h->side ? h->side : st;   // weight-gradient stream
-    float* dY2 = h->Sb;
-    float* dY1 = h->side ? h->Sd : h->Sb;
-    void* dYs2 = h->dYs;
-    void* dYs1 = h->side ? h->dYs1 : h->dYs;
+    float* dY = h->Sb;
+    void* dYs = h->dYs;
     float* dA1 = h->Sa;
     // bn2 + relu
     // with pre-split GEMMs both consumers of dY2 read its twin: the fp32 dY2 is not written
     cad::bn_relu_bwd(g, ldg, gcoff, dc.y2, C, dc.b2.mean, dc.b2.invstd, dc.b2.scale, dc.b2.shift, h->P(dc.b2.widx), M,
-                     h->dscr, dc.b2.coef, h->G(dc.b2.widx), h->G(dc.b2.bidx), ps ? nullptr : dY2, st, nullptr, 1,
-                     ps ? dYs2 : nullptr, nullptr, 0, pool);
-    fork_side(h, st);
-    // CAD_BNB=1: bn1's (Σ dz, Σ dz·x̂) come out of conv2's dgrad epilogue as tile partials (no FiLM
-    // between the ReLU and conv2; not on the in-loader S3 pre-split-weight kernels).  Off by default:
-    // measured on MI355X the epilogue's extra y reads cost the dgrad GEMMs more (+4 ms fp32, +7 ms bf16
-    // per step) than the skipped reduction pass saves (~3.8 ms)
-    static const bool bnb_on = std::getenv("CAD_BNB") && std::getenv("CAD_BNB")[0] == '1';
-    const bool bnb = bnb_on && !dc.has_film() && (ps || !h->wsplit);
-    const cad::BnBwdEpi bn1{dc.y1, dc.b1.mean, dc.b1.invstd, dc.b1.scale, dc.b1.shift, h->stats};
-    const int bn_rows = cad::conv3x3_stats_rows(B, Hh, Ww, C);
-    // conv2: wgrad (side) || dgrad (caller's stream)
+                     h->dscr, dc.b2.coef, h->G(dc.b2.widx), h->G(dc.b2.bidx), ps ? nullptr : dY, st, nullptr, 1,
+                     ps ? dYs : nullptr);
+    // conv2: wgrad, dgrad
     if (ps) {
-        cad::conv3x3_wgrad_ps(sv(dYs2, C), C, sv(dc.a1s, C), C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, ws);
-        cad::conv3x3_dgrad_ps(sv(dYs2, C), C, sv(dc.c2.wds, 9 * C), C, dA1, C, B, Hh, Ww, st, bnb ? &bn1 : nullptr);
+        cad::conv3x3_wgrad_ps(sv(dYs, C), C, sv(dc.a1s, C), C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
+        cad::conv3x3_dgrad_ps(sv(dYs, C), C, sv(dc.c2.wds, 9 * C), C, dA1, C, B, Hh, Ww, st);
     } else {
-        if (dc.a1)
-            cad::conv3x3_wgrad(dY2, C, dc.a1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, ws);
-        else
-            cad::conv3x3_wgrad(dY2, C, dc.y1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, ws,
-                               dc.b1.scale, dc.b1.shift);
-        cad::conv3x3_dgrad(dY2, C, dc.c2.wd, C, dA1, C, B, Hh, Ww, st, h->wsplit ? dc.c2.wds : nullptr,
-                           bnb ? &bn1 : nullptr);
+        cad::conv3x3_wgrad(dY, C, dc.a1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
+        cad::conv3x3_dgrad(dY, C, dc.c2.wd, C, dA1, C, B, Hh, Ww, st);
     }
     // FiLM: dgamma/dbeta per (sample, channel); the ReLU sees dA1 * gamma (folded into bn_relu_bwd)
     const int64_t HW = (int64_t)Hh * Ww;
@@ -671,21 +602,19 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     const bool ps1 = ps && in_s.p && dc.c1.ws;
     const bool dy1_f32 = !ps1 || (din && !(ps && dc.c1.wds));
     cad::bn_relu_bwd(dA1, C, 0, dc.y1, C, dc.b1.mean, dc.b1.invstd, dc.b1.scale, dc.b1.shift, h->P(dc.b1.widx), M,
-                     h->dscr, dc.b1.coef, h->G(dc.b1.widx), h->G(dc.b1.bidx), dy1_f32 ? dY1 : nullptr, st,
-                     dc.has_film() ? dc.film.gam : nullptr, HW, ps ? dYs1 : nullptr, bnb ? h->stats : nullptr,
-                     bn_rows);
+                     h->dscr, dc.b1.coef, h->G(dc.b1.widx), h->G(dc.b1.bidx), dy1_f32 ? dY : nullptr, st,
+                     dc.has_film() ? dc.film.gam : nullptr, HW, ps ? dYs : nullptr);
     if (dc.has_film()) cad::film_mlp_bwd(film_view(h, dc), h->camn, B, st);
-    fork_side(h, st);
-    // conv1: wgrad (side) || dgrad (caller's stream)
+    // conv1: wgrad, dgrad
     if (ps1)
-        cad::conv3x3_wgrad_ps(sv(dYs1, C), C, in_s, dc.c1.cin, h->G(dc.c1.pidx), B, Hh, Ww, h->slab, h->slab_cap, ws);
+        cad::conv3x3_wgrad_ps(sv(dYs, C), C, in_s, dc.c1.cin, h->G(dc.c1.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
     else
-        cad::conv3x3_wgrad(dY1, C, in, ldin, 0, dc.c1.cin, h->G(dc.c1.pidx), B, Hh, Ww, h->slab, h->slab_cap, ws);
+        cad::conv3x3_wgrad(dY, C, in, ldin, 0, dc.c1.cin, h->G(dc.c1.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
     if (din) {
         if (ps && dc.c1.wds)
-            cad::conv3x3_dgrad_ps(sv(dYs1, C), C, sv(dc.c1.wds, 9 * C), dc.c1.cin, din, lddin, B, Hh, Ww, st);
+            cad::conv3x3_dgrad_ps(sv(dYs, C), C, sv(dc.c1.wds, 9 * C), dc.c1.cin, din, lddin, B, Hh, Ww, st);
         else
-            cad::conv3x3_dgrad(dY1, C, dc.c1.wd, dc.c1.cin, din, lddin, B, Hh, Ww, st, h->wsplit ? dc.c1.wds : nullptr);
+            cad::conv3x3_dgrad(dY, C, dc.c1.wd, dc.c1.cin, din, lddin, B, Hh, Ww, st);
     }
 }
 
@@ -693,7 +622,7 @@ void repack_dgrad_weights(cad_unet* h, hipStream_t st) {
     const bool ps = h->fwd_np > 0 && h->fwd_np == cad::split_planes();
     auto rp = [&](Conv& c) {   // dgrad repack [ci][tap][co]: rows cin, K = 9*cout
         cad::repack_conv_dgrad(h->P(c.pidx), c.wd, c.cout, c.cin, st);
-        if ((ps || h->wsplit) && c.wds) cad::split_rows(c.wd, 9 * c.cout, 0, 9 * c.cout, c.cin, c.wds, 9 * c.cout, 0, st);
+        if (ps && c.wds) cad::split_rows(c.wd, 9 * c.cout, 0, 9 * c.cout, c.cin, c.wds, 9 * c.cout, 0, st);
     };
     for (int l = 0; l < 5; ++l) {
         if (l > 0) rp(h->enc[l].c1);
@@ -703,7 +632,7 @@ void repack_dgrad_weights(cad_unet* h, hipStream_t st) {
         rp(h->dec[l].c1);
         rp(h->dec[l].c2);
         const Up& u = h->up[l];   // ConvT weights [ci][q][co]: rows cin, K = 4*cout
-        if (ps || h->wsplit) cad::split_rows(h->P(u.widx), 4 * u.cout, 0, 4 * u.cout, u.cin, u.wms, 4 * u.cout, 0, st);
+        if (ps) cad::split_rows(h->P(u.widx), 4 * u.cout, 0, 4 * u.cout, u.cin, u.wms, 4 * u.cout, 0, st);
     }
 }
 
@@ -727,16 +656,14 @@ void backward_stage(cad_unet* h, int stage, const float* dpred, hipStream_t st) 
         const Up& u = h->up[l];
         const float* upin = l == 3 ? h->a2_bott : h->dout[l + 1];
         const void* upins = l == 3 ? h->botts : h->douts[l + 1];
-        const hipStream_t ws = h->side ? h->side : st;
-        // up (ConvTranspose2d) backward: grad of its output = dcat[:, C:2C]; wgrad on the side stream
+        // up (ConvTranspose2d) backward: grad of its output = dcat[:, C:2C]
         if (ps) cad::split_rows(h->dcat[l], 2 * C, C, C, h->Ml(l, B), h->dcats[l], C, 0, st);
-        fork_side(h, st);
         if (ps) {
             cad::convT_wgrad_ps(sv(upins, u.cin), u.cin, sv(h->dcats[l], C), u.cout, h->G(u.widx), B, h->Hl(l + 1),
-                                h->Wl(l + 1), h->slab, h->slab_cap, ws);
+                                h->Wl(l + 1), h->slab, h->slab_cap, st);
         } else {
             cad::convT_wgrad(upin, u.cin, h->dcat[l], 2 * C, C, u.cout, h->G(u.widx), B, h->Hl(l + 1), h->Wl(l + 1),
-                             h->slab, h->slab_cap, ws);
+                             h->slab, h->slab_cap, st);
         }
         cad::colsum(h->dcat[l], 2 * C, C, h->Ml(l, B), C, h->dscr, st);
         cad::colsum_finalize(h->dscr, cad::colsum_slices(h->Ml(l, B)), C, h->G(u.bidx), 1.f, st);
@@ -744,9 +671,7 @@ void backward_stage(cad_unet* h, int stage, const float* dpred, hipStream_t st) 
             cad::convT_dgrad_ps(sv(h->dcats[l], C), u.cout, sv(u.wms, 4 * u.cout), u.cin, h->Sa, B, h->Hl(l + 1),
                                 h->Wl(l + 1), st);
         else
-            cad::convT_dgrad(h->dcat[l], 2 * C, C, u.cout, h->P(u.widx), u.cin, h->Sa, B, h->Hl(l + 1), h->Wl(l + 1), st,
-                             h->wsplit ? u.wms : nullptr);
-        join_side(h, st);   // the stage's gradients are complete on the caller's stream
+            cad::convT_dgrad(h->dcat[l], 2 * C, C, u.cout, h->P(u.widx), u.cin, h->Sa, B, h->Hl(l + 1), h->Wl(l + 1), st);
         return;
     }
     // encoder side: stage 5 = bottleneck (level 4), 6..9 = enc4..enc1 (levels 3..0)
@@ -755,22 +680,14 @@ void backward_stage(cad_unet* h, int stage, const float* dpred, hipStream_t st) 
     const int C = h->Cl(l);
     const float* g = l == 4 ? h->Sa : h->dcat[l];
     const int64_t ldg = l == 4 ? C : 2 * C;
-    // CAD_POOLFOLD=1: the max-pool backward of level l+1 (its gradient in Sc) is folded into this
-    // block's bn2 backward passes instead of a read-modify-write pass over dcat's skip half.  Off by
-    // default: measured on MI355X the gather in both BN-backward passes costs 0.3-0.6 % more than the
-    // pass it removes
-    static const bool fold = std::getenv("CAD_POOLFOLD") && std::getenv("CAD_POOLFOLD")[0] == '1';
-    const cad::PoolGrad pool =
-        fold && l < 4 ? cad::PoolGrad{h->Sc, h->pidx[l + 1], h->Hl(l), h->Wl(l)} : cad::PoolGrad{};
     if (l == 0) {
-        double_conv_bwd(h, e, g, ldg, 0, h->x0, h->x0_ld, sv(h->x0s, h->x0_ld), B, nullptr, 0, st, pool);
-        join_side(h, st);
+        double_conv_bwd(h, e, g, ldg, 0, h->x0, h->x0_ld, sv(h->x0s, h->x0_ld), B, nullptr, 0, st);
         return;
     }
     const int Cp = h->Cl(l - 1);
-    double_conv_bwd(h, e, g, ldg, 0, h->pool[l], Cp, sv(h->pools[l], Cp), B, h->Sc, Cp, st, pool);
-    if (!fold) cad::maxpool_bwd(h->Sc, h->pidx[l], Cp, B, h->Hl(l - 1), h->Wl(l - 1), h->dcat[l - 1], 2 * Cp, st);
-    join_side(h, st);
+    double_conv_bwd(h, e, g, ldg, 0, h->pool[l], Cp, sv(h->pools[l], Cp), B, h->Sc, Cp, st);
+    // max-pool backward: the pooled gradient is added at the recorded argmax of dcat's skip half
+    cad::maxpool_bwd(h->Sc, h->pidx[l], Cp, B, h->Hl(l - 1), h->Wl(l - 1), h->dcat[l - 1], 2 * Cp, st);
 }
 
 void compute_stage_ranges(cad_unet* h) {
@@ -925,8 +842,6 @@ cad_status cad_unet_create_model(const cad_unet_desc* d, int model, int device, 
         h->device = device;
         h->model = model;
         h->x0_ld = model == CAD_MODEL_RAY_FILM ? 8 : 4;
-        const char* fb = std::getenv("CAD_FUSE_BN");
-        h->fuse_bn = fb && fb[0] == '1';
         h->in_ch = d->in_channels;
         h->f = d->init_features;
         h->max_depth = d->max_depth;
@@ -944,15 +859,6 @@ cad_status cad_unet_create_model(const cad_unet_desc* d, int model, int device, 
         real.base = static_cast<char*>(base);
         layout(h.get(), real);
         require(real.off == sz.off, "internal: arena layout differs between the sizing and the real pass", CAD_ERR_STATE);
-        // off by default: measured +1 % on MI355X (the S3 GEMMs hold the chip at its power limit,
-        // the B1 ones at its memory latency), and concurrent kernels blur the per-launch HIP-event
-        // timing bench.py reports as roofline.achieved
-        const char* ov = std::getenv("CAD_OVERLAP");
-        if (ov && ov[0] == '1') {
-            HIPCHK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
-            HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
-            HIPCHK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
-        }
         compute_stage_ranges(h.get());
         default_init(h.get());
         HIPCHK(hipDeviceSynchronize());
@@ -963,12 +869,6 @@ cad_status cad_unet_create_model(const cad_unet_desc* d, int model, int device, 
 void cad_unet_destroy(cad_unet* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
-    if (h->side) {
-        (void)hipStreamSynchronize(h->side);
-        (void)hipStreamDestroy(h->side);
-        (void)hipEventDestroy(h->ev_fork);
-        (void)hipEventDestroy(h->ev_join);
-    }
     (void)hipFree(h->arena_base);
     delete h;
 }
@@ -1090,7 +990,22 @@ int64_t cad_unet_debug_buffer(cad_unet* h, const char* name, float* host, int64_
         }
     }
     else if (n == "camn") { p = h->camn; cnt = (int64_t)B * 4; }
-    if (!p || cnt < 0) return -1;
+    if (!p || cnt < 0) {
+        g_err = "unknown debug buffer '" + n + "'";
+        return -1;
+    }
+    // With pre-split operands (bf16 engine) the last forward/backward wrote only the bf16 twins of
+    // these buffers: their fp32 copies are stale, so refuse them rather than return old data
+    if (h->fwd_np > 0) {
+        const bool film = h->model != CAD_MODEL_BASELINE;
+        const bool twin_only = n == "Sb" || n == "bott" || (n.compare(0, 4, "pool") == 0) ||
+                               (n.compare(0, 4, "dout") == 0 && n != "dout0") ||
+                               (!film && n.size() > 5 && n.substr(5) == "a1");
+        if (twin_only) {
+            g_err = "debug buffer '" + n + "' holds no fp32 copy on the pre-split (bf16) engine";
+            return -1;
+        }
+    }
     if (host) {
         if (numel < cnt) return -1;
         if (hipDeviceSynchronize() != hipSuccess) return -1;

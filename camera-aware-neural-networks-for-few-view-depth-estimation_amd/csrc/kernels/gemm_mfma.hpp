@@ -31,9 +31,6 @@ namespace cad {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-#ifndef CAD_XCD_SWIZZLE
-#define CAD_XCD_SWIZZLE 1
-#endif
 // K-stage geometry for stage depth KB (16 or 32)
 template <int KB>
 struct KS {
@@ -57,25 +54,14 @@ struct GemmArgs {
     float* C; int64_t ldc; int c_coff;
     const float* bias;
     float* stats;         // BN partials [gridDim.x][2][N]  (sum, sumsq) or nullptr
-    // fused BatchNorm-apply + ReLU on a gathered operand: x -> max(0, x*sc[c] + sh[c]) (in-image only)
-    const float *a_sc, *a_sh, *b_sc, *b_sh;
     int kstages_per_split;
     int64_t slab_stride;  // elements between split-K slabs
     // conv3x3 forward/dgrad on pre-split operands: K stages in channel-major order (stage s = tap
     // s % 9 of channel block s / 9, KB channels per block) instead of tap-major, so the nine taps of
     // a channel block re-read the same input rows back to back (L2 hits) — needs cin % KB == 0
     int cimajor;
-    int conv_cin;         // cin of that contraction (the B loader walks the same (tap, ci) order)
-    // BN-backward partials in a dgrad epilogue (EpiStoreBnBwd): the pre-BN activation y [M][N] and
-    // the BatchNorm's per-channel mean, invstd, scale, shift of the ReLU(BN(y)) this output feeds
-    const float *e_y, *e_mean, *e_invstd, *e_scale, *e_shift;
 };
 
-__device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
-__device__ __forceinline__ float4 bn_relu4(float4 v, float4 s, float4 h) {
-    return make_float4(fmaxf(v.x * s.x + h.x, 0.f), fmaxf(v.y * s.y + h.y, 0.f), fmaxf(v.z * s.z + h.z, 0.f),
-                       fmaxf(v.w * s.w + h.w, 0.f));
-}
 
 // --------------------------------------------------------------------------------------------
 // Operand fetch: buffer loads against a per-workgroup base.  Every loader builds ONE buffer
@@ -149,26 +135,19 @@ __device__ __forceinline__ void tapci_advance(int& tap, int& ci, int cin) {
 }
 
 // op(pix, k=(tap,ci)) = X[(b, y+ky-1, x+kx-1)*ld + coff + ci], zero outside the image.
-// BNR: X is a pre-BatchNorm conv output; relu(x*sc[ci] + sh[ci]) is applied to in-image elements
-// in finish(), i.e. when the stage is written to LDS after the MFMAs of the previous stage, so the
-// transform never stalls on the global loads it depends on.
-template <int ROWS, int KB, bool BNR = false>
+template <int ROWS, int KB>
 struct KcIm2col3x3 {
     using G = KS<KB>;
     static constexpr int NV = ROWS / G::RPP;
     __amdgpu_buffer_rsrc_t rs;
-    const float *sc, *sh;
-    float4 s4, h4;     // BNR: coefficients of the loaded stage
-    bool gm[NV];       // BNR: in-image mask of the loaded stage
     int ld4;           // row stride in bytes
     uint32_t poff[NV]; // byte offset of the thread's pixel from the block base
     int y[NV], x[NV];
     bool ok[NV];
     int H, W, cin, tap, ci;
     __device__ void init(const float* P, int64_t ld_, int coff, int cin_, int B, int H_, int W_,
-                         int row0, int tid, int kbeg, const float* sc_ = nullptr, const float* sh_ = nullptr) {
+                         int row0, int tid, int kbeg) {
         H = H_; W = W_; cin = cin_; ld4 = (int)ld_ * 4;
-        sc = sc_; sh = sh_;
         const int pb = max(row0 - W_ - 1, 0);   // first pixel of the block's halo window
         rs = make_rsrc(P + (int64_t)pb * ld_ + coff);
         const int k = kbeg * KB + (tid % G::TPR) * 4;
@@ -190,25 +169,15 @@ struct KcIm2col3x3 {
         const int t = kin ? tap : 0;
         const int dy = t / 3 - 1, dx = t - 3 * (t / 3) - 1;
         const int off = (dy * W + dx) * ld4 + ci * 4;
-        if constexpr (BNR) {
-            s4 = *reinterpret_cast<const float4*>(sc + ci);
-            h4 = *reinterpret_cast<const float4*>(sh + ci);
-        }
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             const int yy = y[j] + dy, xx = x[j] + dx;
             const bool g = ok[j] && kin && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
-            if constexpr (BNR) gm[j] = g;
             v[j] = bload4(rs, g ? poff[j] + (uint32_t)off : kOOB);
         }
         tapci_advance<KB>(tap, ci, cin);
     }
-    __device__ void finish(float4 (&v)[NV]) {
-        if constexpr (BNR) {
-#pragma unroll
-            for (int j = 0; j < NV; ++j) v[j] = gm[j] ? bn_relu4(v[j], s4, h4) : f4zero();
-        }
-    }
+    __device__ void finish(float4 (&)[NV]) {}
 };
 
 // op(lowres pix (b,y,x), k=(q=(dy,dx), co)) = G[(b, 2y+dy, 2x+dx)*ld + coff + co]
@@ -302,20 +271,18 @@ struct MNcDense : MNcBase<ROWS, KB> {   // op(r, k) = P[k*ld + coff + r], r < nr
     __device__ void finish(float4 (&)[NV]) {}
 };
 
-// op(j=(tap,ci), k=pix) = X[(b,y+ky-1,x+kx-1)*ld + coff + ci]   (BNR: relu(x*sc+sh) in-image)
-template <int ROWS, int KB, bool BNR = false>
+// op(j=(tap,ci), k=pix) = X[(b,y+ky-1,x+kx-1)*ld + coff + ci]
+template <int ROWS, int KB>
 struct MNcIm2col3x3 : MNcBase<ROWS, KB> {
     using Base = MNcBase<ROWS, KB>;
     static constexpr int NV = Base::NV;
     __amdgpu_buffer_rsrc_t rs;
-    float4 s4, h4;
-    bool gm[NV];       // BNR: in-image mask of the loaded stage (transform deferred to finish())
     int ld4, H, W, Kp, dy, dx, pb;
     int tapoff;        // byte offset of the thread's (tap, ci) relative to its pixel
     int k[NV], x[NV], y[NV];
     bool rok;
     __device__ void init(const float* P, int64_t ld_, int coff, int cin, int B, int H_, int W_,
-                         int row0, int tid, int kbeg, const float* sc = nullptr, const float* sh = nullptr) {
+                         int row0, int tid, int kbeg) {
         ld4 = (int)ld_ * 4; H = H_; W = W_; Kp = B * H_ * W_;
         const int j = row0 + (tid % Base::TPR) * 4;
         rok = j < 9 * cin;
@@ -325,10 +292,6 @@ struct MNcIm2col3x3 : MNcBase<ROWS, KB> {
         pb = max(kbeg * KB - W_ - 1, 0);
         rs = make_rsrc(P + (int64_t)pb * ld_ + coff);
         tapoff = (dy * W + dx) * ld4 + ci * 4;
-        if constexpr (BNR) {
-            s4 = *reinterpret_cast<const float4*>(sc + ci);
-            h4 = *reinterpret_cast<const float4*>(sh + ci);
-        }
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
             k[i] = kbeg * KB + tid / Base::TPR + Base::KSTEP * i;
@@ -342,19 +305,13 @@ struct MNcIm2col3x3 : MNcBase<ROWS, KB> {
         for (int j = 0; j < NV; ++j) {
             const int yy = y[j] + dy, xx = x[j] + dx;
             const bool g = rok && k[j] < Kp && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
-            if constexpr (BNR) gm[j] = g;
             v[j] = bload4(rs, g ? (uint32_t)((k[j] - pb) * ld4 + tapoff) : kOOB);
             int b = 0;
             px_advance<KB>(x[j], y[j], b, W, H);
             k[j] += KB;
         }
     }
-    __device__ void finish(float4 (&v)[NV]) {
-        if constexpr (BNR) {
-#pragma unroll
-            for (int j = 0; j < NV; ++j) v[j] = gm[j] ? bn_relu4(v[j], s4, h4) : f4zero();
-        }
-    }
+    __device__ void finish(float4 (&)[NV]) {}
 };
 
 // op(j=(q,co), k=lowres pix (b,y,x)) = G[(b,2y+dy,2x+dx)*ld + coff + co]
@@ -456,11 +413,6 @@ struct OpLds {
 // plus static constexpr bool STATS (per-column BN partial sums written to a.stats).
 // blockIdx.x -> M tile, blockIdx.y -> N tile, blockIdx.z -> split-K slice.
 // --------------------------------------------------------------------------------------------
-// epilogues declaring BNBWD accumulate BN-backward partials (Σ dz, Σ dz·x̂) instead of (Σ v, Σ v²)
-template <class E, class = void>
-struct is_bnbwd : std::false_type {};
-template <class E>
-struct is_bnbwd<E, std::void_t<decltype(E::BNBWD)>> : std::integral_constant<bool, E::BNBWD> {};
 template <class E, class = void>
 struct is_structured : std::false_type {};
 template <class E>
@@ -478,7 +430,7 @@ __device__ __forceinline__ TileId xcd_tile() {
     const int nwg = nx * ny * gridDim.z;
     const int L = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
     int logical = L;
-    if (CAD_XCD_SWIZZLE && nwg > 8) {
+    if (nwg > 8) {
         const int q = nwg / 8, r = nwg % 8, xcd = L % 8;
         logical = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
     }
@@ -492,11 +444,7 @@ __device__ __forceinline__ TileId xcd_tile() {
 // A wave whose sub-tile lies entirely past M or N (in the tail tile of a dimension that is not a
 // multiple of the tile: e.g. the 576 = 2.25 x 256 columns of a 64-channel weight gradient) skips its
 // MFMAs, leaving the SIMD to co-resident waves; it still stages operands and joins every barrier.
-#ifndef CAD_WAVE_SKIP
-#define CAD_WAVE_SKIP 1
-#endif
 __device__ __forceinline__ bool wave_live(const GemmArgs& a, int m0, int n0, int wrows, int wcols) {
-    if constexpr (!CAD_WAVE_SKIP) return true;
     return m0 + wrows < a.M && n0 + wcols < a.N;
 }
 
@@ -507,38 +455,22 @@ __device__ __forceinline__ const float* epi_row_base(const GemmArgs& a, int m0, 
 }
 
 // Epilogue shared by the engines.  Each wave owns MI x NJ blocks of 32x32: a (32 MI) x (32 NJ)
-// sub-tile; the tile is WM x WN waves.  A block's 16 accumulator values per lane are visited as four
-// "quads" of 4 consecutive rows at one column:
-//   32x32 MFMA layout (acc: floatx16 [MI][NJ]): quad g = registers 4g..4g+3, rows 4(lane>>5) + 8g,
-//     column lane & 31;
-//   16x16 MFMA layout (acc: floatx4 [2MI][2NJ], the four 16x16 sub-blocks s = (s>>1, s&1) of a
-//     block): quad s = sub-block s, rows 16(s>>1) + 4(lane>>4), column 16(s&1) + (lane&15).
-// `lds` is free scratch (the main loop ended on a barrier).
-template <int MI, int NJ>
-__device__ __forceinline__ void epi_quad(const floatx16 (&acc)[MI][NJ], int i, int j, int g, float (&v)[4]) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = acc[i][j][4 * g + r];
-}
-template <int MI, int NJ>
-__device__ __forceinline__ void epi_quad(const floatx4 (&acc)[2 * MI][2 * NJ], int i, int j, int g, float (&v)[4]) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = acc[2 * i + (g >> 1)][2 * j + (g & 1)][r];
-}
-
-template <int WM, int WN, int MI, int NJ, class Epi, class Acc>
-__device__ __forceinline__ void gemm_epilogue_t(const GemmArgs& a, const Acc& acc, const TileId& tile, float* lds,
-                                                Epi epi) {
-    constexpr bool S16 = std::is_same<std::remove_cv_t<std::remove_all_extents_t<Acc>>, floatx4>::value;
+// sub-tile; the tile is WM x WN waves.  A block's 16 accumulator values per lane (32x32 MFMA layout)
+// are visited as four "quads" of 4 consecutive rows at one column: quad g = registers 4g..4g+3, rows
+// 4(lane>>5) + 8g, column lane & 31.  `lds` is free scratch (the main loop ended on a barrier).
+template <int WM, int WN, int MI, int NJ, class Epi>
+__device__ __forceinline__ void gemm_epilogue_t(const GemmArgs& a, const floatx16 (&acc)[MI][NJ], const TileId& tile,
+                                                float* lds, Epi epi) {
     constexpr int BM = 32 * MI * WM, BN = 32 * NJ * WN;
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
     const int wm = wave / WN, wn = wave % WN;
     const int m0 = tile.x * BM, n0 = tile.y * BN;
     // With STATS the per-column BN partials are accumulated in the same pass (each accumulator is read once: keeping them live
-    // for a second pass costs 64 VGPRs and an occupancy step).  ssum[j][slot]: the lane's column(s) of block column j.
-    float ssum[NJ][2], ssq[NJ][2];
+    // for a second pass costs 64 VGPRs and an occupancy step).  ssum[j]: the lane's column of block column j.
+    float ssum[NJ], ssq[NJ];
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) ssum[j][0] = ssq[j][0] = ssum[j][1] = ssq[j][1] = 0.f;
+    for (int j = 0; j < NJ; ++j) ssum[j] = ssq[j] = 0.f;
     // Row-major epilogues (EpiStore, EpiSlab) store through a buffer descriptor based at the tile's
     // first output row whose range ends at row M: rows past M are dropped by the range check and
     // columns past N get an out-of-range offset, so each store is one 32-bit offset add.
@@ -550,51 +482,26 @@ __device__ __forceinline__ void gemm_epilogue_t(const GemmArgs& a, const Acc& ac
     for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-            if constexpr (is_structured<Epi>::value && !S16) {
+            if constexpr (is_structured<Epi>::value) {
                 static_assert(!Epi::STATS, "structured epilogues carry no BN partials");
                 epi.block(a, m0 + wm * 32 * MI + i * 32 + 4 * (lane >> 5), n0 + wn * 32 * NJ + j * 32 + (lane & 31),
                           acc[i][j]);
                 continue;
-            }
+            } else {
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int slot = S16 ? (g & 1) : 0;
-                const int cw = S16 ? j * 32 + 16 * (g & 1) + (lane & 15) : j * 32 + (lane & 31);
-                const int rw = S16 ? i * 32 + 16 * (g >> 1) + 4 * (lane >> 4) : i * 32 + 4 * (lane >> 5) + 8 * g;
-                const int n = n0 + wn * 32 * NJ + cw;
-                const int mr = wm * 32 * MI + rw;   // tile-relative row of the quad's first register
-                float v[4];
-                epi_quad<MI, NJ>(acc, i, j, g, v);
-                if constexpr (is_structured<Epi>::value) {
-                    static_assert(!Epi::STATS, "structured epilogues carry no BN partials");
-                    epi.quad(a, m0 + mr, n, v);
-                } else {
+                for (int g = 0; g < 4; ++g) {
+                    const int n = n0 + wn * 32 * NJ + j * 32 + (lane & 31);
+                    const int mr = wm * 32 * MI + i * 32 + 4 * (lane >> 5) + 8 * g;   // tile-relative row
                     const uint32_t lo = n < a.N ? (uint32_t)(mr * ldc4 + (int64_t)n * 4) : kOOB;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[r]), rs,
+                        const float v = acc[i][j][4 * g + r];
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rs,
                                                               lo + (uint32_t)(r * ldc4), 0, 0);
-                        if constexpr (Epi::STATS && !is_bnbwd<Epi>::value) {
-                            const float vm = m0 + mr + r < a.M ? v[r] : 0.f;
-                            ssum[j][slot] += vm;
-                            ssq[j][slot] += vm * vm;
-                        }
-                    }
-                    if constexpr (is_bnbwd<Epi>::value) {
-                        // v = dL/d relu(bn(y)): Σ dz and Σ dz·x̂ with dz = v·[y·scale + shift > 0]
-                        // (the same test and x̂ as k_bn_relu_bwd), x̂ = (y − mean)·invstd
-                        if (n < a.N) {
-                            const float sc = a.e_scale[n], sh = a.e_shift[n], mu = a.e_mean[n], is = a.e_invstd[n];
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) {
-                                const int m = m0 + mr + r;
-                                if (m < a.M) {
-                                    const float y = a.e_y[(int64_t)m * a.N + n];
-                                    const float dz = y * sc + sh > 0.f ? v[r] : 0.f;
-                                    ssum[j][slot] += dz;
-                                    ssq[j][slot] += dz * ((y - mu) * is);
-                                }
-                            }
+                        if constexpr (Epi::STATS) {
+                            const float vm = m0 + mr + r < a.M ? v : 0.f;
+                            ssum[j] += vm;
+                            ssq[j] += vm * vm;
                         }
                     }
                 }
@@ -606,22 +513,16 @@ __device__ __forceinline__ void gemm_epilogue_t(const GemmArgs& a, const Acc& ac
         // the main loop ended on a barrier, so the LDS operand buffers are free for the reduction
         float* red = lds;   // [WM][BN][2]
 #pragma unroll
-        for (int j = 0; j < NJ; ++j)
-#pragma unroll
-            for (int slot = 0; slot < (S16 ? 2 : 1); ++slot) {
-                float s = ssum[j][slot], q = ssq[j][slot];
-                if constexpr (S16) {   // lanes sharing a column: lane & 15 equal
-                    s += __shfl_xor(s, 16);
-                    q += __shfl_xor(q, 16);
-                }
-                s += __shfl_xor(s, 32);
-                q += __shfl_xor(q, 32);
-                if (S16 ? lane < 16 : lane < 32) {
-                    const int cl = wn * 32 * NJ + j * 32 + (S16 ? 16 * slot + lane : lane);
-                    red[(wm * BN + cl) * 2 + 0] = s;
-                    red[(wm * BN + cl) * 2 + 1] = q;
-                }
+        for (int j = 0; j < NJ; ++j) {
+            float s = ssum[j], q = ssq[j];
+            s += __shfl_xor(s, 32);
+            q += __shfl_xor(q, 32);
+            if (lane < 32) {
+                const int cl = wn * 32 * NJ + j * 32 + lane;
+                red[(wm * BN + cl) * 2 + 0] = s;
+                red[(wm * BN + cl) * 2 + 1] = q;
             }
+        }
         __syncthreads();
         for (int c = tid; c < BN; c += 256) {
             float s = 0.f, q = 0.f;

@@ -44,7 +44,6 @@ struct PKc {
 
 template <int ROWS, int KB, int NP>
 struct PsKcBase {
-    static constexpr bool PRESPLIT = true;
     using G = PKc<ROWS, KB, NP>;
     static constexpr int NV = G::NV;
     using Regs = uint4[NV];
@@ -458,9 +457,8 @@ __device__ __forceinline__ void gemm_body_ps(const GemmArgs& a, InitA init_a, In
     init_a(la, m0, tid, kbeg);
     init_b(lb, n0, tid, kbeg);
 
-    constexpr bool S16 = Mma16<NP, KB>::ON;
-    WaveAcc<MI, NJ, S16> acc;
-    acc.zero();
+    floatx16 acc[MI][NJ];
+    acc_zero(acc);
 
     auto store_ab = [&](int buf, const typename LA::Regs& xa, const typename LB::Regs& xb) {
         uint16_t* da = lds + buf * (SA + SB);
@@ -470,22 +468,18 @@ __device__ __forceinline__ void gemm_body_ps(const GemmArgs& a, InitA init_a, In
     auto compute = [&](int buf) {
         const uint16_t* sa = lds + buf * (SA + SB);
         const uint16_t* sb = sa + SA;
-        if constexpr (S16) {
-            stage16_kc<NP, KB, BM, BN, MI, NJ, false>(acc.v, sa, sb, wm * 32 * MI, wn * 32 * NJ);
-        } else {
 #pragma unroll
-            for (int q = 0; q < S3<KB>::KSTEPS; ++q) {
-                bf16x8 fa[MI][NP], fb[NJ][NP];
+        for (int q = 0; q < S3<KB>::KSTEPS; ++q) {
+            bf16x8 fa[MI][NP], fb[NJ][NP];
 #pragma unroll
-                for (int j = 0; j < NJ; ++j) s3_frag<BN, KB, NP>(sb, wn * 32 * NJ + j * 32, q, fb[j]);
+            for (int j = 0; j < NJ; ++j) s3_frag<BN, KB, NP>(sb, wn * 32 * NJ + j * 32, q, fb[j]);
 #pragma unroll
-                for (int i = 0; i < MI; ++i) s3_frag<BM, KB, NP>(sa, wm * 32 * MI + i * 32, q, fa[i]);
-                s3_mfma<NP>(acc.v, fa, fb);
-            }
+            for (int i = 0; i < MI; ++i) s3_frag<BM, KB, NP>(sa, wm * 32 * MI + i * 32, q, fa[i]);
+            s3_mfma<NP>(acc, fa, fb);
         }
     };
     ps_pipeline(la, lb, kbeg, kend, compute, store_ab);
-    gemm_epilogue_t<WM, WN, MI, NJ>(a, acc.v, tile, reinterpret_cast<float*>(lds), epi);
+    gemm_epilogue_t<WM, WN, MI, NJ>(a, acc, tile, reinterpret_cast<float*>(lds), epi);
 }
 
 template <int NP, int WM, int WN, int MI, int NJ, int KB, class LA, class LB, class Epi, class InitA, class InitB>
@@ -508,9 +502,8 @@ __device__ __forceinline__ void gemm_body_psm(const GemmArgs& a, InitA init_a, I
     init_a(la, m0, tid, kbeg);
     init_b(lb, n0, tid, kbeg);
 
-    constexpr bool S16 = Mma16<NP, KB>::ON;
-    WaveAcc<MI, NJ, S16> acc;
-    acc.zero();
+    floatx16 acc[MI][NJ];
+    acc_zero(acc);
 
     auto store_ab = [&](int buf, const typename LA::Regs& xa, const typename LB::Regs& xb) {
         char* da = lds + buf * (SA + SB);
@@ -522,22 +515,18 @@ __device__ __forceinline__ void gemm_body_psm(const GemmArgs& a, InitA init_a, I
         if (!live) return;
         const char* sa = lds + buf * (SA + SB);
         const char* sb = sa + SA;
-        if constexpr (S16) {
-            stage16_mn<NP, KB, BM, BN, MI, NJ>(acc.v, sa, sb, wm * 32 * MI, wn * 32 * NJ);
-        } else {
 #pragma unroll
-            for (int q = 0; q < S3<KB>::KSTEPS; ++q) {
-                bf16x8 fa[MI][NP], fb[NJ][NP];
+        for (int q = 0; q < S3<KB>::KSTEPS; ++q) {
+            bf16x8 fa[MI][NP], fb[NJ][NP];
 #pragma unroll
-                for (int j = 0; j < NJ; ++j) s3m_frag<BN, KB, NP>(sb, wn * 32 * NJ + j * 32, q, fb[j]);
+            for (int j = 0; j < NJ; ++j) s3m_frag<BN, KB, NP>(sb, wn * 32 * NJ + j * 32, q, fb[j]);
 #pragma unroll
-                for (int i = 0; i < MI; ++i) s3m_frag<BM, KB, NP>(sa, wm * 32 * MI + i * 32, q, fa[i]);
-                s3_mfma<NP>(acc.v, fa, fb);
-            }
+            for (int i = 0; i < MI; ++i) s3m_frag<BM, KB, NP>(sa, wm * 32 * MI + i * 32, q, fa[i]);
+            s3_mfma<NP>(acc, fa, fb);
         }
     };
     ps_pipeline(la, lb, kbeg, kend, compute, store_ab);
-    gemm_epilogue_t<WM, WN, MI, NJ>(a, acc.v, tile, reinterpret_cast<float*>(lds), epi);
+    gemm_epilogue_t<WM, WN, MI, NJ>(a, acc, tile, reinterpret_cast<float*>(lds), epi);
 }
 
 // --------------------------------------------------------------------------------------------

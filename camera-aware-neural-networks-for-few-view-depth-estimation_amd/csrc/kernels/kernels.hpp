@@ -14,60 +14,47 @@ void prof_push(const char* name, double flops, hipStream_t st);
 void prof_pop(hipStream_t st);
 
 // ---------------- convolutions (conv_kernels.hip) ----------------
-// GEMM engine of the forward / dgrad contractions: 0 = exact fp32 MFMA (v_mfma_f32_32x32x2_f32),
-// 1 = S3: fp32 operands split exactly into three bf16 terms on the bf16 matrix cores (gemm_s3.hpp)
+// GEMM engine of the conv / ConvT contractions: 0 = exact fp32 MFMA (v_mfma_f32_32x32x2_f32),
+// 1 = S3: fp32 operands split exactly into three bf16 terms on the bf16 matrix cores (gemm_s3.hpp),
+// 2 = B1: bf16-rounded operands, fp32 accumulation
 void set_gemm_engine(int e);
 int gemm_engine();
 // y = conv3x3(x) (+ per-tile BN partials [rows][2][cout] when stats != nullptr)
-// in_scale/in_shift != nullptr: x is a pre-BN conv output and the loader applies
-// relu(x*scale[c] + shift[c]) on the fly (BN-apply + ReLU fused into the consumer)
-// w_split etc. (optional): the same weights pre-split (3 planes, gemm_ps.hpp layout) for the S3
-// engine, which then stages them without conversion
 void conv3x3_fwd(const float* x, int64_t ldx, int xcoff, int cin, const float* w, int cout, float* y,
-                 int64_t ldy, int ycoff, int B, int H, int W, float* stats, hipStream_t st,
-                 const float* in_scale = nullptr, const float* in_shift = nullptr, const void* w_split = nullptr);
+                 int64_t ldy, int ycoff, int B, int H, int W, float* stats, hipStream_t st);
 int conv3x3_stats_rows(int B, int H, int W, int cout);
-// BN-backward partials from a conv3x3 dgrad epilogue (EpiStoreBnBwd) whose output g feeds
-// relu(bn(y)): y [M][cin] and that BatchNorm's coefficients; writes stats [tiles][2][cin] =
-// per-tile (Σ dz, Σ dz·x̂), tiles = conv3x3_stats_rows(B, H, W, cin)
-struct BnBwdEpi {
-    const float *y, *mean, *invstd, *scale, *shift;
-    float* stats;
-};
 // dx[pix][ci] = conv3x3(dz, wd) with wd = repacked [ci][tap'][co]
 void conv3x3_dgrad(const float* dz, int cout, const float* wd, int cin, float* dx, int64_t lddx,
-                   int B, int H, int W, hipStream_t st, const void* wd_split = nullptr, const BnBwdEpi* bn = nullptr);
+                   int B, int H, int W, hipStream_t st);
 // dw[co][tap][ci] = sum_pix dz[pix][co] * im2col(x)[pix][tap,ci]
 void conv3x3_wgrad(const float* dz, int cout, const float* x, int64_t ldx, int xcoff, int cin, float* dw,
-                   int B, int H, int W, float* slab, int64_t slab_cap, hipStream_t st,
-                   const float* x_scale = nullptr, const float* x_shift = nullptr);
+                   int B, int H, int W, float* slab, int64_t slab_cap, hipStream_t st);
 // ConvTranspose2d(k2,s2): (B,H,W,cin) -> (B,2H,2W,cout) written at channel offset ycoff of rows ldy
 void convT_fwd(const float* x, int64_t ldx, int cin, const float* wf, const float* bias, int cout,
-               float* y, int64_t ldy, int ycoff, int B, int H, int W, hipStream_t st, const void* wf_split = nullptr);
+               float* y, int64_t ldy, int ycoff, int B, int H, int W, hipStream_t st);
 void convT_dgrad(const float* g, int64_t ldg, int gcoff, int cout, const float* wm, int cin, float* dx,
-                 int B, int H, int W, hipStream_t st, const void* wm_split = nullptr);
+                 int B, int H, int W, hipStream_t st);
 void convT_wgrad(const float* x, int cin, const float* g, int64_t ldg, int gcoff, int cout, float* dw,
                  int B, int H, int W, float* slab, int64_t slab_cap, hipStream_t st);
 int64_t wgrad_slab_floats(int M, int N, int Kpix);
 
-// ---- pre-split operands (gemm_ps.hpp): tensors split into bf16 planes once, by a split pass after
-// their producer, and read by the S3 (NP = 3) / B1 (NP = 1) GEMMs without per-fetch conversion.
-// A view: p = split rows of `ld` channels (ld, coff, channel counts multiples of 8).
+// ---- pre-split operands (gemm_ps.hpp): on the B1 engine, tensors written once as bf16 twins by
+// their producer (or a split pass after it) and read by the B1 GEMMs without per-fetch conversion.
+// A view: p = bf16 rows of `ld` channels (ld, coff, channel counts multiples of 8).
 struct Split {
     const void* p = nullptr;
     int64_t ld = 0;
     int coff = 0;
 };
-int split_planes();                    // NP of the current engine: 3 (S3), 1 (B1), 0 (f32: no split)
-inline bool ps_ok(int channels) { return split_planes() > 0 && channels % 8 == 0; }
-constexpr int kMaxPlanes = 3;          // buffers are sized for NP = 3 (bytes = elems * 2 * 3)
+int split_planes();                    // planes of the pre-split twins: 1 on B1, 0 otherwise (no twins)
+constexpr int kMaxPlanes = 1;          // twin bytes = elems * 2 * kMaxPlanes
 // out[row][ocoff + c] (split, ld ldo) = split(x[row][xcoff + c]), c < C, rows < M
 void split_rows(const float* x, int64_t ldx, int xcoff, int C, int64_t M, void* out, int64_t ldo, int ocoff,
                 hipStream_t st);
 void conv3x3_fwd_ps(Split x, int cin, Split w, int cout, float* y, int64_t ldy, int ycoff, int B, int H, int W,
                     float* stats, hipStream_t st);
 void conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t lddx, int B, int H, int W,
-                      hipStream_t st, const BnBwdEpi* bn = nullptr);
+                      hipStream_t st);
 void conv3x3_wgrad_ps(Split dz, int cout, Split x, int cin, float* dw, int B, int H, int W, float* slab,
                       int64_t slab_cap, hipStream_t st);
 void convT_fwd_ps(Split x, int cin, Split wf, const float* bias, int cout, float* y, int64_t ldy, int ycoff, int B,
@@ -93,24 +80,14 @@ void bn_eval_coeffs(const float* gamma, const float* beta, const float* run_mean
 // offset oscoff, split_planes() planes; see Split below)
 void bn_relu_fwd(const float* y, int C, const float* scale, const float* shift, float* out, int64_t ldo,
                  int ocoff, int64_t M, hipStream_t st, void* os = nullptr, int64_t ldos = 0, int oscoff = 0);
-// MaxPool2d(2) backward folded into a consumer of its gradient: g[pixel] += dpool[parent] where the
-// pixel is the parent's recorded argmax (H, W: the pooled-from grid); g = nullptr: none
-struct PoolGrad {
-    const float* g = nullptr;
-    const uint8_t* idx = nullptr;
-    int H = 0, W = 0;
-};
 // BN+ReLU backward: dy = k1*dz - k2 - k3*xhat, dz = g*[y*scale+shift > 0];
 // writes dgamma/dbeta (grad buffer) and dy (dense [M][C]).  gmul != nullptr: g is first multiplied
 // by gmul[sample][c] (sample = row / HW) — the FiLM gamma sitting between this ReLU and the consumer.
 // dy_split != nullptr: also the pre-split twin of dy (dense, ld C)
-// tile_part != nullptr: (Σ dz, Σ dz·x̂) already reduced per GEMM tile by the producing dgrad
-// (BnBwdEpi, [tile_rows][2][C]); only those partials are summed (no pass over g and y)
 void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, const float* mean,
                  const float* invstd, const float* scale, const float* shift, const float* gamma,
                  int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
-                 hipStream_t st, const float* gmul = nullptr, int64_t HW = 1, void* dy_split = nullptr,
-                 const float* tile_part = nullptr, int tile_rows = 0, PoolGrad pool = PoolGrad{});
+                 hipStream_t st, const float* gmul = nullptr, int64_t HW = 1, void* dy_split = nullptr);
 // out_split != nullptr: also the pooled output's split twin (dense, ld C); out may then be nullptr
 void maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float* out, uint8_t* idx,
                  hipStream_t st, void* out_split = nullptr);

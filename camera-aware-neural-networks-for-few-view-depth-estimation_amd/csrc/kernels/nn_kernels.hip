@@ -79,28 +79,6 @@ __global__ void k_colfinal(const double* part, int S, int N, double* tot, float*
     }
 }
 
-// g (4 channels c..c+3 of row r) plus the max-pool gradient routed to this pixel (k_maxpool_bwd_gather's
-// addition, done where g is consumed instead of as a read-modify-write pass over g)
-__device__ __forceinline__ float4 add_pool_grad(float4 gv, const PoolGrad& p, int64_t r, int c, int C) {
-    if (!p.g) return gv;
-    const int64_t HW = (int64_t)p.H * p.W;
-    const int b = (int)(r / HW);
-    const int64_t q = r - b * HW;
-    const int y = (int)(q / p.W), x = (int)(q - (int64_t)y * p.W);
-    const int Ho = p.H >> 1, Wo = p.W >> 1;
-    if (y >= 2 * Ho || x >= 2 * Wo) return gv;
-    const int code = ((y & 1) << 1) | (x & 1);
-    const int64_t op = ((int64_t)b * Ho + (y >> 1)) * Wo + (x >> 1);
-    const uchar4 a = *reinterpret_cast<const uchar4*>(p.idx + op * C + c);
-    if (a.x != code && a.y != code && a.z != code && a.w != code) return gv;
-    const float4 d = *reinterpret_cast<const float4*>(p.g + op * C + c);
-    if (a.x == code) gv.x += d.x;
-    if (a.y == code) gv.y += d.y;
-    if (a.z == code) gv.z += d.z;
-    if (a.w == code) gv.w += d.w;
-    return gv;
-}
-
 namespace {
 struct OpSum {
     const float* x; int64_t ld; int coff;
@@ -112,9 +90,8 @@ struct OpSum {
 struct OpBnBwd {
     const float *g, *y, *mean, *invstd, *scale, *shift, *gmul;
     int64_t ldg; int gcoff, C; int64_t HW;
-    PoolGrad pool;
     __device__ void operator()(int64_t r, int c4, double (&acc)[2][4]) const {
-        float4 gv = add_pool_grad(*reinterpret_cast<const float4*>(g + r * ldg + gcoff + c4 * 4), pool, r, c4 * 4, C);
+        float4 gv = *reinterpret_cast<const float4*>(g + r * ldg + gcoff + c4 * 4);
         if (gmul) {
             const float4 m = *reinterpret_cast<const float4*>(gmul + (r / HW) * C + c4 * 4);
             gv.x *= m.x; gv.y *= m.y; gv.z *= m.z; gv.w *= m.w;
@@ -258,10 +235,7 @@ void bn_relu_fwd(const float* y, int C, const float* scale, const float* shift, 
     const int64_t n4 = M * C / 4;
     const int np = os ? split_planes() : 0;
     char* o = static_cast<char*>(os);
-    if (np == 3)
-        hipLaunchKernelGGL(k_bn_relu_fwd<3>, dim3(ew_blocks(n4)), dim3(256), 0, st, y, C, scale, shift, out, ldo, ocoff,
-                           n4, o, ldos, oscoff);
-    else if (np == 1)
+    if (np == 1)
         hipLaunchKernelGGL(k_bn_relu_fwd<1>, dim3(ew_blocks(n4)), dim3(256), 0, st, y, C, scale, shift, out, ldo, ocoff,
                            n4, o, ldos, oscoff);
     else
@@ -289,12 +263,12 @@ __global__ void k_bn_relu_bwd(const float* __restrict__ g, int64_t ldg, int gcof
                               int C, const float* __restrict__ mean, const float* __restrict__ invstd,
                               const float* __restrict__ scale, const float* __restrict__ shift,
                               const float* __restrict__ coef, float* __restrict__ dy, int64_t n4,
-                              const float* __restrict__ gmul, int64_t HW, char* __restrict__ os, PoolGrad pool) {
+                              const float* __restrict__ gmul, int64_t HW, char* __restrict__ os) {
     const int C4 = C >> 2;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = i / C4;
         const int c0 = (int)(i - r * C4) * 4;
-        float4 gv = add_pool_grad(*reinterpret_cast<const float4*>(g + r * ldg + gcoff + c0), pool, r, c0, C);
+        float4 gv = *reinterpret_cast<const float4*>(g + r * ldg + gcoff + c0);
         if (gmul) {
             const float4 m = *reinterpret_cast<const float4*>(gmul + (r / HW) * C + c0);
             gv.x *= m.x; gv.y *= m.y; gv.z *= m.z; gv.w *= m.w;
@@ -318,32 +292,22 @@ __global__ void k_bn_relu_bwd(const float* __restrict__ g, int64_t ldg, int gcof
 void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, const float* mean,
                  const float* invstd, const float* scale, const float* shift, const float* gamma,
                  int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
-                 hipStream_t st, const float* gmul, int64_t HW, void* dy_split, const float* tile_part,
-                 int tile_rows, PoolGrad pool) {
+                 hipStream_t st, const float* gmul, int64_t HW, void* dy_split) {
     double* tot = scratch;
     double* part = scratch + 2 * C;
-    int S;
-    if (tile_part) {   // [rows][2][C] partials -> part[s][2C] (the layout OpBnBwd's slices have)
-        if (pool.g) throw std::runtime_error("bn_relu_bwd: tile partials exclude a folded max-pool gradient");
-        S = launch_colreduce<1>(OpSum{tile_part, 2 * C, 0}, tile_rows, 2 * C, part, st);
-    } else {
-        OpBnBwd op{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW, pool};
-        S = launch_colreduce<2>(op, M, C, part, st);
-    }
+    OpBnBwd op{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW};
+    const int S = launch_colreduce<2>(op, M, C, part, st);
     launch_colfinal(part, S, 2 * C, tot, nullptr, 1.f, st);
     hipLaunchKernelGGL(k_bn_bwd_coef, dim3(cdiv(C, 64)), dim3(64), 0, st, tot, C, M, gamma, invstd, coef, dgamma, dbeta);
     const int64_t n4 = M * C / 4;
     const int np = dy_split ? split_planes() : 0;
     char* os = static_cast<char*>(dy_split);
-    if (np == 3)
-        hipLaunchKernelGGL(k_bn_relu_bwd<3>, dim3(ew_blocks(n4)), dim3(256), 0, st, g, ldg, gcoff, y, C, mean, invstd,
-                           scale, shift, coef, dy, n4, gmul, HW, os, pool);
-    else if (np == 1)
+    if (np == 1)
         hipLaunchKernelGGL(k_bn_relu_bwd<1>, dim3(ew_blocks(n4)), dim3(256), 0, st, g, ldg, gcoff, y, C, mean, invstd,
-                           scale, shift, coef, dy, n4, gmul, HW, os, pool);
+                           scale, shift, coef, dy, n4, gmul, HW, os);
     else
         hipLaunchKernelGGL(k_bn_relu_bwd<0>, dim3(ew_blocks(n4)), dim3(256), 0, st, g, ldg, gcoff, y, C, mean, invstd,
-                           scale, shift, coef, dy, n4, gmul, HW, os, pool);
+                           scale, shift, coef, dy, n4, gmul, HW, os);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -387,35 +351,10 @@ void maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float*
     const int64_t n4 = (int64_t)B * (H / 2) * (W / 2) * C / 4;
     const int np = out_split ? split_planes() : 0;
     char* os = static_cast<char*>(out_split);
-    if (np == 3)
-        hipLaunchKernelGGL(k_maxpool_fwd<3>, dim3(ew_blocks(n4)), dim3(256), 0, st, x, ldx, C, B, H, W, out, idx, n4, os);
-    else if (np == 1)
+    if (np == 1)
         hipLaunchKernelGGL(k_maxpool_fwd<1>, dim3(ew_blocks(n4)), dim3(256), 0, st, x, ldx, C, B, H, W, out, idx, n4, os);
     else
         hipLaunchKernelGGL(k_maxpool_fwd<0>, dim3(ew_blocks(n4)), dim3(256), 0, st, x, ldx, C, B, H, W, out, idx, n4, os);
-}
-// dx[argmax] += dout  (in place on the skip half of the decoder concat gradient)
-__global__ void k_maxpool_bwd(const float* __restrict__ dout, const uint8_t* __restrict__ idx, int C, int B,
-                              int H, int W, float* __restrict__ dx, int64_t lddx, int64_t n4) {
-    const int C4 = C >> 2, Ho = H >> 1, Wo = W >> 1;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t op = i / C4;
-        const int c = (int)(i - op * C4) * 4;
-        const int xo = (int)(op % Wo);
-        const int64_t t = op / Wo;
-        const int yo = (int)(t % Ho);
-        const int b = (int)(t / Ho);
-        const int64_t p00 = ((int64_t)b * H + 2 * yo) * W + 2 * xo;
-        float4 d = *reinterpret_cast<const float4*>(dout + op * C + c);
-        uchar4 a = *reinterpret_cast<const uchar4*>(idx + op * C + c);
-        const float da[4] = {d.x, d.y, d.z, d.w};
-        const uint8_t aa[4] = {a.x, a.y, a.z, a.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int64_t p = p00 + (aa[e] >> 1) * W + (aa[e] & 1);
-            dx[p * lddx + c + e] += da[e];
-        }
-    }
 }
 // gather form: one thread per (INPUT pixel, 4 channels) inside the pooled region, coalesced float4
 // read-modify-write of dx; adds dout[parent] where this pixel is the recorded argmax

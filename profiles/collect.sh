@@ -14,15 +14,15 @@ OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 cd "$ROOT"
-ARGS="--steps 3 --warmup 1 --no-cpu-baseline --config $CFG"
+ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-extra --config $CFG"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
     python3 bench.py $ARGS > "$OUT/trace.json" 2> "$OUT/trace.err"
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- \
-    python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --config $CFG > "$OUT/fetch.json" 2> "$OUT/fetch.err"
+    python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-extra --config $CFG > "$OUT/fetch.json" 2> "$OUT/fetch.err"
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- \
-    python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --config $CFG > "$OUT/write.json" 2> "$OUT/write.err"
+    python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-extra --config $CFG > "$OUT/write.json" 2> "$OUT/write.err"
 timeout -k 10 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
     SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT \
     --output-format csv -d "$OUT/sq" -o run -- \
-    python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --config $CFG > "$OUT/sq.json" 2> "$OUT/sq.err"
+    python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-extra --config $CFG > "$OUT/sq.json" 2> "$OUT/sq.err"
 python3 profiles/summarize.py "$OUT" "$TAG"

@@ -59,7 +59,7 @@ def test_film_train_steps_vs_reference_fixture(cad, dev, oracle, name):
     grads = net.grads()
     # judged against the fp64 oracle next to the REFERENCE's own distance from it: these f=4 nets
     # have near-constant outputs (smoothness signs of 1-ulp neighbours) and 2-3-sample BatchNorm1d,
-    # which make individual gradients fp32-ill-conditioned (tests/_diag_film.py)
+    # which make individual gradients fp32-ill-conditioned
     r64 = oracle.Trainer(oracle.synth_init(f, model=model), oracle.init_buffers(f, model=model),
                          weights=meta["weights"], dtype=torch.float64, model=model).forward_backward(
         fx["input.rgb"], fx["input.gt"], fx["input.K"])
@@ -173,6 +173,67 @@ def test_film_train_step_vs_oracle(cad, dev, oracle, model, f, B, H, W):
     pe = net.forward_cam(rg, cad.camera_from_K(kg))
     pe_ref, pe64 = ref.predict_eval(rgb, K), ref64.predict_eval(rgb, K)
     assert max_rel_err(pe.cpu(), pe64) < max(1e-3, 3 * max_rel_err(pe_ref, pe64))
+
+
+@pytest.fixture
+def bf16_engine(cad):
+    lib = cad.load_library()
+    prev = lib.cad_get_gemm_engine()
+    assert lib.cad_set_gemm_engine(2) == 0   # CAD_GEMM_BF16
+    yield
+    lib.cad_set_gemm_engine(prev)
+
+
+@pytest.mark.parametrize("model,f,B,H,W", [("rayfilm", 32, 4, 48, 64), ("rayfilm", 64, 2, 64, 64),
+                                           ("film", 16, 2, 64, 96)])
+def test_film_train_step_bf16_engine_vs_oracle(cad, dev, oracle, bf16_engine, model, f, B, H, W):
+    """Config 3's arithmetic (BASELINE configs[2]: the ray+FiLM U-Net with bf16 GEMMs): every conv /
+    ConvT contraction multiplies bf16-rounded operands with fp32 accumulation, on the pre-split path
+    (f % 8 == 0: operands written as bf16 twins by their producers, FiLM'd a1 included; enc1's
+    8-channel rgb+ray input split once).  Yardstick: the oracle with the same operand rounding
+    (Trainer(model, gemm_operands="bf16")) in fp64, with the criteria of
+    test_gpu_model.py::test_train_step_bf16_engine_vs_oracle and the FiLM allowances of
+    test_film_train_step_vs_oracle."""
+    params = oracle.init_params(f, seed=f, model=model)
+    bufs = oracle.init_buffers(f, model=model)
+    rgb, gt, K = [torch.from_numpy(a) for a in oracle.synth_batch(B, H, W)]
+    ref = oracle.Trainer(params, bufs, model=model, gemm_operands="bf16")
+    ref64 = oracle.Trainer(params, bufs, dtype=torch.float64, model=model, gemm_operands="bf16")
+    exact64 = oracle.Trainer(params, bufs, dtype=torch.float64, model=model)
+    r, r64, e64 = ref.step(rgb, gt, K), ref64.step(rgb, gt, K), exact64.step(rgb, gt, K)
+    state = dict(params)
+    state.update(bufs)
+    net, loss, tr = _build(cad, model, f, B, H, W, (1.0, 0.1, 0.001, 0.01), state)
+    rg, gg, kg = rgb.to(dev), gt.to(dev), K.to(dev)
+    pred = net.forward_cam(rg, cad.camera_from_K(kg))
+    loss5, dpred = loss.forward_with_intrinsics(pred, gg, rg, kg)
+    net.backward(dpred)
+    torch.cuda.synchronize()
+    assert max_rel_err(pred.cpu(), r64["pred"]) < max(1e-3, 5 * max_rel_err(r["pred"], r64["pred"]))
+    assert abs(loss5[0].item() - r64["loss"]) <= max(1e-3 * abs(r64["loss"]), 5 * abs(r["loss"] - r64["loss"]))
+    assert max_rel_err(pred.cpu(), e64["pred"]) < 5e-2
+    grads = net.grads()
+    for (n, _), g32, g64 in zip(oracle.param_spec(f, model=model), r["grads"], r64["grads"]):
+        if _zero_grad_bias(n, B):   # true gradient is 0: noise well below the weight-gradient scale
+            w = grads[n[: -len("bias")] + "weight"]
+            assert grads[n].abs().max().item() <= 1e-2 * w.abs().max().item() + 1e-12, n
+            continue
+        ours, ref32 = max_rel_err(grads[n], g64), max_rel_err(g32, g64)
+        cos = torch.nn.functional.cosine_similarity(grads[n].double().reshape(1, -1), g64.reshape(1, -1)).item()
+        cos32 = torch.nn.functional.cosine_similarity(g32.double().reshape(1, -1), g64.reshape(1, -1)).item()
+        assert cos > min(0.999, 1 - 3 * (1 - cos32)) and ours < max(0.25, 5 * ref32), (n, cos, cos32, ours, ref32)
+    cad.clip_grad_norm_(net, 1.0)
+    tr.optimizer.step()
+    for _ in range(3):
+        p_ref = ref.step(rgb, gt, K)["pred"]
+        p64 = ref64.step(rgb, gt, K)["pred"]
+        tr.train_step(rg, gg, kg)
+    torch.cuda.synchronize()
+    assert max_rel_err(tr.pred.cpu(), p64) < max(2e-3, 5 * max_rel_err(p_ref, p64))
+    net.eval()
+    pe = net.forward_cam(rg, cad.camera_from_K(kg))
+    pe_ref, pe64 = ref.predict_eval(rgb, K), ref64.predict_eval(rgb, K)
+    assert max_rel_err(pe.cpu(), pe64) < max(2e-3, 5 * max_rel_err(pe_ref, pe64))
 
 
 def test_film_batch_one_skips_batchnorm1d(cad, dev, oracle):

@@ -204,3 +204,50 @@ def test_s3_engine_accuracy_matches_fp32(cad, dev, cin, cout, H, W):
         errs[eng] = max_rel_err(nchw(y.cpu()), ref)
     lib.cad_set_gemm_engine(prev)
     assert errs[1] < max(2.0 * errs[0], 2e-6), errs
+
+
+def _profile(lib):
+    import json
+    n = lib.cad_profile_report(None, 0)
+    buf = C.create_string_buffer(n)
+    lib.cad_profile_report(buf, n)
+    return json.loads(buf.value.decode())
+
+
+# (engine, B, H, W): K = B*H*W pixels large enough for >= 48 split-K slabs of the 64 x 576 L0-type
+# weight gradient, so finish_slabs takes its two-level reduction (conv_kernels.hip): 24-slab groups,
+# then the group heads, then the remainder slabs
+SLAB2 = [("s3", 1, 96, 256, 48, 0), ("s3", 1, 100, 256, 50, 2), ("f32", 1, 100, 256, 50, 2),
+         ("bf16", 2, 96, 256, 48, 0)]
+
+
+@pytest.mark.parametrize("eng,B,H,W,splits,rem", SLAB2)
+def test_wgrad_two_level_slab_reduction(cad, dev, eng, B, H, W, splits, rem):
+    """The many-slab weight-gradient path that only the 480x640 L0 layers take in the U-Net: both
+    remainder branches (rem == 0: 3 reduction launches; rem > 0: 4) against fp64, and the launch
+    profile proves which plan ran (every k_slab_reduce launch is recorded)."""
+    lib = cad.load_library()
+    prev = lib.cad_get_gemm_engine()
+    assert lib.cad_set_gemm_engine(ENGINES[eng]) == 0
+    cin = cout = 64
+    g = torch.Generator().manual_seed(H * 7 + B)
+    x = torch.randn(B, cin, H, W, generator=g)
+    dy = torch.randn(B, cout, H, W, generator=g) / (H * W) ** 0.5
+    xd = q(x, eng).double()
+    wd = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, requires_grad=True)
+    F.conv2d(xd, wd, None, 1, 1).backward(q(dy, eng).double())
+    dw = torch.zeros(cout, 3, 3, cin, device=dev)
+    xg, dyg = nhwc(x).to(dev), nhwc(dy).to(dev)
+    torch.cuda.synchronize()
+    lib.cad_profile_reset()
+    lib.cad_profile_enable(1)
+    try:
+        assert lib.cad_op_conv3x3_wgrad(_p(dyg), cout, _p(xg), cin, 0, cin, _p(dw), B, H, W, _s()) == 0
+        torch.cuda.synchronize()
+        prof = _profile(lib)
+    finally:
+        lib.cad_profile_enable(0)
+        lib.cad_set_gemm_engine(prev)
+    reduce_launches = sum(r["launches"] for r in prof if "k_slab_reduce" in r["name"])
+    assert reduce_launches == (3 if rem == 0 else 4), prof
+    assert max_rel_err(dw.cpu().permute(0, 3, 1, 2), wd.grad) < TOL
