@@ -96,6 +96,19 @@ SIGNATURES = {
     "cad_aug_sampler_create": (I, [C.c_void_p, C.c_uint32, C.POINTER(P)]),
     "cad_aug_sampler_destroy": (None, [P]),
     "cad_aug_sampler_draw": (I, [P, I, I, C.c_void_p]),
+    "cad_loss_forward_backward_masked": (I, [P, P, P, P, P, P, I, P, P, P]),
+    "cad_comm_get_unique_id": (I, [C.c_void_p]),
+    "cad_comm_create": (I, [C.c_void_p, I, I, I, C.POINTER(P)]),
+    "cad_comm_destroy": (None, [P]),
+    "cad_comm_rank": (I, [P]),
+    "cad_comm_size": (I, [P]),
+    "cad_comm_allreduce": (I, [P, P, I64, I, P]),
+    "cad_comm_broadcast": (I, [P, P, I64, I, P]),
+    "cad_comm_broadcast_params": (I, [P, P, I, P]),
+    "cad_grad_allreduce": (I, [P, P, P]),
+    "cad_unet_backward_allreduce": (I, [P, P, P, I64, P]),
+    "cad_plan_grad_buckets": (I, [I64P, I64P, I, I64, I64P, I64P, C.POINTER(I)]),
+    "cad_model_grad_layout": (I, [I, I, I, C.POINTER(I), I64P, I64P, I64P]),
 }
 
 

@@ -15,14 +15,25 @@
 // and ignores it); TensorBoard events are written as a CSV of scalars (no Python tensorboard here);
 // the dataset is data.dataset_name: "synthetic" (SUN-RGB-D-shaped counter-based samples) — decoding
 // the real SUN RGB-D JPEG/PNG files needs OpenCV, absent on this image.
+#include <signal.h>
+#include <spawn.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <filesystem>
 #include <fstream>
 #include <iostream>
+#include <algorithm>
+#include <memory>
+#include <random>
+#include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../../include/cad/cad.hpp"
@@ -37,6 +48,8 @@ struct Args {
     std::string config = "configs/train_config.yaml", experiment = "baseline_unet", resume;
     int gpu = 0;
     bool debug = false, tensorboard = true;
+    bool dry_run = false;   // print the (per-rank) run plan and exit before any GPU call
+    std::vector<std::string> argv;
 };
 
 void usage() {
@@ -47,11 +60,13 @@ void usage() {
                  "  -g, --gpu arg         GPU ID (default: 0)\n"
                  "  -d, --debug           Enable debug mode\n"
                  "      --tensorboard arg Enable TensorBoard-style scalar logging (default: true)\n"
+                 "      --dry-run         Print the run plan (per data-parallel rank) and exit; no GPU use\n"
                  "  -h, --help            Print help\n";
 }
 
 Args parse_args(int argc, char** argv) {
     Args a;
+    a.argv.assign(argv, argv + argc);
     for (int i = 1; i < argc; ++i) {
         std::string k = argv[i], v;
         auto eq = k.find('=');
@@ -67,6 +82,7 @@ Args parse_args(int argc, char** argv) {
         else if (k == "-r" || k == "--resume") a.resume = next();
         else if (k == "-g" || k == "--gpu") a.gpu = std::stoi(next());
         else if (k == "-d" || k == "--debug") a.debug = v.empty() ? true : (v == "true" || v == "1");
+        else if (k == "--dry-run") a.dry_run = true;
         else if (k == "--tensorboard") {
             std::string t = (!v.empty() || (i + 1 < argc && argv[i + 1][0] != '-')) ? next() : "true";
             a.tensorboard = t == "true" || t == "1";
@@ -84,6 +100,11 @@ struct Config {   // the TrainingConfig fields the step uses (trainer.h:24-92)
     std::string checkpoint_dir = "./checkpoints", log_dir = "./logs", experiment_name = "baseline_unet";
     std::string dataset = "sunrgbd";
     int n_train = 64, n_val = 16;
+    // hardware: (configs/train_config.yaml:176-183; parsed but unused by the reference)
+    bool distributed = false;
+    int num_gpus = 1;
+    std::vector<int> gpu_ids;
+    std::string backend = "nccl";
 };
 
 Config load_config(const yaml_lite::Node& y, const std::string& experiment) {   // train_main.cpp:60-167
@@ -133,6 +154,12 @@ Config load_config(const yaml_lite::Node& y, const std::string& experiment) {   
         c.dataset = d["dataset_name"].as<std::string>("sunrgbd");
         c.n_train = d["num_train_samples"].as<int>(64);
         c.n_val = d["num_val_samples"].as<int>(16);
+    }
+    if (auto& hw = y["hardware"]) {
+        c.distributed = hw["distributed"].as<bool>(false);
+        c.num_gpus = hw["num_gpus"].as<int>(1);
+        c.backend = hw["backend"].as<std::string>("nccl");
+        for (float v : hw["gpu_ids"].as<std::vector<float>>({})) c.gpu_ids.push_back((int)v);
     }
     c.checkpoint_dir += "/" + c.experiment_name;   // :163-164
     c.log_dir += "/" + c.experiment_name;
@@ -247,46 +274,224 @@ void load_checkpoint(const std::string& path, BaselineUNetImpl& m, optim::Adam& 
     }
 }
 
+// ---- data-parallel job: one process per GPU (hardware.distributed / num_gpus / gpu_ids,
+// configs/train_config.yaml:176-183 — keys the reference parses but never uses) ----
+constexpr const char* kEnvRank = "CAD_DP_RANK";
+constexpr const char* kEnvWorld = "CAD_DP_WORLD";
+constexpr const char* kEnvDevice = "CAD_DP_DEVICE";
+constexpr const char* kEnvIdFile = "CAD_DP_ID_FILE";
+
+struct Rank {
+    int rank = 0, world = 1, device = 0;
+    bool dp = false;        // a communicator is built (distributed: true, even for one GPU)
+    std::string id_file;    // the launcher's rendezvous file ("" for a single process)
+};
+
+std::vector<int> dp_devices(const Config& c) {
+    std::vector<int> ids = c.gpu_ids;
+    if ((int)ids.size() < c.num_gpus) {
+        ids.clear();
+        for (int i = 0; i < c.num_gpus; ++i) ids.push_back(i);
+    }
+    ids.resize((size_t)c.num_gpus);
+    return ids;
+}
+
+// The launcher: starts one child per GPU (this process makes no GPU call at all, so starting a fresh
+// program is safe), forwards the exit status of the first child that fails, and stops the others
+// then (a rank blocked in a collective would otherwise wait forever).
+int launch_ranks(const Args& args, const Config& c) {
+    const std::vector<int> devs = dp_devices(c);
+    char tmpl[] = "/tmp/cad_dp_XXXXXX";
+    if (!mkdtemp(tmpl)) throw std::runtime_error("cannot create the rendezvous directory");
+    const std::string dir = tmpl, id_file = dir + "/rccl_id";
+    std::vector<char*> argv;
+    for (const auto& s : args.argv) argv.push_back(const_cast<char*>(s.c_str()));
+    argv.push_back(nullptr);
+    std::vector<pid_t> pids;
+    for (int r = 0; r < c.num_gpus; ++r) {
+        std::vector<std::string> env;
+        for (char** e = environ; *e; ++e)
+            if (std::strncmp(*e, "CAD_DP_", 7) != 0) env.push_back(*e);
+        env.push_back(std::string(kEnvRank) + "=" + std::to_string(r));
+        env.push_back(std::string(kEnvWorld) + "=" + std::to_string(c.num_gpus));
+        env.push_back(std::string(kEnvDevice) + "=" + std::to_string(devs[(size_t)r]));
+        env.push_back(std::string(kEnvIdFile) + "=" + id_file);
+        std::vector<char*> envp;
+        for (auto& e : env) envp.push_back(const_cast<char*>(e.c_str()));
+        envp.push_back(nullptr);
+        pid_t pid;
+        if (posix_spawn(&pid, "/proc/self/exe", nullptr, nullptr, argv.data(), envp.data()) != 0) {
+            for (pid_t p : pids) kill(p, SIGTERM);
+            throw std::runtime_error("cannot start rank " + std::to_string(r));
+        }
+        pids.push_back(pid);
+    }
+    int rc = 0;
+    for (size_t left = pids.size(); left > 0; --left) {
+        int st = 0;
+        const pid_t p = waitpid(-1, &st, 0);
+        if (p < 0) break;
+        const int code = WIFEXITED(st) ? WEXITSTATUS(st) : 128 + (WIFSIGNALED(st) ? WTERMSIG(st) : 0);
+        if (code != 0 && rc == 0) {
+            rc = code;
+            std::cerr << "rank " << (std::find(pids.begin(), pids.end(), p) - pids.begin()) << " failed (status "
+                      << code << "); stopping the other ranks\n";
+            for (pid_t q : pids)
+                if (q != p) kill(q, SIGTERM);
+        }
+    }
+    std::error_code ec;
+    fs::remove_all(dir, ec);
+    return rc;
+}
+
+Rank rank_of_process(const Config& c, const Args& args) {
+    Rank r;
+    if (const char* e = std::getenv(kEnvRank)) {
+        r.rank = std::atoi(e);
+        r.world = std::atoi(std::getenv(kEnvWorld) ? std::getenv(kEnvWorld) : "1");
+        r.device = std::atoi(std::getenv(kEnvDevice) ? std::getenv(kEnvDevice) : "0");
+        r.id_file = std::getenv(kEnvIdFile) ? std::getenv(kEnvIdFile) : "";
+        r.dp = true;
+        if (r.world < 1 || r.rank < 0 || r.rank >= r.world || r.id_file.empty())
+            throw std::runtime_error("inconsistent data-parallel rank environment");
+    } else {
+        r.device = c.distributed && !c.gpu_ids.empty() ? c.gpu_ids[0] : args.gpu;
+        r.dp = c.distributed;   // one GPU, distributed: a single-rank communicator
+    }
+    return r;
+}
+
+// RCCL id rendezvous through the launcher's file: rank 0 writes it (write, then rename: readers never
+// see a partial file), the others poll for it.  A dry run exchanges random bytes instead.
+distributed::UniqueId exchange_id(const Rank& r, bool dry) {
+    distributed::UniqueId id{};
+    auto draw = [&] {
+        if (!dry) return distributed::Communicator::unique_id();
+        std::random_device rd;
+        distributed::UniqueId x{};
+        for (auto& b : x) b = (uint8_t)rd();
+        return x;
+    };
+    if (r.id_file.empty()) return draw();
+    if (r.rank == 0) {
+        id = draw();
+        const std::string tmp = r.id_file + ".tmp";
+        {
+            std::ofstream f(tmp, std::ios::binary);
+            f.write(reinterpret_cast<const char*>(id.data()), (std::streamsize)id.size());
+            if (!f) throw std::runtime_error("cannot write " + tmp);
+        }
+        fs::rename(tmp, r.id_file);
+        return id;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        std::error_code ec;
+        if (fs::exists(r.id_file, ec) && fs::file_size(r.id_file, ec) == id.size()) {
+            std::ifstream f(r.id_file, std::ios::binary);
+            f.read(reinterpret_cast<char*>(id.data()), (std::streamsize)id.size());
+            if (f) return id;
+        }
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(300))
+            throw std::runtime_error("rank " + std::to_string(r.rank) + ": no communicator id from rank 0");
+        std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    }
+}
+
+// global batch bi = samples [bi*B*world, (bi+1)*B*world); rank r takes its r-th B-slice.  With more
+// than one rank the last partial global batch is dropped (every replica must step together).
+struct Shard {
+    int64_t first;
+    int n;
+};
+int steps_per_epoch(int n_train, int B, int world) {
+    return world > 1 ? n_train / (B * world) : (n_train + B - 1) / B;
+}
+Shard shard_of(int bi, int n_train, int B, const Rank& r) {
+    const int64_t first = (int64_t)bi * B * r.world + (int64_t)r.rank * B;
+    return {first, (int)std::min<int64_t>(B, n_train - first)};
+}
+
+int dry_run(const Config& c, const Rank& r) {
+    const auto id = exchange_id(r, true);
+    uint64_t h = 1469598103934665603ull;   // FNV-1a of the rendezvous bytes: equal on every rank
+    for (uint8_t b : id) h = (h ^ b) * 1099511628211ull;
+    int ns = 0;
+    int64_t off[16], cnt[16], n_flat = 0;
+    cad::check(cad_model_grad_layout(CAD_MODEL_BASELINE, 3, c.init_features, &ns, off, cnt, &n_flat), "layout");
+    int64_t boff[16], bcnt[16];
+    int blast[16];
+    const int nb = cad_plan_grad_buckets(off, cnt, ns, 25 << 18, boff, bcnt, blast);
+    const int spe = steps_per_epoch(c.n_train, c.batch_size, r.world);
+    std::ostringstream o;
+    o << "{\"rank\": " << r.rank << ", \"world\": " << r.world << ", \"device\": " << r.device
+      << ", \"communicator\": " << (r.dp ? "true" : "false") << ", \"id_hash\": " << h
+      << ", \"steps_per_epoch\": " << spe << ", \"global_batch\": " << c.batch_size * r.world << ", \"first_step_samples\": [";
+    const Shard s0 = shard_of(0, c.n_train, c.batch_size, r);
+    o << s0.first << ", " << s0.first + s0.n << "], \"n_flat\": " << n_flat << ", \"buckets\": [";
+    for (int i = 0; i < nb; ++i) o << (i ? ", " : "") << "[" << boff[i] << ", " << bcnt[i] << ", " << blast[i] << "]";
+    o << "]}";
+    std::cout << o.str() << std::endl;
+    return 0;
+}
+
 int run(const Args& args) {
-    std::cout << "Loading configuration from: " << args.config << "\n";
     yaml_lite::Node y = yaml_lite::load_file(args.config);
     Config c = load_config(y, args.experiment);
     if (args.debug || (y["debug"] && y["debug"]["enabled"].as<bool>(false))) {   // :297-301
-        std::cout << "Debug mode enabled - using reduced dataset\n";
         c.num_epochs = y["debug"]["num_epochs"].as<int>(2);
         c.log_interval = y["debug"]["log_interval"].as<int>(1);
     }
+    if (c.distributed && c.backend != "nccl" && c.backend != "rccl")
+        throw std::runtime_error("hardware.backend '" + c.backend + "': this build exchanges gradients over RCCL (\"nccl\")");
+    if (c.distributed && c.num_gpus > 1 && !std::getenv(kEnvRank)) return launch_ranks(args, c);
+    const Rank R = rank_of_process(c, args);
+    if (args.dry_run) return dry_run(c, R);
+    const bool lead = R.rank == 0;   // logs, validation and checkpoints (rank 0's replica)
+    if (lead) std::cout << "Loading configuration from: " << args.config << "\n";
+    if (args.debug && lead) std::cout << "Debug mode enabled - using reduced dataset\n";
     if (c.dataset != "synthetic")
         throw std::runtime_error("dataset '" + c.dataset + "': SUN RGB-D JPEG/PNG decoding needs OpenCV, which this "
                                  "build does not include; set data.dataset_name: \"synthetic\"");
     int ndev = 0;
     cad::check(cad_device_count(&ndev), "device query");
-    if (args.gpu < 0 || args.gpu >= ndev) throw std::runtime_error("GPU " + std::to_string(args.gpu) + " not available");
-    cad::check(cad_set_device(args.gpu), "set device");
-    fs::create_directories(c.checkpoint_dir);
-    fs::create_directories(c.log_dir);
+    if (R.device < 0 || R.device >= ndev) throw std::runtime_error("GPU " + std::to_string(R.device) + " not available");
+    cad::check(cad_set_device(R.device), "set device");
+    if (lead) {
+        fs::create_directories(c.checkpoint_dir);
+        fs::create_directories(c.log_dir);
+    }
 
     const int B = c.batch_size, H = c.height, W = c.width;
-    cad::Workspace ws{B, H, W, args.gpu};
+    cad::Workspace ws{B, H, W, R.device};
     BaselineUNetImpl model(3, c.init_features, c.max_depth, ws);
     CombinedDepthLoss loss_fn(c.si, c.grad, c.smooth, c.reproj, ws);
     optim::Adam opt(model, c.learning_rate, c.weight_decay);
-    std::cout << "Model: baseline_unet (f=" << c.init_features << "), parameters: " << model.count_parameters() << "\n"
-              << "Using MI355X device " << args.gpu << "\n"
-              << "Training samples: " << c.n_train << " (synthetic), validation samples: " << c.n_val << "\n";
+    std::unique_ptr<distributed::Communicator> comm;
+    if (R.dp) comm = std::make_unique<distributed::Communicator>(exchange_id(R, false), R.world, R.rank, R.device);
+    if (lead)
+        std::cout << "Model: baseline_unet (f=" << c.init_features << "), parameters: " << model.count_parameters() << "\n"
+                  << "Using MI355X device " << R.device
+                  << (R.dp ? " (data-parallel rank 0 of " + std::to_string(R.world) + ", RCCL)" : std::string()) << "\n"
+                  << "Training samples: " << c.n_train << " (synthetic), validation samples: " << c.n_val << "\n";
     if (!args.resume.empty()) {
         load_checkpoint(args.resume, model, opt);
-        std::cout << "Resumed from " << args.resume << " (optimizer step " << opt.step_count() << ")\n";
+        if (lead) std::cout << "Resumed from " << args.resume << " (optimizer step " << opt.step_count() << ")\n";
     }
+    if (comm) comm->broadcast_parameters(model, 0);   // identical replicas
 
-    std::ofstream train_log(c.log_dir + "/training.log", std::ios::app);
-    std::ofstream metrics_csv(c.log_dir + "/metrics.csv", std::ios::app);
-    if (metrics_csv.tellp() == 0)
-        metrics_csv << "epoch,step,train_loss,val_loss,abs_rel,sq_rel,rmse,rmse_log,a1,a2,a3,learning_rate,time_elapsed\n";
-    std::ofstream tb;
-    if (args.tensorboard) {
-        tb.open(c.log_dir + "/tensorboard_scalars.csv", std::ios::app);
-        if (tb.tellp() == 0) tb << "tag,step,value\n";
+    std::ofstream train_log, metrics_csv, tb;
+    if (lead) {
+        train_log.open(c.log_dir + "/training.log", std::ios::app);
+        metrics_csv.open(c.log_dir + "/metrics.csv", std::ios::app);
+        if (metrics_csv.tellp() == 0)
+            metrics_csv << "epoch,step,train_loss,val_loss,abs_rel,sq_rel,rmse,rmse_log,a1,a2,a3,learning_rate,time_elapsed\n";
+        if (args.tensorboard) {
+            tb.open(c.log_dir + "/tensorboard_scalars.csv", std::ios::app);
+            if (tb.tellp() == 0) tb << "tag,step,value\n";
+        }
     }
 
     const int64_t HW = (int64_t)H * W;
@@ -294,8 +499,8 @@ int run(const Args& args) {
     hb.rgb.resize((size_t)(B * 3 * HW));
     hb.gt.resize((size_t)(B * HW));
     hb.K.resize((size_t)B * 9);
-    DeviceTensor rgb = DeviceTensor::empty({B, 3, H, W}, args.gpu), gt = DeviceTensor::empty({B, 1, H, W}, args.gpu),
-                 K = DeviceTensor::empty({B, 3, 3}, args.gpu), pred = DeviceTensor::empty({B, 1, H, W}, args.gpu);
+    DeviceTensor rgb = DeviceTensor::empty({B, 3, H, W}, R.device), gt = DeviceTensor::empty({B, 1, H, W}, R.device),
+                 K = DeviceTensor::empty({B, 3, 3}, R.device), pred = DeviceTensor::empty({B, 1, H, W}, R.device);
     auto upload = [&](int64_t first, int n, int64_t split_offset) {
         for (int i = 0; i < n; ++i)
             make_sample(split_offset + first + i, H, W, hb.rgb.data() + i * 3 * HW, hb.gt.data() + i * HW, hb.K.data() + i * 9);
@@ -306,36 +511,43 @@ int run(const Args& args) {
     };
     const auto t0 = std::chrono::steady_clock::now();
     int64_t global_step = opt.step_count();
-    const int start_epoch = 1 + (int)(global_step / std::max(1, (c.n_train + B - 1) / B));
+    const int nb = steps_per_epoch(c.n_train, B, R.world);
+    if (nb < 1) throw std::runtime_error("fewer training samples than one global batch");
+    const int start_epoch = 1 + (int)(global_step / nb);
+    constexpr int64_t kBucketElems = 25 << 18;   // 25 MB gradient buckets
     for (int epoch = start_epoch; epoch <= c.num_epochs; ++epoch) {
         model.train();
         double total = 0.0;
-        int seen = 0;
-        const int nb = (c.n_train + B - 1) / B;
+        int64_t seen = 0;
         for (int bi = 0; bi < nb; ++bi) {   // enhanced.h:266-329
-            const int n = std::min(B, c.n_train - bi * B);   // last partial batch (:269-270)
-            upload((int64_t)bi * B, n, 0);
+            const Shard sh = shard_of(bi, c.n_train, B, R);   // last partial batch (:269-270) on one rank
+            upload(sh.first, sh.n, 0);
             opt.zero_grad();
             model.forward_into(rgb, pred);
             DeviceTensor l = loss_fn.forwardWithIntrinsics(pred, gt, rgb, K);
-            model.backward(loss_fn.dpred());
-            double gnorm = c.use_grad_clip ? clip_grad_norm_(model, c.grad_clip_value) : 0.0;
-            if (!c.use_grad_clip) cad::check(cad_clip_grad_norm(model.handle(), INFINITY, 1.f, nullptr), "noclip");
+            if (comm) comm->backward_allreduce(model, loss_fn.dpred(), kBucketElems);
+            else model.backward(loss_fn.dpred());
+            // clip_grad_norm_ on the mean gradient (the SUM all-reduce's 1/world folded in)
+            const double gnorm = c.use_grad_clip ? clip_grad_norm_(model, c.grad_clip_value, nullptr, 1.0 / R.world) : 0.0;
+            if (!c.use_grad_clip)
+                cad::check(cad_clip_grad_norm(model.handle(), INFINITY, 1.f / R.world, nullptr), "noclip");
             opt.step();
-            const float lv = l.to_host()[0];   // loss.item<float>() (:307)
+            if (comm) comm->allreduce(l.data, 5);   // the logged loss: mean over replicas
+            const float lv = l.to_host()[0] / R.world;   // loss.item<float>() (:307)
             if (!std::isfinite(lv)) throw std::runtime_error("non-finite loss at step " + std::to_string(global_step));
-            total += (double)lv * n;
-            seen += n;
+            total += (double)lv * sh.n * R.world;
+            seen += (int64_t)sh.n * R.world;
             ++global_step;
-            if ((bi + 1) % c.log_interval == 0 || bi == nb - 1) {
+            if (lead && ((bi + 1) % c.log_interval == 0 || bi == nb - 1)) {
                 std::cout << "\r  [" << (100 * (bi + 1) / nb) << "%] Batch " << (bi + 1) << "/" << nb
                           << " | Loss: " << lv << std::flush;
                 if (tb) tb << "batch_loss/train," << global_step << "," << lv << "\ntraining/gradient_norm,"
                            << global_step << "," << gnorm << "\n";
             }
         }
+        if (!lead) continue;   // validation, logs and checkpoints: rank 0 (identical replicas)
         std::cout << "\n";
-        const float train_loss = (float)(total / std::max(1, seen));
+        const float train_loss = (float)(total / std::max<int64_t>(1, seen));
         float val_loss = 0.f;
         DepthMetrics vm{};
         if (c.val_interval > 0 && epoch % c.val_interval == 0 && c.n_val > 0) {   // validateEpoch :339-395
@@ -373,8 +585,10 @@ int run(const Args& args) {
             save_checkpoint(c.checkpoint_dir + "/" + c.experiment_name + "_epoch_" + std::to_string(epoch) + ".cadckpt",
                             model, opt);
     }
-    save_checkpoint(c.checkpoint_dir + "/final_model.cadckpt", model, opt);
-    std::cout << "Training complete.\n";
+    if (lead) {
+        save_checkpoint(c.checkpoint_dir + "/final_model.cadckpt", model, opt);
+        std::cout << "Training complete.\n";
+    }
     return 0;
 }
 

@@ -141,6 +141,10 @@ struct Up {
 
 }  // namespace
 
+namespace cad {
+void set_last_error(const std::string& msg) { g_err = msg; }
+}  // namespace cad
+
 struct cad_unet {
     int device = 0;
     int model = CAD_MODEL_BASELINE;
@@ -1045,6 +1049,27 @@ cad_status cad_unet_forward_cam(cad_unet* h, const float* rgb, const float* cam4
 
 int cad_unet_num_stages(const cad_unet*) { return kStages; }
 
+cad_status cad_model_grad_layout(int model, int in_channels, int init_features, int* nstages, int64_t stage_off[16],
+                                 int64_t stage_cnt[16], int64_t* n_flat) {
+    return guard([&] {
+        require(model == CAD_MODEL_BASELINE || model == CAD_MODEL_INTRINSICS_FILM || model == CAD_MODEL_RAY_FILM,
+                "unknown model kind");
+        require(in_channels == 3 && init_features >= 4 && init_features % 4 == 0, "bad model description");
+        cad_unet t;   // tables only: no device memory is touched
+        t.model = model;
+        t.in_ch = in_channels;
+        t.f = init_features;
+        build_tables(&t);
+        compute_stage_ranges(&t);
+        if (nstages) *nstages = kStages;
+        for (int s = 0; s < kStages; ++s) {
+            if (stage_off) stage_off[s] = t.stage_range[s].first;
+            if (stage_cnt) stage_cnt[s] = t.stage_range[s].second;
+        }
+        if (n_flat) *n_flat = t.n_flat;
+    });
+}
+
 cad_status cad_unet_backward_stage(cad_unet* h, int stage, const float* ddepth, void* stream) {
     return guard([&] {
         require(h->have_fwd, "backward needs a preceding train-mode forward", CAD_ERR_STATE);
@@ -1171,11 +1196,16 @@ void cad_loss_destroy(cad_loss* l) {
 }
 cad_status cad_loss_forward_backward(cad_loss* l, const float* pred, const float* gt, const float* rgb, const float* K,
                                      int B, float* loss5, float* dpred, void* stream) {
+    return cad_loss_forward_backward_masked(l, pred, gt, rgb, K, nullptr, B, loss5, dpred, stream);
+}
+cad_status cad_loss_forward_backward_masked(cad_loss* l, const float* pred, const float* gt, const float* rgb,
+                                            const float* K, const uint8_t* mask, int B, float* loss5, float* dpred,
+                                            void* stream) {
     return guard([&] {
         require(pred && gt && rgb && K && dpred, "null tensor");
         require(B >= 1 && B <= l->Bmax, "batch exceeds max_batch");
         HIPCHK(hipSetDevice(l->device));
-        cad::loss_fwd_bwd(pred, gt, rgb, K, B, l->H, l->W, l->w, loss5 ? loss5 : l->out5, dpred, l->ws, S(stream));
+        cad::loss_fwd_bwd(pred, gt, rgb, K, mask, B, l->H, l->W, l->w, loss5 ? loss5 : l->out5, dpred, l->ws, S(stream));
         if (loss5) HIPCHK(hipMemcpyAsync(l->out5, loss5, 5 * sizeof(float), hipMemcpyDeviceToDevice, S(stream)));
         HIPCHK(hipGetLastError());
     });

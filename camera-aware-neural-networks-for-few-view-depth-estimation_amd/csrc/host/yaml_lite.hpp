@@ -93,13 +93,18 @@ struct Line {
     std::string text;
 };
 
-inline std::shared_ptr<Node> parse_block(const std::vector<Line>& L, size_t& i, int indent) {
+inline bool is_item(const Line& ln) { return ln.text.rfind("- ", 0) == 0 || ln.text == "-"; }
+
+// list_only: a block sequence written at its key's own indentation ("key:\n- a\n- b", the form
+// yaml.safe_dump emits) ends at the first line of that indentation that is not an item
+inline std::shared_ptr<Node> parse_block(const std::vector<Line>& L, size_t& i, int indent, bool list_only = false) {
     auto node = std::make_shared<Node>();
     while (i < L.size() && L[i].indent >= indent) {
         const Line& ln = L[i];
+        if (list_only && ln.indent == indent && !is_item(ln)) break;
         if (ln.indent > indent && node->kind == Node::Null) indent = ln.indent;
         if (ln.indent != indent) throw std::runtime_error("yaml: bad indentation near '" + ln.text + "'");
-        if (ln.text.rfind("- ", 0) == 0 || ln.text == "-") {
+        if (is_item(ln)) {
             node->kind = Node::List;
             std::string item = ln.text.size() > 1 ? trim(ln.text.substr(2)) : "";
             ++i;
@@ -115,12 +120,26 @@ inline std::shared_ptr<Node> parse_block(const std::vector<Line>& L, size_t& i, 
         ++i;
         if (rest.empty()) {
             if (i < L.size() && L[i].indent > indent) node->map.push_back({key, parse_block(L, i, L[i].indent)});
+            else if (i < L.size() && L[i].indent == indent && is_item(L[i]))
+                node->map.push_back({key, parse_block(L, i, indent, true)});
             else node->map.push_back({key, std::make_shared<Node>()});
         } else {
             node->map.push_back({key, scalar_or_flow(rest)});
         }
     }
     return node;
+}
+
+// "key: ..." (a colon outside quotes followed by a blank or the end of the line)
+inline bool is_mapping_entry(const std::string& t) {
+    if (t.empty() || t.front() == '[') return false;
+    bool sq = false, dq = false;
+    for (size_t i = 0; i < t.size(); ++i) {
+        if (t[i] == '\'' && !dq) sq = !sq;
+        else if (t[i] == '"' && !sq) dq = !dq;
+        else if (t[i] == ':' && !sq && !dq && (i + 1 == t.size() || t[i + 1] == ' ')) return true;
+    }
+    return false;
 }
 
 inline Node parse(const std::string& text) {
@@ -132,7 +151,14 @@ inline Node parse(const std::string& text) {
         if (trim(s).empty() || trim(s) == "---") continue;
         int ind = 0;
         while (ind < (int)s.size() && s[ind] == ' ') ++ind;
-        L.push_back({ind, trim(s)});
+        std::string t = trim(s);
+        // "- key: v" opens a mapping inside a list item: split it into "-" and "key: v" two columns in
+        while (t.rfind("- ", 0) == 0 && is_mapping_entry(trim(t.substr(2)))) {
+            L.push_back({ind, "-"});
+            ind += 2;
+            t = trim(t.substr(2));
+        }
+        L.push_back({ind, t});
     }
     size_t i = 0;
     if (L.empty()) return Node();

@@ -487,19 +487,22 @@ __device__ __forceinline__ void gemm_epilogue_t(const GemmArgs& a, const floatx1
                 epi.block(a, m0 + wm * 32 * MI + i * 32 + 4 * (lane >> 5), n0 + wn * 32 * NJ + j * 32 + (lane & 31),
                           acc[i][j]);
                 continue;
-            } else {
+            }
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const int n = n0 + wn * 32 * NJ + j * 32 + (lane & 31);
-                    const int mr = wm * 32 * MI + i * 32 + 4 * (lane >> 5) + 8 * g;   // tile-relative row
+            for (int g = 0; g < 4; ++g) {
+                const int n = n0 + wn * 32 * NJ + j * 32 + (lane & 31);
+                const int mr = wm * 32 * MI + i * 32 + 4 * (lane >> 5) + 8 * g;   // tile-relative row
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = acc[i][j][4 * g + r];
+                if constexpr (!is_structured<Epi>::value) {
                     const uint32_t lo = n < a.N ? (uint32_t)(mr * ldc4 + (int64_t)n * 4) : kOOB;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const float v = acc[i][j][4 * g + r];
-                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rs,
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[r]), rs,
                                                               lo + (uint32_t)(r * ldc4), 0, 0);
                         if constexpr (Epi::STATS) {
-                            const float vm = m0 + mr + r < a.M ? v : 0.f;
+                            const float vm = m0 + mr + r < a.M ? v[r] : 0.f;
                             ssum[j] += vm;
                             ssq[j] += vm * vm;
                         }

@@ -115,9 +115,10 @@ struct LossWorkspace {
 };
 int64_t loss_workspace_floats(int B, int H, int W);
 int64_t loss_part_doubles(int B, int H, int W);
-// total/components -> out[5] = {total, si, grad, smooth, reproj}; dpred = dL/dpred
-void loss_fwd_bwd(const float* pred, const float* gt, const float* rgb, const float* K, int B, int H,
-                  int W, const float w[4], float* out5, float* dpred, LossWorkspace ws, hipStream_t st);
+// total/components -> out[5] = {total, si, grad, smooth, reproj}; dpred = dL/dpred.  mask (nullable,
+// B*H*W bytes, nonzero = valid) replaces gt > eps in the SI and reprojection terms (valid_mask)
+void loss_fwd_bwd(const float* pred, const float* gt, const float* rgb, const float* K, const uint8_t* mask, int B,
+                  int H, int W, const float w[4], float* out5, float* dpred, LossWorkspace ws, hipStream_t st);
 
 // ---------------- optimizer (optim_kernels.hip) ----------------
 int sumsq_blocks(int64_t n);

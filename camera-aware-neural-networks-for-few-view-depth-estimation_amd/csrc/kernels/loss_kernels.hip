@@ -4,12 +4,12 @@
 // atomics, bitwise-reproducible), one pooled pyramid, one elementwise dL/dpred pass.
 //
 // Semantics reproduced (file:line in /root/reference/src/loss/depth_loss.h):
-//   SI      :33-64   mask gt>eps (global over batch); d = log(clamp p) - log(clamp g);
+//   SI      :33-64   mask gt>eps (global over batch) or the caller's valid_mask; d = log(clamp p) - log(clamp g);
 //                    L = sum d^2/n - lam (sum d)^2/n^2; n == 0 -> 0 and no gradient.
 //   grad    :95-166  4 scales, avg_pool2d(k=2^s) then log(clamp), forward differences, L1 means,
 //                    mask IGNORED (invalid gt contributes log(1e-6)), /num_scales.
 //   smooth  :189-234 per-sample mean normalisation, |dI| averaged over the 3 channels, exp(-|dI|).
-//   reproj  :268-331 integer pixel grid, eps added to fx/fy and inside the sqrt, mean over mask.
+//   reproj  :268-331 integer pixel grid, eps added to fx/fy and inside the sqrt, mean over the same mask.
 // clamp(x, eps, 1000) passes gradient where eps <= x <= 1000; |x|' = sgn(x) with sgn(0) = 0.
 #include <algorithm>
 
@@ -65,7 +65,8 @@ enum { S_N = 0, S_SD, S_SD2, S_SE, S_GX0, S_GY0 = S_GX0 + kScales, S_SMX = S_GY0
 
 // pass A: SI + reproj sums (global) and per-sample sum(pred)
 __global__ __launch_bounds__(kTPB) void k_passA(const float* __restrict__ pred, const float* __restrict__ gt,
-                                                const float* __restrict__ K, Geo g, double* partA, int nb) {
+                                                const float* __restrict__ K, const uint8_t* __restrict__ mask, Geo g,
+                                                double* partA, int nb) {
     __shared__ double red[4 * 5];
     const int b = blockIdx.y;
     const int64_t HW = (int64_t)g.H * g.W;
@@ -75,7 +76,7 @@ __global__ __launch_bounds__(kTPB) void k_passA(const float* __restrict__ pred, 
     for (int64_t i = (int64_t)blockIdx.x * kTPB + threadIdx.x; i < HW; i += (int64_t)nb * kTPB) {
         const float p = pred[b * HW + i], t = gt[b * HW + i];
         v[4] += p;
-        if (t > kEps) {
+        if (mask ? mask[b * HW + i] != 0 : t > kEps) {
             const float d = logf(clampf(p)) - logf(clampf(t));
             v[0] += 1.0;
             v[1] += d;
@@ -286,7 +287,8 @@ __device__ float dgrad_scale(const float* pred, const float* gt, const float* lo
 }
 
 __global__ void k_dpred(const float* __restrict__ pred, const float* __restrict__ gt, const float* __restrict__ rgb,
-                        const float* __restrict__ K, const float* __restrict__ avgP, const float* __restrict__ logP,
+                        const float* __restrict__ K, const uint8_t* __restrict__ mask, const float* __restrict__ avgP,
+                        const float* __restrict__ logP,
                         const float* __restrict__ logG, Geo g, const double* dsc, float w0, float w1, float w2,
                         float w3, SmoothCtx c, float* __restrict__ dpred) {
     const int64_t HW = (int64_t)g.H * g.W, n = (int64_t)g.B * HW;
@@ -299,7 +301,7 @@ __global__ void k_dpred(const float* __restrict__ pred, const float* __restrict_
         const int x = (int)(pi % g.W), y = (int)(pi / g.W);
         const float p = pred[i], t = gt[i];
         float grad = 0.f;
-        if (t > kEps && cnt > 0) {
+        if ((mask ? mask[i] != 0 : t > kEps) && cnt > 0) {
             // SI
             const float d = logf(clampf(p)) - logf(clampf(t));
             const float dd = 2.f * d * inv_n - sd_term;
@@ -368,8 +370,8 @@ int64_t loss_part_doubles(int B, int H, int W) {
     return (int64_t)B * nb * 5 + 1024 * 2 * kScales + (int64_t)B * nb * 3 + S_PB + 2 * B + 64;
 }
 
-void loss_fwd_bwd(const float* pred, const float* gt, const float* rgb, const float* K, int B, int H, int W,
-                  const float w[4], float* out5, float* dpred, LossWorkspace ws, hipStream_t st) {
+void loss_fwd_bwd(const float* pred, const float* gt, const float* rgb, const float* K, const uint8_t* mask, int B,
+                  int H, int W, const float w[4], float* out5, float* dpred, LossWorkspace ws, hipStream_t st) {
     Geo g = make_geo(B, H, W);
     const int64_t HW = (int64_t)H * W;
     const int nb = nb_per_sample(B, HW);
@@ -387,7 +389,7 @@ void loss_fwd_bwd(const float* pred, const float* gt, const float* rgb, const fl
     c.inv_nx = 1.f / ((float)B * H * (W - 1));
     c.inv_ny = 1.f / ((float)B * (H - 1) * W);
 
-    hipLaunchKernelGGL(k_passA, dim3(nb, B), dim3(kTPB), 0, st, pred, gt, K, g, partA, nb);
+    hipLaunchKernelGGL(k_passA, dim3(nb, B), dim3(kTPB), 0, st, pred, gt, K, mask, g, partA, nb);
     for (int s = 1; s < kScales; ++s) {
         const int64_t n = (int64_t)B * g.Hs[s] * g.Ws[s];
         if (n > 0)
@@ -400,7 +402,7 @@ void loss_fwd_bwd(const float* pred, const float* gt, const float* rgb, const fl
     hipLaunchKernelGGL(k_reduce2, dim3(1), dim3(kTPB), 0, st, partS, nb, g, dsc, w[0], w[1], w[2], w[3], out5);
     const int64_t n = (int64_t)B * HW;
     hipLaunchKernelGGL(k_dpred, dim3(std::max(1, std::min(8192, cdiv(n, 256)))), dim3(256), 0, st, pred, gt, rgb, K,
-                       avgP, logP, logG, g, dsc, w[0], w[1], w[2], w[3], c, dpred);
+                       mask, avgP, logP, logG, g, dsc, w[0], w[1], w[2], w[3], c, dpred);
 }
 
 }  // namespace cad

@@ -261,28 +261,35 @@ class Adam:
 
 
 class CombinedDepthLoss:
-    """CombinedDepthLoss(si_weight, grad_weight, smooth_weight, reproj_weight) with its backward."""
+    """CombinedDepthLoss(si_weight, grad_weight, smooth_weight, reproj_weight) with its backward
+    (depth_loss.h:366-479).  forward_with_intrinsics / forward take the reference's optional
+    valid_mask (bool or uint8 device tensor (B,1,H,W)); it replaces gt > 1e-6 in the SI and
+    reprojection terms, the gradient-matching term ignores it (depth_loss.h:137)."""
 
     def __init__(self, si_weight=1.0, grad_weight=0.1, smooth_weight=0.001, reproj_weight=0.01, *, batch, height,
                  width, device=0):
         self.lib = _abi.load()
         self.device = torch.device("cuda", device)
         self.weights = (si_weight, grad_weight, smooth_weight, reproj_weight)
-        self.height, self.width = height, width
+        self.batch, self.height, self.width = batch, height, width
+        self.h = self._create(reproj_weight)
+        self.h_noreproj = None   # forward() (no reprojection term), created on first use
+
+    def _create(self, reproj_weight):
         h = C.c_void_p()
-        check(self.lib.cad_loss_create(si_weight, grad_weight, smooth_weight, reproj_weight, batch, height, width,
-                                       device, C.byref(h)), "cad_loss_create")
-        self.h = h
+        si, gr, sm, _ = self.weights
+        check(self.lib.cad_loss_create(si, gr, sm, reproj_weight, self.batch, self.height, self.width,
+                                       self.device.index or 0, C.byref(h)), "cad_loss_create")
+        return h
 
     def __del__(self):
-        h = getattr(self, "h", None)
-        if h is not None and h.value:
-            self.lib.cad_loss_destroy(h)
-            self.h = None
+        for attr in ("h", "h_noreproj"):
+            h = getattr(self, attr, None)
+            if h is not None and h.value:
+                self.lib.cad_loss_destroy(h)
+                setattr(self, attr, None)
 
-    def forward_with_intrinsics(self, pred, gt, image, intrinsics, loss5=None, dpred=None):
-        """forwardWithIntrinsics + backward. Returns (loss5, dpred): loss5 = device tensor
-        [total, si, grad, smooth, reproj]; dpred = dL/dpred (B,1,H,W)."""
+    def _run(self, h, pred, gt, image, intrinsics, valid_mask, loss5, dpred):
         B = pred.shape[0]
         assert pred.shape[2] == self.height and pred.shape[3] == self.width
         K = intrinsics.reshape(B, 3, 3).contiguous()
@@ -290,18 +297,47 @@ class CombinedDepthLoss:
             loss5 = torch.empty(5, dtype=torch.float32, device=self.device)
         if dpred is None:
             dpred = torch.empty_like(pred)
-        check(self.lib.cad_loss_forward_backward(self.h, _ptr(pred), _ptr(gt), _ptr(image), _ptr(K), B, _ptr(loss5),
-                                                 _ptr(dpred), _stream(self.device)), "cad_loss_forward_backward")
+        m = None
+        if valid_mask is not None:
+            assert valid_mask.numel() == pred.numel(), "valid_mask must be (B,1,H,W)"
+            mt = valid_mask.reshape(pred.shape).to(torch.uint8).contiguous()
+            m = C.c_void_p(mt.data_ptr())
+        check(self.lib.cad_loss_forward_backward_masked(h, _ptr(pred), _ptr(gt), _ptr(image), _ptr(K), m, B,
+                                                        _ptr(loss5), _ptr(dpred), _stream(self.device)),
+              "cad_loss_forward_backward")
         return loss5, dpred
+
+    def forward_with_intrinsics(self, pred, gt, image, intrinsics, valid_mask=None, loss5=None, dpred=None):
+        """forwardWithIntrinsics + backward. Returns (loss5, dpred): loss5 = device tensor
+        [total, si, grad, smooth, reproj]; dpred = dL/dpred (B,1,H,W)."""
+        return self._run(self.h, pred, gt, image, intrinsics, valid_mask, loss5, dpred)
 
     forwardWithIntrinsics = forward_with_intrinsics
 
-    def get_components_with_intrinsics(self, pred, gt, image, intrinsics):
-        loss5, _ = self.forward_with_intrinsics(pred, gt, image, intrinsics)
+    def forward(self, pred, gt, image, valid_mask=None, loss5=None, dpred=None):
+        """forward (depth_loss.h:390-404): SI + grad + smooth, no reprojection term (the kernels still
+        take intrinsics for their pixel grid; identity K is passed)."""
+        if self.h_noreproj is None:
+            self.h_noreproj = self._create(0.0)
+        B = pred.shape[0]
+        K = torch.eye(3, dtype=torch.float32, device=self.device).expand(B, 3, 3).contiguous()
+        return self._run(self.h_noreproj, pred, gt, image, K, valid_mask, loss5, dpred)
+
+    def get_components_with_intrinsics(self, pred, gt, image, intrinsics, valid_mask=None):
+        """getComponentsWithIntrinsics: the four terms (host floats); scratch outputs of its own, so a
+        caller's loss5 / dL/dpred are left as they were."""
+        loss5, _ = self.forward_with_intrinsics(pred, gt, image, intrinsics, valid_mask)
         v = loss5.cpu().tolist()
         return {"si_loss": v[1], "grad_loss": v[2], "smooth_loss": v[3], "reproj_loss": v[4]}
 
     getComponentsWithIntrinsics = get_components_with_intrinsics
+
+    def get_components(self, pred, gt, image, valid_mask=None):
+        loss5, _ = self.forward(pred, gt, image, valid_mask)
+        v = loss5.cpu().tolist()
+        return {"si_loss": v[1], "grad_loss": v[2], "smooth_loss": v[3]}
+
+    getComponents = get_components
 
 
 def depth_metrics(pred: torch.Tensor, gt: torch.Tensor) -> dict:

@@ -31,6 +31,13 @@
  *                                   enhanced.h:97-101, :304
  *   cad_unet_flat                   flat gradient slab for the data-parallel RCCL all-reduce (new:
  *                                   the reference is single-device)
+ *   cad_comm_* / cad_grad_allreduce / cad_unet_backward_allreduce
+ *                                   data-parallel replicas over RCCL (new; SURVEY.md §8(b) proposal
+ *                                   cad_grad_allreduce, §8(e) semantics; hardware.num_gpus /
+ *                                   distributed keys of configs/train_config.yaml:178-183, which the
+ *                                   reference parses but never uses)
+ *   cad_loss_forward_backward_masked forwardWithIntrinsics(pred, gt, image, K, valid_mask)
+ *                                   depth_loss.h:416-433 with the optional mask
  *   cad_depth_metrics               computeDepthMetrics (abs_rel ...)          enhanced.h:400-439
  *   cad_ray_directions              RayDirectionComputer::computeRayDirections
  *                                   src/preprocessing/ray_direction_computer.cpp:17-62
@@ -177,6 +184,45 @@ int64_t cad_adam_step_count(const cad_adam* a);
 cad_status cad_adam_state(cad_adam* a, float** m, float** v);
 cad_status cad_adam_set_step_count(cad_adam* a, int64_t step);
 
+/* ---- data-parallel gradient exchange: RCCL over xGMI, one process per GPU (new: the reference is
+ * single-device).  Semantics: every replica runs the same step on
+ * its own shard of the global batch (BN statistics and loss masks per replica); the gradient slab is
+ * SUM-all-reduced and the 1/world mean folded into cad_clip_grad_norm(.., prescale = 1/world);
+ * clip and Adam are then identical on every replica. ---- */
+typedef struct cad_comm cad_comm;
+#define CAD_COMM_ID_BYTES 128
+#define CAD_REDUCE_SUM 0
+#define CAD_REDUCE_MAX 1
+/* rank 0 draws the communicator id (ncclGetUniqueId) and hands its bytes to every rank */
+cad_status cad_comm_get_unique_id(uint8_t id[CAD_COMM_ID_BYTES]);
+/* collective: every rank of the job calls it with the same id (ncclCommInitRank) */
+cad_status cad_comm_create(const uint8_t id[CAD_COMM_ID_BYTES], int nranks, int rank, int device, cad_comm** out);
+void cad_comm_destroy(cad_comm* c);
+int cad_comm_rank(const cad_comm* c);
+int cad_comm_size(const cad_comm* c);
+/* in-place fp32 all-reduce / broadcast on `stream` (e.g. loss and metric scalars, initial weights) */
+cad_status cad_comm_allreduce(cad_comm* c, float* buf, int64_t count, int op, void* stream);
+cad_status cad_comm_broadcast(cad_comm* c, float* buf, int64_t count, int root, void* stream);
+/* the flat parameter slab of `h` from rank `root` (identical replicas at start / after a resume) */
+cad_status cad_comm_broadcast_params(cad_unet* h, cad_comm* c, int root, void* stream);
+/* SUM all-reduce of the whole gradient slab after a backward (no overlap; SURVEY §8(b)'s proposal) */
+cad_status cad_grad_allreduce(cad_unet* h, cad_comm* c, void* stream);
+/* loss.backward() with the exchange overlapped: every backward stage is enqueued on `stream`; as soon
+ * as the stages of a bucket (>= bucket_elems floats, decoder first, cad_plan_grad_buckets) are
+ * enqueued, its SUM all-reduce is issued on the communicator's stream behind an event, so RCCL runs
+ * while the remaining dgrad/wgrad kernels do; `stream` finally waits for every all-reduce. */
+cad_status cad_unet_backward_allreduce(cad_unet* h, cad_comm* c, const float* ddepth, int64_t bucket_elems,
+                                       void* stream);
+/* the bucket plan (host only): consecutive backward stages [stage_off, +stage_cnt) grouped greedily
+ * into contiguous buckets of >= bucket_elems floats (the last takes the rest).  Writes up to nstages
+ * buckets (nullable outputs); returns the bucket count, or -1 on bad input. */
+int cad_plan_grad_buckets(const int64_t* stage_off, const int64_t* stage_cnt, int nstages, int64_t bucket_elems,
+                          int64_t* bucket_off, int64_t* bucket_cnt, int* bucket_last_stage);
+/* host only (no device): the flat gradient slab layout of a model family — backward stage count (at
+ * most 16) and each stage's [offset, offset+count) — as cad_unet_stage_grad_range reports it */
+cad_status cad_model_grad_layout(int model, int in_channels, int init_features, int* nstages, int64_t stage_off[16],
+                                 int64_t stage_cnt[16], int64_t* n_flat);
+
 /* ---- loss: CombinedDepthLoss ---- */
 cad_status cad_loss_create(float si_weight, float grad_weight, float smooth_weight, float reproj_weight,
                            int max_batch, int height, int width, int device, cad_loss** out);
@@ -185,6 +231,13 @@ void cad_loss_destroy(cad_loss* l);
  * dpred (device, B*H*W) = dL/dpred.  K (B,3,3) row-major. */
 cad_status cad_loss_forward_backward(cad_loss* l, const float* pred, const float* gt, const float* rgb,
                                      const float* K, int B, float* loss5, float* dpred, void* stream);
+/* the same with forwardWithIntrinsics' optional valid_mask (depth_loss.h:416-433): mask (device,
+ * B*H*W bytes, nonzero = valid) replaces the default gt > 1e-6 mask of the scale-invariant and
+ * reprojection terms (:38-40, :320-322); the gradient-matching term ignores it like the reference
+ * (:137) and smoothness never takes one (:189).  mask == NULL: cad_loss_forward_backward. */
+cad_status cad_loss_forward_backward_masked(cad_loss* l, const float* pred, const float* gt, const float* rgb,
+                                            const float* K, const uint8_t* mask, int B, float* loss5, float* dpred,
+                                            void* stream);
 /* getComponentsWithIntrinsics: host copy of {total, si, grad, smooth, reproj} of the last call */
 cad_status cad_loss_get_components(cad_loss* l, float out5[5], void* stream);
 

@@ -11,10 +11,12 @@
 #ifndef CAD_CAD_HPP
 #define CAD_CAD_HPP
 
+#include <array>
 #include <cstdint>
 #include <map>
 #include <memory>
 #include <numeric>
+#include <optional>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -59,6 +61,28 @@ struct DeviceTensor {
         std::vector<float> h((size_t)numel());
         check(cad_memcpy(h.data(), data, numel() * (int64_t)sizeof(float), 1, nullptr), "cad_memcpy d2h");
         return h;
+    }
+};
+
+// device bool mask (B,1,H,W) as bytes, nonzero = valid: the reference's optional valid_mask tensor
+struct DeviceMask {
+    uint8_t* data = nullptr;
+    std::vector<int64_t> shape;
+    int device = 0;
+    std::shared_ptr<void> owner;
+    int64_t numel() const {
+        return std::accumulate(shape.begin(), shape.end(), int64_t(1), std::multiplies<int64_t>());
+    }
+    static DeviceMask from_host(const uint8_t* host, std::vector<int64_t> shape, int device = 0) {
+        DeviceMask m;
+        m.shape = std::move(shape);
+        m.device = device;
+        void* p = nullptr;
+        check(cad_malloc(device, m.numel(), &p), "cad_malloc");
+        m.data = static_cast<uint8_t*>(p);
+        m.owner = std::shared_ptr<void>(p, [](void* q) { cad_free(q); });
+        check(cad_memcpy(m.data, host, m.numel(), 0, nullptr), "cad_memcpy h2d");
+        return m;
     }
 };
 
@@ -212,26 +236,31 @@ public:
     CombinedDepthLoss(const CombinedDepthLoss&) = delete;
     CombinedDepthLoss& operator=(const CombinedDepthLoss&) = delete;
 
-    // forwardWithIntrinsics (depth_loss.h:416-433): returns the 5-float device tensor
-    // {total, si, grad, smooth, reproj}; dL/dpred is left in dpred()
+    // forwardWithIntrinsics(pred, gt, image, intrinsics, valid_mask) (depth_loss.h:416-433): returns the
+    // 5-float device tensor {total, si, grad, smooth, reproj}; dL/dpred is left in dpred().  valid_mask
+    // replaces gt > 1e-6 in the SI and reprojection terms (grad matching ignores it, :137).
     DeviceTensor forwardWithIntrinsics(const DeviceTensor& pred, const DeviceTensor& gt, const DeviceTensor& image,
-                                       const DeviceTensor& intrinsics, void* stream = nullptr) {
-        return run(get(true), pred, gt, image, intrinsics, stream);
+                                       const DeviceTensor& intrinsics,
+                                       const std::optional<cad::DeviceMask>& valid_mask = std::nullopt,
+                                       void* stream = nullptr) {
+        return run(get(true), pred, gt, image, intrinsics, valid_mask, stream);
     }
-    // forward (depth_loss.h:390-404): SI + grad + smooth (no reprojection term)
+    // forward(pred, gt, image, valid_mask) (depth_loss.h:390-404): SI + grad + smooth, no reprojection
     DeviceTensor forward(const DeviceTensor& pred, const DeviceTensor& gt, const DeviceTensor& image,
-                         const DeviceTensor& intrinsics, void* stream = nullptr) {
-        return run(get(false), pred, gt, image, intrinsics, stream);
+                         const std::optional<cad::DeviceMask>& valid_mask = std::nullopt, void* stream = nullptr) {
+        return run(get(false), pred, gt, image, identity_K(pred.size(0)), valid_mask, stream);
     }
     std::map<std::string, float> getComponentsWithIntrinsics(const DeviceTensor& pred, const DeviceTensor& gt,
-                                                             const DeviceTensor& image, const DeviceTensor& K) {
-        DeviceTensor l = forwardWithIntrinsics(pred, gt, image, K);
+                                                             const DeviceTensor& image, const DeviceTensor& K,
+                                                             const std::optional<cad::DeviceMask>& valid_mask = std::nullopt) {
+        DeviceTensor l = forwardWithIntrinsics(pred, gt, image, K, valid_mask);
         auto v = l.to_host();
         return {{"si_loss", v[1]}, {"grad_loss", v[2]}, {"smooth_loss", v[3]}, {"reproj_loss", v[4]}};
     }
     std::map<std::string, float> getComponents(const DeviceTensor& pred, const DeviceTensor& gt,
-                                               const DeviceTensor& image, const DeviceTensor& K) {
-        DeviceTensor l = forward(pred, gt, image, K);
+                                               const DeviceTensor& image,
+                                               const std::optional<cad::DeviceMask>& valid_mask = std::nullopt) {
+        DeviceTensor l = forward(pred, gt, image, valid_mask);
         auto v = l.to_host();
         return {{"si_loss", v[1]}, {"grad_loss", v[2]}, {"smooth_loss", v[3]}};
     }
@@ -246,18 +275,29 @@ private:
         return h;
     }
     DeviceTensor run(cad_loss* h, const DeviceTensor& pred, const DeviceTensor& gt, const DeviceTensor& image,
-                     const DeviceTensor& K, void* stream) {
+                     const DeviceTensor& K, const std::optional<cad::DeviceMask>& mask, void* stream) {
+        if (mask && mask->numel() != pred.numel()) throw std::runtime_error("valid_mask must be (B,1,H,W)");
         if (dpred_.numel() != pred.numel()) dpred_ = DeviceTensor::empty(pred.shape, ws_.device);
         DeviceTensor l = DeviceTensor::empty({5}, ws_.device);
-        cad::check(cad_loss_forward_backward(h, pred.data, gt.data, image.data, K.data, (int)pred.size(0), l.data,
-                                             dpred_.data, stream), "forwardWithIntrinsics");
+        cad::check(cad_loss_forward_backward_masked(h, pred.data, gt.data, image.data, K.data, mask ? mask->data : nullptr,
+                                                    (int)pred.size(0), l.data, dpred_.data, stream),
+                   "forwardWithIntrinsics");
         return l;
+    }
+    // the kernels take intrinsics for their pixel grid even when the reprojection weight is 0
+    const DeviceTensor& identity_K(int64_t B) {
+        if (eye_.numel() < B * 9) {
+            std::vector<float> h((size_t)(B * 9), 0.f);
+            for (int64_t b = 0; b < B; ++b) h[b * 9] = h[b * 9 + 4] = h[b * 9 + 8] = 1.f;
+            eye_ = DeviceTensor::from_host(h.data(), {B, 3, 3}, ws_.device);
+        }
+        return eye_;
     }
     float w_[4];
     cad::Workspace ws_;
     cad_loss* with_ = nullptr;
     cad_loss* without_ = nullptr;
-    DeviceTensor dpred_;
+    DeviceTensor dpred_, eye_;
 };
 
 namespace optim {
@@ -282,13 +322,53 @@ private:
 };
 }  // namespace optim
 
-// torch::nn::utils::clip_grad_norm_(model->parameters(), max_norm) -> total norm (synchronises)
-inline double clip_grad_norm_(BaselineUNetImpl& model, double max_norm, void* stream = nullptr) {
-    cad::check(cad_clip_grad_norm(model.handle(), (float)max_norm, 1.0f, stream), "clip_grad_norm_");
+// torch::nn::utils::clip_grad_norm_(model->parameters(), max_norm) -> total norm (synchronises).
+// prescale scales the gradients first (1/world after a SUM all-reduce: the norm of the mean gradient)
+inline double clip_grad_norm_(BaselineUNetImpl& model, double max_norm, void* stream = nullptr, double prescale = 1.0) {
+    cad::check(cad_clip_grad_norm(model.handle(), (float)max_norm, (float)prescale, stream), "clip_grad_norm_");
     float n = 0.f;
     cad::check(cad_unet_last_grad_norm(model.handle(), &n, stream), "clip_grad_norm_");
     return n;
 }
+
+// Data-parallel replicas over RCCL (new: the reference is single-device).  One
+// process per GPU; rank 0 draws the id (unique_id()) and every rank builds the communicator from it.
+namespace distributed {
+using UniqueId = std::array<uint8_t, CAD_COMM_ID_BYTES>;
+class Communicator {
+public:
+    static UniqueId unique_id() {
+        UniqueId id{};
+        cad::check(cad_comm_get_unique_id(id.data()), "cad_comm_get_unique_id");
+        return id;
+    }
+    Communicator(const UniqueId& id, int world_size, int rank, int device) {
+        cad::check(cad_comm_create(id.data(), world_size, rank, device, &h_), "cad_comm_create");
+    }
+    ~Communicator() { cad_comm_destroy(h_); }
+    Communicator(const Communicator&) = delete;
+    Communicator& operator=(const Communicator&) = delete;
+    int rank() const { return cad_comm_rank(h_); }
+    int size() const { return cad_comm_size(h_); }
+    void allreduce(float* buf, int64_t count, int op = CAD_REDUCE_SUM, void* stream = nullptr) {
+        cad::check(cad_comm_allreduce(h_, buf, count, op, stream), "cad_comm_allreduce");
+    }
+    // identical replicas: rank `root`'s parameters everywhere
+    void broadcast_parameters(BaselineUNetImpl& m, int root = 0, void* stream = nullptr) {
+        cad::check(cad_comm_broadcast_params(m.handle(), h_, root, stream), "cad_comm_broadcast_params");
+    }
+    // loss.backward() with the bucketed gradient all-reduce overlapped (decoder-first buckets)
+    void backward_allreduce(BaselineUNetImpl& m, const DeviceTensor& ddepth, int64_t bucket_elems = 25 << 18,
+                            void* stream = nullptr) {
+        cad::check(cad_unet_backward_allreduce(m.handle(), h_, ddepth.data, bucket_elems, stream),
+                   "cad_unet_backward_allreduce");
+    }
+    cad_comm* handle() const { return h_; }
+
+private:
+    cad_comm* h_ = nullptr;
+};
+}  // namespace distributed
 
 // computeDepthMetrics (tensorboard_trainer_enhanced.h:400-439), averaged over the batch
 struct DepthMetrics {

@@ -346,9 +346,10 @@ def unet_forward(x, p, bufs, train=True, max_depth=10.0, model="baseline", K=Non
 # --------------------------------------------------------------------------------------------
 # Losses (depth_loss.h)
 # --------------------------------------------------------------------------------------------
-def si_loss(pred, gt, lam=0.5, eps=EPS):
-    """ScaleInvariantLoss::forward (depth_loss.h:33-64): 0-dim result, zeros(1) when n == 0."""
-    mask = gt > eps
+def si_loss(pred, gt, lam=0.5, eps=EPS, valid_mask=None):
+    """ScaleInvariantLoss::forward (depth_loss.h:33-64): 0-dim result, zeros(1) when n == 0;
+    valid_mask (bool) replaces gt > eps (:38-40)."""
+    mask = valid_mask if valid_mask is not None else gt > eps
     pred = torch.clamp(pred, eps, 1000.0)
     gt = torch.clamp(gt, eps, 1000.0)
     d = (torch.log(pred) - torch.log(gt)).masked_select(mask)
@@ -393,8 +394,8 @@ def smooth_loss(pred, image, eps=EPS):
     return (dx * torch.exp(-ix)).mean() + (dy * torch.exp(-iy)).mean()
 
 
-def reproj_loss(pred, gt, K, eps=EPS):
-    """ReprojectionLoss::forward (depth_loss.h:268-331)."""
+def reproj_loss(pred, gt, K, eps=EPS, valid_mask=None):
+    """ReprojectionLoss::forward (depth_loss.h:268-331); valid_mask replaces gt > eps (:320-322)."""
     B, _, H, W = pred.shape
     if K.dim() == 2:
         K = K.unsqueeze(0).expand(B, 3, 3)
@@ -410,18 +411,19 @@ def reproj_loss(pred, gt, K, eps=EPS):
     tY = (gy - cy) * gt / (fy + eps)
     dX, dY, dZ = pX - tX, pY - tY, pred - gt
     err = torch.sqrt(dX * dX + dY * dY + dZ * dZ + eps)
-    e = err.masked_select(gt > eps)
+    e = err.masked_select(valid_mask if valid_mask is not None else gt > eps)
     if e.numel() == 0:
         return torch.zeros(1, dtype=pred.dtype)
     return e.mean()
 
 
-def combined_loss(pred, gt, image, K, weights=(1.0, 0.1, 0.001, 0.01)):
-    """CombinedDepthLoss::forwardWithIntrinsics (depth_loss.h:416-433). Returns (total, comps)."""
-    si = si_loss(pred, gt)
+def combined_loss(pred, gt, image, K, weights=(1.0, 0.1, 0.001, 0.01), valid_mask=None):
+    """CombinedDepthLoss::forwardWithIntrinsics (depth_loss.h:416-433). Returns (total, comps).
+    valid_mask reaches the SI and reprojection terms; the gradient-matching term ignores it (:137)."""
+    si = si_loss(pred, gt, valid_mask=valid_mask)
     gr = grad_loss(pred, gt)
     sm = smooth_loss(pred, image)
-    rp = reproj_loss(pred, gt, K)
+    rp = reproj_loss(pred, gt, K, valid_mask=valid_mask)
     w = [torch.tensor(float(x), dtype=torch.float32).item() for x in weights]
     total = w[0] * si + w[1] * gr + w[2] * sm + w[3] * rp
     comps = {"si_loss": float(si.detach()), "grad_loss": float(gr.detach()), "smooth_loss": float(sm.detach()),
@@ -429,10 +431,10 @@ def combined_loss(pred, gt, image, K, weights=(1.0, 0.1, 0.001, 0.01)):
     return total, comps
 
 
-def loss_and_dpred(pred, gt, image, K, weights=(1.0, 0.1, 0.001, 0.01)):
+def loss_and_dpred(pred, gt, image, K, weights=(1.0, 0.1, 0.001, 0.01), valid_mask=None):
     """Fused-loss reference: (total, comps, dL/dpred) for the GPU loss kernels' parity tests."""
     p = pred.detach().clone().requires_grad_(True)
-    total, comps = combined_loss(p, gt, image, K, weights)
+    total, comps = combined_loss(p, gt, image, K, weights, valid_mask)
     total.sum().backward()
     return float(total), comps, p.grad.detach()
 

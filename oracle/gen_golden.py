@@ -30,6 +30,8 @@ FIXTURES = {
     "loss_b2_120x160": ["--mode", "loss", "--B", "2", "--H", "120", "--W", "160"],
     "loss_b3_50x70": ["--mode", "loss", "--B", "3", "--H", "50", "--W", "70"],
     "loss_b2_32x48_allholes": ["--mode", "loss", "--B", "2", "--H", "32", "--W", "48", "--holes-all", "1"],
+    # forwardWithIntrinsics' optional valid_mask (depth_loss.h:416-433), independent of gt
+    "loss_b2_48x64_mask": ["--mode", "loss", "--B", "2", "--H", "48", "--W", "64", "--mask-seed", "77"],
 }
 
 

@@ -258,7 +258,7 @@ double abs_rel_per_sample(torch::Tensor pred, torch::Tensor gt) {
 
 struct Args {
     std::string mode = "golden", out = ".", model = "baseline", init = "default";
-    int f = 8, B = 2, H = 64, W = 64, steps = 3, threads = 1, warmup = 1, holes_all = 0;
+    int f = 8, B = 2, H = 64, W = 64, steps = 3, threads = 1, warmup = 1, holes_all = 0, mask_seed = 0;
     float w[4] = {1.0f, 0.1f, 0.001f, 0.01f};
     float lr = 1e-4f, wd = 1e-5f, clip = 1.0f;
 };
@@ -282,6 +282,7 @@ Args parse(int argc, char** argv) {
         else if (k == "--lr") a.lr = std::stof(v);
         else if (k == "--wd") a.wd = std::stof(v);
         else if (k == "--holes-all") a.holes_all = std::stoi(v);
+        else if (k == "--mask-seed") a.mask_seed = std::stoi(v);
         else { fprintf(stderr, "unknown arg %s\n", k.c_str()); exit(2); }
     }
     return a;
@@ -336,24 +337,35 @@ int main(int argc, char** argv) {
     if (a.mode == "loss") {
         // Loss-only golden: pred = 0.05 + 9.9*U[0,1) (seed 0xBEEF), gt/rgb/K from make_batch;
         // --holes-all makes every gt pixel invalid (the n == 0 branches of depth_loss.h:53,325).
+        // --mask-seed S passes forwardWithIntrinsics' optional valid_mask (:416-433): u01(S, i) < 0.8,
+        // independent of gt (so it also admits gt == 0 pixels, and drops valid ones).
         auto pred = torch::empty({a.B, 1, a.H, a.W});
         float* pp = pred.data_ptr<float>();
         for (int64_t i = 0; i < pred.numel(); ++i) pp[i] = 0.05f + 9.9f * u01(0xBEEF, i);
         if (a.holes_all) batch.gt.zero_();
+        torch::optional<torch::Tensor> mask = torch::nullopt;
+        torch::Tensor maskf;
+        if (a.mask_seed) {
+            maskf = torch::empty({a.B, 1, a.H, a.W});
+            float* mp = maskf.data_ptr<float>();
+            for (int64_t i = 0; i < maskf.numel(); ++i) mp[i] = u01((uint64_t)a.mask_seed, i) < 0.8f ? 1.f : 0.f;
+            mask = maskf > 0.5f;
+        }
         pred.requires_grad_(true);
-        auto total = loss_fn.forwardWithIntrinsics(pred, batch.gt, batch.rgb, batch.K);
+        auto total = loss_fn.forwardWithIntrinsics(pred, batch.gt, batch.rgb, batch.K, mask);
         total.backward();
         torch::NoGradGuard ng;
-        auto comps = loss_fn.getComponentsWithIntrinsics(pred.detach(), batch.gt, batch.rgb, batch.K);
+        auto comps = loss_fn.getComponentsWithIntrinsics(pred.detach(), batch.gt, batch.rgb, batch.K, mask);
         Dumper d(a.out);
         d.add("input.pred", pred);
         d.add("input.gt", batch.gt);
+        if (a.mask_seed) d.add("input.mask", maskf);
         d.add("dpred", pred.grad());
         std::ostringstream meta;
         meta.precision(9);
         meta << "{\"B\": " << a.B << ", \"H\": " << a.H << ", \"W\": " << a.W << ", \"weights\": ["
              << a.w[0] << ", " << a.w[1] << ", " << a.w[2] << ", " << a.w[3] << "], \"holes_all\": "
-             << a.holes_all << ", \"total\": " << total.item<float>() << ", \"total_dim\": " << total.dim()
+             << a.holes_all << ", \"mask_seed\": " << a.mask_seed << ", \"total\": " << total.item<float>() << ", \"total_dim\": " << total.dim()
              << ", \"components\": {";
         bool first = true;
         for (auto& kv : comps) { meta << (first ? "" : ", ") << "\"" << kv.first << "\": " << kv.second; first = false; }

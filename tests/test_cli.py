@@ -1,6 +1,8 @@
 """Drop-in CLI (build/train, the reference's ./build/train --config) and its YAML-subset reader.
 CPU: flags, error behaviour (train_main.cpp:503-506: "Error: <what>", exit 1), YAML parity with
 PyYAML on the shipped configs.  GPU: a short synthetic run, metrics.csv, checkpoints, resume."""
+import ctypes as C
+import json
 import os
 import subprocess
 
@@ -32,12 +34,21 @@ def _flatten(d, path=""):
     return out
 
 
+@pytest.mark.parametrize("dumped", [False, True])
 @pytest.mark.parametrize("cfg", ["train_config.yaml", "train_config_mi355x.yaml"])
-def test_yaml_lite_matches_pyyaml(tmp_path, cfg):
+def test_yaml_lite_matches_pyyaml(tmp_path, cfg, dumped):
+    """The shipped configs as written, and re-emitted by yaml.safe_dump (block lists at the key's own
+    indentation, quoting chosen by PyYAML) — the form tools that rewrite configs produce."""
     exe = tmp_path / "yaml_probe"
     subprocess.run(["g++", "-std=c++17", "-O1", "-o", str(exe), os.path.join(ROOT, "tests", "yaml_probe.cpp")],
                    check=True)
     path = os.path.join(ROOT, "configs", cfg)
+    if dumped:
+        d = yaml.safe_load(open(path))
+        d.setdefault("hardware", {})["gpu_ids"] = [3, 5]
+        d["hardware"]["nested"] = [{"a": 1, "b": [1, 2]}, {"c": "x y"}]
+        path = tmp_path / cfg
+        path.write_text(yaml.safe_dump(d))
     out = subprocess.run([str(exe), path], check=True, capture_output=True, text=True).stdout
     ours = dict(line.split("=", 1) for line in out.strip().splitlines())
     ref = _flatten(yaml.safe_load(open(path)))
@@ -85,3 +96,80 @@ def test_cli_train_resume(train_bin, tmp_path):
     assert "optimizer step 6" in r.stdout
     rows = (tmp_path / "logs" / "baseline_unet" / "metrics.csv").read_text().strip().splitlines()
     assert rows[-1].startswith("3,9,")
+
+
+def _dp_cfg(tmp_path, **hw):
+    cfg = {"data": {"dataset_name": "synthetic", "num_train_samples": 100, "num_val_samples": 8, "input_height": 64,
+                    "input_width": 64},
+           "model": {"init_features": 16}, "training": {"batch_size": 8, "num_epochs": 1},
+           "hardware": dict({"device": "cuda", "gpu_ids": [3, 5], "num_gpus": 2, "distributed": True,
+                             "backend": "nccl"}, **hw)}
+    p = tmp_path / "dp.yaml"
+    p.write_text(yaml.safe_dump(cfg))
+    return p
+
+
+def test_cli_data_parallel_plan(train_bin, tmp_path, cad):
+    """build/train's data-parallel plumbing on the CPU (--dry-run stops every rank before its first GPU
+    call and stands in for the collective): hardware.num_gpus ranks are started as child processes,
+    each bound to its gpu_ids entry; rank 0's communicator id reaches every rank through the
+    rendezvous file; each rank trains its own B-slice of the global batch (last partial global batch
+    dropped); the bucket plan is the library's (cad_plan_grad_buckets)."""
+    p = _dp_cfg(tmp_path)
+    r = subprocess.run([train_bin, "-c", str(p), "--dry-run"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    plans = sorted((json.loads(line) for line in r.stdout.strip().splitlines()), key=lambda d: d["rank"])
+    assert [d["rank"] for d in plans] == [0, 1] and all(d["world"] == 2 and d["communicator"] for d in plans)
+    assert [d["device"] for d in plans] == [3, 5]
+    assert plans[0]["id_hash"] == plans[1]["id_hash"]
+    assert [d["first_step_samples"] for d in plans] == [[0, 8], [8, 16]]
+    assert all(d["steps_per_epoch"] == 100 // 16 and d["global_batch"] == 16 for d in plans)
+    lib = cad.load_library()
+    ns, off, cnt, nf = C.c_int(), (C.c_int64 * 16)(), (C.c_int64 * 16)(), C.c_int64()
+    assert lib.cad_model_grad_layout(0, 3, 16, C.byref(ns), off, cnt, C.byref(nf)) == 0
+    bo, bc, bl = (C.c_int64 * 16)(), (C.c_int64 * 16)(), (C.c_int * 16)()
+    nb = lib.cad_plan_grad_buckets(off, cnt, ns.value, 25 << 18, bo, bc, bl)
+    assert plans[0]["buckets"] == [[bo[i], bc[i], bl[i]] for i in range(nb)] == plans[1]["buckets"]
+    assert plans[0]["n_flat"] == nf.value
+
+
+def test_cli_data_parallel_single_process_and_errors(train_bin, tmp_path):
+    # one GPU with distributed: true -> one process with a single-rank communicator
+    p = _dp_cfg(tmp_path, num_gpus=1, gpu_ids=[2])
+    r = subprocess.run([train_bin, "-c", str(p), "--dry-run"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout.strip())
+    assert (d["rank"], d["world"], d["device"], d["communicator"], d["steps_per_epoch"]) == (0, 1, 2, True, 13)
+    # distributed: false ignores num_gpus (the reference's default), no communicator
+    p = _dp_cfg(tmp_path, distributed=False)
+    d = json.loads(subprocess.run([train_bin, "-c", str(p), "--dry-run"], capture_output=True, text=True,
+                                  timeout=60).stdout.strip())
+    assert (d["world"], d["communicator"]) == (1, False)
+    # the gradient exchange is RCCL: another backend is refused with the reference's error contract
+    p = _dp_cfg(tmp_path, backend="gloo")
+    r = subprocess.run([train_bin, "-c", str(p), "--dry-run"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and r.stderr.startswith("Error: hardware.backend")
+
+
+@pytest.mark.gpu
+def test_cli_distributed_single_rank_matches_plain(train_bin, tmp_path):
+    """distributed: true on one GPU runs the RCCL path (communicator, parameter broadcast, bucketed
+    all-reduce overlapped with the backward, loss all-reduce) on a single-rank communicator: the
+    trajectory must equal the plain single-process run bit for bit."""
+    rows = {}
+    for dist in (False, True):
+        cfg = yaml.safe_load(open(os.path.join(ROOT, "configs", "train_config.yaml")))
+        cfg["data"].update(dataset_name="synthetic", num_train_samples=16, num_val_samples=8, input_height=64,
+                           input_width=64)
+        cfg["training"].update(num_epochs=2, batch_size=8)
+        cfg["checkpointing"]["checkpoint_dir"] = str(tmp_path / f"ckpt{dist}")
+        cfg["logging"]["log_dir"] = str(tmp_path / f"logs{dist}")
+        cfg["hardware"] = {"device": "cuda", "gpu_ids": [0], "num_gpus": 1, "distributed": dist, "backend": "nccl"}
+        p = tmp_path / f"cfg{dist}.yaml"
+        p.write_text(yaml.safe_dump(cfg))
+        r = subprocess.run([train_bin, "-c", str(p)], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        assert ("RCCL" in r.stdout) == dist
+        csv = (tmp_path / f"logs{dist}" / "baseline_unet" / "metrics.csv").read_text().strip().splitlines()
+        rows[dist] = [line.split(",")[:11] for line in csv[1:]]   # all but learning_rate, time
+    assert rows[True] == rows[False]

@@ -34,6 +34,16 @@ def _zero_grad_bias(name, B):
     return B > 1 and (name.endswith("film.fc1.bias") or name.endswith("film.fc2.bias"))
 
 
+def _zero_true_grad(name, B):
+    """Parameters whose exact gradient is 0, so every finite-precision path returns rounding noise:
+    the Linear biases in front of a train-mode BatchNorm1d (B > 1), and with B == 2 also those
+    Linears' weights — BatchNorm1d over two samples maps them to x_hat = +-1 exactly, and its
+    backward dx = (g/s)(dy - mean(dy) - x_hat mean(dy x_hat)) is then identically 0 (film_layer.h:85,91)."""
+    if _zero_grad_bias(name, B):
+        return True
+    return B == 2 and (name.endswith("film.fc1.weight") or name.endswith("film.fc2.weight"))
+
+
 @pytest.mark.parametrize("name", FILM)
 def test_film_train_steps_vs_reference_fixture(cad, dev, oracle, name):
     fx, meta = oracle.load_fixture(os.path.join(GOLDEN, name))
@@ -214,9 +224,9 @@ def test_film_train_step_bf16_engine_vs_oracle(cad, dev, oracle, bf16_engine, mo
     assert max_rel_err(pred.cpu(), e64["pred"]) < 5e-2
     grads = net.grads()
     for (n, _), g32, g64 in zip(oracle.param_spec(f, model=model), r["grads"], r64["grads"]):
-        if _zero_grad_bias(n, B):   # true gradient is 0: noise well below the weight-gradient scale
-            w = grads[n[: -len("bias")] + "weight"]
-            assert grads[n].abs().max().item() <= 1e-2 * w.abs().max().item() + 1e-12, n
+        if _zero_true_grad(n, B):   # true gradient is 0: noise well below the FiLM head's gradient scale
+            head = grads[n[: n.index("film.") + 5] + "fc_gamma.weight"]
+            assert grads[n].abs().max().item() <= 1e-2 * head.abs().max().item() + 1e-12, n
             continue
         ours, ref32 = max_rel_err(grads[n], g64), max_rel_err(g32, g64)
         cos = torch.nn.functional.cosine_similarity(grads[n].double().reshape(1, -1), g64.reshape(1, -1)).item()

@@ -11,7 +11,7 @@ from conftest import GOLDEN, max_rel_err
 
 pytestmark = pytest.mark.gpu
 
-LOSS_FIXTURES = ["loss_b2_120x160", "loss_b3_50x70", "loss_b2_32x48_allholes"]
+LOSS_FIXTURES = ["loss_b2_120x160", "loss_b3_50x70", "loss_b2_32x48_allholes", "loss_b2_48x64_mask"]
 
 
 def _pred(B, H, W):
@@ -29,7 +29,9 @@ def test_loss_vs_reference_fixture(cad, dev, oracle, name):
     gt = fx["input.gt"].numpy()
     loss = cad.CombinedDepthLoss(*meta["weights"], batch=B, height=H, width=W)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
-    loss5, dpred = loss.forward_with_intrinsics(t(pred), t(gt), t(rgb), t(K))
+    # forwardWithIntrinsics' optional valid_mask (depth_loss.h:416-433) when the fixture has one
+    mask = t(fx["input.mask"].numpy() > 0.5) if "input.mask" in fx else None
+    loss5, dpred = loss.forward_with_intrinsics(t(pred), t(gt), t(rgb), t(K), valid_mask=mask)
     v = loss5.cpu().numpy()
     comps = meta["components"]
     ref = [meta["total"], comps["si_loss"], comps["grad_loss"], comps["smooth_loss"], comps["reproj_loss"]]

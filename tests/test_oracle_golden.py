@@ -12,7 +12,7 @@ import torch
 from conftest import GOLDEN, max_rel_err
 
 TRAIN = ["train_f4_b2_64x64", "train_f4_b3_96x128_si"]
-LOSS = ["loss_b2_120x160", "loss_b3_50x70", "loss_b2_32x48_allholes"]
+LOSS = ["loss_b2_120x160", "loss_b3_50x70", "loss_b2_32x48_allholes", "loss_b2_48x64_mask"]
 
 
 @pytest.fixture(autouse=True)
@@ -89,8 +89,9 @@ def test_oracle_loss_vs_reference(oracle, name):
     fx, meta = oracle.load_fixture(os.path.join(GOLDEN, name))
     B, H, W = meta["B"], meta["H"], meta["W"]
     rgb, _, K = oracle.synth_batch(B, H, W)
+    mask = fx["input.mask"] > 0.5 if "input.mask" in fx else None   # forwardWithIntrinsics' valid_mask
     total, comps, dpred = oracle.loss_and_dpred(fx["input.pred"], fx["input.gt"], torch.from_numpy(rgb),
-                                                torch.from_numpy(K), meta["weights"])
+                                                torch.from_numpy(K), meta["weights"], valid_mask=mask)
     assert abs(total - meta["total"]) <= 1e-6 * max(1.0, abs(meta["total"]))
     for k, v in meta["components"].items():
         assert abs(comps[k] - v) <= 1e-6 * max(1.0, abs(v)), k
