@@ -396,6 +396,55 @@ class GradBucketer:
         self.pending = []
 
 
+class Communicator:
+    """RCCL communicator of libcad (cad_comm_* in cad.h; C++: cad::distributed::Communicator), the
+    data-parallel exchange build/train uses: one rank per GPU, rank 0's 128-byte unique id handed to
+    the others out of band (a file, a torch.distributed broadcast_object_list, ...).
+
+    backward_allreduce(model, ddepth) runs the backward with the decoder-first bucketed SUM
+    all-reduce issued on the communicator's own stream as each bucket's last stage is enqueued; the
+    caller's stream waits for the last one, so clip (prescale 1/world) and Adam see the reduced slab."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        lib = _abi.load()
+        buf = (C.c_uint8 * 128)()
+        check(lib.cad_comm_get_unique_id(buf), "cad_comm_get_unique_id")
+        return bytes(buf)
+
+    def __init__(self, uid: bytes, world: int, rank: int, device: int = 0):
+        assert len(uid) == 128, "unique id is 128 bytes"
+        self.lib = _abi.load()
+        self.device = torch.device("cuda", device)
+        h = C.c_void_p()
+        check(self.lib.cad_comm_create((C.c_uint8 * 128)(*uid), world, rank, device, C.byref(h)), "cad_comm_create")
+        self.h = h
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            self.lib.cad_comm_destroy(h)
+            self.h = None
+
+    def rank(self) -> int:
+        return self.lib.cad_comm_rank(self.h)
+
+    def size(self) -> int:
+        return self.lib.cad_comm_size(self.h)
+
+    def allreduce(self, t: torch.Tensor, op="sum"):
+        check(self.lib.cad_comm_allreduce(self.h, _ptr(t), t.numel(), {"sum": 0, "max": 1}[op], _stream(self.device)),
+              "cad_comm_allreduce")
+        return t
+
+    def broadcast_parameters(self, model: BaselineUNet, root=0):
+        check(self.lib.cad_comm_broadcast_params(model.h, self.h, root, _stream(self.device)), "broadcast_params")
+
+    def backward_allreduce(self, model: BaselineUNet, ddepth: torch.Tensor, bucket_elems=25 << 18):
+        check(self.lib.cad_unet_backward_allreduce(model.h, self.h, _ptr(ddepth), bucket_elems,
+                                                   _stream(self.device)), "cad_unet_backward_allreduce")
+
+
 class Trainer:
     """One optimisation step of TensorBoardTrainerEnhanced::trainEpoch (enhanced.h:287-304):
     zero_grad, forward, forwardWithIntrinsics, backward, clip_grad_norm_(max 1.0), Adam.step.
@@ -403,15 +452,21 @@ class Trainer:
     Data-parallel: with `process_group` set, gradient buckets are all-reduced
     (RCCL over xGMI via torch.distributed) as soon as their backward stage is enqueued, overlapping
     the rest of the backward; the mean (1/world) is folded into clip + Adam.  BN statistics and
-    loss masks stay per replica (DDP semantics, no SyncBN)."""
+    loss masks stay per replica (DDP semantics, no SyncBN).  With `communicator` (a libcad
+    Communicator) the same exchange runs inside the library (cad_unet_backward_allreduce), as in
+    build/train."""
 
     def __init__(self, model: BaselineUNet, loss_fn: CombinedDepthLoss, lr=1e-4, weight_decay=1e-5,
-                 grad_clip=1.0, use_grad_clip=True, process_group=None, bucket_mb=25.0):
+                 grad_clip=1.0, use_grad_clip=True, process_group=None, bucket_mb=25.0, communicator=None):
         self.model, self.loss_fn = model, loss_fn
         self.optimizer = Adam(model, lr=lr, weight_decay=weight_decay)
         self.grad_clip = grad_clip if use_grad_clip else float("inf")
         self.pg = process_group
+        self.comm = communicator
         self.world = 1
+        assert process_group is None or communicator is None, "one gradient exchange"
+        if communicator is not None:
+            self.world = communicator.size()
         if process_group is not None:
             import torch.distributed as dist
             self.world = dist.get_world_size(process_group)
@@ -435,7 +490,10 @@ class Trainer:
         else:
             m.forward(rgb, out=self.pred)
         self.loss_fn.forward_with_intrinsics(self.pred, gt, rgb, K, loss5=self.loss5, dpred=self.dpred)
-        if self.world > 1:
+        if self.comm is not None:
+            self.comm.backward_allreduce(m, self.dpred, self.bucket_elems)
+            clip_grad_norm_(m, self.grad_clip, prescale=1.0 / self.world)
+        elif self.world > 1:
             bk = GradBucketer(m.flat_grads, m.num_stages, self.bucket_elems, self.pg)
             m.backward(self.dpred, on_stage=bk.on_stage)
             bk.wait()

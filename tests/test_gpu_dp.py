@@ -1,0 +1,136 @@
+"""Data-parallel training step on the MI355X.
+
+* libcad's own RCCL exchange (Communicator / cad_unet_backward_allreduce, the path build/train
+  runs) on a single-rank communicator: every collective is then the identity, so the trajectory
+  must equal the plain single-process Trainer bit for bit — this pins the bucketing, the event
+  hand-off between the compute and communication streams and the 1/world prescale.
+* two ranks sharing cuda:0 over torch.distributed gloo (RCCL refuses two ranks on one device, and
+  the 8-GPU runs are the driver's): each rank trains its shard through cad.Trainer's decoder-first
+  bucketed all-reduce; the replicas must stay identical and equal the oracle's single-process
+  emulation of DP (per-shard loss and BN statistics, mean gradient, global clip, Adam).
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import ROOT, max_rel_err
+
+pytestmark = pytest.mark.gpu
+
+F, B, H, W = 16, 2, 64, 96
+WEIGHTS = (1.0, 0.1, 0.001, 0.01)
+
+
+def _model(cad, state, batch=B):
+    m = cad.BaselineUNet(3, F, 10.0, batch=batch, height=H, width=W)
+    m.load_state_dict(state)
+    return m, cad.CombinedDepthLoss(*WEIGHTS, batch=batch, height=H, width=W)
+
+
+def test_single_rank_communicator_matches_plain(cad, dev, oracle):
+    params, bufs = oracle.init_params(F, seed=5), oracle.init_buffers(F)
+    state = dict(params)
+    state.update(bufs)
+    rgb, gt, K = [torch.from_numpy(a).to(dev) for a in oracle.synth_batch(B, H, W)]
+    comm = cad.Communicator(cad.Communicator.unique_id(), 1, 0, 0)
+    assert (comm.rank(), comm.size()) == (0, 1)
+    # collectives on one rank: identity (sum and max), in place
+    t = torch.randn(1000, device=dev)
+    ref = t.clone()
+    comm.allreduce(t)
+    comm.allreduce(t, "max")
+    torch.cuda.synchronize()
+    assert torch.equal(t, ref)
+    out = {}
+    for use_comm in (False, True):
+        m, loss = _model(cad, state)
+        if use_comm:
+            comm.broadcast_parameters(m)
+        tr = cad.Trainer(m, loss, lr=1e-4, weight_decay=1e-5, grad_clip=1.0, communicator=comm if use_comm else None,
+                         bucket_mb=0.5)   # 0.5 MB buckets: several buckets at f=16
+        losses = [tr.train_step(rgb, gt, K).clone() for _ in range(3)]
+        torch.cuda.synchronize()
+        out[use_comm] = (m.flat_params.clone(), torch.stack(losses), tr.pred.clone(), m.last_grad_norm())
+        del tr, m, loss
+    assert torch.equal(out[True][0], out[False][0])
+    assert torch.equal(out[True][1], out[False][1])
+    assert torch.equal(out[True][2], out[False][2])
+    assert out[True][3] == out[False][3]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _gloo_worker(rank, world, port, q):
+    import sys
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, ROOT)
+    import cad_pkg
+    cad = cad_pkg.load()
+    from oracle import cad_oracle as O
+    try:
+        dev = torch.device("cuda", 0)
+        params, bufs = O.init_params(F, seed=7), O.init_buffers(F)
+        state = dict(params)
+        state.update(bufs)
+        rgb, gt, K = [torch.from_numpy(a) for a in O.synth_batch(B * world, H, W)]
+        sl = slice(rank * B, (rank + 1) * B)
+        m, loss = _model(cad, state)
+        tr = cad.Trainer(m, loss, lr=1e-4, weight_decay=1e-5, grad_clip=1.0, process_group=dist.group.WORLD,
+                         bucket_mb=0.5)
+        l = tr.train_step(rgb[sl].to(dev), gt[sl].to(dev), K[sl].to(dev))[0].item()
+        torch.cuda.synchronize()
+        q.put((rank, l, m.flat_params.cpu(), m.named_parameters(), m.named_buffers(), m.last_grad_norm(), None))
+    except Exception as e:   # report instead of hanging the parent on q.get
+        q.put((rank, None, None, None, None, None, repr(e)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_gloo_step_vs_oracle_dp(oracle):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gloo_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r[0]: r[1:] for r in (q.get(timeout=240) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[-1] is None for r in res.values()), [r[-1] for r in res.values()]
+    # replicas identical after the exchange
+    assert torch.equal(res[0][1], res[1][1])
+    assert res[0][4] == res[1][4]
+    # oracle emulation: per-shard forward/backward (own BN batch statistics), mean, clip, Adam
+    params, bufs = oracle.init_params(F, seed=7), oracle.init_buffers(F)
+    rgb, gt, K = [torch.from_numpy(a) for a in oracle.synth_batch(B * world, H, W)]
+    shard, grads = [], []
+    for r in range(world):
+        t = oracle.Trainer(params, bufs, weights=WEIGHTS)
+        _, _, lr_, _, g = t.forward_backward(rgb[r * B:(r + 1) * B], gt[r * B:(r + 1) * B], K[r * B:(r + 1) * B])
+        shard.append(t)
+        grads.append(g)
+        assert abs(res[r][0] - float(lr_)) <= 1e-4 * abs(float(lr_)), (r, res[r][0], float(lr_))
+    mean = [sum(gs) / world for gs in zip(*grads)]
+    t = oracle.Trainer(params, bufs, weights=WEIGHTS)
+    t.apply(mean)
+    lr = 1e-4
+    for n, p in res[0][2].items():
+        d = (p - t.p[n]).abs()
+        # Adam's first step is ~lr*sign(g): only a rounding-level gradient's sign flip moves more
+        assert d.max().item() <= 2 * lr + 1e-6 and d.mean().item() < 1e-6, (n, d.max().item(), d.mean().item())
+    # BN running statistics stay per replica: each rank's equal its own shard's
+    for r in range(world):
+        for n, b in res[r][3].items():
+            assert max_rel_err(b, shard[r].bufs[n]) < 1e-4, (r, n)
