@@ -31,6 +31,12 @@ class AdamOpts(C.Structure):
     _fields_ = [("lr", F), ("beta1", F), ("beta2", F), ("eps", F), ("weight_decay", F)]
 
 
+class ArchiveEntry(C.Structure):
+    """cad_archive_entry (cad.h): one tensor / empty submodule of a torch::save archive."""
+    _fields_ = [("name", C.c_char_p), ("kind", I), ("dtype", I), ("ndim", I), ("shape", C.c_int64 * 8),
+                ("data", C.c_void_p)]
+
+
 # name: (restype, argtypes)
 SIGNATURES = {
     "cad_abi_version": (I, []),
@@ -109,6 +115,16 @@ SIGNATURES = {
     "cad_unet_backward_allreduce": (I, [P, P, P, I64, P]),
     "cad_plan_grad_buckets": (I, [I64P, I64P, I, I64, I64P, I64P, C.POINTER(I)]),
     "cad_model_grad_layout": (I, [I, I, I, C.POINTER(I), I64P, I64P, I64P]),
+    "cad_unet_save_torch": (I, [P, C.c_char_p]),
+    "cad_unet_load_torch": (I, [P, C.c_char_p]),
+    "cad_unet_num_batches_tracked": (I64, [P]),
+    "cad_archive_write": (I, [C.c_char_p, C.POINTER(ArchiveEntry), I]),
+    "cad_archive_open": (I, [C.c_char_p, C.POINTER(P)]),
+    "cad_archive_close": (None, [P]),
+    "cad_archive_count": (I, [P]),
+    "cad_archive_find": (I, [P, C.c_char_p]),
+    "cad_archive_info": (I, [P, I, C.POINTER(C.c_char_p), C.POINTER(I), C.POINTER(I), I64P]),
+    "cad_archive_read": (I, [P, I, P, I64]),
 }
 
 

@@ -3,7 +3,7 @@
 // on libcad_hip.so through the C++ drop-in classes of include/cad/cad.hpp.
 //
 //   build/train -c configs/train_config.yaml [-e baseline_unet] [-g 0] [-d] [--tensorboard true]
-//               [-r checkpoint.cadckpt]
+//               [-r checkpoint.cadckpt | model.pt]
 //
 // Same flags and defaults (train_main.cpp:38-45), same YAML keys (loadConfig :60-167, main :297-430),
 // same per-batch step (enhanced.h:287-304), sample-weighted epoch loss (:308,333), validation every
@@ -56,7 +56,8 @@ void usage() {
     std::cout << "train - Train depth estimation models (MI355X)\n"
                  "  -c, --config arg      Path to config file (default: configs/train_config.yaml)\n"
                  "  -e, --experiment arg  Experiment name (default: baseline_unet)\n"
-                 "  -r, --resume arg      Resume from checkpoint (.cadckpt)\n"
+                 "  -r, --resume arg      Resume from checkpoint (.cadckpt: weights + optimizer;\n"
+                 "                        .pt: torch::save model archive, weights only)\n"
                  "  -g, --gpu arg         GPU ID (default: 0)\n"
                  "  -d, --debug           Enable debug mode\n"
                  "      --tensorboard arg Enable TensorBoard-style scalar logging (default: true)\n"
@@ -198,6 +199,10 @@ void make_sample(int64_t s, int H, int W, float* rgb, float* gt, float* K) {
     K[4] = (even ? 519.470f : 570.342f) * sy;
     K[5] = (even ? 253.736f : 240.0f) * sy;
     K[8] = 1.f;
+}
+
+bool ends_with(const std::string& s, const std::string& suf) {
+    return s.size() >= suf.size() && s.compare(s.size() - suf.size(), suf.size(), suf) == 0;
 }
 
 // ---- checkpoint (.cadckpt): named tensors in reference layout + Adam state ----
@@ -477,8 +482,13 @@ int run(const Args& args) {
                   << (R.dp ? " (data-parallel rank 0 of " + std::to_string(R.world) + ", RCCL)" : std::string()) << "\n"
                   << "Training samples: " << c.n_train << " (synthetic), validation samples: " << c.n_val << "\n";
     if (!args.resume.empty()) {
-        load_checkpoint(args.resume, model, opt);
-        if (lead) std::cout << "Resumed from " << args.resume << " (optimizer step " << opt.step_count() << ")\n";
+        if (ends_with(args.resume, ".pt")) {   // a torch::save model archive (ours or the reference's)
+            load(model, args.resume);
+            if (lead) std::cout << "Loaded model weights from " << args.resume << " (optimizer state starts fresh)\n";
+        } else {
+            load_checkpoint(args.resume, model, opt);
+            if (lead) std::cout << "Resumed from " << args.resume << " (optimizer step " << opt.step_count() << ")\n";
+        }
     }
     if (comm) comm->broadcast_parameters(model, 0);   // identical replicas
 
@@ -581,11 +591,17 @@ int run(const Args& args) {
                    << "\nmetrics/abs_rel," << epoch << "," << vm.abs_rel << "\n";
         std::cout << "Epoch " << epoch << "/" << c.num_epochs << " | train " << train_loss << " | val " << val_loss
                   << " | abs_rel " << vm.abs_rel << " | " << el << " s\n";
-        if (c.save_interval > 0 && epoch % c.save_interval == 0)
-            save_checkpoint(c.checkpoint_dir + "/" + c.experiment_name + "_epoch_" + std::to_string(epoch) + ".cadckpt",
-                            model, opt);
+        if (c.save_interval > 0 && epoch % c.save_interval == 0) {
+            // the reference's checkpoint, torch::save(model_, <dir>/<exp>_epoch_N.pt) (enhanced.h:656-662),
+            // plus the optimizer state it never saves (.cadckpt: full resume)
+            const std::string stem = c.checkpoint_dir + "/" + c.experiment_name + "_epoch_" + std::to_string(epoch);
+            save(model, stem + ".pt");
+            save_checkpoint(stem + ".cadckpt", model, opt);
+            std::cout << "Checkpoint saved: " << stem << ".pt\n";
+        }
     }
     if (lead) {
+        save(model, c.checkpoint_dir + "/final_model.pt");   // production_trainer.h:323-330
         save_checkpoint(c.checkpoint_dir + "/final_model.cadckpt", model, opt);
         std::cout << "Training complete.\n";
     }

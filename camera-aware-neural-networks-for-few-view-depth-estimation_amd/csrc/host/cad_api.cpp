@@ -24,6 +24,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <memory>
 #include <random>
 #include <stdexcept>
@@ -154,6 +155,9 @@ struct cad_unet {
     float max_depth = 10.f;
     bool train = true;
     bool have_fwd = false;
+    // BatchNorm num_batches_tracked (torch::save state): the BatchNorm2d layers count every
+    // train-mode forward, FiLM's BatchNorm1d only those with B > 1 (film_layer.h:85,91)
+    int64_t nbt = 0, nbt_film = 0;
     int fwd_B = 0;
     std::vector<PInfo> params;
     std::vector<BufInfo> bufs;
@@ -1030,6 +1034,175 @@ cad_status cad_unet_use_external_slabs(cad_unet* h, float* params, float* grads)
     });
 }
 
+// ---- torch::save / torch::load checkpoints (torch_archive.cpp holds the format) ----
+int64_t cad_unet_num_batches_tracked(const cad_unet* h) { return h ? h->nbt : -1; }
+
+cad_status cad_unet_save_torch(cad_unet* h, const char* path) {
+    return guard([&] {
+        require(h && path, "null argument");
+        HIPCHK(hipSetDevice(h->device));
+        HIPCHK(hipDeviceSynchronize());
+        std::deque<std::vector<float>> data;
+        std::deque<std::string> names;
+        std::vector<cad_archive_entry> E;
+        auto entry = [&](const std::string& name, int kind, int dtype, int ndim, const int64_t* shape, const void* d) {
+            names.push_back(name);
+            cad_archive_entry e{};
+            e.name = names.back().c_str();
+            e.kind = kind; e.dtype = dtype; e.ndim = ndim; e.data = d;
+            for (int k = 0; k < ndim; ++k) e.shape[k] = shape[k];
+            E.push_back(e);
+        };
+        // parameters in named_parameters() order; the encoder blocks' MaxPool2d ("pool", registered
+        // before "conv", baseline_unet.h:56 / intrinsics_unet.h:65) has no tensors but is a submodule
+        const char* pooled[4] = {"enc2.", "enc3.", "enc4.", "bottleneck."};
+        bool placed[4] = {};
+        for (size_t i = 0; i < h->params.size(); ++i) {
+            const PInfo& p = h->params[i];
+            for (int k = 0; k < 4; ++k)
+                if (!placed[k] && p.name.rfind(std::string(pooled[k]) + "conv.", 0) == 0) {
+                    entry(std::string(pooled[k]) + "pool", 2, CAD_DTYPE_F32, 0, nullptr, nullptr);
+                    placed[k] = true;
+                }
+            data.emplace_back((size_t)p.n_ref);
+            get_slab_tensor(h, h->flat_p, (int)i, data.back().data(), p.n_ref);
+            entry(p.name, 0, CAD_DTYPE_F32, p.ndim, p.shape, data.back().data());
+        }
+        // buffers: running_mean, running_var, num_batches_tracked per BatchNorm
+        for (const BufInfo& b : h->bufs) {
+            data.emplace_back((size_t)b.C);
+            HIPCHK(hipMemcpy(data.back().data(), b.ptr, sizeof(float) * b.C, hipMemcpyDeviceToHost));
+            const int64_t C = b.C;
+            entry(b.name, 1, CAD_DTYPE_F32, 1, &C, data.back().data());
+            const std::string tail = ".running_var";
+            if (b.name.size() > tail.size() && b.name.compare(b.name.size() - tail.size(), tail.size(), tail) == 0) {
+                const bool film = b.name.find(".film.") != std::string::npos;
+                entry(b.name.substr(0, b.name.size() - tail.size()) + ".num_batches_tracked", 1, CAD_DTYPE_I64, 0,
+                      nullptr, film ? &h->nbt_film : &h->nbt);
+            }
+        }
+        if (cad_archive_write(path, E.data(), (int)E.size()) != CAD_OK) throw std::runtime_error(cad_last_error());
+    });
+}
+
+}  // extern "C"
+
+namespace {
+float half_to_float(uint16_t h) {
+    const uint32_t sign = (uint32_t)(h & 0x8000) << 16, exp = (h >> 10) & 0x1F, man = h & 0x3FF;
+    float v;
+    if (exp == 0) v = std::ldexp((float)man, -24);                    // zero / subnormal
+    else if (exp == 31) v = man ? NAN : INFINITY;
+    else v = std::ldexp((float)(man | 0x400), (int)exp - 25);
+    uint32_t w;
+    std::memcpy(&w, &v, 4);
+    w |= sign;
+    std::memcpy(&v, &w, 4);
+    return v;
+}
+
+// one archive tensor as fp32 host values (float dtypes converted; integer dtypes refused)
+std::vector<float> archive_f32(const cad_archive* a, int i, const std::string& name) {
+    int dt = 0, nd = 0;
+    int64_t shp[8];
+    if (cad_archive_info(a, i, nullptr, &dt, &nd, shp) != CAD_OK) throw std::runtime_error(cad_last_error());
+    int64_t n = 1;
+    for (int k = 0; k < nd; ++k) n *= shp[k];
+    std::vector<float> out((size_t)n);
+    auto read = [&](void* dst, int64_t bytes) {
+        if (cad_archive_read(a, i, dst, bytes) != CAD_OK) throw std::runtime_error(cad_last_error());
+    };
+    if (dt == CAD_DTYPE_F32) {
+        read(out.data(), n * 4);
+    } else if (dt == CAD_DTYPE_F64) {
+        std::vector<double> t((size_t)n);
+        read(t.data(), n * 8);
+        for (int64_t k = 0; k < n; ++k) out[(size_t)k] = (float)t[(size_t)k];
+    } else if (dt == CAD_DTYPE_F16 || dt == CAD_DTYPE_BF16) {
+        std::vector<uint16_t> t((size_t)n);
+        read(t.data(), n * 2);
+        for (int64_t k = 0; k < n; ++k) {
+            const uint16_t u = t[(size_t)k];
+            if (dt == CAD_DTYPE_BF16) {
+                const uint32_t w = (uint32_t)u << 16;
+                std::memcpy(&out[(size_t)k], &w, 4);
+            } else {
+                out[(size_t)k] = half_to_float(u);
+            }
+        }
+    } else {
+        throw std::runtime_error("'" + name + "' is not a floating-point tensor in the archive");
+    }
+    return out;
+}
+}  // namespace
+
+extern "C" {
+
+cad_status cad_unet_load_torch(cad_unet* h, const char* path) {
+    return guard([&] {
+        require(h && path, "null argument");
+        cad_archive* raw = nullptr;
+        if (cad_archive_open(path, &raw) != CAD_OK) throw std::runtime_error(cad_last_error());
+        std::unique_ptr<cad_archive, void (*)(cad_archive*)> a(raw, cad_archive_close);
+        HIPCHK(hipSetDevice(h->device));
+        HIPCHK(hipDeviceSynchronize());
+        auto find = [&](const std::string& name, int ndim, const int64_t* shape) {
+            const int i = cad_archive_find(a.get(), name.c_str());
+            require(i >= 0, "checkpoint has no '" + name + "'");
+            int nd = 0;
+            int64_t shp[8];
+            cad_archive_info(a.get(), i, nullptr, nullptr, &nd, shp);
+            bool same = nd == ndim;
+            for (int k = 0; same && k < nd; ++k) same = shp[k] == shape[k];
+            require(same, "shape mismatch for '" + name + "' between the checkpoint and the model");
+            return i;
+        };
+        // read everything first: a failing checkpoint leaves the model untouched
+        std::vector<std::vector<float>> pv, bv;
+        for (const PInfo& p : h->params) pv.push_back(archive_f32(a.get(), find(p.name, p.ndim, p.shape), p.name));
+        for (const BufInfo& b : h->bufs) {
+            const int64_t C = b.C;
+            bv.push_back(archive_f32(a.get(), find(b.name, 1, &C), b.name));
+        }
+        auto counter = [&](bool film) -> int64_t {
+            int64_t v = -1;
+            for (const BufInfo& b : h->bufs) {
+                const std::string tail = ".running_var";
+                if (b.name.size() <= tail.size() || b.name.compare(b.name.size() - tail.size(), tail.size(), tail) != 0) continue;
+                if ((b.name.find(".film.") != std::string::npos) != film) continue;
+                const std::string n = b.name.substr(0, b.name.size() - tail.size()) + ".num_batches_tracked";
+                const int i = find(n, 0, nullptr);
+                int dt = 0;
+                cad_archive_info(a.get(), i, nullptr, &dt, nullptr, nullptr);
+                int64_t x = 0;
+                if (dt == CAD_DTYPE_I64) {
+                    if (cad_archive_read(a.get(), i, &x, 8) != CAD_OK) throw std::runtime_error(cad_last_error());
+                } else if (dt == CAD_DTYPE_I32) {
+                    int32_t y = 0;
+                    if (cad_archive_read(a.get(), i, &y, 4) != CAD_OK) throw std::runtime_error(cad_last_error());
+                    x = y;
+                } else {
+                    throw std::runtime_error("'" + n + "' is not an integer tensor");
+                }
+                v = std::max(v, x);
+            }
+            return v;
+        };
+        const int64_t n2 = counter(false), n1 = counter(true);
+        for (size_t i = 0; i < h->params.size(); ++i) {
+            std::vector<float> inter;
+            ref_to_int(h->params[i], pv[i].data(), inter);
+            HIPCHK(hipMemcpy(h->flat_p + h->params[i].off, inter.data(), sizeof(float) * h->params[i].n_int,
+                             hipMemcpyHostToDevice));
+        }
+        for (size_t i = 0; i < h->bufs.size(); ++i)
+            HIPCHK(hipMemcpy(h->bufs[i].ptr, bv[i].data(), sizeof(float) * h->bufs[i].C, hipMemcpyHostToDevice));
+        if (n2 >= 0) h->nbt = n2;
+        if (n1 >= 0) h->nbt_film = n1;
+    });
+}
+
 cad_status cad_unet_forward(cad_unet* h, const float* rgb, float* depth, int B, void* stream) {
     return cad_unet_forward_cam(h, rgb, nullptr, depth, B, stream);
 }
@@ -1042,6 +1215,10 @@ cad_status cad_unet_forward_cam(cad_unet* h, const float* rgb, const float* cam4
         HIPCHK(hipSetDevice(h->device));
         unet_forward(h, rgb, cam4, depth, B, S(stream));
         HIPCHK(hipGetLastError());
+        if (h->train) {
+            ++h->nbt;
+            if (B > 1) ++h->nbt_film;
+        }
         h->have_fwd = h->train;
         h->fwd_B = B;
     });

@@ -189,10 +189,26 @@ class BaselineUNet:
         assert self.lib.cad_unet_debug_buffer(self.h, name.encode(), out.ctypes.data_as(_abi.FP), n) == n
         return torch.from_numpy(out)
 
+    def num_batches_tracked(self) -> int:
+        return int(self.lib.cad_unet_num_batches_tracked(self.h))
+
     def last_grad_norm(self) -> float:
         v = C.c_float()
         check(self.lib.cad_unet_last_grad_norm(self.h, C.byref(v), _stream(self.device)), "last_grad_norm")
         return float(v.value)
+
+
+def save(model: BaselineUNet, path: str):
+    """torch::save(model_, path) (tensorboard_trainer_enhanced.h:656-662): the TorchScript archive
+    LibTorch writes for the module, readable by the reference's torch::load (cad_unet_save_torch)."""
+    check(model.lib.cad_unet_save_torch(model.h, str(path).encode()), "cad_unet_save_torch")
+
+
+def load(model: BaselineUNet, path: str):
+    """torch::load(model, path): parameters, BatchNorm buffers and num_batches_tracked from a
+    torch::save archive (the reference's or ours); every model tensor must be present with its shape."""
+    torch.cuda.synchronize(model.device)
+    check(model.lib.cad_unet_load_torch(model.h, str(path).encode()), "cad_unet_load_torch")
 
 
 class IntrinsicsConditionedUNet(BaselineUNet):

@@ -184,6 +184,47 @@ int64_t cad_adam_step_count(const cad_adam* a);
 cad_status cad_adam_state(cad_adam* a, float** m, float** v);
 cad_status cad_adam_set_step_count(cad_adam* a, int64_t step);
 
+/* ---- checkpoints in the reference's format: torch::save(model_, path) / torch::load(model, path)
+ * (tensorboard_trainer_enhanced.h:656-662; production_trainer.h:323-330 writes final_model.pt).
+ * cad_unet_save_torch writes the TorchScript zip archive LibTorch's OutputArchive produces for the
+ * module (every parameter and buffer under its named_parameters()/named_buffers() name, BatchNorm
+ * num_batches_tracked included, parameterless submodules such as the encoders' MaxPool2d kept), so
+ * torch::load of the reference model reads it; cad_unet_load_torch reads such an archive (from the
+ * reference or from us) into the model: every model tensor must be present with its shape (extra
+ * archive entries are ignored, as torch::load ignores them).  Synchronous. */
+cad_status cad_unet_save_torch(cad_unet* h, const char* path);
+cad_status cad_unet_load_torch(cad_unet* h, const char* path);
+/* BatchNorm num_batches_tracked: train-mode forwards since creation (or the loaded value) */
+int64_t cad_unet_num_batches_tracked(const cad_unet* h);
+
+/* host-only archive I/O underneath (no device needed).  Entries are written in the order given:
+ * a module's parameters (kind 0), then its buffers (kind 1), then its children in first-appearance
+ * order; kind 2 declares a parameterless submodule (e.g. "enc2.pool") at its registration position. */
+#define CAD_DTYPE_F32 0
+#define CAD_DTYPE_I64 1
+#define CAD_DTYPE_F64 2
+#define CAD_DTYPE_F16 3
+#define CAD_DTYPE_BF16 4
+#define CAD_DTYPE_I32 5
+typedef struct {
+    const char* name;  /* dotted path, e.g. "enc1.bn1.running_mean" */
+    int kind;          /* 0 parameter, 1 buffer, 2 empty submodule */
+    int dtype;         /* CAD_DTYPE_* */
+    int ndim;          /* 0..8 (0 = scalar) */
+    int64_t shape[8];
+    const void* data;  /* contiguous host data */
+} cad_archive_entry;
+cad_status cad_archive_write(const char* path, const cad_archive_entry* entries, int n);
+/* reader: a data-only pickle interpreter (nothing named in the file is executed) over torch::save
+ * module archives and Python torch.save state dicts; tensors are listed under dotted names */
+typedef struct cad_archive cad_archive;
+cad_status cad_archive_open(const char* path, cad_archive** out);
+void cad_archive_close(cad_archive* a);
+int cad_archive_count(const cad_archive* a);
+int cad_archive_find(const cad_archive* a, const char* name); /* -1 if absent */
+cad_status cad_archive_info(const cad_archive* a, int i, const char** name, int* dtype, int* ndim, int64_t shape[8]);
+cad_status cad_archive_read(const cad_archive* a, int i, void* dst, int64_t bytes); /* raw, in its dtype */
+
 /* ---- data-parallel gradient exchange: RCCL over xGMI, one process per GPU (new: the reference is
  * single-device).  Semantics: every replica runs the same step on
  * its own shard of the global batch (BN statistics and loss masks per replica); the gradient slab is

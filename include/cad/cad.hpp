@@ -331,6 +331,15 @@ inline double clip_grad_norm_(BaselineUNetImpl& model, double max_norm, void* st
     return n;
 }
 
+// torch::save(model_, path) / torch::load(model, path) (tensorboard_trainer_enhanced.h:656-662): the
+// TorchScript archive LibTorch writes for the module; either side reads the other's files.
+inline void save(const BaselineUNetImpl& model, const std::string& path) {
+    cad::check(cad_unet_save_torch(model.handle(), path.c_str()), "torch::save");
+}
+inline void load(BaselineUNetImpl& model, const std::string& path) {
+    cad::check(cad_unet_load_torch(model.handle(), path.c_str()), "torch::load");
+}
+
 // Data-parallel replicas over RCCL (new: the reference is single-device).  One
 // process per GPU; rank 0 draws the id (unique_id()) and every rank builds the communicator from it.
 namespace distributed {

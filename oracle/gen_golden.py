@@ -8,6 +8,7 @@ All fixtures are generated single-threaded (torch::set_num_threads(1)) with manu
 import os
 import subprocess
 import sys
+import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
@@ -32,6 +33,10 @@ FIXTURES = {
     "loss_b2_32x48_allholes": ["--mode", "loss", "--B", "2", "--H", "32", "--W", "48", "--holes-all", "1"],
     # forwardWithIntrinsics' optional valid_mask (depth_loss.h:416-433), independent of gt
     "loss_b2_48x64_mask": ["--mode", "loss", "--B", "2", "--H", "48", "--W", "64", "--mask-seed", "77"],
+    # a checkpoint written by the reference's own torch::save(model_, path) (enhanced.h:656-662) after
+    # one training step from LibTorch's default init (seed 42): only the archive is kept
+    "ckpt_baseline_f4": ["--mode", "save", "--f", "4", "--B", "2", "--H", "32", "--W", "32", "--steps", "1",
+                         "--ckpt", "{out}/baseline_unet_epoch_1.pt"],
 }
 
 
@@ -44,6 +49,10 @@ def main():
             continue
         out = os.path.join(GOLDEN, name)
         os.makedirs(out, exist_ok=True)
+        if "--ckpt" in args:   # keep the archive, not the tensor dump
+            with tempfile.TemporaryDirectory() as tmp:
+                subprocess.run([HARNESS, "--threads", "1", "--out", tmp] + [a.format(out=out) for a in args], check=True)
+            continue
         subprocess.run([HARNESS, "--threads", "1", "--out", out] + args, check=True)
 
 

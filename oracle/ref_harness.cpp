@@ -257,7 +257,7 @@ double abs_rel_per_sample(torch::Tensor pred, torch::Tensor gt) {
 }
 
 struct Args {
-    std::string mode = "golden", out = ".", model = "baseline", init = "default";
+    std::string mode = "golden", out = ".", model = "baseline", init = "default", ckpt;
     int f = 8, B = 2, H = 64, W = 64, steps = 3, threads = 1, warmup = 1, holes_all = 0, mask_seed = 0;
     float w[4] = {1.0f, 0.1f, 0.001f, 0.01f};
     float lr = 1e-4f, wd = 1e-5f, clip = 1.0f;
@@ -269,6 +269,7 @@ Args parse(int argc, char** argv) {
         std::string k = argv[i], v = argv[i + 1];
         if (k == "--mode") a.mode = v;
         else if (k == "--out") a.out = v;
+        else if (k == "--ckpt") a.ckpt = v;
         else if (k == "--model") a.model = v;
         else if (k == "--init") a.init = v;
         else if (k == "--f") a.f = std::stoi(v);
@@ -331,6 +332,27 @@ int main(int argc, char** argv) {
         printf("{\"images_per_s\": %.6f, \"seconds\": %.3f, \"steps\": %d, \"batch\": %d, \"H\": %d, "
                "\"W\": %d, \"f\": %d, \"threads\": %d, \"last_loss\": %.6f, \"model\": \"%s\"}\n",
                a.steps * a.B / s, s, a.steps, a.B, a.H, a.W, a.f, a.threads, last, a.model.c_str());
+        return 0;
+    }
+
+    if (a.mode == "save" || a.mode == "load") {
+        // Checkpoint compatibility: "save" trains --steps steps (so the BN running statistics and
+        // num_batches_tracked are not the defaults) and writes the reference's checkpoint,
+        // torch::save(model_, path) (tensorboard_trainer_enhanced.h:656-662); "load" reads a
+        // checkpoint into a fresh --model with torch::load(model, path) — the archive reader a
+        // reference user resumes or evaluates with.  Both dump every named parameter and buffer.
+        if (a.mode == "load") torch::load(model, a.ckpt);
+        else {
+            for (int i = 0; i < a.steps; ++i) step(nullptr, nullptr, nullptr, nullptr);
+            torch::save(model, a.ckpt);
+        }
+        Dumper d(a.out);
+        for (auto& kv : model->named_parameters()) d.add("param." + kv.key(), kv.value());
+        for (auto& kv : model->named_buffers()) d.add("buffer." + kv.key(), kv.value());
+        std::ostringstream meta;
+        meta << "{\"model\": \"" << a.model << "\", \"f\": " << a.f << ", \"mode\": \"" << a.mode << "\", \"steps\": " << a.steps << "}";
+        d.finish(meta.str());
+        printf("%s %s\n", a.mode.c_str(), a.ckpt.c_str());
         return 0;
     }
 

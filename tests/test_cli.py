@@ -87,6 +87,15 @@ def test_cli_train_resume(train_bin, tmp_path):
     assert len(rows) == 3
     ck = tmp_path / "ckpt" / "baseline_unet"
     assert (ck / "baseline_unet_epoch_2.cadckpt").exists() and (ck / "final_model.cadckpt").exists()
+    # the reference's checkpoint files, torch::save archives (enhanced.h:656-662): PyTorch reads them
+    for name in ("baseline_unet_epoch_2.pt", "final_model.pt"):
+        import torch
+        sd = torch.jit.load(str(ck / name)).state_dict()
+        assert len(sd) == 18 + 18 * 5 + 4 * 2 + 2 and int(sd["enc1.bn1.num_batches_tracked"]) == 6
+    # weights-only start from a .pt (optimizer fresh)
+    r = subprocess.run([train_bin, "-c", str(p), "-r", str(ck / "final_model.pt")], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0 and "Loaded model weights" in r.stdout, r.stderr
     # resume: continue to epoch 3 from the saved optimizer state
     cfg["training"]["num_epochs"] = 3
     p.write_text(yaml.safe_dump(cfg))

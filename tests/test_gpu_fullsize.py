@@ -13,15 +13,18 @@ This is the only parity check that exercises what the headline step alone exerci
 Step = TensorBoardTrainerEnhanced::trainEpoch body (tensorboard_trainer_enhanced.h:287-304).
 Tolerances (fp32 vs fp32, different summation orders; the north-star's 1e-3 relative):
   prediction <= 1e-4 normalised max error (north-star bound 1e-3), loss <= 1e-5 relative (1e-4 bound),
-  dL/dpred <= 1e-3, grad norm <= 1e-4 relative, every parameter gradient cosine >= 0.9999 and
-  normalised max error <= 1e-2 (both sides are fp32 with different summation orders; a weight
-  gradient in front of a train-mode BatchNorm sums millions of mean-free terms, so its fp32 rounding
-  is relatively large: measured on MI355X the worst is enc2.conv.conv1.weight at cosine 0.999986,
-  5.4e-3), BN running stats <= 1e-4, parameters after Adam within 2 lr (Adam's
+  dL/dpred <= 1e-3, grad norm <= 1e-4 relative; parameter gradients are judged against the oracle
+  in fp64 (the exact-arithmetic yardstick), like the small-size tests: cosine >= 0.9999 and normalised
+  max error <= max(1e-2, 3x the fp32 oracle's own error).  A weight gradient in front of a train-mode
+  BatchNorm sums millions of mean-free terms, so fp32 rounding on EITHER side is relatively large
+  there (measured on MI355X: bottleneck.conv.conv2.weight differs from the fp32 oracle by 3.7e-2
+  normalised max error at cosine 0.99998).  BN running stats <= 1e-4, parameters after Adam within 2 lr (Adam's
   first step is lr * g / (|g| + eps): only a sign flip of a rounding-level gradient moves a weight
   by more than rounding), and the eval-mode prediction / abs_rel of the updated model <= 1e-4.
-Host memory: the CPU autograd graph of a bs32 480x640 step is ~80 GB (the box allows 270 GB)."""
+Host memory: the CPU autograd graph of a bs32 480x640 step is ~80 GB in fp32 and ~160 GB in fp64,
+one after the other (the box allows 270 GB)."""
 import sys
+import threading
 import time
 
 import pytest
@@ -39,6 +42,11 @@ def _beat(msg, t0):
     # progress straight to the real stderr (pytest captures sys.stderr): a long CPU oracle step
     # must not look like a hung GPU job
     print(f"[fullsize +{time.time() - t0:6.1f}s] {msg}", file=sys.__stderr__, flush=True)
+
+
+def _heartbeat(t0, stop, period=30.0):
+    while not stop.wait(period):
+        _beat("... oracle still running", t0)
 
 
 @pytest.mark.timeout(1500)
@@ -75,10 +83,17 @@ def test_bs32_480x640_train_step_vs_oracle(cad, dev, oracle):
     torch.cuda.empty_cache()
     _beat("GPU step done; oracle step on the host cores", t0)
 
-    # ---- oracle on the host (fp32) ----
-    ref = oracle.Trainer(params, bufs, weights=WEIGHTS)
-    r = ref.step(rgb, gt, K)
-    _beat(f"oracle step done (loss {r['loss']:.6f}, ours {g_loss5[0].item():.6f})", t0)
+    # ---- oracle on the host: fp32 (the reference's arithmetic), then fp64 (the yardstick) ----
+    stop = threading.Event()
+    threading.Thread(target=_heartbeat, args=(t0, stop), daemon=True).start()
+    try:
+        ref = oracle.Trainer(params, bufs, weights=WEIGHTS)
+        r = ref.step(rgb, gt, K)
+        _beat(f"oracle fp32 step done (loss {r['loss']:.6f}, ours {g_loss5[0].item():.6f})", t0)
+        g64 = oracle.Trainer(params, bufs, weights=WEIGHTS, dtype=torch.float64).forward_backward(rgb, gt, K)[4]
+        _beat("oracle fp64 forward/backward done", t0)
+    finally:
+        stop.set()
 
     e_pred = max_rel_err(g_pred, r["pred"])
     assert e_pred < 1e-4, e_pred
@@ -87,13 +102,15 @@ def test_bs32_480x640_train_step_vs_oracle(cad, dev, oracle):
     assert max_rel_err(g_dpred, r["dpred"]) < 1e-3
     assert abs(g_norm - r["norm"]) <= 1e-4 * r["norm"], (g_norm, r["norm"])
     worst = []
-    for (n, _), g32 in zip(oracle.param_spec(F), r["grads"]):
+    for (n, _), g32, gd in zip(oracle.param_spec(F), r["grads"], g64):
         ours = g_grads[n]
-        cos = torch.nn.functional.cosine_similarity(ours.double().reshape(1, -1), g32.double().reshape(1, -1)).item()
-        worst.append((max_rel_err(ours, g32), n, cos))
+        cos = torch.nn.functional.cosine_similarity(ours.double().reshape(1, -1), gd.reshape(1, -1)).item()
+        worst.append((max_rel_err(ours, gd), max_rel_err(g32, gd), n, cos))
+    del g64
     worst.sort(reverse=True)
-    _beat(f"gradients, worst normalised max errors: {worst[:4]}; lowest cosine {min(w[2] for w in worst):.7f}", t0)
-    bad = [w for w in worst if not (w[2] >= 0.9999 and w[0] <= 1e-2)]
+    _beat(f"gradients vs fp64 (ours, fp32 oracle, name, cosine): {worst[:4]}; "
+          f"lowest cosine {min(w[3] for w in worst):.7f}", t0)
+    bad = [w for w in worst if not (w[3] >= 0.9999 and w[0] <= max(1e-2, 3 * w[1]))]
     assert not bad, bad
     lr = 1e-4
     moved = []
