@@ -17,7 +17,7 @@ def __getattr__(name):
                 "Trainer", "Communicator", "save", "load", "clip_grad_norm_", "depth_metrics", "ray_directions", "camera_from_K"):
         from . import model
         return getattr(model, name)
-    if name in ("BatchAssembler", "AugSampler"):
+    if name in ("BatchAssembler", "AugSampler", "SunRGBDDataset", "PrefetchLoader"):
         from . import batch
         return getattr(batch, name)
     raise AttributeError(name)

@@ -125,6 +125,16 @@ SIGNATURES = {
     "cad_archive_find": (I, [P, C.c_char_p]),
     "cad_archive_info": (I, [P, I, C.POINTER(C.c_char_p), C.POINTER(I), C.POINTER(I), I64P]),
     "cad_archive_read": (I, [P, I, P, I64]),
+    "cad_dataset_open": (I, [C.c_char_p, C.POINTER(C.c_char_p), I, C.POINTER(P)]),
+    "cad_dataset_synthetic": (I, [I64, I, I, C.c_uint32, C.POINTER(P)]),
+    "cad_dataset_destroy": (None, [P]),
+    "cad_dataset_size": (I64, [P]),
+    "cad_dataset_image_dir": (C.c_char_p, [P, I64]),
+    "cad_dataset_read": (I, [P, I64, P, I64, P, I64, P]),
+    "cad_loader_create": (I, [P, I, I, I, P, C.c_uint32, I, I, I, C.POINTER(P)]),
+    "cad_loader_destroy": (None, [P]),
+    "cad_loader_start_epoch": (I, [P, I64P, I64]),
+    "cad_loader_next": (I, [P, P, P, P, P]),
 }
 
 
@@ -132,7 +142,12 @@ class Sample(C.Structure):
     """cad_sample (cad.h): one decoded sample and its augmentation parameters."""
     _fields_ = [("rgb", P), ("depth", P), ("h0", I), ("w0", I), ("bgr", I), ("depth_scale", F),
                 ("K", F * 9), ("aug", I), ("crop", I), ("crop_scale", F), ("crop_x", I), ("crop_y", I),
-                ("flip", I), ("jitter", I), ("brightness", F), ("contrast", F)]
+                ("flip", I), ("jitter", I), ("brightness", F), ("contrast", F), ("dh0", I), ("dw0", I)]
+
+
+class DecodedInfo(C.Structure):
+    """cad_decoded_info (cad.h)."""
+    _fields_ = [("h0", I), ("w0", I), ("dh0", I), ("dw0", I), ("depth_scale", F), ("K", F * 9)]
 
 
 class AugConfig(C.Structure):

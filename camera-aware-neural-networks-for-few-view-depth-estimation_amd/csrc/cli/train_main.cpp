@@ -100,7 +100,11 @@ struct Config {   // the TrainingConfig fields the step uses (trainer.h:24-92)
     int init_features = 64, height = 240, width = 320, seed = 42;
     std::string checkpoint_dir = "./checkpoints", log_dir = "./logs", experiment_name = "baseline_unet";
     std::string dataset = "sunrgbd";
+    std::string manifest_path = "./data/sunrgbd_manifest.json";
     int n_train = 64, n_val = 16;
+    // data.augmentation (train_main.cpp:377-386 -> AugmentationConfig, random_seed 42)
+    bool aug_crop = true, aug_flip = true, aug_jitter = true;
+    float aug_flip_p = 0.5f, aug_brightness = 0.2f, aug_contrast = 0.2f;
     // hardware: (configs/train_config.yaml:176-183; parsed but unused by the reference)
     bool distributed = false;
     int num_gpus = 1;
@@ -155,6 +159,15 @@ Config load_config(const yaml_lite::Node& y, const std::string& experiment) {   
         c.dataset = d["dataset_name"].as<std::string>("sunrgbd");
         c.n_train = d["num_train_samples"].as<int>(64);
         c.n_val = d["num_val_samples"].as<int>(16);
+        c.manifest_path = d["manifest_path"].as<std::string>("./data/sunrgbd_manifest.json");
+        if (auto& a = d["augmentation"]) {
+            c.aug_crop = a["random_crop"].as<bool>(true);
+            c.aug_flip = a["horizontal_flip"].as<bool>(true);
+            c.aug_flip_p = a["flip_probability"].as<float>(0.5f);
+            c.aug_jitter = a["color_jitter"].as<bool>(true);
+            c.aug_brightness = a["brightness"].as<float>(0.2f);
+            c.aug_contrast = a["contrast"].as<float>(0.2f);
+        }
     }
     if (auto& hw = y["hardware"]) {
         c.distributed = hw["distributed"].as<bool>(false);
@@ -453,13 +466,25 @@ int run(const Args& args) {
         throw std::runtime_error("hardware.backend '" + c.backend + "': this build exchanges gradients over RCCL (\"nccl\")");
     if (c.distributed && c.num_gpus > 1 && !std::getenv(kEnvRank)) return launch_ranks(args, c);
     const Rank R = rank_of_process(c, args);
+    // the dataset: "synthetic" = generated batches; anything else = the SUN RGB-D manifest through the
+    // prefetch ring (cad_dataset / cad_loader: decode on host threads, pinned double-buffered upload,
+    // resize + augmentation on device).  Like the reference, train and validation read the same
+    // manifest (its split argument is unused, sunrgbd_loader.cpp:39-78); validation takes the first
+    // min(500, size) samples (validateEpoch :343) without augmentation.
+    const bool real = c.dataset != "synthetic";
+    std::unique_ptr<cad_dataset, void (*)(cad_dataset*)> ds(nullptr, cad_dataset_destroy);
+    if (real) {
+        cad_dataset* d = nullptr;
+        cad::check(cad_dataset_open(c.manifest_path.c_str(), nullptr, 0, &d), "SunRGBDLoader");
+        ds.reset(d);
+        c.n_train = (int)cad_dataset_size(d);
+        c.n_val = std::min(500, c.n_train);
+        if (c.n_train == 0) throw std::runtime_error("no usable samples in " + c.manifest_path);
+    }
     if (args.dry_run) return dry_run(c, R);
     const bool lead = R.rank == 0;   // logs, validation and checkpoints (rank 0's replica)
     if (lead) std::cout << "Loading configuration from: " << args.config << "\n";
     if (args.debug && lead) std::cout << "Debug mode enabled - using reduced dataset\n";
-    if (c.dataset != "synthetic")
-        throw std::runtime_error("dataset '" + c.dataset + "': SUN RGB-D JPEG/PNG decoding needs OpenCV, which this "
-                                 "build does not include; set data.dataset_name: \"synthetic\"");
     int ndev = 0;
     cad::check(cad_device_count(&ndev), "device query");
     if (R.device < 0 || R.device >= ndev) throw std::runtime_error("GPU " + std::to_string(R.device) + " not available");
@@ -480,7 +505,8 @@ int run(const Args& args) {
         std::cout << "Model: baseline_unet (f=" << c.init_features << "), parameters: " << model.count_parameters() << "\n"
                   << "Using MI355X device " << R.device
                   << (R.dp ? " (data-parallel rank 0 of " + std::to_string(R.world) + ", RCCL)" : std::string()) << "\n"
-                  << "Training samples: " << c.n_train << " (synthetic), validation samples: " << c.n_val << "\n";
+                  << "Training samples: " << c.n_train << (real ? " (" + c.manifest_path + ")" : std::string(" (synthetic)"))
+                  << ", validation samples: " << c.n_val << "\n";
     if (!args.resume.empty()) {
         if (ends_with(args.resume, ".pt")) {   // a torch::save model archive (ours or the reference's)
             load(model, args.resume);
@@ -519,6 +545,25 @@ int run(const Args& args) {
         cad::check(cad_memcpy(K.data, hb.K.data(), 4 * n * 9, 0, nullptr), "h2d");
         rgb.shape[0] = gt.shape[0] = K.shape[0] = pred.shape[0] = n;
     };
+    std::unique_ptr<cad_loader, void (*)(cad_loader*)> train_L(nullptr, cad_loader_destroy), val_L(nullptr, cad_loader_destroy);
+    if (real) {
+        cad_aug_config ac{};
+        ac.enable_random_crop = c.aug_crop; ac.crop_scale_min = 0.7f; ac.crop_scale_max = 1.0f;
+        ac.enable_horizontal_flip = c.aug_flip; ac.horizontal_flip_prob = c.aug_flip_p;
+        ac.enable_color_jitter = c.aug_jitter; ac.brightness_delta = c.aug_brightness; ac.contrast_delta = c.aug_contrast;
+        const int threads = (int)std::max(2u, std::min(8u, std::thread::hardware_concurrency()));
+        cad_loader* L = nullptr;
+        cad::check(cad_loader_create(ds.get(), B, H, W, &ac, 42, threads, 2, R.device, &L), "train loader");
+        train_L.reset(L);
+        cad::check(cad_loader_create(ds.get(), B, H, W, nullptr, 42, threads, 2, R.device, &L), "val loader");
+        val_L.reset(L);
+    }
+    auto fetch = [&](cad_loader* L, int expect) {
+        const int n = cad_loader_next(L, rgb.data, gt.data, K.data, nullptr);
+        if (n < 0) throw std::runtime_error(std::string("data loader: ") + cad_last_error());
+        if (n != expect) throw std::runtime_error("data loader: batch of " + std::to_string(n) + ", expected " + std::to_string(expect));
+        rgb.shape[0] = gt.shape[0] = K.shape[0] = pred.shape[0] = n;
+    };
     const auto t0 = std::chrono::steady_clock::now();
     int64_t global_step = opt.step_count();
     const int nb = steps_per_epoch(c.n_train, B, R.world);
@@ -529,9 +574,18 @@ int run(const Args& args) {
         model.train();
         double total = 0.0;
         int64_t seen = 0;
+        if (real) {   // this rank's samples of the epoch, in step order
+            std::vector<int64_t> order;
+            for (int bi = 0; bi < nb; ++bi) {
+                const Shard sh = shard_of(bi, c.n_train, B, R);
+                for (int j = 0; j < sh.n; ++j) order.push_back(sh.first + j);
+            }
+            cad::check(cad_loader_start_epoch(train_L.get(), order.data(), (int64_t)order.size()), "start epoch");
+        }
         for (int bi = 0; bi < nb; ++bi) {   // enhanced.h:266-329
             const Shard sh = shard_of(bi, c.n_train, B, R);   // last partial batch (:269-270) on one rank
-            upload(sh.first, sh.n, 0);
+            if (real) fetch(train_L.get(), sh.n);
+            else upload(sh.first, sh.n, 0);
             opt.zero_grad();
             model.forward_into(rgb, pred);
             DeviceTensor l = loss_fn.forwardWithIntrinsics(pred, gt, rgb, K);
@@ -564,9 +618,11 @@ int run(const Args& args) {
             model.eval();
             double vl = 0.0;
             int vn = 0;
+            if (real) cad::check(cad_loader_start_epoch(val_L.get(), nullptr, c.n_val), "validation");
             for (int64_t s = 0; s < c.n_val; s += B) {
                 const int n = (int)std::min<int64_t>(B, c.n_val - s);
-                upload(s, n, 1 << 20);
+                if (real) fetch(val_L.get(), n);
+                else upload(s, n, 1 << 20);
                 model.forward_into(rgb, pred);
                 DeviceTensor l = loss_fn.forwardWithIntrinsics(pred, gt, rgb, K);
                 // the reference evaluates sample by sample (batch 1); loss over a batch of n equals the

@@ -1489,6 +1489,9 @@ cad_status cad_batcher_assemble(cad_batcher* b, const cad_sample* samples, int B
             cad::BatchSample& d = b->host[i];
             d = cad::BatchSample{};
             d.rgb = s.rgb; d.depth = s.depth; d.h0 = s.h0; d.w0 = s.w0; d.bgr = s.bgr;
+            require((s.dh0 == 0) == (s.dw0 == 0) && s.dh0 >= 0 && s.dw0 >= 0, "sample " + std::to_string(i) + ": bad depth size");
+            d.dh0 = s.dh0 ? s.dh0 : s.h0;
+            d.dw0 = s.dw0 ? s.dw0 : s.w0;
             d.depth_scale = s.depth_scale;
             // intrinsics with the reference's float operations
             float* k = Kh + 9 * i;

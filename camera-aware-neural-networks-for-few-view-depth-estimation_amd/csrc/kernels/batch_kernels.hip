@@ -81,8 +81,9 @@ __global__ void k_batch_resize(const BatchSample* __restrict__ smp, int H, int W
             const float x10 = (float)r1[lx.i0 * 3 + cs] / 255.0f, x11 = (float)r1[lx.i1 * 3 + cs] / 255.0f;
             rgb[((int64_t)b * 3 + c) * HW + p] = lerp2(x00, x01, x10, x11, ly, lx);
         }
-        const int ny = nearest_axis(y, s.h0, H), nx = nearest_axis(x, s.w0, W);
-        dep[(int64_t)b * HW + p] = __fmul_rn((float)s.depth[(int64_t)ny * s.w0 + nx], s.depth_scale);
+        // depth has its own size (kv2: 512x424 depth under a 1920x1080 image); nearest from it
+        const int ny = nearest_axis(y, s.dh0, H), nx = nearest_axis(x, s.dw0, W);
+        dep[(int64_t)b * HW + p] = __fmul_rn((float)s.depth[(int64_t)ny * s.dw0 + nx], s.depth_scale);
     }
 }
 

@@ -132,8 +132,9 @@ void adam_step(float* p, float* g, float* m, float* v, int64_t n, const float* n
 // an array of these lives in device memory for the launch.
 struct BatchSample {
     const uint8_t* rgb;      // HWC u8, h0 x w0 x 3 (bgr = 1: OpenCV channel order)
-    const uint16_t* depth;   // HW u16
+    const uint16_t* depth;   // HW u16, dh0 x dw0
     int h0, w0, bgr;
+    int dh0, dw0;
     float depth_scale;       // metres per depth unit (1/1000)
     int aug;                 // 0: output = stage 1 (resize); 1: crop / flip / jitter / resize of stage 1
     int cy, cx, ch, cw;      // crop window of the H x W stage-1 image (already clamped to it)

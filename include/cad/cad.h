@@ -308,6 +308,7 @@ typedef struct {
     int flip;               /* applyHorizontalFlip */
     int jitter;             /* applyColorJitter with brightness, contrast */
     float brightness, contrast;
+    int dh0, dw0;           /* depth map size when it differs from the image's (0: h0 x w0) */
 } cad_sample;
 typedef struct cad_batcher cad_batcher;
 cad_status cad_batcher_create(int max_batch, int height, int width, int device, cad_batcher** out);
@@ -331,6 +332,44 @@ void cad_aug_sampler_destroy(cad_aug_sampler* s);
 /* fills sample->aug/crop/flip/jitter fields with augmentSample's draws, in its order, for an image
  * already resized to height x width */
 cad_status cad_aug_sampler_draw(cad_aug_sampler* s, int height, int width, cad_sample* sample);
+
+/* ---- the loader: SunRGBDLoader's manifest + decoding (src/data/sunrgbd_loader.cpp:39-102, 221-275)
+ * and a prefetch ring into the batcher.  cad_dataset_open reads the JSON manifest: "images" entries
+ * with valid == true, a sensor_type in sensors[] (NULL/0: kv1, kv2, realsense, xtion — the loader's
+ * default) and an existing <path>/intrinsics.txt, in manifest order (paths relative to the working
+ * directory, as in the reference).  A sample decodes <path>/image/<first .jpg|.png|.ppm> as RGB u8
+ * and <path>/depth/<first .png|.pgm> as u16 (16-bit: metres = value / 1000; 8-bit: value), PNG and
+ * binary PNM only (JPEG needs a decoder this build lacks and fails with a message). */
+typedef struct cad_dataset cad_dataset;
+typedef struct {
+    int h0, w0;        /* rgb size */
+    int dh0, dw0;      /* depth size */
+    float depth_scale; /* metres per depth unit */
+    float K[9];        /* intrinsics.txt, row-major */
+} cad_decoded_info;
+cad_status cad_dataset_open(const char* manifest_path, const char* const* sensors, int n_sensors, cad_dataset** out);
+/* n procedurally generated decoded samples of height x width (the synthetic dataset) */
+cad_status cad_dataset_synthetic(int64_t n, int height, int width, uint32_t seed, cad_dataset** out);
+void cad_dataset_destroy(cad_dataset* d);
+int64_t cad_dataset_size(const cad_dataset* d);
+const char* cad_dataset_image_dir(const cad_dataset* d, int64_t i); /* NULL for synthetic */
+/* host decode of sample i into rgb (h0*w0*3 bytes) and depth (dh0*dw0 u16); either may be NULL to
+ * query info only */
+cad_status cad_dataset_read(const cad_dataset* d, int64_t i, uint8_t* rgb, int64_t rgb_cap, uint16_t* depth,
+                            int64_t depth_cap, cad_decoded_info* info);
+/* Prefetch ring: `threads` host workers decode up to `slots` (>= 2) batches ahead into pinned
+ * buffers; each batch is uploaded on the loader's copy stream and assembled on the caller's stream
+ * by a cad_batcher (resize; with aug != NULL, augmentSample's draws from a mt19937 seeded `seed`,
+ * drawn in sample order).  The dataset must outlive the loader. */
+typedef struct cad_loader cad_loader;
+cad_status cad_loader_create(const cad_dataset* ds, int batch, int height, int width, const cad_aug_config* aug,
+                             uint32_t seed, int threads, int slots, int device, cad_loader** out);
+void cad_loader_destroy(cad_loader* L);
+/* the epoch's sample order (NULL: 0..n-1); batches of `batch`, the last one partial (trainEpoch) */
+cad_status cad_loader_start_epoch(cad_loader* L, const int64_t* order, int64_t n);
+/* the next batch into rgb (B,3,H,W), depth (B,1,H,W), K (B,3,3) device fp32, asynchronously on
+ * `stream`; returns its size B (0 at the end of the epoch, -1 on error: cad_last_error()) */
+int cad_loader_next(cad_loader* L, float* rgb, float* depth, float* K, void* stream);
 
 /* ---- debugging: synchronous host copy of an internal NHWC activation buffer by name
  * ("x0", "cat<l>", "dcat<l>", "pool<l>", "dout<l>", "bott", "Sa", "Sb", "Sc",

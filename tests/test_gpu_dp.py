@@ -132,8 +132,10 @@ def test_two_rank_gloo_step_vs_oracle_dp(oracle):
     lr = 1e-4
     for n, p in res[0][2].items():
         d = (torch.from_numpy(p) - t.p[n]).abs()
-        # Adam's first step is ~lr*sign(g): only a rounding-level gradient's sign flip moves more
-        assert d.max().item() <= 2 * lr + 1e-6 and d.mean().item() < 1e-6, (n, d.max().item(), d.mean().item())
+        # Adam's first step is ~lr*sign(g): only a rounding-level gradient's sign flip moves a weight by
+        # more than rounding (by up to 2 lr), and such flips are rare
+        flips = int((d > 1e-5).sum())
+        assert d.max().item() <= 2 * lr + 1e-6 and flips <= max(1, 0.01 * d.numel()), (n, d.max().item(), flips)
     # BN running statistics stay per replica: each rank's equal its own shard's
     for r in range(world):
         for n, b in res[r][3].items():

@@ -52,6 +52,15 @@ def _heartbeat(t0, stop, period=30.0):
 @pytest.mark.timeout(1500)
 def test_bs32_480x640_train_step_vs_oracle(cad, dev, oracle):
     t0 = time.time()
+    stop = threading.Event()
+    threading.Thread(target=_heartbeat, args=(t0, stop), daemon=True).start()
+    try:
+        _run(cad, dev, oracle, t0)
+    finally:
+        stop.set()
+
+
+def _run(cad, dev, oracle, t0):
     params, bufs = oracle.init_params(F, seed=42), oracle.init_buffers(F)
     rgb, gt, K = [torch.from_numpy(a) for a in oracle.synth_batch(B, H, W)]
 
@@ -65,8 +74,11 @@ def test_bs32_480x640_train_step_vs_oracle(cad, dev, oracle):
     tr = cad.Trainer(model, loss, lr=1e-4, weight_decay=1e-5, grad_clip=1.0)
     rg, gg, kg = rgb.to(dev), gt.to(dev), K.to(dev)
     model.train()
+    _beat("model built; GPU forward", t0)
     pred = model.forward(rg)
     loss5, dpred = loss.forward_with_intrinsics(pred, gg, rg, kg)
+    torch.cuda.synchronize()
+    _beat("GPU forward + loss done; backward", t0)
     model.backward(dpred)
     torch.cuda.synchronize()
     g_pred, g_dpred, g_loss5 = pred.cpu(), dpred.cpu(), loss5.cpu()
@@ -84,16 +96,11 @@ def test_bs32_480x640_train_step_vs_oracle(cad, dev, oracle):
     _beat("GPU step done; oracle step on the host cores", t0)
 
     # ---- oracle on the host: fp32 (the reference's arithmetic), then fp64 (the yardstick) ----
-    stop = threading.Event()
-    threading.Thread(target=_heartbeat, args=(t0, stop), daemon=True).start()
-    try:
-        ref = oracle.Trainer(params, bufs, weights=WEIGHTS)
-        r = ref.step(rgb, gt, K)
-        _beat(f"oracle fp32 step done (loss {r['loss']:.6f}, ours {g_loss5[0].item():.6f})", t0)
-        g64 = oracle.Trainer(params, bufs, weights=WEIGHTS, dtype=torch.float64).forward_backward(rgb, gt, K)[4]
-        _beat("oracle fp64 forward/backward done", t0)
-    finally:
-        stop.set()
+    ref = oracle.Trainer(params, bufs, weights=WEIGHTS)
+    r = ref.step(rgb, gt, K)
+    _beat(f"oracle fp32 step done (loss {r['loss']:.6f}, ours {g_loss5[0].item():.6f})", t0)
+    g64 = oracle.Trainer(params, bufs, weights=WEIGHTS, dtype=torch.float64).forward_backward(rgb, gt, K)[4]
+    _beat("oracle fp64 forward/backward done", t0)
 
     e_pred = max_rel_err(g_pred, r["pred"])
     assert e_pred < 1e-4, e_pred
