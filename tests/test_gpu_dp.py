@@ -130,12 +130,15 @@ def test_two_rank_gloo_step_vs_oracle_dp(oracle):
     t = oracle.Trainer(params, bufs, weights=WEIGHTS)
     t.apply(mean)
     lr = 1e-4
+    g_mean = {n: g for (n, _), g in zip(oracle.param_spec(F), mean)}
     for n, p in res[0][2].items():
         d = (torch.from_numpy(p) - t.p[n]).abs()
-        # Adam's first step is ~lr*sign(g): only a rounding-level gradient's sign flip moves a weight by
-        # more than rounding (by up to 2 lr), and such flips are rare
-        flips = int((d > 1e-5).sum())
-        assert d.max().item() <= 2 * lr + 1e-6 and flips <= max(1, 0.01 * d.numel()), (n, d.max().item(), flips)
+        # Adam's first step is ~lr*sign(g): a weight moves by more than rounding (by up to 2 lr) only
+        # where the mean gradient is rounding-level, so that the two fp32 paths disagree on its sign
+        g = g_mean[n].abs()
+        flip = d > 1e-5
+        assert d.max().item() <= 2 * lr + 1e-6, (n, d.max().item())
+        assert (g[flip] <= 1e-2 * g.max()).all(), (n, int(flip.sum()), g[flip].max().item(), g.max().item())
     # BN running statistics stay per replica: each rank's equal its own shard's
     for r in range(world):
         for n, b in res[r][3].items():

@@ -17,10 +17,11 @@ Tolerances (fp32 vs fp32, different summation orders; the north-star's 1e-3 rela
   in fp64 (the exact-arithmetic yardstick), like the small-size tests: cosine >= 0.9999 and normalised
   max error <= max(1e-2, 3x the fp32 oracle's own error).  A weight gradient in front of a train-mode
   BatchNorm sums millions of mean-free terms, so fp32 rounding on EITHER side is relatively large
-  there (measured on MI355X: bottleneck.conv.conv2.weight differs from the fp32 oracle by 3.7e-2
-  normalised max error at cosine 0.99998).  BN running stats <= 1e-4, parameters after Adam within 2 lr (Adam's
-  first step is lr * g / (|g| + eps): only a sign flip of a rounding-level gradient moves a weight
-  by more than rounding), and the eval-mode prediction / abs_rel of the updated model <= 1e-4.
+  there (measured on MI355X: bottleneck.conv.conv2.weight is 3.7e-2 normalised max error from fp64,
+  the LibTorch-fp32 oracle 2.9e-2, both at cosine 0.99998).  BN running stats <= 1e-4; parameters
+  after Adam within 2 lr, moving by more than rounding only where the two fp32 gradients may disagree
+  in sign (Adam's first step is lr * g / (|g| + eps): |g| within 3x their max error against fp64,
+  checked element by element); the eval-mode prediction / abs_rel of the updated model <= 1e-4.
 Host memory: the CPU autograd graph of a bs32 480x640 step is ~80 GB in fp32 and ~160 GB in fp64,
 one after the other (the box allows 270 GB)."""
 import sys
@@ -108,11 +109,15 @@ def _run(cad, dev, oracle, t0):
     assert abs(g_loss5[1].item() - r["comps"]["si_loss"]) <= 1e-5 * abs(r["comps"]["si_loss"])
     assert max_rel_err(g_dpred, r["dpred"]) < 1e-3
     assert abs(g_norm - r["norm"]) <= 1e-4 * r["norm"], (g_norm, r["norm"])
-    worst = []
+    worst, flip_thr = [], {}
     for (n, _), g32, gd in zip(oracle.param_spec(F), r["grads"], g64):
         ours = g_grads[n]
         cos = torch.nn.functional.cosine_similarity(ours.double().reshape(1, -1), gd.reshape(1, -1)).item()
         worst.append((max_rel_err(ours, gd), max_rel_err(g32, gd), n, cos))
+        # a gradient element whose sign the two fp32 paths may disagree on: |g| within 3x the larger
+        # of the two paths' max error against fp64
+        err = max((ours.double() - gd).abs().max().item(), (g32.double() - gd).abs().max().item())
+        flip_thr[n] = (gd.abs(), 3 * err)
     del g64
     worst.sort(reverse=True)
     _beat(f"gradients vs fp64 (ours, fp32 oracle, name, cosine): {worst[:4]}; "
@@ -123,10 +128,15 @@ def _run(cad, dev, oracle, t0):
     moved = []
     for n, p in g_params.items():
         d = (p - ref.p[n]).abs()
-        moved.append((d.mean().item(), d.max().item(), n))
+        # Adam's first step is ~lr * sign(g): a parameter moves by more than rounding (up to 2 lr) only
+        # where the two fp32 gradients may differ in sign (|g| within their error of fp64)
+        g, thr = flip_thr[n]
+        flip = d > 1e-5
+        unexplained = int((g[flip] > thr).sum()) if n in flip_thr else int(flip.sum())
+        moved.append((unexplained, d.max().item(), int(flip.sum()), n))
     moved.sort(reverse=True)
-    _beat(f"params after Adam, largest mean |diff|: {moved[:3]}", t0)
-    assert all(mx <= 2 * lr + 1e-6 and mean < 1e-6 for mean, mx, _ in moved), moved[:3]
+    _beat(f"params after Adam (unexplained moves, max |diff|, moves > 1e-5, name): {moved[:3]}", t0)
+    assert all(u == 0 and mx <= 2 * lr + 1e-6 for u, mx, _, _ in moved), moved[:3]
     for n, b in g_bufs.items():
         assert max_rel_err(b, ref.bufs[n]) < 1e-4, n
     # eval-mode forward of the updated model (BN running statistics) and the metric's abs_rel
