@@ -23,6 +23,7 @@ workloads (configs[2], configs[3]'s per-GPU step) in the same process.
 import argparse
 import ctypes as C
 import json
+import re
 import os
 import sys
 import time
@@ -340,7 +341,8 @@ def main():
         roof = None
         if dom:
             achieved = dom["gflop"] / dom["ms"]   # GFLOP/ms == TFLOP/s
-            kname = dom["name"].split("<")[0]   # k_<op>_<engine>[p]: p = pre-split operands
+            # k_<op>[_win]_<engine>[p]: engine s3 / bf16 / none (f32); p = pre-split operands
+            kname = re.search(r"(k_\w+)", dom["name"]).group(1)
             s3 = kname.endswith("_s3")
             b1 = kname.endswith(("_bf16", "_bf16p"))
             peak = S3_PEAK_TFLOPS if s3 else BF16_MFMA_PEAK_TFLOPS if b1 else FP32_MFMA_PEAK_TFLOPS

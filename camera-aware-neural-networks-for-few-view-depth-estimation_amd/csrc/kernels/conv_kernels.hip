@@ -10,6 +10,7 @@
 #include "gemm_mfma.hpp"
 #include "gemm_s3.hpp"
 #include "gemm_ps.hpp"
+#include "gemm_win.hpp"
 #include "kernels.hpp"
 
 namespace cad {
@@ -172,6 +173,16 @@ template <int WM, int WN, int KB>
 __global__ __launch_bounds__(256) void k_conv3x3_wgrad_s3(GemmArgs a) { conv3x3_wgrad_np<3, WM, WN, 2, 2, KB>(a); }
 template <int WM, int WN, int KB>
 __global__ __launch_bounds__(256) void k_convT_wgrad_s3(GemmArgs a) { convT_wgrad_np<3, WM, WN, 2, 2, KB>(a); }
+
+// window-tiled conv3x3 forward/dgrad (gemm_win.hpp): BM = R*CW output pixels of one image; 128x128
+// tiles (WM = WN = 2) or, for N <= 64, 256x64 (WM = 4, WN = 1)
+template <int R, int CW, class Epi>
+__global__ __launch_bounds__(256, 3) void k_conv3x3_win_s3(GemmArgs a) {
+    conv3x3_win_body<3, R, CW, R * CW == 128 ? 2 : 4, R * CW == 128 ? 2 : 1, Epi>(a);
+}
+
+// window-tiled conv3x3 weight gradient (gemm_win.hpp): 64 co x 64 ci x 9 taps per workgroup, split-K
+__global__ __launch_bounds__(256, 2) void k_conv3x3_wgrad_win_s3(GemmArgs a) { conv3x3_wgrad_win_body<3>(a); }
 
 template <int WM, int WN, int KB, class Epi>
 __global__ __launch_bounds__(256) void k_conv3x3_fwd_bf16(GemmArgs a) { conv3x3_fwd_np<1, WM, WN, 2, 2, KB, Epi>(a); }
@@ -395,6 +406,62 @@ void launch_engine(Cfg c, bool fwd_kind, GemmArgs& a, hipStream_t st) {
     launch_on_engine<F, T3, TB>(c, kb, a, 1, st);
 }
 
+// Window-tiled conv3x3 forward/dgrad (S3 engine): the block shape for a given layer, or R = 0 when
+// the im2col kernel serves it (channels not a multiple of 16: enc1.conv1; no CW dividing W)
+struct WinPick {
+    int R = 0, CW = 0;
+    int bn() const { return R * CW == 128 ? 128 : 64; }
+};
+WinPick pick_win(int cin, int W, int N) {
+    WinPick w;
+    if (engine() != 1 || cin % 16 || (std::getenv("CAD_WIN") && std::getenv("CAD_WIN")[0] == '0')) return w;
+    const int BM = N <= 64 ? 256 : 128;
+    if (N % (BM == 128 ? 128 : 64)) return w;
+    static const int c128[] = {64, 32, 16, 8}, c256[] = {128, 64};
+    const int* cws = BM == 128 ? c128 : c256;
+    const int ncw = BM == 128 ? 4 : 2;
+    for (int i = 0; i < ncw; ++i)
+        if (W % cws[i] == 0) {
+            w.CW = cws[i];
+            w.R = BM / cws[i];
+            return w;
+        }
+    return w;
+}
+int win_blocks(const WinPick& w, int B, int H, int W) { return B * cdiv(H, w.R) * (W / w.CW); }
+
+template <int R, int CW, class Epi>
+void launch_win1(const GemmArgs& a, hipStream_t st) {
+    const dim3 grid(win_blocks(WinPick{R, CW}, a.B, a.H, a.W), cdiv(a.N, R * CW == 128 ? 128 : 64));
+    if (prof_enabled()) {
+        char name[160];
+        snprintf(name, sizeof(name), "void cad::k_conv3x3_win_s3<%d, %d, cad::%s>(cad::GemmArgs)", R, CW,
+                 Epi::STATS ? "EpiStoreStats" : "EpiStore");
+        prof_push(name, 2.0 * a.M * a.N * (double)a.K, st);
+        hipLaunchKernelGGL((k_conv3x3_win_s3<R, CW, Epi>), grid, dim3(256), 0, st, a);
+        prof_pop(st);
+    } else {
+        hipLaunchKernelGGL((k_conv3x3_win_s3<R, CW, Epi>), grid, dim3(256), 0, st, a);
+    }
+}
+template <class Epi>
+void launch_win(const WinPick& w, const GemmArgs& a, hipStream_t st) {
+    if (w.R * w.CW == 128) {
+        switch (w.CW) {
+            case 64: launch_win1<2, 64, Epi>(a, st); return;
+            case 32: launch_win1<4, 32, Epi>(a, st); return;
+            case 16: launch_win1<8, 16, Epi>(a, st); return;
+            case 8: launch_win1<16, 8, Epi>(a, st); return;
+        }
+    } else {
+        switch (w.CW) {
+            case 128: launch_win1<2, 128, Epi>(a, st); return;
+            case 64: launch_win1<4, 64, Epi>(a, st); return;
+        }
+    }
+    throw std::runtime_error("window conv: block shape not built");
+}
+
 // split-K planning for the weight-gradient GEMMs: aim for >= ~2048 workgroups, >= 32 K-stages each.
 // A K-slice is also a loader's buffer window (gemm_mfma.hpp: 32-bit offsets from the slice's first
 // pixel): `kbytes` = bytes one K step spans in the widest operand; slices stay below 1 GB.
@@ -446,6 +513,34 @@ void finish_slabs(float* slab, int splits, int64_t per, float* dw, hipStream_t s
     slab_reduce(slab, splits, per, 1, dw, bx, 1, st);
 }
 
+// window-tiled weight gradient (S3): cout, cin multiples of 64, W a multiple of 16
+bool use_wgrad_win(int cout, int cin, int W) {
+    return engine() == 1 && cout % 64 == 0 && cin % 64 == 0 && W % 16 == 0 &&
+           !(std::getenv("CAD_WIN") && std::getenv("CAD_WIN")[0] == '0');
+}
+void launch_wgrad_win(GemmArgs& a, float* dw, float* slab, int64_t slab_cap, int64_t kbytes, hipStream_t st) {
+    const int cin = a.b_cin;
+    const int tiles = (a.M / 64) * (cin / 64);
+    const int nst = a.K / 16;
+    int s = std::max(1, std::min(cdiv(2048, tiles), nst / 32));
+    const int64_t per = (int64_t)a.M * a.N;
+    if (slab_cap > 0) s = (int)std::max<int64_t>(1, std::min<int64_t>(s, slab_cap / per));
+    const int64_t need = (int64_t)cdiv((int64_t)a.K * kbytes, (int64_t)1 << 30);
+    if (need > s) {
+        if (need * per > slab_cap) throw std::runtime_error("weight-gradient K-slice exceeds the 1 GB window and the slab");
+        s = (int)need;
+    }
+    a.kstages_per_split = cdiv(nst, s);
+    s = cdiv(nst, a.kstages_per_split);
+    a.ldc = a.N; a.slab_stride = per;
+    a.C = s == 1 ? dw : slab;
+    const dim3 grid(a.M / 64, cin / 64, s);
+    if (prof_enabled()) prof_push("void cad::k_conv3x3_wgrad_win_s3(cad::GemmArgs)", 2.0 * a.M * a.N * (double)a.K, st);
+    hipLaunchKernelGGL(k_conv3x3_wgrad_win_s3, grid, dim3(256), 0, st, a);
+    if (prof_enabled()) prof_pop(st);
+    if (s > 1) finish_slabs(slab, s, per, dw, st);
+}
+
 // weight-gradient GEMM (M x N over K = pixels): split-K slabs, then the deterministic reduction
 template <template <int, int, int> class F, template <int, int, int> class T3, template <int, int, int> class TB>
 void launch_wgrad(GemmArgs& a, float* dw, float* slab, int64_t slab_cap, int64_t kbytes, hipStream_t st) {
@@ -465,7 +560,9 @@ void launch_wgrad(GemmArgs& a, float* dw, float* slab, int64_t slab_cap, int64_t
 void set_gemm_engine(int e) { g_engine = (e == 1 || e == 2) ? e : 0; }
 int gemm_engine() { return engine(); }
 
-int conv3x3_stats_rows(int B, int H, int W, int cout) {
+int conv3x3_stats_rows(int cin, int B, int H, int W, int cout) {
+    const WinPick w = pick_win(cin, W, cout);
+    if (w.R) return win_blocks(w, B, H, W);
     return cdiv((int64_t)B * H * W, tile_m(pick_cfg(B * H * W, cout)));
 }
 
@@ -478,6 +575,11 @@ void conv3x3_fwd(const float* x, int64_t ldx, int xcoff, int cin, const float* w
     a.Bm = w; a.ldb = 9 * cin; a.b_coff = 0;
     a.C = y; a.ldc = ldy; a.c_coff = ycoff;
     a.stats = stats;
+    if (const WinPick w = pick_win(cin, W, cout); w.R) {
+        if (stats) launch_win<EpiStoreStats>(w, a, st);
+        else launch_win<EpiStore>(w, a, st);
+        return;
+    }
     const Cfg c = pick_cfg(a.M, a.N);
     if (stats) launch_engine<KConvFwdS, KConvFwdS3, KConvFwdSB>(c, true, a, st);
     else launch_engine<KConvFwd, KConvFwd3, KConvFwdB>(c, true, a, st);
@@ -502,6 +604,10 @@ void conv3x3_dgrad(const float* dz, int cout, const float* wd, int cin, float* d
     a.A = dz; a.lda = cout; a.a_coff = 0; a.a_cin = cout;
     a.Bm = wd; a.ldb = 9 * cout;
     a.C = dx; a.ldc = lddx; a.c_coff = 0;
+    if (const WinPick w = pick_win(cout, W, cin); w.R) {
+        launch_win<EpiStore>(w, a, st);
+        return;
+    }
     launch_engine<KConvFwd, KConvFwd3, KConvFwdB>(pick_cfg(a.M, a.N), true, a, st);
 }
 
@@ -529,6 +635,10 @@ void conv3x3_wgrad(const float* dz, int cout, const float* x, int64_t ldx, int x
     a.B = B; a.H = H; a.W = W;
     a.A = dz; a.lda = cout; a.a_coff = 0;
     a.Bm = x; a.ldb = ldx; a.b_coff = xcoff; a.b_cin = cin;
+    if (use_wgrad_win(cout, cin, W)) {
+        launch_wgrad_win(a, dw, slab, slab_cap, 4 * std::max<int64_t>(a.lda, ldx), st);
+        return;
+    }
     launch_wgrad<KConvWgrad, KConvWgrad3, KConvWgradB>(a, dw, slab, slab_cap, 4 * std::max<int64_t>(a.lda, ldx), st);
 }
 

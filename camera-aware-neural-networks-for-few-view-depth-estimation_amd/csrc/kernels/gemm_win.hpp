@@ -1,0 +1,455 @@
+// Window-tiled conv3x3 forward / dgrad on the S3 (NP = 3) and B1 (NP = 1) engines.
+//
+// The im2col GEMM (gemm_s3.hpp + KcIm2col3x3) fetches and splits every input element once per tap
+// that reads it: 9 fetches + 9 three-plane splits per element and output tile.  Here a workgroup
+// owns an R x CW block of output pixels of one image (BM = R*CW) and walks K in stages of
+// (16-channel block cb, kernel row ky): the stage's A operand is the input WINDOW of R rows x (CW+2)
+// columns (the block's rows shifted by ky-1, one halo column each side) x 16 channels, fetched and
+// split ONCE, and the three taps kx = 0, 1, 2 of the kernel row read it at column offsets kx — the
+// shift is a whole LDS row (one window pixel = 32 B per plane), so the fragment reads stay aligned
+// ds_read_b128.  Per three k16 steps the A traffic (global loads, split VALU, LDS stores) drops from
+// 3*BM*16 to R*(CW+2)*16 elements (~2.9x).  B is the three taps' weights (Kc, 3 x BN x 16).
+//
+//   C[pix][n] = sum_{cb, ky, kx, ci} X[(b, y+ky-1, x+kx-1)][cb*16+ci] * Wt[n][(3ky+kx)*cin + cb*16+ci]
+//
+// Per stage and wave: 3 k16 steps x MI x NJ blocks x NP products (S3: 72 MFMAs).  LDS holds ONE
+// stage (A window + B taps; 49.5 KB for BM = BN = 128 on S3, so 3 workgroups per CU), register-staged:
+// the next stage's global loads are in flight during the MFMAs, then barrier / store / barrier.
+// Requirements (host: conv_kernels.hip pick_win): cin % 16 == 0, W % CW == 0, N % BN == 0; rows past H in the
+// last block row are computed on zeros and not stored.  Accumulation order differs from the im2col
+// kernel (cb-major), so the two agree to rounding, not bit for bit.
+#pragma once
+#include "gemm_s3.hpp"
+
+namespace cad {
+
+template <int R, int CW, int BN>
+struct WinGeo {
+    static constexpr int BM = R * CW;
+    static constexpr int WC = CW + 2;              // window columns
+    static constexpr int WPIX = R * WC;            // window pixels per stage
+    static constexpr int NFA = WPIX * 4;           // A float4s per stage (16 channels = 4 float4)
+    static constexpr int NVA = (NFA + 255) / 256;  // per thread
+    static constexpr int NFB = 3 * BN * 4;         // B float4s per stage (3 taps x BN rows x 16 k)
+    static_assert(NFB % 256 == 0, "BN");
+    static constexpr int NVB = NFB / 256;
+    static constexpr int PLA = WPIX * 16;          // bf16 elements per A plane
+    static constexpr int PLB = BN * 16;            // bf16 elements per B plane (one tap)
+};
+
+// A: the input window of stage (cb, ky) of the block whose first output pixel is (b, y0, x0)
+template <int R, int CW, int BN>
+struct WinA {
+    using G = WinGeo<R, CW, BN>;
+    __amdgpu_buffer_rsrc_t rs;
+    int poff[G::NVA];   // byte offset of the element at ky = 0, cb = 0 from the base (valid elements)
+    int wr[G::NVA];     // window row of the element; a large negative value marks x / tail padding
+    int H, y0, rowbytes, cb, ky;
+    __device__ void init(const float* P, int64_t ld, int coff, int H_, int W, int b, int y0_, int x0, int tid,
+                         int kbeg) {
+        H = H_; y0 = y0_;
+        const int ld4 = (int)ld * 4;
+        rowbytes = W * ld4;
+        const int64_t pbase = ((int64_t)b * H + y0 - 1) * W + x0 - 1;   // window pixel (0, 0) at ky = 0
+        const int64_t pb = pbase > 0 ? pbase : 0;
+        rs = make_rsrc(P + pb * ld + coff);
+#pragma unroll
+        for (int j = 0; j < G::NVA; ++j) {
+            const int f = tid + 256 * j;
+            const int w = f >> 2, q = f & 3;
+            const int r = w / G::WC, c = w - r * G::WC;
+            const int x = x0 - 1 + c;
+            const bool ok = f < G::NFA && (unsigned)x < (unsigned)W;
+            wr[j] = ok ? r : -(1 << 28);
+            poff[j] = (int)((r * (int64_t)W + c + (pbase - pb)) * ld4) + q * 16;
+        }
+        cb = kbeg / 3;
+        ky = kbeg - 3 * cb;
+    }
+    __device__ void load(float4 (&v)[G::NVA]) {
+        const int add = ky * rowbytes + cb * 64;
+#pragma unroll
+        for (int j = 0; j < G::NVA; ++j) {
+            const int y = y0 - 1 + ky + wr[j];
+            v[j] = bload4(rs, (unsigned)y < (unsigned)H ? (uint32_t)(poff[j] + add) : kOOB);
+        }
+        if (++ky == 3) { ky = 0; ++cb; }
+    }
+};
+
+// B: weights of the three taps (3ky + kx) of stage (cb, ky); Wt[n][tap*cin + ci], row stride ldb.
+// Element f = tid + 256 j of a stage is (tap t, row, quarter q) with f = (t*BN + row)*4 + q; as 256
+// divides BN*4, t and the row step are compile-time functions of j: one base offset per thread.
+// The host guarantees N % BN == 0 (pick_win), so every row is in range.
+template <int R, int CW, int BN>
+struct WinB {
+    using G = WinGeo<R, CW, BN>;
+    static constexpr int JPT = BN * 4 / 256;   // j per tap
+    __amdgpu_buffer_rsrc_t rs;
+    int base, ldb4, cin4, cb, ky;
+    __device__ void init(const float* Wt, int64_t ldb, int cin, int n0, int tid, int kbeg) {
+        rs = make_rsrc(Wt + (int64_t)n0 * ldb);
+        ldb4 = (int)ldb * 4;
+        cin4 = cin * 4;
+        base = (tid >> 2) * ldb4 + (tid & 3) * 16;
+        cb = kbeg / 3;
+        ky = kbeg - 3 * cb;
+    }
+    __device__ void load(float4 (&v)[G::NVB]) {
+        const int add = base + 3 * ky * cin4 + cb * 64;
+#pragma unroll
+        for (int j = 0; j < G::NVB; ++j) {
+            const int t = j / JPT, rstep = (j % JPT) * 64;   // 64 rows per 256 float4s
+            v[j] = bload4(rs, (uint32_t)(add + rstep * ldb4 + t * cin4));
+        }
+        if (++ky == 3) { ky = 0; ++cb; }
+    }
+};
+
+// Window epilogue: tile row mr -> output pixel (b, y0 + mr / CW, x0 + mr % CW), rows past H dropped.
+// EpiStore / EpiStoreStats semantics of gemm_epilogue_t (stats row = the block's linear index).
+template <int WM, int WN, int MI, int NJ, int CW, class Epi>
+__device__ __forceinline__ void win_epilogue(const GemmArgs& a, const floatx16 (&acc)[MI][NJ], int tile_lin, int n0,
+                                             int b, int y0, int x0, float* lds) {
+    constexpr int BN = 32 * NJ * WN;
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int wm = wave / WN, wn = wave % WN;
+    float ssum[NJ], ssq[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) ssum[j] = ssq[j] = 0.f;
+    const int64_t ldc4 = a.ldc * 4;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(a.C + (((int64_t)b * a.H + y0) * a.W + x0) * a.ldc + a.c_coff);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int n = n0 + wn * 32 * NJ + j * 32 + (lane & 31);
+                const int mr = wm * 32 * MI + i * 32 + 4 * (lane >> 5) + 8 * g;   // 4 rows mr..mr+3: same r
+                const int r = mr / CW, c = mr - r * CW;
+                const bool ok = n < a.N && y0 + r < a.H;
+                const uint32_t lo = ok ? (uint32_t)((r * (int64_t)a.W + c) * ldc4 + (int64_t)n * 4) : kOOB;
+                float v[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] = acc[i][j][4 * g + q];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[q]), rs,
+                                                          lo + (uint32_t)(q * ldc4), 0, 0);
+                    if constexpr (Epi::STATS) {
+                        const float vm = y0 + r < a.H ? v[q] : 0.f;
+                        ssum[j] += vm;
+                        ssq[j] += vm * vm;
+                    }
+                }
+            }
+        }
+    if constexpr (Epi::STATS) {
+        float* red = lds;   // [WM][BN][2]
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            float s = ssum[j], q = ssq[j];
+            s += __shfl_xor(s, 32);
+            q += __shfl_xor(q, 32);
+            if (lane < 32) {
+                const int cl = wn * 32 * NJ + j * 32 + lane;
+                red[(wm * BN + cl) * 2 + 0] = s;
+                red[(wm * BN + cl) * 2 + 1] = q;
+            }
+        }
+        __syncthreads();
+        for (int c = tid; c < BN; c += 256) {
+            float s = 0.f, q = 0.f;
+#pragma unroll
+            for (int w = 0; w < WM; ++w) { s += red[(w * BN + c) * 2]; q += red[(w * BN + c) * 2 + 1]; }
+            const int n = n0 + c;
+            if (n < a.N) {
+                a.stats[(int64_t)tile_lin * 2 * a.N + n] = s;
+                a.stats[(int64_t)tile_lin * 2 * a.N + a.N + n] = q;
+            }
+        }
+    }
+}
+
+// blocks: gridDim.x = B * ceil(H / R) * (W / CW) output blocks (XCD-aware order), gridDim.y = N tiles
+template <int NP, int R, int CW, int WM, int WN, class Epi>
+__device__ __forceinline__ void conv3x3_win_body(const GemmArgs& a) {
+    constexpr int MI = 2, NJ = 2;
+    constexpr int BM = 32 * MI * WM, BN = 32 * NJ * WN;
+    static_assert(BM == R * CW, "tile");
+    using G = WinGeo<R, CW, BN>;
+    constexpr int SA = NP * G::PLA, SB = 3 * NP * G::PLB;   // bf16 elements
+    __shared__ __attribute__((aligned(16))) uint16_t lds[SA + SB];
+
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int wm = wave / WN, wn = wave % WN;
+    const TileId tile = xcd_tile();
+    const int nbx = a.W / CW, nby = (a.H + R - 1) / R;
+    const int tx = tile.x % nbx, t2 = tile.x / nbx, ty = t2 % nby, b = t2 / nby;
+    const int y0 = ty * R, x0 = tx * CW, n0 = tile.y * BN;
+    const int cin = a.a_cin;
+    const int S = 3 * (cin / 16);   // stages
+
+    WinA<R, CW, BN> la;
+    WinB<R, CW, BN> lb;
+    la.init(a.A, a.lda, a.a_coff, a.H, a.W, b, y0, x0, tid, 0);
+    lb.init(a.Bm, a.ldb, cin, n0, tid, 0);
+
+    // window pixel of the lane's A row in each of its MI blocks (tap kx adds kx)
+    int wpix[MI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+        const int p = wm * 32 * MI + i * 32 + (lane & 31);
+        const int r = p / CW;
+        wpix[i] = r * G::WC + (p - r * CW);
+    }
+
+    floatx16 acc[MI][NJ];
+    acc_zero(acc);
+    float4 ra[G::NVA], rb[G::NVB];
+
+    auto store = [&]() {
+#pragma unroll
+        for (int j = 0; j < G::NVA; ++j) {
+            const int f = tid + 256 * j;
+            if (f < G::NFA) {
+                const auto sp = split_np<NP>(ra[j]);
+                const int off = s3_off<16>(f >> 2, (f & 3) * 4);
+#pragma unroll
+                for (int p = 0; p < NP; ++p) *reinterpret_cast<uint2*>(lds + p * G::PLA + off) = sp.p[p];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < G::NVB; ++j) {
+            const int f = tid + 256 * j;
+            const int t = f / (BN * 4), rem = f - t * (BN * 4);
+            const auto sp = split_np<NP>(rb[j]);
+            const int off = SA + t * NP * G::PLB + s3_off<16>(rem >> 2, (rem & 3) * 4);
+#pragma unroll
+            for (int p = 0; p < NP; ++p) *reinterpret_cast<uint2*>(lds + off + p * G::PLB) = sp.p[p];
+        }
+    };
+    auto compute = [&]() {
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+            bf16x8 fa[MI][NP], fb[NJ][NP];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) s3_frag<BN, 16, NP>(lds + SA + kx * NP * G::PLB, wn * 32 * NJ + j * 32, 0, fb[j]);
+#pragma unroll
+            for (int i = 0; i < MI; ++i) {
+                const uint16_t* base = lds + s3_off<16>(wpix[i] + kx, (lane >> 5) * 8);
+#pragma unroll
+                for (int p = 0; p < NP; ++p) fa[i][p] = *reinterpret_cast<const bf16x8*>(base + p * G::PLA);
+            }
+            s3_mfma<NP>(acc, fa, fb);
+        }
+    };
+
+    if (S > 0) {
+        la.load(ra);
+        lb.load(rb);
+        store();
+    }
+    __syncthreads();
+    for (int s = 0; s < S; ++s) {
+        const bool more = s + 1 < S;
+        if (more) {
+            la.load(ra);
+            lb.load(rb);
+        }
+        compute();
+        __syncthreads();
+        if (more) {
+            store();
+            __syncthreads();
+        }
+    }
+    win_epilogue<WM, WN, MI, NJ, CW, Epi>(a, acc, tile.x, n0, b, y0, x0, reinterpret_cast<float*>(lds));
+}
+
+// ------------------------------------------------------------------------------------------------
+// Window-tiled conv3x3 weight gradient (S3 / B1):  dW[co][tap][ci] = sum_pix dZ[pix][co] X[pix+tap][ci]
+//
+// The im2col weight-gradient GEMM (M = cout, N = 9*cin, K = pixels; MNcIm2col3x3) fetches and splits
+// X once per tap and N tile.  Here a workgroup owns a 64 (co) x 64 (ci) channel pair over ALL nine
+// taps (output 64 x 9 x 64) and a slice of K; a stage is 16 consecutive pixels of one image row:
+//   A = dZ[16 px][64 co]                           MNc planes [16 k-rows][64]
+//   B = X window rows y-1..y+1, columns x0-1..x0+16   MNc planes [3 x 18 k-rows][64]
+// and tap (ky, kx) reads B's k-rows ky*18 + kx .. +15 (a k-row = a pixel, so the shift is a whole
+// LDS row: the transposed ds_read_b64_tr_b16 fragment reads of gemm_s3.hpp apply unchanged).
+// Wave w owns the 32x32 (co, ci) block (w & 1, w >> 1) for all nine taps: 9 accumulators, one A and
+// nine B fragments per k16 step, 9 x NP products.  Per stage: 1024 + 3456 elements fetched and split
+// for 64 x 576 x 16 MACs (the im2col kernel: 5120 per 64 x 256 x 16).  Double-buffered LDS (2 x 40 KB
+// on S3: 2 workgroups per CU, the register budget's occupancy as well).  Split-K slices of whole
+// stages write slabs (EpiSlab layout) reduced by the host's deterministic slab reduction.
+// Requirements (host): cout % 64 == 0, cin % 64 == 0, W % 16 == 0.
+// ------------------------------------------------------------------------------------------------
+constexpr int kWgRows = 64;                      // channels per operand block
+constexpr int kWgWinK = 3 * 18;                  // B window k-rows
+using WgM = S3M<kWgRows>;                        // 64-column planes: 192 B per k-row (padded)
+
+template <int ROWS, int NP>
+__device__ __forceinline__ void mnc_frag_at(const char* s, int plane_bytes, int rb, int krow0, bf16x8 (&f)[NP]) {
+    const int lane = threadIdx.x & 63;
+    const int g = (lane >> 4) & 1, h = lane >> 5, i = lane & 15;
+    const int krow = krow0 + 8 * h + (i >> 2);
+    const int col = rb + 16 * g + 4 * (i & 3);
+    const char* b0 = s + S3M<ROWS>::off(krow, col);
+    const char* b1 = s + S3M<ROWS>::off(krow + 4, col);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        typedef __attribute__((address_space(3))) v4i16 lds_v4;
+        const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(b0 + p * plane_bytes));
+        const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(b1 + p * plane_bytes));
+        const uint2 ul = __builtin_bit_cast(uint2, lo), uh = __builtin_bit_cast(uint2, hi);
+        f[p] = __builtin_bit_cast(bf16x8, make_uint4(ul.x, ul.y, uh.x, uh.y));
+    }
+}
+
+// pixel walk of a K-slice: stage s = 16 pixels (x0 .. x0+15) of row y of image b
+struct WgPos {
+    int b, y, x0;
+    __device__ void init(int stage, int H, int W) {
+        const int segs = W >> 4;
+        const int row = stage / segs;
+        x0 = (stage - row * segs) << 4;
+        y = row % H;
+        b = row / H;
+    }
+    __device__ void next(int H, int W) {
+        x0 += 16;
+        if (x0 == W) { x0 = 0; if (++y == H) { y = 0; ++b; } }
+    }
+};
+
+template <int NP>
+__device__ __forceinline__ void conv3x3_wgrad_win_body(const GemmArgs& a) {
+    constexpr int PLA = 16 * WgM::STRIDE, PLB = kWgWinK * WgM::STRIDE;   // plane bytes
+    constexpr int SA = NP * PLA, SB = NP * PLB;
+    constexpr int NVB = (kWgWinK * 16 + 255) / 256;   // 16 float4 per k-row of 64 channels
+    __shared__ __attribute__((aligned(16))) char lds[2 * (SA + SB)];
+
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6;
+    const int cbk = wave & 1, cib = wave >> 1;
+    const TileId tile = xcd_tile();
+    const int co0 = tile.x * 64, ci0 = tile.y * 64;
+    const int H = a.H, W = a.W;
+    const int nst = (a.K) >> 4;                        // stages (K = B*H*W, W % 16 == 0)
+    const int kbeg = tile.z * a.kstages_per_split;
+    const int kend = min(nst, kbeg + a.kstages_per_split);
+    const int cin = a.b_cin;
+
+    // operand bases: the slice's first pixel minus one row and one pixel (the window's reach back)
+    const int64_t p0 = (int64_t)kbeg * 16;
+    const int64_t pb = p0 - W - 1 > 0 ? p0 - W - 1 : 0;
+    const int lda4 = (int)a.lda * 4, ldb4 = (int)a.ldb * 4;
+    const __amdgpu_buffer_rsrc_t rsa = make_rsrc(a.A + p0 * a.lda + a.a_coff + co0);
+    const __amdgpu_buffer_rsrc_t rsb = make_rsrc(a.Bm + pb * a.ldb + a.b_coff + ci0);
+    // A: thread owns k-row tid/16 (pixel), columns 4(tid%16)..+3
+    const uint32_t aoff = (uint32_t)((tid >> 4) * lda4 + (tid & 15) * 16);
+    // B: element f = tid + 256 j -> window k-row kr = f/16 (ky = kr/18, kk = kr%18), column group f%16
+    int brel[NVB], bky[NVB], bkk[NVB];
+#pragma unroll
+    for (int j = 0; j < NVB; ++j) {
+        const int f = tid + 256 * j;
+        const int kr = f >> 4;
+        const bool in = kr < kWgWinK;
+        bky[j] = in ? kr / 18 : -(1 << 28);   // out-of-window slots: never in range
+        bkk[j] = kr - (kr / 18) * 18;
+        brel[j] = in ? ((kr / 18 - 1) * W + bkk[j] - 1) * ldb4 + (f & 15) * 16 : 0;
+    }
+
+    floatx16 acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+    WgPos pos;
+    pos.init(kbeg, H, W);
+    float4 ra, rb[NVB];
+    auto load = [&]() {
+        const int64_t pix = ((int64_t)pos.b * H + pos.y) * W + pos.x0;   // first pixel of the stage
+        ra = bload4(rsa, (uint32_t)((pix - p0) * lda4) + aoff);
+        const int sb = (int)((pix - pb) * ldb4);
+#pragma unroll
+        for (int j = 0; j < NVB; ++j) {
+            const int yy = pos.y + bky[j] - 1, xx = pos.x0 + bkk[j] - 1;
+            const bool ok = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+            rb[j] = bload4(rsb, ok ? (uint32_t)(sb + brel[j]) : kOOB);
+        }
+        pos.next(H, W);
+    };
+    auto store = [&](int buf) {
+        char* da = lds + buf * (SA + SB);
+        {
+            const auto sp = split_np<NP>(ra);
+            const int off = WgM::off(tid >> 4, (tid & 15) * 4);
+#pragma unroll
+            for (int p = 0; p < NP; ++p) *reinterpret_cast<uint2*>(da + p * PLA + off) = sp.p[p];
+        }
+#pragma unroll
+        for (int j = 0; j < NVB; ++j) {
+            const int f = tid + 256 * j;
+            if ((f >> 4) < kWgWinK) {
+                const auto sp = split_np<NP>(rb[j]);
+                const int off = WgM::off(f >> 4, (f & 15) * 4);
+#pragma unroll
+                for (int p = 0; p < NP; ++p) *reinterpret_cast<uint2*>(da + SA + p * PLB + off) = sp.p[p];
+            }
+        }
+    };
+    auto compute = [&](int buf) {
+        const char* sa = lds + buf * (SA + SB);
+        const char* sb = sa + SA;
+        bf16x8 fa[1][NP];
+        mnc_frag_at<kWgRows, NP>(sa, PLA, cbk * 32, 0, fa[0]);
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            bf16x8 fb[NP];
+            mnc_frag_at<kWgRows, NP>(sb, PLB, cib * 32, (t / 3) * 18 + (t % 3), fb);
+            if constexpr (NP == 3) {   // the six products of s3_mfma, smallest first
+                constexpr int P[6] = {2, 1, 0, 1, 0, 0};
+                constexpr int Q[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+                for (int u = 0; u < 6; ++u)
+                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][P[u]], fb[Q[u]], acc[t], 0, 0, 0);
+            } else {
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][0], fb[0], acc[t], 0, 0, 0);
+            }
+        }
+    };
+
+    if (kbeg < kend) {
+        load();
+        store(0);
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int kt = kbeg; kt < kend; ++kt) {
+        const bool more = kt + 1 < kend;
+        if (more) load();
+        compute(cur);
+        if (more) store(cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
+    }
+    // slab z: C[z][co][tap*cin + ci] (row stride a.ldc = 9*cin)
+    const int lane = tid & 63;
+    float* dst = a.C + (int64_t)tile.z * a.slab_stride;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int n = t * cin + ci0 + cib * 32 + (lane & 31);
+            const int co = co0 + cbk * 32 + 4 * (lane >> 5) + 8 * g;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) dst[(int64_t)(co + q) * a.ldc + n] = acc[t][4 * g + q];
+        }
+}
+
+}  // namespace cad

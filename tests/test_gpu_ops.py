@@ -92,6 +92,57 @@ def test_conv3x3_fwd_dgrad_wgrad(cad, dev, engine, B, H, W, cin, cout):
     assert max_rel_err(dw.cpu().permute(0, 3, 1, 2), wd.grad) < TOL
 
 
+WIN_SHAPES = [  # B, H, W, cin, cout: the window-tiled S3 forward/dgrad (gemm_win.hpp) block shapes
+    (2, 6, 64, 64, 128),    # R x CW = 2 x 64, three block rows
+    (1, 9, 32, 32, 128),    # 4 x 32, last block row partial (rows past H)
+    (2, 5, 48, 16, 128),    # 8 x 16 (48 = 3 x 16), 16 input channels (one channel block)
+    (1, 4, 128, 64, 64),    # N <= 64: 256 x 64 tile, 2 x 128
+    (2, 7, 64, 128, 64),    # N <= 64: 4 x 64, partial block row; dgrad N = 128: 2 x 64
+    (1, 13, 40, 256, 256),  # 16 x 8, H = 13 < R
+    (3, 5, 16, 64, 192),    # wgrad window: 16-pixel stages = whole rows, 3 images (halo rows at image edges)
+]
+
+
+@pytest.mark.parametrize("B,H,W,cin,cout", WIN_SHAPES)
+def test_conv3x3_window_kernel(cad, dev, B, H, W, cin, cout):
+    """S3 engine, window-tiled forward and dgrad (input read through a strided, channel-offset view as
+    in the decoder concat buffer; output likewise) against fp64."""
+    lib = cad.load_library()
+    prev = lib.cad_get_gemm_engine()
+    assert lib.cad_set_gemm_engine(1) == 0
+    try:
+        g = torch.Generator().manual_seed(H * W + cin + cout)
+        x = torch.randn(B, cin, H, W, generator=g)
+        w = torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)
+        dy = torch.randn(B, cout, H, W, generator=g)
+        xd, wd = x.double().requires_grad_(), w.double()
+        y_ref = F.conv2d(xd, wd, None, 1, 1)
+        y_ref.backward(dy.double())
+        ldx = cin + 12
+        xbuf = torch.zeros(B, H, W, ldx)
+        xbuf[..., 8:8 + cin] = nhwc(x)
+        xg, wg = xbuf.to(dev), w.permute(0, 2, 3, 1).contiguous().to(dev)
+        ld = cout + 8
+        ybuf = torch.full((B, H, W, ld), 7.0, device=dev)
+        assert lib.cad_op_conv3x3_fwd(_p(xg), ldx, 8, cin, _p(wg), cout, _p(ybuf), ld, 4, B, H, W, _s()) == 0
+        torch.cuda.synchronize()
+        assert max_rel_err(nchw(ybuf[..., 4:4 + cout].cpu()), y_ref.detach()) < TOL
+        assert (ybuf[..., :4] == 7).all() and (ybuf[..., 4 + cout:] == 7).all()
+        dx = torch.zeros(B, H, W, cin, device=dev)
+        assert lib.cad_op_conv3x3_dgrad(_p(nhwc(dy).to(dev)), cout, _p(wg), cin, _p(dx), cin, B, H, W, _s()) == 0
+        torch.cuda.synchronize()
+        assert max_rel_err(nchw(dx.cpu()), xd.grad) < TOL
+        # weight gradient: window-tiled when cout, cin % 64 == 0 and W % 16 == 0 (x read through the view)
+        wdd = w.double().requires_grad_()
+        F.conv2d(x.double(), wdd, None, 1, 1).backward(dy.double())
+        dw = torch.zeros(cout, 3, 3, cin, device=dev)
+        assert lib.cad_op_conv3x3_wgrad(_p(nhwc(dy).to(dev)), cout, _p(xg), ldx, 8, cin, _p(dw), B, H, W, _s()) == 0
+        torch.cuda.synchronize()
+        assert max_rel_err(dw.cpu().permute(0, 3, 1, 2), wdd.grad) < TOL
+    finally:
+        lib.cad_set_gemm_engine(prev)
+
+
 def test_conv3x3_wgrad_strided_input(cad, dev):
     """wgrad reading its input from the skip half of a concat-style buffer (ld = 2C, coff = C)."""
     lib = cad.load_library()
