@@ -414,7 +414,7 @@ struct WinPick {
 };
 WinPick pick_win(int cin, int W, int N) {
     WinPick w;
-    if (engine() != 1 || cin % 16 || (std::getenv("CAD_WIN") && std::getenv("CAD_WIN")[0] == '0')) return w;
+    if (engine() != 1 || cin % 16) return w;
     const int BM = N <= 64 ? 256 : 128;
     if (N % (BM == 128 ? 128 : 64)) return w;
     static const int c128[] = {64, 32, 16, 8}, c256[] = {128, 64};
@@ -515,8 +515,7 @@ void finish_slabs(float* slab, int splits, int64_t per, float* dw, hipStream_t s
 
 // window-tiled weight gradient (S3): cout, cin multiples of 64, W a multiple of 16
 bool use_wgrad_win(int cout, int cin, int W) {
-    return engine() == 1 && cout % 64 == 0 && cin % 64 == 0 && W % 16 == 0 &&
-           !(std::getenv("CAD_WIN") && std::getenv("CAD_WIN")[0] == '0');
+    return engine() == 1 && cout % 64 == 0 && cin % 64 == 0 && W % 16 == 0;
 }
 void launch_wgrad_win(GemmArgs& a, float* dw, float* slab, int64_t slab_cap, int64_t kbytes, hipStream_t st) {
     const int cin = a.b_cin;
