@@ -124,15 +124,18 @@ def _run(cad, dev, oracle, t0):
           f"lowest cosine {min(w[3] for w in worst):.7f}", t0)
     bad = [w for w in worst if not (w[3] >= 0.9999 and w[0] <= max(1e-2, 3 * w[1]))]
     assert not bad, bad
-    lr = 1e-4
+    lr, wd, eps = 1e-4, 1e-5, 1e-8
+    coef = min(1.0, 1.0 / (r["norm"] + 1e-6))   # clip_grad_norm_(1.0) scale of the oracle step
     moved = []
     for n, p in g_params.items():
         d = (p - ref.p[n]).abs()
-        # Adam's first step is ~lr * sign(g): a parameter moves by more than rounding (up to 2 lr) only
-        # where the two fp32 gradients may differ in sign (|g| within their error of fp64)
+        # Adam's first step is lr * g' / (|g'| + eps) with g' = clipped g + wd * w (coupled L2): a weight
+        # moves by more than rounding only where the two fp32 paths may disagree on g' — its sign, or
+        # its size where |g'| is comparable to eps
         g, thr = flip_thr[n]
+        g_adam = (g * coef + wd * params[n].double()).abs()
         flip = d > 1e-5
-        unexplained = int((g[flip] > thr).sum()) if n in flip_thr else int(flip.sum())
+        unexplained = int((g_adam[flip] > max(thr * coef, 100 * eps)).sum())
         moved.append((unexplained, d.max().item(), int(flip.sum()), n))
     moved.sort(reverse=True)
     _beat(f"params after Adam (unexplained moves, max |diff|, moves > 1e-5, name): {moved[:3]}", t0)
