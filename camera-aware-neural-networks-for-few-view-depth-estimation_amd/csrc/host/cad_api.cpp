@@ -483,8 +483,8 @@ void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin,
     const int64_t M = h->Ml(l, B);
     const bool tr = h->train;
     const bool ps = h->fwd_np > 0;
-    auto bn = [&](BN& b, int cin) {
-        const int rows = cad::conv3x3_stats_rows(cin, B, Hh, Ww, C);
+    auto bn = [&](BN& b, int cin, bool ps_conv) {
+        const int rows = cad::conv3x3_stats_rows(cin, B, Hh, Ww, C, ps_conv);
         if (tr)
             cad::bn_fwd_finalize(h->stats, rows, C, M, h->P(b.widx), h->P(b.bidx), b.rm, b.rv, 0.1f, 1e-5f, h->dscr,
                                  b.mean, b.invstd, b.scale, b.shift, st);
@@ -492,11 +492,12 @@ void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin,
             cad::bn_eval_coeffs(h->P(b.widx), h->P(b.bidx), b.rm, b.rv, C, 1e-5f, b.mean, b.invstd, b.scale, b.shift, st);
     };
     float* stats = tr ? h->stats : nullptr;
-    if (ps && in_s.p && dc.c1.ws)
+    const bool ps1 = ps && in_s.p && dc.c1.ws;
+    if (ps1)
         cad::conv3x3_fwd_ps(in_s, dc.c1.cin, sv(dc.c1.ws, 9 * dc.c1.cin), C, dc.y1, C, 0, B, Hh, Ww, stats, st);
     else
         cad::conv3x3_fwd(in, ldin, 0, dc.c1.cin, h->P(dc.c1.pidx), C, dc.y1, C, 0, B, Hh, Ww, stats, st);
-    bn(dc.b1, dc.c1.cin);
+    bn(dc.b1, dc.c1.cin, ps1);
     if (dc.has_film()) {   // FiLMDoubleConvImpl::forward (intrinsics_unet.h:38-52)
         cad::film_apply(dc.y1, C, dc.b1.scale, dc.b1.shift, dc.film.gam, dc.film.bet, B, (int64_t)Hh * Ww, dc.a1, st);
         if (ps) cad::split_rows(dc.a1, C, 0, C, M, dc.a1s, C, 0, st);
@@ -509,7 +510,7 @@ void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin,
         cad::conv3x3_fwd_ps(sv(dc.a1s, C), C, sv(dc.c2.ws, 9 * C), C, dc.y2, C, 0, B, Hh, Ww, stats, st);
     else
         cad::conv3x3_fwd(dc.a1, C, 0, C, h->P(dc.c2.pidx), C, dc.y2, C, 0, B, Hh, Ww, stats, st);
-    bn(dc.b2, C);
+    bn(dc.b2, C, ps);
     const bool twin = ps && out_s.p;
     cad::bn_relu_fwd(dc.y2, C, dc.b2.scale, dc.b2.shift, (out_f32 || !twin) ? out : nullptr, ldo, ocoff, M, st,
                      twin ? const_cast<void*>(out_s.p) : nullptr, out_s.ld, out_s.coff);

@@ -181,6 +181,12 @@ __global__ __launch_bounds__(256, 3) void k_conv3x3_win_s3(GemmArgs a) {
     conv3x3_win_body<3, R, CW, R * CW == 128 ? 2 : 4, R * CW == 128 ? 2 : 1, Epi>(a);
 }
 
+// window-tiled conv3x3 forward/dgrad on the pre-split bf16 twins (B1)
+template <int R, int CW, class Epi>
+__global__ __launch_bounds__(256, 3) void k_conv3x3_win_bf16p(GemmArgs a) {
+    conv3x3_win_ps_body<R, CW, R * CW == 128 ? 2 : 4, R * CW == 128 ? 2 : 1, Epi>(a);
+}
+
 // window-tiled conv3x3 weight gradient (gemm_win.hpp): 64 co x 64 ci x 9 taps per workgroup, split-K
 __global__ __launch_bounds__(256, 2) void k_conv3x3_wgrad_win_s3(GemmArgs a) { conv3x3_wgrad_win_body<3>(a); }
 
@@ -430,36 +436,55 @@ WinPick pick_win(int cin, int W, int N) {
 }
 int win_blocks(const WinPick& w, int B, int H, int W) { return B * cdiv(H, w.R) * (W / w.CW); }
 
-template <int R, int CW, class Epi>
+// PS = false: S3 window kernel (fp32 operands, in-loader split); true: B1 on the pre-split twins
+template <bool PS, int R, int CW, class Epi>
 void launch_win1(const GemmArgs& a, hipStream_t st) {
     const dim3 grid(win_blocks(WinPick{R, CW}, a.B, a.H, a.W), cdiv(a.N, R * CW == 128 ? 128 : 64));
+    auto fn = PS ? (void (*)(GemmArgs))k_conv3x3_win_bf16p<R, CW, Epi> : (void (*)(GemmArgs))k_conv3x3_win_s3<R, CW, Epi>;
     if (prof_enabled()) {
         char name[160];
-        snprintf(name, sizeof(name), "void cad::k_conv3x3_win_s3<%d, %d, cad::%s>(cad::GemmArgs)", R, CW,
-                 Epi::STATS ? "EpiStoreStats" : "EpiStore");
+        snprintf(name, sizeof(name), "void cad::k_conv3x3_win_%s<%d, %d, cad::%s>(cad::GemmArgs)", PS ? "bf16p" : "s3", R,
+                 CW, Epi::STATS ? "EpiStoreStats" : "EpiStore");
         prof_push(name, 2.0 * a.M * a.N * (double)a.K, st);
-        hipLaunchKernelGGL((k_conv3x3_win_s3<R, CW, Epi>), grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL(fn, grid, dim3(256), 0, st, a);
         prof_pop(st);
     } else {
-        hipLaunchKernelGGL((k_conv3x3_win_s3<R, CW, Epi>), grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL(fn, grid, dim3(256), 0, st, a);
     }
 }
-template <class Epi>
+template <class Epi, bool PS = false>
 void launch_win(const WinPick& w, const GemmArgs& a, hipStream_t st) {
     if (w.R * w.CW == 128) {
         switch (w.CW) {
-            case 64: launch_win1<2, 64, Epi>(a, st); return;
-            case 32: launch_win1<4, 32, Epi>(a, st); return;
-            case 16: launch_win1<8, 16, Epi>(a, st); return;
-            case 8: launch_win1<16, 8, Epi>(a, st); return;
+            case 64: launch_win1<PS, 2, 64, Epi>(a, st); return;
+            case 32: launch_win1<PS, 4, 32, Epi>(a, st); return;
+            case 16: launch_win1<PS, 8, 16, Epi>(a, st); return;
+            case 8: launch_win1<PS, 16, 8, Epi>(a, st); return;
         }
     } else {
         switch (w.CW) {
-            case 128: launch_win1<2, 128, Epi>(a, st); return;
-            case 64: launch_win1<4, 64, Epi>(a, st); return;
+            case 128: launch_win1<PS, 2, 128, Epi>(a, st); return;
+            case 64: launch_win1<PS, 4, 64, Epi>(a, st); return;
         }
     }
     throw std::runtime_error("window conv: block shape not built");
+}
+// B1 window kernel on the pre-split twins: 32-channel stages
+WinPick pick_win_ps(int cin, int W, int N, int acoff) {
+    WinPick w;
+    if (engine() != 2 || cin % 32 || acoff % 8) return w;
+    const int BM = N <= 64 ? 256 : 128;
+    if (N % (BM == 128 ? 128 : 64)) return w;
+    static const int c128[] = {64, 32, 16, 8}, c256[] = {128, 64};
+    const int* cws = BM == 128 ? c128 : c256;
+    const int ncw = BM == 128 ? 4 : 2;
+    for (int i = 0; i < ncw; ++i)
+        if (W % cws[i] == 0) {
+            w.CW = cws[i];
+            w.R = BM / cws[i];
+            return w;
+        }
+    return w;
 }
 
 // split-K planning for the weight-gradient GEMMs: aim for >= ~2048 workgroups, >= 32 K-stages each.
@@ -559,8 +584,8 @@ void launch_wgrad(GemmArgs& a, float* dw, float* slab, int64_t slab_cap, int64_t
 void set_gemm_engine(int e) { g_engine = (e == 1 || e == 2) ? e : 0; }
 int gemm_engine() { return engine(); }
 
-int conv3x3_stats_rows(int cin, int B, int H, int W, int cout) {
-    const WinPick w = pick_win(cin, W, cout);
+int conv3x3_stats_rows(int cin, int B, int H, int W, int cout, bool ps) {
+    const WinPick w = ps ? pick_win_ps(cin, W, cout, 0) : pick_win(cin, W, cout);
     if (w.R) return win_blocks(w, B, H, W);
     return cdiv((int64_t)B * H * W, tile_m(pick_cfg(B * H * W, cout)));
 }
@@ -686,6 +711,11 @@ void conv3x3_fwd_ps(Split x, int cin, Split w, int cout, float* y, int64_t ldy, 
     a.Bm = (const float*)w.p; a.ldb = w.ld; a.b_coff = w.coff;
     a.C = y; a.ldc = ldy; a.c_coff = ycoff;
     a.stats = stats;
+    if (const WinPick wp = pick_win_ps(cin, W, cout, x.coff); wp.R && w.coff == 0) {
+        if (stats) launch_win<EpiStoreStats, true>(wp, a, st);
+        else launch_win<EpiStore, true>(wp, a, st);
+        return;
+    }
     const Cfg c = pick_cfg(a.M, a.N);
     const int kb = ps_kb(true, c);
     a.kstages_per_split = cdiv(a.K, kb);
@@ -705,6 +735,10 @@ void conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t 
     a.A = (const float*)dz.p; a.lda = dz.ld; a.a_coff = dz.coff; a.a_cin = cout;
     a.Bm = (const float*)wd.p; a.ldb = wd.ld; a.b_coff = wd.coff;
     a.C = dx; a.ldc = lddx; a.c_coff = 0;
+    if (const WinPick wp = pick_win_ps(cout, W, cin, dz.coff); wp.R && wd.coff == 0) {
+        launch_win<EpiStore, true>(wp, a, st);
+        return;
+    }
     const Cfg c = pick_cfg(a.M, a.N);
     const int kb = ps_kb(true, c);
     a.kstages_per_split = cdiv(a.K, kb);

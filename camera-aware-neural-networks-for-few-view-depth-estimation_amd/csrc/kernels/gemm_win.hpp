@@ -271,6 +271,149 @@ __device__ __forceinline__ void conv3x3_win_body(const GemmArgs& a) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// B1 window kernel on pre-split operands (the bf16 twins of gemm_ps.hpp, NP = 1: plain NHWC bf16):
+// the same blocks and window walk, with 32-channel stages (cb, ky) and no conversion at all — the
+// loaders move 16-B pieces (8 channels) global -> registers -> LDS.  LDS images use the 80-B rows of
+// S3<32> (conflict-free ds_read_b128): A window [R*(CW+2)][32] + B [3 taps][BN][32], one stage
+// (41 KB for 128x128), 6 k16 steps x MI x NJ MFMAs per wave and stage.
+// Requirements (host): A channels % 32 == 0, twin offsets % 8 == 0, W % CW == 0, N % BN == 0.
+// ------------------------------------------------------------------------------------------------
+template <int R, int CW, int BN>
+struct WinPsGeo {
+    static constexpr int WC = CW + 2;
+    static constexpr int WPIX = R * WC;
+    static constexpr int LDK = S3<32>::LDK;               // 40 bf16 per LDS row
+    static constexpr int NTA = WPIX * 4;                   // A pieces per stage (4 x 8 channels per pixel)
+    static constexpr int NVA = (NTA + 255) / 256;
+    static constexpr int NTB = BN * 4;                     // B pieces per tap
+    static constexpr int JB = (NTB + 255) / 256;
+    static constexpr int SA = WPIX * LDK, SBT = BN * LDK;  // bf16 elements: A image, one tap of B
+};
+
+template <int R, int CW, int WM, int WN, class Epi>
+__device__ __forceinline__ void conv3x3_win_ps_body(const GemmArgs& a) {
+    constexpr int MI = 2, NJ = 2;
+    constexpr int BM = 32 * MI * WM, BN = 32 * NJ * WN;
+    static_assert(BM == R * CW, "tile");
+    using G = WinPsGeo<R, CW, BN>;
+    __shared__ __attribute__((aligned(16))) uint16_t lds[G::SA + 3 * G::SBT];
+
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int wm = wave / WN, wn = wave % WN;
+    const TileId tile = xcd_tile();
+    const int nbx = a.W / CW, nby = (a.H + R - 1) / R;
+    const int tx = tile.x % nbx, t2 = tile.x / nbx, ty = t2 % nby, b = t2 / nby;
+    const int y0 = ty * R, x0 = tx * CW, n0 = tile.y * BN;
+    const int H = a.H, W = a.W, cin = a.a_cin;
+    const int S = 3 * (cin / 32);
+
+    // A: bf16 rows of lda elements; piece (window pixel w, group g) of stage (cb, ky)
+    const int rowb = (int)a.lda * 2;
+    const int64_t pbase = ((int64_t)b * H + y0 - 1) * W + x0 - 1;
+    const int64_t pb = pbase > 0 ? pbase : 0;
+    const __amdgpu_buffer_rsrc_t rsa =
+        make_rsrc(reinterpret_cast<const float*>(reinterpret_cast<const char*>(a.A) + (pb * a.lda + a.a_coff) * 2));
+    int aoff[G::NVA], awr[G::NVA], alds[G::NVA];
+#pragma unroll
+    for (int j = 0; j < G::NVA; ++j) {
+        const int f = tid + 256 * j;
+        const int w = f >> 2, g = f & 3;
+        const int r = w / G::WC, c = w - r * G::WC;
+        const int x = x0 - 1 + c;
+        const bool ok = f < G::NTA && (unsigned)x < (unsigned)W;
+        awr[j] = ok ? r : -(1 << 28);
+        aoff[j] = (int)((r * (int64_t)W + c + (pbase - pb)) * rowb) + g * 16;
+        alds[j] = (f < G::NTA ? w : 0) * G::LDK + g * 8;
+    }
+    // B: weight twin rows of ldb elements (ldb = 9*cin), piece (tap, row, group)
+    const int rowbb = (int)a.ldb * 2;
+    const __amdgpu_buffer_rsrc_t rsb =
+        make_rsrc(reinterpret_cast<const float*>(reinterpret_cast<const char*>(a.Bm) + ((int64_t)n0 * a.ldb + a.b_coff) * 2));
+    int boff[G::JB], blds[G::JB];
+#pragma unroll
+    for (int jj = 0; jj < G::JB; ++jj) {
+        const int task = tid + 256 * jj;
+        const int row = task >> 2, g = task & 3;
+        boff[jj] = row * rowbb + g * 16;
+        blds[jj] = (task < G::NTB ? row : 0) * G::LDK + g * 8;
+    }
+    auto bact = [&](int jj) { return 256 * (jj + 1) <= G::NTB || tid + 256 * jj < G::NTB; };
+
+    int wpix[MI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+        const int p = wm * 32 * MI + i * 32 + (lane & 31);
+        const int r = p / CW;
+        wpix[i] = r * G::WC + (p - r * CW);
+    }
+
+    floatx16 acc[MI][NJ];
+    acc_zero(acc);
+    uint4 ra[G::NVA], rb[3 * G::JB];
+    int cb = 0, ky = 0;
+    auto load = [&]() {
+        const int adda = ky * W * rowb + cb * 64;                   // 32 channels = 64 bytes
+#pragma unroll
+        for (int j = 0; j < G::NVA; ++j) {
+            const int y = y0 - 1 + ky + awr[j];
+            ra[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  rsa, (unsigned)y < (unsigned)H ? (uint32_t)(aoff[j] + adda) : kOOB, 0, 0));
+        }
+        const int addb = 3 * ky * cin * 2 + cb * 64;
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+#pragma unroll
+            for (int jj = 0; jj < G::JB; ++jj)
+                if (bact(jj))
+                    rb[t * G::JB + jj] = __builtin_bit_cast(
+                        uint4, __builtin_amdgcn_raw_buffer_load_b128(rsb, (uint32_t)(boff[jj] + addb + t * cin * 2), 0, 0));
+        if (++ky == 3) { ky = 0; ++cb; }
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int j = 0; j < G::NVA; ++j)
+            if (tid + 256 * j < G::NTA) *reinterpret_cast<uint4*>(lds + alds[j]) = ra[j];
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+#pragma unroll
+            for (int jj = 0; jj < G::JB; ++jj)
+                if (bact(jj)) *reinterpret_cast<uint4*>(lds + G::SA + t * G::SBT + blds[jj]) = rb[t * G::JB + jj];
+    };
+    auto compute = [&]() {
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                bf16x8 fa[MI][1], fb[NJ][1];
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) s3_frag<BN, 32, 1>(lds + G::SA + kx * G::SBT, wn * 32 * NJ + j * 32, q, fb[j]);
+#pragma unroll
+                for (int i = 0; i < MI; ++i)
+                    fa[i][0] = *reinterpret_cast<const bf16x8*>(lds + (wpix[i] + kx) * G::LDK + q * 16 + (lane >> 5) * 8);
+                s3_mfma<1>(acc, fa, fb);
+            }
+    };
+
+    if (S > 0) {
+        load();
+        store();
+    }
+    __syncthreads();
+    for (int s = 0; s < S; ++s) {
+        const bool more = s + 1 < S;
+        if (more) load();
+        compute();
+        __syncthreads();
+        if (more) {
+            store();
+            __syncthreads();
+        }
+    }
+    win_epilogue<WM, WN, MI, NJ, CW, Epi>(a, acc, tile.x, n0, b, y0, x0, reinterpret_cast<float*>(lds));
+}
+
+// ------------------------------------------------------------------------------------------------
 // Window-tiled conv3x3 weight gradient (S3 / B1):  dW[co][tap][ci] = sum_pix dZ[pix][co] X[pix+tap][ci]
 //
 // The im2col weight-gradient GEMM (M = cout, N = 9*cin, K = pixels; MNcIm2col3x3) fetches and splits

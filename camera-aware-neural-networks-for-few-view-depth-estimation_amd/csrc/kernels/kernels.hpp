@@ -22,7 +22,8 @@ int gemm_engine();
 // y = conv3x3(x) (+ per-tile BN partials [rows][2][cout] when stats != nullptr)
 void conv3x3_fwd(const float* x, int64_t ldx, int xcoff, int cin, const float* w, int cout, float* y,
                  int64_t ldy, int ycoff, int B, int H, int W, float* stats, hipStream_t st);
-int conv3x3_stats_rows(int cin, int B, int H, int W, int cout);   // BN partial rows of conv3x3_fwd
+// BN partial rows of conv3x3_fwd (ps = true: of conv3x3_fwd_ps on the pre-split twins)
+int conv3x3_stats_rows(int cin, int B, int H, int W, int cout, bool ps = false);
 // dx[pix][ci] = conv3x3(dz, wd) with wd = repacked [ci][tap'][co]
 void conv3x3_dgrad(const float* dz, int cout, const float* wd, int cin, float* dx, int64_t lddx,
                    int B, int H, int W, hipStream_t st);

@@ -117,7 +117,7 @@ def _run(cad, dev, oracle, t0):
         # a gradient element whose sign the two fp32 paths may disagree on: |g| within 3x the larger
         # of the two paths' max error against fp64
         err = max((ours.double() - gd).abs().max().item(), (g32.double() - gd).abs().max().item())
-        flip_thr[n] = (gd.abs(), 3 * err)
+        flip_thr[n] = (gd, 3 * err)
     del g64
     worst.sort(reverse=True)
     _beat(f"gradients vs fp64 (ours, fp32 oracle, name, cosine): {worst[:4]}; "
@@ -126,7 +126,8 @@ def _run(cad, dev, oracle, t0):
     assert not bad, bad
     lr, wd, eps = 1e-4, 1e-5, 1e-8
     coef = min(1.0, 1.0 / (r["norm"] + 1e-6))   # clip_grad_norm_(1.0) scale of the oracle step
-    moved = []
+    moved, diag = [], []
+    ref_g32 = {n: g for (n, _), g in zip(oracle.param_spec(F), r["grads"])}
     for n, p in g_params.items():
         d = (p - ref.p[n]).abs()
         # Adam's first step is lr * g' / (|g'| + eps) with g' = clipped g + wd * w (coupled L2): a weight
@@ -135,10 +136,20 @@ def _run(cad, dev, oracle, t0):
         g, thr = flip_thr[n]
         g_adam = (g * coef + wd * params[n].double()).abs()
         flip = d > 1e-5
-        unexplained = int((g_adam[flip] > max(thr * coef, 100 * eps)).sum())
+        un = flip & (g_adam > max(thr * coef, 100 * eps))
+        unexplained = int(un.sum())
         moved.append((unexplained, d.max().item(), int(flip.sum()), n))
+        if unexplained:   # what each side saw for those weights
+            w0 = params[n].double()
+            idx = un.nonzero()[:4]
+            diag.append((n, thr * coef, [(tuple(i.tolist()), (g * coef)[tuple(i)].item(), (g_grads[n].double() * coef)[tuple(i)].item(),
+                                         (ref_g32[n].double() * coef)[tuple(i)].item(), (wd * w0)[tuple(i)].item(),
+                                         (p.double() - w0)[tuple(i)].item(), (ref.p[n].double() - w0)[tuple(i)].item())
+                                        for i in idx]))
     moved.sort(reverse=True)
     _beat(f"params after Adam (unexplained moves, max |diff|, moves > 1e-5, name): {moved[:3]}", t0)
+    for dg in diag:
+        _beat(f"unexplained {dg[0]} thr {dg[1]:.3e}: (index, fp64 g, ours, fp32 oracle, wd*w, our step, oracle step) {dg[2]}", t0)
     assert all(u == 0 and mx <= 2 * lr + 1e-6 for u, mx, _, _ in moved), moved[:3]
     for n, b in g_bufs.items():
         assert max_rel_err(b, ref.bufs[n]) < 1e-4, n

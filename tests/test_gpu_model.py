@@ -171,7 +171,7 @@ def bf16_engine(cad):
     lib.cad_set_gemm_engine(prev)
 
 
-@pytest.mark.parametrize("f,B,H,W", [(16, 2, 64, 96), (32, 2, 48, 64), (64, 2, 64, 64)])
+@pytest.mark.parametrize("f,B,H,W", [(16, 2, 64, 96), (32, 2, 48, 64), (64, 2, 64, 64), (64, 2, 48, 128)])
 def test_train_step_bf16_engine_vs_oracle(cad, dev, oracle, bf16_engine, f, B, H, W):
     """The bf16 configs (BASELINE configs 3-5): every conv/ConvT contraction multiplies bf16-rounded
     operands with fp32 accumulation; BN, the head, the loss, clip and Adam stay fp32.  Yardstick: the
