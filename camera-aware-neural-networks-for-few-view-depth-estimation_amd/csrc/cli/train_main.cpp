@@ -1,6 +1,7 @@
 // build/train — drop-in for the reference's `./build/train --config <yaml>` entry point
 // (src/training/train_main.cpp:279-507 driving TensorBoardTrainerEnhanced, enhanced.h:142-334),
-// on libcad_hip.so through the C++ drop-in classes of include/cad/cad.hpp.
+// on libcad_hip.so through the C++ drop-in classes of include/cad/cad.hpp and the trainer of
+// include/cad/trainer.hpp (SunRGBDLoader + TensorBoardTrainerEnhanced).
 //
 //   build/train -c configs/train_config.yaml [-e baseline_unet] [-g 0] [-d] [--tensorboard true]
 //               [-r checkpoint.cadckpt | model.pt]
@@ -13,8 +14,9 @@
 // Deliberate differences: the model lives on the GPU (the reference never moves it,
 // SURVEY §0 fact 2); --resume really resumes (params + BN buffers + Adam state; the reference parses
 // and ignores it); TensorBoard events are written as a CSV of scalars (no Python tensorboard here);
-// the dataset is data.dataset_name: "synthetic" (SUN-RGB-D-shaped counter-based samples) — decoding
-// the real SUN RGB-D JPEG/PNG files needs OpenCV, absent on this image.
+// model.architecture selects the FiLM models (the reference always builds BaselineUNet);
+// data.dataset_name "synthetic" trains on generated samples, anything else on the manifest's PNG/PNM
+// files (JPEG decoding needs a decoder this image lacks); hardware.distributed runs DP over RCCL.
 #include <signal.h>
 #include <spawn.h>
 #include <sys/wait.h>
@@ -37,6 +39,7 @@
 #include <vector>
 
 #include "../../../include/cad/cad.hpp"
+#include "../../../include/cad/trainer.hpp"
 #include "../host/yaml_lite.hpp"
 
 namespace fs = std::filesystem;
@@ -99,8 +102,10 @@ struct Config {   // the TrainingConfig fields the step uses (trainer.h:24-92)
     float si = 1.0f, grad = 0.1f, smooth = 0.001f, reproj = 0.01f, max_depth = 10.0f;
     int init_features = 64, height = 240, width = 320, seed = 42;
     std::string checkpoint_dir = "./checkpoints", log_dir = "./logs", experiment_name = "baseline_unet";
-    std::string dataset = "sunrgbd";
+    std::string dataset = "sunrgbd", data_dir = "./data/sunrgbd";
     std::string manifest_path = "./data/sunrgbd_manifest.json";
+    std::vector<std::string> sensor_types;   // data.sensor_types (empty: all four)
+    std::string architecture = "baseline_unet";
     int n_train = 64, n_val = 16;
     // data.augmentation (train_main.cpp:377-386 -> AugmentationConfig, random_seed 42)
     bool aug_crop = true, aug_flip = true, aug_jitter = true;
@@ -149,9 +154,15 @@ Config load_config(const yaml_lite::Node& y, const std::string& experiment) {   
         if (ex["training"] && ex["training"]["batch_size"]) c.batch_size = ex["training"]["batch_size"].as<int>();
         if (ex["experiment"] && ex["experiment"]["name"]) c.experiment_name = ex["experiment"]["name"].as<std::string>();
     }
-    if (auto& m = y["model"]) {   // :325-333 (architecture key ignored, like the reference)
+    if (auto& m = y["model"]) {   // :325-333
         c.init_features = m["init_features"].as<int>(64);
         c.max_depth = m["max_depth"].as<float>(10.0f);
+        // the reference parses model.architecture and always builds BaselineUNet; here it selects the
+        // FiLM models of configs 3 (intrinsics_unet: FiLM blocks; ray_film_unet: + ray-enhanced enc1)
+        c.architecture = m["architecture"].as<std::string>("baseline_unet");
+        if (c.architecture != "baseline_unet" && c.architecture != "intrinsics_unet" && c.architecture != "ray_film_unet")
+            throw std::runtime_error("model.architecture '" + c.architecture +
+                                     "': this build trains baseline_unet, intrinsics_unet or ray_film_unet");
     }
     if (auto& d = y["data"]) {
         c.height = d["input_height"].as<int>(240);
@@ -160,6 +171,8 @@ Config load_config(const yaml_lite::Node& y, const std::string& experiment) {   
         c.n_train = d["num_train_samples"].as<int>(64);
         c.n_val = d["num_val_samples"].as<int>(16);
         c.manifest_path = d["manifest_path"].as<std::string>("./data/sunrgbd_manifest.json");
+        c.data_dir = d["data_dir"].as<std::string>("./data/sunrgbd");
+        c.sensor_types = d["sensor_types"].as<std::vector<std::string>>({});
         if (auto& a = d["augmentation"]) {
             c.aug_crop = a["random_crop"].as<bool>(true);
             c.aug_flip = a["horizontal_flip"].as<bool>(true);
@@ -180,116 +193,8 @@ Config load_config(const yaml_lite::Node& y, const std::string& experiment) {   
     return c;
 }
 
-// ---- synthetic SUN-RGB-D-shaped samples (same generator as synthetic.py / SURVEY §8d) ----
-uint64_t splitmix64(uint64_t seed, uint64_t idx) {
-    uint64_t z = seed + (idx + 1) * 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-float u01(uint64_t seed, uint64_t idx) { return (float)((uint32_t)(splitmix64(seed, idx) >> 32) >> 8) * (1.0f / 16777216.0f); }
-
-struct HostBatch {
-    std::vector<float> rgb, gt, K;
-};
-// sample s of a split = sample s of one virtual batch (split offsets keep train/val disjoint)
-void make_sample(int64_t s, int H, int W, float* rgb, float* gt, float* K) {
-    const int64_t HW = (int64_t)H * W;
-    for (int64_t i = 0; i < 3 * HW; ++i) rgb[i] = u01(0xC0FFEE, s * 3 * HW + i);
-    for (int v = 0; v < H; ++v)
-        for (int u = 0; u < W; ++u) {
-            const int64_t idx = s * HW + (int64_t)v * W + u;
-            double d = 0.5 + 9.0 * (0.5 + 0.5 * std::sin(2.0 * M_PI * ((double)u / W * 1.3 + (double)v / H * 0.7 + 0.1 * s)));
-            d = std::min(9.5, std::max(0.5, d));
-            if (u01(0xD3E7, idx) < 0.15f || v < H / 16) d = 0.0;
-            gt[(int64_t)v * W + u] = (float)d;
-        }
-    const bool even = s % 2 == 0;
-    const float sx = (float)W / 640.f, sy = (float)H / 480.f;
-    std::fill(K, K + 9, 0.f);
-    K[0] = (even ? 518.858f : 570.342f) * sx;
-    K[2] = (even ? 325.582f : 320.0f) * sx;
-    K[4] = (even ? 519.470f : 570.342f) * sy;
-    K[5] = (even ? 253.736f : 240.0f) * sy;
-    K[8] = 1.f;
-}
-
 bool ends_with(const std::string& s, const std::string& suf) {
     return s.size() >= suf.size() && s.compare(s.size() - suf.size(), suf.size(), suf) == 0;
-}
-
-// ---- checkpoint (.cadckpt): named tensors in reference layout + Adam state ----
-void save_checkpoint(const std::string& path, BaselineUNetImpl& m, optim::Adam& opt) {
-    std::ofstream f(path, std::ios::binary);
-    if (!f) throw std::runtime_error("cannot write checkpoint " + path);
-    auto ps = m.named_parameters();
-    auto bs = m.named_buffers();
-    ps.insert(ps.end(), bs.begin(), bs.end());
-    f.write("CADCKPT1", 8);
-    int32_t n = (int32_t)ps.size();
-    f.write((const char*)&n, 4);
-    for (auto& t : ps) {
-        int32_t ln = (int32_t)t.name.size(), nd = (int32_t)t.shape.size();
-        f.write((const char*)&ln, 4);
-        f.write(t.name.data(), ln);
-        f.write((const char*)&nd, 4);
-        f.write((const char*)t.shape.data(), 8 * nd);
-        f.write((const char*)t.value.data(), 4 * (int64_t)t.value.size());
-    }
-    float *mp, *vp, *pp;
-    int64_t nflat;
-    cad::check(cad_unet_flat(m.handle(), &pp, nullptr, &nflat), "flat");
-    cad::check(cad_adam_state(opt.handle(), &mp, &vp), "adam_state");
-    std::vector<float> buf((size_t)nflat);
-    int64_t step = opt.step_count();
-    f.write("ADAM", 4);
-    f.write((const char*)&step, 8);
-    f.write((const char*)&nflat, 8);
-    for (float* src : {mp, vp}) {
-        cad::check(cad_memcpy(buf.data(), src, 4 * nflat, 1, nullptr), "d2h");
-        f.write((const char*)buf.data(), 4 * nflat);
-    }
-}
-
-void load_checkpoint(const std::string& path, BaselineUNetImpl& m, optim::Adam& opt) {
-    std::ifstream f(path, std::ios::binary);
-    if (!f) throw std::runtime_error("Cannot open checkpoint: " + path);
-    char magic[8];
-    f.read(magic, 8);
-    if (std::memcmp(magic, "CADCKPT1", 8) != 0) throw std::runtime_error("not a .cadckpt file: " + path);
-    int32_t n;
-    f.read((char*)&n, 4);
-    std::vector<NamedTensor> ts((size_t)n);
-    for (auto& t : ts) {
-        int32_t ln, nd;
-        f.read((char*)&ln, 4);
-        t.name.resize((size_t)ln);
-        f.read(&t.name[0], ln);
-        f.read((char*)&nd, 4);
-        t.shape.resize((size_t)nd);
-        f.read((char*)t.shape.data(), 8 * nd);
-        int64_t cnt = 1;
-        for (auto s : t.shape) cnt *= s;
-        t.value.resize((size_t)cnt);
-        f.read((char*)t.value.data(), 4 * cnt);
-    }
-    if (m.load(ts) != n) throw std::runtime_error("checkpoint does not match the model: " + path);
-    char tag[4];
-    if (f.read(tag, 4) && std::memcmp(tag, "ADAM", 4) == 0) {
-        int64_t step, nflat, mine;
-        f.read((char*)&step, 8);
-        f.read((char*)&nflat, 8);
-        float *mp, *vp;
-        cad::check(cad_unet_flat(m.handle(), nullptr, nullptr, &mine), "flat");
-        if (nflat != mine) throw std::runtime_error("optimizer state size mismatch in " + path);
-        cad::check(cad_adam_state(opt.handle(), &mp, &vp), "adam_state");
-        std::vector<float> buf((size_t)nflat);
-        for (float* dst : {mp, vp}) {
-            f.read((char*)buf.data(), 4 * nflat);
-            cad::check(cad_memcpy(dst, buf.data(), 4 * nflat, 0, nullptr), "h2d");
-        }
-        cad::check(cad_adam_set_step_count(opt.handle(), step), "set_step");
-    }
 }
 
 // ---- data-parallel job: one process per GPU (hardware.distributed / num_gpus / gpu_ids,
@@ -472,12 +377,14 @@ int run(const Args& args) {
     // manifest (its split argument is unused, sunrgbd_loader.cpp:39-78); validation takes the first
     // min(500, size) samples (validateEpoch :343) without augmentation.
     const bool real = c.dataset != "synthetic";
-    std::unique_ptr<cad_dataset, void (*)(cad_dataset*)> ds(nullptr, cad_dataset_destroy);
-    if (real) {
+    if (real) {   // the sample count, read on the host before any GPU call
+        std::vector<const char*> sens;
+        for (const auto& x : c.sensor_types) sens.push_back(x.c_str());
         cad_dataset* d = nullptr;
-        cad::check(cad_dataset_open(c.manifest_path.c_str(), nullptr, 0, &d), "SunRGBDLoader");
-        ds.reset(d);
+        cad::check(cad_dataset_open(c.manifest_path.c_str(), sens.empty() ? nullptr : sens.data(), (int)sens.size(), &d),
+                   "SunRGBDLoader");
         c.n_train = (int)cad_dataset_size(d);
+        cad_dataset_destroy(d);
         c.n_val = std::min(500, c.n_train);
         if (c.n_train == 0) throw std::runtime_error("no usable samples in " + c.manifest_path);
     }
@@ -489,178 +396,77 @@ int run(const Args& args) {
     cad::check(cad_device_count(&ndev), "device query");
     if (R.device < 0 || R.device >= ndev) throw std::runtime_error("GPU " + std::to_string(R.device) + " not available");
     cad::check(cad_set_device(R.device), "set device");
-    if (lead) {
-        fs::create_directories(c.checkpoint_dir);
-        fs::create_directories(c.log_dir);
-    }
 
-    const int B = c.batch_size, H = c.height, W = c.width;
-    cad::Workspace ws{B, H, W, R.device};
-    BaselineUNetImpl model(3, c.init_features, c.max_depth, ws);
-    CombinedDepthLoss loss_fn(c.si, c.grad, c.smooth, c.reproj, ws);
-    optim::Adam opt(model, c.learning_rate, c.weight_decay);
-    std::unique_ptr<distributed::Communicator> comm;
-    if (R.dp) comm = std::make_unique<distributed::Communicator>(exchange_id(R, false), R.world, R.rank, R.device);
+    // the loaders (train_main.cpp:366-395): both splits read the same manifest (the reference's split
+    // argument is unused); train augments (AugmentationConfig from data.augmentation, seed 42)
+    std::shared_ptr<SunRGBDLoader> train_loader, val_loader;
+    if (real) {
+        train_loader = std::make_shared<SunRGBDLoader>(c.data_dir, c.manifest_path, "train");
+        val_loader = std::make_shared<SunRGBDLoader>(c.data_dir, c.manifest_path, "test");
+        if (!c.sensor_types.empty()) {
+            train_loader->filterBySensorType(c.sensor_types);
+            val_loader->filterBySensorType(c.sensor_types);
+        }
+        AugmentationConfig ac;
+        ac.enable_random_crop = c.aug_crop;
+        ac.enable_horizontal_flip = c.aug_flip;
+        ac.horizontal_flip_prob = c.aug_flip_p;
+        ac.enable_color_jitter = c.aug_jitter;
+        ac.brightness_delta = c.aug_brightness;
+        ac.contrast_delta = c.aug_contrast;
+        train_loader->enableAugmentation(ac);
+    } else {   // disjoint generated splits
+        train_loader = SunRGBDLoader::synthetic(c.n_train, c.height, c.width, (uint32_t)c.seed);
+        if (c.n_val > 0) val_loader = SunRGBDLoader::synthetic(c.n_val, c.height, c.width, (uint32_t)c.seed + 1);
+    }
+    for (auto& L : {train_loader, val_loader})
+        if (L) L->setTargetDimensions(c.height, c.width);
+
+    cad::Workspace ws{c.batch_size, c.height, c.width, R.device};
+    std::shared_ptr<BaselineUNetImpl> model;
+    if (c.architecture == "intrinsics_unet")
+        model = std::make_shared<IntrinsicsConditionedUNetImpl>(3, c.init_features, 4, c.max_depth, ws);
+    else if (c.architecture == "ray_film_unet")
+        model = std::make_shared<RayConditionedUNetImpl>(3, c.init_features, 4, c.max_depth, ws);
+    else
+        model = std::make_shared<BaselineUNetImpl>(3, c.init_features, c.max_depth, ws);
+    auto loss_fn = std::make_shared<CombinedDepthLoss>(c.si, c.grad, c.smooth, c.reproj, ws);
+    std::shared_ptr<distributed::Communicator> comm;
+    if (R.dp) comm = std::make_shared<distributed::Communicator>(exchange_id(R, false), R.world, R.rank, R.device);
     if (lead)
-        std::cout << "Model: baseline_unet (f=" << c.init_features << "), parameters: " << model.count_parameters() << "\n"
-                  << "Using MI355X device " << R.device
+        std::cout << "Model: " << c.architecture << " (f=" << c.init_features << "), parameters: " << model->count_parameters()
+                  << "\nUsing MI355X device " << R.device
                   << (R.dp ? " (data-parallel rank 0 of " + std::to_string(R.world) + ", RCCL)" : std::string()) << "\n"
                   << "Training samples: " << c.n_train << (real ? " (" + c.manifest_path + ")" : std::string(" (synthetic)"))
-                  << ", validation samples: " << c.n_val << "\n";
+                  << ", validation samples: " << (real ? std::min(500, c.n_train) : c.n_val) << "\n";
+
+    TensorBoardTrainerEnhanced::Config tc;   // train_main.cpp:436-458
+    tc.num_epochs = c.num_epochs;
+    tc.batch_size = c.batch_size;
+    tc.learning_rate = c.learning_rate;
+    tc.weight_decay = c.weight_decay;
+    tc.use_grad_clip = c.use_grad_clip;
+    tc.grad_clip_value = c.grad_clip_value;
+    tc.val_interval = c.val_interval;
+    tc.log_interval = c.log_interval;
+    tc.save_interval = c.save_interval;
+    tc.checkpoint_dir = c.checkpoint_dir;
+    tc.log_dir = c.log_dir;
+    tc.experiment_name = c.experiment_name;
+    tc.device = R.device;
+    tc.tensorboard = args.tensorboard;
+    TensorBoardTrainerEnhanced trainer(model, model, loss_fn, tc, comm);
     if (!args.resume.empty()) {
-        if (ends_with(args.resume, ".pt")) {   // a torch::save model archive (ours or the reference's)
-            load(model, args.resume);
-            if (lead) std::cout << "Loaded model weights from " << args.resume << " (optimizer state starts fresh)\n";
-        } else {
-            load_checkpoint(args.resume, model, opt);
-            if (lead) std::cout << "Resumed from " << args.resume << " (optimizer step " << opt.step_count() << ")\n";
+        trainer.loadCheckpoint(args.resume);
+        if (lead) {
+            if (ends_with(args.resume, ".pt"))   // a torch::save model archive (ours or the reference's)
+                std::cout << "Loaded model weights from " << args.resume << " (optimizer state starts fresh)\n";
+            else
+                std::cout << "Resumed from " << args.resume << " (optimizer step " << trainer.optimizer().step_count() << ")\n";
         }
     }
-    if (comm) comm->broadcast_parameters(model, 0);   // identical replicas
-
-    std::ofstream train_log, metrics_csv, tb;
-    if (lead) {
-        train_log.open(c.log_dir + "/training.log", std::ios::app);
-        metrics_csv.open(c.log_dir + "/metrics.csv", std::ios::app);
-        if (metrics_csv.tellp() == 0)
-            metrics_csv << "epoch,step,train_loss,val_loss,abs_rel,sq_rel,rmse,rmse_log,a1,a2,a3,learning_rate,time_elapsed\n";
-        if (args.tensorboard) {
-            tb.open(c.log_dir + "/tensorboard_scalars.csv", std::ios::app);
-            if (tb.tellp() == 0) tb << "tag,step,value\n";
-        }
-    }
-
-    const int64_t HW = (int64_t)H * W;
-    HostBatch hb;
-    hb.rgb.resize((size_t)(B * 3 * HW));
-    hb.gt.resize((size_t)(B * HW));
-    hb.K.resize((size_t)B * 9);
-    DeviceTensor rgb = DeviceTensor::empty({B, 3, H, W}, R.device), gt = DeviceTensor::empty({B, 1, H, W}, R.device),
-                 K = DeviceTensor::empty({B, 3, 3}, R.device), pred = DeviceTensor::empty({B, 1, H, W}, R.device);
-    auto upload = [&](int64_t first, int n, int64_t split_offset) {
-        for (int i = 0; i < n; ++i)
-            make_sample(split_offset + first + i, H, W, hb.rgb.data() + i * 3 * HW, hb.gt.data() + i * HW, hb.K.data() + i * 9);
-        cad::check(cad_memcpy(rgb.data, hb.rgb.data(), 4 * n * 3 * HW, 0, nullptr), "h2d");
-        cad::check(cad_memcpy(gt.data, hb.gt.data(), 4 * n * HW, 0, nullptr), "h2d");
-        cad::check(cad_memcpy(K.data, hb.K.data(), 4 * n * 9, 0, nullptr), "h2d");
-        rgb.shape[0] = gt.shape[0] = K.shape[0] = pred.shape[0] = n;
-    };
-    std::unique_ptr<cad_loader, void (*)(cad_loader*)> train_L(nullptr, cad_loader_destroy), val_L(nullptr, cad_loader_destroy);
-    if (real) {
-        cad_aug_config ac{};
-        ac.enable_random_crop = c.aug_crop; ac.crop_scale_min = 0.7f; ac.crop_scale_max = 1.0f;
-        ac.enable_horizontal_flip = c.aug_flip; ac.horizontal_flip_prob = c.aug_flip_p;
-        ac.enable_color_jitter = c.aug_jitter; ac.brightness_delta = c.aug_brightness; ac.contrast_delta = c.aug_contrast;
-        const int threads = (int)std::max(2u, std::min(8u, std::thread::hardware_concurrency()));
-        cad_loader* L = nullptr;
-        cad::check(cad_loader_create(ds.get(), B, H, W, &ac, 42, threads, 2, R.device, &L), "train loader");
-        train_L.reset(L);
-        cad::check(cad_loader_create(ds.get(), B, H, W, nullptr, 42, threads, 2, R.device, &L), "val loader");
-        val_L.reset(L);
-    }
-    auto fetch = [&](cad_loader* L, int expect) {
-        const int n = cad_loader_next(L, rgb.data, gt.data, K.data, nullptr);
-        if (n < 0) throw std::runtime_error(std::string("data loader: ") + cad_last_error());
-        if (n != expect) throw std::runtime_error("data loader: batch of " + std::to_string(n) + ", expected " + std::to_string(expect));
-        rgb.shape[0] = gt.shape[0] = K.shape[0] = pred.shape[0] = n;
-    };
-    const auto t0 = std::chrono::steady_clock::now();
-    int64_t global_step = opt.step_count();
-    const int nb = steps_per_epoch(c.n_train, B, R.world);
-    if (nb < 1) throw std::runtime_error("fewer training samples than one global batch");
-    const int start_epoch = 1 + (int)(global_step / nb);
-    constexpr int64_t kBucketElems = 25 << 18;   // 25 MB gradient buckets
-    for (int epoch = start_epoch; epoch <= c.num_epochs; ++epoch) {
-        model.train();
-        double total = 0.0;
-        int64_t seen = 0;
-        if (real) {   // this rank's samples of the epoch, in step order
-            std::vector<int64_t> order;
-            for (int bi = 0; bi < nb; ++bi) {
-                const Shard sh = shard_of(bi, c.n_train, B, R);
-                for (int j = 0; j < sh.n; ++j) order.push_back(sh.first + j);
-            }
-            cad::check(cad_loader_start_epoch(train_L.get(), order.data(), (int64_t)order.size()), "start epoch");
-        }
-        for (int bi = 0; bi < nb; ++bi) {   // enhanced.h:266-329
-            const Shard sh = shard_of(bi, c.n_train, B, R);   // last partial batch (:269-270) on one rank
-            if (real) fetch(train_L.get(), sh.n);
-            else upload(sh.first, sh.n, 0);
-            opt.zero_grad();
-            model.forward_into(rgb, pred);
-            DeviceTensor l = loss_fn.forwardWithIntrinsics(pred, gt, rgb, K);
-            if (comm) comm->backward_allreduce(model, loss_fn.dpred(), kBucketElems);
-            else model.backward(loss_fn.dpred());
-            // clip_grad_norm_ on the mean gradient (the SUM all-reduce's 1/world folded in)
-            const double gnorm = c.use_grad_clip ? clip_grad_norm_(model, c.grad_clip_value, nullptr, 1.0 / R.world) : 0.0;
-            if (!c.use_grad_clip)
-                cad::check(cad_clip_grad_norm(model.handle(), INFINITY, 1.f / R.world, nullptr), "noclip");
-            opt.step();
-            if (comm) comm->allreduce(l.data, 5);   // the logged loss: mean over replicas
-            const float lv = l.to_host()[0] / R.world;   // loss.item<float>() (:307)
-            if (!std::isfinite(lv)) throw std::runtime_error("non-finite loss at step " + std::to_string(global_step));
-            total += (double)lv * sh.n * R.world;
-            seen += (int64_t)sh.n * R.world;
-            ++global_step;
-            if (lead && ((bi + 1) % c.log_interval == 0 || bi == nb - 1)) {
-                std::cout << "\r  [" << (100 * (bi + 1) / nb) << "%] Batch " << (bi + 1) << "/" << nb
-                          << " | Loss: " << lv << std::flush;
-                if (tb) tb << "batch_loss/train," << global_step << "," << lv << "\ntraining/gradient_norm,"
-                           << global_step << "," << gnorm << "\n";
-            }
-        }
-        if (!lead) continue;   // validation, logs and checkpoints: rank 0 (identical replicas)
-        std::cout << "\n";
-        const float train_loss = (float)(total / std::max<int64_t>(1, seen));
-        float val_loss = 0.f;
-        DepthMetrics vm{};
-        if (c.val_interval > 0 && epoch % c.val_interval == 0 && c.n_val > 0) {   // validateEpoch :339-395
-            model.eval();
-            double vl = 0.0;
-            int vn = 0;
-            if (real) cad::check(cad_loader_start_epoch(val_L.get(), nullptr, c.n_val), "validation");
-            for (int64_t s = 0; s < c.n_val; s += B) {
-                const int n = (int)std::min<int64_t>(B, c.n_val - s);
-                if (real) fetch(val_L.get(), n);
-                else upload(s, n, 1 << 20);
-                model.forward_into(rgb, pred);
-                DeviceTensor l = loss_fn.forwardWithIntrinsics(pred, gt, rgb, K);
-                // the reference evaluates sample by sample (batch 1); loss over a batch of n equals the
-                // per-sample mean only for n == 1, so report the batch loss weighted by n
-                vl += (double)l.to_host()[0] * n;
-                DepthMetrics m = computeDepthMetrics(pred, gt);
-                vm.abs_rel += m.abs_rel * n; vm.sq_rel += m.sq_rel * n; vm.rmse += m.rmse * n;
-                vm.rmse_log += m.rmse_log * n; vm.a1 += m.a1 * n; vm.a2 += m.a2 * n; vm.a3 += m.a3 * n;
-                vn += n;
-            }
-            val_loss = (float)(vl / vn);
-            for (float* p : {&vm.abs_rel, &vm.sq_rel, &vm.rmse, &vm.rmse_log, &vm.a1, &vm.a2, &vm.a3}) *p /= vn;
-        }
-        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        metrics_csv << epoch << "," << global_step << "," << train_loss << "," << val_loss << "," << vm.abs_rel << ","
-                    << vm.sq_rel << "," << vm.rmse << "," << vm.rmse_log << "," << vm.a1 << "," << vm.a2 << "," << vm.a3
-                    << "," << c.learning_rate << "," << el << "\n";
-        metrics_csv.flush();
-        train_log << "Epoch " << epoch << " train_loss " << train_loss << " val_loss " << val_loss << " abs_rel "
-                  << vm.abs_rel << "\n";
-        if (tb) tb << "loss/train," << epoch << "," << train_loss << "\nloss/val," << epoch << "," << val_loss
-                   << "\nmetrics/abs_rel," << epoch << "," << vm.abs_rel << "\n";
-        std::cout << "Epoch " << epoch << "/" << c.num_epochs << " | train " << train_loss << " | val " << val_loss
-                  << " | abs_rel " << vm.abs_rel << " | " << el << " s\n";
-        if (c.save_interval > 0 && epoch % c.save_interval == 0) {
-            // the reference's checkpoint, torch::save(model_, <dir>/<exp>_epoch_N.pt) (enhanced.h:656-662),
-            // plus the optimizer state it never saves (.cadckpt: full resume)
-            const std::string stem = c.checkpoint_dir + "/" + c.experiment_name + "_epoch_" + std::to_string(epoch);
-            save(model, stem + ".pt");
-            save_checkpoint(stem + ".cadckpt", model, opt);
-            std::cout << "Checkpoint saved: " << stem << ".pt\n";
-        }
-    }
-    if (lead) {
-        save(model, c.checkpoint_dir + "/final_model.pt");   // production_trainer.h:323-330
-        save_checkpoint(c.checkpoint_dir + "/final_model.cadckpt", model, opt);
-        std::cout << "Training complete.\n";
-    }
+    trainer.train(train_loader, val_loader);
+    if (lead) std::cout << "Training complete.\n";
     return 0;
 }
 

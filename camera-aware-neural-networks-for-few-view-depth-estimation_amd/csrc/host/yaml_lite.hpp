@@ -201,5 +201,12 @@ inline std::vector<float> Node::as<std::vector<float>>(const std::vector<float>&
     for (auto& n : list) v.push_back(n->as<float>(0.f));
     return v;
 }
+template <>
+inline std::vector<std::string> Node::as<std::vector<std::string>>(const std::vector<std::string>& def) const {
+    if (kind != List) return def;
+    std::vector<std::string> v;
+    for (auto& n : list) v.push_back(n->as<std::string>(""));
+    return v;
+}
 
 }  // namespace yaml_lite

@@ -104,7 +104,9 @@ def test_cli_train_resume(train_bin, tmp_path):
     assert r.returncode == 0, r.stderr
     assert "optimizer step 6" in r.stdout
     rows = (tmp_path / "logs" / "baseline_unet" / "metrics.csv").read_text().strip().splitlines()
-    assert rows[-1].startswith("3,9,")
+    # the step column is the reference's global_step_ at logEpochMetrics: steps before this epoch
+    # (enhanced.h:230-233)
+    assert rows[-1].startswith("3,6,")
 
 
 def _dp_cfg(tmp_path, **hw):
@@ -116,6 +118,52 @@ def _dp_cfg(tmp_path, **hw):
     p = tmp_path / "dp.yaml"
     p.write_text(yaml.safe_dump(cfg))
     return p
+
+
+def test_cli_model_architecture_key(train_bin, tmp_path):
+    """model.architecture selects the network (the reference parses it and always builds BaselineUNet);
+    an architecture this build does not train is refused before any GPU call."""
+    p = _dp_cfg(tmp_path, distributed=False)
+    cfg = yaml.safe_load(p.read_text())
+    cfg["model"]["architecture"] = "geometry_aware"
+    p.write_text(yaml.safe_dump(cfg))
+    r = subprocess.run([train_bin, "-c", str(p), "--dry-run"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and r.stderr.startswith("Error: model.architecture 'geometry_aware'")
+    for arch in ("baseline_unet", "intrinsics_unet", "ray_film_unet"):
+        cfg["model"]["architecture"] = arch
+        p.write_text(yaml.safe_dump(cfg))
+        r = subprocess.run([train_bin, "-c", str(p), "--dry-run"], capture_output=True, text=True, timeout=60)
+        assert r.returncode == 0, (arch, r.stderr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("arch", ["intrinsics_unet", "ray_film_unet"])
+def test_cli_trains_film_models(train_bin, tmp_path, arch):
+    """The config-3 networks through build/train (TensorBoardTrainerEnhanced: camera from each batch's
+    K, FiLM forward, per-sample validation) with their torch::save checkpoints."""
+    cfg = yaml.safe_load(open(os.path.join(ROOT, "configs", "train_config.yaml")))
+    cfg["data"].update(dataset_name="synthetic", num_train_samples=8, num_val_samples=3, input_height=48,
+                       input_width=64)
+    cfg["model"].update(architecture=arch, init_features=8)
+    cfg["training"].update(num_epochs=2, batch_size=4, val_interval=1)
+    cfg["checkpointing"].update(checkpoint_dir=str(tmp_path / "ckpt"), save_interval=1)
+    cfg["logging"]["log_dir"] = str(tmp_path / "logs")
+    p = tmp_path / "cfg.yaml"
+    p.write_text(yaml.safe_dump(cfg))
+    r = subprocess.run([train_bin, "-c", str(p)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert f"Model: {arch}" in r.stdout
+    rows = (tmp_path / "logs" / "baseline_unet" / "metrics.csv").read_text().strip().splitlines()
+    assert [row.split(",")[:2] for row in rows[1:]] == [["1", "0"], ["2", "2"]]
+    vals = [float(x) for x in rows[-1].split(",")[2:5]]
+    assert all(v == v and v > 0 for v in vals)
+    import torch
+    sd = torch.jit.load(str(tmp_path / "ckpt" / "baseline_unet" / "baseline_unet_epoch_2.pt")).state_dict()
+    assert "enc1.film.fc1.weight" in sd and int(sd["enc1.film.bn1.num_batches_tracked"]) == 4
+    if arch == "ray_film_unet":
+        assert tuple(sd["enc1.conv1.weight"].shape) == (8, 6, 3, 3)   # rgb + rays
+    tb = (tmp_path / "logs" / "baseline_unet" / "tensorboard_scalars.csv").read_text()
+    assert "loss_components/reproj_loss,2," in tb and "metrics/abs_rel,2," in tb
 
 
 def test_cli_data_parallel_plan(train_bin, tmp_path, cad):
@@ -240,6 +288,6 @@ def test_cli_trains_from_manifest(train_bin, tmp_path):
     assert r.returncode == 0, r.stderr
     assert "Training samples: 6 (./manifest.json)" in r.stdout
     rows = (tmp_path / "logs" / "baseline_unet" / "metrics.csv").read_text().strip().splitlines()
-    assert len(rows) == 3 and rows[-1].startswith("2,4,")   # 2 steps per epoch (4 + 2 samples)
+    assert len(rows) == 3 and rows[-1].startswith("2,2,")   # 2 steps per epoch (4 + 2 samples)
     vals = [float(x) for x in rows[-1].split(",")[2:5]]
     assert all(v == v and v > 0 for v in vals)   # finite train loss, val loss, abs_rel
