@@ -213,6 +213,62 @@ def extra_leg(cad, lib, dev, config, steps=5, warmup=2, B=32, H=480, W=640, f=64
     return out
 
 
+def resunet_macs_per_image(H=480, W=640):
+    """Forward multiply-accumulates of one image through the config-5 network (resunet.cpp layout),
+    and how many of them have a dgrad (all but the stem conv, whose input is the image)."""
+    macs = 0
+    h, w = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    stem = h * w * 64 * 3 * 49
+    h, w = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    cin = 64
+    for L, (wd, n) in enumerate(zip((64, 128, 256, 512), (3, 4, 6, 3))):
+        for i in range(n):
+            s = 2 if (L > 0 and i == 0) else 1
+            ho, wo = (h - 1) // s + 1, (w - 1) // s + 1
+            macs += h * w * cin * wd + ho * wo * (wd * 9 * wd + wd * 4 * wd)
+            if i == 0:
+                macs += ho * wo * cin * 4 * wd
+            cin, h, w = 4 * wd, ho, wo
+    for l, cu, C, sk in ((4, 2048, 512, 1024), (3, 512, 256, 512), (2, 256, 128, 256), (1, 128, 64, 64), (0, 64, 32, 0)):
+        hh, ww = H >> l, W >> l
+        macs += (hh // 2) * (ww // 2) * cu * 4 * C + hh * ww * (sk + C) * 9 * C + hh * ww * C * 9 * C
+    macs += H * W * 32
+    return stem + macs, macs
+
+
+def extra_leg_resunet(cad, dev, steps=5, warmup=2, B=32, H=480, W=640):
+    """configs[4]'s per-GPU step: ResNet-50 encoder + U-Net decoder (resunet.cpp), bs32 480x640, full
+    loss, bf16 contraction operands (the fp8 conv-GEMM the config names is not built: DESIGN.md §9)."""
+    import torch
+    from cad_amd import synthetic
+    model = cad.ResNetUNet(batch=B, height=H, width=W, device=dev.index)
+    loss = cad.CombinedDepthLoss(1.0, 0.1, 0.001, 0.01, batch=B, height=H, width=W, device=dev.index)
+    rgb, gt, K = (t.to(dev) for t in synthetic.device_batch(B, H, W, "cpu"))
+    pred = torch.empty((B, 1, H, W), device=dev)
+    dpred, loss5 = torch.empty_like(pred), torch.zeros(5, device=dev)
+    for _ in range(warmup):
+        model.train_step(loss, rgb, gt, K, pred=pred, dpred=dpred, loss5=loss5)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        model.train_step(loss, rgb, gt, K, pred=pred, dpred=dpred, loss5=loss5)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    last = loss5[0].item()
+    params = model.count_parameters()
+    del model, loss
+    torch.cuda.empty_cache()
+    value = B * steps / dt
+    fwd, with_dgrad = resunet_macs_per_image(H, W)
+    flop_img = 2 * (2 * fwd + with_dgrad)   # forward + wgrad of every conv, dgrad of all but the stem
+    return {"workload": "ResNet-50 encoder + U-Net decoder train step, configs[4] per-GPU: bs32 480x640, "
+                        "bf16 GEMM operands (fp8 not built), full loss",
+            "value": round(value, 3), "unit": "images/s", "ms_per_step": round(1e3 * dt / steps, 3), "steps": steps,
+            "warmup": warmup, "dtype": "bf16", "params": params, "last_loss": last,
+            "gflop_per_image": round(flop_img / 1e9, 2),
+            "mfma_frac_dense_bf16": round(flop_img * value / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4)}
+
+
 def pmc_traffic(kernel_name):
     """HBM bytes per launch of `kernel_name` from the committed rocprofv3 PMC summary, if any."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -374,6 +430,11 @@ def main():
                     log(f"extra leg config {cfg}: {extra[f'config{cfg}']}")
                 except Exception as e:
                     log(f"extra leg config {cfg} failed: {e}")
+            try:
+                extra["config5"] = extra_leg_resunet(cad, dev)
+                log(f"extra leg config 5: {extra['config5']}")
+            except Exception as e:
+                log(f"extra leg config 5 failed: {e}")
             try:
                 dp = data_path(cad, dev, B, H, W)
             except Exception as e:

@@ -27,6 +27,10 @@ class UnetDesc(C.Structure):
                 ("height", I), ("width", I)]
 
 
+class ResUnetDesc(C.Structure):
+    _fields_ = [("in_channels", I), ("max_batch", I), ("height", I), ("width", I), ("max_depth", F)]
+
+
 class AdamOpts(C.Structure):
     _fields_ = [("lr", F), ("beta1", F), ("beta2", F), ("eps", F), ("weight_decay", F)]
 
@@ -52,6 +56,21 @@ SIGNATURES = {
     "cad_set_gemm_engine": (I, [I]),
     "cad_get_gemm_engine": (I, []),
     "cad_unet_create": (I, [C.POINTER(UnetDesc), I, C.POINTER(P)]),
+    "cad_resunet_create": (I, [C.POINTER(ResUnetDesc), I, C.POINTER(P)]),
+    "cad_resunet_destroy": (None, [P]),
+    "cad_resunet_count_parameters": (I64, [P]),
+    "cad_resunet_num_tensors": (I, [P, I]),
+    "cad_resunet_tensor_info": (I, [P, I, I, C.POINTER(C.c_char_p), C.POINTER(I), I64P]),
+    "cad_resunet_set_tensor": (I, [P, I, I, FP, I64]),
+    "cad_resunet_get_tensor": (I, [P, I, I, FP, I64]),
+    "cad_resunet_get_grad": (I, [P, I, FP, I64]),
+    "cad_resunet_train": (I, [P, I]),
+    "cad_resunet_flat": (I, [P, C.POINTER(P), C.POINTER(P), I64P]),
+    "cad_resunet_forward": (I, [P, P, P, I, P]),
+    "cad_resunet_backward": (I, [P, P, P]),
+    "cad_resunet_clip_grad_norm": (I, [P, F, F, P]),
+    "cad_resunet_last_grad_norm": (I, [P, FP, P]),
+    "cad_resunet_adam_step": (I, [P, F, F, F, F, F, P]),
     "cad_unet_create_model": (I, [C.POINTER(UnetDesc), I, I, C.POINTER(P)]),
     "cad_unet_model": (I, [P]),
     "cad_unet_forward_cam": (I, [P, P, P, P, I, P]),

@@ -249,6 +249,28 @@ __device__ __forceinline__ void convT_wgrad_psb(const GemmArgs& a) {
         [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.b_cin, a.B, a.H, a.W, r0, t, kb); },
         EpiSlab{});
 }
+// dense GEMMs on twins (config-5 network: 1x1 and im2col convolutions): C[m][n] = sum_k A[m][k] B[n][k]
+template <int NP, int WM, int WN, int MI, int NJ, int KB, class Epi>
+__device__ __forceinline__ void dense_nt_psb(const GemmArgs& a) {
+    using LA = PsKcDense<32 * MI * WM, KB, NP>;
+    using LB = PsKcDense<32 * NJ * WN, KB, NP>;
+    gemm_body_ps<NP, WM, WN, MI, NJ, KB, LA, LB>(
+        a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t, kb); },
+        [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, Epi{});
+}
+// ... and their weight gradients: C[m][n] = sum_k A[k][m] B[k][n] (k = pixel)
+template <int NP, int WM, int WN, int MI, int NJ, int KB>
+__device__ __forceinline__ void dense_tn_psb(const GemmArgs& a) {
+    using LA = PsMNcDense<32 * MI * WM, KB, NP>;
+    using LB = PsMNcDense<32 * NJ * WN, KB, NP>;
+    gemm_body_psm<NP, WM, WN, MI, NJ, KB, LA, LB>(
+        a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t, kb); },
+        [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, EpiSlab{});
+}
+template <int WM, int WN, int KB, class Epi>
+__global__ __launch_bounds__(256) void k_dense_bf16p(GemmArgs a) { dense_nt_psb<1, WM, WN, 2, 2, KB, Epi>(a); }
+template <int WM, int WN, int KB>
+__global__ __launch_bounds__(256) void k_dense_wgrad_bf16p(GemmArgs a) { dense_tn_psb<1, WM, WN, 2, 2, KB>(a); }
 template <int WM, int WN, int KB, class Epi>
 __global__ __launch_bounds__(256) void k_conv3x3_fwd_bf16p(GemmArgs a) { conv3x3_fwd_psb<1, WM, WN, 2, 2, KB, Epi>(a); }
 template <int WM, int WN, int KB>
@@ -388,6 +410,10 @@ CAD_KT(KConvTWgrad, (k_convT_wgrad<WM, WN, KB>), "void cad::k_convT_wgrad<%d, %d
            "void cad::k_conv3x3_wgrad_" #SUF "<%d, %d, %d>(cad::GemmArgs)")                                \
     CAD_KT(KConvTWgrad##T, (k_convT_wgrad_##SUF<WM, WN, KB>),                                              \
            "void cad::k_convT_wgrad_" #SUF "<%d, %d, %d>(cad::GemmArgs)")
+CAD_KT(KDenseP1, (k_dense_bf16p<WM, WN, KB, EpiStore>), "void cad::k_dense_bf16p<%d, %d, %d, cad::EpiStore>(cad::GemmArgs)")
+CAD_KT(KDenseSP1, (k_dense_bf16p<WM, WN, KB, EpiStoreStats>),
+       "void cad::k_dense_bf16p<%d, %d, %d, cad::EpiStoreStats>(cad::GemmArgs)")
+CAD_KT(KDenseWgradP1, (k_dense_wgrad_bf16p<WM, WN, KB>), "void cad::k_dense_wgrad_bf16p<%d, %d, %d>(cad::GemmArgs)")
 // in-loader split engines: KConvFwd3 ... (S3), KConvFwdB ... (B1); pre-split B1: KConvFwdP1 ...
 CAD_NP_KT(s3, 3)
 CAD_NP_KT(bf16, B)
@@ -764,6 +790,50 @@ void conv3x3_wgrad_ps(Split dz, int cout, Split x, int cin, float* dw, int B, in
     a.ldc = a.N; a.slab_stride = per;
     a.C = s == 1 ? dw : slab;
     launch_kb<KConvWgradP1, 32>(c, kb, a, s, st);
+    if (s > 1) finish_slabs(slab, s, per, dw, st);
+}
+
+int dense_stats_rows(int64_t M, int N) { return cdiv(M, tile_m(pick_cfg((int)M, N))); }
+
+void dense_fwd_ps(Split x, int K, Split w, int N, float* y, int64_t ldy, int ycoff, int64_t M, float* stats,
+                  hipStream_t st) {
+    ps_check(x, K, "dense x");
+    ps_check(w, K, "dense w");
+    if (M > INT32_MAX) throw std::runtime_error("dense GEMM: too many rows");
+    GemmArgs a{};
+    a.M = (int)M; a.N = N; a.K = K;
+    a.B = 1; a.H = 1; a.W = (int)M;
+    a.A = (const float*)x.p; a.lda = x.ld; a.a_coff = x.coff;
+    a.Bm = (const float*)w.p; a.ldb = w.ld; a.b_coff = w.coff;
+    a.C = y; a.ldc = ldy; a.c_coff = ycoff;
+    a.stats = stats;
+    const Cfg c = pick_cfg(a.M, a.N);
+    const int kb = ps_kb(true, c);
+    a.kstages_per_split = cdiv(a.K, kb);
+    if (stats) launch_kb<KDenseSP1, 32, 64>(c, kb, a, 1, st);
+    else launch_kb<KDenseP1, 32, 64>(c, kb, a, 1, st);
+}
+
+void dense_wgrad_ps(Split dz, int N, Split x, int K, float* dw, int64_t ldw, int64_t M, float* slab, int64_t slab_cap,
+                    hipStream_t st) {
+    ps_check(dz, N, "dense wgrad dz");
+    ps_check(x, K, "dense wgrad x");
+    if (ldw != K) throw std::runtime_error("dense wgrad: dw rows must be dense");
+    if (M > INT32_MAX) throw std::runtime_error("dense GEMM: too many rows");
+    GemmArgs a{};
+    a.M = N; a.N = K; a.K = (int)M;
+    a.B = 1; a.H = 1; a.W = (int)M;
+    a.A = (const float*)dz.p; a.lda = dz.ld; a.a_coff = dz.coff;
+    a.Bm = (const float*)x.p; a.ldb = x.ld; a.b_coff = x.coff;
+    const Cfg c = pick_cfg(a.M, a.N);
+    const int kb = ps_kb(false, c);
+    int s = plan_splits(a, c, kb, slab_cap, 2 * kMaxPlanes * std::max<int64_t>(dz.ld, x.ld));
+    a.kstages_per_split = cdiv(cdiv(a.K, kb), s);
+    s = cdiv(cdiv(a.K, kb), a.kstages_per_split);
+    const int64_t per = (int64_t)a.M * a.N;
+    a.ldc = a.N; a.slab_stride = per;
+    a.C = s == 1 ? dw : slab;
+    launch_kb<KDenseWgradP1, 32>(c, kb, a, s, st);
     if (s > 1) finish_slabs(slab, s, per, dw, st);
 }
 

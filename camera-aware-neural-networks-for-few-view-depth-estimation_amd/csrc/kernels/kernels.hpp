@@ -64,6 +64,39 @@ void convT_dgrad_ps(Split g, int cout, Split wm, int cin, float* dx, int B, int 
 void convT_wgrad_ps(Split x, int cin, Split g, int cout, float* dw, int B, int H, int W, float* slab,
                     int64_t slab_cap, hipStream_t st);
 
+// ---- dense GEMMs on the pre-split twins (the 1x1 / im2col convolutions of the config-5 network) ----
+// y[m][ycoff + n] = sum_k x[m][k] w[n][k]  (+ BN partials [rows][2][N] when stats != nullptr)
+void dense_fwd_ps(Split x, int K, Split w, int N, float* y, int64_t ldy, int ycoff, int64_t M, float* stats,
+                  hipStream_t st);
+int dense_stats_rows(int64_t M, int N);
+// dw[n][k] = sum_m dz[m][n] x[m][k]  (reduction over the M pixels; split-K slabs)
+void dense_wgrad_ps(Split dz, int N, Split x, int K, float* dw, int64_t ldw, int64_t M, float* slab, int64_t slab_cap,
+                    hipStream_t st);
+
+// ---------------- config-5 network kernels (res_kernels.hip) ----------------
+// col[pix_out][k] bf16, k = (ky*KW + kx)*C + c, rows padded with zeros to Kp (% 8)
+void im2col_f32(const float* x, int64_t ldx, int xcoff, int C, int B, int H, int W, int KH, int KW, int S, int P,
+                void* col, int Kp, hipStream_t st);
+void im2col_ps(Split x, int C, int B, int H, int W, int KH, int KW, int S, int P, void* col, int Kp, hipStream_t st);
+// dx[pix_in][c] (overwritten, ld lddx) = sum of dcol[pix_out][tap*C + c] over the taps reading pix_in
+void col2im(const float* dcol, int Kc, int C, int B, int H, int W, int KH, int KW, int S, int P, float* dx,
+            int64_t lddx, hipStream_t st);
+void maxpool3s2_fwd(const float* x, int C, int B, int H, int W, float* out, uint8_t* idx, void* out_split,
+                    hipStream_t st);
+void maxpool3s2_bwd(const float* dout, const uint8_t* idx, int C, int B, int H, int W, float* dx, hipStream_t st);
+// out = relu(y*scale + shift + (yd ? yd*dscale + dshift : x)), fp32 [M][C] + twin
+void bn_add_relu(const float* y, const float* scale, const float* shift, const float* yd, const float* dscale,
+                 const float* dshift, const float* x, int64_t ldx, int C, int64_t M, float* out, void* out_split,
+                 hipStream_t st);
+void relu_mask(const float* g, int64_t ldg, int gcoff, const float* out, int C, int64_t M, float* gs, hipStream_t st);
+// dst[(b, S*oy, S*ox)][c] += src[(b, oy, ox)][scoff + c] over the strided grid of a B x H x W image
+void add_strided(float* dst, int64_t lddst, const float* src, int64_t ldsrc, int scoff, int C, int B, int H, int W,
+                 int S, hipStream_t st);
+// twin rows dst[(b,oy,ox)][dcoff + c] = src[(b, S*oy, S*ox)][c]
+void copy_twin(Split src, int C, int B, int H, int W, int S, void* dst, int64_t ldd, int dcoff, hipStream_t st);
+// wt[k][n] = bf16(w[n][k])
+void transpose_split(const float* w, int64_t ldw, int N, int K, void* wt, hipStream_t st);
+
 // ---------------- NN elementwise / reductions (nn_kernels.hip) ----------------
 // column partial sums: part[s][c] (double) over row slices; returns number of slices
 int colsum_slices(int64_t R);
@@ -84,11 +117,13 @@ void bn_relu_fwd(const float* y, int C, const float* scale, const float* shift, 
 // BN+ReLU backward: dy = k1*dz - k2 - k3*xhat, dz = g*[y*scale+shift > 0];
 // writes dgamma/dbeta (grad buffer) and dy (dense [M][C]).  gmul != nullptr: g is first multiplied
 // by gmul[sample][c] (sample = row / HW) — the FiLM gamma sitting between this ReLU and the consumer.
-// dy_split != nullptr: also the pre-split twin of dy (dense, ld C)
+// dy_split != nullptr: also the pre-split twin of dy (dense, ld C).  relu = false: plain BN backward
+// (dz = g; the bottleneck's last BN, whose ReLU sits after the residual add)
 void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, const float* mean,
                  const float* invstd, const float* scale, const float* shift, const float* gamma,
                  int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
-                 hipStream_t st, const float* gmul = nullptr, int64_t HW = 1, void* dy_split = nullptr);
+                 hipStream_t st, const float* gmul = nullptr, int64_t HW = 1, void* dy_split = nullptr,
+                 bool relu = true);
 // out_split != nullptr: also the pooled output's split twin (dense, ld C); out may then be nullptr
 void maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float* out, uint8_t* idx,
                  hipStream_t st, void* out_split = nullptr);

@@ -89,7 +89,7 @@ struct OpSum {
 };
 struct OpBnBwd {
     const float *g, *y, *mean, *invstd, *scale, *shift, *gmul;
-    int64_t ldg; int gcoff, C; int64_t HW;
+    int64_t ldg; int gcoff, C; int64_t HW; bool relu;
     __device__ void operator()(int64_t r, int c4, double (&acc)[2][4]) const {
         float4 gv = *reinterpret_cast<const float4*>(g + r * ldg + gcoff + c4 * 4);
         if (gmul) {
@@ -102,7 +102,7 @@ struct OpBnBwd {
         for (int e = 0; e < 4; ++e) {
             const int c = c4 * 4 + e;
             const float z = ya[e] * scale[c] + shift[c];
-            const float dz = z > 0.f ? ga[e] : 0.f;
+            const float dz = (!relu || z > 0.f) ? ga[e] : 0.f;
             const float xh = (ya[e] - mean[c]) * invstd[c];
             acc[0][e] += dz;
             acc[1][e] += (double)dz * xh;
@@ -263,7 +263,7 @@ __global__ void k_bn_relu_bwd(const float* __restrict__ g, int64_t ldg, int gcof
                               int C, const float* __restrict__ mean, const float* __restrict__ invstd,
                               const float* __restrict__ scale, const float* __restrict__ shift,
                               const float* __restrict__ coef, float* __restrict__ dy, int64_t n4,
-                              const float* __restrict__ gmul, int64_t HW, char* __restrict__ os) {
+                              const float* __restrict__ gmul, int64_t HW, char* __restrict__ os, bool relu) {
     const int C4 = C >> 2;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = i / C4;
@@ -280,7 +280,7 @@ __global__ void k_bn_relu_bwd(const float* __restrict__ g, int64_t ldg, int gcof
         for (int e = 0; e < 4; ++e) {
             const int c = c0 + e;
             const float z = ya[e] * scale[c] + shift[c];
-            const float dz = z > 0.f ? ga[e] : 0.f;
+            const float dz = (!relu || z > 0.f) ? ga[e] : 0.f;
             const float xh = (ya[e] - mean[c]) * invstd[c];
             o[e] = coef[c] * dz - coef[C + c] - coef[2 * C + c] * xh;
         }
@@ -292,10 +292,10 @@ __global__ void k_bn_relu_bwd(const float* __restrict__ g, int64_t ldg, int gcof
 void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, const float* mean,
                  const float* invstd, const float* scale, const float* shift, const float* gamma,
                  int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
-                 hipStream_t st, const float* gmul, int64_t HW, void* dy_split) {
+                 hipStream_t st, const float* gmul, int64_t HW, void* dy_split, bool relu) {
     double* tot = scratch;
     double* part = scratch + 2 * C;
-    OpBnBwd op{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW};
+    OpBnBwd op{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW, relu};
     const int S = launch_colreduce<2>(op, M, C, part, st);
     launch_colfinal(part, S, 2 * C, tot, nullptr, 1.f, st);
     hipLaunchKernelGGL(k_bn_bwd_coef, dim3(cdiv(C, 64)), dim3(64), 0, st, tot, C, M, gamma, invstd, coef, dgamma, dbeta);
@@ -304,10 +304,10 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
     char* os = static_cast<char*>(dy_split);
     if (np == 1)
         hipLaunchKernelGGL(k_bn_relu_bwd<1>, dim3(ew_blocks(n4)), dim3(256), 0, st, g, ldg, gcoff, y, C, mean, invstd,
-                           scale, shift, coef, dy, n4, gmul, HW, os);
+                           scale, shift, coef, dy, n4, gmul, HW, os, relu);
     else
         hipLaunchKernelGGL(k_bn_relu_bwd<0>, dim3(ew_blocks(n4)), dim3(256), 0, st, g, ldg, gcoff, y, C, mean, invstd,
-                           scale, shift, coef, dy, n4, gmul, HW, os);
+                           scale, shift, coef, dy, n4, gmul, HW, os, relu);
 }
 
 // ------------------------------------------------------------------------------------------

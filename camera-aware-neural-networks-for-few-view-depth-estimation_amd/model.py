@@ -519,3 +519,145 @@ class Trainer:
             clip_grad_norm_(m, self.grad_clip)
         self.optimizer.step()
         return self.loss5
+
+
+class ResNetUNet:
+    """Config-5 network (BASELINE configs[4]): ResNet-50 encoder + U-Net decoder on MI355X, bf16
+    operands (cad_resunet_*; resunet.cpp).  No reference model exists — parity is unpinned and the
+    network is checked against the torch fp32 restatement in oracle/resunet_oracle.py.
+
+    Parameter names follow torchvision's ResNet-50 under "encoder." and the U-Net decoder
+    ("dec4".."dec0", "out_conv").  train_step() = forward, CombinedDepthLoss, backward,
+    clip_grad_norm_, Adam (moments owned by the model)."""
+
+    def __init__(self, in_channels=3, max_depth=10.0, *, batch, height, width, device=0):
+        self.lib = _abi.load()
+        self.device = torch.device("cuda", device)
+        self.batch, self.height, self.width, self.max_depth = batch, height, width, max_depth
+        desc = _abi.ResUnetDesc(in_channels, batch, height, width, max_depth)
+        h = C.c_void_p()
+        check(self.lib.cad_resunet_create(C.byref(desc), device, C.byref(h)), "cad_resunet_create")
+        self.h = h
+        self._param_info = [self._info(0, i) for i in range(self.lib.cad_resunet_num_tensors(h, 0))]
+        self._buffer_info = [self._info(1, i) for i in range(self.lib.cad_resunet_num_tensors(h, 1))]
+        p, g, n = C.c_void_p(), C.c_void_p(), C.c_int64()
+        check(self.lib.cad_resunet_flat(h, C.byref(p), C.byref(g), C.byref(n)), "cad_resunet_flat")
+        self.n_flat = n.value
+        self._flat_g = g.value
+        self.training = True
+
+    def _info(self, kind, idx):
+        name, nd, shape = C.c_char_p(), C.c_int(), (C.c_int64 * 4)()
+        check(self.lib.cad_resunet_tensor_info(self.h, kind, idx, C.byref(name), C.byref(nd), shape), "tensor_info")
+        return name.value.decode(), tuple(shape[i] for i in range(nd.value))
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            self.lib.cad_resunet_destroy(h)
+            self.h = None
+
+    def train(self, mode=True):
+        self.training = bool(mode)
+        check(self.lib.cad_resunet_train(self.h, int(mode)), "cad_resunet_train")
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+    def count_parameters(self) -> int:
+        return int(self.lib.cad_resunet_count_parameters(self.h))
+
+    def _get(self, kind, idx, shape):
+        out = np.empty(int(np.prod(shape)) if shape else 1, np.float32)
+        check(self.lib.cad_resunet_get_tensor(self.h, kind, idx, out.ctypes.data_as(_abi.FP), out.size), "get_tensor")
+        return torch.from_numpy(out.reshape(shape))
+
+    def named_parameters(self):
+        torch.cuda.synchronize(self.device)
+        return OrderedDict((n, self._get(0, i, s)) for i, (n, s) in enumerate(self._param_info))
+
+    def named_buffers(self):
+        torch.cuda.synchronize(self.device)
+        return OrderedDict((n, self._get(1, i, s)) for i, (n, s) in enumerate(self._buffer_info))
+
+    def state_dict(self):
+        d = self.named_parameters()
+        d.update(self.named_buffers())
+        return d
+
+    def load_state_dict(self, state, strict=True):
+        torch.cuda.synchronize(self.device)
+        names = {n: (0, i, s) for i, (n, s) in enumerate(self._param_info)}
+        names.update({n: (1, i, s) for i, (n, s) in enumerate(self._buffer_info)})
+        missing = [n for n in names if n not in state]
+        if strict and missing:
+            raise KeyError(f"missing keys: {missing[:5]}")
+        for n, (kind, i, s) in names.items():
+            if n not in state:
+                continue
+            v = np.ascontiguousarray(torch.as_tensor(state[n]).detach().cpu().float().numpy())
+            assert tuple(v.shape) == tuple(s), f"{n}: shape {v.shape} != {s}"
+            check(self.lib.cad_resunet_set_tensor(self.h, kind, i, v.ctypes.data_as(_abi.FP), v.size), f"set {n}")
+
+    def grads(self):
+        torch.cuda.synchronize(self.device)
+        out = OrderedDict()
+        for i, (n, s) in enumerate(self._param_info):
+            g = np.empty(int(np.prod(s)), np.float32)
+            check(self.lib.cad_resunet_get_grad(self.h, i, g.ctypes.data_as(_abi.FP), g.size), "get_grad")
+            out[n] = torch.from_numpy(g.reshape(s))
+        return out
+
+    def flat_grads_ptr(self) -> int:
+        """Device address of the flat gradient slab (n_flat floats): the data-parallel all-reduce buffer."""
+        return self._flat_g
+
+    def forward(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        B, Cc, H, W = x.shape
+        assert Cc == 3 and H == self.height and W == self.width and B <= self.batch, "input shape mismatch"
+        if out is None:
+            out = torch.empty((B, 1, H, W), dtype=torch.float32, device=self.device)
+        check(self.lib.cad_resunet_forward(self.h, _ptr(x), _ptr(out), B, _stream(self.device)), "cad_resunet_forward")
+        return out
+
+    __call__ = forward
+
+    def backward(self, ddepth: torch.Tensor):
+        check(self.lib.cad_resunet_backward(self.h, _ptr(ddepth), _stream(self.device)), "cad_resunet_backward")
+
+    def clip_grad_norm_(self, max_norm: float, prescale: float = 1.0):
+        check(self.lib.cad_resunet_clip_grad_norm(self.h, float(max_norm), float(prescale), _stream(self.device)), "clip")
+
+    def last_grad_norm(self) -> float:
+        v = C.c_float()
+        check(self.lib.cad_resunet_last_grad_norm(self.h, C.byref(v), _stream(self.device)), "last_grad_norm")
+        return float(v.value)
+
+    def adam_step(self, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5):
+        check(self.lib.cad_resunet_adam_step(self.h, lr, betas[0], betas[1], eps, weight_decay, _stream(self.device)),
+              "adam_step")
+
+    def train_step(self, loss_fn: "CombinedDepthLoss", rgb, gt, K, lr=1e-4, weight_decay=1e-5, grad_clip=1.0,
+                   pred=None, dpred=None, loss5=None, process_group=None):
+        """One optimisation step (enhanced.h:287-304 sequence).  With process_group: the flat gradient
+        slab is SUM-all-reduced (RCCL) after the backward and clipped as the mean."""
+        pred = self.forward(rgb, out=pred)
+        loss5, dpred = loss_fn.forward_with_intrinsics(pred, gt, rgb, K, loss5=loss5, dpred=dpred)
+        self.backward(dpred)
+        world = 1
+        if process_group is not None:
+            import torch.distributed as dist
+            world = dist.get_world_size(process_group)
+            g = _flat_view(self._flat_g, self.n_flat, self.device)
+            dist.all_reduce(g, group=process_group)
+        self.clip_grad_norm_(grad_clip if grad_clip else float("inf"), 1.0 / world)
+        self.adam_step(lr=lr, weight_decay=weight_decay)
+        return loss5, pred
+
+
+def _flat_view(addr: int, n: int, device) -> torch.Tensor:
+    """A torch view of a libcad-owned device slab (for torch.distributed collectives)."""
+    class _A:
+        __cuda_array_interface__ = {"shape": (n,), "typestr": "<f4", "data": (addr, False), "version": 3}
+    return torch.as_tensor(_A(), device=device)

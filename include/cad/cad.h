@@ -403,6 +403,36 @@ cad_status cad_op_convT_wgrad(const float* x, int cin, const float* g, int64_t l
 cad_status cad_op_maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float* out,
                               uint8_t* idx, void* stream);
 
+/* ---- config-5 network (BASELINE configs[4]): ResNet-50 encoder + U-Net decoder, bf16 operands ----
+ * No reference counterpart: architecture in resunet.cpp / DESIGN.md §9;
+ * torchvision ResNet-50 parameter names under "encoder.", decoder "dec4".."dec0", "out_conv".
+ * Same life cycle as cad_unet: forward (train: BN batch statistics), backward (dL/ddepth), clip,
+ * Adam (moments owned by the model). height / width multiples of 32. */
+typedef struct cad_resunet cad_resunet;
+typedef struct {
+    int in_channels;   /* 3 */
+    int max_batch;
+    int height, width;
+    float max_depth;
+} cad_resunet_desc;
+cad_status cad_resunet_create(const cad_resunet_desc* d, int device, cad_resunet** out);
+void cad_resunet_destroy(cad_resunet* h);
+int64_t cad_resunet_count_parameters(const cad_resunet* h);
+int cad_resunet_num_tensors(const cad_resunet* h, int kind);   /* 0 parameters, 1 buffers */
+cad_status cad_resunet_tensor_info(const cad_resunet* h, int kind, int idx, const char** name, int* ndim,
+                                   int64_t shape[4]);
+cad_status cad_resunet_set_tensor(cad_resunet* h, int kind, int idx, const float* host, int64_t numel);
+cad_status cad_resunet_get_tensor(const cad_resunet* h, int kind, int idx, float* host, int64_t numel);
+cad_status cad_resunet_get_grad(const cad_resunet* h, int idx, float* host, int64_t numel);
+cad_status cad_resunet_train(cad_resunet* h, int train);
+cad_status cad_resunet_flat(cad_resunet* h, float** params, float** grads, int64_t* n);
+cad_status cad_resunet_forward(cad_resunet* h, const float* rgb, float* depth, int B, void* stream);
+cad_status cad_resunet_backward(cad_resunet* h, const float* ddepth, void* stream);
+cad_status cad_resunet_clip_grad_norm(cad_resunet* h, float max_norm, float prescale, void* stream);
+cad_status cad_resunet_last_grad_norm(cad_resunet* h, float* total_norm, void* stream);
+cad_status cad_resunet_adam_step(cad_resunet* h, float lr, float beta1, float beta2, float eps, float weight_decay,
+                                 void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,157 @@
+"""Test infrastructure only (tests/, bench.py's cpu_baseline leg): a torch CPU restatement of the
+config-5 network — ResNet-50 encoder + U-Net decoder (resunet.cpp) — that the HIP path
+is checked against.
+
+PARITY UNPINNED: the reference repository has no such model (BASELINE.json configs[4] names it,
+SURVEY.md §8(f) rank 4), so there is nothing of the reference to pin this restatement to.  What it
+pins instead: the module semantics are torch's own (F.conv2d, F.batch_norm, F.max_pool2d,
+F.conv_transpose2d — the same functions torchvision's ResNet-50 and the reference's U-Net decoder
+blocks are made of, baseline_unet.h:83-102), parameter names and shapes are torchvision's, and the
+loss / clip / Adam are the U-Net oracle's (cad_oracle.py, pinned to the reference's fixtures).
+
+operands="bf16" rounds every contraction operand to bf16 (forward x and w, dgrad dy, wgrad dy) as the
+GPU path does (cad_oracle._GEMM); "exact" is plain fp32 (or fp64 with dtype=float64).
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+
+import torch
+import torch.nn.functional as F
+
+from . import cad_oracle as O
+
+WIDTHS, NBLOCKS = (64, 128, 256, 512), (3, 4, 6, 3)
+DEC = [(4, 2048, 512, 1024), (3, 512, 256, 512), (2, 256, 128, 256), (1, 128, 64, 64), (0, 64, 32, 0)]   # (l, cin_up, C, skipC)
+
+
+def param_spec():
+    """(name, shape) in the C++ registration order (cad_resunet_tensor_info)."""
+    spec = [("encoder.conv1.weight", (64, 3, 7, 7)), ("encoder.bn1.weight", (64,)), ("encoder.bn1.bias", (64,))]
+    cin = 64
+    for L, (w, n) in enumerate(zip(WIDTHS, NBLOCKS)):
+        for i in range(n):
+            pre = f"encoder.layer{L + 1}.{i}."
+            spec += [(pre + "conv1.weight", (w, cin, 1, 1)), (pre + "bn1.weight", (w,)), (pre + "bn1.bias", (w,)),
+                     (pre + "conv2.weight", (w, w, 3, 3)), (pre + "bn2.weight", (w,)), (pre + "bn2.bias", (w,)),
+                     (pre + "conv3.weight", (4 * w, w, 1, 1)), (pre + "bn3.weight", (4 * w,)),
+                     (pre + "bn3.bias", (4 * w,))]
+            if i == 0:
+                spec += [(pre + "downsample.0.weight", (4 * w, cin, 1, 1)), (pre + "downsample.1.weight", (4 * w,)),
+                         (pre + "downsample.1.bias", (4 * w,))]
+            cin = 4 * w
+    for l, cu, C, sk in DEC:
+        pre = f"dec{l}."
+        spec += [(pre + "up.weight", (cu, C, 2, 2)), (pre + "up.bias", (C,)),
+                 (pre + "conv.conv1.weight", (C, sk + C, 3, 3)), (pre + "conv.bn1.weight", (C,)),
+                 (pre + "conv.bn1.bias", (C,)), (pre + "conv.conv2.weight", (C, C, 3, 3)),
+                 (pre + "conv.bn2.weight", (C,)), (pre + "conv.bn2.bias", (C,))]
+    spec += [("out_conv.weight", (1, 32, 1, 1)), ("out_conv.bias", (1,))]
+    return spec
+
+
+def buffer_spec():
+    out = []
+    for n, s in param_spec():
+        if n.endswith(".weight") and len(s) == 1:
+            pre = n[: -len("weight")]
+            out += [(pre + "running_mean", s), (pre + "running_var", s)]
+    return out
+
+
+def init(seed=0):
+    """Random parameters (conv / ConvT U(+-1/sqrt(fan_in)), BN gamma U(0.5, 1.5), beta U(-0.2, 0.2)) and
+    the default buffers — a generic point, not the GPU default init."""
+    g = torch.Generator().manual_seed(seed)
+    p = OrderedDict()
+    for n, s in param_spec():
+        if len(s) == 1 and (".bn" in n or "downsample.1" in n or "encoder.bn1" in n):
+            p[n] = (torch.rand(s, generator=g) + 0.5) if n.endswith("weight") else (torch.rand(s, generator=g) - 0.5) * 0.4
+        else:
+            if n.endswith("up.weight"):
+                fan = s[1] * 4
+            elif n.endswith("up.bias"):
+                fan = 4 * s[0]
+            elif n.startswith("out_conv"):
+                fan = 32
+            else:
+                fan = s[1] * s[2] * s[3]
+            p[n] = (torch.rand(s, generator=g) * 2 - 1) / fan ** 0.5
+    bufs = OrderedDict((n, torch.zeros(s) if "mean" in n else torch.ones(s)) for n, s in buffer_spec())
+    return p, bufs
+
+
+def _rnd(x):
+    return O._RoundOperand.apply(x) if O._GEMM["operands"] == "bf16" else x
+
+
+def _conv(x, w, stride, pad):
+    y = F.conv2d(_rnd(x), _rnd(w), None, stride, pad)
+    return O._RoundGradOperand.apply(y) if O._GEMM["operands"] == "bf16" else y
+
+
+def _bottleneck(x, p, bufs, pre, stride, down, train):
+    t = F.relu(O._bn(_conv(x, p[pre + "conv1.weight"], 1, 0), p, bufs, pre + "bn1", train))
+    t = F.relu(O._bn(_conv(t, p[pre + "conv2.weight"], stride, 1), p, bufs, pre + "bn2", train))
+    t = O._bn(_conv(t, p[pre + "conv3.weight"], 1, 0), p, bufs, pre + "bn3", train)
+    sc = O._bn(_conv(x, p[pre + "downsample.0.weight"], stride, 0), p, bufs, pre + "downsample.1", train) if down else x
+    return F.relu(t + sc)
+
+
+def forward(x, p, bufs, train=True, max_depth=10.0):
+    x1 = F.relu(O._bn(_conv(x, p["encoder.conv1.weight"], 2, 3), p, bufs, "encoder.bn1", train))
+    y = F.max_pool2d(x1, 3, 2, 1)
+    feats = []
+    for L, n in enumerate(NBLOCKS):
+        for i in range(n):
+            y = _bottleneck(y, p, bufs, f"encoder.layer{L + 1}.{i}.", 2 if (L > 0 and i == 0) else 1, i == 0, train)
+        feats.append(y)
+    skips = {4: feats[2], 3: feats[1], 2: feats[0], 1: x1}
+    for l, cu, C, sk in DEC:
+        pre = f"dec{l}."
+        up = O._convT2x2(y, p[pre + "up.weight"], p[pre + "up.bias"])
+        y = torch.cat([skips[l], up], 1) if sk else up
+        y = F.relu(O._bn(_conv(y, p[pre + "conv.conv1.weight"], 1, 1), p, bufs, pre + "conv.bn1", train))
+        y = F.relu(O._bn(_conv(y, p[pre + "conv.conv2.weight"], 1, 1), p, bufs, pre + "conv.bn2", train))
+    z = F.conv2d(y, p["out_conv.weight"], p["out_conv.bias"])
+    return torch.sigmoid(z) * max_depth
+
+
+class Trainer:
+    """forward, CombinedDepthLoss, backward, clip_grad_norm_(1.0), Adam — the GPU train_step's sequence."""
+
+    def __init__(self, params, buffers, weights=(1.0, 0.1, 0.001, 0.01), lr=1e-4, wd=1e-5, clip=1.0,
+                 dtype=torch.float32, operands="bf16"):
+        self.dtype, self.operands = dtype, operands
+        self.p = OrderedDict((k, v.clone().to(dtype)) for k, v in params.items())
+        self.bufs = OrderedDict((k, v.clone().to(dtype)) for k, v in buffers.items())
+        self.weights, self.clip = weights, clip
+        self.opt = O.Adam(self.p, lr=lr, weight_decay=wd)
+
+    def step(self, rgb, gt, K):
+        rgb, gt, K = rgb.to(self.dtype), gt.to(self.dtype), K.to(self.dtype)
+        for v in self.p.values():
+            v.requires_grad_(True)
+            v.grad = None
+        prev, O._GEMM["operands"] = O._GEMM["operands"], self.operands
+        try:
+            pred = forward(rgb, self.p, self.bufs, True)
+            loss, comps = O.combined_loss(pred, gt, rgb, K, self.weights)
+            loss.sum().backward()
+        finally:
+            O._GEMM["operands"] = prev
+        grads = [v.grad.detach().clone() for v in self.p.values()]
+        for v in self.p.values():
+            v.requires_grad_(False)
+        pre = [g.clone() for g in grads]
+        norm = O.clip_grad_norm_(grads, self.clip)
+        self.opt.step(grads)
+        return dict(pred=pred.detach(), loss=float(loss), comps=comps, grads=pre, norm=norm)
+
+    @torch.no_grad()
+    def predict_eval(self, rgb):
+        prev, O._GEMM["operands"] = O._GEMM["operands"], self.operands
+        try:
+            return forward(rgb.to(self.dtype), self.p, self.bufs, False)
+        finally:
+            O._GEMM["operands"] = prev
