@@ -130,6 +130,7 @@ struct DoubleConv {
     Film film;     // film.p0 < 0: plain DoubleConv
     int level = 0;
     float *y1 = nullptr, *a1 = nullptr, *y2 = nullptr;
+    bool y1b = false, y2b = false;   // y1 / y2 hold bf16 values (bf16 engine, pre-split conv of the last forward)
     void* a1s = nullptr;   // pre-split a1 (gemm_ps.hpp)
     int first_param = 0, last_param = 0;   // [first, last] indices in named_parameters()
     bool has_film() const { return film.p0 >= 0; }
@@ -493,27 +494,32 @@ void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin,
     };
     float* stats = tr ? h->stats : nullptr;
     const bool ps1 = ps && in_s.p && dc.c1.ws;
+    // the pre-split (bf16 engine) convolutions store their pre-BN outputs as bf16 (BN statistics are
+    // those of the stored values); BN apply / backward and FiLM read them as such
+    dc.y1b = ps1;
+    dc.y2b = ps;
     if (ps1)
-        cad::conv3x3_fwd_ps(in_s, dc.c1.cin, sv(dc.c1.ws, 9 * dc.c1.cin), C, dc.y1, C, 0, B, Hh, Ww, stats, st);
+        cad::conv3x3_fwd_ps(in_s, dc.c1.cin, sv(dc.c1.ws, 9 * dc.c1.cin), C, dc.y1, C, 0, B, Hh, Ww, stats, st, true);
     else
         cad::conv3x3_fwd(in, ldin, 0, dc.c1.cin, h->P(dc.c1.pidx), C, dc.y1, C, 0, B, Hh, Ww, stats, st);
     bn(dc.b1, dc.c1.cin, ps1);
     if (dc.has_film()) {   // FiLMDoubleConvImpl::forward (intrinsics_unet.h:38-52)
-        cad::film_apply(dc.y1, C, dc.b1.scale, dc.b1.shift, dc.film.gam, dc.film.bet, B, (int64_t)Hh * Ww, dc.a1, st);
+        cad::film_apply(dc.y1, C, dc.b1.scale, dc.b1.shift, dc.film.gam, dc.film.bet, B, (int64_t)Hh * Ww, dc.a1, st,
+                        dc.y1b);
         if (ps) cad::split_rows(dc.a1, C, 0, C, M, dc.a1s, C, 0, st);
     } else {
         // pre-split GEMMs read only a1's twin (conv2 and its weight gradient): the fp32 a1 is not written
         cad::bn_relu_fwd(dc.y1, C, dc.b1.scale, dc.b1.shift, ps ? nullptr : dc.a1, C, 0, M, st, ps ? dc.a1s : nullptr,
-                         C, 0);
+                         C, 0, dc.y1b);
     }
     if (ps)
-        cad::conv3x3_fwd_ps(sv(dc.a1s, C), C, sv(dc.c2.ws, 9 * C), C, dc.y2, C, 0, B, Hh, Ww, stats, st);
+        cad::conv3x3_fwd_ps(sv(dc.a1s, C), C, sv(dc.c2.ws, 9 * C), C, dc.y2, C, 0, B, Hh, Ww, stats, st, true);
     else
         cad::conv3x3_fwd(dc.a1, C, 0, C, h->P(dc.c2.pidx), C, dc.y2, C, 0, B, Hh, Ww, stats, st);
     bn(dc.b2, C, ps);
     const bool twin = ps && out_s.p;
     cad::bn_relu_fwd(dc.y2, C, dc.b2.scale, dc.b2.shift, (out_f32 || !twin) ? out : nullptr, ldo, ocoff, M, st,
-                     twin ? const_cast<void*>(out_s.p) : nullptr, out_s.ld, out_s.coff);
+                     twin ? const_cast<void*>(out_s.p) : nullptr, out_s.ld, out_s.coff, dc.y2b);
 }
 
 void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth, int B, hipStream_t st) {
@@ -593,7 +599,7 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     // with pre-split GEMMs both consumers of dY2 read its twin: the fp32 dY2 is not written
     cad::bn_relu_bwd(g, ldg, gcoff, dc.y2, C, dc.b2.mean, dc.b2.invstd, dc.b2.scale, dc.b2.shift, h->P(dc.b2.widx), M,
                      h->dscr, dc.b2.coef, h->G(dc.b2.widx), h->G(dc.b2.bidx), ps ? nullptr : dY, st, nullptr, 1,
-                     ps ? dYs : nullptr);
+                     ps ? dYs : nullptr, true, dc.y2b);
     // conv2: wgrad, dgrad
     if (ps) {
         cad::conv3x3_wgrad_ps(sv(dYs, C), C, sv(dc.a1s, C), C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
@@ -605,14 +611,15 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     // FiLM: dgamma/dbeta per (sample, channel); the ReLU sees dA1 * gamma (folded into bn_relu_bwd)
     const int64_t HW = (int64_t)Hh * Ww;
     if (dc.has_film())
-        cad::film_affine_bwd(dA1, dc.y1, C, dc.b1.scale, dc.b1.shift, B, HW, h->dscr, dc.film.dgam, dc.film.dbet, st);
+        cad::film_affine_bwd(dA1, dc.y1, C, dc.b1.scale, dc.b1.shift, B, HW, h->dscr, dc.film.dgam, dc.film.dbet, st,
+                             dc.y1b);
     // bn1 + relu; the fp32 dY1 only when a conv1 GEMM below reads it (enc1's 4-channel input keeps the
     // in-loader weight gradient)
     const bool ps1 = ps && in_s.p && dc.c1.ws;
     const bool dy1_f32 = !ps1 || (din && !(ps && dc.c1.wds));
     cad::bn_relu_bwd(dA1, C, 0, dc.y1, C, dc.b1.mean, dc.b1.invstd, dc.b1.scale, dc.b1.shift, h->P(dc.b1.widx), M,
                      h->dscr, dc.b1.coef, h->G(dc.b1.widx), h->G(dc.b1.bidx), dy1_f32 ? dY : nullptr, st,
-                     dc.has_film() ? dc.film.gam : nullptr, HW, ps ? dYs : nullptr);
+                     dc.has_film() ? dc.film.gam : nullptr, HW, ps ? dYs : nullptr, true, dc.y1b);
     if (dc.has_film()) cad::film_mlp_bwd(film_view(h, dc), h->camn, B, st);
     // conv1: wgrad, dgrad
     if (ps1)
@@ -1009,7 +1016,8 @@ int64_t cad_unet_debug_buffer(cad_unet* h, const char* name, float* host, int64_
         const bool film = h->model != CAD_MODEL_BASELINE;
         const bool twin_only = n == "Sb" || n == "bott" || (n.compare(0, 4, "pool") == 0) ||
                                (n.compare(0, 4, "dout") == 0 && n != "dout0") ||
-                               (!film && n.size() > 5 && n.substr(5) == "a1");
+                               (!film && n.size() > 5 && n.substr(5) == "a1") ||
+                               (n.size() > 5 && (n.substr(5) == "y1" || n.substr(5) == "y2"));   // bf16 values
         if (twin_only) {
             g_err = "debug buffer '" + n + "' holds no fp32 copy on the pre-split (bf16) engine";
             return -1;

@@ -20,7 +20,8 @@
 //     dec0: up 64 -> 32            -> DC(32 -> 32)      /1
 //     out_conv 1x1 (32 -> 1), sigmoid * max_depth
 //
-// Contractions (all on the B1 pre-split engine: bf16 operand twins, fp32 accumulation):
+// Contractions (all on the B1 pre-split engine: bf16 operand twins, fp32 accumulation; the pre-BN
+// conv outputs are stored as bf16, their BN statistics taken from the stored values):
 //   3x3 stride-1 convolutions: the window kernels (conv3x3_*_ps, gemm_win.hpp / gemm_ps.hpp);
 //   1x1 convolutions: dense GEMMs straight on the activation twins (stride 2: subsampled twin);
 //   7x7/2 stem and 3x3/2 convolutions: im2col twin + dense GEMM, col2im gather for the dgrad;
@@ -484,7 +485,7 @@ void unit_fwd(cad_resunet* h, Unit& u, cad::Split in, int B, int Hin, int Win, v
     float* stats = h->train ? h->stats : nullptr;
     int rows = 0;
     if (c.win) {
-        cad::conv3x3_fwd_ps(in, c.cin, tw(c.ws, c.Kp), c.cout, u.y, c.cout, 0, B, Hin, Win, stats, st);
+        cad::conv3x3_fwd_ps(in, c.cin, tw(c.ws, c.Kp), c.cout, u.y, c.cout, 0, B, Hin, Win, stats, st, true);
         rows = cad::conv3x3_stats_rows(c.cin, B, Hin, Win, c.cout, true);
     } else {
         cad::Split a = in;
@@ -497,7 +498,7 @@ void unit_fwd(cad_resunet* h, Unit& u, cad::Split in, int B, int Hin, int Win, v
                 a = tw(col, c.Kp);
             }
         }
-        cad::dense_fwd_ps(a, c.Kp, tw(c.ws, c.Kp), c.cout, u.y, c.cout, 0, Mo, stats, st);
+        cad::dense_fwd_ps(a, c.Kp, tw(c.ws, c.Kp), c.cout, u.y, c.cout, 0, Mo, stats, st, true);
         rows = cad::dense_stats_rows(Mo, c.cout);
     }
     RBN& b = u.b;
@@ -532,14 +533,14 @@ void forward(cad_resunet* h, const float* rgb, float* depth, int B, hipStream_t 
     cad::im2col_f32(h->x0, 4, 0, 4, B, h->H, h->W, 7, 7, 2, 3, h->stem_col, sc.Kp, st);
     {
         float* stats = h->train ? h->stats : nullptr;
-        cad::dense_fwd_ps(tw(h->stem_col, sc.Kp), sc.Kp, tw(sc.ws, sc.Kp), 64, h->stem.y, 64, 0, M1, stats, st);
+        cad::dense_fwd_ps(tw(h->stem_col, sc.Kp), sc.Kp, tw(sc.ws, sc.Kp), 64, h->stem.y, 64, 0, M1, stats, st, true);
         RBN& b = h->stem.b;
         if (h->train)
             cad::bn_fwd_finalize(h->stats, cad::dense_stats_rows(M1, 64), 64, M1, h->P(b.widx), h->P(b.bidx), b.rm, b.rv,
                                  0.1f, 1e-5f, h->dscr, b.mean, b.invstd, b.scale, b.shift, st);
         else
             cad::bn_eval_coeffs(h->P(b.widx), h->P(b.bidx), b.rm, b.rv, 64, 1e-5f, b.mean, b.invstd, b.scale, b.shift, st);
-        cad::bn_relu_fwd(h->stem.y, 64, b.scale, b.shift, h->s_out, 64, 0, M1, st, h->s_outs, 64, 0);
+        cad::bn_relu_fwd(h->stem.y, 64, b.scale, b.shift, h->s_out, 64, 0, M1, st, h->s_outs, 64, 0, true);
     }
     cad::maxpool3s2_fwd(h->s_out, 64, B, H1, W1, h->pool, h->pidx, h->pools, st);
     // bottlenecks
@@ -548,13 +549,13 @@ void forward(cad_resunet* h, const float* rgb, float* depth, int B, hipStream_t 
     for (Bott& b : h->blocks) {
         const int64_t Mi = h->M(B, b.H, b.W), Mo = h->M(B, b.Ho, b.Wo);
         unit_fwd(h, b.u1, tw(xsw, b.cin), B, b.H, b.W, nullptr, nullptr, st);
-        cad::bn_relu_fwd(b.u1.y, b.w, b.u1.b.scale, b.u1.b.shift, nullptr, b.w, 0, Mi, st, b.t1s, b.w, 0);
+        cad::bn_relu_fwd(b.u1.y, b.w, b.u1.b.scale, b.u1.b.shift, nullptr, b.w, 0, Mi, st, b.t1s, b.w, 0, true);
         unit_fwd(h, b.u2, tw(b.t1s, b.w), B, b.H, b.W, b.col2, nullptr, st);
-        cad::bn_relu_fwd(b.u2.y, b.w, b.u2.b.scale, b.u2.b.shift, nullptr, b.w, 0, Mo, st, b.t2s, b.w, 0);
+        cad::bn_relu_fwd(b.u2.y, b.w, b.u2.b.scale, b.u2.b.shift, nullptr, b.w, 0, Mo, st, b.t2s, b.w, 0, true);
         unit_fwd(h, b.u3, tw(b.t2s, b.w), B, b.Ho, b.Wo, nullptr, nullptr, st);
         if (b.down) unit_fwd(h, b.ud, tw(xsw, b.cin), B, b.H, b.W, nullptr, b.xs, st);
         cad::bn_add_relu(b.u3.y, b.u3.b.scale, b.u3.b.shift, b.down ? b.ud.y : nullptr, b.ud.b.scale, b.ud.b.shift, xf,
-                         b.cin, b.cout, Mo, b.out, b.outs, st);
+                         b.cin, b.cout, Mo, b.out, b.outs, st, true);
         xf = b.out;
         xsw = b.outs;
     }
@@ -571,9 +572,9 @@ void forward(cad_resunet* h, const float* rgb, float* depth, int B, hipStream_t 
         cad::split_rows(d.upf, d.cout_up, 0, d.cout_up, Md, d.cats, cc, d.skipC, st);
         if (d.skipC) cad::copy_twin(tw(skips[j], d.skipC), d.skipC, B, d.H, d.W, 1, d.cats, cc, 0, st);
         unit_fwd(h, d.u1, tw(d.cats, cc), B, d.H, d.W, nullptr, nullptr, st);
-        cad::bn_relu_fwd(d.u1.y, d.C, d.u1.b.scale, d.u1.b.shift, nullptr, d.C, 0, Md, st, d.a1s, d.C, 0);
+        cad::bn_relu_fwd(d.u1.y, d.C, d.u1.b.scale, d.u1.b.shift, nullptr, d.C, 0, Md, st, d.a1s, d.C, 0, true);
         unit_fwd(h, d.u2, tw(d.a1s, d.C), B, d.H, d.W, nullptr, nullptr, st);
-        cad::bn_relu_fwd(d.u2.y, d.C, d.u2.b.scale, d.u2.b.shift, d.out, d.C, 0, Md, st, d.outs, d.C, 0);
+        cad::bn_relu_fwd(d.u2.y, d.C, d.u2.b.scale, d.u2.b.shift, d.out, d.C, 0, Md, st, d.outs, d.C, 0, true);
         prev = d.outs;
     }
     cad::head_fwd(h->dec.back().out, 32, h->P(h->head_w), h->P(h->head_b), h->max_depth, h->sig, depth,
@@ -611,7 +612,7 @@ void unit_bwd(cad_resunet* h, Unit& u, const float* g, int64_t ldg, int gcoff, b
     const int64_t Mo = h->M(B, Ho, Wo);
     RBN& b = u.b;
     cad::bn_relu_bwd(g, ldg, gcoff, u.y, b.C, b.mean, b.invstd, b.scale, b.shift, h->P(b.widx), Mo, h->dscr, b.coef,
-                     h->G(b.widx), h->G(b.bidx), nullptr, st, nullptr, 1, h->dYs, relu);
+                     h->G(b.widx), h->G(b.bidx), nullptr, st, nullptr, 1, h->dYs, relu, true);
     const cad::Split dz = tw(h->dYs, c.cout);
     if (c.win) {
         cad::conv3x3_wgrad_ps(dz, c.cout, in, c.cin, h->G(c.pidx), B, Hin, Win, h->slab, h->slab_cap, st);
@@ -696,7 +697,7 @@ void backward(cad_resunet* h, const float* ddepth, hipStream_t st) {
     cad::add_strided(gs, 64, d1.dcat, d1.skipC + d1.cout_up, 0, 64, B, H1, W1, 1, st);
     RBN& sb = h->stem.b;
     cad::bn_relu_bwd(gs, 64, 0, h->stem.y, 64, sb.mean, sb.invstd, sb.scale, sb.shift, h->P(sb.widx), M1, h->dscr, sb.coef,
-                     h->G(sb.widx), h->G(sb.bidx), nullptr, st, nullptr, 1, h->dYs, true);
+                     h->G(sb.widx), h->G(sb.bidx), nullptr, st, nullptr, 1, h->dYs, true, true);
     cad::dense_wgrad_ps(tw(h->dYs, 64), 64, tw(h->stem_col, h->stem.c.Kp), h->stem.c.Kp, h->G(h->stem.c.pidx),
                         h->stem.c.Kp, M1, h->slab, h->slab_cap, st);
 }

@@ -19,6 +19,7 @@ namespace cad {
 // descriptor based at row_base (gemm_mfma.hpp gemm_epilogue).
 struct EpiStore {
     static constexpr bool STATS = false;
+    static constexpr bool BF16 = false;
     __device__ static const float* row_base(const GemmArgs& a, int m0, int) {
         return a.C + (int64_t)m0 * a.ldc + a.c_coff;
     }
@@ -26,11 +27,24 @@ struct EpiStore {
 struct EpiStoreStats : EpiStore {
     static constexpr bool STATS = true;
 };
+// bf16 outputs (round-to-nearest-even; a.C addresses bf16 rows of ldc elements): the pre-BN conv
+// outputs of the bf16 engine.  BN partials are taken from the rounded values BN normalises.
+struct EpiStoreB16 {
+    static constexpr bool STATS = false;
+    static constexpr bool BF16 = true;
+    __device__ static const float* row_base(const GemmArgs& a, int m0, int) {
+        return reinterpret_cast<const float*>(reinterpret_cast<const char*>(a.C) + ((int64_t)m0 * a.ldc + a.c_coff) * 2);
+    }
+};
+struct EpiStoreStatsB16 : EpiStoreB16 {
+    static constexpr bool STATS = true;
+};
 // ConvTranspose2d(k2,s2) pixel shuffle: n = (q=(dy,dx), co) -> high-res pixel (2y+dy, 2x+dx).
 // The column (q, co) is fixed per lane and sub-block, and rows advance in small steps, so the
 // epilogue carries (x, y, b) incrementally instead of dividing per element (STRUCTURED epilogue).
 struct EpiConvT {
     static constexpr bool STATS = false;
+    static constexpr bool BF16 = false;
     static constexpr bool STRUCTURED = true;
     __device__ void operator()(const GemmArgs& a, int m, int n, float v, int) const {
         const int cout = a.N >> 2;
@@ -64,6 +78,7 @@ struct EpiConvT {
 };
 struct EpiSlab {   // split-K partial: slab z holds C[m][n] of K-slice z
     static constexpr bool STATS = false;
+    static constexpr bool BF16 = false;
     __device__ static const float* row_base(const GemmArgs& a, int m0, int z) {
         return a.C + (int64_t)z * a.slab_stride + (int64_t)m0 * a.ldc;
     }
@@ -413,6 +428,13 @@ CAD_KT(KConvTWgrad, (k_convT_wgrad<WM, WN, KB>), "void cad::k_convT_wgrad<%d, %d
 CAD_KT(KDenseP1, (k_dense_bf16p<WM, WN, KB, EpiStore>), "void cad::k_dense_bf16p<%d, %d, %d, cad::EpiStore>(cad::GemmArgs)")
 CAD_KT(KDenseSP1, (k_dense_bf16p<WM, WN, KB, EpiStoreStats>),
        "void cad::k_dense_bf16p<%d, %d, %d, cad::EpiStoreStats>(cad::GemmArgs)")
+CAD_KT(KDenseP1B, (k_dense_bf16p<WM, WN, KB, EpiStoreB16>), "void cad::k_dense_bf16p<%d, %d, %d, cad::EpiStoreB16>(cad::GemmArgs)")
+CAD_KT(KDenseSP1B, (k_dense_bf16p<WM, WN, KB, EpiStoreStatsB16>),
+       "void cad::k_dense_bf16p<%d, %d, %d, cad::EpiStoreStatsB16>(cad::GemmArgs)")
+CAD_KT(KConvFwdP1B, (k_conv3x3_fwd_bf16p<WM, WN, KB, EpiStoreB16>),
+       "void cad::k_conv3x3_fwd_bf16p<%d, %d, %d, cad::EpiStoreB16>(cad::GemmArgs)")
+CAD_KT(KConvFwdSP1B, (k_conv3x3_fwd_bf16p<WM, WN, KB, EpiStoreStatsB16>),
+       "void cad::k_conv3x3_fwd_bf16p<%d, %d, %d, cad::EpiStoreStatsB16>(cad::GemmArgs)")
 CAD_KT(KDenseWgradP1, (k_dense_wgrad_bf16p<WM, WN, KB>), "void cad::k_dense_wgrad_bf16p<%d, %d, %d>(cad::GemmArgs)")
 // in-loader split engines: KConvFwd3 ... (S3), KConvFwdB ... (B1); pre-split B1: KConvFwdP1 ...
 CAD_NP_KT(s3, 3)
@@ -469,8 +491,8 @@ void launch_win1(const GemmArgs& a, hipStream_t st) {
     auto fn = PS ? (void (*)(GemmArgs))k_conv3x3_win_bf16p<R, CW, Epi> : (void (*)(GemmArgs))k_conv3x3_win_s3<R, CW, Epi>;
     if (prof_enabled()) {
         char name[160];
-        snprintf(name, sizeof(name), "void cad::k_conv3x3_win_%s<%d, %d, cad::%s>(cad::GemmArgs)", PS ? "bf16p" : "s3", R,
-                 CW, Epi::STATS ? "EpiStoreStats" : "EpiStore");
+        snprintf(name, sizeof(name), "void cad::k_conv3x3_win_%s<%d, %d, cad::%s%s>(cad::GemmArgs)", PS ? "bf16p" : "s3",
+                 R, CW, Epi::STATS ? "EpiStoreStats" : "EpiStore", Epi::BF16 ? "B16" : "");
         prof_push(name, 2.0 * a.M * a.N * (double)a.K, st);
         hipLaunchKernelGGL(fn, grid, dim3(256), 0, st, a);
         prof_pop(st);
@@ -727,7 +749,7 @@ void ps_check(const Split& s, int channels, const char* what) {
 }  // namespace
 
 void conv3x3_fwd_ps(Split x, int cin, Split w, int cout, float* y, int64_t ldy, int ycoff, int B, int H, int W,
-                    float* stats, hipStream_t st) {
+                    float* stats, hipStream_t st, bool y_bf16) {
     ps_check(x, cin, "conv3x3_fwd x");
     ps_check(w, 9 * cin, "conv3x3_fwd w");
     GemmArgs a{};
@@ -738,8 +760,13 @@ void conv3x3_fwd_ps(Split x, int cin, Split w, int cout, float* y, int64_t ldy, 
     a.C = y; a.ldc = ldy; a.c_coff = ycoff;
     a.stats = stats;
     if (const WinPick wp = pick_win_ps(cin, W, cout, x.coff); wp.R && w.coff == 0) {
-        if (stats) launch_win<EpiStoreStats, true>(wp, a, st);
-        else launch_win<EpiStore, true>(wp, a, st);
+        if (y_bf16) {
+            if (stats) launch_win<EpiStoreStatsB16, true>(wp, a, st);
+            else launch_win<EpiStoreB16, true>(wp, a, st);
+        } else {
+            if (stats) launch_win<EpiStoreStats, true>(wp, a, st);
+            else launch_win<EpiStore, true>(wp, a, st);
+        }
         return;
     }
     const Cfg c = pick_cfg(a.M, a.N);
@@ -747,8 +774,13 @@ void conv3x3_fwd_ps(Split x, int cin, Split w, int cout, float* y, int64_t ldy, 
     a.kstages_per_split = cdiv(a.K, kb);
     // channel-major K order: the nine taps of a channel block re-read the same input rows back to back
     a.cimajor = cin % kb == 0;
-    if (stats) launch_kb<KConvFwdSP1, 32, 64>(c, kb, a, 1, st);
-    else launch_kb<KConvFwdP1, 32, 64>(c, kb, a, 1, st);
+    if (y_bf16) {
+        if (stats) launch_kb<KConvFwdSP1B, 32, 64>(c, kb, a, 1, st);
+        else launch_kb<KConvFwdP1B, 32, 64>(c, kb, a, 1, st);
+    } else {
+        if (stats) launch_kb<KConvFwdSP1, 32, 64>(c, kb, a, 1, st);
+        else launch_kb<KConvFwdP1, 32, 64>(c, kb, a, 1, st);
+    }
 }
 
 void conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t lddx, int B, int H, int W,
@@ -796,7 +828,7 @@ void conv3x3_wgrad_ps(Split dz, int cout, Split x, int cin, float* dw, int B, in
 int dense_stats_rows(int64_t M, int N) { return cdiv(M, tile_m(pick_cfg((int)M, N))); }
 
 void dense_fwd_ps(Split x, int K, Split w, int N, float* y, int64_t ldy, int ycoff, int64_t M, float* stats,
-                  hipStream_t st) {
+                  hipStream_t st, bool y_bf16) {
     ps_check(x, K, "dense x");
     ps_check(w, K, "dense w");
     if (M > INT32_MAX) throw std::runtime_error("dense GEMM: too many rows");
@@ -810,8 +842,13 @@ void dense_fwd_ps(Split x, int K, Split w, int N, float* y, int64_t ldy, int yco
     const Cfg c = pick_cfg(a.M, a.N);
     const int kb = ps_kb(true, c);
     a.kstages_per_split = cdiv(a.K, kb);
-    if (stats) launch_kb<KDenseSP1, 32, 64>(c, kb, a, 1, st);
-    else launch_kb<KDenseP1, 32, 64>(c, kb, a, 1, st);
+    if (y_bf16) {
+        if (stats) launch_kb<KDenseSP1B, 32, 64>(c, kb, a, 1, st);
+        else launch_kb<KDenseP1B, 32, 64>(c, kb, a, 1, st);
+    } else {
+        if (stats) launch_kb<KDenseSP1, 32, 64>(c, kb, a, 1, st);
+        else launch_kb<KDenseP1, 32, 64>(c, kb, a, 1, st);
+    }
 }
 
 void dense_wgrad_ps(Split dz, int N, Split x, int K, float* dw, int64_t ldw, int64_t M, float* slab, int64_t slab_cap,

@@ -14,6 +14,7 @@
 // the same two-level slice scheme as the BN reductions.
 #include <algorithm>
 
+#include "ew_load.hpp"
 #include "kernels.hpp"
 
 namespace cad {
@@ -171,6 +172,7 @@ void film_mlp_fwd(const FilmLayer& L, const float* camn, int B, bool train, hipS
 // ------------------------------------------------------------------------------------------
 // a16/a17 affine: a1 = gamma[b,c] * relu(y1 * scale[c] + shift[c]) + beta[b,c]
 // ------------------------------------------------------------------------------------------
+template <bool YB>
 __global__ void k_film_apply(const float* __restrict__ y, int C, const float* __restrict__ scale,
                              const float* __restrict__ shift, const float* __restrict__ gam,
                              const float* __restrict__ bet, int64_t HW, float* __restrict__ out, int64_t n4) {
@@ -179,7 +181,7 @@ __global__ void k_film_apply(const float* __restrict__ y, int C, const float* __
         const int64_t r = i / C4;
         const int c = (int)(i - r * C4) * 4;
         const int64_t bc = (r / HW) * C + c;
-        const float4 v = *reinterpret_cast<const float4*>(y + i * 4);
+        const float4 v = load4<YB>(y, i * 4);
         const float4 s = *reinterpret_cast<const float4*>(scale + c);
         const float4 t = *reinterpret_cast<const float4*>(shift + c);
         const float4 g = *reinterpret_cast<const float4*>(gam + bc);
@@ -193,9 +195,14 @@ __global__ void k_film_apply(const float* __restrict__ y, int C, const float* __
     }
 }
 void film_apply(const float* y, int C, const float* scale, const float* shift, const float* gam, const float* bet,
-                int B, int64_t HW, float* out, hipStream_t st) {
+                int B, int64_t HW, float* out, hipStream_t st, bool y_bf16) {
     const int64_t n4 = (int64_t)B * HW * C / 4;
-    hipLaunchKernelGGL(k_film_apply, dim3(ew_blocks(n4)), dim3(256), 0, st, y, C, scale, shift, gam, bet, HW, out, n4);
+    if (y_bf16)
+        hipLaunchKernelGGL(k_film_apply<true>, dim3(ew_blocks(n4)), dim3(256), 0, st, y, C, scale, shift, gam, bet, HW, out,
+                           n4);
+    else
+        hipLaunchKernelGGL(k_film_apply<false>, dim3(ew_blocks(n4)), dim3(256), 0, st, y, C, scale, shift, gam, bet, HW,
+                           out, n4);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -204,6 +211,7 @@ void film_apply(const float* y, int C, const float* scale, const float* shift, c
 // ------------------------------------------------------------------------------------------
 int film_reduce_slices(int64_t HW) { return (int)std::max<int64_t>(1, std::min<int64_t>(64, HW / 1024)); }
 
+template <bool YB>
 __global__ __launch_bounds__(256) void k_film_reduce(const float* __restrict__ dA, const float* __restrict__ y,
                                                      int C, const float* __restrict__ scale,
                                                      const float* __restrict__ shift, int64_t HW, int64_t rps,
@@ -221,7 +229,7 @@ __global__ __launch_bounds__(256) void k_film_reduce(const float* __restrict__ d
         for (int64_t r = r0 + threadIdx.y; r < r1; r += RY) {
             const int64_t off = ((int64_t)b * HW + r) * C + c4 * 4;
             const float4 d = *reinterpret_cast<const float4*>(dA + off);
-            const float4 v = *reinterpret_cast<const float4*>(y + off);
+            const float4 v = load4<YB>(y, off);
             ag[0] += (double)d.x * fmaxf(v.x * s.x + t.x, 0.f);
             ag[1] += (double)d.y * fmaxf(v.y * s.y + t.y, 0.f);
             ag[2] += (double)d.z * fmaxf(v.z * s.z + t.z, 0.f);
@@ -257,15 +265,19 @@ __global__ void k_film_reduce_final(const double* __restrict__ part, int S, int 
     dbet[i] = (float)be;
 }
 void film_affine_bwd(const float* dA, const float* y, int C, const float* scale, const float* shift, int B, int64_t HW,
-                     double* scratch, float* dgam, float* dbet, hipStream_t st) {
+                     double* scratch, float* dgam, float* dbet, hipStream_t st, bool y_bf16) {
     const int C4 = C >> 2;
     const int CX = std::min(C4, 64);
     const int RY = std::max(1, 256 / CX);
     const int S = film_reduce_slices(HW);
     const int64_t rps = (HW + S - 1) / S;
     const size_t shm = (size_t)RY * CX * 8 * sizeof(double);
-    hipLaunchKernelGGL(k_film_reduce, dim3(cdiv(C4, CX), S, B), dim3(CX, RY), shm, st, dA, y, C, scale, shift, HW, rps,
-                       scratch);
+    if (y_bf16)
+        hipLaunchKernelGGL(k_film_reduce<true>, dim3(cdiv(C4, CX), S, B), dim3(CX, RY), shm, st, dA, y, C, scale, shift, HW,
+                           rps, scratch);
+    else
+        hipLaunchKernelGGL(k_film_reduce<false>, dim3(cdiv(C4, CX), S, B), dim3(CX, RY), shm, st, dA, y, C, scale, shift,
+                           HW, rps, scratch);
     hipLaunchKernelGGL(k_film_reduce_final, dim3(cdiv((int64_t)B * C, 256)), dim3(256), 0, st, scratch, S, C, B, dgam,
                        dbet);
 }

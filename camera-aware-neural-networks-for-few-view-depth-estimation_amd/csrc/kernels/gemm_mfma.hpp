@@ -474,7 +474,8 @@ __device__ __forceinline__ void gemm_epilogue_t(const GemmArgs& a, const floatx1
     // Row-major epilogues (EpiStore, EpiSlab) store through a buffer descriptor based at the tile's
     // first output row whose range ends at row M: rows past M are dropped by the range check and
     // columns past N get an out-of-range offset, so each store is one 32-bit offset add.
-    const int64_t ldc4 = a.ldc * 4;
+    constexpr int ES = Epi::BF16 ? 2 : 4;   // output element bytes
+    const int64_t ldc4 = a.ldc * ES;
     const int64_t bytes = (int64_t)(a.M - m0) * ldc4;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(epi_row_base<Epi>(a, m0, tile.z),
                                                 (uint32_t)(bytes < (int64_t)kRecords ? bytes : kRecords));
@@ -495,12 +496,20 @@ __device__ __forceinline__ void gemm_epilogue_t(const GemmArgs& a, const floatx1
                 float v[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[r] = acc[i][j][4 * g + r];
+                if constexpr (Epi::BF16) {   // the stored (rounded) values, which BN then normalises
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = (float)(__bf16)v[r];
+                }
                 if constexpr (!is_structured<Epi>::value) {
-                    const uint32_t lo = n < a.N ? (uint32_t)(mr * ldc4 + (int64_t)n * 4) : kOOB;
+                    const uint32_t lo = n < a.N ? (uint32_t)(mr * ldc4 + (int64_t)n * ES) : kOOB;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[r]), rs,
-                                                              lo + (uint32_t)(r * ldc4), 0, 0);
+                        if constexpr (Epi::BF16)
+                            __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, (__bf16)v[r]), rs,
+                                                                  lo + (uint32_t)(r * ldc4), 0, 0);
+                        else
+                            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[r]), rs,
+                                                                  lo + (uint32_t)(r * ldc4), 0, 0);
                         if constexpr (Epi::STATS) {
                             const float vm = m0 + mr + r < a.M ? v[r] : 0.f;
                             ssum[j] += vm;

@@ -118,8 +118,10 @@ __device__ __forceinline__ void win_epilogue(const GemmArgs& a, const floatx16 (
     float ssum[NJ], ssq[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) ssum[j] = ssq[j] = 0.f;
-    const int64_t ldc4 = a.ldc * 4;
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(a.C + (((int64_t)b * a.H + y0) * a.W + x0) * a.ldc + a.c_coff);
+    constexpr int ES = Epi::BF16 ? 2 : 4;   // output element bytes
+    const int64_t ldc4 = a.ldc * ES;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const float*>(
+        reinterpret_cast<const char*>(a.C) + ((((int64_t)b * a.H + y0) * a.W + x0) * a.ldc + a.c_coff) * ES));
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -130,14 +132,22 @@ __device__ __forceinline__ void win_epilogue(const GemmArgs& a, const floatx16 (
                 const int mr = wm * 32 * MI + i * 32 + 4 * (lane >> 5) + 8 * g;   // 4 rows mr..mr+3: same r
                 const int r = mr / CW, c = mr - r * CW;
                 const bool ok = n < a.N && y0 + r < a.H;
-                const uint32_t lo = ok ? (uint32_t)((r * (int64_t)a.W + c) * ldc4 + (int64_t)n * 4) : kOOB;
+                const uint32_t lo = ok ? (uint32_t)((r * (int64_t)a.W + c) * ldc4 + (int64_t)n * ES) : kOOB;
                 float v[4];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) v[q] = acc[i][j][4 * g + q];
+                if constexpr (Epi::BF16) {   // the stored (rounded) values, which BN then normalises
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) v[q] = (float)(__bf16)v[q];
+                }
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[q]), rs,
-                                                          lo + (uint32_t)(q * ldc4), 0, 0);
+                    if constexpr (Epi::BF16)
+                        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, (__bf16)v[q]), rs,
+                                                              lo + (uint32_t)(q * ldc4), 0, 0);
+                    else
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[q]), rs,
+                                                              lo + (uint32_t)(q * ldc4), 0, 0);
                     if constexpr (Epi::STATS) {
                         const float vm = y0 + r < a.H ? v[q] : 0.f;
                         ssum[j] += vm;

@@ -52,8 +52,9 @@ constexpr int kMaxPlanes = 1;          // twin bytes = elems * 2 * kMaxPlanes
 // out[row][ocoff + c] (split, ld ldo) = split(x[row][xcoff + c]), c < C, rows < M
 void split_rows(const float* x, int64_t ldx, int xcoff, int C, int64_t M, void* out, int64_t ldo, int ocoff,
                 hipStream_t st);
+// y_bf16: y is written as bf16 rows of ldy elements (the bf16 engine's pre-BN outputs)
 void conv3x3_fwd_ps(Split x, int cin, Split w, int cout, float* y, int64_t ldy, int ycoff, int B, int H, int W,
-                    float* stats, hipStream_t st);
+                    float* stats, hipStream_t st, bool y_bf16 = false);
 void conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t lddx, int B, int H, int W,
                       hipStream_t st);
 void conv3x3_wgrad_ps(Split dz, int cout, Split x, int cin, float* dw, int B, int H, int W, float* slab,
@@ -67,7 +68,7 @@ void convT_wgrad_ps(Split x, int cin, Split g, int cout, float* dw, int B, int H
 // ---- dense GEMMs on the pre-split twins (the 1x1 / im2col convolutions of the config-5 network) ----
 // y[m][ycoff + n] = sum_k x[m][k] w[n][k]  (+ BN partials [rows][2][N] when stats != nullptr)
 void dense_fwd_ps(Split x, int K, Split w, int N, float* y, int64_t ldy, int ycoff, int64_t M, float* stats,
-                  hipStream_t st);
+                  hipStream_t st, bool y_bf16 = false);
 int dense_stats_rows(int64_t M, int N);
 // dw[n][k] = sum_m dz[m][n] x[m][k]  (reduction over the M pixels; split-K slabs)
 void dense_wgrad_ps(Split dz, int N, Split x, int K, float* dw, int64_t ldw, int64_t M, float* slab, int64_t slab_cap,
@@ -87,7 +88,7 @@ void maxpool3s2_bwd(const float* dout, const uint8_t* idx, int C, int B, int H, 
 // out = relu(y*scale + shift + (yd ? yd*dscale + dshift : x)), fp32 [M][C] + twin
 void bn_add_relu(const float* y, const float* scale, const float* shift, const float* yd, const float* dscale,
                  const float* dshift, const float* x, int64_t ldx, int C, int64_t M, float* out, void* out_split,
-                 hipStream_t st);
+                 hipStream_t st, bool y_bf16 = false);
 void relu_mask(const float* g, int64_t ldg, int gcoff, const float* out, int C, int64_t M, float* gs, hipStream_t st);
 // dst[(b, S*oy, S*ox)][c] += src[(b, oy, ox)][scoff + c] over the strided grid of a B x H x W image
 void add_strided(float* dst, int64_t lddst, const float* src, int64_t ldsrc, int scoff, int C, int B, int H, int W,
@@ -112,8 +113,10 @@ void bn_eval_coeffs(const float* gamma, const float* beta, const float* run_mean
                     int C, float eps, float* mean, float* invstd, float* scale, float* shift, hipStream_t st);
 // os != nullptr: also writes the output's pre-split twin (split rows of ldos channels at channel
 // offset oscoff, split_planes() planes; see Split below)
+// y_bf16: y holds bf16 values (conv outputs of the bf16 engine; also in bn_relu_bwd, film_*, bn_add_relu)
 void bn_relu_fwd(const float* y, int C, const float* scale, const float* shift, float* out, int64_t ldo,
-                 int ocoff, int64_t M, hipStream_t st, void* os = nullptr, int64_t ldos = 0, int oscoff = 0);
+                 int ocoff, int64_t M, hipStream_t st, void* os = nullptr, int64_t ldos = 0, int oscoff = 0,
+                 bool y_bf16 = false);
 // BN+ReLU backward: dy = k1*dz - k2 - k3*xhat, dz = g*[y*scale+shift > 0];
 // writes dgamma/dbeta (grad buffer) and dy (dense [M][C]).  gmul != nullptr: g is first multiplied
 // by gmul[sample][c] (sample = row / HW) — the FiLM gamma sitting between this ReLU and the consumer.
@@ -123,7 +126,7 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
                  const float* invstd, const float* scale, const float* shift, const float* gamma,
                  int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
                  hipStream_t st, const float* gmul = nullptr, int64_t HW = 1, void* dy_split = nullptr,
-                 bool relu = true);
+                 bool relu = true, bool y_bf16 = false);
 // out_split != nullptr: also the pooled output's split twin (dense, ld C); out may then be nullptr
 void maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float* out, uint8_t* idx,
                  hipStream_t st, void* out_split = nullptr);
@@ -202,10 +205,10 @@ void film_mlp_fwd(const FilmLayer& L, const float* camn, int B, bool train, hipS
 void film_mlp_bwd(const FilmLayer& L, const float* camn, int B, hipStream_t st);
 // a1 = gam[b,c] * relu(y*scale[c] + shift[c]) + bet[b,c]   (NHWC [B*HW][C])
 void film_apply(const float* y, int C, const float* scale, const float* shift, const float* gam, const float* bet,
-                int B, int64_t HW, float* out, hipStream_t st);
+                int B, int64_t HW, float* out, hipStream_t st, bool y_bf16 = false);
 // dgam[b,c] = sum_hw dA * relu(y*scale+shift), dbet[b,c] = sum_hw dA
 void film_affine_bwd(const float* dA, const float* y, int C, const float* scale, const float* shift, int B, int64_t HW,
-                     double* scratch, float* dgam, float* dbet, hipStream_t st);
+                     double* scratch, float* dgam, float* dbet, hipStream_t st, bool y_bf16 = false);
 int64_t film_reduce_doubles(int B, int64_t HW, int C);
 
 }  // namespace cad

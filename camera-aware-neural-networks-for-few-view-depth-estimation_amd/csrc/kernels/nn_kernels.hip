@@ -12,6 +12,7 @@
 #include <stdexcept>
 
 #include "gemm_s3.hpp"   // split_np (pre-split twins written by the elementwise passes)
+#include "ew_load.hpp"
 #include "kernels.hpp"
 
 namespace cad {
@@ -87,6 +88,7 @@ struct OpSum {
         acc[0][0] += v.x; acc[0][1] += v.y; acc[0][2] += v.z; acc[0][3] += v.w;
     }
 };
+template <bool YB>
 struct OpBnBwd {
     const float *g, *y, *mean, *invstd, *scale, *shift, *gmul;
     int64_t ldg; int gcoff, C; int64_t HW; bool relu;
@@ -96,7 +98,7 @@ struct OpBnBwd {
             const float4 m = *reinterpret_cast<const float4*>(gmul + (r / HW) * C + c4 * 4);
             gv.x *= m.x; gv.y *= m.y; gv.z *= m.z; gv.w *= m.w;
         }
-        float4 yv = *reinterpret_cast<const float4*>(y + r * C + c4 * 4);
+        float4 yv = load4<YB>(y, r * C + c4 * 4);
         const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, ya[4] = {yv.x, yv.y, yv.z, yv.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -210,7 +212,7 @@ __device__ __forceinline__ void split4_store(char* os, int64_t ldos, int oscoff,
     for (int p = 0; p < NP; ++p) *reinterpret_cast<uint2*>(d + p * 16) = sp.p[p];
 }
 
-template <int NP>
+template <int NP, bool YB>
 __global__ void k_bn_relu_fwd(const float* __restrict__ y, int C, const float* __restrict__ scale,
                               const float* __restrict__ shift, float* __restrict__ out, int64_t ldo,
                               int ocoff, int64_t n4, char* __restrict__ os, int64_t ldos, int oscoff) {
@@ -218,7 +220,7 @@ __global__ void k_bn_relu_fwd(const float* __restrict__ y, int C, const float* _
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = i / C4;
         const int c = (int)(i - r * C4) * 4;
-        float4 v = *reinterpret_cast<const float4*>(y + i * 4);
+        float4 v = load4<YB>(y, i * 4);
         float4 s = *reinterpret_cast<const float4*>(scale + c);
         float4 t = *reinterpret_cast<const float4*>(shift + c);
         float4 o;
@@ -231,16 +233,16 @@ __global__ void k_bn_relu_fwd(const float* __restrict__ y, int C, const float* _
     }
 }
 void bn_relu_fwd(const float* y, int C, const float* scale, const float* shift, float* out, int64_t ldo,
-                 int ocoff, int64_t M, hipStream_t st, void* os, int64_t ldos, int oscoff) {
+                 int ocoff, int64_t M, hipStream_t st, void* os, int64_t ldos, int oscoff, bool y_bf16) {
     const int64_t n4 = M * C / 4;
     const int np = os ? split_planes() : 0;
     char* o = static_cast<char*>(os);
-    if (np == 1)
-        hipLaunchKernelGGL(k_bn_relu_fwd<1>, dim3(ew_blocks(n4)), dim3(256), 0, st, y, C, scale, shift, out, ldo, ocoff,
-                           n4, o, ldos, oscoff);
-    else
-        hipLaunchKernelGGL(k_bn_relu_fwd<0>, dim3(ew_blocks(n4)), dim3(256), 0, st, y, C, scale, shift, out, ldo, ocoff,
-                           n4, o, ldos, oscoff);
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(ew_blocks(n4)), dim3(256), 0, st, y, C, scale, shift, out, ldo, ocoff, n4, o, ldos,
+                           oscoff);
+    };
+    if (np == 1) y_bf16 ? go(k_bn_relu_fwd<1, true>) : go(k_bn_relu_fwd<1, false>);
+    else y_bf16 ? go(k_bn_relu_fwd<0, true>) : go(k_bn_relu_fwd<0, false>);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -258,7 +260,7 @@ __global__ void k_bn_bwd_coef(const double* tot, int C, int64_t M, const float* 
     coef[C + c] = (float)(k1 * sdz / (double)M);
     coef[2 * C + c] = (float)(k1 * sdzx / (double)M);
 }
-template <int NP>
+template <int NP, bool YB>
 __global__ void k_bn_relu_bwd(const float* __restrict__ g, int64_t ldg, int gcoff, const float* __restrict__ y,
                               int C, const float* __restrict__ mean, const float* __restrict__ invstd,
                               const float* __restrict__ scale, const float* __restrict__ shift,
@@ -273,7 +275,7 @@ __global__ void k_bn_relu_bwd(const float* __restrict__ g, int64_t ldg, int gcof
             const float4 m = *reinterpret_cast<const float4*>(gmul + (r / HW) * C + c0);
             gv.x *= m.x; gv.y *= m.y; gv.z *= m.z; gv.w *= m.w;
         }
-        float4 yv = *reinterpret_cast<const float4*>(y + i * 4);
+        float4 yv = load4<YB>(y, i * 4);
         const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, ya[4] = {yv.x, yv.y, yv.z, yv.w};
         float o[4];
 #pragma unroll
@@ -292,22 +294,24 @@ __global__ void k_bn_relu_bwd(const float* __restrict__ g, int64_t ldg, int gcof
 void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, const float* mean,
                  const float* invstd, const float* scale, const float* shift, const float* gamma,
                  int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
-                 hipStream_t st, const float* gmul, int64_t HW, void* dy_split, bool relu) {
+                 hipStream_t st, const float* gmul, int64_t HW, void* dy_split, bool relu, bool y_bf16) {
     double* tot = scratch;
     double* part = scratch + 2 * C;
-    OpBnBwd op{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW, relu};
-    const int S = launch_colreduce<2>(op, M, C, part, st);
+    const int S = y_bf16 ? launch_colreduce<2>(OpBnBwd<true>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW, relu},
+                                               M, C, part, st)
+                         : launch_colreduce<2>(OpBnBwd<false>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW, relu},
+                                               M, C, part, st);
     launch_colfinal(part, S, 2 * C, tot, nullptr, 1.f, st);
     hipLaunchKernelGGL(k_bn_bwd_coef, dim3(cdiv(C, 64)), dim3(64), 0, st, tot, C, M, gamma, invstd, coef, dgamma, dbeta);
     const int64_t n4 = M * C / 4;
     const int np = dy_split ? split_planes() : 0;
     char* os = static_cast<char*>(dy_split);
-    if (np == 1)
-        hipLaunchKernelGGL(k_bn_relu_bwd<1>, dim3(ew_blocks(n4)), dim3(256), 0, st, g, ldg, gcoff, y, C, mean, invstd,
-                           scale, shift, coef, dy, n4, gmul, HW, os, relu);
-    else
-        hipLaunchKernelGGL(k_bn_relu_bwd<0>, dim3(ew_blocks(n4)), dim3(256), 0, st, g, ldg, gcoff, y, C, mean, invstd,
-                           scale, shift, coef, dy, n4, gmul, HW, os, relu);
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(ew_blocks(n4)), dim3(256), 0, st, g, ldg, gcoff, y, C, mean, invstd, scale, shift,
+                           coef, dy, n4, gmul, HW, os, relu);
+    };
+    if (np == 1) y_bf16 ? go(k_bn_relu_bwd<1, true>) : go(k_bn_relu_bwd<1, false>);
+    else y_bf16 ? go(k_bn_relu_bwd<0, true>) : go(k_bn_relu_bwd<0, false>);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -12,6 +12,7 @@
 #include <stdexcept>
 
 #include "gemm_s3.hpp"   // split1 (fp32 -> bf16 round-to-nearest-even)
+#include "ew_load.hpp"
 #include "kernels.hpp"
 
 namespace cad {
@@ -228,6 +229,7 @@ void maxpool3s2_bwd(const float* dout, const uint8_t* idx, int C, int B, int H, 
 // bottleneck join: out = relu(y*s + t + r), r = yd*sd + td (projection shortcut) or x (identity,
 // row stride ldx); out fp32 dense [M][C] and its bf16 twin
 // ------------------------------------------------------------------------------------------
+template <bool YB>
 __global__ void k_bn_add_relu(const float* __restrict__ y, const float* __restrict__ s, const float* __restrict__ t,
                               const float* __restrict__ yd, const float* __restrict__ sd, const float* __restrict__ td,
                               const float* __restrict__ x, int64_t ldx, int C, float* __restrict__ out,
@@ -236,11 +238,11 @@ __global__ void k_bn_add_relu(const float* __restrict__ y, const float* __restri
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = i / C4;
         const int c = (int)(i - r * C4) * 4;
-        const float4 v = *reinterpret_cast<const float4*>(y + i * 4);
+        const float4 v = load4<YB>(y, i * 4);
         const float4 a = *reinterpret_cast<const float4*>(s + c), b = *reinterpret_cast<const float4*>(t + c);
         float4 q;
         if (yd) {
-            const float4 w = *reinterpret_cast<const float4*>(yd + i * 4);
+            const float4 w = load4<YB>(yd, i * 4);
             const float4 e = *reinterpret_cast<const float4*>(sd + c), f = *reinterpret_cast<const float4*>(td + c);
             q = make_float4(w.x * e.x + f.x, w.y * e.y + f.y, w.z * e.z + f.z, w.w * e.w + f.w);
         } else {
@@ -254,10 +256,14 @@ __global__ void k_bn_add_relu(const float* __restrict__ y, const float* __restri
 }
 void bn_add_relu(const float* y, const float* scale, const float* shift, const float* yd, const float* dscale,
                  const float* dshift, const float* x, int64_t ldx, int C, int64_t M, float* out, void* out_split,
-                 hipStream_t st) {
+                 hipStream_t st, bool y_bf16) {
     const int64_t n4 = M * C / 4;
-    hipLaunchKernelGGL(k_bn_add_relu, dim3(ew_blocks(n4)), dim3(256), 0, st, y, scale, shift, yd, dscale, dshift, x,
-                       ldx, C, out, (uint16_t*)out_split, n4);
+    if (y_bf16)
+        hipLaunchKernelGGL(k_bn_add_relu<true>, dim3(ew_blocks(n4)), dim3(256), 0, st, y, scale, shift, yd, dscale, dshift,
+                           x, ldx, C, out, (uint16_t*)out_split, n4);
+    else
+        hipLaunchKernelGGL(k_bn_add_relu<false>, dim3(ew_blocks(n4)), dim3(256), 0, st, y, scale, shift, yd, dscale, dshift,
+                           x, ldx, C, out, (uint16_t*)out_split, n4);
 }
 // gs = g * [out > 0]  (g rows ldg at channel offset gcoff; out and gs dense [M][C])
 __global__ void k_relu_mask(const float* __restrict__ g, int64_t ldg, int gcoff, const float* __restrict__ out, int C,

@@ -9,8 +9,9 @@ F.conv_transpose2d — the same functions torchvision's ResNet-50 and the refere
 blocks are made of, baseline_unet.h:83-102), parameter names and shapes are torchvision's, and the
 loss / clip / Adam are the U-Net oracle's (cad_oracle.py, pinned to the reference's fixtures).
 
-operands="bf16" rounds every contraction operand to bf16 (forward x and w, dgrad dy, wgrad dy) as the
-GPU path does (cad_oracle._GEMM); "exact" is plain fp32 (or fp64 with dtype=float64).
+operands="bf16" rounds every contraction operand to bf16 (forward x and w, dgrad dy, wgrad dy) and the
+stored pre-BN conv outputs, as the GPU path does (cad_oracle._GEMM); "exact" is plain fp32 (or fp64
+with dtype=float64).
 """
 from __future__ import annotations
 
@@ -87,7 +88,8 @@ def _rnd(x):
 
 def _conv(x, w, stride, pad):
     y = F.conv2d(_rnd(x), _rnd(w), None, stride, pad)
-    return O._RoundGradOperand.apply(y) if O._GEMM["operands"] == "bf16" else y
+    # bf16: the dy operand of dgrad / wgrad rounded, and the pre-BN output stored as bf16
+    return O._RoundOperand.apply(O._RoundGradOperand.apply(y)) if O._GEMM["operands"] == "bf16" else y
 
 
 def _bottleneck(x, p, bufs, pre, stride, down, train):
