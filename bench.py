@@ -18,7 +18,7 @@ region, timed live with HIP events on its launch stream) against its engine's MF
 cpu_baseline: the oracle restatement (LibTorch CPU, the reference's ATen kernels) on a bounded
 sample of the workload on this host's cores; parity: the same sampled steps on the GPU compared live
 with it (prediction, losses, eval-mode abs_rel).  bf16_workloads: bounded runs of the other BASELINE
-workloads (configs[2], configs[3]'s per-GPU step) in the same process.
+workloads (configs[2], configs[3]'s and configs[4]'s per-GPU steps) in the same process.
 """
 import argparse
 import ctypes as C
