@@ -568,10 +568,9 @@ void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth
         const void* upins = l == 3 ? h->botts : h->douts[l + 1];
         const Up& u = h->up[l];
         const int C = h->Cl(l);
-        if (ps) {
-            cad::convT_fwd_ps(sv(upins, u.cin), u.cin, sv(u.wfs, u.cin), h->P(u.bidx), u.cout, h->cat[l], 2 * C, C, B,
-                              h->Hl(l + 1), h->Wl(l + 1), st);
-            cad::split_rows(h->cat[l], 2 * C, C, C, h->Ml(l, B), h->cats[l], 2 * C, C, st);
+        if (ps) {   // the up half goes straight into the concat twin (its fp32 copy has no reader)
+            cad::convT_fwd_ps(sv(upins, u.cin), u.cin, sv(u.wfs, u.cin), h->P(u.bidx), u.cout,
+                              static_cast<float*>(h->cats[l]), 2 * C, C, B, h->Hl(l + 1), h->Wl(l + 1), st, true);
         } else {
             cad::convT_fwd(upin, u.cin, u.cin, u.wf, h->P(u.bidx), u.cout, h->cat[l], 2 * C, C, B, h->Hl(l + 1),
                            h->Wl(l + 1), st);
@@ -1015,6 +1014,7 @@ int64_t cad_unet_debug_buffer(cad_unet* h, const char* name, float* host, int64_
     if (h->fwd_np > 0) {
         const bool film = h->model != CAD_MODEL_BASELINE;
         const bool twin_only = n == "Sb" || n == "bott" || (n.compare(0, 4, "pool") == 0) ||
+                               (n.compare(0, 3, "cat") == 0) ||   // up half: twin only
                                (n.compare(0, 4, "dout") == 0 && n != "dout0") ||
                                (!film && n.size() > 5 && n.substr(5) == "a1") ||
                                (n.size() > 5 && (n.substr(5) == "y1" || n.substr(5) == "y2"));   // bf16 values

@@ -140,7 +140,6 @@ struct Bott {
 struct Dec {
     int up_w = -1, up_b = -1, cin_up = 0, cout_up = 0, skipC = 0, C = 0, H = 0, W = 0;   // output geometry
     Unit u1, u2;
-    float* upf = nullptr;      // ConvT output [M][cout_up]
     void* cats = nullptr;      // twin [M][skipC + cout_up]
     void* a1s = nullptr;
     float* out = nullptr;
@@ -351,7 +350,6 @@ void layout(cad_resunet* h, Arena& a) {
     for (Dec& d : h->dec) {
         const int64_t Md = h->M(B, d.H, d.W);
         const int cc = d.skipC + d.cout_up;
-        d.upf = a.f(Md * d.cout_up);
         d.cats = a.tw(Md * cc);
         d.wf = a.f((int64_t)4 * d.cout_up * d.cin_up);
         d.wfs = a.tw((int64_t)4 * d.cout_up * d.cin_up);
@@ -567,9 +565,8 @@ void forward(cad_resunet* h, const float* rgb, float* depth, int B, hipStream_t 
         Dec& d = h->dec[j];
         const int cc = d.skipC + d.cout_up;
         const int64_t Md = h->M(B, d.H, d.W);
-        cad::convT_fwd_ps(tw(prev, d.cin_up), d.cin_up, tw(d.wfs, d.cin_up), h->P(d.up_b), d.cout_up, d.upf, d.cout_up, 0, B,
-                          d.H / 2, d.W / 2, st);
-        cad::split_rows(d.upf, d.cout_up, 0, d.cout_up, Md, d.cats, cc, d.skipC, st);
+        cad::convT_fwd_ps(tw(prev, d.cin_up), d.cin_up, tw(d.wfs, d.cin_up), h->P(d.up_b), d.cout_up,
+                          static_cast<float*>(d.cats), cc, d.skipC, B, d.H / 2, d.W / 2, st, true);
         if (d.skipC) cad::copy_twin(tw(skips[j], d.skipC), d.skipC, B, d.H, d.W, 1, d.cats, cc, 0, st);
         unit_fwd(h, d.u1, tw(d.cats, cc), B, d.H, d.W, nullptr, nullptr, st);
         cad::bn_relu_fwd(d.u1.y, d.C, d.u1.b.scale, d.u1.b.shift, nullptr, d.C, 0, Md, st, d.a1s, d.C, 0, true);
@@ -605,8 +602,10 @@ void prep_weights_bwd(cad_resunet* h, hipStream_t st) {
 
 // BN (+ReLU) backward of unit u: g (ld ldg, coff) -> dYs twin; then the conv's wgrad from the
 // input twin `in` (or its col / subsample) and, if dx, its dgrad into dx (ld lddx, overwritten)
+// add: a matrix added to the 1x1 stride-1 dgrad output (the identity shortcut's gradient)
 void unit_bwd(cad_resunet* h, Unit& u, const float* g, int64_t ldg, int gcoff, bool relu, cad::Split in, int B,
-              int Hin, int Win, const void* col, const void* xs, float* dx, int64_t lddx, hipStream_t st) {
+              int Hin, int Win, const void* col, const void* xs, float* dx, int64_t lddx, hipStream_t st,
+              const float* add = nullptr) {
     RConv& c = u.c;
     const int Ho = (Hin + 2 * c.p - c.k) / c.s + 1, Wo = (Win + 2 * c.p - c.k) / c.s + 1;
     const int64_t Mo = h->M(B, Ho, Wo);
@@ -625,7 +624,7 @@ void unit_bwd(cad_resunet* h, Unit& u, const float* g, int64_t ldg, int gcoff, b
     cad::dense_wgrad_ps(dz, c.cout, a, c.Kp, h->G(c.pidx), c.Kp, Mo, h->slab, h->slab_cap, st);
     if (!dx) return;
     if (c.k == 1 && c.s == 1) {
-        cad::dense_fwd_ps(dz, c.cout, tw(c.wts, c.cout), c.cin, dx, lddx, 0, Mo, nullptr, st);
+        cad::dense_fwd_ps(dz, c.cout, tw(c.wts, c.cout), c.cin, dx, lddx, 0, Mo, nullptr, st, false, add);
     } else if (c.k == 1) {   // stride-2 1x1: dgrad on the subsampled grid, scattered by the caller
         cad::dense_fwd_ps(dz, c.cout, tw(c.wts, c.cout), c.cin, dx, c.cin, 0, Mo, nullptr, st);
     } else {
@@ -679,12 +678,12 @@ void backward(cad_resunet* h, const float* ddepth, hipStream_t st) {
         float* gn = g == h->gA ? h->gB : h->gA;   // gradient of the block input
         unit_bwd(h, b.u3, h->gS, b.cout, 0, false, tw(b.t2s, b.w), B, b.Ho, b.Wo, nullptr, nullptr, h->dT, b.w, st);
         unit_bwd(h, b.u2, h->dT, b.w, 0, true, tw(b.t1s, b.w), B, b.H, b.W, b.col2, nullptr, h->dT, b.w, st);
-        unit_bwd(h, b.u1, h->dT, b.w, 0, true, tw(xsw, b.cin), B, b.H, b.W, nullptr, nullptr, gn, b.cin, st);
+        // identity shortcut: its gradient gS is added inside conv1's dgrad epilogue
+        unit_bwd(h, b.u1, h->dT, b.w, 0, true, tw(xsw, b.cin), B, b.H, b.W, nullptr, nullptr, gn, b.cin, st,
+                 b.down ? nullptr : h->gS);
         if (b.down) {
             unit_bwd(h, b.ud, h->gS, b.cout, 0, false, tw(xsw, b.cin), B, b.H, b.W, nullptr, b.xs, h->dT, b.cin, st);
             cad::add_strided(gn, b.cin, h->dT, b.cin, 0, b.cin, B, b.H, b.W, b.s, st);
-        } else {
-            cad::add_strided(gn, b.cin, h->gS, b.cout, 0, b.cin, B, b.H, b.W, 1, st);
         }
         g = gn;
     }

@@ -20,6 +20,7 @@ namespace cad {
 struct EpiStore {
     static constexpr bool STATS = false;
     static constexpr bool BF16 = false;
+    static constexpr bool ADD = false;
     __device__ static const float* row_base(const GemmArgs& a, int m0, int) {
         return a.C + (int64_t)m0 * a.ldc + a.c_coff;
     }
@@ -27,11 +28,21 @@ struct EpiStore {
 struct EpiStoreStats : EpiStore {
     static constexpr bool STATS = true;
 };
+// C[m][n] = acc + R[m][n], R = a.bias read as a matrix with C's row stride and channel offset (the
+// config-5 bottleneck's identity shortcut gradient added in the dgrad that produces the block-input
+// gradient: no separate add pass)
+struct EpiStoreAdd : EpiStore {
+    static constexpr bool ADD = true;
+    __device__ static const float* add_base(const GemmArgs& a, int m0) {
+        return a.bias + (int64_t)m0 * a.ldc + a.c_coff;
+    }
+};
 // bf16 outputs (round-to-nearest-even; a.C addresses bf16 rows of ldc elements): the pre-BN conv
 // outputs of the bf16 engine.  BN partials are taken from the rounded values BN normalises.
 struct EpiStoreB16 {
     static constexpr bool STATS = false;
     static constexpr bool BF16 = true;
+    static constexpr bool ADD = false;
     __device__ static const float* row_base(const GemmArgs& a, int m0, int) {
         return reinterpret_cast<const float*>(reinterpret_cast<const char*>(a.C) + ((int64_t)m0 * a.ldc + a.c_coff) * 2);
     }
@@ -45,6 +56,7 @@ struct EpiStoreStatsB16 : EpiStoreB16 {
 struct EpiConvT {
     static constexpr bool STATS = false;
     static constexpr bool BF16 = false;
+    static constexpr bool ADD = false;
     static constexpr bool STRUCTURED = true;
     __device__ void operator()(const GemmArgs& a, int m, int n, float v, int) const {
         const int cout = a.N >> 2;
@@ -76,9 +88,40 @@ struct EpiConvT {
         }
     }
 };
+// EpiConvT writing bf16 (a.C addresses bf16 rows of ldc elements): the bf16 engine's up half of
+// the decoder concat, written straight into the consumers' twin
+struct EpiConvTB16 {
+    static constexpr bool STATS = false;
+    static constexpr bool BF16 = false;   // (row-major store path unused: structured)
+    static constexpr bool ADD = false;
+    static constexpr bool STRUCTURED = true;
+    __device__ void operator()(const GemmArgs&, int, int, float, int) const {}
+    __device__ void block(const GemmArgs& a, int mbase, int n, const floatx16& acc) const {
+        if (n >= a.N) return;
+        const int cout = a.N >> 2;
+        const int q = n / cout, co = n - q * cout;
+        const float bias = a.bias[co];
+        uint16_t* dst = reinterpret_cast<uint16_t*>(const_cast<float*>(a.C)) + a.c_coff + co;
+        const int64_t W2 = 2 * a.W;
+        int x = mbase % a.W, t = mbase / a.W, y = t % a.H, b = t / a.H;
+        int cur = 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int off = (r & 3) + 8 * (r >> 2);
+            x += off - cur;
+            cur = off;
+            while (x >= a.W) { x -= a.W; if (++y == a.H) { y = 0; ++b; } }
+            if (mbase + off < a.M) {
+                const int64_t hp = ((int64_t)b * (2 * a.H) + 2 * y + (q >> 1)) * W2 + 2 * x + (q & 1);
+                dst[hp * a.ldc] = __builtin_bit_cast(uint16_t, (__bf16)(acc[r] + bias));
+            }
+        }
+    }
+};
 struct EpiSlab {   // split-K partial: slab z holds C[m][n] of K-slice z
     static constexpr bool STATS = false;
     static constexpr bool BF16 = false;
+    static constexpr bool ADD = false;
     __device__ static const float* row_base(const GemmArgs& a, int m0, int z) {
         return a.C + (int64_t)z * a.slab_stride + (int64_t)m0 * a.ldc;
     }
@@ -230,13 +273,13 @@ __device__ __forceinline__ void conv3x3_fwd_psb(const GemmArgs& a) {
         [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb, a.cimajor, a.a_cin); },
         Epi{});
 }
-template <int NP, int WM, int WN, int MI, int NJ, int KB>
+template <int NP, int WM, int WN, int MI, int NJ, int KB, class Epi = EpiConvT>
 __device__ __forceinline__ void convT_fwd_psb(const GemmArgs& a) {
     using LA = PsKcDense<32 * MI * WM, KB, NP>;
     using LB = PsKcDense<32 * NJ * WN, KB, NP>;
     gemm_body_ps<NP, WM, WN, MI, NJ, KB, LA, LB>(
         a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t, kb); },
-        [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, EpiConvT{});
+        [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, Epi{});
 }
 template <int NP, int WM, int WN, int MI, int NJ, int KB>
 __device__ __forceinline__ void convT_dgrad_psb(const GemmArgs& a) {
@@ -290,6 +333,10 @@ template <int WM, int WN, int KB, class Epi>
 __global__ __launch_bounds__(256) void k_conv3x3_fwd_bf16p(GemmArgs a) { conv3x3_fwd_psb<1, WM, WN, 2, 2, KB, Epi>(a); }
 template <int WM, int WN, int KB>
 __global__ __launch_bounds__(256) void k_convT_fwd_bf16p(GemmArgs a) { convT_fwd_psb<1, WM, WN, 2, 2, KB>(a); }
+template <int WM, int WN, int KB>
+__global__ __launch_bounds__(256) void k_convT_fwd_bf16pt(GemmArgs a) {
+    convT_fwd_psb<1, WM, WN, 2, 2, KB, EpiConvTB16>(a);
+}
 template <int WM, int WN, int KB>
 __global__ __launch_bounds__(256) void k_convT_dgrad_bf16p(GemmArgs a) { convT_dgrad_psb<1, WM, WN, 2, 2, KB>(a); }
 template <int WM, int WN, int KB>
@@ -436,6 +483,8 @@ CAD_KT(KConvFwdP1B, (k_conv3x3_fwd_bf16p<WM, WN, KB, EpiStoreB16>),
 CAD_KT(KConvFwdSP1B, (k_conv3x3_fwd_bf16p<WM, WN, KB, EpiStoreStatsB16>),
        "void cad::k_conv3x3_fwd_bf16p<%d, %d, %d, cad::EpiStoreStatsB16>(cad::GemmArgs)")
 CAD_KT(KDenseWgradP1, (k_dense_wgrad_bf16p<WM, WN, KB>), "void cad::k_dense_wgrad_bf16p<%d, %d, %d>(cad::GemmArgs)")
+CAD_KT(KConvTFwdP1T, (k_convT_fwd_bf16pt<WM, WN, KB>), "void cad::k_convT_fwd_bf16pt<%d, %d, %d>(cad::GemmArgs)")
+CAD_KT(KDenseAddP1, (k_dense_bf16p<WM, WN, KB, EpiStoreAdd>), "void cad::k_dense_bf16p<%d, %d, %d, cad::EpiStoreAdd>(cad::GemmArgs)")
 // in-loader split engines: KConvFwd3 ... (S3), KConvFwdB ... (B1); pre-split B1: KConvFwdP1 ...
 CAD_NP_KT(s3, 3)
 CAD_NP_KT(bf16, B)
@@ -828,7 +877,7 @@ void conv3x3_wgrad_ps(Split dz, int cout, Split x, int cin, float* dw, int B, in
 int dense_stats_rows(int64_t M, int N) { return cdiv(M, tile_m(pick_cfg((int)M, N))); }
 
 void dense_fwd_ps(Split x, int K, Split w, int N, float* y, int64_t ldy, int ycoff, int64_t M, float* stats,
-                  hipStream_t st, bool y_bf16) {
+                  hipStream_t st, bool y_bf16, const float* add) {
     ps_check(x, K, "dense x");
     ps_check(w, K, "dense w");
     if (M > INT32_MAX) throw std::runtime_error("dense GEMM: too many rows");
@@ -839,10 +888,14 @@ void dense_fwd_ps(Split x, int K, Split w, int N, float* y, int64_t ldy, int yco
     a.Bm = (const float*)w.p; a.ldb = w.ld; a.b_coff = w.coff;
     a.C = y; a.ldc = ldy; a.c_coff = ycoff;
     a.stats = stats;
+    a.bias = add;
     const Cfg c = pick_cfg(a.M, a.N);
     const int kb = ps_kb(true, c);
     a.kstages_per_split = cdiv(a.K, kb);
-    if (y_bf16) {
+    if (add) {
+        if (stats || y_bf16) throw std::runtime_error("dense GEMM: the added matrix needs fp32 output");
+        launch_kb<KDenseAddP1, 32, 64>(c, kb, a, 1, st);
+    } else if (y_bf16) {
         if (stats) launch_kb<KDenseSP1B, 32, 64>(c, kb, a, 1, st);
         else launch_kb<KDenseP1B, 32, 64>(c, kb, a, 1, st);
     } else {
@@ -875,7 +928,7 @@ void dense_wgrad_ps(Split dz, int N, Split x, int K, float* dw, int64_t ldw, int
 }
 
 void convT_fwd_ps(Split x, int cin, Split wf, const float* bias, int cout, float* y, int64_t ldy, int ycoff, int B,
-                  int H, int W, hipStream_t st) {
+                  int H, int W, hipStream_t st, bool y_bf16) {
     ps_check(x, cin, "convT_fwd x");
     ps_check(wf, cin, "convT_fwd w");
     GemmArgs a{};
@@ -887,7 +940,8 @@ void convT_fwd_ps(Split x, int cin, Split wf, const float* bias, int cout, float
     const Cfg c = pick_cfg(a.M, a.N);
     const int kb = ps_kb(false, c);
     a.kstages_per_split = cdiv(a.K, kb);
-    launch_kb<KConvTFwdP1, 32>(c, kb, a, 1, st);
+    if (y_bf16) launch_kb<KConvTFwdP1T, 32>(c, kb, a, 1, st);
+    else launch_kb<KConvTFwdP1, 32>(c, kb, a, 1, st);
 }
 
 void convT_dgrad_ps(Split g, int cout, Split wm, int cin, float* dx, int B, int H, int W, hipStream_t st) {

@@ -479,6 +479,11 @@ __device__ __forceinline__ void gemm_epilogue_t(const GemmArgs& a, const floatx1
     const int64_t bytes = (int64_t)(a.M - m0) * ldc4;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(epi_row_base<Epi>(a, m0, tile.z),
                                                 (uint32_t)(bytes < (int64_t)kRecords ? bytes : kRecords));
+    auto add_rsrc = [&]() {
+        if constexpr (Epi::ADD) return make_rsrc(Epi::add_base(a, m0), (uint32_t)(bytes < (int64_t)kRecords ? bytes : kRecords));
+        else return rs;
+    };
+    const __amdgpu_buffer_rsrc_t rsadd = add_rsrc();
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -496,6 +501,13 @@ __device__ __forceinline__ void gemm_epilogue_t(const GemmArgs& a, const floatx1
                 float v[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[r] = acc[i][j][4 * g + r];
+                if constexpr (Epi::ADD) {
+                    const uint32_t lo = n < a.N ? (uint32_t)(mr * ldc4 + (int64_t)n * ES) : kOOB;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        v[r] += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                              rsadd, lo + (uint32_t)(r * ldc4), 0, 0));
+                }
                 if constexpr (Epi::BF16) {   // the stored (rounded) values, which BN then normalises
 #pragma unroll
                     for (int r = 0; r < 4; ++r) v[r] = (float)(__bf16)v[r];

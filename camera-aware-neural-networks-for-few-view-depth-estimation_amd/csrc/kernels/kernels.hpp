@@ -59,16 +59,18 @@ void conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t 
                       hipStream_t st);
 void conv3x3_wgrad_ps(Split dz, int cout, Split x, int cin, float* dw, int B, int H, int W, float* slab,
                       int64_t slab_cap, hipStream_t st);
+// y_bf16: y is a bf16 twin (rows of ldy elements) — the up half of the decoder concat twin
 void convT_fwd_ps(Split x, int cin, Split wf, const float* bias, int cout, float* y, int64_t ldy, int ycoff, int B,
-                  int H, int W, hipStream_t st);
+                  int H, int W, hipStream_t st, bool y_bf16 = false);
 void convT_dgrad_ps(Split g, int cout, Split wm, int cin, float* dx, int B, int H, int W, hipStream_t st);
 void convT_wgrad_ps(Split x, int cin, Split g, int cout, float* dw, int B, int H, int W, float* slab,
                     int64_t slab_cap, hipStream_t st);
 
 // ---- dense GEMMs on the pre-split twins (the 1x1 / im2col convolutions of the config-5 network) ----
 // y[m][ycoff + n] = sum_k x[m][k] w[n][k]  (+ BN partials [rows][2][N] when stats != nullptr)
+// add != nullptr: y = x w^T + add (add rows with y's stride and offset; fp32 output, no stats)
 void dense_fwd_ps(Split x, int K, Split w, int N, float* y, int64_t ldy, int ycoff, int64_t M, float* stats,
-                  hipStream_t st, bool y_bf16 = false);
+                  hipStream_t st, bool y_bf16 = false, const float* add = nullptr);
 int dense_stats_rows(int64_t M, int N);
 // dw[n][k] = sum_m dz[m][n] x[m][k]  (reduction over the M pixels; split-K slabs)
 void dense_wgrad_ps(Split dz, int N, Split x, int K, float* dw, int64_t ldw, int64_t M, float* slab, int64_t slab_cap,
