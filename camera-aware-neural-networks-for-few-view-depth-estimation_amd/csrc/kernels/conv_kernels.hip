@@ -244,6 +244,12 @@ template <int R, int CW, class Epi>
 __global__ __launch_bounds__(256, 3) void k_conv3x3_win_bf16p(GemmArgs a) {
     conv3x3_win_ps_body<R, CW, R * CW == 128 ? 2 : 4, R * CW == 128 ? 2 : 1, Epi>(a);
 }
+// ... with 4 x 2 blocks of 32 x 32 per wave: 256 x 128 tiles (N % 128 == 0; BN64 = false) or
+// 512 x 64 tiles (N == 64)
+template <int R, int CW, class Epi, bool BN64 = false>
+__global__ __launch_bounds__(256, 2) void k_conv3x3_win_bf16p4(GemmArgs a) {
+    conv3x3_win_ps_body<R, CW, BN64 ? 4 : 2, BN64 ? 1 : 2, Epi, 4>(a);
+}
 
 // window-tiled conv3x3 weight gradient (gemm_win.hpp): 64 co x 64 ci x 9 taps per workgroup, split-K
 __global__ __launch_bounds__(256, 2) void k_conv3x3_wgrad_win_s3(GemmArgs a) { conv3x3_wgrad_win_body<3>(a); }
@@ -513,7 +519,8 @@ void launch_engine(Cfg c, bool fwd_kind, GemmArgs& a, hipStream_t st) {
 // the im2col kernel serves it (channels not a multiple of 16: enc1.conv1; no CW dividing W)
 struct WinPick {
     int R = 0, CW = 0;
-    int bn() const { return R * CW == 128 ? 128 : 64; }
+    bool big = false;   // B1 4 x 2 blocks per wave (k_conv3x3_win_bf16p4): 256 x 128, or 512 x 64 tiles
+    int bn() const { return big ? (R * CW == 256 ? 128 : 64) : R * CW == 128 ? 128 : 64; }
 };
 WinPick pick_win(int cin, int W, int N) {
     WinPick w;
@@ -534,14 +541,18 @@ WinPick pick_win(int cin, int W, int N) {
 int win_blocks(const WinPick& w, int B, int H, int W) { return B * cdiv(H, w.R) * (W / w.CW); }
 
 // PS = false: S3 window kernel (fp32 operands, in-loader split); true: B1 on the pre-split twins
-template <bool PS, int R, int CW, class Epi>
+template <bool PS, int R, int CW, class Epi, bool BIG = false>
 void launch_win1(const GemmArgs& a, hipStream_t st) {
-    const dim3 grid(win_blocks(WinPick{R, CW}, a.B, a.H, a.W), cdiv(a.N, R * CW == 128 ? 128 : 64));
-    auto fn = PS ? (void (*)(GemmArgs))k_conv3x3_win_bf16p<R, CW, Epi> : (void (*)(GemmArgs))k_conv3x3_win_s3<R, CW, Epi>;
+    constexpr int BN = BIG ? (R * CW == 256 ? 128 : 64) : R * CW == 128 ? 128 : 64;
+    const dim3 grid(win_blocks(WinPick{R, CW}, a.B, a.H, a.W), cdiv(a.N, BN));
+    void (*fn)(GemmArgs);
+    if constexpr (BIG) fn = k_conv3x3_win_bf16p4<R, CW, Epi, BN == 64>;
+    else fn = PS ? (void (*)(GemmArgs))k_conv3x3_win_bf16p<R, CW, Epi> : (void (*)(GemmArgs))k_conv3x3_win_s3<R, CW, Epi>;
     if (prof_enabled()) {
         char name[160];
-        snprintf(name, sizeof(name), "void cad::k_conv3x3_win_%s<%d, %d, cad::%s%s>(cad::GemmArgs)", PS ? "bf16p" : "s3",
-                 R, CW, Epi::STATS ? "EpiStoreStats" : "EpiStore", Epi::BF16 ? "B16" : "");
+        snprintf(name, sizeof(name), "void cad::k_conv3x3_win_%s<%d, %d, cad::%s%s>(cad::GemmArgs)",
+                 BIG ? "bf16p4" : PS ? "bf16p" : "s3", R, CW, Epi::STATS ? "EpiStoreStats" : "EpiStore",
+                 Epi::BF16 ? "B16" : "");
         prof_push(name, 2.0 * a.M * a.N * (double)a.K, st);
         hipLaunchKernelGGL(fn, grid, dim3(256), 0, st, a);
         prof_pop(st);
@@ -551,6 +562,25 @@ void launch_win1(const GemmArgs& a, hipStream_t st) {
 }
 template <class Epi, bool PS = false>
 void launch_win(const WinPick& w, const GemmArgs& a, hipStream_t st) {
+    if constexpr (PS) {
+        if (w.big && w.R * w.CW == 256) {
+            switch (w.CW) {
+                case 128: launch_win1<PS, 2, 128, Epi, true>(a, st); return;
+                case 64: launch_win1<PS, 4, 64, Epi, true>(a, st); return;
+                case 32: launch_win1<PS, 8, 32, Epi, true>(a, st); return;
+                case 16: launch_win1<PS, 16, 16, Epi, true>(a, st); return;
+                case 8: launch_win1<PS, 32, 8, Epi, true>(a, st); return;
+            }
+            throw std::runtime_error("window conv: block shape not built");
+        }
+        if (w.big) {   // 512 x 64
+            switch (w.CW) {
+                case 128: launch_win1<PS, 4, 128, Epi, true>(a, st); return;
+                case 64: launch_win1<PS, 8, 64, Epi, true>(a, st); return;
+            }
+            throw std::runtime_error("window conv: block shape not built");
+        }
+    }
     if (w.R * w.CW == 128) {
         switch (w.CW) {
             case 64: launch_win1<PS, 2, 64, Epi>(a, st); return;
@@ -570,6 +600,23 @@ void launch_win(const WinPick& w, const GemmArgs& a, hipStream_t st) {
 WinPick pick_win_ps(int cin, int W, int N, int acoff) {
     WinPick w;
     if (engine() != 2 || cin % 32 || acoff % 8) return w;
+    if (N % 128 == 0) {   // 256 x 128 tiles
+        static const int cb[] = {128, 64, 32, 16, 8};
+        for (int cw : cb)
+            if (W % cw == 0) {
+                w.CW = cw;
+                w.R = 256 / cw;
+                w.big = true;
+                return w;
+            }
+        return w;
+    }
+    if (N == 64 && (W % 128 == 0 || W % 64 == 0)) {   // 512 x 64 tiles
+        w.CW = W % 128 == 0 ? 128 : 64;
+        w.R = 512 / w.CW;
+        w.big = true;
+        return w;
+    }
     const int BM = N <= 64 ? 256 : 128;
     if (N % (BM == 128 ? 128 : 64)) return w;
     static const int c128[] = {64, 32, 16, 8}, c256[] = {128, 64};

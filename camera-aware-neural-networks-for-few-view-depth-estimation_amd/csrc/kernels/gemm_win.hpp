@@ -300,9 +300,11 @@ struct WinPsGeo {
     static constexpr int SA = WPIX * LDK, SBT = BN * LDK;  // bf16 elements: A image, one tap of B
 };
 
-template <int R, int CW, int WM, int WN, class Epi>
+// MI = 4: 128 x 64 per wave (256 x 128 tiles) — two fragment reads per three MFMAs instead of one per
+// MFMA: the 128 x 128 tile's LDS reads cap its MFMA rate near one half (B1 has one product per k step)
+template <int R, int CW, int WM, int WN, class Epi, int MI = 2>
 __device__ __forceinline__ void conv3x3_win_ps_body(const GemmArgs& a) {
-    constexpr int MI = 2, NJ = 2;
+    constexpr int NJ = 2;
     constexpr int BM = 32 * MI * WM, BN = 32 * NJ * WN;
     static_assert(BM == R * CW, "tile");
     using G = WinPsGeo<R, CW, BN>;
