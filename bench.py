@@ -275,7 +275,11 @@ def pmc_traffic(kernel_name):
     try:
         with open(path) as fh:
             d = json.load(fh)
-        return d.get(kernel_name, {}).get("hbm_bytes_per_launch")
+        # rocprofv3 prints a non-template kernel without its "void " return type
+        for k in (kernel_name, kernel_name[5:] if kernel_name.startswith("void ") else None):
+            if k and k in d:
+                return d[k].get("hbm_bytes_per_launch")
+        return None
     except Exception:
         return None
 
