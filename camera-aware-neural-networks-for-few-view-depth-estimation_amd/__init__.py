@@ -15,7 +15,7 @@ def __getattr__(name):
     # lazy: importing the package must not require torch / a GPU (CPU tests only check the ABI)
     if name in ("BaselineUNet", "IntrinsicsConditionedUNet", "RayConditionedUNet", "CombinedDepthLoss", "Adam",
                 "Trainer", "Communicator", "save", "load", "clip_grad_norm_", "depth_metrics", "ray_directions", "camera_from_K",
-                "ResNetUNet"):
+                "ResNetUNet", "GeometryAwareNetwork", "LightweightGeometryNetwork"):
         from . import model
         return getattr(model, name)
     if name in ("BatchAssembler", "AugSampler", "SunRGBDDataset", "PrefetchLoader"):

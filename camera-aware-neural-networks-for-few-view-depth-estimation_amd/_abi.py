@@ -31,6 +31,11 @@ class ResUnetDesc(C.Structure):
     _fields_ = [("in_channels", I), ("max_batch", I), ("height", I), ("width", I), ("max_depth", F)]
 
 
+class GeoNetDesc(C.Structure):
+    _fields_ = [("variant", I), ("in_channels", I), ("init_features", I), ("camera_dim", I), ("max_depth", F),
+                ("use_pcl", I), ("use_attention", I), ("max_batch", I), ("height", I), ("width", I)]
+
+
 class AdamOpts(C.Structure):
     _fields_ = [("lr", F), ("beta1", F), ("beta2", F), ("eps", F), ("weight_decay", F)]
 
@@ -71,6 +76,22 @@ SIGNATURES = {
     "cad_resunet_clip_grad_norm": (I, [P, F, F, P]),
     "cad_resunet_last_grad_norm": (I, [P, FP, P]),
     "cad_resunet_adam_step": (I, [P, F, F, F, F, F, P]),
+    "cad_geonet_create": (I, [C.POINTER(GeoNetDesc), I, C.POINTER(P)]),
+    "cad_geonet_destroy": (None, [P]),
+    "cad_geonet_count_parameters": (I64, [P]),
+    "cad_geonet_num_tensors": (I, [P, I]),
+    "cad_geonet_tensor_info": (I, [P, I, I, C.POINTER(C.c_char_p), C.POINTER(I), I64P]),
+    "cad_geonet_set_tensor": (I, [P, I, I, FP, I64]),
+    "cad_geonet_get_tensor": (I, [P, I, I, FP, I64]),
+    "cad_geonet_get_grad": (I, [P, I, FP, I64]),
+    "cad_geonet_train": (I, [P, I]),
+    "cad_geonet_flat": (I, [P, C.POINTER(P), C.POINTER(P), I64P]),
+    "cad_geonet_forward": (I, [P, P, P, P, P, I, P]),
+    "cad_geonet_backward": (I, [P, P, P]),
+    "cad_geonet_clip_grad_norm": (I, [P, F, F, P]),
+    "cad_geonet_last_grad_norm": (I, [P, FP, P]),
+    "cad_geonet_adam_step": (I, [P, F, F, F, F, F, P]),
+    "cad_geonet_num_batches_tracked": (I64, [P, I]),
     "cad_unet_create_model": (I, [C.POINTER(UnetDesc), I, I, C.POINTER(P)]),
     "cad_unet_model": (I, [P]),
     "cad_unet_forward_cam": (I, [P, P, P, P, I, P]),

@@ -213,4 +213,55 @@ void film_affine_bwd(const float* dA, const float* y, int C, const float* scale,
                      double* scratch, float* dgam, float* dbet, hipStream_t st, bool y_bf16 = false);
 int64_t film_reduce_doubles(int B, int64_t HW, int C);
 
+// ---------------- geometry-aware family (attn_kernels.hip) ----------------
+// GeometryAwareNetwork input: NHWC8 [r g b rx ry rz 0 0] from NCHW rgb and NCHW rays
+void pack_rgb_rays(const float* rgb, const float* rays, int B, int H, int W, float* out, hipStream_t st);
+// per-(sample, channel) mean over H*W of x[(b*HW + r)*ldx + xcoff + c] -> avg [B][C]; with mx != nullptr
+// also the max and its first-occurrence pixel index (amax, within the sample)
+int chan_pool_slices(int64_t HW);
+void chan_pool(const float* x, int64_t ldx, int xcoff, int C, int B, int64_t HW, double* part, float* avg, float* mx,
+               int* amax, hipStream_t st);
+int64_t attn_scratch_doubles(int B, int64_t HW, int C);   // scratch of cbam_* / pcl_* at one level
+
+// One CBAMImpl (spatial_attention.h:142-191): parameters, saved forward state, gradients, scratch.
+struct Cbam {
+    int C = 0, Cr = 0;   // Cr = max(1, C / 16)
+    const float *w1, *b1, *w2, *b2, *wsp;   // channel_attention.fc1 [Cr][C], fc2 [C][Cr]; spatial conv [2][7][7]
+    float *gw1, *gb1, *gw2, *gb2, *gwsp;
+    float *avg, *mx;          // [B][C] pooled vectors
+    int* amax;                // [B][C] argmax pixel of mx
+    float *ha, *hm;           // [B][Cr] relu(fc1(.)) of the avg / max branch
+    float* att;               // [B][C] channel attention
+    float* s;                 // [M][2] channel mean / max of x*att
+    int* sidx;                // [M] argmax channel
+    float* sa;                // [M] spatial attention
+    float *dlog, *ds;         // backward: [M] conv-logit grad, [M][2] grad of s
+    float *dO, *dha, *dhm, *dva, *dvm;   // [B][C], [B][Cr], [B][Cr], [B][C], [B][C]
+};
+// out (rows of ldo, channel offset ocoff) = CBAM(x), x dense [B*H*W][C]
+void cbam_fwd(const Cbam& A, const float* x, int B, int H, int W, float* out, int64_t ldo, int ocoff, double* scratch,
+              hipStream_t st);
+// dx (dense) = d CBAM / dx given g = grad of the output; writes the parameter gradients
+void cbam_bwd(const Cbam& A, const float* x, const float* g, int64_t ldg, int gcoff, int B, int H, int W, float* dx,
+              double* scratch, hipStream_t st);
+
+// One PerspectiveCorrectionLayerImpl (pcl_layer.h:29-181, hidden 128)
+constexpr int kPclHidden = 128;
+struct Pcl {
+    int C = 0;
+    const float *w1, *b1, *w2, *b2, *w3, *b3;   // loc_fc1 [128][C+4], loc_fc2 [128][128], fc_transform [6][128]
+    float *gw1, *gb1, *gw2, *gb2, *gw3, *gb3;
+    float* pooled;            // [B][C]
+    float *h1, *h2;           // [B][128]
+    float *tp, *theta;        // [B][6] transform parameters, affine matrix (row-major 2x3)
+    float* dgrid;             // [M][2]
+    float *dtp, *dh1, *dh2, *dpooled;   // [B][6], [B][128], [B][128], [B][C]
+};
+// out (rows of ldo, channel offset ocoff) = PCL(u, camn), u dense [B*H*W][C]
+void pcl_fwd(const Pcl& P, const float* u, const float* camn, int B, int H, int W, float* out, int64_t ldo, int ocoff,
+             double* scratch, hipStream_t st);
+// du (dense, overwritten) = d PCL / du given g = grad of the output; writes the parameter gradients
+void pcl_bwd(const Pcl& P, const float* u, const float* camn, const float* g, int64_t ldg, int gcoff, int B, int H,
+             int W, float* du, double* scratch, hipStream_t st);
+
 }  // namespace cad

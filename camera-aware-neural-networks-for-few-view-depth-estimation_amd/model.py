@@ -530,47 +530,55 @@ class ResNetUNet:
     ("dec4".."dec0", "out_conv").  train_step() = forward, CombinedDepthLoss, backward,
     clip_grad_norm_, Adam (moments owned by the model)."""
 
+    _PREFIX = "cad_resunet_"
+
+    def _f(self, name):
+        return getattr(self.lib, self._PREFIX + name)
+
     def __init__(self, in_channels=3, max_depth=10.0, *, batch, height, width, device=0):
         self.lib = _abi.load()
         self.device = torch.device("cuda", device)
         self.batch, self.height, self.width, self.max_depth = batch, height, width, max_depth
         desc = _abi.ResUnetDesc(in_channels, batch, height, width, max_depth)
         h = C.c_void_p()
-        check(self.lib.cad_resunet_create(C.byref(desc), device, C.byref(h)), "cad_resunet_create")
+        check(self._f("create")(C.byref(desc), device, C.byref(h)), "cad_resunet_create")
+        self._init_handle(h)
+
+    def _init_handle(self, h):
         self.h = h
-        self._param_info = [self._info(0, i) for i in range(self.lib.cad_resunet_num_tensors(h, 0))]
-        self._buffer_info = [self._info(1, i) for i in range(self.lib.cad_resunet_num_tensors(h, 1))]
+        self._param_info = [self._info(0, i) for i in range(self._f("num_tensors")(h, 0))]
+        self._buffer_info = [self._info(1, i) for i in range(self._f("num_tensors")(h, 1))]
         p, g, n = C.c_void_p(), C.c_void_p(), C.c_int64()
-        check(self.lib.cad_resunet_flat(h, C.byref(p), C.byref(g), C.byref(n)), "cad_resunet_flat")
+        check(self._f("flat")(h, C.byref(p), C.byref(g), C.byref(n)), "flat")
         self.n_flat = n.value
         self._flat_g = g.value
         self.training = True
 
     def _info(self, kind, idx):
         name, nd, shape = C.c_char_p(), C.c_int(), (C.c_int64 * 4)()
-        check(self.lib.cad_resunet_tensor_info(self.h, kind, idx, C.byref(name), C.byref(nd), shape), "tensor_info")
+        check(self._f("tensor_info")(self.h, kind, idx, C.byref(name), C.byref(nd), shape), "tensor_info")
         return name.value.decode(), tuple(shape[i] for i in range(nd.value))
 
     def __del__(self):
         h = getattr(self, "h", None)
         if h is not None and h.value:
-            self.lib.cad_resunet_destroy(h)
+            self._f("destroy")(h)
             self.h = None
 
     def train(self, mode=True):
         self.training = bool(mode)
-        check(self.lib.cad_resunet_train(self.h, int(mode)), "cad_resunet_train")
+        check(self._f("train")(self.h, int(mode)), "cad_resunet_train")
         return self
 
     def eval(self):
         return self.train(False)
 
     def count_parameters(self) -> int:
-        return int(self.lib.cad_resunet_count_parameters(self.h))
+        return int(self._f("count_parameters")(self.h))
 
     def _get(self, kind, idx, shape):
         out = np.empty(int(np.prod(shape)) if shape else 1, np.float32)
-        check(self.lib.cad_resunet_get_tensor(self.h, kind, idx, out.ctypes.data_as(_abi.FP), out.size), "get_tensor")
+        check(self._f("get_tensor")(self.h, kind, idx, out.ctypes.data_as(_abi.FP), out.size), "get_tensor")
         return torch.from_numpy(out.reshape(shape))
 
     def named_parameters(self):
@@ -598,14 +606,14 @@ class ResNetUNet:
                 continue
             v = np.ascontiguousarray(torch.as_tensor(state[n]).detach().cpu().float().numpy())
             assert tuple(v.shape) == tuple(s), f"{n}: shape {v.shape} != {s}"
-            check(self.lib.cad_resunet_set_tensor(self.h, kind, i, v.ctypes.data_as(_abi.FP), v.size), f"set {n}")
+            check(self._f("set_tensor")(self.h, kind, i, v.ctypes.data_as(_abi.FP), v.size), f"set {n}")
 
     def grads(self):
         torch.cuda.synchronize(self.device)
         out = OrderedDict()
         for i, (n, s) in enumerate(self._param_info):
             g = np.empty(int(np.prod(s)), np.float32)
-            check(self.lib.cad_resunet_get_grad(self.h, i, g.ctypes.data_as(_abi.FP), g.size), "get_grad")
+            check(self._f("get_grad")(self.h, i, g.ctypes.data_as(_abi.FP), g.size), "get_grad")
             out[n] = torch.from_numpy(g.reshape(s))
         return out
 
@@ -618,24 +626,24 @@ class ResNetUNet:
         assert Cc == 3 and H == self.height and W == self.width and B <= self.batch, "input shape mismatch"
         if out is None:
             out = torch.empty((B, 1, H, W), dtype=torch.float32, device=self.device)
-        check(self.lib.cad_resunet_forward(self.h, _ptr(x), _ptr(out), B, _stream(self.device)), "cad_resunet_forward")
+        check(self._f("forward")(self.h, _ptr(x), _ptr(out), B, _stream(self.device)), "cad_resunet_forward")
         return out
 
     __call__ = forward
 
     def backward(self, ddepth: torch.Tensor):
-        check(self.lib.cad_resunet_backward(self.h, _ptr(ddepth), _stream(self.device)), "cad_resunet_backward")
+        check(self._f("backward")(self.h, _ptr(ddepth), _stream(self.device)), "cad_resunet_backward")
 
     def clip_grad_norm_(self, max_norm: float, prescale: float = 1.0):
-        check(self.lib.cad_resunet_clip_grad_norm(self.h, float(max_norm), float(prescale), _stream(self.device)), "clip")
+        check(self._f("clip_grad_norm")(self.h, float(max_norm), float(prescale), _stream(self.device)), "clip")
 
     def last_grad_norm(self) -> float:
         v = C.c_float()
-        check(self.lib.cad_resunet_last_grad_norm(self.h, C.byref(v), _stream(self.device)), "last_grad_norm")
+        check(self._f("last_grad_norm")(self.h, C.byref(v), _stream(self.device)), "last_grad_norm")
         return float(v.value)
 
     def adam_step(self, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5):
-        check(self.lib.cad_resunet_adam_step(self.h, lr, betas[0], betas[1], eps, weight_decay, _stream(self.device)),
+        check(self._f("adam_step")(self.h, lr, betas[0], betas[1], eps, weight_decay, _stream(self.device)),
               "adam_step")
 
     def train_step(self, loss_fn: "CombinedDepthLoss", rgb, gt, K, lr=1e-4, weight_decay=1e-5, grad_clip=1.0,
@@ -654,6 +662,77 @@ class ResNetUNet:
         self.clip_grad_norm_(grad_clip if grad_clip else float("inf"), 1.0 / world)
         self.adam_step(lr=lr, weight_decay=weight_decay)
         return loss5, pred
+
+
+class GeometryAwareNetwork(ResNetUNet):
+    """GeometryAwareNetworkImpl(in_channels, init_features, camera_dim, max_depth, use_pcl, use_attention)
+    (src/models/geometry_aware_network.h:201-347) on MI355X (cad_geonet_*; geonet.cpp): RayEnhancedConv
+    encoder with CBAM, ConvTranspose + PerspectiveCorrectionLayer + CBAM decoder, six levels.
+    forward(rgb, ray_directions, camera_intrinsics (B,4)) as the reference; parameter / buffer names
+    are its named_parameters() / named_buffers().  Arithmetic: the process GEMM engine (default S3,
+    fp32-accurate).  train_step(): forward, CombinedDepthLoss, backward, clip_grad_norm_, Adam."""
+
+    _PREFIX = "cad_geonet_"
+    _VARIANT = 0
+
+    def __init__(self, in_channels=3, init_features=64, camera_dim=4, max_depth=10.0, use_pcl=True,
+                 use_attention=True, *, batch, height, width, device=0):
+        self.lib = _abi.load()
+        self.device = torch.device("cuda", device)
+        self.batch, self.height, self.width, self.max_depth = batch, height, width, max_depth
+        desc = _abi.GeoNetDesc(self._VARIANT, in_channels, init_features, camera_dim, max_depth, int(use_pcl),
+                               int(use_attention), batch, height, width)
+        h = C.c_void_p()
+        check(self._f("create")(C.byref(desc), device, C.byref(h)), "cad_geonet_create")
+        self._init_handle(h)
+
+    def forward(self, rgb, ray_directions, camera_intrinsics, out=None):
+        B, Cc, H, W = rgb.shape
+        assert Cc == 3 and H == self.height and W == self.width and B <= self.batch, "input shape mismatch"
+        assert tuple(ray_directions.shape) == (B, 3, H, W), "ray_directions must be (B, 3, H, W)"
+        assert tuple(camera_intrinsics.shape) == (B, 4), "camera_intrinsics must be (B, 4) [fx, fy, cx, cy]"
+        rgb, rays, cam = (t.contiguous().float() for t in (rgb, ray_directions, camera_intrinsics))
+        if out is None:
+            out = torch.empty((B, 1, H, W), dtype=torch.float32, device=self.device)
+        check(self._f("forward")(self.h, _ptr(rgb), _ptr(rays), _ptr(cam), _ptr(out), B, _stream(self.device)),
+              "cad_geonet_forward")
+        return out
+
+    __call__ = forward
+
+    def num_batches_tracked(self, film=False) -> int:
+        return int(self._f("num_batches_tracked")(self.h, int(film)))
+
+    def train_step(self, loss_fn: "CombinedDepthLoss", rgb, gt, K, lr=1e-4, weight_decay=1e-5, grad_clip=1.0,
+                   rays=None, pred=None, dpred=None, loss5=None, process_group=None):
+        """One optimisation step (enhanced.h:287-304 sequence) fed the loader's batch: rays default to
+        RayDirectionComputer's from K (a18), intrinsics = [K00, K11, K02, K12] (a15)."""
+        if rays is None:
+            rays = ray_directions(K, rgb.shape[2], rgb.shape[3])
+        pred = self.forward(rgb, rays, camera_from_K(K), out=pred)
+        loss5, dpred = loss_fn.forward_with_intrinsics(pred, gt, rgb, K, loss5=loss5, dpred=dpred)
+        self.backward(dpred)
+        world = 1
+        if process_group is not None:
+            import torch.distributed as dist
+            world = dist.get_world_size(process_group)
+            g = _flat_view(self._flat_g, self.n_flat, self.device)
+            dist.all_reduce(g, group=process_group)
+        self.clip_grad_norm_(grad_clip if grad_clip else float("inf"), 1.0 / world)
+        self.adam_step(lr=lr, weight_decay=weight_decay)
+        return loss5, pred
+
+
+class LightweightGeometryNetwork(GeometryAwareNetwork):
+    """LightweightGeometryNetworkImpl(in_channels, init_features=32, camera_dim, max_depth)
+    (geometry_aware_network.h:355-440): five levels, PCL and CBAM always on."""
+
+    _VARIANT = 1
+
+    def __init__(self, in_channels=3, init_features=32, camera_dim=4, max_depth=10.0, *, batch, height, width,
+                 device=0):
+        super().__init__(in_channels, init_features, camera_dim, max_depth, True, True, batch=batch, height=height,
+                         width=width, device=device)
 
 
 def _flat_view(addr: int, n: int, device) -> torch.Tensor:

@@ -433,6 +433,52 @@ cad_status cad_resunet_last_grad_norm(cad_resunet* h, float* total_norm, void* s
 cad_status cad_resunet_adam_step(cad_resunet* h, float lr, float beta1, float beta2, float eps, float weight_decay,
                                  void* stream);
 
+/* ---- geometry-aware family, src/models/geometry_aware_network.h ----
+ *   cad_geonet_create (CAD_GEONET_FULL)   GeometryAwareNetworkImpl(3, f, 4, max_depth, use_pcl,
+ *                                         use_attention)  geometry_aware_network.h:201-278
+ *   cad_geonet_create (CAD_GEONET_LIGHT)  LightweightGeometryNetworkImpl(3, f, 4, max_depth)  :355-383
+ *   cad_geonet_forward                    GeometryAwareNetworkImpl::forward(rgb, ray_directions,
+ *                                         camera_intrinsics (B,4) [fx, fy, cx, cy])  :289-318 / :385-402
+ *     (RayEnhancedConvImpl :17-65, GeometryEncoderBlockImpl :74-104, GeometryDecoderBlockImpl
+ *      :112-170, CBAMImpl spatial_attention.h:142-191, PerspectiveCorrectionLayerImpl pcl_layer.h:29-181)
+ * rgb, rays (B,3,H,W) NCHW device fp32; depth (B,1,H,W).  Parameter / buffer names and order are the
+ * reference module's named_parameters() / named_buffers() (float buffers).  Same life cycle as
+ * cad_resunet.  H, W multiples of 32 (FULL, 5 pools) or 16 (LIGHT). */
+#define CAD_GEONET_FULL 0
+#define CAD_GEONET_LIGHT 1
+typedef struct cad_geonet cad_geonet;
+typedef struct {
+    int variant;        /* CAD_GEONET_FULL / CAD_GEONET_LIGHT */
+    int in_channels;    /* 3 */
+    int init_features;  /* 64 (FULL default), 32 (LIGHT default) */
+    int camera_dim;     /* 4 */
+    float max_depth;    /* 10.0 */
+    int use_pcl;        /* FULL only (LIGHT: always 1) */
+    int use_attention;  /* FULL only (LIGHT: always 1) */
+    int max_batch;
+    int height, width;
+} cad_geonet_desc;
+cad_status cad_geonet_create(const cad_geonet_desc* d, int device, cad_geonet** out);
+void cad_geonet_destroy(cad_geonet* h);
+int64_t cad_geonet_count_parameters(const cad_geonet* h);
+int cad_geonet_num_tensors(const cad_geonet* h, int kind);   /* 0 parameters, 1 buffers */
+cad_status cad_geonet_tensor_info(const cad_geonet* h, int kind, int idx, const char** name, int* ndim,
+                                  int64_t shape[4]);
+cad_status cad_geonet_set_tensor(cad_geonet* h, int kind, int idx, const float* host, int64_t numel);
+cad_status cad_geonet_get_tensor(const cad_geonet* h, int kind, int idx, float* host, int64_t numel);
+cad_status cad_geonet_get_grad(const cad_geonet* h, int idx, float* host, int64_t numel);
+cad_status cad_geonet_train(cad_geonet* h, int train);
+cad_status cad_geonet_flat(cad_geonet* h, float** params, float** grads, int64_t* n);
+cad_status cad_geonet_forward(cad_geonet* h, const float* rgb, const float* rays, const float* cam4, float* depth,
+                              int B, void* stream);
+cad_status cad_geonet_backward(cad_geonet* h, const float* ddepth, void* stream);
+cad_status cad_geonet_clip_grad_norm(cad_geonet* h, float max_norm, float prescale, void* stream);
+cad_status cad_geonet_last_grad_norm(cad_geonet* h, float* total_norm, void* stream);
+cad_status cad_geonet_adam_step(cad_geonet* h, float lr, float beta1, float beta2, float eps, float weight_decay,
+                                void* stream);
+/* BatchNorm num_batches_tracked: film = 0 the BatchNorm2d layers, 1 FiLM's BatchNorm1d (B > 1 only) */
+int64_t cad_geonet_num_batches_tracked(const cad_geonet* h, int film);
+
 #ifdef __cplusplus
 }
 #endif

@@ -92,7 +92,8 @@ def synth_batch(B: int, H: int, W: int, rgb_seed: int = 0xC0FFEE, hole_seed: int
 # --------------------------------------------------------------------------------------------
 # Model: BaselineUNetImpl (baseline_unet.h:122-208) as named parameter/buffer dictionaries.
 # --------------------------------------------------------------------------------------------
-MODELS = ("baseline", "film", "rayfilm")
+MODELS = ("baseline", "film", "rayfilm", "geo", "geolite")
+GEO_LEVELS = {"geo": 6, "geolite": 5}   # GeometryAwareNetworkImpl / LightweightGeometryNetworkImpl
 FILM_CAMERA_DIM, FILM_H1, FILM_HIDDEN = 4, 128, 256   # FiLMLayerImpl(4, C) defaults (film_layer.h:47-66)
 
 
@@ -117,11 +118,58 @@ def _double_conv_spec(prefix, cin, cout, film=False):
     return spec + (_film_spec(prefix + "film.", cout) if film else [])
 
 
+def _cbam_spec(prefix, C):
+    # CBAMImpl(C) (spatial_attention.h:150-157): ChannelAttentionImpl fc1/fc2 (reduction 16, :38-50),
+    # SpatialAttentionImpl conv 2 -> 1, 7x7, no bias (:93-99)
+    cr = max(1, C // 16)
+    return [(prefix + "channel_attention.fc1.weight", (cr, C)), (prefix + "channel_attention.fc1.bias", (cr,)),
+            (prefix + "channel_attention.fc2.weight", (C, cr)), (prefix + "channel_attention.fc2.bias", (C,)),
+            (prefix + "spatial_attention.conv.weight", (1, 2, 7, 7))]
+
+
+def _pcl_spec(prefix, C, hidden=128):
+    # PerspectiveCorrectionLayerImpl(C, 4, 128) (pcl_layer.h:45-63): loc_fc1, loc_fc2, fc_transform
+    return [(prefix + "loc_fc1.weight", (hidden, C + 4)), (prefix + "loc_fc1.bias", (hidden,)),
+            (prefix + "loc_fc2.weight", (hidden, hidden)), (prefix + "loc_fc2.bias", (hidden,)),
+            (prefix + "fc_transform.weight", (6, hidden)), (prefix + "fc_transform.bias", (6,))]
+
+
+def _geo_names(model):
+    nl = GEO_LEVELS[model]
+    enc = ["enc1"] + [f"enc{l + 1}" for l in range(1, nl - 1)] + ["bottleneck"]
+    return nl, enc
+
+
+def _geo_spec(f, in_ch, model, use_pcl=True, use_attention=True):
+    # GeometryAwareNetworkImpl ctor (geometry_aware_network.h:241-278) / LightweightGeometryNetworkImpl
+    # (:368-383): enc1 = RayEnhancedConv(in, f, 4, true); GeometryEncoderBlock = pool, conv, attention;
+    # GeometryDecoderBlock = up, conv, pcl, attention (:74-170); out_conv
+    nl, enc = _geo_names(model)
+    spec = _double_conv_spec("enc1.", in_ch + 3, f, True)
+    for l in range(1, nl):
+        spec += _double_conv_spec(f"{enc[l]}.conv.", f << (l - 1), f << l, True)
+        if use_attention:
+            spec += _cbam_spec(f"{enc[l]}.attention.", f << l)
+    for l in range(nl - 2, -1, -1):
+        cin, cout = f << (l + 1), f << l
+        pre = f"dec{l + 1}."
+        spec += [(pre + "up.weight", (cin, cout, 2, 2)), (pre + "up.bias", (cout,))]
+        spec += _double_conv_spec(pre + "conv.", cin, cout, True)
+        if use_pcl:
+            spec += _pcl_spec(pre + "pcl.", cout)
+        if use_attention:
+            spec += _cbam_spec(pre + "attention.", cout)
+    return spec + [("out_conv.weight", (1, f, 1, 1)), ("out_conv.bias", (1,))]
+
+
 def param_spec(f: int = 64, in_ch: int = 3, model: str = "baseline"):
     """named_parameters() order of BaselineUNetImpl(in_ch, f) (registration order, :144-166),
     IntrinsicsConditionedUNetImpl(in_ch, f, 4) (intrinsics_unet.h:168-195), or the config-3
-    composite "rayfilm" (enc1 = RayEnhancedConv(in_ch, f, 4, use_rays) with in_ch + 3 inputs)."""
+    composite "rayfilm" (enc1 = RayEnhancedConv(in_ch, f, 4, use_rays) with in_ch + 3 inputs);
+    "geo" / "geolite": GeometryAwareNetworkImpl / LightweightGeometryNetworkImpl."""
     assert model in MODELS, model
+    if model in GEO_LEVELS:
+        return _geo_spec(f, in_ch, model)
     film = model != "baseline"
     spec = _double_conv_spec("enc1.", in_ch + (3 if model == "rayfilm" else 0), f, film)
     for i, name in enumerate(["enc2", "enc3", "enc4", "bottleneck"]):
@@ -158,6 +206,10 @@ def init_params(f: int = 64, seed: int = 42, in_ch: int = 3, model: str = "basel
     for name, shape in param_spec(f, in_ch, model):
         if ".bn" in name:
             params[name] = torch.ones(shape) if name.endswith("weight") else torch.zeros(shape)
+            continue
+        if ".fc_transform." in name:   # identity transform (pcl_layer.h:61-63)
+            params[name] = (torch.zeros(shape) if name.endswith("weight")
+                            else torch.tensor([1.0, 1.0, 0.0, 0.0, 0.0, 0.0]))
             continue
         if ".fc_gamma." in name or ".fc_beta." in name:
             if name.endswith("weight"):
@@ -324,10 +376,60 @@ def _decoder(x, skip, p, bufs, pre, train, cam=None):
     return _double_conv(torch.cat([skip, x], 1), p, bufs, pre + "conv.", train, cam)
 
 
+def _cbam(x, p, pre):
+    """CBAMImpl::forward (spatial_attention.h:165-175): channel then spatial attention."""
+    B, C = x.shape[:2]
+    def mlp(v):   # ChannelAttentionImpl::forward (:58-75), shared fc1 -> relu -> fc2
+        h = F.relu(F.linear(v, p[pre + "channel_attention.fc1.weight"], p[pre + "channel_attention.fc1.bias"]))
+        return F.linear(h, p[pre + "channel_attention.fc2.weight"], p[pre + "channel_attention.fc2.bias"])
+    att = torch.sigmoid(mlp(F.adaptive_avg_pool2d(x, 1).view(B, C)) + mlp(F.adaptive_max_pool2d(x, 1).view(B, C)))
+    x = x * att.view(B, C, 1, 1)
+    # SpatialAttentionImpl::forward (:105-117)
+    s = torch.cat([torch.mean(x, 1, keepdim=True), torch.max(x, 1, keepdim=True)[0]], 1)
+    return x * torch.sigmoid(F.conv2d(s, p[pre + "spatial_attention.conv.weight"], None, 1, 3))
+
+
+def _pcl(x, cam, p, pre):
+    """PerspectiveCorrectionLayerImpl::forward (pcl_layer.h:76-111) + buildAffineMatrix (:148-178)."""
+    B = x.shape[0]
+    loc = torch.cat([F.adaptive_avg_pool2d(x, 1).view(B, -1), cam], 1)
+    h = F.relu(F.linear(loc, p[pre + "loc_fc1.weight"], p[pre + "loc_fc1.bias"]))
+    h = F.relu(F.linear(h, p[pre + "loc_fc2.weight"], p[pre + "loc_fc2.bias"]))
+    t = F.linear(h, p[pre + "fc_transform.weight"], p[pre + "fc_transform.bias"])
+    c, s = torch.cos(t[:, 4]), torch.sin(t[:, 4])
+    theta = torch.stack([torch.stack([t[:, 0] * c, -s + t[:, 5], t[:, 2]], 1),
+                         torch.stack([s, t[:, 1] * c, t[:, 3]], 1)], 1)
+    grid = F.affine_grid(theta, list(x.shape), align_corners=False)
+    return F.grid_sample(x, grid, mode="bilinear", padding_mode="zeros", align_corners=False)
+
+
+def geo_forward(x, p, bufs, train, max_depth, model, K):
+    """GeometryAwareNetworkImpl::forward (geometry_aware_network.h:289-318) /
+    LightweightGeometryNetworkImpl::forward (:385-402) fed (rgb, rays_from_K(K), cam_from_K(K));
+    getDownsampledRays only feeds PCL's unused ray argument (pcl_layer.h:76-111) and is omitted."""
+    nl, enc = _geo_names(model)
+    cam = normalize_cam(cam_from_K(K.to(x.dtype)), x.shape[3], x.shape[2])
+    x = torch.cat([x, rays_from_K(K, x.shape[2], x.shape[3]).to(x.dtype)], 1)
+    skips = [_double_conv(x, p, bufs, "enc1.", train, cam)]
+    for l in range(1, nl):   # GeometryEncoderBlockImpl::forward (:92-103)
+        y = _double_conv(F.max_pool2d(skips[-1], 2), p, bufs, f"{enc[l]}.conv.", train, cam)
+        skips.append(_cbam(y, p, f"{enc[l]}.attention."))
+    x = skips[-1]
+    for l in range(nl - 2, -1, -1):   # GeometryDecoderBlockImpl::forward (:141-167)
+        pre = f"dec{l + 1}."
+        u = _pcl(_convT2x2(x, p[pre + "up.weight"], p[pre + "up.bias"]), cam, p, pre + "pcl.")
+        y = _double_conv(torch.cat([skips[l], u], 1), p, bufs, pre + "conv.", train, cam)
+        x = _cbam(y, p, pre + "attention.")
+    x = F.conv2d(x, p["out_conv.weight"], p["out_conv.bias"])
+    return torch.sigmoid(x) * max_depth
+
+
 def unet_forward(x, p, bufs, train=True, max_depth=10.0, model="baseline", K=None):
     """BaselineUNetImpl::forward (baseline_unet.h:174-195); model "film":
     IntrinsicsConditionedUNetImpl::forward(x, cam_from_K(K)) (intrinsics_unet.h:204-228); "rayfilm":
-    the same wiring with enc1 fed cat(x, rays_from_K(K))."""
+    the same wiring with enc1 fed cat(x, rays_from_K(K)); "geo" / "geolite": geo_forward."""
+    if model in GEO_LEVELS:
+        return geo_forward(x, p, bufs, train, max_depth, model, K)
     cam = None
     if model != "baseline":
         cam = normalize_cam(cam_from_K(K.to(x.dtype)), x.shape[3], x.shape[2])

@@ -27,6 +27,14 @@ FIXTURES = {
                                "--W", "64", "--steps", "3"],
     "train_rayfilm_f4_b3_64x96": ["--mode", "golden", "--model", "rayfilm", "--init", "synth", "--f", "4", "--B", "3", "--H", "64",
                                   "--W", "96", "--steps", "2"],
+    # geometry-aware family: GeometryAwareNetwork (6 levels, CBAM + PCL, B = 2:
+    # FiLM's BatchNorm1d over two samples) and LightweightGeometryNetwork (5 levels, B = 3); lean: the
+    # parameters after the last step are not stored (the losses, BN buffers and the eval prediction
+    # pin the trajectory)
+    "train_geo_f4_b2_64x64": ["--mode", "golden", "--model", "geo", "--init", "synth", "--f", "4", "--B", "2",
+                              "--H", "64", "--W", "64", "--steps", "2", "--lean", "1"],
+    "train_geolite_f4_b3_48x64": ["--mode", "golden", "--model", "geolite", "--init", "synth", "--f", "4", "--B", "3",
+                                  "--H", "48", "--W", "64", "--steps", "2", "--lean", "1"],
     # loss-only goldens (depth_loss.h) incl. a size whose pyramid floors (50x70 -> 6x8 at k=8)
     "loss_b2_120x160": ["--mode", "loss", "--B", "2", "--H", "120", "--W", "160"],
     "loss_b3_50x70": ["--mode", "loss", "--B", "3", "--H", "50", "--W", "70"],

@@ -16,6 +16,10 @@
 //   rayfilm   the config-3 composite of SURVEY §8 "Recommended config-3 model": enc1 =
 //             RayEnhancedConv(3, f, 4, true) (geometry_aware_network.h:17-65) fed cat(rgb, rays),
 //             enc2..dec1 = FiLMEncoderBlock / FiLMDecoderBlock (intrinsics_unet.h:59-113).
+//   geo       GeometryAwareNetworkImpl(3, f, 4, 10, true, true)  models/geometry_aware_network.h:201-347
+//             (RayEnhancedConv + CBAM encoders, ConvT + PCL + CBAM decoders, 6 levels) fed
+//             (rgb, rays, (B,4) [fx, fy, cx, cy])
+//   geolite   LightweightGeometryNetworkImpl(3, f, 4, 10)          geometry_aware_network.h:355-440
 //
 // Inputs are the synthetic SUN-RGB-D-shaped batches of SURVEY.md §8(d): a counter-based
 // splitmix64 stream so that every consumer (this harness, oracle/cad_oracle.py, bench.py) can
@@ -209,6 +213,14 @@ Net make_net(const std::string& kind, int f) {
         auto m = std::make_shared<RayFiLMUNetImpl>(f, 10.0f);
         n.mod = m;
         n.fwd = [m](const Batch& b) { return m->forward(b.rgb, b.cam4, b.rays); };
+    } else if (kind == "geo") {
+        auto m = std::make_shared<GeometryAwareNetworkImpl>(3, f, 4, 10.0f, true, true);
+        n.mod = m;
+        n.fwd = [m](const Batch& b) { return m->forward(b.rgb, b.rays, b.cam4); };
+    } else if (kind == "geolite") {
+        auto m = std::make_shared<LightweightGeometryNetworkImpl>(3, f, 4, 10.0f);
+        n.mod = m;
+        n.fwd = [m](const Batch& b) { return m->forward(b.rgb, b.rays, b.cam4); };
     } else {
         fprintf(stderr, "unknown --model %s\n", kind.c_str());
         exit(2);
@@ -258,7 +270,7 @@ double abs_rel_per_sample(torch::Tensor pred, torch::Tensor gt) {
 
 struct Args {
     std::string mode = "golden", out = ".", model = "baseline", init = "default", ckpt;
-    int f = 8, B = 2, H = 64, W = 64, steps = 3, threads = 1, warmup = 1, holes_all = 0, mask_seed = 0;
+    int f = 8, B = 2, H = 64, W = 64, steps = 3, threads = 1, warmup = 1, holes_all = 0, mask_seed = 0, lean = 0;
     float w[4] = {1.0f, 0.1f, 0.001f, 0.01f};
     float lr = 1e-4f, wd = 1e-5f, clip = 1.0f;
 };
@@ -284,6 +296,7 @@ Args parse(int argc, char** argv) {
         else if (k == "--wd") a.wd = std::stof(v);
         else if (k == "--holes-all") a.holes_all = std::stoi(v);
         else if (k == "--mask-seed") a.mask_seed = std::stoi(v);
+        else if (k == "--lean") a.lean = std::stoi(v);   // golden: no final.param.* (large models)
         else { fprintf(stderr, "unknown arg %s\n", k.c_str()); exit(2); }
     }
     return a;
@@ -402,7 +415,7 @@ int main(int argc, char** argv) {
     d.add("input.gt", batch.gt);
     d.add("input.K", batch.K);
     if (a.model != "baseline") d.add("input.cam4", batch.cam4);
-    if (a.model == "rayfilm") d.add("input.rays", batch.rays);
+    if (a.model == "rayfilm" || a.model == "geo" || a.model == "geolite") d.add("input.rays", batch.rays);
     if (!synth) {   // synth init: regenerated by the tests, buffers are the module defaults
         for (auto& kv : model->named_parameters()) d.add("init." + kv.key(), kv.value());
         for (auto& kv : model->named_buffers())
@@ -431,7 +444,8 @@ int main(int argc, char** argv) {
             if (kv.value().is_floating_point()) d.add("step1." + kv.key(), kv.value());
     }
     for (int s = 1; s < a.steps; ++s) losses.push_back(step(nullptr, nullptr, nullptr, nullptr));
-    for (auto& kv : model->named_parameters()) d.add("final.param." + kv.key(), kv.value());
+    if (!a.lean)
+        for (auto& kv : model->named_parameters()) d.add("final.param." + kv.key(), kv.value());
     for (auto& kv : model->named_buffers())
         if (kv.value().is_floating_point()) d.add("final." + kv.key(), kv.value());
     // eval-mode forward after training (BN running statistics) + a20 abs_rel

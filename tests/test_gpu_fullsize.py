@@ -39,10 +39,20 @@ B, H, W, F = 32, 480, 640, 64
 WEIGHTS = (1.0, 0.0, 0.0, 0.0)
 
 
+_CAPMAN = [None]
+
+
 def _beat(msg, t0):
-    # progress straight to the real stderr (pytest captures sys.stderr): a long CPU oracle step
-    # must not look like a hung GPU job
-    print(f"[fullsize +{time.time() - t0:6.1f}s] {msg}", file=sys.__stderr__, flush=True)
+    # progress to the real terminal: pytest's fd-level capture swallows even sys.__stderr__, and a long
+    # CPU oracle step must not look like a hung GPU job (a runner that sees no output for minutes
+    # kills it), so global capture is suspended around the line
+    line = f"[fullsize +{time.time() - t0:6.1f}s] {msg}"
+    cm = _CAPMAN[0]
+    if cm is None:
+        print(line, file=sys.__stderr__, flush=True)
+        return
+    with cm.global_and_fixture_disabled():
+        print(line, file=sys.stderr, flush=True)
 
 
 def _heartbeat(t0, stop, period=30.0):
@@ -51,7 +61,8 @@ def _heartbeat(t0, stop, period=30.0):
 
 
 @pytest.mark.timeout(1500)
-def test_bs32_480x640_train_step_vs_oracle(cad, dev, oracle):
+def test_bs32_480x640_train_step_vs_oracle(cad, dev, oracle, pytestconfig):
+    _CAPMAN[0] = pytestconfig.pluginmanager.getplugin("capturemanager")
     t0 = time.time()
     stop = threading.Event()
     threading.Thread(target=_heartbeat, args=(t0, stop), daemon=True).start()
