@@ -814,4 +814,30 @@ cad_status cad_geonet_adam_step(cad_geonet* h, float lr, float beta1, float beta
 
 int64_t cad_geonet_num_batches_tracked(const cad_geonet* h, int film) { return h ? (film ? h->nbt_film : h->nbt) : -1; }
 
+// test hook: copies an activation / gradient buffer of the last step to the host (NHWC rows).
+// "cat<l>" [M][2C] decoder concat, "dcat<l>" its gradient, "x<l>" decoder output, "u<l>" ConvT output,
+// "z<l>" encoder CBAM input; returns the element count (host == nullptr: count only), -1 if unknown
+int64_t cad_geonet_debug_buffer(cad_geonet* h, const char* name, float* host, int64_t numel) {
+    if (!h || !name) return -1;
+    const std::string n(name);
+    const int B = h->fwd_B;
+    if (n.size() < 2) return -1;
+    const std::string key = n.substr(0, n.size() - 1);
+    const int l = n.back() - '0';
+    if (l < 0 || l >= h->nl) return -1;
+    const float* src = nullptr;
+    int64_t cnt = 0;
+    if (key == "cat" && l < h->nl - 1) { src = h->cat[l]; cnt = 2 * h->Ml(l, B) * h->Cl(l); }
+    else if (key == "dcat" && l < h->nl - 1) { src = h->dcat[l]; cnt = 2 * h->Ml(l, B) * h->Cl(l); }
+    else if (key == "x" && l < h->nl - 1) { src = h->dec[l].x; cnt = h->Ml(l, B) * h->Cl(l); }
+    else if (key == "u" && l < h->nl - 1) { src = h->dec[l].u; cnt = h->Ml(l, B) * h->Cl(l); }
+    else if (key == "z" && l > 0 && h->enc[l].z) { src = h->enc[l].z; cnt = h->Ml(l, B) * h->Cl(l); }
+    else return -1;
+    if (!host) return cnt;
+    if (numel < cnt || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(host, src, sizeof(float) * cnt, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    return cnt;
+}
+
 }  // extern "C"

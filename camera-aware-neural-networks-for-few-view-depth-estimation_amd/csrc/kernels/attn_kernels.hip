@@ -57,7 +57,7 @@ __device__ __forceinline__ float grid_base(int idx, int n) {
 int chan_pool_slices(int64_t HW) { return (int)std::max<int64_t>(1, std::min<int64_t>(64, HW / 256)); }
 int64_t attn_scratch_doubles(int B, int64_t HW, int C) {
     const int S = chan_pool_slices(HW);
-    return std::max<int64_t>((int64_t)B * S * 3 * C, (int64_t)S * 98 + (int64_t)B * S * 8) + 64;
+    return std::max<int64_t>((int64_t)B * S * 3 * C, (int64_t)256 * 98 + (int64_t)B * 64 * 8) + 64;
 }
 
 // ------------------------------------------------------------------------------------------

@@ -703,6 +703,15 @@ class GeometryAwareNetwork(ResNetUNet):
     def num_batches_tracked(self, film=False) -> int:
         return int(self._f("num_batches_tracked")(self.h, int(film)))
 
+    def debug_buffer(self, name: str) -> torch.Tensor:
+        """Test hook: a buffer of the last step as NHWC rows ("cat<l>", "dcat<l>", "x<l>", "u<l>", "z<l>")."""
+        n = int(self._f("debug_buffer")(self.h, name.encode(), None, 0))
+        if n < 0:
+            raise KeyError(name)
+        out = np.empty(n, np.float32)
+        check(0 if self._f("debug_buffer")(self.h, name.encode(), out.ctypes.data_as(_abi.FP), n) == n else 1, name)
+        return torch.from_numpy(out)
+
     def train_step(self, loss_fn: "CombinedDepthLoss", rgb, gt, K, lr=1e-4, weight_decay=1e-5, grad_clip=1.0,
                    rays=None, pred=None, dpred=None, loss5=None, process_group=None):
         """One optimisation step (enhanced.h:287-304 sequence) fed the loader's batch: rays default to

@@ -478,6 +478,9 @@ cad_status cad_geonet_adam_step(cad_geonet* h, float lr, float beta1, float beta
                                 void* stream);
 /* BatchNorm num_batches_tracked: film = 0 the BatchNorm2d layers, 1 FiLM's BatchNorm1d (B > 1 only) */
 int64_t cad_geonet_num_batches_tracked(const cad_geonet* h, int film);
+/* test hook: buffer of the last step ("cat<l>", "dcat<l>", "x<l>", "u<l>", "z<l>"; NHWC rows) -> host;
+ * returns the element count (host NULL: count only) or -1 */
+int64_t cad_geonet_debug_buffer(cad_geonet* h, const char* name, float* host, int64_t numel);
 
 #ifdef __cplusplus
 }

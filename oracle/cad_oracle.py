@@ -403,11 +403,15 @@ def _pcl(x, cam, p, pre):
     return F.grid_sample(x, grid, mode="bilinear", padding_mode="zeros", align_corners=False)
 
 
+GEO_DEBUG = {}
+
+
 def geo_forward(x, p, bufs, train, max_depth, model, K):
     """GeometryAwareNetworkImpl::forward (geometry_aware_network.h:289-318) /
     LightweightGeometryNetworkImpl::forward (:385-402) fed (rgb, rays_from_K(K), cam_from_K(K));
     getDownsampledRays only feeds PCL's unused ray argument (pcl_layer.h:76-111) and is omitted."""
     nl, enc = _geo_names(model)
+    keep = GEO_DEBUG.get("keep")   # test hook: {name: tensor} of the intermediate activations
     cam = normalize_cam(cam_from_K(K.to(x.dtype)), x.shape[3], x.shape[2])
     x = torch.cat([x, rays_from_K(K, x.shape[2], x.shape[3]).to(x.dtype)], 1)
     skips = [_double_conv(x, p, bufs, "enc1.", train, cam)]
@@ -417,9 +421,16 @@ def geo_forward(x, p, bufs, train, max_depth, model, K):
     x = skips[-1]
     for l in range(nl - 2, -1, -1):   # GeometryDecoderBlockImpl::forward (:141-167)
         pre = f"dec{l + 1}."
-        u = _pcl(_convT2x2(x, p[pre + "up.weight"], p[pre + "up.bias"]), cam, p, pre + "pcl.")
-        y = _double_conv(torch.cat([skips[l], u], 1), p, bufs, pre + "conv.", train, cam)
+        u0 = _convT2x2(x, p[pre + "up.weight"], p[pre + "up.bias"])
+        u = _pcl(u0, cam, p, pre + "pcl.")
+        cat = torch.cat([skips[l], u], 1)
+        y = _double_conv(cat, p, bufs, pre + "conv.", train, cam)
         x = _cbam(y, p, pre + "attention.")
+        if keep is not None:
+            for k, t in ((f"cat{l}", cat), (f"u{l}", u0), (f"x{l}", x)):
+                if t.requires_grad:
+                    t.retain_grad()
+                keep[k] = t
     x = F.conv2d(x, p["out_conv.weight"], p["out_conv.bias"])
     return torch.sigmoid(x) * max_depth
 
