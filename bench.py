@@ -269,6 +269,41 @@ def extra_leg_resunet(cad, dev, steps=5, warmup=2, B=32, H=480, W=640):
             "mfma_frac_dense_bf16": round(flop_img * value / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4)}
 
 
+def extra_leg_geonet(cad, lib, dev, steps=3, warmup=2, B=8, H=480, W=640, f=64):
+    """The geometry-aware family (no BASELINE config names it): one
+    GeometryAwareNetwork(3, 64, 4, 10, use_pcl, use_attention) train step at 480x640 on the fp32 (S3)
+    engine, full loss, bs8 (its six-level activations with CBAM / PCL state are ~4x the U-Net's)."""
+    import torch
+    from cad_amd import synthetic
+    prev = lib.cad_get_gemm_engine()
+    lib.cad_set_gemm_engine(1)
+    try:
+        model = cad.GeometryAwareNetwork(3, f, 4, 10.0, batch=B, height=H, width=W, device=dev.index)
+        loss = cad.CombinedDepthLoss(1.0, 0.1, 0.001, 0.01, batch=B, height=H, width=W, device=dev.index)
+        rgb, gt, K = (t.to(dev) for t in synthetic.device_batch(B, H, W, "cpu"))
+        rays = cad.ray_directions(K, H, W)
+        pred = torch.empty((B, 1, H, W), device=dev)
+        dpred, loss5 = torch.empty_like(pred), torch.zeros(5, device=dev)
+        for _ in range(warmup):
+            model.train_step(loss, rgb, gt, K, rays=rays, pred=pred, dpred=dpred, loss5=loss5)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            model.train_step(loss, rgb, gt, K, rays=rays, pred=pred, dpred=dpred, loss5=loss5)
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        last = loss5[0].item()
+        params = model.count_parameters()
+        del model, loss
+        torch.cuda.empty_cache()
+    finally:
+        lib.cad_set_gemm_engine(prev)
+    return {"workload": f"GeometryAwareNetwork(3, {f}) train step (CBAM + PCL, six levels): bs{B} {H}x{W} "
+                        "fp32 (S3) GEMMs, full loss",
+            "value": round(B * steps / dt, 3), "unit": "images/s", "ms_per_step": round(1e3 * dt / steps, 3),
+            "steps": steps, "warmup": warmup, "dtype": "fp32", "params": params, "last_loss": last}
+
+
 def pmc_traffic(kernel_name):
     """HBM bytes per launch of `kernel_name` from the committed rocprofv3 PMC summary, if any."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -439,6 +474,11 @@ def main():
                 log(f"extra leg config 5: {extra['config5']}")
             except Exception as e:
                 log(f"extra leg config 5 failed: {e}")
+            try:
+                extra["geometry"] = extra_leg_geonet(cad, lib, dev)
+                log(f"extra leg geometry-aware network: {extra['geometry']}")
+            except Exception as e:
+                log(f"extra leg geometry-aware network failed: {e}")
             try:
                 dp = data_path(cad, dev, B, H, W)
             except Exception as e:

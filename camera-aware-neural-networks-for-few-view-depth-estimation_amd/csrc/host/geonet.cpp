@@ -814,20 +814,29 @@ cad_status cad_geonet_adam_step(cad_geonet* h, float lr, float beta1, float beta
 
 int64_t cad_geonet_num_batches_tracked(const cad_geonet* h, int film) { return h ? (film ? h->nbt_film : h->nbt) : -1; }
 
-// test hook: copies an activation / gradient buffer of the last step to the host (NHWC rows).
-// "cat<l>" [M][2C] decoder concat, "dcat<l>" its gradient, "x<l>" decoder output, "u<l>" ConvT output,
-// "z<l>" encoder CBAM input; returns the element count (host == nullptr: count only), -1 if unknown
+// test hook: copies a buffer of the last step to the host (NHWC rows; int32 buffers bit-copied).
+//   "cat<l>" [M][2C] decoder concat, "dcat<l>" its gradient, "x<l>" decoder output, "u<l>" ConvT output,
+//   "z<l>" encoder CBAM input; CBAM decisions of encoder ("e") / decoder ("d") block l:
+//   "amax<e|d><l>" [B][C] argmax pixel of the channel max-pool, "sidx<e|d><l>" [M] argmax channel
+// returns the element count (host == nullptr: count only), -1 if unknown
 int64_t cad_geonet_debug_buffer(cad_geonet* h, const char* name, float* host, int64_t numel) {
     if (!h || !name) return -1;
     const std::string n(name);
     const int B = h->fwd_B;
     if (n.size() < 2) return -1;
-    const std::string key = n.substr(0, n.size() - 1);
     const int l = n.back() - '0';
     if (l < 0 || l >= h->nl) return -1;
-    const float* src = nullptr;
+    std::string key = n.substr(0, n.size() - 1);
+    const void* src = nullptr;
     int64_t cnt = 0;
-    if (key == "cat" && l < h->nl - 1) { src = h->cat[l]; cnt = 2 * h->Ml(l, B) * h->Cl(l); }
+    if (key == "amaxe" || key == "amaxd" || key == "sidxe" || key == "sidxd") {
+        const bool enc = key.back() == 'e';
+        if (!enc && l > h->nl - 2) return -1;
+        const GBlock& b = enc ? h->enc[l] : h->dec[l].blk;
+        if (b.cb0 < 0) return -1;
+        if (key[0] == 'a') { src = b.A.amax; cnt = (int64_t)B * b.A.C; }
+        else { src = b.A.sidx; cnt = h->Ml(l, B); }
+    } else if (key == "cat" && l < h->nl - 1) { src = h->cat[l]; cnt = 2 * h->Ml(l, B) * h->Cl(l); }
     else if (key == "dcat" && l < h->nl - 1) { src = h->dcat[l]; cnt = 2 * h->Ml(l, B) * h->Cl(l); }
     else if (key == "x" && l < h->nl - 1) { src = h->dec[l].x; cnt = h->Ml(l, B) * h->Cl(l); }
     else if (key == "u" && l < h->nl - 1) { src = h->dec[l].u; cnt = h->Ml(l, B) * h->Cl(l); }

@@ -377,15 +377,31 @@ def _decoder(x, skip, p, bufs, pre, train, cam=None):
 
 
 def _cbam(x, p, pre):
-    """CBAMImpl::forward (spatial_attention.h:165-175): channel then spatial attention."""
+    """CBAMImpl::forward (spatial_attention.h:165-175): channel then spatial attention.
+    Test hook GEO_DEBUG["force"][pre] = (argmax pixel [B][C], argmax channel [B*H*W]): the two max
+    reductions select those elements instead (same values up to rounding; the gradients are routed
+    as the run that made the decisions routed them)."""
     B, C = x.shape[:2]
+    force = GEO_DEBUG.get("force", {}).get(pre)
     def mlp(v):   # ChannelAttentionImpl::forward (:58-75), shared fc1 -> relu -> fc2
         h = F.relu(F.linear(v, p[pre + "channel_attention.fc1.weight"], p[pre + "channel_attention.fc1.bias"]))
         return F.linear(h, p[pre + "channel_attention.fc2.weight"], p[pre + "channel_attention.fc2.bias"])
-    att = torch.sigmoid(mlp(F.adaptive_avg_pool2d(x, 1).view(B, C)) + mlp(F.adaptive_max_pool2d(x, 1).view(B, C)))
+    if force is None:
+        mx = F.adaptive_max_pool2d(x, 1).view(B, C)
+    else:
+        mx = x.reshape(B, C, -1).gather(2, force[0].view(B, C, 1)).view(B, C)
+        true = F.adaptive_max_pool2d(x, 1).view(B, C)   # how far the forced choice is from a true argmax
+        GEO_DEBUG.setdefault("gap", []).append(((true - mx).abs().max() / true.abs().max().clamp_min(1e-30)).item())
+    att = torch.sigmoid(mlp(F.adaptive_avg_pool2d(x, 1).view(B, C)) + mlp(mx))
     x = x * att.view(B, C, 1, 1)
     # SpatialAttentionImpl::forward (:105-117)
-    s = torch.cat([torch.mean(x, 1, keepdim=True), torch.max(x, 1, keepdim=True)[0]], 1)
+    if force is None:
+        smax = torch.max(x, 1, keepdim=True)[0]
+    else:
+        smax = x.gather(1, force[1].view(B, 1, x.shape[2], x.shape[3]))
+        true = torch.max(x, 1, keepdim=True)[0]
+        GEO_DEBUG.setdefault("gap", []).append(((true - smax).abs().max() / true.abs().max().clamp_min(1e-30)).item())
+    s = torch.cat([torch.mean(x, 1, keepdim=True), smax], 1)
     return x * torch.sigmoid(F.conv2d(s, p[pre + "spatial_attention.conv.weight"], None, 1, 3))
 
 
