@@ -93,6 +93,8 @@ SIGNATURES = {
     "cad_geonet_adam_step": (I, [P, F, F, F, F, F, P]),
     "cad_geonet_num_batches_tracked": (I64, [P, I]),
     "cad_geonet_debug_buffer": (I64, [P, C.c_char_p, FP, I64]),
+    "cad_op_cbam": (I, [P, P, P, I, I, I, I, P, P, P, P]),
+    "cad_op_pcl": (I, [P, P, P, P, I, I, I, I, P, P, P, P, P]),
     "cad_unet_create_model": (I, [C.POINTER(UnetDesc), I, I, C.POINTER(P)]),
     "cad_unet_model": (I, [P]),
     "cad_unet_forward_cam": (I, [P, P, P, P, I, P]),

@@ -814,6 +814,76 @@ cad_status cad_geonet_adam_step(cad_geonet* h, float lr, float beta1, float beta
 
 int64_t cad_geonet_num_batches_tracked(const cad_geonet* h, int film) { return h ? (film ? h->nbt_film : h->nbt) : -1; }
 
+// ---- operator-level entry points (tests): one CBAM / one PCL forward + backward on device tensors.
+// Parameters and gradients packed in the reference's registration order; state is allocated per
+// call (test use only).
+cad_status cad_op_cbam(const float* x, const float* g, const float* params, int B, int H, int W, int C, float* out,
+                       float* dx, float* grads, void* stream) {
+    return gguard([&] {
+        need(x && g && params && out && dx && grads && B > 0 && H > 0 && W > 0 && C > 0, "bad argument");
+        const int Cr = std::max(1, C / 16);
+        const int64_t M = (int64_t)B * H * W, HW = (int64_t)H * W;
+        Arena sz, real;
+        cad::Cbam A{};
+        auto lay = [&](Arena& a) {
+            A.C = C; A.Cr = Cr;
+            A.avg = a.f((int64_t)B * C); A.mx = a.f((int64_t)B * C); A.amax = a.i((int64_t)B * C);
+            A.ha = a.f((int64_t)B * Cr); A.hm = a.f((int64_t)B * Cr); A.att = a.f((int64_t)B * C);
+            A.s = a.f(2 * M); A.sidx = a.i(M); A.sa = a.f(M); A.dlog = a.f(M); A.ds = a.f(2 * M);
+            A.dO = a.f((int64_t)B * C); A.dha = a.f((int64_t)B * Cr); A.dhm = a.f((int64_t)B * Cr);
+            A.dva = a.f((int64_t)B * C); A.dvm = a.f((int64_t)B * C);
+            return a.d(cad::attn_scratch_doubles(B, HW, C));
+        };
+        lay(sz);
+        void* base = nullptr;
+        GCHK(hipMalloc(&base, sz.off + 4096));
+        real.base = static_cast<char*>(base);
+        double* scr = lay(real);
+        const int64_t o1 = (int64_t)Cr * C, o2 = o1 + Cr, o3 = o2 + (int64_t)C * Cr, o4 = o3 + C;
+        A.w1 = params; A.b1 = params + o1; A.w2 = params + o2; A.b2 = params + o3; A.wsp = params + o4;
+        A.gw1 = grads; A.gb1 = grads + o1; A.gw2 = grads + o2; A.gb2 = grads + o3; A.gwsp = grads + o4;
+        cad::cbam_fwd(A, x, B, H, W, out, C, 0, scr, S(stream));
+        cad::cbam_bwd(A, x, g, C, 0, B, H, W, dx, scr, S(stream));
+        const hipError_t e = hipStreamSynchronize(S(stream));
+        (void)hipFree(base);
+        GCHK(e);
+    });
+}
+
+cad_status cad_op_pcl(const float* u, const float* camn, const float* g, const float* params, int B, int H, int W,
+                      int C, float* out, float* du, float* grads, float* theta, void* stream) {
+    return gguard([&] {
+        need(u && camn && g && params && out && du && grads && B > 0 && H > 0 && W > 0 && C > 0, "bad argument");
+        const int Hd = cad::kPclHidden;
+        const int64_t M = (int64_t)B * H * W, HW = (int64_t)H * W;
+        Arena sz, real;
+        cad::Pcl P{};
+        auto lay = [&](Arena& a) {
+            P.C = C;
+            P.pooled = a.f((int64_t)B * C); P.h1 = a.f((int64_t)B * Hd); P.h2 = a.f((int64_t)B * Hd);
+            P.tp = a.f((int64_t)B * 6); P.theta = a.f((int64_t)B * 6); P.dgrid = a.f(2 * M);
+            P.dtp = a.f((int64_t)B * 6); P.dh1 = a.f((int64_t)B * Hd); P.dh2 = a.f((int64_t)B * Hd);
+            P.dpooled = a.f((int64_t)B * C);
+            return a.d(cad::attn_scratch_doubles(B, HW, C));
+        };
+        lay(sz);
+        void* base = nullptr;
+        GCHK(hipMalloc(&base, sz.off + 4096));
+        real.base = static_cast<char*>(base);
+        double* scr = lay(real);
+        const int64_t K1 = C + 4, o1 = (int64_t)Hd * K1, o2 = o1 + Hd, o3 = o2 + (int64_t)Hd * Hd, o4 = o3 + Hd,
+                      o5 = o4 + 6 * Hd;
+        P.w1 = params; P.b1 = params + o1; P.w2 = params + o2; P.b2 = params + o3; P.w3 = params + o4; P.b3 = params + o5;
+        P.gw1 = grads; P.gb1 = grads + o1; P.gw2 = grads + o2; P.gb2 = grads + o3; P.gw3 = grads + o4; P.gb3 = grads + o5;
+        cad::pcl_fwd(P, u, camn, B, H, W, out, C, 0, scr, S(stream));
+        cad::pcl_bwd(P, u, camn, g, C, 0, B, H, W, du, scr, S(stream));
+        if (theta) (void)hipMemcpyAsync(theta, P.theta, sizeof(float) * 6 * B, hipMemcpyDeviceToDevice, S(stream));
+        const hipError_t e = hipStreamSynchronize(S(stream));
+        (void)hipFree(base);
+        GCHK(e);
+    });
+}
+
 // test hook: copies a buffer of the last step to the host (NHWC rows; int32 buffers bit-copied).
 //   "cat<l>" [M][2C] decoder concat, "dcat<l>" its gradient, "x<l>" decoder output, "u<l>" ConvT output,
 //   "z<l>" encoder CBAM input; CBAM decisions of encoder ("e") / decoder ("d") block l:

@@ -478,6 +478,16 @@ cad_status cad_geonet_adam_step(cad_geonet* h, float lr, float beta1, float beta
                                 void* stream);
 /* BatchNorm num_batches_tracked: film = 0 the BatchNorm2d layers, 1 FiLM's BatchNorm1d (B > 1 only) */
 int64_t cad_geonet_num_batches_tracked(const cad_geonet* h, int film);
+/* operator-level entry points (tests; state allocated per call): one CBAMImpl forward + backward
+ * (spatial_attention.h:142-191) / one PerspectiveCorrectionLayerImpl forward + backward (pcl_layer.h:
+ * 76-178) on device NHWC tensors [B*H*W][C]; params / grads packed in registration order
+ * (CBAM: fc1.w [C/16][C], fc1.b, fc2.w [C][C/16], fc2.b, spatial conv.w [2][7][7]; PCL: loc_fc1.w
+ * [128][C+4], loc_fc1.b, loc_fc2.w [128][128], loc_fc2.b, fc_transform.w [6][128], fc_transform.b);
+ * g = gradient of the output; camn (B,4) the normalised intrinsics; theta (nullable) <- (B,2,3) */
+cad_status cad_op_cbam(const float* x, const float* g, const float* params, int B, int H, int W, int C, float* out,
+                       float* dx, float* grads, void* stream);
+cad_status cad_op_pcl(const float* u, const float* camn, const float* g, const float* params, int B, int H, int W,
+                      int C, float* out, float* du, float* grads, float* theta, void* stream);
 /* test hook: buffer of the last step ("cat<l>", "dcat<l>", "x<l>", "u<l>", "z<l>"; NHWC rows) -> host;
  * returns the element count (host NULL: count only) or -1 */
 int64_t cad_geonet_debug_buffer(cad_geonet* h, const char* name, float* host, int64_t numel);
