@@ -224,6 +224,112 @@ public:
                                         CAD_MODEL_RAY_FILM) {}
 };
 
+// GeometryAwareNetworkImpl(in, f, camera_dim, max_depth, use_pcl, use_attention)
+// (geometry_aware_network.h:201-347) and LightweightGeometryNetworkImpl(in, f, camera_dim, max_depth)
+// (:355-440): forward(rgb, ray_directions (B,3,H,W), camera_intrinsics (B,4) [fx, fy, cx, cy]).
+// Training: backward(dL/ddepth), then clip_grad_norm_ / adam_step on the model-owned slabs.
+class GeometryAwareNetworkImpl {
+public:
+    explicit GeometryAwareNetworkImpl(int in_channels = 3, int init_features = 64, int camera_dim = 4,
+                                      float max_depth_value = 10.0f, bool use_pcl = true, bool use_attention = true,
+                                      cad::Workspace ws = {})
+        : GeometryAwareNetworkImpl(CAD_GEONET_FULL, in_channels, init_features, camera_dim, max_depth_value, use_pcl,
+                                   use_attention, ws) {}
+    ~GeometryAwareNetworkImpl() { cad_geonet_destroy(h_); }
+    GeometryAwareNetworkImpl(const GeometryAwareNetworkImpl&) = delete;
+    GeometryAwareNetworkImpl& operator=(const GeometryAwareNetworkImpl&) = delete;
+
+    DeviceTensor forward(const DeviceTensor& rgb, const DeviceTensor& ray_directions,
+                         const DeviceTensor& camera_intrinsics, void* stream = nullptr) {
+        if (rgb.dim() != 4 || rgb.size(1) != 3) throw std::runtime_error("forward: expected rgb (B,3,H,W)");
+        if (ray_directions.dim() != 4 || ray_directions.size(0) != rgb.size(0) || ray_directions.size(1) != 3)
+            throw std::runtime_error("forward: expected ray_directions (B,3,H,W)");
+        if (camera_intrinsics.dim() != 2 || camera_intrinsics.size(0) != rgb.size(0) || camera_intrinsics.size(1) != 4)
+            throw std::runtime_error("forward: expected camera_intrinsics (B,4)");
+        DeviceTensor out = DeviceTensor::empty({rgb.size(0), 1, rgb.size(2), rgb.size(3)}, ws_.device);
+        cad::check(cad_geonet_forward(h_, rgb.data, ray_directions.data, camera_intrinsics.data, out.data,
+                                      (int)rgb.size(0), stream),
+                   "forward");
+        return out;
+    }
+    DeviceTensor operator()(const DeviceTensor& rgb, const DeviceTensor& rays, const DeviceTensor& intrinsics) {
+        return forward(rgb, rays, intrinsics);
+    }
+    void backward(const DeviceTensor& ddepth, void* stream = nullptr) {
+        cad::check(cad_geonet_backward(h_, ddepth.data, stream), "backward");
+    }
+    // torch::nn::utils::clip_grad_norm_(parameters(), max_norm) (prescale: 1/world after a gradient
+    // all-reduce) and torch::optim::Adam(AdamOptions(lr).weight_decay(wd)).step()
+    void clip_grad_norm_(float max_norm, float prescale = 1.0f, void* stream = nullptr) {
+        cad::check(cad_geonet_clip_grad_norm(h_, max_norm, prescale, stream), "clip_grad_norm_");
+    }
+    void adam_step(float lr, float weight_decay, float beta1 = 0.9f, float beta2 = 0.999f, float eps = 1e-8f,
+                   void* stream = nullptr) {
+        cad::check(cad_geonet_adam_step(h_, lr, beta1, beta2, eps, weight_decay, stream), "adam_step");
+    }
+    int64_t count_parameters() const { return cad_geonet_count_parameters(h_); }
+    void train(bool on = true) { cad::check(cad_geonet_train(h_, on ? 1 : 0), "train"); }
+    void eval() { train(false); }
+    std::vector<NamedTensor> named_parameters() const { return fetch(0); }
+    std::vector<NamedTensor> named_buffers() const { return fetch(1); }
+    int load(const std::vector<NamedTensor>& ts) {
+        int n = 0;
+        for (int kind = 0; kind < 2; ++kind)
+            for (int i = 0; i < cad_geonet_num_tensors(h_, kind); ++i) {
+                const char* name;
+                cad::check(cad_geonet_tensor_info(h_, kind, i, &name, nullptr, nullptr), "tensor_info");
+                for (const auto& t : ts)
+                    if (t.name == name) {
+                        cad::check(cad_geonet_set_tensor(h_, kind, i, t.value.data(), (int64_t)t.value.size()), name);
+                        ++n;
+                    }
+            }
+        return n;
+    }
+    cad_geonet* handle() const { return h_; }
+
+    float max_depth;
+
+protected:
+    GeometryAwareNetworkImpl(int variant, int in_channels, int init_features, int camera_dim, float max_depth_value,
+                             bool use_pcl, bool use_attention, cad::Workspace ws)
+        : max_depth(max_depth_value), ws_(ws) {
+        cad_geonet_desc d{variant, in_channels, init_features, camera_dim, max_depth_value, use_pcl ? 1 : 0,
+                          use_attention ? 1 : 0, ws.batch, ws.height, ws.width};
+        cad::check(cad_geonet_create(&d, ws.device, &h_), "cad_geonet_create");
+    }
+
+private:
+    std::vector<NamedTensor> fetch(int kind) const {
+        std::vector<NamedTensor> out;
+        for (int i = 0; i < cad_geonet_num_tensors(h_, kind); ++i) {
+            const char* name;
+            int nd;
+            int64_t shp[4];
+            cad::check(cad_geonet_tensor_info(h_, kind, i, &name, &nd, shp), "tensor_info");
+            NamedTensor t;
+            t.name = name;
+            t.shape.assign(shp, shp + nd);
+            int64_t n = 1;
+            for (int k = 0; k < nd; ++k) n *= shp[k];
+            t.value.resize((size_t)n);
+            cad::check(cad_geonet_get_tensor(h_, kind, i, t.value.data(), n), "get_tensor");
+            out.push_back(std::move(t));
+        }
+        return out;
+    }
+    cad::Workspace ws_;
+    cad_geonet* h_ = nullptr;
+};
+
+class LightweightGeometryNetworkImpl : public GeometryAwareNetworkImpl {
+public:
+    explicit LightweightGeometryNetworkImpl(int in_channels = 3, int init_features = 32, int camera_dim = 4,
+                                            float max_depth_value = 10.0f, cad::Workspace ws = {})
+        : GeometryAwareNetworkImpl(CAD_GEONET_LIGHT, in_channels, init_features, camera_dim, max_depth_value, true,
+                                   true, ws) {}
+};
+
 class CombinedDepthLoss {
 public:
     explicit CombinedDepthLoss(float si_weight = 1.0f, float grad_weight = 0.1f, float smooth_weight = 0.001f,

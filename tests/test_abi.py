@@ -5,6 +5,8 @@ import ctypes as C
 import os
 import subprocess
 
+import pytest
+
 from conftest import ROOT
 
 PKG = os.path.join(ROOT, "camera-aware-neural-networks-for-few-view-depth-estimation_amd")
@@ -63,3 +65,21 @@ def test_argument_validation_without_device(cad):
 def _desc(cad):
     from cad_amd import _abi
     return _abi.UnetDesc(3, 8, 10.0, 1, 32, 32)
+
+
+def test_cpp_dropin_header_links(tmp_path):
+    """include/cad/cad.hpp (the reference class names: BaselineUNetImpl ... GeometryAwareNetworkImpl,
+    LightweightGeometryNetworkImpl) compiles and links against libcad_hip.so (no GPU needed)."""
+    import shutil
+    import subprocess
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pkg = os.path.join(root, "camera-aware-neural-networks-for-few-view-depth-estimation_amd")
+    if not os.path.exists(os.path.join(pkg, "libcad_hip.so")):
+        pytest.skip("libcad_hip.so not built")
+    exe = tmp_path / "hpp_probe"
+    subprocess.run(["g++", "-std=c++17", "-O1", "-I", os.path.join(root, "include"), "-o", str(exe),
+                    os.path.join(root, "tests", "hpp_probe.cpp"), "-L", pkg, "-lcad_hip",
+                    "-Wl,-rpath," + pkg, "-Wl,--allow-shlib-undefined"], check=True)
+    assert exe.exists()

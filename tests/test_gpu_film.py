@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import GOLDEN, max_rel_err
+from conftest import GOLDEN, grad_close, max_rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -172,7 +172,8 @@ def test_film_train_step_vs_oracle(cad, dev, oracle, model, f, B, H, W):
         cos = torch.nn.functional.cosine_similarity(grads[n].double().reshape(1, -1), g64.reshape(1, -1)).item()
         # the 6x8 / 3x4 deep levels of these nets leave a few hundred pixels per BN channel, and
         # FiLM's BatchNorm1d sees B samples: LibTorch fp32 itself lands ~1e-2 off fp64 there
-        assert cos > 0.999 and ours < max(0.25, 5 * ref32), (n, cos, ours, ref32)
+        ok, st = grad_close(grads[n], g64, [g32], k=5.0)
+        assert cos > 0.999 and ok, (n, cos, st)
     ref64 = oracle.Trainer(params, bufs, dtype=torch.float64, model=model)
     ref64.step(rgb, gt, K)
     cad.clip_grad_norm_(net, 1.0)

@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import GOLDEN, max_rel_err
+from conftest import grad_close, GOLDEN, max_rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -107,7 +107,8 @@ def test_train_step_vs_oracle(cad, dev, oracle, f, B, H, W):
     for (n, _), g32, g64 in zip(oracle.param_spec(f), r["grads"], r64["grads"]):
         ours, ref32 = max_rel_err(grads[n], g64), max_rel_err(g32, g64)
         cos = torch.nn.functional.cosine_similarity(grads[n].double().reshape(1, -1), g64.reshape(1, -1)).item()
-        assert cos > 0.9999 and ours < max(0.25, 3 * ref32), (n, cos, ours, ref32)
+        ok, st = grad_close(grads[n], g64, [g32])
+        assert cos > 0.9999 and ok, (n, cos, st)
     # finish step 1 and run three more on every side; compare the outputs (train- and eval-mode)
     # against fp64: within 1e-3, or within 3x the LibTorch fp32 path's own drift from fp64
     # (Adam's early steps are ~lr*sign(g), so sign flips of near-zero gradients are not damped)
@@ -202,7 +203,8 @@ def test_train_step_bf16_engine_vs_oracle(cad, dev, oracle, bf16_engine, f, B, H
         ours, ref32 = max_rel_err(grads[n], g64), max_rel_err(g32, g64)
         cos = torch.nn.functional.cosine_similarity(grads[n].double().reshape(1, -1), g64.reshape(1, -1)).item()
         cos32 = torch.nn.functional.cosine_similarity(g32.double().reshape(1, -1), g64.reshape(1, -1)).item()
-        assert cos > min(0.999, 1 - 3 * (1 - cos32)) and ours < max(0.25, 3 * ref32), (n, cos, cos32, ours, ref32)
+        ok, st = grad_close(grads[n], g64, [g32])
+        assert cos > min(0.999, 1 - 3 * (1 - cos32)) and ok, (n, cos, cos32, st)
     cad.clip_grad_norm_(model, 1.0)
     tr.optimizer.step()
     for _ in range(3):
