@@ -212,37 +212,57 @@ __device__ __forceinline__ void split4_store(char* os, int64_t ldos, int oscoff,
     for (int p = 0; p < NP; ++p) *reinterpret_cast<uint2*>(d + p * 16) = sp.p[p];
 }
 
-template <int NP, bool YB>
-__global__ void k_bn_relu_fwd(const float* __restrict__ y, int C, const float* __restrict__ scale,
-                              const float* __restrict__ shift, float* __restrict__ out, int64_t ldo,
-                              int ocoff, int64_t n4, char* __restrict__ os, int64_t ldos, int oscoff) {
+// BN passes in row-slice form: a thread owns one 4-channel group (its per-channel coefficients stay
+// in registers) and walks the rows of its slice; a wavefront still reads whole contiguous row
+// chunks.  (A flat grid-stride loop reloads every coefficient per element — 7 arrays in the
+// backward — and ran issue-bound below the HBM rate.)
+struct RowGrid {
+    int CX, RY, S;
+    int64_t rps;
+};
+inline RowGrid row_grid(int64_t M, int C) {
+    RowGrid g;
     const int C4 = C >> 2;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t r = i / C4;
-        const int c = (int)(i - r * C4) * 4;
-        float4 v = load4<YB>(y, i * 4);
-        float4 s = *reinterpret_cast<const float4*>(scale + c);
-        float4 t = *reinterpret_cast<const float4*>(shift + c);
+    g.CX = std::min(C4, 64);
+    g.RY = std::max(1, 256 / g.CX);
+    g.S = (int)std::max<int64_t>(1, std::min<int64_t>(65535, cdiv(M, (int64_t)g.RY * 16)));
+    g.rps = (M + g.S - 1) / g.S;
+    return g;
+}
+template <int NP, bool YB>
+__global__ __launch_bounds__(256) void k_bn_relu_fwd_rows(const float* __restrict__ y, int C,
+                                                          const float* __restrict__ scale,
+                                                          const float* __restrict__ shift, float* __restrict__ out,
+                                                          int64_t ldo, int ocoff, int64_t M, int64_t rps,
+                                                          char* __restrict__ os, int64_t ldos, int oscoff) {
+    const int c4 = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c4 >= (C >> 2)) return;
+    const int c = c4 * 4;
+    const float4 s = *reinterpret_cast<const float4*>(scale + c);
+    const float4 t = *reinterpret_cast<const float4*>(shift + c);
+    const int64_t r1 = min(M, (int64_t)(blockIdx.y + 1) * rps);
+    for (int64_t r = (int64_t)blockIdx.y * rps + threadIdx.y; r < r1; r += blockDim.y) {
+        const float4 v = load4<YB>(y, r * C + c);
         float4 o;
         o.x = fmaxf(v.x * s.x + t.x, 0.f);
         o.y = fmaxf(v.y * s.y + t.y, 0.f);
         o.z = fmaxf(v.z * s.z + t.z, 0.f);
         o.w = fmaxf(v.w * s.w + t.w, 0.f);
-        if (out) *reinterpret_cast<float4*>(out + r * ldo + ocoff + c) = o;   // nullptr: only the twin is read
+        if (out) *reinterpret_cast<float4*>(out + r * ldo + ocoff + c) = o;
         if constexpr (NP > 0) split4_store<NP>(os, ldos, oscoff, r, c, o);
     }
 }
 void bn_relu_fwd(const float* y, int C, const float* scale, const float* shift, float* out, int64_t ldo,
                  int ocoff, int64_t M, hipStream_t st, void* os, int64_t ldos, int oscoff, bool y_bf16) {
-    const int64_t n4 = M * C / 4;
     const int np = os ? split_planes() : 0;
     char* o = static_cast<char*>(os);
+    const RowGrid g = row_grid(M, C);
     auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3(ew_blocks(n4)), dim3(256), 0, st, y, C, scale, shift, out, ldo, ocoff, n4, o, ldos,
-                           oscoff);
+        hipLaunchKernelGGL(kern, dim3(cdiv(C >> 2, g.CX), g.S), dim3(g.CX, g.RY), 0, st, y, C, scale, shift, out, ldo,
+                           ocoff, M, g.rps, o, ldos, oscoff);
     };
-    if (np == 1) y_bf16 ? go(k_bn_relu_fwd<1, true>) : go(k_bn_relu_fwd<1, false>);
-    else y_bf16 ? go(k_bn_relu_fwd<0, true>) : go(k_bn_relu_fwd<0, false>);
+    if (np == 1) y_bf16 ? go(k_bn_relu_fwd_rows<1, true>) : go(k_bn_relu_fwd_rows<1, false>);
+    else y_bf16 ? go(k_bn_relu_fwd_rows<0, true>) : go(k_bn_relu_fwd_rows<0, false>);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -261,33 +281,43 @@ __global__ void k_bn_bwd_coef(const double* tot, int C, int64_t M, const float* 
     coef[2 * C + c] = (float)(k1 * sdzx / (double)M);
 }
 template <int NP, bool YB>
-__global__ void k_bn_relu_bwd(const float* __restrict__ g, int64_t ldg, int gcoff, const float* __restrict__ y,
-                              int C, const float* __restrict__ mean, const float* __restrict__ invstd,
-                              const float* __restrict__ scale, const float* __restrict__ shift,
-                              const float* __restrict__ coef, float* __restrict__ dy, int64_t n4,
-                              const float* __restrict__ gmul, int64_t HW, char* __restrict__ os, bool relu) {
-    const int C4 = C >> 2;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t r = i / C4;
-        const int c0 = (int)(i - r * C4) * 4;
+__global__ __launch_bounds__(256) void k_bn_relu_bwd_rows(const float* __restrict__ g, int64_t ldg, int gcoff,
+                                                          const float* __restrict__ y, int C,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd,
+                                                          const float* __restrict__ scale,
+                                                          const float* __restrict__ shift,
+                                                          const float* __restrict__ coef, float* __restrict__ dy,
+                                                          int64_t M, int64_t rps, const float* __restrict__ gmul,
+                                                          int64_t HW, char* __restrict__ os, bool relu) {
+    const int c4 = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c4 >= (C >> 2)) return;
+    const int c0 = c4 * 4;
+    float sc[4], sh[4], mu[4], is[4], k0[4], k1[4], k2[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        sc[e] = scale[c0 + e]; sh[e] = shift[c0 + e]; mu[e] = mean[c0 + e]; is[e] = invstd[c0 + e];
+        k0[e] = coef[c0 + e]; k1[e] = coef[C + c0 + e]; k2[e] = coef[2 * C + c0 + e];
+    }
+    const int64_t r1 = min(M, (int64_t)(blockIdx.y + 1) * rps);
+    for (int64_t r = (int64_t)blockIdx.y * rps + threadIdx.y; r < r1; r += blockDim.y) {
         float4 gv = *reinterpret_cast<const float4*>(g + r * ldg + gcoff + c0);
         if (gmul) {
             const float4 m = *reinterpret_cast<const float4*>(gmul + (r / HW) * C + c0);
             gv.x *= m.x; gv.y *= m.y; gv.z *= m.z; gv.w *= m.w;
         }
-        float4 yv = load4<YB>(y, i * 4);
+        const float4 yv = load4<YB>(y, r * C + c0);
         const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, ya[4] = {yv.x, yv.y, yv.z, yv.w};
         float o[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const int c = c0 + e;
-            const float z = ya[e] * scale[c] + shift[c];
+            const float z = ya[e] * sc[e] + sh[e];
             const float dz = (!relu || z > 0.f) ? ga[e] : 0.f;
-            const float xh = (ya[e] - mean[c]) * invstd[c];
-            o[e] = coef[c] * dz - coef[C + c] - coef[2 * C + c] * xh;
+            const float xh = (ya[e] - mu[e]) * is[e];
+            o[e] = k0[e] * dz - k1[e] - k2[e] * xh;
         }
         const float4 ov = make_float4(o[0], o[1], o[2], o[3]);
-        if (dy) *reinterpret_cast<float4*>(dy + i * 4) = ov;   // nullptr: only the twin is read
+        if (dy) *reinterpret_cast<float4*>(dy + r * C + c0) = ov;
         if constexpr (NP > 0) split4_store<NP>(os, C, 0, r, c0, ov);
     }
 }
@@ -303,15 +333,15 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
                                                M, C, part, st);
     launch_colfinal(part, S, 2 * C, tot, nullptr, 1.f, st);
     hipLaunchKernelGGL(k_bn_bwd_coef, dim3(cdiv(C, 64)), dim3(64), 0, st, tot, C, M, gamma, invstd, coef, dgamma, dbeta);
-    const int64_t n4 = M * C / 4;
     const int np = dy_split ? split_planes() : 0;
     char* os = static_cast<char*>(dy_split);
+    const RowGrid rg = row_grid(M, C);
     auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3(ew_blocks(n4)), dim3(256), 0, st, g, ldg, gcoff, y, C, mean, invstd, scale, shift,
-                           coef, dy, n4, gmul, HW, os, relu);
+        hipLaunchKernelGGL(kern, dim3(cdiv(C >> 2, rg.CX), rg.S), dim3(rg.CX, rg.RY), 0, st, g, ldg, gcoff, y, C, mean,
+                           invstd, scale, shift, coef, dy, M, rg.rps, gmul, HW, os, relu);
     };
-    if (np == 1) y_bf16 ? go(k_bn_relu_bwd<1, true>) : go(k_bn_relu_bwd<1, false>);
-    else y_bf16 ? go(k_bn_relu_bwd<0, true>) : go(k_bn_relu_bwd<0, false>);
+    if (np == 1) y_bf16 ? go(k_bn_relu_bwd_rows<1, true>) : go(k_bn_relu_bwd_rows<1, false>);
+    else y_bf16 ? go(k_bn_relu_bwd_rows<0, true>) : go(k_bn_relu_bwd_rows<0, false>);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -172,7 +172,7 @@ def test_film_train_step_vs_oracle(cad, dev, oracle, model, f, B, H, W):
         cos = torch.nn.functional.cosine_similarity(grads[n].double().reshape(1, -1), g64.reshape(1, -1)).item()
         # the 6x8 / 3x4 deep levels of these nets leave a few hundred pixels per BN channel, and
         # FiLM's BatchNorm1d sees B samples: LibTorch fp32 itself lands ~1e-2 off fp64 there
-        ok, st = grad_close(grads[n], g64, [g32], k=5.0)
+        ok, st = grad_close(grads[n], g64, [g32], k=5.0, bulk_floor=2e-2)
         assert cos > 0.999 and ok, (n, cos, st)
     ref64 = oracle.Trainer(params, bufs, dtype=torch.float64, model=model)
     ref64.step(rgb, gt, K)
