@@ -172,37 +172,49 @@ void film_mlp_fwd(const FilmLayer& L, const float* camn, int B, bool train, hipS
 // ------------------------------------------------------------------------------------------
 // a16/a17 affine: a1 = gamma[b,c] * relu(y1 * scale[c] + shift[c]) + beta[b,c]
 // ------------------------------------------------------------------------------------------
+// row-slice form (as the BN passes, nn_kernels.hip): a thread owns one 4-channel group, keeps its BN
+// scale / shift in registers and re-reads gamma / beta only when its rows cross into the next sample
 template <bool YB>
-__global__ void k_film_apply(const float* __restrict__ y, int C, const float* __restrict__ scale,
-                             const float* __restrict__ shift, const float* __restrict__ gam,
-                             const float* __restrict__ bet, int64_t HW, float* __restrict__ out, int64_t n4) {
-    const int C4 = C >> 2;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t r = i / C4;
-        const int c = (int)(i - r * C4) * 4;
-        const int64_t bc = (r / HW) * C + c;
-        const float4 v = load4<YB>(y, i * 4);
-        const float4 s = *reinterpret_cast<const float4*>(scale + c);
-        const float4 t = *reinterpret_cast<const float4*>(shift + c);
-        const float4 g = *reinterpret_cast<const float4*>(gam + bc);
-        const float4 b = *reinterpret_cast<const float4*>(bet + bc);
+__global__ __launch_bounds__(256) void k_film_apply(const float* __restrict__ y, int C, const float* __restrict__ scale,
+                                                    const float* __restrict__ shift, const float* __restrict__ gam,
+                                                    const float* __restrict__ bet, int64_t HW, float* __restrict__ out,
+                                                    int64_t M, int64_t rps) {
+    const int c4 = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c4 >= (C >> 2)) return;
+    const int c = c4 * 4;
+    const float4 s = *reinterpret_cast<const float4*>(scale + c);
+    const float4 t = *reinterpret_cast<const float4*>(shift + c);
+    int64_t cur = -1;
+    float4 g = make_float4(0.f, 0.f, 0.f, 0.f), b = g;
+    const int64_t r1 = min(M, (int64_t)(blockIdx.y + 1) * rps);
+    for (int64_t r = (int64_t)blockIdx.y * rps + threadIdx.y; r < r1; r += blockDim.y) {
+        const int64_t smp = r / HW;
+        if (smp != cur) {
+            cur = smp;
+            g = *reinterpret_cast<const float4*>(gam + smp * C + c);
+            b = *reinterpret_cast<const float4*>(bet + smp * C + c);
+        }
+        const float4 v = load4<YB>(y, r * C + c);
         float4 o;
         o.x = g.x * fmaxf(v.x * s.x + t.x, 0.f) + b.x;
         o.y = g.y * fmaxf(v.y * s.y + t.y, 0.f) + b.y;
         o.z = g.z * fmaxf(v.z * s.z + t.z, 0.f) + b.z;
         o.w = g.w * fmaxf(v.w * s.w + t.w, 0.f) + b.w;
-        *reinterpret_cast<float4*>(out + i * 4) = o;
+        *reinterpret_cast<float4*>(out + r * C + c) = o;
     }
 }
 void film_apply(const float* y, int C, const float* scale, const float* shift, const float* gam, const float* bet,
                 int B, int64_t HW, float* out, hipStream_t st, bool y_bf16) {
-    const int64_t n4 = (int64_t)B * HW * C / 4;
+    const int64_t M = (int64_t)B * HW;
+    const int C4 = C >> 2, CX = std::min(C4, 64), RY = std::max(1, 256 / CX);
+    const int S = (int)std::max<int64_t>(1, std::min<int64_t>(65535, cdiv(M, (int64_t)RY * 16)));
+    const int64_t rps = (M + S - 1) / S;
     if (y_bf16)
-        hipLaunchKernelGGL(k_film_apply<true>, dim3(ew_blocks(n4)), dim3(256), 0, st, y, C, scale, shift, gam, bet, HW, out,
-                           n4);
+        hipLaunchKernelGGL(k_film_apply<true>, dim3(cdiv(C4, CX), S), dim3(CX, RY), 0, st, y, C, scale, shift, gam, bet,
+                           HW, out, M, rps);
     else
-        hipLaunchKernelGGL(k_film_apply<false>, dim3(ew_blocks(n4)), dim3(256), 0, st, y, C, scale, shift, gam, bet, HW,
-                           out, n4);
+        hipLaunchKernelGGL(k_film_apply<false>, dim3(cdiv(C4, CX), S), dim3(CX, RY), 0, st, y, C, scale, shift, gam, bet,
+                           HW, out, M, rps);
 }
 
 // ------------------------------------------------------------------------------------------
