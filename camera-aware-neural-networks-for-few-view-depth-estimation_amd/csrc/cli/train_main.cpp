@@ -162,7 +162,8 @@ Config load_config(const yaml_lite::Node& y, const std::string& experiment) {   
         c.architecture = m["architecture"].as<std::string>("baseline_unet");
         if (c.architecture != "baseline_unet" && c.architecture != "intrinsics_unet" && c.architecture != "ray_film_unet")
             throw std::runtime_error("model.architecture '" + c.architecture +
-                                     "': this build trains baseline_unet, intrinsics_unet or ray_film_unet");
+                                     "': this CLI trains baseline_unet, intrinsics_unet or ray_film_unet (the geometry_aware "
+                                     "networks train through cad_geonet_* / GeometryAwareNetworkImpl, INTEGRATION.md)");
     }
     if (auto& d = y["data"]) {
         c.height = d["input_height"].as<int>(240);

@@ -354,3 +354,122 @@ def test_op_pcl_vs_autograd(cad, dev, oracle, B, H, W, C, scale):
         k = int(torch.tensor(s).prod())
         assert max_rel_err(grd[off: off + k].cpu().view(s), p["q." + n].grad) < 1e-4, n
         off += k
+
+
+def test_geonet_bf16_engine_step(cad, dev, oracle):
+    """The geometry-aware net on the bf16 contraction engine (CAD_GEMM_BF16: bf16-rounded operands, fp32
+    accumulation): a train step runs, and its prediction stays within bf16 operand rounding of the
+    fp32 (S3) one."""
+    B, H, W, f = 2, 64, 96, 16
+    params, bufs = oracle.synth_init(f, model="geo"), oracle.init_buffers(f, model="geo")
+    st = dict(params)
+    st.update(bufs)
+    rgb, gt, K = [torch.from_numpy(a).to(dev) for a in oracle.synth_batch(B, H, W)]
+    lib = cad.load_library()
+    prev = lib.cad_get_gemm_engine()
+    preds = {}
+    try:
+        for eng in (1, 2):
+            lib.cad_set_gemm_engine(eng)
+            net = _net(cad, "geo", f, B, H, W)
+            net.load_state_dict(st)
+            loss = cad.CombinedDepthLoss(batch=B, height=H, width=W)
+            l5, pred = net.train_step(loss, rgb, gt, K)
+            torch.cuda.synchronize()
+            assert torch.isfinite(l5).all() and all(torch.isfinite(g).all() for g in net.grads().values())
+            preds[eng] = pred.cpu()
+    finally:
+        lib.cad_set_gemm_engine(prev)
+    assert max_rel_err(preds[2], preds[1]) < 2e-2
+
+
+# ---------------- data-parallel (two ranks sharing cuda:0 over gloo) ----------------
+def _geo_dp_worker(rank, world, port, q):
+    import os
+    import sys
+    import numpy as np
+    import torch.distributed as dist
+    from conftest import ROOT
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, ROOT)
+    import cad_pkg
+    cad = cad_pkg.load()
+    from oracle import cad_oracle as O
+    try:
+        dev = torch.device("cuda", 0)
+        B, H, W, f = 2, 64, 64, 8
+        st = dict(O.synth_init(f, model="geolite"))
+        st.update(O.init_buffers(f, model="geolite"))
+        rgb, gt, K = [torch.from_numpy(a) for a in O.synth_batch(B * world, H, W)]
+        sl = slice(rank * B, (rank + 1) * B)
+        net = cad.LightweightGeometryNetwork(3, f, 4, 10.0, batch=B, height=H, width=W)
+        net.load_state_dict(st)
+        loss = cad.CombinedDepthLoss(batch=B, height=H, width=W)
+        l5, _ = net.train_step(loss, rgb[sl].to(dev), gt[sl].to(dev), K[sl].to(dev), process_group=dist.group.WORLD)
+        torch.cuda.synchronize()
+        q.put((rank, l5[0].item(), {k: v.numpy() for k, v in net.named_parameters().items()}, net.last_grad_norm(),
+               None))
+    except Exception as e:   # report instead of hanging the parent on q.get
+        q.put((rank, None, None, None, repr(e)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_geonet_data_parallel_two_ranks(cad, dev, oracle):
+    """GeometryAwareNetwork.train_step(process_group=...) (the flat gradient slab SUM-all-reduced, the
+    1/world mean folded into the clip) on two ranks: replicas stay identical and equal a single-process
+    emulation of the same two shards (per-shard forward / backward with each shard's own BatchNorm
+    statistics, mean gradient, clip, Adam)."""
+    import multiprocessing as mp
+    import socket
+    from cad_amd.model import _flat_view
+    world = 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_geo_dp_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r[0]: r[1:] for r in (q.get(timeout=240) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[-1] is None for r in res.values()), [r[-1] for r in res.values()]
+    for n in res[0][1]:
+        assert (res[0][1][n] == res[1][1][n]).all(), n
+    assert res[0][2] == res[1][2]
+    # emulation in this process: shard gradients, mean, clip + Adam on a third replica
+    B, H, W, f = 2, 64, 64, 8
+    st = dict(oracle.synth_init(f, model="geolite"))
+    st.update(oracle.init_buffers(f, model="geolite"))
+    rgb, gt, K = [torch.from_numpy(a).to(dev) for a in oracle.synth_batch(B * world, H, W)]
+    gs, losses = [], []
+    for r in range(world):
+        net = cad.LightweightGeometryNetwork(3, f, 4, 10.0, batch=B, height=H, width=W)
+        net.load_state_dict(st)
+        loss = cad.CombinedDepthLoss(batch=B, height=H, width=W)
+        sl = slice(r * B, (r + 1) * B)
+        rays = cad.ray_directions(K[sl], H, W)
+        pred = net.forward(rgb[sl], rays, cad.camera_from_K(K[sl]))
+        l5, dpred = loss.forward_with_intrinsics(pred, gt[sl], rgb[sl], K[sl])
+        net.backward(dpred)
+        torch.cuda.synchronize()
+        gs.append(_flat_view(net.flat_grads_ptr(), net.n_flat, dev).clone())
+        losses.append(l5[0].item())
+        assert abs(res[r][0] - losses[-1]) <= 1e-6 * abs(losses[-1]), (r, res[r][0], losses[-1])
+    ref = cad.LightweightGeometryNetwork(3, f, 4, 10.0, batch=B, height=H, width=W)
+    ref.load_state_dict(st)
+    _flat_view(ref.flat_grads_ptr(), ref.n_flat, dev).copy_(gs[0] + gs[1])
+    ref.clip_grad_norm_(1.0, 1.0 / world)
+    ref.adam_step(lr=1e-4, weight_decay=1e-5)
+    torch.cuda.synchronize()
+    assert abs(ref.last_grad_norm() - res[0][2]) <= 1e-6 * res[0][2]
+    # PCL's input gradient is an atomic scatter, so the two runs agree to rounding, not bit for bit:
+    # Adam's first step (~lr * g / |g|) then differs only where a gradient is rounding noise — the
+    # Linear biases in front of FiLM's BatchNorm1d, whose true gradient is 0 — by at most 2 lr
+    for n, v in ref.named_parameters().items():
+        d = (v - torch.from_numpy(res[0][1][n])).abs().max().item()
+        assert d <= (2e-4 + 1e-7 if _zero_grad_bias(n, B) else 1e-6), (n, d)
