@@ -14,7 +14,8 @@
 // Deliberate differences: the model lives on the GPU (the reference never moves it,
 // SURVEY §0 fact 2); --resume really resumes (params + BN buffers + Adam state; the reference parses
 // and ignores it); TensorBoard events are written as a CSV of scalars (no Python tensorboard here);
-// model.architecture selects the FiLM models (the reference always builds BaselineUNet);
+// model.architecture selects the FiLM models and the geometry-aware networks (model.variant,
+// use_pcl, use_attention; single process) — the reference always builds BaselineUNet;
 // data.dataset_name "synthetic" trains on generated samples, anything else on the manifest's PNG/PNM
 // files (JPEG decoding needs a decoder this image lacks); hardware.distributed runs DP over RCCL.
 #include <signal.h>
@@ -106,6 +107,8 @@ struct Config {   // the TrainingConfig fields the step uses (trainer.h:24-92)
     std::string manifest_path = "./data/sunrgbd_manifest.json";
     std::vector<std::string> sensor_types;   // data.sensor_types (empty: all four)
     std::string architecture = "baseline_unet";
+    std::string variant = "full";             // model.variant (geometry_aware: "full" / "lightweight")
+    bool use_pcl = true, use_attention = true;
     int n_train = 64, n_val = 16;
     // data.augmentation (train_main.cpp:377-386 -> AugmentationConfig, random_seed 42)
     bool aug_crop = true, aug_flip = true, aug_jitter = true;
@@ -160,10 +163,17 @@ Config load_config(const yaml_lite::Node& y, const std::string& experiment) {   
         // the reference parses model.architecture and always builds BaselineUNet; here it selects the
         // FiLM models of configs 3 (intrinsics_unet: FiLM blocks; ray_film_unet: + ray-enhanced enc1)
         c.architecture = m["architecture"].as<std::string>("baseline_unet");
-        if (c.architecture != "baseline_unet" && c.architecture != "intrinsics_unet" && c.architecture != "ray_film_unet")
+        if (c.architecture != "baseline_unet" && c.architecture != "intrinsics_unet" && c.architecture != "ray_film_unet" &&
+            c.architecture != "geometry_aware")
             throw std::runtime_error("model.architecture '" + c.architecture +
-                                     "': this CLI trains baseline_unet, intrinsics_unet or ray_film_unet (the geometry_aware "
-                                     "networks train through cad_geonet_* / GeometryAwareNetworkImpl, INTEGRATION.md)");
+                                     "': this CLI trains baseline_unet, intrinsics_unet, ray_film_unet or geometry_aware");
+        // geometry_aware (train_config.yaml:51-57 and its experiments): model.variant full /
+        // lightweight, use_pcl, use_attention (GeometryAwareNetworkImpl / LightweightGeometryNetworkImpl)
+        c.variant = m["variant"].as<std::string>("full");
+        c.use_pcl = m["use_pcl"].as<bool>(true);
+        c.use_attention = m["use_attention"].as<bool>(true);
+        if (c.architecture == "geometry_aware" && c.variant != "full" && c.variant != "lightweight")
+            throw std::runtime_error("model.variant '" + c.variant + "': expected full or lightweight");
     }
     if (auto& d = y["data"]) {
         c.height = d["input_height"].as<int>(240);
@@ -424,6 +434,39 @@ int run(const Args& args) {
         if (L) L->setTargetDimensions(c.height, c.width);
 
     cad::Workspace ws{c.batch_size, c.height, c.width, R.device};
+    if (c.architecture == "geometry_aware") {   // single-process GeometryTrainer (trainer.hpp)
+        if (R.dp) throw std::runtime_error("geometry_aware trains on one GPU here (hardware.distributed: false)");
+        if (!args.resume.empty()) throw std::runtime_error("--resume is not supported for geometry_aware");
+        std::shared_ptr<GeometryAwareNetworkImpl> geo;
+        if (c.variant == "lightweight")
+            geo = std::make_shared<LightweightGeometryNetworkImpl>(3, c.init_features, 4, c.max_depth, ws);
+        else
+            geo = std::make_shared<GeometryAwareNetworkImpl>(3, c.init_features, 4, c.max_depth, c.use_pcl,
+                                                             c.use_attention, ws);
+        auto gloss = std::make_shared<CombinedDepthLoss>(c.si, c.grad, c.smooth, c.reproj, ws);
+        std::cout << "Model: geometry_aware/" << c.variant << " (f=" << c.init_features << ", pcl " << c.use_pcl
+                  << ", attention " << c.use_attention << "), parameters: " << geo->count_parameters()
+                  << "\nUsing MI355X device " << R.device << "\nTraining samples: " << c.n_train
+                  << (real ? " (" + c.manifest_path + ")" : std::string(" (synthetic)")) << "\n";
+        TensorBoardTrainerEnhanced::Config gc;
+        gc.num_epochs = c.num_epochs;
+        gc.batch_size = c.batch_size;
+        gc.learning_rate = c.learning_rate;
+        gc.weight_decay = c.weight_decay;
+        gc.use_grad_clip = c.use_grad_clip;
+        gc.grad_clip_value = c.grad_clip_value;
+        gc.val_interval = c.val_interval;
+        gc.log_interval = c.log_interval;
+        gc.save_interval = c.save_interval;
+        gc.checkpoint_dir = c.checkpoint_dir;
+        gc.log_dir = c.log_dir;
+        gc.experiment_name = c.experiment_name;
+        gc.device = R.device;
+        GeometryTrainer gt(geo, gloss, gc);
+        gt.train(train_loader, val_loader);
+        std::cout << "Training complete.\n";
+        return 0;
+    }
     std::shared_ptr<BaselineUNetImpl> model;
     if (c.architecture == "intrinsics_unet")
         model = std::make_shared<IntrinsicsConditionedUNetImpl>(3, c.init_features, 4, c.max_depth, ws);

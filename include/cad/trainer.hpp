@@ -517,6 +517,159 @@ private:
     DeviceTensor rgb_, gt_, K_, pred_, cam_;
 };
 
+// The same training loop (enhanced.h:142-240, 257-395) for the geometry-aware networks
+// (geometry_aware_network.h: GeometryAwareNetworkImpl / LightweightGeometryNetworkImpl), fed the
+// loader's batch as the reference's forward takes it: rgb, RayDirectionComputer's rays (a18) and the
+// (B,4) intrinsics (a15).  Single process; the Adam moments live in the model; checkpoints are
+// <exp>_epoch_N.cadckpt / final_model.cadckpt (named parameters and buffers, reference layout).
+class GeometryTrainer {
+public:
+    using Config = TensorBoardTrainerEnhanced::Config;
+    GeometryTrainer(std::shared_ptr<GeometryAwareNetworkImpl> model, std::shared_ptr<CombinedDepthLoss> loss_fn,
+                    const Config& config)
+        : model_(std::move(model)), loss_fn_(std::move(loss_fn)), config_(config) {
+        if (!model_ || !loss_fn_) throw std::runtime_error("GeometryTrainer: model and loss are required");
+        std::filesystem::create_directories(config_.checkpoint_dir);
+        std::filesystem::create_directories(config_.log_dir);
+        log_.open(config_.log_dir + "/training.log", std::ios::app);
+        metrics_csv_.open(config_.log_dir + "/metrics.csv", std::ios::app);
+        if (metrics_csv_.tellp() == 0)
+            metrics_csv_ << "epoch,step,train_loss,val_loss,abs_rel,sq_rel,rmse,rmse_log,a1,a2,a3,learning_rate,time_elapsed\n";
+    }
+
+    void train(std::shared_ptr<SunRGBDLoader> train_loader, std::shared_ptr<SunRGBDLoader> val_loader = nullptr) {
+        if (!train_loader) throw std::runtime_error("train: no training loader");
+        const int B = config_.batch_size;
+        const int nb = (int)(((int64_t)train_loader->size() + B - 1) / B);
+        if (nb < 1) throw std::runtime_error("no training samples");
+        msg("=== Starting Training (MI355X, geometry-aware network) ===");
+        msg("Train samples: " + std::to_string(train_loader->size()) + ", batch size " + std::to_string(B) +
+            ", epochs " + std::to_string(config_.num_epochs));
+        const auto t0 = std::chrono::steady_clock::now();
+        int64_t step = 0;
+        for (int epoch = 1; epoch <= config_.num_epochs; ++epoch) {
+            std::cout << "\n" << std::string(60, '=') << "\nEpoch " << epoch << "/" << config_.num_epochs << "\n";
+            const float tl = trainEpoch(*train_loader, nb, step);
+            TensorBoardTrainerEnhanced::ValidationMetrics vm;
+            if (val_loader && config_.val_interval > 0 && epoch % config_.val_interval == 0) vm = validate(*val_loader);
+            if (config_.save_interval > 0 && epoch % config_.save_interval == 0)
+                save(config_.checkpoint_dir + "/" + config_.experiment_name + "_epoch_" + std::to_string(epoch) +
+                     ".cadckpt");
+            const long el = (long)std::chrono::duration_cast<std::chrono::seconds>(std::chrono::steady_clock::now() - t0).count();
+            std::stringstream ss;
+            ss << "Epoch " << epoch << " | Train Loss: " << std::fixed << std::setprecision(4) << tl;
+            if (vm.loss > 0) ss << " | Val Loss: " << vm.loss << " | abs_rel: " << vm.abs_rel << " | rmse: " << vm.rmse;
+            msg(ss.str());
+            metrics_csv_ << epoch << "," << step << "," << tl << "," << vm.loss << "," << vm.abs_rel << "," << vm.sq_rel
+                         << "," << vm.rmse << "," << vm.rmse_log << "," << vm.a1 << "," << vm.a2 << "," << vm.a3 << ","
+                         << config_.learning_rate << "," << el << "\n";
+            metrics_csv_.flush();
+            step += nb;
+        }
+        save(config_.checkpoint_dir + "/final_model.cadckpt");
+        msg("=== Training Complete ===");
+    }
+
+    // named parameters and buffers in the .cadckpt layout (no optimizer section)
+    void save(const std::string& path) {
+        std::ofstream f(path, std::ios::binary);
+        if (!f) throw std::runtime_error("cannot write checkpoint " + path);
+        auto ts = model_->named_parameters();
+        auto bs = model_->named_buffers();
+        ts.insert(ts.end(), bs.begin(), bs.end());
+        f.write("CADCKPT1", 8);
+        const int32_t n = (int32_t)ts.size();
+        f.write((const char*)&n, 4);
+        for (auto& t : ts) {
+            const int32_t ln = (int32_t)t.name.size(), nd = (int32_t)t.shape.size();
+            f.write((const char*)&ln, 4);
+            f.write(t.name.data(), ln);
+            f.write((const char*)&nd, 4);
+            f.write((const char*)t.shape.data(), 8 * nd);
+            f.write((const char*)t.value.data(), 4 * (int64_t)t.value.size());
+        }
+        msg("Checkpoint saved: " + path);
+    }
+
+private:
+    void ensure(const SunRGBDLoader& L) {
+        const int B = config_.batch_size, H = L.target_height(), W = L.target_width(), d = config_.device;
+        if (rgb_.numel() == (int64_t)B * 3 * H * W) return;
+        rgb_ = DeviceTensor::empty({B, 3, H, W}, d);
+        gt_ = DeviceTensor::empty({B, 1, H, W}, d);
+        K_ = DeviceTensor::empty({B, 3, 3}, d);
+        rays_ = DeviceTensor::empty({B, 3, H, W}, d);
+        cam_ = DeviceTensor::empty({B, 4}, d);
+    }
+    int next(cad_loader* ring) {
+        const int n = cad_loader_next(ring, rgb_.data, gt_.data, K_.data, nullptr);
+        if (n < 0) throw std::runtime_error(std::string("data loader: ") + cad_last_error());
+        for (DeviceTensor* t : {&rgb_, &gt_, &K_, &rays_, &cam_}) t->shape[0] = n;
+        const int H = (int)rgb_.size(2), W = (int)rgb_.size(3);
+        cad::check(cad_ray_directions(K_.data, n, H, W, rays_.data, nullptr), "rays");   // a18
+        cad::check(cad_camera_from_K(K_.data, n, cam_.data, nullptr), "camera_from_K");  // a15
+        return n;
+    }
+    float trainEpoch(SunRGBDLoader& L, int nb, int64_t step0) {
+        ensure(L);
+        model_->train();
+        cad_loader* ring = L.ring(config_.batch_size, config_.device, true);
+        cad::check(cad_loader_start_epoch(ring, nullptr, (int64_t)L.size()), "start epoch");
+        double total = 0.0;
+        int64_t seen = 0;
+        for (int bi = 0; bi < nb; ++bi) {
+            const int n = next(ring);
+            DeviceTensor pred = model_->forward(rgb_, rays_, cam_);
+            DeviceTensor l = loss_fn_->forwardWithIntrinsics(pred, gt_, rgb_, K_);
+            model_->backward(loss_fn_->dpred());
+            model_->clip_grad_norm_(config_.use_grad_clip ? config_.grad_clip_value : INFINITY);
+            model_->adam_step(config_.learning_rate, config_.weight_decay);
+            const float lv = l.to_host()[0];
+            if (!std::isfinite(lv)) throw std::runtime_error("non-finite loss at step " + std::to_string(step0 + bi));
+            total += (double)lv * n;
+            seen += n;
+            if ((bi + 1) % std::max(1, config_.log_interval) == 0 || bi == nb - 1)
+                std::cout << "\r  [" << std::setw(3) << (100 * (bi + 1) / nb) << "%] Batch " << (bi + 1) << "/" << nb
+                          << " | Loss: " << std::fixed << std::setprecision(4) << lv << std::flush;
+        }
+        std::cout << std::endl;
+        return (float)(total / std::max<int64_t>(1, seen));
+    }
+    TensorBoardTrainerEnhanced::ValidationMetrics validate(SunRGBDLoader& L) {
+        ensure(L);
+        model_->eval();
+        TensorBoardTrainerEnhanced::ValidationMetrics m;
+        const int64_t ns = std::min<int64_t>(500, (int64_t)L.size());
+        cad_loader* ring = L.ring(1, config_.device, false);
+        cad::check(cad_loader_start_epoch(ring, nullptr, ns), "validation");
+        int count = 0;
+        for (int64_t i = 0; i < ns; ++i) {
+            next(ring);
+            DeviceTensor pred = model_->forward(rgb_, rays_, cam_);
+            DeviceTensor l = loss_fn_->forwardWithIntrinsics(pred, gt_, rgb_, K_);
+            const DepthMetrics s = computeDepthMetrics(pred, gt_);
+            m.loss += l.to_host()[0];
+            m.abs_rel += s.abs_rel; m.sq_rel += s.sq_rel; m.rmse += s.rmse; m.rmse_log += s.rmse_log;
+            m.a1 += s.a1; m.a2 += s.a2; m.a3 += s.a3;
+            ++count;
+        }
+        if (count)
+            for (float* p : {&m.loss, &m.abs_rel, &m.sq_rel, &m.rmse, &m.rmse_log, &m.a1, &m.a2, &m.a3}) *p /= count;
+        model_->train();
+        return m;
+    }
+    void msg(const std::string& s) {
+        std::cout << s << std::endl;
+        if (log_.is_open()) { log_ << s << "\n"; log_.flush(); }
+    }
+
+    std::shared_ptr<GeometryAwareNetworkImpl> model_;
+    std::shared_ptr<CombinedDepthLoss> loss_fn_;
+    Config config_;
+    std::ofstream log_, metrics_csv_;
+    DeviceTensor rgb_, gt_, K_, rays_, cam_;
+};
+
 }  // namespace camera_aware_depth
 
 #endif  // CAD_TRAINER_HPP

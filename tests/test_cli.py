@@ -121,15 +121,21 @@ def _dp_cfg(tmp_path, **hw):
 
 
 def test_cli_model_architecture_key(train_bin, tmp_path):
-    """model.architecture selects the network (the reference parses it and always builds BaselineUNet);
-    an architecture this build does not train is refused before any GPU call."""
+    """model.architecture selects the network (the reference parses it and always builds BaselineUNet),
+    model.variant the geometry-aware one; an architecture / variant this build does not train is
+    refused before any GPU call."""
     p = _dp_cfg(tmp_path, distributed=False)
     cfg = yaml.safe_load(p.read_text())
-    cfg["model"]["architecture"] = "geometry_aware"
+    cfg["model"]["architecture"] = "vision_transformer"
     p.write_text(yaml.safe_dump(cfg))
     r = subprocess.run([train_bin, "-c", str(p), "--dry-run"], capture_output=True, text=True, timeout=60)
-    assert r.returncode == 1 and r.stderr.startswith("Error: model.architecture 'geometry_aware'")
-    for arch in ("baseline_unet", "intrinsics_unet", "ray_film_unet"):
+    assert r.returncode == 1 and r.stderr.startswith("Error: model.architecture 'vision_transformer'")
+    cfg["model"].update(architecture="geometry_aware", variant="tiny")
+    p.write_text(yaml.safe_dump(cfg))
+    r = subprocess.run([train_bin, "-c", str(p), "--dry-run"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and r.stderr.startswith("Error: model.variant 'tiny'")
+    cfg["model"]["variant"] = "lightweight"
+    for arch in ("baseline_unet", "intrinsics_unet", "ray_film_unet", "geometry_aware"):
         cfg["model"]["architecture"] = arch
         p.write_text(yaml.safe_dump(cfg))
         r = subprocess.run([train_bin, "-c", str(p), "--dry-run"], capture_output=True, text=True, timeout=60)
@@ -164,6 +170,34 @@ def test_cli_trains_film_models(train_bin, tmp_path, arch):
         assert tuple(sd["enc1.conv1.weight"].shape) == (8, 6, 3, 3)   # rgb + rays
     tb = (tmp_path / "logs" / "baseline_unet" / "tensorboard_scalars.csv").read_text()
     assert "loss_components/reproj_loss,2," in tb and "metrics/abs_rel,2," in tb
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant,pcl,att", [("full", True, True), ("lightweight", True, True), ("full", False, False)])
+def test_cli_trains_geometry_aware(train_bin, tmp_path, variant, pcl, att):
+    """model.architecture: geometry_aware (train_config.yaml:44-57 and its geometry_aware_full /
+    _lightweight / ablation_rays_only experiments) through build/train: GeometryTrainer over
+    GeometryAwareNetworkImpl / LightweightGeometryNetworkImpl, per-sample validation, metrics.csv,
+    .cadckpt checkpoints."""
+    cfg = yaml.safe_load(open(os.path.join(ROOT, "configs", "train_config.yaml")))
+    cfg["data"].update(dataset_name="synthetic", num_train_samples=8, num_val_samples=3, input_height=64,
+                       input_width=64)
+    cfg["model"].update(architecture="geometry_aware", variant=variant, use_pcl=pcl, use_attention=att,
+                        init_features=8)
+    cfg["training"].update(num_epochs=2, batch_size=4, val_interval=1)
+    cfg["checkpointing"].update(checkpoint_dir=str(tmp_path / "ckpt"), save_interval=1)
+    cfg["logging"]["log_dir"] = str(tmp_path / "logs")
+    p = tmp_path / "cfg.yaml"
+    p.write_text(yaml.safe_dump(cfg))
+    r = subprocess.run([train_bin, "-c", str(p)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert f"Model: geometry_aware/{variant}" in r.stdout
+    rows = (tmp_path / "logs" / "baseline_unet" / "metrics.csv").read_text().strip().splitlines()
+    assert [row.split(",")[:2] for row in rows[1:]] == [["1", "0"], ["2", "2"]]
+    vals = [float(x) for x in rows[-1].split(",")[2:5]]
+    assert all(v == v and v > 0 for v in vals)
+    assert (tmp_path / "ckpt" / "baseline_unet" / "final_model.cadckpt").exists()
+    assert (tmp_path / "ckpt" / "baseline_unet" / "baseline_unet_epoch_2.cadckpt").exists()
 
 
 def test_cli_data_parallel_plan(train_bin, tmp_path, cad):
