@@ -141,7 +141,9 @@ void launch_colfinal(const double* part, int S, int N, double* tot, float* dst, 
 
 // >= 128 rows per slice, at most 512 slices (monotone in R: scratch is sized at the largest R).  The
 // narrow reductions (GEMM tile partials: M/128 rows) then still spread over 512 workgroups.
-int colsum_slices(int64_t R) { return (int)std::max<int64_t>(1, std::min<int64_t>(512, R / 128)); }
+// up to 2048 slices of >= 256 rows: a level-0 reduction (9.8 M rows x 16 channel quads) then runs
+// 2048 workgroups, ~8 per CU (512 left it latency-bound at 2 per CU)
+int colsum_slices(int64_t R) { return (int)std::max<int64_t>(1, std::min<int64_t>(2048, R / 256)); }
 
 void colsum(const float* x, int64_t ld, int coff, int64_t R, int C, double* part, hipStream_t st) {
     launch_colreduce<1>(OpSum{x, ld, coff}, R, C, part, st);
