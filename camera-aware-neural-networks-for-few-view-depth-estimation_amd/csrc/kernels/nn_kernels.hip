@@ -36,8 +36,10 @@ __global__ void k_colreduce(Op op, int64_t R, int C, int64_t rows_per_slice, dou
     for (int o = 0; o < NOUT; ++o)
 #pragma unroll
         for (int e = 0; e < 4; ++e) acc[o][e] = 0.0;
-    if (c4 < C4)
-        for (int64_t r = r0 + threadIdx.y; r < r1; r += RY) op(r, c4, acc);
+    if (c4 < C4) {
+        const auto pc = op.prep(c4);   // per-thread channel coefficients, loaded once
+        for (int64_t r = r0 + threadIdx.y; r < r1; r += RY) op(r, c4, acc, pc);
+    }
     extern __shared__ double red[];   // [RY][CX][NOUT*4]
     double* mine = red + ((int64_t)threadIdx.y * CX + threadIdx.x) * NOUT * 4;
 #pragma unroll
@@ -81,18 +83,32 @@ __global__ void k_colfinal(const double* part, int S, int N, double* tot, float*
 }
 
 namespace {
+struct NoPrep {};
 struct OpSum {
     const float* x; int64_t ld; int coff;
-    __device__ void operator()(int64_t r, int c4, double (&acc)[1][4]) const {
+    __device__ NoPrep prep(int) const { return {}; }
+    __device__ void operator()(int64_t r, int c4, double (&acc)[1][4], NoPrep) const {
         float4 v = *reinterpret_cast<const float4*>(x + r * ld + coff + c4 * 4);
         acc[0][0] += v.x; acc[0][1] += v.y; acc[0][2] += v.z; acc[0][3] += v.w;
     }
+};
+struct BnCoef {
+    float sc[4], sh[4], mu[4], is[4];
 };
 template <bool YB>
 struct OpBnBwd {
     const float *g, *y, *mean, *invstd, *scale, *shift, *gmul;
     int64_t ldg; int gcoff, C; int64_t HW; bool relu;
-    __device__ void operator()(int64_t r, int c4, double (&acc)[2][4]) const {
+    __device__ BnCoef prep(int c4) const {
+        BnCoef k;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int c = c4 * 4 + e;
+            k.sc[e] = scale[c]; k.sh[e] = shift[c]; k.mu[e] = mean[c]; k.is[e] = invstd[c];
+        }
+        return k;
+    }
+    __device__ void operator()(int64_t r, int c4, double (&acc)[2][4], const BnCoef& k) const {
         float4 gv = *reinterpret_cast<const float4*>(g + r * ldg + gcoff + c4 * 4);
         if (gmul) {
             const float4 m = *reinterpret_cast<const float4*>(gmul + (r / HW) * C + c4 * 4);
@@ -102,10 +118,9 @@ struct OpBnBwd {
         const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, ya[4] = {yv.x, yv.y, yv.z, yv.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const int c = c4 * 4 + e;
-            const float z = ya[e] * scale[c] + shift[c];
+            const float z = ya[e] * k.sc[e] + k.sh[e];
             const float dz = (!relu || z > 0.f) ? ga[e] : 0.f;
-            const float xh = (ya[e] - mean[c]) * invstd[c];
+            const float xh = (ya[e] - k.mu[e]) * k.is[e];
             acc[0][e] += dz;
             acc[1][e] += (double)dz * xh;
         }
@@ -113,7 +128,8 @@ struct OpBnBwd {
 };
 struct OpHeadBwd {
     const float *a, *dpred, *sig; float md; int C;
-    __device__ void operator()(int64_t r, int c4, double (&acc)[2][4]) const {
+    __device__ NoPrep prep(int) const { return {}; }
+    __device__ void operator()(int64_t r, int c4, double (&acc)[2][4], NoPrep) const {
         const float s = sig[r];
         const float dp = dpred[r] * md * ((1.f - s) * s);
         float4 v = *reinterpret_cast<const float4*>(a + r * C + c4 * 4);
@@ -352,12 +368,12 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
 template <int NP>
 __global__ void k_maxpool_fwd(const float* __restrict__ x, int64_t ldx, int C, int B, int H, int W,
                               float* __restrict__ out, uint8_t* __restrict__ idx, int64_t n4, char* __restrict__ os) {
-    const int C4 = C >> 2, Ho = H >> 1, Wo = W >> 1;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t op = i / C4;
+    const uint32_t C4 = (uint32_t)C >> 2, Ho = (uint32_t)H >> 1, Wo = (uint32_t)W >> 1;   // n4 < 2^31 (host)
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (uint32_t)n4; i += gridDim.x * blockDim.x) {
+        const uint32_t op = i / C4;
         const int c = (int)(i - op * C4) * 4;
         const int xo = (int)(op % Wo);
-        const int64_t t = op / Wo;
+        const uint32_t t = op / Wo;
         const int yo = (int)(t % Ho);
         const int b = (int)(t / Ho);
         const int64_t p00 = ((int64_t)b * H + 2 * yo) * W + 2 * xo;
@@ -377,14 +393,15 @@ __global__ void k_maxpool_fwd(const float* __restrict__ x, int64_t ldx, int C, i
                 if (va[e] > best[e] || isnan(va[e])) { best[e] = va[e]; arg[e] = (uint8_t)k; }
         }
         const float4 o = make_float4(best[0], best[1], best[2], best[3]);
-        if (out) *reinterpret_cast<float4*>(out + op * C + c) = o;   // nullptr: only the twin is read
+        if (out) *reinterpret_cast<float4*>(out + (int64_t)op * C + c) = o;   // nullptr: only the twin is read
         if constexpr (NP > 0) split4_store<NP>(os, C, 0, op, c, o);
-        *reinterpret_cast<uchar4*>(idx + op * C + c) = make_uchar4(arg[0], arg[1], arg[2], arg[3]);
+        *reinterpret_cast<uchar4*>(idx + (int64_t)op * C + c) = make_uchar4(arg[0], arg[1], arg[2], arg[3]);
     }
 }
 void maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float* out, uint8_t* idx,
                  hipStream_t st, void* out_split) {
     const int64_t n4 = (int64_t)B * (H / 2) * (W / 2) * C / 4;
+    if (n4 >= ((int64_t)1 << 31)) throw std::runtime_error("maxpool_fwd: tensor too large for 32-bit indexing");
     const int np = out_split ? split_planes() : 0;
     char* os = static_cast<char*>(out_split);
     if (np == 1)
@@ -394,34 +411,40 @@ void maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float*
 }
 // gather form: one thread per (INPUT pixel, 4 channels) inside the pooled region, coalesced float4
 // read-modify-write of dx; adds dout[parent] where this pixel is the recorded argmax
-__global__ void k_maxpool_bwd_gather(const float* __restrict__ dout, const uint8_t* __restrict__ idx, int C, int B,
-                                     int H, int W, float* __restrict__ dx, int64_t lddx, int64_t n4) {
-    const int C4 = C >> 2, Ho = H >> 1, Wo = W >> 1, He = 2 * Ho, We = 2 * Wo;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t p = i / C4;          // pixel in the (2Ho x 2Wo) pooled region
-        const int c = (int)(i - p * C4) * 4;
-        const int x = (int)(p % We);
-        const int64_t t = p / We;
-        const int y = (int)(t % He);
-        const int b = (int)(t / He);
-        const int code = ((y & 1) << 1) | (x & 1);
-        const int64_t op = ((int64_t)b * Ho + (y >> 1)) * Wo + (x >> 1);
-        const uchar4 a = *reinterpret_cast<const uchar4*>(idx + op * C + c);
-        if (a.x != code && a.y != code && a.z != code && a.w != code) continue;
-        const float4 d = *reinterpret_cast<const float4*>(dout + op * C + c);
-        float* q = dx + (((int64_t)b * H + y) * W + x) * lddx + c;
-        float4 v = *reinterpret_cast<float4*>(q);
-        if (a.x == code) v.x += d.x;
-        if (a.y == code) v.y += d.y;
-        if (a.z == code) v.z += d.z;
-        if (a.w == code) v.w += d.w;
-        *reinterpret_cast<float4*>(q) = v;
+// one thread per pooled (pixel, 4-channel group): reads its argmax codes and gradient once and adds
+// the gradient into the one input position each channel chose (every input element is owned by
+// exactly one pooled element: no races, and the same single add per element as a gather).  32-bit
+// index arithmetic (the host checks the range).
+__global__ void k_maxpool_bwd_scatter(const float* __restrict__ dout, const uint8_t* __restrict__ idx, int C,
+                                      int H, int W, float* __restrict__ dx, int64_t lddx, uint32_t n4) {
+    const uint32_t C4 = (uint32_t)C >> 2, Ho = (uint32_t)H >> 1, Wo = (uint32_t)W >> 1;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+        const uint32_t op = i / C4;
+        const int c = (int)(i - op * C4) * 4;
+        const uint32_t xo = op % Wo, t = op / Wo;
+        const uint32_t yo = t % Ho, b = t / Ho;
+        const uchar4 a = *reinterpret_cast<const uchar4*>(idx + (int64_t)op * C + c);
+        const float4 d = *reinterpret_cast<const float4*>(dout + (int64_t)op * C + c);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (a.x != k && a.y != k && a.z != k && a.w != k) continue;
+            const int64_t px = ((int64_t)b * H + 2 * yo + (k >> 1)) * W + 2 * xo + (k & 1);
+            float* q = dx + px * lddx + c;
+            float4 v = *reinterpret_cast<float4*>(q);
+            if (a.x == k) v.x += d.x;
+            if (a.y == k) v.y += d.y;
+            if (a.z == k) v.z += d.z;
+            if (a.w == k) v.w += d.w;
+            *reinterpret_cast<float4*>(q) = v;
+        }
     }
 }
 void maxpool_bwd(const float* dout, const uint8_t* idx, int C, int B, int H, int W, float* dx,
                  int64_t lddx, hipStream_t st) {
-    const int64_t n4 = (int64_t)B * (H / 2 * 2) * (W / 2 * 2) * C / 4;
-    hipLaunchKernelGGL(k_maxpool_bwd_gather, dim3(ew_blocks(n4)), dim3(256), 0, st, dout, idx, C, B, H, W, dx, lddx, n4);
+    const int64_t n4 = (int64_t)B * (H / 2) * (W / 2) * C / 4;
+    if (n4 >= ((int64_t)1 << 31)) throw std::runtime_error("maxpool_bwd: tensor too large for 32-bit indexing");
+    hipLaunchKernelGGL(k_maxpool_bwd_scatter, dim3(ew_blocks(n4)), dim3(256), 0, st, dout, idx, C, H, W, dx, lddx,
+                       (uint32_t)n4);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -33,6 +33,13 @@ def _zero_grad_bias(name, B):
     return B > 1 and (name.endswith("film.fc1.bias") or name.endswith("film.fc2.bias"))
 
 
+def _noise_grad_param(name, B):
+    """Parameters whose gradient on a B-sample shard is rounding noise: the zero-gradient biases, and at
+    B == 2 also FiLM's fc1 weight -- BatchNorm1d over two samples maps (x1, x2) to +-d / sqrt(d^2 + 4 eps)
+    ~ +-1, so the gradient reaching fc1 is eps-scale and its sign is set by atomic-order rounding."""
+    return _zero_grad_bias(name, B) or (B == 2 and name.endswith("film.fc1.weight"))
+
+
 def _q(err, q=0.999):
     return torch.quantile(err.flatten().double(), q).item() if err.numel() > 1 else err.max().item()
 
@@ -469,7 +476,7 @@ def test_geonet_data_parallel_two_ranks(cad, dev, oracle):
     assert abs(ref.last_grad_norm() - res[0][2]) <= 1e-6 * res[0][2]
     # PCL's input gradient is an atomic scatter, so the two runs agree to rounding, not bit for bit:
     # Adam's first step (~lr * g / |g|) then differs only where a gradient is rounding noise — the
-    # Linear biases in front of FiLM's BatchNorm1d, whose true gradient is 0 — by at most 2 lr
+    # Linear layers in front of FiLM's two-sample BatchNorm1d (_noise_grad_param) — by at most 2 lr
     for n, v in ref.named_parameters().items():
         d = (v - torch.from_numpy(res[0][1][n])).abs().max().item()
-        assert d <= (2e-4 + 1e-7 if _zero_grad_bias(n, B) else 1e-6), (n, d)
+        assert d <= (2e-4 + 1e-7 if _noise_grad_param(n, B) else 1e-6), (n, d)
