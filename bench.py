@@ -11,13 +11,16 @@ libcad_hip.so.  Synthetic SUN-RGB-D-shaped batches resident in HBM (data loading
   python bench.py --config 3                            # ray+FiLM model, bf16 GEMMs, full loss
   python bench.py --config 4                            # baseline_unet, bf16 GEMMs, full loss
   N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N  (one rank per GPU,
-  RCCL gradient all-reduce overlapped with backward, weak scaling: bs32 per GPU).
+  weak scaling: bs32 per GPU; the gradient exchange is libcad's RCCL communicator — decoder-first
+  buckets all-reduced on its own stream while the backward runs, the build/train path; torch.distributed
+  only hands over the unique id and keeps the host-side barrier / max-over-ranks clock).
 
 Rank 0 prints ONE JSON line.  roofline: the dominant MFMA kernel (largest total time in the timed
 region, timed live with HIP events on its launch stream) against its engine's MFMA ceiling.
 cpu_baseline: the oracle restatement (LibTorch CPU, the reference's ATen kernels) on a bounded
-sample of the workload on this host's cores; parity: the same sampled steps on the GPU compared live
-with it (prediction, losses, eval-mode abs_rel).  bf16_workloads: bounded runs of the other BASELINE
+sample of the workload on this host's physical cores (plus a thread-count sweep); parity: 10
+identical steps on the GPU and the CPU path, compared after step 1 and step 10 (prediction, loss,
+eval-mode prediction and abs_rel).  bf16_workloads: bounded runs of the other BASELINE
 workloads (configs[2], configs[3]'s and configs[4]'s per-GPU steps) in the same process.
 """
 import argparse
@@ -42,7 +45,8 @@ HBM_PEAK_GBS = 8000.0
 FLOP_PER_IMAGE_480x640_F64 = 1.353646e12   # fwd + dgrad + wgrad
 WORKLOADS = {2: "baseline_unet train step, configs[1]: bs32/GPU 480x640 fp32 SI-only loss",
              3: "ray+FiLM conditioned U-Net train step, configs[2]: bs32/GPU 480x640 bf16 GEMMs, full loss",
-             4: "baseline_unet train step, configs[3]: bs32/GPU 480x640 bf16 GEMMs, full loss, DP over RCCL"}
+             4: "baseline_unet train step, configs[3] per-GPU step: bs32/GPU 480x640 bf16 GEMMs, full loss "
+                "(this 1-GPU leg runs no all-reduce; the DP exchange is timed by --gpus N)"}
 PRESETS = {2: ("baseline", "fp32"), 3: ("rayfilm", "bf16"), 4: ("baseline", "bf16")}
 
 
@@ -68,6 +72,8 @@ def parse():
                     help="GEMM arithmetic: fp32 (S3 engine, fp32-accurate) or bf16 operands / fp32 accumulation")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the bf16 workload legs and the data path")
+    ap.add_argument("--exchange", default="rccl", choices=("rccl", "torch"),
+                    help="N>1 gradient exchange: libcad's RCCL communicator (the build/train path) or torch.distributed")
     ap.add_argument("--cpu-sample-batch", type=int, default=8)
     ap.add_argument("--cpu-sample-steps", type=int, default=3)
     a = ap.parse_args()
@@ -105,26 +111,72 @@ def host_cpu():
             "usable_cpus": usable}
 
 
-def cpu_baseline_and_parity(args, cad, dev, lib):
+def cpu_threads():
+    """Threads for the CPU reference path: the host's physical cores (BASELINE.md §3:
+    set_num_threads(<physical cores>)), bounded by the CPUs this process may run on."""
+    h = host_cpu()
+    n = h["physical_cores"] or h["usable_cpus"] or 1
+    return max(1, min(n, h["usable_cpus"] or n)), h
+
+
+def cpu_baseline(args, sweep=(16, 64)):
     """cpu_baseline leg: the oracle restatement (oracle/cad_oracle.py: LibTorch CPU, the ATen kernels
     the reference dispatches; the reference source and its compiled harness stay in the build
     container) timed on this host on a bounded sample of the workload — bs`cpu_sample_batch` at the
-    benchmark resolution, 1 warm-up + `cpu_sample_steps` timed train steps from the same initial
-    weights and batch.  The same steps also run on the GPU (same engine as the headline) and are
-    compared live: step-1 prediction, every step's loss, and after the last step the eval-mode
-    prediction and abs_rel (computeDepthMetrics) on a held-out synthetic batch."""
+    benchmark resolution, 1 warm-up + `cpu_sample_steps` timed train steps at the host's physical core
+    count, then one more step at each thread count of `sweep` (the scaling of the CPU path itself)."""
     import torch
     from oracle import cad_oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
+    threads, host = cpu_threads()
     B, H, W, f = args.cpu_sample_batch, args.height, args.width, args.features
     w = tuple(float(x) for x in args.weights.split(","))
     params = O.init_params(f, seed=42, model=args.model)
     bufs = O.init_buffers(f, model=args.model)
     rgb, gt, K = [torch.from_numpy(a) for a in O.synth_batch(B, H, W)]
-    hr, hg, hk = [torch.from_numpy(a) for a in O.synth_batch(2, H, W, rgb_seed=0xBEEF, hole_seed=0xF00D)]
+    prev = torch.get_num_threads()
+    ref = O.Trainer(params, bufs, weights=w, model=args.model)
+    try:
+        torch.set_num_threads(threads)
+        ref.step(rgb, gt, K)                      # warm-up
+        t0 = time.perf_counter()
+        for _ in range(args.cpu_sample_steps):
+            ref.step(rgb, gt, K)
+        dt = time.perf_counter() - t0
+        rates = {str(threads): round(B * args.cpu_sample_steps / dt, 4)}
+        for t in sweep:
+            if t >= threads:
+                continue
+            torch.set_num_threads(t)
+            t1 = time.perf_counter()
+            ref.step(rgb, gt, K)
+            rates[str(t)] = round(B / (time.perf_counter() - t1), 4)
+    finally:
+        torch.set_num_threads(prev)
+    return {"value": rates[str(threads)], "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": (f"{args.model} bs{B} {H}x{W} f={f} loss weights {args.weights}, fp32 (the reference's only "
+                       f"precision), 1 warm-up + {args.cpu_sample_steps} timed train steps of the oracle restatement "
+                       f"(oracle/cad_oracle.py on LibTorch CPU, {threads} threads = the host's physical cores; BN "
+                       f"statistics over bs{B}, not bs32)"),
+            "seconds": round(dt, 2), "threads_sweep_images_per_s": rates,
+            "threads_sweep_note": "one train step per thread count after the timed steps (same weights, same batch)",
+            "host": host}
 
-    # GPU replica of the sampled steps
+
+def parity_steps(args, cad, dev, steps=10, B=2):
+    """SURVEY §8(d) / BASELINE.md §3: `steps` identical train steps on the GPU (the headline's engine)
+    and on the CPU reference path (oracle restatement, fp32, the host's physical cores) from the same
+    weights and batch (bs`B` at the benchmark resolution); after step 1 and after step `steps`:
+    train-mode prediction max relative error, loss relative error, then the eval-mode prediction
+    (BN running statistics) and the computeDepthMetrics abs_rel of both on a held-out batch."""
+    import torch
+    from oracle import cad_oracle as O
+    threads, _ = cpu_threads()
+    H, W, f = args.height, args.width, args.features
+    w = tuple(float(x) for x in args.weights.split(","))
+    params = O.init_params(f, seed=42, model=args.model)
+    bufs = O.init_buffers(f, model=args.model)
+    rgb, gt, K = [torch.from_numpy(a) for a in O.synth_batch(B, H, W)]
+    hr, hg, hk = [torch.from_numpy(a) for a in O.synth_batch(2, H, W, rgb_seed=0xBEEF, hole_seed=0xF00D)]
     cls = {"baseline": cad.BaselineUNet, "film": cad.IntrinsicsConditionedUNet,
            "rayfilm": cad.RayConditionedUNet}[args.model]
     model = cls(3, f, max_depth=10.0, batch=B, height=H, width=W, device=dev.index)
@@ -134,80 +186,129 @@ def cpu_baseline_and_parity(args, cad, dev, lib):
     loss = cad.CombinedDepthLoss(*w, batch=B, height=H, width=W, device=dev.index)
     tr = cad.Trainer(model, loss, lr=1e-4, weight_decay=1e-5, grad_clip=1.0)
     rg, gg, kg = rgb.to(dev), gt.to(dev), K.to(dev)
-    g_losses, g_pred1 = [], None
-    for i in range(1 + args.cpu_sample_steps):
-        g_losses.append(tr.train_step(rg, gg, kg)[0].item())
-        if i == 0:
-            g_pred1 = tr.pred.cpu()
-    model.eval()
-    hrg, hgg = hr.to(dev), hg.to(dev)
-    g_eval = model(hrg, cad.camera_from_K(hk.to(dev))) if model.conditioned else model(hrg)
-    g_eval = g_eval.cpu()
-    g_absrel = cad.depth_metrics(g_eval.to(dev), hgg)["abs_rel"]
-    del model, loss, tr
-    torch.cuda.empty_cache()
-
-    # the CPU reference path (fp32: the reference's only precision)
+    hrg, hgg, hkg = hr.to(dev), hg.to(dev), hk.to(dev)
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
     ref = O.Trainer(params, bufs, weights=w, model=args.model)
-    r1 = ref.step(rgb, gt, K)                      # warm-up (and parity step 1)
-    c_losses = [r1["loss"]]
-    t0 = time.perf_counter()
-    for _ in range(args.cpu_sample_steps):
-        c_losses.append(ref.step(rgb, gt, K)["loss"])
-    dt = time.perf_counter() - t0
-    c_eval = ref.predict_eval(hr, hk if args.model != "baseline" else None)
-    c_absrel = O.abs_rel_per_sample(c_eval, hg)
 
     def mre(a, b):
         den = b.abs().max().item()
         return (a.double() - b.double()).abs().max().item() / (den if den > 0 else 1.0)
-    host = host_cpu()
-    cpu = {"value": round(B * args.cpu_sample_steps / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
-           "sample": (f"{args.model} bs{B} {H}x{W} f={f} loss weights {args.weights}, fp32 (the reference's only "
-                      f"precision), 1 warm-up + {args.cpu_sample_steps} timed train steps of the oracle restatement "
-                      f"(oracle/cad_oracle.py on LibTorch CPU, {threads} threads; BN statistics over bs{B}, not bs32)"),
-           "seconds": round(dt, 2), "host": host}
-    parity = {"what": (f"the cpu_baseline sample's {1 + args.cpu_sample_steps} train steps on the GPU "
-                       f"({args.dtype} engine) vs the CPU reference path from identical weights and batch, then "
-                       f"eval-mode forward + computeDepthMetrics on a held-out bs2 batch"),
-              "step1_pred_max_rel_err": mre(g_pred1, r1["pred"]),
-              "loss_max_rel_err": max(abs(a - b) / abs(b) for a, b in zip(g_losses, c_losses)),
-              "eval_pred_max_rel_err": mre(g_eval, c_eval),
-              "abs_rel_gpu": round(g_absrel, 6), "abs_rel_cpu_ref": round(c_absrel, 6),
-              "abs_rel_delta": abs(g_absrel - c_absrel)}
-    return cpu, parity
+    out = {"what": (f"{steps} identical train steps on the GPU ({args.dtype} engine) and on the CPU reference path "
+                    f"(fp32, {threads} threads) from the same weights and bs{B} {H}x{W} batch; after step 1 and step "
+                    f"{steps}: train-mode prediction, loss, then eval-mode forward + computeDepthMetrics abs_rel on a "
+                    f"held-out bs2 batch")}
+    try:
+        for k in range(1, steps + 1):
+            gl = tr.train_step(rg, gg, kg)[0].item()
+            r = ref.step(rgb, gt, K)
+            if k in (1, steps):
+                model.eval()
+                g_eval = (model(hrg, cad.camera_from_K(hkg)) if model.conditioned else model(hrg))
+                g_abs = cad.depth_metrics(g_eval, hgg)["abs_rel"]
+                model.train()
+                c_eval = ref.predict_eval(hr, hk if args.model != "baseline" else None)
+                c_abs = O.abs_rel_per_sample(c_eval, hg)
+                out[f"after_step_{k}"] = {
+                    "pred_max_rel_err": mre(tr.pred.cpu(), r["pred"]),
+                    "loss_rel_err": abs(gl - r["loss"]) / abs(r["loss"]),
+                    "eval_pred_max_rel_err": mre(g_eval.cpu(), c_eval),
+                    "abs_rel_gpu": round(g_abs, 6), "abs_rel_cpu_ref": round(c_abs, 6),
+                    "abs_rel_delta": abs(g_abs - c_abs)}
+    finally:
+        torch.set_num_threads(prev)
+        del tr, loss, model
+        torch.cuda.empty_cache()
+    return out
 
 
-def extra_leg(cad, lib, dev, config, steps=5, warmup=2, B=32, H=480, W=640, f=64):
+def profiled(lib):
+    """Context of a timed region whose kernels libcad times with HIP events on their launch streams
+    (csrc/host/profiler.cpp); yields a callable returning the per-kernel report."""
+    import contextlib
+
+    @contextlib.contextmanager
+    def cm():
+        lib.cad_profile_reset()
+        lib.cad_profile_enable(1)
+        box = {}
+        try:
+            yield lambda: box.get("prof", [])
+        finally:
+            lib.cad_profile_enable(0)
+            n = lib.cad_profile_report(None, 0)
+            buf = C.create_string_buffer(n)
+            lib.cad_profile_report(buf, n)
+            box["prof"] = json.loads(buf.value.decode())
+    return cm()
+
+
+def roofline_of(prof, steps, ms_per_step, show=False):
+    """roofline object of the dominant MFMA kernel (largest total time) of a profiled region:
+    achieved = its algorithmic FLOPs / its summed HIP-event durations, against its engine's ceiling."""
+    if show:
+        for r in sorted(prof, key=lambda r: -r["ms"])[:24]:
+            log(f"  {r['ms'] / steps:8.2f} ms/step  {r['gflop'] / r['ms'] if r['ms'] else 0:7.2f} TF/s  "
+                f"x{r['launches'] // steps:<3d} {r['name']}")
+    gemm = [r for r in prof if r["gflop"] > 0]   # (split-K reductions are profiled at 0 FLOP)
+    if not gemm:
+        return None
+    dom = max(gemm, key=lambda r: r["ms"])
+    achieved = dom["gflop"] / dom["ms"]   # GFLOP/ms == TFLOP/s
+    # k_<op>[_win]_<engine>[p]: engine s3 / bf16 / none (f32); p = pre-split operands
+    kname = re.search(r"(k_\w+)", dom["name"]).group(1)
+    s3 = kname.endswith("_s3")
+    b1 = kname.endswith(("_bf16", "_bf16p", "_bf16p4"))
+    peak = S3_PEAK_TFLOPS if s3 else BF16_MFMA_PEAK_TFLOPS if b1 else FP32_MFMA_PEAK_TFLOPS
+    roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": round(peak, 1), "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": pmc_traffic(dom["name"]),
+            "arith": ("fp32 via exact 3-way bf16 split, 6 bf16 MFMA products per fp32 MAC: peak = dense "
+                      "bf16 MFMA 2516.6 / 6; achieved counts algorithmic fp32 FLOPs") if s3 else
+                     ("bf16 operands, fp32 accumulation (v_mfma_f32_32x32x16_bf16): peak = dense bf16 MFMA")
+                     if b1 else "fp32 MFMA (v_mfma_f32_32x32x2_f32)",
+            "kernel": dom["name"], "launches_per_step": dom["launches"] // steps,
+            "avg_launch_ms": round(dom["ms"] / dom["launches"], 4),
+            "gflop_per_launch": round(dom["gflop"] / dom["launches"], 3)}
+    tot_ms = sum(r["ms"] for r in gemm)
+    tot_gf = sum(r["gflop"] for r in gemm)
+    roof["all_gemm_kernels"] = {"tflops": round(tot_gf / tot_ms, 3), "ms_per_step": round(tot_ms / steps, 3),
+                                "share_of_step": round(tot_ms / steps / ms_per_step, 4)}
+    return roof
+
+
+def extra_leg(cad, lib, dev, config, steps=10, warmup=3, B=32, H=480, W=640, f=64):
     """A bounded measurement of another BASELINE workload in the same run (driver-observed):
     configs[2] (ray+FiLM U-Net, bf16 GEMMs, full loss) or configs[3]'s per-GPU step (baseline_unet,
-    bf16 GEMMs, full loss)."""
+    bf16 GEMMs, full loss), with the roofline of its dominant kernel."""
     import torch
     from cad_amd import synthetic
     model_name, dtype = PRESETS[config]
     prev = lib.cad_get_gemm_engine()
     assert lib.cad_set_gemm_engine(2 if dtype == "bf16" else 1) == 0
-    cls = {"baseline": cad.BaselineUNet, "rayfilm": cad.RayConditionedUNet}[model_name]
-    model = cls(3, f, max_depth=10.0, batch=B, height=H, width=W, device=dev.index)
-    loss = cad.CombinedDepthLoss(1.0, 0.1, 0.001, 0.01, batch=B, height=H, width=W, device=dev.index)
-    tr = cad.Trainer(model, loss, lr=1e-4, weight_decay=1e-5, grad_clip=1.0)
-    rgb, gt, K = (t.to(dev) for t in synthetic.device_batch(B, H, W, "cpu"))
-    for _ in range(warmup):
-        tr.train_step(rgb, gt, K)
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        tr.train_step(rgb, gt, K)
-    torch.cuda.synchronize(dev)
-    dt = time.perf_counter() - t0
-    last = tr.loss5[0].item()
-    del tr, loss, model
-    torch.cuda.empty_cache()
-    lib.cad_set_gemm_engine(prev)
+    try:
+        cls = {"baseline": cad.BaselineUNet, "rayfilm": cad.RayConditionedUNet}[model_name]
+        model = cls(3, f, max_depth=10.0, batch=B, height=H, width=W, device=dev.index)
+        loss = cad.CombinedDepthLoss(1.0, 0.1, 0.001, 0.01, batch=B, height=H, width=W, device=dev.index)
+        tr = cad.Trainer(model, loss, lr=1e-4, weight_decay=1e-5, grad_clip=1.0)
+        rgb, gt, K = (t.to(dev) for t in synthetic.device_batch(B, H, W, "cpu"))
+        for _ in range(warmup):
+            tr.train_step(rgb, gt, K)
+        torch.cuda.synchronize(dev)
+        with profiled(lib) as prof:
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                tr.train_step(rgb, gt, K)
+            torch.cuda.synchronize(dev)
+            dt = time.perf_counter() - t0
+        last = tr.loss5[0].item()
+        del tr, loss, model
+        torch.cuda.empty_cache()
+    finally:
+        lib.cad_set_gemm_engine(prev)
     value = B * steps / dt
     out = {"workload": WORKLOADS[config], "value": round(value, 3), "unit": "images/s",
            "ms_per_step": round(1e3 * dt / steps, 3), "steps": steps, "warmup": warmup, "dtype": dtype,
-           "last_loss": last}
+           "last_loss": last, "roofline": roofline_of(prof(), steps, 1e3 * dt / steps)}
     if model_name == "baseline":
         out["mfma_frac_dense_bf16"] = round(FLOP_PER_IMAGE_480x640_F64 * value / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4)
     return out
@@ -236,7 +337,7 @@ def resunet_macs_per_image(H=480, W=640):
     return stem + macs, macs
 
 
-def extra_leg_resunet(cad, dev, steps=5, warmup=2, B=32, H=480, W=640):
+def extra_leg_resunet(cad, lib, dev, steps=10, warmup=3, B=32, H=480, W=640):
     """configs[4]'s per-GPU step: ResNet-50 encoder + U-Net decoder (resunet.cpp), bs32 480x640, full
     loss, bf16 contraction operands (the fp8 conv-GEMM the config names is not built: DESIGN.md §9)."""
     import torch
@@ -249,11 +350,12 @@ def extra_leg_resunet(cad, dev, steps=5, warmup=2, B=32, H=480, W=640):
     for _ in range(warmup):
         model.train_step(loss, rgb, gt, K, pred=pred, dpred=dpred, loss5=loss5)
     torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        model.train_step(loss, rgb, gt, K, pred=pred, dpred=dpred, loss5=loss5)
-    torch.cuda.synchronize(dev)
-    dt = time.perf_counter() - t0
+    with profiled(lib) as prof:
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            model.train_step(loss, rgb, gt, K, pred=pred, dpred=dpred, loss5=loss5)
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
     last = loss5[0].item()
     params = model.count_parameters()
     del model, loss
@@ -266,7 +368,8 @@ def extra_leg_resunet(cad, dev, steps=5, warmup=2, B=32, H=480, W=640):
             "value": round(value, 3), "unit": "images/s", "ms_per_step": round(1e3 * dt / steps, 3), "steps": steps,
             "warmup": warmup, "dtype": "bf16", "params": params, "last_loss": last,
             "gflop_per_image": round(flop_img / 1e9, 2),
-            "mfma_frac_dense_bf16": round(flop_img * value / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4)}
+            "mfma_frac_dense_bf16": round(flop_img * value / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4),
+            "roofline": roofline_of(prof(), steps, 1e3 * dt / steps)}
 
 
 def extra_leg_geonet(cad, lib, dev, steps=3, warmup=2, B=8, H=480, W=640, f=64):
@@ -352,32 +455,46 @@ def data_path(cad, dev, B, H, W, h0=530, w0=730, reps=10):
             "achieved_GBps": round(per_img * B / ms / 1e6, 1), "peak_GBps": HBM_PEAK_GBS}
 
 
-def main():
-    args = parse()
-    import torch
+def setup_dist(args):
+    """N>1: one rank per GPU.  torch.distributed (gloo, host memory only) is the launcher's store and
+    the host-side barrier / max-over-ranks clock; the gradient exchange itself is libcad's RCCL
+    communicator (cad_comm_*, cad_unet_backward_allreduce) — the path build/train uses — created from
+    rank 0's unique id handed over through that store.  --exchange torch selects the torch.distributed
+    bucketed path instead (the only one that runs when several ranks share one GPU: CAD_BENCH_DEVICE)."""
     import torch.distributed as dist
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    # CAD_BENCH_DEVICE / CAD_DIST_BACKEND: rehearsal of the N>1 path on a 1-GPU box (every rank on
-    # one device, gloo) — never set for the driver's runs (one rank per GPU over RCCL)
+    # CAD_BENCH_DEVICE: rehearsal of the N>1 path on a 1-GPU box (every rank on one device) — never set
+    # for the driver's runs (one rank per GPU)
     local = int(os.environ.get("CAD_BENCH_DEVICE", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    pg = None
     if world > 1:
-        backend = os.environ.get("CAD_DIST_BACKEND", "nccl")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
-        pg = dist.group.WORLD
+        dist.init_process_group("gloo")
+    return world, rank, local
 
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world, rank, local = setup_dist(args)
     import cad_pkg
     cad = cad_pkg.load()
+    comm, pg = None, None
+    if world > 1:
+        if args.exchange == "rccl":
+            obj = [cad.Communicator.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            torch.cuda.set_device(local)
+            comm = cad.Communicator(obj[0], world, rank, device=local)
+        else:
+            torch.cuda.set_device(local)
+            pg = dist.new_group(backend=os.environ.get("CAD_DIST_BACKEND", "nccl"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
     from cad_amd import synthetic
     B, H, W, f = args.batch, args.height, args.width, args.features
     w = tuple(float(x) for x in args.weights.split(","))
@@ -385,13 +502,15 @@ def main():
     assert lib.cad_set_gemm_engine(2 if args.dtype == "bf16" else 1) == 0   # CAD_GEMM_BF16 / CAD_GEMM_S3
     cls = {"baseline": cad.BaselineUNet, "film": cad.IntrinsicsConditionedUNet,
            "rayfilm": cad.RayConditionedUNet}[args.model]
-    params_count = None
     model = cls(3, f, max_depth=10.0, batch=B, height=H, width=W, device=local)
     params_count = model.count_parameters()
-    if world > 1:
-        dist.broadcast(model.flat_params, 0)   # identical replicas (DDP semantics)
+    if comm is not None:
+        comm.broadcast_parameters(model, 0)        # identical replicas (DDP semantics)
+    elif pg is not None:
+        dist.broadcast(model.flat_params, 0, group=pg)
     loss = cad.CombinedDepthLoss(*w, batch=B, height=H, width=W, device=local)
-    trainer = cad.Trainer(model, loss, lr=1e-4, weight_decay=1e-5, grad_clip=1.0, process_group=pg)
+    trainer = cad.Trainer(model, loss, lr=1e-4, weight_decay=1e-5, grad_clip=1.0, process_group=pg,
+                          communicator=comm)
     rgb, gt, K = (t.to(dev) for t in synthetic.device_batch(B, H, W, "cpu"))
     if world > 1:   # each replica sees its own shard of the global batch
         rgb = torch.roll(rgb, shifts=rank, dims=0).contiguous()
@@ -401,59 +520,28 @@ def main():
     for i in range(args.warmup):
         trainer.train_step(rgb, gt, K)
     torch.cuda.synchronize(dev)
-    lib.cad_profile_reset()
-    lib.cad_profile_enable(1)
+    with profiled(lib) as prof:
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            trainer.train_step(rgb, gt, K)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
     if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        trainer.train_step(rgb, gt, K)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    lib.cad_profile_enable(0)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     last_loss = trainer.loss5[0].item()
-    n = lib.cad_profile_report(None, 0)
-    buf = C.create_string_buffer(n)
-    lib.cad_profile_report(buf, n)
-    prof = json.loads(buf.value.decode())
 
     if rank == 0:
-        for r in sorted(prof, key=lambda r: -r["ms"]):
-            log(f"  {r['ms'] / args.steps:8.2f} ms/step  {r['gflop'] / r['ms']:7.2f} TF/s  "
-                f"x{r['launches'] // args.steps:<3d} {r['name']}")
         images = B * world * args.steps
         value = images / elapsed
         ms_per_step = 1e3 * elapsed / args.steps
-        gemm = [r for r in prof if r["gflop"] > 0]   # (split-K reductions are profiled at 0 FLOP)
-        dom = max(gemm, key=lambda r: r["ms"]) if gemm else None
-        roof = None
-        if dom:
-            achieved = dom["gflop"] / dom["ms"]   # GFLOP/ms == TFLOP/s
-            # k_<op>[_win]_<engine>[p]: engine s3 / bf16 / none (f32); p = pre-split operands
-            kname = re.search(r"(k_\w+)", dom["name"]).group(1)
-            s3 = kname.endswith("_s3")
-            b1 = kname.endswith(("_bf16", "_bf16p"))
-            peak = S3_PEAK_TFLOPS if s3 else BF16_MFMA_PEAK_TFLOPS if b1 else FP32_MFMA_PEAK_TFLOPS
-            roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": round(peak, 1), "unit": "TFLOP/s",
-                    "frac": round(achieved / peak, 4), "traffic": pmc_traffic(dom["name"]),
-                    "arith": ("fp32 via exact 3-way bf16 split, 6 bf16 MFMA products per fp32 MAC: peak = dense "
-                              "bf16 MFMA 2516.6 / 6; achieved counts algorithmic fp32 FLOPs") if s3 else
-                             ("bf16 operands, fp32 accumulation (v_mfma_f32_32x32x16_bf16): peak = dense bf16 MFMA")
-                             if b1 else "fp32 MFMA (v_mfma_f32_32x32x2_f32)",
-                    "kernel": dom["name"], "launches_per_step": dom["launches"] // args.steps,
-                    "avg_launch_ms": round(dom["ms"] / dom["launches"], 4),
-                    "gflop_per_launch": round(dom["gflop"] / dom["launches"], 3)}
-            tot_ms = sum(r["ms"] for r in gemm)
-            tot_gf = sum(r["gflop"] for r in gemm)
-            roof["all_gemm_kernels"] = {"tflops": round(tot_gf / tot_ms, 3), "ms_per_step": round(tot_ms / args.steps, 3),
-                                        "share_of_step": round(tot_ms / args.steps / ms_per_step, 4)}
+        roof = roofline_of(prof(), args.steps, ms_per_step, show=True)
         step_tflops = (FLOP_PER_IMAGE_480x640_F64 * value / 1e12
                        if (H, W, f, args.model) == (480, 640, 64, "baseline") else None)
         dp, extra, cpu, parity = None, None, None, None
@@ -470,7 +558,7 @@ def main():
                 except Exception as e:
                     log(f"extra leg config {cfg} failed: {e}")
             try:
-                extra["config5"] = extra_leg_resunet(cad, dev)
+                extra["config5"] = extra_leg_resunet(cad, lib, dev)
                 log(f"extra leg config 5: {extra['config5']}")
             except Exception as e:
                 log(f"extra leg config 5 failed: {e}")
@@ -485,9 +573,15 @@ def main():
                 log(f"data-path measurement failed: {e}")
         if world == 1 and not args.no_cpu_baseline:
             try:
-                cpu, parity = cpu_baseline_and_parity(args, cad, dev, lib)
+                cpu = cpu_baseline(args)
+                log(f"cpu baseline: {cpu}")
             except Exception as e:
                 log(f"cpu baseline failed: {e}")
+            try:
+                parity = parity_steps(args, cad, dev)
+                log(f"parity: {parity}")
+            except Exception as e:
+                log(f"parity check failed: {e}")
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
@@ -497,7 +591,11 @@ def main():
                        "model": args.model,
                        "global_batch": B * world, "height": H, "width": W, "init_features": f,
                        "params": params_count, "loss_weights": list(w),
-                       "parallelism": f"dp{world}", "optimizer": "adam(lr1e-4,wd1e-5)+clip1.0"},
+                       "parallelism": f"dp{world}", "optimizer": "adam(lr1e-4,wd1e-5)+clip1.0",
+                       "gradient_exchange": (None if world == 1 else
+                                             "libcad RCCL communicator: decoder-first buckets overlapped with the "
+                                             "backward (cad_unet_backward_allreduce)" if comm is not None else
+                                             "torch.distributed bucketed all-reduce (GradBucketer)")},
             "step_tflops_algorithmic": round(step_tflops, 3) if step_tflops else None,
             "last_loss": last_loss,
             "roofline": roof,
@@ -507,6 +605,7 @@ def main():
             "data_path": dp,
         }
         print(json.dumps(out), flush=True)
+    comm = None
     if world > 1:
         dist.destroy_process_group()
 

@@ -386,11 +386,11 @@ void layout(cad_unet* h, Arena& a) {
     h->Sa = a.f(M0C0);
     h->Sb = a.f(M0C0);
     h->Sc = a.f(h->Ml(1, B) * h->Cl(0));
-    // BN tile partials: rows x 2C, max over layers
+    // BN tile partials: rows x (2C + 1) (S, M2 per channel + the row's count), max over layers
     int64_t st = 0, colmax = 0;
     for (int l = 0; l < 5; ++l) {
         const int64_t r = (h->Ml(l, B) + 63) / 64;   // any tile height: the engine may change at run time
-        st = std::max<int64_t>(st, r * 2 * h->Cl(l));
+        st = std::max<int64_t>(st, r * (2 * h->Cl(l) + 1));
         colmax = std::max<int64_t>(colmax, h->Cl(l));
     }
     h->stats = a.f(st);

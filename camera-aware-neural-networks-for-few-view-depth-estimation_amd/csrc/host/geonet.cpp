@@ -357,7 +357,7 @@ void layout(cad_geonet* h, Arena& a) {
     for (int l = 0; l < nl; ++l) {
         const int64_t M = h->Ml(l, B), HW = (int64_t)h->Hl(l) * h->Wl(l);
         const int C = h->Cl(l);
-        st = std::max<int64_t>(st, (M + 63) / 64 * 2 * C);
+        st = std::max<int64_t>(st, (M + 63) / 64 * (2 * C + 1));   // BN tile partials + counts
         dscr = std::max(dscr, (int64_t)(cad::colsum_slices(M) + 2) * 4 * C + 4 * C + 8192);
         dscr = std::max(dscr, cad::film_reduce_doubles(B, HW, C) + 8192);
         dscr = std::max(dscr, cad::attn_scratch_doubles(B, HW, C) + 8192);

@@ -314,7 +314,7 @@ void layout(cad_resunet* h, Arena& a) {
     h->pools = a.tw(M2 * 64);
     h->pidx = a.u8(M2 * 64);
     track(M1, 64);
-    maxRows2C = std::max<int64_t>(maxRows2C, (int64_t)cad::dense_stats_rows(M1, 64) * 128);
+    maxRows2C = std::max<int64_t>(maxRows2C, (int64_t)cad::dense_stats_rows(M1, 64) * 129);
     for (Bott& b : h->blocks) {
         const int64_t Mi = h->M(B, b.H, b.W), Mo = h->M(B, b.Ho, b.Wo);
         for (Unit* u : {&b.u1, &b.u2, &b.u3, &b.ud}) {
@@ -342,9 +342,9 @@ void layout(cad_resunet* h, Arena& a) {
         for (const Unit* u : {&b.u1, &b.u2, &b.u3, &b.ud}) {
             if (u->c.pidx < 0) continue;
             const int64_t Mu = u == &b.u1 ? Mi : Mo;
-            maxRows2C = std::max<int64_t>(maxRows2C, (int64_t)cad::dense_stats_rows(Mu, u->c.cout) * 2 * u->c.cout);
+            maxRows2C = std::max<int64_t>(maxRows2C, (int64_t)cad::dense_stats_rows(Mu, u->c.cout) * (2 * u->c.cout + 1));
             maxRows2C = std::max<int64_t>(
-                maxRows2C, (int64_t)cad::conv3x3_stats_rows(u->c.cin, B, b.H, b.W, u->c.cout, true) * 2 * u->c.cout);
+                maxRows2C, (int64_t)cad::conv3x3_stats_rows(u->c.cin, B, b.H, b.W, u->c.cout, true) * (2 * u->c.cout + 1));
         }
     }
     for (Dec& d : h->dec) {
@@ -359,8 +359,8 @@ void layout(cad_resunet* h, Arena& a) {
             bn_alloc(a, u->b);
             u->y = a.f(Md * d.C);
             maxRows2C = std::max<int64_t>(
-                maxRows2C, (int64_t)cad::conv3x3_stats_rows(u->c.cin, B, d.H, d.W, d.C, true) * 2 * d.C);
-            maxRows2C = std::max<int64_t>(maxRows2C, (int64_t)cad::dense_stats_rows(Md, d.C) * 2 * d.C);
+                maxRows2C, (int64_t)cad::conv3x3_stats_rows(u->c.cin, B, d.H, d.W, d.C, true) * (2 * d.C + 1));
+            maxRows2C = std::max<int64_t>(maxRows2C, (int64_t)cad::dense_stats_rows(Md, d.C) * (2 * d.C + 1));
         }
         d.a1s = a.tw(Md * d.C);
         d.out = a.f(Md * d.C);

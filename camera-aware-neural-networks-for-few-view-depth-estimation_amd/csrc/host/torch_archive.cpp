@@ -23,6 +23,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <set>
 #include <memory>
 #include <random>
 #include <stdexcept>
@@ -446,7 +447,7 @@ class Unpickler {
 
     uint8_t byte() { return *take(1); }
     const uint8_t* take(size_t n) {
-        if (pos_ + n > b_.size()) throw ArchiveError("pickle: truncated");
+        if (n > b_.size() - pos_) throw ArchiveError("pickle: truncated");   // (no pos_ + n wrap)
         const uint8_t* p = reinterpret_cast<const uint8_t*>(b_.data()) + pos_;
         pos_ += n;
         return p;
@@ -559,8 +560,17 @@ std::string read_range(FILE* f, uint64_t off, uint64_t n) {
     return s;
 }
 
-void collect(const VPtr& v, const std::string& prefix, cad_archive& a) {
+// The module tree of an archive is a few levels deep; anything deeper (or a dict that contains
+// itself through the memo) is malformed input, not a checkpoint.
+constexpr int kMaxDepth = 64;
+constexpr int64_t kMaxNumel = (int64_t)1 << 40;
+
+void collect(const VPtr& v, const std::string& prefix, cad_archive& a, std::set<const Value*>& open, int depth) {
+    if (depth > kMaxDepth) throw ArchiveError("pickle: module tree nested too deeply");
     if (v->kind == Value::Tensor) {
+        if (v->items.empty() || v->items[0]->kind != Value::Storage) throw ArchiveError("tensor '" + prefix + "' has no storage");
+        if (v->strides.size() != v->sizes.size()) throw ArchiveError("tensor '" + prefix + "': sizes and strides differ in rank");
+        if (v->i < 0) throw ArchiveError("tensor '" + prefix + "': negative storage offset");
         cad_archive::T t;
         t.name = prefix;
         t.key = v->items[0]->s;
@@ -569,18 +579,24 @@ void collect(const VPtr& v, const std::string& prefix, cad_archive& a) {
         t.sizes = v->sizes;
         int64_t expect = 1;
         for (int k = (int)t.sizes.size() - 1; k >= 0; --k) {
-            if (t.sizes[(size_t)k] != 1 && v->strides[(size_t)k] != expect)
+            const int64_t n = t.sizes[(size_t)k];
+            if (n < 0 || n > kMaxNumel) throw ArchiveError("tensor '" + prefix + "': bad size");
+            if (n != 1 && v->strides[(size_t)k] != expect)
                 throw ArchiveError("tensor '" + prefix + "' is not contiguous");
-            expect *= t.sizes[(size_t)k];
+            if (n > 0 && expect > kMaxNumel / n) throw ArchiveError("tensor '" + prefix + "': too many elements");
+            expect *= n;
         }
+        if (t.offset > kMaxNumel) throw ArchiveError("tensor '" + prefix + "': bad storage offset");
         a.tensors.push_back(std::move(t));
         return;
     }
     if (v->kind == Value::Object || v->kind == Value::Dict) {
+        if (!open.insert(v.get()).second) throw ArchiveError("pickle: self-referencing module tree");
         for (auto& kv : v->dict) {
             if (kv.first->kind != Value::Str) continue;
-            collect(kv.second, prefix.empty() ? kv.first->s : prefix + "." + kv.first->s, a);
+            collect(kv.second, prefix.empty() ? kv.first->s : prefix + "." + kv.first->s, a, open, depth + 1);
         }
+        open.erase(v.get());
     }
 }
 
@@ -690,7 +706,8 @@ cad_status cad_archive_open(const char* path, cad_archive** out) {
         if (pk->second.method != 0) throw ArchiveError("compressed data.pkl is not supported");
         const std::string pkl = read_range(f.get(), pk->second.data_off, pk->second.size);
         Unpickler up(pkl);
-        collect(up.run(), "", *a);
+        std::set<const Value*> open;
+        collect(up.run(), "", *a, open, 0);
         for (auto& t : a->tensors) {
             auto it = a->entries.find(a->prefix + "/data/" + t.key);
             if (it == a->entries.end()) throw ArchiveError("missing storage record data/" + t.key);

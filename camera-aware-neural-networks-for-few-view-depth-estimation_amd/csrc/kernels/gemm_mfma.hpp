@@ -53,7 +53,7 @@ struct GemmArgs {
     // output
     float* C; int64_t ldc; int c_coff;
     const float* bias;
-    float* stats;         // BN partials [gridDim.x][2][N]  (sum, sumsq) or nullptr
+    float* stats;         // BN partials [gridDim.x][2][N] (sum, M2 about the tile mean) + [gridDim.x] counts, or nullptr
     int kstages_per_split;
     int64_t slab_stride;  // elements between split-K slabs
     // conv3x3 forward/dgrad on pre-split operands: K stages in channel-major order (stage s = tap
@@ -448,6 +448,81 @@ __device__ __forceinline__ bool wave_live(const GemmArgs& a, int m0, int n0, int
     return m0 + wrows < a.M && n0 + wcols < a.N;
 }
 
+// ---------------------------------------------------------------------------------------------
+// BatchNorm partials of a GEMM tile in shifted (Chan / Welford) form.  A tile writes, per column n,
+// S = sum y and M2 = sum (y - mean_tile)^2 over its valid rows, and its valid-row count once:
+//   a.stats[tile][0][n] = S, a.stats[tile][1][n] = M2, a.stats[gridDim.x * 2N + tile] = count.
+// bn_fwd_finalize then forms sum y^2 = sum_t (M2_t + S_t^2 / n_t) in fp64, so the variance is never
+// the fp32 difference E[y^2] - E[y]^2 (which loses ~log2(1 + mu^2/sigma^2) bits; BaselineUNet's
+// train-mode BN normalises with it, baseline_unet.h:32-42).  Each lane accumulates
+// (y - s) and (y - s)^2 about a shift s = its first accumulator of the column (any finite value is
+// exact algebra; one near the column's values keeps the fp32 sums small), then lanes, waves and
+// tiles merge (n, mean, M2) with Chan's pairwise formula.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, float nb, float mb, float m2b) {
+    const float nn = n + nb;
+    if (nn > 0.f) {
+        const float d = mb - mean, f = nb / nn;
+        mean = fmaf(d, f, mean);
+        m2 += m2b + d * d * n * f;
+    }
+    n = nn;
+}
+template <int NJ>
+struct BnTilePartials {
+    float sh[NJ], d1[NJ], d2[NJ];
+    float cnt;
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) sh[j] = d1[j] = d2[j] = 0.f;
+        cnt = 0.f;
+    }
+    __device__ __forceinline__ void shift(int j, float v) { sh[j] = v; }
+    // valid: the row belongs to the output; count it once per row (column block 0)
+    __device__ __forceinline__ void add(int j, float v, bool valid) {
+        const float d = valid ? v - sh[j] : 0.f;
+        d1[j] += d;
+        d2[j] = fmaf(d, d, d2[j]);
+        if (j == 0) cnt += valid ? 1.f : 0.f;
+    }
+    // lanes -> waves (LDS [WM][BN][3]) -> tile; `lds` is free scratch; every thread must call
+    template <int WM, int WN>
+    __device__ __forceinline__ void finish(const GemmArgs& a, float* lds, int tile_x, int n0) {
+        constexpr int BN = 32 * NJ * WN;
+        const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+        const int wm = wave / WN, wn = wave % WN;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            float n = cnt, mean = 0.f, m2 = 0.f;
+            if (n > 0.f) {
+                const float q = d1[j] / n;
+                mean = sh[j] + q;
+                m2 = fmaxf(d2[j] - d1[j] * q, 0.f);
+            }
+            chan_merge(n, mean, m2, __shfl_xor(n, 32), __shfl_xor(mean, 32), __shfl_xor(m2, 32));
+            if (lane < 32) {
+                float* r = lds + (wm * BN + wn * 32 * NJ + j * 32 + lane) * 3;
+                r[0] = n; r[1] = mean; r[2] = m2;
+            }
+        }
+        __syncthreads();
+        for (int c = tid; c < BN; c += 256) {
+            float n = 0.f, mean = 0.f, m2 = 0.f;
+#pragma unroll
+            for (int w = 0; w < WM; ++w) {
+                const float* r = lds + (w * BN + c) * 3;
+                chan_merge(n, mean, m2, r[0], r[1], r[2]);
+            }
+            const int nn = n0 + c;
+            if (nn < a.N) {
+                a.stats[(int64_t)tile_x * 2 * a.N + nn] = n * mean;
+                a.stats[(int64_t)tile_x * 2 * a.N + a.N + nn] = m2;
+            }
+            if (n0 == 0 && c == 0) a.stats[(int64_t)gridDim.x * 2 * a.N + tile_x] = n;
+        }
+    }
+};
+
 template <class Epi>
 __device__ __forceinline__ const float* epi_row_base(const GemmArgs& a, int m0, int z) {
     if constexpr (is_structured<Epi>::value) return a.C;   // unused by structured epilogues
@@ -468,9 +543,12 @@ __device__ __forceinline__ void gemm_epilogue_t(const GemmArgs& a, const floatx1
     const int m0 = tile.x * BM, n0 = tile.y * BN;
     // With STATS the per-column BN partials are accumulated in the same pass (each accumulator is read once: keeping them live
     // for a second pass costs 64 VGPRs and an occupancy step).  ssum[j]: the lane's column of block column j.
-    float ssum[NJ], ssq[NJ];
+    BnTilePartials<NJ> bnp;
+    if constexpr (Epi::STATS) {
+        bnp.init();
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) ssum[j] = ssq[j] = 0.f;
+        for (int j = 0; j < NJ; ++j) bnp.shift(j, acc[0][j][0]);
+    }
     // Row-major epilogues (EpiStore, EpiSlab) store through a buffer descriptor based at the tile's
     // first output row whose range ends at row M: rows past M are dropped by the range check and
     // columns past N get an out-of-range offset, so each store is one 32-bit offset add.
@@ -522,43 +600,15 @@ __device__ __forceinline__ void gemm_epilogue_t(const GemmArgs& a, const floatx1
                         else
                             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[r]), rs,
                                                                   lo + (uint32_t)(r * ldc4), 0, 0);
-                        if constexpr (Epi::STATS) {
-                            const float vm = m0 + mr + r < a.M ? v[r] : 0.f;
-                            ssum[j] += vm;
-                            ssq[j] += vm * vm;
-                        }
+                        if constexpr (Epi::STATS) bnp.add(j, v[r], m0 + mr + r < a.M);
                     }
                 }
             }
         }
 
-    if constexpr (Epi::STATS) {
-        // per-column partial sum / sum of squares over this block's BM rows -> a.stats[bx][2][N];
-        // the main loop ended on a barrier, so the LDS operand buffers are free for the reduction
-        float* red = lds;   // [WM][BN][2]
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            float s = ssum[j], q = ssq[j];
-            s += __shfl_xor(s, 32);
-            q += __shfl_xor(q, 32);
-            if (lane < 32) {
-                const int cl = wn * 32 * NJ + j * 32 + lane;
-                red[(wm * BN + cl) * 2 + 0] = s;
-                red[(wm * BN + cl) * 2 + 1] = q;
-            }
-        }
-        __syncthreads();
-        for (int c = tid; c < BN; c += 256) {
-            float s = 0.f, q = 0.f;
-#pragma unroll
-            for (int w = 0; w < WM; ++w) { s += red[(w * BN + c) * 2]; q += red[(w * BN + c) * 2 + 1]; }
-            const int n = n0 + c;
-            if (n < a.N) {
-                a.stats[(int64_t)tile.x * 2 * a.N + n] = s;
-                a.stats[(int64_t)tile.x * 2 * a.N + a.N + n] = q;
-            }
-        }
-    }
+    // per-column BN partials over this block's BM rows -> a.stats (BnTilePartials); the main loop
+    // ended on a barrier, so the LDS operand buffers are free for the reduction
+    if constexpr (Epi::STATS) bnp.template finish<WM, WN>(a, lds, tile.x, n0);
 }
 template <int WM, int WN, class Epi>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, floatx16 (&acc)[2][2], const TileId& tile,

@@ -111,13 +111,15 @@ struct WinB {
 template <int WM, int WN, int MI, int NJ, int CW, class Epi>
 __device__ __forceinline__ void win_epilogue(const GemmArgs& a, const floatx16 (&acc)[MI][NJ], int tile_lin, int n0,
                                              int b, int y0, int x0, float* lds) {
-    constexpr int BN = 32 * NJ * WN;
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
     const int wm = wave / WN, wn = wave % WN;
-    float ssum[NJ], ssq[NJ];
+    BnTilePartials<NJ> bnp;
+    if constexpr (Epi::STATS) {
+        bnp.init();
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) ssum[j] = ssq[j] = 0.f;
+        for (int j = 0; j < NJ; ++j) bnp.shift(j, acc[0][j][0]);
+    }
     constexpr int ES = Epi::BF16 ? 2 : 4;   // output element bytes
     const int64_t ldc4 = a.ldc * ES;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const float*>(
@@ -148,39 +150,11 @@ __device__ __forceinline__ void win_epilogue(const GemmArgs& a, const floatx16 (
                     else
                         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[q]), rs,
                                                               lo + (uint32_t)(q * ldc4), 0, 0);
-                    if constexpr (Epi::STATS) {
-                        const float vm = y0 + r < a.H ? v[q] : 0.f;
-                        ssum[j] += vm;
-                        ssq[j] += vm * vm;
-                    }
+                    if constexpr (Epi::STATS) bnp.add(j, v[q], y0 + r < a.H);
                 }
             }
         }
-    if constexpr (Epi::STATS) {
-        float* red = lds;   // [WM][BN][2]
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            float s = ssum[j], q = ssq[j];
-            s += __shfl_xor(s, 32);
-            q += __shfl_xor(q, 32);
-            if (lane < 32) {
-                const int cl = wn * 32 * NJ + j * 32 + lane;
-                red[(wm * BN + cl) * 2 + 0] = s;
-                red[(wm * BN + cl) * 2 + 1] = q;
-            }
-        }
-        __syncthreads();
-        for (int c = tid; c < BN; c += 256) {
-            float s = 0.f, q = 0.f;
-#pragma unroll
-            for (int w = 0; w < WM; ++w) { s += red[(w * BN + c) * 2]; q += red[(w * BN + c) * 2 + 1]; }
-            const int n = n0 + c;
-            if (n < a.N) {
-                a.stats[(int64_t)tile_lin * 2 * a.N + n] = s;
-                a.stats[(int64_t)tile_lin * 2 * a.N + a.N + n] = q;
-            }
-        }
-    }
+    if constexpr (Epi::STATS) bnp.template finish<WM, WN>(a, lds, tile_lin, n0);
 }
 
 // blocks: gridDim.x = B * ceil(H / R) * (W / CW) output blocks (XCD-aware order), gridDim.y = N tiles

@@ -92,6 +92,24 @@ struct OpSum {
         acc[0][0] += v.x; acc[0][1] += v.y; acc[0][2] += v.z; acc[0][3] += v.w;
     }
 };
+// BN tile partials (BnTilePartials, gemm_mfma.hpp): per tile row r, S = part[r][c], M2 = part[r][C + c],
+// n = cnt[r]; column sums of S and of M2 + S^2 / n (= sum y^2 of the tile) in fp64
+struct OpBnTile {
+    const float* part; const float* cnt; int C;
+    __device__ NoPrep prep(int) const { return {}; }
+    __device__ void operator()(int64_t r, int c4, double (&acc)[2][4], NoPrep) const {
+        const float4 s = *reinterpret_cast<const float4*>(part + r * 2 * C + c4 * 4);
+        const float4 q = *reinterpret_cast<const float4*>(part + r * 2 * C + C + c4 * 4);
+        const double n = cnt[r];
+        if (n <= 0.0) return;
+        const double sa[4] = {s.x, s.y, s.z, s.w}, qa[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            acc[0][e] += sa[e];
+            acc[1][e] += qa[e] + sa[e] * sa[e] / n;
+        }
+    }
+};
 struct BnCoef {
     float sc[4], sh[4], mu[4], is[4];
 };
@@ -155,10 +173,9 @@ void launch_colfinal(const double* part, int S, int N, double* tot, float* dst, 
 }
 }  // namespace
 
-// >= 128 rows per slice, at most 512 slices (monotone in R: scratch is sized at the largest R).  The
-// narrow reductions (GEMM tile partials: M/128 rows) then still spread over 512 workgroups.
-// up to 2048 slices of >= 256 rows: a level-0 reduction (9.8 M rows x 16 channel quads) then runs
-// 2048 workgroups, ~8 per CU (512 left it latency-bound at 2 per CU)
+// Up to 2048 slices of >= 256 rows: a level-0 reduction (9.8 M rows x 16 channel quads) then runs
+// 2048 workgroups, ~8 per CU (512 left it latency-bound at 2 per CU).  Monotone in R: the callers'
+// dscr scratch must be sized from colsum_slices() of their largest reduction.
 int colsum_slices(int64_t R) { return (int)std::max<int64_t>(1, std::min<int64_t>(2048, R / 256)); }
 
 void colsum(const float* x, int64_t ld, int coff, int64_t R, int C, double* part, hipStream_t st) {
@@ -198,7 +215,9 @@ void bn_fwd_finalize(const float* tile_part, int rows, int C, int64_t count, con
                      hipStream_t st) {
     double* tot = scratch;
     double* part = scratch + 2 * C;
-    const int S = launch_colreduce<1>(OpSum{tile_part, 2 * C, 0}, rows, 2 * C, part, st);
+    // tile_part: [rows][2][C] (S, M2) then [rows] counts (BnTilePartials); the variance below is
+    // E[y^2] - mu^2 in fp64 over per-tile sums y^2 rebuilt from the shifted partials
+    const int S = launch_colreduce<2>(OpBnTile{tile_part, tile_part + (int64_t)rows * 2 * C, C}, rows, C, part, st);
     launch_colfinal(part, S, 2 * C, tot, nullptr, 1.f, st);
     hipLaunchKernelGGL(k_bn_stats, dim3(cdiv(C, 64)), dim3(64), 0, st, tot, C, count, gamma, beta,
                        run_mean, run_var, momentum, eps, mean, invstd, scale, shift);

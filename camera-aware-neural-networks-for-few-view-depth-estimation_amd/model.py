@@ -715,24 +715,6 @@ class GeometryAwareNetwork(ResNetUNet):
             out = out.view(np.int32)
         return torch.from_numpy(out)
 
-    def cbam_decisions(self, model: str):
-        """{CBAM prefix: (argmax pixel [B][C], argmax channel [B][H][W])} of the last forward, keyed like
-        the oracle (cad_oracle.GEO_DEBUG["force"]) so a restatement can route its max-pool gradients
-        exactly as this run did."""
-        from oracle.cad_oracle import _geo_names
-        nl, enc = _geo_names(model)
-        out = {}
-        for l in range(1, nl):
-            try:
-                a = self.debug_buffer(f"amaxe{l}").long()
-            except KeyError:
-                return {}
-            s = self.debug_buffer(f"sidxe{l}").long()
-            out[f"{enc[l]}.attention."] = (a, s)
-        for l in range(nl - 1):
-            out[f"dec{l + 1}.attention."] = (self.debug_buffer(f"amaxd{l}").long(), self.debug_buffer(f"sidxd{l}").long())
-        return out
-
     def train_step(self, loss_fn: "CombinedDepthLoss", rgb, gt, K, lr=1e-4, weight_decay=1e-5, grad_clip=1.0,
                    rays=None, pred=None, dpred=None, loss5=None, process_group=None):
         """One optimisation step (enhanced.h:287-304 sequence) fed the loader's batch: rays default to

@@ -208,3 +208,57 @@ def test_reader_rejects_malformed(cad, tmp_path):
     assert lib.cad_archive_open(str(z).encode(), C.byref(h)) == 0
     assert lib.cad_archive_count(h) == 0
     lib.cad_archive_close(h)
+
+
+def _pkl_str(s):
+    b = s.encode()
+    return b"X" + len(b).to_bytes(4, "little") + b
+
+
+def _tensor_pkl(offset, sizes, strides):
+    """data.pkl of {'w': _rebuild_tensor_v2(storage '0' FloatStorage, offset, sizes, strides, False)}."""
+    def ints(v):
+        return b"(" + b"".join(b"J" + int(x).to_bytes(4, "little", signed=True) for x in v) + b"t"
+    return (b"\x80\x02}" + _pkl_str("w") + b"ctorch._utils\n_rebuild_tensor_v2\n(" +
+            b"(" + _pkl_str("storage") + b"ctorch\nFloatStorage\n" + _pkl_str("0") + _pkl_str("cpu") + b"K\x10tQ" +
+            b"J" + int(offset).to_bytes(4, "little", signed=True) + ints(sizes) + ints(strides) + b"\x89tRs.")
+
+
+@pytest.mark.parametrize("what,pkl,msg", [
+    ("BINUNICODE8 length that wraps pos + n", b"\x80\x02\x8d" + (2 ** 64 - 1).to_bytes(8, "little") + b"abc.",
+     b"truncated"),
+    ("BINUNICODE8 length past the end", b"\x80\x02\x8d" + (1 << 40).to_bytes(8, "little") + b"abc.", b"truncated"),
+    ("dict that contains itself through the memo", b"\x80\x02}q\x00" + _pkl_str("a") + b"h\x00s.", b"self-referencing"),
+    ("strides shorter than sizes", _tensor_pkl(0, [2, 2], [2]), b"rank"),
+    ("negative size", _tensor_pkl(0, [-2, 2], [2, 1]), b"bad size"),
+    ("negative storage offset", _tensor_pkl(-5, [2, 2], [2, 1]), b"negative storage offset"),
+    ("storage record too small", _tensor_pkl(14, [2, 2], [2, 1]), b"too small"),
+])
+def test_reader_rejects_hostile_pickles(cad, tmp_path, what, pkl, msg):
+    """the .pt reader (cad_archive_open, used by --resume and load) bounds-checks every
+    length and index taken from the file: wrapped lengths, cyclic module trees and inconsistent tensor
+    records end in a clean error, never an out-of-bounds read or unbounded recursion."""
+    lib = cad.load_library()
+    z = tmp_path / "bad.pt"
+    with zipfile.ZipFile(z, "w") as f:
+        f.writestr("bad/data.pkl", pkl)
+        f.writestr("bad/data/0", np.zeros(16, np.float32).tobytes())
+    h = C.c_void_p()
+    assert lib.cad_archive_open(str(z).encode(), C.byref(h)) != 0, what
+    assert msg in lib.cad_last_error(), (what, lib.cad_last_error())
+
+
+def test_reader_accepts_the_well_formed_twin(cad, tmp_path):
+    """The hand-built record of test_reader_rejects_hostile_pickles, made consistent, reads back."""
+    lib = cad.load_library()
+    z = tmp_path / "ok.pt"
+    with zipfile.ZipFile(z, "w") as f:
+        f.writestr("ok/data.pkl", _tensor_pkl(4, [2, 3], [3, 1]))
+        f.writestr("ok/data/0", np.arange(16, dtype=np.float32).tobytes())
+    h = C.c_void_p()
+    assert lib.cad_archive_open(str(z).encode(), C.byref(h)) == 0, lib.cad_last_error()
+    assert lib.cad_archive_count(h) == 1
+    out = np.empty(6, np.float32)
+    assert lib.cad_archive_read(h, 0, out.ctypes.data_as(C.c_void_p), out.nbytes) == 0
+    assert np.array_equal(out, np.arange(4, 10, dtype=np.float32))
+    lib.cad_archive_close(h)

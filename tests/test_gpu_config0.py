@@ -1,0 +1,100 @@
+"""BASELINE configs[0] through the drop-in entry point: `build/train --config configs/train_config.yaml`
+(train_main.cpp:279-507) with baseline_unet f=64, bs2, 128x128 over 10 SUN-RGB-D-shaped samples (the
+reference's CPU plumbing run), on the MI355X, against the oracle's trajectory on the same batches.
+
+The weights start from a torch::save archive of the oracle's initial parameters (`-r init.pt`,
+weights-only start as the reference's --resume would take a .pt), the synthetic data set is read on
+the host through the same C ABI the trainer's loader uses (cad_dataset_synthetic / cad_dataset_read:
+decoded u8 rgb, u16 depth, K) and assembled by the oracle's restatement of getSample
+(sunrgbd_loader.cpp:105-169; 128x128 sources, so the resize is the identity).  Compared:
+  * every step's batch loss (tensorboard_scalars.csv batch_loss/train, log_interval 1): the
+    trainer's step = enhanced.h:287-304 (forward, forwardWithIntrinsics, backward, clip 1.0, Adam);
+  * the epoch's train_loss and the validation val_loss / abs_rel of metrics.csv (validateEpoch
+    :339-395 — per-sample eval forwards and computeDepthMetrics :400-439 averaged over samples);
+  * the final weights (final_model.pt) against the oracle's after 5 Adam steps.
+Tolerances: fp32 vs fp32 (S3 engine), the north-star's 1e-3 relative: losses 1e-4 relative, val
+metrics 1e-3, weights within 2 lr per step (Adam's first steps are ~lr sign(g)) and 1e-5 mean."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+import yaml
+
+from conftest import ROOT
+from test_checkpoint import _read_all, _write
+
+pytestmark = pytest.mark.gpu
+
+PKG = os.path.join(ROOT, "camera-aware-neural-networks-for-few-view-depth-estimation_amd")
+TRAIN = os.path.join(ROOT, "build", "train")
+N_TRAIN, N_VAL, BS, HW, F, SEED = 10, 4, 2, 128, 64, 42
+LR = 1e-4
+
+
+def _batches(cad, oracle, n, seed):
+    ds = cad.SunRGBDDataset.synthetic(n, HW, HW, seed=seed)
+    out = []
+    for i in range(n):
+        s = ds.read(i)
+        out.append(oracle.get_sample(s["rgb"], s["depth"], s["K"], HW, HW, depth_scale=s["depth_scale"]))
+    return out
+
+
+def test_config0_build_train_vs_oracle_trajectory(cad, dev, oracle, tmp_path):
+    params, bufs = oracle.init_params(F, seed=SEED), oracle.init_buffers(F)
+    init = tmp_path / "init.pt"
+    _write(cad, init, params, bufs)
+    cfg = yaml.safe_load(open(os.path.join(ROOT, "configs", "train_config.yaml")))
+    cfg["data"].update(dataset_name="synthetic", num_train_samples=N_TRAIN, num_val_samples=N_VAL,
+                       input_height=HW, input_width=HW)
+    cfg["model"].update(architecture="baseline_unet", init_features=F)
+    cfg["experiment"]["seed"] = SEED
+    cfg["training"].update(num_epochs=1, batch_size=BS, log_interval=1, val_interval=1)
+    cfg["checkpointing"].update(checkpoint_dir=str(tmp_path / "ckpt"), save_interval=1)
+    cfg["logging"]["log_dir"] = str(tmp_path / "logs")
+    p = tmp_path / "cfg.yaml"
+    p.write_text(yaml.safe_dump(cfg))
+    subprocess.run(["make", "-C", PKG, "train"], check=True, capture_output=True)
+    r = subprocess.run([TRAIN, "-c", str(p), "-r", str(init)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "Loaded model weights" in r.stdout
+
+    logs = tmp_path / "logs" / "baseline_unet"
+    tb = [l.split(",") for l in (logs / "tensorboard_scalars.csv").read_text().splitlines()]
+    step_losses = [float(v) for tag, _, v in tb if tag == "batch_loss/train"]
+    row = (logs / "metrics.csv").read_text().strip().splitlines()
+    hdr, vals = row[0].split(","), row[1].split(",")
+    m = dict(zip(hdr, vals))
+
+    # the oracle on the same batches, in the trainer's order (one rank: samples 0..9 in pairs)
+    train = _batches(cad, oracle, N_TRAIN, SEED)
+    ref = oracle.Trainer(params, bufs)
+    ref_losses = []
+    for b in range(0, N_TRAIN, BS):
+        rgb, gt, K = (torch.stack([t[k] for t in train[b:b + BS]]) for k in range(3))
+        ref_losses.append(ref.step(rgb, gt, K)["loss"])
+    assert len(step_losses) == len(ref_losses) == N_TRAIN // BS, (step_losses, ref_losses)
+    np.testing.assert_allclose(step_losses, ref_losses, rtol=1e-4)
+    assert abs(float(m["train_loss"]) - np.mean(ref_losses)) <= 1e-4 * np.mean(ref_losses)
+
+    # validation: per-sample eval forwards of the validation split (seed + 1), loss and abs_rel averaged
+    val = _batches(cad, oracle, N_VAL, SEED + 1)
+    v_loss, v_abs = [], []
+    for rgb, gt, K in val:
+        pe = ref.predict_eval(rgb[None])
+        total, _ = oracle.combined_loss(pe, gt[None], rgb[None], K[None])
+        v_loss.append(float(total))
+        v_abs.append(oracle.depth_metrics(pe, gt[None])["abs_rel"])
+    assert abs(float(m["val_loss"]) - np.mean(v_loss)) <= 1e-3 * np.mean(v_loss), (m["val_loss"], np.mean(v_loss))
+    assert abs(float(m["abs_rel"]) - np.mean(v_abs)) <= 1e-3 * np.mean(v_abs), (m["abs_rel"], np.mean(v_abs))
+
+    # final weights after 5 Adam steps
+    got = _read_all(cad, tmp_path / "ckpt" / "baseline_unet" / "final_model.pt")
+    k = N_TRAIN // BS
+    for n, v in ref.p.items():
+        d = np.abs(got[n] - v.numpy())
+        assert d.max() <= 2 * LR * k + 1e-6 and d.mean() < 1e-5, (n, d.max(), d.mean())
+    for n, v in ref.bufs.items():
+        assert np.abs(got[n] - v.numpy()).max() <= 1e-4 * max(1.0, np.abs(v.numpy()).max()), n

@@ -16,7 +16,7 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
-from conftest import ROOT, max_rel_err
+from conftest import grad_close, ROOT, max_rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -144,8 +144,9 @@ def test_two_rank_gloo_step_vs_oracle_dp(oracle):
         assert torch.equal(torch.from_numpy(res[1][5][n]), torch.from_numpy(res[0][5][n])), n
         cos = torch.nn.functional.cosine_similarity(ours.reshape(1, -1), gd.reshape(1, -1)).item()
         e, e32 = max_rel_err(ours, gd), max_rel_err(g32, gd)
-        if not (cos >= 0.9999 and e <= max(0.25, 3 * e32)):   # criterion of test_gpu_model.py
-            bad.append(("grad", n, cos, e, e32))
+        ok, st = grad_close(ours, gd, [g32], bulk_floor=5e-3)   # criterion of test_gpu_model.py
+        if not (cos >= 0.9999 and ok):
+            bad.append(("grad", n, cos, e, e32, st))
         d = (torch.from_numpy(res[0][2][n]) - t.p[n]).abs()
         if d.max().item() > 2 * lr + 1e-6:
             bad.append(("step", n, d.max().item()))
@@ -162,3 +163,41 @@ def test_two_rank_gloo_step_vs_oracle_dp(oracle):
     for r in range(world):
         for n, b in res[r][3].items():
             assert max_rel_err(torch.from_numpy(b), shard[r].bufs[n]) < 1e-4, (r, n)
+
+
+@pytest.mark.parametrize("model,engine", [("baseline", 1), ("baseline", 2), ("rayfilm", 2)])
+def test_backward_stage_writes_stay_in_range(cad, dev, oracle, model, engine):
+    """The overlapped exchange (cad_unet_backward_allreduce, dp.cpp) all-reduces a bucket in place on
+    the communicator's stream while the compute stream runs the later backward stages; that is only
+    correct if no stage writes a gradient outside its own slab range.  Fill the slab with
+    a sentinel, run the backward stage by stage, and check after each stage that it changed nothing
+    outside [offset, offset + count) — in particular nothing of the buckets already handed over."""
+    lib = cad.load_library()
+    prev = lib.cad_get_gemm_engine()
+    lib.cad_set_gemm_engine(engine)
+    try:
+        f, B, H, W = 16, 2, 64, 64
+        cls = {"baseline": cad.BaselineUNet, "rayfilm": cad.RayConditionedUNet}[model]
+        m = cls(3, f, 10.0, batch=B, height=H, width=W)
+        rgb, gt, K = [torch.from_numpy(a).to(dev) for a in oracle.synth_batch(B, H, W)]
+        loss = cad.CombinedDepthLoss(batch=B, height=H, width=W)
+        pred = m(rgb, cad.camera_from_K(K)) if m.conditioned else m(rgb)
+        _, dpred = loss.forward_with_intrinsics(pred, gt, rgb, K)
+        torch.cuda.synchronize()
+        m.flat_grads.fill_(1234.5)
+        snaps = [m.flat_grads.clone()]
+
+        def on_stage(s, off, cnt):
+            torch.cuda.synchronize()
+            cur = m.flat_grads.clone()
+            changed = (cur != snaps[-1]).nonzero().flatten()
+            outside = changed[(changed < off) | (changed >= off + cnt)]
+            assert outside.numel() == 0, (s, off, cnt, outside[:8].tolist())
+            snaps.append(cur)
+        m.backward(dpred, on_stage=on_stage)
+        torch.cuda.synchronize()
+        assert len(snaps) == m.num_stages + 1
+        # every parameter gradient was written by some stage
+        assert not (m.flat_grads == 1234.5).all()
+    finally:
+        lib.cad_set_gemm_engine(prev)

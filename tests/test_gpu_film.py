@@ -172,7 +172,7 @@ def test_film_train_step_vs_oracle(cad, dev, oracle, model, f, B, H, W):
         cos = torch.nn.functional.cosine_similarity(grads[n].double().reshape(1, -1), g64.reshape(1, -1)).item()
         # the 6x8 / 3x4 deep levels of these nets leave a few hundred pixels per BN channel, and
         # FiLM's BatchNorm1d sees B samples: LibTorch fp32 itself lands ~1e-2 off fp64 there
-        ok, st = grad_close(grads[n], g64, [g32], k=5.0, bulk_floor=2e-2)
+        ok, st = grad_close(grads[n], g64, [g32], k=5.0, bulk_floor=5e-3)
         assert cos > 0.999 and ok, (n, cos, st)
     ref64 = oracle.Trainer(params, bufs, dtype=torch.float64, model=model)
     ref64.step(rgb, gt, K)
@@ -246,7 +246,8 @@ def test_film_train_step_bf16_engine_vs_oracle(cad, dev, oracle, bf16_engine, mo
         # fp32-vs-fp64 accumulation does (the multi-step outputs below stay tight)
         k = 5 if (".film." in n and not n.endswith(("fc_gamma.bias", "fc_beta.bias", "fc_gamma.weight",
                                                      "fc_beta.weight"))) else 3
-        assert cos > min(0.999, 1 - k * (1 - cos32)) and ours < max(0.25, 5 * ref32), (n, cos, cos32, ours, ref32)
+        ok, st = grad_close(grads[n], g64, [g32], k=k, bulk_floor=5e-3)
+        assert cos > min(0.999, 1 - k * (1 - cos32)) and ok, (n, cos, cos32, ours, ref32, st)
     cad.clip_grad_norm_(net, 1.0)
     tr.optimizer.step()
     for _ in range(3):

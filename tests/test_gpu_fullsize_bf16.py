@@ -1,0 +1,224 @@
+"""Parity at the benchmarked size for the bf16 workloads: one bs32 480x640
+training step of
+
+  * configs[2]: the ray + FiLM conditioned U-Net (SURVEY §8 "recommended config-3 model":
+    RayEnhancedConv enc1 + FiLM blocks, intrinsics_unet.h:16-113, geometry_aware_network.h:26-65),
+  * configs[3]'s per-GPU step: baseline_unet (baseline_unet.h:122-208),
+  * configs[4]'s per-GPU step: the ResNet-50 encoder + U-Net decoder (no reference model: PARITY
+    UNPINNED, bounded against oracle/resunet_oracle.py),
+
+on the B1 engine (bf16 contraction operands, fp32 accumulation; BN / FiLM / head / loss / clip / Adam
+in fp32) with the full 4-term loss, against the oracle run on the box's host cores with the SAME
+operand rounding in fp32 (cad_oracle.Trainer(gemm_operands="bf16"); resunet_oracle operands="bf16").
+Step = TensorBoardTrainerEnhanced::trainEpoch body (tensorboard_trainer_enhanced.h:287-304).
+
+What only this size exercises: the bf16 twin buffers past 2 GB, the B1 weight-gradient slab
+reductions over ~1800 slabs, BN statistics over 9.8 M pixels, the FiLM / ray pack over 9.8 M pixels
+per batch, clip over all gradients.
+
+Both sides round the same operands to bf16, but an fp32 difference of one ulp in a value that sits
+next to a bf16 rounding boundary becomes a one-bf16-ulp (2^-8) difference of that operand: about
+1e-6 / 4e-3 of the rounded values differ by 4e-3 relative on every layer, on either side.  So the
+criteria (measured values in DESIGN.md §5) are: prediction and dL/dpred within 1e-3 normalised max
+error (the north-star bound), every loss term and the clip norm within 1e-4 relative, every parameter
+gradient at cosine >= 0.9999 with its bulk (99.9th percentile of |ours - oracle| / max|oracle|)
+within 5e-3, parameters after Adam within 2 lr (Adam's first step is ~lr sign(g)) with fewer than
+1e-4 of them moving by more than 1e-5, BN running statistics within 1e-4, and the eval-mode
+prediction / abs_rel of the updated model within 1e-3.  No fp64 run at this size (the fp32 configs[1]
+test, test_gpu_fullsize.py, already spends ~5 minutes of host time on one)."""
+import sys
+import threading
+import time
+
+import pytest
+import torch
+
+from conftest import max_rel_err
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+B, H, W, F = 32, 480, 640, 64
+WEIGHTS = (1.0, 0.1, 0.001, 0.01)
+LR = 1e-4
+
+_CAPMAN = [None]
+
+
+def _beat(msg, t0):
+    line = f"[fullsize-bf16 +{time.time() - t0:6.1f}s] {msg}"
+    cm = _CAPMAN[0]
+    if cm is None:
+        print(line, file=sys.__stderr__, flush=True)
+        return
+    with cm.global_and_fixture_disabled():
+        print(line, file=sys.stderr, flush=True)
+
+
+def _heartbeat(t0, stop, period=30.0):
+    while not stop.wait(period):
+        _beat("... oracle still running", t0)
+
+
+@pytest.fixture
+def bf16_engine(cad):
+    lib = cad.load_library()
+    prev = lib.cad_get_gemm_engine()
+    assert lib.cad_set_gemm_engine(2) == 0   # CAD_GEMM_BF16
+    yield
+    lib.cad_set_gemm_engine(prev)
+
+
+@pytest.fixture
+def beat(pytestconfig):
+    _CAPMAN[0] = pytestconfig.pluginmanager.getplugin("capturemanager")
+    t0 = time.time()
+    stop = threading.Event()
+    threading.Thread(target=_heartbeat, args=(t0, stop), daemon=True).start()
+    yield lambda msg: _beat(msg, t0)
+    stop.set()
+
+
+def _cos(a, b):
+    return torch.nn.functional.cosine_similarity(a.double().reshape(1, -1), b.double().reshape(1, -1)).item()
+
+
+def _bulk(a, b):
+    e = (a.double() - b.double()).abs().flatten() / (b.abs().max().item() or 1.0)
+    return torch.quantile(e, 0.999).item() if e.numel() > 1 else e.max().item()
+
+
+def _judge(beat, g, r, g_grads, g_norm, g_params, g_bufs, ref_p, ref_bufs, spec, params0):
+    """Shared criteria (module docstring).  g: dict of GPU results, r: the oracle step."""
+    e_pred = max_rel_err(g["pred"], r["pred"])
+    e_dpred = max_rel_err(g["dpred"], r["dpred"])
+    l5 = g["loss5"]
+    comps = [r["loss"], r["comps"]["si_loss"], r["comps"]["grad_loss"], r["comps"]["smooth_loss"],
+             r["comps"]["reproj_loss"]]
+    e_loss = [abs(a - b) / abs(b) for a, b in zip(l5, comps)]
+    e_norm = abs(g_norm - r["norm"]) / r["norm"]
+    rows = []
+    for (n, _), gr in zip(spec, r["grads"]):
+        if gr is None:
+            continue
+        rows.append((_bulk(g_grads[n], gr), 1 - _cos(g_grads[n], gr), max_rel_err(g_grads[n], gr), n))
+    rows.sort(reverse=True)
+    moved, worst_move, n_all = 0, 0.0, 0
+    for n, p in g_params.items():
+        d = (p - ref_p[n]).abs()
+        moved += int((d > 1e-5).sum())
+        n_all += d.numel()
+        worst_move = max(worst_move, d.max().item())
+    e_bufs = max(max_rel_err(b, ref_bufs[n]) for n, b in g_bufs.items()) if g_bufs else 0.0
+    beat(f"pred {e_pred:.3e}  dpred {e_dpred:.3e}  loss terms {[f'{x:.2e}' for x in e_loss]}  clip norm {e_norm:.2e}")
+    beat(f"gradients (bulk, 1-cos, max, name), worst by bulk: {rows[:4]}")
+    beat(f"worst 1-cos: {max(x[1] for x in rows):.3e}; params after Adam: max |diff| {worst_move:.3e}, "
+         f"{moved} of {n_all} moved > 1e-5; BN buffers {e_bufs:.2e}")
+    assert e_pred < 1e-3, e_pred
+    assert e_dpred < 1e-3, e_dpred
+    assert max(e_loss) < 1e-4, e_loss
+    assert e_norm < 1e-4, (g_norm, r["norm"])
+    bad = [x for x in rows if not (x[0] <= 5e-3 and x[1] <= 1e-4)]
+    assert not bad, bad[:5]
+    assert worst_move <= 2 * LR + 1e-6 and moved <= 1e-4 * n_all, (worst_move, moved, n_all)
+    assert e_bufs < 1e-4, e_bufs
+
+
+@pytest.mark.timeout(1500)
+@pytest.mark.parametrize("model", ["rayfilm", "baseline"])
+def test_bs32_480x640_bf16_step_vs_oracle(cad, dev, oracle, bf16_engine, beat, model):
+    """configs[2] (rayfilm) and configs[3]'s per-GPU step (baseline) at the benchmarked size."""
+    params = oracle.init_params(F, seed=42, model=model)
+    bufs = oracle.init_buffers(F, model=model)
+    rgb, gt, K = [torch.from_numpy(a) for a in oracle.synth_batch(B, H, W)]
+    cls = {"baseline": cad.BaselineUNet, "rayfilm": cad.RayConditionedUNet}[model]
+    m = cls(3, F, 10.0, batch=B, height=H, width=W)
+    assert m.count_parameters() == {"baseline": 31037633, "rayfilm": 32862465}[model]
+    state = dict(params)
+    state.update(bufs)
+    m.load_state_dict(state)
+    loss = cad.CombinedDepthLoss(*WEIGHTS, batch=B, height=H, width=W)
+    tr = cad.Trainer(m, loss, lr=LR, weight_decay=1e-5, grad_clip=1.0)
+    rg, gg, kg = rgb.to(dev), gt.to(dev), K.to(dev)
+    m.train()
+    beat(f"{model}: GPU step")
+    pred = m(rg, cad.camera_from_K(kg)) if m.conditioned else m(rg)
+    loss5, dpred = loss.forward_with_intrinsics(pred, gg, rg, kg)
+    m.backward(dpred)
+    torch.cuda.synchronize()
+    g = {"pred": pred.cpu(), "dpred": dpred.cpu(), "loss5": loss5.cpu().tolist()}
+    g_grads = m.grads()
+    cad.clip_grad_norm_(m, 1.0)
+    tr.optimizer.step()
+    torch.cuda.synchronize()
+    g_norm = m.last_grad_norm()
+    g_params, g_bufs = m.named_parameters(), m.named_buffers()
+    m.eval()
+    g_eval = (m(rg[:4], cad.camera_from_K(kg[:4])) if m.conditioned else m(rg[:4])).cpu()
+    g_absrel = cad.depth_metrics(g_eval.to(dev), gg[:4])["abs_rel"]
+    del m, loss, tr, pred, dpred
+    torch.cuda.empty_cache()
+    beat(f"{model}: GPU step done (loss {g['loss5'][0]:.6f}); oracle step (bf16 operands, fp32) on the host")
+
+    ref = oracle.Trainer(params, bufs, weights=WEIGHTS, model=model, gemm_operands="bf16")
+    r = ref.step(rgb, gt, K)
+    beat(f"{model}: oracle step done (loss {r['loss']:.6f})")
+    _judge(beat, g, r, g_grads, g_norm, g_params, {k: v for k, v in g_bufs.items() if "running" in k},
+           ref.p, ref.bufs, oracle.param_spec(F, model=model), params)
+    r_eval = ref.predict_eval(rgb[:4], K[:4] if model != "baseline" else None)
+    r_absrel = oracle.abs_rel_per_sample(r_eval, gt[:4])
+    e_eval = max_rel_err(g_eval, r_eval)
+    beat(f"{model}: eval pred {e_eval:.3e}; abs_rel gpu {g_absrel:.6f} cpu {r_absrel:.6f}")
+    assert e_eval < 1e-3, e_eval
+    assert abs(g_absrel - r_absrel) <= 1e-3 * r_absrel, (g_absrel, r_absrel)
+
+
+@pytest.mark.timeout(1500)
+def test_bs32_480x640_resunet_step_vs_oracle(cad, dev, oracle, beat):
+    """configs[4]'s per-GPU network at bs32 480x640 (PARITY UNPINNED: the reference has no ResNet
+    model; oracle/resunet_oracle.py restates the network with torch modules and the U-Net oracle's
+    loss / clip / Adam, with the GPU path's bf16 operand rounding)."""
+    from oracle import resunet_oracle as R
+    p, b = R.init(seed=3)
+    rgb, gt, K = [torch.from_numpy(a) for a in oracle.synth_batch(B, H, W)]
+    m = cad.ResNetUNet(batch=B, height=H, width=W)
+    state = dict(p)
+    state.update(b)
+    m.load_state_dict(state)
+    loss = cad.CombinedDepthLoss(*WEIGHTS, batch=B, height=H, width=W)
+    rg, gg, kg = rgb.to(dev), gt.to(dev), K.to(dev)
+    beat("resunet: GPU step")
+    pred = m.forward(rg)
+    loss5, dpred = loss.forward_with_intrinsics(pred, gg, rg, kg)
+    m.backward(dpred)
+    torch.cuda.synchronize()
+    g = {"pred": pred.cpu(), "dpred": dpred.cpu(), "loss5": loss5.cpu().tolist()}
+    g_grads = m.grads()
+    m.clip_grad_norm_(1.0)
+    m.adam_step(lr=LR, weight_decay=1e-5)
+    torch.cuda.synchronize()
+    g_norm = m.last_grad_norm()
+    g_params, g_bufs = m.named_parameters(), m.named_buffers()
+    del m, loss, pred, dpred
+    torch.cuda.empty_cache()
+    beat("resunet: oracle step (bf16 operands, fp32) on the host")
+    ref = R.Trainer(p, b, WEIGHTS, operands="bf16")
+    r = ref.step(rgb, gt, K)
+    beat(f"resunet: oracle done (loss {r['loss']:.6f}, ours {g['loss5'][0]:.6f})")
+    # deep in a random-init ResNet-50 BatchNorm over few pixels per channel amplifies rounding-flip
+    # noise (test_gpu_resunet.py: the fp32-accumulation emulation itself sits at whole-gradient cosine
+    # ~0.95 from fp64 at B=2); at bs32 480x640 every BN normalises over >= 9600 values per channel
+    e_pred = max_rel_err(g["pred"], r["pred"])
+    e_loss = abs(g["loss5"][0] - r["loss"]) / abs(r["loss"])
+    e_norm = abs(g_norm - r["norm"]) / r["norm"]
+    flat = torch.cat([g_grads[n].reshape(-1) for n, _ in R.param_spec()])
+    flat_r = torch.cat([x.reshape(-1) for x in r["grads"]])
+    cos_all = _cos(flat, flat_r)
+    rows = sorted(((1 - _cos(g_grads[n], gr), n) for (n, _), gr in zip(R.param_spec(), r["grads"])), reverse=True)
+    beat(f"resunet: pred {e_pred:.3e}; loss {e_loss:.2e}; clip norm {e_norm:.2e}; whole-gradient cosine "
+         f"{cos_all:.6f}; worst (1-cos, name): {rows[:3]}")
+    assert e_pred < 1e-2, e_pred
+    assert e_loss < 1e-3, e_loss
+    assert e_norm < 1e-2, e_norm
+    assert cos_all > 0.999, cos_all
+    worst_move = max((v - ref.p[n]).abs().max().item() for n, v in g_params.items())
+    assert worst_move <= 2 * LR + 1e-6, worst_move

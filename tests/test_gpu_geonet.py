@@ -40,6 +40,23 @@ def _noise_grad_param(name, B):
     return _zero_grad_bias(name, B) or (B == 2 and name.endswith("film.fc1.weight"))
 
 
+def cbam_decisions(net, model, oracle):
+    """{CBAM prefix: (argmax pixel [B][C], argmax channel [B][H][W])} of the net's last forward
+    (cad_geonet_debug_buffer "amax*/sidx*"), keyed like cad_oracle.GEO_DEBUG["force"] so the
+    restatement routes its max-pool gradients exactly as the GPU run did."""
+    nl, enc = oracle._geo_names(model)
+    out = {}
+    for l in range(1, nl):
+        try:
+            a = net.debug_buffer(f"amaxe{l}").long()
+        except KeyError:
+            return {}
+        out[f"{enc[l]}.attention."] = (a, net.debug_buffer(f"sidxe{l}").long())
+    for l in range(nl - 1):
+        out[f"dec{l + 1}.attention."] = (net.debug_buffer(f"amaxd{l}").long(), net.debug_buffer(f"sidxd{l}").long())
+    return out
+
+
 def _q(err, q=0.999):
     return torch.quantile(err.flatten().double(), q).item() if err.numel() > 1 else err.max().item()
 
@@ -199,7 +216,7 @@ def _wider(cad, dev, oracle, model, f, B, H, W):
     # is therefore run with the GPU's own decisions (cad_geonet_debug_buffer "amax*/sidx*") — each
     # checked to be a true argmax of the fp64 run within 1e-4 relative, the fp32 forward's own drift
     # from fp64 at the deepest levels (4e-5 measured) — and the gradients compared tightly.
-    oracle.GEO_DEBUG["force"] = net.cbam_decisions(model)
+    oracle.GEO_DEBUG["force"] = cbam_decisions(net, model, oracle)
     oracle.GEO_DEBUG["gap"] = []
     try:
         r32 = oracle.Trainer(params, bufs, model=model).forward_backward(rgb, gt, K)

@@ -111,7 +111,7 @@ def test_train_step_vs_oracle(cad, dev, oracle, f, B, H, W):
         # 1.3e-3..2.4e-3 (sum_pix dY * rgb with rgb >= 0 cancels ~150x, so it carries the level-0 dY's
         # accumulated fp32 error; the wgrad kernel alone is 7e-7 from fp64 on such data) and mid-level
         # BN biases up to 1.2e-2 (sums over a few thousand pixels that move with ReLU decisions near 0)
-        ok, st = grad_close(grads[n], g64, [g32], bulk_floor=2e-2)
+        ok, st = grad_close(grads[n], g64, [g32], bulk_floor=5e-3)
         assert cos > 0.9999 and ok, (n, cos, st)
     # finish step 1 and run three more on every side; compare the outputs (train- and eval-mode)
     # against fp64: within 1e-3, or within 3x the LibTorch fp32 path's own drift from fp64
@@ -207,7 +207,7 @@ def test_train_step_bf16_engine_vs_oracle(cad, dev, oracle, bf16_engine, f, B, H
         ours, ref32 = max_rel_err(grads[n], g64), max_rel_err(g32, g64)
         cos = torch.nn.functional.cosine_similarity(grads[n].double().reshape(1, -1), g64.reshape(1, -1)).item()
         cos32 = torch.nn.functional.cosine_similarity(g32.double().reshape(1, -1), g64.reshape(1, -1)).item()
-        ok, st = grad_close(grads[n], g64, [g32], bulk_floor=2e-2)
+        ok, st = grad_close(grads[n], g64, [g32], bulk_floor=5e-3)
         assert cos > min(0.999, 1 - 3 * (1 - cos32)) and ok, (n, cos, cos32, st)
     cad.clip_grad_norm_(model, 1.0)
     tr.optimizer.step()
