@@ -986,6 +986,7 @@ int64_t cad_unet_debug_buffer(cad_unet* h, const char* name, float* host, int64_
         return n[pre.size()] - '0';
     };
     int l;
+    bool bf16 = false;   // the buffer holds bf16 values (widened to fp32 on the copy)
     if (n == "x0") { p = h->x0; cnt = h->Ml(0, B) * h->x0_ld; }
     else if (n == "Sa" || n == "Sb") { p = n == "Sa" ? h->Sa : h->Sb; cnt = h->Ml(0, B) * h->Cl(0); }
     else if (n == "Sc") { p = h->Sc; cnt = h->Ml(1, B) * h->Cl(0); }
@@ -999,6 +1000,7 @@ int64_t cad_unet_debug_buffer(cad_unet* h, const char* name, float* host, int64_
         const std::string t = n.size() > 5 ? n.substr(5) : "";
         p = t == "y1" ? dc.y1 : t == "a1" ? dc.a1 : t == "y2" ? dc.y2 : nullptr;
         cnt = p ? h->Ml(l, B) * h->Cl(l) : -1;
+        bf16 = (t == "y1" && dc.y1b) || (t == "y2" && dc.y2b);
         if (dc.has_film() && (t == "gamma" || t == "beta")) {
             p = t == "gamma" ? dc.film.gam : dc.film.bet;
             cnt = (int64_t)B * h->Cl(l);
@@ -1016,8 +1018,7 @@ int64_t cad_unet_debug_buffer(cad_unet* h, const char* name, float* host, int64_
         const bool twin_only = n == "Sb" || n == "bott" || (n.compare(0, 4, "pool") == 0) ||
                                (n.compare(0, 3, "cat") == 0) ||   // up half: twin only
                                (n.compare(0, 4, "dout") == 0 && n != "dout0") ||
-                               (!film && n.size() > 5 && n.substr(5) == "a1") ||
-                               (n.size() > 5 && (n.substr(5) == "y1" || n.substr(5) == "y2"));   // bf16 values
+                               (!film && n.size() > 5 && n.substr(5) == "a1");
         if (twin_only) {
             g_err = "debug buffer '" + n + "' holds no fp32 copy on the pre-split (bf16) engine";
             return -1;
@@ -1026,7 +1027,16 @@ int64_t cad_unet_debug_buffer(cad_unet* h, const char* name, float* host, int64_
     if (host) {
         if (numel < cnt) return -1;
         if (hipDeviceSynchronize() != hipSuccess) return -1;
-        if (hipMemcpy(host, p, sizeof(float) * cnt, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+        if (bf16) {   // pre-BN conv outputs of the bf16 engine: the stored bf16 values, widened
+            std::vector<uint16_t> tmp((size_t)cnt);
+            if (hipMemcpy(tmp.data(), p, sizeof(uint16_t) * cnt, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+            for (int64_t i = 0; i < cnt; ++i) {
+                const uint32_t u = (uint32_t)tmp[(size_t)i] << 16;
+                std::memcpy(host + i, &u, 4);
+            }
+        } else if (hipMemcpy(host, p, sizeof(float) * cnt, hipMemcpyDeviceToHost) != hipSuccess) {
+            return -1;
+        }
     }
     return cnt;
 }

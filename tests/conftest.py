@@ -64,3 +64,40 @@ def grad_close(ours, g64, witnesses, k=3.0, bulk_floor=1e-3, max_floor=5e-2):
     wm = max(err(w).max().item() for w in witnesses)
     ok = bulk(e) <= max(bulk_floor, k * wb) and e.max().item() <= max(max_floor, k * wm)
     return ok, (e.max().item(), bulk(e), wb)
+
+
+def unet_bn_blocks(model="baseline"):
+    """(GPU debug-buffer tag, oracle DoubleConv prefix, level) of every DoubleConv of the U-Net family:
+    enc0..enc4 = enc1, enc2.conv .. bottleneck.conv; dec0..dec3 = dec1.conv .. dec4.conv."""
+    enc = [("enc0", "enc1.", 0)] + [(f"enc{l}", f"{n}.conv.", l)
+                                     for l, n in zip(range(1, 5), ("enc2", "enc3", "enc4", "bottleneck"))]
+    return enc + [(f"dec{l}", f"dec{l + 1}.conv.", l) for l in range(4)]
+
+
+def gpu_relu_decisions(net, params, f, B, H, W, model="baseline"):
+    """The ReLU decisions of `net`'s last train-mode forward, for cad_oracle.RELU_FORCE.
+
+    Rebuilt from the stored pre-BN conv outputs (cad_unet_debug_buffer "<tag>_y1|_y2", the values the
+    GPU normalised) exactly as the BN-apply kernel takes them: batch statistics in fp64, mean and
+    1/sqrt(var + eps) rounded to fp32, scale = gamma * invstd and shift = beta - mean * scale in fp32,
+    decision = sign(y * scale + shift) (the kernel's fused multiply-add keeps the exact sign, which the
+    fp64 evaluation of the same product and sum reproduces)."""
+    import numpy as np
+    import torch
+    masks = {}
+    eps = float(np.float32(1e-5))
+    for tag, pre, l in unet_bn_blocks(model):
+        C, h, w = f << l, H >> l, W >> l
+        for k in ("1", "2"):
+            y = net.debug_buffer(f"{tag}_y{k}")[: B * h * w * C].double().reshape(B * h * w, C)
+            mu = y.mean(0)
+            var = y.var(0, unbiased=False)
+            mu32 = mu.float()
+            inv = (1.0 / torch.sqrt(var + eps)).float()
+            g = params[pre + "bn" + k + ".weight"].float()
+            b = params[pre + "bn" + k + ".bias"].float()
+            sc = g * inv
+            sh = (b.double() - mu32.double() * sc.double()).float()   # fma(-mean, scale, beta)
+            z = y * sc.double() + sh.double()
+            masks[pre + "bn" + k] = (z > 0).reshape(B, h, w, C).permute(0, 3, 1, 2).contiguous()
+    return masks

@@ -94,10 +94,13 @@ def _gloo_worker(rank, world, port, q):
         # when this process exits
         np_ = lambda d: {k: v.numpy() for k, v in d.items()}
         # grads(): the exchanged mean gradient as the clip left it (clip scales in place)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from conftest import gpu_relu_decisions
+        masks = np_(gpu_relu_decisions(m, params, F, B, H, W))   # this shard's ReLU decisions
         q.put((rank, l, m.flat_params.cpu().numpy(), np_(m.named_parameters()), np_(m.named_buffers()),
-               m.last_grad_norm(), np_(m.grads()), None))
+               m.last_grad_norm(), np_(m.grads()), masks, None))
     except Exception as e:   # report instead of hanging the parent on q.get
-        q.put((rank, None, None, None, None, None, None, repr(e)))
+        q.put((rank, None, None, None, None, None, None, None, repr(e)))
     dist.destroy_process_group()
 
 
@@ -120,18 +123,22 @@ def test_two_rank_gloo_step_vs_oracle_dp(oracle):
     # oracle emulation: per-shard forward/backward (own BN batch statistics), mean, clip, Adam
     params, bufs = oracle.init_params(F, seed=7), oracle.init_buffers(F)
     rgb, gt, K = [torch.from_numpy(a) for a in oracle.synth_batch(B * world, H, W)]
-    shard, grads = [], []
-    for r in range(world):
-        t = oracle.Trainer(params, bufs, weights=WEIGHTS)
-        _, _, lr_, _, g = t.forward_backward(rgb[r * B:(r + 1) * B], gt[r * B:(r + 1) * B], K[r * B:(r + 1) * B])
+    shard, grads, grads64 = [], [], []
+    for r in range(world):   # each shard with its replica's ReLU decisions (see test_gpu_model.py)
+        oracle.RELU_FORCE.update({k: torch.from_numpy(v) for k, v in res[r][6].items()})
+        try:
+            t = oracle.Trainer(params, bufs, weights=WEIGHTS)
+            sh = (rgb[r * B:(r + 1) * B], gt[r * B:(r + 1) * B], K[r * B:(r + 1) * B])
+            _, _, lr_, _, g = t.forward_backward(*sh)
+            # the exact-arithmetic yardstick: the same shard in fp64
+            grads64.append(oracle.Trainer(params, bufs, weights=WEIGHTS, dtype=torch.float64).forward_backward(*sh)[4])
+        finally:
+            oracle.RELU_FORCE.clear()
         shard.append(t)
         grads.append(g)
         assert abs(res[r][0] - float(lr_)) <= 1e-4 * abs(float(lr_)), (r, res[r][0], float(lr_))
     mean = [sum(gs) / world for gs in zip(*grads)]
-    # the exact-arithmetic yardstick: the same two shards in fp64
-    mean64 = [sum(gs) / world for gs in zip(*[
-        oracle.Trainer(params, bufs, weights=WEIGHTS, dtype=torch.float64).forward_backward(
-            rgb[r * B:(r + 1) * B], gt[r * B:(r + 1) * B], K[r * B:(r + 1) * B])[4] for r in range(world)])]
+    mean64 = [sum(gs) / world for gs in zip(*grads64)]
     t = oracle.Trainer(params, bufs, weights=WEIGHTS)
     t.apply(mean)
     lr, wd, eps = 1e-4, 1e-5, 1e-8
@@ -178,7 +185,7 @@ def test_backward_stage_writes_stay_in_range(cad, dev, oracle, model, engine):
     try:
         f, B, H, W = 16, 2, 64, 64
         cls = {"baseline": cad.BaselineUNet, "rayfilm": cad.RayConditionedUNet}[model]
-        m = cls(3, f, 10.0, batch=B, height=H, width=W)
+        m = cls(3, f, max_depth=10.0, batch=B, height=H, width=W)
         rgb, gt, K = [torch.from_numpy(a).to(dev) for a in oracle.synth_batch(B, H, W)]
         loss = cad.CombinedDepthLoss(batch=B, height=H, width=W)
         pred = m(rgb, cad.camera_from_K(K)) if m.conditioned else m(rgb)

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import GOLDEN, grad_close, max_rel_err
+from conftest import GOLDEN, grad_close, gpu_relu_decisions, max_rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -149,9 +149,6 @@ def test_film_train_step_vs_oracle(cad, dev, oracle, model, f, B, H, W):
     params = oracle.init_params(f, seed=f, model=model)
     bufs = oracle.init_buffers(f, model=model)
     rgb, gt, K = [torch.from_numpy(a) for a in oracle.synth_batch(B, H, W)]
-    ref = oracle.Trainer(params, bufs, model=model)
-    r = ref.step(rgb, gt, K)
-    r64 = oracle.Trainer(params, bufs, dtype=torch.float64, model=model).step(rgb, gt, K)
     state = dict(params)
     state.update(bufs)
     net, loss, tr = _build(cad, model, f, B, H, W, (1.0, 0.1, 0.001, 0.01), state)
@@ -160,6 +157,13 @@ def test_film_train_step_vs_oracle(cad, dev, oracle, model, f, B, H, W):
     loss5, dpred = loss.forward_with_intrinsics(pred, gg, rg, kg)
     net.backward(dpred)
     torch.cuda.synchronize()
+    ref = oracle.Trainer(params, bufs, model=model)
+    oracle.RELU_FORCE.update(gpu_relu_decisions(net, params, f, B, H, W, model))   # this run's ReLU ties
+    try:
+        r = ref.step(rgb, gt, K)
+        r64 = oracle.Trainer(params, bufs, dtype=torch.float64, model=model).step(rgb, gt, K)
+    finally:
+        oracle.RELU_FORCE.clear()
     assert max_rel_err(pred.cpu(), r["pred"]) < 1e-4
     assert abs(loss5[0].item() - r["loss"]) <= 1e-4 * abs(r["loss"])
     grads = net.grads()
@@ -215,10 +219,6 @@ def test_film_train_step_bf16_engine_vs_oracle(cad, dev, oracle, bf16_engine, mo
     params = oracle.init_params(f, seed=f, model=model)
     bufs = oracle.init_buffers(f, model=model)
     rgb, gt, K = [torch.from_numpy(a) for a in oracle.synth_batch(B, H, W)]
-    ref = oracle.Trainer(params, bufs, model=model, gemm_operands="bf16")
-    ref64 = oracle.Trainer(params, bufs, dtype=torch.float64, model=model, gemm_operands="bf16")
-    exact64 = oracle.Trainer(params, bufs, dtype=torch.float64, model=model)
-    r, r64, e64 = ref.step(rgb, gt, K), ref64.step(rgb, gt, K), exact64.step(rgb, gt, K)
     state = dict(params)
     state.update(bufs)
     net, loss, tr = _build(cad, model, f, B, H, W, (1.0, 0.1, 0.001, 0.01), state)
@@ -227,6 +227,15 @@ def test_film_train_step_bf16_engine_vs_oracle(cad, dev, oracle, bf16_engine, mo
     loss5, dpred = loss.forward_with_intrinsics(pred, gg, rg, kg)
     net.backward(dpred)
     torch.cuda.synchronize()
+    ref = oracle.Trainer(params, bufs, model=model, gemm_operands="bf16")
+    ref64 = oracle.Trainer(params, bufs, dtype=torch.float64, model=model, gemm_operands="bf16")
+    exact64 = oracle.Trainer(params, bufs, dtype=torch.float64, model=model)
+    oracle.RELU_FORCE.update(gpu_relu_decisions(net, params, f, B, H, W, model))   # this run's ReLU ties
+    try:
+        r, r64 = ref.step(rgb, gt, K), ref64.step(rgb, gt, K)
+    finally:
+        oracle.RELU_FORCE.clear()
+    e64 = exact64.step(rgb, gt, K)
     assert max_rel_err(pred.cpu(), r64["pred"]) < max(1e-3, 5 * max_rel_err(r["pred"], r64["pred"]))
     assert abs(loss5[0].item() - r64["loss"]) <= max(1e-3 * abs(r64["loss"]), 5 * abs(r["loss"] - r64["loss"]))
     assert max_rel_err(pred.cpu(), e64["pred"]) < 5e-2

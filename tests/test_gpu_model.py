@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import grad_close, GOLDEN, max_rel_err
+from conftest import grad_close, gpu_relu_decisions, GOLDEN, max_rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -90,9 +90,6 @@ def test_train_step_vs_oracle(cad, dev, oracle, f, B, H, W):
     params = oracle.init_params(f, seed=f)
     bufs = oracle.init_buffers(f)
     rgb, gt, K = [torch.from_numpy(a) for a in oracle.synth_batch(B, H, W)]
-    ref = oracle.Trainer(params, bufs)
-    r = ref.step(rgb, gt, K)
-    r64 = oracle.Trainer(params, bufs, dtype=torch.float64).step(rgb, gt, K)
     state = dict(params)
     state.update(bufs)
     model, loss, tr = _build(cad, f, B, H, W, (1.0, 0.1, 0.001, 0.01), state)
@@ -101,6 +98,16 @@ def test_train_step_vs_oracle(cad, dev, oracle, f, B, H, W):
     loss5, dpred = loss.forward_with_intrinsics(pred, gg, rg, kg)
     model.backward(dpred)
     torch.cuda.synchronize()
+    # the oracle step takes this run's ReLU decisions (cad_oracle.RELU_FORCE): a pre-activation within
+    # rounding of 0 is a tie either fp32 path may break either way, and one such element moves a
+    # decoder BN bias gradient (per-pixel terms cancelling ~50x) by ~1% of its scale
+    oracle.RELU_FORCE.update(gpu_relu_decisions(model, params, f, B, H, W))
+    try:
+        ref = oracle.Trainer(params, bufs)
+        r = ref.step(rgb, gt, K)
+        r64 = oracle.Trainer(params, bufs, dtype=torch.float64).step(rgb, gt, K)
+    finally:
+        oracle.RELU_FORCE.clear()
     assert max_rel_err(pred.cpu(), r["pred"]) < 1e-4
     assert abs(loss5[0].item() - r["loss"]) <= 1e-4 * abs(r["loss"])
     grads = model.grads()
@@ -187,10 +194,6 @@ def test_train_step_bf16_engine_vs_oracle(cad, dev, oracle, bf16_engine, f, B, H
     params = oracle.init_params(f, seed=f)
     bufs = oracle.init_buffers(f)
     rgb, gt, K = [torch.from_numpy(a) for a in oracle.synth_batch(B, H, W)]
-    ref = oracle.Trainer(params, bufs, gemm_operands="bf16")
-    ref64 = oracle.Trainer(params, bufs, dtype=torch.float64, gemm_operands="bf16")
-    exact64 = oracle.Trainer(params, bufs, dtype=torch.float64)
-    r, r64, e64 = ref.step(rgb, gt, K), ref64.step(rgb, gt, K), exact64.step(rgb, gt, K)
     state = dict(params)
     state.update(bufs)
     model, loss, tr = _build(cad, f, B, H, W, (1.0, 0.1, 0.001, 0.01), state)
@@ -199,6 +202,15 @@ def test_train_step_bf16_engine_vs_oracle(cad, dev, oracle, bf16_engine, f, B, H
     loss5, dpred = loss.forward_with_intrinsics(pred, gg, rg, kg)
     model.backward(dpred)
     torch.cuda.synchronize()
+    ref = oracle.Trainer(params, bufs, gemm_operands="bf16")
+    ref64 = oracle.Trainer(params, bufs, dtype=torch.float64, gemm_operands="bf16")
+    exact64 = oracle.Trainer(params, bufs, dtype=torch.float64)
+    oracle.RELU_FORCE.update(gpu_relu_decisions(model, params, f, B, H, W))   # this run's ReLU ties
+    try:
+        r, r64 = ref.step(rgb, gt, K), ref64.step(rgb, gt, K)
+    finally:
+        oracle.RELU_FORCE.clear()
+    e64 = exact64.step(rgb, gt, K)
     assert max_rel_err(pred.cpu(), r64["pred"]) < max(1e-3, 5 * max_rel_err(r["pred"], r64["pred"]))
     assert abs(loss5[0].item() - r64["loss"]) <= max(1e-3 * abs(r64["loss"]), 5 * abs(r["loss"] - r64["loss"]))
     assert max_rel_err(pred.cpu(), e64["pred"]) < 5e-2
