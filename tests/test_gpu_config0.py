@@ -14,8 +14,8 @@ decoded u8 rgb, u16 depth, K) and assembled by the oracle's restatement of getSa
   * the final weights (final_model.pt) against the oracle's after 5 Adam steps.
 Tolerances: fp32 vs fp32 (S3 engine), the north-star's 1e-3 relative: losses 1e-4 relative, val
 metrics 1e-3, weights within 2 lr per step (Adam's first steps are ~lr sign(g), so a near-zero gradient
-whose sign two fp32 paths disagree on moves a weight by up to 2 lr) and 2e-5 mean (the reference-fixture
-tests' multi-step bound, test_gpu_model.py)."""
+whose sign two fp32 paths disagree on moves a weight by up to 2 lr), and the training update of every
+tensor (final - initial weights) at cosine > 0.95 to the oracle's, > 0.99 over the whole model."""
 import os
 import subprocess
 
@@ -92,11 +92,24 @@ def test_config0_build_train_vs_oracle_trajectory(cad, dev, oracle, tmp_path):
     assert abs(float(m["val_loss"]) - np.mean(v_loss)) <= 1e-3 * np.mean(v_loss), (m["val_loss"], np.mean(v_loss))
     assert abs(float(m["abs_rel"]) - np.mean(v_abs)) <= 1e-3 * np.mean(v_abs), (m["abs_rel"], np.mean(v_abs))
 
-    # final weights after 5 Adam steps
+    # final weights after 5 Adam steps: every weight within 2 lr per step of the oracle's, and the
+    # training update (final - initial) pointing the oracle's way, per tensor and as a whole
     got = _read_all(cad, tmp_path / "ckpt" / "baseline_unet" / "final_model.pt")
     k = N_TRAIN // BS
+    rows, du, dr = [], [], []
     for n, v in ref.p.items():
         d = np.abs(got[n] - v.numpy())
-        assert d.max() <= 2 * LR * k + 1e-6 and d.mean() < 2e-5, (n, d.max(), d.mean())
+        u = (got[n] - params[n].numpy()).ravel().astype(np.float64)
+        w = (v.numpy() - params[n].numpy()).ravel().astype(np.float64)
+        cos = float(u @ w / (np.linalg.norm(u) * np.linalg.norm(w) + 1e-30))
+        rows.append((cos, float(d.max()), float(d.mean()), n))
+        du.append(u)
+        dr.append(w)
+    du, dr = np.concatenate(du), np.concatenate(dr)
+    cos_all = float(du @ dr / (np.linalg.norm(du) * np.linalg.norm(dr)))
+    rows.sort()
+    print(f"\nupdate cosine (whole model) {cos_all:.6f}; worst tensors (cos, max |dw|, mean |dw|, name): {rows[:4]}")
+    assert all(r[1] <= 2 * LR * k + 1e-6 for r in rows), rows
+    assert cos_all > 0.99 and rows[0][0] > 0.95, (cos_all, rows[:4])
     for n, v in ref.bufs.items():
         assert np.abs(got[n] - v.numpy()).max() <= 1e-4 * max(1.0, np.abs(v.numpy()).max()), n
