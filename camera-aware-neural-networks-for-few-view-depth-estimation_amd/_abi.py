@@ -170,6 +170,7 @@ SIGNATURES = {
     "cad_archive_read": (I, [P, I, P, I64]),
     "cad_dataset_open": (I, [C.c_char_p, C.POINTER(C.c_char_p), I, C.POINTER(P)]),
     "cad_dataset_synthetic": (I, [I64, I, I, C.c_uint32, C.POINTER(P)]),
+    "cad_jpeg_decode": (I, [P, I64, P, I64, C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
     "cad_dataset_destroy": (None, [P]),
     "cad_dataset_size": (I64, [P]),
     "cad_dataset_image_dir": (C.c_char_p, [P, I64]),

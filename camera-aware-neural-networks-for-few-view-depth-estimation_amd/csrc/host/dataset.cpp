@@ -15,8 +15,8 @@
 //                                           8-bit -> value as metres (convertTo CV_32F, scale 1)
 //               loadIntrinsics :261-275     9 whitespace-separated floats, row-major
 // PNG is decoded here (zlib inflate + the five scanline filters, non-interlaced, 8/16-bit gray /
-// gray+alpha / RGB / RGBA and 8-bit palette); JPEG needs libjpeg headers this image lacks, so .jpg
-// files fail with a message naming the file (convert them to PNG or PPM).
+// gray+alpha / RGB / RGBA and 8-bit palette); JPEG by jpeg.cpp, which restates libjpeg-turbo's default
+// decompression (sequential Huffman, ISLOW IDCT, fancy upsampling, jdcolor.c tables) bit for bit.
 //
 // The manifest is JSON (the reference uses nlohmann::json, absent here): a small RFC 8259 parser.
 #include <hip/hip_runtime.h>
@@ -39,6 +39,7 @@
 #include <vector>
 
 #include "../../../include/cad/cad.h"
+#include "jpeg.hpp"
 
 namespace cad {
 void set_last_error(const std::string& msg);
@@ -371,12 +372,25 @@ std::string lower_ext(const fs::path& p) {
     return e;
 }
 
+Image decode_jpeg(const std::string& bytes, const std::string& path) {
+    cad::jpeg::Decoded d;
+    try {
+        d = cad::jpeg::decode(reinterpret_cast<const uint8_t*>(bytes.data()), bytes.size());
+    } catch (const std::exception& e) {
+        throw DataError(std::string(e.what()) + ": " + path);
+    }
+    Image im;
+    im.h = d.h;
+    im.w = d.w;
+    im.c = d.c;
+    im.px.assign(d.px.begin(), d.px.end());
+    return im;
+}
+
 Image decode_image(const std::string& path) {
     const std::string ext = lower_ext(path);
-    if (ext == ".jpg" || ext == ".jpeg")
-        throw DataError("JPEG decoding is not available in this build (no libjpeg headers in the image); convert " +
-                        path + " to PNG or PPM");
     const std::string bytes = slurp(path, "image");
+    if (ext == ".jpg" || ext == ".jpeg") return decode_jpeg(bytes, path);
     if (ext == ".png") return decode_png(bytes, path);
     if (ext == ".ppm" || ext == ".pgm" || ext == ".pnm") return decode_pnm(bytes, path);
     throw DataError("unsupported image format: " + path);
@@ -641,6 +655,21 @@ cad_status cad_dataset_open(const char* manifest_path, const char* const* sensor
         }
         ds->n = (int64_t)ds->items.size();
         *out = ds.release();
+    });
+}
+
+cad_status cad_jpeg_decode(const uint8_t* data, int64_t size, uint8_t* out, int64_t cap, int* height, int* width,
+                           int* channels) {
+    return data_guard([&] {
+        if (!data || size < 0) throw DataError("bad arguments");
+        const cad::jpeg::Decoded d = cad::jpeg::decode(data, (size_t)size);
+        if (height) *height = d.h;
+        if (width) *width = d.w;
+        if (channels) *channels = d.c;
+        if (out) {
+            if (cap < (int64_t)d.px.size()) throw DataError("output buffer too small");
+            std::memcpy(out, d.px.data(), d.px.size());
+        }
     });
 }
 

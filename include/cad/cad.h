@@ -339,8 +339,15 @@ cad_status cad_aug_sampler_draw(cad_aug_sampler* s, int height, int width, cad_s
  * default) and an existing <path>/intrinsics.txt, in manifest order (paths relative to the working
  * directory, as in the reference).  A sample decodes <path>/image/<first .jpg|.png|.ppm> as RGB u8
  * and <path>/depth/<first .png|.pgm> as u16 (16-bit: metres = value / 1000; 8-bit: value), PNG and
- * binary PNM only (JPEG needs a decoder this build lacks and fails with a message). */
+ * binary PNM, and baseline / extended-sequential Huffman JPEG (csrc/host/jpeg.cpp: libjpeg-turbo's
+ * default decompression — ISLOW IDCT, fancy upsampling, jdcolor.c YCbCr->RGB — restated bit for bit;
+ * progressive / arithmetic / 12-bit / CMYK JPEGs fail with a message). */
 typedef struct cad_dataset cad_dataset;
+/* decode a JPEG file held in memory (what cv::imread(IMREAD_COLOR) decodes for the loader,
+ * sunrgbd_loader.cpp:86,222, before its BGR order): height x width x channels u8 samples (channels 1
+ * gray or 3 RGB) into out (out == NULL: dimensions only) */
+cad_status cad_jpeg_decode(const uint8_t* data, int64_t size, uint8_t* out, int64_t cap, int* height, int* width,
+                           int* channels);
 typedef struct {
     int h0, w0;        /* rgb size */
     int dh0, dw0;      /* depth size */

@@ -1,0 +1,60 @@
+"""Writes the JPEG decoder fixtures of tests/test_jpeg.py (run in the build container, where PIL is
+importable; the files are committed): <name>.jpg encoded by PIL and <name>.npy = PIL's decode of it
+(libjpeg-turbo, the library behind the reference's cv::imread(IMREAD_COLOR), sunrgbd_loader.cpp:86,222,
+with its default settings: ISLOW IDCT, fancy upsampling).  RGB (H, W, 3) or gray (H, W) uint8.
+
+  python tests/golden/jpeg/make_fixtures.py"""
+import io
+import json
+import os
+
+import numpy as np
+from PIL import Image, features
+
+OUT = os.path.dirname(os.path.abspath(__file__))
+CASES = {
+    # name: (H, W, gray, save kwargs)
+    "yuv420_odd_37x53_q90": (37, 53, False, dict(quality=90, subsampling=2)),
+    "yuv422_48x64_q75": (48, 64, False, dict(quality=75, subsampling=1)),
+    "yuv444_16x24_q95": (16, 24, False, dict(quality=95, subsampling=0)),
+    "gray_33x17_q85": (33, 17, True, dict(quality=85)),
+    "yuv420_120x160_q100": (120, 160, False, dict(quality=100, subsampling=2)),
+    "yuv420_121x161_q50_optimized": (121, 161, False, dict(quality=50, subsampling=2, optimize=True)),
+    "yuv420_2x2_q90": (2, 2, False, dict(quality=90, subsampling=2)),
+    "yuv422_5x3_q90": (5, 3, False, dict(quality=90, subsampling=1)),
+    "yuv420_64x64_restart3": (64, 64, False, dict(quality=90, subsampling=2, restart_marker_blocks=3)),
+    "yuv420_96x128_restart_rows": (96, 128, False, dict(quality=80, subsampling=2, restart_marker_rows=1)),
+}
+
+
+def image(h, w, gray, seed):
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:h, 0:w]
+    base = np.stack([128 + 100 * np.sin(x / 7.0 + c) * np.cos(y / 5.0 - c) for c in range(3)], -1)
+    a = np.clip(base + rng.normal(0, 25, base.shape), 0, 255).astype(np.uint8)
+    return Image.fromarray(a[..., 0] if gray else a)
+
+
+def main():
+    meta = {"libjpeg": features.version("jpg"), "libjpeg_turbo": bool(features.check_feature("libjpeg_turbo")),
+            "cases": {}}
+    for k, (name, (h, w, gray, kw)) in enumerate(sorted(CASES.items())):
+        bio = io.BytesIO()
+        image(h, w, gray, k).save(bio, "JPEG", **kw)
+        data = bio.getvalue()
+        with open(os.path.join(OUT, name + ".jpg"), "wb") as fh:
+            fh.write(data)
+        dec = np.asarray(Image.open(io.BytesIO(data)).convert("L" if gray else "RGB"))
+        np.save(os.path.join(OUT, name + ".npy"), dec)
+        meta["cases"][name] = {"shape": list(dec.shape), "bytes": len(data)}
+    # a progressive file: the decoder refuses it with a message
+    bio = io.BytesIO()
+    image(16, 16, False, 99).save(bio, "JPEG", quality=90, progressive=True)
+    with open(os.path.join(OUT, "progressive_16x16.jpg"), "wb") as fh:
+        fh.write(bio.getvalue())
+    with open(os.path.join(OUT, "fixtures.json"), "w") as fh:
+        json.dump(meta, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()

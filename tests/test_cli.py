@@ -266,8 +266,9 @@ def test_cli_distributed_single_rank_matches_plain(train_bin, tmp_path):
     assert rows[True] == rows[False]
 
 
-def _manifest_tree(tmp_path, n=6):
-    """n PNG samples under tmp_path (paths in the manifest relative to it, the run's cwd)."""
+def _manifest_tree(tmp_path, n=6, rgb_ext=".png"):
+    """n samples (RGB frames PNG or JPEG, depth PNG) under tmp_path (paths in the manifest relative to
+    it, the run's cwd)."""
     import numpy as np
     from PIL import Image
     rng = np.random.default_rng(0)
@@ -277,7 +278,7 @@ def _manifest_tree(tmp_path, n=6):
         d = tmp_path / rel
         (d / "image").mkdir(parents=True)
         (d / "depth").mkdir(parents=True)
-        Image.fromarray(rng.integers(0, 256, (60, 80, 3), dtype=np.uint8)).save(d / "image" / "rgb.png")
+        Image.fromarray(rng.integers(0, 256, (60, 80, 3), dtype=np.uint8)).save(d / "image" / ("rgb" + rgb_ext))
         Image.fromarray(rng.integers(500, 9000, (60, 80), dtype=np.uint16)).save(d / "depth" / "depth.png")
         (d / "intrinsics.txt").write_text("518.8 0 325.5\n0 519.4 253.7\n0 0 1\n")
         images.append({"path": rel, "sensor_type": "kv1", "valid": True})
@@ -306,10 +307,11 @@ def test_cli_manifest_dataset_plan(train_bin, tmp_path):
 
 
 @pytest.mark.gpu
-def test_cli_trains_from_manifest(train_bin, tmp_path):
-    """build/train on PNG samples from a SUN RGB-D manifest through the prefetch ring (decode threads,
-    pinned upload, device resize + augmentation)."""
-    _manifest_tree(tmp_path, 6)
+@pytest.mark.parametrize("rgb_ext", [".png", ".jpg"])
+def test_cli_trains_from_manifest(train_bin, tmp_path, rgb_ext):
+    """build/train on SUN RGB-D manifest samples (PNG, or JPEG RGB frames as SUN RGB-D ships them)
+    through the prefetch ring (decode threads, pinned upload, device resize + augmentation)."""
+    _manifest_tree(tmp_path, 6, rgb_ext)
     cfg = yaml.safe_load(open(os.path.join(ROOT, "configs", "train_config.yaml")))
     cfg["data"].update(dataset_name="sunrgbd", manifest_path="./manifest.json", input_height=48, input_width=64)
     cfg["model"]["init_features"] = 16

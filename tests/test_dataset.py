@@ -159,11 +159,12 @@ def test_png_palette_and_8bit_depth_and_pil_files(cad, tmp_path):
 
 
 def test_loader_errors(cad, tmp_path):
-    # JPEG needs a decoder this build does not have: a clear message naming the file
+    # a JPEG process the decoder does not implement (progressive): a clear message naming the file
     rng = np.random.default_rng(1)
-    m = _one_sample(tmp_path, lambda d: PIL.fromarray(rng.integers(0, 256, (8, 8, 3), dtype=np.uint8)).save(d / "x.jpg"),
+    m = _one_sample(tmp_path, lambda d: PIL.fromarray(rng.integers(0, 256, (8, 8, 3), dtype=np.uint8)).save(
+                        d / "x.jpg", progressive=True),
                     lambda d: PIL.fromarray(np.zeros((8, 8), np.uint16)).save(d / "d.png"))
-    with pytest.raises(cad.CadError, match="JPEG decoding is not available.*x.jpg"):
+    with pytest.raises(cad.CadError, match="progressive JPEG is not supported.*x.jpg"):
         cad.SunRGBDDataset(m).read(0)
     with pytest.raises(cad.CadError, match="Cannot open manifest"):
         cad.SunRGBDDataset(tmp_path / "nope.json")
