@@ -73,6 +73,11 @@ SIGNATURES = {
     "cad_resunet_flat": (I, [P, C.POINTER(P), C.POINTER(P), I64P]),
     "cad_resunet_forward": (I, [P, P, P, I, P]),
     "cad_resunet_backward": (I, [P, P, P]),
+    "cad_resunet_num_stages": (I, [P]),
+    "cad_resunet_grad_layout": (I, [C.POINTER(I), I64P, I64P, I64P]),
+    "cad_resunet_stage_grad_range": (I, [P, I, I64P, I64P]),
+    "cad_resunet_backward_stage": (I, [P, I, P, P]),
+    "cad_resunet_backward_allreduce": (I, [P, P, P, I64, P]),
     "cad_resunet_clip_grad_norm": (I, [P, F, F, P]),
     "cad_resunet_last_grad_norm": (I, [P, FP, P]),
     "cad_resunet_adam_step": (I, [P, F, F, F, F, F, P]),
@@ -88,6 +93,11 @@ SIGNATURES = {
     "cad_geonet_flat": (I, [P, C.POINTER(P), C.POINTER(P), I64P]),
     "cad_geonet_forward": (I, [P, P, P, P, P, I, P]),
     "cad_geonet_backward": (I, [P, P, P]),
+    "cad_geonet_num_stages": (I, [P]),
+    "cad_geonet_grad_layout": (I, [C.POINTER(GeoNetDesc), C.POINTER(I), I64P, I64P, I64P]),
+    "cad_geonet_stage_grad_range": (I, [P, I, I64P, I64P]),
+    "cad_geonet_backward_stage": (I, [P, I, P, P]),
+    "cad_geonet_backward_allreduce": (I, [P, P, P, I64, P]),
     "cad_geonet_clip_grad_norm": (I, [P, F, F, P]),
     "cad_geonet_last_grad_norm": (I, [P, FP, P]),
     "cad_geonet_adam_step": (I, [P, F, F, F, F, F, P]),

@@ -66,6 +66,46 @@ inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 }  // namespace
 
+namespace {
+// The overlapped exchange for any model with a staged backward (stage s writes only the gradients in
+// its slab range; ranges decrease with s): every stage is enqueued on `stream`; when the stages of a
+// bucket are enqueued, an event on `stream` gates the bucket's SUM all-reduce on the communicator's
+// stream, so RCCL runs while the later stages do; `stream` finally waits for every all-reduce.
+template <class Range, class Stage>
+void staged_backward_allreduce(cad_comm* c, float* g, int ns, Range range, Stage stage, int64_t bucket_elems,
+                               void* stream) {
+    DP_HIP(hipSetDevice(c->device));
+    std::vector<int64_t> off((size_t)ns), cnt((size_t)ns), boff((size_t)ns), bcnt((size_t)ns);
+    std::vector<int> blast((size_t)ns);
+    for (int s = 0; s < ns; ++s)
+        if (range(s, &off[(size_t)s], &cnt[(size_t)s]) != CAD_OK) throw DpError(CAD_ERR_INVALID, "stage range");
+    const int nb = cad_plan_grad_buckets(off.data(), cnt.data(), ns, std::max<int64_t>(bucket_elems, 1), boff.data(),
+                                         bcnt.data(), blast.data());
+    if (nb <= 0) throw DpError(CAD_ERR_INVALID, "no gradient buckets");
+    while ((int)c->ready.size() < nb) {
+        hipEvent_t e;
+        DP_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->ready.push_back(e);
+    }
+    int b = 0;
+    for (int s = 0; s < ns; ++s) {
+        const cad_status st = stage(s);
+        if (st != CAD_OK) throw DpError(st, std::string("backward stage: ") + cad_last_error());
+        if (b < nb && blast[(size_t)b] == s) {
+            // the bucket's gradients are final once the work enqueued so far on `stream` is done
+            DP_HIP(hipEventRecord(c->ready[(size_t)b], S(stream)));
+            DP_HIP(hipStreamWaitEvent(c->stream, c->ready[(size_t)b], 0));
+            DP_NCCL(ncclAllReduce(g + boff[(size_t)b], g + boff[(size_t)b], (size_t)bcnt[(size_t)b], ncclFloat32,
+                                  ncclSum, c->comm, c->stream));
+            ++b;
+        }
+    }
+    DP_HIP(hipEventRecord(c->done, c->stream));
+    DP_HIP(hipStreamWaitEvent(S(stream), c->done, 0));   // clip / Adam see the reduced slab
+}
+
+}  // namespace
+
 extern "C" {
 
 int cad_plan_grad_buckets(const int64_t* stage_off, const int64_t* stage_cnt, int nstages, int64_t bucket_elems,
@@ -164,41 +204,42 @@ cad_status cad_comm_broadcast_params(cad_unet* h, cad_comm* c, int root, void* s
     });
 }
 
+
 cad_status cad_unet_backward_allreduce(cad_unet* h, cad_comm* c, const float* ddepth, int64_t bucket_elems,
                                        void* stream) {
     return dp_guard([&] {
         if (!h || !c || !ddepth) throw DpError(CAD_ERR_INVALID, "null argument");
-        DP_HIP(hipSetDevice(c->device));
-        const int ns = cad_unet_num_stages(h);
-        std::vector<int64_t> off((size_t)ns), cnt((size_t)ns), boff((size_t)ns), bcnt((size_t)ns);
-        std::vector<int> blast((size_t)ns);
-        for (int s = 0; s < ns; ++s)
-            if (cad_unet_stage_grad_range(h, s, &off[(size_t)s], &cnt[(size_t)s]) != CAD_OK)
-                throw DpError(CAD_ERR_INVALID, "stage range");
-        const int nb = cad_plan_grad_buckets(off.data(), cnt.data(), ns, std::max<int64_t>(bucket_elems, 1), boff.data(),
-                                             bcnt.data(), blast.data());
         float* g = nullptr;
         if (cad_unet_flat(h, nullptr, &g, nullptr) != CAD_OK) throw DpError(CAD_ERR_INVALID, "cad_unet_flat failed");
-        while ((int)c->ready.size() < nb) {
-            hipEvent_t e;
-            DP_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            c->ready.push_back(e);
-        }
-        int b = 0;
-        for (int s = 0; s < ns; ++s) {
-            const cad_status st = cad_unet_backward_stage(h, s, ddepth, stream);
-            if (st != CAD_OK) throw DpError(st, std::string("backward stage: ") + cad_last_error());
-            if (b < nb && blast[(size_t)b] == s) {
-                // the bucket's gradients are final once the work enqueued so far on `stream` is done
-                DP_HIP(hipEventRecord(c->ready[(size_t)b], S(stream)));
-                DP_HIP(hipStreamWaitEvent(c->stream, c->ready[(size_t)b], 0));
-                DP_NCCL(ncclAllReduce(g + boff[(size_t)b], g + boff[(size_t)b], (size_t)bcnt[(size_t)b], ncclFloat32,
-                                      ncclSum, c->comm, c->stream));
-                ++b;
-            }
-        }
-        DP_HIP(hipEventRecord(c->done, c->stream));
-        DP_HIP(hipStreamWaitEvent(S(stream), c->done, 0));   // clip / Adam see the reduced slab
+        staged_backward_allreduce(
+            c, g, cad_unet_num_stages(h), [&](int s, int64_t* o, int64_t* n) { return cad_unet_stage_grad_range(h, s, o, n); },
+            [&](int s) { return cad_unet_backward_stage(h, s, ddepth, stream); }, bucket_elems, stream);
+    });
+}
+
+cad_status cad_resunet_backward_allreduce(cad_resunet* h, cad_comm* c, const float* ddepth, int64_t bucket_elems,
+                                          void* stream) {
+    return dp_guard([&] {
+        if (!h || !c || !ddepth) throw DpError(CAD_ERR_INVALID, "null argument");
+        float* g = nullptr;
+        if (cad_resunet_flat(h, nullptr, &g, nullptr) != CAD_OK) throw DpError(CAD_ERR_INVALID, "cad_resunet_flat failed");
+        staged_backward_allreduce(
+            c, g, cad_resunet_num_stages(h),
+            [&](int s, int64_t* o, int64_t* n) { return cad_resunet_stage_grad_range(h, s, o, n); },
+            [&](int s) { return cad_resunet_backward_stage(h, s, ddepth, stream); }, bucket_elems, stream);
+    });
+}
+
+cad_status cad_geonet_backward_allreduce(cad_geonet* h, cad_comm* c, const float* ddepth, int64_t bucket_elems,
+                                         void* stream) {
+    return dp_guard([&] {
+        if (!h || !c || !ddepth) throw DpError(CAD_ERR_INVALID, "null argument");
+        float* g = nullptr;
+        if (cad_geonet_flat(h, nullptr, &g, nullptr) != CAD_OK) throw DpError(CAD_ERR_INVALID, "cad_geonet_flat failed");
+        staged_backward_allreduce(
+            c, g, cad_geonet_num_stages(h),
+            [&](int s, int64_t* o, int64_t* n) { return cad_geonet_stage_grad_range(h, s, o, n); },
+            [&](int s) { return cad_geonet_backward_stage(h, s, ddepth, stream); }, bucket_elems, stream);
     });
 }
 

@@ -171,6 +171,7 @@ struct cad_geonet {
     int64_t Ml(int l, int B) const { return (int64_t)B * Hl(l) * Wl(l); }
     float* P(int i) const { return flat_p + params[i].off; }
     float* G(int i) const { return flat_g + params[i].off; }
+    std::vector<std::pair<int64_t, int64_t>> stage_range;   // staged backward: each stage's slab range
 };
 
 namespace {
@@ -512,17 +513,27 @@ void block_bwd(cad_geonet* h, GBlock& b, const float* g, int64_t ldg, int gcoff,
     if (din) cad::conv3x3_dgrad(dY, C, b.c1.wd, b.c1.cin, din, lddin, B, Hh, Ww, st);
 }
 
-void backward(cad_geonet* h, const float* dpred, hipStream_t st) {
+// Backward in stages whose parameter gradients are contiguous, decreasing-offset slab ranges
+// (registration order enc1, enc2.., bottleneck, dec<nl-1>..dec1, out_conv): 0 head, 1..nl-1 the
+// decoders dec1..dec<nl-1>, then the encoders bottleneck..enc2, last enc1 — the data-parallel
+// exchange (dp.cpp) all-reduces a finished range while the later stages run.
+int num_stages(const cad_geonet* h) { return 1 + (h->nl - 1) + (h->nl - 1) + 1; }
+
+void backward_stage(cad_geonet* h, int stage, const float* dpred, hipStream_t st) {
     const int B = h->fwd_B, nl = h->nl;
-    auto rp = [&](GConv& c) { cad::repack_conv_dgrad(h->P(c.pidx), c.wd, c.cout, c.cin, st); };
-    for (int l = 0; l < nl; ++l) {
-        if (l > 0) rp(h->enc[l].c1);
-        rp(h->enc[l].c2);
+    if (stage == 0) {
+        auto rp = [&](GConv& c) { cad::repack_conv_dgrad(h->P(c.pidx), c.wd, c.cout, c.cin, st); };
+        for (int l = 0; l < nl; ++l) {
+            if (l > 0) rp(h->enc[l].c1);
+            rp(h->enc[l].c2);
+        }
+        for (int l = 0; l <= nl - 2; ++l) { rp(h->dec[l].blk.c1); rp(h->dec[l].blk.c2); }
+        cad::head_bwd(h->dec[0].x, h->f, h->P(h->head_w), dpred, h->sig, h->max_depth, h->Sx, h->Ml(0, B), h->dscr,
+                      h->G(h->head_w), h->G(h->head_b), st);
+        return;
     }
-    for (int l = 0; l <= nl - 2; ++l) { rp(h->dec[l].blk.c1); rp(h->dec[l].blk.c2); }
-    cad::head_bwd(h->dec[0].x, h->f, h->P(h->head_w), dpred, h->sig, h->max_depth, h->Sx, h->Ml(0, B), h->dscr,
-                  h->G(h->head_w), h->G(h->head_b), st);
-    for (int l = 0; l <= nl - 2; ++l) {   // Sx = grad of dec[l].x
+    if (stage <= nl - 1) {   // decoder level l = stage - 1; Sx = grad of dec[l].x
+        const int l = stage - 1;
         GDec& d = h->dec[l];
         const int C = d.cout;
         const int64_t M = h->Ml(l, B);
@@ -540,15 +551,52 @@ void backward(cad_geonet* h, const float* dpred, hipStream_t st) {
         cad::colsum(gu, ldgu, gcu, M, C, h->dscr, st);
         cad::colsum_finalize(h->dscr, cad::colsum_slices(M), C, h->G(d.up_b), 1.f, st);
         cad::convT_dgrad(gu, ldgu, gcu, C, h->P(d.up_w), d.cin, h->Sx, B, h->Hl(l + 1), h->Wl(l + 1), st);
+        return;
     }
-    for (int l = nl - 1; l >= 1; --l) {   // encoders; Sx = grad of the bottleneck output
+    const int l = nl - 1 - (stage - nl);   // encoders: bottleneck (nl - 1) .. enc2 (1), then enc1 (0)
+    if (l >= 1) {
         GBlock& e = h->enc[l];
         const int C = h->Cl(l), Cp = h->Cl(l - 1);
         const float* g = l == nl - 1 ? h->Sx : h->dcat[l];
         block_bwd(h, e, g, l == nl - 1 ? C : 2 * C, 0, h->pool[l], Cp, B, h->Sc, Cp, st);
         cad::maxpool_bwd(h->Sc, h->pidx[l], Cp, B, h->Hl(l - 1), h->Wl(l - 1), h->dcat[l - 1], 2 * Cp, st);
+        return;
     }
     block_bwd(h, h->enc[0], h->dcat[0], 2 * h->Cl(0), 0, h->x0, 8, B, nullptr, 0, st);
+}
+
+void backward(cad_geonet* h, const float* dpred, hipStream_t st) {
+    for (int s = 0; s < num_stages(h); ++s) backward_stage(h, s, dpred, st);
+}
+
+void compute_stage_ranges(cad_geonet* h) {
+    const int nl = h->nl;
+    std::vector<std::string> pre = {"out_conv."};
+    for (int l = 0; l <= nl - 2; ++l) pre.push_back("dec" + std::to_string(l + 1) + ".");
+    for (int l = nl - 1; l >= 0; --l)
+        pre.push_back(l == 0 ? std::string("enc1.") : l == nl - 1 ? std::string("bottleneck.")
+                                                                    : "enc" + std::to_string(l + 1) + ".");
+    h->stage_range.clear();
+    std::vector<int> owner(h->params.size(), -1);
+    for (size_t s = 0; s < pre.size(); ++s) {
+        int64_t lo = INT64_MAX, hi = -1;
+        for (size_t i = 0; i < h->params.size(); ++i)
+            if (h->params[i].name.compare(0, pre[s].size(), pre[s]) == 0) {
+                if (owner[i] >= 0) throw std::logic_error("parameter in two backward stages: " + h->params[i].name);
+                owner[i] = (int)s;
+                lo = std::min(lo, h->params[i].off);
+                hi = std::max(hi, h->params[i].off + h->params[i].n_int);
+            }
+        if (hi < 0) throw std::logic_error("empty backward stage " + pre[s]);
+        h->stage_range.push_back({lo, hi - lo});
+    }
+    for (size_t i = 0; i < h->params.size(); ++i) {
+        if (owner[i] < 0) throw std::logic_error("parameter in no backward stage: " + h->params[i].name);
+        for (size_t s = 0; s < pre.size(); ++s)
+            if ((int)s != owner[i] && h->params[i].off < h->stage_range[s].first + h->stage_range[s].second &&
+                h->params[i].off + h->params[i].n_int > h->stage_range[s].first)
+                throw std::logic_error("backward stage ranges overlap at " + h->params[i].name);
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -661,6 +709,7 @@ cad_status cad_geonet_create(const cad_geonet_desc* d, int device, cad_geonet** 
         h->use_pcl = d->variant == CAD_GEONET_LIGHT ? true : d->use_pcl != 0;
         h->use_attention = d->variant == CAD_GEONET_LIGHT ? true : d->use_attention != 0;
         build(h.get());
+        compute_stage_ranges(h.get());
         Arena sz;
         layout(h.get(), sz);
         void* base = nullptr;
@@ -784,6 +833,50 @@ cad_status cad_geonet_backward(cad_geonet* h, const float* ddepth, void* stream)
         need(h->have_fwd, "backward needs a train-mode forward first", CAD_ERR_STATE);
         GCHK(hipSetDevice(h->device));
         backward(h, ddepth, S(stream));
+        GCHK(hipGetLastError());
+    });
+}
+
+int cad_geonet_num_stages(const cad_geonet* h) { return h ? num_stages(h) : -1; }
+
+cad_status cad_geonet_grad_layout(const cad_geonet_desc* d, int* nstages, int64_t stage_off[16], int64_t stage_cnt[16],
+                                  int64_t* n_flat) {
+    return gguard([&] {
+        need(d && (d->variant == CAD_GEONET_FULL || d->variant == CAD_GEONET_LIGHT), "unknown geonet variant");
+        need(d->in_channels == 3 && d->init_features >= 4 && d->init_features % 4 == 0, "bad model description");
+        cad_geonet t;   // tables only: no device memory is touched
+        t.variant = d->variant;
+        t.nl = d->variant == CAD_GEONET_FULL ? 6 : 5;
+        t.f = d->init_features;
+        t.H = t.W = 1 << t.nl;
+        t.use_pcl = d->variant == CAD_GEONET_LIGHT ? true : d->use_pcl != 0;
+        t.use_attention = d->variant == CAD_GEONET_LIGHT ? true : d->use_attention != 0;
+        build(&t);
+        compute_stage_ranges(&t);
+        need((int)t.stage_range.size() <= 16, "too many stages");
+        if (nstages) *nstages = (int)t.stage_range.size();
+        for (size_t s = 0; s < t.stage_range.size(); ++s) {
+            if (stage_off) stage_off[s] = t.stage_range[s].first;
+            if (stage_cnt) stage_cnt[s] = t.stage_range[s].second;
+        }
+        if (n_flat) *n_flat = t.n_flat;
+    });
+}
+
+cad_status cad_geonet_stage_grad_range(const cad_geonet* h, int stage, int64_t* offset, int64_t* count) {
+    return gguard([&] {
+        need(h && stage >= 0 && stage < (int)h->stage_range.size(), "stage out of range");
+        if (offset) *offset = h->stage_range[(size_t)stage].first;
+        if (count) *count = h->stage_range[(size_t)stage].second;
+    });
+}
+
+cad_status cad_geonet_backward_stage(cad_geonet* h, int stage, const float* ddepth, void* stream) {
+    return gguard([&] {
+        need(h->have_fwd, "backward needs a train-mode forward first", CAD_ERR_STATE);
+        need(stage >= 0 && stage < num_stages(h), "stage out of range");
+        GCHK(hipSetDevice(h->device));
+        backward_stage(h, stage, ddepth, S(stream));
         GCHK(hipGetLastError());
     });
 }

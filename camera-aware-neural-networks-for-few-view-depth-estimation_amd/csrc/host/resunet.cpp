@@ -130,6 +130,7 @@ struct Unit {   // conv + BN (+ its pre-BN output y)
     float* y = nullptr;
 };
 struct Bott {
+    std::string prefix;        // "encoder.layer<L>.<i>."
     Unit u1, u2, u3, ud;
     bool down = false;
     int s = 1, cin = 0, w = 0, cout = 0, H = 0, W = 0, Ho = 0, Wo = 0;   // input geometry
@@ -138,6 +139,7 @@ struct Bott {
     void* outs = nullptr;
 };
 struct Dec {
+    int l = 0;                 // "dec<l>." (output at 1/2^l)
     int up_w = -1, up_b = -1, cin_up = 0, cout_up = 0, skipC = 0, C = 0, H = 0, W = 0;   // output geometry
     Unit u1, u2;
     void* cats = nullptr;      // twin [M][skipC + cout_up]
@@ -186,6 +188,10 @@ struct cad_resunet {
     int64_t slab_cap = 0;
     float *gA = nullptr, *gB = nullptr, *gS = nullptr, *dT = nullptr, *dcol = nullptr;
     void* dYs = nullptr;
+    // staged backward (data-parallel exchange, dp.cpp): the gradient of the current stage's output,
+    // and each stage's contiguous slab range [off, off + cnt)
+    float* bwd_g = nullptr;
+    std::vector<std::pair<int64_t, int64_t>> stage_range;
     float* P(int i) const { return flat_p + params[i].off; }
     float* G(int i) const { return flat_g + params[i].off; }
     int64_t M(int B, int h, int w) const { return (int64_t)B * h * w; }
@@ -235,6 +241,7 @@ void build(cad_resunet* h) {
         for (int i = 0; i < nblocks[L]; ++i) {
             Bott b;
             const std::string pre = "encoder.layer" + std::to_string(L + 1) + "." + std::to_string(i) + ".";
+            b.prefix = pre;
             b.s = (L > 0 && i == 0) ? 2 : 1;
             b.cin = cin; b.w = widths[L]; b.cout = 4 * widths[L];
             b.down = i == 0;
@@ -255,6 +262,7 @@ void build(cad_resunet* h) {
     for (int j = 0; j < 5; ++j) {
         const int l = 4 - j;   // dec4 .. dec0, output at 1/2^l
         Dec d;
+        d.l = l;
         const std::string pre = "dec" + std::to_string(l) + ".";
         d.cin_up = cup; d.cout_up = outC[j]; d.skipC = skipC[j]; d.C = outC[j];
         d.H = h->H >> l; d.W = h->W >> l;
@@ -633,39 +641,48 @@ void unit_bwd(cad_resunet* h, Unit& u, const float* g, int64_t ldg, int gcoff, b
     }
 }
 
-void backward(cad_resunet* h, const float* ddepth, hipStream_t st) {
+// Backward in stages whose parameter gradients are contiguous, decreasing-offset slab ranges (the
+// registration order is stem, layer1..layer4, dec4..dec0, head): 0 head, 1..5 dec0..dec4, then the
+// bottleneck blocks from layer4's last to layer1's first, last the stem.  A stage writes only its own
+// range, so the data-parallel exchange can all-reduce a finished range while later stages run.
+int num_stages(const cad_resunet* h) { return 6 + (int)h->blocks.size() + 1; }
+
+void backward_stage(cad_resunet* h, int stage, const float* ddepth, hipStream_t st) {
     const int B = h->fwd_B;
-    prep_weights_bwd(h, st);
-    // head
-    Dec& d0 = h->dec.back();
-    float* g = h->gA;   // gradient of the current stage's output
-    cad::head_bwd(d0.out, 32, h->P(h->head_w), ddepth, h->sig, h->max_depth, g, h->M(B, h->H, h->W), h->dscr,
-                  h->G(h->head_w), h->G(h->head_b), st);
-    // decoder, dec0 .. dec4
-    const void* prevs[5];
-    prevs[0] = h->blocks.back().outs;
-    for (int j = 1; j < 5; ++j) prevs[j] = h->dec[j - 1].outs;
-    for (int j = 4; j >= 0; --j) {
+    const int nb = (int)h->blocks.size();
+    if (stage == 0) {   // head
+        prep_weights_bwd(h, st);
+        Dec& d0 = h->dec.back();
+        h->bwd_g = h->gA;
+        cad::head_bwd(d0.out, 32, h->P(h->head_w), ddepth, h->sig, h->max_depth, h->bwd_g, h->M(B, h->H, h->W),
+                      h->dscr, h->G(h->head_w), h->G(h->head_b), st);
+        return;
+    }
+    float* g = h->bwd_g;
+    if (stage <= 5) {   // decoder: h->dec[4] (dec0) first
+        const int j = 5 - stage;
         Dec& d = h->dec[j];
+        const void* prev = j == 0 ? h->blocks.back().outs : h->dec[j - 1].outs;
         const int cc = d.skipC + d.cout_up;
         const int64_t Md = h->M(B, d.H, d.W);
         unit_bwd(h, d.u2, g, d.C, 0, true, tw(d.a1s, d.C), B, d.H, d.W, nullptr, nullptr, h->dT, d.C, st);
         unit_bwd(h, d.u1, h->dT, d.C, 0, true, tw(d.cats, cc), B, d.H, d.W, nullptr, nullptr, d.dcat, cc, st);
         // ConvTranspose backward on the up half of dcat
         cad::split_rows(d.dcat, cc, d.skipC, d.cout_up, Md, h->dYs, d.cout_up, 0, st);
-        cad::convT_wgrad_ps(tw(prevs[j], d.cin_up), d.cin_up, tw(h->dYs, d.cout_up), d.cout_up, h->G(d.up_w), B, d.H / 2,
+        cad::convT_wgrad_ps(tw(prev, d.cin_up), d.cin_up, tw(h->dYs, d.cout_up), d.cout_up, h->G(d.up_w), B, d.H / 2,
                             d.W / 2, h->slab, h->slab_cap, st);
         cad::colsum(d.dcat, cc, d.skipC, Md, d.cout_up, h->dscr, st);
         cad::colsum_finalize(h->dscr, cad::colsum_slices(Md), d.cout_up, h->G(d.up_b), 1.f, st);
         float* gn = g == h->gA ? h->gB : h->gA;
-        cad::convT_dgrad_ps(tw(h->dYs, d.cout_up), d.cout_up, tw(d.wms, 4 * d.cout_up), d.cin_up, gn, B, d.H / 2, d.W / 2,
-                            st);
-        g = gn;
+        cad::convT_dgrad_ps(tw(h->dYs, d.cout_up), d.cout_up, tw(d.wms, 4 * d.cout_up), d.cin_up, gn, B, d.H / 2,
+                            d.W / 2, st);
+        h->bwd_g = gn;
+        return;
     }
-    // encoder: g = gradient of layer4's output
-    const int stage_last[4] = {h->stage_end[0] - 1, h->stage_end[1] - 1, h->stage_end[2] - 1, h->stage_end[3] - 1};
-    for (int bi = (int)h->blocks.size() - 1; bi >= 0; --bi) {
+    if (stage < 6 + nb) {   // encoder bottleneck block bi; g = gradient of its output
+        const int bi = nb - 1 - (stage - 6);
         Bott& b = h->blocks[bi];
+        const int stage_last[3] = {h->stage_end[0] - 1, h->stage_end[1] - 1, h->stage_end[2] - 1};
         // skip gradients of the decoder concat (x4 = layer3, x3 = layer2, x2 = layer1 outputs)
         for (int L = 0; L < 3; ++L)
             if (bi == stage_last[L]) {
@@ -685,7 +702,8 @@ void backward(cad_resunet* h, const float* ddepth, hipStream_t st) {
             unit_bwd(h, b.ud, h->gS, b.cout, 0, false, tw(xsw, b.cin), B, b.H, b.W, nullptr, b.xs, h->dT, b.cin, st);
             cad::add_strided(gn, b.cin, h->dT, b.cin, 0, b.cin, B, b.H, b.W, b.s, st);
         }
-        g = gn;
+        h->bwd_g = gn;
+        return;
     }
     // stem: max-pool backward, the dec1 skip gradient (x1), bn1 + relu, conv1 weight gradient
     const int H1 = (h->H - 1) / 2 + 1, W1 = (h->W - 1) / 2 + 1;
@@ -699,6 +717,42 @@ void backward(cad_resunet* h, const float* ddepth, hipStream_t st) {
                      h->G(sb.widx), h->G(sb.bidx), nullptr, st, nullptr, 1, h->dYs, true, true);
     cad::dense_wgrad_ps(tw(h->dYs, 64), 64, tw(h->stem_col, h->stem.c.Kp), h->stem.c.Kp, h->G(h->stem.c.pidx),
                         h->stem.c.Kp, M1, h->slab, h->slab_cap, st);
+}
+
+void backward(cad_resunet* h, const float* ddepth, hipStream_t st) {
+    for (int s = 0; s < num_stages(h); ++s) backward_stage(h, s, ddepth, st);
+}
+
+// the slab range of each stage, from the parameter names (checked contiguous: no other stage's
+// parameter inside it)
+void compute_stage_ranges(cad_resunet* h) {
+    std::vector<std::vector<std::string>> pre;
+    pre.push_back({"out_conv."});
+    for (int j = 4; j >= 0; --j) pre.push_back({"dec" + std::to_string(h->dec[j].l) + "."});
+    for (int bi = (int)h->blocks.size() - 1; bi >= 0; --bi) pre.push_back({h->blocks[bi].prefix});
+    pre.push_back({"encoder.conv1.", "encoder.bn1."});
+    h->stage_range.clear();
+    std::vector<int> owner(h->params.size(), -1);
+    for (size_t s = 0; s < pre.size(); ++s) {
+        int64_t lo = INT64_MAX, hi = -1;
+        for (size_t i = 0; i < h->params.size(); ++i)
+            for (const std::string& p : pre[s])
+                if (h->params[i].name.compare(0, p.size(), p) == 0) {
+                    if (owner[i] >= 0) throw std::logic_error("parameter in two backward stages: " + h->params[i].name);
+                    owner[i] = (int)s;
+                    lo = std::min(lo, h->params[i].off);
+                    hi = std::max(hi, h->params[i].off + h->params[i].n_int);
+                }
+        if (hi < 0) throw std::logic_error("empty backward stage");
+        h->stage_range.push_back({lo, hi - lo});
+    }
+    for (size_t i = 0; i < h->params.size(); ++i) {
+        if (owner[i] < 0) throw std::logic_error("parameter in no backward stage: " + h->params[i].name);
+        for (size_t s = 0; s < pre.size(); ++s)
+            if ((int)s != owner[i] && h->params[i].off < h->stage_range[s].first + h->stage_range[s].second &&
+                h->params[i].off + h->params[i].n_int > h->stage_range[s].first)
+                throw std::logic_error("backward stage ranges overlap at " + h->params[i].name);
+    }
 }
 
 }  // namespace
@@ -724,6 +778,7 @@ cad_status cad_resunet_create(const cad_resunet_desc* d, int device, cad_resunet
         h->max_depth = d->max_depth;
         EngineScope es;
         build(h.get());
+        compute_stage_ranges(h.get());
         Arena sz;
         layout(h.get(), sz);
         void* base = nullptr;
@@ -853,6 +908,43 @@ cad_status cad_resunet_backward(cad_resunet* h, const float* ddepth, void* strea
         RCHK(hipSetDevice(h->device));
         EngineScope es;
         backward(h, ddepth, S(stream));
+        RCHK(hipGetLastError());
+    });
+}
+
+int cad_resunet_num_stages(const cad_resunet* h) { return h ? num_stages(h) : -1; }
+
+cad_status cad_resunet_grad_layout(int* nstages, int64_t stage_off[32], int64_t stage_cnt[32], int64_t* n_flat) {
+    return rguard([&] {
+        cad_resunet t;   // tables only: no device memory is touched
+        t.H = t.W = 64;
+        build(&t);
+        compute_stage_ranges(&t);
+        need((int)t.stage_range.size() <= 32, "too many stages");
+        if (nstages) *nstages = (int)t.stage_range.size();
+        for (size_t s = 0; s < t.stage_range.size(); ++s) {
+            if (stage_off) stage_off[s] = t.stage_range[s].first;
+            if (stage_cnt) stage_cnt[s] = t.stage_range[s].second;
+        }
+        if (n_flat) *n_flat = t.n_flat;
+    });
+}
+
+cad_status cad_resunet_stage_grad_range(const cad_resunet* h, int stage, int64_t* offset, int64_t* count) {
+    return rguard([&] {
+        need(h && stage >= 0 && stage < (int)h->stage_range.size(), "stage out of range");
+        if (offset) *offset = h->stage_range[(size_t)stage].first;
+        if (count) *count = h->stage_range[(size_t)stage].second;
+    });
+}
+
+cad_status cad_resunet_backward_stage(cad_resunet* h, int stage, const float* ddepth, void* stream) {
+    return rguard([&] {
+        need(h->have_fwd, "backward needs a train-mode forward first", CAD_ERR_STATE);
+        need(stage >= 0 && stage < num_stages(h), "stage out of range");
+        RCHK(hipSetDevice(h->device));
+        EngineScope es;
+        backward_stage(h, stage, ddepth, S(stream));
         RCHK(hipGetLastError());
     });
 }

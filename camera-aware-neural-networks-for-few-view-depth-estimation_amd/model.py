@@ -453,12 +453,20 @@ class Communicator:
               "cad_comm_allreduce")
         return t
 
-    def broadcast_parameters(self, model: BaselineUNet, root=0):
-        check(self.lib.cad_comm_broadcast_params(model.h, self.h, root, _stream(self.device)), "broadcast_params")
+    def broadcast_parameters(self, model, root=0):
+        """Identical replicas: the flat parameter slab of `model` (any family) from rank `root`."""
+        if isinstance(model, BaselineUNet):
+            check(self.lib.cad_comm_broadcast_params(model.h, self.h, root, _stream(self.device)), "broadcast_params")
+        else:
+            check(self.lib.cad_comm_broadcast(self.h, model._flat_p, model.n_flat, root, _stream(self.device)),
+                  "cad_comm_broadcast")
 
-    def backward_allreduce(self, model: BaselineUNet, ddepth: torch.Tensor, bucket_elems=25 << 18):
-        check(self.lib.cad_unet_backward_allreduce(model.h, self.h, _ptr(ddepth), bucket_elems,
-                                                   _stream(self.device)), "cad_unet_backward_allreduce")
+    def backward_allreduce(self, model, ddepth: torch.Tensor, bucket_elems=25 << 18):
+        """The model's staged backward with the overlapped SUM exchange (cad_unet_backward_allreduce,
+        cad_resunet_backward_allreduce, cad_geonet_backward_allreduce)."""
+        fn = (self.lib.cad_unet_backward_allreduce if isinstance(model, BaselineUNet)
+              else getattr(self.lib, model._PREFIX + "backward_allreduce"))
+        check(fn(model.h, self.h, _ptr(ddepth), bucket_elems, _stream(self.device)), "backward_allreduce")
 
 
 class Trainer:
@@ -551,7 +559,14 @@ class ResNetUNet:
         p, g, n = C.c_void_p(), C.c_void_p(), C.c_int64()
         check(self._f("flat")(h, C.byref(p), C.byref(g), C.byref(n)), "flat")
         self.n_flat = n.value
+        self._flat_p = p.value
         self._flat_g = g.value
+        self.num_stages = self._f("num_stages")(h)
+        self.stage_ranges = []
+        for st in range(self.num_stages):
+            off, cnt = C.c_int64(), C.c_int64()
+            check(self._f("stage_grad_range")(h, st, C.byref(off), C.byref(cnt)), "stage range")
+            self.stage_ranges.append((off.value, cnt.value))
         self.training = True
 
     def _info(self, kind, idx):
@@ -631,8 +646,39 @@ class ResNetUNet:
 
     __call__ = forward
 
-    def backward(self, ddepth: torch.Tensor):
-        check(self._f("backward")(self.h, _ptr(ddepth), _stream(self.device)), "cad_resunet_backward")
+    @property
+    def flat_grads(self) -> torch.Tensor:
+        """A torch view of the flat gradient slab (the data-parallel all-reduce buffer)."""
+        return _flat_view(self._flat_g, self.n_flat, self.device)
+
+    @property
+    def flat_params(self) -> torch.Tensor:
+        return _flat_view(self._flat_p, self.n_flat, self.device)
+
+    def backward(self, ddepth: torch.Tensor, on_stage=None):
+        """Backward of the last train-mode forward; on_stage(stage, offset, count) after each stage is
+        enqueued (its gradients flat_grads[offset:offset+count] are then final on the stream)."""
+        st = _stream(self.device)
+        if on_stage is None:
+            check(self._f("backward")(self.h, _ptr(ddepth), st), self._PREFIX + "backward")
+            return
+        for s in range(self.num_stages):
+            check(self._f("backward_stage")(self.h, s, _ptr(ddepth), st), f"backward stage {s}")
+            on_stage(s, *self.stage_ranges[s])
+
+    def _exchange_backward(self, dpred, process_group, communicator, bucket_mb):
+        """backward + the data-parallel SUM exchange of the gradient slab; returns the world size."""
+        if communicator is not None:
+            communicator.backward_allreduce(self, dpred, int(bucket_mb * (1 << 20) / 4))
+            return communicator.size()
+        if process_group is not None:
+            import torch.distributed as dist
+            bk = GradBucketer(self.flat_grads, self.num_stages, int(bucket_mb * (1 << 20) / 4), process_group)
+            self.backward(dpred, on_stage=bk.on_stage)
+            bk.wait()
+            return dist.get_world_size(process_group)
+        self.backward(dpred)
+        return 1
 
     def clip_grad_norm_(self, max_norm: float, prescale: float = 1.0):
         check(self._f("clip_grad_norm")(self.h, float(max_norm), float(prescale), _stream(self.device)), "clip")
@@ -647,18 +693,13 @@ class ResNetUNet:
               "adam_step")
 
     def train_step(self, loss_fn: "CombinedDepthLoss", rgb, gt, K, lr=1e-4, weight_decay=1e-5, grad_clip=1.0,
-                   pred=None, dpred=None, loss5=None, process_group=None):
-        """One optimisation step (enhanced.h:287-304 sequence).  With process_group: the flat gradient
-        slab is SUM-all-reduced (RCCL) after the backward and clipped as the mean."""
+                   pred=None, dpred=None, loss5=None, process_group=None, communicator=None, bucket_mb=25.0):
+        """One optimisation step (enhanced.h:287-304 sequence).  Data-parallel (process_group over
+        torch.distributed, or a libcad Communicator): decoder-first gradient buckets SUM-all-reduced
+        while the rest of the backward runs, clipped as the mean."""
         pred = self.forward(rgb, out=pred)
         loss5, dpred = loss_fn.forward_with_intrinsics(pred, gt, rgb, K, loss5=loss5, dpred=dpred)
-        self.backward(dpred)
-        world = 1
-        if process_group is not None:
-            import torch.distributed as dist
-            world = dist.get_world_size(process_group)
-            g = _flat_view(self._flat_g, self.n_flat, self.device)
-            dist.all_reduce(g, group=process_group)
+        world = self._exchange_backward(dpred, process_group, communicator, bucket_mb)
         self.clip_grad_norm_(grad_clip if grad_clip else float("inf"), 1.0 / world)
         self.adam_step(lr=lr, weight_decay=weight_decay)
         return loss5, pred
@@ -716,20 +757,16 @@ class GeometryAwareNetwork(ResNetUNet):
         return torch.from_numpy(out)
 
     def train_step(self, loss_fn: "CombinedDepthLoss", rgb, gt, K, lr=1e-4, weight_decay=1e-5, grad_clip=1.0,
-                   rays=None, pred=None, dpred=None, loss5=None, process_group=None):
+                   rays=None, pred=None, dpred=None, loss5=None, process_group=None, communicator=None,
+                   bucket_mb=25.0):
         """One optimisation step (enhanced.h:287-304 sequence) fed the loader's batch: rays default to
-        RayDirectionComputer's from K (a18), intrinsics = [K00, K11, K02, K12] (a15)."""
+        RayDirectionComputer's from K (a18), intrinsics = [K00, K11, K02, K12] (a15).  Data-parallel
+        exchange as ResNetUNet.train_step."""
         if rays is None:
             rays = ray_directions(K, rgb.shape[2], rgb.shape[3])
         pred = self.forward(rgb, rays, camera_from_K(K), out=pred)
         loss5, dpred = loss_fn.forward_with_intrinsics(pred, gt, rgb, K, loss5=loss5, dpred=dpred)
-        self.backward(dpred)
-        world = 1
-        if process_group is not None:
-            import torch.distributed as dist
-            world = dist.get_world_size(process_group)
-            g = _flat_view(self._flat_g, self.n_flat, self.device)
-            dist.all_reduce(g, group=process_group)
+        world = self._exchange_backward(dpred, process_group, communicator, bucket_mb)
         self.clip_grad_norm_(grad_clip if grad_clip else float("inf"), 1.0 / world)
         self.adam_step(lr=lr, weight_decay=weight_decay)
         return loss5, pred

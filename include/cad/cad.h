@@ -435,6 +435,17 @@ cad_status cad_resunet_train(cad_resunet* h, int train);
 cad_status cad_resunet_flat(cad_resunet* h, float** params, float** grads, int64_t* n);
 cad_status cad_resunet_forward(cad_resunet* h, const float* rgb, float* depth, int B, void* stream);
 cad_status cad_resunet_backward(cad_resunet* h, const float* ddepth, void* stream);
+/* staged backward (decoder first; stage s writes only the gradients in its flat-slab range, ranges
+ * decreasing with s) and the overlapped data-parallel exchange over it (cad_unet_backward_allreduce's
+ * semantics: SUM buckets of >= bucket_elems floats on the communicator's stream) */
+int cad_resunet_num_stages(const cad_resunet* h);
+/* host only (no device): the stage count (23) and each stage's [offset, offset+count), as
+ * cad_resunet_stage_grad_range reports them, and the slab size */
+cad_status cad_resunet_grad_layout(int* nstages, int64_t stage_off[32], int64_t stage_cnt[32], int64_t* n_flat);
+cad_status cad_resunet_stage_grad_range(const cad_resunet* h, int stage, int64_t* offset, int64_t* count);
+cad_status cad_resunet_backward_stage(cad_resunet* h, int stage, const float* ddepth, void* stream);
+cad_status cad_resunet_backward_allreduce(cad_resunet* h, cad_comm* c, const float* ddepth, int64_t bucket_elems,
+                                          void* stream);
 cad_status cad_resunet_clip_grad_norm(cad_resunet* h, float max_norm, float prescale, void* stream);
 cad_status cad_resunet_last_grad_norm(cad_resunet* h, float* total_norm, void* stream);
 cad_status cad_resunet_adam_step(cad_resunet* h, float lr, float beta1, float beta2, float eps, float weight_decay,
@@ -479,6 +490,15 @@ cad_status cad_geonet_flat(cad_geonet* h, float** params, float** grads, int64_t
 cad_status cad_geonet_forward(cad_geonet* h, const float* rgb, const float* rays, const float* cam4, float* depth,
                               int B, void* stream);
 cad_status cad_geonet_backward(cad_geonet* h, const float* ddepth, void* stream);
+/* staged backward and the overlapped data-parallel exchange (as cad_resunet_*) */
+int cad_geonet_num_stages(const cad_geonet* h);
+/* host only (no device): the stage layout of the network `d` describes (as cad_resunet_grad_layout) */
+cad_status cad_geonet_grad_layout(const cad_geonet_desc* d, int* nstages, int64_t stage_off[16], int64_t stage_cnt[16],
+                                  int64_t* n_flat);
+cad_status cad_geonet_stage_grad_range(const cad_geonet* h, int stage, int64_t* offset, int64_t* count);
+cad_status cad_geonet_backward_stage(cad_geonet* h, int stage, const float* ddepth, void* stream);
+cad_status cad_geonet_backward_allreduce(cad_geonet* h, cad_comm* c, const float* ddepth, int64_t bucket_elems,
+                                         void* stream);
 cad_status cad_geonet_clip_grad_norm(cad_geonet* h, float max_norm, float prescale, void* stream);
 cad_status cad_geonet_last_grad_norm(cad_geonet* h, float* total_norm, void* stream);
 cad_status cad_geonet_adam_step(cad_geonet* h, float lr, float beta1, float beta2, float eps, float weight_decay,

@@ -319,13 +319,29 @@ class _RoundGradOperand(torch.autograd.Function):
         return g.to(torch.bfloat16).to(g.dtype)
 
 
-def _conv3x3(x, w):
+# Test hook for the bf16 arithmetic: {conv name ("enc1.conv1", "dec2.conv.conv2", ...): tensor (B,C,H,W)}.
+# A listed convolution computes its output as usual, records it in Y_OWN[name], and passes the given
+# value on instead (its gradient flows to its own output unchanged).  The full-size bf16 tests impose
+# the GPU run's stored (bf16) pre-BN outputs this way, layer by layer, so each convolution is judged
+# on identical inputs — otherwise a one-ulp fp32 difference next to a bf16 rounding boundary makes the
+# two runs' stored values differ by 2^-8 and the difference compounds over the 18 layers.
+Y_FORCE = {}
+Y_OWN = {}
+
+
+def _conv3x3(x, w, name=None):
     if _GEMM["operands"] == "bf16":
         y = _RoundGradOperand.apply(F.conv2d(_RoundOperand.apply(x), _RoundOperand.apply(w), None, 1, 1))
         # the bf16 engine stores the pre-BN outputs of its pre-split convolutions as bf16 (all but the
         # one on the raw 3-channel image, which runs the in-loader kernel with fp32 outputs)
-        return y if x.shape[1] == 3 else _RoundOperand.apply(y)
-    return F.conv2d(x, w, None, 1, 1)
+        y = y if x.shape[1] == 3 else _RoundOperand.apply(y)
+    else:
+        y = F.conv2d(x, w, None, 1, 1)
+    forced = Y_FORCE.get(name) if name else None
+    if forced is None:
+        return y
+    Y_OWN[name] = y.detach().clone()
+    return y + (forced.to(y.dtype) - y).detach()
 
 
 def _convT2x2(x, w, b):
@@ -372,11 +388,11 @@ def _film(x, c, p, bufs, pre, train):
 def _double_conv(x, p, bufs, pre, train, cam=None):
     # DoubleConvImpl::forward (baseline_unet.h:32-43); with `cam`: FiLMDoubleConvImpl::forward
     # (intrinsics_unet.h:38-52) = RayEnhancedConvImpl::forward after its cat (geometry_aware_network.h:47-64)
-    x = _conv3x3(x, p[pre + "conv1.weight"])
+    x = _conv3x3(x, p[pre + "conv1.weight"], pre + "conv1")
     x = _bn_relu(x, p, bufs, pre + "bn1", train)
     if cam is not None:
         x = _film(x, cam, p, bufs, pre + "film.", train)
-    x = _conv3x3(x, p[pre + "conv2.weight"])
+    x = _conv3x3(x, p[pre + "conv2.weight"], pre + "conv2")
     return _bn_relu(x, p, bufs, pre + "bn2", train)
 
 

@@ -101,3 +101,15 @@ def gpu_relu_decisions(net, params, f, B, H, W, model="baseline"):
             z = y * sc.double() + sh.double()
             masks[pre + "bn" + k] = (z > 0).reshape(B, h, w, C).permute(0, 3, 1, 2).contiguous()
     return masks
+
+
+def gpu_conv_outputs(net, f, B, H, W, model="baseline"):
+    """The stored pre-BN outputs of every 3x3 convolution of `net`'s last forward (bf16 values on the
+    bf16 engine), NCHW float, keyed like cad_oracle.Y_FORCE ("enc1.conv1", "dec2.conv.conv2", ...)."""
+    out = {}
+    for tag, pre, l in unet_bn_blocks(model):
+        C, h, w = f << l, H >> l, W >> l
+        for k in ("1", "2"):
+            y = net.debug_buffer(f"{tag}_y{k}")[: B * h * w * C].reshape(B, h, w, C)
+            out[pre + "conv" + k] = y.permute(0, 3, 1, 2).contiguous()
+    return out

@@ -79,3 +79,51 @@ def test_bucket_plan_rejects_bad_input(cad):
     sc = (C.c_int64 * 2)(5, -1)
     assert lib.cad_plan_grad_buckets(so, sc, 2, 4, None, None, None) == -1
     assert lib.cad_plan_grad_buckets(so, sc, 0, 4, None, None, None) == -1
+
+
+def _resunet_layout(lib):
+    ns, nf = C.c_int(), C.c_int64()
+    off, cnt = (C.c_int64 * 32)(), (C.c_int64 * 32)()
+    assert lib.cad_resunet_grad_layout(C.byref(ns), off, cnt, C.byref(nf)) == 0, lib.cad_last_error()
+    return [(off[i], cnt[i]) for i in range(ns.value)], nf.value
+
+
+def _geonet_layout(cad, lib, variant, f, pcl=1, att=1):
+    from cad_amd._abi import GeoNetDesc
+    d = GeoNetDesc(variant, 3, f, 4, 10.0, pcl, att, 1, 64, 64)
+    ns, nf = C.c_int(), C.c_int64()
+    off, cnt = (C.c_int64 * 16)(), (C.c_int64 * 16)()
+    assert lib.cad_geonet_grad_layout(C.byref(d), C.byref(ns), off, cnt, C.byref(nf)) == 0, lib.cad_last_error()
+    return [(off[i], cnt[i]) for i in range(ns.value)], nf.value
+
+
+@pytest.mark.parametrize("family", ["resunet", "geo_full", "geo_light", "geo_rays_only"])
+def test_other_families_stage_layout_and_plan(cad, family):
+    """configs[4]'s ResNet-50 + U-Net decoder and the geometry-aware networks exchange gradients the
+    same way (cad_resunet_backward_allreduce / cad_geonet_backward_allreduce, dp.cpp): their staged
+    backward writes strictly decreasing, disjoint slab ranges that cover every parameter, so every
+    bucket of the plan is final once its last stage is enqueued."""
+    lib = cad.load_library()
+    if family == "resunet":
+        stages, n_flat = _resunet_layout(lib)
+        assert len(stages) == 1 + 5 + 16 + 1   # head, dec0..dec4, 16 bottlenecks, stem
+        n_params = 40918977
+    else:
+        variant, f, pcl, att = {"geo_full": (0, 64, 1, 1), "geo_light": (1, 32, 1, 1),
+                                "geo_rays_only": (0, 16, 0, 0)}[family]
+        stages, n_flat = _geonet_layout(cad, lib, variant, f, pcl, att)
+        nl = 6 if variant == 0 else 5
+        assert len(stages) == 1 + (nl - 1) + (nl - 1) + 1
+        n_params = {"geo_full": 129070759}.get(family)
+    for (a, na), (b, nb) in zip(stages, stages[1:]):
+        assert 0 <= a - (b + nb) < 64
+    assert stages[-1][0] == 0 and stages[0][0] + stages[0][1] <= n_flat
+    if n_params:
+        assert sum(c for _, c in stages) >= n_params
+    for mb in (1, 25):
+        elems = int(mb * (1 << 20) / 4)
+        buckets = _plan(lib, stages, elems)
+        assert buckets[0][0] + buckets[0][1] == stages[0][0] + stages[0][1] and buckets[-1][0] == 0
+        for (a, na, la), (b, nb, lb) in zip(buckets, buckets[1:]):   # adjacent up to the 64-float alignment
+            assert 0 <= a - (b + nb) < 64 and lb > la
+        assert all(c >= elems for _, c, _ in buckets[:-1]) and buckets[-1][2] == len(stages) - 1

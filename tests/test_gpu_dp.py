@@ -208,3 +208,78 @@ def test_backward_stage_writes_stay_in_range(cad, dev, oracle, model, engine):
         assert not (m.flat_grads == 1234.5).all()
     finally:
         lib.cad_set_gemm_engine(prev)
+
+
+def _family(cad, oracle, family, B=2, H=64, W=64):
+    if family == "resunet":
+        from oracle import resunet_oracle as R
+        p, b = R.init(seed=3)
+        m = cad.ResNetUNet(batch=B, height=H, width=W)
+        m.load_state_dict({**p, **b})
+        step = lambda loss, rgb, gt, K, **kw: m.train_step(loss, rgb, gt, K, **kw)
+    else:
+        m = cad.GeometryAwareNetwork(3, 8, 4, 10.0, batch=B, height=H, width=W) if family == "geo" else \
+            cad.LightweightGeometryNetwork(3, 8, 4, 10.0, batch=B, height=H, width=W)
+        step = lambda loss, rgb, gt, K, **kw: m.train_step(loss, rgb, gt, K, **kw)
+    return m, step
+
+
+@pytest.mark.parametrize("family", ["resunet", "geo", "geolite"])
+def test_other_families_staged_backward(cad, dev, oracle, family):
+    """configs[4]'s network and the geometry-aware ones back-propagate in stages (cad_resunet_ /
+    cad_geonet_backward_stage) that write only their own slab ranges (the overlapped exchange's
+    invariant, as test_backward_stage_writes_stay_in_range) and together equal the one-call backward
+    bit for bit."""
+    B, H, W = 2, 64, 64
+    m, _ = _family(cad, oracle, family, B, H, W)
+    rgb, gt, K = [torch.from_numpy(a).to(dev) for a in oracle.synth_batch(B, H, W)]
+    loss = cad.CombinedDepthLoss(batch=B, height=H, width=W)
+    fwd = (lambda: m.forward(rgb)) if family == "resunet" else \
+        (lambda: m.forward(rgb, cad.ray_directions(K, H, W), cad.camera_from_K(K)))
+    pred = fwd()
+    _, dpred = loss.forward_with_intrinsics(pred, gt, rgb, K)
+    m.backward(dpred)
+    torch.cuda.synchronize()
+    plain = m.flat_grads.clone()
+    pred = fwd()
+    _, dpred = loss.forward_with_intrinsics(pred, gt, rgb, K)
+    torch.cuda.synchronize()
+    m.flat_grads.fill_(1234.5)
+    snaps = [m.flat_grads.clone()]
+
+    def on_stage(s, off, cnt):
+        torch.cuda.synchronize()
+        cur = m.flat_grads.clone()
+        changed = (cur != snaps[-1]).nonzero().flatten()
+        outside = changed[(changed < off) | (changed >= off + cnt)]
+        assert outside.numel() == 0, (family, s, off, cnt, outside[:8].tolist())
+        snaps.append(cur)
+    m.backward(dpred, on_stage=on_stage)
+    torch.cuda.synchronize()
+    assert len(snaps) == m.num_stages + 1
+    staged = m.flat_grads.clone()
+    touched = staged != 1234.5
+    assert torch.equal(staged[touched], plain[touched]), family
+    assert (plain[~touched] == 0).all()   # untouched = alignment padding, zero in the plain run
+
+
+@pytest.mark.parametrize("family", ["resunet", "geo"])
+def test_other_families_single_rank_communicator_matches_plain(cad, dev, oracle, family):
+    """train_step(communicator=...) — the staged backward with the RCCL bucket exchange on the
+    communicator's stream (cad_resunet_ / cad_geonet_backward_allreduce) — on one rank equals the
+    plain step bit for bit over three steps (identity all-reduce, stream hand-off, 1/world prescale)."""
+    B, H, W = 2, 64, 64
+    rgb, gt, K = [torch.from_numpy(a).to(dev) for a in oracle.synth_batch(B, H, W)]
+    comm = cad.Communicator(cad.Communicator.unique_id(), 1, 0, 0)
+    out = {}
+    for use in (False, True):
+        m, step = _family(cad, oracle, family, B, H, W)
+        if use:
+            comm.broadcast_parameters(m)
+        loss = cad.CombinedDepthLoss(batch=B, height=H, width=W)
+        losses = [step(loss, rgb, gt, K, communicator=comm if use else None, bucket_mb=0.25)[0].clone()
+                  for _ in range(3)]
+        torch.cuda.synchronize()
+        out[use] = (m.flat_params.clone(), torch.stack(losses))
+        del m, loss
+    assert torch.equal(out[True][0], out[False][0]) and torch.equal(out[True][1], out[False][1])
