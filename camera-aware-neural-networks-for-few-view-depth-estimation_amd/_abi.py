@@ -145,6 +145,7 @@ SIGNATURES = {
     "cad_op_conv3x3_fwd": (I, [P, I64, I, I, P, I, P, I64, I, I, I, I, P]),
     "cad_op_conv3x3_dgrad": (I, [P, I, P, I, P, I64, I, I, I, P]),
     "cad_op_conv3x3_wgrad": (I, [P, I, P, I64, I, I, P, I, I, I, P]),
+    "cad_op_conv3x3_wgrad_bf16": (I, [P, I64, I, P, I64, I, I, P, I, I, I, P]),
     "cad_op_convT_fwd": (I, [P, I, P, P, I, P, I64, I, I, I, I, P]),
     "cad_op_convT_dgrad": (I, [P, I64, I, I, P, I, P, I, I, I, P]),
     "cad_op_convT_wgrad": (I, [P, I, P, I64, I, I, P, I, I, I, P]),

@@ -1637,6 +1637,19 @@ cad_status cad_op_conv3x3_wgrad(const float* dz, int cout, const float* x, int64
         HIPCHK(hipGetLastError());
     });
 }
+cad_status cad_op_conv3x3_wgrad_bf16(const void* dz, int64_t lddz, int cout, const void* x, int64_t ldx, int xcoff,
+                                     int cin, float* dw, int B, int H, int W, void* stream) {
+    return guard([&] {
+        require(cad::gemm_engine() == 2, "the pre-split weight gradient runs on the bf16 engine (CAD_GEMM_BF16)");
+        const int64_t cap = cad::wgrad_slab_floats(cout, 9 * cin, B * H * W);
+        float* slab = nullptr;
+        HIPCHK(hipMallocAsync((void**)&slab, sizeof(float) * (size_t)std::max<int64_t>(cap, 4), S(stream)));
+        cad::conv3x3_wgrad_ps(cad::Split{dz, lddz, 0}, cout, cad::Split{x, ldx, xcoff}, cin, dw, B, H, W, slab, cap,
+                              S(stream));
+        HIPCHK(hipFreeAsync(slab, S(stream)));
+        HIPCHK(hipGetLastError());
+    });
+}
 cad_status cad_op_convT_fwd(const float* x, int cin, const float* w, const float* bias, int cout, float* y,
                             int64_t ldy, int ycoff, int B, int H, int W, void* stream) {
     return guard([&] {

@@ -529,8 +529,78 @@ void pcl_fwd(const Pcl& P, const float* u, const float* camn, int B, int H, int 
 // ------------------------------------------------------------------------------------------
 // PCL backward
 // ------------------------------------------------------------------------------------------
-// one wavefront per output pixel: input gradient scattered (fp32 atomics into du, zeroed first),
-// grid gradient reduced over the channels -> dgrid[p] (d gx, d gy)
+// The input gradient is GATHERED: each input pixel sums, in a fixed row-major order, the bilinear
+// weights of the output pixels whose sampling cell touches it, so the backward is deterministic run
+// to run (a scatter with fp32 atomics is not).  Those output pixels lie in the preimage of the 2x2
+// input cell under the sample's affine map: ix = a j + b i + c0, iy = d j + e i + f0 in pixel units,
+// a = th0, b = th1 W/H, d = th3 H/W, e = th4.  A near-singular map (a preimage box of more than
+// kGsGatherMax output pixels per input pixel) keeps the atomic scatter for that sample.
+constexpr int kGsGatherMax = 1024;
+struct GsFoot {
+    float inv00, inv01, inv10, inv11, c0, f0;   // (j, i) = inv * ((ix, iy) - (c0, f0))
+    int hj, hi;                                 // half extents of the preimage box (+2 guard)
+    bool gather;
+};
+__device__ __forceinline__ GsFoot gs_foot(const float* th, int H, int W) {
+    GsFoot f;
+    const float a = th[0], bb = th[1] * (float)W / (float)H, d = th[3] * (float)H / (float)W, e = th[4];
+    const float det = a * e - bb * d;
+    const GsPos o = gs_pos(th, 0, 0, H, W);
+    f.c0 = o.ix;
+    f.f0 = o.iy;
+    f.gather = false;
+    f.hj = f.hi = 0;
+    f.inv00 = f.inv01 = f.inv10 = f.inv11 = 0.f;
+    if (!(fabsf(det) > 1e-6f)) return f;
+    f.inv00 = e / det;
+    f.inv01 = -bb / det;
+    f.inv10 = -d / det;
+    f.inv11 = a / det;
+    const float ej = fabsf(f.inv00) + fabsf(f.inv01), ei = fabsf(f.inv10) + fabsf(f.inv11);
+    if (!(ej < 4096.f && ei < 4096.f)) return f;
+    f.hj = (int)ceilf(ej) + 2;
+    f.hi = (int)ceilf(ei) + 2;
+    f.gather = (int64_t)(2 * f.hj + 1) * (2 * f.hi + 1) <= kGsGatherMax;
+    return f;
+}
+
+// one wavefront per input pixel of a gather-mode sample, lanes over channels
+__global__ __launch_bounds__(256) void k_grid_sample_bwd_gather(Pcl P, const float* __restrict__ g, int64_t ldg,
+                                                                int gcoff, int H, int W, float* __restrict__ du,
+                                                                int64_t M) {
+    const int lane = threadIdx.x & 63;
+    const int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (p >= M) return;
+    const int C = P.C;
+    const int64_t HW = (int64_t)H * W, b = p / HW, yx = p - b * HW;
+    const int yy = (int)(yx / W), xx = (int)(yx - (int64_t)yy * W);
+    const float* th = P.theta + b * 6;
+    const GsFoot f = gs_foot(th, H, W);
+    if (!f.gather) return;
+    const float rx = (float)xx - f.c0, ry = (float)yy - f.f0;
+    const int cj = (int)floorf(f.inv00 * rx + f.inv01 * ry), ci = (int)floorf(f.inv10 * rx + f.inv11 * ry);
+    const int j0 = max(0, cj - f.hj), j1 = min(W - 1, cj + f.hj + 1);
+    const int i0 = max(0, ci - f.hi), i1 = min(H - 1, ci + f.hi + 1);
+    for (int c0 = 0; c0 < C; c0 += 64) {
+        const int c = c0 + lane;
+        float acc = 0.f;
+        for (int i = i0; i <= i1; ++i)
+            for (int j = j0; j <= j1; ++j) {
+                const GsPos q = gs_pos(th, i, j, H, W);
+                const float xw = floorf(q.ix), yn = floorf(q.iy);
+                const int x0 = (int)xw, y0 = (int)yn;
+                const int dx = xx - x0, dy = yy - y0;   // 0/1: which corner of (i, j)'s cell this pixel is
+                if ((unsigned)dx > 1u || (unsigned)dy > 1u) continue;
+                const float w = q.ix - xw, e_ = 1.f - w, nn = q.iy - yn, s = 1.f - nn;
+                const float wt = (dy ? nn : s) * (dx ? w : e_);
+                if (c < C) acc += wt * g[(b * HW + (int64_t)i * W + j) * ldg + gcoff + c];
+            }
+        if (c < C) du[p * C + c] = acc;
+    }
+}
+
+// one wavefront per output pixel: grid gradient reduced over the channels -> dgrid[p] (d gx, d gy);
+// the input gradient scattered with fp32 atomics (du zeroed first) only for near-singular samples
 __global__ __launch_bounds__(256) void k_grid_sample_bwd(Pcl P, const float* __restrict__ u,
                                                          const float* __restrict__ g, int64_t ldg, int gcoff, int H,
                                                          int W, float* __restrict__ du, int64_t M) {
@@ -540,6 +610,7 @@ __global__ __launch_bounds__(256) void k_grid_sample_bwd(Pcl P, const float* __r
     const int C = P.C;
     const int64_t HW = (int64_t)H * W, b = p / HW, yx = p - b * HW;
     const int i = (int)(yx / W), j = (int)(yx - (int64_t)i * W);
+    const bool scatter = !gs_foot(P.theta + b * 6, H, W).gather;
     const GsPos q = gs_pos(P.theta + b * 6, i, j, H, W);
     const float xw = floorf(q.ix), yn = floorf(q.iy);
     const float w = q.ix - xw, e_ = 1.f - w, nn = q.iy - yn, s = 1.f - nn;
@@ -559,6 +630,7 @@ __global__ __launch_bounds__(256) void k_grid_sample_bwd(Pcl P, const float* __r
         const float vsw = in_sw ? u[o_sw + c] : 0.f, vse = in_se ? u[o_se + c] : 0.f;
         gx += ((vne - vnw) * s + (vse - vsw) * nn) * go;
         gy += ((vsw - vnw) * e_ + (vse - vne) * w) * go;
+        if (!scatter) continue;
         if (in_nw) unsafeAtomicAdd(du + o_nw + c, (s * e_) * go);
         if (in_ne) unsafeAtomicAdd(du + o_ne + c, (s * w) * go);
         if (in_sw) unsafeAtomicAdd(du + o_sw + c, (nn * e_) * go);
@@ -700,6 +772,7 @@ void pcl_bwd(const Pcl& P, const float* u, const float* camn, const float* g, in
     const int64_t HW = (int64_t)H * W, M = (int64_t)B * HW, n = M * P.C;
     (void)hipMemsetAsync(du, 0, sizeof(float) * n, st);
     hipLaunchKernelGGL(k_grid_sample_bwd, dim3(cdiv(M, 4)), dim3(256), 0, st, P, u, g, ldg, gcoff, H, W, du, M);
+    hipLaunchKernelGGL(k_grid_sample_bwd_gather, dim3(cdiv(M, 4)), dim3(256), 0, st, P, g, ldg, gcoff, H, W, du, M);
     const int S = (int)std::max<int64_t>(1, std::min<int64_t>(64, HW / 2048));
     hipLaunchKernelGGL(k_pcl_dtheta, dim3(S, B), dim3(256), 0, st, P, H, W, (HW + S - 1) / S, scratch);
     hipLaunchKernelGGL(k_pcl_mlp_bwd, dim3(B), dim3(kPclHidden), 0, st, P, scratch, S);

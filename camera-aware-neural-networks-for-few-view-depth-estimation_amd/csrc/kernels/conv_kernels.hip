@@ -253,6 +253,8 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_win_bf16p4(GemmArgs a) {
 
 // window-tiled conv3x3 weight gradient (gemm_win.hpp): 64 co x 64 ci x 9 taps per workgroup, split-K
 __global__ __launch_bounds__(256, 2) void k_conv3x3_wgrad_win_s3(GemmArgs a) { conv3x3_wgrad_win_body<3>(a); }
+template <int P>
+__global__ __launch_bounds__(256, 2) void k_conv3x3_wgrad_win_bf16p(GemmArgs a) { conv3x3_wgrad_win_ps_body<P>(a); }
 
 template <int WM, int WN, int KB, class Epi>
 __global__ __launch_bounds__(256) void k_conv3x3_fwd_bf16(GemmArgs a) { conv3x3_fwd_np<1, WM, WN, 2, 2, KB, Epi>(a); }
@@ -900,6 +902,49 @@ void conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t 
     launch_kb<KConvFwdP1, 32, 64>(c, kb, a, 1, st);
 }
 
+// B1 window weight gradient (conv3x3_wgrad_win_ps_body): stage = P pixels of an image row
+#ifndef CAD_WGWIN_P
+#define CAD_WGWIN_P 32
+#endif
+#ifdef CAD_NO_WGWIN   // A/B builds (make VARIANT=... EXTRA=-DCAD_NO_WGWIN): the im2col kernel only
+constexpr bool g_no_wgwin = true;
+#else
+constexpr bool g_no_wgwin = false;
+#endif
+int wgrad_win_ps_stage(int cout, int cin, int W) {
+    if (cout % 64 || cin % 64) return 0;
+    for (int p : {CAD_WGWIN_P, 32, 16})
+        if (W % p == 0) return p;
+    return 0;
+}
+template <int P>
+void launch_wgrad_win_ps1(GemmArgs& a, float* dw, float* slab, int64_t slab_cap, hipStream_t st) {
+    const int cin = a.b_cin;
+    const int tiles = (a.M / 64) * (cin / 64);
+    const int nst = a.K / P;
+    int s = std::max(1, std::min(cdiv(2048, tiles), nst / 16));
+    const int64_t per = (int64_t)a.M * a.N;
+    if (slab_cap > 0) s = (int)std::max<int64_t>(1, std::min<int64_t>(s, slab_cap / per));
+    // a K-slice is a loader window of 32-bit byte offsets: keep it below 1 GB in either operand
+    const int64_t kbytes = 2 * std::max<int64_t>(a.lda, a.ldb);
+    const int64_t need = (int64_t)cdiv((int64_t)a.K * kbytes, (int64_t)1 << 30);
+    if (need > s) {
+        if (need * per > slab_cap) throw std::runtime_error("weight-gradient K-slice exceeds the 1 GB window and the slab");
+        s = (int)need;
+    }
+    a.kstages_per_split = cdiv(nst, s);
+    s = cdiv(nst, a.kstages_per_split);
+    a.ldc = a.N; a.slab_stride = per;
+    a.C = s == 1 ? dw : slab;
+    const dim3 grid(a.M / 64, cin / 64, s);
+    char name[96];
+    std::snprintf(name, sizeof name, "void cad::k_conv3x3_wgrad_win_bf16p<%d>(cad::GemmArgs)", P);
+    if (prof_enabled()) prof_push(name, 2.0 * a.M * a.N * (double)a.K, st);
+    hipLaunchKernelGGL(k_conv3x3_wgrad_win_bf16p<P>, grid, dim3(256), 0, st, a);
+    if (prof_enabled()) prof_pop(st);
+    if (s > 1) finish_slabs(slab, s, per, dw, st);
+}
+
 void conv3x3_wgrad_ps(Split dz, int cout, Split x, int cin, float* dw, int B, int H, int W, float* slab,
                       int64_t slab_cap, hipStream_t st) {
     ps_check(dz, cout, "conv3x3_wgrad dz");
@@ -909,6 +954,14 @@ void conv3x3_wgrad_ps(Split dz, int cout, Split x, int cin, float* dw, int B, in
     a.B = B; a.H = H; a.W = W;
     a.A = (const float*)dz.p; a.lda = dz.ld; a.a_coff = dz.coff;
     a.Bm = (const float*)x.p; a.ldb = x.ld; a.b_coff = x.coff; a.b_cin = cin;
+    if (!g_no_wgwin)
+        switch (wgrad_win_ps_stage(cout, cin, W)) {
+#if CAD_WGWIN_P == 64
+            case 64: launch_wgrad_win_ps1<64>(a, dw, slab, slab_cap, st); return;
+#endif
+            case 32: launch_wgrad_win_ps1<32>(a, dw, slab, slab_cap, st); return;
+            case 16: launch_wgrad_win_ps1<16>(a, dw, slab, slab_cap, st); return;
+        }
     const Cfg c = pick_cfg(a.M, a.N);
     const int kb = ps_kb(false, c);
     int s = plan_splits(a, c, kb, slab_cap, 2 * kMaxPlanes * std::max<int64_t>(dz.ld, x.ld));

@@ -20,6 +20,7 @@
 // kernel (cb-major), so the two agree to rounding, not bit for bit.
 #pragma once
 #include "gemm_s3.hpp"
+#include "gemm_ps.hpp"
 
 namespace cad {
 
@@ -569,6 +570,152 @@ __device__ __forceinline__ void conv3x3_wgrad_win_body(const GemmArgs& a) {
     }
     // slab z: C[z][co][tap*cin + ci] (row stride a.ldc = 9*cin)
     const int lane = tid & 63;
+    float* dst = a.C + (int64_t)tile.z * a.slab_stride;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int n = t * cin + ci0 + cib * 32 + (lane & 31);
+            const int co = co0 + cbk * 32 + 4 * (lane >> 5) + 8 * g;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) dst[(int64_t)(co + q) * a.ldc + n] = acc[t][4 * g + q];
+        }
+}
+
+
+// ------------------------------------------------------------------------------------------------
+// B1 window weight gradient on the bf16 twins (pre-split, NP = 1: plain NHWC bf16 rows).  The same
+// decomposition as conv3x3_wgrad_win_body — a workgroup owns a 64 (co) x 64 (ci) channel pair over all
+// nine taps and a split-K slice; wave w the 32x32 block (w & 1, w >> 1) of every tap — with stages of
+// P pixels of one image row (P/16 k16 steps: 9 P/16 MFMAs per wave and barrier) and no conversion:
+// the loaders move 16-B pieces (8 channels) global -> registers -> LDS.
+//   A = dZ[P px][64 co]                  planes [P k-rows][64]        (S3M<64>: 192-B k-rows)
+//   B = X rows y-1..y+1 x (P+2) px x 64 ci  planes [3 (P+2) k-rows][64]
+// Tap (ky, kx) reads B's k-rows ky (P+2) + kx + 16 s .. of k16 step s (ds_read_b64_tr_b16 fragments).
+// Per stage 64 P + 192 (P+2) elements for 64 x 576 x P MACs: X is fetched once per pixel and co-block
+// (the im2col GEMM fetches it once per tap).  Requirements (host): cout, cin % 64, W % P, twin
+// channel offsets % 8.
+// ------------------------------------------------------------------------------------------------
+template <int P>
+__device__ __forceinline__ void conv3x3_wgrad_win_ps_body(const GemmArgs& a) {
+    static_assert(P % 16 == 0, "stage");
+    constexpr int KW = 3 * (P + 2);                    // B window k-rows
+    constexpr int PLA = P * WgM::STRIDE, PLB = KW * WgM::STRIDE;   // bytes per operand image
+    constexpr int NCA = P * 8, NCB = KW * 8;           // 16-B pieces (8 channels) per stage
+    constexpr int NVA = (NCA + 255) / 256, NVB = (NCB + 255) / 256;
+    __shared__ __attribute__((aligned(16))) char lds[2 * (PLA + PLB)];
+
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6;
+    const int cbk = wave & 1, cib = wave >> 1;
+    const TileId tile = xcd_tile();
+    const int co0 = tile.x * 64, ci0 = tile.y * 64;
+    const int H = a.H, W = a.W;
+    const int nst = a.K / P;                           // stages (K = B*H*W, W % P == 0)
+    const int kbeg = tile.z * a.kstages_per_split;
+    const int kend = min(nst, kbeg + a.kstages_per_split);
+    const int segs = W / P;
+
+    // operand bases: the slice's first pixel (A) / minus one row and one pixel (B, the window's reach)
+    const int64_t p0 = (int64_t)kbeg * P;
+    const int64_t pb = p0 - W - 1 > 0 ? p0 - W - 1 : 0;
+    const int rowA = (int)a.lda * 2, rowB = (int)a.ldb * 2;   // bytes per twin row
+    const __amdgpu_buffer_rsrc_t rsa =
+        make_rsrc(ps_at(a.A, (p0 * a.lda + a.a_coff + co0) * 2));
+    const __amdgpu_buffer_rsrc_t rsb =
+        make_rsrc(ps_at(a.Bm, (pb * a.ldb + a.b_coff + ci0) * 2));
+    int aoff[NVA], alds[NVA];
+#pragma unroll
+    for (int j = 0; j < NVA; ++j) {
+        const int f = tid + 256 * j;
+        const int kr = f >> 3, g = f & 7;
+        aoff[j] = f < NCA ? kr * rowA + g * 16 : -1;
+        alds[j] = WgM::off(f < NCA ? kr : 0, g * 8);
+    }
+    int brel[NVB], bky[NVB], bkk[NVB], blds[NVB];
+#pragma unroll
+    for (int j = 0; j < NVB; ++j) {
+        const int f = tid + 256 * j;
+        const int kr = f >> 3, g = f & 7;
+        const bool in = f < NCB;
+        bky[j] = in ? kr / (P + 2) : -(1 << 28);        // out-of-window slots: never in range
+        bkk[j] = in ? kr - (kr / (P + 2)) * (P + 2) : 0;
+        brel[j] = in ? ((bky[j] - 1) * W + bkk[j] - 1) * rowB + g * 16 : 0;
+        blds[j] = WgM::off(in ? kr : 0, g * 8);
+    }
+
+    floatx16 acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+    // stage position: pixels x0 .. x0+P-1 of row y of image b
+    int sb_ = 0, sy = 0, sx0 = 0;
+    {
+        const int row = kbeg / segs;
+        sx0 = (kbeg - row * segs) * P;
+        sy = row % H;
+        sb_ = row / H;
+    }
+    uint4 ra[NVA], rb[NVB];
+    auto load = [&]() {
+        const int64_t pix = ((int64_t)sb_ * H + sy) * W + sx0;
+#pragma unroll
+        for (int j = 0; j < NVA; ++j)
+            ra[j] = bload16(rsa, aoff[j] >= 0 ? (uint32_t)((pix - p0) * rowA) + (uint32_t)aoff[j] : kOOB);
+        const int sbase = (int)((pix - pb) * rowB);
+#pragma unroll
+        for (int j = 0; j < NVB; ++j) {
+            const int yy = sy + bky[j] - 1, xx = sx0 + bkk[j] - 1;
+            const bool ok = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+            rb[j] = bload16(rsb, ok ? (uint32_t)(sbase + brel[j]) : kOOB);
+        }
+        sx0 += P;
+        if (sx0 == W) { sx0 = 0; if (++sy == H) { sy = 0; ++sb_; } }
+    };
+    auto store = [&](int buf) {
+        char* da = lds + buf * (PLA + PLB);
+#pragma unroll
+        for (int j = 0; j < NVA; ++j)
+            if (NCA % 256 == 0 || tid + 256 * j < NCA) *reinterpret_cast<uint4*>(da + alds[j]) = ra[j];
+#pragma unroll
+        for (int j = 0; j < NVB; ++j)
+            if (NCB % 256 == 0 || tid + 256 * j < NCB) *reinterpret_cast<uint4*>(da + PLA + blds[j]) = rb[j];
+    };
+    auto compute = [&](int buf) {
+        const char* sa = lds + buf * (PLA + PLB);
+        const char* sb = sa + PLA;
+#pragma unroll
+        for (int q = 0; q < P / 16; ++q) {
+            bf16x8 fa[1];
+            mnc_frag_at<kWgRows, 1>(sa, PLA, cbk * 32, 16 * q, fa);
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                bf16x8 fb[1];
+                mnc_frag_at<kWgRows, 1>(sb, PLB, cib * 32, (t / 3) * (P + 2) + (t % 3) + 16 * q, fb);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], acc[t], 0, 0, 0);
+            }
+        }
+    };
+
+    if (kbeg < kend) {
+        load();
+        store(0);
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int kt = kbeg; kt < kend; ++kt) {
+        const bool more = kt + 1 < kend;
+        if (more) load();
+        compute(cur);
+        if (more) store(cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
+    }
+    // slab z: C[z][co][tap*cin + ci] (row stride a.ldc = 9*cin)
+    const int lane = tid & 63;
+    const int cin = a.b_cin;
     float* dst = a.C + (int64_t)tile.z * a.slab_stride;
 #pragma unroll
     for (int t = 0; t < 9; ++t)

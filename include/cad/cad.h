@@ -401,6 +401,12 @@ cad_status cad_op_conv3x3_dgrad(const float* dz, int cout, const float* w_ohwi, 
                                 int64_t lddx, int B, int H, int W, void* stream);
 cad_status cad_op_conv3x3_wgrad(const float* dz, int cout, const float* x, int64_t ldx, int xcoff, int cin,
                                 float* dw_ohwi, int B, int H, int W, void* stream);
+/* the bf16 engine's weight gradient on pre-split bf16 NHWC operands (the twins the engine stores):
+ * dz rows of lddz bf16, x rows of ldx bf16 at channel offset xcoff (% 8); fp32 OHWI result.  Window
+ * kernel when cout, cin % 64 == 0 and W % 16 == 0, the im2col GEMM otherwise.  Requires
+ * cad_set_gemm_engine(CAD_GEMM_BF16). */
+cad_status cad_op_conv3x3_wgrad_bf16(const void* dz, int64_t lddz, int cout, const void* x, int64_t ldx, int xcoff,
+                                     int cin, float* dw_ohwi, int B, int H, int W, void* stream);
 cad_status cad_op_convT_fwd(const float* x, int cin, const float* w_iqo, const float* bias, int cout,
                             float* y, int64_t ldy, int ycoff, int B, int H, int W, void* stream);
 cad_status cad_op_convT_dgrad(const float* g, int64_t ldg, int gcoff, int cout, const float* w_iqo, int cin,

@@ -103,6 +103,19 @@ def gpu_relu_decisions(net, params, f, B, H, W, model="baseline"):
     return masks
 
 
+def gpu_film_params(net, params, f, B, model="rayfilm"):
+    """The FiLM (gamma, beta) of every FiLM DoubleConv of `net`'s last forward (cad_unet_debug_buffer
+    "<tag>_gamma|_beta", (B, C) each), keyed like cad_oracle.FILM_FORCE ("enc1.film.", ...)."""
+    out = {}
+    for tag, pre, l in unet_bn_blocks(model):
+        if pre + "film.fc1.weight" not in params:
+            continue
+        C = f << l
+        out[pre + "film."] = tuple(net.debug_buffer(f"{tag}_{t}")[: B * C].reshape(B, C).clone()
+                                   for t in ("gamma", "beta"))
+    return out
+
+
 def gpu_conv_outputs(net, f, B, H, W, model="baseline"):
     """The stored pre-BN outputs of every 3x3 convolution of `net`'s last forward (bf16 values on the
     bf16 engine), NCHW float, keyed like cad_oracle.Y_FORCE ("enc1.conv1", "dec2.conv.conv2", ...)."""

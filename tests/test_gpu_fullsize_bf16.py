@@ -17,21 +17,28 @@ reductions over ~1800 slabs, BN statistics over 9.8 M pixels, the FiLM / ray pac
 per batch, clip over all gradients.
 
 Both sides round the same operands to bf16, but an fp32 difference of one ulp in a value that sits
-next to a bf16 rounding boundary becomes a one-bf16-ulp (2^-8) difference of that operand: about
-1e-6 / 4e-3 of the rounded values differ by 4e-3 relative on every layer, on either side, and the
-oracle takes this run's ReLU decisions (cad_oracle.RELU_FORCE, as the small-size tests).  Sums that
-cancel heavily amplify that noise: a BatchNorm affine gradient is a per-channel sum over 9.8 M pixels
-whose terms cancel 50-2000x.  So the criteria (measured values in DESIGN.md §5) are:
-  * prediction and dL/dpred: bulk (99.9th percentile of |ours - oracle| / max|oracle|) within the
-    north-star's 1e-3; max within 1e-2 (prediction) and 5e-2 (dL/dpred: the gradient-matching term is
-    an L1 norm whose sign flips with the prediction's last bits);
+next to a bf16 rounding boundary becomes a one-bf16-ulp (2^-8) difference of that operand, and a
+pre-activation within rounding of 0 takes either ReLU branch.  Left alone, those flips compound layer
+by layer (measured: prediction bulk 2.5e-3, BatchNorm affine gradients — per-channel sums over 9.8 M
+pixels that cancel 50-2000x — off by up to 27%).  So the oracle runs LAYER-WISE on the GPU's own
+intermediate decisions: every 3x3 convolution's stored bf16 output (cad_oracle.Y_FORCE), every ReLU
+decision (RELU_FORCE) and every FiLM modulation (FILM_FORCE) are imposed, and each of them is judged
+on its own first:
+  * every convolution's own output on the identical inputs within 1 bf16 ulp of the GPU's (fraction
+    differing < 1e-3), the FiLM gamma / beta reported against the oracle's own;
+then the whole step (BN, ReLU masks, FiLM, pool, ConvT, head, 4-term loss, backward, clip, Adam):
+  * prediction bulk (99.9th percentile of |ours - oracle| / max|oracle|) < 1e-5, max < 1e-4;
+    dL/dpred bulk < 1e-5, max < 1e-2 (the gradient-matching term is an L1 norm whose sign flips with
+    the prediction's last bits);
   * every loss term and the clip norm within 1e-4 relative;
-  * whole-gradient cosine >= 0.9999; every conv / ConvT / head weight gradient at cosine >= 0.999; the
-    BatchNorm affine gradients (the cancelling sums above) at cosine >= 0.9;
+  * whole-gradient cosine >= 0.99999; every conv / ConvT / head weight gradient at 1-cos < 2e-4; BN
+    and FiLM affine gradients at 1-cos < 2e-3; the FiLM fc1 / fc2 biases (their true gradient is 0:
+    each feeds a BatchNorm1d) at a norm below 1e-2 of their weight gradient's;
   * parameters after Adam within 2 lr, moving by more than 1e-5 only where the oracle's |g| is within
     3x the tensor's largest gradient disagreement (Adam's first step is ~lr sign(g));
-  * BN running statistics within 1e-4; the eval-mode prediction of the updated model as the
-    prediction, abs_rel within 1e-3.
+  * BN running statistics within 1e-4; the eval-mode prediction of the updated model (no forcing:
+    a fresh forward of both) bulk < 5e-4, max < 1e-3, abs_rel within 1e-5 relative.
+Measured values: DESIGN.md §5.
 No fp64 run at this size (the fp32 configs[1] test, test_gpu_fullsize.py, already spends ~5 minutes
 of host time on one)."""
 import sys
@@ -41,7 +48,7 @@ import time
 import pytest
 import torch
 
-from conftest import gpu_conv_outputs, gpu_relu_decisions, max_rel_err
+from conftest import gpu_conv_outputs, gpu_film_params, gpu_relu_decisions, max_rel_err
 
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 
@@ -104,16 +111,20 @@ def _judge(beat, g, r, g_grads, g_norm, g_params, g_bufs, ref_p, ref_bufs, spec,
              r["comps"]["reproj_loss"]]
     e_loss = [abs(a - b) / abs(b) for a, b in zip(l5, comps)]
     e_norm = abs(g_norm - r["norm"]) / r["norm"]
-    conv, bn, flat_g, flat_r = [], [], [], []
+    conv, bn, zero, flat_g, flat_r = [], [], [], [], []
     for (n, _), gr in zip(spec, r["grads"]):
         if gr is None:
             continue
-        row = (1 - _cos(g_grads[n], gr), _bulk(g_grads[n], gr), n)
-        (conv if gr.dim() >= 2 else bn).append(row)
         flat_g.append(g_grads[n].reshape(-1))
         flat_r.append(gr.reshape(-1))
+        if ".film.fc1.bias" in n or ".film.fc2.bias" in n:   # a Linear bias feeding BatchNorm1d
+            zero.append((g_grads[n].norm().item() / (g_grads[n.replace("bias", "weight")].norm().item() or 1.0), n))
+            continue
+        row = (1 - _cos(g_grads[n], gr), _bulk(g_grads[n], gr), n)
+        (conv if gr.dim() >= 2 else bn).append(row)
     conv.sort(reverse=True)
     bn.sort(reverse=True)
+    zero.sort(reverse=True)
     cos_all = _cos(torch.cat(flat_g), torch.cat(flat_r))
     # Adam's first step is ~lr sign(g): a weight moves by more than rounding only where the two
     # gradients may disagree in sign, i.e. |g| within 3x the tensor's largest |ours - oracle|
@@ -133,16 +144,19 @@ def _judge(beat, g, r, g_grads, g_norm, g_params, g_bufs, ref_p, ref_bufs, spec,
     beat(f"pred max {e_pred:.3e} bulk {b_pred:.3e}; dpred max {e_dpred:.3e} bulk {b_dpred:.3e}; loss terms "
          f"{[f'{x:.2e}' for x in e_loss]}; clip norm {e_norm:.2e}; whole-gradient cosine {cos_all:.7f}")
     beat(f"conv / ConvT / head weight gradients (1-cos, bulk, name), worst: {conv[:4]}")
-    beat(f"BN affine gradients (1-cos, bulk, name), worst: {bn[:4]}")
+    beat(f"BN / FiLM affine gradients (1-cos, bulk, name), worst: {bn[:4]}")
+    if zero:
+        beat(f"FiLM fc1/fc2 biases (true gradient 0): |g| / |g of the weight|, worst: {zero[:3]}")
     beat(f"params after Adam: max |diff| {worst_move:.3e}, {moved} of {n_all} moved > 1e-5, {unexplained} of them "
          f"where |g| exceeds 3x the tensor's gradient disagreement; BN buffers {e_bufs:.2e}")
-    checks = [("pred", b_pred < 1e-3 and e_pred < 1e-2, (b_pred, e_pred)),
-              ("dpred", b_dpred < 1e-3 and e_dpred < 5e-2, (b_dpred, e_dpred)),
+    checks = [("pred", b_pred < 1e-5 and e_pred < 1e-4, (b_pred, e_pred)),
+              ("dpred", b_dpred < 1e-5 and e_dpred < 1e-2, (b_dpred, e_dpred)),
               ("loss terms", max(e_loss) < 1e-4, e_loss),
               ("clip norm", e_norm < 1e-4, (g_norm, r["norm"])),
-              ("whole-gradient cosine", cos_all > 0.9999, cos_all),
-              ("conv gradients", conv[0][0] < 1e-3, conv[:4]),
-              ("BN affine gradients", bn[0][0] < 0.1, bn[:4]),
+              ("whole-gradient cosine", cos_all > 0.99999, cos_all),
+              ("conv gradients", conv[0][0] < 2e-4, conv[:4]),
+              ("BN affine gradients", bn[0][0] < 2e-3, bn[:4]),
+              ("zero-gradient biases", not zero or zero[0][0] < 1e-2, zero[:3]),
               ("Adam", worst_move <= 2 * LR + 1e-6 and unexplained == 0, (worst_move, unexplained)),
               ("BN buffers", e_bufs < 1e-4, e_bufs)]
     return [c for c in checks if not c[1]]
@@ -174,6 +188,7 @@ def test_bs32_480x640_bf16_step_vs_oracle(cad, dev, oracle, bf16_engine, beat, m
     g_grads = m.grads()
     relu = gpu_relu_decisions(m, params, F, B, H, W, model)
     yf = gpu_conv_outputs(m, F, B, H, W, model)
+    ff = gpu_film_params(m, params, F, B, model)
     cad.clip_grad_norm_(m, 1.0)
     tr.optimizer.step()
     torch.cuda.synchronize()
@@ -189,15 +204,23 @@ def test_bs32_480x640_bf16_step_vs_oracle(cad, dev, oracle, bf16_engine, beat, m
     ref = oracle.Trainer(params, bufs, weights=WEIGHTS, model=model, gemm_operands="bf16")
     oracle.RELU_FORCE.update(relu)
     oracle.Y_FORCE.update(yf)
+    oracle.FILM_FORCE.update(ff)
     try:
         r = ref.step(rgb, gt, K)
     finally:
         oracle.RELU_FORCE.clear()
         oracle.Y_FORCE.clear()
+        oracle.FILM_FORCE.clear()
     del relu
-    # every convolution judged on identical inputs: its own output vs the GPU's stored one, in units
-    # of the stored value's bf16 spacing (2^(e-7) for |y| in [2^e, 2^(e+1))); enc1.conv1 of the
-    # baseline (3-channel image, in-loader kernel) stores fp32
+    # every convolution judged on identical inputs (conv outputs, ReLU decisions and FiLM modulation
+    # imposed): its own output vs the GPU's stored one, in units of the bf16 spacing of the larger of
+    # the two (2^(e-7) for |y| in [2^e, 2^(e+1))), floored at 2^-20 of the layer's largest |y| (the
+    # fp32 accumulation error of a sum that cancels to ~0, below which bf16 spacing means nothing);
+    # enc1.conv1 of the baseline (3-channel image, in-loader kernel) stores fp32
+    for n, (fg, fb) in ff.items():
+        beat(f"{model}: FiLM {n} gamma/beta vs the oracle's own: "
+             f"{max_rel_err(fg, oracle.FILM_OWN[n][0]):.2e} / {max_rel_err(fb, oracle.FILM_OWN[n][1]):.2e}")
+    oracle.FILM_OWN.clear()
     rows = []
     for n, gy in yf.items():
         own = oracle.Y_OWN.pop(n).float()
@@ -205,9 +228,10 @@ def test_bs32_480x640_bf16_step_vs_oracle(cad, dev, oracle, bf16_engine, beat, m
         if model == "baseline" and n == "enc1.conv1":
             rows.append((d.max().item() / gy.abs().max().item(), 0.0, n))
             continue
-        ulp = torch.exp2(torch.floor(torch.log2(gy.double().abs().clamp_min(1e-30))) - 7)
+        big = torch.maximum(gy.double().abs(), own.double().abs()).clamp_min(2.0 ** -20 * gy.abs().max().item())
+        ulp = torch.exp2(torch.floor(torch.log2(big)) - 7)
         rows.append(((d / ulp).max().item(), (d > 0).double().mean().item(), n))
-        del own, d, ulp
+        del own, d, ulp, big
     oracle.Y_OWN.clear()
     del yf
     rows.sort(reverse=True)
@@ -222,9 +246,9 @@ def test_bs32_480x640_bf16_step_vs_oracle(cad, dev, oracle, bf16_engine, beat, m
     e_eval = max_rel_err(g_eval, r_eval)
     b_eval = _bulk(g_eval, r_eval)
     beat(f"{model}: eval pred max {e_eval:.3e} bulk {b_eval:.3e}; abs_rel gpu {g_absrel:.6f} cpu {r_absrel:.6f}")
-    if not (b_eval < 1e-3 and e_eval < 1e-2):
+    if not (b_eval < 5e-4 and e_eval < 1e-3):
         bad.append(("eval pred", False, (b_eval, e_eval)))
-    if not abs(g_absrel - r_absrel) <= 1e-3 * r_absrel:
+    if not abs(g_absrel - r_absrel) <= 1e-5 * r_absrel:
         bad.append(("abs_rel", False, (g_absrel, r_absrel)))
     assert not bad, bad
 

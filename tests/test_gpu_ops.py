@@ -161,6 +161,55 @@ def test_conv3x3_wgrad_strided_input(cad, dev):
     assert max_rel_err(dw.cpu().permute(0, 3, 1, 2), wd.grad) < TOL
 
 
+WGRAD_BF16_SHAPES = [  # B, H, W, cin, cout, xcoff: the bf16 engine's weight gradient on bf16 twins
+    (2, 6, 64, 64, 128, 0),     # window kernel, 32-pixel stages, two per row
+    (3, 5, 16, 64, 192, 8),     # 16-pixel stages (W % 32 != 0), halo rows at image edges, channel offset
+    (1, 40, 96, 128, 64, 0),    # 3 stages per row, many K-splits over 120 stages
+    (2, 9, 32, 256, 128, 64),   # skip half of a concat-style twin
+    (2, 6, 20, 64, 64, 0),      # W % 16 != 0: the im2col GEMM
+    (2, 5, 16, 32, 64, 0),      # cin % 64 != 0: the im2col GEMM
+]
+
+
+@pytest.mark.parametrize("B,H,W,cin,cout,xcoff", WGRAD_BF16_SHAPES)
+def test_conv3x3_wgrad_bf16_twins(cad, dev, B, H, W, cin, cout, xcoff):
+    """cad_op_conv3x3_wgrad_bf16 (B1 window weight gradient, conv3x3_wgrad_win_ps_body) against the
+    fp64 contraction of the same bf16 operands: the only admitted error is fp32 accumulation."""
+    lib = cad.load_library()
+    prev = lib.cad_get_gemm_engine()
+    assert lib.cad_set_gemm_engine(2) == 0
+    try:
+        g = torch.Generator().manual_seed(B * H * W + cin + cout + xcoff)
+        x = torch.randn(B, cin, H, W, generator=g).bfloat16()
+        dy = torch.randn(B, cout, H, W, generator=g).bfloat16()
+        wd = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, requires_grad=True)
+        F.conv2d(x.double(), wd, None, 1, 1).backward(dy.double())
+        ldx = xcoff + cin + 8
+        xbuf = torch.zeros(B, H, W, ldx, dtype=torch.bfloat16)
+        xbuf[..., xcoff:xcoff + cin] = nhwc(x)
+        xg, dyg = xbuf.to(dev), nhwc(dy).to(dev)
+        dw = torch.full((cout, 3, 3, cin), 7.0, device=dev)
+        assert lib.cad_op_conv3x3_wgrad_bf16(_p(dyg), cout, cout, _p(xg), ldx, xcoff, cin, _p(dw), B, H, W,
+                                             _s()) == 0, lib.cad_last_error()
+        torch.cuda.synchronize()
+        assert max_rel_err(dw.cpu().permute(0, 3, 1, 2), wd.grad) < TOL
+    finally:
+        lib.cad_set_gemm_engine(prev)
+
+
+def test_conv3x3_wgrad_bf16_needs_bf16_engine(cad, dev):
+    lib = cad.load_library()
+    prev = lib.cad_get_gemm_engine()
+    assert lib.cad_set_gemm_engine(1) == 0
+    try:
+        t = torch.zeros(64, dtype=torch.bfloat16, device=dev)
+        dw = torch.zeros(64, device=dev)
+        assert lib.cad_op_conv3x3_wgrad_bf16(_p(t), 64, 64, _p(t), 64, 0, 64, _p(dw), 1, 1, 1, _s()) != 0
+        assert b"bf16 engine" in lib.cad_last_error()
+    finally:
+        lib.cad_set_gemm_engine(prev)
+
+
 CONVT_SHAPES = [(2, 8, 12, 128, 64), (1, 4, 5, 1024, 512), (3, 6, 6, 32, 16), (2, 3, 4, 8, 4)]
 
 
