@@ -504,9 +504,9 @@ void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin,
         cad::conv3x3_fwd(in, ldin, 0, dc.c1.cin, h->P(dc.c1.pidx), C, dc.y1, C, 0, B, Hh, Ww, stats, st);
     bn(dc.b1, dc.c1.cin, ps1);
     if (dc.has_film()) {   // FiLMDoubleConvImpl::forward (intrinsics_unet.h:38-52)
-        cad::film_apply(dc.y1, C, dc.b1.scale, dc.b1.shift, dc.film.gam, dc.film.bet, B, (int64_t)Hh * Ww, dc.a1, st,
-                        dc.y1b);
-        if (ps) cad::split_rows(dc.a1, C, 0, C, M, dc.a1s, C, 0, st);
+        // pre-split GEMMs read only a1's twin (written by the same pass): the fp32 a1 is not written
+        cad::film_apply(dc.y1, C, dc.b1.scale, dc.b1.shift, dc.film.gam, dc.film.bet, B, (int64_t)Hh * Ww,
+                        ps ? nullptr : dc.a1, st, dc.y1b, ps ? dc.a1s : nullptr);
     } else {
         // pre-split GEMMs read only a1's twin (conv2 and its weight gradient): the fp32 a1 is not written
         cad::bn_relu_fwd(dc.y1, C, dc.b1.scale, dc.b1.shift, ps ? nullptr : dc.a1, C, 0, M, st, ps ? dc.a1s : nullptr,
@@ -1014,11 +1014,10 @@ int64_t cad_unet_debug_buffer(cad_unet* h, const char* name, float* host, int64_
     // With pre-split operands (bf16 engine) the last forward/backward wrote only the bf16 twins of
     // these buffers: their fp32 copies are stale, so refuse them rather than return old data
     if (h->fwd_np > 0) {
-        const bool film = h->model != CAD_MODEL_BASELINE;
         const bool twin_only = n == "Sb" || n == "bott" || (n.compare(0, 4, "pool") == 0) ||
                                (n.compare(0, 3, "cat") == 0) ||   // up half: twin only
                                (n.compare(0, 4, "dout") == 0 && n != "dout0") ||
-                               (!film && n.size() > 5 && n.substr(5) == "a1");
+                               (n.size() > 5 && n.substr(5) == "a1");
         if (twin_only) {
             g_err = "debug buffer '" + n + "' holds no fp32 copy on the pre-split (bf16) engine";
             return -1;

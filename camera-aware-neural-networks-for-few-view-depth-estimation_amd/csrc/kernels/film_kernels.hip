@@ -14,6 +14,7 @@
 // the same two-level slice scheme as the BN reductions.
 #include <algorithm>
 
+#include "gemm_s3.hpp"   // split_np (the bf16 twin of the modulated activations)
 #include "ew_load.hpp"
 #include "kernels.hpp"
 
@@ -122,51 +123,60 @@ __device__ void bn1d_relu_col(float* zx, float* h, int ldz, int j, int B, bool b
     }
 }
 
-__global__ __launch_bounds__(256) void k_film_hidden_fwd(FilmLayer L, const float* __restrict__ camn, int B,
-                                                         int train) {
+// fc1 (4 -> 128) + BN1d + ReLU: one thread per feature column, the batch in a loop
+__global__ __launch_bounds__(H1) void k_film_l1_fwd(FilmLayer L, const float* __restrict__ camn, int B, int train) {
     const int j = threadIdx.x;
-    const bool bn = B > 1;
-    if (j < H1) {
-        for (int b = 0; b < B; ++b) {
-            float z = L.b1[j];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) z += camn[b * 4 + k] * L.w1[j * 4 + k];
-            L.xh1[b * H1 + j] = z;
-        }
-        bn1d_relu_col(L.xh1, L.h1, H1, j, B, bn, train, L.g1, L.be1, L.rm1, L.rv1, L.is1);
-    }
-    __syncthreads();
     for (int b = 0; b < B; ++b) {
-        float z = L.b2[j];
-        const float* hr = L.h1 + b * H1;
-        const float* wr = L.w2 + j * H1;
-        for (int k = 0; k < H1; ++k) z += hr[k] * wr[k];
-        L.xh2[b * H2 + j] = z;
+        float z = L.b1[j];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) z += camn[b * 4 + k] * L.w1[j * 4 + k];
+        L.xh1[b * H1 + j] = z;
     }
-    bn1d_relu_col(L.xh2, L.h2, H2, j, B, bn, train, L.g2, L.be2, L.rm2, L.rv2, L.is2);
+    bn1d_relu_col(L.xh1, L.h1, H1, j, B, B > 1, train, L.g1, L.be1, L.rm1, L.rv1, L.is1);
 }
 
-// gamma / beta: column o in [0, 2C): o < C -> gamma[:, o], else beta[:, o - C]
-__global__ __launch_bounds__(256) void k_film_head_fwd(FilmLayer L, int B) {
-    const int o = blockIdx.x * blockDim.x + threadIdx.x;
-    const int C = L.C;
-    if (o >= 2 * C) return;
-    const bool isg = o < C;
-    const int c = isg ? o : o - C;
-    const float* w = (isg ? L.wg : L.wb) + (int64_t)c * H2;
-    const float bias = (isg ? L.bg : L.bb)[c];
-    float* dst = isg ? L.gam : L.bet;
-    for (int b = 0; b < B; ++b) {
-        const float* hr = L.h2 + b * H2;
-        float z = bias;
-        for (int k = 0; k < H2; ++k) z += hr[k] * w[k];
-        dst[b * C + c] = z;
+// Y[b][o] = bias[o] + sum_k X[b][k] W[o][k] (nn.Linear, W row-major [O][K]): one thread per output
+// (b, o), o fastest — X[b] is a wavefront-wide broadcast, the weight rows stream through L1/L2 in
+// 16-B pieces — summed bias first, then k in order (the arithmetic of the sequential form exactly).
+// blockIdx.y selects one of two (W, bias, Y) sets (the gamma / beta heads in one launch).
+template <int K>
+__global__ __launch_bounds__(256) void k_film_linear(const float* __restrict__ X, const float* __restrict__ W0,
+                                                     const float* __restrict__ b0, float* __restrict__ Y0,
+                                                     const float* __restrict__ W1, const float* __restrict__ b1,
+                                                     float* __restrict__ Y1, int B, int O) {
+    static_assert(K % 4 == 0, "K");
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)B * O) return;
+    const int b = (int)(t / O), o = (int)(t - (int64_t)b * O);
+    const float* W = (blockIdx.y ? W1 : W0) + (int64_t)o * K;
+    const float* x = X + (int64_t)b * K;
+    float z = (blockIdx.y ? b1 : b0)[o];
+#pragma unroll 8
+    for (int k = 0; k < K; k += 4) {
+        const float4 w = *reinterpret_cast<const float4*>(W + k);
+        const float4 v = *reinterpret_cast<const float4*>(x + k);
+        z += v.x * w.x;
+        z += v.y * w.y;
+        z += v.z * w.z;
+        z += v.w * w.w;
     }
+    (blockIdx.y ? Y1 : Y0)[t] = z;
+}
+
+// BN1d + ReLU over the fc2 outputs (already in xh2): one thread per feature column
+__global__ __launch_bounds__(H2) void k_film_l2_bn(FilmLayer L, int B, int train) {
+    bn1d_relu_col(L.xh2, L.h2, H2, threadIdx.x, B, B > 1, train, L.g2, L.be2, L.rm2, L.rv2, L.is2);
 }
 
 void film_mlp_fwd(const FilmLayer& L, const float* camn, int B, bool train, hipStream_t st) {
-    hipLaunchKernelGGL(k_film_hidden_fwd, dim3(1), dim3(H2), 0, st, L, camn, B, (int)train);
-    hipLaunchKernelGGL(k_film_head_fwd, dim3(cdiv(2 * L.C, 256)), dim3(256), 0, st, L, B);
+    hipLaunchKernelGGL(k_film_l1_fwd, dim3(1), dim3(H1), 0, st, L, camn, B, (int)train);
+    hipLaunchKernelGGL(k_film_linear<H1>, dim3(cdiv((int64_t)B * H2, 256), 1), dim3(256), 0, st, (const float*)L.h1,
+                       (const float*)L.w2, (const float*)L.b2, L.xh2, (const float*)nullptr, (const float*)nullptr,
+                       (float*)nullptr, B, H2);
+    hipLaunchKernelGGL(k_film_l2_bn, dim3(1), dim3(H2), 0, st, L, B, (int)train);
+    hipLaunchKernelGGL(k_film_linear<H2>, dim3(cdiv((int64_t)B * L.C, 256), 2), dim3(256), 0, st, (const float*)L.h2,
+                       (const float*)L.wg, (const float*)L.bg, L.gam, (const float*)L.wb, (const float*)L.bb, L.bet,
+                       B, L.C);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -174,11 +184,13 @@ void film_mlp_fwd(const FilmLayer& L, const float* camn, int B, bool train, hipS
 // ------------------------------------------------------------------------------------------
 // row-slice form (as the BN passes, nn_kernels.hip): a thread owns one 4-channel group, keeps its BN
 // scale / shift in registers and re-reads gamma / beta only when its rows cross into the next sample
-template <bool YB>
+// os: the bf16 twin (pre-split operand of conv2 and its weight gradient, rows of C); out (fp32) may be
+// null when only the twin has readers
+template <bool YB, bool TW>
 __global__ __launch_bounds__(256) void k_film_apply(const float* __restrict__ y, int C, const float* __restrict__ scale,
                                                     const float* __restrict__ shift, const float* __restrict__ gam,
                                                     const float* __restrict__ bet, int64_t HW, float* __restrict__ out,
-                                                    int64_t M, int64_t rps) {
+                                                    char* __restrict__ os, int64_t M, int64_t rps) {
     const int c4 = blockIdx.x * blockDim.x + threadIdx.x;
     if (c4 >= (C >> 2)) return;
     const int c = c4 * 4;
@@ -200,21 +212,23 @@ __global__ __launch_bounds__(256) void k_film_apply(const float* __restrict__ y,
         o.y = g.y * fmaxf(v.y * s.y + t.y, 0.f) + b.y;
         o.z = g.z * fmaxf(v.z * s.z + t.z, 0.f) + b.z;
         o.w = g.w * fmaxf(v.w * s.w + t.w, 0.f) + b.w;
-        *reinterpret_cast<float4*>(out + r * C + c) = o;
+        if (out) *reinterpret_cast<float4*>(out + r * C + c) = o;
+        if constexpr (TW) *reinterpret_cast<uint2*>(os + (r * C + c) * 2) = split_np<1>(o).p[0];
     }
 }
 void film_apply(const float* y, int C, const float* scale, const float* shift, const float* gam, const float* bet,
-                int B, int64_t HW, float* out, hipStream_t st, bool y_bf16) {
+                int B, int64_t HW, float* out, hipStream_t st, bool y_bf16, void* os) {
     const int64_t M = (int64_t)B * HW;
     const int C4 = C >> 2, CX = std::min(C4, 64), RY = std::max(1, 256 / CX);
     const int S = (int)std::max<int64_t>(1, std::min<int64_t>(65535, cdiv(M, (int64_t)RY * 16)));
     const int64_t rps = (M + S - 1) / S;
-    if (y_bf16)
-        hipLaunchKernelGGL(k_film_apply<true>, dim3(cdiv(C4, CX), S), dim3(CX, RY), 0, st, y, C, scale, shift, gam, bet,
-                           HW, out, M, rps);
-    else
-        hipLaunchKernelGGL(k_film_apply<false>, dim3(cdiv(C4, CX), S), dim3(CX, RY), 0, st, y, C, scale, shift, gam, bet,
-                           HW, out, M, rps);
+    char* o = static_cast<char*>(os);
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(cdiv(C4, CX), S), dim3(CX, RY), 0, st, y, C, scale, shift, gam, bet, HW, out, o,
+                           M, rps);
+    };
+    if (os) y_bf16 ? go(k_film_apply<true, true>) : go(k_film_apply<false, true>);
+    else y_bf16 ? go(k_film_apply<true, false>) : go(k_film_apply<false, false>);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -315,15 +329,28 @@ __global__ __launch_bounds__(256) void k_film_head_bwd_w(FilmLayer L, int B) {
     if (k < H2) (isg ? L.gwg : L.gwb)[(int64_t)c * H2 + k] = acc;
     else (isg ? L.gbg : L.gbb)[c] = acc;
 }
-// dh2[b][k] = Σ_c dgam[b][c] Wg[c][k] + dbet[b][c] Wb[c][k]
+// dh2[b][k] = Σ_c dgam[b][c] Wg[c][k] + Σ_c dbet[b][c] Wb[c][k], summed in that order: one thread per
+// (b, k), k fastest (coalesced weight rows, dgam / dbet broadcast); loads run 8 terms ahead of the
+// dependent FMA chain
 __global__ __launch_bounds__(256) void k_film_dh2(FilmLayer L, int B) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= B * H2) return;
     const int b = t / H2, k = t - b * H2;
     const int C = L.C;
     float acc = 0.f;
-    for (int c = 0; c < C; ++c) acc += L.dgam[b * C + c] * L.wg[(int64_t)c * H2 + k];
-    for (int c = 0; c < C; ++c) acc += L.dbet[b * C + c] * L.wb[(int64_t)c * H2 + k];
+    for (int pass = 0; pass < 2; ++pass) {
+        const float* d = (pass ? L.dbet : L.dgam) + (int64_t)b * C;
+        const float* w = (pass ? L.wb : L.wg) + k;
+        int c = 0;
+        for (; c + 8 <= C; c += 8) {
+            float dv[8], wv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) { dv[u] = d[c + u]; wv[u] = w[(int64_t)(c + u) * H2]; }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc += dv[u] * wv[u];
+        }
+        for (; c < C; ++c) acc += d[c] * w[(int64_t)c * H2];
+    }
     L.dh2[t] = acc;
 }
 
@@ -351,49 +378,64 @@ __device__ void bn1d_relu_bwd_col(float* dh, const float* h, const float* xh, in
     for (int b = 0; b < B; ++b) dh[b * ldz + j] = k1 * dh[b * ldz + j] - k2 - k3 * xh[b * ldz + j];
 }
 
-__global__ __launch_bounds__(256) void k_film_hidden_bwd(FilmLayer L, const float* __restrict__ camn, int B) {
+// layer 2: dh2 -> dz2 (in place) through BN1d + ReLU, fc2 bias gradient
+__global__ __launch_bounds__(H2) void k_film_l2_bwd(FilmLayer L, int B) {
     const int j = threadIdx.x;
-    const bool bn = B > 1;
-    // layer 2: dh2 -> dz2 (in place), fc2 grads
-    bn1d_relu_bwd_col(L.dh2, L.h2, L.xh2, H2, j, B, bn, L.g2, L.is2, L.gg2, L.gbe2);
-    {
-        float db = 0.f;
-        for (int b = 0; b < B; ++b) db += L.dh2[b * H2 + j];
-        L.gb2[j] = db;
-        for (int k = 0; k < H1; ++k) {
-            float acc = 0.f;
-            for (int b = 0; b < B; ++b) acc += L.dh2[b * H2 + j] * L.h1[b * H1 + k];
-            L.gw2[j * H1 + k] = acc;
+    bn1d_relu_bwd_col(L.dh2, L.h2, L.xh2, H2, j, B, B > 1, L.g2, L.is2, L.gg2, L.gbe2);
+    float db = 0.f;
+    for (int b = 0; b < B; ++b) db += L.dh2[b * H2 + j];
+    L.gb2[j] = db;
+}
+
+// fc2 weight gradient gw2[j][k] = Σ_b dz2[b][j] h1[b][k]: one thread per weight (k fastest)
+__global__ __launch_bounds__(256) void k_film_gw2(FilmLayer L, int B) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= H2 * H1) return;
+    const int j = t / H1, k = t - j * H1;
+    float acc = 0.f;
+    for (int b = 0; b < B; ++b) acc += L.dh2[b * H2 + j] * L.h1[b * H1 + k];
+    L.gw2[t] = acc;
+}
+
+// layer 1: dh1[b][j] = Σ_jj dz2[b][jj] W2[jj][j] (thread (j, q) for the samples b = q mod 8), then
+// BN1d + ReLU backward and the fc1 gradients per column
+__global__ __launch_bounds__(1024) void k_film_l1_bwd(FilmLayer L, const float* __restrict__ camn, int B) {
+    const int j = threadIdx.x & (H1 - 1), q = threadIdx.x / H1;
+    for (int b0 = q; b0 < B; b0 += 32) {
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int jj = 0; jj < H2; ++jj) {
+            const float w = L.w2[jj * H1 + j];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (b0 + 8 * u < B) acc[u] += L.dh2[(b0 + 8 * u) * H2 + jj] * w;
         }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (b0 + 8 * u < B) L.dh1[(b0 + 8 * u) * H1 + j] = acc[u];
     }
     __syncthreads();
-    // layer 1: dh1[b][k] = Σ_j dz2[b][j] W2[j][k] -> dz1, fc1 grads
-    if (j < H1) {
-        for (int b = 0; b < B; ++b) {
-            float acc = 0.f;
-            for (int jj = 0; jj < H2; ++jj) acc += L.dh2[b * H2 + jj] * L.w2[jj * H1 + j];
-            L.dh1[b * H1 + j] = acc;
-        }
-        bn1d_relu_bwd_col(L.dh1, L.h1, L.xh1, H1, j, B, bn, L.g1, L.is1, L.gg1, L.gbe1);
-        float db = 0.f;
-        float dw[4] = {0.f, 0.f, 0.f, 0.f};
-        for (int b = 0; b < B; ++b) {
-            const float d = L.dh1[b * H1 + j];
-            db += d;
+    if (q != 0) return;
+    bn1d_relu_bwd_col(L.dh1, L.h1, L.xh1, H1, j, B, B > 1, L.g1, L.is1, L.gg1, L.gbe1);
+    float db = 0.f;
+    float dw[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < B; ++b) {
+        const float d = L.dh1[b * H1 + j];
+        db += d;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) dw[k] += d * camn[b * 4 + k];
-        }
-        L.gb1[j] = db;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) L.gw1[j * 4 + k] = dw[k];
+        for (int k = 0; k < 4; ++k) dw[k] += d * camn[b * 4 + k];
     }
+    L.gb1[j] = db;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) L.gw1[j * 4 + k] = dw[k];
 }
 
 void film_mlp_bwd(const FilmLayer& L, const float* camn, int B, hipStream_t st) {
     const int64_t nw = (int64_t)2 * L.C * (H2 + 1);
     hipLaunchKernelGGL(k_film_head_bwd_w, dim3(cdiv(nw, 256)), dim3(256), 0, st, L, B);
     hipLaunchKernelGGL(k_film_dh2, dim3(cdiv((int64_t)B * H2, 256)), dim3(256), 0, st, L, B);
-    hipLaunchKernelGGL(k_film_hidden_bwd, dim3(1), dim3(H2), 0, st, L, camn, B);
+    hipLaunchKernelGGL(k_film_l2_bwd, dim3(1), dim3(H2), 0, st, L, B);
+    hipLaunchKernelGGL(k_film_gw2, dim3(cdiv(H2 * H1, 256)), dim3(256), 0, st, L, B);
+    hipLaunchKernelGGL(k_film_l1_bwd, dim3(1), dim3(8 * H1), 0, st, L, camn, B);
 }
 
 }  // namespace cad

@@ -205,9 +205,10 @@ struct FilmLayer {
 };
 void film_mlp_fwd(const FilmLayer& L, const float* camn, int B, bool train, hipStream_t st);
 void film_mlp_bwd(const FilmLayer& L, const float* camn, int B, hipStream_t st);
-// a1 = gam[b,c] * relu(y*scale[c] + shift[c]) + bet[b,c]   (NHWC [B*HW][C])
+// a1 = gam[b,c] * relu(y*scale[c] + shift[c]) + bet[b,c]   (NHWC [B*HW][C]); out (fp32, may be null)
+// and / or os (its bf16 twin, rows of C; the B1 engine's operand)
 void film_apply(const float* y, int C, const float* scale, const float* shift, const float* gam, const float* bet,
-                int B, int64_t HW, float* out, hipStream_t st, bool y_bf16 = false);
+                int B, int64_t HW, float* out, hipStream_t st, bool y_bf16 = false, void* os = nullptr);
 // dgam[b,c] = sum_hw dA * relu(y*scale+shift), dbet[b,c] = sum_hw dA
 void film_affine_bwd(const float* dA, const float* y, int C, const float* scale, const float* shift, int B, int64_t HW,
                      double* scratch, float* dgam, float* dbet, hipStream_t st, bool y_bf16 = false);

@@ -383,7 +383,7 @@ int cad_loader_next(cad_loader* L, float* rgb, float* depth, float* K, void* str
  *  "enc<l>.y1|a1|y2", "dec<l>.y1|a1|y2"); numel = rows*channels of the last forward's batch.
  * Returns the element count (host may be NULL to query), or -1 for an unknown name — and, on the
  * bf16 engine (pre-split operands), for the buffers whose fp32 copy that path does not write
- * ("Sb", "bott", "pool<l>", "dout1..3", the a1 of non-FiLM blocks); cad_last_error() says which. */
+ * ("Sb", "bott", "pool<l>", "dout1..3", every block's a1); cad_last_error() says which. */
 int64_t cad_unet_debug_buffer(cad_unet* h, const char* name, float* host, int64_t numel);
 
 /* ---- launch profiler: HIP events around every MFMA GEMM launch on its own stream ---- */

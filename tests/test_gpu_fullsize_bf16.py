@@ -24,8 +24,9 @@ pixels that cancel 50-2000x — off by up to 27%).  So the oracle runs LAYER-WIS
 intermediate decisions: every 3x3 convolution's stored bf16 output (cad_oracle.Y_FORCE), every ReLU
 decision (RELU_FORCE) and every FiLM modulation (FILM_FORCE) are imposed, and each of them is judged
 on its own first:
-  * every convolution's own output on the identical inputs within 1 bf16 ulp of the GPU's (fraction
-    differing < 1e-3), the FiLM gamma / beta reported against the oracle's own;
+  * every convolution's own output on the identical inputs within 1 bf16 ulp of the GPU's (values
+    below 2^-10 of the layer's largest: within that level's spacing; fraction differing < 5e-3), the
+    FiLM gamma / beta reported against the oracle's own;
 then the whole step (BN, ReLU masks, FiLM, pool, ConvT, head, 4-term loss, backward, clip, Adam):
   * prediction bulk (99.9th percentile of |ours - oracle| / max|oracle|) < 1e-5, max < 1e-4;
     dL/dpred bulk < 1e-5, max < 1e-2 (the gradient-matching term is an L1 norm whose sign flips with
@@ -214,8 +215,11 @@ def test_bs32_480x640_bf16_step_vs_oracle(cad, dev, oracle, bf16_engine, beat, m
     del relu
     # every convolution judged on identical inputs (conv outputs, ReLU decisions and FiLM modulation
     # imposed): its own output vs the GPU's stored one, in units of the bf16 spacing of the larger of
-    # the two (2^(e-7) for |y| in [2^e, 2^(e+1))), floored at 2^-20 of the layer's largest |y| (the
-    # fp32 accumulation error of a sum that cancels to ~0, below which bf16 spacing means nothing);
+    # the two (2^(e-7) for |y| in [2^e, 2^(e+1))), floored at the spacing of 2^-10 of the layer's
+    # largest |y|: a sum that cancels to ~0 carries the fp32 accumulation error of its 576-4608 terms
+    # (~sqrt(K) 2^-24 of their size, measured up to 3.6e-6 of the layer's max), far above its own bf16
+    # spacing.  A rounded value that sits within that accumulation error of a bf16 rounding boundary
+    # flips on either side: ~1e-3 of the values (measured 1.5e-3 at most), so the fraction bound is 5e-3.
     # enc1.conv1 of the baseline (3-channel image, in-loader kernel) stores fp32
     for n, (fg, fb) in ff.items():
         beat(f"{model}: FiLM {n} gamma/beta vs the oracle's own: "
@@ -228,7 +232,7 @@ def test_bs32_480x640_bf16_step_vs_oracle(cad, dev, oracle, bf16_engine, beat, m
         if model == "baseline" and n == "enc1.conv1":
             rows.append((d.max().item() / gy.abs().max().item(), 0.0, n))
             continue
-        big = torch.maximum(gy.double().abs(), own.double().abs()).clamp_min(2.0 ** -20 * gy.abs().max().item())
+        big = torch.maximum(gy.double().abs(), own.double().abs()).clamp_min(2.0 ** -10 * gy.abs().max().item())
         ulp = torch.exp2(torch.floor(torch.log2(big)) - 7)
         rows.append(((d / ulp).max().item(), (d > 0).double().mean().item(), n))
         del own, d, ulp, big
@@ -237,7 +241,7 @@ def test_bs32_480x640_bf16_step_vs_oracle(cad, dev, oracle, bf16_engine, beat, m
     rows.sort(reverse=True)
     beat(f"{model}: conv outputs on identical inputs (max |own - gpu| in bf16 ulps, fraction differing, name): "
          f"{rows[:5]}")
-    bad = [] if all(x[0] <= 1.0 and x[1] < 1e-3 for x in rows) else [("conv outputs", False, rows[:5])]
+    bad = [] if all(x[0] <= 1.0 and x[1] < 5e-3 for x in rows) else [("conv outputs", False, rows[:5])]
     beat(f"{model}: oracle step done (loss {r['loss']:.6f})")
     bad += _judge(beat, g, r, g_grads, g_norm, g_params, {k: v for k, v in g_bufs.items() if "running" in k},
                   ref.p, ref.bufs, oracle.param_spec(F, model=model), params)
