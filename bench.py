@@ -40,6 +40,8 @@ FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 = 
 # (1024 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz = 2516.6 TFLOP/s dense bf16), so its fp32-equivalent
 # ceiling is 2516.6 / 6.
 BF16_MFMA_PEAK_TFLOPS = 2516.6
+# block-scaled MXFP8 (v_mfma_scale_f32_32x32x64_f8f6f4 with E4M3 operands): 2x the bf16 rate
+MX8_MFMA_PEAK_TFLOPS = 2 * BF16_MFMA_PEAK_TFLOPS
 S3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6.0
 HBM_PEAK_GBS = 8000.0
 FLOP_PER_IMAGE_480x640_F64 = 1.353646e12   # fwd + dgrad + wgrad
@@ -259,13 +261,18 @@ def roofline_of(prof, steps, ms_per_step, show=False):
     kname = re.search(r"(k_\w+)", dom["name"]).group(1)
     s3 = kname.endswith("_s3")
     b1 = kname.endswith(("_bf16", "_bf16p", "_bf16p4"))
-    peak = S3_PEAK_TFLOPS if s3 else BF16_MFMA_PEAK_TFLOPS if b1 else FP32_MFMA_PEAK_TFLOPS
+    x8 = kname.endswith("_x8")
+    peak = (S3_PEAK_TFLOPS if s3 else BF16_MFMA_PEAK_TFLOPS if b1 else MX8_MFMA_PEAK_TFLOPS if x8
+            else FP32_MFMA_PEAK_TFLOPS)
     roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": round(peak, 1), "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": pmc_traffic(dom["name"]),
             "arith": ("fp32 via exact 3-way bf16 split, 6 bf16 MFMA products per fp32 MAC: peak = dense "
                       "bf16 MFMA 2516.6 / 6; achieved counts algorithmic fp32 FLOPs") if s3 else
                      ("bf16 operands, fp32 accumulation (v_mfma_f32_32x32x16_bf16): peak = dense bf16 MFMA")
-                     if b1 else "fp32 MFMA (v_mfma_f32_32x32x2_f32)",
+                     if b1 else
+                     ("MXFP8 E4M3 operands, one E8M0 scale per 32 k, fp32 accumulation "
+                      "(v_mfma_scale_f32_32x32x64_f8f6f4): peak = 2 x dense bf16") if x8 else
+                     "fp32 MFMA (v_mfma_f32_32x32x2_f32)",
             "kernel": dom["name"], "launches_per_step": dom["launches"] // steps,
             "avg_launch_ms": round(dom["ms"] / dom["launches"], 4),
             "gflop_per_launch": round(dom["gflop"] / dom["launches"], 3)}
@@ -337,12 +344,13 @@ def resunet_macs_per_image(H=480, W=640):
     return stem + macs, macs
 
 
-def extra_leg_resunet(cad, lib, dev, steps=10, warmup=3, B=32, H=480, W=640):
+def extra_leg_resunet(cad, lib, dev, steps=10, warmup=3, B=32, H=480, W=640, fp8=False):
     """configs[4]'s per-GPU step: ResNet-50 encoder + U-Net decoder (resunet.cpp), bs32 480x640, full
-    loss, bf16 contraction operands (the fp8 conv-GEMM the config names is not built: DESIGN.md §9)."""
+    loss, bf16 contraction operands; fp8=True: the forward conv-GEMMs on MXFP8 E4M3 operands
+    (cad_resunet_set_fp8, the "fp8 MFMA conv-GEMM" configs[4] names)."""
     import torch
     from cad_amd import synthetic
-    model = cad.ResNetUNet(batch=B, height=H, width=W, device=dev.index)
+    model = cad.ResNetUNet(batch=B, height=H, width=W, device=dev.index, fp8=fp8)
     loss = cad.CombinedDepthLoss(1.0, 0.1, 0.001, 0.01, batch=B, height=H, width=W, device=dev.index)
     rgb, gt, K = (t.to(dev) for t in synthetic.device_batch(B, H, W, "cpu"))
     pred = torch.empty((B, 1, H, W), device=dev)
@@ -358,15 +366,18 @@ def extra_leg_resunet(cad, lib, dev, steps=10, warmup=3, B=32, H=480, W=640):
         dt = time.perf_counter() - t0
     last = loss5[0].item()
     params = model.count_parameters()
+    model_fp8_units = model.fp8_units if fp8 else 0
     del model, loss
     torch.cuda.empty_cache()
     value = B * steps / dt
     fwd, with_dgrad = resunet_macs_per_image(H, W)
     flop_img = 2 * (2 * fwd + with_dgrad)   # forward + wgrad of every conv, dgrad of all but the stem
     return {"workload": "ResNet-50 encoder + U-Net decoder train step, configs[4] per-GPU: bs32 480x640, "
-                        "bf16 GEMM operands (fp8 not built), full loss",
+                        + ("forward conv-GEMMs on MXFP8 E4M3 operands (backward bf16)" if fp8 else
+                           "bf16 GEMM operands") + ", full loss",
+            "fp8_units": model_fp8_units,
             "value": round(value, 3), "unit": "images/s", "ms_per_step": round(1e3 * dt / steps, 3), "steps": steps,
-            "warmup": warmup, "dtype": "bf16", "params": params, "last_loss": last,
+            "warmup": warmup, "dtype": "fp8+bf16" if fp8 else "bf16", "params": params, "last_loss": last,
             "gflop_per_image": round(flop_img / 1e9, 2),
             "mfma_frac_dense_bf16": round(flop_img * value / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4),
             "roofline": roofline_of(prof(), steps, 1e3 * dt / steps)}
@@ -557,11 +568,12 @@ def main():
                     log(f"extra leg config {cfg}: {extra[f'config{cfg}']}")
                 except Exception as e:
                     log(f"extra leg config {cfg} failed: {e}")
-            try:
-                extra["config5"] = extra_leg_resunet(cad, lib, dev)
-                log(f"extra leg config 5: {extra['config5']}")
-            except Exception as e:
-                log(f"extra leg config 5 failed: {e}")
+            for key, fp8 in (("config5", False), ("config5_fp8", True)):
+                try:
+                    extra[key] = extra_leg_resunet(cad, lib, dev, fp8=fp8)
+                    log(f"extra leg {key}: {extra[key]}")
+                except Exception as e:
+                    log(f"extra leg {key} failed: {e}")
             try:
                 extra["geometry"] = extra_leg_geonet(cad, lib, dev)
                 log(f"extra leg geometry-aware network: {extra['geometry']}")

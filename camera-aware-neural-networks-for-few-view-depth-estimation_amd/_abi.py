@@ -70,6 +70,8 @@ SIGNATURES = {
     "cad_resunet_get_tensor": (I, [P, I, I, FP, I64]),
     "cad_resunet_get_grad": (I, [P, I, FP, I64]),
     "cad_resunet_train": (I, [P, I]),
+    "cad_resunet_set_fp8": (I, [P, I]),
+    "cad_resunet_fp8_units": (I, [P]),
     "cad_resunet_flat": (I, [P, C.POINTER(P), C.POINTER(P), I64P]),
     "cad_resunet_forward": (I, [P, P, P, I, P]),
     "cad_resunet_backward": (I, [P, P, P]),
@@ -146,6 +148,9 @@ SIGNATURES = {
     "cad_op_conv3x3_dgrad": (I, [P, I, P, I, P, I64, I, I, I, P]),
     "cad_op_conv3x3_wgrad": (I, [P, I, P, I64, I, I, P, I, I, I, P]),
     "cad_op_conv3x3_wgrad_bf16": (I, [P, I64, I, P, I64, I, I, P, I, I, I, P]),
+    "cad_op_mx8_quantize": (I, [P, I, I64, I, I, I64, P, P, I64, I, P]),
+    "cad_op_dense_x8": (I, [P, P, I64, I, P, P, I64, I, P, I64, P]),
+    "cad_op_conv3x3_x8": (I, [P, P, I64, I, P, P, I64, I, P, I, I, I, P]),
     "cad_op_convT_fwd": (I, [P, I, P, P, I, P, I64, I, I, I, I, P]),
     "cad_op_convT_dgrad": (I, [P, I64, I, I, P, I, P, I, I, I, P]),
     "cad_op_convT_wgrad": (I, [P, I, P, I64, I, I, P, I, I, I, P]),

@@ -1649,6 +1649,38 @@ cad_status cad_op_conv3x3_wgrad_bf16(const void* dz, int64_t lddz, int cout, con
         HIPCHK(hipGetLastError());
     });
 }
+cad_status cad_op_mx8_quantize(const void* src, int src_bf16, int64_t lds, int scoff, int C, int64_t M, void* q,
+                               void* s, int64_t ldq, int qcoff, void* stream) {
+    return guard([&] {
+        require(src && q && s && M >= 0, "null argument");
+        cad::Mx8 d;
+        d.q = q; d.s = s; d.ld = ldq; d.coff = qcoff;
+        cad::mx8_quantize(src, src_bf16 != 0, lds, scoff, C, M, d, S(stream));
+        HIPCHK(hipGetLastError());
+    });
+}
+cad_status cad_op_dense_x8(const void* xq, const void* xs, int64_t ldx, int K, const void* wq, const void* ws,
+                           int64_t ldw, int N, float* y, int64_t M, void* stream) {
+    return guard([&] {
+        require(cad::dense_x8_ok(K, N), "dense MX-fp8 GEMM: K % 128 == 0 and N % 64 == 0 required");
+        cad::Mx8 x, w;
+        x.q = xq; x.s = xs; x.ld = ldx;
+        w.q = wq; w.s = ws; w.ld = ldw;
+        cad::dense_fwd_x8(x, K, w, N, y, N, 0, M, nullptr, S(stream));
+        HIPCHK(hipGetLastError());
+    });
+}
+cad_status cad_op_conv3x3_x8(const void* xq, const void* xs, int64_t ldx, int cin, const void* wq, const void* ws,
+                             int64_t ldw, int cout, float* y, int B, int H, int W, void* stream) {
+    return guard([&] {
+        require(cad::conv3x3_x8_ok(cin, W, cout), "MX-fp8 window conv: cin % 64, cout % 64, a block width dividing W");
+        cad::Mx8 x, w;
+        x.q = xq; x.s = xs; x.ld = ldx;
+        w.q = wq; w.s = ws; w.ld = ldw;
+        cad::conv3x3_fwd_x8(x, cin, w, cout, y, cout, 0, B, H, W, nullptr, S(stream));
+        HIPCHK(hipGetLastError());
+    });
+}
 cad_status cad_op_convT_fwd(const float* x, int cin, const float* w, const float* bias, int cout, float* y,
                             int64_t ldy, int ycoff, int B, int H, int W, void* stream) {
     return guard([&] {

@@ -123,6 +123,10 @@ struct RConv {
     void *ws = nullptr;        // forward weight twin [cout][Kp]
     void *wts = nullptr;       // dgrad twin: window [cin][9][cout] repack, else W^T [Kp][cout]
     float* wd = nullptr;       // fp32 repack scratch of the window dgrad
+    // MX-fp8 forward (cad_resunet_set_fp8): eligible contractions read MXFP8 operands
+    bool x8 = false;
+    uint8_t *wq = nullptr, *wsc = nullptr;   // forward weights [cout][ldq] e4m3 + [cout][ldq / 32] e8m0
+    int64_t ldq = 0;
 };
 struct Unit {   // conv + BN (+ its pre-BN output y)
     RConv c;
@@ -159,6 +163,9 @@ struct cad_resunet {
     bool train = true;
     int fwd_B = 0;
     bool have_fwd = false;
+    bool fp8 = false;          // forward conv-GEMMs on MX-fp8 operands where eligible (x8 units)
+    uint8_t *xq = nullptr, *xsc = nullptr;   // MX scratch of the current contraction's A operand
+    int64_t xq_cap = 0;
     int64_t nbt = 0;
     std::vector<RParam> params;
     std::vector<RBuf> bufs;
@@ -282,6 +289,23 @@ void build(cad_resunet* h) {
     h->n_flat = (h->n_flat + 63) & ~int64_t(63);
 }
 
+inline int64_t up128(int64_t x) { return (x + 127) & ~int64_t(127); }
+
+// MX-fp8 eligibility of a forward contraction (input width Win): the window kernel for the 3x3
+// stride-1 convolutions, the dense GEMM for the 1x1 / im2col ones (K = Kp)
+bool x8_eligible(const RConv& c, int Win) {
+    if (c.win) return cad::conv3x3_x8_ok(c.cin, Win, c.cout);
+    return c.Kp % 32 == 0 && cad::dense_x8_ok(c.Kp, c.cout);
+}
+// rows and channels of the A operand the contraction reads (window: the input; dense: the input,
+// its stride-2 subsample or its im2col rows)
+void x8_operand_shape(const RConv& c, int B, int Hin, int Win, int64_t& rows, int& chans) {
+    const int Ho = (Hin + 2 * c.p - c.k) / c.s + 1, Wo = (Win + 2 * c.p - c.k) / c.s + 1;
+    if (c.win) { rows = (int64_t)B * Hin * Win; chans = c.cin; }
+    else if (c.k == 1) { rows = (int64_t)B * Ho * Wo; chans = c.cin; }
+    else { rows = (int64_t)B * Ho * Wo; chans = c.Kp; }
+}
+
 void bn_alloc(Arena& a, RBN& b) {
     b.rm = a.f(b.C); b.rv = a.f(b.C);
     b.mean = a.f(b.C); b.invstd = a.f(b.C); b.scale = a.f(b.C); b.shift = a.f(b.C); b.coef = a.f(3 * b.C);
@@ -305,8 +329,25 @@ void layout(cad_resunet* h, Arena& a) {
     h->norm_coef = a.f(4);
     const int H1 = (h->H - 1) / 2 + 1, W1 = (h->W - 1) / 2 + 1;
     const int64_t M0 = h->M(B, h->H, h->W), M1 = h->M(B, H1, W1);
-    int64_t maxMC = 0, maxRows2C = 0, maxCol = 0;
+    int64_t maxMC = 0, maxRows2C = 0, maxCol = 0, maxX8 = 0;
     auto track = [&](int64_t M, int C) { maxMC = std::max(maxMC, M * C); };
+    // MX-fp8 forward of a unit on a B x Hin x Win input: weights, A-operand scratch, BN partial rows
+    auto x8_prep = [&](Unit& u, int Hin, int Win) {
+        RConv& c = u.c;
+        c.x8 = x8_eligible(c, Win);
+        if (!c.x8) return;
+        c.ldq = up128(c.Kp);
+        c.wq = a.u8((int64_t)c.cout * c.ldq);
+        c.wsc = a.u8((int64_t)c.cout * (c.ldq >> 5));
+        int64_t rows = 0;
+        int chans = 0;
+        x8_operand_shape(c, B, Hin, Win, rows, chans);
+        maxX8 = std::max(maxX8, rows * up128(chans));
+        const int Ho = (Hin + 2 * c.p - c.k) / c.s + 1, Wo = (Win + 2 * c.p - c.k) / c.s + 1;
+        const int srows = c.win ? cad::conv3x3_x8_stats_rows(c.cin, B, Hin, Win, c.cout)
+                                : cad::dense_x8_stats_rows(h->M(B, Ho, Wo), c.cout);
+        maxRows2C = std::max<int64_t>(maxRows2C, (int64_t)srows * (2 * c.cout + 1));
+    };
     // stem
     h->x0 = a.f(M0 * 4);
     RConv& sc = h->stem.c;
@@ -329,6 +370,7 @@ void layout(cad_resunet* h, Arena& a) {
             if (u->c.pidx < 0) continue;
             conv_alloc(a, u->c);
             bn_alloc(a, u->b);
+            x8_prep(*u, u == &b.u3 ? b.Ho : b.H, u == &b.u3 ? b.Wo : b.W);
         }
         b.u1.y = a.f(Mi * b.w);
         b.t1s = a.tw(Mi * b.w);
@@ -365,6 +407,7 @@ void layout(cad_resunet* h, Arena& a) {
         for (Unit* u : {&d.u1, &d.u2}) {
             conv_alloc(a, u->c);
             bn_alloc(a, u->b);
+            x8_prep(*u, d.H, d.W);
             u->y = a.f(Md * d.C);
             maxRows2C = std::max<int64_t>(
                 maxRows2C, (int64_t)cad::conv3x3_stats_rows(u->c.cin, B, d.H, d.W, d.C, true) * (2 * d.C + 1));
@@ -385,6 +428,9 @@ void layout(cad_resunet* h, Arena& a) {
     h->dT = a.f(maxMC);
     h->dYs = a.tw(maxMC);
     h->dcol = a.f(std::max<int64_t>(maxCol, 1));
+    h->xq_cap = maxX8;
+    h->xq = a.u8(maxX8);
+    h->xsc = a.u8(maxX8 / 32);
     int64_t sl = 0;
     for (const RParam& p : h->params)
         if (p.kind == R_CONV) sl = std::max<int64_t>(sl, (int64_t)p.cout * p.Kp * 64);
@@ -490,7 +536,33 @@ void unit_fwd(cad_resunet* h, Unit& u, cad::Split in, int B, int Hin, int Win, v
     const int64_t Mo = h->M(B, Ho, Wo);
     float* stats = h->train ? h->stats : nullptr;
     int rows = 0;
-    if (c.win) {
+    if (h->fp8 && c.x8) {   // MX-fp8 operand (quantised from the bf16 twin), fp8 MFMA contraction
+        cad::Split a = in;
+        int64_t arows = 0;
+        int chans = 0;
+        x8_operand_shape(c, B, Hin, Win, arows, chans);
+        if (!c.win && c.s > 1) {
+            if (c.k == 1) {
+                cad::copy_twin(in, c.cin, B, Hin, Win, c.s, xs, c.cin, 0, st);
+                a = tw(xs, c.cin);
+            } else {
+                cad::im2col_ps(in, c.cin, B, Hin, Win, c.k, c.k, c.s, c.p, col, c.Kp, st);
+                a = tw(col, c.Kp);
+            }
+        }
+        cad::Mx8 xa, wa;
+        xa.q = h->xq; xa.s = h->xsc; xa.ld = up128(chans);
+        wa.q = c.wq; wa.s = c.wsc; wa.ld = c.ldq;
+        if (arows * xa.ld > h->xq_cap) throw RError(CAD_ERR_INVALID, "MX-fp8 scratch too small");
+        cad::mx8_quantize(a.p, true, a.ld, a.coff, chans, arows, xa, st);
+        if (c.win) {
+            cad::conv3x3_fwd_x8(xa, c.cin, wa, c.cout, u.y, c.cout, 0, B, Hin, Win, stats, st, true);
+            rows = cad::conv3x3_x8_stats_rows(c.cin, B, Hin, Win, c.cout);
+        } else {
+            cad::dense_fwd_x8(xa, c.Kp, wa, c.cout, u.y, c.cout, 0, Mo, stats, st, true);
+            rows = cad::dense_x8_stats_rows(Mo, c.cout);
+        }
+    } else if (c.win) {
         cad::conv3x3_fwd_ps(in, c.cin, tw(c.ws, c.Kp), c.cout, u.y, c.cout, 0, B, Hin, Win, stats, st, true);
         rows = cad::conv3x3_stats_rows(c.cin, B, Hin, Win, c.cout, true);
     } else {
@@ -516,7 +588,14 @@ void unit_fwd(cad_resunet* h, Unit& u, cad::Split in, int B, int Hin, int Win, v
 }
 
 void prep_weights_fwd(cad_resunet* h, hipStream_t st) {
-    auto sw = [&](RConv& c) { cad::split_rows(h->P(c.pidx), c.Kp, 0, c.Kp, c.cout, c.ws, c.Kp, 0, st); };
+    auto sw = [&](RConv& c) {
+        cad::split_rows(h->P(c.pidx), c.Kp, 0, c.Kp, c.cout, c.ws, c.Kp, 0, st);
+        if (h->fp8 && c.x8) {
+            cad::Mx8 d;
+            d.q = c.wq; d.s = c.wsc; d.ld = c.ldq;
+            cad::mx8_quantize(h->P(c.pidx), false, c.Kp, 0, c.Kp, c.cout, d, st);
+        }
+    };
     sw(h->stem.c);
     for (Bott& b : h->blocks)
         for (Unit* u : {&b.u1, &b.u2, &b.u3, &b.ud})
@@ -879,6 +958,23 @@ cad_status cad_resunet_get_grad(const cad_resunet* h, int idx, float* host, int6
 
 cad_status cad_resunet_train(cad_resunet* h, int train) {
     return rguard([&] { h->train = train != 0; });
+}
+
+cad_status cad_resunet_set_fp8(cad_resunet* h, int on) {
+    return rguard([&] {
+        need(h, "null network");
+        h->fp8 = on != 0;
+    });
+}
+
+int cad_resunet_fp8_units(const cad_resunet* h) {
+    if (!h) return -1;
+    int n = 0;
+    auto cnt = [&](const Unit& u) { n += u.c.pidx >= 0 && u.c.x8; };
+    cnt(h->stem);
+    for (const Bott& b : h->blocks) { cnt(b.u1); cnt(b.u2); cnt(b.u3); cnt(b.ud); }
+    for (const Dec& d : h->dec) { cnt(d.u1); cnt(d.u2); }
+    return n;
 }
 
 cad_status cad_resunet_flat(cad_resunet* h, float** params, float** grads, int64_t* n) {

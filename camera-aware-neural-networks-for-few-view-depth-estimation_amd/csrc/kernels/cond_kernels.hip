@@ -22,7 +22,9 @@ __global__ void k_rays(const float* __restrict__ K, int B, int H, int W, float* 
         const float x = ((float)u - k[2]) * fx_inv;
         const float y = ((float)v - k[5]) * fy_inv;
         const float z = 1.0f;
-        const float nrm = sqrtf(x * x + y * y + z * z);
+        // (x*x + y*y) + 1 with one rounding per operation, as the fp32 reference evaluates it (no FMA
+        // contraction: a contracted norm moves a ray by an fp32 ulp, which flips its bf16 rounding)
+        const float nrm = sqrtf(__fadd_rn(__fadd_rn(__fmul_rn(x, x), __fmul_rn(y, y)), z));
         float* o = rays + (int64_t)b * 3 * HW + p;
         o[0] = x / nrm;
         o[HW] = y / nrm;

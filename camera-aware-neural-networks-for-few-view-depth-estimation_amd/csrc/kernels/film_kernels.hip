@@ -69,7 +69,9 @@ __global__ void k_rgb_rays_to_nhwc8(const float* __restrict__ rgb, const float* 
         const float x = ((float)u - c[2]) * fx_inv;
         const float y = ((float)v - c[3]) * fy_inv;
         const float z = 1.0f;
-        const float nrm = sqrtf(x * x + y * y + z * z);
+        // (x*x + y*y) + 1 with one rounding per operation, as the fp32 reference evaluates it (no FMA
+        // contraction: a contracted norm moves a ray by an fp32 ulp, which flips its bf16 rounding)
+        const float nrm = sqrtf(__fadd_rn(__fadd_rn(__fmul_rn(x, x), __fmul_rn(y, y)), z));
         const float* s = rgb + b * 3 * HW + yx;
         float4* o = reinterpret_cast<float4*>(out + p * 8);
         o[0] = make_float4(s[0], s[HW], s[2 * HW], x / nrm);

@@ -76,6 +76,29 @@ int dense_stats_rows(int64_t M, int N);
 void dense_wgrad_ps(Split dz, int N, Split x, int K, float* dw, int64_t ldw, int64_t M, float* slab, int64_t slab_cap,
                     hipStream_t st);
 
+// ---- MX-fp8 operands (gemm_mx8.hpp, mx8_kernels.hip): OCP MXFP8 E4M3 with one E8M0 scale per 32
+// consecutive k elements, for the block-scaled MFMA.  q = element bytes [rows][ld], s = scale bytes
+// [rows][ld / 32]; ld % 128 == 0, coff % 64 == 0 (the config-5 network's forward contractions).
+struct Mx8 {
+    const void* q = nullptr;
+    const void* s = nullptr;
+    int64_t ld = 0;
+    int coff = 0;
+};
+// dst rows [coff, coff + C) = MX(src rows [scoff, scoff + C)), src fp32 (src_bf16 = false) or bf16
+// rows of lds elements; C % 32 == 0
+void mx8_quantize(const void* src, bool src_bf16, int64_t lds, int scoff, int C, int64_t M, Mx8 dst, hipStream_t st);
+// y[m][ycoff + n] = sum_k x[m][k] w[n][k] on MX operands (+ BN partials when stats); K % 128 == 0
+bool dense_x8_ok(int K, int N);
+void dense_fwd_x8(Mx8 x, int K, Mx8 w, int N, float* y, int64_t ldy, int ycoff, int64_t M, float* stats, hipStream_t st,
+                  bool y_bf16 = false);
+int dense_x8_stats_rows(int64_t M, int N);
+// window-tiled conv3x3 forward on MX operands; w rows [cout][9 cin] in (tap, ci) order
+bool conv3x3_x8_ok(int cin, int W, int N);
+void conv3x3_fwd_x8(Mx8 x, int cin, Mx8 w, int cout, float* y, int64_t ldy, int ycoff, int B, int H, int W,
+                    float* stats, hipStream_t st, bool y_bf16 = false);
+int conv3x3_x8_stats_rows(int cin, int B, int H, int W, int cout);
+
 // ---------------- config-5 network kernels (res_kernels.hip) ----------------
 // col[pix_out][k] bf16, k = (ky*KW + kx)*C + c, rows padded with zeros to Kp (% 8)
 void im2col_f32(const float* x, int64_t ldx, int xcoff, int C, int B, int H, int W, int KH, int KW, int S, int P,

@@ -543,7 +543,7 @@ class ResNetUNet:
     def _f(self, name):
         return getattr(self.lib, self._PREFIX + name)
 
-    def __init__(self, in_channels=3, max_depth=10.0, *, batch, height, width, device=0):
+    def __init__(self, in_channels=3, max_depth=10.0, *, batch, height, width, device=0, fp8=False):
         self.lib = _abi.load()
         self.device = torch.device("cuda", device)
         self.batch, self.height, self.width, self.max_depth = batch, height, width, max_depth
@@ -551,6 +551,19 @@ class ResNetUNet:
         h = C.c_void_p()
         check(self._f("create")(C.byref(desc), device, C.byref(h)), "cad_resunet_create")
         self._init_handle(h)
+        self.set_fp8(fp8)
+
+    def set_fp8(self, on=True):
+        """MX-fp8 forward conv-GEMMs (cad_resunet_set_fp8): every eligible forward contraction on OCP
+        MXFP8 E4M3 operands (one E8M0 scale per 32 channels); the backward stays on bf16 operands."""
+        check(self._f("set_fp8")(self.h, int(bool(on))), "cad_resunet_set_fp8")
+        self.fp8 = bool(on)
+        return self
+
+    @property
+    def fp8_units(self) -> int:
+        """number of convolutions whose forward runs on MX-fp8 operands when fp8 is on"""
+        return int(self._f("fp8_units")(self.h))
 
     def _init_handle(self, h):
         self.h = h

@@ -416,6 +416,21 @@ cad_status cad_op_convT_wgrad(const float* x, int cin, const float* g, int64_t l
 cad_status cad_op_maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float* out,
                               uint8_t* idx, void* stream);
 
+/* MX-fp8 operands (OCP MXFP8 E4M3, one E8M0 scale per 32 consecutive k; the config-5 network's forward
+ * conv-GEMMs, kernels.hpp Mx8): q = element bytes [rows][ldq], s = scale bytes [rows][ldq / 32],
+ * ldq % 128 == 0.  quantize: rows [qcoff, qcoff + C) of (q, s) from src rows [scoff, scoff + C)
+ * (fp32, or bf16 when src_bf16), C % 32 == 0. */
+cad_status cad_op_mx8_quantize(const void* src, int src_bf16, int64_t lds, int scoff, int C, int64_t M, void* q,
+                               void* s, int64_t ldq, int qcoff, void* stream);
+/* y[m][n] (fp32, dense [M][N]) = sum_k x[m][k] w[n][k] on MX operands; K % 128 == 0, N % 64 == 0 */
+cad_status cad_op_dense_x8(const void* xq, const void* xs, int64_t ldx, int K, const void* wq, const void* ws,
+                           int64_t ldw, int N, float* y, int64_t M, void* stream);
+/* y[pix][co] (fp32, dense [B*H*W][cout]) = conv3x3(x) on MX operands: x rows [pix][ldx] (cin channels),
+ * w rows [cout][ldw] in (tap, ci) order (ldw >= 9 cin); cin % 64, cout % 64 and a window block width
+ * dividing W (the window kernel), else CAD_ERR_INVALID */
+cad_status cad_op_conv3x3_x8(const void* xq, const void* xs, int64_t ldx, int cin, const void* wq, const void* ws,
+                             int64_t ldw, int cout, float* y, int B, int H, int W, void* stream);
+
 /* ---- config-5 network (BASELINE configs[4]): ResNet-50 encoder + U-Net decoder, bf16 operands ----
  * No reference counterpart: architecture in resunet.cpp / DESIGN.md §9;
  * torchvision ResNet-50 parameter names under "encoder.", decoder "dec4".."dec0", "out_conv".
@@ -438,6 +453,14 @@ cad_status cad_resunet_set_tensor(cad_resunet* h, int kind, int idx, const float
 cad_status cad_resunet_get_tensor(const cad_resunet* h, int kind, int idx, float* host, int64_t numel);
 cad_status cad_resunet_get_grad(const cad_resunet* h, int idx, float* host, int64_t numel);
 cad_status cad_resunet_train(cad_resunet* h, int train);
+/* MX-fp8 forward conv-GEMMs (configs[4] "bf16 with fp8 MFMA conv-GEMM"): on = 1 runs
+ * every eligible forward contraction (the 1x1 / im2col GEMMs with K % 128 == 0, the 3x3 window
+ * convolutions with cin % 64 == 0) on OCP MXFP8 E4M3 operands with one E8M0 scale per 32 channels
+ * (v_mfma_scale_f32_32x32x64_f8f6f4, fp32 accumulation); the stem, ConvTs, the backward (dgrad,
+ * wgrad) and everything else stay as on 0 (bf16 operands).  Default 0.  fp8_units: how many
+ * convolutions are eligible. */
+cad_status cad_resunet_set_fp8(cad_resunet* h, int on);
+int cad_resunet_fp8_units(const cad_resunet* h);
 cad_status cad_resunet_flat(cad_resunet* h, float** params, float** grads, int64_t* n);
 cad_status cad_resunet_forward(cad_resunet* h, const float* rgb, float* depth, int B, void* stream);
 cad_status cad_resunet_backward(cad_resunet* h, const float* ddepth, void* stream);

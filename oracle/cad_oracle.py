@@ -345,7 +345,7 @@ def _conv3x3(x, w, name=None):
 
 
 def _convT2x2(x, w, b):
-    if _GEMM["operands"] == "bf16":
+    if _GEMM["operands"] in ("bf16", "mx8"):   # (mx8: the config-5 fp8 network keeps its ConvTs on bf16)
         y = _RoundGradOperand.apply(F.conv_transpose2d(_RoundOperand.apply(x), _RoundOperand.apply(w), None, stride=2))
         return y + b.view(1, -1, 1, 1)
     return F.conv_transpose2d(x, w, b, stride=2)

@@ -10,8 +10,9 @@ blocks are made of, baseline_unet.h:83-102), parameter names and shapes are torc
 loss / clip / Adam are the U-Net oracle's (cad_oracle.py, pinned to the reference's fixtures).
 
 operands="bf16" rounds every contraction operand to bf16 (forward x and w, dgrad dy, wgrad dy) and the
-stored pre-BN conv outputs, as the GPU path does (cad_oracle._GEMM); "exact" is plain fp32 (or fp64
-with dtype=float64).
+stored pre-BN conv outputs, as the GPU path does (cad_oracle._GEMM); "mx8" is the fp8 network
+(cad_resunet_set_fp8): the eligible forward contractions on MXFP8 E4M3 operands (x8_eligible,
+mx8_quantize), everything else as "bf16"; "exact" is plain fp32 (or fp64 with dtype=float64).
 """
 from __future__ import annotations
 
@@ -82,14 +83,82 @@ def init(seed=0):
     return p, bufs
 
 
+# ---- MX-fp8 (OCP MXFP8 E4M3, gemm_mx8.hpp): the config-5 network's forward conv-GEMM operands ----
+def mx8_quantize(x):
+    """Quantise along the last dim in blocks of 32 (gemm_mx8.hpp mx8_quant_block): returns (e4m3 element
+    codes as uint8, e8m0 scale codes as uint8, the dequantised fp32 values).  shared exponent =
+    floor(log2 amax) (fp32 exponent field; 0 / subnormal blocks: -127) - 8, clamped to [-127, 127];
+    element = e4m3 round-to-nearest-even of clamp(v * 2^-shared, +-448)."""
+    v = x.float().reshape(*x.shape[:-1], x.shape[-1] // 32, 32)
+    amax = v.abs().amax(-1)
+    e = ((amax.view(torch.int32) >> 23) & 0xFF) - 127
+    sh = (e - 8).clamp(-127, 127)
+    one = torch.ones_like(amax)
+    inv = torch.ldexp(one, (-sh.clamp(max=126)).to(torch.int32))
+    q = (v * inv.unsqueeze(-1)).clamp(-448.0, 448.0).to(torch.float8_e4m3fn)
+    deq = (q.float().double() * torch.ldexp(one.double(), sh.to(torch.int32)).unsqueeze(-1)).float()
+    return q.view(torch.uint8).reshape(x.shape), (sh + 127).to(torch.uint8), deq.reshape(x.shape)
+
+
+def mx8_dequant(q, s):
+    """(element codes [.., K] uint8, scale codes [.., K/32] uint8) -> fp64 values"""
+    vals = q.view(torch.float8_e4m3fn).double().reshape(*q.shape[:-1], q.shape[-1] // 32, 32)
+    sc = torch.ldexp(torch.ones(s.shape, dtype=torch.float64), s.to(torch.int32) - 127)
+    return (vals * sc.unsqueeze(-1)).reshape(q.shape)
+
+
+def x8_eligible(k, stride, cin, cout, width):
+    """resunet.cpp x8_eligible: which forward contractions run on MX-fp8 operands (cin = the stored
+    input channels; width = the input width).  3x3 stride 1: the window kernel (mx8_kernels.hip
+    pick_win_x8: cin % 64, cout 64 with a 128/64 block width dividing W, or cout % 128 with 64/32/16/8);
+    other convolutions: the dense GEMM on K = k*k*cin (padded to 8) with K % 128 and cout % 64."""
+    if k == 3 and stride == 1 and cin % 8 == 0:
+        if cin % 64 or cout % 64:
+            return False
+        if cout == 64:
+            return width % 128 == 0 or width % 64 == 0
+        return cout % 128 == 0 and any(width % c == 0 for c in (64, 32, 16, 8))
+    kp = (k * k * cin + 7) // 8 * 8
+    return kp % 128 == 0 and cout % 64 == 0
+
+
+def _mx8_channels(t):
+    """MX-quantise-dequantise along dim 1 (channels; per (kh, kw) tap for a weight tensor)"""
+    return mx8_quantize(t.movedim(1, -1).contiguous())[2].to(t.dtype).movedim(-1, 1)
+
+
+class _X8Conv(torch.autograd.Function):
+    """The fp8 network's eligible convolutions (cad_resunet_set_fp8): forward on MX-fp8 operands — the
+    bf16 activation twin and the fp32 weights, each quantised along channels — and the backward on
+    bf16 operands (dgrad: bf16 w, wgrad: the bf16 twin x; the incoming dy is rounded by the caller)."""
+
+    @staticmethod
+    def forward(ctx, x, w, stride, pad):
+        xb = x.to(torch.bfloat16).to(x.dtype)
+        ctx.save_for_backward(xb, w.to(torch.bfloat16).to(w.dtype))
+        ctx.stride, ctx.pad = stride, pad
+        return F.conv2d(_mx8_channels(xb), _mx8_channels(w), None, stride, pad)
+
+    @staticmethod
+    def backward(ctx, g):
+        xb, wb = ctx.saved_tensors
+        gx = torch.nn.grad.conv2d_input(xb.shape, wb, g, ctx.stride, ctx.pad)
+        gw = torch.nn.grad.conv2d_weight(xb, wb.shape, g, ctx.stride, ctx.pad)
+        return gx, gw, None, None
+
+
 def _rnd(x):
-    return O._RoundOperand.apply(x) if O._GEMM["operands"] == "bf16" else x
+    return O._RoundOperand.apply(x) if O._GEMM["operands"] in ("bf16", "mx8") else x
 
 
 def _conv(x, w, stride, pad):
-    y = F.conv2d(_rnd(x), _rnd(w), None, stride, pad)
-    # bf16: the dy operand of dgrad / wgrad rounded, and the pre-BN output stored as bf16
-    return O._RoundOperand.apply(O._RoundGradOperand.apply(y)) if O._GEMM["operands"] == "bf16" else y
+    mode = O._GEMM["operands"]
+    if mode == "mx8" and x8_eligible(w.shape[2], stride, x.shape[1], w.shape[0], x.shape[3]):
+        y = _X8Conv.apply(x, w, stride, pad)
+    else:
+        y = F.conv2d(_rnd(x), _rnd(w), None, stride, pad)
+    # bf16 / mx8: the dy operand of dgrad / wgrad rounded, and the pre-BN output stored as bf16
+    return O._RoundOperand.apply(O._RoundGradOperand.apply(y)) if mode in ("bf16", "mx8") else y
 
 
 def _bottleneck(x, p, bufs, pre, stride, down, train):

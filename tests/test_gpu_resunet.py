@@ -102,13 +102,72 @@ def test_train_step_vs_oracle(cad, dev, oracle):
     assert max_rel_err(pe, pe_ref) < 5e-2
 
 
+def test_fp8_train_step_vs_oracle(cad, dev, oracle):
+    """cad_resunet_set_fp8: the eligible forward contractions on MXFP8 E4M3 operands (gemm_mx8.hpp),
+    the rest bf16.  Yardstick: resunet_oracle operands="mx8" (the same quantisation: bf16 twin -> MX
+    along channels, fp32 weights -> MX along channels per tap; bf16 backward) with fp32 and with fp64
+    accumulation; ours within 3x their spread of the fp64 one, as test_train_step_vs_oracle.  Then the
+    size of the fp8 effect itself: the fp8 step against the bf16 network's (reported, loosely bounded)."""
+    B, H, W = 2, 256, 256
+    p, b, m, rgb, gt, K = _setup(cad, oracle, B, H, W)
+    m.set_fp8(True)
+    assert m.fp8_units >= 30, m.fp8_units   # 1x1 / strided / window convolutions of the encoder and decoder
+    loss = cad.CombinedDepthLoss(*WEIGHTS, batch=B, height=H, width=W)
+    rg, gg, kg = rgb.to(dev), gt.to(dev), K.to(dev)
+    pred = m.forward(rg)
+    loss5, dpred = loss.forward_with_intrinsics(pred, gg, rg, kg)
+    m.backward(dpred)
+    torch.cuda.synchronize()
+    g_pred, g_loss = pred.cpu(), loss5.cpu()
+    grads = m.grads()
+    m.clip_grad_norm_(1.0)
+    m.adam_step(lr=1e-4, weight_decay=1e-5)
+    torch.cuda.synchronize()
+    g_norm = m.last_grad_norm()
+    after = m.named_parameters()
+    r = R.Trainer(p, b, WEIGHTS, operands="mx8").step(rgb, gt, K)
+    rx = R.Trainer(p, b, WEIGHTS, dtype=torch.float64, operands="mx8").step(rgb, gt, K)
+    e_pred, e_ref = max_rel_err(g_pred, rx["pred"]), max_rel_err(r["pred"], rx["pred"])
+    assert e_pred < max(1e-3, 3 * e_ref), (e_pred, e_ref)
+    e_loss, e_loss32 = abs(g_loss[0].item() - rx["loss"]) / abs(rx["loss"]), abs(r["loss"] - rx["loss"]) / abs(rx["loss"])
+    assert e_loss <= max(1e-4, 3 * e_loss32), (e_loss, e_loss32)
+    assert abs(g_norm - rx["norm"]) <= max(1e-3, 3 * abs(r["norm"] - rx["norm"]) / rx["norm"]) * rx["norm"]
+    cosf = lambda a, b: torch.nn.functional.cosine_similarity(a.double().reshape(1, -1), b.double().reshape(1, -1)).item()
+    flat = torch.cat([grads[n].reshape(-1) for n, _ in R.param_spec()])
+    cos_all = cosf(flat, torch.cat([g.reshape(-1) for g in rx["grads"]]))
+    cos_all32 = cosf(torch.cat([g.reshape(-1) for g in r["grads"]]), torch.cat([g.reshape(-1) for g in rx["grads"]]))
+    bad = []
+    for (n, _), g32, gx in zip(R.param_spec(), r["grads"], rx["grads"]):
+        ours = grads[n].double()
+        cos, cos32 = cosf(ours, gx), cosf(g32, gx)
+        e, e32 = max_rel_err(ours, gx), max_rel_err(g32, gx)
+        if not (cos > min(0.9999, 1 - 3 * (1 - cos32)) and e < max(1e-2, 3 * e32)):
+            bad.append((n, cos, cos32, e, e32))
+    # the fp8 effect: the same step on bf16 operands (the bf16 network's own yardstick)
+    rb = R.Trainer(p, b, WEIGHTS, dtype=torch.float64, operands="bf16").step(rgb, gt, K)
+    e_fp8 = max_rel_err(rx["pred"], rb["pred"])
+    print(f"\nfp8 network: pred err {e_pred:.3e} (emulation {e_ref:.3e}); loss {g_loss[0].item():.6f} vs "
+          f"{rx['loss']:.6f}; whole-gradient cosine {cos_all:.6f} (emulation {cos_all32:.6f}); fp8 vs bf16 "
+          f"operands: pred {e_fp8:.3e}, loss {rx['loss']:.6f} vs {rb['loss']:.6f}; units {m.fp8_units}")
+    assert not bad, bad[:5]
+    assert cos_all > min(0.99999, 1 - 3 * (1 - cos_all32)), (cos_all, cos_all32)
+    assert e_fp8 < 0.2 and abs(rx["loss"] - rb["loss"]) < 0.05 * abs(rb["loss"])
+    for n, v in after.items():
+        assert (v - p[n]).abs().max().item() <= 2e-4 + 1e-6, n
+    m.eval()   # eval forward on fp8 operands too
+    pe = m.forward(rg).cpu()
+    assert torch.isfinite(pe).all()
+
+
 def test_bench_shape_runs(cad, dev, oracle):
     B, H, W = 2, 480, 640
     m = cad.ResNetUNet(batch=B, height=H, width=W)
     loss = cad.CombinedDepthLoss(*WEIGHTS, batch=B, height=H, width=W)
     rgb, gt, K = [torch.from_numpy(a).to(dev) for a in oracle.synth_batch(B, H, W)]
-    for _ in range(2):
-        loss5, pred = m.train_step(loss, rgb, gt, K)
-    torch.cuda.synchronize()
-    assert torch.isfinite(loss5).all() and bool(((pred > 0) & (pred < 10)).all())
-    assert 0 < m.last_grad_norm() < 1e6
+    for fp8 in (False, True):
+        m.set_fp8(fp8)
+        for _ in range(2):
+            loss5, pred = m.train_step(loss, rgb, gt, K)
+        torch.cuda.synchronize()
+        assert torch.isfinite(loss5).all() and bool(((pred > 0) & (pred < 10)).all())
+        assert 0 < m.last_grad_norm() < 1e6

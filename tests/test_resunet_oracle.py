@@ -25,3 +25,40 @@ def test_forward_shapes_and_bf16_emulation():
     t16 = R.Trainer(p, b, operands="bf16").predict_eval(x)
     assert t32.shape == (2, 1, 64, 64) and bool(((t32 > 0) & (t32 < 10)).all())
     assert (t16 - t32).abs().max() / t32.abs().max() < 5e-2
+
+
+def test_mx8_quantize_known_answers():
+    """MXFP8 E4M3 (gemm_mx8.hpp): shared exponent floor(log2 amax) - 8, e4m3fn RNE elements saturated at
+    448; the GPU quantiser is held bit-exact to this function on the box (tests/test_gpu_mx8.py)."""
+    v = torch.zeros(4, 32)
+    v[0, 0] = 1.0                   # amax 1 -> scale 2^-8 (code 119); 1.0 -> 256 = e4m3 0x78
+    v[0, 1] = 1.0625                # 272: a tie between 256 and 288 -> even mantissa (256)
+    v[0, 2] = 1.0625 + 2 ** -20     # just above the tie -> 288 (0x79)
+    v[0, 3] = -0.5                  # 128 -> 0xF0
+    v[1, :] = 500.0                 # amax 500 -> scale 2^0; 500 saturates at 448 (0x7E)
+    v[2, 5] = 2.0 ** -40            # tiny block: shared exponent -48 (code 79), element 256
+    # v[3]: a zero block -> scale code 0 (2^-127), elements 0
+    q, s, d = R.mx8_quantize(v)
+    assert s[:, 0].tolist() == [119, 127, 79, 0]
+    assert q[0, :4].tolist() == [0x78, 0x78, 0x79, 0xF0]
+    assert q[1].unique().tolist() == [0x7E] and d[1, 0].item() == 448.0
+    assert q[2, 5].item() == 0x78 and d[2, 5].item() == 2.0 ** -40
+    assert q[3].abs().sum().item() == 0 and d[3].abs().sum().item() == 0
+    assert torch.equal(R.mx8_dequant(q, s).float(), d)
+
+
+def test_mx8_emulation_and_eligibility():
+    """operands="mx8" (the fp8 network, cad_resunet_set_fp8): the eligible forward contractions on MX
+    operands; at 480x640 that is every 1x1 / strided / window conv of the encoder and decoder except
+    the stem, the 64-wide layer-1 convolutions at W = 160 and the 32-channel dec0 block."""
+    assert R.x8_eligible(1, 1, 256, 64, 160) and R.x8_eligible(3, 2, 128, 128, 160)
+    assert not R.x8_eligible(1, 1, 64, 64, 160)      # K = 64 (< one 128-deep stage)
+    assert not R.x8_eligible(3, 1, 64, 64, 160)      # 256x64 window tiles need W % 64
+    assert R.x8_eligible(3, 1, 1536, 512, 40) and not R.x8_eligible(3, 1, 32, 32, 640)
+    assert not R.x8_eligible(7, 2, 4, 64, 640)       # stem: K = 196 -> 200
+    p, b = R.init(seed=3)
+    x = torch.rand(2, 3, 64, 64, generator=torch.Generator().manual_seed(1))
+    t16 = R.Trainer(p, b, operands="bf16").predict_eval(x)
+    t8 = R.Trainer(p, b, operands="mx8").predict_eval(x)
+    e = ((t8 - t16).abs().max() / t16.abs().max()).item()
+    assert 1e-6 < e < 0.2, e   # fp8 changes the result, boundedly
