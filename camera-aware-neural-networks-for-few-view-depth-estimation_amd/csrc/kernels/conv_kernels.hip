@@ -144,6 +144,9 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_win_bf16p4(GemmArgs a) {
 __global__ __launch_bounds__(256, 2) void k_conv3x3_wgrad_win_s3(GemmArgs a) { conv3x3_wgrad_win_body<3>(a); }
 template <int P>
 __global__ __launch_bounds__(256, 2) void k_conv3x3_wgrad_win_bf16p(GemmArgs a) { conv3x3_wgrad_win_ps_body<P>(a); }
+// ... with LDS-DMA staging (3-stage ring, conv3x3_wgrad_win_dma_body)
+template <int P>
+__global__ __launch_bounds__(256, 2) void k_conv3x3_wgrad_win_bf16d(GemmArgs a) { conv3x3_wgrad_win_dma_body<P>(a); }
 
 template <int WM, int WN, int KB, class Epi>
 __global__ __launch_bounds__(256) void k_conv3x3_fwd_bf16(GemmArgs a) { conv3x3_fwd_np<1, WM, WN, 2, 2, KB, Epi>(a); }
@@ -806,6 +809,15 @@ int wgrad_win_ps_stage(int cout, int cin, int W) {
         if (W % p == 0) return p;
     return 0;
 }
+// LDS-DMA weight-gradient kernel (k_conv3x3_wgrad_win_bf16d): default; CAD_WGDMA=0 selects the
+// register-staged one (A/B switch)
+bool wg_dma() {
+    static const bool on = [] {
+        const char* e = std::getenv("CAD_WGDMA");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 template <int P>
 void launch_wgrad_win_ps1(GemmArgs& a, float* dw, float* slab, int64_t slab_cap, hipStream_t st) {
     const int cin = a.b_cin;
@@ -826,10 +838,12 @@ void launch_wgrad_win_ps1(GemmArgs& a, float* dw, float* slab, int64_t slab_cap,
     a.ldc = a.N; a.slab_stride = per;
     a.C = s == 1 ? dw : slab;
     const dim3 grid(a.M / 64, cin / 64, s);
+    const bool dma = wg_dma();
     char name[96];
-    std::snprintf(name, sizeof name, "void cad::k_conv3x3_wgrad_win_bf16p<%d>(cad::GemmArgs)", P);
+    std::snprintf(name, sizeof name, "void cad::k_conv3x3_wgrad_win_bf16%c<%d>(cad::GemmArgs)", dma ? 'd' : 'p', P);
     if (prof_enabled()) prof_push(name, 2.0 * a.M * a.N * (double)a.K, st);
-    hipLaunchKernelGGL(k_conv3x3_wgrad_win_bf16p<P>, grid, dim3(256), 0, st, a);
+    if (dma) hipLaunchKernelGGL(k_conv3x3_wgrad_win_bf16d<P>, grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(k_conv3x3_wgrad_win_bf16p<P>, grid, dim3(256), 0, st, a);
     if (prof_enabled()) prof_pop(st);
     if (s > 1) finish_slabs(slab, s, per, dw, st);
 }

@@ -728,4 +728,190 @@ __device__ __forceinline__ void conv3x3_wgrad_win_ps_body(const GemmArgs& a) {
         }
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// B1 window weight gradient with LDS-DMA staging (round 3).  The decomposition of
+// conv3x3_wgrad_win_ps_body (64 co x 64 ci x 9 taps per workgroup, P-pixel stages of one image row),
+// but the operands travel global -> LDS by buffer_load ... lds (no staging registers, no ds_write):
+// one DMA wave-instruction moves 8 k-rows (pixels) x 128 B (64 channels) into a lane-linear LDS
+// image of unpadded 128-B k-rows.  Bank conflicts of the transposed fragment reads
+// (ds_read_b64_tr_b16: 4 consecutive k-rows x 64 B per 32-lane group; with 128-B rows, k-rows r and
+// r + 2 would share banks) are removed by swizzling on the SOURCE side: LDS 16-B chunk c of k-row kr
+// holds global chunk c ^ 4((kr >> 1) & 1), so any 4 consecutive k-rows cover disjoint bank ranges.
+// A ring of NBUF = 3 stages keeps two stages in flight: iteration kt waits (counted vmcnt) for stage
+// kt, passes ONE barrier (after which every wave has finished stage kt - 1, so its buffer is free),
+// issues the DMA of stage kt + 2 into that buffer and computes stage kt.  Out-of-image halo pixels
+// and the padding k-rows read past the buffer range: the DMA writes zeros for them.
+// Per stage (P = 32): 4 + 13 DMA wave-instructions (17 KB), 18 MFMAs per wave; LDS 3 x 17 KB.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int wgd_off(int kr, int byte) {   // LDS byte of (k-row, byte in the row)
+    return kr * 128 + ((((byte >> 4) ^ (((kr >> 1) & 1) << 2))) << 4) + (byte & 15);
+}
+__device__ __forceinline__ void wgd_frag(const char* s, int rb, int krow0, bf16x8& f) {
+    const int lane = threadIdx.x & 63;
+    const int g = (lane >> 4) & 1, h = lane >> 5, i = lane & 15;
+    const int krow = krow0 + 8 * h + (i >> 2);
+    const int byte = 2 * (rb + 16 * g + 4 * (i & 3));
+    typedef __attribute__((address_space(3))) v4i16 lds_v4;
+    const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(s + wgd_off(krow, byte)));
+    const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(s + wgd_off(krow + 4, byte)));
+    const uint2 ul = __builtin_bit_cast(uint2, lo), uh = __builtin_bit_cast(uint2, hi);
+    f = __builtin_bit_cast(bf16x8, make_uint4(ul.x, ul.y, uh.x, uh.y));
+}
+template <int P>
+struct WgdGeo {
+    static constexpr int KW = 3 * (P + 2);            // B window k-rows
+    static constexpr int NIA = P / 8;                 // DMA wave-instructions of A per stage
+    static constexpr int NIB = (KW + 7) / 8;          // ... of B
+    static constexpr int NI = NIA + NIB;
+    static constexpr int SLOTS = (NI + 3) / 4;        // per wave (wave w issues j = w, w + 4, ...)
+    static constexpr int WAIT = NI / 4;               // instructions every wave issues per stage
+    static constexpr int SA = P * 128, SB = NIB * 8 * 128, STAGE = SA + SB;
+    static constexpr int NBUF = 3;
+};
+
+// One LDS-DMA wave-instruction: buffer_load_dwordx4 ... lds (16 B per lane to M0 + 16 lane).  Issued
+// by inline asm so the compiler's wait-count pass does not see it: otherwise, unable to prove that the
+// fragment reads of the current ring slot do not alias the DMA's destination, it waits vmcnt(0)
+// before them and drains the ring; the kernel counts these loads itself (wgd_wait_barrier).
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+struct DmaRsrc {
+    i32x4_t d;
+};
+__device__ __forceinline__ DmaRsrc dma_rsrc(const void* base) {
+    const uint64_t a = reinterpret_cast<uint64_t>(base);
+    DmaRsrc r;
+    r.d[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+    r.d[1] = __builtin_amdgcn_readfirstlane((int)((uint32_t)(a >> 32) & 0xFFFF));
+    r.d[2] = (int)kRecords;
+    r.d[3] = 0x00020000;
+    return r;
+}
+__device__ __forceinline__ void dma16(const DmaRsrc& r, const void* lds_dst, uint32_t voff) {
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+        (uint32_t)reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) void*)lds_dst));
+    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(r.d), "s"(m0)
+                 : "memory", "m0");
+}
+
+template <int WAITN>
+__device__ __forceinline__ void wgd_wait_barrier() {
+    // the wave's DMAs of the stage about to be read have landed (at most WAITN newer ones pending),
+    // then every wave's: a raw barrier (a __syncthreads fence would drain the in-flight DMAs too)
+    if constexpr (WAITN == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(WAITN) : "memory");
+}
+
+template <int P>
+__device__ __forceinline__ void conv3x3_wgrad_win_dma_body(const GemmArgs& a) {
+    static_assert(P % 16 == 0, "stage");
+    using G = WgdGeo<P>;
+    __shared__ __attribute__((aligned(1024))) char lds[G::NBUF * G::STAGE];
+
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;   // (uniform: scalar branches)
+    const int cbk = wave & 1, cib = wave >> 1;
+    const TileId tile = xcd_tile();
+    const int co0 = tile.x * 64, ci0 = tile.y * 64;
+    const int H = a.H, W = a.W;
+    const int nst = a.K / P;
+    const int kbeg = tile.z * a.kstages_per_split;
+    const int kend = min(nst, kbeg + a.kstages_per_split);
+    const int segs = W / P;
+
+    const int64_t p0 = (int64_t)kbeg * P;
+    const int64_t pb = p0 - W - 1 > 0 ? p0 - W - 1 : 0;
+    const int rowA = (int)a.lda * 2, rowB = (int)a.ldb * 2;
+    const DmaRsrc rsa = dma_rsrc(ps_at(a.A, (p0 * a.lda + a.a_coff + co0) * 2));
+    const DmaRsrc rsb = dma_rsrc(ps_at(a.Bm, (pb * a.ldb + a.b_coff + ci0) * 2));
+
+    // this wave's DMA slots: instruction j = wave + 4 t; lane -> k-row 8 j' + lane / 8, LDS chunk lane % 8
+    const int lrow = lane >> 3, lch = lane & 7;
+    int sj[G::SLOTS];        // instruction index (or -1)
+    int soff[G::SLOTS];      // A: byte offset of the lane's piece from the stage's first pixel; B: relative window offset
+    int sky[G::SLOTS], skk[G::SLOTS];
+#pragma unroll
+    for (int t = 0; t < G::SLOTS; ++t) {
+        const int j = wave + 4 * t;
+        sj[t] = j < G::NI ? j : -1;
+        if (j < G::NIA) {
+            const int kr = 8 * j + lrow;
+            const int gch = lch ^ (((kr >> 1) & 1) << 2);
+            soff[t] = kr * rowA + gch * 16;
+            sky[t] = 0; skk[t] = 0;
+        } else {
+            const int kr = 8 * (j - G::NIA) + lrow;
+            const int gch = lch ^ (((kr >> 1) & 1) << 2);
+            const bool in = kr < G::KW;
+            sky[t] = in ? kr / (P + 2) : -(1 << 28);   // padding k-rows: never in range
+            skk[t] = in ? kr - (kr / (P + 2)) * (P + 2) : 0;
+            soff[t] = in ? ((sky[t] - 1) * W + skk[t] - 1) * rowB + gch * 16 : 0;
+        }
+    }
+    auto issue = [&](int stage, int buf) {   // DMA of stage `stage` (absolute) into ring slot buf
+        const int row = stage / segs;
+        const int sx0 = (stage - row * segs) * P, sy = row % H, sb = row / H;
+        const int64_t pix = ((int64_t)sb * H + sy) * W + sx0;
+        const uint32_t da = (uint32_t)((pix - p0) * rowA), db = (uint32_t)((pix - pb) * rowB);
+        char* base = lds + buf * G::STAGE;
+#pragma unroll
+        for (int t = 0; t < G::SLOTS; ++t) {
+            const int j = sj[t];
+            if (j < 0) continue;   // wave-uniform
+            if (j < G::NIA) {
+                dma16(rsa, base + j * 1024, da + (uint32_t)soff[t]);
+            } else {
+                const int yy = sy + sky[t] - 1, xx = sx0 + skk[t] - 1;
+                const bool ok = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+                dma16(rsb, base + G::SA + (j - G::NIA) * 1024, ok ? db + (uint32_t)soff[t] : kOOB);
+            }
+        }
+    };
+
+    floatx16 acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+    auto compute = [&](int buf) {
+        const char* sa = lds + buf * G::STAGE;
+        const char* sb = sa + G::SA;
+#pragma unroll
+        for (int q = 0; q < P / 16; ++q) {
+            bf16x8 fa;
+            wgd_frag(sa, cbk * 32, 16 * q, fa);
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                bf16x8 fb;
+                wgd_frag(sb, cib * 32, (t / 3) * (P + 2) + (t % 3) + 16 * q, fb);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, acc[t], 0, 0, 0);
+            }
+        }
+    };
+
+    if (kbeg < kend) issue(kbeg, 0);
+    if (kbeg + 1 < kend) issue(kbeg + 1, 1);
+    int buf = 0;
+    for (int kt = kbeg; kt < kend; ++kt) {
+        if (kt + 1 < kend) wgd_wait_barrier<G::WAIT>();   // stage kt landed; stage kt + 1 may still fly
+        else wgd_wait_barrier<0>();
+        if (kt + 2 < kend) issue(kt + 2, buf == 0 ? 2 : buf - 1);   // the slot of stage kt - 1
+        compute(buf);
+        buf = buf == 2 ? 0 : buf + 1;
+    }
+    // slab z: C[z][co][tap*cin + ci] (row stride a.ldc = 9*cin)
+    const int cin = a.b_cin;
+    float* dst = a.C + (int64_t)tile.z * a.slab_stride;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int n = t * cin + ci0 + cib * 32 + (lane & 31);
+            const int co = co0 + cbk * 32 + 4 * (lane >> 5) + 8 * g;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) dst[(int64_t)(co + q) * a.ldc + n] = acc[t][4 * g + q];
+        }
+}
+
 }  // namespace cad
