@@ -260,7 +260,7 @@ def roofline_of(prof, steps, ms_per_step, show=False):
     # k_<op>[_win]_<engine>[p]: engine s3 / bf16 / none (f32); p = pre-split operands
     kname = re.search(r"(k_\w+)", dom["name"]).group(1)
     s3 = kname.endswith("_s3")
-    b1 = kname.endswith(("_bf16", "_bf16p", "_bf16p4"))
+    b1 = kname.endswith(("_bf16", "_bf16p", "_bf16p4", "_bf16d"))
     x8 = kname.endswith("_x8")
     peak = (S3_PEAK_TFLOPS if s3 else BF16_MFMA_PEAK_TFLOPS if b1 else MX8_MFMA_PEAK_TFLOPS if x8
             else FP32_MFMA_PEAK_TFLOPS)

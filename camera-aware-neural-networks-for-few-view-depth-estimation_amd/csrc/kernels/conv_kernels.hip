@@ -140,13 +140,19 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_win_bf16p4(GemmArgs a) {
     conv3x3_win_ps_body<R, CW, BN64 ? 4 : 2, BN64 ? 1 : 2, Epi, 4>(a);
 }
 
+// ... the same tiles with LDS-DMA staging (conv3x3_win_dma_body: 3-stage ring, one workgroup per CU)
+template <int R, int CW, class Epi, bool BN64 = false>
+__global__ __launch_bounds__(256, 1) void k_conv3x3_win_bf16d(GemmArgs a) {
+    conv3x3_win_dma_body<R, CW, BN64 ? 4 : 2, BN64 ? 1 : 2, Epi, 4, 3>(a);
+}
+
 // window-tiled conv3x3 weight gradient (gemm_win.hpp): 64 co x 64 ci x 9 taps per workgroup, split-K
 __global__ __launch_bounds__(256, 2) void k_conv3x3_wgrad_win_s3(GemmArgs a) { conv3x3_wgrad_win_body<3>(a); }
 template <int P>
 __global__ __launch_bounds__(256, 2) void k_conv3x3_wgrad_win_bf16p(GemmArgs a) { conv3x3_wgrad_win_ps_body<P>(a); }
 // ... with LDS-DMA staging (3-stage ring, conv3x3_wgrad_win_dma_body)
-template <int P>
-__global__ __launch_bounds__(256, 2) void k_conv3x3_wgrad_win_bf16d(GemmArgs a) { conv3x3_wgrad_win_dma_body<P>(a); }
+template <int P, int NBUF>
+__global__ __launch_bounds__(256, 2) void k_conv3x3_wgrad_win_bf16d(GemmArgs a) { conv3x3_wgrad_win_dma_body<P, NBUF>(a); }
 
 template <int WM, int WN, int KB, class Epi>
 __global__ __launch_bounds__(256) void k_conv3x3_fwd_bf16(GemmArgs a) { conv3x3_fwd_np<1, WM, WN, 2, 2, KB, Epi>(a); }
@@ -433,6 +439,17 @@ WinPick pick_win(int cin, int W, int N) {
     return w;
 }
 int win_blocks(const WinPick& w, int B, int H, int W) { return B * cdiv(H, w.R) * (W / w.CW); }
+// B1 window conv forward / dgrad with LDS-DMA staging (k_conv3x3_win_bf16d): off by default —
+// measured on MI355X at the configs[3] shapes it runs 657-821 TFLOP/s against 894-1047 for the
+// register-staged k_conv3x3_win_bf16p4 (its 3-stage ring takes 132 KB of LDS: one workgroup and one
+// wave per SIMD, against two); CAD_WINDMA=1 selects it (A/B switch)
+bool win_dma() {
+    static const bool on = [] {
+        const char* e = std::getenv("CAD_WINDMA");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
 
 // PS = false: S3 window kernel (fp32 operands, in-loader split); true: B1 on the pre-split twins
 template <bool PS, int R, int CW, class Epi, bool BIG = false>
@@ -440,12 +457,13 @@ void launch_win1(const GemmArgs& a, hipStream_t st) {
     constexpr int BN = BIG ? (R * CW == 256 ? 128 : 64) : R * CW == 128 ? 128 : 64;
     const dim3 grid(win_blocks(WinPick{R, CW}, a.B, a.H, a.W), cdiv(a.N, BN));
     void (*fn)(GemmArgs);
-    if constexpr (BIG) fn = k_conv3x3_win_bf16p4<R, CW, Epi, BN == 64>;
+    const bool dma = BIG && win_dma();
+    if constexpr (BIG) fn = dma ? k_conv3x3_win_bf16d<R, CW, Epi, BN == 64> : k_conv3x3_win_bf16p4<R, CW, Epi, BN == 64>;
     else fn = PS ? (void (*)(GemmArgs))k_conv3x3_win_bf16p<R, CW, Epi> : (void (*)(GemmArgs))k_conv3x3_win_s3<R, CW, Epi>;
     if (prof_enabled()) {
         char name[160];
         snprintf(name, sizeof(name), "void cad::k_conv3x3_win_%s<%d, %d, cad::%s%s>(cad::GemmArgs)",
-                 BIG ? "bf16p4" : PS ? "bf16p" : "s3", R, CW, Epi::STATS ? "EpiStoreStats" : "EpiStore",
+                 dma ? "bf16d" : BIG ? "bf16p4" : PS ? "bf16p" : "s3", R, CW, Epi::STATS ? "EpiStoreStats" : "EpiStore",
                  Epi::BF16 ? "B16" : "");
         prof_push(name, 2.0 * a.M * a.N * (double)a.K, st);
         hipLaunchKernelGGL(fn, grid, dim3(256), 0, st, a);
@@ -805,18 +823,31 @@ constexpr bool g_no_wgwin = false;
 #endif
 int wgrad_win_ps_stage(int cout, int cin, int W) {
     if (cout % 64 || cin % 64) return 0;
-    for (int p : {CAD_WGWIN_P, 32, 16})
+    static const int pref = [] {
+        const char* e = std::getenv("CAD_WGP");   // A/B tuning: preferred stage width (64 | 32)
+        return (e && e[0] == '6') ? 64 : CAD_WGWIN_P;
+    }();
+    for (int p : {pref, 32, 16})
         if (W % p == 0) return p;
     return 0;
 }
-// LDS-DMA weight-gradient kernel (k_conv3x3_wgrad_win_bf16d): default; CAD_WGDMA=0 selects the
-// register-staged one (A/B switch)
+// LDS-DMA weight-gradient kernel (k_conv3x3_wgrad_win_bf16d): default (MI355X, configs[3] shapes:
+// 1016 vs 996 TFLOP/s at 32-pixel stages, 890 vs 830 at 16); CAD_WGDMA=0 selects the register-staged
+// one (A/B switch)
 bool wg_dma() {
     static const bool on = [] {
         const char* e = std::getenv("CAD_WGDMA");
         return !(e && e[0] == '0');
     }();
     return on;
+}
+// ring depth of the DMA kernel (CAD_WGBUF=2|3; A/B tuning switch)
+int wg_nbuf() {
+    static const int n = [] {
+        const char* e = std::getenv("CAD_WGBUF");
+        return (e && e[0] == '2') ? 2 : 3;
+    }();
+    return n;
 }
 template <int P>
 void launch_wgrad_win_ps1(GemmArgs& a, float* dw, float* slab, int64_t slab_cap, hipStream_t st) {
@@ -839,10 +870,13 @@ void launch_wgrad_win_ps1(GemmArgs& a, float* dw, float* slab, int64_t slab_cap,
     a.C = s == 1 ? dw : slab;
     const dim3 grid(a.M / 64, cin / 64, s);
     const bool dma = wg_dma();
+    const int nbuf = wg_nbuf();
     char name[96];
-    std::snprintf(name, sizeof name, "void cad::k_conv3x3_wgrad_win_bf16%c<%d>(cad::GemmArgs)", dma ? 'd' : 'p', P);
+    if (dma) std::snprintf(name, sizeof name, "void cad::k_conv3x3_wgrad_win_bf16d<%d, %d>(cad::GemmArgs)", P, nbuf);
+    else std::snprintf(name, sizeof name, "void cad::k_conv3x3_wgrad_win_bf16p<%d>(cad::GemmArgs)", P);
     if (prof_enabled()) prof_push(name, 2.0 * a.M * a.N * (double)a.K, st);
-    if (dma) hipLaunchKernelGGL(k_conv3x3_wgrad_win_bf16d<P>, grid, dim3(256), 0, st, a);
+    if (dma && nbuf == 2) hipLaunchKernelGGL((k_conv3x3_wgrad_win_bf16d<P, 2>), grid, dim3(256), 0, st, a);
+    else if (dma) hipLaunchKernelGGL((k_conv3x3_wgrad_win_bf16d<P, 3>), grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL(k_conv3x3_wgrad_win_bf16p<P>, grid, dim3(256), 0, st, a);
     if (prof_enabled()) prof_pop(st);
     if (s > 1) finish_slabs(slab, s, per, dw, st);
@@ -859,9 +893,7 @@ void conv3x3_wgrad_ps(Split dz, int cout, Split x, int cin, float* dw, int B, in
     a.Bm = (const float*)x.p; a.ldb = x.ld; a.b_coff = x.coff; a.b_cin = cin;
     if (!g_no_wgwin)
         switch (wgrad_win_ps_stage(cout, cin, W)) {
-#if CAD_WGWIN_P == 64
             case 64: launch_wgrad_win_ps1<64>(a, dw, slab, slab_cap, st); return;
-#endif
             case 32: launch_wgrad_win_ps1<32>(a, dw, slab, slab_cap, st); return;
             case 16: launch_wgrad_win_ps1<16>(a, dw, slab, slab_cap, st); return;
         }
