@@ -189,6 +189,9 @@ struct cad_unet {
     void* dcats[4] = {};          // up half of dcat, [M_l][C_l]
     void* dYs = nullptr;          // split dL/dz scratch (largest level)
     int fwd_np = 0;
+    // the last forward ran decoder level 0's bn2 + ReLU fused with the head (head_fusable): dout[0]
+    // was not written, the backward rebuilds the head's input gradient per row
+    bool head_fused = false;
     // backward
     float* dcat[4] = {};
     float *Sa = nullptr, *Sb = nullptr, *Sc = nullptr;
@@ -478,8 +481,11 @@ void split_weights(const cad_unet* h, hipStream_t st) {   // forward weights, ev
 // in_s / out_s: split twins of the block input / output (p == nullptr: none)
 // out_f32 = false: with pre-split GEMMs downstream only the output's twin is read (decoder outputs
 // above level 0, the bottleneck), so the fp32 output is not written
+// head_pred != nullptr: the block's bn2 + ReLU feeds the depth head directly (level-0 fusion): sig
+// and head_pred are written, out is not
 void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin, cad::Split in_s, int B, float* out,
-                     int64_t ldo, int ocoff, cad::Split out_s, hipStream_t st, bool out_f32 = true) {
+                     int64_t ldo, int ocoff, cad::Split out_s, hipStream_t st, bool out_f32 = true,
+                     float* head_pred = nullptr) {
     const int l = dc.level, Hh = h->Hl(l), Ww = h->Wl(l), C = dc.c1.cout;
     const int64_t M = h->Ml(l, B);
     const bool tr = h->train;
@@ -517,9 +523,23 @@ void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin,
     else
         cad::conv3x3_fwd(dc.a1, C, 0, C, h->P(dc.c2.pidx), C, dc.y2, C, 0, B, Hh, Ww, stats, st);
     bn(dc.b2, C, ps);
+    if (head_pred) {
+        cad::bn_relu_head_fwd(dc.y2, C, dc.b2.scale, dc.b2.shift, h->P(h->head_w), h->P(h->head_b), h->max_depth, h->sig,
+                              head_pred, M, st, dc.y2b);
+        return;
+    }
     const bool twin = ps && out_s.p;
     cad::bn_relu_fwd(dc.y2, C, dc.b2.scale, dc.b2.shift, (out_f32 || !twin) ? out : nullptr, ldo, ocoff, M, st,
                      twin ? const_cast<void*>(out_s.p) : nullptr, out_s.ld, out_s.coff, dc.y2b);
+}
+
+// CAD_HEADFUSE=0 keeps the unfused level-0 passes (A/B measurements)
+bool head_fusion_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("CAD_HEADFUSE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
 }
 
 void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth, int B, hipStream_t st) {
@@ -563,6 +583,7 @@ void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth
             double_conv_fwd(h, h->enc[4], h->pool[4], Cp, pin, B, h->a2_bott, h->Cl(4), 0, sv(h->botts, h->Cl(4)), st,
                             false);
     }
+    h->head_fused = head_fusion_on() && cad::head_fusable(f);
     for (int l = 3; l >= 0; --l) {
         const float* upin = l == 3 ? h->a2_bott : h->dout[l + 1];
         const void* upins = l == 3 ? h->botts : h->douts[l + 1];
@@ -576,9 +597,10 @@ void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth
                            h->Wl(l + 1), st);
         }
         double_conv_fwd(h, h->dec[l], h->cat[l], 2 * C, sv(h->cats[l], 2 * C), B, h->dout[l], C, 0,
-                        l > 0 ? sv(h->douts[l], C) : none, st, l == 0);
+                        l > 0 ? sv(h->douts[l], C) : none, st, l == 0, l == 0 && h->head_fused ? depth : nullptr);
     }
-    cad::head_fwd(h->dout[0], f, h->P(h->head_w), h->P(h->head_b), h->max_depth, h->sig, depth, h->Ml(0, B), st);
+    if (!h->head_fused)
+        cad::head_fwd(h->dout[0], f, h->P(h->head_w), h->P(h->head_b), h->max_depth, h->sig, depth, h->Ml(0, B), st);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -586,8 +608,10 @@ void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth
 // ------------------------------------------------------------------------------------------
 // g: grad wrt the DoubleConv output (ld ldg, channel offset gcoff); in: the block input (ld ldin,
 // cin channels; in_s its split twin); din: where conv1's dgrad goes (nullptr = not needed), ld lddin.
+// head != nullptr (level-0 fusion): g is null and bn2's upstream gradient is the head's, rebuilt per row.
 void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, int gcoff, const float* in,
-                     int64_t ldin, cad::Split in_s, int B, float* din, int64_t lddin, hipStream_t st) {
+                     int64_t ldin, cad::Split in_s, int B, float* din, int64_t lddin, hipStream_t st,
+                     const cad::HeadGrad* head = nullptr) {
     const int l = dc.level, Hh = h->Hl(l), Ww = h->Wl(l), C = dc.c1.cout;
     const int64_t M = h->Ml(l, B);
     const bool ps = h->fwd_np > 0 && h->fwd_np == cad::split_planes();
@@ -598,7 +622,7 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     // with pre-split GEMMs both consumers of dY2 read its twin: the fp32 dY2 is not written
     cad::bn_relu_bwd(g, ldg, gcoff, dc.y2, C, dc.b2.mean, dc.b2.invstd, dc.b2.scale, dc.b2.shift, h->P(dc.b2.widx), M,
                      h->dscr, dc.b2.coef, h->G(dc.b2.widx), h->G(dc.b2.bidx), ps ? nullptr : dY, st, nullptr, 1,
-                     ps ? dYs : nullptr, true, dc.y2b);
+                     ps ? dYs : nullptr, true, dc.y2b, head);
     // conv2: wgrad, dgrad
     if (ps) {
         cad::conv3x3_wgrad_ps(sv(dYs, C), C, sv(dc.a1s, C), C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
@@ -660,14 +684,23 @@ void backward_stage(cad_unet* h, int stage, const float* dpred, hipStream_t st) 
     const bool ps = h->fwd_np > 0 && h->fwd_np == cad::split_planes();
     if (stage == 0) {
         repack_dgrad_weights(h, st);
-        cad::head_bwd(h->dout[0], f, h->P(h->head_w), dpred, h->sig, h->max_depth, h->Sa, h->Ml(0, B), h->dscr,
-                      h->G(h->head_w), h->G(h->head_b), st);
+        if (h->head_fused) {   // head weight / bias gradient from dec1's bn2 input; its input gradient: stage 1
+            const DoubleConv& d = h->dec[0];
+            cad::head_bwd_y(d.y2, f, d.b2.scale, d.b2.shift, dpred, h->sig, h->max_depth, h->Ml(0, B), h->dscr,
+                            h->G(h->head_w), h->G(h->head_b), st, d.y2b);
+        } else {
+            cad::head_bwd(h->dout[0], f, h->P(h->head_w), dpred, h->sig, h->max_depth, h->Sa, h->Ml(0, B), h->dscr,
+                          h->G(h->head_w), h->G(h->head_b), st);
+        }
         return;
     }
     if (stage <= 4) {   // decoder level l = stage-1; grad of its output is in Sa
         const int l = stage - 1;
         const int C = h->Cl(l);
-        double_conv_bwd(h, h->dec[l], h->Sa, C, 0, h->cat[l], 2 * C, sv(h->cats[l], 2 * C), B, h->dcat[l], 2 * C, st);
+        const cad::HeadGrad hg{dpred, h->sig, h->P(h->head_w), h->max_depth};
+        const bool hf = l == 0 && h->head_fused;
+        double_conv_bwd(h, h->dec[l], hf ? nullptr : h->Sa, C, 0, h->cat[l], 2 * C, sv(h->cats[l], 2 * C), B, h->dcat[l],
+                        2 * C, st, hf ? &hg : nullptr);
         const Up& u = h->up[l];
         const float* upin = l == 3 ? h->a2_bott : h->dout[l + 1];
         const void* upins = l == 3 ? h->botts : h->douts[l + 1];
@@ -1009,6 +1042,10 @@ int64_t cad_unet_debug_buffer(cad_unet* h, const char* name, float* host, int64_
     else if (n == "camn") { p = h->camn; cnt = (int64_t)B * 4; }
     if (!p || cnt < 0) {
         g_err = "unknown debug buffer '" + n + "'";
+        return -1;
+    }
+    if (n == "dout0" && h->head_fused) {
+        g_err = "debug buffer 'dout0' is not written when decoder level 0 is fused with the head (CAD_HEADFUSE=0 keeps it)";
         return -1;
     }
     // With pre-split operands (bf16 engine) the last forward/backward wrote only the bf16 twins of

@@ -147,11 +147,18 @@ void bn_relu_fwd(const float* y, int C, const float* scale, const float* shift, 
 // by gmul[sample][c] (sample = row / HW) — the FiLM gamma sitting between this ReLU and the consumer.
 // dy_split != nullptr: also the pre-split twin of dy (dense, ld C).  relu = false: plain BN backward
 // (dz = g; the bottleneck's last BN, whose ReLU sits after the residual add)
+// head != nullptr: g is the depth head's input gradient dp[r] * w[c] rebuilt per row (g, gmul null)
+struct HeadGrad {
+    const float* dpred = nullptr;
+    const float* sig = nullptr;
+    const float* w = nullptr;
+    float md = 0.f;
+};
 void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, const float* mean,
                  const float* invstd, const float* scale, const float* shift, const float* gamma,
                  int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
                  hipStream_t st, const float* gmul = nullptr, int64_t HW = 1, void* dy_split = nullptr,
-                 bool relu = true, bool y_bf16 = false);
+                 bool relu = true, bool y_bf16 = false, const HeadGrad* head = nullptr);
 // out_split != nullptr: also the pooled output's split twin (dense, ld C); out may then be nullptr
 void maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float* out, uint8_t* idx,
                  hipStream_t st, void* out_split = nullptr);
@@ -163,6 +170,14 @@ void head_fwd(const float* a, int C, const float* w, const float* b, float max_d
 void head_bwd(const float* a, int C, const float* w, const float* dpred, const float* sig,
               float max_depth, float* da, int64_t M, double* scratch, float* dw, float* db,
               hipStream_t st);
+// level-0 fusion: BN apply + ReLU + head in one pass (relu(y*scale+shift) is never stored; sig / pred
+// bit-identical to bn_relu_fwd + head_fwd) and the head weight/bias gradient from y (no stored
+// activation); head_fusable: C / 4 a power of two <= 32
+bool head_fusable(int C);
+void bn_relu_head_fwd(const float* y, int C, const float* scale, const float* shift, const float* w, const float* b,
+                      float max_depth, float* sig, float* pred, int64_t M, hipStream_t st, bool y_bf16);
+void head_bwd_y(const float* y, int C, const float* scale, const float* shift, const float* dpred, const float* sig,
+                float max_depth, int64_t M, double* scratch, float* dw, float* db, hipStream_t st, bool y_bf16);
 // computeDepthMetrics partial sums per (sample, block): {n, |d|/g, d^2/g, d^2, dlog^2, a1, a2, a3}
 int metrics_blocks(int64_t HW);
 void depth_metrics_partials(const float* pred, const float* gt, int B, int64_t HW, double* part, int nb,

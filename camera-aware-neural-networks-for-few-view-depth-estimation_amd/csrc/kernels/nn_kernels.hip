@@ -10,12 +10,20 @@
 //   head: baseline_unet.h:191-192  x = out_conv(x); x = sigmoid(x) * max_depth
 #include <algorithm>
 #include <stdexcept>
+#include <type_traits>
 
 #include "gemm_s3.hpp"   // split_np (pre-split twins written by the elementwise passes)
 #include "ew_load.hpp"
 #include "kernels.hpp"
 
 namespace cad {
+// The BN apply and the head's dot product are written with explicit fma / mul so that every pass
+// that evaluates them (bn_relu_fwd, the fused level-0 pass, the head kernels, the backward's
+// rebuilds) rounds identically, whatever contraction the compiler would pick per kernel.
+__device__ __forceinline__ float bn_relu1(float y, float s, float t) { return fmaxf(__fmaf_rn(y, s, t), 0.f); }
+__device__ __forceinline__ float head_dot4(float4 a, float4 w) {
+    return __fmaf_rn(a.w, w.w, __fmaf_rn(a.z, w.z, __fmaf_rn(a.y, w.y, __fmul_rn(a.x, w.x))));
+}
 namespace {
 inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 inline int ew_blocks(int64_t n) { return (int)std::min<int64_t>(std::max<int64_t>(1, cdiv(n, 256)), 8192); }
@@ -111,32 +119,43 @@ struct OpBnTile {
     }
 };
 struct BnCoef {
-    float sc[4], sh[4], mu[4], is[4];
+    float sc[4], sh[4], mu[4], is[4], hw[4];
 };
-template <bool YB>
+// HG: the upstream gradient is the depth head's, g[r][c] = dp[r] * w[c] with
+// dp = dpred * max_depth * s (1 - s) (k_head_da's values, rebuilt per row instead of read)
+template <bool YB, bool HG = false>
 struct OpBnBwd {
     const float *g, *y, *mean, *invstd, *scale, *shift, *gmul;
     int64_t ldg; int gcoff, C; int64_t HW; bool relu;
+    HeadGrad hg;
     __device__ BnCoef prep(int c4) const {
         BnCoef k;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int c = c4 * 4 + e;
             k.sc[e] = scale[c]; k.sh[e] = shift[c]; k.mu[e] = mean[c]; k.is[e] = invstd[c];
+            if constexpr (HG) k.hw[e] = hg.w[c];
         }
         return k;
     }
     __device__ void operator()(int64_t r, int c4, double (&acc)[2][4], const BnCoef& k) const {
-        float4 gv = *reinterpret_cast<const float4*>(g + r * ldg + gcoff + c4 * 4);
-        if (gmul) {
-            const float4 m = *reinterpret_cast<const float4*>(gmul + (r / HW) * C + c4 * 4);
-            gv.x *= m.x; gv.y *= m.y; gv.z *= m.z; gv.w *= m.w;
+        float4 gv;
+        if constexpr (HG) {
+            const float s = hg.sig[r];
+            const float dp = hg.dpred[r] * hg.md * ((1.f - s) * s);
+            gv = make_float4(dp * k.hw[0], dp * k.hw[1], dp * k.hw[2], dp * k.hw[3]);
+        } else {
+            gv = *reinterpret_cast<const float4*>(g + r * ldg + gcoff + c4 * 4);
+            if (gmul) {
+                const float4 m = *reinterpret_cast<const float4*>(gmul + (r / HW) * C + c4 * 4);
+                gv.x *= m.x; gv.y *= m.y; gv.z *= m.z; gv.w *= m.w;
+            }
         }
         float4 yv = load4<YB>(y, r * C + c4 * 4);
         const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, ya[4] = {yv.x, yv.y, yv.z, yv.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const float z = ya[e] * k.sc[e] + k.sh[e];
+            const float z = __fmaf_rn(ya[e], k.sc[e], k.sh[e]);
             const float dz = (!relu || z > 0.f) ? ga[e] : 0.f;
             const float xh = (ya[e] - k.mu[e]) * k.is[e];
             acc[0][e] += dz;
@@ -153,6 +172,30 @@ struct OpHeadBwd {
         float4 v = *reinterpret_cast<const float4*>(a + r * C + c4 * 4);
         acc[0][0] += (double)dp * v.x; acc[0][1] += (double)dp * v.y;
         acc[0][2] += (double)dp * v.z; acc[0][3] += (double)dp * v.w;
+        if (c4 == 0) acc[1][0] += dp;
+    }
+};
+// the same sums with the head input a = relu(y * scale + shift) rebuilt from the level-0 BN input
+// (bn_relu_head_fwd's values; the fp32 activation is never stored)
+struct AffCoef {
+    float sc[4], sh[4];
+};
+template <bool YB>
+struct OpHeadBwdY {
+    const float *y, *scale, *shift, *dpred, *sig; float md; int C;
+    __device__ AffCoef prep(int c4) const {
+        AffCoef k;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { k.sc[e] = scale[c4 * 4 + e]; k.sh[e] = shift[c4 * 4 + e]; }
+        return k;
+    }
+    __device__ void operator()(int64_t r, int c4, double (&acc)[2][4], const AffCoef& k) const {
+        const float s = sig[r];
+        const float dp = dpred[r] * md * ((1.f - s) * s);
+        const float4 yv = load4<YB>(y, r * C + c4 * 4);
+        const float ya[4] = {yv.x, yv.y, yv.z, yv.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[0][e] += (double)dp * bn_relu1(ya[e], k.sc[e], k.sh[e]);
         if (c4 == 0) acc[1][0] += dp;
     }
 };
@@ -281,10 +324,10 @@ __global__ __launch_bounds__(256) void k_bn_relu_fwd_rows(const float* __restric
     for (int64_t r = (int64_t)blockIdx.y * rps + threadIdx.y; r < r1; r += blockDim.y) {
         const float4 v = load4<YB>(y, r * C + c);
         float4 o;
-        o.x = fmaxf(v.x * s.x + t.x, 0.f);
-        o.y = fmaxf(v.y * s.y + t.y, 0.f);
-        o.z = fmaxf(v.z * s.z + t.z, 0.f);
-        o.w = fmaxf(v.w * s.w + t.w, 0.f);
+        o.x = bn_relu1(v.x, s.x, t.x);
+        o.y = bn_relu1(v.y, s.y, t.y);
+        o.z = bn_relu1(v.z, s.z, t.z);
+        o.w = bn_relu1(v.w, s.w, t.w);
         if (out) *reinterpret_cast<float4*>(out + r * ldo + ocoff + c) = o;
         if constexpr (NP > 0) split4_store<NP>(os, ldos, oscoff, r, c, o);
     }
@@ -317,7 +360,7 @@ __global__ void k_bn_bwd_coef(const double* tot, int C, int64_t M, const float* 
     coef[C + c] = (float)(k1 * sdz / (double)M);
     coef[2 * C + c] = (float)(k1 * sdzx / (double)M);
 }
-template <int NP, bool YB>
+template <int NP, bool YB, bool HG>
 __global__ __launch_bounds__(256) void k_bn_relu_bwd_rows(const float* __restrict__ g, int64_t ldg, int gcoff,
                                                           const float* __restrict__ y, int C,
                                                           const float* __restrict__ mean,
@@ -326,32 +369,40 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_rows(const float* __restric
                                                           const float* __restrict__ shift,
                                                           const float* __restrict__ coef, float* __restrict__ dy,
                                                           int64_t M, int64_t rps, const float* __restrict__ gmul,
-                                                          int64_t HW, char* __restrict__ os, bool relu) {
+                                                          int64_t HW, char* __restrict__ os, bool relu, HeadGrad hg) {
     const int c4 = blockIdx.x * blockDim.x + threadIdx.x;
     if (c4 >= (C >> 2)) return;
     const int c0 = c4 * 4;
-    float sc[4], sh[4], mu[4], is[4], k0[4], k1[4], k2[4];
+    float sc[4], sh[4], mu[4], is[4], k0[4], k1[4], k2[4], hw[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         sc[e] = scale[c0 + e]; sh[e] = shift[c0 + e]; mu[e] = mean[c0 + e]; is[e] = invstd[c0 + e];
         k0[e] = coef[c0 + e]; k1[e] = coef[C + c0 + e]; k2[e] = coef[2 * C + c0 + e];
+        hw[e] = HG ? hg.w[c0 + e] : 0.f;
     }
     const int64_t r1 = min(M, (int64_t)(blockIdx.y + 1) * rps);
     for (int64_t r = (int64_t)blockIdx.y * rps + threadIdx.y; r < r1; r += blockDim.y) {
-        float4 gv = *reinterpret_cast<const float4*>(g + r * ldg + gcoff + c0);
-        if (gmul) {
-            const float4 m = *reinterpret_cast<const float4*>(gmul + (r / HW) * C + c0);
-            gv.x *= m.x; gv.y *= m.y; gv.z *= m.z; gv.w *= m.w;
+        float4 gv;
+        if constexpr (HG) {
+            const float s = hg.sig[r];
+            const float dp = hg.dpred[r] * hg.md * ((1.f - s) * s);
+            gv = make_float4(dp * hw[0], dp * hw[1], dp * hw[2], dp * hw[3]);
+        } else {
+            gv = *reinterpret_cast<const float4*>(g + r * ldg + gcoff + c0);
+            if (gmul) {
+                const float4 m = *reinterpret_cast<const float4*>(gmul + (r / HW) * C + c0);
+                gv.x *= m.x; gv.y *= m.y; gv.z *= m.z; gv.w *= m.w;
+            }
         }
         const float4 yv = load4<YB>(y, r * C + c0);
         const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, ya[4] = {yv.x, yv.y, yv.z, yv.w};
         float o[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const float z = ya[e] * sc[e] + sh[e];
+            const float z = __fmaf_rn(ya[e], sc[e], sh[e]);
             const float dz = (!relu || z > 0.f) ? ga[e] : 0.f;
             const float xh = (ya[e] - mu[e]) * is[e];
-            o[e] = k0[e] * dz - k1[e] - k2[e] * xh;
+            o[e] = __fsub_rn(__fmaf_rn(k0[e], dz, -k1[e]), __fmul_rn(k2[e], xh));
         }
         const float4 ov = make_float4(o[0], o[1], o[2], o[3]);
         if (dy) *reinterpret_cast<float4*>(dy + r * C + c0) = ov;
@@ -361,13 +412,20 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_rows(const float* __restric
 void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, const float* mean,
                  const float* invstd, const float* scale, const float* shift, const float* gamma,
                  int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
-                 hipStream_t st, const float* gmul, int64_t HW, void* dy_split, bool relu, bool y_bf16) {
+                 hipStream_t st, const float* gmul, int64_t HW, void* dy_split, bool relu, bool y_bf16,
+                 const HeadGrad* head) {
     double* tot = scratch;
     double* part = scratch + 2 * C;
-    const int S = y_bf16 ? launch_colreduce<2>(OpBnBwd<true>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW, relu},
-                                               M, C, part, st)
-                         : launch_colreduce<2>(OpBnBwd<false>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW, relu},
-                                               M, C, part, st);
+    const HeadGrad hg = head ? *head : HeadGrad{};
+    if (head && (g || gmul)) throw std::runtime_error("bn_relu_bwd: head gradient with an explicit gradient");
+    auto red = [&](auto yb, auto hgc) {
+        constexpr bool YB = decltype(yb)::value, HG = decltype(hgc)::value;
+        return launch_colreduce<2>(OpBnBwd<YB, HG>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW, relu, hg},
+                                   M, C, part, st);
+    };
+    using T = std::true_type;
+    using F = std::false_type;
+    const int S = head ? (y_bf16 ? red(T{}, T{}) : red(F{}, T{})) : (y_bf16 ? red(T{}, F{}) : red(F{}, F{}));
     launch_colfinal(part, S, 2 * C, tot, nullptr, 1.f, st);
     hipLaunchKernelGGL(k_bn_bwd_coef, dim3(cdiv(C, 64)), dim3(64), 0, st, tot, C, M, gamma, invstd, coef, dgamma, dbeta);
     const int np = dy_split ? split_planes() : 0;
@@ -375,10 +433,15 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
     const RowGrid rg = row_grid(M, C);
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(cdiv(C >> 2, rg.CX), rg.S), dim3(rg.CX, rg.RY), 0, st, g, ldg, gcoff, y, C, mean,
-                           invstd, scale, shift, coef, dy, M, rg.rps, gmul, HW, os, relu);
+                           invstd, scale, shift, coef, dy, M, rg.rps, gmul, HW, os, relu, hg);
     };
-    if (np == 1) y_bf16 ? go(k_bn_relu_bwd_rows<1, true>) : go(k_bn_relu_bwd_rows<1, false>);
-    else y_bf16 ? go(k_bn_relu_bwd_rows<0, true>) : go(k_bn_relu_bwd_rows<0, false>);
+    if (head) {
+        if (np == 1) y_bf16 ? go(k_bn_relu_bwd_rows<1, true, true>) : go(k_bn_relu_bwd_rows<1, false, true>);
+        else y_bf16 ? go(k_bn_relu_bwd_rows<0, true, true>) : go(k_bn_relu_bwd_rows<0, false, true>);
+    } else {
+        if (np == 1) y_bf16 ? go(k_bn_relu_bwd_rows<1, true, false>) : go(k_bn_relu_bwd_rows<1, false, false>);
+        else y_bf16 ? go(k_bn_relu_bwd_rows<0, true, false>) : go(k_bn_relu_bwd_rows<0, false, false>);
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -489,7 +552,7 @@ __global__ void k_head_fwd(const float* __restrict__ a, int C, const float* __re
         float z = 0.f;
         for (int c = 0; c < C; c += 4) {
             float4 v = *reinterpret_cast<const float4*>(row + c);
-            z += v.x * w[c] + v.y * w[c + 1] + v.z * w[c + 2] + v.w * w[c + 3];
+            z = __fadd_rn(z, head_dot4(v, make_float4(w[c], w[c + 1], w[c + 2], w[c + 3])));
         }
         z += b[0];
         const float s = 1.f / (1.f + expf(-z));
@@ -507,9 +570,9 @@ __global__ __launch_bounds__(256) void k_head_fwd_coop(const float* __restrict__
     for (int64_t p = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / TPP; p < M;
          p += (int64_t)gridDim.x * blockDim.x / TPP) {
         float4 v = *reinterpret_cast<const float4*>(a + p * C + sub * 4);
-        float z = v.x * wv.x + v.y * wv.y + v.z * wv.z + v.w * wv.w;
+        float z = head_dot4(v, wv);
 #pragma unroll
-        for (int o = TPP / 2; o > 0; o >>= 1) z += __shfl_xor(z, o);
+        for (int o = TPP / 2; o > 0; o >>= 1) z = __fadd_rn(z, __shfl_xor(z, o));
         if (sub == 0) {
             z += b[0];
             const float s = 1.f / (1.f + expf(-z));
@@ -550,6 +613,76 @@ void head_bwd(const float* a, int C, const float* w, const float* dpred, const f
     double* part = scratch + 2 * C;
     const int S = launch_colreduce<2>(OpHeadBwd{a, dpred, sig, max_depth, C}, M, C, part, st);
     // part[s][0][c] -> dw ; part[s][1][0] -> db
+    launch_colfinal(part, S, 2 * C, scratch, nullptr, 1.f, st);
+    hipLaunchKernelGGL(k_colfinal, dim3(1), dim3(64, kFinalLanes), 0, st, scratch, 1, C, nullptr, dw, 1.f);
+    hipLaunchKernelGGL(k_colfinal, dim3(1), dim3(64, kFinalLanes), 0, st, scratch + C, 1, 1, nullptr, db, 1.f);
+}
+
+// Level-0 fusion (decoder level 0's bn2 + ReLU + the depth head in one pass): the block's activation
+// a = relu(y * scale + shift) only feeds the head, so it is reduced in registers and never stored.
+// The row-slice grid puts a row's C/4 channel groups on adjacent lanes; they are reduced with the
+// same xor butterfly as k_head_fwd_coop (for C/4 <= 2 that equals k_head_fwd's sequential sum), so
+// sig / pred are bit-identical to bn_relu_fwd + head_fwd.
+bool head_fusable(int C) {
+    const int c4 = C / 4;
+    return C % 4 == 0 && c4 >= 1 && c4 <= 32 && (c4 & (c4 - 1)) == 0;
+}
+template <bool YB, int TPP>
+__global__ __launch_bounds__(256) void k_bn_relu_head_fwd_rows(const float* __restrict__ y, const float* __restrict__ scale,
+                                                               const float* __restrict__ shift, const float* __restrict__ w,
+                                                               const float* __restrict__ b, float md, float* __restrict__ sig,
+                                                               float* __restrict__ pred, int64_t M, int64_t rps) {
+    constexpr int C = 4 * TPP;
+    const int c = threadIdx.x * 4;   // blockDim.x == TPP
+    const float4 s = *reinterpret_cast<const float4*>(scale + c);
+    const float4 t = *reinterpret_cast<const float4*>(shift + c);
+    const float4 wv = *reinterpret_cast<const float4*>(w + c);
+    const float bias = b[0];
+    const int64_t r1 = min(M, (int64_t)(blockIdx.y + 1) * rps);
+    for (int64_t r = (int64_t)blockIdx.y * rps + threadIdx.y; r < r1; r += blockDim.y) {
+        const float4 v = load4<YB>(y, r * C + c);
+        float4 a;
+        a.x = bn_relu1(v.x, s.x, t.x);
+        a.y = bn_relu1(v.y, s.y, t.y);
+        a.z = bn_relu1(v.z, s.z, t.z);
+        a.w = bn_relu1(v.w, s.w, t.w);
+        float z = head_dot4(a, wv);
+#pragma unroll
+        for (int o = TPP / 2; o > 0; o >>= 1) z = __fadd_rn(z, __shfl_xor(z, o));
+        if (threadIdx.x == 0) {
+            z += bias;
+            const float sg = 1.f / (1.f + expf(-z));
+            sig[r] = sg;
+            pred[r] = sg * md;
+        }
+    }
+}
+void bn_relu_head_fwd(const float* y, int C, const float* scale, const float* shift, const float* w, const float* b,
+                      float max_depth, float* sig, float* pred, int64_t M, hipStream_t st, bool y_bf16) {
+    if (!head_fusable(C)) throw std::runtime_error("bn_relu_head_fwd: C / 4 must be a power of two <= 32");
+    const RowGrid g = row_grid(M, C);   // CX = C / 4: one row's channel groups on adjacent lanes
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(1, g.S), dim3(g.CX, g.RY), 0, st, y, scale, shift, w, b, max_depth, sig, pred, M,
+                           g.rps);
+    };
+    auto pick = [&](auto yb) {
+        constexpr bool YB = decltype(yb)::value;
+        switch (C / 4) {
+            case 1: go(k_bn_relu_head_fwd_rows<YB, 1>); break;
+            case 2: go(k_bn_relu_head_fwd_rows<YB, 2>); break;
+            case 4: go(k_bn_relu_head_fwd_rows<YB, 4>); break;
+            case 8: go(k_bn_relu_head_fwd_rows<YB, 8>); break;
+            case 16: go(k_bn_relu_head_fwd_rows<YB, 16>); break;
+            default: go(k_bn_relu_head_fwd_rows<YB, 32>); break;
+        }
+    };
+    y_bf16 ? pick(std::true_type{}) : pick(std::false_type{});
+}
+void head_bwd_y(const float* y, int C, const float* scale, const float* shift, const float* dpred, const float* sig,
+                float max_depth, int64_t M, double* scratch, float* dw, float* db, hipStream_t st, bool y_bf16) {
+    double* part = scratch + 2 * C;
+    const int S = y_bf16 ? launch_colreduce<2>(OpHeadBwdY<true>{y, scale, shift, dpred, sig, max_depth, C}, M, C, part, st)
+                         : launch_colreduce<2>(OpHeadBwdY<false>{y, scale, shift, dpred, sig, max_depth, C}, M, C, part, st);
     launch_colfinal(part, S, 2 * C, scratch, nullptr, 1.f, st);
     hipLaunchKernelGGL(k_colfinal, dim3(1), dim3(64, kFinalLanes), 0, st, scratch, 1, C, nullptr, dw, 1.f);
     hipLaunchKernelGGL(k_colfinal, dim3(1), dim3(64, kFinalLanes), 0, st, scratch + C, 1, 1, nullptr, db, 1.f);

@@ -1,0 +1,35 @@
+"""Level-0 head fusion (nn_kernels.hip bn_relu_head_fwd / head_bwd_y / bn_relu_bwd's HeadGrad form,
+wired in cad_api.cpp): decoder level 0's bn2 + ReLU feed the depth head without storing the fp32
+activation, and the backward rebuilds the head's input gradient per row.  The fused passes keep
+the unfused arithmetic and summation order, so two training steps with and without the fusion
+(CAD_HEADFUSE=0, read once per process) must agree BIT FOR BIT: predictions, losses, every gradient
+and every parameter after the Adam steps.  Widths cover C/4 = 1, 2 (k_head_fwd's sequential sum)
+and the butterfly forms, and 24 (not fusable: both runs take the unfused path)."""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(tmp_path, fuse, args):
+    out = tmp_path / f"fuse{fuse}.pt"
+    env = dict(os.environ, CAD_HEADFUSE=str(fuse))
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "headfuse_ab.py"), *map(str, args), str(out)],
+                   check=True, env=env, timeout=300)
+    return torch.load(out, weights_only=True)
+
+
+@pytest.mark.parametrize("kind,eng,f,B,H,W", [("baseline", 2, 4, 2, 64, 64), ("baseline", 2, 8, 2, 48, 64),
+                                              ("baseline", 1, 64, 2, 64, 96), ("film", 1, 32, 2, 64, 64),
+                                              ("rayfilm", 2, 16, 3, 64, 96), ("baseline", 2, 96, 1, 32, 32)])
+def test_head_fusion_bit_identical(tmp_path, kind, eng, f, B, H, W):
+    a = _run(tmp_path, 0, (kind, eng, f, B, H, W))
+    b = _run(tmp_path, 1, (kind, eng, f, B, H, W))
+    assert a.keys() == b.keys()
+    bad = [k for k in a if not torch.equal(a[k], b[k])]
+    assert not bad, bad[:8]
