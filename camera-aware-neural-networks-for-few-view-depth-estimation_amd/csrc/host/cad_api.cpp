@@ -131,6 +131,10 @@ struct DoubleConv {
     int level = 0;
     float *y1 = nullptr, *a1 = nullptr, *y2 = nullptr;
     bool y1b = false, y2b = false;   // y1 / y2 hold bf16 values (bf16 engine, pre-split conv of the last forward)
+    // conv1 keeps fp32 outputs on the bf16 engine: enc1 on the raw (non-negative) rgb, whose BN mean is
+    // many standard deviations from zero, so bf16-stored values would cost x-hat several % (measured:
+    // enc1.bn1 gradients 5x further from fp64 than the fp32 oracle's)
+    bool y1_f32 = false;
     void* a1s = nullptr;   // pre-split a1 (gemm_ps.hpp)
     int first_param = 0, last_param = 0;   // [first, last] indices in named_parameters()
     bool has_film() const { return film.p0 >= 0; }
@@ -151,7 +155,7 @@ struct cad_unet {
     int device = 0;
     int model = CAD_MODEL_BASELINE;
     int in_ch = 3, f = 64, Bmax = 1, H = 0, W = 0;
-    int x0_ld = 4;               // NHWC4 rgb (baseline, film) or NHWC8 rgb+rays (ray_film)
+    int x0_ld = 8;               // NHWC8: rgb + zero channels (baseline, film) or rgb + rays (ray_film)
     float* camn = nullptr;       // normalised intrinsics (Bmax x 4) of the last forward
     float max_depth = 10.f;
     bool train = true;
@@ -181,7 +185,7 @@ struct cad_unet {
     float* sig = nullptr;
     // pre-split operand twins (gemm_ps.hpp, bf16): written by their producer on the B1 engine, read by
     // the pre-split GEMMs; fwd_np = planes of the last forward (0: fp32 operands only)
-    void* x0s = nullptr;          // RAY_FILM's NHWC8 input (8 channels)
+    void* x0s = nullptr;          // the NHWC8 input's twin (enc1.conv1 on the pre-split kernels)
     void* cats[4] = {};
     void* pools[5] = {};
     void* botts = nullptr;
@@ -284,10 +288,13 @@ void add_double_conv(cad_unet* h, DoubleConv& dc, const std::string& pre, int ci
 
 void build_tables(cad_unet* h) {
     const int f = h->f;
+    // enc1.conv1 runs on 8 internal input channels (zero-padded weights and input): the pre-split
+    // kernels' 16-B pieces, so its forward and weight gradient read bf16 twins like the rest
     if (h->model == CAD_MODEL_RAY_FILM)   // RayEnhancedConv(3, f, 4, true): conv1 sees rgb + rays
         add_double_conv(h, h->enc[0], "enc1.", h->in_ch + 3, 8, f, 0);
     else
-        add_double_conv(h, h->enc[0], "enc1.", h->in_ch, 4, f, 0);
+        add_double_conv(h, h->enc[0], "enc1.", h->in_ch, 8, f, 0);
+    h->enc[0].y1_f32 = h->model != CAD_MODEL_RAY_FILM;
     const char* enames[4] = {"enc2", "enc3", "enc4", "bottleneck"};
     for (int i = 0; i < 4; ++i)
         add_double_conv(h, h->enc[i + 1], std::string(enames[i]) + ".conv.", f << i, f << i, f << (i + 1), i + 1);
@@ -331,7 +338,7 @@ void layout(cad_unet* h, Arena& a) {
     // pre-split (bf16) twin of `elems` fp32 values
     auto sp = [&](int64_t elems) -> void* { return a.take((size_t)elems * 2 * cad::kMaxPlanes); };
     auto conv_split_alloc = [&](Conv& c, bool dgrad) {
-        if (c.cin % 8) return;   // enc1.conv1 of the 3-channel models: in-loader split
+        if (c.cin % 8) return;   // (every conv of this family has cin % 8 == 0)
         const int64_t n = (int64_t)c.cout * 9 * c.cin;
         c.ws = sp(n);
         if (dgrad) c.wds = sp(n);
@@ -481,6 +488,18 @@ void split_weights(const cad_unet* h, hipStream_t st) {   // forward weights, ev
 // in_s / out_s: split twins of the block input / output (p == nullptr: none)
 // out_f32 = false: with pre-split GEMMs downstream only the output's twin is read (decoder outputs
 // above level 0, the bottleneck), so the fp32 output is not written
+// A/B switches read once per process: CAD_ENC1PS=0 runs enc1.conv1 on the in-loader kernel (fp32
+// input, fp32 dY), CAD_ENC1BF16=1 stores its output as bf16 like the other convolutions
+int env_flag(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    return e && e[0] ? std::atoi(e) : dflt;
+}
+// conv1 of a block runs on the pre-split twins (its input twin and weight twin exist)
+bool conv1_presplit(cad_unet* h, const DoubleConv& dc, bool ps, const cad::Split& in_s) {
+    static const bool enc1_ps = env_flag("CAD_ENC1PS", 1) != 0;
+    return ps && in_s.p && dc.c1.ws && (enc1_ps || &dc != &h->enc[0]);
+}
+
 // head_pred != nullptr: the block's bn2 + ReLU feeds the depth head directly (level-0 fusion): sig
 // and head_pred are written, out is not
 void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin, cad::Split in_s, int B, float* out,
@@ -499,13 +518,14 @@ void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin,
             cad::bn_eval_coeffs(h->P(b.widx), h->P(b.bidx), b.rm, b.rv, C, 1e-5f, b.mean, b.invstd, b.scale, b.shift, st);
     };
     float* stats = tr ? h->stats : nullptr;
-    const bool ps1 = ps && in_s.p && dc.c1.ws;
+    const bool ps1 = conv1_presplit(h, dc, ps, in_s);
     // the pre-split (bf16 engine) convolutions store their pre-BN outputs as bf16 (BN statistics are
     // those of the stored values); BN apply / backward and FiLM read them as such
-    dc.y1b = ps1;
+    static const bool enc1_bf16 = env_flag("CAD_ENC1BF16", 0) != 0;
+    dc.y1b = ps1 && (!dc.y1_f32 || enc1_bf16);
     dc.y2b = ps;
     if (ps1)
-        cad::conv3x3_fwd_ps(in_s, dc.c1.cin, sv(dc.c1.ws, 9 * dc.c1.cin), C, dc.y1, C, 0, B, Hh, Ww, stats, st, true);
+        cad::conv3x3_fwd_ps(in_s, dc.c1.cin, sv(dc.c1.ws, 9 * dc.c1.cin), C, dc.y1, C, 0, B, Hh, Ww, stats, st, dc.y1b);
     else
         cad::conv3x3_fwd(in, ldin, 0, dc.c1.cin, h->P(dc.c1.pidx), C, dc.y1, C, 0, B, Hh, Ww, stats, st);
     bn(dc.b1, dc.c1.cin, ps1);
@@ -561,7 +581,7 @@ void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth
     if (h->model == CAD_MODEL_RAY_FILM)
         cad::rgb_rays_to_nhwc8(rgb, cam4, B, h->H, h->W, h->x0, st);
     else
-        cad::rgb_to_nhwc4(rgb, h->x0, B, h->H, h->W, st);
+        cad::rgb_to_nhwc8(rgb, h->x0, B, h->H, h->W, st);
     const cad::Split none{};
     cad::Split x0s = none;
     if (ps && h->x0s) {
@@ -638,7 +658,7 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
                              dc.y1b);
     // bn1 + relu; the fp32 dY1 only when a conv1 GEMM below reads it (enc1's 4-channel input keeps the
     // in-loader weight gradient)
-    const bool ps1 = ps && in_s.p && dc.c1.ws;
+    const bool ps1 = conv1_presplit(h, dc, ps, in_s);
     const bool dy1_f32 = !ps1 || (din && !(ps && dc.c1.wds));
     cad::bn_relu_bwd(dA1, C, 0, dc.y1, C, dc.b1.mean, dc.b1.invstd, dc.b1.scale, dc.b1.shift, h->P(dc.b1.widx), M,
                      h->dscr, dc.b1.coef, h->G(dc.b1.widx), h->G(dc.b1.bidx), dy1_f32 ? dY : nullptr, st,
@@ -889,7 +909,7 @@ cad_status cad_unet_create_model(const cad_unet_desc* d, int model, int device, 
         auto h = std::make_unique<cad_unet>();
         h->device = device;
         h->model = model;
-        h->x0_ld = model == CAD_MODEL_RAY_FILM ? 8 : 4;
+        h->x0_ld = 8;
         h->in_ch = d->in_channels;
         h->f = d->init_features;
         h->max_depth = d->max_depth;

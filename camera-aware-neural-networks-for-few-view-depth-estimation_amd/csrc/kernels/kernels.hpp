@@ -165,6 +165,7 @@ void maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float*
 void maxpool_bwd(const float* dout, const uint8_t* idx, int C, int B, int H, int W, float* dx,
                  int64_t lddx, hipStream_t st);
 void rgb_to_nhwc4(const float* rgb, float* out, int B, int H, int W, hipStream_t st);
+void rgb_to_nhwc8(const float* rgb, float* out, int B, int H, int W, hipStream_t st);
 void head_fwd(const float* a, int C, const float* w, const float* b, float max_depth, float* sig,
               float* pred, int64_t M, hipStream_t st);
 void head_bwd(const float* a, int C, const float* w, const float* dpred, const float* sig,

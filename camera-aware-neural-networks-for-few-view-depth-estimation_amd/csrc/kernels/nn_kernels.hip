@@ -543,6 +543,20 @@ void rgb_to_nhwc4(const float* rgb, float* out, int B, int H, int W, hipStream_t
     const int64_t n = (int64_t)B * H * W;
     hipLaunchKernelGGL(k_rgb_to_nhwc4, dim3(ew_blocks(n)), dim3(256), 0, st, rgb, out, (int64_t)H * W, n);
 }
+// NHWC8 (rgb + 5 zero channels): the row width of the pre-split (bf16 twin) conv loaders, 16-B pieces
+__global__ void k_rgb_to_nhwc8(const float* __restrict__ rgb, float* __restrict__ out, int64_t HW, int64_t n) {
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = p / HW, yx = p - b * HW;
+        const float* s = rgb + b * 3 * HW + yx;
+        float4* o = reinterpret_cast<float4*>(out + p * 8);
+        o[0] = make_float4(s[0], s[HW], s[2 * HW], 0.f);
+        o[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+}
+void rgb_to_nhwc8(const float* rgb, float* out, int B, int H, int W, hipStream_t st) {
+    const int64_t n = (int64_t)B * H * W;
+    hipLaunchKernelGGL(k_rgb_to_nhwc8, dim3(ew_blocks(n)), dim3(256), 0, st, rgb, out, (int64_t)H * W, n);
+}
 
 __global__ void k_head_fwd(const float* __restrict__ a, int C, const float* __restrict__ w,
                            const float* __restrict__ b, float md, float* __restrict__ sig,
