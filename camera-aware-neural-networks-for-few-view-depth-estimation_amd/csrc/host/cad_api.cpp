@@ -637,6 +637,7 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     const bool ps = h->fwd_np > 0 && h->fwd_np == cad::split_planes();
     float* dY = h->Sb;
     void* dYs = h->dYs;
+    // conv2's input gradient; the bf16 engine stores it as bf16 (read by FiLM's and bn1's backward)
     float* dA1 = h->Sa;
     // bn2 + relu
     // with pre-split GEMMs both consumers of dY2 read its twin: the fp32 dY2 is not written
@@ -646,7 +647,7 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     // conv2: wgrad, dgrad
     if (ps) {
         cad::conv3x3_wgrad_ps(sv(dYs, C), C, sv(dc.a1s, C), C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
-        cad::conv3x3_dgrad_ps(sv(dYs, C), C, sv(dc.c2.wds, 9 * C), C, dA1, C, B, Hh, Ww, st);
+        cad::conv3x3_dgrad_ps(sv(dYs, C), C, sv(dc.c2.wds, 9 * C), C, dA1, C, B, Hh, Ww, st, true);
     } else {
         cad::conv3x3_wgrad(dY, C, dc.a1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
         cad::conv3x3_dgrad(dY, C, dc.c2.wd, C, dA1, C, B, Hh, Ww, st);
@@ -655,14 +656,14 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     const int64_t HW = (int64_t)Hh * Ww;
     if (dc.has_film())
         cad::film_affine_bwd(dA1, dc.y1, C, dc.b1.scale, dc.b1.shift, B, HW, h->dscr, dc.film.dgam, dc.film.dbet, st,
-                             dc.y1b);
+                             dc.y1b, ps);
     // bn1 + relu; the fp32 dY1 only when a conv1 GEMM below reads it (enc1's 4-channel input keeps the
     // in-loader weight gradient)
     const bool ps1 = conv1_presplit(h, dc, ps, in_s);
     const bool dy1_f32 = !ps1 || (din && !(ps && dc.c1.wds));
     cad::bn_relu_bwd(dA1, C, 0, dc.y1, C, dc.b1.mean, dc.b1.invstd, dc.b1.scale, dc.b1.shift, h->P(dc.b1.widx), M,
                      h->dscr, dc.b1.coef, h->G(dc.b1.widx), h->G(dc.b1.bidx), dy1_f32 ? dY : nullptr, st,
-                     dc.has_film() ? dc.film.gam : nullptr, HW, ps ? dYs : nullptr, true, dc.y1b);
+                     dc.has_film() ? dc.film.gam : nullptr, HW, ps ? dYs : nullptr, true, dc.y1b, nullptr, ps);
     if (dc.has_film()) cad::film_mlp_bwd(film_view(h, dc), h->camn, B, st);
     // conv1: wgrad, dgrad
     if (ps1)

@@ -792,7 +792,7 @@ void conv3x3_fwd_ps(Split x, int cin, Split w, int cout, float* y, int64_t ldy, 
 }
 
 void conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t lddx, int B, int H, int W,
-                      hipStream_t st) {
+                      hipStream_t st, bool dx_bf16) {
     ps_check(dz, cout, "conv3x3_dgrad dz");
     ps_check(wd, 9 * cout, "conv3x3_dgrad w");
     GemmArgs a{};
@@ -802,14 +802,16 @@ void conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t 
     a.Bm = (const float*)wd.p; a.ldb = wd.ld; a.b_coff = wd.coff;
     a.C = dx; a.ldc = lddx; a.c_coff = 0;
     if (const WinPick wp = pick_win_ps(cout, W, cin, dz.coff); wp.R && wd.coff == 0) {
-        launch_win<EpiStore, true>(wp, a, st);
+        if (dx_bf16) launch_win<EpiStoreB16, true>(wp, a, st);
+        else launch_win<EpiStore, true>(wp, a, st);
         return;
     }
     const Cfg c = pick_cfg(a.M, a.N);
     const int kb = ps_kb(true, c);
     a.kstages_per_split = cdiv(a.K, kb);
     a.cimajor = cout % kb == 0;
-    launch_kb<KConvFwdP1, 32, 64>(c, kb, a, 1, st);
+    if (dx_bf16) launch_kb<KConvFwdP1B, 32, 64>(c, kb, a, 1, st);
+    else launch_kb<KConvFwdP1, 32, 64>(c, kb, a, 1, st);
 }
 
 // B1 window weight gradient (conv3x3_wgrad_win_ps_body): stage = P pixels of an image row

@@ -239,7 +239,7 @@ void film_apply(const float* y, int C, const float* scale, const float* shift, c
 // ------------------------------------------------------------------------------------------
 int film_reduce_slices(int64_t HW) { return (int)std::max<int64_t>(1, std::min<int64_t>(64, HW / 1024)); }
 
-template <bool YB>
+template <bool YB, bool GB = false>   // GB: dA holds bf16 values
 __global__ __launch_bounds__(256) void k_film_reduce(const float* __restrict__ dA, const float* __restrict__ y,
                                                      int C, const float* __restrict__ scale,
                                                      const float* __restrict__ shift, int64_t HW, int64_t rps,
@@ -256,7 +256,7 @@ __global__ __launch_bounds__(256) void k_film_reduce(const float* __restrict__ d
         const float4 t = *reinterpret_cast<const float4*>(shift + c4 * 4);
         for (int64_t r = r0 + threadIdx.y; r < r1; r += RY) {
             const int64_t off = ((int64_t)b * HW + r) * C + c4 * 4;
-            const float4 d = *reinterpret_cast<const float4*>(dA + off);
+            const float4 d = load4<GB>(dA, off);
             const float4 v = load4<YB>(y, off);
             ag[0] += (double)d.x * fmaxf(v.x * s.x + t.x, 0.f);
             ag[1] += (double)d.y * fmaxf(v.y * s.y + t.y, 0.f);
@@ -293,14 +293,20 @@ __global__ void k_film_reduce_final(const double* __restrict__ part, int S, int 
     dbet[i] = (float)be;
 }
 void film_affine_bwd(const float* dA, const float* y, int C, const float* scale, const float* shift, int B, int64_t HW,
-                     double* scratch, float* dgam, float* dbet, hipStream_t st, bool y_bf16) {
+                     double* scratch, float* dgam, float* dbet, hipStream_t st, bool y_bf16, bool dA_bf16) {
     const int C4 = C >> 2;
     const int CX = std::min(C4, 64);
     const int RY = std::max(1, 256 / CX);
     const int S = film_reduce_slices(HW);
     const int64_t rps = (HW + S - 1) / S;
     const size_t shm = (size_t)RY * CX * 8 * sizeof(double);
-    if (y_bf16)
+    if (y_bf16 && dA_bf16)
+        hipLaunchKernelGGL((k_film_reduce<true, true>), dim3(cdiv(C4, CX), S, B), dim3(CX, RY), shm, st, dA, y, C, scale,
+                           shift, HW, rps, scratch);
+    else if (dA_bf16)
+        hipLaunchKernelGGL((k_film_reduce<false, true>), dim3(cdiv(C4, CX), S, B), dim3(CX, RY), shm, st, dA, y, C, scale,
+                           shift, HW, rps, scratch);
+    else if (y_bf16)
         hipLaunchKernelGGL(k_film_reduce<true>, dim3(cdiv(C4, CX), S, B), dim3(CX, RY), shm, st, dA, y, C, scale, shift, HW,
                            rps, scratch);
     else

@@ -55,8 +55,9 @@ void split_rows(const float* x, int64_t ldx, int xcoff, int C, int64_t M, void* 
 // y_bf16: y is written as bf16 rows of ldy elements (the bf16 engine's pre-BN outputs)
 void conv3x3_fwd_ps(Split x, int cin, Split w, int cout, float* y, int64_t ldy, int ycoff, int B, int H, int W,
                     float* stats, hipStream_t st, bool y_bf16 = false);
+// dx_bf16: dx is written as bf16 rows of lddx elements (the bf16 engine's conv2 input gradient)
 void conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t lddx, int B, int H, int W,
-                      hipStream_t st);
+                      hipStream_t st, bool dx_bf16 = false);
 void conv3x3_wgrad_ps(Split dz, int cout, Split x, int cin, float* dw, int B, int H, int W, float* slab,
                       int64_t slab_cap, hipStream_t st);
 // y_bf16: y is a bf16 twin (rows of ldy elements) — the up half of the decoder concat twin
@@ -158,7 +159,7 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
                  const float* invstd, const float* scale, const float* shift, const float* gamma,
                  int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
                  hipStream_t st, const float* gmul = nullptr, int64_t HW = 1, void* dy_split = nullptr,
-                 bool relu = true, bool y_bf16 = false, const HeadGrad* head = nullptr);
+                 bool relu = true, bool y_bf16 = false, const HeadGrad* head = nullptr, bool g_bf16 = false);
 // out_split != nullptr: also the pooled output's split twin (dense, ld C); out may then be nullptr
 void maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float* out, uint8_t* idx,
                  hipStream_t st, void* out_split = nullptr);
@@ -250,7 +251,8 @@ void film_apply(const float* y, int C, const float* scale, const float* shift, c
                 int B, int64_t HW, float* out, hipStream_t st, bool y_bf16 = false, void* os = nullptr);
 // dgam[b,c] = sum_hw dA * relu(y*scale+shift), dbet[b,c] = sum_hw dA
 void film_affine_bwd(const float* dA, const float* y, int C, const float* scale, const float* shift, int B, int64_t HW,
-                     double* scratch, float* dgam, float* dbet, hipStream_t st, bool y_bf16 = false);
+                     double* scratch, float* dgam, float* dbet, hipStream_t st, bool y_bf16 = false,
+                     bool dA_bf16 = false);
 int64_t film_reduce_doubles(int B, int64_t HW, int C);
 
 // ---------------- geometry-aware family (attn_kernels.hip) ----------------

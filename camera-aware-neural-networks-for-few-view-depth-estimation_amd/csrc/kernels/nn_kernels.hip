@@ -123,7 +123,8 @@ struct BnCoef {
 };
 // HG: the upstream gradient is the depth head's, g[r][c] = dp[r] * w[c] with
 // dp = dpred * max_depth * s (1 - s) (k_head_da's values, rebuilt per row instead of read)
-template <bool YB, bool HG = false>
+// GB: g holds bf16 values (the bf16 engine's conv2 dgrad output)
+template <bool YB, bool HG = false, bool GB = false>
 struct OpBnBwd {
     const float *g, *y, *mean, *invstd, *scale, *shift, *gmul;
     int64_t ldg; int gcoff, C; int64_t HW; bool relu;
@@ -145,7 +146,7 @@ struct OpBnBwd {
             const float dp = hg.dpred[r] * hg.md * ((1.f - s) * s);
             gv = make_float4(dp * k.hw[0], dp * k.hw[1], dp * k.hw[2], dp * k.hw[3]);
         } else {
-            gv = *reinterpret_cast<const float4*>(g + r * ldg + gcoff + c4 * 4);
+            gv = load4<GB>(g, r * ldg + gcoff + c4 * 4);
             if (gmul) {
                 const float4 m = *reinterpret_cast<const float4*>(gmul + (r / HW) * C + c4 * 4);
                 gv.x *= m.x; gv.y *= m.y; gv.z *= m.z; gv.w *= m.w;
@@ -360,7 +361,7 @@ __global__ void k_bn_bwd_coef(const double* tot, int C, int64_t M, const float* 
     coef[C + c] = (float)(k1 * sdz / (double)M);
     coef[2 * C + c] = (float)(k1 * sdzx / (double)M);
 }
-template <int NP, bool YB, bool HG>
+template <int NP, bool YB, bool HG, bool GB = false>
 __global__ __launch_bounds__(256) void k_bn_relu_bwd_rows(const float* __restrict__ g, int64_t ldg, int gcoff,
                                                           const float* __restrict__ y, int C,
                                                           const float* __restrict__ mean,
@@ -388,7 +389,7 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_rows(const float* __restric
             const float dp = hg.dpred[r] * hg.md * ((1.f - s) * s);
             gv = make_float4(dp * hw[0], dp * hw[1], dp * hw[2], dp * hw[3]);
         } else {
-            gv = *reinterpret_cast<const float4*>(g + r * ldg + gcoff + c0);
+            gv = load4<GB>(g, r * ldg + gcoff + c0);
             if (gmul) {
                 const float4 m = *reinterpret_cast<const float4*>(gmul + (r / HW) * C + c0);
                 gv.x *= m.x; gv.y *= m.y; gv.z *= m.z; gv.w *= m.w;
@@ -413,19 +414,21 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
                  const float* invstd, const float* scale, const float* shift, const float* gamma,
                  int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
                  hipStream_t st, const float* gmul, int64_t HW, void* dy_split, bool relu, bool y_bf16,
-                 const HeadGrad* head) {
+                 const HeadGrad* head, bool g_bf16) {
     double* tot = scratch;
     double* part = scratch + 2 * C;
     const HeadGrad hg = head ? *head : HeadGrad{};
-    if (head && (g || gmul)) throw std::runtime_error("bn_relu_bwd: head gradient with an explicit gradient");
-    auto red = [&](auto yb, auto hgc) {
-        constexpr bool YB = decltype(yb)::value, HG = decltype(hgc)::value;
-        return launch_colreduce<2>(OpBnBwd<YB, HG>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW, relu, hg},
+    if (head && (g || gmul || g_bf16)) throw std::runtime_error("bn_relu_bwd: head gradient with an explicit gradient");
+    auto red = [&](auto yb, auto hgc, auto gbc) {
+        constexpr bool YB = decltype(yb)::value, HG = decltype(hgc)::value, GB = decltype(gbc)::value;
+        return launch_colreduce<2>(OpBnBwd<YB, HG, GB>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW, relu, hg},
                                    M, C, part, st);
     };
     using T = std::true_type;
     using F = std::false_type;
-    const int S = head ? (y_bf16 ? red(T{}, T{}) : red(F{}, T{})) : (y_bf16 ? red(T{}, F{}) : red(F{}, F{}));
+    const int S = head     ? (y_bf16 ? red(T{}, T{}, F{}) : red(F{}, T{}, F{}))
+                  : g_bf16 ? (y_bf16 ? red(T{}, F{}, T{}) : red(F{}, F{}, T{}))
+                           : (y_bf16 ? red(T{}, F{}, F{}) : red(F{}, F{}, F{}));
     launch_colfinal(part, S, 2 * C, tot, nullptr, 1.f, st);
     hipLaunchKernelGGL(k_bn_bwd_coef, dim3(cdiv(C, 64)), dim3(64), 0, st, tot, C, M, gamma, invstd, coef, dgamma, dbeta);
     const int np = dy_split ? split_planes() : 0;
@@ -438,6 +441,9 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
     if (head) {
         if (np == 1) y_bf16 ? go(k_bn_relu_bwd_rows<1, true, true>) : go(k_bn_relu_bwd_rows<1, false, true>);
         else y_bf16 ? go(k_bn_relu_bwd_rows<0, true, true>) : go(k_bn_relu_bwd_rows<0, false, true>);
+    } else if (g_bf16) {
+        if (np == 1) y_bf16 ? go(k_bn_relu_bwd_rows<1, true, false, true>) : go(k_bn_relu_bwd_rows<1, false, false, true>);
+        else y_bf16 ? go(k_bn_relu_bwd_rows<0, true, false, true>) : go(k_bn_relu_bwd_rows<0, false, false, true>);
     } else {
         if (np == 1) y_bf16 ? go(k_bn_relu_bwd_rows<1, true, false>) : go(k_bn_relu_bwd_rows<1, false, false>);
         else y_bf16 ? go(k_bn_relu_bwd_rows<0, true, false>) : go(k_bn_relu_bwd_rows<0, false, false>);

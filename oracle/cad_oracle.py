@@ -289,7 +289,8 @@ def rays_from_K(K, H, W):
 # GEMM operand precision of the conv / ConvT contractions.  "exact": the reference's fp32 (or the
 # fp64 yardstick).  "bf16": the bf16 configs' arithmetic (BASELINE configs 3-5, cad.h CAD_GEMM_BF16):
 # every contraction multiplies bf16-rounded operands — forward (x, w), dgrad (dy, w) and wgrad
-# (dy, x) — and accumulates in the working dtype; the conv outputs (pre-BN) are stored as bf16;
+# (dy, x) — and accumulates in the working dtype; the conv outputs (pre-BN) are stored as bf16, and
+# in the U-Net family so is each DoubleConv's conv2 input gradient;
 # BN, FiLM, the 1x1 head, the loss and the optimizer stay in the working dtype.  Not a reference behaviour (the reference has no bf16 path):
 # the yardstick the GPU bf16 engine is checked against.
 _GEMM = {"operands": "exact"}
@@ -399,25 +400,29 @@ def _film(x, c, p, bufs, pre, train):
     return gamma[:, :, None, None] * x + beta[:, :, None, None]
 
 
-def _double_conv(x, p, bufs, pre, train, cam=None):
+def _double_conv(x, p, bufs, pre, train, cam=None, da1_bf16=False):
     # DoubleConvImpl::forward (baseline_unet.h:32-43); with `cam`: FiLMDoubleConvImpl::forward
     # (intrinsics_unet.h:38-52) = RayEnhancedConvImpl::forward after its cat (geometry_aware_network.h:47-64)
     x = _conv3x3(x, p[pre + "conv1.weight"], pre + "conv1")
     x = _bn_relu(x, p, bufs, pre + "bn1", train)
     if cam is not None:
         x = _film(x, cam, p, bufs, pre + "film.", train)
+    if da1_bf16 and _GEMM["operands"] == "bf16":
+        # the U-Net family's bf16 engine stores conv2's input gradient (its dgrad output, read by the
+        # FiLM and bn1 backward) as bf16 (cad_api.cpp double_conv_bwd)
+        x = _RoundGradOperand.apply(x)
     x = _conv3x3(x, p[pre + "conv2.weight"], pre + "conv2")
     return _bn_relu(x, p, bufs, pre + "bn2", train)
 
 
-def _decoder(x, skip, p, bufs, pre, train, cam=None):
+def _decoder(x, skip, p, bufs, pre, train, cam=None, da1_bf16=False):
     # DecoderBlockImpl::forward (baseline_unet.h:83-102): up, pad-if-needed, cat({skip, up}), conv
     # (FiLMDecoderBlockImpl::forward, intrinsics_unet.h:91-110, is the same with a FiLM conv)
     x = _convT2x2(x, p[pre + "up.weight"], p[pre + "up.bias"])
     dh, dw = skip.shape[2] - x.shape[2], skip.shape[3] - x.shape[3]
     if dh > 0 or dw > 0:
         x = F.pad(x, (dw // 2, dw - dw // 2, dh // 2, dh - dh // 2))
-    return _double_conv(torch.cat([skip, x], 1), p, bufs, pre + "conv.", train, cam)
+    return _double_conv(torch.cat([skip, x], 1), p, bufs, pre + "conv.", train, cam, da1_bf16)
 
 
 def _cbam(x, p, pre):
@@ -506,15 +511,17 @@ def unet_forward(x, p, bufs, train=True, max_depth=10.0, model="baseline", K=Non
         cam = normalize_cam(cam_from_K(K.to(x.dtype)), x.shape[3], x.shape[2])
         if model == "rayfilm":
             x = torch.cat([x, rays_from_K(K, x.shape[2], x.shape[3]).to(x.dtype)], 1)
-    s1 = _double_conv(x, p, bufs, "enc1.", train, cam)
-    s2 = _double_conv(F.max_pool2d(s1, 2), p, bufs, "enc2.conv.", train, cam)
-    s3 = _double_conv(F.max_pool2d(s2, 2), p, bufs, "enc3.conv.", train, cam)
-    s4 = _double_conv(F.max_pool2d(s3, 2), p, bufs, "enc4.conv.", train, cam)
-    xb = _double_conv(F.max_pool2d(s4, 2), p, bufs, "bottleneck.conv.", train, cam)
-    x = _decoder(xb, s4, p, bufs, "dec4.", train, cam)
-    x = _decoder(x, s3, p, bufs, "dec3.", train, cam)
-    x = _decoder(x, s2, p, bufs, "dec2.", train, cam)
-    x = _decoder(x, s1, p, bufs, "dec1.", train, cam)
+    # (the GPU's pre-split path, and with it the bf16 conv2 input gradient, needs f % 8 == 0)
+    r = p["enc1.conv1.weight"].shape[0] % 8 == 0
+    s1 = _double_conv(x, p, bufs, "enc1.", train, cam, r)
+    s2 = _double_conv(F.max_pool2d(s1, 2), p, bufs, "enc2.conv.", train, cam, r)
+    s3 = _double_conv(F.max_pool2d(s2, 2), p, bufs, "enc3.conv.", train, cam, r)
+    s4 = _double_conv(F.max_pool2d(s3, 2), p, bufs, "enc4.conv.", train, cam, r)
+    xb = _double_conv(F.max_pool2d(s4, 2), p, bufs, "bottleneck.conv.", train, cam, r)
+    x = _decoder(xb, s4, p, bufs, "dec4.", train, cam, r)
+    x = _decoder(x, s3, p, bufs, "dec3.", train, cam, r)
+    x = _decoder(x, s2, p, bufs, "dec2.", train, cam, r)
+    x = _decoder(x, s1, p, bufs, "dec1.", train, cam, r)
     x = F.conv2d(x, p["out_conv.weight"], p["out_conv.bias"])
     return torch.sigmoid(x) * max_depth
 
