@@ -405,24 +405,27 @@ __global__ __launch_bounds__(256) void k_film_gw2(FilmLayer L, int B) {
     L.gw2[t] = acc;
 }
 
-// layer 1: dh1[b][j] = Σ_jj dz2[b][jj] W2[jj][j] (thread (j, q) for the samples b = q mod 8), then
-// BN1d + ReLU backward and the fc1 gradients per column
-__global__ __launch_bounds__(1024) void k_film_l1_bwd(FilmLayer L, const float* __restrict__ camn, int B) {
-    const int j = threadIdx.x & (H1 - 1), q = threadIdx.x / H1;
-    for (int b0 = q; b0 < B; b0 += 32) {
-        float acc[4] = {0.f, 0.f, 0.f, 0.f};
-        for (int jj = 0; jj < H2; ++jj) {
-            const float w = L.w2[jj * H1 + j];
+// layer 1: dh1[b][j] = Σ_jj dz2[b][jj] W2[jj][j], one thread per (b, j) (j fastest: coalesced weight
+// rows, dz2 broadcast), loads 8 terms ahead of the dependent FMA chain (jj ascending)
+__global__ __launch_bounds__(256) void k_film_dh1(FilmLayer L, int B) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= B * H1) return;
+    const int b = t / H1, j = t - b * H1;
+    const float* d = L.dh2 + (int64_t)b * H2;
+    const float* w = L.w2 + j;
+    float acc = 0.f;
+    for (int jj = 0; jj < H2; jj += 8) {
+        float dv[8], wv[8];
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (b0 + 8 * u < B) acc[u] += L.dh2[(b0 + 8 * u) * H2 + jj] * w;
-        }
+        for (int u = 0; u < 8; ++u) { dv[u] = d[jj + u]; wv[u] = w[(jj + u) * H1]; }
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (b0 + 8 * u < B) L.dh1[(b0 + 8 * u) * H1 + j] = acc[u];
+        for (int u = 0; u < 8; ++u) acc += dv[u] * wv[u];
     }
-    __syncthreads();
-    if (q != 0) return;
+    L.dh1[t] = acc;
+}
+// then BN1d + ReLU backward and the fc1 gradients per column
+__global__ __launch_bounds__(H1) void k_film_l1_bwd(FilmLayer L, const float* __restrict__ camn, int B) {
+    const int j = threadIdx.x;
     bn1d_relu_bwd_col(L.dh1, L.h1, L.xh1, H1, j, B, B > 1, L.g1, L.is1, L.gg1, L.gbe1);
     float db = 0.f;
     float dw[4] = {0.f, 0.f, 0.f, 0.f};
@@ -443,7 +446,8 @@ void film_mlp_bwd(const FilmLayer& L, const float* camn, int B, hipStream_t st) 
     hipLaunchKernelGGL(k_film_dh2, dim3(cdiv((int64_t)B * H2, 256)), dim3(256), 0, st, L, B);
     hipLaunchKernelGGL(k_film_l2_bwd, dim3(1), dim3(H2), 0, st, L, B);
     hipLaunchKernelGGL(k_film_gw2, dim3(cdiv(H2 * H1, 256)), dim3(256), 0, st, L, B);
-    hipLaunchKernelGGL(k_film_l1_bwd, dim3(1), dim3(8 * H1), 0, st, L, camn, B);
+    hipLaunchKernelGGL(k_film_dh1, dim3(cdiv((int64_t)B * H1, 256)), dim3(256), 0, st, L, B);
+    hipLaunchKernelGGL(k_film_l1_bwd, dim3(1), dim3(H1), 0, st, L, camn, B);
 }
 
 }  // namespace cad

