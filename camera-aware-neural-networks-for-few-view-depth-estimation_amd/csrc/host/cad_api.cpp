@@ -553,6 +553,12 @@ void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin,
                      twin ? const_cast<void*>(out_s.p) : nullptr, out_s.ld, out_s.coff, dc.y2b);
 }
 
+// CAD_POOLFOLD=0 keeps the max-pool backward scatter (A/B measurements; bit-identical)
+bool pool_fold_on() {
+    static const bool on = env_flag("CAD_POOLFOLD", 1) != 0;
+    return on;
+}
+
 // CAD_HEADFUSE=0 keeps the unfused level-0 passes (A/B measurements)
 bool head_fusion_on() {
     static const bool on = [] {
@@ -631,7 +637,7 @@ void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth
 // head != nullptr (level-0 fusion): g is null and bn2's upstream gradient is the head's, rebuilt per row.
 void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, int gcoff, const float* in,
                      int64_t ldin, cad::Split in_s, int B, float* din, int64_t lddin, hipStream_t st,
-                     const cad::HeadGrad* head = nullptr) {
+                     const cad::HeadGrad* head = nullptr, const cad::PoolAdd* pool = nullptr) {
     const int l = dc.level, Hh = h->Hl(l), Ww = h->Wl(l), C = dc.c1.cout;
     const int64_t M = h->Ml(l, B);
     const bool ps = h->fwd_np > 0 && h->fwd_np == cad::split_planes();
@@ -643,7 +649,7 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     // with pre-split GEMMs both consumers of dY2 read its twin: the fp32 dY2 is not written
     cad::bn_relu_bwd(g, ldg, gcoff, dc.y2, C, dc.b2.mean, dc.b2.invstd, dc.b2.scale, dc.b2.shift, h->P(dc.b2.widx), M,
                      h->dscr, dc.b2.coef, h->G(dc.b2.widx), h->G(dc.b2.bidx), ps ? nullptr : dY, st, nullptr, 1,
-                     ps ? dYs : nullptr, true, dc.y2b, head);
+                     ps ? dYs : nullptr, true, dc.y2b, head, false, pool);
     // conv2: wgrad, dgrad
     if (ps) {
         cad::conv3x3_wgrad_ps(sv(dYs, C), C, sv(dc.a1s, C), C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
@@ -749,14 +755,20 @@ void backward_stage(cad_unet* h, int stage, const float* dpred, hipStream_t st) 
     const int C = h->Cl(l);
     const float* g = l == 4 ? h->Sa : h->dcat[l];
     const int64_t ldg = l == 4 ? C : 2 * C;
+    // the max-pool backward of the level below (its pooled gradient in Sc, written by the previous
+    // stage) is folded into this block's bn2 backward instead of scattered into dcat beforehand
+    const cad::PoolAdd pa{h->Sc, h->pidx[l + 1], h->Hl(l), h->Wl(l)};
+    const cad::PoolAdd* pool = l < 4 && pool_fold_on() ? &pa : nullptr;
     if (l == 0) {
-        double_conv_bwd(h, e, g, ldg, 0, h->x0, h->x0_ld, sv(h->x0s, h->x0_ld), B, nullptr, 0, st);
+        double_conv_bwd(h, e, g, ldg, 0, h->x0, h->x0_ld, sv(h->x0s, h->x0_ld), B, nullptr, 0, st, nullptr, pool);
         return;
     }
     const int Cp = h->Cl(l - 1);
-    double_conv_bwd(h, e, g, ldg, 0, h->pool[l], Cp, sv(h->pools[l], Cp), B, h->Sc, Cp, st);
+    double_conv_bwd(h, e, g, ldg, 0, h->pool[l], Cp, sv(h->pools[l], Cp), B, h->Sc, Cp, st, nullptr, pool);
     // max-pool backward: the pooled gradient is added at the recorded argmax of dcat's skip half
-    cad::maxpool_bwd(h->Sc, h->pidx[l], Cp, B, h->Hl(l - 1), h->Wl(l - 1), h->dcat[l - 1], 2 * Cp, st);
+    // (folded into the next stage's bn2 backward unless CAD_POOLFOLD=0)
+    if (!pool_fold_on())
+        cad::maxpool_bwd(h->Sc, h->pidx[l], Cp, B, h->Hl(l - 1), h->Wl(l - 1), h->dcat[l - 1], 2 * Cp, st);
 }
 
 void compute_stage_ranges(cad_unet* h) {

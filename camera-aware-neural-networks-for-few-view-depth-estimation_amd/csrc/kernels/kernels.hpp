@@ -155,11 +155,20 @@ struct HeadGrad {
     const float* w = nullptr;
     float md = 0.f;
 };
+// pool != nullptr: the max-pool backward folded in — g[r][c] += d[pooled r][c] where r is the
+// recorded argmax of its 2x2 window (idx, scan order 0..3), instead of a scatter into g beforehand;
+// H, W: g's image size (r < 2^32)
+struct PoolAdd {
+    const float* d = nullptr;
+    const uint8_t* idx = nullptr;
+    int H = 0, W = 0;
+};
 void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, const float* mean,
                  const float* invstd, const float* scale, const float* shift, const float* gamma,
                  int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
                  hipStream_t st, const float* gmul = nullptr, int64_t HW = 1, void* dy_split = nullptr,
-                 bool relu = true, bool y_bf16 = false, const HeadGrad* head = nullptr, bool g_bf16 = false);
+                 bool relu = true, bool y_bf16 = false, const HeadGrad* head = nullptr, bool g_bf16 = false,
+                 const PoolAdd* pool = nullptr);
 // out_split != nullptr: also the pooled output's split twin (dense, ld C); out may then be nullptr
 void maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float* out, uint8_t* idx,
                  hipStream_t st, void* out_split = nullptr);

@@ -123,12 +123,32 @@ struct BnCoef {
 };
 // HG: the upstream gradient is the depth head's, g[r][c] = dp[r] * w[c] with
 // dp = dpred * max_depth * s (1 - s) (k_head_da's values, rebuilt per row instead of read)
-// GB: g holds bf16 values (the bf16 engine's conv2 dgrad output)
-template <bool YB, bool HG = false, bool GB = false>
+// the folded max-pool backward (PoolAdd): row r of the full-resolution gradient receives the pooled
+// gradient of its window where r is that window's recorded argmax — the same fp32 add the scatter
+// (k_maxpool_bwd_scatter) makes
+__device__ __forceinline__ float4 pool_add(const PoolAdd& pa, int C, int64_t r, int c, float4 gv) {
+    const uint32_t rr = (uint32_t)r, W = (uint32_t)pa.W, H = (uint32_t)pa.H;
+    const uint32_t x = rr % W, t = rr / W, y = t % H, b = t / H;
+    const uint32_t op = (b * (H >> 1) + (y >> 1)) * (W >> 1) + (x >> 1);
+    const int k = (int)(((y & 1) << 1) | (x & 1));
+    const uchar4 a = *reinterpret_cast<const uchar4*>(pa.idx + (int64_t)op * C + c);
+    if (a.x == k || a.y == k || a.z == k || a.w == k) {
+        const float4 d = *reinterpret_cast<const float4*>(pa.d + (int64_t)op * C + c);
+        if (a.x == k) gv.x += d.x;
+        if (a.y == k) gv.y += d.y;
+        if (a.z == k) gv.z += d.z;
+        if (a.w == k) gv.w += d.w;
+    }
+    return gv;
+}
+
+// GB: g holds bf16 values (the bf16 engine's conv2 dgrad output); PA: max-pool backward folded in
+template <bool YB, bool HG = false, bool GB = false, bool PA = false>
 struct OpBnBwd {
     const float *g, *y, *mean, *invstd, *scale, *shift, *gmul;
     int64_t ldg; int gcoff, C; int64_t HW; bool relu;
     HeadGrad hg;
+    PoolAdd pa;
     __device__ BnCoef prep(int c4) const {
         BnCoef k;
 #pragma unroll
@@ -147,6 +167,7 @@ struct OpBnBwd {
             gv = make_float4(dp * k.hw[0], dp * k.hw[1], dp * k.hw[2], dp * k.hw[3]);
         } else {
             gv = load4<GB>(g, r * ldg + gcoff + c4 * 4);
+            if constexpr (PA) gv = pool_add(pa, C, r, c4 * 4, gv);
             if (gmul) {
                 const float4 m = *reinterpret_cast<const float4*>(gmul + (r / HW) * C + c4 * 4);
                 gv.x *= m.x; gv.y *= m.y; gv.z *= m.z; gv.w *= m.w;
@@ -361,7 +382,7 @@ __global__ void k_bn_bwd_coef(const double* tot, int C, int64_t M, const float* 
     coef[C + c] = (float)(k1 * sdz / (double)M);
     coef[2 * C + c] = (float)(k1 * sdzx / (double)M);
 }
-template <int NP, bool YB, bool HG, bool GB = false>
+template <int NP, bool YB, bool HG, bool GB = false, bool PA = false>
 __global__ __launch_bounds__(256) void k_bn_relu_bwd_rows(const float* __restrict__ g, int64_t ldg, int gcoff,
                                                           const float* __restrict__ y, int C,
                                                           const float* __restrict__ mean,
@@ -370,7 +391,8 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_rows(const float* __restric
                                                           const float* __restrict__ shift,
                                                           const float* __restrict__ coef, float* __restrict__ dy,
                                                           int64_t M, int64_t rps, const float* __restrict__ gmul,
-                                                          int64_t HW, char* __restrict__ os, bool relu, HeadGrad hg) {
+                                                          int64_t HW, char* __restrict__ os, bool relu, HeadGrad hg,
+                                                          PoolAdd pa) {
     const int c4 = blockIdx.x * blockDim.x + threadIdx.x;
     if (c4 >= (C >> 2)) return;
     const int c0 = c4 * 4;
@@ -390,6 +412,7 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_rows(const float* __restric
             gv = make_float4(dp * hw[0], dp * hw[1], dp * hw[2], dp * hw[3]);
         } else {
             gv = load4<GB>(g, r * ldg + gcoff + c0);
+            if constexpr (PA) gv = pool_add(pa, C, r, c0, gv);
             if (gmul) {
                 const float4 m = *reinterpret_cast<const float4*>(gmul + (r / HW) * C + c0);
                 gv.x *= m.x; gv.y *= m.y; gv.z *= m.z; gv.w *= m.w;
@@ -414,21 +437,36 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
                  const float* invstd, const float* scale, const float* shift, const float* gamma,
                  int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
                  hipStream_t st, const float* gmul, int64_t HW, void* dy_split, bool relu, bool y_bf16,
-                 const HeadGrad* head, bool g_bf16) {
+                 const HeadGrad* head, bool g_bf16, const PoolAdd* pool) {
     double* tot = scratch;
     double* part = scratch + 2 * C;
     const HeadGrad hg = head ? *head : HeadGrad{};
-    if (head && (g || gmul || g_bf16)) throw std::runtime_error("bn_relu_bwd: head gradient with an explicit gradient");
-    auto red = [&](auto yb, auto hgc, auto gbc) {
-        constexpr bool YB = decltype(yb)::value, HG = decltype(hgc)::value, GB = decltype(gbc)::value;
-        return launch_colreduce<2>(OpBnBwd<YB, HG, GB>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW, relu, hg},
-                                   M, C, part, st);
-    };
+    const PoolAdd pa = pool ? *pool : PoolAdd{};
+    if (head && (g || gmul || g_bf16 || pool)) throw std::runtime_error("bn_relu_bwd: head gradient with an explicit gradient");
+    if (pool && (g_bf16 || M >= ((int64_t)1 << 32) || pa.H <= 0 || pa.W <= 0 || ((pa.H | pa.W) & 1) ||
+                 M % ((int64_t)pa.H * pa.W) != 0))
+        throw std::runtime_error("bn_relu_bwd: folded max-pool backward layout");
+    // g source: 0 fp32, 1 head, 2 bf16, 3 fp32 + folded max-pool backward
+    const int gm = head ? 1 : g_bf16 ? 2 : pool ? 3 : 0;
     using T = std::true_type;
     using F = std::false_type;
-    const int S = head     ? (y_bf16 ? red(T{}, T{}, F{}) : red(F{}, T{}, F{}))
-                  : g_bf16 ? (y_bf16 ? red(T{}, F{}, T{}) : red(F{}, F{}, T{}))
-                           : (y_bf16 ? red(T{}, F{}, F{}) : red(F{}, F{}, F{}));
+    auto with_mode = [&](auto fn) {
+        switch (gm) {
+            case 1: return fn(T{}, F{}, F{});
+            case 2: return fn(F{}, T{}, F{});
+            case 3: return fn(F{}, F{}, T{});
+            default: return fn(F{}, F{}, F{});
+        }
+    };
+    const int S = with_mode([&](auto hgc, auto gbc, auto pac) {
+        constexpr bool HG = decltype(hgc)::value, GB = decltype(gbc)::value, PA = decltype(pac)::value;
+        return y_bf16 ? launch_colreduce<2>(OpBnBwd<true, HG, GB, PA>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C,
+                                                                     HW, relu, hg, pa},
+                                            M, C, part, st)
+                      : launch_colreduce<2>(OpBnBwd<false, HG, GB, PA>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff,
+                                                                      C, HW, relu, hg, pa},
+                                            M, C, part, st);
+    });
     launch_colfinal(part, S, 2 * C, tot, nullptr, 1.f, st);
     hipLaunchKernelGGL(k_bn_bwd_coef, dim3(cdiv(C, 64)), dim3(64), 0, st, tot, C, M, gamma, invstd, coef, dgamma, dbeta);
     const int np = dy_split ? split_planes() : 0;
@@ -436,18 +474,14 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
     const RowGrid rg = row_grid(M, C);
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(cdiv(C >> 2, rg.CX), rg.S), dim3(rg.CX, rg.RY), 0, st, g, ldg, gcoff, y, C, mean,
-                           invstd, scale, shift, coef, dy, M, rg.rps, gmul, HW, os, relu, hg);
+                           invstd, scale, shift, coef, dy, M, rg.rps, gmul, HW, os, relu, hg, pa);
     };
-    if (head) {
-        if (np == 1) y_bf16 ? go(k_bn_relu_bwd_rows<1, true, true>) : go(k_bn_relu_bwd_rows<1, false, true>);
-        else y_bf16 ? go(k_bn_relu_bwd_rows<0, true, true>) : go(k_bn_relu_bwd_rows<0, false, true>);
-    } else if (g_bf16) {
-        if (np == 1) y_bf16 ? go(k_bn_relu_bwd_rows<1, true, false, true>) : go(k_bn_relu_bwd_rows<1, false, false, true>);
-        else y_bf16 ? go(k_bn_relu_bwd_rows<0, true, false, true>) : go(k_bn_relu_bwd_rows<0, false, false, true>);
-    } else {
-        if (np == 1) y_bf16 ? go(k_bn_relu_bwd_rows<1, true, false>) : go(k_bn_relu_bwd_rows<1, false, false>);
-        else y_bf16 ? go(k_bn_relu_bwd_rows<0, true, false>) : go(k_bn_relu_bwd_rows<0, false, false>);
-    }
+    with_mode([&](auto hgc, auto gbc, auto pac) {
+        constexpr bool HG = decltype(hgc)::value, GB = decltype(gbc)::value, PA = decltype(pac)::value;
+        if (np == 1) y_bf16 ? go(k_bn_relu_bwd_rows<1, true, HG, GB, PA>) : go(k_bn_relu_bwd_rows<1, false, HG, GB, PA>);
+        else y_bf16 ? go(k_bn_relu_bwd_rows<0, true, HG, GB, PA>) : go(k_bn_relu_bwd_rows<0, false, HG, GB, PA>);
+        return 0;
+    });
 }
 
 // ------------------------------------------------------------------------------------------

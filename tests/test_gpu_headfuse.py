@@ -16,9 +16,9 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(tmp_path, fuse, args):
-    out = tmp_path / f"fuse{fuse}.pt"
-    env = dict(os.environ, CAD_HEADFUSE=str(fuse))
+def _run(tmp_path, fuse, args, var="CAD_HEADFUSE"):
+    out = tmp_path / f"{var}{fuse}.pt"
+    env = dict(os.environ, **{var: str(fuse)})
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "headfuse_ab.py"), *map(str, args), str(out)],
                    check=True, env=env, timeout=300)
     return torch.load(out, weights_only=True)
@@ -31,5 +31,17 @@ def test_head_fusion_bit_identical(tmp_path, kind, eng, f, B, H, W):
     a = _run(tmp_path, 0, (kind, eng, f, B, H, W))
     b = _run(tmp_path, 1, (kind, eng, f, B, H, W))
     assert a.keys() == b.keys()
+    bad = [k for k in a if not torch.equal(a[k], b[k])]
+    assert not bad, bad[:8]
+
+
+@pytest.mark.parametrize("kind,eng,f,B,H,W", [("baseline", 2, 16, 2, 64, 96), ("baseline", 1, 64, 2, 64, 64),
+                                              ("rayfilm", 2, 32, 2, 48, 64)])
+def test_pool_fold_bit_identical(tmp_path, kind, eng, f, B, H, W):
+    """The max-pool backward folded into the encoder's bn2 backward (nn_kernels.hip pool_add) makes
+    the scatter's fp32 add per element: two training steps with and without it (CAD_POOLFOLD=0)
+    agree bit for bit."""
+    a = _run(tmp_path, 0, (kind, eng, f, B, H, W), "CAD_POOLFOLD")
+    b = _run(tmp_path, 1, (kind, eng, f, B, H, W), "CAD_POOLFOLD")
     bad = [k for k in a if not torch.equal(a[k], b[k])]
     assert not bad, bad[:8]
