@@ -553,6 +553,13 @@ void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin,
                      twin ? const_cast<void*>(out_s.p) : nullptr, out_s.ld, out_s.coff, dc.y2b);
 }
 
+// CAD_DCATSPLIT=0: the decoder conv1 dgrad writes all of dcat in fp32 and the up half's twin is split
+// from it (A/B measurements; bit-identical)
+bool dcat_split_on() {
+    static const bool on = env_flag("CAD_DCATSPLIT", 1) != 0;
+    return on;
+}
+
 // CAD_POOLFOLD=0 keeps the max-pool backward scatter (A/B measurements; bit-identical)
 bool pool_fold_on() {
     static const bool on = env_flag("CAD_POOLFOLD", 1) != 0;
@@ -637,7 +644,8 @@ void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth
 // head != nullptr (level-0 fusion): g is null and bn2's upstream gradient is the head's, rebuilt per row.
 void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, int gcoff, const float* in,
                      int64_t ldin, cad::Split in_s, int B, float* din, int64_t lddin, hipStream_t st,
-                     const cad::HeadGrad* head = nullptr, const cad::PoolAdd* pool = nullptr) {
+                     const cad::HeadGrad* head = nullptr, const cad::PoolAdd* pool = nullptr, void* din_hi = nullptr,
+                     bool* din_hi_done = nullptr) {
     const int l = dc.level, Hh = h->Hl(l), Ww = h->Wl(l), C = dc.c1.cout;
     const int64_t M = h->Ml(l, B);
     const bool ps = h->fwd_np > 0 && h->fwd_np == cad::split_planes();
@@ -677,9 +685,12 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     else
         cad::conv3x3_wgrad(dY, C, in, ldin, 0, dc.c1.cin, h->G(dc.c1.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
     if (din) {
-        if (ps && dc.c1.wds)
-            cad::conv3x3_dgrad_ps(sv(dYs, C), C, sv(dc.c1.wds, 9 * C), dc.c1.cin, din, lddin, B, Hh, Ww, st);
-        else
+        // din_hi: the upper half of din's columns goes straight into that bf16 twin (decoder concat)
+        if (ps && dc.c1.wds) {
+            const bool done = cad::conv3x3_dgrad_ps(sv(dYs, C), C, sv(dc.c1.wds, 9 * C), dc.c1.cin, din, lddin, B, Hh, Ww,
+                                                    st, false, din_hi, dc.c1.cin / 2, dc.c1.cin / 2);
+            if (din_hi_done) *din_hi_done = done && din_hi;
+        } else
             cad::conv3x3_dgrad(dY, C, dc.c1.wd, dc.c1.cin, din, lddin, B, Hh, Ww, st);
     }
 }
@@ -726,13 +737,16 @@ void backward_stage(cad_unet* h, int stage, const float* dpred, hipStream_t st) 
         const int C = h->Cl(l);
         const cad::HeadGrad hg{dpred, h->sig, h->P(h->head_w), h->max_depth};
         const bool hf = l == 0 && h->head_fused;
+        // the bf16 engine's conv1 dgrad writes dcat's up half straight into its twin (dcats) when its
+        // window kernel runs; otherwise the twin is split from the fp32 half
+        bool up_twin = false;
         double_conv_bwd(h, h->dec[l], hf ? nullptr : h->Sa, C, 0, h->cat[l], 2 * C, sv(h->cats[l], 2 * C), B, h->dcat[l],
-                        2 * C, st, hf ? &hg : nullptr);
+                        2 * C, st, hf ? &hg : nullptr, nullptr, ps && dcat_split_on() ? h->dcats[l] : nullptr, &up_twin);
         const Up& u = h->up[l];
         const float* upin = l == 3 ? h->a2_bott : h->dout[l + 1];
         const void* upins = l == 3 ? h->botts : h->douts[l + 1];
         // up (ConvTranspose2d) backward: grad of its output = dcat[:, C:2C]
-        if (ps) cad::split_rows(h->dcat[l], 2 * C, C, C, h->Ml(l, B), h->dcats[l], C, 0, st);
+        if (ps && !up_twin) cad::split_rows(h->dcat[l], 2 * C, C, C, h->Ml(l, B), h->dcats[l], C, 0, st);
         if (ps) {
             cad::convT_wgrad_ps(sv(upins, u.cin), u.cin, sv(h->dcats[l], C), u.cout, h->G(u.widx), B, h->Hl(l + 1),
                                 h->Wl(l + 1), h->slab, h->slab_cap, st);
@@ -740,7 +754,9 @@ void backward_stage(cad_unet* h, int stage, const float* dpred, hipStream_t st) 
             cad::convT_wgrad(upin, u.cin, h->dcat[l], 2 * C, C, u.cout, h->G(u.widx), B, h->Hl(l + 1), h->Wl(l + 1),
                              h->slab, h->slab_cap, st);
         }
-        cad::colsum(h->dcat[l], 2 * C, C, h->Ml(l, B), C, h->dscr, st);
+        // ConvT bias gradient: on the bf16 engine the sum of the (bf16) gradient the ConvT GEMMs read
+        if (ps) cad::colsum_bf16(h->dcats[l], C, 0, h->Ml(l, B), C, h->dscr, st);
+        else cad::colsum(h->dcat[l], 2 * C, C, h->Ml(l, B), C, h->dscr, st);
         cad::colsum_finalize(h->dscr, cad::colsum_slices(h->Ml(l, B)), C, h->G(u.bidx), 1.f, st);
         if (ps)
             cad::convT_dgrad_ps(sv(h->dcats[l], C), u.cout, sv(u.wms, 4 * u.cout), u.cin, h->Sa, B, h->Hl(l + 1),

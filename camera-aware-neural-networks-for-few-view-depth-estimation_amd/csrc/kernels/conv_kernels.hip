@@ -791,8 +791,10 @@ void conv3x3_fwd_ps(Split x, int cin, Split w, int cout, float* y, int64_t ldy, 
     }
 }
 
-void conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t lddx, int B, int H, int W,
-                      hipStream_t st, bool dx_bf16) {
+bool conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t lddx, int B, int H, int W,
+                      hipStream_t st, bool dx_bf16, void* hi, int64_t ldhi, int split_n) {
+    // the split store needs 32-column blocks on one side of split_n; otherwise dx is written whole
+    if (hi && (dx_bf16 || split_n <= 0 || split_n % 32 || split_n >= cin || ldhi < cin - split_n)) hi = nullptr;
     ps_check(dz, cout, "conv3x3_dgrad dz");
     ps_check(wd, 9 * cout, "conv3x3_dgrad w");
     GemmArgs a{};
@@ -802,9 +804,14 @@ void conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t 
     a.Bm = (const float*)wd.p; a.ldb = wd.ld; a.b_coff = wd.coff;
     a.C = dx; a.ldc = lddx; a.c_coff = 0;
     if (const WinPick wp = pick_win_ps(cout, W, cin, dz.coff); wp.R && wd.coff == 0) {
+        if (hi) {
+            a.C2 = hi; a.ldc2 = ldhi; a.split_n = split_n;
+            launch_win<EpiStoreSplitB16, true>(wp, a, st);
+            return true;
+        }
         if (dx_bf16) launch_win<EpiStoreB16, true>(wp, a, st);
         else launch_win<EpiStore, true>(wp, a, st);
-        return;
+        return false;
     }
     const Cfg c = pick_cfg(a.M, a.N);
     const int kb = ps_kb(true, c);
@@ -812,6 +819,7 @@ void conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t 
     a.cimajor = cout % kb == 0;
     if (dx_bf16) launch_kb<KConvFwdP1B, 32, 64>(c, kb, a, 1, st);
     else launch_kb<KConvFwdP1, 32, 64>(c, kb, a, 1, st);
+    return false;
 }
 
 // B1 window weight gradient (conv3x3_wgrad_win_ps_body): stage = P pixels of an image row

@@ -11,6 +11,7 @@ struct EpiStore {
     static constexpr bool STATS = false;
     static constexpr bool BF16 = false;
     static constexpr bool ADD = false;
+    static constexpr bool SPLIT = false;
     __device__ static const float* row_base(const GemmArgs& a, int m0, int) {
         return a.C + (int64_t)m0 * a.ldc + a.c_coff;
     }
@@ -33,12 +34,19 @@ struct EpiStoreB16 {
     static constexpr bool STATS = false;
     static constexpr bool BF16 = true;
     static constexpr bool ADD = false;
+    static constexpr bool SPLIT = false;
     __device__ static const float* row_base(const GemmArgs& a, int m0, int) {
         return reinterpret_cast<const float*>(reinterpret_cast<const char*>(a.C) + ((int64_t)m0 * a.ldc + a.c_coff) * 2);
     }
 };
 struct EpiStoreStatsB16 : EpiStoreB16 {
     static constexpr bool STATS = true;
+};
+// window epilogue only: columns [0, split_n) fp32 into C, [split_n, N) bf16 into C2 (the decoder conv1
+// dgrad writes dcat's skip half for the encoder's BN backward and the up half straight into the twin
+// the ConvT gradients read)
+struct EpiStoreSplitB16 : EpiStore {
+    static constexpr bool SPLIT = true;
 };
 // ConvTranspose2d(k2,s2) pixel shuffle: n = (q=(dy,dx), co) -> high-res pixel (2y+dy, 2x+dx).
 // The column (q, co) is fixed per lane and sub-block, and rows advance in small steps, so the

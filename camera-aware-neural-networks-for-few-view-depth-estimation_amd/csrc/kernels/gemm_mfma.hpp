@@ -60,6 +60,9 @@ struct GemmArgs {
     // s % 9 of channel block s / 9, KB channels per block) instead of tap-major, so the nine taps of
     // a channel block re-read the same input rows back to back (L2 hits) — needs cin % KB == 0
     int cimajor;
+    // split store (EpiStoreSplitB16): output columns n >= split_n go to the bf16 rows C2 (ldc2 elements,
+    // column n - split_n) instead of C
+    void* C2; int64_t ldc2; int split_n;
 };
 
 

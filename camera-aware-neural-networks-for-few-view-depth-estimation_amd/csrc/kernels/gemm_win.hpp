@@ -125,6 +125,13 @@ __device__ __forceinline__ void win_epilogue(const GemmArgs& a, const floatx16 (
     const int64_t ldc4 = a.ldc * ES;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const float*>(
         reinterpret_cast<const char*>(a.C) + ((((int64_t)b * a.H + y0) * a.W + x0) * a.ldc + a.c_coff) * ES));
+    [[maybe_unused]] __amdgpu_buffer_rsrc_t rs2;
+    [[maybe_unused]] int64_t ldc2b = 0;
+    if constexpr (Epi::SPLIT) {
+        ldc2b = a.ldc2 * 2;
+        rs2 = make_rsrc(reinterpret_cast<const float*>(static_cast<const char*>(a.C2) +
+                                                       (((int64_t)b * a.H + y0) * a.W + x0) * ldc2b));
+    }
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -142,6 +149,17 @@ __device__ __forceinline__ void win_epilogue(const GemmArgs& a, const floatx16 (
                 if constexpr (Epi::BF16) {   // the stored (rounded) values, which BN then normalises
 #pragma unroll
                     for (int q = 0; q < 4; ++q) v[q] = (float)(__bf16)v[q];
+                }
+                if constexpr (Epi::SPLIT) {
+                    if (n >= a.split_n) {   // uniform per 32-column block (host: split_n % 32 == 0)
+                        const uint32_t lo2 =
+                            ok ? (uint32_t)((r * (int64_t)a.W + c) * ldc2b + (int64_t)(n - a.split_n) * 2) : kOOB;
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, (__bf16)v[q]), rs2,
+                                                                  lo2 + (uint32_t)(q * ldc2b), 0, 0);
+                        continue;
+                    }
                 }
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {

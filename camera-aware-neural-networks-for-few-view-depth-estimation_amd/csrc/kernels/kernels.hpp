@@ -55,9 +55,12 @@ void split_rows(const float* x, int64_t ldx, int xcoff, int C, int64_t M, void* 
 // y_bf16: y is written as bf16 rows of ldy elements (the bf16 engine's pre-BN outputs)
 void conv3x3_fwd_ps(Split x, int cin, Split w, int cout, float* y, int64_t ldy, int ycoff, int B, int H, int W,
                     float* stats, hipStream_t st, bool y_bf16 = false);
-// dx_bf16: dx is written as bf16 rows of lddx elements (the bf16 engine's conv2 input gradient)
-void conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t lddx, int B, int H, int W,
-                      hipStream_t st, bool dx_bf16 = false);
+// dx_bf16: dx is written as bf16 rows of lddx elements (the bf16 engine's conv2 input gradient).
+// hi != nullptr: columns [split_n, cin) go to the bf16 rows hi (ldhi elements) instead of dx when the
+// window kernel runs and split_n % 32 == 0 (returns true); otherwise all of dx is written as fp32
+// (returns false)
+bool conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t lddx, int B, int H, int W,
+                      hipStream_t st, bool dx_bf16 = false, void* hi = nullptr, int64_t ldhi = 0, int split_n = 0);
 void conv3x3_wgrad_ps(Split dz, int cout, Split x, int cin, float* dw, int B, int H, int W, float* slab,
                       int64_t slab_cap, hipStream_t st);
 // y_bf16: y is a bf16 twin (rows of ldy elements) — the up half of the decoder concat twin
@@ -128,6 +131,8 @@ void transpose_split(const float* w, int64_t ldw, int N, int K, void* wt, hipStr
 // column partial sums: part[s][c] (double) over row slices; returns number of slices
 int colsum_slices(int64_t R);
 void colsum(const float* x, int64_t ld, int coff, int64_t R, int C, double* part, hipStream_t st);
+// colsum of bf16 rows (x: bf16 elements, ld / coff in elements)
+void colsum_bf16(const void* x, int64_t ld, int coff, int64_t R, int C, double* part, hipStream_t st);
 void colsum_finalize(const double* part, int S, int C, float* dst, float scale, hipStream_t st);
 // BatchNorm2d (train mode) from conv-epilogue partials [rows][2][C]
 void bn_fwd_finalize(const float* tile_part, int rows, int C, int64_t count, const float* gamma,

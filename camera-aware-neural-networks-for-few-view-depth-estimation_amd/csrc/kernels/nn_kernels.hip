@@ -100,6 +100,14 @@ struct OpSum {
         acc[0][0] += v.x; acc[0][1] += v.y; acc[0][2] += v.z; acc[0][3] += v.w;
     }
 };
+struct OpSumB16 {
+    const float* x; int64_t ld; int coff;
+    __device__ NoPrep prep(int) const { return {}; }
+    __device__ void operator()(int64_t r, int c4, double (&acc)[1][4], NoPrep) const {
+        const float4 v = load4<true>(x, r * ld + coff + c4 * 4);
+        acc[0][0] += v.x; acc[0][1] += v.y; acc[0][2] += v.z; acc[0][3] += v.w;
+    }
+};
 // BN tile partials (BnTilePartials, gemm_mfma.hpp): per tile row r, S = part[r][c], M2 = part[r][C + c],
 // n = cnt[r]; column sums of S and of M2 + S^2 / n (= sum y^2 of the tile) in fp64
 struct OpBnTile {
@@ -245,6 +253,9 @@ int colsum_slices(int64_t R) { return (int)std::max<int64_t>(1, std::min<int64_t
 
 void colsum(const float* x, int64_t ld, int coff, int64_t R, int C, double* part, hipStream_t st) {
     launch_colreduce<1>(OpSum{x, ld, coff}, R, C, part, st);
+}
+void colsum_bf16(const void* x, int64_t ld, int coff, int64_t R, int C, double* part, hipStream_t st) {
+    launch_colreduce<1>(OpSumB16{static_cast<const float*>(x), ld, coff}, R, C, part, st);
 }
 void colsum_finalize(const double* part, int S, int C, float* dst, float scale, hipStream_t st) {
     launch_colfinal(part, S, C, nullptr, dst, scale, st);

@@ -345,10 +345,12 @@ def _conv3x3(x, w, name=None):
     return y + (forced.to(y.dtype) - y).detach()
 
 
-def _convT2x2(x, w, b):
+def _convT2x2(x, w, b, bias_bf16=False):
     if _GEMM["operands"] in ("bf16", "mx8"):   # (mx8: the config-5 fp8 network keeps its ConvTs on bf16)
-        y = _RoundGradOperand.apply(F.conv_transpose2d(_RoundOperand.apply(x), _RoundOperand.apply(w), None, stride=2))
-        return y + b.view(1, -1, 1, 1)
+        y = F.conv_transpose2d(_RoundOperand.apply(x), _RoundOperand.apply(w), None, stride=2)
+        if bias_bf16:   # U-Net family: the bias gradient sums the same bf16 gradient the GEMMs read
+            return _RoundGradOperand.apply(y + b.view(1, -1, 1, 1))
+        return _RoundGradOperand.apply(y) + b.view(1, -1, 1, 1)
     return F.conv_transpose2d(x, w, b, stride=2)
 
 
@@ -418,7 +420,7 @@ def _double_conv(x, p, bufs, pre, train, cam=None, da1_bf16=False):
 def _decoder(x, skip, p, bufs, pre, train, cam=None, da1_bf16=False):
     # DecoderBlockImpl::forward (baseline_unet.h:83-102): up, pad-if-needed, cat({skip, up}), conv
     # (FiLMDecoderBlockImpl::forward, intrinsics_unet.h:91-110, is the same with a FiLM conv)
-    x = _convT2x2(x, p[pre + "up.weight"], p[pre + "up.bias"])
+    x = _convT2x2(x, p[pre + "up.weight"], p[pre + "up.bias"], da1_bf16)
     dh, dw = skip.shape[2] - x.shape[2], skip.shape[3] - x.shape[3]
     if dh > 0 or dw > 0:
         x = F.pad(x, (dw // 2, dw - dw // 2, dh // 2, dh - dh // 2))
