@@ -645,7 +645,7 @@ void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth
 void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, int gcoff, const float* in,
                      int64_t ldin, cad::Split in_s, int B, float* din, int64_t lddin, hipStream_t st,
                      const cad::HeadGrad* head = nullptr, const cad::PoolAdd* pool = nullptr, void* din_hi = nullptr,
-                     bool* din_hi_done = nullptr) {
+                     bool* din_hi_done = nullptr, bool g_bf16 = false) {
     const int l = dc.level, Hh = h->Hl(l), Ww = h->Wl(l), C = dc.c1.cout;
     const int64_t M = h->Ml(l, B);
     const bool ps = h->fwd_np > 0 && h->fwd_np == cad::split_planes();
@@ -657,7 +657,7 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     // with pre-split GEMMs both consumers of dY2 read its twin: the fp32 dY2 is not written
     cad::bn_relu_bwd(g, ldg, gcoff, dc.y2, C, dc.b2.mean, dc.b2.invstd, dc.b2.scale, dc.b2.shift, h->P(dc.b2.widx), M,
                      h->dscr, dc.b2.coef, h->G(dc.b2.widx), h->G(dc.b2.bidx), ps ? nullptr : dY, st, nullptr, 1,
-                     ps ? dYs : nullptr, true, dc.y2b, head, false, pool);
+                     ps ? dYs : nullptr, true, dc.y2b, head, g_bf16, pool);
     // conv2: wgrad, dgrad
     if (ps) {
         cad::conv3x3_wgrad_ps(sv(dYs, C), C, sv(dc.a1s, C), C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
@@ -740,8 +740,10 @@ void backward_stage(cad_unet* h, int stage, const float* dpred, hipStream_t st) 
         // the bf16 engine's conv1 dgrad writes dcat's up half straight into its twin (dcats) when its
         // window kernel runs; otherwise the twin is split from the fp32 half
         bool up_twin = false;
+        // above level 0 the block-output gradient in Sa comes from the ConvT dgrad: bf16 on the bf16 engine
         double_conv_bwd(h, h->dec[l], hf ? nullptr : h->Sa, C, 0, h->cat[l], 2 * C, sv(h->cats[l], 2 * C), B, h->dcat[l],
-                        2 * C, st, hf ? &hg : nullptr, nullptr, ps && dcat_split_on() ? h->dcats[l] : nullptr, &up_twin);
+                        2 * C, st, hf ? &hg : nullptr, nullptr, ps && dcat_split_on() ? h->dcats[l] : nullptr, &up_twin,
+                        ps && l > 0);
         const Up& u = h->up[l];
         const float* upin = l == 3 ? h->a2_bott : h->dout[l + 1];
         const void* upins = l == 3 ? h->botts : h->douts[l + 1];
@@ -760,7 +762,7 @@ void backward_stage(cad_unet* h, int stage, const float* dpred, hipStream_t st) 
         cad::colsum_finalize(h->dscr, cad::colsum_slices(h->Ml(l, B)), C, h->G(u.bidx), 1.f, st);
         if (ps)
             cad::convT_dgrad_ps(sv(h->dcats[l], C), u.cout, sv(u.wms, 4 * u.cout), u.cin, h->Sa, B, h->Hl(l + 1),
-                                h->Wl(l + 1), st);
+                                h->Wl(l + 1), st, true);
         else
             cad::convT_dgrad(h->dcat[l], 2 * C, C, u.cout, h->P(u.widx), u.cin, h->Sa, B, h->Hl(l + 1), h->Wl(l + 1), st);
         return;
@@ -780,7 +782,9 @@ void backward_stage(cad_unet* h, int stage, const float* dpred, hipStream_t st) 
         return;
     }
     const int Cp = h->Cl(l - 1);
-    double_conv_bwd(h, e, g, ldg, 0, h->pool[l], Cp, sv(h->pools[l], Cp), B, h->Sc, Cp, st, nullptr, pool);
+    // the bottleneck's output gradient (Sa) comes from dec4's ConvT dgrad: bf16 on the bf16 engine
+    double_conv_bwd(h, e, g, ldg, 0, h->pool[l], Cp, sv(h->pools[l], Cp), B, h->Sc, Cp, st, nullptr, pool, nullptr,
+                    nullptr, ps && l == 4);
     // max-pool backward: the pooled gradient is added at the recorded argmax of dcat's skip half
     // (folded into the next stage's bn2 backward unless CAD_POOLFOLD=0)
     if (!pool_fold_on())

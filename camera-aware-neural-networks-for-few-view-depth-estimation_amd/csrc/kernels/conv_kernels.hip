@@ -187,13 +187,13 @@ __device__ __forceinline__ void convT_fwd_psb(const GemmArgs& a) {
         a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.M, a.K, r0, t, kb); },
         [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, Epi{});
 }
-template <int NP, int WM, int WN, int MI, int NJ, int KB>
+template <int NP, int WM, int WN, int MI, int NJ, int KB, class Epi = EpiStore>
 __device__ __forceinline__ void convT_dgrad_psb(const GemmArgs& a) {
     using LA = PsKcUpGather<32 * MI * WM, KB, NP>;
     using LB = PsKcDense<32 * NJ * WN, KB, NP>;
     gemm_body_ps<NP, WM, WN, MI, NJ, KB, LA, LB>(
         a, [&](LA& l, int r0, int t, int kb) { l.init(a.A, a.lda, a.a_coff, a.a_cin, a.B, a.H, a.W, r0, t, kb); },
-        [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, EpiStore{});
+        [&](LB& l, int r0, int t, int kb) { l.init(a.Bm, a.ldb, a.b_coff, a.N, a.K, r0, t, kb); }, Epi{});
 }
 template <int NP, int WM, int WN, int MI, int NJ, int KB>
 __device__ __forceinline__ void conv3x3_wgrad_psb(const GemmArgs& a) {
@@ -245,6 +245,10 @@ __global__ __launch_bounds__(256) void k_convT_fwd_bf16pt(GemmArgs a) {
 }
 template <int WM, int WN, int KB>
 __global__ __launch_bounds__(256) void k_convT_dgrad_bf16p(GemmArgs a) { convT_dgrad_psb<1, WM, WN, 2, 2, KB>(a); }
+template <int WM, int WN, int KB>
+__global__ __launch_bounds__(256) void k_convT_dgrad_bf16pb(GemmArgs a) {
+    convT_dgrad_psb<1, WM, WN, 2, 2, KB, EpiStoreB16>(a);
+}
 template <int WM, int WN, int KB>
 __global__ __launch_bounds__(256) void k_conv3x3_wgrad_bf16p(GemmArgs a) { conv3x3_wgrad_psb<1, WM, WN, 2, 2, KB>(a); }
 template <int WM, int WN, int KB>
@@ -390,6 +394,7 @@ CAD_KT(KConvFwdSP1B, (k_conv3x3_fwd_bf16p<WM, WN, KB, EpiStoreStatsB16>),
        "void cad::k_conv3x3_fwd_bf16p<%d, %d, %d, cad::EpiStoreStatsB16>(cad::GemmArgs)")
 CAD_KT(KDenseWgradP1, (k_dense_wgrad_bf16p<WM, WN, KB>), "void cad::k_dense_wgrad_bf16p<%d, %d, %d>(cad::GemmArgs)")
 CAD_KT(KConvTFwdP1T, (k_convT_fwd_bf16pt<WM, WN, KB>), "void cad::k_convT_fwd_bf16pt<%d, %d, %d>(cad::GemmArgs)")
+CAD_KT(KConvTDgradP1B, (k_convT_dgrad_bf16pb<WM, WN, KB>), "void cad::k_convT_dgrad_bf16pb<%d, %d, %d>(cad::GemmArgs)")
 CAD_KT(KDenseAddP1, (k_dense_bf16p<WM, WN, KB, EpiStoreAdd>), "void cad::k_dense_bf16p<%d, %d, %d, cad::EpiStoreAdd>(cad::GemmArgs)")
 // in-loader split engines: KConvFwd3 ... (S3), KConvFwdB ... (B1); pre-split B1: KConvFwdP1 ...
 CAD_NP_KT(s3, 3)
@@ -989,7 +994,7 @@ void convT_fwd_ps(Split x, int cin, Split wf, const float* bias, int cout, float
     else launch_kb<KConvTFwdP1, 32>(c, kb, a, 1, st);
 }
 
-void convT_dgrad_ps(Split g, int cout, Split wm, int cin, float* dx, int B, int H, int W, hipStream_t st) {
+void convT_dgrad_ps(Split g, int cout, Split wm, int cin, float* dx, int B, int H, int W, hipStream_t st, bool dx_bf16) {
     ps_check(g, cout, "convT_dgrad g");
     ps_check(wm, 4 * cout, "convT_dgrad w");
     GemmArgs a{};
@@ -1001,7 +1006,8 @@ void convT_dgrad_ps(Split g, int cout, Split wm, int cin, float* dx, int B, int 
     const Cfg c = pick_cfg(a.M, a.N);
     const int kb = ps_kb(false, c);
     a.kstages_per_split = cdiv(a.K, kb);
-    launch_kb<KConvTDgradP1, 32>(c, kb, a, 1, st);
+    if (dx_bf16) launch_kb<KConvTDgradP1B, 32>(c, kb, a, 1, st);
+    else launch_kb<KConvTDgradP1, 32>(c, kb, a, 1, st);
 }
 
 void convT_wgrad_ps(Split x, int cin, Split g, int cout, float* dw, int B, int H, int W, float* slab,

@@ -66,7 +66,9 @@ void conv3x3_wgrad_ps(Split dz, int cout, Split x, int cin, float* dw, int B, in
 // y_bf16: y is a bf16 twin (rows of ldy elements) — the up half of the decoder concat twin
 void convT_fwd_ps(Split x, int cin, Split wf, const float* bias, int cout, float* y, int64_t ldy, int ycoff, int B,
                   int H, int W, hipStream_t st, bool y_bf16 = false);
-void convT_dgrad_ps(Split g, int cout, Split wm, int cin, float* dx, int B, int H, int W, hipStream_t st);
+// dx_bf16: dx written as bf16 rows of cin elements (the bf16 engine's decoder-input gradient)
+void convT_dgrad_ps(Split g, int cout, Split wm, int cin, float* dx, int B, int H, int W, hipStream_t st,
+                    bool dx_bf16 = false);
 void convT_wgrad_ps(Split x, int cin, Split g, int cout, float* dw, int B, int H, int W, float* slab,
                     int64_t slab_cap, hipStream_t st);
 

@@ -420,6 +420,10 @@ def _double_conv(x, p, bufs, pre, train, cam=None, da1_bf16=False):
 def _decoder(x, skip, p, bufs, pre, train, cam=None, da1_bf16=False):
     # DecoderBlockImpl::forward (baseline_unet.h:83-102): up, pad-if-needed, cat({skip, up}), conv
     # (FiLMDecoderBlockImpl::forward, intrinsics_unet.h:91-110, is the same with a FiLM conv)
+    if da1_bf16 and _GEMM["operands"] == "bf16":
+        # the U-Net family's bf16 engine stores the ConvT's input gradient (its dgrad output: the
+        # gradient of the block below's output, read by that block's bn2 backward) as bf16
+        x = _RoundGradOperand.apply(x)
     x = _convT2x2(x, p[pre + "up.weight"], p[pre + "up.bias"], da1_bf16)
     dh, dw = skip.shape[2] - x.shape[2], skip.shape[3] - x.shape[3]
     if dh > 0 or dw > 0:
