@@ -191,6 +191,7 @@ struct cad_unet {
     void* botts = nullptr;
     void* douts[4] = {};          // l = 1..3 (dout[0] feeds only the head)
     void* dcats[4] = {};          // up half of dcat, [M_l][C_l]
+    void* dskips[4] = {};         // skip half of dcat, [M_l][C_l] (the bf16 engine's encoder bn2 gradient)
     void* dYs = nullptr;          // split dL/dz scratch (largest level)
     int fwd_np = 0;
     // the last forward ran decoder level 0's bn2 + ReLU fused with the head (head_fusable): dout[0]
@@ -387,6 +388,7 @@ void layout(cad_unet* h, Arena& a) {
         h->up[l].wms = sp((int64_t)4 * h->up[l].cout * h->up[l].cin);
         h->dcat[l] = a.f(2 * MC);
         h->dcats[l] = sp(MC);
+        h->dskips[l] = sp(MC);
     }
     h->x0 = a.f(h->Ml(0, B) * h->x0_ld);
     if (h->x0_ld % 8 == 0) h->x0s = sp(h->Ml(0, B) * h->x0_ld);
@@ -645,7 +647,7 @@ void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth
 void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, int gcoff, const float* in,
                      int64_t ldin, cad::Split in_s, int B, float* din, int64_t lddin, hipStream_t st,
                      const cad::HeadGrad* head = nullptr, const cad::PoolAdd* pool = nullptr, void* din_hi = nullptr,
-                     bool* din_hi_done = nullptr, bool g_bf16 = false) {
+                     bool* din_hi_done = nullptr, bool g_bf16 = false, bool din_bf16 = false) {
     const int l = dc.level, Hh = h->Hl(l), Ww = h->Wl(l), C = dc.c1.cout;
     const int64_t M = h->Ml(l, B);
     const bool ps = h->fwd_np > 0 && h->fwd_np == cad::split_planes();
@@ -688,7 +690,7 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
         // din_hi: the upper half of din's columns goes straight into that bf16 twin (decoder concat)
         if (ps && dc.c1.wds) {
             const bool done = cad::conv3x3_dgrad_ps(sv(dYs, C), C, sv(dc.c1.wds, 9 * C), dc.c1.cin, din, lddin, B, Hh, Ww,
-                                                    st, false, din_hi, dc.c1.cin / 2, dc.c1.cin / 2);
+                                                    st, din_bf16, din_hi, dc.c1.cin / 2, dc.c1.cin / 2);
             if (din_hi_done) *din_hi_done = done && din_hi;
         } else
             cad::conv3x3_dgrad(dY, C, dc.c1.wd, dc.c1.cin, din, lddin, B, Hh, Ww, st);
@@ -737,18 +739,26 @@ void backward_stage(cad_unet* h, int stage, const float* dpred, hipStream_t st) 
         const int C = h->Cl(l);
         const cad::HeadGrad hg{dpred, h->sig, h->P(h->head_w), h->max_depth};
         const bool hf = l == 0 && h->head_fused;
-        // the bf16 engine's conv1 dgrad writes dcat's up half straight into its twin (dcats) when its
-        // window kernel runs; otherwise the twin is split from the fp32 half
+        // the bf16 engine keeps dcat as two bf16 halves: the skip half (dskips, the encoder bn2 gradient)
+        // and the up half (dcats, the ConvT GEMMs' operand).  The conv1 dgrad writes both straight from
+        // its window kernel when the shape allows (split store); otherwise it writes dcat in fp32 and the
+        // halves are split from it (same rounding)
+        const bool split = ps && dcat_split_on() &&
+                           cad::conv3x3_dgrad_split_ok(sv(h->dYs, C), C, sv(h->dec[l].c1.wds, 9 * C), 2 * C, h->Wl(l), C);
         bool up_twin = false;
         // above level 0 the block-output gradient in Sa comes from the ConvT dgrad: bf16 on the bf16 engine
-        double_conv_bwd(h, h->dec[l], hf ? nullptr : h->Sa, C, 0, h->cat[l], 2 * C, sv(h->cats[l], 2 * C), B, h->dcat[l],
-                        2 * C, st, hf ? &hg : nullptr, nullptr, ps && dcat_split_on() ? h->dcats[l] : nullptr, &up_twin,
-                        ps && l > 0);
+        double_conv_bwd(h, h->dec[l], hf ? nullptr : h->Sa, C, 0, h->cat[l], 2 * C, sv(h->cats[l], 2 * C), B,
+                        split ? static_cast<float*>(h->dskips[l]) : h->dcat[l], split ? C : 2 * C, st,
+                        hf ? &hg : nullptr, nullptr, split ? h->dcats[l] : nullptr, &up_twin, ps && l > 0, split);
+        if (split != up_twin) throw std::runtime_error("decoder dgrad split store not taken");
         const Up& u = h->up[l];
         const float* upin = l == 3 ? h->a2_bott : h->dout[l + 1];
         const void* upins = l == 3 ? h->botts : h->douts[l + 1];
         // up (ConvTranspose2d) backward: grad of its output = dcat[:, C:2C]
-        if (ps && !up_twin) cad::split_rows(h->dcat[l], 2 * C, C, C, h->Ml(l, B), h->dcats[l], C, 0, st);
+        if (ps && !split) {
+            cad::split_rows(h->dcat[l], 2 * C, C, C, h->Ml(l, B), h->dcats[l], C, 0, st);
+            cad::split_rows(h->dcat[l], 2 * C, 0, C, h->Ml(l, B), h->dskips[l], C, 0, st);
+        }
         if (ps) {
             cad::convT_wgrad_ps(sv(upins, u.cin), u.cin, sv(h->dcats[l], C), u.cout, h->G(u.widx), B, h->Hl(l + 1),
                                 h->Wl(l + 1), h->slab, h->slab_cap, st);
@@ -771,23 +781,28 @@ void backward_stage(cad_unet* h, int stage, const float* dpred, hipStream_t st) 
     const int l = 4 - (stage - 5);
     DoubleConv& e = h->enc[l];
     const int C = h->Cl(l);
-    const float* g = l == 4 ? h->Sa : h->dcat[l];
-    const int64_t ldg = l == 4 ? C : 2 * C;
+    // bn2's gradient: the bottleneck's from dec4's ConvT dgrad (Sa), the others the skip half of dcat
+    // (bf16 in dskips on the bf16 engine)
+    const float* g = l == 4 ? h->Sa : ps ? static_cast<const float*>(h->dskips[l]) : h->dcat[l];
+    const int64_t ldg = l == 4 || ps ? C : 2 * C;
     // the max-pool backward of the level below (its pooled gradient in Sc, written by the previous
     // stage) is folded into this block's bn2 backward instead of scattered into dcat beforehand
+    // (always on the bf16 engine, whose skip gradient is bf16)
+    const bool fold = pool_fold_on() || ps;
     const cad::PoolAdd pa{h->Sc, h->pidx[l + 1], h->Hl(l), h->Wl(l)};
-    const cad::PoolAdd* pool = l < 4 && pool_fold_on() ? &pa : nullptr;
+    const cad::PoolAdd* pool = l < 4 && fold ? &pa : nullptr;
     if (l == 0) {
-        double_conv_bwd(h, e, g, ldg, 0, h->x0, h->x0_ld, sv(h->x0s, h->x0_ld), B, nullptr, 0, st, nullptr, pool);
+        double_conv_bwd(h, e, g, ldg, 0, h->x0, h->x0_ld, sv(h->x0s, h->x0_ld), B, nullptr, 0, st, nullptr, pool, nullptr,
+                        nullptr, ps);
         return;
     }
     const int Cp = h->Cl(l - 1);
     // the bottleneck's output gradient (Sa) comes from dec4's ConvT dgrad: bf16 on the bf16 engine
     double_conv_bwd(h, e, g, ldg, 0, h->pool[l], Cp, sv(h->pools[l], Cp), B, h->Sc, Cp, st, nullptr, pool, nullptr,
-                    nullptr, ps && l == 4);
+                    nullptr, ps);
     // max-pool backward: the pooled gradient is added at the recorded argmax of dcat's skip half
     // (folded into the next stage's bn2 backward unless CAD_POOLFOLD=0)
-    if (!pool_fold_on())
+    if (!fold)
         cad::maxpool_bwd(h->Sc, h->pidx[l], Cp, B, h->Hl(l - 1), h->Wl(l - 1), h->dcat[l - 1], 2 * Cp, st);
 }
 

@@ -796,10 +796,18 @@ void conv3x3_fwd_ps(Split x, int cin, Split w, int cout, float* y, int64_t ldy, 
     }
 }
 
+bool conv3x3_dgrad_split_ok(Split dz, int cout, Split wd, int cin, int W, int split_n) {
+    return split_n > 0 && split_n % 32 == 0 && split_n < cin && pick_win_ps(cout, W, cin, dz.coff).R && wd.coff == 0;
+}
+
 bool conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t lddx, int B, int H, int W,
                       hipStream_t st, bool dx_bf16, void* hi, int64_t ldhi, int split_n) {
     // the split store needs 32-column blocks on one side of split_n; otherwise dx is written whole
-    if (hi && (dx_bf16 || split_n <= 0 || split_n % 32 || split_n >= cin || ldhi < cin - split_n)) hi = nullptr;
+    // (in fp32: a bf16 lower half needs the split, conv3x3_dgrad_split_ok)
+    if (hi && (!conv3x3_dgrad_split_ok(dz, cout, wd, cin, W, split_n) || ldhi < cin - split_n)) {
+        if (dx_bf16) throw std::runtime_error("conv3x3_dgrad_ps: bf16 split store not possible for this shape");
+        hi = nullptr;
+    }
     ps_check(dz, cout, "conv3x3_dgrad dz");
     ps_check(wd, 9 * cout, "conv3x3_dgrad w");
     GemmArgs a{};
@@ -811,7 +819,8 @@ bool conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t 
     if (const WinPick wp = pick_win_ps(cout, W, cin, dz.coff); wp.R && wd.coff == 0) {
         if (hi) {
             a.C2 = hi; a.ldc2 = ldhi; a.split_n = split_n;
-            launch_win<EpiStoreSplitB16, true>(wp, a, st);
+            if (dx_bf16) launch_win<EpiStoreSplit2B16, true>(wp, a, st);
+            else launch_win<EpiStoreSplitB16, true>(wp, a, st);
             return true;
         }
         if (dx_bf16) launch_win<EpiStoreB16, true>(wp, a, st);

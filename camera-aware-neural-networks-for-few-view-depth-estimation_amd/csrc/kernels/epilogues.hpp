@@ -48,6 +48,10 @@ struct EpiStoreStatsB16 : EpiStoreB16 {
 struct EpiStoreSplitB16 : EpiStore {
     static constexpr bool SPLIT = true;
 };
+// ... with the lower columns also bf16 (C: bf16 rows of ldc elements)
+struct EpiStoreSplit2B16 : EpiStoreB16 {
+    static constexpr bool SPLIT = true;
+};
 // ConvTranspose2d(k2,s2) pixel shuffle: n = (q=(dy,dx), co) -> high-res pixel (2y+dy, 2x+dx).
 // The column (q, co) is fixed per lane and sub-block, and rows advance in small steps, so the
 // epilogue carries (x, y, b) incrementally instead of dividing per element (STRUCTURED epilogue).

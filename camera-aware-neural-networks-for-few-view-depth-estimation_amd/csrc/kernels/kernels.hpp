@@ -59,8 +59,10 @@ void conv3x3_fwd_ps(Split x, int cin, Split w, int cout, float* y, int64_t ldy, 
 // hi != nullptr: columns [split_n, cin) go to the bf16 rows hi (ldhi elements) instead of dx when the
 // window kernel runs and split_n % 32 == 0 (returns true); otherwise all of dx is written as fp32
 // (returns false)
+// (with dx_bf16 as well: both halves bf16, dx rows of lddx elements; requires conv3x3_dgrad_split_ok)
 bool conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t lddx, int B, int H, int W,
                       hipStream_t st, bool dx_bf16 = false, void* hi = nullptr, int64_t ldhi = 0, int split_n = 0);
+bool conv3x3_dgrad_split_ok(Split dz, int cout, Split wd, int cin, int W, int split_n);
 void conv3x3_wgrad_ps(Split dz, int cout, Split x, int cin, float* dw, int B, int H, int W, float* slab,
                       int64_t slab_cap, hipStream_t st);
 // y_bf16: y is a bf16 twin (rows of ldy elements) — the up half of the decoder concat twin

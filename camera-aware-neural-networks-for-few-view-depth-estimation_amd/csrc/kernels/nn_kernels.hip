@@ -454,11 +454,11 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
     const HeadGrad hg = head ? *head : HeadGrad{};
     const PoolAdd pa = pool ? *pool : PoolAdd{};
     if (head && (g || gmul || g_bf16 || pool)) throw std::runtime_error("bn_relu_bwd: head gradient with an explicit gradient");
-    if (pool && (g_bf16 || M >= ((int64_t)1 << 32) || pa.H <= 0 || pa.W <= 0 || ((pa.H | pa.W) & 1) ||
+    if (pool && (M >= ((int64_t)1 << 32) || pa.H <= 0 || pa.W <= 0 || ((pa.H | pa.W) & 1) ||
                  M % ((int64_t)pa.H * pa.W) != 0))
         throw std::runtime_error("bn_relu_bwd: folded max-pool backward layout");
-    // g source: 0 fp32, 1 head, 2 bf16, 3 fp32 + folded max-pool backward
-    const int gm = head ? 1 : g_bf16 ? 2 : pool ? 3 : 0;
+    // g source: 0 fp32, 1 head, 2 bf16, 3 fp32 + folded max-pool backward, 4 bf16 + folded max-pool backward
+    const int gm = head ? 1 : (g_bf16 && pool) ? 4 : g_bf16 ? 2 : pool ? 3 : 0;
     using T = std::true_type;
     using F = std::false_type;
     auto with_mode = [&](auto fn) {
@@ -466,6 +466,7 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
             case 1: return fn(T{}, F{}, F{});
             case 2: return fn(F{}, T{}, F{});
             case 3: return fn(F{}, F{}, T{});
+            case 4: return fn(F{}, T{}, T{});
             default: return fn(F{}, F{}, F{});
         }
     };

@@ -428,6 +428,10 @@ def _decoder(x, skip, p, bufs, pre, train, cam=None, da1_bf16=False):
     dh, dw = skip.shape[2] - x.shape[2], skip.shape[3] - x.shape[3]
     if dh > 0 or dw > 0:
         x = F.pad(x, (dw // 2, dw - dw // 2, dh // 2, dh - dh // 2))
+    if da1_bf16 and _GEMM["operands"] == "bf16":
+        # ... and the skip half of the concat's gradient (the decoder conv1 dgrad's lower columns), to
+        # which the max-pool path's fp32 gradient is then added
+        skip = _RoundGradOperand.apply(skip)
     return _double_conv(torch.cat([skip, x], 1), p, bufs, pre + "conv.", train, cam, da1_bf16)
 
 

@@ -35,14 +35,17 @@ def test_head_fusion_bit_identical(tmp_path, kind, eng, f, B, H, W):
     assert not bad, bad[:8]
 
 
-@pytest.mark.parametrize("var", ["CAD_POOLFOLD", "CAD_DCATSPLIT"])
-@pytest.mark.parametrize("kind,eng,f,B,H,W", [("baseline", 2, 16, 2, 64, 96), ("baseline", 1, 64, 2, 64, 64),
-                                              ("rayfilm", 1, 32, 2, 48, 64)])
+@pytest.mark.parametrize("var,kind,eng,f,B,H,W", [("CAD_POOLFOLD", "baseline", 2, 16, 2, 64, 96),
+                                                  ("CAD_POOLFOLD", "rayfilm", 2, 32, 2, 48, 64),
+                                                  ("CAD_DCATSPLIT", "baseline", 1, 64, 2, 64, 64),
+                                                  ("CAD_DCATSPLIT", "rayfilm", 1, 32, 2, 48, 64),
+                                                  ("CAD_DCATSPLIT", "film", 1, 16, 2, 64, 96)])
 def test_backward_fusions_bit_identical(tmp_path, var, kind, eng, f, B, H, W):
-    """CAD_POOLFOLD: the max-pool backward folded into the encoder's bn2 backward (nn_kernels.hip
-    pool_add) makes the scatter's fp32 add per element.  CAD_DCATSPLIT: the decoder conv1 dgrad writes
-    dcat's up half straight into its bf16 twin (EpiStoreSplitB16) with the rounding split_rows applies.
-    Two training steps with and without each agree bit for bit."""
+    """CAD_POOLFOLD (fp32 engines; the bf16 engine always folds): the max-pool backward folded into the
+    encoder's bn2 backward (nn_kernels.hip pool_add) makes the scatter's fp32 add per element.
+    CAD_DCATSPLIT (bf16 engine): the decoder conv1 dgrad writes dcat's two halves straight into their
+    bf16 buffers (EpiStoreSplit2B16) with the rounding split_rows applies.  Two training steps with
+    and without each agree bit for bit."""
     a = _run(tmp_path, 0, (kind, eng, f, B, H, W), var)
     b = _run(tmp_path, 1, (kind, eng, f, B, H, W), var)
     bad = [k for k in a if not torch.equal(a[k], b[k])]
