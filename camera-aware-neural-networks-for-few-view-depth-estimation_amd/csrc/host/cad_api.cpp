@@ -603,17 +603,19 @@ void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth
         cad::split_rows(h->x0, h->x0_ld, 0, h->x0_ld, h->Ml(0, B), h->x0s, h->x0_ld, 0, st);
         x0s = sv(h->x0s, h->x0_ld);
     }
-    double_conv_fwd(h, h->enc[0], h->x0, h->x0_ld, x0s, B, h->cat[0], 2 * f, 0, sv(h->cats[0], 2 * f), st);
+    // on the bf16 engine the encoder outputs are written only as the concat twin: the max-pool reads
+    // it (the decoder conv1 and its gradients read it anyway)
+    double_conv_fwd(h, h->enc[0], h->x0, h->x0_ld, x0s, B, h->cat[0], 2 * f, 0, sv(h->cats[0], 2 * f), st, !ps);
     for (int l = 1; l <= 4; ++l) {
         const int Cp = h->Cl(l - 1);
         // pre-split GEMMs read only the pooled twin (enc conv1 and its weight gradient)
         const bool ptwin = ps && h->pools[l];
-        cad::maxpool_fwd(h->cat[l - 1], 2 * Cp, Cp, B, h->Hl(l - 1), h->Wl(l - 1), ptwin ? nullptr : h->pool[l],
-                         h->pidx[l], st, ptwin ? h->pools[l] : nullptr);
+        cad::maxpool_fwd(ps ? static_cast<const float*>(h->cats[l - 1]) : h->cat[l - 1], 2 * Cp, Cp, B, h->Hl(l - 1),
+                         h->Wl(l - 1), ptwin ? nullptr : h->pool[l], h->pidx[l], st, ptwin ? h->pools[l] : nullptr, ps);
         const cad::Split pin = sv(h->pools[l], Cp);
         if (l < 4)
             double_conv_fwd(h, h->enc[l], h->pool[l], Cp, pin, B, h->cat[l], 2 * h->Cl(l), 0,
-                            sv(h->cats[l], 2 * h->Cl(l)), st);
+                            sv(h->cats[l], 2 * h->Cl(l)), st, !ps);
         else
             double_conv_fwd(h, h->enc[4], h->pool[4], Cp, pin, B, h->a2_bott, h->Cl(4), 0, sv(h->botts, h->Cl(4)), st,
                             false);

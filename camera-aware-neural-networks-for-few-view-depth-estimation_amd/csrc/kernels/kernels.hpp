@@ -179,8 +179,9 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
                  bool relu = true, bool y_bf16 = false, const HeadGrad* head = nullptr, bool g_bf16 = false,
                  const PoolAdd* pool = nullptr);
 // out_split != nullptr: also the pooled output's split twin (dense, ld C); out may then be nullptr
+// x_bf16: x is a bf16 twin (rows of ldx elements; requires out_split)
 void maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float* out, uint8_t* idx,
-                 hipStream_t st, void* out_split = nullptr);
+                 hipStream_t st, void* out_split = nullptr, bool x_bf16 = false);
 void maxpool_bwd(const float* dout, const uint8_t* idx, int C, int B, int H, int W, float* dx,
                  int64_t lddx, hipStream_t st);
 void rgb_to_nhwc4(const float* rgb, float* out, int B, int H, int W, hipStream_t st);

@@ -499,7 +499,10 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
 // ------------------------------------------------------------------------------------------
 // MaxPool2d(2) (baseline_unet.h:55 / :62), argmax kept as uint8 in scan order 0..3
 // ------------------------------------------------------------------------------------------
-template <int NP>
+// XB: x holds bf16 values (the bf16 engine pools the encoder outputs' twin: bf16 rounding is
+// monotone, so the pooled twin equals the one of the fp32 maximum; ties of the rounded values go to
+// the first in scan order)
+template <int NP, bool XB = false>
 __global__ void k_maxpool_fwd(const float* __restrict__ x, int64_t ldx, int C, int B, int H, int W,
                               float* __restrict__ out, uint8_t* __restrict__ idx, int64_t n4, char* __restrict__ os) {
     const uint32_t C4 = (uint32_t)C >> 2, Ho = (uint32_t)H >> 1, Wo = (uint32_t)W >> 1;   // n4 < 2^31 (host)
@@ -515,12 +518,12 @@ __global__ void k_maxpool_fwd(const float* __restrict__ x, int64_t ldx, int C, i
         float best[4];
         uint8_t arg[4] = {0, 0, 0, 0};
         {
-            float4 v = *reinterpret_cast<const float4*>(x + pp[0] * ldx + c);
+            const float4 v = load4<XB>(x, pp[0] * ldx + c);
             best[0] = v.x; best[1] = v.y; best[2] = v.z; best[3] = v.w;
         }
 #pragma unroll
         for (int k = 1; k < 4; ++k) {
-            float4 v = *reinterpret_cast<const float4*>(x + pp[k] * ldx + c);
+            const float4 v = load4<XB>(x, pp[k] * ldx + c);
             const float va[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int e = 0; e < 4; ++e)
@@ -533,12 +536,16 @@ __global__ void k_maxpool_fwd(const float* __restrict__ x, int64_t ldx, int C, i
     }
 }
 void maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float* out, uint8_t* idx,
-                 hipStream_t st, void* out_split) {
+                 hipStream_t st, void* out_split, bool x_bf16) {
     const int64_t n4 = (int64_t)B * (H / 2) * (W / 2) * C / 4;
     if (n4 >= ((int64_t)1 << 31)) throw std::runtime_error("maxpool_fwd: tensor too large for 32-bit indexing");
     const int np = out_split ? split_planes() : 0;
     char* os = static_cast<char*>(out_split);
-    if (np == 1)
+    if (x_bf16 && np != 1) throw std::runtime_error("maxpool_fwd: bf16 input needs the twin output");
+    if (x_bf16)
+        hipLaunchKernelGGL((k_maxpool_fwd<1, true>), dim3(ew_blocks(n4)), dim3(256), 0, st, x, ldx, C, B, H, W, out, idx,
+                           n4, os);
+    else if (np == 1)
         hipLaunchKernelGGL(k_maxpool_fwd<1>, dim3(ew_blocks(n4)), dim3(256), 0, st, x, ldx, C, B, H, W, out, idx, n4, os);
     else
         hipLaunchKernelGGL(k_maxpool_fwd<0>, dim3(ew_blocks(n4)), dim3(256), 0, st, x, ldx, C, B, H, W, out, idx, n4, os);

@@ -524,10 +524,14 @@ def unet_forward(x, p, bufs, train=True, max_depth=10.0, model="baseline", K=Non
     # (the GPU's pre-split path, and with it the bf16 conv2 input gradient, needs f % 8 == 0)
     r = p["enc1.conv1.weight"].shape[0] % 8 == 0
     s1 = _double_conv(x, p, bufs, "enc1.", train, cam, r)
-    s2 = _double_conv(F.max_pool2d(s1, 2), p, bufs, "enc2.conv.", train, cam, r)
-    s3 = _double_conv(F.max_pool2d(s2, 2), p, bufs, "enc3.conv.", train, cam, r)
-    s4 = _double_conv(F.max_pool2d(s3, 2), p, bufs, "enc4.conv.", train, cam, r)
-    xb = _double_conv(F.max_pool2d(s4, 2), p, bufs, "bottleneck.conv.", train, cam, r)
+    # the bf16 engine pools the encoder outputs' bf16 twin (same pooled values; ties of the rounded
+    # values go to the first in scan order, as in max_pool2d)
+    rb = r and _GEMM["operands"] == "bf16"
+    pool = lambda t: F.max_pool2d(_RoundOperand.apply(t) if rb else t, 2)
+    s2 = _double_conv(pool(s1), p, bufs, "enc2.conv.", train, cam, r)
+    s3 = _double_conv(pool(s2), p, bufs, "enc3.conv.", train, cam, r)
+    s4 = _double_conv(pool(s3), p, bufs, "enc4.conv.", train, cam, r)
+    xb = _double_conv(pool(s4), p, bufs, "bottleneck.conv.", train, cam, r)
     x = _decoder(xb, s4, p, bufs, "dec4.", train, cam, r)
     x = _decoder(x, s3, p, bufs, "dec3.", train, cam, r)
     x = _decoder(x, s2, p, bufs, "dec2.", train, cam, r)
