@@ -167,10 +167,25 @@ struct HeadGrad {
 // pool != nullptr: the max-pool backward folded in — g[r][c] += d[pooled r][c] where r is the
 // recorded argmax of its 2x2 window (idx, scan order 0..3), instead of a scatter into g beforehand;
 // H, W: g's image size (r < 2^32)
+// unsigned 32-bit division by an invariant d >= 2 (Granlund-Montgomery: q = (t + ((n - t) >> 1)) >> s,
+// t = mulhi(m, n); exact for every 32-bit n)
+struct FastDiv {
+    uint32_t m = 0;
+    int s = 0;
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+    int l = 0;
+    while ((1ull << l) < d) ++l;   // ceil(log2 d)
+    FastDiv f;
+    f.m = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
+    f.s = l - 1;
+    return f;
+}
 struct PoolAdd {
     const float* d = nullptr;
     const uint8_t* idx = nullptr;
     int H = 0, W = 0;
+    FastDiv divW, divH;   // set by bn_relu_bwd
 };
 void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, const float* mean,
                  const float* invstd, const float* scale, const float* shift, const float* gamma,

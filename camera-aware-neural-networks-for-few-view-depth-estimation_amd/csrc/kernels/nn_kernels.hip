@@ -134,9 +134,14 @@ struct BnCoef {
 // the folded max-pool backward (PoolAdd): row r of the full-resolution gradient receives the pooled
 // gradient of its window where r is that window's recorded argmax — the same fp32 add the scatter
 // (k_maxpool_bwd_scatter) makes
+__device__ __forceinline__ uint32_t fdiv(const FastDiv& f, uint32_t n) {
+    const uint32_t t = __umulhi(f.m, n);
+    return (t + ((n - t) >> 1)) >> f.s;
+}
 __device__ __forceinline__ float4 pool_add(const PoolAdd& pa, int C, int64_t r, int c, float4 gv) {
     const uint32_t rr = (uint32_t)r, W = (uint32_t)pa.W, H = (uint32_t)pa.H;
-    const uint32_t x = rr % W, t = rr / W, y = t % H, b = t / H;
+    const uint32_t t = fdiv(pa.divW, rr), b = fdiv(pa.divH, t);
+    const uint32_t x = rr - t * W, y = t - b * H;
     const uint32_t op = (b * (H >> 1) + (y >> 1)) * (W >> 1) + (x >> 1);
     const int k = (int)(((y & 1) << 1) | (x & 1));
     const uchar4 a = *reinterpret_cast<const uchar4*>(pa.idx + (int64_t)op * C + c);
@@ -452,11 +457,15 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
     double* tot = scratch;
     double* part = scratch + 2 * C;
     const HeadGrad hg = head ? *head : HeadGrad{};
-    const PoolAdd pa = pool ? *pool : PoolAdd{};
+    PoolAdd pa = pool ? *pool : PoolAdd{};
     if (head && (g || gmul || g_bf16 || pool)) throw std::runtime_error("bn_relu_bwd: head gradient with an explicit gradient");
     if (pool && (M >= ((int64_t)1 << 32) || pa.H <= 0 || pa.W <= 0 || ((pa.H | pa.W) & 1) ||
                  M % ((int64_t)pa.H * pa.W) != 0))
         throw std::runtime_error("bn_relu_bwd: folded max-pool backward layout");
+    if (pool) {
+        pa.divW = make_fastdiv((uint32_t)pa.W);
+        pa.divH = make_fastdiv((uint32_t)pa.H);
+    }
     // g source: 0 fp32, 1 head, 2 bf16, 3 fp32 + folded max-pool backward, 4 bf16 + folded max-pool backward
     const int gm = head ? 1 : (g_bf16 && pool) ? 4 : g_bf16 ? 2 : pool ? 3 : 0;
     using T = std::true_type;
