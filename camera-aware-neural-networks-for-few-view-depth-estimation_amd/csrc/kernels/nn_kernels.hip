@@ -696,7 +696,7 @@ void head_bwd(const float* a, int C, const float* w, const float* dpred, const f
     const int S = launch_colreduce<2>(OpHeadBwd{a, dpred, sig, max_depth, C}, M, C, part, st);
     // part[s][0][c] -> dw ; part[s][1][0] -> db
     launch_colfinal(part, S, 2 * C, scratch, nullptr, 1.f, st);
-    hipLaunchKernelGGL(k_colfinal, dim3(1), dim3(64, kFinalLanes), 0, st, scratch, 1, C, nullptr, dw, 1.f);
+    hipLaunchKernelGGL(k_colfinal, dim3(cdiv(C, 64)), dim3(64, kFinalLanes), 0, st, scratch, 1, C, nullptr, dw, 1.f);
     hipLaunchKernelGGL(k_colfinal, dim3(1), dim3(64, kFinalLanes), 0, st, scratch + C, 1, 1, nullptr, db, 1.f);
 }
 
@@ -766,7 +766,7 @@ void head_bwd_y(const float* y, int C, const float* scale, const float* shift, c
     const int S = y_bf16 ? launch_colreduce<2>(OpHeadBwdY<true>{y, scale, shift, dpred, sig, max_depth, C}, M, C, part, st)
                          : launch_colreduce<2>(OpHeadBwdY<false>{y, scale, shift, dpred, sig, max_depth, C}, M, C, part, st);
     launch_colfinal(part, S, 2 * C, scratch, nullptr, 1.f, st);
-    hipLaunchKernelGGL(k_colfinal, dim3(1), dim3(64, kFinalLanes), 0, st, scratch, 1, C, nullptr, dw, 1.f);
+    hipLaunchKernelGGL(k_colfinal, dim3(cdiv(C, 64)), dim3(64, kFinalLanes), 0, st, scratch, 1, C, nullptr, dw, 1.f);
     hipLaunchKernelGGL(k_colfinal, dim3(1), dim3(64, kFinalLanes), 0, st, scratch + C, 1, 1, nullptr, db, 1.f);
 }
 
