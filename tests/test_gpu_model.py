@@ -76,7 +76,9 @@ def test_train_steps_vs_reference_fixture(cad, dev, oracle, name):
     assert abs(m["abs_rel"] - meta["final_abs_rel_eval"]) <= 1e-3 * meta["final_abs_rel_eval"]
 
 
-@pytest.mark.parametrize("f,B,H,W", [(16, 2, 64, 96), (32, 2, 48, 64), (64, 1, 64, 64)])
+# f=96: the reference's production width (configs/train_config_production.yaml): 96/192/384/768/1536
+# channels take the im2col weight-gradient and non-power-of-two head paths
+@pytest.mark.parametrize("f,B,H,W", [(16, 2, 64, 96), (32, 2, 48, 64), (64, 1, 64, 64), (96, 1, 64, 64)])
 def test_train_step_vs_oracle(cad, dev, oracle, f, B, H, W):
     """Wider nets (all convolution code paths at channel counts >= 16) against the oracle.
 
@@ -183,7 +185,8 @@ def bf16_engine(cad):
     lib.cad_set_gemm_engine(prev)
 
 
-@pytest.mark.parametrize("f,B,H,W", [(16, 2, 64, 96), (32, 2, 48, 64), (64, 2, 64, 64), (64, 2, 48, 128)])
+@pytest.mark.parametrize("f,B,H,W", [(16, 2, 64, 96), (32, 2, 48, 64), (64, 2, 64, 64), (64, 2, 48, 128),
+                                     (96, 2, 64, 64)])
 def test_train_step_bf16_engine_vs_oracle(cad, dev, oracle, bf16_engine, f, B, H, W):
     """The bf16 configs (BASELINE configs 3-5): every conv/ConvT contraction multiplies bf16-rounded
     operands with fp32 accumulation; BN, the head, the loss, clip and Adam stay fp32.  Yardstick: the
