@@ -169,7 +169,12 @@ def parity_steps(args, cad, dev, steps=10, B=2):
     and on the CPU reference path (oracle restatement, fp32, the host's physical cores) from the same
     weights and batch (bs`B` at the benchmark resolution); after step 1 and after step `steps`:
     train-mode prediction max relative error, loss relative error, then the eval-mode prediction
-    (BN running statistics) and the computeDepthMetrics abs_rel of both on a held-out batch."""
+    (BN running statistics) and the computeDepthMetrics abs_rel of both on a held-out batch.
+    Witness: the same trajectory in fp64 (the oracle restatement evaluated by ATen's GPU kernels in
+    fp64 — the exact-arithmetic yardstick), so each fp32 path's own drift from exact arithmetic is
+    reported beside the GPU-vs-CPU difference: Adam's first steps move every weight by ~lr sign(g),
+    so gradients whose sign sits within fp32 rounding of zero move weights apart on ANY two fp32 paths
+    and the trajectories separate; `drift_ratio` = GPU drift / CPU-path drift from fp64."""
     import torch
     from oracle import cad_oracle as O
     threads, _ = cpu_threads()
@@ -192,6 +197,7 @@ def parity_steps(args, cad, dev, steps=10, B=2):
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     ref = O.Trainer(params, bufs, weights=w, model=args.model)
+    ref64 = O.Trainer(params, bufs, weights=w, model=args.model, dtype=torch.float64, device=dev)
 
     def mre(a, b):
         den = b.abs().max().item()
@@ -199,11 +205,13 @@ def parity_steps(args, cad, dev, steps=10, B=2):
     out = {"what": (f"{steps} identical train steps on the GPU ({args.dtype} engine) and on the CPU reference path "
                     f"(fp32, {threads} threads) from the same weights and bs{B} {H}x{W} batch; after step 1 and step "
                     f"{steps}: train-mode prediction, loss, then eval-mode forward + computeDepthMetrics abs_rel on a "
-                    f"held-out bs2 batch")}
+                    f"held-out bs2 batch; fp64_witness: both paths' distance from the same trajectory in fp64 "
+                    f"(the restatement on ATen's GPU kernels)")}
     try:
         for k in range(1, steps + 1):
             gl = tr.train_step(rg, gg, kg)[0].item()
             r = ref.step(rgb, gt, K)
+            r64 = ref64.step(rgb, gt, K)
             if k in (1, steps):
                 model.eval()
                 g_eval = (model(hrg, cad.camera_from_K(hkg)) if model.conditioned else model(hrg))
@@ -211,15 +219,22 @@ def parity_steps(args, cad, dev, steps=10, B=2):
                 model.train()
                 c_eval = ref.predict_eval(hr, hk if args.model != "baseline" else None)
                 c_abs = O.abs_rel_per_sample(c_eval, hg)
+                e64 = ref64.predict_eval(hr, hk if args.model != "baseline" else None).cpu()
+                p64 = r64["pred"].cpu()
+                gpu64, cpu64 = mre(tr.pred.cpu(), p64), mre(r["pred"], p64)
                 out[f"after_step_{k}"] = {
                     "pred_max_rel_err": mre(tr.pred.cpu(), r["pred"]),
                     "loss_rel_err": abs(gl - r["loss"]) / abs(r["loss"]),
                     "eval_pred_max_rel_err": mre(g_eval.cpu(), c_eval),
                     "abs_rel_gpu": round(g_abs, 6), "abs_rel_cpu_ref": round(c_abs, 6),
-                    "abs_rel_delta": abs(g_abs - c_abs)}
+                    "abs_rel_delta": abs(g_abs - c_abs),
+                    "fp64_witness": {
+                        "pred_gpu_vs_fp64": gpu64, "pred_cpu_ref_vs_fp64": cpu64,
+                        "eval_pred_gpu_vs_fp64": mre(g_eval.cpu(), e64), "eval_pred_cpu_ref_vs_fp64": mre(c_eval, e64),
+                        "drift_ratio": gpu64 / cpu64 if cpu64 > 0 else None}}
     finally:
         torch.set_num_threads(prev)
-        del tr, loss, model
+        del tr, loss, model, ref64
         torch.cuda.empty_cache()
     return out
 
@@ -486,6 +501,18 @@ def setup_dist(args):
     return world, rank, local
 
 
+def rccl_unique_id(cad, rank):
+    """Rank 0's 128-byte RCCL unique id (cad_comm_get_unique_id: host-side bootstrap, no GPU call),
+    handed to every rank through the launcher's gloo store (tests/test_bench_dist.py covers it on CPU)."""
+    import torch.distributed as dist
+    obj = [cad.Communicator.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    uid = obj[0]
+    if not isinstance(uid, bytes) or len(uid) != 128:
+        raise RuntimeError(f"rank {rank}: bad RCCL unique id from rank 0 ({type(uid).__name__})")
+    return uid
+
+
 def main():
     args = parse()
     import torch
@@ -497,10 +524,9 @@ def main():
     comm, pg = None, None
     if world > 1:
         if args.exchange == "rccl":
-            obj = [cad.Communicator.unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(obj, src=0)
+            uid = rccl_unique_id(cad, rank)
             torch.cuda.set_device(local)
-            comm = cad.Communicator(obj[0], world, rank, device=local)
+            comm = cad.Communicator(uid, world, rank, device=local)
         else:
             torch.cuda.set_device(local)
             pg = dist.new_group(backend=os.environ.get("CAD_DIST_BACKEND", "nccl"))

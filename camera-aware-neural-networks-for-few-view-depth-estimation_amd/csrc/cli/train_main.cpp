@@ -16,8 +16,8 @@
 // and ignores it); TensorBoard events are written as a CSV of scalars (no Python tensorboard here);
 // model.architecture selects the FiLM models and the geometry-aware networks (model.variant,
 // use_pcl, use_attention; single process) — the reference always builds BaselineUNet;
-// data.dataset_name "synthetic" trains on generated samples, anything else on the manifest's PNG/PNM
-// files (JPEG decoding needs a decoder this image lacks); hardware.distributed runs DP over RCCL.
+// data.dataset_name "synthetic" trains on generated samples, anything else on the manifest's PNG / PNM /
+// JPEG files (csrc/host/jpeg.cpp decodes as cv::imread does); hardware.distributed runs DP over RCCL.
 #include <signal.h>
 #include <spawn.h>
 #include <sys/wait.h>

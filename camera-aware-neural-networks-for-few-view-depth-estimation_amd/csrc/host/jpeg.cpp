@@ -14,7 +14,8 @@
 //   * YCbCr -> RGB through the fixed-point tables of jdcolor.c (16 fraction bits);
 //   * JFIF / Adobe APP14 / component-id colour-space inference (jdapimin.c default_decompress_parms).
 // Not supported (clear error): progressive and lossless processes, arithmetic coding, 12-bit samples,
-// CMYK / YCCK (SUN RGB-D's frames are baseline 8-bit YCbCr).  EXIF orientation is not applied.
+// CMYK / YCCK (SUN RGB-D's frames are baseline 8-bit YCbCr).  The EXIF orientation tag is applied as
+// cv::imread(IMREAD_COLOR) applies it.
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
@@ -49,12 +50,21 @@ struct Huffman {
     // 9-bit lookahead: (length << 8) | value, 0 = longer code
     uint16_t look[512];
 
-    void build(const uint8_t bits[17], const uint8_t* v, int nv) {
+    // is_dc: a DC table's symbols are coefficient sizes, at most 15 (jdhuff.c jpeg_make_d_derived_tbl
+    // rejects larger ones; a baseline decoder needs <= 11, checked where the symbol is used)
+    void build(const uint8_t bits[17], const uint8_t* v, int nv, bool is_dc) {
         std::memcpy(vals, v, (size_t)nv);
+        if (is_dc)
+            for (int i = 0; i < nv; ++i)
+                if (vals[i] > 15) throw JpegError("bad Huffman table (DC symbol > 15)");
         int code = 0, k = 0;
         std::memset(look, 0, sizeof look);
         for (int l = 1; l <= 16; ++l) {
             valoff[l] = k - code;
+            // an over-full length is rejected before any lookahead entry is written: the codes of
+            // length l must fit in l bits and none may be all ones (jdhuff.c jpeg_make_d_derived_tbl,
+            // code >= 1 << si -> JERR_BAD_HUFF_TABLE)
+            if (bits[l] && code + (int)bits[l] >= (1 << l)) throw JpegError("bad Huffman table");
             if (bits[l]) {
                 for (int i = 0; i < bits[l]; ++i, ++code, ++k) {
                     if (l <= 9) {
@@ -66,7 +76,6 @@ struct Huffman {
             } else {
                 maxcode[l] = -1;
             }
-            if (bits[l] && code >= (1 << l)) throw JpegError("bad Huffman table");   // (jdhuff.c check)
             code <<= 1;
         }
         maxcode[17] = 0x7FFFFFFF;   // sentinel
@@ -375,6 +384,65 @@ inline uint8_t clamp255(int v) { return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v)
 
 uint16_t be16(const uint8_t* p) { return (uint16_t)(p[0] << 8 | p[1]); }
 
+// EXIF orientation (tag 0x0112 of IFD0 in an APP1 "Exif\0\0" segment, TIFF byte order "II" / "MM");
+// 1 when absent or unreadable.  cv::imread(IMREAD_COLOR) applies it (OpenCV's ExifTransform).
+int exif_orientation(const uint8_t* b, int n) {
+    if (n < 14 || std::memcmp(b, "Exif\0\0", 6) != 0) return 1;
+    const uint8_t* t = b + 6;
+    const int64_t tn = n - 6;
+    bool le;
+    if (t[0] == 'I' && t[1] == 'I') le = true;
+    else if (t[0] == 'M' && t[1] == 'M') le = false;
+    else return 1;
+    auto u16 = [&](int64_t o) -> uint32_t { return le ? (uint32_t)(t[o] | t[o + 1] << 8) : (uint32_t)(t[o] << 8 | t[o + 1]); };
+    auto u32 = [&](int64_t o) -> uint32_t {
+        return le ? (uint32_t)t[o] | (uint32_t)t[o + 1] << 8 | (uint32_t)t[o + 2] << 16 | (uint32_t)t[o + 3] << 24
+                  : (uint32_t)t[o] << 24 | (uint32_t)t[o + 1] << 16 | (uint32_t)t[o + 2] << 8 | (uint32_t)t[o + 3];
+    };
+    if (u16(2) != 42) return 1;
+    const int64_t ifd = u32(4);
+    if (ifd + 2 > tn) return 1;
+    const int64_t cnt = u16(ifd);
+    for (int64_t i = 0; i < cnt; ++i) {
+        const int64_t e = ifd + 2 + 12 * i;
+        if (e + 12 > tn) return 1;
+        if (u16(e) == 0x0112) {
+            if (u16(e + 2) != 3) return 1;   // SHORT
+            const uint32_t v = u16(e + 8);
+            return v >= 1 && v <= 8 ? (int)v : 1;
+        }
+    }
+    return 1;
+}
+
+// the EXIF orientation transform of an (h, w, c) image, as OpenCV's ExifTransform applies it:
+// 2 flip left-right, 3 rotate 180, 4 flip top-bottom, 5 transpose, 6 rotate 90 clockwise,
+// 7 transverse (transpose + rotate 180), 8 rotate 90 counter-clockwise
+void apply_orientation(Decoded& d, int o) {
+    if (o <= 1) return;
+    const int h = d.h, w = d.w, c = d.c;
+    const bool swap = o >= 5;
+    const int oh = swap ? w : h, ow = swap ? h : w;
+    std::vector<uint8_t> px((size_t)oh * ow * c);
+    for (int y = 0; y < oh; ++y)
+        for (int x = 0; x < ow; ++x) {
+            int sy, sx;   // source pixel of output (y, x)
+            switch (o) {
+                case 2: sy = y; sx = w - 1 - x; break;
+                case 3: sy = h - 1 - y; sx = w - 1 - x; break;
+                case 4: sy = h - 1 - y; sx = x; break;
+                case 5: sy = x; sx = y; break;
+                case 6: sy = h - 1 - x; sx = y; break;
+                case 7: sy = h - 1 - x; sx = w - 1 - y; break;
+                default: sy = x; sx = w - 1 - y; break;   // 8
+            }
+            std::memcpy(&px[((size_t)y * ow + x) * c], &d.px[((size_t)sy * w + sx) * c], (size_t)c);
+        }
+    d.px.swap(px);
+    d.h = oh;
+    d.w = ow;
+}
+
 }  // namespace
 
 Decoded decode(const uint8_t* data, size_t size) {
@@ -387,7 +455,7 @@ Decoded decode(const uint8_t* data, size_t size) {
     std::vector<Component> comps;
     int W = 0, H = 0, hmax = 1, vmax = 1, restart = 0;
     bool jfif = false, adobe = false, frame = false, any_scan = false;
-    int adobe_transform = -1;
+    int adobe_transform = -1, orientation = 1;
 
     auto seg = [&](const uint8_t*& q) -> std::pair<const uint8_t*, int> {
         if (q + 2 > end) throw JpegError("truncated marker segment");
@@ -418,7 +486,7 @@ Decoded decode(const uint8_t* data, size_t size) {
                 int total = 0;
                 for (int l = 1; l <= 16; ++l) total += bits[l] = b[k + l];
                 if (total > 256 || k + 17 + total > n) throw JpegError("bad DHT counts");
-                (tc ? ac[th] : dc[th]).build(bits, b + k + 17, total);
+                (tc ? ac[th] : dc[th]).build(bits, b + k + 17, total, tc == 0);
                 k += 17 + total;
             }
         } else if (m == 0xDB) {                               // DQT
@@ -437,6 +505,8 @@ Decoded decode(const uint8_t* data, size_t size) {
             restart = be16(b);
         } else if (m == 0xE0) {                               // APP0
             if (n >= 5 && std::memcmp(b, "JFIF\0", 5) == 0) jfif = true;
+        } else if (m == 0xE1) {                               // APP1 (EXIF orientation)
+            if (orientation == 1) orientation = exif_orientation(b, n);
         } else if (m == 0xEE) {                               // APP14
             if (n >= 12 && std::memcmp(b, "Adobe", 5) == 0) {
                 adobe = true;
@@ -529,8 +599,8 @@ Decoded decode(const uint8_t* data, size_t size) {
                             const int gx = ux * nbx + bx, gy = uy * nby + by;
                             int16_t* blk = &c->coef[((size_t)gy * c->bw + gx) * 64];
                             const int t = bits.decode(dc[c->td]);
-                            int diff = t ? extend(bits.get(t), t) : 0;
                             if (t > 11) throw JpegError("bad DC coefficient");
+                            const int diff = t ? extend(bits.get(t), t) : 0;
                             c->pred += diff;
                             blk[0] = (int16_t)c->pred;
                             for (int k = 1; k < 64; ++k) {
@@ -579,6 +649,7 @@ Decoded decode(const uint8_t* data, size_t size) {
         out.px.resize((size_t)W * H);
         const Component& c = comps[0];
         for (int r = 0; r < H; ++r) std::memcpy(&out.px[(size_t)r * W], &c.plane[(size_t)r * c.bw * 8], (size_t)W);
+        apply_orientation(out, orientation);
         return out;
     }
     // colour space (jdapimin.c default_decompress_parms): JFIF -> YCbCr; Adobe transform 0 -> RGB;
@@ -615,6 +686,7 @@ Decoded decode(const uint8_t* data, size_t size) {
             }
         }
     }
+    apply_orientation(out, orientation);
     return out;
 }
 

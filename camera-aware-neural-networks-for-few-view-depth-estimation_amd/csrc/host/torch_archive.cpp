@@ -565,8 +565,14 @@ std::string read_range(FILE* f, uint64_t off, uint64_t n) {
 constexpr int kMaxDepth = 64;
 constexpr int64_t kMaxNumel = (int64_t)1 << 40;
 
-void collect(const VPtr& v, const std::string& prefix, cad_archive& a, std::set<const Value*>& open, int depth) {
+// Total nodes one traversal may visit: a memoised dict reused k times per level is a DAG, not a cycle,
+// and would otherwise be walked k^depth times.
+constexpr int64_t kMaxVisits = (int64_t)1 << 20;
+
+void collect(const VPtr& v, const std::string& prefix, cad_archive& a, std::set<const Value*>& open, int depth,
+             int64_t& visits) {
     if (depth > kMaxDepth) throw ArchiveError("pickle: module tree nested too deeply");
+    if (++visits > kMaxVisits) throw ArchiveError("pickle: module tree too large (shared sub-trees)");
     if (v->kind == Value::Tensor) {
         if (v->items.empty() || v->items[0]->kind != Value::Storage) throw ArchiveError("tensor '" + prefix + "' has no storage");
         if (v->strides.size() != v->sizes.size()) throw ArchiveError("tensor '" + prefix + "': sizes and strides differ in rank");
@@ -594,7 +600,7 @@ void collect(const VPtr& v, const std::string& prefix, cad_archive& a, std::set<
         if (!open.insert(v.get()).second) throw ArchiveError("pickle: self-referencing module tree");
         for (auto& kv : v->dict) {
             if (kv.first->kind != Value::Str) continue;
-            collect(kv.second, prefix.empty() ? kv.first->s : prefix + "." + kv.first->s, a, open, depth + 1);
+            collect(kv.second, prefix.empty() ? kv.first->s : prefix + "." + kv.first->s, a, open, depth + 1, visits);
         }
         open.erase(v.get());
     }
@@ -707,7 +713,8 @@ cad_status cad_archive_open(const char* path, cad_archive** out) {
         const std::string pkl = read_range(f.get(), pk->second.data_off, pk->second.size);
         Unpickler up(pkl);
         std::set<const Value*> open;
-        collect(up.run(), "", *a, open, 0);
+        int64_t visits = 0;
+        collect(up.run(), "", *a, open, 0, visits);
         for (auto& t : a->tensors) {
             auto it = a->entries.find(a->prefix + "/data/" + t.key);
             if (it == a->entries.end()) throw ArchiveError("missing storage record data/" + t.key);

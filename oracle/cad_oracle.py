@@ -278,8 +278,8 @@ def rays_from_K(K, H, W):
     fxi = (1.0 / K[:, 0, 0]).view(-1, 1, 1)
     fyi = (1.0 / K[:, 1, 1]).view(-1, 1, 1)
     cx, cy = K[:, 0, 2].view(-1, 1, 1), K[:, 1, 2].view(-1, 1, 1)
-    u = torch.arange(W, dtype=torch.float32).view(1, 1, W)
-    v = torch.arange(H, dtype=torch.float32).view(1, H, 1)
+    u = torch.arange(W, dtype=torch.float32, device=K.device).view(1, 1, W)
+    v = torch.arange(H, dtype=torch.float32, device=K.device).view(1, H, 1)
     x = ((u - cx) * fxi).expand(-1, H, W)
     y = ((v - cy) * fyi).expand(-1, H, W)
     n = torch.sqrt(x * x + y * y + 1.0)
@@ -552,7 +552,7 @@ def si_loss(pred, gt, lam=0.5, eps=EPS, valid_mask=None):
     d = (torch.log(pred) - torch.log(gt)).masked_select(mask)
     n = d.numel()
     if n == 0:
-        return torch.zeros(1, dtype=pred.dtype)
+        return torch.zeros(1, dtype=pred.dtype, device=pred.device)
     return torch.pow(d, 2).sum() / n - lam * torch.pow(d.sum(), 2) / (n * n)
 
 
@@ -567,7 +567,7 @@ def _grad_scale(pred, gt):
 
 def grad_loss(pred, gt, num_scales=4, eps=EPS):
     """GradientMatchingLoss::forward (depth_loss.h:95-124): shape-[1] result."""
-    total = torch.zeros(1, dtype=pred.dtype)
+    total = torch.zeros(1, dtype=pred.dtype, device=pred.device)
     for s in range(num_scales):
         ps, gs = pred, gt
         if s > 0:
@@ -596,8 +596,8 @@ def reproj_loss(pred, gt, K, eps=EPS, valid_mask=None):
     B, _, H, W = pred.shape
     if K.dim() == 2:
         K = K.unsqueeze(0).expand(B, 3, 3)
-    gy = torch.arange(0, H, dtype=pred.dtype).view(1, H, 1).expand(1, H, W)
-    gx = torch.arange(0, W, dtype=pred.dtype).view(1, 1, W).expand(1, H, W)
+    gy = torch.arange(0, H, dtype=pred.dtype, device=pred.device).view(1, H, 1).expand(1, H, W)
+    gx = torch.arange(0, W, dtype=pred.dtype, device=pred.device).view(1, 1, W).expand(1, H, W)
     fx = K[:, 0, 0].view(B, 1, 1, 1)
     fy = K[:, 1, 1].view(B, 1, 1, 1)
     cx = K[:, 0, 2].view(B, 1, 1, 1)
@@ -610,7 +610,7 @@ def reproj_loss(pred, gt, K, eps=EPS, valid_mask=None):
     err = torch.sqrt(dX * dX + dY * dY + dZ * dZ + eps)
     e = err.masked_select(valid_mask if valid_mask is not None else gt > eps)
     if e.numel() == 0:
-        return torch.zeros(1, dtype=pred.dtype)
+        return torch.zeros(1, dtype=pred.dtype, device=pred.device)
     return e.mean()
 
 
@@ -682,19 +682,23 @@ class Trainer:
     """One replica of TensorBoardTrainerEnhanced's step (enhanced.h:287-304) on host cores."""
 
     def __init__(self, params, buffers, weights=(1.0, 0.1, 0.001, 0.01), lr=1e-4, wd=1e-5,
-                 clip=1.0, max_depth=10.0, dtype=torch.float32, model="baseline", gemm_operands="exact"):
+                 clip=1.0, max_depth=10.0, dtype=torch.float32, model="baseline", gemm_operands="exact",
+                 device=None):
         # dtype=float64 gives the exact-arithmetic yardstick the fp32 paths are both measured against;
-        # gemm_operands="bf16" the bf16 configs' contraction arithmetic (see _GEMM)
+        # gemm_operands="bf16" the bf16 configs' contraction arithmetic (see _GEMM).  device: where
+        # ATen evaluates this restatement — the host by default; the full-size test evaluates the
+        # fp64 yardstick with ATen's GPU kernels (any exact-enough arithmetic serves as a yardstick)
         self.dtype = dtype
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
         self.gemm_operands = gemm_operands
         self.model = model
-        self.p = OrderedDict((k, v.clone().to(dtype)) for k, v in params.items())
-        self.bufs = OrderedDict((k, v.clone().to(dtype)) for k, v in buffers.items())
+        self.p = OrderedDict((k, v.clone().to(self.device, dtype)) for k, v in params.items())
+        self.bufs = OrderedDict((k, v.clone().to(self.device, dtype)) for k, v in buffers.items())
         self.weights, self.clip, self.max_depth = weights, clip, max_depth
         self.opt = Adam(self.p, lr=lr, weight_decay=wd)
 
     def forward_backward(self, rgb, gt, K):
-        rgb, gt, K = rgb.to(self.dtype), gt.to(self.dtype), K.to(self.dtype)
+        rgb, gt, K = (t.to(self.device, self.dtype) for t in (rgb, gt, K))
         for v in self.p.values():
             v.requires_grad_(True)
             v.grad = None
@@ -724,10 +728,11 @@ class Trainer:
 
     @torch.no_grad()
     def predict_eval(self, rgb, K=None):
-        Kd = K.to(self.dtype) if K is not None else None
+        Kd = K.to(self.device, self.dtype) if K is not None else None
         prev, _GEMM["operands"] = _GEMM["operands"], self.gemm_operands
         try:
-            return unet_forward(rgb.to(self.dtype), self.p, self.bufs, False, self.max_depth, self.model, Kd)
+            return unet_forward(rgb.to(self.device, self.dtype), self.p, self.bufs, False, self.max_depth, self.model,
+                                Kd)
         finally:
             _GEMM["operands"] = prev
 

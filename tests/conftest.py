@@ -13,6 +13,26 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running")
 
 
+# Order of the slow (full-size) tests at the end of the session: cheapest first, so a session that
+# runs out of time loses the fewest checks.
+_SLOW_ORDER = ("test_gpu_fullsize_bf16.py::test_bs32_480x640_resunet", "test_gpu_fullsize.py",
+               "test_gpu_fullsize_bf16.py::test_bs32_480x640_bf16_step_vs_oracle[baseline]",
+               "test_gpu_fullsize_bf16.py::test_bs32_480x640_bf16_step_vs_oracle[rayfilm]")
+
+
+def pytest_collection_modifyitems(session, config, items):
+    """Slow-marked items run after everything else (stable order otherwise): a full-size test that
+    overruns the session's time budget can then never starve the operator, fixture and model tests."""
+    def rank(it):
+        if it.get_closest_marker("slow") is None:
+            return 0
+        for k, pat in enumerate(_SLOW_ORDER):
+            if pat in it.nodeid:
+                return 1 + k
+        return 1 + len(_SLOW_ORDER)
+    items[:] = [it for _, _, it in sorted((rank(it), i, it) for i, it in enumerate(items))]
+
+
 @pytest.fixture(scope="session")
 def cad():
     import cad_pkg
@@ -81,32 +101,37 @@ def unet_bn_blocks(model="baseline"):
     return enc + [(f"dec{l}", f"dec{l + 1}.conv.", l) for l in range(4)]
 
 
-def gpu_relu_decisions(net, params, f, B, H, W, model="baseline"):
+def gpu_relu_decisions(net, params, f, B, H, W, model="baseline", dev=None):
     """The ReLU decisions of `net`'s last train-mode forward, for cad_oracle.RELU_FORCE.
 
     Rebuilt from the stored pre-BN conv outputs (cad_unet_debug_buffer "<tag>_y1|_y2", the values the
     GPU normalised) exactly as the BN-apply kernel takes them: batch statistics in fp64, mean and
     1/sqrt(var + eps) rounded to fp32, scale = gamma * invstd and shift = beta - mean * scale in fp32,
     decision = sign(y * scale + shift) (the kernel's fused multiply-add keeps the exact sign, which the
-    fp64 evaluation of the same product and sum reproduces)."""
+    fp64 evaluation of the same product and sum reproduces).  `dev`: where this bookkeeping runs (the
+    GPU at full size: it is test arithmetic on the stored values, not the oracle); masks come back on
+    the host."""
     import numpy as np
     import torch
     masks = {}
     eps = float(np.float32(1e-5))
+    dev = dev or torch.device("cpu")
     for tag, pre, l in unet_bn_blocks(model):
         C, h, w = f << l, H >> l, W >> l
         for k in ("1", "2"):
-            y = net.debug_buffer(f"{tag}_y{k}")[: B * h * w * C].double().reshape(B * h * w, C)
+            y = net.debug_buffer(f"{tag}_y{k}")[: B * h * w * C].to(dev).double().reshape(B * h * w, C)
             mu = y.mean(0)
             var = y.var(0, unbiased=False)
             mu32 = mu.float()
             inv = (1.0 / torch.sqrt(var + eps)).float()
-            g = params[pre + "bn" + k + ".weight"].float()
-            b = params[pre + "bn" + k + ".bias"].float()
+            g = params[pre + "bn" + k + ".weight"].float().to(dev)
+            b = params[pre + "bn" + k + ".bias"].float().to(dev)
             sc = g * inv
             sh = (b.double() - mu32.double() * sc.double()).float()   # fma(-mean, scale, beta)
             z = y * sc.double() + sh.double()
-            masks[pre + "bn" + k] = (z > 0).reshape(B, h, w, C).permute(0, 3, 1, 2).contiguous()
+            del y
+            masks[pre + "bn" + k] = (z > 0).reshape(B, h, w, C).permute(0, 3, 1, 2).contiguous().cpu()
+            del z
     return masks
 
 

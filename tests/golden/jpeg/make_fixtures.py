@@ -35,6 +35,14 @@ def image(h, w, gray, seed):
     return Image.fromarray(a[..., 0] if gray else a)
 
 
+def _exif_be(o):
+    """An Exif APP1 body with a big-endian ("MM") TIFF header whose IFD0 holds one entry: orientation o."""
+    import struct
+    tiff = b"MM" + struct.pack(">HI", 42, 8) + struct.pack(">H", 1) + struct.pack(">HHIHH", 0x0112, 3, 1, o, 0) \
+        + struct.pack(">I", 0)
+    return b"Exif\x00\x00" + tiff
+
+
 def main():
     meta = {"libjpeg": features.version("jpg"), "libjpeg_turbo": bool(features.check_feature("libjpeg_turbo")),
             "cases": {}}
@@ -47,6 +55,23 @@ def main():
         dec = np.asarray(Image.open(io.BytesIO(data)).convert("L" if gray else "RGB"))
         np.save(os.path.join(OUT, name + ".npy"), dec)
         meta["cases"][name] = {"shape": list(dec.shape), "bytes": len(data)}
+    # EXIF orientation 1..8 (APP1, both TIFF byte orders): the expected pixels are the decode with the
+    # orientation applied (PIL ImageOps.exif_transpose; OpenCV's imread(IMREAD_COLOR) applies the tag
+    # the same way, loadsave.cpp ExifTransform)
+    from PIL import ImageOps
+    for o in range(1, 9):
+        name = f"exif_orient{o}_yuv420_24x40"
+        ex = Image.Exif()
+        ex[0x0112] = o
+        exb = ex.tobytes() if o % 2 else _exif_be(o)   # big-endian TIFF header for the even cases
+        bio = io.BytesIO()
+        image(24, 40, False, 200 + o).save(bio, "JPEG", quality=90, subsampling=2, exif=exb)
+        data = bio.getvalue()
+        with open(os.path.join(OUT, name + ".jpg"), "wb") as fh:
+            fh.write(data)
+        dec = np.asarray(ImageOps.exif_transpose(Image.open(io.BytesIO(data))).convert("RGB"))
+        np.save(os.path.join(OUT, name + ".npy"), dec)
+        meta["cases"][name] = {"shape": list(dec.shape), "bytes": len(data), "orientation": o}
     # a progressive file: the decoder refuses it with a message
     bio = io.BytesIO()
     image(16, 16, False, 99).save(bio, "JPEG", quality=90, progressive=True)

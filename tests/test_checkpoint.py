@@ -224,7 +224,17 @@ def _tensor_pkl(offset, sizes, strides):
             b"J" + int(offset).to_bytes(4, "little", signed=True) + ints(sizes) + ints(strides) + b"\x89tRs.")
 
 
+def _dag_pkl(levels=60):
+    """data.pkl of a dict tree whose every level holds the previous level's (memoised) dict twice: a
+    DAG, not a cycle, with 2^levels root-to-leaf paths."""
+    out = b"\x80\x02}q\x00"
+    for k in range(1, levels + 1):
+        out += b"}q" + bytes([k]) + b"(" + _pkl_str("a") + b"h" + bytes([k - 1]) + _pkl_str("b") + b"h" + bytes([k - 1]) + b"u"
+    return out + b"."
+
+
 @pytest.mark.parametrize("what,pkl,msg", [
+    ("memoised dict shared twice per level (DAG, 2^60 paths)", _dag_pkl(), b"too large"),
     ("BINUNICODE8 length that wraps pos + n", b"\x80\x02\x8d" + (2 ** 64 - 1).to_bytes(8, "little") + b"abc.",
      b"truncated"),
     ("BINUNICODE8 length past the end", b"\x80\x02\x8d" + (1 << 40).to_bytes(8, "little") + b"abc.", b"truncated"),

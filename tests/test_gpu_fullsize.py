@@ -22,8 +22,9 @@ Tolerances (fp32 vs fp32, different summation orders; the north-star's 1e-3 rela
   after Adam within 2 lr, moving by more than rounding only where the two fp32 gradients may disagree
   in sign (Adam's first step is lr * g / (|g| + eps): |g| within 3x their max error against fp64,
   checked element by element); the eval-mode prediction / abs_rel of the updated model <= 1e-4.
-Host memory: the CPU autograd graph of a bs32 480x640 step is ~80 GB in fp32 and ~160 GB in fp64,
-one after the other (the box allows 270 GB)."""
+Host memory: the CPU autograd graph of the fp32 oracle step at bs32 480x640 is ~80 GB (the box allows
+270 GB); the fp64 yardstick's (~160 GB) lives in the GPU's 288 GB HBM, after the product's buffers are
+freed."""
 import sys
 import threading
 import time
@@ -111,8 +112,12 @@ def _run(cad, dev, oracle, t0):
     ref = oracle.Trainer(params, bufs, weights=WEIGHTS)
     r = ref.step(rgb, gt, K)
     _beat(f"oracle fp32 step done (loss {r['loss']:.6f}, ours {g_loss5[0].item():.6f})", t0)
-    g64 = oracle.Trainer(params, bufs, weights=WEIGHTS, dtype=torch.float64).forward_backward(rgb, gt, K)[4]
-    _beat("oracle fp64 forward/backward done", t0)
+    # the fp64 yardstick is the same restatement evaluated by ATen's GPU kernels in fp64 (its host
+    # evaluation took 220 s of the session's budget; any exact-enough arithmetic is a yardstick)
+    g64 = [g.cpu() for g in oracle.Trainer(params, bufs, weights=WEIGHTS, dtype=torch.float64,
+                                           device=dev).forward_backward(rgb, gt, K)[4]]
+    torch.cuda.empty_cache()
+    _beat("oracle fp64 forward/backward (ATen GPU kernels) done", t0)
 
     e_pred = max_rel_err(g_pred, r["pred"])
     assert e_pred < 1e-4, e_pred

@@ -188,7 +188,7 @@ def test_bs32_480x640_bf16_step_vs_oracle(cad, dev, oracle, bf16_engine, beat, m
     torch.cuda.synchronize()
     g = {"pred": pred.cpu(), "dpred": dpred.cpu(), "loss5": loss5.cpu().tolist()}
     g_grads = m.grads()
-    relu = gpu_relu_decisions(m, params, F, B, H, W, model)
+    relu = gpu_relu_decisions(m, params, F, B, H, W, model, dev=dev)
     yf = gpu_conv_outputs(m, F, B, H, W, model)
     ff = gpu_film_params(m, params, F, B, model)
     cad.clip_grad_norm_(m, 1.0)
@@ -233,9 +233,11 @@ def test_bs32_480x640_bf16_step_vs_oracle(cad, dev, oracle, bf16_engine, beat, m
         beat(f"{model}: FiLM {n} gamma/beta vs the oracle's own: "
              f"{max_rel_err(fg, oracle.FILM_OWN[n][0]):.2e} / {max_rel_err(fb, oracle.FILM_OWN[n][1]):.2e}")
     oracle.FILM_OWN.clear()
+    # (this bookkeeping over the ~4.7 G stored outputs runs on the GPU: test arithmetic, not the oracle)
     rows = []
-    for n, gy in yf.items():
-        own = oracle.Y_OWN.pop(n).float()
+    for n in list(yf):
+        gy = yf.pop(n).to(dev)
+        own = oracle.Y_OWN.pop(n).float().to(dev)
         d = (own.double() - gy.double()).abs()
         if model == "baseline" and n == "enc1.conv1":
             rows.append((d.max().item() / gy.abs().max().item(), 0.0, 0.0, n))
@@ -244,7 +246,8 @@ def test_bs32_480x640_bf16_step_vs_oracle(cad, dev, oracle, bf16_engine, beat, m
         ulp = torch.exp2(torch.floor(torch.log2(big)) - 7)
         du = d / ulp
         rows.append((du.max().item(), (d > 0).double().mean().item(), (du > 1.0).double().mean().item(), n))
-        del own, d, ulp, big, du
+        del own, d, ulp, big, du, gy
+    torch.cuda.empty_cache()
     oracle.Y_OWN.clear()
     del yf
     rows.sort(reverse=True)
