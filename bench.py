@@ -44,7 +44,7 @@ BF16_MFMA_PEAK_TFLOPS = 2516.6
 MX8_MFMA_PEAK_TFLOPS = 2 * BF16_MFMA_PEAK_TFLOPS
 S3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6.0
 HBM_PEAK_GBS = 8000.0
-FLOP_PER_IMAGE_480x640_F64 = 1.353646e12   # fwd + dgrad + wgrad
+FLOP_PER_IMAGE_480x640_F64 = 1.353646e12   # fwd + dgrad + wgrad (= flop_per_image(64))
 WORKLOADS = {2: "baseline_unet train step, configs[1]: bs32/GPU 480x640 fp32 SI-only loss",
              3: "ray+FiLM conditioned U-Net train step, configs[2]: bs32/GPU 480x640 bf16 GEMMs, full loss",
              4: "baseline_unet train step, configs[3] per-GPU step: bs32/GPU 480x640 bf16 GEMMs, full loss "
@@ -113,15 +113,20 @@ def host_cpu():
             "usable_cpus": usable}
 
 
+CPU_SHARE = 16   # host CPUs one GPU's job may use on the MI355X boxes (OMP_NUM_THREADS there)
+
+
 def cpu_threads():
     """Threads for the CPU reference path: the host's physical cores (BASELINE.md §3:
-    set_num_threads(<physical cores>)), bounded by the CPUs this process may run on."""
+    set_num_threads(<physical cores>)), bounded by the CPUs this process may run on and by one GPU's
+    CPU share of the box (16; round 3 measured the oracle 2x faster at 16 threads than at 128 there)."""
     h = host_cpu()
     n = h["physical_cores"] or h["usable_cpus"] or 1
-    return max(1, min(n, h["usable_cpus"] or n)), h
+    share = int(os.environ.get("OMP_NUM_THREADS", CPU_SHARE) or CPU_SHARE)
+    return max(1, min(n, h["usable_cpus"] or n, share)), h
 
 
-def cpu_baseline(args, sweep=(16, 64)):
+def cpu_baseline(args, sweep=(8,)):
     """cpu_baseline leg: the oracle restatement (oracle/cad_oracle.py: LibTorch CPU, the ATen kernels
     the reference dispatches; the reference source and its compiled harness stay in the build
     container) timed on this host on a bounded sample of the workload — bs`cpu_sample_batch` at the
@@ -157,7 +162,7 @@ def cpu_baseline(args, sweep=(16, 64)):
     return {"value": rates[str(threads)], "unit": "images/s", "cores": threads, "kind": "port",
             "sample": (f"{args.model} bs{B} {H}x{W} f={f} loss weights {args.weights}, fp32 (the reference's only "
                        f"precision), 1 warm-up + {args.cpu_sample_steps} timed train steps of the oracle restatement "
-                       f"(oracle/cad_oracle.py on LibTorch CPU, {threads} threads = the host's physical cores; BN "
+                       f"(oracle/cad_oracle.py on LibTorch CPU, {threads} threads = one GPU's share of the host's cores; BN "
                        f"statistics over bs{B}, not bs32)"),
             "seconds": round(dt, 2), "threads_sweep_images_per_s": rates,
             "threads_sweep_note": "one train step per thread count after the timed steps (same weights, same batch)",
@@ -298,6 +303,21 @@ def roofline_of(prof, steps, ms_per_step, show=False):
     return roof
 
 
+def flop_per_image(f=64, H=480, W=640):
+    """Algorithmic FLOPs of one trained image through BaselineUNet(3, f) (forward + dgrad +
+    wgrad of every conv / ConvT / the head; enc1.conv1 has no dgrad, its input is the image):
+    1,353.646 GFLOP at f = 64, 3,044.023 at f = 96 (train_config_production.yaml)."""
+    P = lambda l: (H >> l) * (W >> l)
+    t = 2 * 2 * P(0) * f * 27 + 3 * 2 * P(0) * f * 9 * f + 3 * 2 * P(0) * f
+    for l in range(1, 5):          # enc2..enc4, bottleneck: C/2 -> C, C -> C
+        C = f << l
+        t += 3 * (2 * P(l) * C * 9 * C // 2 + 2 * P(l) * C * 9 * C)
+    for l in range(4):             # dec: ConvT 2C -> C (2x2/s2), conv1 cat 2C -> C, conv2 C -> C
+        C = f << l
+        t += 3 * (2 * P(l) * 2 * C * C + 2 * P(l) * C * 9 * 2 * C + 2 * P(l) * C * 9 * C)
+    return float(t)
+
+
 def extra_leg(cad, lib, dev, config, steps=10, warmup=3, B=32, H=480, W=640, f=64):
     """A bounded measurement of another BASELINE workload in the same run (driver-observed):
     configs[2] (ray+FiLM U-Net, bf16 GEMMs, full loss) or configs[3]'s per-GPU step (baseline_unet,
@@ -310,7 +330,8 @@ def extra_leg(cad, lib, dev, config, steps=10, warmup=3, B=32, H=480, W=640, f=6
     try:
         cls = {"baseline": cad.BaselineUNet, "rayfilm": cad.RayConditionedUNet}[model_name]
         model = cls(3, f, max_depth=10.0, batch=B, height=H, width=W, device=dev.index)
-        loss = cad.CombinedDepthLoss(1.0, 0.1, 0.001, 0.01, batch=B, height=H, width=W, device=dev.index)
+        lw = (1.0, 0.0, 0.0, 0.0) if config == 2 else (1.0, 0.1, 0.001, 0.01)
+        loss = cad.CombinedDepthLoss(*lw, batch=B, height=H, width=W, device=dev.index)
         tr = cad.Trainer(model, loss, lr=1e-4, weight_decay=1e-5, grad_clip=1.0)
         rgb, gt, K = (t.to(dev) for t in synthetic.device_batch(B, H, W, "cpu"))
         for _ in range(warmup):
@@ -328,11 +349,18 @@ def extra_leg(cad, lib, dev, config, steps=10, warmup=3, B=32, H=480, W=640, f=6
     finally:
         lib.cad_set_gemm_engine(prev)
     value = B * steps / dt
-    out = {"workload": WORKLOADS[config], "value": round(value, 3), "unit": "images/s",
+    wl = WORKLOADS[config] if f == 64 else (
+        f"baseline_unet f={f} (train_config_production.yaml: init_features 96) train step, bs{B}/GPU {H}x{W} "
+        f"{dtype} GEMMs, " + ("SI-only loss" if config == 2 else "full loss"))
+    out = {"workload": wl, "value": round(value, 3), "unit": "images/s", "init_features": f,
            "ms_per_step": round(1e3 * dt / steps, 3), "steps": steps, "warmup": warmup, "dtype": dtype,
            "last_loss": last, "roofline": roofline_of(prof(), steps, 1e3 * dt / steps)}
-    if model_name == "baseline":
-        out["mfma_frac_dense_bf16"] = round(FLOP_PER_IMAGE_480x640_F64 * value / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4)
+    if model_name == "baseline" and (H, W) == (480, 640):
+        fl = flop_per_image(f, H, W)
+        out["step_tflops_algorithmic"] = round(fl * value / 1e12, 3)
+        out["mfma_frac_dense_bf16"] = round(fl * value / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4)
+        if dtype == "fp32":
+            out["mfma_frac_s3_ceiling"] = round(fl * value / 1e12 / S3_PEAK_TFLOPS, 4)
     return out
 
 
@@ -594,6 +622,13 @@ def main():
                     log(f"extra leg config {cfg}: {extra[f'config{cfg}']}")
                 except Exception as e:
                     log(f"extra leg config {cfg} failed: {e}")
+            for cfg in (2, 4):   # the reference's production width (train_config_production.yaml:26-27)
+                key = f"config{cfg}_f96"
+                try:
+                    extra[key] = extra_leg(cad, lib, dev, cfg, f=96)
+                    log(f"extra leg {key}: {extra[key]}")
+                except Exception as e:
+                    log(f"extra leg {key} failed: {e}")
             for key, fp8 in (("config5", False), ("config5_fp8", True)):
                 try:
                     extra[key] = extra_leg_resunet(cad, lib, dev, fp8=fp8)

@@ -278,6 +278,8 @@ __global__ void k_slab_reduce(float* __restrict__ slab, int nsplit, int64_t stri
     if (i >= n) return;
     const int z0 = blockIdx.y * nsplit;   // level 1: this group's slabs; level 2: gridDim.y == 1
     float4 s = *reinterpret_cast<const float4*>(slab + (int64_t)z0 * zstep * stride + i);
+    // unrolled: the slabs' loads in flight together, the adds in slab order (same sums bit for bit)
+#pragma unroll 8
     for (int z = 1; z < nsplit; ++z) {
         float4 t = *reinterpret_cast<const float4*>(slab + (int64_t)(z0 + z) * zstep * stride + i);
         s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;

@@ -77,7 +77,10 @@ __global__ void k_colfinal(const double* part, int S, int N, double* tot, float*
     const int n = blockIdx.x * 64 + threadIdx.x;
     const int sy = threadIdx.y;
     double s = 0.0;
+    // unrolled so the independent loads of a thread are in flight together (the adds stay in order:
+    // the same sum bit for bit); one load per iteration left it latency-bound (~20 us per launch)
     if (n < N)
+#pragma unroll 8
         for (int i = sy; i < S; i += kFinalLanes) s += part[(int64_t)i * N + n];
     __shared__ double red[kFinalLanes][64];
     red[sy][threadIdx.x] = s;

@@ -103,7 +103,7 @@ def mx8_quantize(x):
 def mx8_dequant(q, s):
     """(element codes [.., K] uint8, scale codes [.., K/32] uint8) -> fp64 values"""
     vals = q.view(torch.float8_e4m3fn).double().reshape(*q.shape[:-1], q.shape[-1] // 32, 32)
-    sc = torch.ldexp(torch.ones(s.shape, dtype=torch.float64), s.to(torch.int32) - 127)
+    sc = torch.ldexp(torch.ones(s.shape, dtype=torch.float64, device=s.device), s.to(torch.int32) - 127)
     return (vals * sc.unsqueeze(-1)).reshape(q.shape)
 
 
@@ -192,15 +192,18 @@ class Trainer:
     """forward, CombinedDepthLoss, backward, clip_grad_norm_(1.0), Adam — the GPU train_step's sequence."""
 
     def __init__(self, params, buffers, weights=(1.0, 0.1, 0.001, 0.01), lr=1e-4, wd=1e-5, clip=1.0,
-                 dtype=torch.float32, operands="bf16"):
+                 dtype=torch.float32, operands="bf16", device=None):
+        # device: where ATen evaluates the restatement (host by default; the full-size test evaluates
+        # its fp64 witness with ATen's GPU kernels)
         self.dtype, self.operands = dtype, operands
-        self.p = OrderedDict((k, v.clone().to(dtype)) for k, v in params.items())
-        self.bufs = OrderedDict((k, v.clone().to(dtype)) for k, v in buffers.items())
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self.p = OrderedDict((k, v.clone().to(self.device, dtype)) for k, v in params.items())
+        self.bufs = OrderedDict((k, v.clone().to(self.device, dtype)) for k, v in buffers.items())
         self.weights, self.clip = weights, clip
         self.opt = O.Adam(self.p, lr=lr, weight_decay=wd)
 
     def step(self, rgb, gt, K):
-        rgb, gt, K = rgb.to(self.dtype), gt.to(self.dtype), K.to(self.dtype)
+        rgb, gt, K = (t.to(self.device, self.dtype) for t in (rgb, gt, K))
         for v in self.p.values():
             v.requires_grad_(True)
             v.grad = None
@@ -223,6 +226,6 @@ class Trainer:
     def predict_eval(self, rgb):
         prev, O._GEMM["operands"] = O._GEMM["operands"], self.operands
         try:
-            return forward(rgb.to(self.dtype), self.p, self.bufs, False)
+            return forward(rgb.to(self.device, self.dtype), self.p, self.bufs, False)
         finally:
             O._GEMM["operands"] = prev

@@ -17,7 +17,9 @@ TRAIN = os.path.join(ROOT, "build", "train")
 
 @pytest.fixture(scope="module")
 def train_bin():
-    subprocess.run(["make", "-C", PKG, "train"], check=True, capture_output=True)
+    # (-o libcad_hip.so: the library is never rebuilt here — on a GPU box its object files are absent,
+    # and a rebuild would recompile every kernel inside the test session)
+    subprocess.run(["make", "-C", PKG, "-o", "libcad_hip.so", "train"], check=True, capture_output=True)
     return TRAIN
 
 

@@ -61,7 +61,7 @@ def test_config0_build_train_vs_oracle_trajectory(cad, dev, oracle, tmp_path):
     cfg["logging"]["log_dir"] = str(tmp_path / "logs")
     p = tmp_path / "cfg.yaml"
     p.write_text(yaml.safe_dump(cfg))
-    subprocess.run(["make", "-C", PKG, "train"], check=True, capture_output=True)
+    subprocess.run(["make", "-C", PKG, "-o", "libcad_hip.so", "train"], check=True, capture_output=True)
     r = subprocess.run([TRAIN, "-c", str(p), "-r", str(init)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert "Loaded model weights" in r.stdout
