@@ -265,7 +265,7 @@ def profiled(lib):
     return cm()
 
 
-def roofline_of(prof, steps, ms_per_step, show=False):
+def roofline_of(prof, steps, ms_per_step, show=False, table="pmc_traffic.json"):
     """roofline object of the dominant MFMA kernel (largest total time) of a profiled region:
     achieved = its algorithmic FLOPs / its summed HIP-event durations, against its engine's ceiling."""
     if show:
@@ -285,7 +285,7 @@ def roofline_of(prof, steps, ms_per_step, show=False):
     peak = (S3_PEAK_TFLOPS if s3 else BF16_MFMA_PEAK_TFLOPS if b1 else MX8_MFMA_PEAK_TFLOPS if x8
             else FP32_MFMA_PEAK_TFLOPS)
     roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": round(peak, 1), "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": pmc_traffic(dom["name"]),
+            "frac": round(achieved / peak, 4), "traffic": pmc_traffic(dom["name"], table),
             "arith": ("fp32 via exact 3-way bf16 split, 6 bf16 MFMA products per fp32 MAC: peak = dense "
                       "bf16 MFMA 2516.6 / 6; achieved counts algorithmic fp32 FLOPs") if s3 else
                      ("bf16 operands, fp32 accumulation (v_mfma_f32_32x32x16_bf16): peak = dense bf16 MFMA")
@@ -423,7 +423,7 @@ def extra_leg_resunet(cad, lib, dev, steps=10, warmup=3, B=32, H=480, W=640, fp8
             "warmup": warmup, "dtype": "fp8+bf16" if fp8 else "bf16", "params": params, "last_loss": last,
             "gflop_per_image": round(flop_img / 1e9, 2),
             "mfma_frac_dense_bf16": round(flop_img * value / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4),
-            "roofline": roofline_of(prof(), steps, 1e3 * dt / steps)}
+            "roofline": roofline_of(prof(), steps, 1e3 * dt / steps, table="pmc_traffic_c5.json")}
 
 
 def extra_leg_geonet(cad, lib, dev, steps=3, warmup=2, B=8, H=480, W=640, f=64):
@@ -461,9 +461,11 @@ def extra_leg_geonet(cad, lib, dev, steps=3, warmup=2, B=8, H=480, W=640, f=64):
             "steps": steps, "warmup": warmup, "dtype": "fp32", "params": params, "last_loss": last}
 
 
-def pmc_traffic(kernel_name):
-    """HBM bytes per launch of `kernel_name` from the committed rocprofv3 PMC summary, if any."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def pmc_traffic(kernel_name, table="pmc_traffic.json"):
+    """HBM bytes per launch of `kernel_name` from the committed rocprofv3 PMC summary, if any
+    (profiles/pmc_traffic.json: the U-Net workloads; pmc_traffic_c5.json: configs[4]'s network, whose
+    kernels share names with the U-Net's at other shapes)."""
+    path = os.path.join(ROOT, "profiles", table)
     try:
         with open(path) as fh:
             d = json.load(fh)

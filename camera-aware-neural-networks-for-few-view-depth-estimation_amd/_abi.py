@@ -148,6 +148,8 @@ SIGNATURES = {
     "cad_op_conv3x3_dgrad": (I, [P, I, P, I, P, I64, I, I, I, P]),
     "cad_op_conv3x3_wgrad": (I, [P, I, P, I64, I, I, P, I, I, I, P]),
     "cad_op_conv3x3_wgrad_bf16": (I, [P, I64, I, P, I64, I, I, P, I, I, I, P]),
+    "cad_op_conv3x3_fwd_bf16": (I, [P, I64, I, I, P, I, P, I64, I, I, I, I, I, I, P]),
+    "cad_op_conv3x3_dgrad_bf16": (I, [P, I64, I, P, I, P, I64, I, I, I, I, P]),
     "cad_op_mx8_quantize": (I, [P, I, I64, I, I, I64, P, P, I64, I, P]),
     "cad_op_dense_x8": (I, [P, P, I64, I, P, P, I64, I, P, I64, P]),
     "cad_op_conv3x3_x8": (I, [P, P, I64, I, P, P, I64, I, P, I, I, I, P]),

@@ -1756,6 +1756,46 @@ cad_status cad_op_conv3x3_wgrad_bf16(const void* dz, int64_t lddz, int cout, con
         HIPCHK(hipGetLastError());
     });
 }
+cad_status cad_op_conv3x3_fwd_bf16(const void* x, int64_t ldx, int xcoff, int cin, const float* w, int cout, void* y,
+                                  int64_t ldy, int ycoff, int y_bf16, int with_stats, int B, int H, int W, void* stream) {
+    return guard([&] {
+        require(cad::gemm_engine() == 2, "the pre-split convolution runs on the bf16 engine (CAD_GEMM_BF16)");
+        require(x && w && y && cin % 8 == 0 && xcoff % 8 == 0 && ldx % 8 == 0 && B > 0 && H > 0 && W > 0,
+                "bad arguments (bf16 rows: ldx, xcoff, cin multiples of 8)");
+        void* ws = nullptr;
+        float* stats = nullptr;
+        HIPCHK(hipMallocAsync(&ws, sizeof(uint16_t) * (size_t)cout * 9 * cin, S(stream)));
+        cad::split_rows(w, 9 * cin, 0, 9 * cin, cout, ws, 9 * cin, 0, S(stream));
+        if (with_stats) {
+            const int rows = cad::conv3x3_stats_rows(cin, B, H, W, cout, true);
+            HIPCHK(hipMallocAsync((void**)&stats, sizeof(float) * ((size_t)rows * (2 * cout + 1) + 4), S(stream)));
+        }
+        cad::conv3x3_fwd_ps(cad::Split{x, ldx, xcoff}, cin, cad::Split{ws, 9 * cin, 0}, cout, static_cast<float*>(y), ldy,
+                            ycoff, B, H, W, stats, S(stream), y_bf16 != 0);
+        if (stats) HIPCHK(hipFreeAsync(stats, S(stream)));
+        HIPCHK(hipFreeAsync(ws, S(stream)));
+        HIPCHK(hipGetLastError());
+    });
+}
+cad_status cad_op_conv3x3_dgrad_bf16(const void* dz, int64_t lddz, int cout, const float* w, int cin, void* dx,
+                                    int64_t lddx, int dx_bf16, int B, int H, int W, void* stream) {
+    return guard([&] {
+        require(cad::gemm_engine() == 2, "the pre-split convolution runs on the bf16 engine (CAD_GEMM_BF16)");
+        require(dz && w && dx && cout % 8 == 0 && cin % 8 == 0 && lddz % 8 == 0 && B > 0 && H > 0 && W > 0,
+                "bad arguments (bf16 rows: lddz, cout, cin multiples of 8)");
+        float* wd = nullptr;
+        void* wds = nullptr;
+        HIPCHK(hipMallocAsync((void**)&wd, sizeof(float) * (size_t)cout * 9 * cin, S(stream)));
+        HIPCHK(hipMallocAsync(&wds, sizeof(uint16_t) * (size_t)cout * 9 * cin, S(stream)));
+        cad::repack_conv_dgrad(w, wd, cout, cin, S(stream));
+        cad::split_rows(wd, 9 * cout, 0, 9 * cout, cin, wds, 9 * cout, 0, S(stream));
+        cad::conv3x3_dgrad_ps(cad::Split{dz, lddz, 0}, cout, cad::Split{wds, 9 * cout, 0}, cin, static_cast<float*>(dx),
+                              lddx, B, H, W, S(stream), dx_bf16 != 0);
+        HIPCHK(hipFreeAsync(wds, S(stream)));
+        HIPCHK(hipFreeAsync(wd, S(stream)));
+        HIPCHK(hipGetLastError());
+    });
+}
 cad_status cad_op_mx8_quantize(const void* src, int src_bf16, int64_t lds, int scoff, int C, int64_t M, void* q,
                                void* s, int64_t ldq, int qcoff, void* stream) {
     return guard([&] {

@@ -109,9 +109,28 @@ struct WinB {
 
 // Window epilogue: tile row mr -> output pixel (b, y0 + mr / CW, x0 + mr % CW), rows past H dropped.
 // EpiStore / EpiStoreStats semantics of gemm_epilogue_t (stats row = the block's linear index).
+// Timing experiments only (variant builds, `make VARIANT=... EXTRA=-DCAD_XP_WIN=k`; wrong outputs):
+// 1 = no stores (the epilogue's store cost), 2 = no BN partials, 3 = neither.
+#ifndef CAD_XP_WIN
+#define CAD_XP_WIN 0
+#endif
 template <int WM, int WN, int MI, int NJ, int CW, class Epi>
 __device__ __forceinline__ void win_epilogue(const GemmArgs& a, const floatx16 (&acc)[MI][NJ], int tile_lin, int n0,
                                              int b, int y0, int x0, float* lds) {
+    if constexpr (CAD_XP_WIN != 0) {
+        if constexpr ((CAD_XP_WIN & 1) != 0 && ((CAD_XP_WIN & 2) != 0 || !Epi::STATS)) {
+            // keep the accumulators live so the main loop is not removed
+            float t = 0.f;
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) t += acc[i][j][q];
+            if (t == 1234.5f) a.stats[0] = t;
+            return;
+        }
+    }
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
     const int wm = wave / WN, wn = wave % WN;
@@ -163,17 +182,19 @@ __device__ __forceinline__ void win_epilogue(const GemmArgs& a, const floatx16 (
                 }
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    if constexpr (Epi::BF16)
-                        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, (__bf16)v[q]), rs,
-                                                              lo + (uint32_t)(q * ldc4), 0, 0);
-                    else
-                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[q]), rs,
-                                                              lo + (uint32_t)(q * ldc4), 0, 0);
-                    if constexpr (Epi::STATS) bnp.add(j, v[q], y0 + r < a.H);
+                    if constexpr ((CAD_XP_WIN & 1) == 0) {
+                        if constexpr (Epi::BF16)
+                            __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, (__bf16)v[q]), rs,
+                                                                  lo + (uint32_t)(q * ldc4), 0, 0);
+                        else
+                            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[q]), rs,
+                                                                  lo + (uint32_t)(q * ldc4), 0, 0);
+                    }
+                    if constexpr (Epi::STATS && (CAD_XP_WIN & 2) == 0) bnp.add(j, v[q], y0 + r < a.H);
                 }
             }
         }
-    if constexpr (Epi::STATS) bnp.template finish<WM, WN>(a, lds, tile_lin, n0);
+    if constexpr (Epi::STATS && (CAD_XP_WIN & 2) == 0) bnp.template finish<WM, WN>(a, lds, tile_lin, n0);
 }
 
 // blocks: gridDim.x = B * ceil(H / R) * (W / CW) output blocks (XCD-aware order), gridDim.y = N tiles

@@ -407,6 +407,17 @@ cad_status cad_op_conv3x3_wgrad(const float* dz, int cout, const float* x, int64
  * cad_set_gemm_engine(CAD_GEMM_BF16). */
 cad_status cad_op_conv3x3_wgrad_bf16(const void* dz, int64_t lddz, int cout, const void* x, int64_t ldx, int xcoff,
                                      int cin, float* dw_ohwi, int B, int H, int W, void* stream);
+/* the bf16 engine's 3x3 convolution forward / input gradient on pre-split bf16 NHWC operands (the twins
+ * the engine stores), fp32 OHWI weights rounded to bf16 inside (the dgrad repacks them first):
+ * window kernels (gemm_win.hpp) when the shape allows, the im2col GEMM otherwise.  y / dx: fp32 rows, or
+ * bf16 rows with y_bf16 / dx_bf16.  with_stats: the forward also forms its BN tile partials (the
+ * EpiStoreStats epilogue; the partials are discarded — timing and coverage).  Requires
+ * cad_set_gemm_engine(CAD_GEMM_BF16); the bf16 forms of baseline_unet.h:32-42 DoubleConv's convs. */
+cad_status cad_op_conv3x3_fwd_bf16(const void* x, int64_t ldx, int xcoff, int cin, const float* w_ohwi, int cout,
+                                   void* y, int64_t ldy, int ycoff, int y_bf16, int with_stats, int B, int H, int W,
+                                   void* stream);
+cad_status cad_op_conv3x3_dgrad_bf16(const void* dz, int64_t lddz, int cout, const float* w_ohwi, int cin, void* dx,
+                                     int64_t lddx, int dx_bf16, int B, int H, int W, void* stream);
 cad_status cad_op_convT_fwd(const float* x, int cin, const float* w_iqo, const float* bias, int cout,
                             float* y, int64_t ldy, int ycoff, int B, int H, int W, void* stream);
 cad_status cad_op_convT_dgrad(const float* g, int64_t ldg, int gcoff, int cout, const float* w_iqo, int cin,

@@ -117,8 +117,10 @@ def main():
         fa, wa = sum(f) / len(f), sum(w) / len(w)
         traffic[k] = {"launches": len(f), "fetch_kb_avg": fa, "write_kb_avg": wa,
                       "hbm_bytes_per_launch": round((2 * fa + wa) * 1024)}
-    if traffic:   # merged: kernel names differ per engine, so several configs share the file
-        path = os.path.join(here, "pmc_traffic.json")
+    if traffic:   # merged: kernel names differ per engine, so several configs share the file —
+        # except config 5 (ResNet U-Net), whose kernels share names with the U-Net's at other shapes:
+        # its tags ("*_c5*") go to their own file
+        path = os.path.join(here, "pmc_traffic_c5.json" if "_c5" in tag else "pmc_traffic.json")
         merged = {}
         if os.path.exists(path):
             with open(path) as fh:

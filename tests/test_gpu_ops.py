@@ -351,3 +351,53 @@ def test_wgrad_two_level_slab_reduction(cad, dev, eng, B, H, W, splits, rem):
     reduce_launches = sum(r["launches"] for r in prof if "k_slab_reduce" in r["name"])
     assert reduce_launches == (3 if rem == 0 else 4), prof
     assert max_rel_err(dw.cpu().permute(0, 3, 1, 2), wd.grad) < TOL
+
+
+B1_WIN_SHAPES = [  # B, H, W, cin, cout: the bf16 engine's window forward / dgrad (k_conv3x3_win_bf16p4) tiles
+    (1, 6, 128, 64, 64),    # N == 64: 512 x 64 tile, CW 128; dgrad N = 64 likewise
+    (2, 9, 64, 32, 128),    # 256 x 128, CW 64, partial block row; dgrad N = 32 (im2col pre-split)
+    (1, 5, 32, 128, 128),   # CW 32
+    (2, 7, 16, 64, 256),    # CW 16; dgrad N = 64 with W 16 (512 x 64 needs W % 64: im2col)
+    (1, 13, 40, 256, 256),  # CW 8 (40 = 5 x 8), H = 13 < R = 32
+]
+
+
+@pytest.mark.parametrize("B,H,W,cin,cout", B1_WIN_SHAPES)
+def test_conv3x3_bf16_window_kernels(cad, dev, B, H, W, cin, cout):
+    """bf16 engine (cad_op_conv3x3_fwd_bf16 / _dgrad_bf16: the pre-split twins the step stores) against the
+    fp64 contraction of the bf16-rounded operands: fp32 outputs within TOL; bf16 outputs the fp64 value
+    rounded to bf16 (an fp32-accumulated sum sitting next to a rounding boundary may round the other
+    way: at most one bf16 ulp, on a small fraction of the outputs); the BN-statistics epilogue
+    produces the same outputs."""
+    lib = cad.load_library()
+    prev = lib.cad_get_gemm_engine()
+    assert lib.cad_set_gemm_engine(2) == 0
+    try:
+        g = torch.Generator().manual_seed(7 * B + H + cin + cout)
+        x = torch.randn(B, cin, H, W, generator=g).bfloat16()
+        w = torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)
+        dz = torch.randn(B, cout, H, W, generator=g).bfloat16()
+        xd, wd, dzd = x.double().requires_grad_(), w.bfloat16().double().requires_grad_(), dz.double()
+        y_ref = F.conv2d(xd, wd, None, 1, 1)
+        y_ref.backward(dzd)
+        xg, wg, dzg = nhwc(x).to(dev), w.permute(0, 2, 3, 1).contiguous().to(dev), nhwc(dz).to(dev)
+        for stats in (0, 1):
+            y = torch.zeros(B, H, W, cout, device=dev)
+            assert lib.cad_op_conv3x3_fwd_bf16(_p(xg), cin, 0, cin, _p(wg), cout, _p(y), cout, 0, 0, stats, B, H, W,
+                                               _s()) == 0, lib.cad_last_error()
+            torch.cuda.synchronize()
+            assert max_rel_err(nchw(y.cpu()), y_ref.detach()) < TOL, stats
+        yb = torch.zeros(B, H, W, cout, dtype=torch.bfloat16, device=dev)
+        assert lib.cad_op_conv3x3_fwd_bf16(_p(xg), cin, 0, cin, _p(wg), cout, _p(yb), cout, 0, 1, 1, B, H, W, _s()) == 0
+        torch.cuda.synchronize()
+        want = nhwc(y_ref.detach()).bfloat16()
+        diff = (yb.cpu().float() - want.float()).abs()
+        ulp = torch.exp2(torch.floor(torch.log2(want.float().abs().clamp_min(1e-30))) - 7)
+        assert (diff <= ulp + 0).all() and (diff > 0).float().mean().item() < 1e-2
+        dx = torch.zeros(B, H, W, cin, device=dev)
+        assert lib.cad_op_conv3x3_dgrad_bf16(_p(dzg), cout, cout, _p(wg), cin, _p(dx), cin, 0, B, H, W, _s()) == 0, \
+            lib.cad_last_error()
+        torch.cuda.synchronize()
+        assert max_rel_err(nchw(dx.cpu()), xd.grad) < TOL
+    finally:
+        lib.cad_set_gemm_engine(prev)
