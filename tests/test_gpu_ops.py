@@ -366,9 +366,9 @@ B1_WIN_SHAPES = [  # B, H, W, cin, cout: the bf16 engine's window forward / dgra
 def test_conv3x3_bf16_window_kernels(cad, dev, B, H, W, cin, cout):
     """bf16 engine (cad_op_conv3x3_fwd_bf16 / _dgrad_bf16: the pre-split twins the step stores) against the
     fp64 contraction of the bf16-rounded operands: fp32 outputs within TOL; bf16 outputs the fp64 value
-    rounded to bf16 (an fp32-accumulated sum sitting next to a rounding boundary may round the other
-    way: at most one bf16 ulp, on a small fraction of the outputs); the BN-statistics epilogue
-    produces the same outputs."""
+    rounded to bf16 (an fp32-accumulated sum next to a rounding boundary may round the other way: at
+    most one bf16 spacing — floored at that of 2^-10 of the largest output — on under 1e-2 of the
+    outputs); the BN-statistics epilogue produces the same outputs."""
     lib = cad.load_library()
     prev = lib.cad_get_gemm_engine()
     assert lib.cad_set_gemm_engine(2) == 0
@@ -390,10 +390,14 @@ def test_conv3x3_bf16_window_kernels(cad, dev, B, H, W, cin, cout):
         yb = torch.zeros(B, H, W, cout, dtype=torch.bfloat16, device=dev)
         assert lib.cad_op_conv3x3_fwd_bf16(_p(xg), cin, 0, cin, _p(wg), cout, _p(yb), cout, 0, 1, 1, B, H, W, _s()) == 0
         torch.cuda.synchronize()
-        want = nhwc(y_ref.detach()).bfloat16()
-        diff = (yb.cpu().float() - want.float()).abs()
-        ulp = torch.exp2(torch.floor(torch.log2(want.float().abs().clamp_min(1e-30))) - 7)
-        assert (diff <= ulp + 0).all() and (diff > 0).float().mean().item() < 1e-2
+        want = nhwc(y_ref.detach()).bfloat16().float()
+        got = yb.cpu().float()
+        diff = (got - want).abs()
+        # one bf16 spacing of the larger of the two, floored at the spacing of 2^-10 of the layer's largest
+        # value (an output whose terms cancel to ~0 carries fp32 accumulation error far above its own ulp)
+        big = torch.maximum(got.abs(), want.abs()).clamp_min(2.0 ** -10 * want.abs().max().item())
+        ulp = torch.exp2(torch.floor(torch.log2(big)) - 7)
+        assert (diff <= ulp).all() and (diff > 0).float().mean().item() < 1e-2, (diff / ulp).max().item()
         dx = torch.zeros(B, H, W, cin, device=dev)
         assert lib.cad_op_conv3x3_dgrad_bf16(_p(dzg), cout, cout, _p(wg), cin, _p(dx), cin, 0, B, H, W, _s()) == 0, \
             lib.cad_last_error()
