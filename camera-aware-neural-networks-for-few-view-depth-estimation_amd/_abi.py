@@ -154,6 +154,7 @@ SIGNATURES = {
     "cad_op_dense_x8": (I, [P, P, I64, I, P, P, I64, I, P, I64, P]),
     "cad_op_conv3x3_x8": (I, [P, P, I64, I, P, P, I64, I, P, I, I, I, P]),
     "cad_op_convT_fwd": (I, [P, I, P, P, I, P, I64, I, I, I, I, P]),
+    "cad_op_convT_fwd_bf16": (I, [P, I64, I, I, P, P, I, P, I64, I, I, I, I, P]),
     "cad_op_convT_dgrad": (I, [P, I64, I, I, P, I, P, I, I, I, P]),
     "cad_op_convT_wgrad": (I, [P, I, P, I64, I, I, P, I, I, I, P]),
     "cad_op_maxpool_fwd": (I, [P, I64, I, I, I, I, P, P, P]),

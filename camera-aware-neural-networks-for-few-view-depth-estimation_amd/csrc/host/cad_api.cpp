@@ -135,6 +135,10 @@ struct DoubleConv {
     // many standard deviations from zero, so bf16-stored values would cost x-hat several % (measured:
     // enc1.bn1 gradients 5x further from fp64 than the fp32 oracle's)
     bool y1_f32 = false;
+    // the last forward recomputed conv1 instead of storing y1 (enc1: rc1_on): its consumers (bn1
+    // apply, bn1 backward, the y1 debug buffer) relaunch the conv GEMM from the input and weights
+    // that forward used (the twins on the bf16 engine, the rc_w snapshot on S3)
+    bool y1_rc = false;
     void* a1s = nullptr;   // pre-split a1 (gemm_ps.hpp)
     int first_param = 0, last_param = 0;   // [first, last] indices in named_parameters()
     bool has_film() const { return film.p0 >= 0; }
@@ -204,6 +208,10 @@ struct cad_unet {
     double* dscr = nullptr;    // column-reduction scratch
     float* slab = nullptr;
     int64_t slab_cap = 0;
+    // recomputed enc1.conv1 (rc1_on): per-tile BN-backward partials, and the fp32 weights the last
+    // forward used (S3 engine; the bf16 engine's weight twin is already such a copy)
+    double* rc_part = nullptr;
+    float* rc_w = nullptr;
     // stage grad ranges
     std::vector<std::pair<int64_t, int64_t>> stage_range;
 
@@ -418,6 +426,9 @@ void layout(cad_unet* h, Arena& a) {
     }
     h->slab_cap = std::min<int64_t>(sl, (int64_t)64 << 20);
     h->slab = a.f(h->slab_cap);
+    // recomputed enc1.conv1: tiles of at least 64 rows (the tile height follows the engine at run time)
+    h->rc_part = a.d((h->Ml(0, B) + 63) / 64 * 2 * h->Cl(0));
+    h->rc_w = a.f((int64_t)h->enc[0].c1.cout * 9 * h->enc[0].c1.cin);
     // buffers table (running stats), named_buffers() order (parameter order of the BNs)
     h->bufs.clear();
     auto add_bn_bufs = [&](const std::string& pre, BN& b) {
@@ -475,16 +486,29 @@ void split_into(const float* x, int64_t ldx, int xcoff, int C, int64_t M, void* 
                 hipStream_t st) {
     if (out) cad::split_rows(x, ldx, xcoff, C, M, out, ldo, ocoff, st);
 }
-void split_weights(const cad_unet* h, hipStream_t st) {   // forward weights, every forward (they change per step)
-    auto sw = [&](const Conv& c) {
-        if (c.ws) cad::split_rows(h->P(c.pidx), 9 * c.cin, 0, 9 * c.cin, c.cout, c.ws, 9 * c.cin, 0, st);
-    };
-    for (int l = 0; l < 5; ++l) { sw(h->enc[l].c1); sw(h->enc[l].c2); }
+void wprep_add(cad::WPrepList& L, int kind, const float* src, float* d32, void* d16, int cout, int cin, int64_t n) {
+    if (!d32 && !d16) return;
+    if (L.njobs == cad::kWPrepMaxJobs) throw std::runtime_error("weight_prep: job list full");
+    cad::WPrepJob& j = L.job[L.njobs++];
+    j.src = src; j.d32 = d32; j.d16 = d16; j.kind = kind; j.cout = cout; j.cin = cin; j.n = n;
+}
+// forward weights, every forward (they change per step), in one launch: the ConvT forward repack
+// [q][co][ci] (rows 4*cout, K = cin) and, with pre-split operands, the bf16 twins of the conv weights
+// and of that repack
+void prep_fwd_weights(const cad_unet* h, bool ps, hipStream_t st) {
+    cad::WPrepList L{};
     for (int l = 0; l < 4; ++l) {
-        sw(h->dec[l].c1); sw(h->dec[l].c2);
-        const Up& u = h->up[l];   // forward repack [q][co][ci]: rows 4*cout, K = cin
-        cad::split_rows(u.wf, u.cin, 0, u.cin, 4 * u.cout, u.wfs, u.cin, 0, st);
+        const Up& u = h->up[l];
+        wprep_add(L, cad::WPREP_CONVT, h->P(u.widx), u.wf, ps ? u.wfs : nullptr, u.cout, u.cin, (int64_t)4 * u.cout * u.cin);
     }
+    if (ps) {
+        auto sw = [&](const Conv& c) {
+            if (c.ws) wprep_add(L, cad::WPREP_SPLIT, h->P(c.pidx), nullptr, c.ws, c.cout, c.cin, (int64_t)c.cout * 9 * c.cin);
+        };
+        for (int l = 0; l < 5; ++l) { sw(h->enc[l].c1); sw(h->enc[l].c2); }
+        for (int l = 0; l < 4; ++l) { sw(h->dec[l].c1); sw(h->dec[l].c2); }
+    }
+    cad::weight_prep(L, st);
 }
 
 // in_s / out_s: split twins of the block input / output (p == nullptr: none)
@@ -500,6 +524,33 @@ int env_flag(const char* name, int dflt) {
 bool conv1_presplit(cad_unet* h, const DoubleConv& dc, bool ps, const cad::Split& in_s) {
     static const bool enc1_ps = env_flag("CAD_ENC1PS", 1) != 0;
     return ps && in_s.p && dc.c1.ws && (enc1_ps || &dc != &h->enc[0]);
+}
+// enc1.conv1 recomputed instead of stored (round 4): its K = 9 x 8 GEMM reads 16 B per pixel (the
+// NHWC8 input twin; 32 B fp32 on S3) and is cheaper to run again than its fp32 output is to write and
+// re-read three times (256 B per pixel at f = 64).  Plain DoubleConv only (the FiLM blocks' affine
+// passes read y1 as well), on the S3 engine or on the bf16 engine's pre-split kernels with the fp32
+// y1 of enc1.  On the S3 engine the recomputation costs six bf16 products per MAC and four
+// launches (stats, apply, backward sums, backward apply) — about what the fp32 y1 traffic costs — so
+// it is off there.  Measured on the bf16 engine (configs[3], MI355X): 487.2 vs 487.4 / 488.8 img/s —
+// the three recomputing GEMMs (0.56 + 0.78 + 0.86 ms, their 2-byte epilogue stores and gradient loads
+// at ~3 TB/s) cost what the removed BN passes did, so it is off by default too.  CAD_RC1=0 (default):
+// stored y1; 1: recompute on the bf16 engine; 2: on both (A/B switch; the same arithmetic bit for bit,
+// tests/test_gpu_headfuse.py).
+bool rc1_on(cad_unet* h, const DoubleConv& dc, bool ps1) {
+    static const int mode = env_flag("CAD_RC1", 0);
+    if (mode <= 0 || &dc != &h->enc[0] || dc.has_film()) return false;
+    const int e = cad::gemm_engine();
+    if (e == 1) return mode >= 2 && !ps1;
+    if (e == 2) return ps1 && dc.y1_f32 && !dc.y1b;
+    return false;
+}
+// the recomputed conv1's operands: the input as the forward read it and the weights it used
+struct Rc1Ops {
+    const void* x; int64_t ldx; const void* w;
+};
+Rc1Ops rc1_ops(cad_unet* h, const DoubleConv& dc, const float* in, int64_t ldin, const cad::Split& in_s, bool ps1) {
+    if (ps1) return {in_s.p, in_s.ld, dc.c1.ws};
+    return {in, ldin, h->rc_w};
 }
 
 // head_pred != nullptr: the block's bn2 + ReLU feeds the depth head directly (level-0 fusion): sig
@@ -526,12 +577,30 @@ void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin,
     static const bool enc1_bf16 = env_flag("CAD_ENC1BF16", 0) != 0;
     dc.y1b = ps1 && (!dc.y1_f32 || enc1_bf16);
     dc.y2b = ps;
-    if (ps1)
+    dc.y1_rc = rc1_on(h, dc, ps1);
+    if (dc.y1_rc) {   // statistics only; the BN apply recomputes the conv (rc1_on)
+        if (!ps1)
+            HIPCHK(hipMemcpyAsync(h->rc_w, h->P(dc.c1.pidx), sizeof(float) * (size_t)C * 9 * dc.c1.cin,
+                                  hipMemcpyDeviceToDevice, st));
+        const Rc1Ops o = rc1_ops(h, dc, in, ldin, in_s, ps1);
+        cad::RecomputeArgs r;
+        r.mode = cad::Recompute::Stats;
+        r.stats = stats;
+        if (tr) cad::conv3x3_recompute(o.x, o.ldx, dc.c1.cin, o.w, C, B, Hh, Ww, r, st);
+        bn(dc.b1, dc.c1.cin, ps1);
+        r.mode = cad::Recompute::BnRelu;
+        r.scale = dc.b1.scale; r.shift = dc.b1.shift;
+        r.out = ps ? dc.a1s : dc.a1; r.ldo = C; r.out_bf16 = ps;
+        cad::conv3x3_recompute(o.x, o.ldx, dc.c1.cin, o.w, C, B, Hh, Ww, r, st);
+    } else if (ps1) {
         cad::conv3x3_fwd_ps(in_s, dc.c1.cin, sv(dc.c1.ws, 9 * dc.c1.cin), C, dc.y1, C, 0, B, Hh, Ww, stats, st, dc.y1b);
-    else
+    } else {
         cad::conv3x3_fwd(in, ldin, 0, dc.c1.cin, h->P(dc.c1.pidx), C, dc.y1, C, 0, B, Hh, Ww, stats, st);
-    bn(dc.b1, dc.c1.cin, ps1);
-    if (dc.has_film()) {   // FiLMDoubleConvImpl::forward (intrinsics_unet.h:38-52)
+    }
+    if (!dc.y1_rc) bn(dc.b1, dc.c1.cin, ps1);
+    if (dc.y1_rc) {
+        // (a1 written by the recompute above)
+    } else if (dc.has_film()) {   // FiLMDoubleConvImpl::forward (intrinsics_unet.h:38-52)
         // pre-split GEMMs read only a1's twin (written by the same pass): the fp32 a1 is not written
         cad::film_apply(dc.y1, C, dc.b1.scale, dc.b1.shift, dc.film.gam, dc.film.bet, B, (int64_t)Hh * Ww,
                         ps ? nullptr : dc.a1, st, dc.y1b, ps ? dc.a1s : nullptr);
@@ -584,9 +653,7 @@ void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth
     // its loaders (pre-split S3 operands are 6 bytes per element: measured 112 -> 101 img/s).
     h->fwd_np = h->f % 8 ? 0 : cad::split_planes();
     const bool ps = h->fwd_np > 0;
-    for (int l = 0; l < 4; ++l)
-        cad::repack_convT_fwd(h->P(h->up[l].widx), h->up[l].wf, h->up[l].cin, h->up[l].cout, st);
-    if (ps) split_weights(h, st);
+    prep_fwd_weights(h, ps, st);
     if (h->model != CAD_MODEL_BASELINE) {
         // a14 normalisation, then every block's FiLM MLP (gamma/beta depend on the camera only)
         cad::camera_normalize(cam4, B, h->H, h->W, h->camn, st);
@@ -679,9 +746,26 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     // in-loader weight gradient)
     const bool ps1 = conv1_presplit(h, dc, ps, in_s);
     const bool dy1_f32 = !ps1 || (din && !(ps && dc.c1.wds));
-    cad::bn_relu_bwd(dA1, C, 0, dc.y1, C, dc.b1.mean, dc.b1.invstd, dc.b1.scale, dc.b1.shift, h->P(dc.b1.widx), M,
-                     h->dscr, dc.b1.coef, h->G(dc.b1.widx), h->G(dc.b1.bidx), dy1_f32 ? dY : nullptr, st,
-                     dc.has_film() ? dc.film.gam : nullptr, HW, ps ? dYs : nullptr, true, dc.y1b, nullptr, ps);
+    if (dc.y1_rc) {   // bn1 backward on the recomputed conv1 (rc1_on): the sums, then the apply
+        if (din || (ps && dy1_f32) || (!ps && !dy1_f32)) throw std::runtime_error("recomputed conv1: unexpected block");
+        const Rc1Ops o = rc1_ops(h, dc, in, ldin, in_s, ps1);
+        cad::RecomputeArgs r;
+        r.mode = cad::Recompute::BwdSums;
+        r.scale = dc.b1.scale; r.shift = dc.b1.shift; r.mean = dc.b1.mean; r.invstd = dc.b1.invstd;
+        r.g = dA1; r.ldg = C; r.g_bf16 = ps;
+        r.part = h->rc_part;
+        cad::conv3x3_recompute(o.x, o.ldx, dc.c1.cin, o.w, C, B, Hh, Ww, r, st);
+        cad::bn_bwd_from_tiles(h->rc_part, cad::recompute_tiles(dc.c1.cin, B, Hh, Ww, C), C, M, h->P(dc.b1.widx),
+                               dc.b1.invstd, dc.b1.coef, h->G(dc.b1.widx), h->G(dc.b1.bidx), h->dscr, st);
+        r.mode = cad::Recompute::BwdApply;
+        r.coef = dc.b1.coef;
+        r.out = ps ? dYs : static_cast<void*>(dY); r.ldo = C; r.out_bf16 = ps;
+        cad::conv3x3_recompute(o.x, o.ldx, dc.c1.cin, o.w, C, B, Hh, Ww, r, st);
+    } else {
+        cad::bn_relu_bwd(dA1, C, 0, dc.y1, C, dc.b1.mean, dc.b1.invstd, dc.b1.scale, dc.b1.shift, h->P(dc.b1.widx), M,
+                         h->dscr, dc.b1.coef, h->G(dc.b1.widx), h->G(dc.b1.bidx), dy1_f32 ? dY : nullptr, st,
+                         dc.has_film() ? dc.film.gam : nullptr, HW, ps ? dYs : nullptr, true, dc.y1b, nullptr, ps);
+    }
     if (dc.has_film()) cad::film_mlp_bwd(film_view(h, dc), h->camn, B, st);
     // conv1: wgrad, dgrad
     if (ps1)
@@ -699,11 +783,11 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     }
 }
 
-void repack_dgrad_weights(cad_unet* h, hipStream_t st) {
+void repack_dgrad_weights(cad_unet* h, hipStream_t st) {   // one launch (prep_fwd_weights)
     const bool ps = h->fwd_np > 0 && h->fwd_np == cad::split_planes();
+    cad::WPrepList L{};
     auto rp = [&](Conv& c) {   // dgrad repack [ci][tap][co]: rows cin, K = 9*cout
-        cad::repack_conv_dgrad(h->P(c.pidx), c.wd, c.cout, c.cin, st);
-        if (ps && c.wds) cad::split_rows(c.wd, 9 * c.cout, 0, 9 * c.cout, c.cin, c.wds, 9 * c.cout, 0, st);
+        wprep_add(L, cad::WPREP_DGRAD, h->P(c.pidx), c.wd, ps ? c.wds : nullptr, c.cout, c.cin, (int64_t)c.cout * 9 * c.cin);
     };
     for (int l = 0; l < 5; ++l) {
         if (l > 0) rp(h->enc[l].c1);
@@ -713,8 +797,9 @@ void repack_dgrad_weights(cad_unet* h, hipStream_t st) {
         rp(h->dec[l].c1);
         rp(h->dec[l].c2);
         const Up& u = h->up[l];   // ConvT weights [ci][q][co]: rows cin, K = 4*cout
-        if (ps) cad::split_rows(h->P(u.widx), 4 * u.cout, 0, 4 * u.cout, u.cin, u.wms, 4 * u.cout, 0, st);
+        if (ps) wprep_add(L, cad::WPREP_SPLIT, h->P(u.widx), nullptr, u.wms, u.cout, u.cin, (int64_t)4 * u.cout * u.cin);
     }
+    cad::weight_prep(L, st);
 }
 
 // stages: 0 head, 1..4 dec1..dec4, 5 bottleneck, 6..9 enc4..enc1
@@ -1113,6 +1198,27 @@ int64_t cad_unet_debug_buffer(cad_unet* h, const char* name, float* host, int64_
     if (!p || cnt < 0) {
         g_err = "unknown debug buffer '" + n + "'";
         return -1;
+    }
+    if (l == 0 && n == "enc0_y1" && h->enc[0].y1_rc) {
+        // the last forward recomputed enc1.conv1 instead of storing it: run it once more into y1 from
+        // the same input and weights (cad_unet_debug_buffer is a test hook; CAD_RC1=0 stores y1)
+        DoubleConv& dc = h->enc[0];
+        const bool ps1 = h->fwd_np > 0 && h->x0s && dc.c1.ws;
+        const cad::Split in_s = ps1 ? sv(h->x0s, h->x0_ld) : cad::Split{};
+        const Rc1Ops o = rc1_ops(h, dc, h->x0, h->x0_ld, in_s, ps1);
+        cad::RecomputeArgs r;
+        r.mode = cad::Recompute::Store;
+        r.out = dc.y1; r.ldo = h->Cl(0);
+        try {
+            cad::conv3x3_recompute(o.x, o.ldx, dc.c1.cin, o.w, h->Cl(0), B, h->Hl(0), h->Wl(0), r, nullptr);
+        } catch (const std::exception& e) {
+            g_err = e.what();
+            return -1;
+        }
+        if (hipDeviceSynchronize() != hipSuccess) {
+            g_err = "recomputing enc0_y1 failed";
+            return -1;
+        }
     }
     if (n == "dout0" && h->head_fused) {
         g_err = "debug buffer 'dout0' is not written when decoder level 0 is fused with the head (CAD_HEADFUSE=0 keeps it)";
@@ -1836,6 +1942,26 @@ cad_status cad_op_convT_fwd(const float* x, int cin, const float* w, const float
         HIPCHK(hipMallocAsync((void**)&wf, sizeof(float) * (size_t)cout * 4 * cin, S(stream)));
         cad::repack_convT_fwd(w, wf, cin, cout, S(stream));
         cad::convT_fwd(x, cin, cin, wf, bias, cout, y, ldy, ycoff, B, H, W, S(stream));
+        HIPCHK(hipFreeAsync(wf, S(stream)));
+        HIPCHK(hipGetLastError());
+    });
+}
+cad_status cad_op_convT_fwd_bf16(const void* x, int64_t ldx, int xcoff, int cin, const float* w, const float* bias,
+                                 int cout, void* y, int64_t ldy, int ycoff, int B, int H, int W, void* stream) {
+    return guard([&] {
+        require(cad::gemm_engine() == 2, "the pre-split ConvTranspose runs on the bf16 engine (CAD_GEMM_BF16)");
+        require(x && w && bias && y && cin % 8 == 0 && cout % 8 == 0 && xcoff % 8 == 0 && ldx % 8 == 0 && B > 0 &&
+                    H > 0 && W > 0,
+                "bad arguments (bf16 rows: ldx, xcoff, cin, cout multiples of 8)");
+        float* wf = nullptr;
+        void* wfs = nullptr;
+        HIPCHK(hipMallocAsync((void**)&wf, sizeof(float) * (size_t)cout * 4 * cin, S(stream)));
+        HIPCHK(hipMallocAsync(&wfs, sizeof(uint16_t) * (size_t)cout * 4 * cin, S(stream)));
+        cad::repack_convT_fwd(w, wf, cin, cout, S(stream));
+        cad::split_rows(wf, cin, 0, cin, 4 * cout, wfs, cin, 0, S(stream));
+        cad::convT_fwd_ps(cad::Split{x, ldx, xcoff}, cin, cad::Split{wfs, cin, 0}, bias, cout, static_cast<float*>(y),
+                          ldy, ycoff, B, H, W, S(stream), true);
+        HIPCHK(hipFreeAsync(wfs, S(stream)));
         HIPCHK(hipFreeAsync(wf, S(stream)));
         HIPCHK(hipGetLastError());
     });

@@ -140,6 +140,13 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_win_bf16p4(GemmArgs a) {
     conv3x3_win_ps_body<R, CW, BN64 ? 4 : 2, BN64 ? 1 : 2, Epi, 4>(a);
 }
 
+// ... 256 x 96 tiles (2 x 3 blocks of 32 x 32 per wave, four waves down M) for N % 96 == 0: the 96 and
+// 192-channel levels at f = 96
+template <int R, int CW, class Epi>
+__global__ __launch_bounds__(256, 2) void k_conv3x3_win_bf16p3(GemmArgs a) {
+    conv3x3_win_ps_body<R, CW, 4, 1, Epi, 2, 3>(a);
+}
+
 // ... the same tiles with LDS-DMA staging (conv3x3_win_dma_body: 3-stage ring, one workgroup per CU)
 template <int R, int CW, class Epi, bool BN64 = false>
 __global__ __launch_bounds__(256, 1) void k_conv3x3_win_bf16d(GemmArgs a) {
@@ -248,6 +255,16 @@ __global__ __launch_bounds__(256) void k_convT_dgrad_bf16p(GemmArgs a) { convT_d
 template <int WM, int WN, int KB>
 __global__ __launch_bounds__(256) void k_convT_dgrad_bf16pb(GemmArgs a) {
     convT_dgrad_psb<1, WM, WN, 2, 2, KB, EpiStoreB16>(a);
+}
+// ... 256 x 128 tiles (2 x 2 waves of 4 x 2 blocks): each A row-stage feeds twice the MFMA work (the
+// ConvT GEMMs' K is cin or 4 cout, 128..2048: short main loops that the 128 x 128 tile left issue-bound)
+template <int KB>
+__global__ __launch_bounds__(256, 2) void k_convT_fwd_bf16pt4(GemmArgs a) {
+    convT_fwd_psb<1, 2, 2, 4, 2, KB, EpiConvTB16>(a);
+}
+template <int KB>
+__global__ __launch_bounds__(256, 2) void k_convT_dgrad_bf16pb4(GemmArgs a) {
+    convT_dgrad_psb<1, 2, 2, 4, 2, KB, EpiStoreB16>(a);
 }
 template <int WM, int WN, int KB>
 __global__ __launch_bounds__(256) void k_conv3x3_wgrad_bf16p(GemmArgs a) { conv3x3_wgrad_psb<1, WM, WN, 2, 2, KB>(a); }
@@ -395,6 +412,24 @@ CAD_KT(KConvFwdP1B, (k_conv3x3_fwd_bf16p<WM, WN, KB, EpiStoreB16>),
 CAD_KT(KConvFwdSP1B, (k_conv3x3_fwd_bf16p<WM, WN, KB, EpiStoreStatsB16>),
        "void cad::k_conv3x3_fwd_bf16p<%d, %d, %d, cad::EpiStoreStatsB16>(cad::GemmArgs)")
 CAD_KT(KDenseWgradP1, (k_dense_wgrad_bf16p<WM, WN, KB>), "void cad::k_dense_wgrad_bf16p<%d, %d, %d>(cad::GemmArgs)")
+// recomputed convolution (conv3x3_recompute): S3 in-loader and B1 pre-split forms
+#define CAD_RC_KT(T, E, ES)                                                                                   \
+    CAD_KT(KRcS3##T, (k_conv3x3_fwd_s3<WM, WN, KB, E>), "void cad::k_conv3x3_fwd_s3<%d, %d, %d, cad::" ES ">(cad::GemmArgs)") \
+    CAD_KT(KRcP1##T, (k_conv3x3_fwd_bf16p<WM, WN, KB, E>), "void cad::k_conv3x3_fwd_bf16p<%d, %d, %d, cad::" ES ">(cad::GemmArgs)")
+using EpiBnReluF = EpiBnRelu<false>;
+using EpiBnReluB = EpiBnRelu<true>;
+using EpiBnBwdSumsF = EpiBnBwdSums<false>;
+using EpiBnBwdSumsB = EpiBnBwdSums<true>;
+using EpiBnBwdApplyF = EpiBnBwdApply<false, false>;
+using EpiBnBwdApplyB = EpiBnBwdApply<true, true>;
+CAD_RC_KT(Stats, EpiStatsOnly, "EpiStatsOnly")
+CAD_RC_KT(Relu, EpiBnReluF, "EpiBnRelu<false>")
+CAD_RC_KT(ReluB, EpiBnReluB, "EpiBnRelu<true>")
+CAD_RC_KT(Sums, EpiBnBwdSumsF, "EpiBnBwdSums<false>")
+CAD_RC_KT(SumsB, EpiBnBwdSumsB, "EpiBnBwdSums<true>")
+CAD_RC_KT(Apply, EpiBnBwdApplyF, "EpiBnBwdApply<false, false>")
+CAD_RC_KT(ApplyB, EpiBnBwdApplyB, "EpiBnBwdApply<true, true>")
+#undef CAD_RC_KT
 CAD_KT(KConvTFwdP1T, (k_convT_fwd_bf16pt<WM, WN, KB>), "void cad::k_convT_fwd_bf16pt<%d, %d, %d>(cad::GemmArgs)")
 CAD_KT(KConvTDgradP1B, (k_convT_dgrad_bf16pb<WM, WN, KB>), "void cad::k_convT_dgrad_bf16pb<%d, %d, %d>(cad::GemmArgs)")
 CAD_KT(KDenseAddP1, (k_dense_bf16p<WM, WN, KB, EpiStoreAdd>), "void cad::k_dense_bf16p<%d, %d, %d, cad::EpiStoreAdd>(cad::GemmArgs)")
@@ -427,7 +462,8 @@ void launch_engine(Cfg c, bool fwd_kind, GemmArgs& a, hipStream_t st) {
 struct WinPick {
     int R = 0, CW = 0;
     bool big = false;   // B1 4 x 2 blocks per wave (k_conv3x3_win_bf16p4): 256 x 128, or 512 x 64 tiles
-    int bn() const { return big ? (R * CW == 256 ? 128 : 64) : R * CW == 128 ? 128 : 64; }
+    bool n96 = false;   // B1 256 x 96 tiles (k_conv3x3_win_bf16p3)
+    int bn() const { return n96 ? 96 : big ? (R * CW == 256 ? 128 : 64) : R * CW == 128 ? 128 : 64; }
 };
 WinPick pick_win(int cin, int W, int N) {
     WinPick w;
@@ -459,19 +495,21 @@ bool win_dma() {
 }
 
 // PS = false: S3 window kernel (fp32 operands, in-loader split); true: B1 on the pre-split twins
-template <bool PS, int R, int CW, class Epi, bool BIG = false>
+template <bool PS, int R, int CW, class Epi, bool BIG = false, bool N96 = false>
 void launch_win1(const GemmArgs& a, hipStream_t st) {
-    constexpr int BN = BIG ? (R * CW == 256 ? 128 : 64) : R * CW == 128 ? 128 : 64;
+    constexpr int BN = N96 ? 96 : BIG ? (R * CW == 256 ? 128 : 64) : R * CW == 128 ? 128 : 64;
+    if (a.N % BN) throw std::runtime_error("window conv: N not a multiple of the tile");
     const dim3 grid(win_blocks(WinPick{R, CW}, a.B, a.H, a.W), cdiv(a.N, BN));
     void (*fn)(GemmArgs);
-    const bool dma = BIG && win_dma();
-    if constexpr (BIG) fn = dma ? k_conv3x3_win_bf16d<R, CW, Epi, BN == 64> : k_conv3x3_win_bf16p4<R, CW, Epi, BN == 64>;
+    const bool dma = BIG && !N96 && win_dma();
+    if constexpr (N96) fn = k_conv3x3_win_bf16p3<R, CW, Epi>;
+    else if constexpr (BIG) fn = dma ? k_conv3x3_win_bf16d<R, CW, Epi, BN == 64> : k_conv3x3_win_bf16p4<R, CW, Epi, BN == 64>;
     else fn = PS ? (void (*)(GemmArgs))k_conv3x3_win_bf16p<R, CW, Epi> : (void (*)(GemmArgs))k_conv3x3_win_s3<R, CW, Epi>;
     if (prof_enabled()) {
         char name[160];
         snprintf(name, sizeof(name), "void cad::k_conv3x3_win_%s<%d, %d, cad::%s%s>(cad::GemmArgs)",
-                 dma ? "bf16d" : BIG ? "bf16p4" : PS ? "bf16p" : "s3", R, CW, Epi::STATS ? "EpiStoreStats" : "EpiStore",
-                 Epi::BF16 ? "B16" : "");
+                 N96 ? "bf16p3" : dma ? "bf16d" : BIG ? "bf16p4" : PS ? "bf16p" : "s3", R, CW,
+                 Epi::STATS ? "EpiStoreStats" : "EpiStore", Epi::BF16 ? "B16" : "");
         prof_push(name, 2.0 * a.M * a.N * (double)a.K, st);
         hipLaunchKernelGGL(fn, grid, dim3(256), 0, st, a);
         prof_pop(st);
@@ -482,6 +520,16 @@ void launch_win1(const GemmArgs& a, hipStream_t st) {
 template <class Epi, bool PS = false>
 void launch_win(const WinPick& w, const GemmArgs& a, hipStream_t st) {
     if constexpr (PS) {
+        if (w.n96) {   // 256 x 96
+            switch (w.CW) {
+                case 128: launch_win1<PS, 2, 128, Epi, true, true>(a, st); return;
+                case 64: launch_win1<PS, 4, 64, Epi, true, true>(a, st); return;
+                case 32: launch_win1<PS, 8, 32, Epi, true, true>(a, st); return;
+                case 16: launch_win1<PS, 16, 16, Epi, true, true>(a, st); return;
+                case 8: launch_win1<PS, 32, 8, Epi, true, true>(a, st); return;
+            }
+            throw std::runtime_error("window conv: block shape not built");
+        }
         if (w.big && w.R * w.CW == 256) {
             switch (w.CW) {
                 case 128: launch_win1<PS, 2, 128, Epi, true>(a, st); return;
@@ -534,6 +582,18 @@ WinPick pick_win_ps(int cin, int W, int N, int acoff) {
         w.CW = W % 128 == 0 ? 128 : 64;
         w.R = 512 / w.CW;
         w.big = true;
+        return w;
+    }
+    if (N % 96 == 0) {   // 256 x 96 tiles (f = 96: 96 and 192 channels)
+        static const int cb[] = {128, 64, 32, 16, 8};
+        for (int cw : cb)
+            if (W % cw == 0) {
+                w.CW = cw;
+                w.R = 256 / cw;
+                w.big = true;
+                w.n96 = true;
+                return w;
+            }
         return w;
     }
     const int BM = N <= 64 ? 256 : 128;
@@ -988,6 +1048,73 @@ void dense_wgrad_ps(Split dz, int N, Split x, int K, float* dw, int64_t ldw, int
     if (s > 1) finish_slabs(slab, s, per, dw, st);
 }
 
+int recompute_tiles(int cin, int B, int H, int W, int cout) {
+    (void)cin;
+    return cdiv((int64_t)B * H * W, tile_m(pick_cfg(B * H * W, cout)));
+}
+
+void conv3x3_recompute(const void* x, int64_t ldx, int cin, const void* w, int cout, int B, int H, int W,
+                       const RecomputeArgs& r, hipStream_t st) {
+    const bool ps = engine() == 2;
+    if (ps ? pick_win_ps(cin, W, cout, 0).R != 0 : pick_win(cin, W, cout).R != 0)
+        throw std::runtime_error("conv3x3_recompute: shape runs the window kernel (not the im2col GEMM)");
+    if (engine() == 0) throw std::runtime_error("conv3x3_recompute: not built for the f32 engine");
+    GemmArgs a{};
+    a.M = B * H * W; a.N = cout; a.K = 9 * cin;
+    a.B = B; a.H = H; a.W = W;
+    a.A = static_cast<const float*>(x); a.lda = ldx; a.a_coff = 0; a.a_cin = cin;
+    a.Bm = static_cast<const float*>(w); a.ldb = 9 * cin; a.b_coff = 0;
+    a.C = static_cast<float*>(r.out); a.ldc = r.ldo; a.c_coff = 0;
+    a.stats = r.stats;
+    a.bn_scale = r.scale; a.bn_shift = r.shift; a.bn_mean = r.mean; a.bn_invstd = r.invstd; a.bn_coef = r.coef;
+    a.bn_g = r.g; a.bn_ldg = r.ldg; a.bn_part = r.part;
+    const Cfg c = pick_cfg(a.M, a.N);
+    // exactly the K-stage depth / order of conv3x3_fwd (S3) and conv3x3_fwd_ps (B1) for this shape
+    const int kb = ps ? ps_kb(true, c) : kS3KB;
+    a.kstages_per_split = cdiv(a.K, kb);
+    if (ps) a.cimajor = cin % kb == 0;
+    const bool gb = r.g_bf16, ob = r.out_bf16;
+    switch (r.mode) {
+        case Recompute::Store:
+            ps ? launch_kb<KConvFwdP1, 32, 64>(c, kb, a, 1, st) : launch_kb<KConvFwd3, kS3KB>(c, kb, a, 1, st);
+            return;
+        case Recompute::Stats:
+            ps ? launch_kb<KRcP1Stats, 32, 64>(c, kb, a, 1, st) : launch_kb<KRcS3Stats, kS3KB>(c, kb, a, 1, st);
+            return;
+        case Recompute::BnRelu:
+            if (ob != ps) throw std::runtime_error("conv3x3_recompute: BnRelu writes bf16 exactly on the bf16 engine");
+            ps ? launch_kb<KRcP1ReluB, 32, 64>(c, kb, a, 1, st) : launch_kb<KRcS3Relu, kS3KB>(c, kb, a, 1, st);
+            return;
+        case Recompute::BwdSums:
+            if (gb != ps) throw std::runtime_error("conv3x3_recompute: upstream gradient is bf16 exactly on the bf16 engine");
+            ps ? launch_kb<KRcP1SumsB, 32, 64>(c, kb, a, 1, st) : launch_kb<KRcS3Sums, kS3KB>(c, kb, a, 1, st);
+            return;
+        case Recompute::BwdApply:
+            if (gb != ps || ob != ps) throw std::runtime_error("conv3x3_recompute: BwdApply bf16 exactly on the bf16 engine");
+            ps ? launch_kb<KRcP1ApplyB, 32, 64>(c, kb, a, 1, st) : launch_kb<KRcS3Apply, kS3KB>(c, kb, a, 1, st);
+            return;
+    }
+}
+
+// CAD_BIGT bit 1: ConvT forward, bit 2: ConvT dgrad on the 256 x 128 tiles (bf16 outputs).  Measured at
+// configs[3] (4 launches per step each): dgrad 1.20 -> 1.11 ms, forward 1.47 -> 1.49 ms; default 2
+int bigt_mask() {
+    static const int m = [] {
+        const char* e = std::getenv("CAD_BIGT");
+        return e && e[0] ? std::atoi(e) : 2;
+    }();
+    return m;
+}
+void launch_big(void (*fn)(GemmArgs), const char* name, const GemmArgs& a, hipStream_t st) {
+    const dim3 grid(cdiv(a.M, 256), cdiv(a.N, 128), 1);
+    if (prof_enabled()) {
+        prof_push(name, 2.0 * a.M * a.N * (double)a.K, st);
+        hipLaunchKernelGGL(fn, grid, dim3(256), 0, st, a);
+        prof_pop(st);
+    } else {
+        hipLaunchKernelGGL(fn, grid, dim3(256), 0, st, a);
+    }
+}
 void convT_fwd_ps(Split x, int cin, Split wf, const float* bias, int cout, float* y, int64_t ldy, int ycoff, int B,
                   int H, int W, hipStream_t st, bool y_bf16) {
     ps_check(x, cin, "convT_fwd x");
@@ -1001,6 +1128,10 @@ void convT_fwd_ps(Split x, int cin, Split wf, const float* bias, int cout, float
     const Cfg c = pick_cfg(a.M, a.N);
     const int kb = ps_kb(false, c);
     a.kstages_per_split = cdiv(a.K, kb);
+    if (y_bf16 && (bigt_mask() & 1) && a.N >= 128 && a.M >= 4096) {
+        launch_big(k_convT_fwd_bf16pt4<32>, "void cad::k_convT_fwd_bf16pt4<32>(cad::GemmArgs)", a, st);
+        return;
+    }
     if (y_bf16) launch_kb<KConvTFwdP1T, 32>(c, kb, a, 1, st);
     else launch_kb<KConvTFwdP1, 32>(c, kb, a, 1, st);
 }
@@ -1017,6 +1148,10 @@ void convT_dgrad_ps(Split g, int cout, Split wm, int cin, float* dx, int B, int 
     const Cfg c = pick_cfg(a.M, a.N);
     const int kb = ps_kb(false, c);
     a.kstages_per_split = cdiv(a.K, kb);
+    if (dx_bf16 && (bigt_mask() & 2) && a.N >= 128 && a.M >= 4096) {
+        launch_big(k_convT_dgrad_bf16pb4<32>, "void cad::k_convT_dgrad_bf16pb4<32>(cad::GemmArgs)", a, st);
+        return;
+    }
     if (dx_bf16) launch_kb<KConvTDgradP1B, 32>(c, kb, a, 1, st);
     else launch_kb<KConvTDgradP1, 32>(c, kb, a, 1, st);
 }

@@ -63,6 +63,12 @@ struct GemmArgs {
     // split store (EpiStoreSplitB16): output columns n >= split_n go to the bf16 rows C2 (ldc2 elements,
     // column n - split_n) instead of C
     void* C2; int64_t ldc2; int split_n;
+    // BatchNorm epilogues of a recomputed convolution (EpiBnRelu / EpiBnBwdSums / EpiBnBwdApply,
+    // epilogues.hpp): the BN's per-channel coefficients, the upstream gradient (bf16 or fp32 rows of
+    // bn_ldg elements) and the per-tile fp64 partials [gridDim.x][2][N]
+    const float *bn_scale, *bn_shift, *bn_mean, *bn_invstd, *bn_coef;
+    const void* bn_g; int64_t bn_ldg;
+    double* bn_part;
 };
 
 
@@ -417,6 +423,22 @@ struct OpLds {
 // blockIdx.x -> M tile, blockIdx.y -> N tile, blockIdx.z -> split-K slice.
 // --------------------------------------------------------------------------------------------
 template <class E, class = void>
+struct is_nostore : std::false_type {};   // a row-major epilogue that only forms BN partials
+template <class E>
+struct is_nostore<E, std::void_t<decltype(E::NOSTORE)>> : std::integral_constant<bool, E::NOSTORE> {};
+template <class E, class = void>
+struct has_finish : std::false_type {};   // a structured epilogue with per-block state and a tile finish
+template <class E>
+struct has_finish<E, std::void_t<decltype(E::FINISH)>> : std::integral_constant<bool, E::FINISH> {};
+template <class E, class = void>
+struct has_wave_store : std::false_type {};   // a structured epilogue that may store a wave's sub-tile at once
+template <class E>
+struct has_wave_store<E, std::void_t<decltype(E::WAVE_STORE)>> : std::integral_constant<bool, E::WAVE_STORE> {};
+template <class E, class = void>
+struct has_prefetch : std::false_type {};   // a structured epilogue that loads its operands for all blocks first
+template <class E>
+struct has_prefetch<E, std::void_t<decltype(E::PREFETCH)>> : std::integral_constant<bool, E::PREFETCH> {};
+template <class E, class = void>
 struct is_structured : std::false_type {};
 template <class E>
 struct is_structured<E, std::void_t<decltype(E::STRUCTURED)>> : std::integral_constant<bool, E::STRUCTURED> {};
@@ -565,14 +587,31 @@ __device__ __forceinline__ void gemm_epilogue_t(const GemmArgs& a, const floatx1
         else return rs;
     };
     const __amdgpu_buffer_rsrc_t rsadd = add_rsrc();
+    // the wave's MI x NJ blocks staged through its own LDS slice and stored as 16-byte pieces (when the
+    // epilogue's layout allows: wave_store returns false otherwise)
+    if constexpr (has_wave_store<Epi>::value) {
+        if (epi.template wave_store<MI, NJ>(a, acc, m0 + wm * 32 * MI, n0 + wn * 32 * NJ,
+                                            lds + wave * Epi::template lds_floats_per_wave<NJ>()))
+            return;
+    }
+    // one memory round trip for the whole tile instead of one per block
+    if constexpr (has_prefetch<Epi>::value)
+        epi.template prefetch<MI, NJ>(a, m0 + wm * 32 * MI + 4 * (lane >> 5), n0 + wn * 32 * NJ + (lane & 31));
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             if constexpr (is_structured<Epi>::value) {
                 static_assert(!Epi::STATS, "structured epilogues carry no BN partials");
-                epi.block(a, m0 + wm * 32 * MI + i * 32 + 4 * (lane >> 5), n0 + wn * 32 * NJ + j * 32 + (lane & 31),
-                          acc[i][j]);
+                if constexpr (has_prefetch<Epi>::value)
+                    epi.block_p(a, m0 + wm * 32 * MI + i * 32 + 4 * (lane >> 5),
+                                n0 + wn * 32 * NJ + j * 32 + (lane & 31), acc[i][j], i * NJ + j, j);
+                else if constexpr (has_finish<Epi>::value)
+                    epi.block_j(a, m0 + wm * 32 * MI + i * 32 + 4 * (lane >> 5),
+                                n0 + wn * 32 * NJ + j * 32 + (lane & 31), acc[i][j], j);
+                else
+                    epi.block(a, m0 + wm * 32 * MI + i * 32 + 4 * (lane >> 5), n0 + wn * 32 * NJ + j * 32 + (lane & 31),
+                              acc[i][j]);
                 continue;
             }
 #pragma unroll
@@ -597,12 +636,14 @@ __device__ __forceinline__ void gemm_epilogue_t(const GemmArgs& a, const floatx1
                     const uint32_t lo = n < a.N ? (uint32_t)(mr * ldc4 + (int64_t)n * ES) : kOOB;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        if constexpr (Epi::BF16)
-                            __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, (__bf16)v[r]), rs,
-                                                                  lo + (uint32_t)(r * ldc4), 0, 0);
-                        else
-                            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[r]), rs,
-                                                                  lo + (uint32_t)(r * ldc4), 0, 0);
+                        if constexpr (!is_nostore<Epi>::value) {
+                            if constexpr (Epi::BF16)
+                                __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, (__bf16)v[r]), rs,
+                                                                      lo + (uint32_t)(r * ldc4), 0, 0);
+                            else
+                                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[r]), rs,
+                                                                      lo + (uint32_t)(r * ldc4), 0, 0);
+                        }
                         if constexpr (Epi::STATS) bnp.add(j, v[r], m0 + mr + r < a.M);
                     }
                 }
@@ -612,6 +653,7 @@ __device__ __forceinline__ void gemm_epilogue_t(const GemmArgs& a, const floatx1
     // per-column BN partials over this block's BM rows -> a.stats (BnTilePartials); the main loop
     // ended on a barrier, so the LDS operand buffers are free for the reduction
     if constexpr (Epi::STATS) bnp.template finish<WM, WN>(a, lds, tile.x, n0);
+    if constexpr (has_finish<Epi>::value) epi.template finish<WM, WN, NJ>(a, lds, tile.x, n0);
 }
 template <int WM, int WN, class Epi>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, floatx16 (&acc)[2][2], const TileId& tile,

@@ -315,10 +315,11 @@ struct WinPsGeo {
 };
 
 // MI = 4: 128 x 64 per wave (256 x 128 tiles) — two fragment reads per three MFMAs instead of one per
-// MFMA: the 128 x 128 tile's LDS reads cap its MFMA rate near one half (B1 has one product per k step)
-template <int R, int CW, int WM, int WN, class Epi, int MI = 2>
+// MFMA: the 128 x 128 tile's LDS reads cap its MFMA rate near one half (B1 has one product per k step).
+// NJ = 3 (with MI = 2, WM = 4, WN = 1): 256 x 96 tiles for the 96 / 192-channel levels of the
+// reference's production width (train_config_production.yaml: init_features 96).
+template <int R, int CW, int WM, int WN, class Epi, int MI = 2, int NJ = 2>
 __device__ __forceinline__ void conv3x3_win_ps_body(const GemmArgs& a) {
-    constexpr int NJ = 2;
     constexpr int BM = 32 * MI * WM, BN = 32 * NJ * WN;
     static_assert(BM == R * CW, "tile");
     using G = WinPsGeo<R, CW, BN>;

@@ -65,6 +65,27 @@ bool conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t 
 bool conv3x3_dgrad_split_ok(Split dz, int cout, Split wd, int cin, int W, int split_n);
 void conv3x3_wgrad_ps(Split dz, int cout, Split x, int cin, float* dw, int B, int H, int W, float* slab,
                       int64_t slab_cap, hipStream_t st);
+// ---- recomputed convolution (enc1.conv1, epilogues.hpp "Recomputed convolution"): the im2col
+// conv3x3 forward GEMM that conv3x3_fwd (S3 / f32 engines: x, w fp32) or conv3x3_fwd_ps (B1: x, w
+// twins) would run for this shape — same kernel, tile and K order, so the same accumulators — with a
+// consumer's epilogue instead of the output store.
+enum class Recompute { Stats, BnRelu, BwdSums, BwdApply, Store };   // Store: y itself (fp32 rows out)
+struct RecomputeArgs {
+    Recompute mode = Recompute::Stats;
+    float* stats = nullptr;                                    // Stats: BN tile partials (conv3x3_stats_rows)
+    const float *scale = nullptr, *shift = nullptr, *mean = nullptr, *invstd = nullptr, *coef = nullptr;
+    const void* g = nullptr; int64_t ldg = 0; bool g_bf16 = false;   // BwdSums / BwdApply: upstream gradient
+    void* out = nullptr; int64_t ldo = 0; bool out_bf16 = false;     // BnRelu / BwdApply output rows
+    double* part = nullptr;                                    // BwdSums: [recompute_tiles][2][cout]
+};
+int recompute_tiles(int cin, int B, int H, int W, int cout);   // row tiles of the recomputed GEMM
+void conv3x3_recompute(const void* x, int64_t ldx, int cin, const void* w, int cout, int B, int H, int W,
+                       const RecomputeArgs& r, hipStream_t st);
+// BN backward coefficients from the per-tile partials of EpiBnBwdSums (k_bn_bwd_coef's outputs:
+// coef [3][C], dgamma, dbeta); scratch: colsum scratch of the tile count
+void bn_bwd_from_tiles(const double* part, int tiles, int C, int64_t M, const float* gamma, const float* invstd,
+                       float* coef, float* dgamma, float* dbeta, double* scratch, hipStream_t st);
+
 // y_bf16: y is a bf16 twin (rows of ldy elements) — the up half of the decoder concat twin
 void convT_fwd_ps(Split x, int cin, Split wf, const float* bias, int cout, float* y, int64_t ldy, int ycoff, int B,
                   int H, int W, hipStream_t st, bool y_bf16 = false);
@@ -220,6 +241,26 @@ void depth_metrics_partials(const float* pred, const float* gt, int B, int64_t H
                             hipStream_t st);
 void repack_conv_dgrad(const float* w, float* wd, int cout, int cin, hipStream_t st);
 void repack_convT_fwd(const float* wm, float* wf, int cin, int cout, hipStream_t st);
+// Per-step weight preparation in one launch (the weights change every step): a list of jobs, each
+// one weight tensor ->  fp32 repack (d32, optional) and/or its bf16 twin (d16, optional; the
+// k_split_rows<1> rounding).  Kinds: WPREP_SPLIT  [rows][K] -> bf16 same layout;
+// WPREP_DGRAD  OHWI [co][tap][ci] -> [ci][8 - tap][co] (repack_conv_dgrad);
+// WPREP_CONVT  [ci][q][co] -> [q][co][ci] (repack_convT_fwd).  n = elements, a multiple of 8.
+enum { WPREP_SPLIT = 0, WPREP_DGRAD = 1, WPREP_CONVT = 2 };
+struct WPrepJob {
+    const float* src;
+    float* d32;
+    void* d16;
+    int kind, cout, cin;
+    int blk0;   // first block of this job (filled by weight_prep)
+    int64_t n;
+};
+constexpr int kWPrepMaxJobs = 24;
+struct WPrepList {
+    WPrepJob job[kWPrepMaxJobs];
+    int njobs;
+};
+void weight_prep(WPrepList& list, hipStream_t st);
 
 // ---------------- losses (loss_kernels.hip) ----------------
 struct LossWorkspace {

@@ -111,6 +111,14 @@ struct OpSumB16 {
         acc[0][0] += v.x; acc[0][1] += v.y; acc[0][2] += v.z; acc[0][3] += v.w;
     }
 };
+struct OpSumD {   // fp64 rows (per-tile partials of a recomputed convolution's BN backward)
+    const double* x; int C;
+    __device__ NoPrep prep(int) const { return {}; }
+    __device__ void operator()(int64_t r, int c4, double (&acc)[1][4], NoPrep) const {
+        const double* p = x + r * C + c4 * 4;
+        acc[0][0] += p[0]; acc[0][1] += p[1]; acc[0][2] += p[2]; acc[0][3] += p[3];
+    }
+};
 // BN tile partials (BnTilePartials, gemm_mfma.hpp): per tile row r, S = part[r][c], M2 = part[r][C + c],
 // n = cnt[r]; column sums of S and of M2 + S^2 / n (= sum y^2 of the tile) in fp64
 struct OpBnTile {
@@ -400,6 +408,15 @@ __global__ void k_bn_bwd_coef(const double* tot, int C, int64_t M, const float* 
     coef[c] = k1;
     coef[C + c] = (float)(k1 * sdz / (double)M);
     coef[2 * C + c] = (float)(k1 * sdzx / (double)M);
+}
+void bn_bwd_from_tiles(const double* part, int tiles, int C, int64_t M, const float* gamma, const float* invstd,
+                       float* coef, float* dgamma, float* dbeta, double* scratch, hipStream_t st) {
+    double* tot = scratch;
+    double* p2 = scratch + 2 * C;
+    // columns [0, C): sum dz, [C, 2C): sum dz xhat — tot as bn_relu_bwd's colreduce leaves it
+    const int S = launch_colreduce<1>(OpSumD{part, 2 * C}, tiles, 2 * C, p2, st);
+    launch_colfinal(p2, S, 2 * C, tot, nullptr, 1.f, st);
+    hipLaunchKernelGGL(k_bn_bwd_coef, dim3(cdiv(C, 64)), dim3(64), 0, st, tot, C, M, gamma, invstd, coef, dgamma, dbeta);
 }
 template <int NP, bool YB, bool HG, bool GB = false, bool PA = false>
 __global__ __launch_bounds__(256) void k_bn_relu_bwd_rows(const float* __restrict__ g, int64_t ldg, int gcoff,
@@ -829,6 +846,59 @@ __global__ void k_repack_convT_fwd(const float* __restrict__ wm, float* __restri
 }
 void repack_convT_fwd(const float* wm, float* wf, int cin, int cout, hipStream_t st) {
     hipLaunchKernelGGL(k_repack_convT_fwd, dim3(ew_blocks((int64_t)4 * cout * cin)), dim3(256), 0, st, wm, wf, cin, cout);
+}
+
+// one thread per 8 consecutive outputs; blocks are dealt to jobs in order (block-uniform job lookup)
+__global__ __launch_bounds__(256) void k_weight_prep(WPrepList list) {
+    int j = 0;
+    while (j + 1 < list.njobs && (int)blockIdx.x >= list.job[j + 1].blk0) ++j;
+    const WPrepJob& jb = list.job[j];
+    const int64_t i = ((int64_t)(blockIdx.x - jb.blk0) * 256 + threadIdx.x) * 8;
+    if (i >= jb.n) return;
+    const int ne = (int)min<int64_t>(8, jb.n - i);
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int64_t k = i + (e < ne ? e : 0);
+        int64_t src;
+        if (jb.kind == WPREP_SPLIT) {
+            src = k;
+        } else if (jb.kind == WPREP_DGRAD) {   // k = (ci*9 + t)*cout + co  <-  w[co][8 - t][ci]
+            const int co = (int)(k % jb.cout);
+            const int64_t t2 = k / jb.cout;
+            const int t = (int)(t2 % 9), ci = (int)(t2 / 9);
+            src = ((int64_t)co * 9 + (8 - t)) * jb.cin + ci;
+        } else {   // WPREP_CONVT: k = qc*cin + ci  <-  wm[ci][qc]
+            const int ci = (int)(k % jb.cin);
+            src = (int64_t)ci * 4 * jb.cout + k / jb.cin;
+        }
+        v[e] = jb.src[src];
+    }
+    if (jb.d32) {
+        if (ne == 8) {
+            *reinterpret_cast<float4*>(jb.d32 + i) = make_float4(v[0], v[1], v[2], v[3]);
+            *reinterpret_cast<float4*>(jb.d32 + i + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        } else {
+            for (int e = 0; e < ne; ++e) jb.d32[i + e] = v[e];
+        }
+    }
+    if (jb.d16) {   // n % 8 == 0 (weight_prep)
+        const auto sa = split_np<1>(make_float4(v[0], v[1], v[2], v[3]));
+        const auto sb = split_np<1>(make_float4(v[4], v[5], v[6], v[7]));
+        *reinterpret_cast<uint4*>(static_cast<char*>(jb.d16) + i * 2) = make_uint4(sa.p[0].x, sa.p[0].y, sb.p[0].x, sb.p[0].y);
+    }
+}
+void weight_prep(WPrepList& list, hipStream_t st) {
+    if (list.njobs <= 0) return;
+    if (list.njobs > kWPrepMaxJobs) throw std::runtime_error("weight_prep: too many jobs");
+    int blocks = 0;
+    for (int j = 0; j < list.njobs; ++j) {
+        WPrepJob& jb = list.job[j];
+        if (jb.d16 && jb.n % 8) throw std::runtime_error("weight_prep: bf16 twin size not a multiple of 8");
+        jb.blk0 = blocks;
+        blocks += (int)cdiv(cdiv(jb.n, 8), (int64_t)256);
+    }
+    hipLaunchKernelGGL(k_weight_prep, dim3(blocks), dim3(256), 0, st, list);
 }
 
 }  // namespace cad

@@ -420,6 +420,13 @@ cad_status cad_op_conv3x3_dgrad_bf16(const void* dz, int64_t lddz, int cout, con
                                      int64_t lddx, int dx_bf16, int B, int H, int W, void* stream);
 cad_status cad_op_convT_fwd(const float* x, int cin, const float* w_iqo, const float* bias, int cout,
                             float* y, int64_t ldy, int ycoff, int B, int H, int W, void* stream);
+/* the bf16 engine's ConvTranspose2d(k2, s2) forward (baseline_unet.h:91 `up`) on a pre-split bf16 NHWC
+ * input (rows of ldx, channel offset xcoff), fp32 [ci][dy][dx][co] weights rounded to bf16 inside:
+ * y (bf16 rows of ldy at channel offset ycoff, the decoder concat's up half) = x * w + bias, pixel-
+ * shuffled.  Requires cad_set_gemm_engine(CAD_GEMM_BF16). */
+cad_status cad_op_convT_fwd_bf16(const void* x, int64_t ldx, int xcoff, int cin, const float* w_iqo,
+                                 const float* bias, int cout, void* y, int64_t ldy, int ycoff, int B, int H, int W,
+                                 void* stream);
 cad_status cad_op_convT_dgrad(const float* g, int64_t ldg, int gcoff, int cout, const float* w_iqo, int cin,
                               float* dx, int B, int H, int W, void* stream);
 cad_status cad_op_convT_wgrad(const float* x, int cin, const float* g, int64_t ldg, int gcoff, int cout,

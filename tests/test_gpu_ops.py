@@ -210,7 +210,10 @@ def test_conv3x3_wgrad_bf16_needs_bf16_engine(cad, dev):
         lib.cad_set_gemm_engine(prev)
 
 
-CONVT_SHAPES = [(2, 8, 12, 128, 64), (1, 4, 5, 1024, 512), (3, 6, 6, 32, 16), (2, 3, 4, 8, 4)]
+CONVT_SHAPES = [(2, 8, 12, 128, 64), (1, 4, 5, 1024, 512), (3, 6, 6, 32, 16), (2, 3, 4, 8, 4),
+                # W % 32 == 0: the pixel-shuffle epilogue's one-run-per-block store; M = 96 leaves a
+                # partial 128-row tile
+                (2, 5, 32, 64, 32), (1, 3, 32, 128, 64), (1, 2, 64, 256, 128)]
 
 
 @pytest.mark.parametrize("B,H,W,cin,cout", CONVT_SHAPES)
@@ -243,6 +246,41 @@ def test_convT(cad, dev, engine, B, H, W, cin, cout):
     assert lib.cad_op_convT_wgrad(_p(xg), cin, _p(gg), 2 * cout, cout, cout, _p(dw), B, H, W, _s()) == 0
     torch.cuda.synchronize()
     assert max_rel_err(dw.cpu().permute(0, 3, 1, 2), wdd.grad) < TOL
+
+
+CONVT_BF16_SHAPES = [(2, 8, 12, 128, 64), (1, 3, 32, 128, 64), (2, 5, 64, 64, 32), (1, 4, 40, 256, 128),
+                     (1, 2, 160, 128, 64)]
+
+
+@pytest.mark.parametrize("B,H,W,cin,cout", CONVT_BF16_SHAPES)
+def test_convT_fwd_bf16(cad, dev, B, H, W, cin, cout):
+    """bf16 engine ConvTranspose forward (cad_op_convT_fwd_bf16: bf16 twin in, bf16 up half of a concat
+    twin out) against the fp64 contraction of the bf16-rounded operands plus bias, rounded to bf16: within
+    one bf16 spacing (floored at that of 2^-10 of the largest output), under 1e-2 of the outputs differing;
+    the other half of the concat rows untouched."""
+    lib = cad.load_library()
+    prev = lib.cad_get_gemm_engine()
+    assert lib.cad_set_gemm_engine(2) == 0
+    try:
+        g = torch.Generator().manual_seed(5 * B + H + W + cin + cout)
+        x = torch.randn(B, cin, H, W, generator=g).bfloat16()
+        w = torch.randn(cin, cout, 2, 2, generator=g) / cin ** 0.5
+        b = torch.randn(cout, generator=g)
+        y_ref = F.conv_transpose2d(x.double(), w.bfloat16().double(), b.double(), stride=2)
+        xg, wg = nhwc(x).to(dev), w.permute(0, 2, 3, 1).contiguous().to(dev)
+        ybuf = torch.full((B, 2 * H, 2 * W, 2 * cout), 7.0, dtype=torch.bfloat16, device=dev)
+        assert lib.cad_op_convT_fwd_bf16(_p(xg), cin, 0, cin, _p(wg), _p(b.to(dev)), cout, _p(ybuf), 2 * cout, cout,
+                                         B, H, W, _s()) == 0, lib.cad_last_error()
+        torch.cuda.synchronize()
+        got = ybuf[..., cout:].cpu().float()
+        assert (ybuf[..., :cout].cpu().float() == 7.0).all()
+        want = nhwc(y_ref).bfloat16().float()
+        diff = (got - want).abs()
+        big = torch.maximum(got.abs(), want.abs()).clamp_min(2.0 ** -10 * want.abs().max().item())
+        ulp = torch.exp2(torch.floor(torch.log2(big)) - 7)
+        assert (diff <= ulp).all() and (diff > 0).float().mean().item() < 1e-2, (diff / ulp).max().item()
+    finally:
+        lib.cad_set_gemm_engine(prev)
 
 
 def test_maxpool(cad, dev):
@@ -359,6 +397,9 @@ B1_WIN_SHAPES = [  # B, H, W, cin, cout: the bf16 engine's window forward / dgra
     (1, 5, 32, 128, 128),   # CW 32
     (2, 7, 16, 64, 256),    # CW 16; dgrad N = 64 with W 16 (512 x 64 needs W % 64: im2col)
     (1, 13, 40, 256, 256),  # CW 8 (40 = 5 x 8), H = 13 < R = 32
+    (1, 5, 128, 96, 96),    # f = 96 level 0: 256 x 96 tiles (k_conv3x3_win_bf16p3), CW 128, forward and dgrad
+    (2, 6, 64, 192, 96),    # dec4.conv1 at f = 96: forward N = 96; dgrad N = 192 = two 96-column tiles
+    (1, 3, 32, 96, 192),    # level 1 at f = 96: N = 192, CW 32; dgrad N = 96
 ]
 
 

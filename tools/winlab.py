@@ -1,7 +1,7 @@
 """Timing lab for the bf16 engine's convolution kernels at the configs[3] shapes (bs32 480x640,
 f=64: levels 0-4): each operator launched `reps` times on random bf16 operands (not zeros: the chip
 holds a different clock on zeros, MI355X_MICROARCH.md DVFS item 1) and timed with HIP events.
-  python tools/winlab.py [--reps 20] [--only fwd|dgrad|wgrad]      (CAD_LIB=libcad_hip_<variant>.so for A/B)"""
+  python tools/winlab.py [--reps 20] [--only fwd|dgrad|wgrad|convT]      (CAD_LIB=libcad_hip_<variant>.so for A/B)"""
 import argparse
 import ctypes as C
 import json
@@ -36,6 +36,9 @@ for l in range(4):
     Cl = 64 << l
     CASES.append((f"dec{l}.conv1", l, 2 * Cl, Cl, "fwd", "stats"))
     CASES.append((f"dec{l}.conv1", l, 2 * Cl, Cl, "dgrad", "b16"))
+for l in range(4):
+    Cl = 64 << l
+    CASES.append((f"up{l}", l + 1, 2 * Cl, Cl, "convT", ""))
 out = []
 for name, l, cin, cout, kind, epi in CASES:
     if args.only and kind != args.only:
@@ -55,6 +58,13 @@ for name, l, cin, cout, kind, epi in CASES:
         dx = torch.empty(M, cin, device=dev, dtype=torch.bfloat16)
         call = lambda: lib.cad_op_conv3x3_dgrad_bf16(P(dz), cout, cout, P(wt), cin, P(dx), cin, 1, B, h, w, s)  # noqa
         flop = 2.0 * M * cout * 9 * cin
+    elif kind == "convT":
+        x = torch.randn(M, cin, device=dev, generator=g).bfloat16()
+        wt = torch.randn(cin, 2, 2, cout, device=dev, generator=g) * (1.0 / cin ** 0.5)
+        bias = torch.randn(cout, device=dev, generator=g)
+        y = torch.empty(4 * M, 2 * cout, device=dev, dtype=torch.bfloat16)
+        call = lambda: lib.cad_op_convT_fwd_bf16(P(x), cin, 0, cin, P(wt), P(bias), cout, P(y), 2 * cout, cout, B, h, w, s)  # noqa
+        flop = 2.0 * M * 4 * cout * cin
     else:
         dz = torch.randn(M, cout, device=dev, generator=g).bfloat16()
         x = torch.randn(M, cin, device=dev, generator=g).bfloat16()
