@@ -155,11 +155,14 @@ __global__ __launch_bounds__(256, 1) void k_conv3x3_win_bf16d(GemmArgs a) {
 
 // window-tiled conv3x3 weight gradient (gemm_win.hpp): 64 co x 64 ci x 9 taps per workgroup, split-K
 __global__ __launch_bounds__(256, 2) void k_conv3x3_wgrad_win_s3(GemmArgs a) { conv3x3_wgrad_win_body<3>(a); }
+__global__ __launch_bounds__(256, 2) void k_conv3x3_wgrad_strip_s3(GemmArgs a) { conv3x3_wgrad_strip_body<3>(a); }
 template <int P>
 __global__ __launch_bounds__(256, 2) void k_conv3x3_wgrad_win_bf16p(GemmArgs a) { conv3x3_wgrad_win_ps_body<P>(a); }
 // ... with LDS-DMA staging (3-stage ring, conv3x3_wgrad_win_dma_body)
 template <int P, int NBUF>
 __global__ __launch_bounds__(256, 2) void k_conv3x3_wgrad_win_bf16d(GemmArgs a) { conv3x3_wgrad_win_dma_body<P, NBUF>(a); }
+template <int P>
+__global__ __launch_bounds__(256, 2) void k_conv3x3_wgrad_strip_bf16d(GemmArgs a) { conv3x3_wgrad_strip_dma_body<P>(a); }
 
 template <int WM, int WN, int KB, class Epi>
 __global__ __launch_bounds__(256) void k_conv3x3_fwd_bf16(GemmArgs a) { conv3x3_fwd_np<1, WM, WN, 2, 2, KB, Epi>(a); }
@@ -665,25 +668,46 @@ void finish_slabs(float* slab, int splits, int64_t per, float* dw, hipStream_t s
 bool use_wgrad_win(int cout, int cin, int W) {
     return engine() == 1 && cout % 64 == 0 && cin % 64 == 0 && W % 16 == 0;
 }
+// CAD_WGSTRIP=0: the row-major S3 window weight gradient (k_conv3x3_wgrad_win_s3) instead of the
+// strip-order one (A/B switch)
+bool wg_strip() {
+    static const bool on = [] {
+        const char* e = std::getenv("CAD_WGSTRIP");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 void launch_wgrad_win(GemmArgs& a, float* dw, float* slab, int64_t slab_cap, int64_t kbytes, hipStream_t st) {
     const int cin = a.b_cin;
     const int tiles = (a.M / 64) * (cin / 64);
     const int nst = a.K / 16;
+    const bool strip = wg_strip();
     int s = std::max(1, std::min(cdiv(2048, tiles), nst / 32));
     const int64_t per = (int64_t)a.M * a.N;
     if (slab_cap > 0) s = (int)std::max<int64_t>(1, std::min<int64_t>(s, slab_cap / per));
-    const int64_t need = (int64_t)cdiv((int64_t)a.K * kbytes, (int64_t)1 << 30);
-    if (need > s) {
-        if (need * per > slab_cap) throw std::runtime_error("weight-gradient K-slice exceeds the 1 GB window and the slab");
-        s = (int)need;
+    // operand window of a slice: its pixels (strip order: from its first image's start, one image more)
+    const int64_t img = (int64_t)a.H * a.W;
+    auto span_ok = [&](int splits) {
+        const int64_t px = (int64_t)cdiv(nst, splits) * 16;
+        const int64_t span = strip ? (cdiv(px, img) + 1) * img : px;
+        return span * kbytes <= ((int64_t)1 << 30);
+    };
+    if (!span_ok(s)) {
+        int need = s;
+        while (!span_ok(need) && need < nst) ++need;
+        if (!span_ok(need) || (int64_t)need * per > slab_cap)
+            throw std::runtime_error("weight-gradient K-slice exceeds the 1 GB window and the slab");
+        s = need;
     }
     a.kstages_per_split = cdiv(nst, s);
     s = cdiv(nst, a.kstages_per_split);
     a.ldc = a.N; a.slab_stride = per;
     a.C = s == 1 ? dw : slab;
     const dim3 grid(a.M / 64, cin / 64, s);
-    if (prof_enabled()) prof_push("void cad::k_conv3x3_wgrad_win_s3(cad::GemmArgs)", 2.0 * a.M * a.N * (double)a.K, st);
-    hipLaunchKernelGGL(k_conv3x3_wgrad_win_s3, grid, dim3(256), 0, st, a);
+    const char* name = strip ? "void cad::k_conv3x3_wgrad_strip_s3(cad::GemmArgs)" : "void cad::k_conv3x3_wgrad_win_s3(cad::GemmArgs)";
+    if (prof_enabled()) prof_push(name, 2.0 * a.M * a.N * (double)a.K, st);
+    if (strip) hipLaunchKernelGGL(k_conv3x3_wgrad_strip_s3, grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(k_conv3x3_wgrad_win_s3, grid, dim3(256), 0, st, a);
     if (prof_enabled()) prof_pop(st);
     if (s > 1) finish_slabs(slab, s, per, dw, st);
 }
@@ -943,25 +967,37 @@ void launch_wgrad_win_ps1(GemmArgs& a, float* dw, float* slab, int64_t slab_cap,
     int s = std::max(1, std::min(cdiv(2048, tiles), nst / 16));
     const int64_t per = (int64_t)a.M * a.N;
     if (slab_cap > 0) s = (int)std::max<int64_t>(1, std::min<int64_t>(s, slab_cap / per));
-    // a K-slice is a loader window of 32-bit byte offsets: keep it below 1 GB in either operand
+    // a K-slice is a loader window of 32-bit byte offsets: keep it below 1 GB in either operand (the
+    // strip walk's window starts at the slice's first image: one image more)
+    const bool dma = wg_dma();
+    const bool strip = dma && wg_strip();
     const int64_t kbytes = 2 * std::max<int64_t>(a.lda, a.ldb);
-    const int64_t need = (int64_t)cdiv((int64_t)a.K * kbytes, (int64_t)1 << 30);
-    if (need > s) {
-        if (need * per > slab_cap) throw std::runtime_error("weight-gradient K-slice exceeds the 1 GB window and the slab");
-        s = (int)need;
+    const int64_t img = (int64_t)a.H * a.W;
+    auto span_ok = [&](int splits) {
+        const int64_t px = (int64_t)cdiv(nst, splits) * P;
+        const int64_t span = strip ? (cdiv(px, img) + 1) * img : px;
+        return span * kbytes <= ((int64_t)1 << 30);
+    };
+    if (!span_ok(s)) {
+        int need = s;
+        while (!span_ok(need) && need < nst) ++need;
+        if (!span_ok(need) || (int64_t)need * per > slab_cap)
+            throw std::runtime_error("weight-gradient K-slice exceeds the 1 GB window and the slab");
+        s = need;
     }
     a.kstages_per_split = cdiv(nst, s);
     s = cdiv(nst, a.kstages_per_split);
     a.ldc = a.N; a.slab_stride = per;
     a.C = s == 1 ? dw : slab;
     const dim3 grid(a.M / 64, cin / 64, s);
-    const bool dma = wg_dma();
     const int nbuf = wg_nbuf();
     char name[96];
-    if (dma) std::snprintf(name, sizeof name, "void cad::k_conv3x3_wgrad_win_bf16d<%d, %d>(cad::GemmArgs)", P, nbuf);
+    if (strip) std::snprintf(name, sizeof name, "void cad::k_conv3x3_wgrad_strip_bf16d<%d>(cad::GemmArgs)", P);
+    else if (dma) std::snprintf(name, sizeof name, "void cad::k_conv3x3_wgrad_win_bf16d<%d, %d>(cad::GemmArgs)", P, nbuf);
     else std::snprintf(name, sizeof name, "void cad::k_conv3x3_wgrad_win_bf16p<%d>(cad::GemmArgs)", P);
     if (prof_enabled()) prof_push(name, 2.0 * a.M * a.N * (double)a.K, st);
-    if (dma && nbuf == 2) hipLaunchKernelGGL((k_conv3x3_wgrad_win_bf16d<P, 2>), grid, dim3(256), 0, st, a);
+    if (strip) hipLaunchKernelGGL(k_conv3x3_wgrad_strip_bf16d<P>, grid, dim3(256), 0, st, a);
+    else if (dma && nbuf == 2) hipLaunchKernelGGL((k_conv3x3_wgrad_win_bf16d<P, 2>), grid, dim3(256), 0, st, a);
     else if (dma) hipLaunchKernelGGL((k_conv3x3_wgrad_win_bf16d<P, 3>), grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL(k_conv3x3_wgrad_win_bf16p<P>, grid, dim3(256), 0, st, a);
     if (prof_enabled()) prof_pop(st);

@@ -624,6 +624,189 @@ __device__ __forceinline__ void conv3x3_wgrad_win_body(const GemmArgs& a) {
 
 
 // ------------------------------------------------------------------------------------------------
+// The same weight gradient with the stages walked down 16-pixel-wide column strips (round 4): stage s
+// = pixels x0..x0+15 of row y, y fastest, so consecutive stages share two of their three window rows.
+// The window rows live in a ring of four 18-pixel row slots (row yy in slot (yy + 1) & 3): a stage
+// fetches and splits ONE new row (rows y'-1..y'+1 at a strip's start or a slice's first stage),
+// against three in the row-major walk, whose re-fetches 40 stages apart missed a 4 MB XCD L2 shared
+// by ~64 workgroups (FETCH_SIZE 7.9 GB per level-0 launch against 2.4 GB of operands).  LDS: A double-
+// buffered (2 x 9 KB) + the ring (4 x 18 k-rows x NP planes = 41 KB on S3): 59 KB, two workgroups per
+// CU.  Same products per (co, tap, ci) and pixel; the sums run in strip order (a different fp32 order
+// than the row-major walk: both are deterministic).
+// The host's window: a slice's operand span (its images, from the first image's start) below 2 GB.
+// ------------------------------------------------------------------------------------------------
+struct WgStrip {
+    int b, seg, y;
+    __device__ void init(int stage, int H, int W) {
+        const int per_img = (W >> 4) * H;
+        b = stage / per_img;
+        const int r = stage - b * per_img;
+        seg = r / H;
+        y = r - seg * H;
+    }
+    __device__ void next(int H, int W) {
+        if (++y == H) { y = 0; if (++seg == (W >> 4)) { seg = 0; ++b; } }
+    }
+};
+
+template <int NP>
+__device__ __forceinline__ void conv3x3_wgrad_strip_body(const GemmArgs& a) {
+    constexpr int PLA = 16 * WgM::STRIDE;
+    constexpr int SLOT = 18 * WgM::STRIDE;              // one window row, one plane
+    constexpr int PLB = 4 * SLOT;                        // the ring, one plane
+    constexpr int SA = NP * PLA, SB = NP * PLB;
+    constexpr int NVR = (18 * 16 + 255) / 256;           // float4 per thread per window row (288 per row)
+    __shared__ __attribute__((aligned(16))) char lds[2 * SA + SB];
+
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6;
+    const int cbk = wave & 1, cib = wave >> 1;
+    const TileId tile = xcd_tile();
+    const int co0 = tile.x * 64, ci0 = tile.y * 64;
+    const int H = a.H, W = a.W;
+    const int nst = a.K >> 4;
+    const int kbeg = tile.z * a.kstages_per_split;
+    const int kend = min(nst, kbeg + a.kstages_per_split);
+
+    WgStrip pos;
+    pos.init(min(kbeg, nst - 1), H, W);
+    // operand bases: the slice's first image start (A), minus one row and one pixel (B)
+    const int64_t p0 = (int64_t)pos.b * H * W;
+    const int64_t pb = p0 - W - 1 > 0 ? p0 - W - 1 : 0;
+    const int lda4 = (int)a.lda * 4, ldb4 = (int)a.ldb * 4;
+    const __amdgpu_buffer_rsrc_t rsa = make_rsrc(a.A + p0 * a.lda + a.a_coff + co0);
+    const __amdgpu_buffer_rsrc_t rsb = make_rsrc(a.Bm + pb * a.ldb + a.b_coff + ci0);
+    const uint32_t aoff = (uint32_t)((tid >> 4) * lda4 + (tid & 15) * 16);
+    // window-row element f = tid + 256 j: pixel kk = f / 16 (x0 - 1 + kk), column group f % 16
+    int bkk[NVR];
+    bool bin[NVR];
+#pragma unroll
+    for (int j = 0; j < NVR; ++j) {
+        const int f = tid + 256 * j;
+        bin[j] = f < 18 * 16;
+        bkk[j] = f >> 4;
+    }
+
+    floatx16 acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+    float4 ra, rb[3][NVR];
+    auto load_a = [&](const WgStrip& q) {
+        const int64_t pix = ((int64_t)q.b * H + q.y) * W + q.seg * 16;
+        ra = bload4(rsa, (uint32_t)((pix - p0) * lda4) + aoff);
+    };
+    auto load_row = [&](const WgStrip& q, int yy, float4 (&r)[NVR]) {
+        const int64_t pix = ((int64_t)q.b * H + yy) * W + q.seg * 16 - 1;   // window pixel kk = 0
+        const bool rowok = (unsigned)yy < (unsigned)H;
+#pragma unroll
+        for (int j = 0; j < NVR; ++j) {
+            const int xx = q.seg * 16 + bkk[j] - 1;
+            const bool ok = bin[j] && rowok && (unsigned)xx < (unsigned)W;
+            r[j] = bload4(rsb, ok ? (uint32_t)((pix + bkk[j] - pb) * ldb4 + (tid & 15) * 16) : kOOB);
+        }
+    };
+    auto store_a = [&](int buf) {
+        const auto sp = split_np<NP>(ra);
+        const int off = WgM::off(tid >> 4, (tid & 15) * 4);
+#pragma unroll
+        for (int p = 0; p < NP; ++p) *reinterpret_cast<uint2*>(lds + buf * SA + p * PLA + off) = sp.p[p];
+    };
+    auto store_row = [&](int yy, const float4 (&r)[NVR]) {
+        char* d = lds + 2 * SA + ((yy + 1) & 3) * SLOT;
+#pragma unroll
+        for (int j = 0; j < NVR; ++j)
+            if (bin[j]) {
+                const auto sp = split_np<NP>(r[j]);
+                const int off = WgM::off(bkk[j], (tid & 15) * 4);
+#pragma unroll
+                for (int p = 0; p < NP; ++p) *reinterpret_cast<uint2*>(d + p * PLB + off) = sp.p[p];
+            }
+    };
+    auto compute = [&](int buf, int y) {
+        const char* sa = lds + buf * SA;
+        const char* sb = lds + 2 * SA;
+        bf16x8 fa[1][NP];
+        mnc_frag_at<kWgRows, NP>(sa, PLA, cbk * 32, 0, fa[0]);
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+            const int slot = (y + ky) & 3;   // row y + ky - 1
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+                const int t = ky * 3 + kx;
+                bf16x8 fb[NP];
+                mnc_frag_at<kWgRows, NP>(sb, PLB, cib * 32, slot * 18 + kx, fb);
+                if constexpr (NP == 3) {   // the six products of s3_mfma, smallest first
+                    constexpr int P[6] = {2, 1, 0, 1, 0, 0};
+                    constexpr int Q[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+                    for (int u = 0; u < 6; ++u)
+                        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][P[u]], fb[Q[u]], acc[t], 0, 0, 0);
+                } else {
+                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][0], fb[0], acc[t], 0, 0, 0);
+                }
+            }
+        }
+    };
+
+    if (kbeg < kend) {   // (uniform; an empty slice writes a zero slab)
+    // prologue: A and the three window rows of the first stage
+    load_a(pos);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) load_row(pos, pos.y - 1 + k, rb[k]);
+    store_a(0);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) store_row(pos.y - 1 + k, rb[k]);
+    __syncthreads();
+    int cur = 0;
+    for (int kt = kbeg; kt < kend; ++kt) {
+        const bool more = kt + 1 < kend;
+        WgStrip nx = pos;
+        nx.next(H, W);
+        const bool fresh = nx.y == 0;   // a new strip: three rows (uniform)
+        if (more) {
+            load_a(nx);
+            if (fresh) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) load_row(nx, k - 1, rb[k]);
+            } else {
+                load_row(nx, nx.y + 1, rb[0]);
+            }
+        }
+        compute(cur, pos.y);
+        if (more) {
+            store_a(cur ^ 1);
+            if (fresh) {
+                __syncthreads();   // the ring slots of the finished strip may still be read
+#pragma unroll
+                for (int k = 0; k < 3; ++k) store_row(k - 1, rb[k]);
+            } else {
+                store_row(nx.y + 1, rb[0]);   // slot of row y - 2: free since the last barrier
+            }
+        }
+        __syncthreads();
+        cur ^= 1;
+        pos = nx;
+    }
+    }
+    // slab z: C[z][co][tap*cin + ci] (row stride a.ldc = 9*cin)
+    const int lane = tid & 63;
+    float* dst = a.C + (int64_t)tile.z * a.slab_stride;
+    const int cin = a.b_cin;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int n = t * cin + ci0 + cib * 32 + (lane & 31);
+            const int co = co0 + cbk * 32 + 4 * (lane >> 5) + 8 * g;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) dst[(int64_t)(co + q) * a.ldc + n] = acc[t][4 * g + q];
+        }
+}
+
+// ------------------------------------------------------------------------------------------------
 // B1 window weight gradient on the bf16 twins (pre-split, NP = 1: plain NHWC bf16 rows).  The same
 // decomposition as conv3x3_wgrad_win_body — a workgroup owns a 64 (co) x 64 (ci) channel pair over all
 // nine taps and a split-K slice; wave w the 32x32 block (w & 1, w >> 1) of every tap — with stages of
@@ -955,6 +1138,152 @@ __device__ __forceinline__ void conv3x3_wgrad_win_dma_body(const GemmArgs& a) {
         }
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// The LDS-DMA weight gradient walked down P-pixel-wide column strips (round 4; the strip order of
+// conv3x3_wgrad_strip_body).  A slice is a sequence of STEPS: each step DMAs one window row (P + 2
+// pixels, padded to whole 8-row DMA instructions) into a ring of 8 row slots (step i -> slot i & 7) and
+// one A stage (dZ, P pixels) into a ring of NBUF = 3 stage slots; step i computes the stage whose
+// rows came in steps i - 2, i - 1, i.  A strip (and the slice's first strip) opens with two steps that
+// only load rows y0 - 1 and y0 (their A DMA reads the out-of-range offset: zeros, never read), so every
+// step issues the same DMA instructions and the counted vmcnt of the round-3 kernel applies unchanged.
+// Per stage: 1 + P/8 + ... = (P + 2)/8 + P/8 DMA instructions (9 at P = 32) against 3 (P + 2)/8 + P/8
+// (17): X fetched once per strip (plus the 2-row preamble) instead of three times.
+// ------------------------------------------------------------------------------------------------
+template <int P>
+struct WgsGeo {
+    static constexpr int NIA = P / 8;                   // DMA instructions of A per step
+    static constexpr int NIR = (P + 2 + 7) / 8;         // ... of one window row
+    static constexpr int NI = NIA + NIR;
+    static constexpr int SLOTS = (NI + 3) / 4;          // per wave
+    static constexpr int WAIT = NI / 4;
+    static constexpr int SA = P * 128, ROW = NIR * 8 * 128, KR = NIR * 8;   // bytes; k-rows per row slot
+    static constexpr int NBUF = 3, NROW = 8;
+};
+
+template <int P>
+__device__ __forceinline__ void conv3x3_wgrad_strip_dma_body(const GemmArgs& a) {
+    static_assert(P % 16 == 0, "stage");
+    using G = WgsGeo<P>;
+    __shared__ __attribute__((aligned(1024))) char lds[G::NBUF * G::SA + G::NROW * G::ROW];
+    char* const ldsB = lds + G::NBUF * G::SA;
+
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int cbk = wave & 1, cib = wave >> 1;
+    const TileId tile = xcd_tile();
+    const int co0 = tile.x * 64, ci0 = tile.y * 64;
+    const int H = a.H, W = a.W;
+    const int segs = W / P;
+    const int nst = a.K / P;
+    const int kbeg = tile.z * a.kstages_per_split;
+    const int kend = min(nst, kbeg + a.kstages_per_split);
+
+    // strip walk: stage s -> strip s / H (= image b, column segment), row y = s % H
+    const int s0 = min(kbeg, nst - 1);
+    const int b0 = s0 / (segs * H);
+    const int64_t p0 = (int64_t)b0 * H * W;   // the slice's first image (operand window base)
+    const int64_t pb = p0 - W - 1 > 0 ? p0 - W - 1 : 0;
+    const int rowA = (int)a.lda * 2, rowB = (int)a.ldb * 2;
+    const DmaRsrc rsa = dma_rsrc(ps_at(a.A, (p0 * a.lda + a.a_coff + co0) * 2));
+    const DmaRsrc rsb = dma_rsrc(ps_at(a.Bm, (pb * a.ldb + a.b_coff + ci0) * 2));
+
+    const int lrow = lane >> 3, lch = lane & 7;
+    int sj[G::SLOTS], soff[G::SLOTS], skr[G::SLOTS];
+#pragma unroll
+    for (int t = 0; t < G::SLOTS; ++t) {
+        const int j = wave + 4 * t;
+        sj[t] = j < G::NI ? j : -1;
+        const int kr = 8 * (j < G::NIA ? j : j - G::NIA) + lrow;   // k-row within the A stage / row slot
+        const int gch = lch ^ (((kr >> 1) & 1) << 2);
+        skr[t] = kr;
+        soff[t] = (j < G::NIA ? kr * rowA : (kr - 1) * rowB) + gch * 16;   // B: pixel x0 - 1 + kr
+    }
+    // steps: each strip of the slice contributes its stages + 2 (rows y0 - 1, y0 first)
+    const int nsteps = kbeg < kend ? (kend - kbeg) + 2 * ((kend - 1) / H - kbeg / H + 1) : 0;
+    // issue-side walk: strip index and the row the next step loads
+    int w_strip = kbeg / H, w_row = kbeg % H - 1, w_ylo = kbeg % H;
+    auto issue = [&](int step) {   // DMAs of the walk's current step into its slots, then advance
+        const int sb = w_strip / segs, sx0 = (w_strip - sb * segs) * P;
+        const int ya = w_row - 1;   // the stage this step computes (when >= w_ylo)
+        const bool hasA = ya >= w_ylo;
+        const int64_t rowpix = ((int64_t)sb * H + w_row) * W + sx0;
+        const uint32_t da = hasA ? (uint32_t)((((int64_t)sb * H + ya) * W + sx0 - p0) * rowA) : 0u;
+        const bool rowok = (unsigned)w_row < (unsigned)H;
+        char* baseA = lds + (step % G::NBUF) * G::SA;
+        char* baseB = ldsB + (step & (G::NROW - 1)) * G::ROW;
+#pragma unroll
+        for (int t = 0; t < G::SLOTS; ++t) {
+            const int j = sj[t];
+            if (j < 0) continue;   // wave-uniform
+            if (j < G::NIA) {
+                dma16(rsa, baseA + j * 1024, hasA ? da + (uint32_t)soff[t] : kOOB);
+            } else {
+                const int xx = sx0 + skr[t] - 1;
+                const bool ok = rowok && skr[t] < P + 2 && (unsigned)xx < (unsigned)W;
+                dma16(rsb, baseB + (j - G::NIA) * 1024,
+                      ok ? (uint32_t)((rowpix - pb) * rowB) + (uint32_t)soff[t] : kOOB);
+            }
+        }
+        // advance: the next row of this strip, or the next strip's preamble
+        if (++w_row == H + 1) { ++w_strip; w_row = -1; w_ylo = 0; }
+    };
+
+    floatx16 acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+    auto compute = [&](int step) {
+        const char* sa = lds + (step % G::NBUF) * G::SA;
+#pragma unroll
+        for (int q = 0; q < P / 16; ++q) {
+            bf16x8 fa;
+            wgd_frag(sa, cbk * 32, 16 * q, fa);
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky) {
+                const char* sr = ldsB + ((step - 2 + ky) & (G::NROW - 1)) * G::ROW;
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx) {
+                    bf16x8 fb;
+                    wgd_frag(sr, cib * 32, kx + 16 * q, fb);
+                    acc[ky * 3 + kx] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, acc[ky * 3 + kx], 0, 0, 0);
+                }
+            }
+        }
+    };
+
+    // compute steps: a step computes iff its A stage exists (bit step % NBUF of comp)
+    int comp = 0;
+    auto issue_step = [&](int step) {
+        const int bit = 1 << (step % G::NBUF);
+        comp = w_row - 1 >= w_ylo ? comp | bit : comp & ~bit;
+        issue(step);
+    };
+    if (nsteps > 0) issue_step(0);
+    if (nsteps > 1) issue_step(1);
+    for (int i = 0; i < nsteps; ++i) {
+        if (i + 1 < nsteps) wgd_wait_barrier<G::WAIT>();   // step i landed; i + 1 may still fly
+        else wgd_wait_barrier<0>();
+        const bool ci = (comp >> (i % G::NBUF)) & 1;   // (read before step i + 2 reuses the slot)
+        // step i + 2 reuses the A slot of step i - 1 and the row slot of step i - 6: finished (barrier)
+        if (i + 2 < nsteps) issue_step(i + 2);
+        if (ci) compute(i);
+    }
+    // slab z: C[z][co][tap*cin + ci] (row stride a.ldc = 9*cin)
+    const int cin = a.b_cin;
+    float* dst = a.C + (int64_t)tile.z * a.slab_stride;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int n = t * cin + ci0 + cib * 32 + (lane & 31);
+            const int co = co0 + cbk * 32 + 4 * (lane >> 5) + 8 * g;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) dst[(int64_t)(co + q) * a.ldc + n] = acc[t][4 * g + q];
+        }
+}
 
 // ------------------------------------------------------------------------------------------------
 // B1 window conv forward / dgrad with LDS-DMA staging (round 3): conv3x3_win_ps_body's blocks and
