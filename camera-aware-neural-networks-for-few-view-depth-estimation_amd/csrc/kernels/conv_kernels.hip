@@ -269,6 +269,13 @@ template <int KB>
 __global__ __launch_bounds__(256, 2) void k_convT_dgrad_bf16pb4(GemmArgs a) {
     convT_dgrad_psb<1, 2, 2, 4, 2, KB, EpiStoreB16>(a);
 }
+// ... with LDS-DMA staging (gemm_dense_dma_body: 3-stage ring)
+__global__ __launch_bounds__(256, 2) void k_convT_fwd_bf16dt(GemmArgs a) {
+    gemm_dense_dma_body<2, 2, 2, 2, false, EpiConvTB16>(a);
+}
+__global__ __launch_bounds__(256, 2) void k_convT_dgrad_bf16db(GemmArgs a) {
+    gemm_dense_dma_body<2, 2, 2, 2, true, EpiStoreB16>(a);
+}
 template <int WM, int WN, int KB>
 __global__ __launch_bounds__(256) void k_conv3x3_wgrad_bf16p(GemmArgs a) { conv3x3_wgrad_psb<1, WM, WN, 2, 2, KB>(a); }
 template <int WM, int WN, int KB>
@@ -1151,6 +1158,26 @@ void launch_big(void (*fn)(GemmArgs), const char* name, const GemmArgs& a, hipSt
         hipLaunchKernelGGL(fn, grid, dim3(256), 0, st, a);
     }
 }
+// CAD_CONVTDMA bit 1: the bf16 ConvT forward, bit 2: its dgrad on the LDS-DMA dense GEMM.  Measured at
+// configs[3] (4 launches per step): forward 1.47 -> 1.42 ms (default on), dgrad 1.11 (256 x 128 tiles,
+// CAD_BIGT) vs 1.13 ms
+int convt_dma() {
+    static const int m = [] {
+        const char* e = std::getenv("CAD_CONVTDMA");
+        return e && e[0] ? std::atoi(e) : 1;
+    }();
+    return m;
+}
+void launch_dense_dma(void (*fn)(GemmArgs), const char* name, const GemmArgs& a, hipStream_t st) {
+    const dim3 grid(cdiv(a.M, 128), cdiv(a.N, 128), 1);
+    if (prof_enabled()) {
+        prof_push(name, 2.0 * a.M * a.N * (double)a.K, st);
+        hipLaunchKernelGGL(fn, grid, dim3(256), 0, st, a);
+        prof_pop(st);
+    } else {
+        hipLaunchKernelGGL(fn, grid, dim3(256), 0, st, a);
+    }
+}
 void convT_fwd_ps(Split x, int cin, Split wf, const float* bias, int cout, float* y, int64_t ldy, int ycoff, int B,
                   int H, int W, hipStream_t st, bool y_bf16) {
     ps_check(x, cin, "convT_fwd x");
@@ -1164,6 +1191,10 @@ void convT_fwd_ps(Split x, int cin, Split wf, const float* bias, int cout, float
     const Cfg c = pick_cfg(a.M, a.N);
     const int kb = ps_kb(false, c);
     a.kstages_per_split = cdiv(a.K, kb);
+    if (y_bf16 && (convt_dma() & 1) && a.N >= 128 && a.K % 8 == 0 && a.lda % 8 == 0 && a.a_coff % 8 == 0) {
+        launch_dense_dma(k_convT_fwd_bf16dt, "void cad::k_convT_fwd_bf16dt(cad::GemmArgs)", a, st);
+        return;
+    }
     if (y_bf16 && (bigt_mask() & 1) && a.N >= 128 && a.M >= 4096) {
         launch_big(k_convT_fwd_bf16pt4<32>, "void cad::k_convT_fwd_bf16pt4<32>(cad::GemmArgs)", a, st);
         return;
@@ -1184,6 +1215,10 @@ void convT_dgrad_ps(Split g, int cout, Split wm, int cin, float* dx, int B, int 
     const Cfg c = pick_cfg(a.M, a.N);
     const int kb = ps_kb(false, c);
     a.kstages_per_split = cdiv(a.K, kb);
+    if (dx_bf16 && (convt_dma() & 2) && a.N >= 128 && cout % 32 == 0 && a.lda % 8 == 0 && a.a_coff % 8 == 0) {
+        launch_dense_dma(k_convT_dgrad_bf16db, "void cad::k_convT_dgrad_bf16db(cad::GemmArgs)", a, st);
+        return;
+    }
     if (dx_bf16 && (bigt_mask() & 2) && a.N >= 128 && a.M >= 4096) {
         launch_big(k_convT_dgrad_bf16pb4<32>, "void cad::k_convT_dgrad_bf16pb4<32>(cad::GemmArgs)", a, st);
         return;

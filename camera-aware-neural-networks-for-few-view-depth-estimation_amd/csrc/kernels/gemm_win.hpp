@@ -1418,4 +1418,112 @@ __device__ __forceinline__ void conv3x3_win_dma_body(const GemmArgs& a) {
     win_epilogue<WM, WN, MI, NJ, CW, Epi>(a, acc, tile.x, n0, b, y0, x0, reinterpret_cast<float*>(lds));
 }
 
+// ------------------------------------------------------------------------------------------------
+// Dense bf16 GEMM C[m][n] = sum_k A[m][k] B[n][k] with LDS-DMA staging (round 4): the ConvT forward
+// (A = the low-res twin, K = cin) and, with UPG, the ConvT input gradient (A row m gathers the four
+// high-res pixels (2y + dy, 2x + dx) of dL/dup: K = (q = (dy, dx), co), cout % 32 == 0 so a 32-deep
+// stage stays in one q).  The register-staged gemm_body_ps keeps one stage in flight with 8 MFMAs per
+// wave and stage (128 x 128): its load latency is exposed (the ConvT GEMMs ran at 430-630 TFLOP/s).
+// Here a ring of 3 stages keeps two in flight with no staging registers (48 KB of LDS for 128 x 128:
+// three workgroups per CU).  LDS rows are unpadded 64-B (32 bf16) with the source-side chunk swizzle of
+// conv3x3_win_dma_body (wind_off); a DMA wave-instruction fills 16 rows.  M / N tails and K tails
+// (K % 8 == 0) read the out-of-range offset: zeros.
+// ------------------------------------------------------------------------------------------------
+template <int BM, int BN>
+struct DenseDGeo {
+    static constexpr int NIA = BM / 16, NIB = BN / 16, NI = NIA + NIB;
+    static constexpr int SLOTS = (NI + 3) / 4, WAIT = NI / 4;
+    static constexpr int SA = BM * 64, STAGE = (BM + BN) * 64, NBUF = 3;
+};
+template <int WM, int WN, int MI, int NJ, bool UPG, class Epi>
+__device__ __forceinline__ void gemm_dense_dma_body(const GemmArgs& a) {
+    constexpr int BM = 32 * MI * WM, BN = 32 * NJ * WN;
+    using G = DenseDGeo<BM, BN>;
+    __shared__ __attribute__((aligned(1024))) char lds[G::NBUF * G::STAGE];
+
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int wm = wave / WN, wn = wave % WN;
+    const TileId tile = xcd_tile();
+    const int m0 = tile.x * BM, n0 = tile.y * BN;
+    const int K = a.K, S = (K + 31) / 32;
+    const int rowa = (int)a.lda * 2, rowb = (int)a.ldb * 2;
+    const int W2 = 2 * a.W;
+    // A base: row m0 (UPG: its high-res pixel (2y, 2x)); offsets relative to it
+    auto hp = [&](int m) {   // high-res pixel of low-res row m, q = 0
+        const int x = m % a.W, t = m / a.W, y = t % a.H, b = t / a.H;
+        return ((int64_t)b * (2 * a.H) + 2 * y) * W2 + 2 * x;
+    };
+    const int64_t abase = UPG ? hp(min(m0, a.M - 1)) : (int64_t)m0;
+    const DmaRsrc rsa = dma_rsrc(reinterpret_cast<const char*>(a.A) + (abase * a.lda + a.a_coff) * 2);
+    const DmaRsrc rsb = dma_rsrc(reinterpret_cast<const char*>(a.Bm) + ((int64_t)n0 * a.ldb + a.b_coff) * 2);
+
+    const int lrow = lane >> 2, lch = lane & 3;
+    int sj[G::SLOTS], soff[G::SLOTS], sch[G::SLOTS];
+#pragma unroll
+    for (int t = 0; t < G::SLOTS; ++t) {
+        const int j = wave + 4 * t;
+        sj[t] = j < G::NI ? j : -1;
+        const int r = 16 * (j < G::NIA ? j : j - G::NIA) + lrow;
+        const int gch = lch ^ ((r >> 2) & 3);
+        sch[t] = 8 * gch;   // k offset of the lane's piece within the stage
+        if (j < G::NIA) {
+            const int m = m0 + r;
+            soff[t] = m < a.M ? (int)((UPG ? hp(m) - abase : (int64_t)r) * rowa) + gch * 16 : -1;
+        } else {
+            soff[t] = n0 + r < a.N ? r * rowb + gch * 16 : -1;
+        }
+    }
+    const int cout = a.a_cin;   // (UPG) K = 4 cout
+    auto issue = [&](int stage, int buf) {
+        const int k0 = stage * 32;
+        int adda = k0 * 2;
+        if constexpr (UPG) {
+            const int q = k0 / cout, co = k0 - q * cout;
+            adda = ((q >> 1) * W2 + (q & 1)) * rowa + co * 2;
+        }
+        char* base = lds + buf * G::STAGE;
+#pragma unroll
+        for (int t = 0; t < G::SLOTS; ++t) {
+            const int j = sj[t];
+            if (j < 0) continue;   // wave-uniform
+            const bool ok = soff[t] >= 0 && k0 + sch[t] < K;
+            if (j < G::NIA) dma16(rsa, base + j * 1024, ok ? (uint32_t)(soff[t] + adda) : kOOB);
+            else dma16(rsb, base + G::SA + (j - G::NIA) * 1024, ok ? (uint32_t)(soff[t] + k0 * 2) : kOOB);
+        }
+    };
+
+    floatx16 acc[MI][NJ];
+    acc_zero(acc);
+    const int h = lane >> 5;
+    auto compute = [&](int buf) {
+        const char* sa = lds + buf * G::STAGE;
+        const char* sb = sa + G::SA;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            bf16x8 fa[MI][1], fb[NJ][1];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+                fb[j][0] = *reinterpret_cast<const bf16x8*>(sb + wind_off(wn * 32 * NJ + j * 32 + (lane & 31), 2 * q + h));
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+                fa[i][0] = *reinterpret_cast<const bf16x8*>(sa + wind_off(wm * 32 * MI + i * 32 + (lane & 31), 2 * q + h));
+            s3_mfma<1>(acc, fa, fb);
+        }
+    };
+
+    if (S > 0) issue(0, 0);
+    if (S > 1) issue(1, 1);
+    int buf = 0;
+    for (int s = 0; s < S; ++s) {
+        if (s + 1 < S) wgd_wait_barrier<G::WAIT>();
+        else wgd_wait_barrier<0>();
+        if (s + 2 < S) issue(s + 2, buf == 0 ? G::NBUF - 1 : buf - 1);
+        compute(buf);
+        buf = buf == G::NBUF - 1 ? 0 : buf + 1;
+    }
+    __syncthreads();   // the ring is the epilogue's scratch
+    gemm_epilogue_t<WM, WN, MI, NJ>(a, acc, tile, reinterpret_cast<float*>(lds), Epi{});
+}
+
 }  // namespace cad

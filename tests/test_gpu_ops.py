@@ -58,6 +58,8 @@ CONV_SHAPES = [  # B, H, W, cin, cout
     (2, 4, 4, 8, 4), (1, 30, 40, 256, 128),
     # M <= 64 with N > 64: the 64x256 tile (bottleneck at small images)
     (1, 4, 4, 512, 1024), (1, 8, 8, 256, 512), (2, 3, 4, 64, 128),
+    # few-channel input (enc1.conv1) at several split-K slices, two output-channel blocks
+    (2, 40, 64, 4, 128), (1, 48, 96, 8, 64),
 ]
 
 
@@ -168,6 +170,8 @@ WGRAD_BF16_SHAPES = [  # B, H, W, cin, cout, xcoff: the bf16 engine's weight gra
     (2, 9, 32, 256, 128, 64),   # skip half of a concat-style twin
     (2, 6, 20, 64, 64, 0),      # W % 16 != 0: the im2col GEMM
     (2, 5, 16, 32, 64, 0),      # cin % 64 != 0: the im2col GEMM
+    (2, 40, 64, 8, 64, 0),      # cin = 8 (the NHWC8 image twin): the im2col GEMM, several K-splits
+    (1, 30, 80, 8, 128, 8),     # ... at a channel offset, two output-channel blocks
 ]
 
 
