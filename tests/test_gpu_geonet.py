@@ -249,6 +249,9 @@ def _wider(cad, dev, oracle, model, f, B, H, W):
             bad.append((n, st))
     worst.sort(reverse=True)
     print("worst gradients vs fp64 ((max, p99.9, fp32-oracles p99.9, cosine), name):", worst[:4])
+    if os.environ.get("CAD_GEO_ALLGRADS"):
+        for st_, n_ in worst:
+            print("  %-40s max %.2e p99.9 %.2e witness %.2e cos %.7f" % (n_, *st_))
     assert not bad, bad
 
 
