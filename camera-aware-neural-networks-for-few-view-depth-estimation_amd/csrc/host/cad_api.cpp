@@ -737,9 +737,13 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
         cad::conv3x3_wgrad(dY, C, dc.a1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
         cad::conv3x3_dgrad(dY, C, dc.c2.wd, C, dA1, C, B, Hh, Ww, st);
     }
-    // FiLM: dgamma/dbeta per (sample, channel); the ReLU sees dA1 * gamma (folded into bn_relu_bwd)
+    // FiLM: dgamma/dbeta per (sample, channel); the ReLU sees dA1 * gamma (folded into bn_relu_bwd).  By
+    // default the FiLM sums come from bn1's backward reduction pass over the same (dA1, y1) (round 4;
+    // CAD_FILMFUSE=0: the separate film_affine_bwd pass)
     const int64_t HW = (int64_t)Hh * Ww;
-    if (dc.has_film())
+    static const bool film_fuse = env_flag("CAD_FILMFUSE", 1) != 0;
+    const bool film_sep = dc.has_film() && (!film_fuse || dc.y1_rc);
+    if (film_sep)
         cad::film_affine_bwd(dA1, dc.y1, C, dc.b1.scale, dc.b1.shift, B, HW, h->dscr, dc.film.dgam, dc.film.dbet, st,
                              dc.y1b, ps);
     // bn1 + relu; the fp32 dY1 only when a conv1 GEMM below reads it (enc1's 4-channel input keeps the
@@ -762,9 +766,11 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
         r.out = ps ? dYs : static_cast<void*>(dY); r.ldo = C; r.out_bf16 = ps;
         cad::conv3x3_recompute(o.x, o.ldx, dc.c1.cin, o.w, C, B, Hh, Ww, r, st);
     } else {
+        const bool ff = dc.has_film() && !film_sep;
         cad::bn_relu_bwd(dA1, C, 0, dc.y1, C, dc.b1.mean, dc.b1.invstd, dc.b1.scale, dc.b1.shift, h->P(dc.b1.widx), M,
                          h->dscr, dc.b1.coef, h->G(dc.b1.widx), h->G(dc.b1.bidx), dy1_f32 ? dY : nullptr, st,
-                         dc.has_film() ? dc.film.gam : nullptr, HW, ps ? dYs : nullptr, true, dc.y1b, nullptr, ps);
+                         dc.has_film() ? dc.film.gam : nullptr, HW, ps ? dYs : nullptr, true, dc.y1b, nullptr, ps,
+                         nullptr, ff ? dc.film.dgam : nullptr, ff ? dc.film.dbet : nullptr);
     }
     if (dc.has_film()) cad::film_mlp_bwd(film_view(h, dc), h->camn, B, st);
     // conv1: wgrad, dgrad

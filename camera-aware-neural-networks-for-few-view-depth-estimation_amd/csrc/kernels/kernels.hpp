@@ -213,7 +213,7 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
                  int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
                  hipStream_t st, const float* gmul = nullptr, int64_t HW = 1, void* dy_split = nullptr,
                  bool relu = true, bool y_bf16 = false, const HeadGrad* head = nullptr, bool g_bf16 = false,
-                 const PoolAdd* pool = nullptr);
+                 const PoolAdd* pool = nullptr, float* film_dgam = nullptr, float* film_dbet = nullptr);
 // out_split != nullptr: also the pooled output's split twin (dense, ld C); out may then be nullptr
 // x_bf16: x is a bf16 twin (rows of ldx elements; requires out_split)
 void maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float* out, uint8_t* idx,

@@ -209,6 +209,40 @@ struct OpBnBwd {
         }
     }
 };
+// OpBnBwd of a FiLM block (gmul = gamma[b][c]) that also forms the FiLM affine's sums in the same pass
+// over (g, y): acc[2] = sum g a, acc[3] = sum g with g the raw gradient of the FiLM output and a =
+// relu(y scale + shift) (k_film_reduce's sums; slices aligned to samples by the caller)
+template <bool YB, bool GB>
+struct OpBnBwdFilm {
+    const float *g, *y, *mean, *invstd, *scale, *shift, *gmul;
+    int64_t ldg; int gcoff, C; int64_t HW;
+    __device__ BnCoef prep(int c4) const {
+        BnCoef k;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int c = c4 * 4 + e;
+            k.sc[e] = scale[c]; k.sh[e] = shift[c]; k.mu[e] = mean[c]; k.is[e] = invstd[c];
+        }
+        return k;
+    }
+    __device__ void operator()(int64_t r, int c4, double (&acc)[4][4], const BnCoef& k) const {
+        const float4 gr = load4<GB>(g, r * ldg + gcoff + c4 * 4);
+        const float4 m = *reinterpret_cast<const float4*>(gmul + (r / HW) * C + c4 * 4);
+        const float4 yv = load4<YB>(y, r * C + c4 * 4);
+        const float g0[4] = {gr.x, gr.y, gr.z, gr.w}, ga[4] = {gr.x * m.x, gr.y * m.y, gr.z * m.z, gr.w * m.w};
+        const float ya[4] = {yv.x, yv.y, yv.z, yv.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float z = __fmaf_rn(ya[e], k.sc[e], k.sh[e]);
+            const float dz = z > 0.f ? ga[e] : 0.f;
+            const float xh = (ya[e] - k.mu[e]) * k.is[e];
+            acc[0][e] += dz;
+            acc[1][e] += (double)dz * xh;
+            acc[2][e] += (double)g0[e] * fmaxf(z, 0.f);
+            acc[3][e] += g0[e];
+        }
+    }
+};
 struct OpHeadBwd {
     const float *a, *dpred, *sig; float md; int C;
     __device__ NoPrep prep(int) const { return {}; }
@@ -256,6 +290,15 @@ int launch_colreduce(const Op& op, int64_t R, int C, double* part, hipStream_t s
     const size_t shm = (size_t)RY * CX * NOUT * 4 * sizeof(double);
     hipLaunchKernelGGL((k_colreduce<NOUT, Op>), dim3(cdiv(C4, CX), S), dim3(CX, RY), shm, st, op, R, C, rps, part);
     return S;
+}
+// ... with caller-chosen slices (S slices of rps rows)
+template <int NOUT, class Op>
+void launch_colreduce_slices(const Op& op, int64_t R, int C, int S, int64_t rps, double* part, hipStream_t st) {
+    const int C4 = C >> 2;
+    const int CX = std::min(C4, 64);
+    const int RY = std::max(1, 256 / CX);
+    const size_t shm = (size_t)RY * CX * NOUT * 4 * sizeof(double);
+    hipLaunchKernelGGL((k_colreduce<NOUT, Op>), dim3(cdiv(C4, CX), S), dim3(CX, RY), shm, st, op, R, C, rps, part);
 }
 void launch_colfinal(const double* part, int S, int N, double* tot, float* dst, float scale, hipStream_t st) {
     hipLaunchKernelGGL(k_colfinal, dim3(cdiv(N, 64)), dim3(64, kFinalLanes), 0, st, part, S, N, tot, dst, scale);
@@ -469,13 +512,53 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_rows(const float* __restric
         if constexpr (NP > 0) split4_store<NP>(os, C, 0, r, c0, ov);
     }
 }
+// FiLM sums from OpBnBwdFilm's sample-aligned slices: dgam[b][c] = sum over sample b's k slices
+__global__ void k_film_from_parts(const double* __restrict__ part, int k, int C, int B, float* __restrict__ dgam,
+                                  float* __restrict__ dbet) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B * C) return;
+    const int b = i / C, c = i - b * C;
+    double g = 0.0, be = 0.0;
+    for (int s = b * k; s < (b + 1) * k; ++s) {
+        const double* p = part + (int64_t)s * 4 * C;
+        g += p[2 * C + c];
+        be += p[3 * C + c];
+    }
+    dgam[i] = (float)g;
+    dbet[i] = (float)be;
+}
 void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, const float* mean,
                  const float* invstd, const float* scale, const float* shift, const float* gamma,
                  int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
                  hipStream_t st, const float* gmul, int64_t HW, void* dy_split, bool relu, bool y_bf16,
-                 const HeadGrad* head, bool g_bf16, const PoolAdd* pool) {
+                 const HeadGrad* head, bool g_bf16, const PoolAdd* pool, float* film_dgam, float* film_dbet) {
     double* tot = scratch;
     double* part = scratch + 2 * C;
+    if (film_dgam) {
+        // a FiLM block's bn1: the BN sums and the FiLM affine's per-(sample, channel) sums in one pass,
+        // k slices per sample (rows per slice dividing HW; >= 256 rows, <= 2048 slices in all)
+        if (!gmul || !g || head || pool || !relu || M % HW) throw std::runtime_error("bn_relu_bwd: FiLM sums layout");
+        const int B = (int)(M / HW);
+        int k = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)64, HW / 256, (int64_t)(2048 / std::max(B, 1))}));
+        while (HW % k) --k;
+        const int S = B * k;
+        part = scratch + 4 * C;
+        if (y_bf16 && g_bf16)
+            launch_colreduce_slices<4>(OpBnBwdFilm<true, true>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW},
+                                       M, C, S, HW / k, part, st);
+        else if (y_bf16)
+            launch_colreduce_slices<4>(OpBnBwdFilm<true, false>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW},
+                                       M, C, S, HW / k, part, st);
+        else if (g_bf16)
+            launch_colreduce_slices<4>(OpBnBwdFilm<false, true>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW},
+                                       M, C, S, HW / k, part, st);
+        else
+            launch_colreduce_slices<4>(OpBnBwdFilm<false, false>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW},
+                                       M, C, S, HW / k, part, st);
+        launch_colfinal(part, S, 4 * C, tot, nullptr, 1.f, st);   // tot[0, 2C): the BN sums
+        hipLaunchKernelGGL(k_film_from_parts, dim3(cdiv((int64_t)B * C, 256)), dim3(256), 0, st, part, k, C, B,
+                           film_dgam, film_dbet);
+    }
     const HeadGrad hg = head ? *head : HeadGrad{};
     PoolAdd pa = pool ? *pool : PoolAdd{};
     if (head && (g || gmul || g_bf16 || pool)) throw std::runtime_error("bn_relu_bwd: head gradient with an explicit gradient");
@@ -499,7 +582,7 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
             default: return fn(F{}, F{}, F{});
         }
     };
-    const int S = with_mode([&](auto hgc, auto gbc, auto pac) {
+    const int S = film_dgam ? 0 : with_mode([&](auto hgc, auto gbc, auto pac) {
         constexpr bool HG = decltype(hgc)::value, GB = decltype(gbc)::value, PA = decltype(pac)::value;
         return y_bf16 ? launch_colreduce<2>(OpBnBwd<true, HG, GB, PA>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C,
                                                                      HW, relu, hg, pa},
@@ -508,7 +591,7 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
                                                                       C, HW, relu, hg, pa},
                                             M, C, part, st);
     });
-    launch_colfinal(part, S, 2 * C, tot, nullptr, 1.f, st);
+    if (!film_dgam) launch_colfinal(part, S, 2 * C, tot, nullptr, 1.f, st);
     hipLaunchKernelGGL(k_bn_bwd_coef, dim3(cdiv(C, 64)), dim3(64), 0, st, tot, C, M, gamma, invstd, coef, dgamma, dbeta);
     const int np = dy_split ? split_planes() : 0;
     char* os = static_cast<char*>(dy_split);
