@@ -276,6 +276,11 @@ __global__ __launch_bounds__(256, 2) void k_convT_fwd_bf16dt(GemmArgs a) {
 __global__ __launch_bounds__(256, 2) void k_convT_dgrad_bf16db(GemmArgs a) {
     gemm_dense_dma_body<2, 2, 2, 2, true, EpiStoreB16>(a);
 }
+// dense (1x1-conv / im2col) forward GEMMs of the config-5 network on the same DMA body
+template <class Epi>
+__global__ __launch_bounds__(256, 2) void k_dense_bf16d(GemmArgs a) {
+    gemm_dense_dma_body<2, 2, 2, 2, false, Epi>(a);
+}
 template <int WM, int WN, int KB>
 __global__ __launch_bounds__(256) void k_conv3x3_wgrad_bf16p(GemmArgs a) { conv3x3_wgrad_psb<1, WM, WN, 2, 2, KB>(a); }
 template <int WM, int WN, int KB>
@@ -588,7 +593,11 @@ WinPick pick_win_ps(int cin, int W, int N, int acoff) {
             }
         return w;
     }
-    if (N == 64 && (W % 128 == 0 || W % 64 == 0)) {   // 512 x 64 tiles
+    static const bool big64 = [] {   // A/B: CAD_WIN64=0 -> 256 x 64 tiles for N = 64
+        const char* e = std::getenv("CAD_WIN64");
+        return !(e && e[0] == '0');
+    }();
+    if (N == 64 && big64 && (W % 128 == 0 || W % 64 == 0)) {   // 512 x 64 tiles
         w.CW = W % 128 == 0 ? 128 : 64;
         w.R = 512 / w.CW;
         w.big = true;
@@ -1040,6 +1049,7 @@ void conv3x3_wgrad_ps(Split dz, int cout, Split x, int cin, float* dw, int B, in
 
 int dense_stats_rows(int64_t M, int N) { return cdiv(M, tile_m(pick_cfg((int)M, N))); }
 
+void launch_dense_dma(void (*fn)(GemmArgs), const char* name, const GemmArgs& a, hipStream_t st);
 void dense_fwd_ps(Split x, int K, Split w, int N, float* y, int64_t ldy, int ycoff, int64_t M, float* stats,
                   hipStream_t st, bool y_bf16, const float* add) {
     ps_check(x, K, "dense x");
@@ -1056,6 +1066,20 @@ void dense_fwd_ps(Split x, int K, Split w, int N, float* y, int64_t ldy, int yco
     const Cfg c = pick_cfg(a.M, a.N);
     const int kb = ps_kb(true, c);
     a.kstages_per_split = cdiv(a.K, kb);
+    static const bool ddma = [] {   // A/B: CAD_DENSEDMA=1 -> the LDS-DMA dense GEMM on 128 x 128 tiles
+        const char* e = std::getenv("CAD_DENSEDMA");
+        return e && e[0] == '1';
+    }();
+    if (ddma && c == C22 && K % 8 == 0 && x.ld % 8 == 0 && x.coff % 8 == 0 && w.ld % 8 == 0 && w.coff % 8 == 0) {
+        if (add && (stats || y_bf16)) throw std::runtime_error("dense GEMM: the added matrix needs fp32 output");
+        if (add) launch_dense_dma(k_dense_bf16d<EpiStoreAdd>, "void cad::k_dense_bf16d<cad::EpiStoreAdd>(cad::GemmArgs)", a, st);
+        else if (y_bf16 && stats)
+            launch_dense_dma(k_dense_bf16d<EpiStoreStatsB16>, "void cad::k_dense_bf16d<cad::EpiStoreStatsB16>(cad::GemmArgs)", a, st);
+        else if (y_bf16) launch_dense_dma(k_dense_bf16d<EpiStoreB16>, "void cad::k_dense_bf16d<cad::EpiStoreB16>(cad::GemmArgs)", a, st);
+        else if (stats) launch_dense_dma(k_dense_bf16d<EpiStoreStats>, "void cad::k_dense_bf16d<cad::EpiStoreStats>(cad::GemmArgs)", a, st);
+        else launch_dense_dma(k_dense_bf16d<EpiStore>, "void cad::k_dense_bf16d<cad::EpiStore>(cad::GemmArgs)", a, st);
+        return;
+    }
     if (add) {
         if (stats || y_bf16) throw std::runtime_error("dense GEMM: the added matrix needs fp32 output");
         launch_kb<KDenseAddP1, 32, 64>(c, kb, a, 1, st);
