@@ -980,7 +980,11 @@ void launch_wgrad_win_ps1(GemmArgs& a, float* dw, float* slab, int64_t slab_cap,
     const int cin = a.b_cin;
     const int tiles = (a.M / 64) * (cin / 64);
     const int nst = a.K / P;
-    int s = std::max(1, std::min(cdiv(2048, tiles), nst / 16));
+    static const int wgs = [] {   // A/B: CAD_WGSLABS = workgroups the split-K aims for (default 2048)
+        const char* e = std::getenv("CAD_WGSLABS");
+        return e && e[0] ? std::max(64, std::atoi(e)) : 2048;
+    }();
+    int s = std::max(1, std::min(cdiv(wgs, tiles), nst / 16));
     const int64_t per = (int64_t)a.M * a.N;
     if (slab_cap > 0) s = (int)std::max<int64_t>(1, std::min<int64_t>(s, slab_cap / per));
     // a K-slice is a loader window of 32-bit byte offsets: keep it below 1 GB in either operand (the
