@@ -680,6 +680,136 @@ void finish_slabs(float* slab, int splits, int64_t per, float* dw, hipStream_t s
     slab_reduce(slab, splits, per, 1, dw, bx, 1, st);
 }
 
+// Weight gradient of the few-channel image layer on S3 (enc1.conv1: cin = 3 or 4, K = 27 / 36): the
+// im2col GEMM runs it on 64 x 256 tiles of which one wave's 64 x 64 block is live (busy 0.25, 1.6 ms at
+// bs32 480x640).  Here every wave of a workgroup owns the whole 64 (co) x 32 NJ (tap, ci) output for
+// its own pixel range — a split-K inside the workgroup — and builds its MFMA fragments straight from
+// global memory (dZ: 8 consecutive pixels of one co per lane; X: the 8 shifted pixels of one (tap, ci)),
+// split exactly into three bf16 planes (the six S3 products, fp32 accumulation).  The four waves'
+// accumulators are summed in LDS in wave order; workgroup partials go through the slab reduction.
+template <int NJ>
+__global__ __launch_bounds__(256) void k_wgrad_narrow_s3(const float* __restrict__ dz, int64_t ldz,
+                                                         const float* __restrict__ x, int64_t ldx, int xoff, int cin,
+                                                         int cout, int B, int H, int W, int ppw,
+                                                         float* __restrict__ out) {
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, c = lane & 31;
+    const int NK = 9 * cin;
+    const int cob = blockIdx.y * 64;
+    const int M = B * H * W;
+    const int p0 = (blockIdx.x * 4 + wave) * ppw, p1 = min(M, p0 + ppw);
+    int ntap[NJ], nci[NJ];
+    bool nok[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int n = 32 * j + c;
+        nok[j] = n < NK;
+        ntap[j] = nok[j] ? n / cin : 0;
+        nci[j] = nok[j] ? n - ntap[j] * cin : 0;
+    }
+    floatx16 acc[2][NJ];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    for (int k0 = p0; k0 < p1; k0 += 16) {
+        const int pb = k0 + 8 * h;   // this lane's 8 pixels pb .. pb + 7
+        float av[2][8], bv[NJ][8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const bool ok = pb + e < p1;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) av[i][e] = ok ? dz[(int64_t)(pb + e) * ldz + cob + 32 * i + c] : 0.f;
+        }
+        int xx = pb % W, r = pb / W, yy = r % H;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int p = pb + e;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int dy = ntap[j] / 3 - 1, dx = ntap[j] % 3 - 1;
+                const bool ok = nok[j] && p < p1 && (unsigned)(yy + dy) < (unsigned)H && (unsigned)(xx + dx) < (unsigned)W;
+                bv[j][e] = ok ? x[(int64_t)(p + dy * W + dx) * ldx + xoff + nci[j]] : 0.f;
+            }
+            if (++xx == W) { xx = 0; if (++yy == H) yy = 0; }
+        }
+        bf16x8 fa[2][3], fb[NJ][3];
+        auto pack = [](const float (&v)[8], bf16x8 (&f)[3]) {
+            const auto sa = split_np<3>(make_float4(v[0], v[1], v[2], v[3]));
+            const auto sb = split_np<3>(make_float4(v[4], v[5], v[6], v[7]));
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+                f[q] = __builtin_bit_cast(bf16x8, make_uint4(sa.p[q].x, sa.p[q].y, sb.p[q].x, sb.p[q].y));
+        };
+#pragma unroll
+        for (int i = 0; i < 2; ++i) pack(av[i], fa[i]);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) pack(bv[j], fb[j]);
+        constexpr int P[6] = {2, 1, 0, 1, 0, 0};
+        constexpr int Q[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+        for (int u = 0; u < 6; ++u)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][P[u]], fb[j][Q[u]], acc[i][j], 0, 0, 0);
+    }
+    // the four waves' partials, summed in wave order (one 32-row block i at a time: 16 NJ values per lane)
+    __shared__ float red[3][NJ * 16][64];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        if (i) __syncthreads();   // the previous round's reads are done
+        if (wave > 0)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) red[wave - 1][j * 16 + r][lane] = acc[i][j][r];
+        __syncthreads();
+        if (wave == 0)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int sidx = j * 16 + r;
+                    const float v = ((acc[i][j][r] + red[0][sidx][lane]) + red[1][sidx][lane]) + red[2][sidx][lane];
+                    // accumulator layout: row (co) 32 i + 8 (r / 4) + 4 h + r % 4, column n = 32 j + c
+                    const int co = cob + 32 * i + 8 * (r >> 2) + 4 * h + (r & 3), n = 32 * j + c;
+                    if (n < NK) out[((int64_t)blockIdx.x * cout + co) * NK + n] = v;
+                }
+    }
+}
+bool wgrad_narrow_s3(const float* dz, int64_t ldz, const float* x, int64_t ldx, int xoff, int cin, int cout, float* dw,
+                     int B, int H, int W, float* slab, int64_t slab_cap, hipStream_t st) {
+    static const bool on = [] {
+        const char* e = std::getenv("CAD_WGNARROW");   // A/B: CAD_WGNARROW=0 keeps the im2col GEMM
+        return !(e && e[0] == '0');
+    }();
+    if (!on || engine() != 1 || cin < 1 || cin > 10 || cout % 64) return false;
+    const int64_t M = (int64_t)B * H * W;
+    if (M >= ((int64_t)1 << 31) - 64) return false;
+    const int64_t per = (int64_t)cout * 9 * cin;
+    if (per % 4) return false;
+    int s = (int)std::min<int64_t>(2048, std::max<int64_t>(1, M / 1024));
+    if (slab_cap > 0) s = (int)std::max<int64_t>(1, std::min<int64_t>(s, slab_cap / per));
+    const int ppw = (int)cdiv(cdiv(M, (int64_t)s * 4), 16) * 16;
+    s = (int)cdiv(M, (int64_t)ppw * 4);
+    if (s > 1 && (int64_t)s * per > slab_cap) return false;
+    float* out = s == 1 ? dw : slab;
+    const dim3 grid(s, cout / 64);
+    if (prof_enabled()) prof_push("cad::k_wgrad_narrow_s3", 2.0 * M * per, st);
+    if (9 * cin <= 32)
+        hipLaunchKernelGGL(k_wgrad_narrow_s3<1>, grid, dim3(256), 0, st, dz, ldz, x, ldx, xoff, cin, cout, B, H, W, ppw, out);
+    else if (9 * cin <= 64)
+        hipLaunchKernelGGL(k_wgrad_narrow_s3<2>, grid, dim3(256), 0, st, dz, ldz, x, ldx, xoff, cin, cout, B, H, W, ppw, out);
+    else
+        hipLaunchKernelGGL(k_wgrad_narrow_s3<3>, grid, dim3(256), 0, st, dz, ldz, x, ldx, xoff, cin, cout, B, H, W, ppw, out);
+    if (prof_enabled()) prof_pop(st);
+    if (s > 1) finish_slabs(slab, s, per, dw, st);
+    return true;
+}
+
 // window-tiled weight gradient (S3): cout, cin multiples of 64, W a multiple of 16
 bool use_wgrad_win(int cout, int cin, int W) {
     return engine() == 1 && cout % 64 == 0 && cin % 64 == 0 && W % 16 == 0;
@@ -826,6 +956,7 @@ void conv3x3_wgrad(const float* dz, int cout, const float* x, int64_t ldx, int x
         launch_wgrad_win(a, dw, slab, slab_cap, 4 * std::max<int64_t>(a.lda, ldx), st);
         return;
     }
+    if (wgrad_narrow_s3(dz, cout, x, ldx, xcoff, cin, cout, dw, B, H, W, slab, slab_cap, st)) return;
     launch_wgrad<KConvWgrad, KConvWgrad3, KConvWgradB>(a, dw, slab, slab_cap, 4 * std::max<int64_t>(a.lda, ldx), st);
 }
 
