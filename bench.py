@@ -25,6 +25,7 @@ workloads (configs[2], configs[3]'s and configs[4]'s per-GPU steps) in the same 
 """
 import argparse
 import ctypes as C
+import gc
 import json
 import re
 import os
@@ -76,8 +77,8 @@ def parse():
     ap.add_argument("--no-extra", action="store_true", help="skip the bf16 workload legs and the data path")
     ap.add_argument("--exchange", default="rccl", choices=("rccl", "torch"),
                     help="N>1 gradient exchange: libcad's RCCL communicator (the build/train path) or torch.distributed")
-    ap.add_argument("--cpu-sample-batch", type=int, default=8)
-    ap.add_argument("--cpu-sample-steps", type=int, default=3)
+    ap.add_argument("--cpu-sample-batch", type=int, default=4)
+    ap.add_argument("--cpu-sample-steps", type=int, default=2)
     a = ap.parse_args()
     preset = {2: ("baseline", "fp32", "1,0,0,0"), 3: ("rayfilm", "bf16", "1,0.1,0.001,0.01"),
               4: ("baseline", "bf16", "1,0.1,0.001,0.01")}[a.config]
@@ -113,25 +114,56 @@ def host_cpu():
             "usable_cpus": usable}
 
 
-CPU_SHARE = 16   # host CPUs one GPU's job may use on the MI355X boxes (OMP_NUM_THREADS there)
+def cpu_quota():
+    """CPUs this job may use by its cgroup quota (cgroup v2 cpu.max / v1 cfs_quota_us), or None when
+    unlimited or unreadable: the GPU boxes give one GPU's job a share of the host's cores this way
+    (their affinity mask still lists every CPU)."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+        if q != "max":
+            return max(1, int(int(q) / int(per)))
+        return None
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as fh:
+            q = int(fh.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fh:
+            per = int(fh.read())
+        return max(1, int(q / per)) if q > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
+def omp_threads_env():
+    """OMP_NUM_THREADS as an int (its first entry, OpenMP's nested-list syntax '8,4' allowed), or None
+    when unset or malformed — recorded, never used to choose the CPU baseline's thread count."""
+    v = os.environ.get("OMP_NUM_THREADS", "")
+    try:
+        n = int(v.split(",")[0])
+        return n if n > 0 else None
+    except ValueError:
+        return None
 
 
 def cpu_threads():
     """Threads for the CPU reference path: the host's physical cores (BASELINE.md §3:
-    set_num_threads(<physical cores>)), bounded by the CPUs this process may run on and by one GPU's
-    CPU share of the box (16; round 3 measured the oracle 2x faster at 16 threads than at 128 there)."""
+    set_num_threads(<physical cores>)), bounded only by the CPUs this process may run on."""
     h = host_cpu()
+    h["cgroup_cpu_quota"] = cpu_quota()
+    h["omp_num_threads_env"] = omp_threads_env()
     n = h["physical_cores"] or h["usable_cpus"] or 1
-    share = int(os.environ.get("OMP_NUM_THREADS", CPU_SHARE) or CPU_SHARE)
-    return max(1, min(n, h["usable_cpus"] or n, share)), h
+    return max(1, min(n, h["usable_cpus"] or n)), h
 
 
-def cpu_baseline(args, sweep=(8,)):
+def cpu_baseline(args, sweep=(16, 8)):
     """cpu_baseline leg: the oracle restatement (oracle/cad_oracle.py: LibTorch CPU, the ATen kernels
     the reference dispatches; the reference source and its compiled harness stay in the build
     container) timed on this host on a bounded sample of the workload — bs`cpu_sample_batch` at the
     benchmark resolution, 1 warm-up + `cpu_sample_steps` timed train steps at the host's physical core
-    count, then one more step at each thread count of `sweep` (the scaling of the CPU path itself)."""
+    count (the reported value), then `cpu_sample_steps` more at each thread count of
+    `sweep` and at the job's cgroup CPU quota (one GPU's share of the box's cores)."""
     import torch
     from oracle import cad_oracle as O
     threads, host = cpu_threads()
@@ -142,6 +174,8 @@ def cpu_baseline(args, sweep=(8,)):
     rgb, gt, K = [torch.from_numpy(a) for a in O.synth_batch(B, H, W)]
     prev = torch.get_num_threads()
     ref = O.Trainer(params, bufs, weights=w, model=args.model)
+    pts = sorted({t for t in sweep + ((host["cgroup_cpu_quota"],) if host["cgroup_cpu_quota"] else ())
+                  if t < threads}, reverse=True)
     try:
         torch.set_num_threads(threads)
         ref.step(rgb, gt, K)                      # warm-up
@@ -150,28 +184,31 @@ def cpu_baseline(args, sweep=(8,)):
             ref.step(rgb, gt, K)
         dt = time.perf_counter() - t0
         rates = {str(threads): round(B * args.cpu_sample_steps / dt, 4)}
-        for t in sweep:
-            if t >= threads:
-                continue
+        for t in pts:
             torch.set_num_threads(t)
             t1 = time.perf_counter()
-            ref.step(rgb, gt, K)
-            rates[str(t)] = round(B / (time.perf_counter() - t1), 4)
+            for _ in range(args.cpu_sample_steps):
+                ref.step(rgb, gt, K)
+            rates[str(t)] = round(B * args.cpu_sample_steps / (time.perf_counter() - t1), 4)
     finally:
         torch.set_num_threads(prev)
+    best = max(rates, key=lambda k: rates[k])
     return {"value": rates[str(threads)], "unit": "images/s", "cores": threads, "kind": "port",
             "sample": (f"{args.model} bs{B} {H}x{W} f={f} loss weights {args.weights}, fp32 (the reference's only "
                        f"precision), 1 warm-up + {args.cpu_sample_steps} timed train steps of the oracle restatement "
-                       f"(oracle/cad_oracle.py on LibTorch CPU, {threads} threads = one GPU's share of the host's cores; BN "
-                       f"statistics over bs{B}, not bs32)"),
+                       f"(oracle/cad_oracle.py on LibTorch CPU) at the host's {threads} physical cores "
+                       f"(BASELINE.md §3); BN statistics over bs{B}, not bs32"),
             "seconds": round(dt, 2), "threads_sweep_images_per_s": rates,
-            "threads_sweep_note": "one train step per thread count after the timed steps (same weights, same batch)",
+            "best_threads": int(best), "best_images_per_s": rates[best],
+            "threads_sweep_note": (f"{args.cpu_sample_steps} train steps per further thread count after the timed "
+                                   f"steps (same weights, same batch); includes the job's cgroup CPU quota "
+                                   f"({host['cgroup_cpu_quota']}) = one GPU's share of the host"),
             "host": host}
 
 
 def parity_steps(args, cad, dev, steps=10, B=2):
     """SURVEY §8(d) / BASELINE.md §3: `steps` identical train steps on the GPU (the headline's engine)
-    and on the CPU reference path (oracle restatement, fp32, the host's physical cores) from the same
+    and on the CPU reference path (oracle restatement, fp32, the job's cgroup CPU share of the host) from the same
     weights and batch (bs`B` at the benchmark resolution); after step 1 and after step `steps`:
     train-mode prediction max relative error, loss relative error, then the eval-mode prediction
     (BN running statistics) and the computeDepthMetrics abs_rel of both on a held-out batch.
@@ -182,7 +219,8 @@ def parity_steps(args, cad, dev, steps=10, B=2):
     and the trajectories separate; `drift_ratio` = GPU drift / CPU-path drift from fp64."""
     import torch
     from oracle import cad_oracle as O
-    threads, _ = cpu_threads()
+    threads, host = cpu_threads()
+    threads = min(threads, host["cgroup_cpu_quota"] or threads)   # a correctness check: the job's CPU share
     H, W, f = args.height, args.width, args.features
     w = tuple(float(x) for x in args.weights.split(","))
     params = O.init_params(f, seed=42, model=args.model)
@@ -543,6 +581,120 @@ def rccl_unique_id(cad, rank):
     return uid
 
 
+def timed_region(step, steps, warmup, world, dev):
+    """W untimed warm-up steps, then exactly `steps` steps bracketed by a barrier + synchronize on
+    both sides; the max over ranks of the elapsed wall time."""
+    import torch
+    import torch.distributed as dist
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    return elapsed
+
+
+def exchange_report(xs, steps, world):
+    """Per-step gradient-exchange accounting of a timed region (Trainer / ResNetUNet exchange_stats):
+    the communicator's rank count, all-reduces and bytes per step, and the exposed exchange time
+    (compute stream idle between its last backward kernel and the release by the last all-reduce)
+    as the mean over timed steps, max over ranks."""
+    import torch
+    import torch.distributed as dist
+    ex = xs["exposed_ms"] / xs["timed_calls"] if xs.get("timed_calls") else None
+    sp = xs["span_ms"] / xs["timed_calls"] if xs.get("timed_calls") and xs.get("span_ms") is not None else None
+    ex_max = ex
+    if world > 1 and ex is not None:
+        t = torch.tensor([ex], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ex_max = t.item()
+    return {"backend": xs.get("backend"), "comm_size": xs.get("comm_size"),
+            "steps_accounted": xs.get("calls"), "allreduces_per_step": xs["buckets"] / max(1, xs["calls"]),
+            "bytes_allreduced_per_step": xs["bytes"] // max(1, xs["calls"]),
+            "exposed_ms_per_step_rank0": None if ex is None else round(ex, 4),
+            "exposed_ms_per_step_max_rank": None if ex_max is None else round(ex_max, 4),
+            "allreduce_span_ms_per_step_rank0": None if sp is None else round(sp, 4)}
+
+
+def dp_leg(cad, lib, dev, world, rank, comm, pg, config=4, steps=10, warmup=3, B=32, H=480, W=640, f=64):
+    """A BASELINE DP workload at N = world ranks with the job's gradient exchange: configs[3]
+    (config=4: baseline_unet, bf16 GEMMs, full loss, bs32 per GPU -> global bs32*N) or configs[4]
+    (config=5: ResNet-50 encoder + U-Net decoder, bf16; fp8=True: MXFP8 forward conv-GEMMs).
+    Every rank runs it (collectives); rank 0 reports whole-job images/s over the max-over-ranks clock
+    and the exchange accounting."""
+    import torch
+    import torch.distributed as dist
+    from cad_amd import synthetic
+    fp8 = config == "5x8"
+    prev = lib.cad_get_gemm_engine()
+    assert lib.cad_set_gemm_engine(2) == 0
+    try:
+        if config == 4:
+            model = cad.BaselineUNet(3, f, max_depth=10.0, batch=B, height=H, width=W, device=dev.index)
+        else:
+            model = cad.ResNetUNet(batch=B, height=H, width=W, device=dev.index, fp8=fp8)
+        if comm is not None:
+            comm.broadcast_parameters(model, 0)
+        elif pg is not None:
+            dist.broadcast(model.flat_params, 0, group=pg)
+        loss = cad.CombinedDepthLoss(1.0, 0.1, 0.001, 0.01, batch=B, height=H, width=W, device=dev.index)
+        rgb, gt, K = (torch.roll(t, shifts=rank, dims=0).contiguous().to(dev)
+                      for t in synthetic.device_batch(B, H, W, "cpu"))
+        if config == 4:
+            tr = cad.Trainer(model, loss, lr=1e-4, weight_decay=1e-5, grad_clip=1.0, process_group=pg,
+                             communicator=comm)
+            tr.set_exchange_timing(True)
+            step = lambda: tr.train_step(rgb, gt, K)
+            stats = tr.exchange_stats
+            last = lambda: tr.loss5[0].item()
+        else:
+            pred = torch.empty((B, 1, H, W), device=dev)
+            dpred, loss5 = torch.empty_like(pred), torch.zeros(5, device=dev)
+            if comm is not None:
+                comm.set_timing(True)
+                stats = lambda: dict(comm.stats(), backend="libcad RCCL communicator", comm_size=comm.size())
+            else:
+                model.exchange_accounting(True)
+                stats = model.exchange_stats
+            step = lambda: model.train_step(loss, rgb, gt, K, pred=pred, dpred=dpred, loss5=loss5,
+                                            process_group=pg, communicator=comm)
+            last = lambda: loss5[0].item()
+        for _ in range(warmup):
+            step()
+        stats()   # warm-up steps are not accounted
+        elapsed = timed_region(step, steps, 0, world, dev)
+        xs = exchange_report(stats(), steps, world)
+        out = {"workload": (WORKLOADS_DP[config] + f", DP over {world} ranks (global bs{B * world})"),
+               "value": round(B * world * steps / elapsed, 3), "unit": "images/s", "n_gpus": world,
+               "ms_per_step": round(1e3 * elapsed / steps, 3), "steps": steps, "warmup": warmup,
+               "dtype": "fp8+bf16" if fp8 else "bf16", "last_loss": last(), "exchange": xs}
+        if comm is not None:
+            comm.set_timing(False)
+            comm.stats()
+        return out
+    finally:
+        lib.cad_set_gemm_engine(prev)
+
+
+WORKLOADS_DP = {4: "baseline_unet train step, configs[3]: bs32/GPU 480x640 bf16 GEMMs, full loss",
+                5: "ResNet-50 encoder + U-Net decoder train step, configs[4]: bs32/GPU 480x640 bf16 GEMM operands, "
+                   "full loss",
+                "5x8": "ResNet-50 encoder + U-Net decoder train step, configs[4]: bs32/GPU 480x640, forward "
+                       "conv-GEMMs on MXFP8 E4M3 operands (backward bf16), full loss"}
+
+
 def main():
     args = parse()
     import torch
@@ -584,25 +736,34 @@ def main():
         gt = torch.roll(gt, shifts=rank, dims=0).contiguous()
         K = torch.roll(K, shifts=rank, dims=0).contiguous()
 
+    if world > 1:
+        trainer.set_exchange_timing(True)
     for i in range(args.warmup):
         trainer.train_step(rgb, gt, K)
-    torch.cuda.synchronize(dev)
+    xstats = trainer.exchange_stats if world > 1 else None
+    if xstats:
+        xstats()   # warm-up steps are not accounted
     with profiled(lib) as prof:
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for i in range(args.steps):
-            trainer.train_step(rgb, gt, K)
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+        elapsed = timed_region(lambda: trainer.train_step(rgb, gt, K), args.steps, 0, world, dev)
+    exchange = exchange_report(xstats(), args.steps, world) if xstats else None
     last_loss = trainer.loss5[0].item()
+    dp_legs = None
+    if world > 1 and not args.no_extra:
+        # the DP workloads BASELINE names for the multi-GPU runs (configs[3], configs[4]) with the same
+        # exchange; every rank runs them, rank 0 reports
+        del trainer, loss, model
+        torch.cuda.empty_cache()
+        dp_legs = {}
+        for key, cfg in (("config4", 4), ("config5", 5), ("config5_fp8", "5x8")):
+            try:
+                dp_legs[key] = dp_leg(cad, lib, dev, world, rank, comm, pg, config=cfg, B=B, H=H, W=W, f=f)
+                if rank == 0:
+                    log(f"DP leg {key}: {dp_legs[key]}")
+            except Exception as e:   # a failing leg must not hang the others: ranks fail alike (same code)
+                log(f"rank {rank}: DP leg {key} failed: {e}")
+                dp_legs[key] = {"error": str(e)[:500]}
+            gc.collect()   # the leg's model and arena go before the next one is created
+            torch.cuda.empty_cache()
 
     if rank == 0:
         images = B * world * args.steps
@@ -612,8 +773,9 @@ def main():
         step_tflops = (FLOP_PER_IMAGE_480x640_F64 * value / 1e12
                        if (H, W, f, args.model) == (480, 640, 64, "baseline") else None)
         dp, extra, cpu, parity = None, None, None, None
-        del trainer, loss, model
-        torch.cuda.empty_cache()
+        if dp_legs is None:
+            del trainer, loss, model
+            torch.cuda.empty_cache()
         if world == 1 and not args.no_extra:
             extra = {}
             for cfg in (3, 4):
@@ -679,6 +841,9 @@ def main():
             "bf16_workloads": extra,
             "data_path": dp,
         }
+        if world > 1:
+            out["exchange"] = exchange
+            out["dp_workloads"] = dp_legs
         print(json.dumps(out), flush=True)
     comm = None
     if world > 1:

@@ -40,6 +40,12 @@ class AdamOpts(C.Structure):
     _fields_ = [("lr", F), ("beta1", F), ("beta2", F), ("eps", F), ("weight_decay", F)]
 
 
+class CommStats(C.Structure):
+    """cad_comm_stats (cad.h): exchange accounting of the overlapped backward all-reduce."""
+    _fields_ = [("calls", I64), ("timed_calls", I64), ("buckets", I64), ("bytes", I64), ("exposed_ms", C.c_double),
+                ("span_ms", C.c_double)]
+
+
 class ArchiveEntry(C.Structure):
     """cad_archive_entry (cad.h): one tensor / empty submodule of a torch::save archive."""
     _fields_ = [("name", C.c_char_p), ("kind", I), ("dtype", I), ("ndim", I), ("shape", C.c_int64 * 8),
@@ -170,6 +176,8 @@ SIGNATURES = {
     "cad_comm_destroy": (None, [P]),
     "cad_comm_rank": (I, [P]),
     "cad_comm_size": (I, [P]),
+    "cad_comm_set_timing": (I, [P, I]),
+    "cad_comm_stats_read": (I, [P, P]),
     "cad_comm_allreduce": (I, [P, P, I64, I, P]),
     "cad_comm_broadcast": (I, [P, P, I64, I, P]),
     "cad_comm_broadcast_params": (I, [P, P, I, P]),

@@ -139,6 +139,7 @@ struct DoubleConv {
     // apply, bn1 backward, the y1 debug buffer) relaunch the conv GEMM from the input and weights
     // that forward used (the twins on the bf16 engine, the rc_w snapshot on S3)
     bool y1_rc = false;
+    bool y1_rc_ps = false;   // ... and did so on the pre-split kernels (the operands rc1_ops picks)
     void* a1s = nullptr;   // pre-split a1 (gemm_ps.hpp)
     int first_param = 0, last_param = 0;   // [first, last] indices in named_parameters()
     bool has_film() const { return film.p0 >= 0; }
@@ -578,6 +579,7 @@ void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin,
     dc.y1b = ps1 && (!dc.y1_f32 || enc1_bf16);
     dc.y2b = ps;
     dc.y1_rc = rc1_on(h, dc, ps1);
+    dc.y1_rc_ps = dc.y1_rc && ps1;
     if (dc.y1_rc) {   // statistics only; the BN apply recomputes the conv (rc1_on)
         if (!ps1)
             HIPCHK(hipMemcpyAsync(h->rc_w, h->P(dc.c1.pidx), sizeof(float) * (size_t)C * 9 * dc.c1.cin,
@@ -1209,7 +1211,7 @@ int64_t cad_unet_debug_buffer(cad_unet* h, const char* name, float* host, int64_
         // the last forward recomputed enc1.conv1 instead of storing it: run it once more into y1 from
         // the same input and weights (cad_unet_debug_buffer is a test hook; CAD_RC1=0 stores y1)
         DoubleConv& dc = h->enc[0];
-        const bool ps1 = h->fwd_np > 0 && h->x0s && dc.c1.ws;
+        const bool ps1 = dc.y1_rc_ps;   // the operands the forward used (not re-derived: CAD_ENC1PS)
         const cad::Split in_s = ps1 ? sv(h->x0s, h->x0_ld) : cad::Split{};
         const Rc1Ops o = rc1_ops(h, dc, h->x0, h->x0_ld, in_s, ps1);
         cad::RecomputeArgs r;
@@ -1956,9 +1958,9 @@ cad_status cad_op_convT_fwd_bf16(const void* x, int64_t ldx, int xcoff, int cin,
                                  int cout, void* y, int64_t ldy, int ycoff, int B, int H, int W, void* stream) {
     return guard([&] {
         require(cad::gemm_engine() == 2, "the pre-split ConvTranspose runs on the bf16 engine (CAD_GEMM_BF16)");
-        require(x && w && bias && y && cin % 8 == 0 && cout % 8 == 0 && xcoff % 8 == 0 && ldx % 8 == 0 && B > 0 &&
-                    H > 0 && W > 0,
-                "bad arguments (bf16 rows: ldx, xcoff, cin, cout multiples of 8)");
+        require(x && w && bias && y && cin % 8 == 0 && cout % 8 == 0 && xcoff % 8 == 0 && ldx % 8 == 0 &&
+                    ldy % 8 == 0 && ycoff % 8 == 0 && B > 0 && H > 0 && W > 0,
+                "bad arguments (bf16 rows: ldx, xcoff, ldy, ycoff, cin, cout multiples of 8)");
         float* wf = nullptr;
         void* wfs = nullptr;
         HIPCHK(hipMallocAsync((void**)&wf, sizeof(float) * (size_t)cout * 4 * cin, S(stream)));

@@ -22,12 +22,26 @@ namespace cad {
 void set_last_error(const std::string& msg);   // cad_api.cpp: the thread-local cad_last_error() text
 }
 
+// timing events of one backward_allreduce call (cad_comm_set_timing)
+struct CommTimes {
+    hipEvent_t bwd_end = nullptr;    // compute stream: after the last backward stage
+    hipEvent_t released = nullptr;   // compute stream: after its wait for the last all-reduce
+    hipEvent_t ar_start = nullptr;   // comm stream: the first bucket may start
+    hipEvent_t ar_end = nullptr;     // comm stream: after the last all-reduce
+};
+constexpr int kMaxTimedCalls = 256;
+
 struct cad_comm {
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0, device = 0;
     hipStream_t stream = nullptr;            // communication stream
     std::vector<hipEvent_t> ready;           // one per bucket slot: its stages are enqueued
     hipEvent_t done = nullptr;               // every issued all-reduce has completed
+    // exchange accounting (cad_comm_stats_read)
+    bool timing = false;
+    std::vector<CommTimes> times;            // event sets, reused after each read
+    int ntimed = 0;                          // sets recorded since the last read
+    cad_comm_stats acc{};
 };
 
 namespace {
@@ -87,6 +101,16 @@ void staged_backward_allreduce(cad_comm* c, float* g, int ns, Range range, Stage
         DP_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         c->ready.push_back(e);
     }
+    // timing events of this call (cad_comm_set_timing): a fresh set per call until the next read
+    CommTimes* t = nullptr;
+    if (c->timing && c->ntimed < kMaxTimedCalls) {
+        if ((int)c->times.size() <= c->ntimed) {
+            CommTimes n;
+            for (hipEvent_t* e : {&n.bwd_end, &n.released, &n.ar_start, &n.ar_end}) DP_HIP(hipEventCreate(e));
+            c->times.push_back(n);
+        }
+        t = &c->times[(size_t)c->ntimed];
+    }
     int b = 0;
     for (int s = 0; s < ns; ++s) {
         const cad_status st = stage(s);
@@ -95,13 +119,25 @@ void staged_backward_allreduce(cad_comm* c, float* g, int ns, Range range, Stage
             // the bucket's gradients are final once the work enqueued so far on `stream` is done
             DP_HIP(hipEventRecord(c->ready[(size_t)b], S(stream)));
             DP_HIP(hipStreamWaitEvent(c->stream, c->ready[(size_t)b], 0));
+            if (t && b == 0) DP_HIP(hipEventRecord(t->ar_start, c->stream));
             DP_NCCL(ncclAllReduce(g + boff[(size_t)b], g + boff[(size_t)b], (size_t)bcnt[(size_t)b], ncclFloat32,
                                   ncclSum, c->comm, c->stream));
+            c->acc.bytes += 4 * bcnt[(size_t)b];
             ++b;
         }
     }
+    c->acc.buckets += nb;
+    ++c->acc.calls;
+    if (t) {
+        DP_HIP(hipEventRecord(t->ar_end, c->stream));
+        DP_HIP(hipEventRecord(t->bwd_end, S(stream)));
+    }
     DP_HIP(hipEventRecord(c->done, c->stream));
     DP_HIP(hipStreamWaitEvent(S(stream), c->done, 0));   // clip / Adam see the reduced slab
+    if (t) {
+        DP_HIP(hipEventRecord(t->released, S(stream)));
+        ++c->ntimed;
+    }
 }
 
 }  // namespace
@@ -168,6 +204,9 @@ void cad_comm_destroy(cad_comm* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     for (hipEvent_t e : c->ready) (void)hipEventDestroy(e);
+    for (CommTimes& t : c->times)
+        for (hipEvent_t e : {t.bwd_end, t.released, t.ar_start, t.ar_end})
+            if (e) (void)hipEventDestroy(e);
     if (c->done) (void)hipEventDestroy(c->done);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -175,6 +214,34 @@ void cad_comm_destroy(cad_comm* c) {
 
 int cad_comm_rank(const cad_comm* c) { return c ? c->rank : -1; }
 int cad_comm_size(const cad_comm* c) { return c ? c->nranks : -1; }
+
+cad_status cad_comm_set_timing(cad_comm* c, int enable) {
+    return dp_guard([&] {
+        if (!c) throw DpError(CAD_ERR_INVALID, "null communicator");
+        c->timing = enable != 0;
+    });
+}
+
+cad_status cad_comm_stats_read(cad_comm* c, cad_comm_stats* out) {
+    return dp_guard([&] {
+        if (!c || !out) throw DpError(CAD_ERR_INVALID, "null argument");
+        DP_HIP(hipSetDevice(c->device));
+        cad_comm_stats s = c->acc;
+        for (int i = 0; i < c->ntimed; ++i) {
+            const CommTimes& t = c->times[(size_t)i];
+            DP_HIP(hipEventSynchronize(t.released));
+            float exposed = 0.f, span = 0.f;
+            DP_HIP(hipEventElapsedTime(&exposed, t.bwd_end, t.released));
+            DP_HIP(hipEventElapsedTime(&span, t.ar_start, t.ar_end));
+            s.exposed_ms += exposed;
+            s.span_ms += span;
+            ++s.timed_calls;
+        }
+        *out = s;
+        c->acc = cad_comm_stats{};
+        c->ntimed = 0;
+    });
+}
 
 cad_status cad_comm_allreduce(cad_comm* c, float* buf, int64_t count, int op, void* stream) {
     return dp_guard([&] {

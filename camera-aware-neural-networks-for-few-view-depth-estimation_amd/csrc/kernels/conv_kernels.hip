@@ -147,12 +147,6 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_win_bf16p3(GemmArgs a) {
     conv3x3_win_ps_body<R, CW, 4, 1, Epi, 2, 3>(a);
 }
 
-// ... the same tiles with LDS-DMA staging (conv3x3_win_dma_body: 3-stage ring, one workgroup per CU)
-template <int R, int CW, class Epi, bool BN64 = false>
-__global__ __launch_bounds__(256, 1) void k_conv3x3_win_bf16d(GemmArgs a) {
-    conv3x3_win_dma_body<R, CW, BN64 ? 4 : 2, BN64 ? 1 : 2, Epi, 4, 3>(a);
-}
-
 // window-tiled conv3x3 weight gradient (gemm_win.hpp): 64 co x 64 ci x 9 taps per workgroup, split-K
 __global__ __launch_bounds__(256, 2) void k_conv3x3_wgrad_win_s3(GemmArgs a) { conv3x3_wgrad_win_body<3>(a); }
 __global__ __launch_bounds__(256, 2) void k_conv3x3_wgrad_strip_s3(GemmArgs a) { conv3x3_wgrad_strip_body<3>(a); }
@@ -271,15 +265,12 @@ __global__ __launch_bounds__(256, 2) void k_convT_dgrad_bf16pb4(GemmArgs a) {
 }
 // ... with LDS-DMA staging (gemm_dense_dma_body: 3-stage ring)
 __global__ __launch_bounds__(256, 2) void k_convT_fwd_bf16dt(GemmArgs a) {
-    gemm_dense_dma_body<2, 2, 2, 2, false, EpiConvTB16>(a);
-}
-__global__ __launch_bounds__(256, 2) void k_convT_dgrad_bf16db(GemmArgs a) {
-    gemm_dense_dma_body<2, 2, 2, 2, true, EpiStoreB16>(a);
+    gemm_dense_dma_body<2, 2, 2, 2, EpiConvTB16>(a);
 }
 // dense (1x1-conv / im2col) forward GEMMs of the config-5 network on the same DMA body
 template <class Epi>
 __global__ __launch_bounds__(256, 2) void k_dense_bf16d(GemmArgs a) {
-    gemm_dense_dma_body<2, 2, 2, 2, false, Epi>(a);
+    gemm_dense_dma_body<2, 2, 2, 2, Epi>(a);
 }
 template <int WM, int WN, int KB>
 __global__ __launch_bounds__(256) void k_conv3x3_wgrad_bf16p(GemmArgs a) { conv3x3_wgrad_psb<1, WM, WN, 2, 2, KB>(a); }
@@ -497,18 +488,6 @@ WinPick pick_win(int cin, int W, int N) {
     return w;
 }
 int win_blocks(const WinPick& w, int B, int H, int W) { return B * cdiv(H, w.R) * (W / w.CW); }
-// B1 window conv forward / dgrad with LDS-DMA staging (k_conv3x3_win_bf16d): off by default —
-// measured on MI355X at the configs[3] shapes it runs 657-821 TFLOP/s against 894-1047 for the
-// register-staged k_conv3x3_win_bf16p4 (its 3-stage ring takes 132 KB of LDS: one workgroup and one
-// wave per SIMD, against two); CAD_WINDMA=1 selects it (A/B switch)
-bool win_dma() {
-    static const bool on = [] {
-        const char* e = std::getenv("CAD_WINDMA");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
-
 // PS = false: S3 window kernel (fp32 operands, in-loader split); true: B1 on the pre-split twins
 template <bool PS, int R, int CW, class Epi, bool BIG = false, bool N96 = false>
 void launch_win1(const GemmArgs& a, hipStream_t st) {
@@ -516,14 +495,13 @@ void launch_win1(const GemmArgs& a, hipStream_t st) {
     if (a.N % BN) throw std::runtime_error("window conv: N not a multiple of the tile");
     const dim3 grid(win_blocks(WinPick{R, CW}, a.B, a.H, a.W), cdiv(a.N, BN));
     void (*fn)(GemmArgs);
-    const bool dma = BIG && !N96 && win_dma();
     if constexpr (N96) fn = k_conv3x3_win_bf16p3<R, CW, Epi>;
-    else if constexpr (BIG) fn = dma ? k_conv3x3_win_bf16d<R, CW, Epi, BN == 64> : k_conv3x3_win_bf16p4<R, CW, Epi, BN == 64>;
+    else if constexpr (BIG) fn = k_conv3x3_win_bf16p4<R, CW, Epi, BN == 64>;
     else fn = PS ? (void (*)(GemmArgs))k_conv3x3_win_bf16p<R, CW, Epi> : (void (*)(GemmArgs))k_conv3x3_win_s3<R, CW, Epi>;
     if (prof_enabled()) {
         char name[160];
         snprintf(name, sizeof(name), "void cad::k_conv3x3_win_%s<%d, %d, cad::%s%s>(cad::GemmArgs)",
-                 N96 ? "bf16p3" : dma ? "bf16d" : BIG ? "bf16p4" : PS ? "bf16p" : "s3", R, CW,
+                 N96 ? "bf16p3" : BIG ? "bf16p4" : PS ? "bf16p" : "s3", R, CW,
                  Epi::STATS ? "EpiStoreStats" : "EpiStore", Epi::BF16 ? "B16" : "");
         prof_push(name, 2.0 * a.M * a.N * (double)a.K, st);
         hipLaunchKernelGGL(fn, grid, dim3(256), 0, st, a);
@@ -1319,9 +1297,9 @@ void launch_big(void (*fn)(GemmArgs), const char* name, const GemmArgs& a, hipSt
         hipLaunchKernelGGL(fn, grid, dim3(256), 0, st, a);
     }
 }
-// CAD_CONVTDMA bit 1: the bf16 ConvT forward, bit 2: its dgrad on the LDS-DMA dense GEMM.  Measured at
-// configs[3] (4 launches per step): forward 1.47 -> 1.42 ms (default on), dgrad 1.11 (256 x 128 tiles,
-// CAD_BIGT) vs 1.13 ms
+// CAD_CONVTDMA bit 1: the bf16 ConvT forward on the LDS-DMA dense GEMM.  Measured at configs[3] (4
+// launches per step): 1.47 -> 1.42 ms (default on).  (Its up-gather input-gradient form, 1.13 ms
+// against the 256 x 128 tiles' 1.11, was removed in round 5.)
 int convt_dma() {
     static const int m = [] {
         const char* e = std::getenv("CAD_CONVTDMA");
@@ -1376,10 +1354,6 @@ void convT_dgrad_ps(Split g, int cout, Split wm, int cin, float* dx, int B, int 
     const Cfg c = pick_cfg(a.M, a.N);
     const int kb = ps_kb(false, c);
     a.kstages_per_split = cdiv(a.K, kb);
-    if (dx_bf16 && (convt_dma() & 2) && a.N >= 128 && cout % 32 == 0 && a.lda % 8 == 0 && a.a_coff % 8 == 0) {
-        launch_dense_dma(k_convT_dgrad_bf16db, "void cad::k_convT_dgrad_bf16db(cad::GemmArgs)", a, st);
-        return;
-    }
     if (dx_bf16 && (bigt_mask() & 2) && a.N >= 128 && a.M >= 4096) {
         launch_big(k_convT_dgrad_bf16pb4<32>, "void cad::k_convT_dgrad_bf16pb4<32>(cad::GemmArgs)", a, st);
         return;

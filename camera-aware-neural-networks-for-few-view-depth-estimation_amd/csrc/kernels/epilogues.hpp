@@ -85,7 +85,8 @@ struct EpiConvTOut {
     __device__ bool wave_store(const GemmArgs& a, const floatx16 (&acc)[MI][NJ], int mw0, int nw0, float* ldsf) const {
         constexpr int WC = 32 * NJ, RS = WC + 8, CH = WC / 8;   // columns, LDS row stride, 16-B pieces per row
         const int cout = a.N >> 2;
-        if (a.W % 32 != 0 || cout % WC != 0) return false;
+        // 16-byte stores: the row stride and channel offset must keep every piece 16-byte aligned
+        if (a.W % 32 != 0 || cout % WC != 0 || a.ldc % 8 != 0 || a.c_coff % 8 != 0) return false;
         if (nw0 >= a.N) return true;   // N % WC == 0: the wave's columns are wholly in or out
         const int lane = threadIdx.x & 63, h = lane >> 5, c = lane & 31;
         const int q = nw0 / cout, co0 = nw0 - q * cout;

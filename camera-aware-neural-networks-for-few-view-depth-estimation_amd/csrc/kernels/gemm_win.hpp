@@ -1285,148 +1285,18 @@ __device__ __forceinline__ void conv3x3_wgrad_strip_dma_body(const GemmArgs& a) 
         }
 }
 
-// ------------------------------------------------------------------------------------------------
-// B1 window conv forward / dgrad with LDS-DMA staging (round 3): conv3x3_win_ps_body's blocks and
-// (32-channel block, ky) stages, with the operands moved global -> LDS by buffer_load ... lds into a
-// ring of NBUF stages (no staging registers, no ds_write, one barrier per stage; two stages in flight
-// with NBUF = 3).  LDS images are unpadded 64-B rows (32 bf16 channels) — window pixels for A, weight
-// rows per tap for B — whose 16-B chunk c of row w sits at c ^ ((w >> 2) & 3): the source-side swizzle
-// that keeps the ds_read_b128 fragment reads of 16 consecutive rows on disjoint banks.  A DMA
-// wave-instruction fills 16 rows; the window is padded to whole instructions (zero rows: the DMA of an
-// out-of-range offset writes zeros), as are out-of-image halo pixels.
-// ------------------------------------------------------------------------------------------------
-template <int R, int CW, int BN, int NBUF>
-struct WinDGeo {
-    static constexpr int WC = CW + 2;
-    static constexpr int WPIX = R * WC;
-    static constexpr int NIA = (WPIX + 15) / 16;          // A DMA wave-instructions per stage
-    static constexpr int NIB = 3 * BN / 16;               // B: 3 taps x BN rows
-    static constexpr int NI = NIA + NIB;
-    static constexpr int SLOTS = (NI + 3) / 4;
-    static constexpr int WAIT = NI / 4;
-    static constexpr int SA = NIA * 1024, SBT = BN * 64, STAGE = SA + 3 * SBT;
-};
+// LDS row image of the DMA kernels below: unpadded 64-B rows (32 bf16) whose 16-B chunk c of row w sits
+// at c ^ ((w >> 2) & 3), the source-side swizzle that keeps the ds_read_b128 fragment reads of 16
+// consecutive rows on disjoint banks.
 __device__ __forceinline__ int wind_off(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
-
-template <int R, int CW, int WM, int WN, class Epi, int MI, int NBUF>
-__device__ __forceinline__ void conv3x3_win_dma_body(const GemmArgs& a) {
-    constexpr int NJ = 2;
-    constexpr int BM = 32 * MI * WM, BN = 32 * NJ * WN;
-    static_assert(BM == R * CW, "tile");
-    static_assert(NBUF == 3, "ring: stage s + 2 reuses the slot of stage s - 1");
-    using G = WinDGeo<R, CW, BN, NBUF>;
-    __shared__ __attribute__((aligned(1024))) char lds[NBUF * G::STAGE];
-
-    const int tid = threadIdx.x;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    const int wm = wave / WN, wn = wave % WN;
-    const TileId tile = xcd_tile();
-    const int nbx = a.W / CW, nby = (a.H + R - 1) / R;
-    const int tx = tile.x % nbx, t2 = tile.x / nbx, ty = t2 % nby, b = t2 / nby;
-    const int y0 = ty * R, x0 = tx * CW, n0 = tile.y * BN;
-    const int H = a.H, W = a.W, cin = a.a_cin;
-    const int S = 3 * (cin / 32);
-
-    const int rowb = (int)a.lda * 2;
-    const int64_t pbase = ((int64_t)b * H + y0 - 1) * W + x0 - 1;
-    const int64_t pb = pbase > 0 ? pbase : 0;
-    const DmaRsrc rsa = dma_rsrc(reinterpret_cast<const char*>(a.A) + (pb * a.lda + a.a_coff) * 2);
-    const DmaRsrc rsb = dma_rsrc(reinterpret_cast<const char*>(a.Bm) + ((int64_t)n0 * a.ldb + a.b_coff) * 2);
-    const int rowbb = (int)a.ldb * 2;
-
-    // this wave's DMA slots (instruction j = wave + 4 t): lane -> row 16 j' + lane / 4, LDS chunk lane % 4
-    const int lrow = lane >> 2, lch = lane & 3;
-    int sj[G::SLOTS], soff[G::SLOTS], swr[G::SLOTS];
-#pragma unroll
-    for (int t = 0; t < G::SLOTS; ++t) {
-        const int j = wave + 4 * t;
-        sj[t] = j < G::NI ? j : -1;
-        if (j < G::NIA) {
-            const int w = 16 * j + lrow;
-            const int r = w / G::WC, c = w - r * G::WC;
-            const int x = x0 - 1 + c;
-            const bool ok = w < G::WPIX && (unsigned)x < (unsigned)W;
-            swr[t] = ok ? r : -(1 << 28);
-            soff[t] = (int)((r * (int64_t)W + c + (pbase - pb)) * rowb) + ((lch ^ ((w >> 2) & 3)) << 4);
-        } else {
-            const int jb = j - G::NIA;                 // tap jb / (BN / 16), rows 16 (jb % (BN / 16)) ..
-            const int tap = jb / (BN / 16), row = 16 * (jb - tap * (BN / 16)) + lrow;
-            swr[t] = tap;
-            soff[t] = row * rowbb + tap * cin * 2 + ((lch ^ ((row >> 2) & 3)) << 4);
-        }
-    }
-    auto issue = [&](int stage, int buf) {   // stage = 3 cb + ky
-        const int cb = stage / 3, ky = stage - 3 * cb;
-        char* base = lds + buf * G::STAGE;
-        const int adda = ky * W * rowb + cb * 64;
-        const int addb = 3 * ky * cin * 2 + cb * 64;
-#pragma unroll
-        for (int t = 0; t < G::SLOTS; ++t) {
-            const int j = sj[t];
-            if (j < 0) continue;
-            if (j < G::NIA) {
-                const int y = y0 - 1 + ky + swr[t];
-                dma16(rsa, base + j * 1024, (unsigned)y < (unsigned)H ? (uint32_t)(soff[t] + adda) : kOOB);
-            } else {
-                const int jb = j - G::NIA;
-                dma16(rsb, base + G::SA + jb * 1024, (uint32_t)(soff[t] + addb));
-            }
-        }
-    };
-
-    int wpix[MI];
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-        const int p = wm * 32 * MI + i * 32 + (lane & 31);
-        const int r = p / CW;
-        wpix[i] = r * G::WC + (p - r * CW);
-    }
-    floatx16 acc[MI][NJ];
-    acc_zero(acc);
-    const int h = lane >> 5;
-    auto compute = [&](int buf) {
-        const char* sa = lds + buf * G::STAGE;
-        const char* sb = sa + G::SA;
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx)
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                bf16x8 fa[MI][1], fb[NJ][1];
-#pragma unroll
-                for (int j = 0; j < NJ; ++j) {
-                    const int row = wn * 32 * NJ + j * 32 + (lane & 31);
-                    fb[j][0] = *reinterpret_cast<const bf16x8*>(sb + kx * G::SBT + wind_off(row, 2 * q + h));
-                }
-#pragma unroll
-                for (int i = 0; i < MI; ++i)
-                    fa[i][0] = *reinterpret_cast<const bf16x8*>(sa + wind_off(wpix[i] + kx, 2 * q + h));
-                s3_mfma<1>(acc, fa, fb);
-            }
-    };
-
-    if (S > 0) issue(0, 0);
-    if (S > 1) issue(1, 1);
-    int buf = 0;
-    for (int s = 0; s < S; ++s) {
-        if (s + 1 < S) wgd_wait_barrier<G::WAIT>();
-        else wgd_wait_barrier<0>();
-        if (s + 2 < S) issue(s + 2, buf == 0 ? NBUF - 1 : buf - 1);
-        compute(buf);
-        buf = buf == NBUF - 1 ? 0 : buf + 1;
-    }
-    __syncthreads();   // the ring is the epilogue's BN scratch
-    win_epilogue<WM, WN, MI, NJ, CW, Epi>(a, acc, tile.x, n0, b, y0, x0, reinterpret_cast<float*>(lds));
-}
 
 // ------------------------------------------------------------------------------------------------
 // Dense bf16 GEMM C[m][n] = sum_k A[m][k] B[n][k] with LDS-DMA staging (round 4): the ConvT forward
-// (A = the low-res twin, K = cin) and, with UPG, the ConvT input gradient (A row m gathers the four
-// high-res pixels (2y + dy, 2x + dx) of dL/dup: K = (q = (dy, dx), co), cout % 32 == 0 so a 32-deep
-// stage stays in one q).  The register-staged gemm_body_ps keeps one stage in flight with 8 MFMAs per
+// (A = the low-res twin, K = cin) and config 5's dense forward GEMMs.  The register-staged gemm_body_ps keeps one stage in flight with 8 MFMAs per
 // wave and stage (128 x 128): its load latency is exposed (the ConvT GEMMs ran at 430-630 TFLOP/s).
 // Here a ring of 3 stages keeps two in flight with no staging registers (48 KB of LDS for 128 x 128:
-// three workgroups per CU).  LDS rows are unpadded 64-B (32 bf16) with the source-side chunk swizzle of
-// conv3x3_win_dma_body (wind_off); a DMA wave-instruction fills 16 rows.  M / N tails and K tails
+// three workgroups per CU).  LDS rows are unpadded 64-B (32 bf16) with the source-side chunk swizzle
+// (wind_off); a DMA wave-instruction fills 16 rows.  M / N tails and K tails
 // (K % 8 == 0) read the out-of-range offset: zeros.
 // ------------------------------------------------------------------------------------------------
 template <int BM, int BN>
@@ -1435,7 +1305,7 @@ struct DenseDGeo {
     static constexpr int SLOTS = (NI + 3) / 4, WAIT = NI / 4;
     static constexpr int SA = BM * 64, STAGE = (BM + BN) * 64, NBUF = 3;
 };
-template <int WM, int WN, int MI, int NJ, bool UPG, class Epi>
+template <int WM, int WN, int MI, int NJ, class Epi>
 __device__ __forceinline__ void gemm_dense_dma_body(const GemmArgs& a) {
     constexpr int BM = 32 * MI * WM, BN = 32 * NJ * WN;
     using G = DenseDGeo<BM, BN>;
@@ -1448,13 +1318,7 @@ __device__ __forceinline__ void gemm_dense_dma_body(const GemmArgs& a) {
     const int m0 = tile.x * BM, n0 = tile.y * BN;
     const int K = a.K, S = (K + 31) / 32;
     const int rowa = (int)a.lda * 2, rowb = (int)a.ldb * 2;
-    const int W2 = 2 * a.W;
-    // A base: row m0 (UPG: its high-res pixel (2y, 2x)); offsets relative to it
-    auto hp = [&](int m) {   // high-res pixel of low-res row m, q = 0
-        const int x = m % a.W, t = m / a.W, y = t % a.H, b = t / a.H;
-        return ((int64_t)b * (2 * a.H) + 2 * y) * W2 + 2 * x;
-    };
-    const int64_t abase = UPG ? hp(min(m0, a.M - 1)) : (int64_t)m0;
+    const int64_t abase = m0;
     const DmaRsrc rsa = dma_rsrc(reinterpret_cast<const char*>(a.A) + (abase * a.lda + a.a_coff) * 2);
     const DmaRsrc rsb = dma_rsrc(reinterpret_cast<const char*>(a.Bm) + ((int64_t)n0 * a.ldb + a.b_coff) * 2);
 
@@ -1469,19 +1333,14 @@ __device__ __forceinline__ void gemm_dense_dma_body(const GemmArgs& a) {
         sch[t] = 8 * gch;   // k offset of the lane's piece within the stage
         if (j < G::NIA) {
             const int m = m0 + r;
-            soff[t] = m < a.M ? (int)((UPG ? hp(m) - abase : (int64_t)r) * rowa) + gch * 16 : -1;
+            soff[t] = m < a.M ? r * rowa + gch * 16 : -1;
         } else {
             soff[t] = n0 + r < a.N ? r * rowb + gch * 16 : -1;
         }
     }
-    const int cout = a.a_cin;   // (UPG) K = 4 cout
     auto issue = [&](int stage, int buf) {
         const int k0 = stage * 32;
-        int adda = k0 * 2;
-        if constexpr (UPG) {
-            const int q = k0 / cout, co = k0 - q * cout;
-            adda = ((q >> 1) * W2 + (q & 1)) * rowa + co * 2;
-        }
+        const int adda = k0 * 2;
         char* base = lds + buf * G::STAGE;
 #pragma unroll
         for (int t = 0; t < G::SLOTS; ++t) {

@@ -448,6 +448,21 @@ class Communicator:
     def size(self) -> int:
         return self.lib.cad_comm_size(self.h)
 
+    def set_timing(self, on=True):
+        """Time every backward_allreduce from now on (cad_comm_set_timing): exposed exchange time and
+        all-reduce span per call, read by stats()."""
+        check(self.lib.cad_comm_set_timing(self.h, int(bool(on))), "cad_comm_set_timing")
+        return self
+
+    def stats(self) -> dict:
+        """Exchange accounting since the last read (cad_comm_stats_read; waits for the recorded events):
+        calls, buckets, bytes all-reduced, and over the timed calls the summed exposed time (last
+        backward kernel -> compute stream released by the last all-reduce) and all-reduce span."""
+        s = _abi.CommStats()
+        check(self.lib.cad_comm_stats_read(self.h, C.byref(s)), "cad_comm_stats_read")
+        return {"calls": s.calls, "timed_calls": s.timed_calls, "buckets": s.buckets, "bytes": s.bytes,
+                "exposed_ms": s.exposed_ms, "span_ms": s.span_ms}
+
     def allreduce(self, t: torch.Tensor, op="sum"):
         check(self.lib.cad_comm_allreduce(self.h, _ptr(t), t.numel(), {"sum": 0, "max": 1}[op], _stream(self.device)),
               "cad_comm_allreduce")
@@ -497,6 +512,36 @@ class Trainer:
         self.bucket_elems = int(bucket_mb * (1 << 20) / 4)
         self.pred = None
         self.loss5 = torch.zeros(5, dtype=torch.float32, device=model.device)
+        self.timing = False
+        self._events = []
+        self._xstats = {"calls": 0, "buckets": 0, "bytes": 0}
+
+    def set_exchange_timing(self, on=True):
+        """Account the data-parallel exchange of the following steps (exchange_stats())."""
+        self.timing = bool(on)
+        if self.comm is not None:
+            self.comm.set_timing(on)
+        return self
+
+    def exchange_stats(self) -> dict:
+        """Gradient-exchange accounting since the last read: the communicator's rank count, bytes
+        all-reduced, buckets, and the exposed (non-overlapped) exchange time summed over timed steps
+        (libcad communicator: cad_comm_stats_read; torch.distributed: CUDA events around the wait)."""
+        if self.comm is not None:
+            out = self.comm.stats()
+            out.update(backend="libcad RCCL communicator", comm_size=self.comm.size())
+            return out
+        if self.pg is None:
+            return {"backend": None, "comm_size": 1, "calls": 0, "timed_calls": 0, "buckets": 0, "bytes": 0,
+                    "exposed_ms": 0.0, "span_ms": None}
+        import torch.distributed as dist
+        torch.cuda.synchronize(self.model.device)
+        out = dict(self._xstats, timed_calls=len(self._events),
+                   exposed_ms=sum(a.elapsed_time(b) for a, b in self._events), span_ms=None,
+                   backend=f"torch.distributed ({dist.get_backend(self.pg)})", comm_size=dist.get_world_size(self.pg))
+        self._events = []
+        self._xstats = {"calls": 0, "buckets": 0, "bytes": 0}
+        return out
 
     def train_step(self, rgb, gt, K):
         m = self.model
@@ -520,7 +565,17 @@ class Trainer:
         elif self.world > 1:
             bk = GradBucketer(m.flat_grads, m.num_stages, self.bucket_elems, self.pg)
             m.backward(self.dpred, on_stage=bk.on_stage)
+            ev = None
+            if self.timing:   # exposed exchange time: after the last backward kernel -> after the wait
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
             bk.wait()
+            if ev is not None:
+                ev[1].record()
+                self._events.append(ev)
+            self._xstats["calls"] += 1
+            self._xstats["buckets"] += len(bk.buckets)
+            self._xstats["bytes"] += 4 * sum(hi - lo for lo, hi in bk.buckets)
             clip_grad_norm_(m, self.grad_clip, prescale=1.0 / self.world)
         else:
             m.backward(self.dpred)
@@ -688,10 +743,40 @@ class ResNetUNet:
             import torch.distributed as dist
             bk = GradBucketer(self.flat_grads, self.num_stages, int(bucket_mb * (1 << 20) / 4), process_group)
             self.backward(dpred, on_stage=bk.on_stage)
+            acct = getattr(self, "_xacct", None)   # exchange_accounting(): events around the wait
+            if acct is not None:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
             bk.wait()
+            if acct is not None:
+                ev[1].record()
+                acct["events"].append(ev)
+                acct["calls"] += 1
+                acct["buckets"] += len(bk.buckets)
+                acct["bytes"] += 4 * sum(hi - lo for lo, hi in bk.buckets)
+                acct["pg"] = process_group
             return dist.get_world_size(process_group)
         self.backward(dpred)
         return 1
+
+    def exchange_accounting(self, on=True):
+        """torch.distributed exchange of train_step(process_group=...): count buckets / bytes and time
+        the exposed wait from now on (exchange_stats()); a libcad Communicator accounts on its own
+        (Communicator.set_timing / stats)."""
+        self._xacct = {"events": [], "calls": 0, "buckets": 0, "bytes": 0, "pg": None} if on else None
+        return self
+
+    def exchange_stats(self) -> dict:
+        import torch.distributed as dist
+        a = getattr(self, "_xacct", None) or {"events": [], "calls": 0, "buckets": 0, "bytes": 0, "pg": None}
+        torch.cuda.synchronize(self.device)
+        out = {"calls": a["calls"], "timed_calls": len(a["events"]), "buckets": a["buckets"], "bytes": a["bytes"],
+               "exposed_ms": sum(x.elapsed_time(y) for x, y in a["events"]), "span_ms": None,
+               "backend": f"torch.distributed ({dist.get_backend(a['pg'])})" if a["pg"] is not None else None,
+               "comm_size": dist.get_world_size(a["pg"]) if a["pg"] is not None else 1}
+        if getattr(self, "_xacct", None) is not None:
+            self.exchange_accounting(True)
+        return out
 
     def clip_grad_norm_(self, max_norm: float, prescale: float = 1.0):
         check(self._f("clip_grad_norm")(self.h, float(max_norm), float(prescale), _stream(self.device)), "clip")

@@ -254,6 +254,23 @@ cad_status cad_grad_allreduce(cad_unet* h, cad_comm* c, void* stream);
  * while the remaining dgrad/wgrad kernels do; `stream` finally waits for every all-reduce. */
 cad_status cad_unet_backward_allreduce(cad_unet* h, cad_comm* c, const float* ddepth, int64_t bucket_elems,
                                        void* stream);
+/* Exchange accounting of the *_backward_allreduce calls (new; no reference counterpart).  With timing
+ * on, each call records HIP timing events: on the compute stream after its last backward kernel and
+ * again once that stream has waited for the last all-reduce (the difference is the exposed, i.e.
+ * non-overlapped, exchange time), and on the communicator's stream around its all-reduces (the span
+ * from the first bucket's start to the last bucket's end).  cad_comm_stats waits for the recorded
+ * events, returns the sums since the last read (or since timing was enabled) and resets them.  At most
+ * 256 calls are timed between reads (later ones are counted in `calls`/`bytes` only). */
+typedef struct cad_comm_stats {
+    int64_t calls;          /* backward_allreduce calls */
+    int64_t timed_calls;    /* calls whose events were recorded */
+    int64_t buckets;        /* all-reduces issued */
+    int64_t bytes;          /* bytes all-reduced (fp32 SUM, in place) */
+    double exposed_ms;      /* sum over timed calls: last backward kernel -> compute stream released */
+    double span_ms;         /* sum over timed calls: first all-reduce start -> last all-reduce end */
+} cad_comm_stats;
+cad_status cad_comm_set_timing(cad_comm* c, int enable);
+cad_status cad_comm_stats_read(cad_comm* c, cad_comm_stats* out);
 /* the bucket plan (host only): consecutive backward stages [stage_off, +stage_cnt) grouped greedily
  * into contiguous buckets of >= bucket_elems floats (the last takes the rest).  Writes up to nstages
  * buckets (nullable outputs); returns the bucket count, or -1 on bad input. */

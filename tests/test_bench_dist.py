@@ -69,7 +69,7 @@ def test_bench_two_ranks_one_gpu():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--exchange", "torch", "--steps", "2", "--warmup", "1", "--batch", "2", "--height", "64",
-           "--width", "64", "--features", "8", "--no-extra", "--no-cpu-baseline"]
+           "--width", "64", "--features", "8", "--no-cpu-baseline"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -79,3 +79,18 @@ def test_bench_two_ranks_one_gpu():
     assert out["value"] > 0 and out["ms_per_step"] > 0 and out["scaling"] == "weak"
     assert "torch.distributed" in out["config"]["gradient_exchange"]
     assert out["last_loss"] == out["last_loss"]   # finite
+    # exchange accounting of the timed steps (what the driver's first multi-GPU run reports)
+    n_flat = out["config"]["params"]
+    x = out["exchange"]
+    assert x["comm_size"] == 2 and x["steps_accounted"] == 2 and "torch.distributed" in x["backend"]
+    assert x["allreduces_per_step"] >= 1 and x["bytes_allreduced_per_step"] >= 4 * n_flat
+    assert x["exposed_ms_per_step_rank0"] is not None and x["exposed_ms_per_step_rank0"] >= 0
+    assert x["exposed_ms_per_step_max_rank"] >= x["exposed_ms_per_step_rank0"] - 1e-9
+    # the DP workloads BASELINE names for N > 1 (configs[3], configs[4] bf16 and MXFP8), same exchange
+    legs = out["dp_workloads"]
+    assert set(legs) == {"config4", "config5", "config5_fp8"}
+    for key, leg in legs.items():
+        assert "error" not in leg, (key, leg)
+        assert leg["n_gpus"] == 2 and leg["value"] > 0 and leg["last_loss"] == leg["last_loss"]
+        assert leg["exchange"]["comm_size"] == 2 and leg["exchange"]["steps_accounted"] == leg["steps"]
+        assert leg["exchange"]["bytes_allreduced_per_step"] > 0

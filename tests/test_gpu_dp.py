@@ -51,9 +51,19 @@ def test_single_rank_communicator_matches_plain(cad, dev, oracle):
             comm.broadcast_parameters(m)
         tr = cad.Trainer(m, loss, lr=1e-4, weight_decay=1e-5, grad_clip=1.0, communicator=comm if use_comm else None,
                          bucket_mb=0.5)   # 0.5 MB buckets: several buckets at f=16
+        if use_comm:   # exchange accounting (bench.py's N > 1 "exchange" block) must not change the step
+            tr.set_exchange_timing(True)
         losses = [tr.train_step(rgb, gt, K).clone() for _ in range(3)]
         torch.cuda.synchronize()
         out[use_comm] = (m.flat_params.clone(), torch.stack(losses), tr.pred.clone(), m.last_grad_norm())
+        if use_comm:
+            xs = tr.exchange_stats()
+            assert xs["comm_size"] == 1 and xs["calls"] == 3 and xs["timed_calls"] == 3
+            assert xs["bytes"] == 3 * 4 * m.n_flat or xs["bytes"] >= 3 * 4 * m.count_parameters()
+            assert xs["buckets"] >= 3 * 2   # several buckets per step at 0.5 MB
+            assert xs["exposed_ms"] >= 0 and xs["span_ms"] >= 0
+            again = tr.exchange_stats()   # read resets
+            assert again["calls"] == 0 and again["timed_calls"] == 0 and again["bytes"] == 0
         del tr, m, loss
     assert torch.equal(out[True][0], out[False][0])
     assert torch.equal(out[True][1], out[False][1])
