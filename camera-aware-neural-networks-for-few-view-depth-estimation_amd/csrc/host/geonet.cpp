@@ -980,7 +980,8 @@ cad_status cad_op_pcl(const float* u, const float* camn, const float* g, const f
 // test hook: copies a buffer of the last step to the host (NHWC rows; int32 buffers bit-copied).
 //   "cat<l>" [M][2C] decoder concat, "dcat<l>" its gradient, "x<l>" decoder output, "u<l>" ConvT output,
 //   "z<l>" encoder CBAM input; CBAM decisions of encoder ("e") / decoder ("d") block l:
-//   "amax<e|d><l>" [B][C] argmax pixel of the channel max-pool, "sidx<e|d><l>" [M] argmax channel
+//   "amax<e|d><l>" [B][C] argmax pixel of the channel max-pool, "sidx<e|d><l>" [M] argmax channel;
+//   "y1<e|d><l>" / "y2<e|d><l>" [M][C] the block's pre-BN conv outputs (the values BN normalised)
 // returns the element count (host == nullptr: count only), -1 if unknown
 int64_t cad_geonet_debug_buffer(cad_geonet* h, const char* name, float* host, int64_t numel) {
     if (!h || !name) return -1;
@@ -999,6 +1000,12 @@ int64_t cad_geonet_debug_buffer(cad_geonet* h, const char* name, float* host, in
         if (b.cb0 < 0) return -1;
         if (key[0] == 'a') { src = b.A.amax; cnt = (int64_t)B * b.A.C; }
         else { src = b.A.sidx; cnt = h->Ml(l, B); }
+    } else if (key == "y1e" || key == "y2e" || key == "y1d" || key == "y2d") {
+        const bool enc = key.back() == 'e';
+        if (!enc && l > h->nl - 2) return -1;
+        const GBlock& b = enc ? h->enc[l] : h->dec[l].blk;
+        src = key[1] == '1' ? b.y1 : b.y2;
+        cnt = h->Ml(l, B) * h->Cl(l);
     } else if (key == "cat" && l < h->nl - 1) { src = h->cat[l]; cnt = 2 * h->Ml(l, B) * h->Cl(l); }
     else if (key == "dcat" && l < h->nl - 1) { src = h->dcat[l]; cnt = 2 * h->Ml(l, B) * h->Cl(l); }
     else if (key == "x" && l < h->nl - 1) { src = h->dec[l].x; cnt = h->Ml(l, B) * h->Cl(l); }

@@ -843,8 +843,9 @@ class GeometryAwareNetwork(ResNetUNet):
         return int(self._f("num_batches_tracked")(self.h, int(film)))
 
     def debug_buffer(self, name: str) -> torch.Tensor:
-        """Test hook: a buffer of the last step as NHWC rows ("cat<l>", "dcat<l>", "x<l>", "u<l>", "z<l>";
-        int32: the CBAM decisions "amax<e|d><l>", "sidx<e|d><l>")."""
+        """Test hook: a buffer of the last step as NHWC rows ("cat<l>", "dcat<l>", "x<l>", "u<l>", "z<l>",
+        the pre-BN conv outputs "y1<e|d><l>", "y2<e|d><l>"; int32: the CBAM decisions "amax<e|d><l>",
+        "sidx<e|d><l>")."""
         n = int(self._f("debug_buffer")(self.h, name.encode(), None, 0))
         if n < 0:
             raise KeyError(name)

@@ -101,6 +101,43 @@ def unet_bn_blocks(model="baseline"):
     return enc + [(f"dec{l}", f"dec{l + 1}.conv.", l) for l in range(4)]
 
 
+def geo_bn_blocks(model):
+    """(geonet debug-buffer suffix, oracle DoubleConv prefix, level) of every FiLM DoubleConv of the
+    geometry-aware family (cad_geonet_debug_buffer "y1<suffix>" / "y2<suffix>")."""
+    from oracle import cad_oracle as O
+    nl, enc = O._geo_names(model)
+    return ([("e0", "enc1.", 0)] + [(f"e{l}", f"{enc[l]}.conv.", l) for l in range(1, nl)] +
+            [(f"d{l}", f"dec{l + 1}.conv.", l) for l in range(nl - 1)])
+
+
+def relu_decisions_from(y, gamma, beta, B, h, w, C, dev):
+    """sign(bn(y)) exactly as the BN-apply kernel evaluates it (see gpu_relu_decisions): (B, C, h, w) bool."""
+    import numpy as np
+    import torch
+    eps = float(np.float32(1e-5))
+    y = y[: B * h * w * C].to(dev).double().reshape(B * h * w, C)
+    mu32 = y.mean(0).float()
+    inv = (1.0 / torch.sqrt(y.var(0, unbiased=False) + eps)).float()
+    sc = gamma.float().to(dev) * inv
+    sh = (beta.double().to(dev) - mu32.double() * sc.double()).float()   # fma(-mean, scale, beta)
+    z = y * sc.double() + sh.double()
+    return (z > 0).reshape(B, h, w, C).permute(0, 3, 1, 2).contiguous().cpu()
+
+
+def geo_relu_decisions(net, params, f, B, H, W, model, dev=None):
+    """The ReLU decisions of a geometry-aware net's last train-mode forward, for cad_oracle.RELU_FORCE,
+    rebuilt from its stored pre-BN conv outputs like gpu_relu_decisions."""
+    import torch
+    dev = dev or torch.device("cpu")
+    masks = {}
+    for sfx, pre, l in geo_bn_blocks(model):
+        C, h, w = f << l, H >> l, W >> l
+        for k in ("1", "2"):
+            masks[pre + "bn" + k] = relu_decisions_from(net.debug_buffer(f"y{k}{sfx}"), params[pre + "bn" + k + ".weight"],
+                                                        params[pre + "bn" + k + ".bias"], B, h, w, C, dev)
+    return masks
+
+
 def gpu_relu_decisions(net, params, f, B, H, W, model="baseline", dev=None):
     """The ReLU decisions of `net`'s last train-mode forward, for cad_oracle.RELU_FORCE.
 

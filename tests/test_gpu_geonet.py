@@ -15,7 +15,7 @@ import os
 import pytest
 import torch
 
-from conftest import GOLDEN, max_rel_err
+from conftest import GOLDEN, geo_relu_decisions, max_rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -180,12 +180,13 @@ def test_geonet_wider_step_vs_oracle(cad, dev, oracle, model, f, B, H, W, engine
     of fp64 depending on the summation order (both GPU engines agree with each other to 3%).  The
     kernels themselves are pinned on well-conditioned inputs by test_op_cbam_vs_autograd /
     test_op_pcl_vs_autograd (1e-5); here the five-level net is held to 3x the two fp32 oracle runs'
-    own deviation (bulk p99.9, max and 1 - cosine), the six-level net to a bulk and max within 5e-2 of
-    fp64 (or 3x the fp32 runs') and cosine >= 0.9995 (measured worst: 2.4e-2 on dec2.conv.bn1.bias,
-    identical on both GPU engines: the BN statistics both engines take from the same epilogue partial
-    sums put a ReLU decision on the other side of zero than fp64 does — one flipped element moves a
-    level's gradients by ~1e-2; cosine 0.99988 worst) — a wiring error (a wrong buffer, level or
-    channel offset) moves gradients by O(1) and their cosine well below that."""
+    own deviation (bulk p99.9, max and 1 - cosine), the six-level net to the U-Net's floors: bulk within
+    5e-3 of fp64 (or 3x the fp32 runs'), cosine >= 0.9999.  Both run with the GPU's ReLU decisions
+    imposed on the oracle (round 5; cad_geonet_debug_buffer "y1/y2<e|d><l>" -> RELU_FORCE): before,
+    a few pre-activations within rounding of zero flipped between the GPU and fp64 and moved whole BN
+    gradients (dec2.conv.bn1.bias 2.4e-2 from fp64, floor 5e-2); with the decisions pinned the worst
+    six-level tensor is 1.3e-3 (dec1.pcl.fc_transform.bias, fp32 witnesses 4.9e-3), cosine
+    >= 0.999999 — a wiring error (a wrong buffer, level or channel offset) moves gradients by O(1)."""
     lib = cad.load_library()
     prev = lib.cad_get_gemm_engine()
     lib.cad_set_gemm_engine({"s3": 1, "f32": 0}[engine])
@@ -218,6 +219,11 @@ def _wider(cad, dev, oracle, model, f, B, H, W):
     # from fp64 at the deepest levels (4e-5 measured) — and the gradients compared tightly.
     oracle.GEO_DEBUG["force"] = cbam_decisions(net, model, oracle)
     oracle.GEO_DEBUG["gap"] = []
+    # ... and with the GPU run's ReLU decisions (cad_oracle.RELU_FORCE, rebuilt from its stored pre-BN
+    # conv outputs as in tests/test_gpu_model.py): a pre-activation within rounding of 0 is a tie
+    # either fp32 path may break either way, and one such element moves a BN bias gradient whose
+    # per-pixel terms cancel by a percent of its scale
+    oracle.RELU_FORCE.update(geo_relu_decisions(net, params, f, B, H, W, model))
     try:
         r32 = oracle.Trainer(params, bufs, model=model).forward_backward(rgb, gt, K)
         nt = torch.get_num_threads()
@@ -230,6 +236,7 @@ def _wider(cad, dev, oracle, model, f, B, H, W):
     finally:
         gaps = oracle.GEO_DEBUG.pop("gap", [])
         oracle.GEO_DEBUG.pop("force", None)
+        oracle.RELU_FORCE.clear()
     assert gaps and max(gaps) < 1e-4, max(gaps)
     assert max_rel_err(pred.cpu(), r64[0]) < max(1e-4, 3 * max_rel_err(r32[0], r64[0]))
     worst, bad = [], []
@@ -241,7 +248,7 @@ def _wider(cad, dev, oracle, model, f, B, H, W):
             # tests/test_gpu_film.py::_ill_conditioned); pinned by the reference fixtures above
             continue
         if model == "geo":
-            ok, st = _grad_ok(grads[n], g64, [g32, g32b], bulk_floor=5e-2, cos_floor=0.9995)
+            ok, st = _grad_ok(grads[n], g64, [g32, g32b], bulk_floor=5e-3)
         else:
             ok, st = _grad_ok(grads[n], g64, [g32, g32b])
         worst.append((st, n))
