@@ -554,11 +554,25 @@ Rc1Ops rc1_ops(cad_unet* h, const DoubleConv& dc, const float* in, int64_t ldin,
     return {in, ldin, h->rc_w};
 }
 
+// the next level's max-pool written by an encoder block's bn2 pass (bn_relu_pool_fwd)
+struct PoolOut {
+    float* pool;      // fp32 pooled output (nullptr: only its twin is read)
+    uint8_t* idx;     // argmax codes
+    void* pool_s;     // pooled twin (bf16 engine)
+};
+// CAD_BNPOOL=0: the encoder bn2 apply and the max-pool as separate passes (A/B measurements;
+// bit-identical, tests/test_gpu_headfuse.py)
+bool bn_pool_on() {
+    static const bool on = env_flag("CAD_BNPOOL", 1) != 0;
+    return on;
+}
+
 // head_pred != nullptr: the block's bn2 + ReLU feeds the depth head directly (level-0 fusion): sig
-// and head_pred are written, out is not
+// and head_pred are written, out is not.  pool != nullptr: the block's bn2 pass also writes the next
+// level's max-pool
 void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin, cad::Split in_s, int B, float* out,
                      int64_t ldo, int ocoff, cad::Split out_s, hipStream_t st, bool out_f32 = true,
-                     float* head_pred = nullptr) {
+                     float* head_pred = nullptr, const PoolOut* pool = nullptr) {
     const int l = dc.level, Hh = h->Hl(l), Ww = h->Wl(l), C = dc.c1.cout;
     const int64_t M = h->Ml(l, B);
     const bool tr = h->train;
@@ -622,6 +636,13 @@ void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin,
         return;
     }
     const bool twin = ps && out_s.p;
+    if (pool) {
+        if (ocoff != 0 || (twin && out_s.coff != 0)) throw std::runtime_error("bn_relu_pool_fwd: offset outputs");
+        cad::bn_relu_pool_fwd(dc.y2, C, dc.b2.scale, dc.b2.shift, (out_f32 || !twin) ? out : nullptr, ldo,
+                              twin ? const_cast<void*>(out_s.p) : nullptr, out_s.ld, B, Hh, Ww, dc.y2b, pool->pool,
+                              pool->idx, pool->pool_s, st);
+        return;
+    }
     cad::bn_relu_fwd(dc.y2, C, dc.b2.scale, dc.b2.shift, (out_f32 || !twin) ? out : nullptr, ldo, ocoff, M, st,
                      twin ? const_cast<void*>(out_s.p) : nullptr, out_s.ld, out_s.coff, dc.y2b);
 }
@@ -673,21 +694,32 @@ void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth
         x0s = sv(h->x0s, h->x0_ld);
     }
     // on the bf16 engine the encoder outputs are written only as the concat twin: the max-pool reads
-    // it (the decoder conv1 and its gradients read it anyway)
-    double_conv_fwd(h, h->enc[0], h->x0, h->x0_ld, x0s, B, h->cat[0], 2 * f, 0, sv(h->cats[0], 2 * f), st, !ps);
+    // it (the decoder conv1 and its gradients read it anyway).  By default each encoder block's bn2 pass
+    // writes the next level's max-pool as well (bn_relu_pool_fwd)
+    auto pool_of = [&](int l) {   // the max-pool into level l; pre-split GEMMs read only the pooled twin
+        const bool ptwin = ps && h->pools[l];
+        return PoolOut{ptwin ? nullptr : h->pool[l], h->pidx[l], ptwin ? h->pools[l] : nullptr};
+    };
+    const bool fuse_pool = bn_pool_on();
+    PoolOut po = pool_of(1);
+    double_conv_fwd(h, h->enc[0], h->x0, h->x0_ld, x0s, B, h->cat[0], 2 * f, 0, sv(h->cats[0], 2 * f), st, !ps, nullptr,
+                    fuse_pool ? &po : nullptr);
     for (int l = 1; l <= 4; ++l) {
         const int Cp = h->Cl(l - 1);
-        // pre-split GEMMs read only the pooled twin (enc conv1 and its weight gradient)
-        const bool ptwin = ps && h->pools[l];
-        cad::maxpool_fwd(ps ? static_cast<const float*>(h->cats[l - 1]) : h->cat[l - 1], 2 * Cp, Cp, B, h->Hl(l - 1),
-                         h->Wl(l - 1), ptwin ? nullptr : h->pool[l], h->pidx[l], st, ptwin ? h->pools[l] : nullptr, ps);
+        if (!fuse_pool) {
+            const PoolOut p = pool_of(l);
+            cad::maxpool_fwd(ps ? static_cast<const float*>(h->cats[l - 1]) : h->cat[l - 1], 2 * Cp, Cp, B, h->Hl(l - 1),
+                             h->Wl(l - 1), p.pool, p.idx, st, p.pool_s, ps);
+        }
         const cad::Split pin = sv(h->pools[l], Cp);
-        if (l < 4)
+        if (l < 4) {
+            po = pool_of(l + 1);
             double_conv_fwd(h, h->enc[l], h->pool[l], Cp, pin, B, h->cat[l], 2 * h->Cl(l), 0,
-                            sv(h->cats[l], 2 * h->Cl(l)), st, !ps);
-        else
+                            sv(h->cats[l], 2 * h->Cl(l)), st, !ps, nullptr, fuse_pool ? &po : nullptr);
+        } else {
             double_conv_fwd(h, h->enc[4], h->pool[4], Cp, pin, B, h->a2_bott, h->Cl(4), 0, sv(h->botts, h->Cl(4)), st,
                             false);
+        }
     }
     h->head_fused = head_fusion_on() && cad::head_fusable(f);
     for (int l = 3; l >= 0; --l) {

@@ -134,10 +134,12 @@ __global__ __launch_bounds__(256, 3) void k_conv3x3_win_bf16p(GemmArgs a) {
     conv3x3_win_ps_body<R, CW, R * CW == 128 ? 2 : 4, R * CW == 128 ? 2 : 1, Epi>(a);
 }
 // ... with 4 x 2 blocks of 32 x 32 per wave: 256 x 128 tiles (N % 128 == 0; BN64 = false) or
-// 512 x 64 tiles (N == 64)
+// 512 x 64 tiles (N == 64).  Blocks at most 16 pixels wide (levels 3-4 of 480 x 640) run the same
+// tile as 8 x 4 blocks of 16 x 16 (v_mfma_f32_16x16x32_bf16): measured on MI355X (tools/winlab.py,
+// configs[3] shapes) 4-6 % faster there, 1-6 % slower on the wider blocks of levels 0-2.
 template <int R, int CW, class Epi, bool BN64 = false>
 __global__ __launch_bounds__(256, 2) void k_conv3x3_win_bf16p4(GemmArgs a) {
-    conv3x3_win_ps_body<R, CW, BN64 ? 4 : 2, BN64 ? 1 : 2, Epi, 4>(a);
+    conv3x3_win_ps_body<R, CW, BN64 ? 4 : 2, BN64 ? 1 : 2, Epi, 4, 2, (CW <= 16) || (CAD_WIN16 != 0)>(a);
 }
 
 // ... 256 x 96 tiles (2 x 3 blocks of 32 x 32 per wave, four waves down M) for N % 96 == 0: the 96 and

@@ -548,6 +548,63 @@ struct BnTilePartials {
     }
 };
 
+// The same partials for 16 x 16 accumulator blocks (v_mfma_f32_16x16x32_bf16: column lane & 15, rows
+// 4 (lane >> 4) + reg): NB16 column blocks of 16 per wave; the four lanes of a column merge by
+// lane ^ 16 and lane ^ 32, then waves and the tile as above.
+template <int NB16>
+struct BnTilePartials16 {
+    float sh[NB16], d1[NB16], d2[NB16];
+    float cnt;
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int j = 0; j < NB16; ++j) sh[j] = d1[j] = d2[j] = 0.f;
+        cnt = 0.f;
+    }
+    __device__ __forceinline__ void shift(int j, float v) { sh[j] = v; }
+    __device__ __forceinline__ void add(int j, float v, bool valid) {
+        const float d = valid ? v - sh[j] : 0.f;
+        d1[j] += d;
+        d2[j] = fmaf(d, d, d2[j]);
+        if (j == 0) cnt += valid ? 1.f : 0.f;
+    }
+    template <int WM, int WN>
+    __device__ __forceinline__ void finish(const GemmArgs& a, float* lds, int tile_x, int n0) {
+        constexpr int BN = 16 * NB16 * WN;
+        const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+        const int wm = wave / WN, wn = wave % WN;
+#pragma unroll
+        for (int j = 0; j < NB16; ++j) {
+            float n = cnt, mean = 0.f, m2 = 0.f;
+            if (n > 0.f) {
+                const float q = d1[j] / n;
+                mean = sh[j] + q;
+                m2 = fmaxf(d2[j] - d1[j] * q, 0.f);
+            }
+            chan_merge(n, mean, m2, __shfl_xor(n, 16), __shfl_xor(mean, 16), __shfl_xor(m2, 16));
+            chan_merge(n, mean, m2, __shfl_xor(n, 32), __shfl_xor(mean, 32), __shfl_xor(m2, 32));
+            if (lane < 16) {
+                float* r = lds + (wm * BN + wn * 16 * NB16 + j * 16 + lane) * 3;
+                r[0] = n; r[1] = mean; r[2] = m2;
+            }
+        }
+        __syncthreads();
+        for (int c = tid; c < BN; c += 256) {
+            float n = 0.f, mean = 0.f, m2 = 0.f;
+#pragma unroll
+            for (int w = 0; w < WM; ++w) {
+                const float* r = lds + (w * BN + c) * 3;
+                chan_merge(n, mean, m2, r[0], r[1], r[2]);
+            }
+            const int nn = n0 + c;
+            if (nn < a.N) {
+                a.stats[(int64_t)tile_x * 2 * a.N + nn] = n * mean;
+                a.stats[(int64_t)tile_x * 2 * a.N + a.N + nn] = m2;
+            }
+            if (n0 == 0 && c == 0) a.stats[(int64_t)gridDim.x * 2 * a.N + tile_x] = n;
+        }
+    }
+};
+
 template <class Epi>
 __device__ __forceinline__ const float* epi_row_base(const GemmArgs& a, int m0, int z) {
     if constexpr (is_structured<Epi>::value) return a.C;   // unused by structured epilogues

@@ -197,6 +197,73 @@ __device__ __forceinline__ void win_epilogue(const GemmArgs& a, const floatx16 (
     if constexpr (Epi::STATS && (CAD_XP_WIN & 2) == 0) bnp.template finish<WM, WN>(a, lds, tile_lin, n0);
 }
 
+// The same epilogue for 16 x 16 accumulator blocks (v_mfma_f32_16x16x32_bf16): a wave's MB x NB
+// blocks; block (i, j) register q of a lane is output row 16 i + 4 (lane >> 4) + q, column
+// 16 j + (lane & 15) of the wave's sub-tile.
+template <int WM, int WN, int MB, int NB, int CW, class Epi>
+__device__ __forceinline__ void win_epilogue16(const GemmArgs& a, const floatx4 (&acc)[MB][NB], int tile_lin, int n0,
+                                               int b, int y0, int x0, float* lds) {
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int wm = wave / WN, wn = wave % WN;
+    BnTilePartials16<NB> bnp;
+    if constexpr (Epi::STATS) {
+        bnp.init();
+#pragma unroll
+        for (int j = 0; j < NB; ++j) bnp.shift(j, acc[0][j][0]);
+    }
+    constexpr int ES = Epi::BF16 ? 2 : 4;
+    const int64_t ldc4 = a.ldc * ES;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const float*>(
+        reinterpret_cast<const char*>(a.C) + ((((int64_t)b * a.H + y0) * a.W + x0) * a.ldc + a.c_coff) * ES));
+    [[maybe_unused]] __amdgpu_buffer_rsrc_t rs2;
+    [[maybe_unused]] int64_t ldc2b = 0;
+    if constexpr (Epi::SPLIT) {
+        ldc2b = a.ldc2 * 2;
+        rs2 = make_rsrc(reinterpret_cast<const float*>(static_cast<const char*>(a.C2) +
+                                                       (((int64_t)b * a.H + y0) * a.W + x0) * ldc2b));
+    }
+#pragma unroll
+    for (int i = 0; i < MB; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const int n = n0 + wn * 16 * NB + j * 16 + (lane & 15);
+            const int mr = wm * 16 * MB + i * 16 + 4 * (lane >> 4);   // 4 rows mr..mr+3: same r
+            const int r = mr / CW, c = mr - r * CW;
+            const bool ok = n < a.N && y0 + r < a.H;
+            float v[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = acc[i][j][q];
+            if constexpr (Epi::BF16) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] = (float)(__bf16)v[q];
+            }
+            if constexpr (Epi::SPLIT) {
+                if (n >= a.split_n) {   // uniform per 16-column block (host: split_n % 32 == 0)
+                    const uint32_t lo2 =
+                        ok ? (uint32_t)((r * (int64_t)a.W + c) * ldc2b + (int64_t)(n - a.split_n) * 2) : kOOB;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, (__bf16)v[q]), rs2,
+                                                              lo2 + (uint32_t)(q * ldc2b), 0, 0);
+                    continue;
+                }
+            }
+            const uint32_t lo = ok ? (uint32_t)((r * (int64_t)a.W + c) * ldc4 + (int64_t)n * ES) : kOOB;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if constexpr (Epi::BF16)
+                    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, (__bf16)v[q]), rs,
+                                                          lo + (uint32_t)(q * ldc4), 0, 0);
+                else
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[q]), rs,
+                                                          lo + (uint32_t)(q * ldc4), 0, 0);
+                if constexpr (Epi::STATS) bnp.add(j, v[q], y0 + r < a.H);
+            }
+        }
+    if constexpr (Epi::STATS) bnp.template finish<WM, WN>(a, lds, tile_lin, n0);
+}
+
 // blocks: gridDim.x = B * ceil(H / R) * (W / CW) output blocks (XCD-aware order), gridDim.y = N tiles
 template <int NP, int R, int CW, int WM, int WN, class Epi>
 __device__ __forceinline__ void conv3x3_win_body(const GemmArgs& a) {
@@ -318,7 +385,13 @@ struct WinPsGeo {
 // MFMA: the 128 x 128 tile's LDS reads cap its MFMA rate near one half (B1 has one product per k step).
 // NJ = 3 (with MI = 2, WM = 4, WN = 1): 256 x 96 tiles for the 96 / 192-channel levels of the
 // reference's production width (train_config_production.yaml: init_features 96).
-template <int R, int CW, int WM, int WN, class Epi, int MI = 2, int NJ = 2>
+// M16: the same tile on v_mfma_f32_16x16x32_bf16 (2 MI x 2 NJ blocks of 16 x 16 per wave, one 32-deep
+// k step per tap): the same LDS image, fragment reads and MFMA cycles per FLOP; the chip holds a
+// higher clock on this shape under load (MI355X_MICROARCH.md, DVFS give-back item 7).
+#ifndef CAD_WIN16
+#define CAD_WIN16 0
+#endif
+template <int R, int CW, int WM, int WN, class Epi, int MI = 2, int NJ = 2, bool M16 = (CAD_WIN16 != 0)>
 __device__ __forceinline__ void conv3x3_win_ps_body(const GemmArgs& a) {
     constexpr int BM = 32 * MI * WM, BN = 32 * NJ * WN;
     static_assert(BM == R * CW, "tile");
@@ -367,16 +440,25 @@ __device__ __forceinline__ void conv3x3_win_ps_body(const GemmArgs& a) {
     }
     auto bact = [&](int jj) { return 256 * (jj + 1) <= G::NTB || tid + 256 * jj < G::NTB; };
 
-    int wpix[MI];
+    constexpr int MR = M16 ? 2 * MI : MI;   // A fragment row blocks per wave (32 or 16 rows)
+    int wpix[MR];
 #pragma unroll
-    for (int i = 0; i < MI; ++i) {
-        const int p = wm * 32 * MI + i * 32 + (lane & 31);
+    for (int i = 0; i < MR; ++i) {
+        const int p = M16 ? wm * 32 * MI + i * 16 + (lane & 15) : wm * 32 * MI + i * 32 + (lane & 31);
         const int r = p / CW;
         wpix[i] = r * G::WC + (p - r * CW);
     }
 
-    floatx16 acc[MI][NJ];
-    acc_zero(acc);
+    floatx16 acc[M16 ? 1 : MI][M16 ? 1 : NJ];
+    floatx4 acc4[M16 ? 2 * MI : 1][M16 ? 2 * NJ : 1];
+    if constexpr (M16) {
+#pragma unroll
+        for (int i = 0; i < 2 * MI; ++i)
+#pragma unroll
+            for (int j = 0; j < 2 * NJ; ++j) acc4[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    } else {
+        acc_zero(acc);
+    }
     uint4 ra[G::NVA], rb[3 * G::JB];
     int cb = 0, ky = 0;
     auto load = [&]() {
@@ -408,18 +490,36 @@ __device__ __forceinline__ void conv3x3_win_ps_body(const GemmArgs& a) {
                 if (bact(jj)) *reinterpret_cast<uint4*>(lds + G::SA + t * G::SBT + blds[jj]) = rb[t * G::JB + jj];
     };
     auto compute = [&]() {
+        if constexpr (M16) {
 #pragma unroll
-        for (int kx = 0; kx < 3; ++kx)
+            for (int kx = 0; kx < 3; ++kx) {
+                bf16x8 fb[2 * NJ];
 #pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                bf16x8 fa[MI][1], fb[NJ][1];
+                for (int j = 0; j < 2 * NJ; ++j)
+                    fb[j] = *reinterpret_cast<const bf16x8*>(lds + G::SA + kx * G::SBT +
+                                                             (wn * 32 * NJ + j * 16 + (lane & 15)) * G::LDK + (lane >> 4) * 8);
 #pragma unroll
-                for (int j = 0; j < NJ; ++j) s3_frag<BN, 32, 1>(lds + G::SA + kx * G::SBT, wn * 32 * NJ + j * 32, q, fb[j]);
+                for (int i = 0; i < 2 * MI; ++i) {
+                    const bf16x8 fa = *reinterpret_cast<const bf16x8*>(lds + (wpix[i] + kx) * G::LDK + (lane >> 4) * 8);
 #pragma unroll
-                for (int i = 0; i < MI; ++i)
-                    fa[i][0] = *reinterpret_cast<const bf16x8*>(lds + (wpix[i] + kx) * G::LDK + q * 16 + (lane >> 5) * 8);
-                s3_mfma<1>(acc, fa, fb);
+                    for (int j = 0; j < 2 * NJ; ++j)
+                        acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[j], acc4[i][j], 0, 0, 0);
+                }
             }
+        } else {
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    bf16x8 fa[MI][1], fb[NJ][1];
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) s3_frag<BN, 32, 1>(lds + G::SA + kx * G::SBT, wn * 32 * NJ + j * 32, q, fb[j]);
+#pragma unroll
+                    for (int i = 0; i < MI; ++i)
+                        fa[i][0] = *reinterpret_cast<const bf16x8*>(lds + (wpix[i] + kx) * G::LDK + q * 16 + (lane >> 5) * 8);
+                    s3_mfma<1>(acc, fa, fb);
+                }
+        }
     };
 
     if (S > 0) {
@@ -437,7 +537,10 @@ __device__ __forceinline__ void conv3x3_win_ps_body(const GemmArgs& a) {
             __syncthreads();
         }
     }
-    win_epilogue<WM, WN, MI, NJ, CW, Epi>(a, acc, tile.x, n0, b, y0, x0, reinterpret_cast<float*>(lds));
+    if constexpr (M16)
+        win_epilogue16<WM, WN, 2 * MI, 2 * NJ, CW, Epi>(a, acc4, tile.x, n0, b, y0, x0, reinterpret_cast<float*>(lds));
+    else
+        win_epilogue<WM, WN, MI, NJ, CW, Epi>(a, acc, tile.x, n0, b, y0, x0, reinterpret_cast<float*>(lds));
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -218,6 +218,13 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
 // x_bf16: x is a bf16 twin (rows of ldx elements; requires out_split)
 void maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float* out, uint8_t* idx,
                  hipStream_t st, void* out_split = nullptr, bool x_bf16 = false);
+// an encoder block's bn2 + ReLU fused with the next level's MaxPool2d(2): writes the block output
+// (fp32 rows `out` (ldo) and/or its 1-plane twin `os` (ldos), channel offset 0) and the pooled output
+// (fp32 `pool` and/or its twin `pool_split`, dense ld C) with the argmax codes, exactly what
+// bn_relu_fwd followed by maxpool_fwd writes (the bf16 engine pools the twin's values)
+void bn_relu_pool_fwd(const float* y, int C, const float* scale, const float* shift, float* out, int64_t ldo,
+                      void* os, int64_t ldos, int B, int H, int W, bool y_bf16, float* pool, uint8_t* idx,
+                      void* pool_split, hipStream_t st);
 void maxpool_bwd(const float* dout, const uint8_t* idx, int C, int B, int H, int W, float* dx,
                  int64_t lddx, hipStream_t st);
 void rgb_to_nhwc4(const float* rgb, float* out, int B, int H, int W, hipStream_t st);

@@ -323,13 +323,33 @@ void colsum_finalize(const double* part, int S, int C, float* dst, float scale, 
 // ------------------------------------------------------------------------------------------
 // BatchNorm forward
 // ------------------------------------------------------------------------------------------
-__global__ void k_bn_stats(const double* tot, int C, int64_t count, const float* gamma, const float* beta,
-                           float* rmean, float* rvar, float momentum, float eps, float* mean,
-                           float* invstd, float* scale, float* shift) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    const double mu = tot[c] / (double)count;
-    double var = tot[C + c] / (double)count - mu * mu;
+// The slice sums of both columns of a channel (part[s][0][c], part[s][1][c]: k_colreduce<2>'s
+// layout) in k_colfinal's order, then the batch statistics, running statistics and the apply
+// coefficients (scale = gamma * invstd, shift = beta - mean * scale)
+__global__ void k_bn_final(const double* part, int S, int C, int64_t count, const float* gamma, const float* beta,
+                           float* rmean, float* rvar, float momentum, float eps, float* mean, float* invstd,
+                           float* scale, float* shift) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    const int sy = threadIdx.y;
+    double s0 = 0.0, s1 = 0.0;
+    if (c < C)
+#pragma unroll 4
+        for (int i = sy; i < S; i += kFinalLanes) {
+            s0 += part[(int64_t)i * 2 * C + c];
+            s1 += part[(int64_t)i * 2 * C + C + c];
+        }
+    __shared__ double red[2][kFinalLanes][64];
+    red[0][sy][threadIdx.x] = s0;
+    red[1][sy][threadIdx.x] = s1;
+    __syncthreads();
+    if (sy != 0 || c >= C) return;
+    s0 = s1 = 0.0;
+    for (int y = 0; y < kFinalLanes; ++y) {
+        s0 += red[0][y][threadIdx.x];
+        s1 += red[1][y][threadIdx.x];
+    }
+    const double mu = s0 / (double)count;
+    double var = s1 / (double)count - mu * mu;
     if (var < 0.0) var = 0.0;
     const float is = (float)(1.0 / sqrt(var + (double)eps));
     mean[c] = (float)mu;
@@ -348,13 +368,17 @@ void bn_fwd_finalize(const float* tile_part, int rows, int C, int64_t count, con
                      const float* beta, float* run_mean, float* run_var, float momentum, float eps,
                      double* scratch, float* mean, float* invstd, float* scale, float* shift,
                      hipStream_t st) {
-    double* tot = scratch;
     double* part = scratch + 2 * C;
     // tile_part: [rows][2][C] (S, M2) then [rows] counts (BnTilePartials); the variance below is
-    // E[y^2] - mu^2 in fp64 over per-tile sums y^2 rebuilt from the shifted partials
-    const int S = launch_colreduce<2>(OpBnTile{tile_part, tile_part + (int64_t)rows * 2 * C, C}, rows, C, part, st);
-    launch_colfinal(part, S, 2 * C, tot, nullptr, 1.f, st);
-    hipLaunchKernelGGL(k_bn_stats, dim3(cdiv(C, 64)), dim3(64), 0, st, tot, C, count, gamma, beta,
+    // E[y^2] - mu^2 in fp64 over per-tile sums y^2 rebuilt from the shifted partials.  Slices of about
+    // one tile row per thread (a few thousand tile rows: colsum_slices' 256-row slices left each thread
+    // a serial chain of 16-64 loads, ~50 us per launch); at most colsum_slices(count) of them, which the
+    // callers' scratch holds (it is sized for the BN backward's 2-output reduction over `count` rows)
+    const int C4 = C >> 2, CX = std::min(C4, 64), RY = std::max(1, 256 / CX);
+    const int S = (int)std::max<int64_t>(1, std::min<int64_t>(colsum_slices(count), cdiv(rows, RY)));
+    launch_colreduce_slices<2>(OpBnTile{tile_part, tile_part + (int64_t)rows * 2 * C, C}, rows, C, S, cdiv(rows, S),
+                               part, st);
+    hipLaunchKernelGGL(k_bn_final, dim3(cdiv(C, 64)), dim3(64, kFinalLanes), 0, st, part, S, C, count, gamma, beta,
                        run_mean, run_var, momentum, eps, mean, invstd, scale, shift);
 }
 
@@ -647,6 +671,85 @@ __global__ void k_maxpool_fwd(const float* __restrict__ x, int64_t ldx, int C, i
         *reinterpret_cast<uchar4*>(idx + (int64_t)op * C + c) = make_uchar4(arg[0], arg[1], arg[2], arg[3]);
     }
 }
+// An encoder block's bn2 + ReLU and the MaxPool2d(2) of the level below in one pass (round 5): one
+// thread per (pooled pixel, 4-channel group) applies the BN affine + ReLU to the four pixels of its
+// window (k_bn_relu_fwd_rows' arithmetic), writes them — the fp32 skip half (`out`) and/or its bf16
+// twin (NP = 1) — and pools the values the separate max-pool would have read back: the twin's bf16
+// values on the bf16 engine (NP = 1: k_maxpool_fwd<1, true>), the fp32 ones otherwise,
+// with its comparison (first in scan order wins ties, NaN propagates).  Saves re-reading the skip half.
+template <int NP, bool YB>
+__global__ __launch_bounds__(256) void k_bn_relu_pool_fwd(const float* __restrict__ y, int C,
+                                                         const float* __restrict__ scale,
+                                                         const float* __restrict__ shift, float* __restrict__ out,
+                                                         int64_t ldo, char* __restrict__ os, int64_t ldos, int H,
+                                                         int W, float* __restrict__ pout, uint8_t* __restrict__ idx,
+                                                         char* __restrict__ pos, int64_t n4) {
+    const uint32_t C4 = (uint32_t)C >> 2, Ho = (uint32_t)H >> 1, Wo = (uint32_t)W >> 1;   // n4 < 2^31 (host)
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (uint32_t)n4; i += gridDim.x * blockDim.x) {
+        const uint32_t op = i / C4;
+        const int c = (int)(i - op * C4) * 4;
+        const uint32_t xo = op % Wo, t = op / Wo;
+        const uint32_t yo = t % Ho, b = t / Ho;
+        const int64_t p00 = ((int64_t)b * H + 2 * yo) * W + 2 * xo;
+        const float4 s = *reinterpret_cast<const float4*>(scale + c);
+        const float4 sh = *reinterpret_cast<const float4*>(shift + c);
+        float best[4];
+        uint8_t arg[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t p = p00 + (k >> 1) * W + (k & 1);
+            const float4 v = load4<YB>(y, p * C + c);
+            float4 o;
+            o.x = bn_relu1(v.x, s.x, sh.x);
+            o.y = bn_relu1(v.y, s.y, sh.y);
+            o.z = bn_relu1(v.z, s.z, sh.z);
+            o.w = bn_relu1(v.w, s.w, sh.w);
+            if (out) *reinterpret_cast<float4*>(out + p * ldo + c) = o;
+            float va[4] = {o.x, o.y, o.z, o.w};
+            if constexpr (NP == 1) {   // the twin, and the values the bf16 engine's max-pool reads from it
+                const auto sp = split_np<1>(o);
+                *reinterpret_cast<uint2*>(os + (p * ldos + c) * 2) = sp.p[0];
+                va[0] = __uint_as_float(sp.p[0].x << 16);
+                va[1] = __uint_as_float(sp.p[0].x & 0xffff0000u);
+                va[2] = __uint_as_float(sp.p[0].y << 16);
+                va[3] = __uint_as_float(sp.p[0].y & 0xffff0000u);
+            }
+            if (k == 0) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) best[e] = va[e];
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (va[e] > best[e] || isnan(va[e])) { best[e] = va[e]; arg[e] = (uint8_t)k; }
+            }
+        }
+        const float4 o = make_float4(best[0], best[1], best[2], best[3]);
+        if (pout) *reinterpret_cast<float4*>(pout + (int64_t)op * C + c) = o;
+        if constexpr (NP == 1) {
+            if (pos) split4_store<1>(pos, C, 0, op, c, o);
+        }
+        *reinterpret_cast<uchar4*>(idx + (int64_t)op * C + c) = make_uchar4(arg[0], arg[1], arg[2], arg[3]);
+    }
+}
+void bn_relu_pool_fwd(const float* y, int C, const float* scale, const float* shift, float* out, int64_t ldo,
+                      void* os, int64_t ldos, int B, int H, int W, bool y_bf16, float* pool, uint8_t* idx,
+                      void* pool_split, hipStream_t st) {
+    const int64_t n4 = (int64_t)B * (H / 2) * (W / 2) * C / 4;
+    if (n4 >= ((int64_t)1 << 31)) throw std::runtime_error("bn_relu_pool_fwd: tensor too large for 32-bit indexing");
+    if (H % 2 || W % 2 || C % 4 || !idx || (!out && !os)) throw std::runtime_error("bn_relu_pool_fwd: bad arguments");
+    const int np = os ? split_planes() : 0;
+    if (np != 0 && np != 1) throw std::runtime_error("bn_relu_pool_fwd: 1-plane twins only");
+    if (pool_split && np != 1) throw std::runtime_error("bn_relu_pool_fwd: a pooled twin needs the block's twin");
+    char* o = static_cast<char*>(os);
+    char* po = static_cast<char*>(pool_split);
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(ew_blocks(n4)), dim3(256), 0, st, y, C, scale, shift, out, ldo, o, ldos, H, W, pool,
+                           idx, po, n4);
+    };
+    if (np == 1) y_bf16 ? go(k_bn_relu_pool_fwd<1, true>) : go(k_bn_relu_pool_fwd<1, false>);
+    else y_bf16 ? go(k_bn_relu_pool_fwd<0, true>) : go(k_bn_relu_pool_fwd<0, false>);
+}
+
 void maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float* out, uint8_t* idx,
                  hipStream_t st, void* out_split, bool x_bf16) {
     const int64_t n4 = (int64_t)B * (H / 2) * (W / 2) * C / 4;
