@@ -213,6 +213,10 @@ struct cad_unet {
     // forward used (S3 engine; the bf16 engine's weight twin is already such a copy)
     double* rc_part = nullptr;
     float* rc_w = nullptr;
+    // per-tile BN-backward sums of bn1 from conv2's input-gradient epilogue (conv3x3_dgrad_*_bnsums):
+    // the same buffer as rc_part (tiles of >= 128 rows at any level fit in its 64-row level-0 sizing;
+    // never live at the same time: each is reduced right after the GEMM that writes it)
+    int64_t part_cap = 0;
     // stage grad ranges
     std::vector<std::pair<int64_t, int64_t>> stage_range;
 
@@ -428,7 +432,8 @@ void layout(cad_unet* h, Arena& a) {
     h->slab_cap = std::min<int64_t>(sl, (int64_t)64 << 20);
     h->slab = a.f(h->slab_cap);
     // recomputed enc1.conv1: tiles of at least 64 rows (the tile height follows the engine at run time)
-    h->rc_part = a.d((h->Ml(0, B) + 63) / 64 * 2 * h->Cl(0));
+    h->part_cap = (h->Ml(0, B) + 63) / 64 * 2 * h->Cl(0);
+    h->rc_part = a.d(h->part_cap);
     h->rc_w = a.f((int64_t)h->enc[0].c1.cout * 9 * h->enc[0].c1.cin);
     // buffers table (running stats), named_buffers() order (parameter order of the BNs)
     h->bufs.clear();
@@ -763,13 +768,25 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     cad::bn_relu_bwd(g, ldg, gcoff, dc.y2, C, dc.b2.mean, dc.b2.invstd, dc.b2.scale, dc.b2.shift, h->P(dc.b2.widx), M,
                      h->dscr, dc.b2.coef, h->G(dc.b2.widx), h->G(dc.b2.bidx), ps ? nullptr : dY, st, nullptr, 1,
                      ps ? dYs : nullptr, true, dc.y2b, head, g_bf16, pool);
-    // conv2: wgrad, dgrad
+    // conv2: wgrad, dgrad.  On the S3 engine (plain blocks) the dgrad's window epilogue also forms
+    // bn1's backward sums over the dL/da1 it stores (conv3x3_dgrad_bnsums), so bn1's backward skips its
+    // column-reduction pass over (dL/da1, y1); CAD_BNSUMS=0 keeps that pass (A/B; the same fp64 sums in
+    // another order, tests/test_gpu_headfuse.py).  (Measured slower on the bf16 engine: conv_kernels.hip)
+    static const bool bnsums = env_flag("CAD_BNSUMS", 1) != 0;
+    int bn1_tiles = 0;
+    cad::BnSums bs;
+    if (bnsums && !ps && !dc.has_film() && !dc.y1_rc && h->rc_part) {
+        bs.y = dc.y1; bs.ldy = C; bs.y_bf16 = dc.y1b;
+        bs.mean = dc.b1.mean; bs.invstd = dc.b1.invstd; bs.scale = dc.b1.scale; bs.shift = dc.b1.shift;
+        bs.part = h->rc_part; bs.part_cap = h->part_cap;
+    }
     if (ps) {
         cad::conv3x3_wgrad_ps(sv(dYs, C), C, sv(dc.a1s, C), C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
         cad::conv3x3_dgrad_ps(sv(dYs, C), C, sv(dc.c2.wds, 9 * C), C, dA1, C, B, Hh, Ww, st, true);
     } else {
         cad::conv3x3_wgrad(dY, C, dc.a1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
-        cad::conv3x3_dgrad(dY, C, dc.c2.wd, C, dA1, C, B, Hh, Ww, st);
+        if (bs.part) bn1_tiles = cad::conv3x3_dgrad_bnsums(dY, C, dc.c2.wd, C, dA1, C, B, Hh, Ww, bs, st);
+        if (!bn1_tiles) cad::conv3x3_dgrad(dY, C, dc.c2.wd, C, dA1, C, B, Hh, Ww, st);
     }
     // FiLM: dgamma/dbeta per (sample, channel); the ReLU sees dA1 * gamma (folded into bn_relu_bwd).  By
     // default the FiLM sums come from bn1's backward reduction pass over the same (dA1, y1) (round 4;
@@ -804,7 +821,8 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
         cad::bn_relu_bwd(dA1, C, 0, dc.y1, C, dc.b1.mean, dc.b1.invstd, dc.b1.scale, dc.b1.shift, h->P(dc.b1.widx), M,
                          h->dscr, dc.b1.coef, h->G(dc.b1.widx), h->G(dc.b1.bidx), dy1_f32 ? dY : nullptr, st,
                          dc.has_film() ? dc.film.gam : nullptr, HW, ps ? dYs : nullptr, true, dc.y1b, nullptr, ps,
-                         nullptr, ff ? dc.film.dgam : nullptr, ff ? dc.film.dbet : nullptr);
+                         nullptr, ff ? dc.film.dgam : nullptr, ff ? dc.film.dbet : nullptr,
+                         bn1_tiles ? h->rc_part : nullptr, bn1_tiles);
     }
     if (dc.has_film()) cad::film_mlp_bwd(film_view(h, dc), h->camn, B, st);
     // conv1: wgrad, dgrad

@@ -504,7 +504,8 @@ void launch_win1(const GemmArgs& a, hipStream_t st) {
         char name[160];
         snprintf(name, sizeof(name), "void cad::k_conv3x3_win_%s<%d, %d, cad::%s%s>(cad::GemmArgs)",
                  N96 ? "bf16p3" : BIG ? "bf16p4" : PS ? "bf16p" : "s3", R, CW,
-                 Epi::STATS ? "EpiStoreStats" : "EpiStore", Epi::BF16 ? "B16" : "");
+                 Epi::STATS ? "EpiStoreStats" : is_bnsums<Epi>::value ? "EpiStoreBnSums" : "EpiStore",
+                 Epi::BF16 ? "B16" : "");
         prof_push(name, 2.0 * a.M * a.N * (double)a.K, st);
         hipLaunchKernelGGL(fn, grid, dim3(256), 0, st, a);
         prof_pop(st);
@@ -1007,6 +1008,40 @@ void conv3x3_fwd_ps(Split x, int cin, Split w, int cout, float* y, int64_t ldy, 
         if (stats) launch_kb<KConvFwdSP1, 32, 64>(c, kb, a, 1, st);
         else launch_kb<KConvFwdP1, 32, 64>(c, kb, a, 1, st);
     }
+}
+
+// conv2's input gradient with bn1's backward column sums from the window epilogue (EpiStoreBnSums):
+// returns the number of tiles whose partials it wrote (0: no window kernel for this shape or the
+// partials do not fit; nothing launched, the caller takes the unfused path).  S3 engine only: measured
+// on MI355X (tools/ab_step.py, same box) fp32 configs[1] 225.7 -> 223.9 ms/step; the bf16 engine's
+// form (bf16 dL/da1, the same epilogue on the B1 window kernels) made configs[3] 64.1 -> 68.2 ms/step —
+// the per-element y load and fp64 sums in the epilogue cost its cheap GEMMs more than the
+// column-reduction pass they replace
+namespace {
+template <bool OB16, bool PS>
+int dgrad_bnsums_launch(const WinPick& wp, GemmArgs& a, const BnSums& bn, hipStream_t st) {
+    const int tiles = win_blocks(wp, a.B, a.H, a.W);
+    if (!bn.part || (int64_t)tiles * 2 * a.N > bn.part_cap) return 0;
+    a.bn_g = bn.y; a.bn_ldg = bn.ldy;
+    a.bn_mean = bn.mean; a.bn_invstd = bn.invstd; a.bn_scale = bn.scale; a.bn_shift = bn.shift;
+    a.bn_part = bn.part;
+    if (bn.y_bf16) launch_win<EpiStoreBnSums<OB16, true>, PS>(wp, a, st);
+    else launch_win<EpiStoreBnSums<OB16, false>, PS>(wp, a, st);
+    return tiles;
+}
+}  // namespace
+
+int conv3x3_dgrad_bnsums(const float* dz, int cout, const float* wd, int cin, float* dx, int64_t lddx, int B, int H,
+                         int W, const BnSums& bn, hipStream_t st) {
+    const WinPick w = pick_win(cout, W, cin);
+    if (!w.R || bn.y_bf16) return 0;
+    GemmArgs a{};
+    a.M = B * H * W; a.N = cin; a.K = 9 * cout;
+    a.B = B; a.H = H; a.W = W;
+    a.A = dz; a.lda = cout; a.a_coff = 0; a.a_cin = cout;
+    a.Bm = wd; a.ldb = 9 * cout;
+    a.C = dx; a.ldc = lddx; a.c_coff = 0;
+    return dgrad_bnsums_launch<false, false>(w, a, bn, st);
 }
 
 bool conv3x3_dgrad_split_ok(Split dz, int cout, Split wd, int cin, int W, int split_n) {

@@ -52,6 +52,22 @@ struct EpiStoreSplitB16 : EpiStore {
 struct EpiStoreSplit2B16 : EpiStoreB16 {
     static constexpr bool SPLIT = true;
 };
+// window epilogue only (round 5): the store, plus the BatchNorm backward's column sums of the BN whose
+// output gradient this GEMM produces (a DoubleConv's conv2 input gradient dL/da1 feeding bn1's
+// backward): per tile, sum dz and sum dz xhat with dz = v [y scale + shift > 0], xhat = (y - mean)
+// invstd, v the stored value (bf16-rounded for OB16) and y the BN input (a.bn_g: rows of a.bn_ldg,
+// bf16 for YB) — OpBnBwd's arithmetic, fp64 per lane — into a.bn_part[tile][2][N].  The separate
+// column-reduction pass over (dL/da1, y) is then not needed.
+template <bool OB16, bool YB>
+struct EpiStoreBnSums {
+    static constexpr bool STATS = false;
+    static constexpr bool BF16 = OB16;
+    static constexpr bool ADD = false;
+    static constexpr bool SPLIT = false;
+    static constexpr bool BNSUMS = true;
+    static constexpr bool Y_BF16 = YB;
+};
+
 // ConvTranspose2d(k2,s2) pixel shuffle: n = (q=(dy,dx), co) -> high-res pixel (2y+dy, 2x+dx).
 // The column (q, co) is fixed per lane and sub-block (STRUCTURED epilogue).  When W % 32 == 0 a
 // 32-row block is one run of 32 pixels of one image row (blocks start at multiples of 32), so its

@@ -439,6 +439,10 @@ struct has_prefetch : std::false_type {};   // a structured epilogue that loads 
 template <class E>
 struct has_prefetch<E, std::void_t<decltype(E::PREFETCH)>> : std::integral_constant<bool, E::PREFETCH> {};
 template <class E, class = void>
+struct is_bnsums : std::false_type {};   // EpiStoreBnSums (epilogues.hpp)
+template <class E>
+struct is_bnsums<E, std::void_t<decltype(E::BNSUMS)>> : std::integral_constant<bool, E::BNSUMS> {};
+template <class E, class = void>
 struct is_structured : std::false_type {};
 template <class E>
 struct is_structured<E, std::void_t<decltype(E::STRUCTURED)>> : std::integral_constant<bool, E::STRUCTURED> {};

@@ -114,6 +114,89 @@ struct WinB {
 #ifndef CAD_XP_WIN
 #define CAD_XP_WIN 0
 #endif
+// BN-backward column sums of a window epilogue (EpiStoreBnSums): NB column blocks of CB (32 or 16)
+// columns per lane; lanes whose lane % CB agree share a column.  y (the BN input) is read at the
+// element the epilogue stores; the per-lane fp64 sums merge over lanes, then waves, into
+// a.bn_part[tile][2][N] (EpiBnBwdSums' layout).
+template <int NB, int CB, bool YB>
+struct WinBnSums {
+    double s0[NB], s1[NB];
+    float sc[NB], sh[NB], mu[NB], is[NB];
+    __amdgpu_buffer_rsrc_t ry;
+    int64_t ldyb;   // bytes per y row
+    __device__ void init(const GemmArgs& a, int b, int y0, int x0, int ncol0) {
+        constexpr int YS = YB ? 2 : 4;
+        ldyb = a.bn_ldg * YS;
+        ry = make_rsrc(reinterpret_cast<const float*>(static_cast<const char*>(a.bn_g) +
+                                                      (((int64_t)b * a.H + y0) * a.W + x0) * ldyb));
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const int n = min(ncol0 + j * CB, a.N - 1);
+            sc[j] = a.bn_scale[n]; sh[j] = a.bn_shift[n]; mu[j] = a.bn_mean[n]; is[j] = a.bn_invstd[n];
+            s0[j] = 0.0; s1[j] = 0.0;
+        }
+    }
+    // four rows of column n at pixel offset pix (r W + c) of the block, row stride one pixel row
+    __device__ void load4(int64_t pix, int n, bool ok, float (&y)[4]) const {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t off = ok ? (uint32_t)((pix + q) * ldyb + (int64_t)n * (YB ? 2 : 4)) : kOOB;
+            if constexpr (YB)
+                y[q] = __uint_as_float((uint32_t)__builtin_amdgcn_raw_buffer_load_b16(ry, off, 0, 0) << 16);
+            else
+                y[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, off, 0, 0));
+        }
+    }
+    __device__ void add(int j, float v, float y) {
+        const float z = __fmaf_rn(y, sc[j], sh[j]);
+        const float dz = z > 0.f ? v : 0.f;
+        const float xh = (y - mu[j]) * is[j];
+        s0[j] += dz;
+        s1[j] += (double)dz * xh;
+    }
+    template <int WM, int WN>
+    __device__ void finish(const GemmArgs& a, float* ldsf, int tile_x, int n0) {
+        constexpr int BN = CB * NB * WN;
+        double* lds = reinterpret_cast<double*>(ldsf);
+        const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+        const int wm = wave / WN, wn = wave % WN;
+        __syncthreads();   // the LDS image may still be read by other waves' last fragments
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            double t0 = s0[j], t1 = s1[j];
+#pragma unroll
+            for (int x = CB; x < 64; x *= 2) {
+                t0 += __shfl_xor(t0, x);
+                t1 += __shfl_xor(t1, x);
+            }
+            if (lane < CB) {
+                double* r = lds + ((int64_t)wm * BN + wn * CB * NB + j * CB + lane) * 2;
+                r[0] = t0;
+                r[1] = t1;
+            }
+        }
+        __syncthreads();
+        for (int c = tid; c < BN; c += 256) {
+            double u0 = 0.0, u1 = 0.0;
+#pragma unroll
+            for (int w = 0; w < WM; ++w) {
+                u0 += lds[((int64_t)w * BN + c) * 2];
+                u1 += lds[((int64_t)w * BN + c) * 2 + 1];
+            }
+            const int n = n0 + c;
+            if (n < a.N) {
+                a.bn_part[((int64_t)tile_x * 2) * a.N + n] = u0;
+                a.bn_part[((int64_t)tile_x * 2 + 1) * a.N + n] = u1;
+            }
+        }
+    }
+};
+template <class Epi>
+constexpr bool epi_y_bf16() {
+    if constexpr (is_bnsums<Epi>::value) return Epi::Y_BF16;
+    else return false;
+}
+
 template <int WM, int WN, int MI, int NJ, int CW, class Epi>
 __device__ __forceinline__ void win_epilogue(const GemmArgs& a, const floatx16 (&acc)[MI][NJ], int tile_lin, int n0,
                                              int b, int y0, int x0, float* lds) {
@@ -140,6 +223,9 @@ __device__ __forceinline__ void win_epilogue(const GemmArgs& a, const floatx16 (
 #pragma unroll
         for (int j = 0; j < NJ; ++j) bnp.shift(j, acc[0][j][0]);
     }
+    constexpr bool BNS = is_bnsums<Epi>::value;
+    [[maybe_unused]] WinBnSums<BNS ? NJ : 1, 32, epi_y_bf16<Epi>()> bns;
+    if constexpr (BNS) bns.init(a, b, y0, x0, n0 + wn * 32 * NJ + (lane & 31));
     constexpr int ES = Epi::BF16 ? 2 : 4;   // output element bytes
     const int64_t ldc4 = a.ldc * ES;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const float*>(
@@ -169,6 +255,14 @@ __device__ __forceinline__ void win_epilogue(const GemmArgs& a, const floatx16 (
 #pragma unroll
                     for (int q = 0; q < 4; ++q) v[q] = (float)(__bf16)v[q];
                 }
+                if constexpr (BNS) {   // rows of one block row: r, c .. c + 3 (CW % 4 == 0); rows past H skipped
+                    float yv[4];
+                    bns.load4(r * (int64_t)a.W + c, n, ok, yv);
+                    if (ok) {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) bns.add(j, v[q], yv[q]);
+                    }
+                }
                 if constexpr (Epi::SPLIT) {
                     if (n >= a.split_n) {   // uniform per 32-column block (host: split_n % 32 == 0)
                         const uint32_t lo2 =
@@ -195,6 +289,7 @@ __device__ __forceinline__ void win_epilogue(const GemmArgs& a, const floatx16 (
             }
         }
     if constexpr (Epi::STATS && (CAD_XP_WIN & 2) == 0) bnp.template finish<WM, WN>(a, lds, tile_lin, n0);
+    if constexpr (BNS) bns.template finish<WM, WN>(a, lds, tile_lin, n0);
 }
 
 // The same epilogue for 16 x 16 accumulator blocks (v_mfma_f32_16x16x32_bf16): a wave's MB x NB
@@ -212,6 +307,9 @@ __device__ __forceinline__ void win_epilogue16(const GemmArgs& a, const floatx4 
 #pragma unroll
         for (int j = 0; j < NB; ++j) bnp.shift(j, acc[0][j][0]);
     }
+    constexpr bool BNS = is_bnsums<Epi>::value;
+    [[maybe_unused]] WinBnSums<BNS ? NB : 1, 16, epi_y_bf16<Epi>()> bns;
+    if constexpr (BNS) bns.init(a, b, y0, x0, n0 + wn * 16 * NB + (lane & 15));
     constexpr int ES = Epi::BF16 ? 2 : 4;
     const int64_t ldc4 = a.ldc * ES;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const float*>(
@@ -250,6 +348,14 @@ __device__ __forceinline__ void win_epilogue16(const GemmArgs& a, const floatx4 
                 }
             }
             const uint32_t lo = ok ? (uint32_t)((r * (int64_t)a.W + c) * ldc4 + (int64_t)n * ES) : kOOB;
+            if constexpr (BNS) {
+                float yv[4];
+                bns.load4(r * (int64_t)a.W + c, n, ok, yv);
+                if (ok) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) bns.add(j, v[q], yv[q]);
+                }
+            }
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 if constexpr (Epi::BF16)
@@ -262,6 +368,7 @@ __device__ __forceinline__ void win_epilogue16(const GemmArgs& a, const floatx4 
             }
         }
     if constexpr (Epi::STATS) bnp.template finish<WM, WN>(a, lds, tile_lin, n0);
+    if constexpr (BNS) bns.template finish<WM, WN>(a, lds, tile_lin, n0);
 }
 
 // blocks: gridDim.x = B * ceil(H / R) * (W / CW) output blocks (XCD-aware order), gridDim.y = N tiles
@@ -414,30 +521,32 @@ __device__ __forceinline__ void conv3x3_win_ps_body(const GemmArgs& a) {
     const int64_t pb = pbase > 0 ? pbase : 0;
     const __amdgpu_buffer_rsrc_t rsa =
         make_rsrc(reinterpret_cast<const float*>(reinterpret_cast<const char*>(a.A) + (pb * a.lda + a.a_coff) * 2));
-    int aoff[G::NVA], awr[G::NVA], alds[G::NVA];
+    // piece j = tid + 256 j is (window pixel w = j 64 + tid / 4, 16-B group tid % 4): its LDS slot is
+    // a compile-time step from piece 0's; its global offset is kept per piece, and whether it lies
+    // inside the image for each kernel row ky is bit 3 j + ky of amask (the per-piece registers of the
+    // loop were the A operand's fragment budget: 250 VGPRs)
+    static_assert(G::NVA <= 10, "amask: 3 bits per piece");
+    int aoff[G::NVA];
+    uint32_t amask = 0;
 #pragma unroll
     for (int j = 0; j < G::NVA; ++j) {
         const int f = tid + 256 * j;
         const int w = f >> 2, g = f & 3;
         const int r = w / G::WC, c = w - r * G::WC;
         const int x = x0 - 1 + c;
-        const bool ok = f < G::NTA && (unsigned)x < (unsigned)W;
-        awr[j] = ok ? r : -(1 << 28);
+        const bool okx = f < G::NTA && (unsigned)x < (unsigned)W;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+            if (okx && (unsigned)(y0 - 1 + ky + r) < (unsigned)H) amask |= 1u << (3 * j + ky);
         aoff[j] = (int)((r * (int64_t)W + c + (pbase - pb)) * rowb) + g * 16;
-        alds[j] = (f < G::NTA ? w : 0) * G::LDK + g * 8;
     }
-    // B: weight twin rows of ldb elements (ldb = 9*cin), piece (tap, row, group)
+    const int alds0 = (tid >> 2) * G::LDK + (tid & 3) * 8;   // piece j: + 64 j LDK
+    // B: weight twin rows of ldb elements (ldb = 9*cin), piece (tap, row, group); piece jj = tid + 256 jj
+    // is row 64 jj + tid / 4
     const int rowbb = (int)a.ldb * 2;
     const __amdgpu_buffer_rsrc_t rsb =
         make_rsrc(reinterpret_cast<const float*>(reinterpret_cast<const char*>(a.Bm) + ((int64_t)n0 * a.ldb + a.b_coff) * 2));
-    int boff[G::JB], blds[G::JB];
-#pragma unroll
-    for (int jj = 0; jj < G::JB; ++jj) {
-        const int task = tid + 256 * jj;
-        const int row = task >> 2, g = task & 3;
-        boff[jj] = row * rowbb + g * 16;
-        blds[jj] = (task < G::NTB ? row : 0) * G::LDK + g * 8;
-    }
+    const int boff0 = (tid >> 2) * rowbb + (tid & 3) * 16, blds0 = (tid >> 2) * G::LDK + (tid & 3) * 8;
     auto bact = [&](int jj) { return 256 * (jj + 1) <= G::NTB || tid + 256 * jj < G::NTB; };
 
     constexpr int MR = M16 ? 2 * MI : MI;   // A fragment row blocks per wave (32 or 16 rows)
@@ -465,29 +574,29 @@ __device__ __forceinline__ void conv3x3_win_ps_body(const GemmArgs& a) {
         const int adda = ky * W * rowb + cb * 64;                   // 32 channels = 64 bytes
 #pragma unroll
         for (int j = 0; j < G::NVA; ++j) {
-            const int y = y0 - 1 + ky + awr[j];
+            const bool in = (amask >> (3 * j + ky)) & 1u;
             ra[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                  rsa, (unsigned)y < (unsigned)H ? (uint32_t)(aoff[j] + adda) : kOOB, 0, 0));
+                                                  rsa, in ? (uint32_t)(aoff[j] + adda) : kOOB, 0, 0));
         }
-        const int addb = 3 * ky * cin * 2 + cb * 64;
+        const int addb = boff0 + 3 * ky * cin * 2 + cb * 64;
 #pragma unroll
         for (int t = 0; t < 3; ++t)
 #pragma unroll
             for (int jj = 0; jj < G::JB; ++jj)
                 if (bact(jj))
                     rb[t * G::JB + jj] = __builtin_bit_cast(
-                        uint4, __builtin_amdgcn_raw_buffer_load_b128(rsb, (uint32_t)(boff[jj] + addb + t * cin * 2), 0, 0));
+                        uint4, __builtin_amdgcn_raw_buffer_load_b128(rsb, (uint32_t)(addb + 64 * jj * rowbb + t * cin * 2), 0, 0));
         if (++ky == 3) { ky = 0; ++cb; }
     };
     auto store = [&]() {
 #pragma unroll
         for (int j = 0; j < G::NVA; ++j)
-            if (tid + 256 * j < G::NTA) *reinterpret_cast<uint4*>(lds + alds[j]) = ra[j];
+            if (tid + 256 * j < G::NTA) *reinterpret_cast<uint4*>(lds + alds0 + 64 * j * G::LDK) = ra[j];
 #pragma unroll
         for (int t = 0; t < 3; ++t)
 #pragma unroll
             for (int jj = 0; jj < G::JB; ++jj)
-                if (bact(jj)) *reinterpret_cast<uint4*>(lds + G::SA + t * G::SBT + blds[jj]) = rb[t * G::JB + jj];
+                if (bact(jj)) *reinterpret_cast<uint4*>(lds + G::SA + t * G::SBT + blds0 + 64 * jj * G::LDK) = rb[t * G::JB + jj];
     };
     auto compute = [&]() {
         if constexpr (M16) {
@@ -507,18 +616,27 @@ __device__ __forceinline__ void conv3x3_win_ps_body(const GemmArgs& a) {
                 }
             }
         } else {
+            // fragments of k step t + 1 read while the MFMAs of step t run (two register sets, the
+            // schedule pinned by sched_barrier): hipcc's own schedule re-read each A fragment right
+            // before its two MFMAs and waited on it (tools/winlab.py: 1-3 % on levels 0-2)
+            bf16x8 fa[2][MI][1], fb[2][NJ][1];
+            auto rd = [&](int t, int buf) {
+                const int kx = t >> 1, q = t & 1;
 #pragma unroll
-            for (int kx = 0; kx < 3; ++kx)
+                for (int j = 0; j < NJ; ++j)
+                    s3_frag<BN, 32, 1>(lds + G::SA + kx * G::SBT, wn * 32 * NJ + j * 32, q, fb[buf][j]);
 #pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    bf16x8 fa[MI][1], fb[NJ][1];
+                for (int i = 0; i < MI; ++i)
+                    fa[buf][i][0] = *reinterpret_cast<const bf16x8*>(lds + (wpix[i] + kx) * G::LDK + q * 16 + (lane >> 5) * 8);
+            };
+            rd(0, 0);
 #pragma unroll
-                    for (int j = 0; j < NJ; ++j) s3_frag<BN, 32, 1>(lds + G::SA + kx * G::SBT, wn * 32 * NJ + j * 32, q, fb[j]);
-#pragma unroll
-                    for (int i = 0; i < MI; ++i)
-                        fa[i][0] = *reinterpret_cast<const bf16x8*>(lds + (wpix[i] + kx) * G::LDK + q * 16 + (lane >> 5) * 8);
-                    s3_mfma<1>(acc, fa, fb);
-                }
+            for (int t = 0; t < 6; ++t) {
+                if (t + 1 < 6) rd(t + 1, (t + 1) & 1);
+                __builtin_amdgcn_sched_barrier(0);
+                s3_mfma<1>(acc, fa[t & 1], fb[t & 1]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
     };
 

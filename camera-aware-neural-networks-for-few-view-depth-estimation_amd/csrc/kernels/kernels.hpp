@@ -213,11 +213,26 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
                  int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
                  hipStream_t st, const float* gmul = nullptr, int64_t HW = 1, void* dy_split = nullptr,
                  bool relu = true, bool y_bf16 = false, const HeadGrad* head = nullptr, bool g_bf16 = false,
-                 const PoolAdd* pool = nullptr, float* film_dgam = nullptr, float* film_dbet = nullptr);
+                 const PoolAdd* pool = nullptr, float* film_dgam = nullptr, float* film_dbet = nullptr,
+                 const double* tile_part = nullptr, int tiles = 0);
+// (tile_part: the column sums were already formed per tile by the producing GEMM's epilogue —
+// conv3x3_dgrad_*_bnsums, [tiles][2][C] — and are only reduced over tiles here)
 // out_split != nullptr: also the pooled output's split twin (dense, ld C); out may then be nullptr
 // x_bf16: x is a bf16 twin (rows of ldx elements; requires out_split)
 void maxpool_fwd(const float* x, int64_t ldx, int C, int B, int H, int W, float* out, uint8_t* idx,
                  hipStream_t st, void* out_split = nullptr, bool x_bf16 = false);
+// BatchNorm-backward column sums taken in a conv input-gradient epilogue (EpiStoreBnSums): the BN
+// input y (rows of ldy, bf16 or fp32) and its coefficients; per-tile fp64 partials [tiles][2][N] into
+// part (capacity part_cap doubles)
+struct BnSums {
+    const void* y = nullptr; int64_t ldy = 0; bool y_bf16 = false;
+    const float *mean = nullptr, *invstd = nullptr, *scale = nullptr, *shift = nullptr;
+    double* part = nullptr; int64_t part_cap = 0;
+};
+// conv3x3 input gradient (S3 engine, fp32 dx) whose window epilogue also forms bn's backward sums over
+// dx: returns the tile count (0 = not available for this shape: nothing launched)
+int conv3x3_dgrad_bnsums(const float* dz, int cout, const float* wd, int cin, float* dx, int64_t lddx, int B, int H,
+                         int W, const BnSums& bn, hipStream_t st);
 // an encoder block's bn2 + ReLU fused with the next level's MaxPool2d(2): writes the block output
 // (fp32 rows `out` (ldo) and/or its 1-plane twin `os` (ldos), channel offset 0) and the pooled output
 // (fp32 `pool` and/or its twin `pool_split`, dense ld C) with the argmax codes, exactly what

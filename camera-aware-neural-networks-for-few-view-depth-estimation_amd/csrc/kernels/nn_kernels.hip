@@ -555,9 +555,11 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
                  const float* invstd, const float* scale, const float* shift, const float* gamma,
                  int64_t M, double* scratch, float* coef, float* dgamma, float* dbeta, float* dy,
                  hipStream_t st, const float* gmul, int64_t HW, void* dy_split, bool relu, bool y_bf16,
-                 const HeadGrad* head, bool g_bf16, const PoolAdd* pool, float* film_dgam, float* film_dbet) {
+                 const HeadGrad* head, bool g_bf16, const PoolAdd* pool, float* film_dgam, float* film_dbet,
+                 const double* tile_part, int tiles) {
     double* tot = scratch;
     double* part = scratch + 2 * C;
+    if (tile_part && (film_dgam || tiles <= 0)) throw std::runtime_error("bn_relu_bwd: tile partials");
     if (film_dgam) {
         // a FiLM block's bn1: the BN sums and the FiLM affine's per-(sample, channel) sums in one pass,
         // k slices per sample (rows per slice dividing HW; >= 256 rows, <= 2048 slices in all)
@@ -606,7 +608,13 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
             default: return fn(F{}, F{}, F{});
         }
     };
-    const int S = film_dgam ? 0 : with_mode([&](auto hgc, auto gbc, auto pac) {
+    if (tile_part) {   // tiles -> slices of about one tile row per thread (as bn_fwd_finalize) -> tot
+        const int C2 = 2 * C, CX = std::min(C2 >> 2, 64), RY = std::max(1, 256 / CX);
+        const int S = (int)std::max<int64_t>(1, std::min<int64_t>(colsum_slices(M), cdiv(tiles, RY)));
+        launch_colreduce_slices<1>(OpSumD{tile_part, C2}, tiles, C2, S, cdiv(tiles, S), part, st);
+        launch_colfinal(part, S, C2, tot, nullptr, 1.f, st);
+    }
+    const int S = (film_dgam || tile_part) ? 0 : with_mode([&](auto hgc, auto gbc, auto pac) {
         constexpr bool HG = decltype(hgc)::value, GB = decltype(gbc)::value, PA = decltype(pac)::value;
         return y_bf16 ? launch_colreduce<2>(OpBnBwd<true, HG, GB, PA>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C,
                                                                      HW, relu, hg, pa},
@@ -615,7 +623,7 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
                                                                       C, HW, relu, hg, pa},
                                             M, C, part, st);
     });
-    if (!film_dgam) launch_colfinal(part, S, 2 * C, tot, nullptr, 1.f, st);
+    if (!film_dgam && !tile_part) launch_colfinal(part, S, 2 * C, tot, nullptr, 1.f, st);
     hipLaunchKernelGGL(k_bn_bwd_coef, dim3(cdiv(C, 64)), dim3(64), 0, st, tot, C, M, gamma, invstd, coef, dgamma, dbeta);
     const int np = dy_split ? split_planes() : 0;
     char* os = static_cast<char*>(dy_split);

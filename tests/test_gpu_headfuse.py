@@ -48,7 +48,11 @@ def test_head_fusion_bit_identical(tmp_path, kind, eng, f, B, H, W):
                                                   ("CAD_BNPOOL", "baseline", 2, 16, 2, 64, 96),
                                                   ("CAD_BNPOOL", "rayfilm", 2, 32, 2, 48, 64),
                                                   ("CAD_BNPOOL", "baseline", 1, 64, 2, 64, 64),
-                                                  ("CAD_BNPOOL", "film", 0, 16, 2, 64, 96)])
+                                                  ("CAD_BNPOOL", "film", 0, 16, 2, 64, 96),
+                                                  ("CAD_BNSUMS", "baseline", 1, 16, 2, 64, 96),
+                                                  ("CAD_BNSUMS", "baseline", 1, 64, 2, 64, 128),
+                                                  ("CAD_BNSUMS", "baseline", 1, 64, 2, 64, 64),
+                                                  ("CAD_BNSUMS", "baseline", 1, 32, 2, 48, 64)])
 def test_backward_fusions_bit_identical(tmp_path, var, kind, eng, f, B, H, W):
     """CAD_POOLFOLD (fp32 engines; the bf16 engine always folds): the max-pool backward folded into the
     encoder's bn2 backward (nn_kernels.hip pool_add) makes the scatter's fp32 add per element.
@@ -58,8 +62,9 @@ def test_backward_fusions_bit_identical(tmp_path, var, kind, eng, f, B, H, W):
     the BN-backward sums in fp64 from per-tile partials instead of row slices (a reordering of fp64 sums
     that would have to land within 1e-16 of an fp32 rounding boundary to show).  CAD_BNPOOL (all engines):
     each encoder block's bn2 + ReLU pass also writes the next level's max-pool (nn_kernels.hip
-    bn_relu_pool_fwd: the same affine, rounding and comparison).  Two training steps with and without
-    each agree bit for bit."""
+    bn_relu_pool_fwd: the same affine, rounding and comparison).  CAD_BNSUMS (S3 engine): bn1's
+    backward sums come from conv2's input-gradient window epilogue (EpiStoreBnSums: fp64 sums of the
+    same fp32 terms in another order).  Two training steps with and without each agree bit for bit."""
     a = _run(tmp_path, 0, (kind, eng, f, B, H, W), var)
     b = _run(tmp_path, 1, (kind, eng, f, B, H, W), var)
     bad = [k for k in a if not torch.equal(a[k], b[k])]
