@@ -209,6 +209,59 @@ struct OpBnBwd {
         }
     }
 };
+// OpBnBwd<YB, false, GB, true> walked over POOLED pixels (round 5): row op = pooled pixel, whose 2 x 2
+// window's four full-resolution rows it visits with the argmax codes and the pooled gradient loaded
+// once (the per-row walk re-derived the window by two divisions and re-read both for each of its four
+// rows).  Each row takes the same fp32 add as pool_add; the fp64 sums run in another order.
+__device__ __forceinline__ int64_t pool_window(const PoolAdd& pa, uint32_t op) {
+    const uint32_t Wo = (uint32_t)pa.W >> 1, Ho = (uint32_t)pa.H >> 1;
+    const uint32_t t = fdiv(pa.divW, op), b = fdiv(pa.divH, t);
+    const uint32_t xo = op - t * Wo, yo = t - b * Ho;
+    return ((int64_t)b * pa.H + 2 * yo) * pa.W + 2 * xo;   // full-res row of the window's (0, 0)
+}
+__device__ __forceinline__ float4 pool_add_k(uchar4 a, float4 d, int k, float4 gv) {
+    if (a.x == k) gv.x += d.x;
+    if (a.y == k) gv.y += d.y;
+    if (a.z == k) gv.z += d.z;
+    if (a.w == k) gv.w += d.w;
+    return gv;
+}
+template <bool YB, bool GB>
+struct OpBnBwdPoolQ {
+    const float *g, *y, *mean, *invstd, *scale, *shift;
+    int64_t ldg; int gcoff, C;
+    PoolAdd pa;   // divW / divH: by the POOLED width / height
+    __device__ BnCoef prep(int c4) const {
+        BnCoef k;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int c = c4 * 4 + e;
+            k.sc[e] = scale[c]; k.sh[e] = shift[c]; k.mu[e] = mean[c]; k.is[e] = invstd[c];
+        }
+        return k;
+    }
+    __device__ void operator()(int64_t op, int c4, double (&acc)[2][4], const BnCoef& k) const {
+        const int c = c4 * 4;
+        const int64_t p00 = pool_window(pa, (uint32_t)op);
+        const uchar4 a = *reinterpret_cast<const uchar4*>(pa.idx + op * C + c);
+        const float4 d = *reinterpret_cast<const float4*>(pa.d + op * C + c);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t r = p00 + (q >> 1) * pa.W + (q & 1);
+            const float4 gv = pool_add_k(a, d, q, load4<GB>(g, r * ldg + gcoff + c));
+            const float4 yv = load4<YB>(y, r * C + c);
+            const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, ya[4] = {yv.x, yv.y, yv.z, yv.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float z = __fmaf_rn(ya[e], k.sc[e], k.sh[e]);
+                const float dz = z > 0.f ? ga[e] : 0.f;
+                const float xh = (ya[e] - k.mu[e]) * k.is[e];
+                acc[0][e] += dz;
+                acc[1][e] += (double)dz * xh;
+            }
+        }
+    }
+};
 // OpBnBwd of a FiLM block (gmul = gamma[b][c]) that also forms the FiLM affine's sums in the same pass
 // over (g, y): acc[2] = sum g a, acc[3] = sum g with g the raw gradient of the FiLM output and a =
 // relu(y scale + shift) (k_film_reduce's sums; slices aligned to samples by the caller)
@@ -536,6 +589,51 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_rows(const float* __restric
         if constexpr (NP > 0) split4_store<NP>(os, C, 0, r, c0, ov);
     }
 }
+// k_bn_relu_bwd_rows<NP, YB, false, GB, true> walked over pooled pixels (OpBnBwdPoolQ's order): the
+// same per-element arithmetic and outputs
+template <int NP, bool YB, bool GB>
+__global__ __launch_bounds__(256) void k_bn_relu_bwd_poolq(const float* __restrict__ g, int64_t ldg, int gcoff,
+                                                           const float* __restrict__ y, int C,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ scale,
+                                                           const float* __restrict__ shift,
+                                                           const float* __restrict__ coef, float* __restrict__ dy,
+                                                           int64_t Mo, int64_t rps, char* __restrict__ os, PoolAdd pa) {
+    const int c4 = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c4 >= (C >> 2)) return;
+    const int c0 = c4 * 4;
+    float sc[4], sh[4], mu[4], is[4], k0[4], k1[4], k2[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        sc[e] = scale[c0 + e]; sh[e] = shift[c0 + e]; mu[e] = mean[c0 + e]; is[e] = invstd[c0 + e];
+        k0[e] = coef[c0 + e]; k1[e] = coef[C + c0 + e]; k2[e] = coef[2 * C + c0 + e];
+    }
+    const int64_t o1 = min(Mo, (int64_t)(blockIdx.y + 1) * rps);
+    for (int64_t op = (int64_t)blockIdx.y * rps + threadIdx.y; op < o1; op += blockDim.y) {
+        const int64_t p00 = pool_window(pa, (uint32_t)op);
+        const uchar4 a = *reinterpret_cast<const uchar4*>(pa.idx + op * C + c0);
+        const float4 d = *reinterpret_cast<const float4*>(pa.d + op * C + c0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t r = p00 + (q >> 1) * pa.W + (q & 1);
+            const float4 gv = pool_add_k(a, d, q, load4<GB>(g, r * ldg + gcoff + c0));
+            const float4 yv = load4<YB>(y, r * C + c0);
+            const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, ya[4] = {yv.x, yv.y, yv.z, yv.w};
+            float o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float z = __fmaf_rn(ya[e], sc[e], sh[e]);
+                const float dz = z > 0.f ? ga[e] : 0.f;
+                const float xh = (ya[e] - mu[e]) * is[e];
+                o[e] = __fsub_rn(__fmaf_rn(k0[e], dz, -k1[e]), __fmul_rn(k2[e], xh));
+            }
+            const float4 ov = make_float4(o[0], o[1], o[2], o[3]);
+            if (dy) *reinterpret_cast<float4*>(dy + r * C + c0) = ov;
+            if constexpr (NP > 0) split4_store<NP>(os, C, 0, r, c0, ov);
+        }
+    }
+}
 // FiLM sums from OpBnBwdFilm's sample-aligned slices: dgam[b][c] = sum over sample b's k slices
 __global__ void k_film_from_parts(const double* __restrict__ part, int k, int C, int B, float* __restrict__ dgam,
                                   float* __restrict__ dbet) {
@@ -595,6 +693,18 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
         pa.divW = make_fastdiv((uint32_t)pa.W);
         pa.divH = make_fastdiv((uint32_t)pa.H);
     }
+    // the folded max-pool backward walked over pooled pixels (OpBnBwdPoolQ / k_bn_relu_bwd_poolq);
+    // CAD_POOLQ=0 keeps the per-row walk (A/B)
+    static const bool poolq_on = [] {
+        const char* e = std::getenv("CAD_POOLQ");
+        return !(e && e[0] == '0');
+    }();
+    const bool quad = pool && poolq_on && !gmul && relu && !tile_part;
+    PoolAdd paq = pa;
+    if (quad) {
+        paq.divW = make_fastdiv((uint32_t)pa.W / 2);
+        paq.divH = make_fastdiv((uint32_t)pa.H / 2);
+    }
     // g source: 0 fp32, 1 head, 2 bf16, 3 fp32 + folded max-pool backward, 4 bf16 + folded max-pool backward
     const int gm = head ? 1 : (g_bf16 && pool) ? 4 : g_bf16 ? 2 : pool ? 3 : 0;
     using T = std::true_type;
@@ -614,7 +724,12 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
         launch_colreduce_slices<1>(OpSumD{tile_part, C2}, tiles, C2, S, cdiv(tiles, S), part, st);
         launch_colfinal(part, S, C2, tot, nullptr, 1.f, st);
     }
-    const int S = (film_dgam || tile_part) ? 0 : with_mode([&](auto hgc, auto gbc, auto pac) {
+    const int S = (film_dgam || tile_part) ? 0 : quad ? (
+        y_bf16 ? (g_bf16 ? launch_colreduce<2>(OpBnBwdPoolQ<true, true>{g, y, mean, invstd, scale, shift, ldg, gcoff, C, paq}, M / 4, C, part, st)
+                         : launch_colreduce<2>(OpBnBwdPoolQ<true, false>{g, y, mean, invstd, scale, shift, ldg, gcoff, C, paq}, M / 4, C, part, st))
+               : (g_bf16 ? launch_colreduce<2>(OpBnBwdPoolQ<false, true>{g, y, mean, invstd, scale, shift, ldg, gcoff, C, paq}, M / 4, C, part, st)
+                         : launch_colreduce<2>(OpBnBwdPoolQ<false, false>{g, y, mean, invstd, scale, shift, ldg, gcoff, C, paq}, M / 4, C, part, st)))
+        : with_mode([&](auto hgc, auto gbc, auto pac) {
         constexpr bool HG = decltype(hgc)::value, GB = decltype(gbc)::value, PA = decltype(pac)::value;
         return y_bf16 ? launch_colreduce<2>(OpBnBwd<true, HG, GB, PA>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C,
                                                                      HW, relu, hg, pa},
@@ -627,6 +742,21 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
     hipLaunchKernelGGL(k_bn_bwd_coef, dim3(cdiv(C, 64)), dim3(64), 0, st, tot, C, M, gamma, invstd, coef, dgamma, dbeta);
     const int np = dy_split ? split_planes() : 0;
     char* os = static_cast<char*>(dy_split);
+    if (quad) {
+        const RowGrid rq = row_grid(M / 4, C);
+        auto goq = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(cdiv(C >> 2, rq.CX), rq.S), dim3(rq.CX, rq.RY), 0, st, g, ldg, gcoff, y, C, mean,
+                               invstd, scale, shift, coef, dy, M / 4, rq.rps, os, paq);
+        };
+        if (np == 1) {
+            if (y_bf16) g_bf16 ? goq(k_bn_relu_bwd_poolq<1, true, true>) : goq(k_bn_relu_bwd_poolq<1, true, false>);
+            else g_bf16 ? goq(k_bn_relu_bwd_poolq<1, false, true>) : goq(k_bn_relu_bwd_poolq<1, false, false>);
+        } else {
+            if (y_bf16) g_bf16 ? goq(k_bn_relu_bwd_poolq<0, true, true>) : goq(k_bn_relu_bwd_poolq<0, true, false>);
+            else g_bf16 ? goq(k_bn_relu_bwd_poolq<0, false, true>) : goq(k_bn_relu_bwd_poolq<0, false, false>);
+        }
+        return;
+    }
     const RowGrid rg = row_grid(M, C);
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(cdiv(C >> 2, rg.CX), rg.S), dim3(rg.CX, rg.RY), 0, st, g, ldg, gcoff, y, C, mean,
