@@ -191,7 +191,7 @@ void film_mlp_fwd(const FilmLayer& L, const float* camn, int B, bool train, hipS
 template <bool YB, bool TW>
 __global__ __launch_bounds__(256) void k_film_apply(const float* __restrict__ y, int C, const float* __restrict__ scale,
                                                     const float* __restrict__ shift, const float* __restrict__ gam,
-                                                    const float* __restrict__ bet, int64_t HW, float* __restrict__ out,
+                                                    const float* __restrict__ bet, FastDiv dHW, float* __restrict__ out,
                                                     char* __restrict__ os, int64_t M, int64_t rps) {
     const int c4 = blockIdx.x * blockDim.x + threadIdx.x;
     if (c4 >= (C >> 2)) return;
@@ -202,7 +202,7 @@ __global__ __launch_bounds__(256) void k_film_apply(const float* __restrict__ y,
     float4 g = make_float4(0.f, 0.f, 0.f, 0.f), b = g;
     const int64_t r1 = min(M, (int64_t)(blockIdx.y + 1) * rps);
     for (int64_t r = (int64_t)blockIdx.y * rps + threadIdx.y; r < r1; r += blockDim.y) {
-        const int64_t smp = r / HW;
+        const int64_t smp = fdiv(dHW, (uint32_t)r);   // (r / HW: a 64-bit division per row)
         if (smp != cur) {
             cur = smp;
             g = *reinterpret_cast<const float4*>(gam + smp * C + c);
@@ -221,12 +221,14 @@ __global__ __launch_bounds__(256) void k_film_apply(const float* __restrict__ y,
 void film_apply(const float* y, int C, const float* scale, const float* shift, const float* gam, const float* bet,
                 int B, int64_t HW, float* out, hipStream_t st, bool y_bf16, void* os) {
     const int64_t M = (int64_t)B * HW;
+    if (M >= ((int64_t)1 << 32) || HW < 2) throw std::runtime_error("film_apply: layout");
+    const FastDiv dHW = make_fastdiv((uint32_t)HW);
     const int C4 = C >> 2, CX = std::min(C4, 64), RY = std::max(1, 256 / CX);
     const int S = (int)std::max<int64_t>(1, std::min<int64_t>(65535, cdiv(M, (int64_t)RY * 16)));
     const int64_t rps = (M + S - 1) / S;
     char* o = static_cast<char*>(os);
     auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3(cdiv(C4, CX), S), dim3(CX, RY), 0, st, y, C, scale, shift, gam, bet, HW, out, o,
+        hipLaunchKernelGGL(kern, dim3(cdiv(C4, CX), S), dim3(CX, RY), 0, st, y, C, scale, shift, gam, bet, dHW, out, o,
                            M, rps);
     };
     if (os) y_bf16 ? go(k_film_apply<true, true>) : go(k_film_apply<false, true>);

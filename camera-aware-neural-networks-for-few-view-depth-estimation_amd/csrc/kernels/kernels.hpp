@@ -202,6 +202,10 @@ inline FastDiv make_fastdiv(uint32_t d) {
     f.s = l - 1;
     return f;
 }
+__device__ __forceinline__ uint32_t fdiv(const FastDiv& f, uint32_t n) {
+    const uint32_t t = __umulhi(f.m, n);
+    return (t + ((n - t) >> 1)) >> f.s;
+}
 struct PoolAdd {
     const float* d = nullptr;
     const uint8_t* idx = nullptr;

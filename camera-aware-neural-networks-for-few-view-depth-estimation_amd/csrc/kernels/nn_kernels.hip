@@ -145,10 +145,6 @@ struct BnCoef {
 // the folded max-pool backward (PoolAdd): row r of the full-resolution gradient receives the pooled
 // gradient of its window where r is that window's recorded argmax — the same fp32 add the scatter
 // (k_maxpool_bwd_scatter) makes
-__device__ __forceinline__ uint32_t fdiv(const FastDiv& f, uint32_t n) {
-    const uint32_t t = __umulhi(f.m, n);
-    return (t + ((n - t) >> 1)) >> f.s;
-}
 __device__ __forceinline__ float4 pool_add(const PoolAdd& pa, int C, int64_t r, int c, float4 gv) {
     const uint32_t rr = (uint32_t)r, W = (uint32_t)pa.W, H = (uint32_t)pa.H;
     const uint32_t t = fdiv(pa.divW, rr), b = fdiv(pa.divH, t);
@@ -173,6 +169,7 @@ struct OpBnBwd {
     int64_t ldg; int gcoff, C; int64_t HW; bool relu;
     HeadGrad hg;
     PoolAdd pa;
+    FastDiv dHW;   // row -> sample of gmul (rows < 2^32)
     __device__ BnCoef prep(int c4) const {
         BnCoef k;
 #pragma unroll
@@ -193,7 +190,7 @@ struct OpBnBwd {
             gv = load4<GB>(g, r * ldg + gcoff + c4 * 4);
             if constexpr (PA) gv = pool_add(pa, C, r, c4 * 4, gv);
             if (gmul) {
-                const float4 m = *reinterpret_cast<const float4*>(gmul + (r / HW) * C + c4 * 4);
+                const float4 m = *reinterpret_cast<const float4*>(gmul + (int64_t)fdiv(dHW, (uint32_t)r) * C + c4 * 4);
                 gv.x *= m.x; gv.y *= m.y; gv.z *= m.z; gv.w *= m.w;
             }
         }
@@ -269,6 +266,7 @@ template <bool YB, bool GB>
 struct OpBnBwdFilm {
     const float *g, *y, *mean, *invstd, *scale, *shift, *gmul;
     int64_t ldg; int gcoff, C; int64_t HW;
+    FastDiv dHW;   // row -> sample (rows < 2^32)
     __device__ BnCoef prep(int c4) const {
         BnCoef k;
 #pragma unroll
@@ -280,7 +278,7 @@ struct OpBnBwdFilm {
     }
     __device__ void operator()(int64_t r, int c4, double (&acc)[4][4], const BnCoef& k) const {
         const float4 gr = load4<GB>(g, r * ldg + gcoff + c4 * 4);
-        const float4 m = *reinterpret_cast<const float4*>(gmul + (r / HW) * C + c4 * 4);
+        const float4 m = *reinterpret_cast<const float4*>(gmul + (int64_t)fdiv(dHW, (uint32_t)r) * C + c4 * 4);
         const float4 yv = load4<YB>(y, r * C + c4 * 4);
         const float g0[4] = {gr.x, gr.y, gr.z, gr.w}, ga[4] = {gr.x * m.x, gr.y * m.y, gr.z * m.z, gr.w * m.w};
         const float ya[4] = {yv.x, yv.y, yv.z, yv.w};
@@ -358,10 +356,15 @@ void launch_colfinal(const double* part, int S, int N, double* tot, float* dst, 
 }
 }  // namespace
 
-// Up to 2048 slices of >= 256 rows: a level-0 reduction (9.8 M rows x 16 channel quads) then runs
-// 2048 workgroups, ~8 per CU (512 left it latency-bound at 2 per CU).  Monotone in R: the callers'
-// dscr scratch must be sized from colsum_slices() of their largest reduction.
-int colsum_slices(int64_t R) { return (int)std::max<int64_t>(1, std::min<int64_t>(2048, R / 256)); }
+// Up to 2048 slices of >= CAD_COLSLICE_ROWS rows: a level-0 reduction (9.8 M rows x 16 channel quads)
+// then runs 2048 workgroups, ~8 per CU (512 left it latency-bound at 2 per CU), and the deep,
+// wide-channel ones (config 5's 1/16-resolution BNs: 38400 rows x 1024 channels) 4x more than with
+// the round-4 256-row slices.  Monotone in R: the callers' dscr scratch must be sized from
+// colsum_slices() of their largest reduction.
+#ifndef CAD_COLSLICE_ROWS
+#define CAD_COLSLICE_ROWS 64
+#endif
+int colsum_slices(int64_t R) { return (int)std::max<int64_t>(1, std::min<int64_t>(2048, R / CAD_COLSLICE_ROWS)); }
 
 void colsum(const float* x, int64_t ld, int coff, int64_t R, int C, double* part, hipStream_t st) {
     launch_colreduce<1>(OpSum{x, ld, coff}, R, C, part, st);
@@ -548,7 +551,7 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_rows(const float* __restric
                                                           const float* __restrict__ coef, float* __restrict__ dy,
                                                           int64_t M, int64_t rps, const float* __restrict__ gmul,
                                                           int64_t HW, char* __restrict__ os, bool relu, HeadGrad hg,
-                                                          PoolAdd pa) {
+                                                          PoolAdd pa, FastDiv dHW) {
     const int c4 = blockIdx.x * blockDim.x + threadIdx.x;
     if (c4 >= (C >> 2)) return;
     const int c0 = c4 * 4;
@@ -570,7 +573,7 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_rows(const float* __restric
             gv = load4<GB>(g, r * ldg + gcoff + c0);
             if constexpr (PA) gv = pool_add(pa, C, r, c0, gv);
             if (gmul) {
-                const float4 m = *reinterpret_cast<const float4*>(gmul + (r / HW) * C + c0);
+                const float4 m = *reinterpret_cast<const float4*>(gmul + (int64_t)fdiv(dHW, (uint32_t)r) * C + c0);
                 gv.x *= m.x; gv.y *= m.y; gv.z *= m.z; gv.w *= m.w;
             }
         }
@@ -658,6 +661,8 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
     double* tot = scratch;
     double* part = scratch + 2 * C;
     if (tile_part && (film_dgam || tiles <= 0)) throw std::runtime_error("bn_relu_bwd: tile partials");
+    if (gmul && (M >= ((int64_t)1 << 32) || HW < 2)) throw std::runtime_error("bn_relu_bwd: FiLM gradient layout");
+    const FastDiv dHW = make_fastdiv(gmul ? (uint32_t)HW : 2u);
     if (film_dgam) {
         // a FiLM block's bn1: the BN sums and the FiLM affine's per-(sample, channel) sums in one pass,
         // k slices per sample (rows per slice dividing HW; >= 256 rows, <= 2048 slices in all)
@@ -668,16 +673,16 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
         const int S = B * k;
         part = scratch + 4 * C;
         if (y_bf16 && g_bf16)
-            launch_colreduce_slices<4>(OpBnBwdFilm<true, true>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW},
+            launch_colreduce_slices<4>(OpBnBwdFilm<true, true>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW, dHW},
                                        M, C, S, HW / k, part, st);
         else if (y_bf16)
-            launch_colreduce_slices<4>(OpBnBwdFilm<true, false>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW},
+            launch_colreduce_slices<4>(OpBnBwdFilm<true, false>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW, dHW},
                                        M, C, S, HW / k, part, st);
         else if (g_bf16)
-            launch_colreduce_slices<4>(OpBnBwdFilm<false, true>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW},
+            launch_colreduce_slices<4>(OpBnBwdFilm<false, true>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW, dHW},
                                        M, C, S, HW / k, part, st);
         else
-            launch_colreduce_slices<4>(OpBnBwdFilm<false, false>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW},
+            launch_colreduce_slices<4>(OpBnBwdFilm<false, false>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C, HW, dHW},
                                        M, C, S, HW / k, part, st);
         launch_colfinal(part, S, 4 * C, tot, nullptr, 1.f, st);   // tot[0, 2C): the BN sums
         hipLaunchKernelGGL(k_film_from_parts, dim3(cdiv((int64_t)B * C, 256)), dim3(256), 0, st, part, k, C, B,
@@ -732,10 +737,10 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
         : with_mode([&](auto hgc, auto gbc, auto pac) {
         constexpr bool HG = decltype(hgc)::value, GB = decltype(gbc)::value, PA = decltype(pac)::value;
         return y_bf16 ? launch_colreduce<2>(OpBnBwd<true, HG, GB, PA>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff, C,
-                                                                     HW, relu, hg, pa},
+                                                                     HW, relu, hg, pa, dHW},
                                             M, C, part, st)
                       : launch_colreduce<2>(OpBnBwd<false, HG, GB, PA>{g, y, mean, invstd, scale, shift, gmul, ldg, gcoff,
-                                                                      C, HW, relu, hg, pa},
+                                                                      C, HW, relu, hg, pa, dHW},
                                             M, C, part, st);
     });
     if (!film_dgam && !tile_part) launch_colfinal(part, S, 2 * C, tot, nullptr, 1.f, st);
@@ -760,7 +765,7 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
     const RowGrid rg = row_grid(M, C);
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(cdiv(C >> 2, rg.CX), rg.S), dim3(rg.CX, rg.RY), 0, st, g, ldg, gcoff, y, C, mean,
-                           invstd, scale, shift, coef, dy, M, rg.rps, gmul, HW, os, relu, hg, pa);
+                           invstd, scale, shift, coef, dy, M, rg.rps, gmul, HW, os, relu, hg, pa, dHW);
     };
     with_mode([&](auto hgc, auto gbc, auto pac) {
         constexpr bool HG = decltype(hgc)::value, GB = decltype(gbc)::value, PA = decltype(pac)::value;

@@ -17,6 +17,7 @@ ap.add_argument("--b", default="", help="VAR=value[,VAR=value] of arm B")
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--steps", type=int, default=10)
 ap.add_argument("--extra", default="", help="more bench.py arguments")
+ap.add_argument("--c5", action="store_true", help="time configs[4]'s per-GPU step (profiles/c5_step.py) instead")
 args = ap.parse_args()
 
 
@@ -31,16 +32,20 @@ def env_of(spec):
 res = {"A": [], "B": []}
 for rep in range(args.reps):
     for arm, spec in (("A", args.a), ("B", args.b)) if rep % 2 == 0 else (("B", args.b), ("A", args.a)):
-        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", str(args.config), "--steps", str(args.steps),
-               "--warmup", "3", "--no-cpu-baseline", "--no-extra", *args.extra.split()]
+        if args.c5:
+            cmd = [sys.executable, os.path.join(ROOT, "profiles", "c5_step.py"), "--steps", str(args.steps), "--warmup", "3",
+                   *args.extra.split()]
+        else:
+            cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", str(args.config), "--steps",
+                   str(args.steps), "--warmup", "3", "--no-cpu-baseline", "--no-extra", *args.extra.split()]
         r = subprocess.run(cmd, capture_output=True, text=True, env=env_of(spec), timeout=600)
         if r.returncode != 0:
             print(json.dumps({"arm": arm, "spec": spec, "error": r.stderr[-2000:]}), flush=True)
             sys.exit(1)
         d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
         g = (d.get("roofline") or {}).get("all_gemm_kernels") or {}
-        out = {"arm": arm, "spec": spec, "rep": rep, "value": d["value"], "ms_per_step": d["ms_per_step"],
-               "gemm_ms": g.get("ms_per_step")}
+        out = {"arm": arm, "spec": spec, "rep": rep, "value": d.get("value", d.get("images_per_s")),
+               "ms_per_step": d["ms_per_step"], "gemm_ms": g.get("ms_per_step")}
         res[arm].append(out)
         print(json.dumps(out), flush=True)
 ma = statistics.median(r["ms_per_step"] for r in res["A"])
