@@ -470,6 +470,25 @@ __device__ __forceinline__ TileId xcd_tile() {
     return t;
 }
 
+// The same XCD-contiguous walk with y (the N tile) fastest: the N tiles of one M block run back to back
+// on one XCD, so its operand A (a window conv's input rows) is fetched into that XCD's L2 once for all
+// of them instead of once per XCD that holds one of them
+__device__ __forceinline__ TileId xcd_tile_yfast() {
+    const int nx = gridDim.x, ny = gridDim.y;
+    const int nwg = nx * ny * gridDim.z;
+    const int L = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+    int logical = L;
+    if (nwg > 8) {
+        const int q = nwg / 8, r = nwg % 8, xcd = L % 8;
+        logical = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
+    }
+    TileId t;
+    t.y = logical % ny;
+    t.x = (logical / ny) % nx;
+    t.z = logical / (nx * ny);
+    return t;
+}
+
 // A wave whose sub-tile lies entirely past M or N (in the tail tile of a dimension that is not a
 // multiple of the tile: e.g. the 576 = 2.25 x 256 columns of a 64-channel weight gradient) skips its
 // MFMAs, leaving the SIMD to co-resident waves; it still stages operands and joins every barrier.

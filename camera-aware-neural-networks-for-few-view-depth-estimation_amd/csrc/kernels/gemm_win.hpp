@@ -508,7 +508,9 @@ __device__ __forceinline__ void conv3x3_win_ps_body(const GemmArgs& a) {
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
     const int wm = wave / WN, wn = wave % WN;
-    const TileId tile = xcd_tile();
+    // N tiles of one pixel block back to back on one XCD: its input window is fetched into that L2 once
+    // (tools/winlab.py: forward 0.5 %, configs[3] step 0.55 %)
+    const TileId tile = xcd_tile_yfast();
     const int nbx = a.W / CW, nby = (a.H + R - 1) / R;
     const int tx = tile.x % nbx, t2 = tile.x / nbx, ty = t2 % nby, b = t2 / nby;
     const int y0 = ty * R, x0 = tx * CW, n0 = tile.y * BN;
