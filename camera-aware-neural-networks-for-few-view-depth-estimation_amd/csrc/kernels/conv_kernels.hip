@@ -159,6 +159,9 @@ template <int P, int NBUF>
 __global__ __launch_bounds__(256, 2) void k_conv3x3_wgrad_win_bf16d(GemmArgs a) { conv3x3_wgrad_win_dma_body<P, NBUF>(a); }
 template <int P>
 __global__ __launch_bounds__(256, 2) void k_conv3x3_wgrad_strip_bf16d(GemmArgs a) { conv3x3_wgrad_strip_dma_body<P>(a); }
+// ... two output rows per step (P = 16 levels)
+template <int P>
+__global__ __launch_bounds__(256, 2) void k_conv3x3_wgrad_strip2_bf16d(GemmArgs a) { conv3x3_wgrad_strip2_dma_body<P>(a); }
 
 template <int WM, int WN, int KB, class Epi>
 __global__ __launch_bounds__(256) void k_conv3x3_fwd_bf16(GemmArgs a) { conv3x3_fwd_np<1, WM, WN, 2, 2, KB, Epi>(a); }
@@ -1121,11 +1124,27 @@ int wg_nbuf() {
     }();
     return n;
 }
+// strip weight gradients two output rows per step (conv3x3_wgrad_strip2_dma_body; 16- and 32-pixel
+// stages): measured on MI355X (tools/winlab.py, configs[3] shapes) 886 -> 1106 TFLOP/s at level 3,
+// 753 -> 820 / 977 -> 1053 / 1024 -> 1110 at levels 0-2; configs[3] 63.07 -> 61.32 ms/step (same box,
+// bit-identical: each accumulator takes the rows in the same order).  CAD_WGSTRIP2=0: one row per step
+// (A/B switch)
+bool wg_strip2() {
+    static const bool on = [] {
+        const char* e = std::getenv("CAD_WGSTRIP2");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 template <int P>
 void launch_wgrad_win_ps1(GemmArgs& a, float* dw, float* slab, int64_t slab_cap, hipStream_t st) {
     const int cin = a.b_cin;
     const int tiles = (a.M / 64) * (cin / 64);
-    const int nst = a.K / P;
+    const bool dma = wg_dma();
+    const bool strip = dma && wg_strip();
+    const bool strip2 = strip && (P == 16 || P == 32) && wg_strip2();
+    const int RS = strip2 ? 2 : 1;   // output rows per stage
+    const int nst = strip2 ? a.B * (a.W / P) * cdiv(a.H, 2) : a.K / P;
     static const int wgs = [] {   // A/B: CAD_WGSLABS = workgroups the split-K aims for (default 2048)
         const char* e = std::getenv("CAD_WGSLABS");
         return e && e[0] ? std::max(64, std::atoi(e)) : 2048;
@@ -1135,12 +1154,10 @@ void launch_wgrad_win_ps1(GemmArgs& a, float* dw, float* slab, int64_t slab_cap,
     if (slab_cap > 0) s = (int)std::max<int64_t>(1, std::min<int64_t>(s, slab_cap / per));
     // a K-slice is a loader window of 32-bit byte offsets: keep it below 1 GB in either operand (the
     // strip walk's window starts at the slice's first image: one image more)
-    const bool dma = wg_dma();
-    const bool strip = dma && wg_strip();
     const int64_t kbytes = 2 * std::max<int64_t>(a.lda, a.ldb);
     const int64_t img = (int64_t)a.H * a.W;
     auto span_ok = [&](int splits) {
-        const int64_t px = (int64_t)cdiv(nst, splits) * P;
+        const int64_t px = (int64_t)cdiv(nst, splits) * P * RS;
         const int64_t span = strip ? (cdiv(px, img) + 1) * img : px;
         return span * kbytes <= ((int64_t)1 << 30);
     };
@@ -1158,11 +1175,13 @@ void launch_wgrad_win_ps1(GemmArgs& a, float* dw, float* slab, int64_t slab_cap,
     const dim3 grid(a.M / 64, cin / 64, s);
     const int nbuf = wg_nbuf();
     char name[96];
-    if (strip) std::snprintf(name, sizeof name, "void cad::k_conv3x3_wgrad_strip_bf16d<%d>(cad::GemmArgs)", P);
+    if (strip2) std::snprintf(name, sizeof name, "void cad::k_conv3x3_wgrad_strip2_bf16d<%d>(cad::GemmArgs)", P);
+    else if (strip) std::snprintf(name, sizeof name, "void cad::k_conv3x3_wgrad_strip_bf16d<%d>(cad::GemmArgs)", P);
     else if (dma) std::snprintf(name, sizeof name, "void cad::k_conv3x3_wgrad_win_bf16d<%d, %d>(cad::GemmArgs)", P, nbuf);
     else std::snprintf(name, sizeof name, "void cad::k_conv3x3_wgrad_win_bf16p<%d>(cad::GemmArgs)", P);
     if (prof_enabled()) prof_push(name, 2.0 * a.M * a.N * (double)a.K, st);
-    if (strip) hipLaunchKernelGGL(k_conv3x3_wgrad_strip_bf16d<P>, grid, dim3(256), 0, st, a);
+    if (strip2) hipLaunchKernelGGL(k_conv3x3_wgrad_strip2_bf16d<P == 32 ? 32 : 16>, grid, dim3(256), 0, st, a);
+    else if (strip) hipLaunchKernelGGL(k_conv3x3_wgrad_strip_bf16d<P>, grid, dim3(256), 0, st, a);
     else if (dma && nbuf == 2) hipLaunchKernelGGL((k_conv3x3_wgrad_win_bf16d<P, 2>), grid, dim3(256), 0, st, a);
     else if (dma) hipLaunchKernelGGL((k_conv3x3_wgrad_win_bf16d<P, 3>), grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL(k_conv3x3_wgrad_win_bf16p<P>, grid, dim3(256), 0, st, a);

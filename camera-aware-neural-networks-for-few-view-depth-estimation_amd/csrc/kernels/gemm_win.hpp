@@ -1508,6 +1508,169 @@ __device__ __forceinline__ void conv3x3_wgrad_strip_dma_body(const GemmArgs& a) 
         }
 }
 
+// ------------------------------------------------------------------------------------------------
+// The same strip walk two output rows per step (round 5; P = 16 and 32).  One 16-pixel row per step left
+// 9 MFMAs per wave between the DMA issue and the barrier (~0.40 MFMA-busy against 0.53 at P = 32); a
+// stage is now a row PAIR (y, y + 1) of a strip: its step DMAs the two dZ rows and the window rows
+// y + 1, y + 2 (rows y - 1, y came with the previous step, or with the strip's one-step preamble), so
+// 18 (P = 16) or 36 (P = 32) MFMAs per wave share one barrier, and each accumulator still takes the
+// rows in order (the sums are bit-identical to the one-row walk).  Row slot of the
+// window rows of step i: 2 i, 2 i + 1 (mod 8); output row y + q, kernel row ky reads slot 2 i - 2 + q + ky.
+// Stage s -> strip s / HP, pair s % HP (HP = ceil(H / 2)); a pair's second row past H is DMA'd as zeros
+// (its dZ is then 0 and adds nothing).  Host: kstages over B * (W / P) * HP pairs.
+// ------------------------------------------------------------------------------------------------
+template <int P>
+struct Wgs2Geo {
+    static constexpr int NIA = 2 * P / 8;               // DMA instructions of A per step (two dZ rows)
+    static constexpr int NIR = (P + 2 + 7) / 8;         // ... of one window row
+    static constexpr int NI = NIA + 2 * NIR;
+    static constexpr int SLOTS = (NI + 3) / 4;          // per wave
+    static constexpr int WAIT = NI / 4;
+    static constexpr int SA = 2 * P * 128, ROW = NIR * 8 * 128;   // bytes
+    static constexpr int NBUF = 3, NROW = 8;
+};
+
+template <int P>
+__device__ __forceinline__ void conv3x3_wgrad_strip2_dma_body(const GemmArgs& a) {
+    static_assert(P % 16 == 0, "stage");
+    using G = Wgs2Geo<P>;
+    __shared__ __attribute__((aligned(1024))) char lds[G::NBUF * G::SA + G::NROW * G::ROW];
+    char* const ldsB = lds + G::NBUF * G::SA;
+
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int cbk = wave & 1, cib = wave >> 1;
+    const TileId tile = xcd_tile();
+    const int co0 = tile.x * 64, ci0 = tile.y * 64;
+    const int H = a.H, W = a.W;
+    const int segs = W / P, HP = (H + 1) / 2;
+    const int nst = a.B * segs * HP;
+    const int kbeg = tile.z * a.kstages_per_split;
+    const int kend = min(nst, kbeg + a.kstages_per_split);
+
+    const int s0 = min(kbeg, nst - 1);
+    const int b0 = s0 / (segs * HP);
+    const int64_t p0 = (int64_t)b0 * H * W;   // the slice's first image (operand window base)
+    const int64_t pb = p0 - W - 1 > 0 ? p0 - W - 1 : 0;
+    const int rowA = (int)a.lda * 2, rowB = (int)a.ldb * 2;
+    const DmaRsrc rsa = dma_rsrc(ps_at(a.A, (p0 * a.lda + a.a_coff + co0) * 2));
+    const DmaRsrc rsb = dma_rsrc(ps_at(a.Bm, (pb * a.ldb + a.b_coff + ci0) * 2));
+
+    // DMA slot t of this wave: instruction j = wave + 4 t; A (j < NIA): k-row kr of the two-row stage,
+    // dZ row kr / P; window (j >= NIA): row rr of the step's two, k-row kr of that row slot
+    const int lrow = lane >> 3, lch = lane & 7;
+    int sj[G::SLOTS], soff[G::SLOTS], skr[G::SLOTS], srr[G::SLOTS];
+#pragma unroll
+    for (int t = 0; t < G::SLOTS; ++t) {
+        const int j = wave + 4 * t;
+        sj[t] = j < G::NI ? j : -1;
+        if (j < G::NIA) {
+            const int kr = 8 * j + lrow;
+            const int gch = lch ^ (((kr >> 1) & 1) << 2);
+            srr[t] = kr / P;
+            skr[t] = kr;
+            soff[t] = (srr[t] * W + kr - srr[t] * P) * rowA + gch * 16;
+        } else {
+            const int jj = j - G::NIA;
+            const int rr = jj / G::NIR, kr = 8 * (jj - rr * G::NIR) + lrow;
+            const int gch = lch ^ (((kr >> 1) & 1) << 2);
+            srr[t] = rr;
+            skr[t] = kr;
+            soff[t] = (rr * W + kr - 1) * rowB + gch * 16;   // window pixel x0 - 1 + kr of row rr
+        }
+    }
+    // steps: each strip of the slice opens with one preamble step (window rows y0 - 1, y0), then one
+    // step per pair
+    const int nsteps = kbeg < kend ? (kend - kbeg) + ((kend - 1) / HP - kbeg / HP + 1) : 0;
+    int w_strip = kbeg / HP, w_pair = kbeg % HP;
+    bool w_pre = true;
+    int comp = 0;   // bit step % NBUF: the step computes (has an A stage)
+    auto issue = [&](int step) {
+        const int sb = w_strip / segs, sx0 = (w_strip - sb * segs) * P;
+        const int y = 2 * w_pair;
+        const int wr = w_pre ? y - 1 : y + 1;   // first window row this step loads
+        const bool hasA = !w_pre;
+        const int bit = 1 << (step % G::NBUF);
+        comp = hasA ? comp | bit : comp & ~bit;
+        const int64_t rowpix = ((int64_t)sb * H + wr) * W + sx0;
+        const uint32_t da = hasA ? (uint32_t)((((int64_t)sb * H + y) * W + sx0 - p0) * rowA) : 0u;
+        const uint32_t db = (uint32_t)((rowpix - pb) * rowB);
+        char* baseA = lds + (step % G::NBUF) * G::SA;
+#pragma unroll
+        for (int t = 0; t < G::SLOTS; ++t) {
+            const int j = sj[t];
+            if (j < 0) continue;   // wave-uniform
+            if (j < G::NIA) {
+                const bool ok = hasA && y + srr[t] < H;
+                dma16(rsa, baseA + j * 1024, ok ? da + (uint32_t)soff[t] : kOOB);
+            } else {
+                const int jj = j - G::NIA, rr = srr[t];
+                const int xx = sx0 + skr[t] - 1;
+                const bool ok = (unsigned)(wr + rr) < (unsigned)H && skr[t] < P + 2 && (unsigned)xx < (unsigned)W;
+                char* dst = ldsB + ((2 * step + rr) & (G::NROW - 1)) * G::ROW + (jj - rr * G::NIR) * 1024;
+                dma16(rsb, dst, ok ? db + (uint32_t)soff[t] : kOOB);
+            }
+        }
+        // advance: the first pair after the preamble, the next pair, or the next strip's preamble
+        if (w_pre) {
+            w_pre = false;
+        } else if (++w_pair == HP) {
+            ++w_strip; w_pair = 0; w_pre = true;
+        }
+    };
+
+    floatx16 acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+    auto compute = [&](int step) {
+        const char* sa = lds + (step % G::NBUF) * G::SA;
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int qq = 0; qq < P / 16; ++qq) {
+                bf16x8 fa;
+                wgd_frag(sa, cbk * 32, q * P + 16 * qq, fa);
+#pragma unroll
+                for (int ky = 0; ky < 3; ++ky) {
+                    const char* sr = ldsB + ((2 * step - 2 + q + ky) & (G::NROW - 1)) * G::ROW;
+#pragma unroll
+                    for (int kx = 0; kx < 3; ++kx) {
+                        bf16x8 fb;
+                        wgd_frag(sr, cib * 32, kx + 16 * qq, fb);
+                        acc[ky * 3 + kx] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, acc[ky * 3 + kx], 0, 0, 0);
+                    }
+                }
+            }
+    };
+
+    if (nsteps > 0) issue(0);
+    if (nsteps > 1) issue(1);
+    for (int i = 0; i < nsteps; ++i) {
+        if (i + 1 < nsteps) wgd_wait_barrier<G::WAIT>();   // step i landed; i + 1 may still fly
+        else wgd_wait_barrier<0>();
+        const bool ci = (comp >> (i % G::NBUF)) & 1;   // (read before step i + 2 reuses the slot)
+        // step i + 2 reuses the A slot of step i - 1 and the row slots of steps i - 2 (rows 2 i - 4,
+        // 2 i - 3), read last by step i - 1's compute: finished (barrier)
+        if (i + 2 < nsteps) issue(i + 2);
+        if (ci) compute(i);
+    }
+    // slab z: C[z][co][tap*cin + ci] (row stride a.ldc = 9*cin)
+    const int cin = a.b_cin;
+    float* dst = a.C + (int64_t)tile.z * a.slab_stride;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int n = t * cin + ci0 + cib * 32 + (lane & 31);
+            const int co = co0 + cbk * 32 + 4 * (lane >> 5) + 8 * g;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) dst[(int64_t)(co + q) * a.ldc + n] = acc[t][4 * g + q];
+        }
+}
+
 // LDS row image of the DMA kernels below: unpadded 64-B rows (32 bf16) whose 16-B chunk c of row w sits
 // at c ^ ((w >> 2) & 3), the source-side swizzle that keeps the ds_read_b128 fragment reads of 16
 // consecutive rows on disjoint banks.

@@ -166,6 +166,8 @@ def test_conv3x3_wgrad_strided_input(cad, dev):
 WGRAD_BF16_SHAPES = [  # B, H, W, cin, cout, xcoff: the bf16 engine's weight gradient on bf16 twins
     (2, 6, 64, 64, 128, 0),     # window kernel, 32-pixel stages, two per row
     (3, 5, 16, 64, 192, 8),     # 16-pixel stages (W % 32 != 0), halo rows at image edges, channel offset
+    (1, 40, 80, 64, 64, 0),     # 16-pixel strips two rows per step: 100 row pairs over several K-splits
+    (2, 7, 48, 128, 64, 64),    # ... odd H (the last pair's second row past the image), channel offset
     (1, 40, 96, 128, 64, 0),    # 3 stages per row, many K-splits over 120 stages
     (2, 9, 32, 256, 128, 64),   # skip half of a concat-style twin
     (2, 6, 20, 64, 64, 0),      # W % 16 != 0: the im2col GEMM

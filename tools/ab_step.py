@@ -45,7 +45,7 @@ for rep in range(args.reps):
         d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
         g = (d.get("roofline") or {}).get("all_gemm_kernels") or {}
         out = {"arm": arm, "spec": spec, "rep": rep, "value": d.get("value", d.get("images_per_s")),
-               "ms_per_step": d["ms_per_step"], "gemm_ms": g.get("ms_per_step")}
+               "ms_per_step": d["ms_per_step"], "gemm_ms": g.get("ms_per_step"), "loss": d.get("last_loss")}
         res[arm].append(out)
         print(json.dumps(out), flush=True)
 ma = statistics.median(r["ms_per_step"] for r in res["A"])
