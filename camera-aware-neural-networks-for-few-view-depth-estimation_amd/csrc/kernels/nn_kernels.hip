@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <stdexcept>
 #include <type_traits>
+#include <utility>
 
 #include "gemm_s3.hpp"   // split_np (pre-split twins written by the elementwise passes)
 #include "ew_load.hpp"
@@ -32,6 +33,18 @@ inline int ew_blocks(int64_t n) { return (int)std::min<int64_t>(std::max<int64_t
 // ------------------------------------------------------------------------------------------
 // generic deterministic column reduction: part[s][o][c] = sum_{rows r in slice s} op(r, c)[o]
 // ------------------------------------------------------------------------------------------
+// an Op may take its per-thread coefficients per slice (prep_slice(c4, r0, r1): the rows r0 .. r1 - 1 of
+// the workgroup's slice) instead of per channel quad only (prep(c4))
+template <class Op, class = void>
+struct has_prep_slice : std::false_type {};
+template <class Op>
+struct has_prep_slice<Op, std::void_t<decltype(std::declval<const Op&>().prep_slice(0, int64_t{0}, int64_t{0}))>>
+    : std::true_type {};
+template <class Op>
+__device__ __forceinline__ auto prep_of(const Op& op, int c4, int64_t r0, int64_t r1) {
+    if constexpr (has_prep_slice<Op>::value) return op.prep_slice(c4, r0, r1);
+    else return op.prep(c4);
+}
 template <int NOUT, class Op>
 __global__ void k_colreduce(Op op, int64_t R, int C, int64_t rows_per_slice, double* part) {
     const int CX = blockDim.x, RY = blockDim.y;
@@ -45,7 +58,7 @@ __global__ void k_colreduce(Op op, int64_t R, int C, int64_t rows_per_slice, dou
 #pragma unroll
         for (int e = 0; e < 4; ++e) acc[o][e] = 0.0;
     if (c4 < C4) {
-        const auto pc = op.prep(c4);   // per-thread channel coefficients, loaded once
+        const auto pc = prep_of(op, c4, r0, r1);   // per-thread channel coefficients, loaded once
         for (int64_t r = r0 + threadIdx.y; r < r1; r += RY) op(r, c4, acc, pc);
     }
     extern __shared__ double red[];   // [RY][CX][NOUT*4]
@@ -262,23 +275,27 @@ struct OpBnBwdPoolQ {
 // OpBnBwd of a FiLM block (gmul = gamma[b][c]) that also forms the FiLM affine's sums in the same pass
 // over (g, y): acc[2] = sum g a, acc[3] = sum g with g the raw gradient of the FiLM output and a =
 // relu(y scale + shift) (k_film_reduce's sums; slices aligned to samples by the caller)
+struct FilmCoef : BnCoef {
+    float4 m;   // the slice's FiLM gamma (its rows lie in one sample: bn_relu_bwd's sample-aligned slices)
+};
 template <bool YB, bool GB>
 struct OpBnBwdFilm {
     const float *g, *y, *mean, *invstd, *scale, *shift, *gmul;
     int64_t ldg; int gcoff, C; int64_t HW;
     FastDiv dHW;   // row -> sample (rows < 2^32)
-    __device__ BnCoef prep(int c4) const {
-        BnCoef k;
+    __device__ FilmCoef prep_slice(int c4, int64_t r0, int64_t) const {
+        FilmCoef k;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int c = c4 * 4 + e;
             k.sc[e] = scale[c]; k.sh[e] = shift[c]; k.mu[e] = mean[c]; k.is[e] = invstd[c];
         }
+        k.m = *reinterpret_cast<const float4*>(gmul + (int64_t)fdiv(dHW, (uint32_t)r0) * C + c4 * 4);
         return k;
     }
-    __device__ void operator()(int64_t r, int c4, double (&acc)[4][4], const BnCoef& k) const {
+    __device__ void operator()(int64_t r, int c4, double (&acc)[4][4], const FilmCoef& k) const {
         const float4 gr = load4<GB>(g, r * ldg + gcoff + c4 * 4);
-        const float4 m = *reinterpret_cast<const float4*>(gmul + (int64_t)fdiv(dHW, (uint32_t)r) * C + c4 * 4);
+        const float4 m = k.m;
         const float4 yv = load4<YB>(y, r * C + c4 * 4);
         const float g0[4] = {gr.x, gr.y, gr.z, gr.w}, ga[4] = {gr.x * m.x, gr.y * m.y, gr.z * m.z, gr.w * m.w};
         const float ya[4] = {yv.x, yv.y, yv.z, yv.w};
@@ -562,8 +579,16 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_rows(const float* __restric
         k0[e] = coef[c0 + e]; k1[e] = coef[C + c0 + e]; k2[e] = coef[2 * C + c0 + e];
         hw[e] = HG ? hg.w[c0 + e] : 0.f;
     }
-    const int64_t r1 = min(M, (int64_t)(blockIdx.y + 1) * rps);
-    for (int64_t r = (int64_t)blockIdx.y * rps + threadIdx.y; r < r1; r += blockDim.y) {
+    const int64_t r0 = (int64_t)blockIdx.y * rps, r1 = min(M, r0 + rps);
+    // FiLM gamma: loaded once when the block's rows lie in one sample (uniform test), else per row
+    float4 gm = make_float4(1.f, 1.f, 1.f, 1.f);
+    bool gm_row = false;
+    if (gmul && r0 < r1) {
+        const uint32_t s0 = fdiv(dHW, (uint32_t)r0), s1 = fdiv(dHW, (uint32_t)(r1 - 1));
+        gm_row = s0 != s1;
+        if (!gm_row) gm = *reinterpret_cast<const float4*>(gmul + (int64_t)s0 * C + c0);
+    }
+    for (int64_t r = r0 + threadIdx.y; r < r1; r += blockDim.y) {
         float4 gv;
         if constexpr (HG) {
             const float s = hg.sig[r];
@@ -573,7 +598,8 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_rows(const float* __restric
             gv = load4<GB>(g, r * ldg + gcoff + c0);
             if constexpr (PA) gv = pool_add(pa, C, r, c0, gv);
             if (gmul) {
-                const float4 m = *reinterpret_cast<const float4*>(gmul + (int64_t)fdiv(dHW, (uint32_t)r) * C + c0);
+                const float4 m = gm_row ? *reinterpret_cast<const float4*>(gmul + (int64_t)fdiv(dHW, (uint32_t)r) * C + c0)
+                                        : gm;
                 gv.x *= m.x; gv.y *= m.y; gv.z *= m.z; gv.w *= m.w;
             }
         }
