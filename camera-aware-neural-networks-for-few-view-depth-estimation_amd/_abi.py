@@ -149,6 +149,7 @@ SIGNATURES = {
     "cad_unet_debug_buffer": (I64, [P, C.c_char_p, FP, I64]),
     "cad_profile_enable": (I, [I]),
     "cad_profile_reset": (I, []),
+    "cad_profile_only": (I, [C.c_char_p]),
     "cad_profile_report": (I, [C.c_char_p, I]),
     "cad_op_conv3x3_fwd": (I, [P, I64, I, I, P, I, P, I64, I, I, I, I, P]),
     "cad_op_conv3x3_dgrad": (I, [P, I, P, I, P, I64, I, I, I, P]),

@@ -3,9 +3,13 @@
 // (as rocprofv3 prints it) and its algorithmic FLOPs (2*M*N*K).  bench.py reads the aggregate to
 // report roofline.achieved for the dominant kernel; rocprofv3 --kernel-trace --stats of the same
 // command cross-checks the average durations.  Disabled: one predictable branch per launch.
+// cad_profile_only(name): events only around the launches of that kernel (the others are not timed):
+// two event records per launch cost ~5 us of stream time each, so a timed region that brackets every
+// GEMM runs ~1-2 % slower than one that brackets only the kernel whose roofline is reported.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstring>
 #include <map>
 #include <string>
 #include <vector>
@@ -27,6 +31,8 @@ struct ProfState {
     std::vector<Rec> recs;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
     size_t used = 0;
+    std::string only;    // non-empty: time only launches of this kernel
+    bool skipped = false;   // the last push was filtered out (its pop records nothing)
 };
 ProfState& ps() {
     static ProfState s;
@@ -38,6 +44,8 @@ bool prof_enabled() { return ps().on; }
 
 void prof_push(const char* name, double flops, hipStream_t st) {
     ProfState& s = ps();
+    s.skipped = !s.only.empty() && std::strcmp(name, s.only.c_str()) != 0;
+    if (s.skipped) return;
     auto it = s.ids.find(name);
     int id;
     if (it == s.ids.end()) {
@@ -60,6 +68,10 @@ void prof_push(const char* name, double flops, hipStream_t st) {
 
 void prof_pop(hipStream_t st) {
     ProfState& s = ps();
+    if (s.skipped) {
+        s.skipped = false;
+        return;
+    }
     (void)hipEventRecord(s.recs.back().b, st);
 }
 
@@ -69,6 +81,12 @@ extern "C" {
 
 cad_status cad_profile_enable(int on) {
     cad::ps().on = on != 0;
+    return CAD_OK;
+}
+
+cad_status cad_profile_only(const char* kernel_name) {
+    cad::ps().only = kernel_name ? kernel_name : "";
+    cad::ps().skipped = false;
     return CAD_OK;
 }
 

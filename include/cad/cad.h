@@ -406,6 +406,8 @@ int64_t cad_unet_debug_buffer(cad_unet* h, const char* name, float* host, int64_
 /* ---- launch profiler: HIP events around every MFMA GEMM launch on its own stream ---- */
 cad_status cad_profile_enable(int on);
 cad_status cad_profile_reset(void);
+/* time only the launches of the kernel named kernel_name (as the report names it); NULL or "": all */
+cad_status cad_profile_only(const char* kernel_name);
 /* writes a JSON array [{"name","launches","ms","gflop"}...] into buf (synchronises); returns the
  * length needed including the terminator */
 int cad_profile_report(char* buf, int cap);
