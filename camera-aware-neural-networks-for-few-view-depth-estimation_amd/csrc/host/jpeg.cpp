@@ -13,9 +13,16 @@
 //     main controller's context rows are;
 //   * YCbCr -> RGB through the fixed-point tables of jdcolor.c (16 fraction bits);
 //   * JFIF / Adobe APP14 / component-id colour-space inference (jdapimin.c default_decompress_parms).
-// Not supported (clear error): progressive and lossless processes, arithmetic coding, 12-bit samples,
-// CMYK / YCCK (SUN RGB-D's frames are baseline 8-bit YCbCr).  The EXIF orientation tag is applied as
-// cv::imread(IMREAD_COLOR) applies it.
+//   * progressive Huffman scans (T.81 Annex G; libjpeg jdphuff.c): DC first / refinement scans
+//     (interleaved or not), AC first scans with end-of-band runs and AC refinement scans with their
+//     correction bits, coefficients kept for the whole image until the last scan; the same IDCT and
+//     upsampling then apply.
+// Not supported (clear error): lossless processes, arithmetic coding, 12-bit samples, CMYK / YCCK
+// (SUN RGB-D's frames are baseline 8-bit YCbCr), and progressive files whose scans leave any of the
+// first nine AC coefficients short of their last bit — libjpeg-turbo then applies its block
+// smoothing (jdcoefct.c smoothing_ok), which this decoder does not restate; a complete progression
+// (every standard encoder's script) refines every coefficient to bit 0.  The EXIF orientation tag is
+// applied as cv::imread(IMREAD_COLOR) applies it.
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
@@ -161,7 +168,84 @@ struct Component {
     std::vector<int16_t> coef;      // bw * bh * 64, natural order
     std::vector<uint8_t> plane;     // (8 bw) x (8 bh) samples
     int pred = 0;
+    int coef_bits[64];              // progressive: the point transform Al of the last scan of each
+                                    // coefficient (-1: not yet coded), libjpeg's coef_bits
 };
+
+// ------------------------------------------------------------------------------------------------
+// progressive scans (jdphuff.c decode_mcu_DC_first / _DC_refine / _AC_first / _AC_refine); blk is
+// one block's 64 coefficients in natural order, as JCOEF (16-bit) values
+// ------------------------------------------------------------------------------------------------
+void dc_first(Bits& bits, const Huffman& h, Component& c, int al, int16_t* blk) {
+    const int t = bits.decode(h);
+    if (t > 11) throw JpegError("bad DC coefficient");
+    const int diff = t ? extend(bits.get(t), t) : 0;
+    c.pred += diff;
+    blk[0] = (int16_t)((uint32_t)c.pred << al);
+}
+void dc_refine(Bits& bits, int al, int16_t* blk) {
+    if (bits.get(1)) blk[0] = (int16_t)(blk[0] | (1 << al));
+}
+void ac_first(Bits& bits, const Huffman& h, int ss, int se, int al, int& eobrun, int16_t* blk) {
+    if (eobrun > 0) {   // a band of zeros
+        --eobrun;
+        return;
+    }
+    for (int k = ss; k <= se; ++k) {
+        const int rs = bits.decode(h);
+        const int r = rs >> 4, s = rs & 15;
+        if (s) {
+            k += r;
+            blk[kNatural[k]] = (int16_t)((uint32_t)extend(bits.get(s), s) << al);
+        } else if (r == 15) {   // ZRL: 16 zeros
+            k += 15;
+        } else {                // EOBr: 2^r + r appended bits blocks end here
+            eobrun = 1 << r;
+            if (r) eobrun += bits.get(r);
+            --eobrun;
+            break;
+        }
+    }
+}
+void ac_refine(Bits& bits, const Huffman& h, int ss, int se, int al, int& eobrun, int16_t* blk) {
+    const int p1 = 1 << al, m1 = -(1 << al);
+    // a correction bit for an already-nonzero coefficient: 1 = its magnitude grows by p1
+    auto correct = [&](int16_t& v) {
+        if (bits.get(1) && (v & p1) == 0) v = (int16_t)(v + (v >= 0 ? p1 : m1));
+    };
+    int k = ss;
+    if (eobrun == 0) {
+        for (; k <= se; ++k) {
+            const int rs = bits.decode(h);
+            int r = rs >> 4, s = rs & 15;
+            if (s) {   // a newly nonzero coefficient of magnitude p1 (s should be 1)
+                s = bits.get(1) ? p1 : m1;
+            } else if (r != 15) {   // EOBr: the rest of this block is handled by the EOB logic below
+                eobrun = 1 << r;
+                if (r) eobrun += bits.get(r);
+                break;
+            }
+            // advance over already-nonzero coefficients (correction bits) and r still-zero ones
+            do {
+                int16_t& v = blk[kNatural[k]];
+                if (v != 0) {
+                    correct(v);
+                } else if (--r < 0) {
+                    break;   // the target zero coefficient
+                }
+                ++k;
+            } while (k <= se);
+            if (s) blk[kNatural[k]] = (int16_t)s;
+        }
+    }
+    if (eobrun > 0) {   // the remaining positions of a block inside an EOB run: correction bits only
+        for (; k <= se; ++k) {
+            int16_t& v = blk[kNatural[k]];
+            if (v != 0) correct(v);
+        }
+        --eobrun;
+    }
+}
 
 // ------------------------------------------------------------------------------------------------
 // ISLOW inverse DCT (jidctint.c): CONST_BITS 13, PASS1_BITS 2; samples through the post-IDCT
@@ -454,7 +538,7 @@ Decoded decode(const uint8_t* data, size_t size) {
     Huffman dc[4], ac[4];
     std::vector<Component> comps;
     int W = 0, H = 0, hmax = 1, vmax = 1, restart = 0;
-    bool jfif = false, adobe = false, frame = false, any_scan = false;
+    bool jfif = false, adobe = false, frame = false, any_scan = false, progressive = false;
     int adobe_transform = -1, orientation = 1;
 
     auto seg = [&](const uint8_t*& q) -> std::pair<const uint8_t*, int> {
@@ -512,8 +596,9 @@ Decoded decode(const uint8_t* data, size_t size) {
                 adobe = true;
                 adobe_transform = b[11];
             }
-        } else if (m == 0xC0 || m == 0xC1) {                  // SOF0 / SOF1: sequential Huffman
+        } else if (m == 0xC0 || m == 0xC1 || m == 0xC2) {     // SOF0 / SOF1: sequential, SOF2: progressive Huffman
             if (frame) throw JpegError("more than one frame");
+            progressive = m == 0xC2;
             if (n < 6 || b[0] != 8) throw JpegError("only 8-bit JPEG samples are supported");
             H = be16(b + 1);
             W = be16(b + 3);
@@ -538,10 +623,11 @@ Decoded decode(const uint8_t* data, size_t size) {
                 c.dw = (int)(((int64_t)W * c.h + hmax - 1) / hmax);
                 c.dh = (int)(((int64_t)H * c.v + vmax - 1) / vmax);
                 c.coef.assign((size_t)c.bw * c.bh * 64, 0);
+                std::fill(c.coef_bits, c.coef_bits + 64, -1);
             }
             frame = true;
-        } else if (m == 0xC2 || m == 0xC6 || m == 0xCA || m == 0xCE) {
-            throw JpegError("progressive JPEG is not supported");
+        } else if (m == 0xC6 || m == 0xCA || m == 0xCE) {
+            throw JpegError("differential / arithmetic-coded progressive JPEG is not supported");
         } else if (m == 0xC3 || m == 0xC7 || m == 0xCB || m == 0xCF) {
             throw JpegError("lossless JPEG is not supported");
         } else if (m == 0xC9 || m == 0xCA || m == 0xCB || m == 0xCD) {
@@ -560,13 +646,27 @@ Decoded decode(const uint8_t* data, size_t size) {
                 if (!c) throw JpegError("SOS names an unknown component");
                 c->td = b[2 + 2 * i] >> 4;
                 c->ta = b[2 + 2 * i] & 15;
-                if (c->td > 3 || c->ta > 3 || !dc[c->td].defined || !ac[c->ta].defined)
-                    throw JpegError("scan uses an undefined Huffman table");
+                if (c->td > 3 || c->ta > 3) throw JpegError("scan uses an undefined Huffman table");
                 sc.push_back(c);
             }
-            const int ss = b[1 + 2 * ns], se = b[2 + 2 * ns], ahl = b[3 + 2 * ns];
-            if (ss != 0 || se != 63 || ahl != 0) throw JpegError("not a sequential scan");
+            const int ss = b[1 + 2 * ns], se = b[2 + 2 * ns], ah = b[3 + 2 * ns] >> 4, al = b[3 + 2 * ns] & 15;
+            // the Huffman tables the scan decodes with: sequential DC + AC, progressive DC first (DC
+            // tables), AC scans (AC tables), DC refinement (none)
+            const bool need_dc = !progressive || (ss == 0 && ah == 0), need_ac = !progressive || ss > 0;
+            for (Component* c : sc)
+                if ((need_dc && !dc[c->td].defined) || (need_ac && !ac[c->ta].defined))
+                    throw JpegError("scan uses an undefined Huffman table");
+            if (!progressive) {
+                if (ss != 0 || se != 63 || ah != 0 || al != 0) throw JpegError("not a sequential scan");
+            } else {   // jdphuff.c start_pass_phuff_decoder's JERR_BAD_PROGRESSION checks
+                const bool bad = (ss == 0 ? se != 0 : (ss > se || se > 63 || ns != 1)) ||
+                                 (ah != 0 && al != ah - 1) || al > 13;
+                if (bad) throw JpegError("bad progressive scan parameters");
+                for (Component* c : sc)
+                    for (int k = ss; k <= se; ++k) c->coef_bits[k] = al;
+            }
             for (Component* c : sc) c->pred = 0;
+            int eobrun = 0;
             // entropy-coded segment
             Bits bits{p, end};
             int mx, my;
@@ -589,6 +689,7 @@ Decoded decode(const uint8_t* data, size_t size) {
                     bits.p = q;
                     bits.at_marker = false;
                     for (Component* c : sc) c->pred = 0;
+                    eobrun = 0;
                     todo = restart;
                 }
                 const int ux = (int)(u % mx), uy = (int)(u / mx);
@@ -598,6 +699,17 @@ Decoded decode(const uint8_t* data, size_t size) {
                         for (int bx = 0; bx < nbx; ++bx) {
                             const int gx = ux * nbx + bx, gy = uy * nby + by;
                             int16_t* blk = &c->coef[((size_t)gy * c->bw + gx) * 64];
+                            if (progressive) {
+                                if (ss == 0) {
+                                    if (ah == 0) dc_first(bits, dc[c->td], *c, al, blk);
+                                    else dc_refine(bits, al, blk);
+                                } else if (ah == 0) {
+                                    ac_first(bits, ac[c->ta], ss, se, al, eobrun, blk);
+                                } else {
+                                    ac_refine(bits, ac[c->ta], ss, se, al, eobrun, blk);
+                                }
+                                continue;
+                            }
                             const int t = bits.decode(dc[c->td]);
                             if (t > 11) throw JpegError("bad DC coefficient");
                             const int diff = t ? extend(bits.get(t), t) : 0;
@@ -629,6 +741,14 @@ Decoded decode(const uint8_t* data, size_t size) {
         // APPn (other), COM: skipped
     }
     if (!frame || !any_scan) throw JpegError("JPEG file has no image data");
+    if (progressive)   // libjpeg-turbo's output pass would smooth these blocks (jdcoefct.c smoothing_ok)
+        for (const Component& c : comps) {
+            if (c.coef_bits[0] < 0) continue;   // no DC scan: no smoothing either
+            for (int k = 1; k < 10; ++k)
+                if (c.coef_bits[k] != 0)
+                    throw JpegError("progressive JPEG with incompletely refined coefficients (block smoothing) "
+                                    "is not supported");
+        }
 
     // dequantise + inverse DCT every block of every component
     for (Component& c : comps) {

@@ -356,9 +356,10 @@ cad_status cad_aug_sampler_draw(cad_aug_sampler* s, int height, int width, cad_s
  * default) and an existing <path>/intrinsics.txt, in manifest order (paths relative to the working
  * directory, as in the reference).  A sample decodes <path>/image/<first .jpg|.png|.ppm> as RGB u8
  * and <path>/depth/<first .png|.pgm> as u16 (16-bit: metres = value / 1000; 8-bit: value), PNG and
- * binary PNM, and baseline / extended-sequential Huffman JPEG (csrc/host/jpeg.cpp: libjpeg-turbo's
- * default decompression — ISLOW IDCT, fancy upsampling, jdcolor.c YCbCr->RGB — restated bit for bit;
- * progressive / arithmetic / 12-bit / CMYK JPEGs fail with a message). */
+ * binary PNM, and baseline / extended-sequential / progressive Huffman JPEG (csrc/host/jpeg.cpp:
+ * libjpeg-turbo's default decompression — ISLOW IDCT, fancy upsampling, jdcolor.c YCbCr->RGB —
+ * restated bit for bit; arithmetic / lossless / 12-bit / CMYK JPEGs and progressions cut short (which
+ * libjpeg-turbo block-smooths) fail with a message). */
 typedef struct cad_dataset cad_dataset;
 /* decode a JPEG file held in memory (what cv::imread(IMREAD_COLOR) decodes for the loader,
  * sunrgbd_loader.cpp:86,222, before its BGR order): height x width x channels u8 samples (channels 1

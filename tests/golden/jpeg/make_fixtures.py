@@ -25,6 +25,18 @@ CASES = {
     "yuv420_64x64_restart3": (64, 64, False, dict(quality=90, subsampling=2, restart_marker_blocks=3)),
     "yuv420_96x128_restart_rows": (96, 128, False, dict(quality=80, subsampling=2, restart_marker_rows=1)),
 }
+# progressive (libjpeg's jpeg_simple_progression script: DC first / refine, spectral bands, successive
+# approximation with end-of-band runs); image seeds 50+ so the sequential cases keep theirs
+PROG_CASES = {
+    "prog_yuv420_odd_37x53_q90": (37, 53, False, dict(quality=90, subsampling=2, progressive=True)),
+    "prog_yuv444_40x24_q95": (40, 24, False, dict(quality=95, subsampling=0, progressive=True)),
+    "prog_yuv422_48x64_q75_optimized": (48, 64, False, dict(quality=75, subsampling=1, progressive=True, optimize=True)),
+    "prog_gray_33x17_q85": (33, 17, True, dict(quality=85, progressive=True)),
+    "prog_yuv420_64x64_restart3": (64, 64, False, dict(quality=90, subsampling=2, progressive=True,
+                                                        restart_marker_blocks=3)),
+    "prog_yuv420_120x160_q100": (120, 160, False, dict(quality=100, subsampling=2, progressive=True)),
+    "prog_yuv420_16x16_q90": (16, 16, False, dict(quality=90, subsampling=2, progressive=True)),
+}
 
 
 def image(h, w, gray, seed):
@@ -55,6 +67,15 @@ def main():
         dec = np.asarray(Image.open(io.BytesIO(data)).convert("L" if gray else "RGB"))
         np.save(os.path.join(OUT, name + ".npy"), dec)
         meta["cases"][name] = {"shape": list(dec.shape), "bytes": len(data)}
+    for k, (name, (h, w, gray, kw)) in enumerate(sorted(PROG_CASES.items())):
+        bio = io.BytesIO()
+        image(h, w, gray, 50 + k).save(bio, "JPEG", **kw)
+        data = bio.getvalue()
+        with open(os.path.join(OUT, name + ".jpg"), "wb") as fh:
+            fh.write(data)
+        dec = np.asarray(Image.open(io.BytesIO(data)).convert("L" if gray else "RGB"))
+        np.save(os.path.join(OUT, name + ".npy"), dec)
+        meta["cases"][name] = {"shape": list(dec.shape), "bytes": len(data), "progressive": True}
     # EXIF orientation 1..8 (APP1, both TIFF byte orders): the expected pixels are the decode with the
     # orientation applied (PIL ImageOps.exif_transpose; OpenCV's imread(IMREAD_COLOR) applies the tag
     # the same way, loadsave.cpp ExifTransform)
@@ -72,11 +93,14 @@ def main():
         dec = np.asarray(ImageOps.exif_transpose(Image.open(io.BytesIO(data))).convert("RGB"))
         np.save(os.path.join(OUT, name + ".npy"), dec)
         meta["cases"][name] = {"shape": list(dec.shape), "bytes": len(data), "orientation": o}
-    # a progressive file: the decoder refuses it with a message
+    # a progressive file cut after its first three scans (the AC coefficients never refined to bit 0):
+    # libjpeg-turbo would smooth its blocks (jdcoefct.c smoothing_ok); the decoder refuses it
     bio = io.BytesIO()
-    image(16, 16, False, 99).save(bio, "JPEG", quality=90, progressive=True)
-    with open(os.path.join(OUT, "progressive_16x16.jpg"), "wb") as fh:
-        fh.write(bio.getvalue())
+    image(48, 64, False, 99).save(bio, "JPEG", quality=90, subsampling=2, progressive=True)
+    data = bio.getvalue()
+    sos = [i for i in range(len(data) - 1) if data[i] == 0xFF and data[i + 1] == 0xDA]
+    with open(os.path.join(OUT, "progressive_partial_48x64.jpg"), "wb") as fh:
+        fh.write(data[:sos[3]] + b"\xff\xd9")
     with open(os.path.join(OUT, "fixtures.json"), "w") as fh:
         json.dump(meta, fh, indent=1)
 

@@ -2,8 +2,10 @@
 RGB-D's RGB frames with cv::imread(path, IMREAD_COLOR) (src/data/sunrgbd_loader.cpp:86,222), i.e.
 libjpeg-turbo's default decompression.  Fixtures (tests/golden/jpeg, made by make_fixtures.py in the
 build container): files PIL encoded and PIL's own libjpeg-turbo decode of them — 4:2:0 / 4:2:2 /
-4:4:4 / gray, odd and tiny sizes, quality 50..100, optimised Huffman tables, restart intervals, and
-the eight EXIF orientations (applied, as imread(IMREAD_COLOR) applies them).
+4:4:4 / gray, odd and tiny sizes, quality 50..100, optimised Huffman tables, restart intervals,
+progressive files (libjpeg's standard progression: spectral selection and successive approximation,
+interleaved DC scans, end-of-band runs, restart intervals), and the eight EXIF orientations (applied,
+as imread(IMREAD_COLOR) applies them).
 The bar is bit-exact.  CPU only (host decoder)."""
 import ctypes as C
 import glob
@@ -48,12 +50,17 @@ def test_fixture_set_covers_the_decoder_paths():
     names = set(CASES)
     assert {"yuv420_odd_37x53_q90", "yuv422_48x64_q75", "yuv444_16x24_q95", "gray_33x17_q85"} <= names
     assert any("restart" in n for n in names) and any("optimized" in n for n in names)
+    prog = {n for n in names if n.startswith("prog_")}
+    assert {"prog_yuv420_odd_37x53_q90", "prog_gray_33x17_q85", "prog_yuv420_64x64_restart3",
+            "prog_yuv422_48x64_q75_optimized", "prog_yuv444_40x24_q95"} <= prog
 
 
 def test_decoder_errors(cad):
-    prog = open(os.path.join(JDIR, "progressive_16x16.jpg"), "rb").read()
-    with pytest.raises(cad.CadError, match="progressive"):
-        _decode(cad, prog)
+    # a progression cut short: libjpeg-turbo would smooth the blocks whose low AC coefficients lack
+    # their last bits (jdcoefct.c smoothing_ok); the decoder refuses such a file
+    part = open(os.path.join(JDIR, "progressive_partial_48x64.jpg"), "rb").read()
+    with pytest.raises(cad.CadError, match="block smoothing"):
+        _decode(cad, part)
     with pytest.raises(cad.CadError, match="not a JPEG"):
         _decode(cad, b"\x89PNG\r\n\x1a\n" + b"\0" * 32)
     good = open(os.path.join(JDIR, "yuv420_odd_37x53_q90.jpg"), "rb").read()
