@@ -159,12 +159,19 @@ def test_png_palette_and_8bit_depth_and_pil_files(cad, tmp_path):
 
 
 def test_loader_errors(cad, tmp_path):
-    # a JPEG process the decoder does not implement (progressive): a clear message naming the file
+    # a progressive frame decodes as libjpeg-turbo decodes it
     rng = np.random.default_rng(1)
-    m = _one_sample(tmp_path, lambda d: PIL.fromarray(rng.integers(0, 256, (8, 8, 3), dtype=np.uint8)).save(
-                        d / "x.jpg", progressive=True),
+    img = PIL.fromarray(rng.integers(0, 256, (8, 8, 3), dtype=np.uint8))
+    m = _one_sample(tmp_path, lambda d: img.save(d / "x.jpg", progressive=True),
                     lambda d: PIL.fromarray(np.zeros((8, 8), np.uint16)).save(d / "d.png"))
-    with pytest.raises(cad.CadError, match="progressive JPEG is not supported.*x.jpg"):
+    s = cad.SunRGBDDataset(m).read(0)
+    assert np.array_equal(s["rgb"], np.asarray(PIL.open(tmp_path / "s0" / "image" / "x.jpg").convert("RGB")))
+    # a JPEG the decoder does not implement (a progression cut short, which libjpeg-turbo would
+    # block-smooth): a clear message naming the file
+    data = (tmp_path / "s0" / "image" / "x.jpg").read_bytes()
+    sos = [i for i in range(len(data) - 1) if data[i] == 0xFF and data[i + 1] == 0xDA]
+    (tmp_path / "s0" / "image" / "x.jpg").write_bytes(data[:sos[2]] + b"\xff\xd9")
+    with pytest.raises(cad.CadError, match="block smoothing.*x.jpg"):
         cad.SunRGBDDataset(m).read(0)
     with pytest.raises(cad.CadError, match="Cannot open manifest"):
         cad.SunRGBDDataset(tmp_path / "nope.json")
