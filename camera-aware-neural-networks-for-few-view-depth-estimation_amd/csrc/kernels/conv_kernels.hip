@@ -1126,9 +1126,10 @@ int wg_nbuf() {
 }
 // strip weight gradients two output rows per step (conv3x3_wgrad_strip2_dma_body; 16- and 32-pixel
 // stages): measured on MI355X (tools/winlab.py, configs[3] shapes) 886 -> 1106 TFLOP/s at level 3,
-// 753 -> 820 / 977 -> 1053 / 1024 -> 1110 at levels 0-2; configs[3] 63.07 -> 61.32 ms/step (same box,
-// bit-identical: each accumulator takes the rows in the same order).  CAD_WGSTRIP2=0: one row per step
-// (A/B switch)
+// 753 -> 820 / 977 -> 1053 / 1024 -> 1110 at levels 0-2; configs[3] 63.07 -> 61.32 ms/step (same box).
+// Within a K-slice each accumulator takes the rows in the same order as the one-row walk, but slices
+// now split at row pairs, so the split-K partials (and the slab sums) can differ by fp32 rounding.
+// CAD_WGSTRIP2=0: one row per step (A/B switch)
 bool wg_strip2() {
     static const bool on = [] {
         const char* e = std::getenv("CAD_WGSTRIP2");

@@ -1513,8 +1513,9 @@ __device__ __forceinline__ void conv3x3_wgrad_strip_dma_body(const GemmArgs& a) 
 // 9 MFMAs per wave between the DMA issue and the barrier (~0.40 MFMA-busy against 0.53 at P = 32); a
 // stage is now a row PAIR (y, y + 1) of a strip: its step DMAs the two dZ rows and the window rows
 // y + 1, y + 2 (rows y - 1, y came with the previous step, or with the strip's one-step preamble), so
-// 18 (P = 16) or 36 (P = 32) MFMAs per wave share one barrier, and each accumulator still takes the
-// rows in order (the sums are bit-identical to the one-row walk).  Row slot of the
+// 18 (P = 16) or 36 (P = 32) MFMAs per wave share one barrier; within a K-slice each accumulator still
+// takes the rows in order (slices now split at row pairs: the slab partials may differ from the one-row
+// walk's by fp32 rounding).  Row slot of the
 // window rows of step i: 2 i, 2 i + 1 (mod 8); output row y + q, kernel row ky reads slot 2 i - 2 + q + ky.
 // Stage s -> strip s / HP, pair s % HP (HP = ceil(H / 2)); a pair's second row past H is DMA'd as zeros
 // (its dZ is then 0 and adds nothing).  Host: kstages over B * (W / P) * HP pairs.
