@@ -166,6 +166,9 @@ struct cad_resunet {
     bool fp8 = false;          // forward conv-GEMMs on MX-fp8 operands where eligible (x8 units)
     uint8_t *xq = nullptr, *xsc = nullptr;   // MX scratch of the current contraction's A operand
     int64_t xq_cap = 0;
+    // the MX copy a BN-apply pass writes of its output for the next contraction (consumed by it before
+    // the next such pass runs: one buffer serves the whole forward)
+    uint8_t *xqp = nullptr, *xscp = nullptr;
     int64_t nbt = 0;
     std::vector<RParam> params;
     std::vector<RBuf> bufs;
@@ -431,6 +434,8 @@ void layout(cad_resunet* h, Arena& a) {
     h->xq_cap = maxX8;
     h->xq = a.u8(maxX8);
     h->xsc = a.u8(maxX8 / 32);
+    h->xqp = a.u8(maxX8);
+    h->xscp = a.u8(maxX8 / 32);
     int64_t sl = 0;
     for (const RParam& p : h->params)
         if (p.kind == R_CONV) sl = std::max<int64_t>(sl, (int64_t)p.cout * p.Kp * 64);
@@ -530,7 +535,19 @@ cad::Split tw(const void* p, int64_t ld, int coff = 0) {
 // conv of unit u on input twin `in` (B x Hin x Win, ld ldin, coff); y = pre-BN output [Mo][cout]
 // (+ BN partials in train mode), then the BN coefficients.  col: im2col buffer (k > 1 or s > 1 and
 // not the window path); xs: the stride-2 1x1 input subsample buffer.
-void unit_fwd(cad_resunet* h, Unit& u, cad::Split in, int B, int Hin, int Win, void* col, void* xs, hipStream_t st) {
+// the MX-fp8 copy of unit u's input that its producer pass can write (nullptr: u quantises itself —
+// not fp8, or its A operand is an im2col / subsampled copy of the input); C = the input's channels
+const cad::Mx8* preq_for(cad_resunet* h, const Unit& u, int64_t rows, cad::Mx8& m) {
+    const RConv& c = u.c;
+    if (!h->fp8 || !c.x8 || !(c.win || (c.k == 1 && c.s == 1)) || c.cin % 32 || rows * up128(c.cin) > h->xq_cap)
+        return nullptr;
+    m.q = h->xqp; m.s = h->xscp; m.ld = up128(c.cin); m.coff = 0;
+    return &m;
+}
+
+// preq: the input's MX copy, already written by the producing pass (preq_for)
+void unit_fwd(cad_resunet* h, Unit& u, cad::Split in, int B, int Hin, int Win, void* col, void* xs, hipStream_t st,
+              const cad::Mx8* preq = nullptr) {
     RConv& c = u.c;
     const int Ho = (Hin + 2 * c.p - c.k) / c.s + 1, Wo = (Win + 2 * c.p - c.k) / c.s + 1;
     const int64_t Mo = h->M(B, Ho, Wo);
@@ -554,7 +571,8 @@ void unit_fwd(cad_resunet* h, Unit& u, cad::Split in, int B, int Hin, int Win, v
         xa.q = h->xq; xa.s = h->xsc; xa.ld = up128(chans);
         wa.q = c.wq; wa.s = c.wsc; wa.ld = c.ldq;
         if (arows * xa.ld > h->xq_cap) throw RError(CAD_ERR_INVALID, "MX-fp8 scratch too small");
-        cad::mx8_quantize(a.p, true, a.ld, a.coff, chans, arows, xa, st);
+        if (preq && (c.win || (c.k == 1 && c.s == 1)) && preq->ld == xa.ld) xa = *preq;
+        else cad::mx8_quantize(a.p, true, a.ld, a.coff, chans, arows, xa, st);
         if (c.win) {
             cad::conv3x3_fwd_x8(xa, c.cin, wa, c.cout, u.y, c.cout, 0, B, Hin, Win, stats, st, true);
             rows = cad::conv3x3_x8_stats_rows(c.cin, B, Hin, Win, c.cout);
@@ -631,16 +649,25 @@ void forward(cad_resunet* h, const float* rgb, float* depth, int B, hipStream_t 
     // bottlenecks
     const float* xf = h->pool;
     const void* xsw = h->pools;
-    for (Bott& b : h->blocks) {
+    // in fp8 mode each BN-apply pass also writes the MX copy its consumer contracts (preq_for): the
+    // bytes mx8_quantize would write from the twin, without re-reading it
+    const cad::Mx8* pq = nullptr;   // the MX copy of the next block's input, written by bn_add_relu
+    cad::Mx8 mnext;
+    for (size_t bi = 0; bi < h->blocks.size(); ++bi) {
+        Bott& b = h->blocks[bi];
         const int64_t Mi = h->M(B, b.H, b.W), Mo = h->M(B, b.Ho, b.Wo);
-        unit_fwd(h, b.u1, tw(xsw, b.cin), B, b.H, b.W, nullptr, nullptr, st);
-        cad::bn_relu_fwd(b.u1.y, b.w, b.u1.b.scale, b.u1.b.shift, nullptr, b.w, 0, Mi, st, b.t1s, b.w, 0, true);
-        unit_fwd(h, b.u2, tw(b.t1s, b.w), B, b.H, b.W, b.col2, nullptr, st);
-        cad::bn_relu_fwd(b.u2.y, b.w, b.u2.b.scale, b.u2.b.shift, nullptr, b.w, 0, Mo, st, b.t2s, b.w, 0, true);
-        unit_fwd(h, b.u3, tw(b.t2s, b.w), B, b.Ho, b.Wo, nullptr, nullptr, st);
+        cad::Mx8 m2, m3;
+        unit_fwd(h, b.u1, tw(xsw, b.cin), B, b.H, b.W, nullptr, nullptr, st, pq);
+        const cad::Mx8* q2 = preq_for(h, b.u2, Mi, m2);
+        cad::bn_relu_fwd(b.u1.y, b.w, b.u1.b.scale, b.u1.b.shift, nullptr, b.w, 0, Mi, st, b.t1s, b.w, 0, true, q2);
+        unit_fwd(h, b.u2, tw(b.t1s, b.w), B, b.H, b.W, b.col2, nullptr, st, q2);
+        const cad::Mx8* q3 = preq_for(h, b.u3, Mo, m3);
+        cad::bn_relu_fwd(b.u2.y, b.w, b.u2.b.scale, b.u2.b.shift, nullptr, b.w, 0, Mo, st, b.t2s, b.w, 0, true, q3);
+        unit_fwd(h, b.u3, tw(b.t2s, b.w), B, b.Ho, b.Wo, nullptr, nullptr, st, q3);
         if (b.down) unit_fwd(h, b.ud, tw(xsw, b.cin), B, b.H, b.W, nullptr, b.xs, st);
+        pq = bi + 1 < h->blocks.size() ? preq_for(h, h->blocks[bi + 1].u1, Mo, mnext) : nullptr;
         cad::bn_add_relu(b.u3.y, b.u3.b.scale, b.u3.b.shift, b.down ? b.ud.y : nullptr, b.ud.b.scale, b.ud.b.shift, xf,
-                         b.cin, b.cout, Mo, b.out, b.outs, st, true);
+                         b.cin, b.cout, Mo, b.out, b.outs, st, true, pq);
         xf = b.out;
         xsw = b.outs;
     }
@@ -656,8 +683,10 @@ void forward(cad_resunet* h, const float* rgb, float* depth, int B, hipStream_t 
                           static_cast<float*>(d.cats), cc, d.skipC, B, d.H / 2, d.W / 2, st, true);
         if (d.skipC) cad::copy_twin(tw(skips[j], d.skipC), d.skipC, B, d.H, d.W, 1, d.cats, cc, 0, st);
         unit_fwd(h, d.u1, tw(d.cats, cc), B, d.H, d.W, nullptr, nullptr, st);
-        cad::bn_relu_fwd(d.u1.y, d.C, d.u1.b.scale, d.u1.b.shift, nullptr, d.C, 0, Md, st, d.a1s, d.C, 0, true);
-        unit_fwd(h, d.u2, tw(d.a1s, d.C), B, d.H, d.W, nullptr, nullptr, st);
+        cad::Mx8 m2;
+        const cad::Mx8* q2 = preq_for(h, d.u2, Md, m2);
+        cad::bn_relu_fwd(d.u1.y, d.C, d.u1.b.scale, d.u1.b.shift, nullptr, d.C, 0, Md, st, d.a1s, d.C, 0, true, q2);
+        unit_fwd(h, d.u2, tw(d.a1s, d.C), B, d.H, d.W, nullptr, nullptr, st, q2);
         cad::bn_relu_fwd(d.u2.y, d.C, d.u2.b.scale, d.u2.b.shift, d.out, d.C, 0, Md, st, d.outs, d.C, 0, true);
         prev = d.outs;
     }

@@ -25,6 +25,7 @@
 #include "gemm_ps.hpp"
 #include "gemm_win.hpp"
 #include "kernels.hpp"   // Mx8
+#include "mx8_quant.hpp"
 
 namespace cad {
 
@@ -35,25 +36,6 @@ __device__ __forceinline__ i32x8 x8_join(uint4 lo, uint4 hi) {
     f[0] = (int)lo.x; f[1] = (int)lo.y; f[2] = (int)lo.z; f[3] = (int)lo.w;
     f[4] = (int)hi.x; f[5] = (int)hi.y; f[6] = (int)hi.z; f[7] = (int)hi.w;
     return f;
-}
-
-constexpr float kE4M3Max = 448.f;
-
-// shared exponent of a block with max |v| = amax (MX spec: floor(log2 amax) - emax_elem)
-__device__ __forceinline__ int mx8_shared_exp(float amax) {
-    const int e = (int)((__float_as_uint(amax) >> 23) & 0xFF) - 127;   // zero / subnormal: -127
-    const int s = e - 8;
-    return s < -127 ? -127 : (s > 127 ? 127 : s);
-}
-// 2^-shared as an fp32 (shared in [-127, 126] is all this is called with: amax < 2^128)
-__device__ __forceinline__ float mx8_inv_scale(int shared) { return __uint_as_float((uint32_t)(127 - shared) << 23); }
-
-// four values (already multiplied by 2^-shared) -> four e4m3 bytes (round to nearest even, saturated)
-__device__ __forceinline__ uint32_t mx8_pack4(float a, float b, float c, float d) {
-    auto sat = [](float x) { return fminf(fmaxf(x, -kE4M3Max), kE4M3Max); };
-    int w = __builtin_amdgcn_cvt_pk_fp8_f32(sat(a), sat(b), 0, false);
-    w = __builtin_amdgcn_cvt_pk_fp8_f32(sat(c), sat(d), w, true);
-    return (uint32_t)w;
 }
 
 // one 32-element block: v[32] -> 32 element bytes (8 words) + the scale byte

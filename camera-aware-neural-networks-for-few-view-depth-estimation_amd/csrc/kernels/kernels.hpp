@@ -142,7 +142,7 @@ void maxpool3s2_bwd(const float* dout, const uint8_t* idx, int C, int B, int H, 
 // out = relu(y*scale + shift + (yd ? yd*dscale + dshift : x)), fp32 [M][C] + twin
 void bn_add_relu(const float* y, const float* scale, const float* shift, const float* yd, const float* dscale,
                  const float* dshift, const float* x, int64_t ldx, int C, int64_t M, float* out, void* out_split,
-                 hipStream_t st, bool y_bf16 = false);
+                 hipStream_t st, bool y_bf16 = false, const Mx8* qx = nullptr);
 void relu_mask(const float* g, int64_t ldg, int gcoff, const float* out, int C, int64_t M, float* gs, hipStream_t st);
 // dst[(b, S*oy, S*ox)][c] += src[(b, oy, ox)][scoff + c] over the strided grid of a B x H x W image
 void add_strided(float* dst, int64_t lddst, const float* src, int64_t ldsrc, int scoff, int C, int B, int H, int W,
@@ -170,9 +170,11 @@ void bn_eval_coeffs(const float* gamma, const float* beta, const float* run_mean
 // os != nullptr: also writes the output's pre-split twin (split rows of ldos channels at channel
 // offset oscoff, split_planes() planes; see Split below)
 // y_bf16: y holds bf16 values (conv outputs of the bf16 engine; also in bn_relu_bwd, film_*, bn_add_relu)
+// qx != nullptr: also the MX-fp8 copy of the twin (C % 32 == 0, qx->ld % 128 == 0, coff 0; the
+// bytes mx8_quantize would write from the twin)
 void bn_relu_fwd(const float* y, int C, const float* scale, const float* shift, float* out, int64_t ldo,
                  int ocoff, int64_t M, hipStream_t st, void* os = nullptr, int64_t ldos = 0, int oscoff = 0,
-                 bool y_bf16 = false);
+                 bool y_bf16 = false, const Mx8* qx = nullptr);
 // BN+ReLU backward: dy = k1*dz - k2 - k3*xhat, dz = g*[y*scale+shift > 0];
 // writes dgamma/dbeta (grad buffer) and dy (dense [M][C]).  gmul != nullptr: g is first multiplied
 // by gmul[sample][c] (sample = row / HW) — the FiLM gamma sitting between this ReLU and the consumer.

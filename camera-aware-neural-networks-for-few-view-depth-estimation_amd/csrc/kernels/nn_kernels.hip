@@ -16,6 +16,7 @@
 #include "gemm_s3.hpp"   // split_np (pre-split twins written by the elementwise passes)
 #include "ew_load.hpp"
 #include "kernels.hpp"
+#include "mx8_quant.hpp"
 
 namespace cad {
 // The BN apply and the head's dot product are written with explicit fma / mul so that every pass
@@ -498,12 +499,16 @@ inline RowGrid row_grid(int64_t M, int C) {
     g.rps = (M + g.S - 1) / g.S;
     return g;
 }
-template <int NP, bool YB>
+// QX: also the MX-fp8 copy of the twin's (bf16-rounded) values for the next fp8 contraction (q / qs,
+// ldq bytes per row): what k_mx8_quantize would write from the twin, without re-reading it
+template <int NP, bool YB, bool QX = false>
 __global__ __launch_bounds__(256) void k_bn_relu_fwd_rows(const float* __restrict__ y, int C,
                                                           const float* __restrict__ scale,
                                                           const float* __restrict__ shift, float* __restrict__ out,
                                                           int64_t ldo, int ocoff, int64_t M, int64_t rps,
-                                                          char* __restrict__ os, int64_t ldos, int oscoff) {
+                                                          char* __restrict__ os, int64_t ldos, int oscoff,
+                                                          uint8_t* __restrict__ q = nullptr, uint8_t* __restrict__ qs = nullptr,
+                                                          int64_t ldq = 0) {
     const int c4 = blockIdx.x * blockDim.x + threadIdx.x;
     if (c4 >= (C >> 2)) return;
     const int c = c4 * 4;
@@ -519,16 +524,34 @@ __global__ __launch_bounds__(256) void k_bn_relu_fwd_rows(const float* __restric
         o.w = bn_relu1(v.w, s.w, t.w);
         if (out) *reinterpret_cast<float4*>(out + r * ldo + ocoff + c) = o;
         if constexpr (NP > 0) split4_store<NP>(os, ldos, oscoff, r, c, o);
+        if constexpr (QX) {
+            const uint2 t = split_np<1>(o).p[0];   // the twin's values
+            mx8_store_group(make_float4(__uint_as_float(t.x << 16), __uint_as_float(t.x & 0xFFFF0000u),
+                                        __uint_as_float(t.y << 16), __uint_as_float(t.y & 0xFFFF0000u)),
+                            q, qs, ldq, r, c);
+        }
     }
 }
 void bn_relu_fwd(const float* y, int C, const float* scale, const float* shift, float* out, int64_t ldo,
-                 int ocoff, int64_t M, hipStream_t st, void* os, int64_t ldos, int oscoff, bool y_bf16) {
+                 int ocoff, int64_t M, hipStream_t st, void* os, int64_t ldos, int oscoff, bool y_bf16, const Mx8* qx) {
     const int np = os ? split_planes() : 0;
     char* o = static_cast<char*>(os);
     const RowGrid g = row_grid(M, C);
+    if (qx) {
+        if (np != 1 || C % 32 || qx->ld % 128 || qx->coff || !qx->q || !qx->s)
+            throw std::runtime_error("bn_relu_fwd: MX-fp8 copy layout");
+        auto* q = static_cast<uint8_t*>(const_cast<void*>(qx->q));
+        auto* qs = static_cast<uint8_t*>(const_cast<void*>(qx->s));
+        auto goq = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(cdiv(C >> 2, g.CX), g.S), dim3(g.CX, g.RY), 0, st, y, C, scale, shift, out, ldo,
+                               ocoff, M, g.rps, o, ldos, oscoff, q, qs, qx->ld);
+        };
+        y_bf16 ? goq(k_bn_relu_fwd_rows<1, true, true>) : goq(k_bn_relu_fwd_rows<1, false, true>);
+        return;
+    }
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(cdiv(C >> 2, g.CX), g.S), dim3(g.CX, g.RY), 0, st, y, C, scale, shift, out, ldo,
-                           ocoff, M, g.rps, o, ldos, oscoff);
+                           ocoff, M, g.rps, o, ldos, oscoff, nullptr, nullptr, 0);
     };
     if (np == 1) y_bf16 ? go(k_bn_relu_fwd_rows<1, true>) : go(k_bn_relu_fwd_rows<1, false>);
     else y_bf16 ? go(k_bn_relu_fwd_rows<0, true>) : go(k_bn_relu_fwd_rows<0, false>);

@@ -14,6 +14,7 @@
 #include "gemm_s3.hpp"   // split1 (fp32 -> bf16 round-to-nearest-even)
 #include "ew_load.hpp"
 #include "kernels.hpp"
+#include "mx8_quant.hpp"
 
 namespace cad {
 namespace {
@@ -229,11 +230,15 @@ void maxpool3s2_bwd(const float* dout, const uint8_t* idx, int C, int B, int H, 
 // bottleneck join: out = relu(y*s + t + r), r = yd*sd + td (projection shortcut) or x (identity,
 // row stride ldx); out fp32 dense [M][C] and its bf16 twin
 // ------------------------------------------------------------------------------------------
-template <bool YB>
+// QX: also the MX-fp8 copy of the twin's values (q / qs, ldq bytes per row; the next block's first
+// contraction reads it instead of quantising the twin again); needs C % 32 == 0: the 8 lanes of a
+// 32-channel block are consecutive and group-aligned in this grid-stride walk
+template <bool YB, bool QX = false>
 __global__ void k_bn_add_relu(const float* __restrict__ y, const float* __restrict__ s, const float* __restrict__ t,
                               const float* __restrict__ yd, const float* __restrict__ sd, const float* __restrict__ td,
                               const float* __restrict__ x, int64_t ldx, int C, float* __restrict__ out,
-                              uint16_t* __restrict__ os, int64_t n4) {
+                              uint16_t* __restrict__ os, int64_t n4, uint8_t* __restrict__ mq = nullptr,
+                              uint8_t* __restrict__ ms = nullptr, int64_t ldq = 0) {
     const int C4 = C >> 2;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = i / C4;
@@ -251,13 +256,30 @@ __global__ void k_bn_add_relu(const float* __restrict__ y, const float* __restri
         const float4 o = make_float4(fmaxf(v.x * a.x + b.x + q.x, 0.f), fmaxf(v.y * a.y + b.y + q.y, 0.f),
                                      fmaxf(v.z * a.z + b.z + q.z, 0.f), fmaxf(v.w * a.w + b.w + q.w, 0.f));
         *reinterpret_cast<float4*>(out + i * 4) = o;
-        if (os) *reinterpret_cast<uint2*>(os + i * 4) = split1(o).p[0];
+        const uint2 tw = split1(o).p[0];
+        if (os) *reinterpret_cast<uint2*>(os + i * 4) = tw;
+        if constexpr (QX)
+            mx8_store_group(make_float4(__uint_as_float(tw.x << 16), __uint_as_float(tw.x & 0xFFFF0000u),
+                                        __uint_as_float(tw.y << 16), __uint_as_float(tw.y & 0xFFFF0000u)),
+                            mq, ms, ldq, r, c);
     }
 }
 void bn_add_relu(const float* y, const float* scale, const float* shift, const float* yd, const float* dscale,
                  const float* dshift, const float* x, int64_t ldx, int C, int64_t M, float* out, void* out_split,
-                 hipStream_t st, bool y_bf16) {
+                 hipStream_t st, bool y_bf16, const Mx8* qx) {
     const int64_t n4 = M * C / 4;
+    if (qx) {
+        if (C % 32 || qx->ld % 128 || qx->coff || !qx->q || !qx->s) throw std::runtime_error("bn_add_relu: MX-fp8 copy layout");
+        auto* q = static_cast<uint8_t*>(const_cast<void*>(qx->q));
+        auto* qs = static_cast<uint8_t*>(const_cast<void*>(qx->s));
+        if (y_bf16)
+            hipLaunchKernelGGL((k_bn_add_relu<true, true>), dim3(ew_blocks(n4)), dim3(256), 0, st, y, scale, shift, yd, dscale,
+                               dshift, x, ldx, C, out, (uint16_t*)out_split, n4, q, qs, qx->ld);
+        else
+            hipLaunchKernelGGL((k_bn_add_relu<false, true>), dim3(ew_blocks(n4)), dim3(256), 0, st, y, scale, shift, yd,
+                               dscale, dshift, x, ldx, C, out, (uint16_t*)out_split, n4, q, qs, qx->ld);
+        return;
+    }
     if (y_bf16)
         hipLaunchKernelGGL(k_bn_add_relu<true>, dim3(ew_blocks(n4)), dim3(256), 0, st, y, scale, shift, yd, dscale, dshift,
                            x, ldx, C, out, (uint16_t*)out_split, n4);

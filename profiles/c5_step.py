@@ -31,4 +31,5 @@ for _ in range(args.steps):
     m.train_step(loss, rgb, gt, K, pred=pred, dpred=dpred, loss5=l5)
 torch.cuda.synchronize()
 dt = (time.perf_counter() - t0) / max(1, args.steps)
-print(f'{{"ms_per_step": {dt * 1e3:.3f}, "images_per_s": {B / dt:.3f}, "fp8": {str(args.fp8).lower()}}}')
+print(f'{{"ms_per_step": {dt * 1e3:.3f}, "images_per_s": {B / dt:.3f}, "fp8": {str(args.fp8).lower()}, '
+      f'"last_loss": {l5[0].item()!r}}}')
