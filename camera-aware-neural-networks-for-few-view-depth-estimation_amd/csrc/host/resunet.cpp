@@ -605,9 +605,29 @@ void unit_fwd(cad_resunet* h, Unit& u, cad::Split in, int B, int Hin, int Win, v
         cad::bn_eval_coeffs(h->P(b.widx), h->P(b.bidx), b.rm, b.rv, b.C, 1e-5f, b.mean, b.invstd, b.scale, b.shift, st);
 }
 
+// the per-step weight conversions (bf16 twins, dgrad / ConvT repacks, transposes) batched into
+// k_weight_prep launches of up to kWPrepMaxJobs tensors each (one launch per tensor before: ~70 small
+// launches per forward and per backward)
+struct PrepBatch {
+    cad::WPrepList L{};
+    hipStream_t st;
+    explicit PrepBatch(hipStream_t s) : st(s) {}
+    void add(int kind, const float* src, float* d32, void* d16, int cout, int cin, int64_t n) {
+        if (L.njobs == cad::kWPrepMaxJobs) flush();
+        cad::WPrepJob& j = L.job[L.njobs++];
+        j.src = src; j.d32 = d32; j.d16 = d16; j.kind = kind; j.cout = cout; j.cin = cin; j.n = n;
+    }
+    void flush() {
+        if (L.njobs) cad::weight_prep(L, st);
+        L.njobs = 0;
+    }
+    ~PrepBatch() { flush(); }
+};
+
 void prep_weights_fwd(cad_resunet* h, hipStream_t st) {
-    auto sw = [&](RConv& c) {
-        cad::split_rows(h->P(c.pidx), c.Kp, 0, c.Kp, c.cout, c.ws, c.Kp, 0, st);
+    PrepBatch pb(st);
+    auto sw = [&](RConv& c) {   // bf16 twin of [cout][Kp] (split_rows' rounding)
+        pb.add(cad::WPREP_SPLIT, h->P(c.pidx), nullptr, c.ws, c.cout, c.Kp, (int64_t)c.cout * c.Kp);
         if (h->fp8 && c.x8) {
             cad::Mx8 d;
             d.q = c.wq; d.s = c.wsc; d.ld = c.ldq;
@@ -621,8 +641,8 @@ void prep_weights_fwd(cad_resunet* h, hipStream_t st) {
     for (Dec& d : h->dec) {
         sw(d.u1.c);
         sw(d.u2.c);
-        cad::repack_convT_fwd(h->P(d.up_w), d.wf, d.cin_up, d.cout_up, st);
-        cad::split_rows(d.wf, d.cin_up, 0, d.cin_up, 4 * d.cout_up, d.wfs, d.cin_up, 0, st);
+        // repack_convT_fwd + its twin
+        pb.add(cad::WPREP_CONVT, h->P(d.up_w), d.wf, d.wfs, d.cout_up, d.cin_up, (int64_t)4 * d.cout_up * d.cin_up);
     }
 }
 
@@ -698,13 +718,12 @@ void forward(cad_resunet* h, const float* rgb, float* depth, int B, hipStream_t 
 // backward
 // ------------------------------------------------------------------------------------------
 void prep_weights_bwd(cad_resunet* h, hipStream_t st) {
+    PrepBatch pb(st);
     auto dw = [&](RConv& c) {
-        if (c.win) {
-            cad::repack_conv_dgrad(h->P(c.pidx), c.wd, c.cout, c.cin, st);
-            cad::split_rows(c.wd, 9 * c.cout, 0, 9 * c.cout, c.cin, c.wts, 9 * c.cout, 0, st);
-        } else {
-            cad::transpose_split(h->P(c.pidx), c.Kp, c.cout, c.Kp, c.wts, st);
-        }
+        if (c.win)   // repack_conv_dgrad + its twin
+            pb.add(cad::WPREP_DGRAD, h->P(c.pidx), c.wd, c.wts, c.cout, c.cin, (int64_t)c.cout * 9 * c.cin);
+        else         // transpose_split: [cout][Kp] -> bf16 [Kp][cout]
+            pb.add(cad::WPREP_TRANSPOSE, h->P(c.pidx), nullptr, c.wts, c.cout, c.Kp, (int64_t)c.cout * c.Kp);
     };
     for (Bott& b : h->blocks)
         for (Unit* u : {&b.u1, &b.u2, &b.u3, &b.ud})
@@ -712,7 +731,7 @@ void prep_weights_bwd(cad_resunet* h, hipStream_t st) {
     for (Dec& d : h->dec) {
         dw(d.u1.c);
         dw(d.u2.c);
-        cad::split_rows(h->P(d.up_w), 4 * d.cout_up, 0, 4 * d.cout_up, d.cin_up, d.wms, 4 * d.cout_up, 0, st);
+        pb.add(cad::WPREP_SPLIT, h->P(d.up_w), nullptr, d.wms, d.cout_up, d.cin_up, (int64_t)4 * d.cout_up * d.cin_up);
     }
 }
 

@@ -647,16 +647,15 @@ void finish_slabs(float* slab, int splits, int64_t per, float* dw, hipStream_t s
     if (splits >= 2 * G && bx < 512) {
         const int groups = splits / G;   // whole groups; the remainder slabs join level 2 one by one
         slab_reduce(slab, G, per, 1, nullptr, bx, groups, st);
-        // level 2: group heads z = 0, G, 2G, ... then the remainder slabs groups*G .. splits-1
-        slab_reduce(slab, groups, per, G, nullptr, bx, 1, st);
+        // level 2: group heads z = 0, G, 2G, ... then the remainder slabs groups*G .. splits-1.  Without
+        // a remainder the level-2 total goes straight to dw; with one it lands next to the remainder (in
+        // the consumed slab groups*G-1, not a group head) and is summed with it in order
         const int rem = splits - groups * G;
         if (rem == 0) {
-            slab_reduce(slab, 1, per, 1, dw, bx, 1, st);
+            slab_reduce(slab, groups, per, G, dw, bx, 1, st);
         } else {
-            // move the level-2 total next to the remainder (into the consumed slab groups*G-1) and sum
-            // it with the remainder slabs in order
             float* tail = slab + (int64_t)(groups * G - 1) * per;
-            slab_reduce(slab, 1, per, 1, tail, bx, 1, st);
+            slab_reduce(slab, groups, per, G, tail, bx, 1, st);
             slab_reduce(tail, rem + 1, per, 1, dw, bx, 1, st);
         }
         return;

@@ -273,8 +273,10 @@ void repack_convT_fwd(const float* wm, float* wf, int cin, int cout, hipStream_t
 // one weight tensor ->  fp32 repack (d32, optional) and/or its bf16 twin (d16, optional; the
 // k_split_rows<1> rounding).  Kinds: WPREP_SPLIT  [rows][K] -> bf16 same layout;
 // WPREP_DGRAD  OHWI [co][tap][ci] -> [ci][8 - tap][co] (repack_conv_dgrad);
-// WPREP_CONVT  [ci][q][co] -> [q][co][ci] (repack_convT_fwd).  n = elements, a multiple of 8.
-enum { WPREP_SPLIT = 0, WPREP_DGRAD = 1, WPREP_CONVT = 2 };
+// WPREP_CONVT  [ci][q][co] -> [q][co][ci] (repack_convT_fwd);
+// WPREP_TRANSPOSE [cout][cin] -> [cin][cout] (transpose_split: N = cout rows of K = cin).
+// n = elements, a multiple of 8.
+enum { WPREP_SPLIT = 0, WPREP_DGRAD = 1, WPREP_CONVT = 2, WPREP_TRANSPOSE = 3 };
 struct WPrepJob {
     const float* src;
     float* d32;

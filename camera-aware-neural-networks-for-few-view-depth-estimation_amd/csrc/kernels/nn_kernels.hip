@@ -1246,9 +1246,12 @@ __global__ __launch_bounds__(256) void k_weight_prep(WPrepList list) {
             const int64_t t2 = k / jb.cout;
             const int t = (int)(t2 % 9), ci = (int)(t2 / 9);
             src = ((int64_t)co * 9 + (8 - t)) * jb.cin + ci;
-        } else {   // WPREP_CONVT: k = qc*cin + ci  <-  wm[ci][qc]
+        } else if (jb.kind == WPREP_CONVT) {   // k = qc*cin + ci  <-  wm[ci][qc]
             const int ci = (int)(k % jb.cin);
             src = (int64_t)ci * 4 * jb.cout + k / jb.cin;
+        } else {   // WPREP_TRANSPOSE: k = kk*cout + co  <-  w[co][kk]
+            const int co = (int)(k % jb.cout);
+            src = (int64_t)co * jb.cin + k / jb.cout;
         }
         v[e] = jb.src[src];
     }
