@@ -1189,10 +1189,58 @@ void launch_wgrad_win_ps1(GemmArgs& a, float* dw, float* slab, int64_t slab_cap,
     if (s > 1) finish_slabs(slab, s, per, dw, st);
 }
 
+// 32-channel weight gradient as a 64-channel one on pixel pairs (config 5's dec0: cout = cin = 32 at full
+// resolution, which the 64-channel window tiles do not take; the im2col kernel ran it at ~215 TFLOP/s).
+// Dense twins (ld = 32) read as rows of 64 channels are images of W / 2 pixel pairs: channel e 32 + c of
+// pair x' is channel c of pixel 2 x' + e.  The 64 x 64 x 9 window weight gradient of that view,
+// P[(e, co)][(ky, t)][(f, ci)] = sum dZ[y][2x' + e][co] X[y + ky - 1][2x' + 2t + f][ci] (t = -1, 0, 1),
+// holds every horizontal offset dx = 2t + f - e of the 3x3 kernel once per output parity e (the
+// zero padding at x' = -1, W/2 is that of pixels -2, -1, W, W + 1): dW[co][ky][dx][ci] =
+// P(e = 0, the (t, f) with 2t + f = dx) + P(e = 1, 2t + f = dx + 1).  Twice the MFMAs of the 32-channel
+// product (the other blocks are discarded) at the window kernels' rate.
+__global__ void k_wgrad_pair_fold(const float* __restrict__ pr, float* __restrict__ dw) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;   // dw[co][tap][ci], 32 x 9 x 32
+    if (i >= 32 * 288) return;
+    const int co = i / 288, n = i - co * 288, tap = n >> 5, ci = n & 31;
+    const int ky = tap / 3, dx = tap - 3 * ky - 1;
+    const int q0 = dx + 2, t0 = (q0 >> 1) - 1, f0 = q0 & 1;   // e = 0: 2t + f = dx (with q = 2(t + 1) + f)
+    const int q1 = dx + 3, t1 = (q1 >> 1) - 1, f1 = q1 & 1;   // e = 1: 2t + f = dx + 1
+    const float v0 = pr[(int64_t)co * 576 + (ky * 3 + t0 + 1) * 64 + f0 * 32 + ci];
+    const float v1 = pr[(int64_t)(32 + co) * 576 + (ky * 3 + t1 + 1) * 64 + f1 * 32 + ci];
+    dw[i] = v0 + v1;
+}
+bool wg_pair32() {   // CAD_WGPAIR=0: the im2col kernel for the 32-channel weight gradient (A/B switch)
+    static const bool on = [] {
+        const char* e = std::getenv("CAD_WGPAIR");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 void conv3x3_wgrad_ps(Split dz, int cout, Split x, int cin, float* dw, int B, int H, int W, float* slab,
                       int64_t slab_cap, hipStream_t st) {
     ps_check(dz, cout, "conv3x3_wgrad dz");
     ps_check(x, cin, "conv3x3_wgrad x");
+    constexpr int64_t kPairPer = 64 * 576;
+    if (!g_no_wgwin && cout == 32 && cin == 32 && dz.ld == 32 && x.ld == 32 && dz.coff == 0 && x.coff == 0 &&
+        W % 2 == 0 && slab && slab_cap >= 2 * kPairPer && wg_pair32()) {
+        const int P = wgrad_win_ps_stage(64, 64, W / 2);
+        if (P) {
+            GemmArgs a{};
+            a.M = 64; a.N = 576; a.K = B * H * (W / 2);
+            a.B = B; a.H = H; a.W = W / 2;
+            a.A = (const float*)dz.p; a.lda = 64; a.a_coff = 0;
+            a.Bm = (const float*)x.p; a.ldb = 64; a.b_coff = 0; a.b_cin = 64;
+            float* pr = slab + (slab_cap - kPairPer);   // the pair product, after the split-K slabs
+            switch (P) {
+                case 64: launch_wgrad_win_ps1<64>(a, pr, slab, slab_cap - kPairPer, st); break;
+                case 32: launch_wgrad_win_ps1<32>(a, pr, slab, slab_cap - kPairPer, st); break;
+                default: launch_wgrad_win_ps1<16>(a, pr, slab, slab_cap - kPairPer, st); break;
+            }
+            hipLaunchKernelGGL(k_wgrad_pair_fold, dim3(cdiv(32 * 288, 256)), dim3(256), 0, st, pr, dw);
+            return;
+        }
+    }
     GemmArgs a{};
     a.M = cout; a.N = 9 * cin; a.K = B * H * W;
     a.B = B; a.H = H; a.W = W;

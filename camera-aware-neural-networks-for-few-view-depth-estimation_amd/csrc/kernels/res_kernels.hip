@@ -86,11 +86,44 @@ __global__ void k_im2col(const T* __restrict__ x, int64_t ldx, int xcoff, int C,
         *reinterpret_cast<uint4*>(col + po * Kp + k0) = pk;
     }
 }
+// the 4-channel fp32 case (the stem's NHWC4 image): an 8-k group is two taps, each one 16-byte load;
+// one thread per group, 32-bit index arithmetic (the 64-bit divisions of the general kernel made it
+// ~4x slower than its 2-byte stores allow)
+__global__ void k_im2col_c4(const float* __restrict__ x, int ldx, int xcoff, int H, int W, int KW, int taps, int S,
+                            int P, int Ho, int Wo, uint16_t* __restrict__ col, int Kp, uint32_t n8) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n8) return;
+    const uint32_t G = (uint32_t)Kp >> 3;
+    const uint32_t po = i / G, g = i - po * G;
+    const uint32_t ox = po % (uint32_t)Wo, t = po / (uint32_t)Wo;
+    const uint32_t oy = t % (uint32_t)Ho, b = t / (uint32_t)Ho;
+    uint32_t w[4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int tap = 2 * (int)g + h;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (tap < taps) {
+            const int ky = tap / KW, kx = tap - ky * KW;
+            const int iy = (int)oy * S - P + ky, ix = (int)ox * S - P + kx;
+            if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+                v = *reinterpret_cast<const float4*>(x + ((int64_t)((int)b * H + iy) * W + ix) * ldx + xcoff);
+        }
+        w[2 * h] = bf16_bits(v.x) | ((uint32_t)bf16_bits(v.y) << 16);
+        w[2 * h + 1] = bf16_bits(v.z) | ((uint32_t)bf16_bits(v.w) << 16);
+    }
+    *reinterpret_cast<uint4*>(col + (int64_t)po * Kp + g * 8) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 void im2col_f32(const float* x, int64_t ldx, int xcoff, int C, int B, int H, int W, int KH, int KW, int S, int P,
                 void* col, int Kp, hipStream_t st) {
     const int Ho = (H + 2 * P - KH) / S + 1, Wo = (W + 2 * P - KW) / S + 1;
     if (Kp % 8 || Kp < KH * KW * C) throw std::runtime_error("im2col: row padding");
     const int64_t n8 = (int64_t)B * Ho * Wo * (Kp / 8);
+    if (C == 4 && ldx % 4 == 0 && xcoff % 4 == 0 && n8 < ((int64_t)1 << 31) && ldx < ((int64_t)1 << 31)) {
+        hipLaunchKernelGGL(k_im2col_c4, dim3(cdiv(n8, 256)), dim3(256), 0, st, x, (int)ldx, xcoff, H, W, KW, KH * KW, S, P,
+                           Ho, Wo, (uint16_t*)col, Kp, (uint32_t)n8);
+        return;
+    }
     hipLaunchKernelGGL(k_im2col<float>, dim3(ew_blocks(n8)), dim3(256), 0, st, x, ldx, xcoff, C, B, H, W, KH, KW, S, P,
                        Ho, Wo, (uint16_t*)col, Kp, n8);
 }
@@ -189,16 +222,19 @@ void maxpool3s2_fwd(const float* x, int C, int B, int H, int W, float* out, uint
 }
 // gather: dx[(b,iy,ix)][c] = sum over the (<= 4) windows holding (iy,ix) whose argmax is it, in
 // window order; overwrites dx
+// (I: the index type — 32-bit when the element count allows: the 64-bit divisions of the position
+// decode cost more than the kernel's memory traffic)
+template <class I>
 __global__ void k_maxpool3s2_bwd(const float* __restrict__ dout, const uint8_t* __restrict__ idx, int C, int B, int H,
                                  int W, int Ho, int Wo, float* __restrict__ dx, int64_t n4) {
-    const int C4 = C >> 2;
+    const I C4 = (I)(C >> 2);
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t p = i / C4;
-        const int c = (int)(i - p * C4) * 4;
-        const int ix = (int)(p % W);
-        const int64_t t = p / W;
-        const int iy = (int)(t % H);
-        const int b = (int)(t / H);
+        const I p = (I)i / C4;
+        const int c = (int)((I)i - p * C4) * 4;
+        const int ix = (int)(p % (I)W);
+        const I t = p / (I)W;
+        const int iy = (int)(t % (I)H);
+        const int b = (int)(t / (I)H);
         float s[4] = {0.f, 0.f, 0.f, 0.f};
         for (int oy = iy / 2; oy <= (iy + 1) / 2 && oy < Ho; ++oy) {
             const int ky = iy - 2 * oy + 1;
@@ -217,13 +253,18 @@ __global__ void k_maxpool3s2_bwd(const float* __restrict__ dout, const uint8_t* 
                 if (a.w == code) s[3] += d.w;
             }
         }
-        *reinterpret_cast<float4*>(dx + p * C + c) = make_float4(s[0], s[1], s[2], s[3]);
+        *reinterpret_cast<float4*>(dx + (int64_t)p * C + c) = make_float4(s[0], s[1], s[2], s[3]);
     }
 }
 void maxpool3s2_bwd(const float* dout, const uint8_t* idx, int C, int B, int H, int W, float* dx, hipStream_t st) {
     const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
     const int64_t n4 = (int64_t)B * H * W * C / 4;
-    hipLaunchKernelGGL(k_maxpool3s2_bwd, dim3(ew_blocks(n4)), dim3(256), 0, st, dout, idx, C, B, H, W, Ho, Wo, dx, n4);
+    if (n4 < ((int64_t)1 << 31))
+        hipLaunchKernelGGL(k_maxpool3s2_bwd<uint32_t>, dim3(cdiv(n4, 256)), dim3(256), 0, st, dout, idx, C, B, H, W, Ho, Wo,
+                           dx, n4);
+    else
+        hipLaunchKernelGGL(k_maxpool3s2_bwd<int64_t>, dim3(ew_blocks(n4)), dim3(256), 0, st, dout, idx, C, B, H, W, Ho, Wo,
+                           dx, n4);
 }
 
 // ------------------------------------------------------------------------------------------

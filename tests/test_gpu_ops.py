@@ -203,6 +203,30 @@ def test_conv3x3_wgrad_bf16_twins(cad, dev, B, H, W, cin, cout, xcoff):
         lib.cad_set_gemm_engine(prev)
 
 
+@pytest.mark.parametrize("B,H,W", [(2, 6, 64), (1, 9, 32), (3, 7, 128), (2, 5, 36)])
+def test_conv3x3_wgrad_bf16_pair32(cad, dev, B, H, W):
+    """cout = cin = 32 on dense twins: the 64-channel window weight gradient on pixel pairs folded back
+    (k_wgrad_pair_fold; W / 2 = 32, 16 (odd H: the last row pair's second row past the image), 64-wide
+    stages; W / 2 = 18 takes the im2col kernel) against the fp64 contraction of the same bf16 operands."""
+    lib = cad.load_library()
+    prev = lib.cad_get_gemm_engine()
+    assert lib.cad_set_gemm_engine(2) == 0
+    try:
+        g = torch.Generator().manual_seed(B * H * W + 32)
+        x = torch.randn(B, 32, H, W, generator=g).bfloat16()
+        dy = torch.randn(B, 32, H, W, generator=g).bfloat16()
+        wd = torch.zeros(32, 32, 3, 3, dtype=torch.float64, requires_grad=True)
+        F.conv2d(x.double(), wd, None, 1, 1).backward(dy.double())
+        xg, dyg = nhwc(x).to(dev), nhwc(dy).to(dev)
+        dw = torch.full((32, 3, 3, 32), 7.0, device=dev)
+        assert lib.cad_op_conv3x3_wgrad_bf16(_p(dyg), 32, 32, _p(xg), 32, 0, 32, _p(dw), B, H, W, _s()) == 0, \
+            lib.cad_last_error()
+        torch.cuda.synchronize()
+        assert max_rel_err(dw.cpu().permute(0, 3, 1, 2), wd.grad) < TOL
+    finally:
+        lib.cad_set_gemm_engine(prev)
+
+
 def test_conv3x3_wgrad_bf16_needs_bf16_engine(cad, dev):
     lib = cad.load_library()
     prev = lib.cad_get_gemm_engine()
