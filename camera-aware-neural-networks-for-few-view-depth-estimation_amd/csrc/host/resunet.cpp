@@ -738,19 +738,23 @@ void prep_weights_bwd(cad_resunet* h, hipStream_t st) {
 // BN (+ReLU) backward of unit u: g (ld ldg, coff) -> dYs twin; then the conv's wgrad from the
 // input twin `in` (or its col / subsample) and, if dx, its dgrad into dx (ld lddx, overwritten)
 // add: a matrix added to the 1x1 stride-1 dgrad output (the identity shortcut's gradient)
+// g_bf16: g is bf16 rows (ldg elements); dx_bf16: dx is written as bf16 rows (window / 1x1 stride-1
+// dgrads only) — the input gradients of a bottleneck's conv2 / conv3 and of a decoder's conv2, which
+// only the BN backward of the unit below reads
 void unit_bwd(cad_resunet* h, Unit& u, const float* g, int64_t ldg, int gcoff, bool relu, cad::Split in, int B,
               int Hin, int Win, const void* col, const void* xs, float* dx, int64_t lddx, hipStream_t st,
-              const float* add = nullptr) {
+              const float* add = nullptr, bool g_bf16 = false, bool dx_bf16 = false) {
     RConv& c = u.c;
     const int Ho = (Hin + 2 * c.p - c.k) / c.s + 1, Wo = (Win + 2 * c.p - c.k) / c.s + 1;
     const int64_t Mo = h->M(B, Ho, Wo);
     RBN& b = u.b;
     cad::bn_relu_bwd(g, ldg, gcoff, u.y, b.C, b.mean, b.invstd, b.scale, b.shift, h->P(b.widx), Mo, h->dscr, b.coef,
-                     h->G(b.widx), h->G(b.bidx), nullptr, st, nullptr, 1, h->dYs, relu, true);
+                     h->G(b.widx), h->G(b.bidx), nullptr, st, nullptr, 1, h->dYs, relu, true, nullptr, g_bf16);
     const cad::Split dz = tw(h->dYs, c.cout);
+    need(!dx_bf16 || !add, "unit_bwd: a bf16 input gradient with an added matrix");
     if (c.win) {
         cad::conv3x3_wgrad_ps(dz, c.cout, in, c.cin, h->G(c.pidx), B, Hin, Win, h->slab, h->slab_cap, st);
-        if (dx) cad::conv3x3_dgrad_ps(dz, c.cout, tw(c.wts, 9 * c.cout), c.cin, dx, lddx, B, Hin, Win, st);
+        if (dx) cad::conv3x3_dgrad_ps(dz, c.cout, tw(c.wts, 9 * c.cout), c.cin, dx, lddx, B, Hin, Win, st, dx_bf16);
         return;
     }
     cad::Split a = in;
@@ -759,8 +763,11 @@ void unit_bwd(cad_resunet* h, Unit& u, const float* g, int64_t ldg, int gcoff, b
     cad::dense_wgrad_ps(dz, c.cout, a, c.Kp, h->G(c.pidx), c.Kp, Mo, h->slab, h->slab_cap, st);
     if (!dx) return;
     if (c.k == 1 && c.s == 1) {
-        cad::dense_fwd_ps(dz, c.cout, tw(c.wts, c.cout), c.cin, dx, lddx, 0, Mo, nullptr, st, false, add);
-    } else if (c.k == 1) {   // stride-2 1x1: dgrad on the subsampled grid, scattered by the caller
+        cad::dense_fwd_ps(dz, c.cout, tw(c.wts, c.cout), c.cin, dx, lddx, 0, Mo, nullptr, st, dx_bf16, add);
+        return;
+    }
+    need(!dx_bf16, "unit_bwd: bf16 input gradient of a strided / im2col convolution");
+    if (c.k == 1) {   // stride-2 1x1: dgrad on the subsampled grid, scattered by the caller
         cad::dense_fwd_ps(dz, c.cout, tw(c.wts, c.cout), c.cin, dx, c.cin, 0, Mo, nullptr, st);
     } else {
         cad::dense_fwd_ps(dz, c.cout, tw(c.wts, c.cout), c.Kp, h->dcol, c.Kp, 0, Mo, nullptr, st);
@@ -792,8 +799,10 @@ void backward_stage(cad_resunet* h, int stage, const float* ddepth, hipStream_t 
         const void* prev = j == 0 ? h->blocks.back().outs : h->dec[j - 1].outs;
         const int cc = d.skipC + d.cout_up;
         const int64_t Md = h->M(B, d.H, d.W);
-        unit_bwd(h, d.u2, g, d.C, 0, true, tw(d.a1s, d.C), B, d.H, d.W, nullptr, nullptr, h->dT, d.C, st);
-        unit_bwd(h, d.u1, h->dT, d.C, 0, true, tw(d.cats, cc), B, d.H, d.W, nullptr, nullptr, d.dcat, cc, st);
+        unit_bwd(h, d.u2, g, d.C, 0, true, tw(d.a1s, d.C), B, d.H, d.W, nullptr, nullptr, h->dT, d.C, st, nullptr,
+                 false, true);
+        unit_bwd(h, d.u1, h->dT, d.C, 0, true, tw(d.cats, cc), B, d.H, d.W, nullptr, nullptr, d.dcat, cc, st, nullptr,
+                 true);
         // ConvTranspose backward on the up half of dcat
         cad::split_rows(d.dcat, cc, d.skipC, d.cout_up, Md, h->dYs, d.cout_up, 0, st);
         cad::convT_wgrad_ps(tw(prev, d.cin_up), d.cin_up, tw(h->dYs, d.cout_up), d.cout_up, h->G(d.up_w), B, d.H / 2,
@@ -820,11 +829,15 @@ void backward_stage(cad_resunet* h, int stage, const float* ddepth, hipStream_t 
         const int64_t Mo = h->M(B, b.Ho, b.Wo);
         cad::relu_mask(g, b.cout, 0, b.out, b.cout, Mo, h->gS, st);
         float* gn = g == h->gA ? h->gB : h->gA;   // gradient of the block input
-        unit_bwd(h, b.u3, h->gS, b.cout, 0, false, tw(b.t2s, b.w), B, b.Ho, b.Wo, nullptr, nullptr, h->dT, b.w, st);
-        unit_bwd(h, b.u2, h->dT, b.w, 0, true, tw(b.t1s, b.w), B, b.H, b.W, b.col2, nullptr, h->dT, b.w, st);
+        // conv3's and (stride 1) conv2's input gradients stored as bf16 (unit_bwd)
+        const bool g2 = b.u2.c.win;
+        unit_bwd(h, b.u3, h->gS, b.cout, 0, false, tw(b.t2s, b.w), B, b.Ho, b.Wo, nullptr, nullptr, h->dT, b.w, st,
+                 nullptr, false, true);
+        unit_bwd(h, b.u2, h->dT, b.w, 0, true, tw(b.t1s, b.w), B, b.H, b.W, b.col2, nullptr, h->dT, b.w, st, nullptr,
+                 true, g2);
         // identity shortcut: its gradient gS is added inside conv1's dgrad epilogue
         unit_bwd(h, b.u1, h->dT, b.w, 0, true, tw(xsw, b.cin), B, b.H, b.W, nullptr, nullptr, gn, b.cin, st,
-                 b.down ? nullptr : h->gS);
+                 b.down ? nullptr : h->gS, g2);
         if (b.down) {
             unit_bwd(h, b.ud, h->gS, b.cout, 0, false, tw(xsw, b.cin), B, b.H, b.W, nullptr, b.xs, h->dT, b.cin, st);
             cad::add_strided(gn, b.cin, h->dT, b.cin, 0, b.cin, B, b.H, b.W, b.s, st);

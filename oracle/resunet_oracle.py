@@ -161,10 +161,17 @@ def _conv(x, w, stride, pad):
     return O._RoundOperand.apply(O._RoundGradOperand.apply(y)) if mode in ("bf16", "mx8") else y
 
 
+def _rgrad(x):
+    """bf16 / mx8: the input gradient of this convolution stored as bf16 (resunet.cpp unit_bwd dx_bf16:
+    a bottleneck's conv3 and stride-1 conv2, a decoder's conv2 — read only by the BN backward below)"""
+    return O._RoundGradOperand.apply(x) if O._GEMM["operands"] in ("bf16", "mx8") else x
+
+
 def _bottleneck(x, p, bufs, pre, stride, down, train):
     t = F.relu(O._bn(_conv(x, p[pre + "conv1.weight"], 1, 0), p, bufs, pre + "bn1", train))
-    t = F.relu(O._bn(_conv(t, p[pre + "conv2.weight"], stride, 1), p, bufs, pre + "bn2", train))
-    t = O._bn(_conv(t, p[pre + "conv3.weight"], 1, 0), p, bufs, pre + "bn3", train)
+    t = F.relu(O._bn(_conv(_rgrad(t) if stride == 1 else t, p[pre + "conv2.weight"], stride, 1), p, bufs, pre + "bn2",
+                     train))
+    t = O._bn(_conv(_rgrad(t), p[pre + "conv3.weight"], 1, 0), p, bufs, pre + "bn3", train)
     sc = O._bn(_conv(x, p[pre + "downsample.0.weight"], stride, 0), p, bufs, pre + "downsample.1", train) if down else x
     return F.relu(t + sc)
 
@@ -183,7 +190,7 @@ def forward(x, p, bufs, train=True, max_depth=10.0):
         up = O._convT2x2(y, p[pre + "up.weight"], p[pre + "up.bias"])
         y = torch.cat([skips[l], up], 1) if sk else up
         y = F.relu(O._bn(_conv(y, p[pre + "conv.conv1.weight"], 1, 1), p, bufs, pre + "conv.bn1", train))
-        y = F.relu(O._bn(_conv(y, p[pre + "conv.conv2.weight"], 1, 1), p, bufs, pre + "conv.bn2", train))
+        y = F.relu(O._bn(_conv(_rgrad(y), p[pre + "conv.conv2.weight"], 1, 1), p, bufs, pre + "conv.bn2", train))
     z = F.conv2d(y, p["out_conv.weight"], p["out_conv.bias"])
     return torch.sigmoid(z) * max_depth
 
