@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
@@ -201,6 +202,7 @@ struct cad_resunet {
     // staged backward (data-parallel exchange, dp.cpp): the gradient of the current stage's output,
     // and each stage's contiguous slab range [off, off + cnt)
     float* bwd_g = nullptr;
+    bool bwd_masked = false;   // bwd_g already carries the ReLU mask of the block whose output it is
     std::vector<std::pair<int64_t, int64_t>> stage_range;
     float* P(int i) const { return flat_p + params[i].off; }
     float* G(int i) const { return flat_g + params[i].off; }
@@ -743,7 +745,7 @@ void prep_weights_bwd(cad_resunet* h, hipStream_t st) {
 // only the BN backward of the unit below reads
 void unit_bwd(cad_resunet* h, Unit& u, const float* g, int64_t ldg, int gcoff, bool relu, cad::Split in, int B,
               int Hin, int Win, const void* col, const void* xs, float* dx, int64_t lddx, hipStream_t st,
-              const float* add = nullptr, bool g_bf16 = false, bool dx_bf16 = false) {
+              const float* add = nullptr, bool g_bf16 = false, bool dx_bf16 = false, const float* mask = nullptr) {
     RConv& c = u.c;
     const int Ho = (Hin + 2 * c.p - c.k) / c.s + 1, Wo = (Win + 2 * c.p - c.k) / c.s + 1;
     const int64_t Mo = h->M(B, Ho, Wo);
@@ -763,10 +765,10 @@ void unit_bwd(cad_resunet* h, Unit& u, const float* g, int64_t ldg, int gcoff, b
     cad::dense_wgrad_ps(dz, c.cout, a, c.Kp, h->G(c.pidx), c.Kp, Mo, h->slab, h->slab_cap, st);
     if (!dx) return;
     if (c.k == 1 && c.s == 1) {
-        cad::dense_fwd_ps(dz, c.cout, tw(c.wts, c.cout), c.cin, dx, lddx, 0, Mo, nullptr, st, dx_bf16, add);
+        cad::dense_fwd_ps(dz, c.cout, tw(c.wts, c.cout), c.cin, dx, lddx, 0, Mo, nullptr, st, dx_bf16, add, mask);
         return;
     }
-    need(!dx_bf16, "unit_bwd: bf16 input gradient of a strided / im2col convolution");
+    need(!dx_bf16 && !mask, "unit_bwd: bf16 / masked input gradient of a strided / im2col convolution");
     if (c.k == 1) {   // stride-2 1x1: dgrad on the subsampled grid, scattered by the caller
         cad::dense_fwd_ps(dz, c.cout, tw(c.wts, c.cout), c.cin, dx, c.cin, 0, Mo, nullptr, st);
     } else {
@@ -781,6 +783,15 @@ void unit_bwd(cad_resunet* h, Unit& u, const float* g, int64_t ldg, int gcoff, b
 // range, so the data-parallel exchange can all-reduce a finished range while later stages run.
 int num_stages(const cad_resunet* h) { return 6 + (int)h->blocks.size() + 1; }
 
+// CAD_MASKFUSE=0: the separate k_relu_mask pass for every block (A/B switch; bit-identical)
+bool mask_fuse_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("CAD_MASKFUSE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 void backward_stage(cad_resunet* h, int stage, const float* ddepth, hipStream_t st) {
     const int B = h->fwd_B;
     const int nb = (int)h->blocks.size();
@@ -788,6 +799,7 @@ void backward_stage(cad_resunet* h, int stage, const float* ddepth, hipStream_t 
         prep_weights_bwd(h, st);
         Dec& d0 = h->dec.back();
         h->bwd_g = h->gA;
+        h->bwd_masked = false;
         cad::head_bwd(d0.out, 32, h->P(h->head_w), ddepth, h->sig, h->max_depth, h->bwd_g, h->M(B, h->H, h->W),
                       h->dscr, h->G(h->head_w), h->G(h->head_b), st);
         return;
@@ -813,6 +825,7 @@ void backward_stage(cad_resunet* h, int stage, const float* ddepth, hipStream_t 
         cad::convT_dgrad_ps(tw(h->dYs, d.cout_up), d.cout_up, tw(d.wms, 4 * d.cout_up), d.cin_up, gn, B, d.H / 2,
                             d.W / 2, st);
         h->bwd_g = gn;
+        h->bwd_masked = false;
         return;
     }
     if (stage < 6 + nb) {   // encoder bottleneck block bi; g = gradient of its output
@@ -822,27 +835,36 @@ void backward_stage(cad_resunet* h, int stage, const float* ddepth, hipStream_t 
         // skip gradients of the decoder concat (x4 = layer3, x3 = layer2, x2 = layer1 outputs)
         for (int L = 0; L < 3; ++L)
             if (bi == stage_last[L]) {
+                need(!h->bwd_masked, "resunet backward: a masked gradient at a skip block");
                 const Dec& d = h->dec[2 - L];
                 cad::add_strided(g, b.cout, d.dcat, d.skipC + d.cout_up, 0, b.cout, B, b.Ho, b.Wo, 1, st);
             }
         const void* xsw = bi ? h->blocks[bi - 1].outs : h->pools;
         const int64_t Mo = h->M(B, b.Ho, b.Wo);
-        cad::relu_mask(g, b.cout, 0, b.out, b.cout, Mo, h->gS, st);
+        // gS = g [out > 0]: already so when the next block's conv1 dgrad epilogue applied the mask
+        float* gS = h->bwd_masked ? g : h->gS;
+        if (!h->bwd_masked) cad::relu_mask(g, b.cout, 0, b.out, b.cout, Mo, h->gS, st);
         float* gn = g == h->gA ? h->gB : h->gA;   // gradient of the block input
+        // identity shortcut (bi > 0: the input is block bi - 1's output, no skip add lands on it — a
+        // layer's last block is followed by a projection block): the conv1 dgrad epilogue adds gS and
+        // applies block bi - 1's ReLU mask (k_relu_mask fused)
+        const bool fuse_mask = !b.down && bi > 0 && mask_fuse_on();
+        const float* mask = fuse_mask ? h->blocks[bi - 1].out : nullptr;
         // conv3's and (stride 1) conv2's input gradients stored as bf16 (unit_bwd)
         const bool g2 = b.u2.c.win;
-        unit_bwd(h, b.u3, h->gS, b.cout, 0, false, tw(b.t2s, b.w), B, b.Ho, b.Wo, nullptr, nullptr, h->dT, b.w, st,
+        unit_bwd(h, b.u3, gS, b.cout, 0, false, tw(b.t2s, b.w), B, b.Ho, b.Wo, nullptr, nullptr, h->dT, b.w, st,
                  nullptr, false, true);
         unit_bwd(h, b.u2, h->dT, b.w, 0, true, tw(b.t1s, b.w), B, b.H, b.W, b.col2, nullptr, h->dT, b.w, st, nullptr,
                  true, g2);
         // identity shortcut: its gradient gS is added inside conv1's dgrad epilogue
         unit_bwd(h, b.u1, h->dT, b.w, 0, true, tw(xsw, b.cin), B, b.H, b.W, nullptr, nullptr, gn, b.cin, st,
-                 b.down ? nullptr : h->gS, g2);
+                 b.down ? nullptr : gS, g2, false, mask);
         if (b.down) {
-            unit_bwd(h, b.ud, h->gS, b.cout, 0, false, tw(xsw, b.cin), B, b.H, b.W, nullptr, b.xs, h->dT, b.cin, st);
+            unit_bwd(h, b.ud, gS, b.cout, 0, false, tw(xsw, b.cin), B, b.H, b.W, nullptr, b.xs, h->dT, b.cin, st);
             cad::add_strided(gn, b.cin, h->dT, b.cin, 0, b.cin, B, b.H, b.W, b.s, st);
         }
         h->bwd_g = gn;
+        h->bwd_masked = fuse_mask;
         return;
     }
     // stem: max-pool backward, the dec1 skip gradient (x1), bn1 + relu, conv1 weight gradient

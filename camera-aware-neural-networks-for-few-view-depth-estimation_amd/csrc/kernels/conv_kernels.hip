@@ -1268,7 +1268,8 @@ int dense_stats_rows(int64_t M, int N) { return cdiv(M, tile_m(pick_cfg((int)M, 
 
 void launch_dense_dma(void (*fn)(GemmArgs), const char* name, const GemmArgs& a, hipStream_t st);
 void dense_fwd_ps(Split x, int K, Split w, int N, float* y, int64_t ldy, int ycoff, int64_t M, float* stats,
-                  hipStream_t st, bool y_bf16, const float* add) {
+                  hipStream_t st, bool y_bf16, const float* add, const float* mask) {
+    if (mask && !add) throw std::runtime_error("dense GEMM: a mask needs the added matrix");
     ps_check(x, K, "dense x");
     ps_check(w, K, "dense w");
     if (M > INT32_MAX) throw std::runtime_error("dense GEMM: too many rows");
@@ -1280,6 +1281,7 @@ void dense_fwd_ps(Split x, int K, Split w, int N, float* y, int64_t ldy, int yco
     a.C = y; a.ldc = ldy; a.c_coff = ycoff;
     a.stats = stats;
     a.bias = add;
+    a.C2 = const_cast<float*>(mask);
     const Cfg c = pick_cfg(a.M, a.N);
     const int kb = ps_kb(true, c);
     a.kstages_per_split = cdiv(a.K, kb);
@@ -1291,7 +1293,9 @@ void dense_fwd_ps(Split x, int K, Split w, int N, float* y, int64_t ldy, int yco
     }();
     if (ddma && c == C22 && K % 8 == 0 && x.ld % 8 == 0 && x.coff % 8 == 0 && w.ld % 8 == 0 && w.coff % 8 == 0) {
         if (add && (stats || y_bf16)) throw std::runtime_error("dense GEMM: the added matrix needs fp32 output");
-        if (add) launch_dense_dma(k_dense_bf16d<EpiStoreAdd>, "void cad::k_dense_bf16d<cad::EpiStoreAdd>(cad::GemmArgs)", a, st);
+        if (add && mask)
+            launch_dense_dma(k_dense_bf16d<EpiStoreAddMask>, "void cad::k_dense_bf16d<cad::EpiStoreAddMask>(cad::GemmArgs)", a, st);
+        else if (add) launch_dense_dma(k_dense_bf16d<EpiStoreAdd>, "void cad::k_dense_bf16d<cad::EpiStoreAdd>(cad::GemmArgs)", a, st);
         else if (y_bf16 && stats)
             launch_dense_dma(k_dense_bf16d<EpiStoreStatsB16>, "void cad::k_dense_bf16d<cad::EpiStoreStatsB16>(cad::GemmArgs)", a, st);
         else if (y_bf16) launch_dense_dma(k_dense_bf16d<EpiStoreB16>, "void cad::k_dense_bf16d<cad::EpiStoreB16>(cad::GemmArgs)", a, st);
@@ -1302,6 +1306,7 @@ void dense_fwd_ps(Split x, int K, Split w, int N, float* y, int64_t ldy, int yco
     if (add) {
         if (stats || y_bf16) throw std::runtime_error("dense GEMM: the added matrix needs fp32 output");
         launch_kb<KDenseAddP1, 32, 64>(c, kb, a, 1, st);
+        if (mask) mask_inplace(y, ldy, ycoff, mask, N, M, st);   // (the register-staged kernels: a pass)
     } else if (y_bf16) {
         if (stats) launch_kb<KDenseSP1B, 32, 64>(c, kb, a, 1, st);
         else launch_kb<KDenseP1B, 32, 64>(c, kb, a, 1, st);

@@ -28,6 +28,14 @@ struct EpiStoreAdd : EpiStore {
         return a.bias + (int64_t)m0 * a.ldc + a.c_coff;
     }
 };
+// ... then zeroed where the fp32 matrix a.C2 (same rows / offset as C) is not > 0: config 5's block-input
+// gradient masked by the previous block's ReLU output (the separate k_relu_mask pass, fused)
+struct EpiStoreAddMask : EpiStoreAdd {
+    static constexpr bool MASK = true;
+    __device__ static const float* mask_base(const GemmArgs& a, int m0) {
+        return static_cast<const float*>(a.C2) + (int64_t)m0 * a.ldc + a.c_coff;
+    }
+};
 // bf16 outputs (round-to-nearest-even; a.C addresses bf16 rows of ldc elements): the pre-BN conv
 // outputs of the bf16 engine.  BN partials are taken from the rounded values BN normalises.
 struct EpiStoreB16 {

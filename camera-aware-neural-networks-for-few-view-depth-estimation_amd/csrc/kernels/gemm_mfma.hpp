@@ -435,6 +435,10 @@ struct has_wave_store : std::false_type {};   // a structured epilogue that may 
 template <class E>
 struct has_wave_store<E, std::void_t<decltype(E::WAVE_STORE)>> : std::integral_constant<bool, E::WAVE_STORE> {};
 template <class E, class = void>
+struct has_mask : std::false_type {};   // an ADD epilogue that also zeroes where its mask matrix is not > 0
+template <class E>
+struct has_mask<E, std::void_t<decltype(E::MASK)>> : std::integral_constant<bool, E::MASK> {};
+template <class E, class = void>
 struct has_prefetch : std::false_type {};   // a structured epilogue that loads its operands for all blocks first
 template <class E>
 struct has_prefetch<E, std::void_t<decltype(E::PREFETCH)>> : std::integral_constant<bool, E::PREFETCH> {};
@@ -667,6 +671,11 @@ __device__ __forceinline__ void gemm_epilogue_t(const GemmArgs& a, const floatx1
         else return rs;
     };
     const __amdgpu_buffer_rsrc_t rsadd = add_rsrc();
+    auto mask_rsrc = [&]() {
+        if constexpr (has_mask<Epi>::value) return make_rsrc(Epi::mask_base(a, m0), (uint32_t)(bytes < (int64_t)kRecords ? bytes : kRecords));
+        else return rs;
+    };
+    [[maybe_unused]] const __amdgpu_buffer_rsrc_t rsmask = mask_rsrc();
     // the wave's MI x NJ blocks staged through its own LDS slice and stored as 16-byte pieces (when the
     // epilogue's layout allows: wave_store returns false otherwise)
     if constexpr (has_wave_store<Epi>::value) {
@@ -707,6 +716,14 @@ __device__ __forceinline__ void gemm_epilogue_t(const GemmArgs& a, const floatx1
                     for (int r = 0; r < 4; ++r)
                         v[r] += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                                               rsadd, lo + (uint32_t)(r * ldc4), 0, 0));
+                    if constexpr (has_mask<Epi>::value) {   // v [mask > 0] (k_relu_mask's arithmetic)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const float mk = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                                           rsmask, lo + (uint32_t)(r * ldc4), 0, 0));
+                            v[r] = mk > 0.f ? v[r] : 0.f;
+                        }
+                    }
                 }
                 if constexpr (Epi::BF16) {   // the stored (rounded) values, which BN then normalises
 #pragma unroll

@@ -98,8 +98,12 @@ void convT_wgrad_ps(Split x, int cin, Split g, int cout, float* dw, int B, int H
 // ---- dense GEMMs on the pre-split twins (the 1x1 / im2col convolutions of the config-5 network) ----
 // y[m][ycoff + n] = sum_k x[m][k] w[n][k]  (+ BN partials [rows][2][N] when stats != nullptr)
 // add != nullptr: y = x w^T + add (add rows with y's stride and offset; fp32 output, no stats)
+// add: y = x w^T + add (fp32 y, rows as y's); mask (with add): then y = 0 where mask (fp32, rows as y's)
+// is not > 0 — relu_mask of the sum, fused
 void dense_fwd_ps(Split x, int K, Split w, int N, float* y, int64_t ldy, int ycoff, int64_t M, float* stats,
-                  hipStream_t st, bool y_bf16 = false, const float* add = nullptr);
+                  hipStream_t st, bool y_bf16 = false, const float* add = nullptr, const float* mask = nullptr);
+// y[r][ycoff + c] = 0 where mask[r][ycoff + c] is not > 0 (rows of ldy; in place)
+void mask_inplace(float* y, int64_t ldy, int ycoff, const float* mask, int C, int64_t M, hipStream_t st);
 int dense_stats_rows(int64_t M, int N);
 // dw[n][k] = sum_m dz[m][n] x[m][k]  (reduction over the M pixels; split-K slabs)
 void dense_wgrad_ps(Split dz, int N, Split x, int K, float* dw, int64_t ldw, int64_t M, float* slab, int64_t slab_cap,

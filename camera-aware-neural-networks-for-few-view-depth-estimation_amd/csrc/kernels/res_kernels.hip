@@ -346,6 +346,23 @@ void relu_mask(const float* g, int64_t ldg, int gcoff, const float* out, int C, 
     hipLaunchKernelGGL(k_relu_mask, dim3(ew_blocks(n4)), dim3(256), 0, st, g, ldg, gcoff, out, C, gs, n4);
 }
 
+__global__ void k_mask_inplace(float* y, int64_t ldy, int ycoff, const float* mask, int C, int64_t n4) {
+    const int C4 = C >> 2;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / C4;
+        const int64_t o = r * ldy + ycoff + (i - r * C4) * 4;
+        const float4 m = *reinterpret_cast<const float4*>(mask + o);
+        float4 v = *reinterpret_cast<const float4*>(y + o);
+        v = make_float4(m.x > 0.f ? v.x : 0.f, m.y > 0.f ? v.y : 0.f, m.z > 0.f ? v.z : 0.f, m.w > 0.f ? v.w : 0.f);
+        *reinterpret_cast<float4*>(y + o) = v;
+    }
+}
+void mask_inplace(float* y, int64_t ldy, int ycoff, const float* mask, int C, int64_t M, hipStream_t st) {
+    if (C % 4 || ldy % 4 || ycoff % 4) throw std::runtime_error("mask_inplace: alignment");
+    const int64_t n4 = M * C / 4;
+    hipLaunchKernelGGL(k_mask_inplace, dim3(ew_blocks(n4)), dim3(256), 0, st, y, ldy, ycoff, mask, C, n4);
+}
+
 // dst[(b, S*oy, S*ox)][c] += src[(b, oy, ox)][scoff + c] for the Ho x Wo grid of src (S = 1 or 2);
 // dst rows of ld lddst over a B x H x W grid
 __global__ void k_add_strided(float* __restrict__ dst, int64_t lddst, const float* __restrict__ src, int64_t ldsrc,
