@@ -203,6 +203,7 @@ struct cad_resunet {
     // and each stage's contiguous slab range [off, off + cnt)
     float* bwd_g = nullptr;
     bool bwd_masked = false;   // bwd_g already carries the ReLU mask of the block whose output it is
+    bool bwd_skip_added = false;   // ... and the decoder concat's skip gradient
     std::vector<std::pair<int64_t, int64_t>> stage_range;
     float* P(int i) const { return flat_p + params[i].off; }
     float* G(int i) const { return flat_g + params[i].off; }
@@ -745,7 +746,8 @@ void prep_weights_bwd(cad_resunet* h, hipStream_t st) {
 // only the BN backward of the unit below reads
 void unit_bwd(cad_resunet* h, Unit& u, const float* g, int64_t ldg, int gcoff, bool relu, cad::Split in, int B,
               int Hin, int Win, const void* col, const void* xs, float* dx, int64_t lddx, hipStream_t st,
-              const float* add = nullptr, bool g_bf16 = false, bool dx_bf16 = false, const float* mask = nullptr) {
+              const float* add = nullptr, bool g_bf16 = false, bool dx_bf16 = false, const float* mask = nullptr,
+              int64_t ldadd = 0) {
     RConv& c = u.c;
     const int Ho = (Hin + 2 * c.p - c.k) / c.s + 1, Wo = (Win + 2 * c.p - c.k) / c.s + 1;
     const int64_t Mo = h->M(B, Ho, Wo);
@@ -765,7 +767,7 @@ void unit_bwd(cad_resunet* h, Unit& u, const float* g, int64_t ldg, int gcoff, b
     cad::dense_wgrad_ps(dz, c.cout, a, c.Kp, h->G(c.pidx), c.Kp, Mo, h->slab, h->slab_cap, st);
     if (!dx) return;
     if (c.k == 1 && c.s == 1) {
-        cad::dense_fwd_ps(dz, c.cout, tw(c.wts, c.cout), c.cin, dx, lddx, 0, Mo, nullptr, st, dx_bf16, add, mask);
+        cad::dense_fwd_ps(dz, c.cout, tw(c.wts, c.cout), c.cin, dx, lddx, 0, Mo, nullptr, st, dx_bf16, add, mask, ldadd);
         return;
     }
     need(!dx_bf16 && !mask, "unit_bwd: bf16 / masked input gradient of a strided / im2col convolution");
@@ -792,6 +794,16 @@ bool mask_fuse_on() {
     return on;
 }
 
+// CAD_SKIPFUSE=0: the decoder skip gradients and the stride-1 projection's dgrad added by separate
+// passes (A/B switch; the skip gradient's add order differs: fp32 rounding)
+bool fuse_skip_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("CAD_SKIPFUSE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 void backward_stage(cad_resunet* h, int stage, const float* ddepth, hipStream_t st) {
     const int B = h->fwd_B;
     const int nb = (int)h->blocks.size();
@@ -799,7 +811,7 @@ void backward_stage(cad_resunet* h, int stage, const float* ddepth, hipStream_t 
         prep_weights_bwd(h, st);
         Dec& d0 = h->dec.back();
         h->bwd_g = h->gA;
-        h->bwd_masked = false;
+        h->bwd_masked = h->bwd_skip_added = false;
         cad::head_bwd(d0.out, 32, h->P(h->head_w), ddepth, h->sig, h->max_depth, h->bwd_g, h->M(B, h->H, h->W),
                       h->dscr, h->G(h->head_w), h->G(h->head_b), st);
         return;
@@ -825,7 +837,7 @@ void backward_stage(cad_resunet* h, int stage, const float* ddepth, hipStream_t 
         cad::convT_dgrad_ps(tw(h->dYs, d.cout_up), d.cout_up, tw(d.wms, 4 * d.cout_up), d.cin_up, gn, B, d.H / 2,
                             d.W / 2, st);
         h->bwd_g = gn;
-        h->bwd_masked = false;
+        h->bwd_masked = h->bwd_skip_added = false;
         return;
     }
     if (stage < 6 + nb) {   // encoder bottleneck block bi; g = gradient of its output
@@ -834,7 +846,7 @@ void backward_stage(cad_resunet* h, int stage, const float* ddepth, hipStream_t 
         const int stage_last[3] = {h->stage_end[0] - 1, h->stage_end[1] - 1, h->stage_end[2] - 1};
         // skip gradients of the decoder concat (x4 = layer3, x3 = layer2, x2 = layer1 outputs)
         for (int L = 0; L < 3; ++L)
-            if (bi == stage_last[L]) {
+            if (bi == stage_last[L] && !h->bwd_skip_added) {
                 need(!h->bwd_masked, "resunet backward: a masked gradient at a skip block");
                 const Dec& d = h->dec[2 - L];
                 cad::add_strided(g, b.cout, d.dcat, d.skipC + d.cout_up, 0, b.cout, B, b.Ho, b.Wo, 1, st);
@@ -850,6 +862,16 @@ void backward_stage(cad_resunet* h, int stage, const float* ddepth, hipStream_t 
         // applies block bi - 1's ReLU mask (k_relu_mask fused)
         const bool fuse_mask = !b.down && bi > 0 && mask_fuse_on();
         const float* mask = fuse_mask ? h->blocks[bi - 1].out : nullptr;
+        // a projection block after a layer's last block (bi - 1): the decoder concat's skip gradient of
+        // that block's output added in this block's conv1 dgrad epilogue (its own row stride)
+        const float* skip = nullptr;
+        int64_t ldskip = 0;
+        for (int L = 0; L < 3; ++L)
+            if (b.down && bi - 1 == stage_last[L] && fuse_skip_on()) {
+                const Dec& d = h->dec[2 - L];
+                skip = d.dcat;
+                ldskip = d.skipC + d.cout_up;
+            }
         // conv3's and (stride 1) conv2's input gradients stored as bf16 (unit_bwd)
         const bool g2 = b.u2.c.win;
         unit_bwd(h, b.u3, gS, b.cout, 0, false, tw(b.t2s, b.w), B, b.Ho, b.Wo, nullptr, nullptr, h->dT, b.w, st,
@@ -858,13 +880,16 @@ void backward_stage(cad_resunet* h, int stage, const float* ddepth, hipStream_t 
                  true, g2);
         // identity shortcut: its gradient gS is added inside conv1's dgrad epilogue
         unit_bwd(h, b.u1, h->dT, b.w, 0, true, tw(xsw, b.cin), B, b.H, b.W, nullptr, nullptr, gn, b.cin, st,
-                 b.down ? nullptr : gS, g2, false, mask);
-        if (b.down) {
+                 b.down ? skip : gS, g2, false, mask, ldskip);
+        if (b.down && b.s == 1 && fuse_skip_on()) {   // the projection's dgrad added to gn in place
+            unit_bwd(h, b.ud, gS, b.cout, 0, false, tw(xsw, b.cin), B, b.H, b.W, nullptr, b.xs, gn, b.cin, st, gn);
+        } else if (b.down) {
             unit_bwd(h, b.ud, gS, b.cout, 0, false, tw(xsw, b.cin), B, b.H, b.W, nullptr, b.xs, h->dT, b.cin, st);
             cad::add_strided(gn, b.cin, h->dT, b.cin, 0, b.cin, B, b.H, b.W, b.s, st);
         }
         h->bwd_g = gn;
         h->bwd_masked = fuse_mask;
+        h->bwd_skip_added = skip != nullptr;
         return;
     }
     // stem: max-pool backward, the dec1 skip gradient (x1), bn1 + relu, conv1 weight gradient

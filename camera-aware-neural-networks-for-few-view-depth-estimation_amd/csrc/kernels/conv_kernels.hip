@@ -1268,8 +1268,11 @@ int dense_stats_rows(int64_t M, int N) { return cdiv(M, tile_m(pick_cfg((int)M, 
 
 void launch_dense_dma(void (*fn)(GemmArgs), const char* name, const GemmArgs& a, hipStream_t st);
 void dense_fwd_ps(Split x, int K, Split w, int N, float* y, int64_t ldy, int ycoff, int64_t M, float* stats,
-                  hipStream_t st, bool y_bf16, const float* add, const float* mask) {
+                  hipStream_t st, bool y_bf16, const float* add, const float* mask, int64_t ldadd) {
     if (mask && !add) throw std::runtime_error("dense GEMM: a mask needs the added matrix");
+    if (ldadd == 0) ldadd = ldy;
+    if (add && ldadd != ldy && (mask || ycoff || ldadd < N))
+        throw std::runtime_error("dense GEMM: an added matrix of its own stride takes no mask / offset");
     ps_check(x, K, "dense x");
     ps_check(w, K, "dense w");
     if (M > INT32_MAX) throw std::runtime_error("dense GEMM: too many rows");
@@ -1282,6 +1285,7 @@ void dense_fwd_ps(Split x, int K, Split w, int N, float* y, int64_t ldy, int yco
     a.stats = stats;
     a.bias = add;
     a.C2 = const_cast<float*>(mask);
+    a.ldc2 = ldadd;
     const Cfg c = pick_cfg(a.M, a.N);
     const int kb = ps_kb(true, c);
     a.kstages_per_split = cdiv(a.K, kb);
@@ -1295,6 +1299,8 @@ void dense_fwd_ps(Split x, int K, Split w, int N, float* y, int64_t ldy, int yco
         if (add && (stats || y_bf16)) throw std::runtime_error("dense GEMM: the added matrix needs fp32 output");
         if (add && mask)
             launch_dense_dma(k_dense_bf16d<EpiStoreAddMask>, "void cad::k_dense_bf16d<cad::EpiStoreAddMask>(cad::GemmArgs)", a, st);
+        else if (add && ldadd != ldy)
+            launch_dense_dma(k_dense_bf16d<EpiStoreAddLd>, "void cad::k_dense_bf16d<cad::EpiStoreAddLd>(cad::GemmArgs)", a, st);
         else if (add) launch_dense_dma(k_dense_bf16d<EpiStoreAdd>, "void cad::k_dense_bf16d<cad::EpiStoreAdd>(cad::GemmArgs)", a, st);
         else if (y_bf16 && stats)
             launch_dense_dma(k_dense_bf16d<EpiStoreStatsB16>, "void cad::k_dense_bf16d<cad::EpiStoreStatsB16>(cad::GemmArgs)", a, st);
@@ -1303,7 +1309,12 @@ void dense_fwd_ps(Split x, int K, Split w, int N, float* y, int64_t ldy, int yco
         else launch_dense_dma(k_dense_bf16d<EpiStore>, "void cad::k_dense_bf16d<cad::EpiStore>(cad::GemmArgs)", a, st);
         return;
     }
-    if (add) {
+    if (add && ldadd != ldy) {   // (the register-staged kernels: the GEMM, then an add pass)
+        if (stats || y_bf16) throw std::runtime_error("dense GEMM: the added matrix needs fp32 output");
+        a.bias = nullptr;
+        launch_kb<KDenseP1, 32, 64>(c, kb, a, 1, st);
+        add_strided(y, ldy, add, ldadd, 0, N, 1, 1, (int)M, 1, st);
+    } else if (add) {
         if (stats || y_bf16) throw std::runtime_error("dense GEMM: the added matrix needs fp32 output");
         launch_kb<KDenseAddP1, 32, 64>(c, kb, a, 1, st);
         if (mask) mask_inplace(y, ldy, ycoff, mask, N, M, st);   // (the register-staged kernels: a pass)

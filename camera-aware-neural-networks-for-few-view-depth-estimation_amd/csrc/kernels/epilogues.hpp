@@ -28,6 +28,12 @@ struct EpiStoreAdd : EpiStore {
         return a.bias + (int64_t)m0 * a.ldc + a.c_coff;
     }
 };
+// ... with the added matrix's own row stride a.ldc2 (config 5: a decoder concat's skip-half gradient
+// added to the block-output gradient a projection block's conv1 dgrad produces)
+struct EpiStoreAddLd : EpiStoreAdd {
+    static constexpr bool ADD_LD = true;
+    __device__ static const float* add_base(const GemmArgs& a, int m0) { return a.bias + (int64_t)m0 * a.ldc2; }
+};
 // ... then zeroed where the fp32 matrix a.C2 (same rows / offset as C) is not > 0: config 5's block-input
 // gradient masked by the previous block's ReLU output (the separate k_relu_mask pass, fused)
 struct EpiStoreAddMask : EpiStoreAdd {

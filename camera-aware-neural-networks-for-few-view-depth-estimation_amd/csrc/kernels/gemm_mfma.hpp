@@ -435,6 +435,10 @@ struct has_wave_store : std::false_type {};   // a structured epilogue that may 
 template <class E>
 struct has_wave_store<E, std::void_t<decltype(E::WAVE_STORE)>> : std::integral_constant<bool, E::WAVE_STORE> {};
 template <class E, class = void>
+struct has_add_ld : std::false_type {};   // an ADD epilogue whose added matrix has its own row stride (a.ldc2)
+template <class E>
+struct has_add_ld<E, std::void_t<decltype(E::ADD_LD)>> : std::integral_constant<bool, E::ADD_LD> {};
+template <class E, class = void>
 struct has_mask : std::false_type {};   // an ADD epilogue that also zeroes where its mask matrix is not > 0
 template <class E>
 struct has_mask<E, std::void_t<decltype(E::MASK)>> : std::integral_constant<bool, E::MASK> {};
@@ -666,9 +670,18 @@ __device__ __forceinline__ void gemm_epilogue_t(const GemmArgs& a, const floatx1
     const int64_t bytes = (int64_t)(a.M - m0) * ldc4;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(epi_row_base<Epi>(a, m0, tile.z),
                                                 (uint32_t)(bytes < (int64_t)kRecords ? bytes : kRecords));
+    // the added matrix's row stride in bytes (fp32 rows)
+    [[maybe_unused]] const int64_t lda4 = [&]() -> int64_t {
+        if constexpr (has_add_ld<Epi>::value) return a.ldc2 * 4;
+        else return ldc4;
+    }();
     auto add_rsrc = [&]() {
-        if constexpr (Epi::ADD) return make_rsrc(Epi::add_base(a, m0), (uint32_t)(bytes < (int64_t)kRecords ? bytes : kRecords));
-        else return rs;
+        if constexpr (Epi::ADD) {
+            const int64_t abytes = (int64_t)(a.M - m0) * lda4;
+            return make_rsrc(Epi::add_base(a, m0), (uint32_t)(abytes < (int64_t)kRecords ? abytes : kRecords));
+        } else {
+            return rs;
+        }
     };
     const __amdgpu_buffer_rsrc_t rsadd = add_rsrc();
     auto mask_rsrc = [&]() {
@@ -712,10 +725,11 @@ __device__ __forceinline__ void gemm_epilogue_t(const GemmArgs& a, const floatx1
                 for (int r = 0; r < 4; ++r) v[r] = acc[i][j][4 * g + r];
                 if constexpr (Epi::ADD) {
                     const uint32_t lo = n < a.N ? (uint32_t)(mr * ldc4 + (int64_t)n * ES) : kOOB;
+                    const uint32_t la = n < a.N ? (uint32_t)(mr * lda4 + (int64_t)n * 4) : kOOB;
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
                         v[r] += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                              rsadd, lo + (uint32_t)(r * ldc4), 0, 0));
+                                                              rsadd, la + (uint32_t)(r * lda4), 0, 0));
                     if constexpr (has_mask<Epi>::value) {   // v [mask > 0] (k_relu_mask's arithmetic)
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {

@@ -99,9 +99,11 @@ void convT_wgrad_ps(Split x, int cin, Split g, int cout, float* dw, int B, int H
 // y[m][ycoff + n] = sum_k x[m][k] w[n][k]  (+ BN partials [rows][2][N] when stats != nullptr)
 // add != nullptr: y = x w^T + add (add rows with y's stride and offset; fp32 output, no stats)
 // add: y = x w^T + add (fp32 y, rows as y's); mask (with add): then y = 0 where mask (fp32, rows as y's)
-// is not > 0 — relu_mask of the sum, fused
+// is not > 0 — relu_mask of the sum, fused; ldadd: the added matrix's row stride (0: ldy; another stride
+// takes no mask and no ycoff)
 void dense_fwd_ps(Split x, int K, Split w, int N, float* y, int64_t ldy, int ycoff, int64_t M, float* stats,
-                  hipStream_t st, bool y_bf16 = false, const float* add = nullptr, const float* mask = nullptr);
+                  hipStream_t st, bool y_bf16 = false, const float* add = nullptr, const float* mask = nullptr,
+                  int64_t ldadd = 0);
 // y[r][ycoff + c] = 0 where mask[r][ycoff + c] is not > 0 (rows of ldy; in place)
 void mask_inplace(float* y, int64_t ldy, int ycoff, const float* mask, int C, int64_t M, hipStream_t st);
 int dense_stats_rows(int64_t M, int N);
