@@ -744,10 +744,12 @@ void prep_weights_bwd(cad_resunet* h, hipStream_t st) {
 // g_bf16: g is bf16 rows (ldg elements); dx_bf16: dx is written as bf16 rows (window / 1x1 stride-1
 // dgrads only) — the input gradients of a bottleneck's conv2 / conv3 and of a decoder's conv2, which
 // only the BN backward of the unit below reads
-void unit_bwd(cad_resunet* h, Unit& u, const float* g, int64_t ldg, int gcoff, bool relu, cad::Split in, int B,
+// hi / ldhi / split_n: the window dgrad's split store (columns >= split_n as bf16 rows of hi); returns
+// whether it ran
+bool unit_bwd(cad_resunet* h, Unit& u, const float* g, int64_t ldg, int gcoff, bool relu, cad::Split in, int B,
               int Hin, int Win, const void* col, const void* xs, float* dx, int64_t lddx, hipStream_t st,
               const float* add = nullptr, bool g_bf16 = false, bool dx_bf16 = false, const float* mask = nullptr,
-              int64_t ldadd = 0) {
+              int64_t ldadd = 0, void* hi = nullptr, int64_t ldhi = 0, int split_n = 0) {
     RConv& c = u.c;
     const int Ho = (Hin + 2 * c.p - c.k) / c.s + 1, Wo = (Win + 2 * c.p - c.k) / c.s + 1;
     const int64_t Mo = h->M(B, Ho, Wo);
@@ -758,17 +760,17 @@ void unit_bwd(cad_resunet* h, Unit& u, const float* g, int64_t ldg, int gcoff, b
     need(!dx_bf16 || !add, "unit_bwd: a bf16 input gradient with an added matrix");
     if (c.win) {
         cad::conv3x3_wgrad_ps(dz, c.cout, in, c.cin, h->G(c.pidx), B, Hin, Win, h->slab, h->slab_cap, st);
-        if (dx) cad::conv3x3_dgrad_ps(dz, c.cout, tw(c.wts, 9 * c.cout), c.cin, dx, lddx, B, Hin, Win, st, dx_bf16);
-        return;
+        return dx && cad::conv3x3_dgrad_ps(dz, c.cout, tw(c.wts, 9 * c.cout), c.cin, dx, lddx, B, Hin, Win, st, dx_bf16,
+                                           hi, ldhi, split_n);
     }
     cad::Split a = in;
     if (c.k == 1 && c.s > 1) a = tw(xs, c.cin);
     else if (c.k > 1 || c.s > 1) a = tw(col, c.Kp);
     cad::dense_wgrad_ps(dz, c.cout, a, c.Kp, h->G(c.pidx), c.Kp, Mo, h->slab, h->slab_cap, st);
-    if (!dx) return;
+    if (!dx) return false;
     if (c.k == 1 && c.s == 1) {
         cad::dense_fwd_ps(dz, c.cout, tw(c.wts, c.cout), c.cin, dx, lddx, 0, Mo, nullptr, st, dx_bf16, add, mask, ldadd);
-        return;
+        return false;
     }
     need(!dx_bf16 && !mask, "unit_bwd: bf16 / masked input gradient of a strided / im2col convolution");
     if (c.k == 1) {   // stride-2 1x1: dgrad on the subsampled grid, scattered by the caller
@@ -777,6 +779,7 @@ void unit_bwd(cad_resunet* h, Unit& u, const float* g, int64_t ldg, int gcoff, b
         cad::dense_fwd_ps(dz, c.cout, tw(c.wts, c.cout), c.Kp, h->dcol, c.Kp, 0, Mo, nullptr, st);
         cad::col2im(h->dcol, c.Kp, c.cin, B, Hin, Win, c.k, c.k, c.s, c.p, dx, lddx, st);
     }
+    return false;
 }
 
 // Backward in stages whose parameter gradients are contiguous, decreasing-offset slab ranges (the
@@ -789,6 +792,16 @@ int num_stages(const cad_resunet* h) { return 6 + (int)h->blocks.size() + 1; }
 bool mask_fuse_on() {
     static const bool on = [] {
         const char* e = std::getenv("CAD_MASKFUSE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// CAD_UPSPLIT=0: the decoder conv1 input gradient's up half split into the ConvT operand by a pass
+// (A/B switch; bit-identical)
+bool up_split_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("CAD_UPSPLIT");
         return !(e && e[0] == '0');
     }();
     return on;
@@ -825,13 +838,23 @@ void backward_stage(cad_resunet* h, int stage, const float* ddepth, hipStream_t 
         const int64_t Md = h->M(B, d.H, d.W);
         unit_bwd(h, d.u2, g, d.C, 0, true, tw(d.a1s, d.C), B, d.H, d.W, nullptr, nullptr, h->dT, d.C, st, nullptr,
                  false, true);
-        unit_bwd(h, d.u1, h->dT, d.C, 0, true, tw(d.cats, cc), B, d.H, d.W, nullptr, nullptr, d.dcat, cc, st, nullptr,
-                 true);
-        // ConvTranspose backward on the up half of dcat
-        cad::split_rows(d.dcat, cc, d.skipC, d.cout_up, Md, h->dYs, d.cout_up, 0, st);
+        // conv1's input gradient: the skip half fp32 into dcat (the encoder's skip adds read it), the up half
+        // straight into the ConvT's bf16 operand dYs (the window dgrad's split store; dec0, all up half:
+        // the dgrad's bf16 output), else split from dcat by a pass (split_rows' rounding, the same values)
+        bool up_done;
+        if (d.skipC == 0 && up_split_on()) {
+            unit_bwd(h, d.u1, h->dT, d.C, 0, true, tw(d.cats, cc), B, d.H, d.W, nullptr, nullptr,
+                     static_cast<float*>(h->dYs), d.cout_up, st, nullptr, true, true);
+            up_done = true;
+        } else {
+            up_done = unit_bwd(h, d.u1, h->dT, d.C, 0, true, tw(d.cats, cc), B, d.H, d.W, nullptr, nullptr, d.dcat, cc, st,
+                               nullptr, true, false, nullptr, 0, up_split_on() ? h->dYs : nullptr, d.cout_up, d.skipC);
+        }
+        if (!up_done) cad::split_rows(d.dcat, cc, d.skipC, d.cout_up, Md, h->dYs, d.cout_up, 0, st);
+        // ConvTranspose backward on the up half; its bias gradient sums the same bf16 gradient
         cad::convT_wgrad_ps(tw(prev, d.cin_up), d.cin_up, tw(h->dYs, d.cout_up), d.cout_up, h->G(d.up_w), B, d.H / 2,
                             d.W / 2, h->slab, h->slab_cap, st);
-        cad::colsum(d.dcat, cc, d.skipC, Md, d.cout_up, h->dscr, st);
+        cad::colsum_bf16(h->dYs, d.cout_up, 0, Md, d.cout_up, h->dscr, st);
         cad::colsum_finalize(h->dscr, cad::colsum_slices(Md), d.cout_up, h->G(d.up_b), 1.f, st);
         float* gn = g == h->gA ? h->gB : h->gA;
         cad::convT_dgrad_ps(tw(h->dYs, d.cout_up), d.cout_up, tw(d.wms, 4 * d.cout_up), d.cin_up, gn, B, d.H / 2,
@@ -896,9 +919,13 @@ void backward_stage(cad_resunet* h, int stage, const float* ddepth, hipStream_t 
     const int H1 = (h->H - 1) / 2 + 1, W1 = (h->W - 1) / 2 + 1;
     const int64_t M1 = h->M(B, H1, W1);
     float* gs = g == h->gA ? h->gB : h->gA;
-    cad::maxpool3s2_bwd(g, h->pidx, 64, B, H1, W1, gs, st);
     const Dec& d1 = h->dec[3];
-    cad::add_strided(gs, 64, d1.dcat, d1.skipC + d1.cout_up, 0, 64, B, H1, W1, 1, st);
+    if (fuse_skip_on()) {   // the dec1 skip gradient added in the gather (the same single add per element)
+        cad::maxpool3s2_bwd(g, h->pidx, 64, B, H1, W1, gs, st, d1.dcat, d1.skipC + d1.cout_up);
+    } else {
+        cad::maxpool3s2_bwd(g, h->pidx, 64, B, H1, W1, gs, st);
+        cad::add_strided(gs, 64, d1.dcat, d1.skipC + d1.cout_up, 0, 64, B, H1, W1, 1, st);
+    }
     RBN& sb = h->stem.b;
     cad::bn_relu_bwd(gs, 64, 0, h->stem.y, 64, sb.mean, sb.invstd, sb.scale, sb.shift, h->P(sb.widx), M1, h->dscr, sb.coef,
                      h->G(sb.widx), h->G(sb.bidx), nullptr, st, nullptr, 1, h->dYs, true, true);

@@ -144,7 +144,10 @@ void col2im(const float* dcol, int Kc, int C, int B, int H, int W, int KH, int K
             int64_t lddx, hipStream_t st);
 void maxpool3s2_fwd(const float* x, int C, int B, int H, int W, float* out, uint8_t* idx, void* out_split,
                     hipStream_t st);
-void maxpool3s2_bwd(const float* dout, const uint8_t* idx, int C, int B, int H, int W, float* dx, hipStream_t st);
+// add (rows of ldadd, first C columns): a matrix added to the gathered gradient (config 5: the dec1 skip
+// gradient of the stem output), else dx is overwritten
+void maxpool3s2_bwd(const float* dout, const uint8_t* idx, int C, int B, int H, int W, float* dx, hipStream_t st,
+                    const float* add = nullptr, int64_t ldadd = 0);
 // out = relu(y*scale + shift + (yd ? yd*dscale + dshift : x)), fp32 [M][C] + twin
 void bn_add_relu(const float* y, const float* scale, const float* shift, const float* yd, const float* dscale,
                  const float* dshift, const float* x, int64_t ldx, int C, int64_t M, float* out, void* out_split,

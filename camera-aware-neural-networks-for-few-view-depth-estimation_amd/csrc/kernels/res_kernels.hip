@@ -226,7 +226,8 @@ void maxpool3s2_fwd(const float* x, int C, int B, int H, int W, float* out, uint
 // decode cost more than the kernel's memory traffic)
 template <class I>
 __global__ void k_maxpool3s2_bwd(const float* __restrict__ dout, const uint8_t* __restrict__ idx, int C, int B, int H,
-                                 int W, int Ho, int Wo, float* __restrict__ dx, int64_t n4) {
+                                 int W, int Ho, int Wo, float* __restrict__ dx, int64_t n4, const float* __restrict__ add,
+                                 int64_t ldadd) {
     const I C4 = (I)(C >> 2);
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
         const I p = (I)i / C4;
@@ -253,18 +254,24 @@ __global__ void k_maxpool3s2_bwd(const float* __restrict__ dout, const uint8_t* 
                 if (a.w == code) s[3] += d.w;
             }
         }
+        if (add) {   // (the separate add pass's single add, in the same order)
+            const float4 q = *reinterpret_cast<const float4*>(add + (int64_t)p * ldadd + c);
+            s[0] += q.x; s[1] += q.y; s[2] += q.z; s[3] += q.w;
+        }
         *reinterpret_cast<float4*>(dx + (int64_t)p * C + c) = make_float4(s[0], s[1], s[2], s[3]);
     }
 }
-void maxpool3s2_bwd(const float* dout, const uint8_t* idx, int C, int B, int H, int W, float* dx, hipStream_t st) {
+void maxpool3s2_bwd(const float* dout, const uint8_t* idx, int C, int B, int H, int W, float* dx, hipStream_t st,
+                    const float* add, int64_t ldadd) {
+    if (add && (ldadd < C || ldadd % 4)) throw std::runtime_error("maxpool3s2_bwd: added matrix layout");
     const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
     const int64_t n4 = (int64_t)B * H * W * C / 4;
     if (n4 < ((int64_t)1 << 31))
         hipLaunchKernelGGL(k_maxpool3s2_bwd<uint32_t>, dim3(cdiv(n4, 256)), dim3(256), 0, st, dout, idx, C, B, H, W, Ho, Wo,
-                           dx, n4);
+                           dx, n4, add, ldadd);
     else
         hipLaunchKernelGGL(k_maxpool3s2_bwd<int64_t>, dim3(ew_blocks(n4)), dim3(256), 0, st, dout, idx, C, B, H, W, Ho, Wo,
-                           dx, n4);
+                           dx, n4, add, ldadd);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -187,7 +187,8 @@ def forward(x, p, bufs, train=True, max_depth=10.0):
     skips = {4: feats[2], 3: feats[1], 2: feats[0], 1: x1}
     for l, cu, C, sk in DEC:
         pre = f"dec{l}."
-        up = O._convT2x2(y, p[pre + "up.weight"], p[pre + "up.bias"])
+        # (bias_bf16: the bias gradient sums the bf16 up-half gradient the ConvT GEMMs read, as resunet.cpp)
+        up = O._convT2x2(y, p[pre + "up.weight"], p[pre + "up.bias"], bias_bf16=True)
         y = torch.cat([skips[l], up], 1) if sk else up
         y = F.relu(O._bn(_conv(y, p[pre + "conv.conv1.weight"], 1, 1), p, bufs, pre + "conv.bn1", train))
         y = F.relu(O._bn(_conv(_rgrad(y), p[pre + "conv.conv2.weight"], 1, 1), p, bufs, pre + "conv.bn2", train))
