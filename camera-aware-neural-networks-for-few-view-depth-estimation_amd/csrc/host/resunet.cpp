@@ -839,25 +839,28 @@ void backward_stage(cad_resunet* h, int stage, const float* ddepth, hipStream_t 
         unit_bwd(h, d.u2, g, d.C, 0, true, tw(d.a1s, d.C), B, d.H, d.W, nullptr, nullptr, h->dT, d.C, st, nullptr,
                  false, true);
         // conv1's input gradient: the skip half fp32 into dcat (the encoder's skip adds read it), the up half
-        // straight into the ConvT's bf16 operand dYs (the window dgrad's split store; dec0, all up half:
-        // the dgrad's bf16 output), else split from dcat by a pass (split_rows' rounding, the same values)
+        // straight into the ConvT's bf16 operand (the window dgrad's split store; dec0, all up half: the
+        // dgrad's bf16 output), else split from dcat by a pass (split_rows' rounding, the same values).
+        // The operand goes to dT — free once bn1's backward has read conv2's input gradient from it — not
+        // to dYs, which the dgrad itself reads (its dz)
+        void* dup = h->dT;
         bool up_done;
         if (d.skipC == 0 && up_split_on()) {
             unit_bwd(h, d.u1, h->dT, d.C, 0, true, tw(d.cats, cc), B, d.H, d.W, nullptr, nullptr,
-                     static_cast<float*>(h->dYs), d.cout_up, st, nullptr, true, true);
+                     static_cast<float*>(dup), d.cout_up, st, nullptr, true, true);
             up_done = true;
         } else {
             up_done = unit_bwd(h, d.u1, h->dT, d.C, 0, true, tw(d.cats, cc), B, d.H, d.W, nullptr, nullptr, d.dcat, cc, st,
-                               nullptr, true, false, nullptr, 0, up_split_on() ? h->dYs : nullptr, d.cout_up, d.skipC);
+                               nullptr, true, false, nullptr, 0, up_split_on() ? dup : nullptr, d.cout_up, d.skipC);
         }
-        if (!up_done) cad::split_rows(d.dcat, cc, d.skipC, d.cout_up, Md, h->dYs, d.cout_up, 0, st);
+        if (!up_done) cad::split_rows(d.dcat, cc, d.skipC, d.cout_up, Md, dup, d.cout_up, 0, st);
         // ConvTranspose backward on the up half; its bias gradient sums the same bf16 gradient
-        cad::convT_wgrad_ps(tw(prev, d.cin_up), d.cin_up, tw(h->dYs, d.cout_up), d.cout_up, h->G(d.up_w), B, d.H / 2,
+        cad::convT_wgrad_ps(tw(prev, d.cin_up), d.cin_up, tw(dup, d.cout_up), d.cout_up, h->G(d.up_w), B, d.H / 2,
                             d.W / 2, h->slab, h->slab_cap, st);
-        cad::colsum_bf16(h->dYs, d.cout_up, 0, Md, d.cout_up, h->dscr, st);
+        cad::colsum_bf16(dup, d.cout_up, 0, Md, d.cout_up, h->dscr, st);
         cad::colsum_finalize(h->dscr, cad::colsum_slices(Md), d.cout_up, h->G(d.up_b), 1.f, st);
         float* gn = g == h->gA ? h->gB : h->gA;
-        cad::convT_dgrad_ps(tw(h->dYs, d.cout_up), d.cout_up, tw(d.wms, 4 * d.cout_up), d.cin_up, gn, B, d.H / 2,
+        cad::convT_dgrad_ps(tw(dup, d.cout_up), d.cout_up, tw(d.wms, 4 * d.cout_up), d.cin_up, gn, B, d.H / 2,
                             d.W / 2, st);
         h->bwd_g = gn;
         h->bwd_masked = h->bwd_skip_added = false;
