@@ -77,8 +77,9 @@ def parse():
     ap.add_argument("--no-extra", action="store_true", help="skip the bf16 workload legs and the data path")
     ap.add_argument("--exchange", default="rccl", choices=("rccl", "torch"),
                     help="N>1 gradient exchange: libcad's RCCL communicator (the build/train path) or torch.distributed")
-    ap.add_argument("--cpu-sample-batch", type=int, default=4)
-    ap.add_argument("--cpu-sample-steps", type=int, default=2)
+    # 1 warm-up + >= 3 timed steps at bs32 480x640, on the job's CPU share
+    ap.add_argument("--cpu-sample-batch", type=int, default=32)
+    ap.add_argument("--cpu-sample-steps", type=int, default=3)
     a = ap.parse_args()
     preset = {2: ("baseline", "fp32", "1,0,0,0"), 3: ("rayfilm", "bf16", "1,0.1,0.001,0.01"),
               4: ("baseline", "bf16", "1,0.1,0.001,0.01")}[a.config]
@@ -148,22 +149,29 @@ def omp_threads_env():
 
 
 def cpu_threads():
-    """Threads for the CPU reference path: the host's physical cores (BASELINE.md §3:
-    set_num_threads(<physical cores>)), bounded only by the CPUs this process may run on."""
+    """Threads for the CPU reference path: the CPUs this job may actually use — the cgroup CPU quota
+    when there is one (the GPU boxes give one GPU's job 16 of the host's 128 physical cores this way;
+    its affinity mask still lists every CPU, and 128 threads under a 16-CPU quota run throttled, 2.5x
+    slower than 16), else the host's physical cores (set_num_threads(<physical
+    cores>)), bounded by the CPUs this process may run on."""
     h = host_cpu()
     h["cgroup_cpu_quota"] = cpu_quota()
     h["omp_num_threads_env"] = omp_threads_env()
     n = h["physical_cores"] or h["usable_cpus"] or 1
-    return max(1, min(n, h["usable_cpus"] or n)), h
+    n = max(1, min(n, h["usable_cpus"] or n))
+    if h["cgroup_cpu_quota"]:
+        n = min(n, h["cgroup_cpu_quota"])
+    return n, h
 
 
-def cpu_baseline(args, sweep=(16, 8)):
+def cpu_baseline(args, over_batch=4):
     """cpu_baseline leg: the oracle restatement (oracle/cad_oracle.py: LibTorch CPU, the ATen kernels
     the reference dispatches; the reference source and its compiled harness stay in the build
-    container) timed on this host on a bounded sample of the workload — bs`cpu_sample_batch` at the
-    benchmark resolution, 1 warm-up + `cpu_sample_steps` timed train steps at the host's physical core
-    count (the reported value), then `cpu_sample_steps` more at each thread count of
-    `sweep` and at the job's cgroup CPU quota (one GPU's share of the box's cores)."""
+    container) timed on this host on a bounded sample of the workload — bs`cpu_sample_batch` (32: the
+    workload's own batch, BN statistics over bs32) at the benchmark resolution, 1 warm-up +
+    `cpu_sample_steps` timed train steps at the job's CPU share (cpu_threads: the
+    cgroup quota, the reported value).  Beside it, labelled as such: one bs`over_batch` step at all of
+    the host's physical cores, which oversubscribes the quota when there is one."""
     import torch
     from oracle import cad_oracle as O
     threads, host = cpu_threads()
@@ -174,36 +182,38 @@ def cpu_baseline(args, sweep=(16, 8)):
     rgb, gt, K = [torch.from_numpy(a) for a in O.synth_batch(B, H, W)]
     prev = torch.get_num_threads()
     ref = O.Trainer(params, bufs, weights=w, model=args.model)
-    pts = sorted({t for t in sweep + ((host["cgroup_cpu_quota"],) if host["cgroup_cpu_quota"] else ())
-                  if t < threads}, reverse=True)
+    over = None
     try:
         torch.set_num_threads(threads)
+        t0 = time.perf_counter()
         ref.step(rgb, gt, K)                      # warm-up
+        warm = time.perf_counter() - t0
         t0 = time.perf_counter()
         for _ in range(args.cpu_sample_steps):
             ref.step(rgb, gt, K)
         dt = time.perf_counter() - t0
-        rates = {str(threads): round(B * args.cpu_sample_steps / dt, 4)}
-        for t in pts:
-            torch.set_num_threads(t)
+        log(f"cpu baseline: warm-up {warm:.1f} s, {args.cpu_sample_steps} steps {dt:.1f} s at {threads} threads")
+        phys = host["physical_cores"] or 0
+        if host["cgroup_cpu_quota"] and phys > threads and over_batch:
+            torch.set_num_threads(phys)
+            sub = tuple(t[:over_batch] for t in (rgb, gt, K))
             t1 = time.perf_counter()
-            for _ in range(args.cpu_sample_steps):
-                ref.step(rgb, gt, K)
-            rates[str(t)] = round(B * args.cpu_sample_steps / (time.perf_counter() - t1), 4)
+            ref.step(*sub)
+            over = {"threads": phys, "batch": over_batch, "steps": 1,
+                    "images_per_s": round(over_batch / (time.perf_counter() - t1), 4),
+                    "note": (f"all {phys} physical cores under the job's {host['cgroup_cpu_quota']}-CPU cgroup quota: "
+                             f"oversubscribed (throttled), not the baseline; one bs{over_batch} step, no own warm-up")}
     finally:
         torch.set_num_threads(prev)
-    best = max(rates, key=lambda k: rates[k])
-    return {"value": rates[str(threads)], "unit": "images/s", "cores": threads, "kind": "port",
+    return {"value": round(B * args.cpu_sample_steps / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
             "sample": (f"{args.model} bs{B} {H}x{W} f={f} loss weights {args.weights}, fp32 (the reference's only "
                        f"precision), 1 warm-up + {args.cpu_sample_steps} timed train steps of the oracle restatement "
-                       f"(oracle/cad_oracle.py on LibTorch CPU) at the host's {threads} physical cores "
-                       f"(BASELINE.md §3); BN statistics over bs{B}, not bs32"),
-            "seconds": round(dt, 2), "threads_sweep_images_per_s": rates,
-            "best_threads": int(best), "best_images_per_s": rates[best],
-            "threads_sweep_note": (f"{args.cpu_sample_steps} train steps per further thread count after the timed "
-                                   f"steps (same weights, same batch); includes the job's cgroup CPU quota "
-                                   f"({host['cgroup_cpu_quota']}) = one GPU's share of the host"),
-            "host": host}
+                       f"(oracle/cad_oracle.py on LibTorch CPU) at {threads} threads = "
+                       + (f"the job's cgroup CPU quota (one GPU's share of the host's {host['physical_cores']} "
+                          f"physical cores)" if host["cgroup_cpu_quota"] else "the host's physical cores")
+                       + " (BASELINE.md §3)"),
+            "seconds": round(dt, 2), "warmup_seconds": round(warm, 2),
+            "oversubscribed_all_cores": over, "host": host}
 
 
 def parity_steps(args, cad, dev, steps=10, B=2):

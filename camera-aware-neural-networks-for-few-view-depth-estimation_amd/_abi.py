@@ -65,6 +65,8 @@ SIGNATURES = {
     "cad_adam_state": (I, [P, C.POINTER(P), C.POINTER(P)]),
     "cad_adam_set_step_count": (I, [P, I64]),
     "cad_set_gemm_engine": (I, [I]),
+    "cad_set_alias_check": (I, [I]),
+    "cad_alias_views_overlap": (I, [P, I64, I64, I64, I64, I, P, I64, I64, I64, I64, I]),
     "cad_get_gemm_engine": (I, []),
     "cad_unet_create": (I, [C.POINTER(UnetDesc), I, C.POINTER(P)]),
     "cad_resunet_create": (I, [C.POINTER(ResUnetDesc), I, C.POINTER(P)]),
@@ -82,6 +84,7 @@ SIGNATURES = {
     "cad_resunet_forward": (I, [P, P, P, I, P]),
     "cad_resunet_backward": (I, [P, P, P]),
     "cad_resunet_num_stages": (I, [P]),
+    "cad_resunet_debug_buffer": (I64, [P, C.c_char_p, FP, I64]),
     "cad_resunet_grad_layout": (I, [C.POINTER(I), I64P, I64P, I64P]),
     "cad_resunet_stage_grad_range": (I, [P, I, I64P, I64P]),
     "cad_resunet_backward_stage": (I, [P, I, P, P]),

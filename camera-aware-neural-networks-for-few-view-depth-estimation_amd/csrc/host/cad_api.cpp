@@ -135,11 +135,6 @@ struct DoubleConv {
     // many standard deviations from zero, so bf16-stored values would cost x-hat several % (measured:
     // enc1.bn1 gradients 5x further from fp64 than the fp32 oracle's)
     bool y1_f32 = false;
-    // the last forward recomputed conv1 instead of storing y1 (enc1: rc1_on): its consumers (bn1
-    // apply, bn1 backward, the y1 debug buffer) relaunch the conv GEMM from the input and weights
-    // that forward used (the twins on the bf16 engine, the rc_w snapshot on S3)
-    bool y1_rc = false;
-    bool y1_rc_ps = false;   // ... and did so on the pre-split kernels (the operands rc1_ops picks)
     void* a1s = nullptr;   // pre-split a1 (gemm_ps.hpp)
     int first_param = 0, last_param = 0;   // [first, last] indices in named_parameters()
     bool has_film() const { return film.p0 >= 0; }
@@ -209,13 +204,10 @@ struct cad_unet {
     double* dscr = nullptr;    // column-reduction scratch
     float* slab = nullptr;
     int64_t slab_cap = 0;
-    // recomputed enc1.conv1 (rc1_on): per-tile BN-backward partials, and the fp32 weights the last
-    // forward used (S3 engine; the bf16 engine's weight twin is already such a copy)
-    double* rc_part = nullptr;
-    float* rc_w = nullptr;
     // per-tile BN-backward sums of bn1 from conv2's input-gradient epilogue (conv3x3_dgrad_*_bnsums):
-    // the same buffer as rc_part (tiles of >= 128 rows at any level fit in its 64-row level-0 sizing;
-    // never live at the same time: each is reduced right after the GEMM that writes it)
+    // tiles of >= 128 rows at any level fit its 64-row level-0 sizing; reduced right after the GEMM
+    // that writes it
+    double* rc_part = nullptr;
     int64_t part_cap = 0;
     // stage grad ranges
     std::vector<std::pair<int64_t, int64_t>> stage_range;
@@ -431,10 +423,9 @@ void layout(cad_unet* h, Arena& a) {
     }
     h->slab_cap = std::min<int64_t>(sl, (int64_t)64 << 20);
     h->slab = a.f(h->slab_cap);
-    // recomputed enc1.conv1: tiles of at least 64 rows (the tile height follows the engine at run time)
+    // bn1's per-tile backward sums: tiles of at least 64 rows
     h->part_cap = (h->Ml(0, B) + 63) / 64 * 2 * h->Cl(0);
     h->rc_part = a.d(h->part_cap);
-    h->rc_w = a.f((int64_t)h->enc[0].c1.cout * 9 * h->enc[0].c1.cin);
     // buffers table (running stats), named_buffers() order (parameter order of the BNs)
     h->bufs.clear();
     auto add_bn_bufs = [&](const std::string& pre, BN& b) {
@@ -531,34 +522,6 @@ bool conv1_presplit(cad_unet* h, const DoubleConv& dc, bool ps, const cad::Split
     static const bool enc1_ps = env_flag("CAD_ENC1PS", 1) != 0;
     return ps && in_s.p && dc.c1.ws && (enc1_ps || &dc != &h->enc[0]);
 }
-// enc1.conv1 recomputed instead of stored (round 4): its K = 9 x 8 GEMM reads 16 B per pixel (the
-// NHWC8 input twin; 32 B fp32 on S3) and is cheaper to run again than its fp32 output is to write and
-// re-read three times (256 B per pixel at f = 64).  Plain DoubleConv only (the FiLM blocks' affine
-// passes read y1 as well), on the S3 engine or on the bf16 engine's pre-split kernels with the fp32
-// y1 of enc1.  On the S3 engine the recomputation costs six bf16 products per MAC and four
-// launches (stats, apply, backward sums, backward apply) — about what the fp32 y1 traffic costs — so
-// it is off there.  Measured on the bf16 engine (configs[3], MI355X): 487.2 vs 487.4 / 488.8 img/s —
-// the three recomputing GEMMs (0.56 + 0.78 + 0.86 ms, their 2-byte epilogue stores and gradient loads
-// at ~3 TB/s) cost what the removed BN passes did, so it is off by default too.  CAD_RC1=0 (default):
-// stored y1; 1: recompute on the bf16 engine; 2: on both (A/B switch; the same arithmetic bit for bit,
-// tests/test_gpu_headfuse.py).
-bool rc1_on(cad_unet* h, const DoubleConv& dc, bool ps1) {
-    static const int mode = env_flag("CAD_RC1", 0);
-    if (mode <= 0 || &dc != &h->enc[0] || dc.has_film()) return false;
-    const int e = cad::gemm_engine();
-    if (e == 1) return mode >= 2 && !ps1;
-    if (e == 2) return ps1 && dc.y1_f32 && !dc.y1b;
-    return false;
-}
-// the recomputed conv1's operands: the input as the forward read it and the weights it used
-struct Rc1Ops {
-    const void* x; int64_t ldx; const void* w;
-};
-Rc1Ops rc1_ops(cad_unet* h, const DoubleConv& dc, const float* in, int64_t ldin, const cad::Split& in_s, bool ps1) {
-    if (ps1) return {in_s.p, in_s.ld, dc.c1.ws};
-    return {in, ldin, h->rc_w};
-}
-
 // the next level's max-pool written by an encoder block's bn2 pass (bn_relu_pool_fwd)
 struct PoolOut {
     float* pool;      // fp32 pooled output (nullptr: only its twin is read)
@@ -597,31 +560,13 @@ void double_conv_fwd(cad_unet* h, DoubleConv& dc, const float* in, int64_t ldin,
     static const bool enc1_bf16 = env_flag("CAD_ENC1BF16", 0) != 0;
     dc.y1b = ps1 && (!dc.y1_f32 || enc1_bf16);
     dc.y2b = ps;
-    dc.y1_rc = rc1_on(h, dc, ps1);
-    dc.y1_rc_ps = dc.y1_rc && ps1;
-    if (dc.y1_rc) {   // statistics only; the BN apply recomputes the conv (rc1_on)
-        if (!ps1)
-            HIPCHK(hipMemcpyAsync(h->rc_w, h->P(dc.c1.pidx), sizeof(float) * (size_t)C * 9 * dc.c1.cin,
-                                  hipMemcpyDeviceToDevice, st));
-        const Rc1Ops o = rc1_ops(h, dc, in, ldin, in_s, ps1);
-        cad::RecomputeArgs r;
-        r.mode = cad::Recompute::Stats;
-        r.stats = stats;
-        if (tr) cad::conv3x3_recompute(o.x, o.ldx, dc.c1.cin, o.w, C, B, Hh, Ww, r, st);
-        bn(dc.b1, dc.c1.cin, ps1);
-        r.mode = cad::Recompute::BnRelu;
-        r.scale = dc.b1.scale; r.shift = dc.b1.shift;
-        r.out = ps ? dc.a1s : dc.a1; r.ldo = C; r.out_bf16 = ps;
-        cad::conv3x3_recompute(o.x, o.ldx, dc.c1.cin, o.w, C, B, Hh, Ww, r, st);
-    } else if (ps1) {
+    if (ps1) {
         cad::conv3x3_fwd_ps(in_s, dc.c1.cin, sv(dc.c1.ws, 9 * dc.c1.cin), C, dc.y1, C, 0, B, Hh, Ww, stats, st, dc.y1b);
     } else {
         cad::conv3x3_fwd(in, ldin, 0, dc.c1.cin, h->P(dc.c1.pidx), C, dc.y1, C, 0, B, Hh, Ww, stats, st);
     }
-    if (!dc.y1_rc) bn(dc.b1, dc.c1.cin, ps1);
-    if (dc.y1_rc) {
-        // (a1 written by the recompute above)
-    } else if (dc.has_film()) {   // FiLMDoubleConvImpl::forward (intrinsics_unet.h:38-52)
+    bn(dc.b1, dc.c1.cin, ps1);
+    if (dc.has_film()) {   // FiLMDoubleConvImpl::forward (intrinsics_unet.h:38-52)
         // pre-split GEMMs read only a1's twin (written by the same pass): the fp32 a1 is not written
         cad::film_apply(dc.y1, C, dc.b1.scale, dc.b1.shift, dc.film.gam, dc.film.bet, B, (int64_t)Hh * Ww,
                         ps ? nullptr : dc.a1, st, dc.y1b, ps ? dc.a1s : nullptr);
@@ -775,7 +720,7 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     static const bool bnsums = env_flag("CAD_BNSUMS", 1) != 0;
     int bn1_tiles = 0;
     cad::BnSums bs;
-    if (bnsums && !ps && !dc.has_film() && !dc.y1_rc && h->rc_part) {
+    if (bnsums && !ps && !dc.has_film() && h->rc_part) {
         bs.y = dc.y1; bs.ldy = C; bs.y_bf16 = dc.y1b;
         bs.mean = dc.b1.mean; bs.invstd = dc.b1.invstd; bs.scale = dc.b1.scale; bs.shift = dc.b1.shift;
         bs.part = h->rc_part; bs.part_cap = h->part_cap;
@@ -793,7 +738,7 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     // CAD_FILMFUSE=0: the separate film_affine_bwd pass)
     const int64_t HW = (int64_t)Hh * Ww;
     static const bool film_fuse = env_flag("CAD_FILMFUSE", 1) != 0;
-    const bool film_sep = dc.has_film() && (!film_fuse || dc.y1_rc);
+    const bool film_sep = dc.has_film() && !film_fuse;
     if (film_sep)
         cad::film_affine_bwd(dA1, dc.y1, C, dc.b1.scale, dc.b1.shift, B, HW, h->dscr, dc.film.dgam, dc.film.dbet, st,
                              dc.y1b, ps);
@@ -801,22 +746,7 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     // in-loader weight gradient)
     const bool ps1 = conv1_presplit(h, dc, ps, in_s);
     const bool dy1_f32 = !ps1 || (din && !(ps && dc.c1.wds));
-    if (dc.y1_rc) {   // bn1 backward on the recomputed conv1 (rc1_on): the sums, then the apply
-        if (din || (ps && dy1_f32) || (!ps && !dy1_f32)) throw std::runtime_error("recomputed conv1: unexpected block");
-        const Rc1Ops o = rc1_ops(h, dc, in, ldin, in_s, ps1);
-        cad::RecomputeArgs r;
-        r.mode = cad::Recompute::BwdSums;
-        r.scale = dc.b1.scale; r.shift = dc.b1.shift; r.mean = dc.b1.mean; r.invstd = dc.b1.invstd;
-        r.g = dA1; r.ldg = C; r.g_bf16 = ps;
-        r.part = h->rc_part;
-        cad::conv3x3_recompute(o.x, o.ldx, dc.c1.cin, o.w, C, B, Hh, Ww, r, st);
-        cad::bn_bwd_from_tiles(h->rc_part, cad::recompute_tiles(dc.c1.cin, B, Hh, Ww, C), C, M, h->P(dc.b1.widx),
-                               dc.b1.invstd, dc.b1.coef, h->G(dc.b1.widx), h->G(dc.b1.bidx), h->dscr, st);
-        r.mode = cad::Recompute::BwdApply;
-        r.coef = dc.b1.coef;
-        r.out = ps ? dYs : static_cast<void*>(dY); r.ldo = C; r.out_bf16 = ps;
-        cad::conv3x3_recompute(o.x, o.ldx, dc.c1.cin, o.w, C, B, Hh, Ww, r, st);
-    } else {
+    {
         const bool ff = dc.has_film() && !film_sep;
         cad::bn_relu_bwd(dA1, C, 0, dc.y1, C, dc.b1.mean, dc.b1.invstd, dc.b1.scale, dc.b1.shift, h->P(dc.b1.widx), M,
                          h->dscr, dc.b1.coef, h->G(dc.b1.widx), h->G(dc.b1.bidx), dy1_f32 ? dY : nullptr, st,
@@ -1256,27 +1186,6 @@ int64_t cad_unet_debug_buffer(cad_unet* h, const char* name, float* host, int64_
     if (!p || cnt < 0) {
         g_err = "unknown debug buffer '" + n + "'";
         return -1;
-    }
-    if (l == 0 && n == "enc0_y1" && h->enc[0].y1_rc) {
-        // the last forward recomputed enc1.conv1 instead of storing it: run it once more into y1 from
-        // the same input and weights (cad_unet_debug_buffer is a test hook; CAD_RC1=0 stores y1)
-        DoubleConv& dc = h->enc[0];
-        const bool ps1 = dc.y1_rc_ps;   // the operands the forward used (not re-derived: CAD_ENC1PS)
-        const cad::Split in_s = ps1 ? sv(h->x0s, h->x0_ld) : cad::Split{};
-        const Rc1Ops o = rc1_ops(h, dc, h->x0, h->x0_ld, in_s, ps1);
-        cad::RecomputeArgs r;
-        r.mode = cad::Recompute::Store;
-        r.out = dc.y1; r.ldo = h->Cl(0);
-        try {
-            cad::conv3x3_recompute(o.x, o.ldx, dc.c1.cin, o.w, h->Cl(0), B, h->Hl(0), h->Wl(0), r, nullptr);
-        } catch (const std::exception& e) {
-            g_err = e.what();
-            return -1;
-        }
-        if (hipDeviceSynchronize() != hipSuccess) {
-            g_err = "recomputing enc0_y1 failed";
-            return -1;
-        }
     }
     if (n == "dout0" && h->head_fused) {
         g_err = "debug buffer 'dout0' is not written when decoder level 0 is fused with the head (CAD_HEADFUSE=0 keeps it)";

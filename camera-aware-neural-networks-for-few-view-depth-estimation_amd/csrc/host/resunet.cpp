@@ -540,9 +540,18 @@ cad::Split tw(const void* p, int64_t ld, int coff = 0) {
 // not the window path); xs: the stride-2 1x1 input subsample buffer.
 // the MX-fp8 copy of unit u's input that its producer pass can write (nullptr: u quantises itself —
 // not fp8, or its A operand is an im2col / subsampled copy of the input); C = the input's channels
+// CAD_MXPREQ=0: every fp8 contraction quantises its operand itself (mx8_quantize), none is written
+// by the producing pass (A/B switch; bit-identical: tests/test_gpu_resunet_switches.py)
+bool mx_preq_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("CAD_MXPREQ");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 const cad::Mx8* preq_for(cad_resunet* h, const Unit& u, int64_t rows, cad::Mx8& m) {
     const RConv& c = u.c;
-    if (!h->fp8 || !c.x8 || !(c.win || (c.k == 1 && c.s == 1)) || c.cin % 32 || rows * up128(c.cin) > h->xq_cap)
+    if (!mx_preq_on() || !h->fp8 || !c.x8 || !(c.win || (c.k == 1 && c.s == 1)) || c.cin % 32 || rows * up128(c.cin) > h->xq_cap)
         return nullptr;
     m.q = h->xqp; m.s = h->xscp; m.ld = up128(c.cin); m.coff = 0;
     return &m;
@@ -611,12 +620,21 @@ void unit_fwd(cad_resunet* h, Unit& u, cad::Split in, int B, int Hin, int Win, v
 // the per-step weight conversions (bf16 twins, dgrad / ConvT repacks, transposes) batched into
 // k_weight_prep launches of up to kWPrepMaxJobs tensors each (one launch per tensor before: ~70 small
 // launches per forward and per backward)
+// CAD_WPREPBATCH=0: one k_weight_prep launch per tensor (A/B switch; bit-identical:
+// tests/test_gpu_resunet_switches.py)
+int wprep_batch() {
+    static const int n = [] {
+        const char* e = std::getenv("CAD_WPREPBATCH");
+        return (e && e[0] == '0') ? 1 : cad::kWPrepMaxJobs;
+    }();
+    return n;
+}
 struct PrepBatch {
     cad::WPrepList L{};
     hipStream_t st;
     explicit PrepBatch(hipStream_t s) : st(s) {}
     void add(int kind, const float* src, float* d32, void* d16, int cout, int cin, int64_t n) {
-        if (L.njobs == cad::kWPrepMaxJobs) flush();
+        if (L.njobs == wprep_batch()) flush();
         cad::WPrepJob& j = L.job[L.njobs++];
         j.src = src; j.d32 = d32; j.d16 = d16; j.kind = kind; j.cout = cout; j.cin = cin; j.n = n;
     }
@@ -624,7 +642,9 @@ struct PrepBatch {
         if (L.njobs) cad::weight_prep(L, st);
         L.njobs = 0;
     }
-    ~PrepBatch() { flush(); }
+    // the owner flushes explicitly; unwinding from an exception drops the pending jobs (a destructor
+    // must not launch, nor throw: weight_prep can)
+    ~PrepBatch() = default;
 };
 
 void prep_weights_fwd(cad_resunet* h, hipStream_t st) {
@@ -647,6 +667,7 @@ void prep_weights_fwd(cad_resunet* h, hipStream_t st) {
         // repack_convT_fwd + its twin
         pb.add(cad::WPREP_CONVT, h->P(d.up_w), d.wf, d.wfs, d.cout_up, d.cin_up, (int64_t)4 * d.cout_up * d.cin_up);
     }
+    pb.flush();
 }
 
 void forward(cad_resunet* h, const float* rgb, float* depth, int B, hipStream_t st) {
@@ -736,6 +757,7 @@ void prep_weights_bwd(cad_resunet* h, hipStream_t st) {
         dw(d.u2.c);
         pb.add(cad::WPREP_SPLIT, h->P(d.up_w), nullptr, d.wms, d.cout_up, d.cin_up, (int64_t)4 * d.cout_up * d.cin_up);
     }
+    pb.flush();
 }
 
 // BN (+ReLU) backward of unit u: g (ld ldg, coff) -> dYs twin; then the conv's wgrad from the
@@ -1144,6 +1166,68 @@ cad_status cad_resunet_backward(cad_resunet* h, const float* ddepth, void* strea
         backward(h, ddepth, S(stream));
         RCHK(hipGetLastError());
     });
+}
+
+// Test hook (tests/test_gpu_fullsize_bf16.py): a buffer of the last train-mode forward as fp32 rows.
+//   "y:<conv>"      the pre-BN output of convolution <conv> ("encoder.conv1", "encoder.layer2.0.conv2",
+//                   "encoder.layer1.0.downsample.0", "dec3.conv.conv1", ...): the stored bf16 values, widened
+//   "scale:<bn>" / "shift:<bn>"  the BN-apply coefficients of BatchNorm <bn> ("encoder.layer1.0.bn1", ...):
+//                   a BN-ReLU's decision is fma(y, scale, shift) > 0, as k_bn_relu_fwd / _bwd evaluate it
+//   "out:<block>"   a bottleneck's output relu(bn3 + shortcut) ("encoder.layer1.0"), "out:encoder.stem"
+//                   relu(bn1(conv1)), "out:dec<l>" a decoder block's output (fp32)
+// Returns the element count (host == nullptr: only the count), -1 for an unknown name.
+int64_t cad_resunet_debug_buffer(cad_resunet* h, const char* name, float* host, int64_t numel) {
+    int64_t cnt = -1;
+    cad_status st = rguard([&] {
+        need(h && name, "null argument");
+        const std::string n(name);
+        const int B = h->fwd_B > 0 ? h->fwd_B : h->Bmax;
+        const int H1 = (h->H - 1) / 2 + 1, W1 = (h->W - 1) / 2 + 1;
+        const void* p = nullptr;
+        bool bf16 = false;
+        auto conv_name = [&](const Unit& u) {
+            const std::string& w = h->params[u.c.pidx].name;
+            return w.substr(0, w.size() - 7);   // strip ".weight"
+        };
+        auto bn_name = [&](const Unit& u) {
+            const std::string& w = h->params[u.b.widx].name;
+            return w.substr(0, w.size() - 7);
+        };
+        auto unit = [&](const Unit& u, int64_t M) {
+            if (u.c.pidx < 0) return;
+            if (n == "y:" + conv_name(u)) { p = u.y; bf16 = true; cnt = M * u.c.cout; }
+            else if (n == "scale:" + bn_name(u)) { p = u.b.scale; cnt = u.b.C; }
+            else if (n == "shift:" + bn_name(u)) { p = u.b.shift; cnt = u.b.C; }
+        };
+        unit(h->stem, h->M(B, H1, W1));
+        if (n == "out:encoder.stem") { p = h->s_out; cnt = h->M(B, H1, W1) * 64; }
+        for (const Bott& b : h->blocks) {
+            unit(b.u1, h->M(B, b.H, b.W));
+            for (const Unit* u : {&b.u2, &b.u3, &b.ud}) unit(*u, h->M(B, b.Ho, b.Wo));
+            if (n == "out:" + b.prefix.substr(0, b.prefix.size() - 1)) { p = b.out; cnt = h->M(B, b.Ho, b.Wo) * b.cout; }
+        }
+        for (const Dec& d : h->dec) {
+            unit(d.u1, h->M(B, d.H, d.W));
+            unit(d.u2, h->M(B, d.H, d.W));
+            if (n == "out:dec" + std::to_string(d.l)) { p = d.out; cnt = h->M(B, d.H, d.W) * d.C; }
+        }
+        need(p != nullptr, "unknown debug buffer '" + n + "'");
+        if (!host) return;
+        need(numel >= cnt, "debug buffer: host array too small");
+        RCHK(hipSetDevice(h->device));
+        RCHK(hipDeviceSynchronize());
+        if (bf16) {
+            std::vector<uint16_t> tmp((size_t)cnt);
+            RCHK(hipMemcpy(tmp.data(), p, sizeof(uint16_t) * cnt, hipMemcpyDeviceToHost));
+            for (int64_t i = 0; i < cnt; ++i) {
+                const uint32_t u = (uint32_t)tmp[(size_t)i] << 16;
+                std::memcpy(host + i, &u, 4);
+            }
+        } else {
+            RCHK(hipMemcpy(host, p, sizeof(float) * cnt, hipMemcpyDeviceToHost));
+        }
+    });
+    return st == CAD_OK ? cnt : -1;
 }
 
 int cad_resunet_num_stages(const cad_resunet* h) { return h ? num_stages(h) : -1; }

@@ -423,24 +423,6 @@ CAD_KT(KConvFwdP1B, (k_conv3x3_fwd_bf16p<WM, WN, KB, EpiStoreB16>),
 CAD_KT(KConvFwdSP1B, (k_conv3x3_fwd_bf16p<WM, WN, KB, EpiStoreStatsB16>),
        "void cad::k_conv3x3_fwd_bf16p<%d, %d, %d, cad::EpiStoreStatsB16>(cad::GemmArgs)")
 CAD_KT(KDenseWgradP1, (k_dense_wgrad_bf16p<WM, WN, KB>), "void cad::k_dense_wgrad_bf16p<%d, %d, %d>(cad::GemmArgs)")
-// recomputed convolution (conv3x3_recompute): S3 in-loader and B1 pre-split forms
-#define CAD_RC_KT(T, E, ES)                                                                                   \
-    CAD_KT(KRcS3##T, (k_conv3x3_fwd_s3<WM, WN, KB, E>), "void cad::k_conv3x3_fwd_s3<%d, %d, %d, cad::" ES ">(cad::GemmArgs)") \
-    CAD_KT(KRcP1##T, (k_conv3x3_fwd_bf16p<WM, WN, KB, E>), "void cad::k_conv3x3_fwd_bf16p<%d, %d, %d, cad::" ES ">(cad::GemmArgs)")
-using EpiBnReluF = EpiBnRelu<false>;
-using EpiBnReluB = EpiBnRelu<true>;
-using EpiBnBwdSumsF = EpiBnBwdSums<false>;
-using EpiBnBwdSumsB = EpiBnBwdSums<true>;
-using EpiBnBwdApplyF = EpiBnBwdApply<false, false>;
-using EpiBnBwdApplyB = EpiBnBwdApply<true, true>;
-CAD_RC_KT(Stats, EpiStatsOnly, "EpiStatsOnly")
-CAD_RC_KT(Relu, EpiBnReluF, "EpiBnRelu<false>")
-CAD_RC_KT(ReluB, EpiBnReluB, "EpiBnRelu<true>")
-CAD_RC_KT(Sums, EpiBnBwdSumsF, "EpiBnBwdSums<false>")
-CAD_RC_KT(SumsB, EpiBnBwdSumsB, "EpiBnBwdSums<true>")
-CAD_RC_KT(Apply, EpiBnBwdApplyF, "EpiBnBwdApply<false, false>")
-CAD_RC_KT(ApplyB, EpiBnBwdApplyB, "EpiBnBwdApply<true, true>")
-#undef CAD_RC_KT
 CAD_KT(KConvTFwdP1T, (k_convT_fwd_bf16pt<WM, WN, KB>), "void cad::k_convT_fwd_bf16pt<%d, %d, %d>(cad::GemmArgs)")
 CAD_KT(KConvTDgradP1B, (k_convT_dgrad_bf16pb<WM, WN, KB>), "void cad::k_convT_dgrad_bf16pb<%d, %d, %d>(cad::GemmArgs)")
 CAD_KT(KDenseAddP1, (k_dense_bf16p<WM, WN, KB, EpiStoreAdd>), "void cad::k_dense_bf16p<%d, %d, %d, cad::EpiStoreAdd>(cad::GemmArgs)")
@@ -868,6 +850,8 @@ int conv3x3_stats_rows(int cin, int B, int H, int W, int cout, bool ps) {
 
 void conv3x3_fwd(const float* x, int64_t ldx, int xcoff, int cin, const float* w, int cout, float* y,
                  int64_t ldy, int ycoff, int B, int H, int W, float* stats, hipStream_t st) {
+    CAD_NO_ALIAS("conv3x3_fwd", {aview(y, (int64_t)B * H * W, ldy, ycoff, cout, 4, "y")},
+                 {aview(x, (int64_t)B * H * W, ldx, xcoff, cin, 4, "x"), aview(w, cout, 9 * cin, 0, 9 * cin, 4, "w")});
     GemmArgs a{};
     a.M = B * H * W; a.N = cout; a.K = 9 * cin;
     a.B = B; a.H = H; a.W = W;
@@ -887,6 +871,8 @@ void conv3x3_fwd(const float* x, int64_t ldx, int xcoff, int cin, const float* w
 
 void convT_fwd(const float* x, int64_t ldx, int cin, const float* wf, const float* bias, int cout,
                float* y, int64_t ldy, int ycoff, int B, int H, int W, hipStream_t st) {
+    CAD_NO_ALIAS("convT_fwd", {aview(y, (int64_t)B * 4 * H * W, ldy, ycoff, cout, 4, "y")},
+                 {aview(x, (int64_t)B * H * W, ldx, 0, cin, 4, "x"), aview(wf, 4 * cout, cin, 0, cin, 4, "w")});
     GemmArgs a{};
     a.M = B * H * W; a.N = 4 * cout; a.K = cin;
     a.B = B; a.H = H; a.W = W;
@@ -898,6 +884,8 @@ void convT_fwd(const float* x, int64_t ldx, int cin, const float* wf, const floa
 
 void conv3x3_dgrad(const float* dz, int cout, const float* wd, int cin, float* dx, int64_t lddx,
                    int B, int H, int W, hipStream_t st) {
+    CAD_NO_ALIAS("conv3x3_dgrad", {aview(dx, (int64_t)B * H * W, lddx, 0, cin, 4, "dx")},
+                 {aview(dz, (int64_t)B * H * W, cout, 0, cout, 4, "dz"), aview(wd, cin, 9 * cout, 0, 9 * cout, 4, "w")});
     GemmArgs a{};
     a.M = B * H * W; a.N = cin; a.K = 9 * cout;
     a.B = B; a.H = H; a.W = W;
@@ -913,6 +901,8 @@ void conv3x3_dgrad(const float* dz, int cout, const float* wd, int cin, float* d
 
 void convT_dgrad(const float* g, int64_t ldg, int gcoff, int cout, const float* wm, int cin, float* dx,
                  int B, int H, int W, hipStream_t st) {
+    CAD_NO_ALIAS("convT_dgrad", {aview(dx, (int64_t)B * H * W, cin, 0, cin, 4, "dx")},
+                 {aview(g, (int64_t)B * 4 * H * W, ldg, gcoff, cout, 4, "g"), aview(wm, cin, 4 * cout, 0, 4 * cout, 4, "w")});
     GemmArgs a{};
     a.M = B * H * W; a.N = cin; a.K = 4 * cout;
     a.B = B; a.H = H; a.W = W;
@@ -930,6 +920,9 @@ int64_t wgrad_slab_floats(int M, int N, int Kpix) {
 
 void conv3x3_wgrad(const float* dz, int cout, const float* x, int64_t ldx, int xcoff, int cin, float* dw,
                    int B, int H, int W, float* slab, int64_t slab_cap, hipStream_t st) {
+    CAD_NO_ALIAS("conv3x3_wgrad",
+                 {aview(dw, cout, 9 * cin, 0, 9 * cin, 4, "dw"), aview(slab, 1, slab_cap, 0, slab ? slab_cap : 0, 4, "slab")},
+                 {aview(dz, (int64_t)B * H * W, cout, 0, cout, 4, "dz"), aview(x, (int64_t)B * H * W, ldx, xcoff, cin, 4, "x")});
     GemmArgs a{};
     a.M = cout; a.N = 9 * cin; a.K = B * H * W;
     a.B = B; a.H = H; a.W = W;
@@ -945,6 +938,9 @@ void conv3x3_wgrad(const float* dz, int cout, const float* x, int64_t ldx, int x
 
 void convT_wgrad(const float* x, int cin, const float* g, int64_t ldg, int gcoff, int cout, float* dw,
                  int B, int H, int W, float* slab, int64_t slab_cap, hipStream_t st) {
+    CAD_NO_ALIAS("convT_wgrad",
+                 {aview(dw, cin, 4 * cout, 0, 4 * cout, 4, "dw"), aview(slab, 1, slab_cap, 0, slab ? slab_cap : 0, 4, "slab")},
+                 {aview(x, (int64_t)B * H * W, cin, 0, cin, 4, "x"), aview(g, (int64_t)B * 4 * H * W, ldg, gcoff, cout, 4, "g")});
     GemmArgs a{};
     a.M = cin; a.N = 4 * cout; a.K = B * H * W;
     a.B = B; a.H = H; a.W = W;
@@ -963,6 +959,7 @@ void split_rows(const float* x, int64_t ldx, int xcoff, int C, int64_t M, void* 
                 hipStream_t st) {
     if (C % 8 || xcoff % 4 || ldx % 4 || ocoff % 8 || ldo % 8) throw std::runtime_error("split_rows: alignment");
     if (split_planes() != 1) throw std::runtime_error("split_rows needs the bf16 engine");
+    CAD_NO_ALIAS("split_rows", {aview(out, M, ldo, ocoff, C, 2, "out")}, {aview(x, M, ldx, xcoff, C, 4, "x")});
     const int G = C / 8;
     const int64_t n = M * G;
     if (n == 0) return;
@@ -981,6 +978,8 @@ void conv3x3_fwd_ps(Split x, int cin, Split w, int cout, float* y, int64_t ldy, 
                     float* stats, hipStream_t st, bool y_bf16) {
     ps_check(x, cin, "conv3x3_fwd x");
     ps_check(w, 9 * cin, "conv3x3_fwd w");
+    CAD_NO_ALIAS("conv3x3_fwd_ps", {aview(y, (int64_t)B * H * W, ldy, ycoff, cout, y_bf16 ? 2 : 4, "y")},
+                 {aview(x.p, (int64_t)B * H * W, x.ld, x.coff, cin, 2, "x"), aview(w.p, cout, w.ld, w.coff, 9 * cin, 2, "w")});
     GemmArgs a{};
     a.M = B * H * W; a.N = cout; a.K = 9 * cin;
     a.B = B; a.H = H; a.W = W;
@@ -1060,6 +1059,10 @@ bool conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t 
     }
     ps_check(dz, cout, "conv3x3_dgrad dz");
     ps_check(wd, 9 * cout, "conv3x3_dgrad w");
+    CAD_NO_ALIAS("conv3x3_dgrad_ps",
+                 {aview(dx, (int64_t)B * H * W, lddx, 0, hi ? split_n : cin, dx_bf16 ? 2 : 4, "dx"),
+                  aview(hi, (int64_t)B * H * W, ldhi, 0, hi ? cin - split_n : 0, 2, "hi (split store)")},
+                 {aview(dz.p, (int64_t)B * H * W, dz.ld, dz.coff, cout, 2, "dz"), aview(wd.p, cin, wd.ld, wd.coff, 9 * cout, 2, "w")});
     GemmArgs a{};
     a.M = B * H * W; a.N = cin; a.K = 9 * cout;
     a.B = B; a.H = H; a.W = W;
@@ -1221,6 +1224,10 @@ void conv3x3_wgrad_ps(Split dz, int cout, Split x, int cin, float* dw, int B, in
                       int64_t slab_cap, hipStream_t st) {
     ps_check(dz, cout, "conv3x3_wgrad dz");
     ps_check(x, cin, "conv3x3_wgrad x");
+    CAD_NO_ALIAS("conv3x3_wgrad_ps",
+                 {aview(dw, cout, 9 * cin, 0, 9 * cin, 4, "dw"), aview(slab, 1, slab_cap, 0, slab ? slab_cap : 0, 4, "slab")},
+                 {aview(dz.p, (int64_t)B * H * W, dz.ld, dz.coff, cout, 2, "dz"),
+                  aview(x.p, (int64_t)B * H * W, x.ld, x.coff, cin, 2, "x")});
     constexpr int64_t kPairPer = 64 * 576;
     if (!g_no_wgwin && cout == 32 && cin == 32 && dz.ld == 32 && x.ld == 32 && dz.coff == 0 && x.coff == 0 &&
         W % 2 == 0 && slab && slab_cap >= 2 * kPairPer && wg_pair32()) {
@@ -1275,6 +1282,11 @@ void dense_fwd_ps(Split x, int K, Split w, int N, float* y, int64_t ldy, int yco
         throw std::runtime_error("dense GEMM: an added matrix of its own stride takes no mask / offset");
     ps_check(x, K, "dense x");
     ps_check(w, K, "dense w");
+    // add == y (same rows): the epilogue's in-place accumulate, declared
+    CAD_NO_ALIAS("dense_fwd_ps", {aview(y, M, ldy, ycoff, N, y_bf16 ? 2 : 4, "y")},
+                 {aview(x.p, M, x.ld, x.coff, K, 2, "x"), aview(w.p, N, w.ld, w.coff, K, 2, "w"),
+                  aview(add == y && ldadd == ldy ? nullptr : add, M, ldadd, ldadd == ldy ? ycoff : 0, N, 4, "add"),
+                  aview(mask, M, ldy, ycoff, N, 4, "mask")});
     if (M > INT32_MAX) throw std::runtime_error("dense GEMM: too many rows");
     GemmArgs a{};
     a.M = (int)M; a.N = N; a.K = K;
@@ -1331,6 +1343,8 @@ void dense_wgrad_ps(Split dz, int N, Split x, int K, float* dw, int64_t ldw, int
                     hipStream_t st) {
     ps_check(dz, N, "dense wgrad dz");
     ps_check(x, K, "dense wgrad x");
+    CAD_NO_ALIAS("dense_wgrad_ps", {aview(dw, N, ldw, 0, K, 4, "dw"), aview(slab, 1, slab_cap, 0, slab ? slab_cap : 0, 4, "slab")},
+                 {aview(dz.p, M, dz.ld, dz.coff, N, 2, "dz"), aview(x.p, M, x.ld, x.coff, K, 2, "x")});
     if (ldw != K) throw std::runtime_error("dense wgrad: dw rows must be dense");
     if (M > INT32_MAX) throw std::runtime_error("dense GEMM: too many rows");
     GemmArgs a{};
@@ -1348,54 +1362,6 @@ void dense_wgrad_ps(Split dz, int N, Split x, int K, float* dw, int64_t ldw, int
     a.C = s == 1 ? dw : slab;
     launch_kb<KDenseWgradP1, 32>(c, kb, a, s, st);
     if (s > 1) finish_slabs(slab, s, per, dw, st);
-}
-
-int recompute_tiles(int cin, int B, int H, int W, int cout) {
-    (void)cin;
-    return cdiv((int64_t)B * H * W, tile_m(pick_cfg(B * H * W, cout)));
-}
-
-void conv3x3_recompute(const void* x, int64_t ldx, int cin, const void* w, int cout, int B, int H, int W,
-                       const RecomputeArgs& r, hipStream_t st) {
-    const bool ps = engine() == 2;
-    if (ps ? pick_win_ps(cin, W, cout, 0).R != 0 : pick_win(cin, W, cout).R != 0)
-        throw std::runtime_error("conv3x3_recompute: shape runs the window kernel (not the im2col GEMM)");
-    if (engine() == 0) throw std::runtime_error("conv3x3_recompute: not built for the f32 engine");
-    GemmArgs a{};
-    a.M = B * H * W; a.N = cout; a.K = 9 * cin;
-    a.B = B; a.H = H; a.W = W;
-    a.A = static_cast<const float*>(x); a.lda = ldx; a.a_coff = 0; a.a_cin = cin;
-    a.Bm = static_cast<const float*>(w); a.ldb = 9 * cin; a.b_coff = 0;
-    a.C = static_cast<float*>(r.out); a.ldc = r.ldo; a.c_coff = 0;
-    a.stats = r.stats;
-    a.bn_scale = r.scale; a.bn_shift = r.shift; a.bn_mean = r.mean; a.bn_invstd = r.invstd; a.bn_coef = r.coef;
-    a.bn_g = r.g; a.bn_ldg = r.ldg; a.bn_part = r.part;
-    const Cfg c = pick_cfg(a.M, a.N);
-    // exactly the K-stage depth / order of conv3x3_fwd (S3) and conv3x3_fwd_ps (B1) for this shape
-    const int kb = ps ? ps_kb(true, c) : kS3KB;
-    a.kstages_per_split = cdiv(a.K, kb);
-    if (ps) a.cimajor = cin % kb == 0;
-    const bool gb = r.g_bf16, ob = r.out_bf16;
-    switch (r.mode) {
-        case Recompute::Store:
-            ps ? launch_kb<KConvFwdP1, 32, 64>(c, kb, a, 1, st) : launch_kb<KConvFwd3, kS3KB>(c, kb, a, 1, st);
-            return;
-        case Recompute::Stats:
-            ps ? launch_kb<KRcP1Stats, 32, 64>(c, kb, a, 1, st) : launch_kb<KRcS3Stats, kS3KB>(c, kb, a, 1, st);
-            return;
-        case Recompute::BnRelu:
-            if (ob != ps) throw std::runtime_error("conv3x3_recompute: BnRelu writes bf16 exactly on the bf16 engine");
-            ps ? launch_kb<KRcP1ReluB, 32, 64>(c, kb, a, 1, st) : launch_kb<KRcS3Relu, kS3KB>(c, kb, a, 1, st);
-            return;
-        case Recompute::BwdSums:
-            if (gb != ps) throw std::runtime_error("conv3x3_recompute: upstream gradient is bf16 exactly on the bf16 engine");
-            ps ? launch_kb<KRcP1SumsB, 32, 64>(c, kb, a, 1, st) : launch_kb<KRcS3Sums, kS3KB>(c, kb, a, 1, st);
-            return;
-        case Recompute::BwdApply:
-            if (gb != ps || ob != ps) throw std::runtime_error("conv3x3_recompute: BwdApply bf16 exactly on the bf16 engine");
-            ps ? launch_kb<KRcP1ApplyB, 32, 64>(c, kb, a, 1, st) : launch_kb<KRcS3Apply, kS3KB>(c, kb, a, 1, st);
-            return;
-    }
 }
 
 // CAD_BIGT bit 1: ConvT forward, bit 2: ConvT dgrad on the 256 x 128 tiles (bf16 outputs).  Measured at
@@ -1441,6 +1407,8 @@ void convT_fwd_ps(Split x, int cin, Split wf, const float* bias, int cout, float
                   int H, int W, hipStream_t st, bool y_bf16) {
     ps_check(x, cin, "convT_fwd x");
     ps_check(wf, cin, "convT_fwd w");
+    CAD_NO_ALIAS("convT_fwd_ps", {aview(y, (int64_t)B * 4 * H * W, ldy, ycoff, cout, y_bf16 ? 2 : 4, "y")},
+                 {aview(x.p, (int64_t)B * H * W, x.ld, x.coff, cin, 2, "x"), aview(wf.p, 4 * cout, wf.ld, wf.coff, cin, 2, "w")});
     GemmArgs a{};
     a.M = B * H * W; a.N = 4 * cout; a.K = cin;
     a.B = B; a.H = H; a.W = W;
@@ -1465,6 +1433,8 @@ void convT_fwd_ps(Split x, int cin, Split wf, const float* bias, int cout, float
 void convT_dgrad_ps(Split g, int cout, Split wm, int cin, float* dx, int B, int H, int W, hipStream_t st, bool dx_bf16) {
     ps_check(g, cout, "convT_dgrad g");
     ps_check(wm, 4 * cout, "convT_dgrad w");
+    CAD_NO_ALIAS("convT_dgrad_ps", {aview(dx, (int64_t)B * H * W, cin, 0, cin, dx_bf16 ? 2 : 4, "dx")},
+                 {aview(g.p, (int64_t)B * 4 * H * W, g.ld, g.coff, cout, 2, "g"), aview(wm.p, cin, wm.ld, wm.coff, 4 * cout, 2, "w")});
     GemmArgs a{};
     a.M = B * H * W; a.N = cin; a.K = 4 * cout;
     a.B = B; a.H = H; a.W = W;
@@ -1486,6 +1456,10 @@ void convT_wgrad_ps(Split x, int cin, Split g, int cout, float* dw, int B, int H
                     int64_t slab_cap, hipStream_t st) {
     ps_check(x, cin, "convT_wgrad x");
     ps_check(g, cout, "convT_wgrad g");
+    CAD_NO_ALIAS("convT_wgrad_ps",
+                 {aview(dw, cin, 4 * cout, 0, 4 * cout, 4, "dw"), aview(slab, 1, slab_cap, 0, slab ? slab_cap : 0, 4, "slab")},
+                 {aview(x.p, (int64_t)B * H * W, x.ld, x.coff, cin, 2, "x"),
+                  aview(g.p, (int64_t)B * 4 * H * W, g.ld, g.coff, cout, 2, "g")});
     GemmArgs a{};
     a.M = cin; a.N = 4 * cout; a.K = B * H * W;
     a.B = B; a.H = H; a.W = W;

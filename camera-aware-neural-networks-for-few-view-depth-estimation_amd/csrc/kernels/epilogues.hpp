@@ -204,183 +204,6 @@ struct EpiConvTOut {
 };
 using EpiConvT = EpiConvTOut<false>;
 using EpiConvTB16 = EpiConvTOut<true>;
-// ---------------------------------------------------------------------------------------------
-// Recomputed convolution (enc1.conv1: K = 9 x 8 on the raw image — cheaper to recompute from its
-// 16-byte-per-pixel input than to store and re-read its fp32 output, 256 B per pixel at f = 64).
-// The same GEMM (same kernel, tile and K order) is launched once per consumer, and the epilogue does
-// the consumer's work on the accumulators, which equal the values the stored path would have written:
-//   EpiStatsOnly     BN statistics only (the forward's EpiStoreStats without its store);
-//   EpiBnRelu<OB16>  a = relu(y scale + shift) (k_bn_relu_fwd_rows' arithmetic), fp32 or bf16 rows;
-//   EpiBnBwdSums<GB> per-tile fp64 partials of sum dz, sum dz xhat (dz = g [z > 0], xhat =
-//                    (y - mean) invstd: OpBnBwd's arithmetic) -> a.bn_part [tile][2][N];
-//   EpiBnBwdApply<GB, OB16>  dy = k0 dz - k1 - k2 xhat (k_bn_relu_bwd_rows' arithmetic).
-// g (the upstream gradient a.bn_g, rows of a.bn_ldg) is bf16 (GB) or fp32.
-// ---------------------------------------------------------------------------------------------
-struct EpiStatsOnly : EpiStore {
-    static constexpr bool STATS = true;
-    static constexpr bool NOSTORE = true;
-};
-__device__ __forceinline__ float epi_bn_relu(float y, float s, float t) { return fmaxf(__fmaf_rn(y, s, t), 0.f); }
-// One lane's view of a 32x32 block in the structured epilogues: rows mb0 + 4h + (r & 3) + 8 (r >> 2)
-// (h = lane >> 5; mb0 uniform over the wave), column n.  Gradient loads and output stores go through
-// buffer descriptors based at the block's first row (32-bit offsets whatever the tensor's size), all
-// 16 loads issued before any use.
-struct EpiRows {
-    int h, mb0;
-    __device__ EpiRows(int mbase) : h((threadIdx.x & 63) >> 5), mb0(mbase - 4 * ((threadIdx.x & 63) >> 5)) {}
-    __device__ int row(int r) const { return 4 * h + (r & 3) + 8 * (r >> 2); }
-};
-template <bool GB>
-__device__ __forceinline__ void epi_load_g16(const GemmArgs& a, const EpiRows& e, int n, float (&g)[16]) {
-    constexpr int ES = GB ? 2 : 4;
-    const __amdgpu_buffer_rsrc_t rs =
-        make_rsrc(reinterpret_cast<const float*>(static_cast<const char*>(a.bn_g) + (int64_t)e.mb0 * a.bn_ldg * ES));
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int row = e.row(r);
-        const uint32_t off = e.mb0 + row < a.M ? (uint32_t)(((int64_t)row * a.bn_ldg + n) * ES) : kOOB;
-        if constexpr (GB)
-            g[r] = (float)__builtin_bit_cast(__bf16, (uint16_t)__builtin_amdgcn_raw_buffer_load_b16(rs, off, 0, 0));
-        else
-            g[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
-    }
-}
-template <bool OB16>
-__device__ __forceinline__ void epi_store16(const GemmArgs& a, const EpiRows& e, int n, const float (&v)[16]) {
-    constexpr int ES = OB16 ? 2 : 4;
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const float*>(
-        reinterpret_cast<const char*>(a.C) + ((int64_t)e.mb0 * a.ldc + a.c_coff) * ES));
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int row = e.row(r);
-        const uint32_t off = e.mb0 + row < a.M ? (uint32_t)(((int64_t)row * a.ldc + n) * ES) : kOOB;
-        if constexpr (OB16)
-            __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, (__bf16)v[r]), rs, off, 0, 0);
-        else
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[r]), rs, off, 0, 0);
-    }
-}
-template <bool OB16>
-struct EpiBnRelu {
-    static constexpr bool STATS = false;
-    static constexpr bool BF16 = false;   // (row-major store path unused: structured)
-    static constexpr bool ADD = false;
-    static constexpr bool STRUCTURED = true;
-    __device__ void operator()(const GemmArgs&, int, int, float, int) const {}
-    // one lane's 16 accumulator rows of a 32x32 block: rows mbase + (r&3) + 8(r>>2), column n
-    __device__ void block(const GemmArgs& a, int mbase, int n, const floatx16& acc) const {
-        if (n >= a.N) return;
-        const EpiRows e(mbase);
-        const float sc = a.bn_scale[n], sh = a.bn_shift[n];
-        float o[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[r] = epi_bn_relu(acc[r], sc, sh);
-        epi_store16<OB16>(a, e, n, o);
-    }
-};
-// The BN column parameters and dL/da of up to 4 blocks (MI x NJ), loaded before any block is
-// processed (gemm_epilogue_t's prefetch hook): the recomputed convolutions have K = 72, so the epilogue's
-// memory latency, not the MFMA loop, sets their time.
-template <bool GB>
-struct EpiBnPrefetch {
-    float g[4][16];
-    float sc[4], sh[4], mu[4], is[4];
-    template <int MI, int NJ>
-    __device__ void prefetch(const GemmArgs& a, int mbase, int nbase) {
-        static_assert(MI * NJ <= 4, "prefetch capacity");
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int n = min(nbase + 32 * j, a.N - 1);
-            sc[j] = a.bn_scale[n], sh[j] = a.bn_shift[n], mu[j] = a.bn_mean[n], is[j] = a.bn_invstd[n];
-        }
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) epi_load_g16<GB>(a, EpiRows(mbase + 32 * i), min(nbase + 32 * j, a.N - 1), g[i * NJ + j]);
-    }
-};
-template <bool GB>
-struct EpiBnBwdSums : EpiBnPrefetch<GB> {
-    static constexpr bool STATS = false;
-    static constexpr bool BF16 = false;
-    static constexpr bool ADD = false;
-    static constexpr bool STRUCTURED = true;
-    static constexpr bool FINISH = true;
-    static constexpr bool PREFETCH = true;
-    double s0[4] = {0.0, 0.0, 0.0, 0.0}, s1[4] = {0.0, 0.0, 0.0, 0.0};   // per block column j (NJ <= 4)
-    __device__ void operator()(const GemmArgs&, int, int, float, int) const {}
-    __device__ void block_p(const GemmArgs& a, int mbase, int n, const floatx16& acc, int b, int j) {
-        if (n >= a.N) return;
-        const EpiRows e(mbase);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            if (e.mb0 + e.row(r) >= a.M) continue;
-            const float y = acc[r];
-            const float z = __fmaf_rn(y, this->sc[j], this->sh[j]);
-            const float dz = z > 0.f ? this->g[b][r] : 0.f;
-            const float xh = (y - this->mu[j]) * this->is[j];
-            s0[j] += dz;
-            s1[j] += (double)dz * xh;
-        }
-    }
-    // lanes L, L + 32 (same column) -> waves of one column group (LDS, fp64) -> a.bn_part[tile][2][N]
-    template <int WM, int WN, int NJ>
-    __device__ void finish(const GemmArgs& a, float* ldsf, int tile_x, int n0) {
-        static_assert(NJ <= 4, "columns per lane");
-        constexpr int BN = 32 * NJ * WN;
-        double* lds = reinterpret_cast<double*>(ldsf);
-        const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-        const int wm = wave / WN, wn = wave % WN;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const double t0 = s0[j] + __shfl_xor(s0[j], 32), t1 = s1[j] + __shfl_xor(s1[j], 32);
-            if (lane < 32) {
-                double* r = lds + ((int64_t)wm * BN + wn * 32 * NJ + j * 32 + lane) * 2;
-                r[0] = t0;
-                r[1] = t1;
-            }
-        }
-        __syncthreads();
-        for (int c = tid; c < BN; c += 256) {
-            double u0 = 0.0, u1 = 0.0;
-#pragma unroll
-            for (int w = 0; w < WM; ++w) {
-                u0 += lds[((int64_t)w * BN + c) * 2];
-                u1 += lds[((int64_t)w * BN + c) * 2 + 1];
-            }
-            const int n = n0 + c;
-            if (n < a.N) {
-                a.bn_part[((int64_t)tile_x * 2) * a.N + n] = u0;
-                a.bn_part[((int64_t)tile_x * 2 + 1) * a.N + n] = u1;
-            }
-        }
-    }
-};
-template <bool GB, bool OB16>
-struct EpiBnBwdApply : EpiBnPrefetch<GB> {
-    static constexpr bool STATS = false;
-    static constexpr bool BF16 = false;
-    static constexpr bool ADD = false;
-    static constexpr bool STRUCTURED = true;
-    static constexpr bool PREFETCH = true;
-    __device__ void operator()(const GemmArgs&, int, int, float, int) const {}
-    __device__ void block_p(const GemmArgs& a, int mbase, int n, const floatx16& acc, int b, int j) const {
-        if (n >= a.N) return;
-        const EpiRows e(mbase);
-        const float k0 = a.bn_coef[n], k1 = a.bn_coef[a.N + n], k2 = a.bn_coef[2 * a.N + n];
-        float o[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float y = acc[r];
-            const float z = __fmaf_rn(y, this->sc[j], this->sh[j]);
-            const float dz = z > 0.f ? this->g[b][r] : 0.f;
-            const float xh = (y - this->mu[j]) * this->is[j];
-            o[r] = __fsub_rn(__fmaf_rn(k0, dz, -k1), __fmul_rn(k2, xh));
-        }
-        epi_store16<OB16>(a, e, n, o);
-    }
-};
-
 struct EpiSlab {   // split-K partial: slab z holds C[m][n] of K-slice z
     static constexpr bool STATS = false;
     static constexpr bool BF16 = false;

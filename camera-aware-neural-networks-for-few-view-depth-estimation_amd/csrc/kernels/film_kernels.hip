@@ -221,7 +221,7 @@ __global__ __launch_bounds__(256) void k_film_apply(const float* __restrict__ y,
 void film_apply(const float* y, int C, const float* scale, const float* shift, const float* gam, const float* bet,
                 int B, int64_t HW, float* out, hipStream_t st, bool y_bf16, void* os) {
     const int64_t M = (int64_t)B * HW;
-    if (M >= ((int64_t)1 << 32) || HW < 2) throw std::runtime_error("film_apply: layout");
+    if (M >= ((int64_t)1 << 32) || HW < 1) throw std::runtime_error("film_apply: layout");
     const FastDiv dHW = make_fastdiv((uint32_t)HW);
     const int C4 = C >> 2, CX = std::min(C4, 64), RY = std::max(1, 256 / CX);
     const int S = (int)std::max<int64_t>(1, std::min<int64_t>(65535, cdiv(M, (int64_t)RY * 16)));

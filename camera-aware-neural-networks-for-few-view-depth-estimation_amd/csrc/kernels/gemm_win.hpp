@@ -567,8 +567,8 @@ __device__ __forceinline__ void conv3x3_win_ps_body(const GemmArgs& a) {
         for (int i = 0; i < 2 * MI; ++i)
 #pragma unroll
             for (int j = 0; j < 2 * NJ; ++j) acc4[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    } else {
-        acc_zero(acc);
+    } else if (S == 0) {
+        acc_zero(acc);   // (never on the host's shapes: cin >= 32; the main loop's first step writes acc)
     }
     uint4 ra[G::NVA], rb[3 * G::JB];
     int cb = 0, ky = 0;
@@ -600,7 +600,8 @@ __device__ __forceinline__ void conv3x3_win_ps_body(const GemmArgs& a) {
             for (int jj = 0; jj < G::JB; ++jj)
                 if (bact(jj)) *reinterpret_cast<uint4*>(lds + G::SA + t * G::SBT + blds0 + 64 * jj * G::LDK) = rb[t * G::JB + jj];
     };
-    auto compute = [&]() {
+    auto compute = [&](auto first_stage) {
+        constexpr bool FIRST = decltype(first_stage)::value;
         if constexpr (M16) {
 #pragma unroll
             for (int kx = 0; kx < 3; ++kx) {
@@ -636,7 +637,8 @@ __device__ __forceinline__ void conv3x3_win_ps_body(const GemmArgs& a) {
             for (int t = 0; t < 6; ++t) {
                 if (t + 1 < 6) rd(t + 1, (t + 1) & 1);
                 __builtin_amdgcn_sched_barrier(0);
-                s3_mfma<1>(acc, fa[t & 1], fb[t & 1]);
+                if (FIRST && t == 0) b1_mfma_first(acc, fa[0], fb[0]);
+                else s3_mfma<1>(acc, fa[t & 1], fb[t & 1]);
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -650,7 +652,8 @@ __device__ __forceinline__ void conv3x3_win_ps_body(const GemmArgs& a) {
     for (int s = 0; s < S; ++s) {
         const bool more = s + 1 < S;
         if (more) load();
-        compute();
+        if (M16 || s > 0) compute(std::false_type{});
+        else compute(std::true_type{});
         __syncthreads();
         if (more) {
             store();

@@ -6,12 +6,42 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <initializer_list>
+
 namespace cad {
 
 // ---------------- launch profiler (host/profiler.cpp) ----------------
 bool prof_enabled();
 void prof_push(const char* name, double flops, hipStream_t st);
 void prof_pop(hipStream_t st);
+
+// ---------------- launch-level aliasing guard (host/alias.cpp) ----------------
+// CAD_ALIAS_CHECK=1 (tests/conftest.py sets it): an instrumented launcher refuses a launch whose output
+// byte range overlaps one of its inputs (std::invalid_argument naming both -> CAD_ERR_INVALID) unless
+// the launcher declares that operand pair in place (it then leaves the pair out);
+// CAD_ALIAS_CHECK=log:<path> only records the finding.  Off by default: CAD_NO_ALIAS tests one cached
+// int and evaluates none of its arguments.
+struct AliasView {
+    const void* p = nullptr;
+    int64_t rows = 0, ld = 0, coff = 0, cols = 0;   // rows of ld elements, columns [coff, coff + cols)
+    int es = 4;                                     // element bytes
+    const char* what = "";
+};
+inline AliasView aview(const void* p, int64_t rows, int64_t ld, int64_t coff, int64_t cols, int es, const char* what) {
+    AliasView v;
+    v.p = p; v.rows = rows; v.ld = ld; v.coff = coff; v.cols = cols; v.es = es; v.what = what;
+    return v;
+}
+int alias_mode();
+bool views_overlap(const AliasView& a, const AliasView& b);
+void alias_check_impl(const char* op, std::initializer_list<AliasView> outs, std::initializer_list<AliasView> ins,
+                      bool same_view_ok = false);
+// CAD_NO_ALIAS("op", {outputs...}, {inputs...} [, same_view_ok])  (variadic: the braced lists hold commas;
+// same_view_ok: an elementwise pass whose output may be exactly one of its inputs)
+#define CAD_NO_ALIAS(...)                                                     \
+    do {                                                                      \
+        if (::cad::alias_mode()) ::cad::alias_check_impl(__VA_ARGS__);        \
+    } while (0)
 
 // ---------------- convolutions (conv_kernels.hip) ----------------
 // GEMM engine of the conv / ConvT contractions: 0 = exact fp32 MFMA (v_mfma_f32_32x32x2_f32),
@@ -65,27 +95,6 @@ bool conv3x3_dgrad_ps(Split dz, int cout, Split wd, int cin, float* dx, int64_t 
 bool conv3x3_dgrad_split_ok(Split dz, int cout, Split wd, int cin, int W, int split_n);
 void conv3x3_wgrad_ps(Split dz, int cout, Split x, int cin, float* dw, int B, int H, int W, float* slab,
                       int64_t slab_cap, hipStream_t st);
-// ---- recomputed convolution (enc1.conv1, epilogues.hpp "Recomputed convolution"): the im2col
-// conv3x3 forward GEMM that conv3x3_fwd (S3 / f32 engines: x, w fp32) or conv3x3_fwd_ps (B1: x, w
-// twins) would run for this shape — same kernel, tile and K order, so the same accumulators — with a
-// consumer's epilogue instead of the output store.
-enum class Recompute { Stats, BnRelu, BwdSums, BwdApply, Store };   // Store: y itself (fp32 rows out)
-struct RecomputeArgs {
-    Recompute mode = Recompute::Stats;
-    float* stats = nullptr;                                    // Stats: BN tile partials (conv3x3_stats_rows)
-    const float *scale = nullptr, *shift = nullptr, *mean = nullptr, *invstd = nullptr, *coef = nullptr;
-    const void* g = nullptr; int64_t ldg = 0; bool g_bf16 = false;   // BwdSums / BwdApply: upstream gradient
-    void* out = nullptr; int64_t ldo = 0; bool out_bf16 = false;     // BnRelu / BwdApply output rows
-    double* part = nullptr;                                    // BwdSums: [recompute_tiles][2][cout]
-};
-int recompute_tiles(int cin, int B, int H, int W, int cout);   // row tiles of the recomputed GEMM
-void conv3x3_recompute(const void* x, int64_t ldx, int cin, const void* w, int cout, int B, int H, int W,
-                       const RecomputeArgs& r, hipStream_t st);
-// BN backward coefficients from the per-tile partials of EpiBnBwdSums (k_bn_bwd_coef's outputs:
-// coef [3][C], dgamma, dbeta); scratch: colsum scratch of the tile count
-void bn_bwd_from_tiles(const double* part, int tiles, int C, int64_t M, const float* gamma, const float* invstd,
-                       float* coef, float* dgamma, float* dbeta, double* scratch, hipStream_t st);
-
 // y_bf16: y is a bf16 twin (rows of ldy elements) — the up half of the decoder concat twin
 void convT_fwd_ps(Split x, int cin, Split wf, const float* bias, int cout, float* y, int64_t ldy, int ycoff, int B,
                   int H, int W, hipStream_t st, bool y_bf16 = false);
@@ -203,19 +212,22 @@ struct HeadGrad {
 // t = mulhi(m, n); exact for every 32-bit n)
 struct FastDiv {
     uint32_t m = 0;
-    int s = 0;
+    int s1 = 0, s2 = 0;
 };
+// n / d = (t + ((n - t) >> s1)) >> s2 with t = mulhi(m, n), l = ceil(log2 d): s1 = 1, s2 = l - 1 for
+// d >= 2; d = 1 gives m = 1, t = 0 and s1 = s2 = 0 (a 1x1 image: sample = row)
 inline FastDiv make_fastdiv(uint32_t d) {
     int l = 0;
     while ((1ull << l) < d) ++l;   // ceil(log2 d)
     FastDiv f;
     f.m = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
-    f.s = l - 1;
+    f.s1 = l > 0 ? 1 : 0;
+    f.s2 = l > 0 ? l - 1 : 0;
     return f;
 }
 __device__ __forceinline__ uint32_t fdiv(const FastDiv& f, uint32_t n) {
     const uint32_t t = __umulhi(f.m, n);
-    return (t + ((n - t) >> 1)) >> f.s;
+    return (t + ((n - t) >> f.s1)) >> f.s2;
 }
 struct PoolAdd {
     const float* d = nullptr;

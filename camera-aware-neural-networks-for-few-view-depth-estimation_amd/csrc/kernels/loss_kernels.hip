@@ -1,7 +1,12 @@
 // Fused depth-loss forward + analytic backward.
 // Replaces CombinedDepthLoss::forwardWithIntrinsics (src/loss/depth_loss.h:416-433) and its autograd
-// backward with 7 small kernels: wavefront/LDS reductions into fixed-order fp64 partials (no
-// atomics, bitwise-reproducible), one pooled pyramid, one elementwise dL/dpred pass.
+// backward with two fused passes over the depth map and two single-block reductions: pass A (SI /
+// reprojection sums, per-sample sum(pred), the scale-0 logs and the smoothness edge weights), the
+// pooled pyramid (one launch for scales 1-3), reduction 1, pass B (smoothness sums and S_b, the
+// gradient-matching sums of every scale, dL/dpred), reduction 2 (the five losses), and, when the
+// smoothness weight is non-zero, the per-sample S_b coupling subtracted from dL/dpred.  Partials are
+// fp64 in a fixed order (no atomics, bitwise-reproducible); index math is 32-bit (multiply-shift
+// division: B*H*W < 2^31, checked).
 //
 // Semantics reproduced (file:line in /root/reference/src/loss/depth_loss.h):
 //   SI      :33-64   mask gt>eps (global over batch) or the caller's valid_mask; d = log(clamp p) - log(clamp g);
@@ -56,128 +61,103 @@ struct Geo {
     int Hs[kScales], Ws[kScales];
     int64_t off[kScales];   // pyramid offsets (scale s >= 1) in floats, per array
     int64_t pyr_n;          // floats per pyramid array
+    int cells;              // pooled cells of one sample over scales 1..3
+    FastDiv dW;             // / W
+    FastDiv dWs[kScales];   // / Ws[s]
+    FastDiv dHs[kScales];   // / Hs[s]
 };
 
 // scalar slots (double) in dsc
 enum { S_N = 0, S_SD, S_SD2, S_SE, S_GX0, S_GY0 = S_GX0 + kScales, S_SMX = S_GY0 + kScales, S_SMY,
        S_PB /* B per-sample sum(pred) */ };
 // per-sample tail after S_PB: [B] sum pred, [B] S_b (sum gn*p)
+constexpr int kPA = 5;                  // pass-A partials per block: n, sum d, sum d^2, sum e, sum pred
+constexpr int kPB = 3 + 2 * kScales;    // pass-B partials: smooth x, smooth y, S_b, |dx| / |dy| per scale
 
-// pass A: SI + reproj sums (global) and per-sample sum(pred)
-__global__ __launch_bounds__(kTPB) void k_passA(const float* __restrict__ pred, const float* __restrict__ gt,
-                                                const float* __restrict__ K, const uint8_t* __restrict__ mask, Geo g,
+__device__ __forceinline__ float edge_w(const float* img, int64_t HW, int64_t i, int64_t step) {   // between i, i+step
+    const float d0 = fabsf(img[i + step] - img[i]);
+    const float d1 = fabsf(img[HW + i + step] - img[HW + i]);
+    const float d2 = fabsf(img[2 * HW + i + step] - img[2 * HW + i]);
+    return expf(-((d0 + d1 + d2) / 3.f));
+}
+
+// Pass A, per (sample, chunk): SI + reprojection sums over the mask, per-sample sum(pred); and, per
+// pixel, the scale-0 logs log(clamp p), log(clamp g) and the smoothness edge weights of its right and
+// lower edges (0 past the border) — each computed once here and read by pass B's stencils (the
+// previous kernels evaluated every log up to 10x and every edge weight up to 10x per pixel)
+__global__ __launch_bounds__(kTPB) void k_lossA(const float* __restrict__ pred, const float* __restrict__ gt,
+                                                const float* __restrict__ rgb, const float* __restrict__ K,
+                                                const uint8_t* __restrict__ mask, Geo g, float* __restrict__ lp0,
+                                                float* __restrict__ lg0, float* __restrict__ wx, float* __restrict__ wy,
                                                 double* partA, int nb) {
-    __shared__ double red[4 * 5];
+    __shared__ double red[4 * kPA];
     const int b = blockIdx.y;
-    const int64_t HW = (int64_t)g.H * g.W;
+    const int HW = g.H * g.W;
     const float* kk = K + b * 9;
     const float fx = kk[0], cx = kk[2], fy = kk[4], cy = kk[5];
-    double v[5] = {0, 0, 0, 0, 0};
-    for (int64_t i = (int64_t)blockIdx.x * kTPB + threadIdx.x; i < HW; i += (int64_t)nb * kTPB) {
-        const float p = pred[b * HW + i], t = gt[b * HW + i];
+    const float* img = rgb + (int64_t)b * 3 * HW;
+    const int64_t o = (int64_t)b * HW;
+    double v[kPA] = {0, 0, 0, 0, 0};
+    for (int i = blockIdx.x * kTPB + threadIdx.x; i < HW; i += nb * kTPB) {
+        const float p = pred[o + i], t = gt[o + i];
+        const int y = (int)fdiv(g.dW, (uint32_t)i), x = i - y * g.W;
+        const float lp = logf(clampf(p)), lg = logf(clampf(t));
+        lp0[o + i] = lp;
+        lg0[o + i] = lg;
+        wx[o + i] = x + 1 < g.W ? edge_w(img, HW, i, 1) : 0.f;
+        wy[o + i] = y + 1 < g.H ? edge_w(img, HW, i, g.W) : 0.f;
         v[4] += p;
-        if (mask ? mask[b * HW + i] != 0 : t > kEps) {
-            const float d = logf(clampf(p)) - logf(clampf(t));
+        if (mask ? mask[o + i] != 0 : t > kEps) {
+            const float d = lp - lg;
             v[0] += 1.0;
             v[1] += d;
             v[2] += (double)d * d;
-            const int u = (int)(i % g.W), vv = (int)(i / g.W);
-            const float gu = (float)u - cx, gv = (float)vv - cy;
+            const float gu = (float)x - cx, gv = (float)y - cy;
             const float dX = (gu * p) / (fx + kEps) - (gu * t) / (fx + kEps);
             const float dY = (gv * p) / (fy + kEps) - (gv * t) / (fy + kEps);
             const float dZ = p - t;
             v[3] += sqrtf(dX * dX + dY * dY + dZ * dZ + kEps);
         }
     }
-    block_sum<5>(v, red);
+    block_sum<kPA>(v, red);
     if (threadIdx.x == 0)
-        for (int i = 0; i < 5; ++i) partA[((int64_t)b * nb + blockIdx.x) * 5 + i] = v[i];
+        for (int q = 0; q < kPA; ++q) partA[((int64_t)b * nb + blockIdx.x) * kPA + q] = v[q];
 }
 
-// pyramid scale s (1..3): avg_pool2d(k) of pred and gt; stores avgP, logP, logG
-__global__ void k_pyramid(const float* __restrict__ pred, const float* __restrict__ gt, Geo g, int s,
+// pyramid, scales 1..3 in one launch: avg_pool2d(k = 2^s) of pred and gt -> avgP, logP, logG
+__global__ void k_lossPyr(const float* __restrict__ pred, const float* __restrict__ gt, Geo g, int total,
                           float* __restrict__ avgP, float* __restrict__ logP, float* __restrict__ logG) {
-    const int k = 1 << s, Hs = g.Hs[s], Ws = g.Ws[s];
-    const int64_t n = (int64_t)g.B * Hs * Ws;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int j = (int)(i % Ws);
-        const int64_t t = i / Ws;
-        const int r = (int)(t % Hs), b = (int)(t / Hs);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        int s = 1, li = i;
+        while (s < kScales - 1 && li >= g.B * g.Hs[s] * g.Ws[s]) { li -= g.B * g.Hs[s] * g.Ws[s]; ++s; }
+        const int k = 1 << s, Hs = g.Hs[s], Ws = g.Ws[s];
+        const int t = (int)fdiv(g.dWs[s], (uint32_t)li), j = li - t * Ws;
+        const int b = (int)fdiv(g.dHs[s], (uint32_t)t), r = t - b * Hs;
         const int64_t base = ((int64_t)b * g.H + r * k) * g.W + j * k;
         float sp = 0.f, sg = 0.f;
-        for (int y = 0; y < k; ++y)
-            for (int x = 0; x < k; ++x) {
-                sp += pred[base + (int64_t)y * g.W + x];
-                sg += gt[base + (int64_t)y * g.W + x];
+        for (int yy = 0; yy < k; ++yy)
+            for (int xx = 0; xx < k; ++xx) {
+                sp += pred[base + (int64_t)yy * g.W + xx];
+                sg += gt[base + (int64_t)yy * g.W + xx];
             }
         const float ap = sp / (float)(k * k), ag = sg / (float)(k * k);
-        avgP[g.off[s] + i] = ap;
-        logP[g.off[s] + i] = logf(clampf(ap));
-        logG[g.off[s] + i] = logf(clampf(ag));
+        avgP[g.off[s] + li] = ap;
+        logP[g.off[s] + li] = logf(clampf(ap));
+        logG[g.off[s] + li] = logf(clampf(ag));
     }
 }
 
-__device__ __forceinline__ float lp_at(const float* pred, const float* logP, const Geo& g, int s, int64_t i) {
-    return s == 0 ? logf(clampf(pred[i])) : logP[g.off[s] + i];
-}
-
-// gradient-matching sums for all scales: |dx| and |dy| per scale
-__global__ __launch_bounds__(kTPB) void k_gradsum(const float* __restrict__ pred, const float* __restrict__ gt,
-                                                  const float* __restrict__ logP, const float* __restrict__ logG,
-                                                  Geo g, double* partG, int64_t total) {
-    __shared__ double red[4 * 2 * kScales];
-    double v[2 * kScales];
-#pragma unroll
-    for (int i = 0; i < 2 * kScales; ++i) v[i] = 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * kTPB + threadIdx.x; i < total; i += (int64_t)gridDim.x * kTPB) {
-        int s = 0;
-        int64_t li = i;
-        while (s < kScales - 1 && li >= (int64_t)g.B * g.Hs[s] * g.Ws[s]) { li -= (int64_t)g.B * g.Hs[s] * g.Ws[s]; ++s; }
-        const int Hs = g.Hs[s], Ws = g.Ws[s];
-        const int j = (int)(li % Ws), r = (int)((li / Ws) % Hs);
-        const float p0 = lp_at(pred, logP, g, s, li);
-        const float g0 = s == 0 ? logf(clampf(gt[li])) : logG[g.off[s] + li];
-        float ax = 0.f, ay = 0.f;
-        if (j + 1 < Ws) {
-            const float p1 = lp_at(pred, logP, g, s, li + 1);
-            const float g1 = s == 0 ? logf(clampf(gt[li + 1])) : logG[g.off[s] + li + 1];
-            ax = fabsf((p1 - p0) - (g1 - g0));
-        }
-        if (r + 1 < Hs) {
-            const float p1 = lp_at(pred, logP, g, s, li + Ws);
-            const float g1 = s == 0 ? logf(clampf(gt[li + Ws])) : logG[g.off[s] + li + Ws];
-            ay = fabsf((p1 - p0) - (g1 - g0));
-        }
-#pragma unroll
-        for (int q = 0; q < kScales; ++q)
-            if (q == s) { v[2 * q] += ax; v[2 * q + 1] += ay; }
-    }
-    block_sum<2 * kScales>(v, red);
-    if (threadIdx.x == 0)
-        for (int q = 0; q < 2 * kScales; ++q) partG[(int64_t)blockIdx.x * 2 * kScales + q] = v[q];
-}
-
-// single block: reduce pass-A and gradsum partials into dsc
-__global__ __launch_bounds__(kTPB) void k_reduce1(const double* partA, int nb, const double* partG, int ng,
-                                                  Geo g, double* dsc) {
-    __shared__ double red[4 * 8];
-    double v[4];
-    for (int q = 0; q < 4; ++q) v[q] = 0.0;
+// single block: pass-A partials -> dsc (SI / reprojection sums, per-sample sum(pred))
+__global__ __launch_bounds__(kTPB) void k_lossR1(const double* partA, int nb, Geo g, double* dsc) {
+    __shared__ double red[4 * 4];
+    double v[4] = {0.0, 0.0, 0.0, 0.0};
     for (int i = threadIdx.x; i < g.B * nb; i += kTPB)
-        for (int q = 0; q < 4; ++q) v[q] += partA[(int64_t)i * 5 + q];
+        for (int q = 0; q < 4; ++q) v[q] += partA[(int64_t)i * kPA + q];
     block_sum<4>(v, red);
     if (threadIdx.x == 0) { dsc[S_N] = v[0]; dsc[S_SD] = v[1]; dsc[S_SD2] = v[2]; dsc[S_SE] = v[3]; }
-    double w[2 * kScales];
-    for (int q = 0; q < 2 * kScales; ++q) w[q] = 0.0;
-    for (int i = threadIdx.x; i < ng; i += kTPB)
-        for (int q = 0; q < 2 * kScales; ++q) w[q] += partG[(int64_t)i * 2 * kScales + q];
-    block_sum<2 * kScales>(w, red);
-    if (threadIdx.x == 0)
-        for (int q = 0; q < kScales; ++q) { dsc[S_GX0 + q] = w[2 * q]; dsc[S_GY0 + q] = w[2 * q + 1]; }
-    // per-sample sum(pred)
     for (int b = 0; b < g.B; ++b) {
         double u[1] = {0.0};
-        for (int i = threadIdx.x; i < nb; i += kTPB) u[0] += partA[((int64_t)b * nb + i) * 5 + 4];
+        for (int i = threadIdx.x; i < nb; i += kTPB) u[0] += partA[((int64_t)b * nb + i) * kPA + 4];
         block_sum<1>(u, red);
         if (threadIdx.x == 0) dsc[S_PB + b] = u[0];
     }
@@ -187,68 +167,164 @@ struct SmoothCtx {
     float inv_nx, inv_ny;
 };
 
-__device__ __forceinline__ float edge_wx(const float* img, int64_t HW, int64_t i) {   // between i, i+1
-    const float d0 = fabsf(img[i + 1] - img[i]);
-    const float d1 = fabsf(img[HW + i + 1] - img[HW + i]);
-    const float d2 = fabsf(img[2 * HW + i + 1] - img[2 * HW + i]);
-    return expf(-((d0 + d1 + d2) / 3.f));
-}
-__device__ __forceinline__ float edge_wy(const float* img, int64_t HW, int64_t i, int W) {   // i, i+W
-    const float d0 = fabsf(img[i + W] - img[i]);
-    const float d1 = fabsf(img[HW + i + W] - img[HW + i]);
-    const float d2 = fabsf(img[2 * HW + i + W] - img[2 * HW + i]);
-    return expf(-((d0 + d1 + d2) / 3.f));
-}
-
-// dL_smooth/dn at pixel i of sample plane (pp = pred plane, img = rgb of the sample).  n = p / denom
-// by true division, as the reference computes it (depth_loss.h:193): the sign of a difference of
-// neighbouring n must come out as the reference's, and a rounded reciprocal can merge neighbours
-// that differ by an ulp (sign 0 instead of +-1).
-__device__ __forceinline__ float smooth_gn(const float* pp, const float* img, int64_t HW, int W, int H,
-                                           int x, int y, int64_t i, float denom, const SmoothCtx& c) {
+// dL_smooth/dn at pixel i of the sample plane (pp = pred plane, wx / wy its edge weights).  n = p /
+// denom by true division, as the reference computes it (depth_loss.h:193): the sign of a difference of
+// neighbouring n must come out as the reference's, and a rounded reciprocal can merge neighbours that
+// differ by an ulp (sign 0 instead of +-1).
+__device__ __forceinline__ float smooth_gn(const float* pp, const float* wxp, const float* wyp, int W, int H, int x,
+                                           int y, int i, float denom, const SmoothCtx& c) {
     const float n0 = pp[i] / denom;
     float gx = 0.f, gy = 0.f;
-    if (x > 0) gx += sgnf(n0 - pp[i - 1] / denom) * edge_wx(img, HW, i - 1);
-    if (x + 1 < W) gx -= sgnf(pp[i + 1] / denom - n0) * edge_wx(img, HW, i);
-    if (y > 0) gy += sgnf(n0 - pp[i - W] / denom) * edge_wy(img, HW, i - W, W);
-    if (y + 1 < H) gy -= sgnf(pp[i + W] / denom - n0) * edge_wy(img, HW, i, W);
+    if (x > 0) gx += sgnf(n0 - pp[i - 1] / denom) * wxp[i - 1];
+    if (x + 1 < W) gx -= sgnf(pp[i + 1] / denom - n0) * wxp[i];
+    if (y > 0) gy += sgnf(n0 - pp[i - W] / denom) * wyp[i - W];
+    if (y + 1 < H) gy -= sgnf(pp[i + W] / denom - n0) * wyp[i];
     return gx * c.inv_nx + gy * c.inv_ny;
 }
 
-// smoothness forward sums (global) and per-sample coupling S_b = sum gn * p
-__global__ __launch_bounds__(kTPB) void k_smooth(const float* __restrict__ pred, const float* __restrict__ rgb,
-                                                 Geo g, const double* dsc, double* partS, int nb, SmoothCtx c) {
-    __shared__ double red[4 * 3];
-    const int b = blockIdx.y;
-    const int64_t HW = (int64_t)g.H * g.W;
-    const float* pp = pred + b * HW;
-    const float* img = rgb + (int64_t)b * 3 * HW;
-    const float mean = (float)(dsc[S_PB + b] / (double)HW);
-    const float denom = mean + kEps;
-    double v[3] = {0, 0, 0};
-    for (int64_t i = (int64_t)blockIdx.x * kTPB + threadIdx.x; i < HW; i += (int64_t)nb * kTPB) {
-        const int x = (int)(i % g.W), y = (int)(i / g.W);
-        const float n0 = pp[i] / denom;
-        if (x + 1 < g.W) v[0] += fabsf(pp[i + 1] / denom - n0) * edge_wx(img, HW, i);
-        if (y + 1 < g.H) v[1] += fabsf(pp[i + g.W] / denom - n0) * edge_wy(img, HW, i, g.W);
-        v[2] += (double)smooth_gn(pp, img, HW, g.W, g.H, x, y, i, denom, c) * pp[i];
-    }
-    block_sum<3>(v, red);
-    if (threadIdx.x == 0)
-        for (int q = 0; q < 3; ++q) partS[((int64_t)b * nb + blockIdx.x) * 3 + q] = v[q];
+// dL/dP_s at pooled pixel li of scale s >= 1 (sign terms of both neighbours), before the 1/4^s factor
+__device__ float dgrad_pyr(const float* logP, const float* logG, const Geo& g, int s, int64_t li, int r, int j) {
+    const int Hs = g.Hs[s], Ws = g.Ws[s];
+    const float* P = logP + g.off[s];
+    const float* G = logG + g.off[s];
+    const float p0 = P[li], g0 = G[li];
+    float ax = 0.f, ay = 0.f;
+    if (j > 0) ax += sgnf((p0 - P[li - 1]) - (g0 - G[li - 1]));
+    if (j + 1 < Ws) ax -= sgnf((P[li + 1] - p0) - (G[li + 1] - g0));
+    if (r > 0) ay += sgnf((p0 - P[li - Ws]) - (g0 - G[li - Ws]));
+    if (r + 1 < Hs) ay -= sgnf((P[li + Ws] - p0) - (G[li + Ws] - g0));
+    const float nx = (float)g.B * Hs * (Ws - 1), ny = (float)g.B * (Hs - 1) * Ws;
+    return ax / nx + ay / ny;
 }
 
-// single block: smooth sums, S_b, final scalar losses
-__global__ __launch_bounds__(kTPB) void k_reduce2(const double* partS, int nb, Geo g, double* dsc, float w0,
-                                                  float w1, float w2, float w3, float* out5) {
-    __shared__ double red[4 * 2];
-    double v[2] = {0.0, 0.0};
-    for (int i = threadIdx.x; i < g.B * nb; i += kTPB) { v[0] += partS[(int64_t)i * 3]; v[1] += partS[(int64_t)i * 3 + 1]; }
-    block_sum<2>(v, red);
-    if (threadIdx.x == 0) { dsc[S_SMX] = v[0]; dsc[S_SMY] = v[1]; }
+// Pass B, per (sample, chunk), after pass A's sums: the smoothness sums and S_b = sum gn p, the
+// gradient-matching |dx| / |dy| sums of every scale, and dL/dpred of every term but the smoothness
+// term's per-sample coupling -w2 S_b / (denom^2 HW), which k_lossC subtracts once S_b is reduced.
+__global__ __launch_bounds__(kTPB) void k_lossB(const float* __restrict__ pred, const float* __restrict__ gt,
+                                                const float* __restrict__ K, const uint8_t* __restrict__ mask,
+                                                const float* __restrict__ lp0, const float* __restrict__ lg0,
+                                                const float* __restrict__ wx, const float* __restrict__ wy,
+                                                const float* __restrict__ avgP, const float* __restrict__ logP,
+                                                const float* __restrict__ logG, Geo g, const double* dsc, float w0,
+                                                float w1, float w2, float w3, SmoothCtx c, float* __restrict__ dpred,
+                                                double* partB, int nb) {
+    __shared__ double red[4 * kPB];
+    const int b = blockIdx.y;
+    const int HW = g.H * g.W, W = g.W;
+    const int64_t o = (int64_t)b * HW;
+    const float* pp = pred + o;
+    const float* lp = lp0 + o;
+    const float* lg = lg0 + o;
+    const float* wxp = wx + o;
+    const float* wyp = wy + o;
+    const float mean = (float)(dsc[S_PB + b] / (double)HW);
+    const float denom = mean + kEps;
+    const double cnt = dsc[S_N];
+    const float inv_n = cnt > 0 ? (float)(1.0 / cnt) : 0.f;
+    const float sd_term = cnt > 0 ? (float)(2.0 * kLam * dsc[S_SD] / (cnt * cnt)) : 0.f;
+    const float* kk = K + b * 9;
+    const float fx = kk[0], cx = kk[2], fy = kk[4], cy = kk[5];
+    const float nx0 = (float)g.B * g.H * (W - 1), ny0 = (float)g.B * (g.H - 1) * W;
+    double v[kPB];
+#pragma unroll
+    for (int q = 0; q < kPB; ++q) v[q] = 0.0;
+    for (int i = blockIdx.x * kTPB + threadIdx.x; i < HW; i += nb * kTPB) {
+        const int y = (int)fdiv(g.dW, (uint32_t)i), x = i - y * W;
+        const float p = pp[i], t = gt[o + i];
+        // smoothness: forward sums and gn
+        const float n0 = p / denom;
+        if (x + 1 < W) v[0] += fabsf(pp[i + 1] / denom - n0) * wxp[i];
+        if (y + 1 < g.H) v[1] += fabsf(pp[i + W] / denom - n0) * wyp[i];
+        const float gn = smooth_gn(pp, wxp, wyp, W, g.H, x, y, i, denom, c);
+        v[2] += (double)gn * p;
+        // gradient matching at scale 0: sums and the sign terms of both neighbours
+        const float p0 = lp[i], g0 = lg[i];
+        float ax = 0.f, ay = 0.f;
+        if (x > 0) ax += sgnf((p0 - lp[i - 1]) - (g0 - lg[i - 1]));
+        if (x + 1 < W) {
+            const float dx = (lp[i + 1] - p0) - (lg[i + 1] - g0);
+            v[3] += fabsf(dx);
+            ax -= sgnf(dx);
+        }
+        if (y > 0) ay += sgnf((p0 - lp[i - W]) - (g0 - lg[i - W]));
+        if (y + 1 < g.H) {
+            const float dy = (lp[i + W] - p0) - (lg[i + W] - g0);
+            v[4] += fabsf(dy);
+            ay -= sgnf(dy);
+        }
+        // dL/dpred
+        float grad = 0.f;
+        if ((mask ? mask[o + i] != 0 : t > kEps) && cnt > 0) {
+            // SI
+            const float d = p0 - g0;
+            const float dd = 2.f * d * inv_n - sd_term;
+            grad += w0 * (dd / clampf(p)) * clampgrad(p);
+            // reprojection
+            const float gu = (float)x - cx, gv = (float)y - cy;
+            const float a = gu / (fx + kEps), bb = gv / (fy + kEps);
+            const float dX = (gu * p) / (fx + kEps) - (gu * t) / (fx + kEps);
+            const float dY = (gv * p) / (fy + kEps) - (gv * t) / (fy + kEps);
+            const float dZ = p - t;
+            const float e = sqrtf(dX * dX + dY * dY + dZ * dZ + kEps);
+            grad += w3 * inv_n * (dX * a + dY * bb + dZ) / e;
+        }
+        float gg = (ax / nx0 + ay / ny0) * clampgrad(p) / clampf(p);
+        for (int s = 1; s < kScales; ++s) {
+            const int r = y >> s, j = x >> s;
+            if (r >= g.Hs[s] || j >= g.Ws[s]) continue;
+            const int64_t li = ((int64_t)b * g.Hs[s] + r) * g.Ws[s] + j;
+            const float ap = avgP[g.off[s] + li];
+            const float dP = dgrad_pyr(logP, logG, g, s, li, r, j);
+            gg += (dP * clampgrad(ap) / clampf(ap)) / (float)(1 << (2 * s));
+        }
+        grad += w1 * gg / (float)kScales;
+        dpred[o + i] = grad + w2 * (gn / denom);
+    }
+    // gradient-matching sums at scales 1..3 over this sample's pooled cells
+    for (int ci = blockIdx.x * kTPB + threadIdx.x; ci < g.cells; ci += nb * kTPB) {
+        int s = 1, li = ci;
+        while (s < kScales - 1 && li >= g.Hs[s] * g.Ws[s]) { li -= g.Hs[s] * g.Ws[s]; ++s; }
+        const int Ws = g.Ws[s];
+        const int r = (int)fdiv(g.dWs[s], (uint32_t)li), j = li - r * Ws;
+        const int64_t q = (int64_t)b * g.Hs[s] * Ws + li;
+        const float* P = logP + g.off[s];
+        const float* G = logG + g.off[s];
+        const float p0 = P[q], g0 = G[q];
+        float ax = 0.f, ay = 0.f;
+        if (j + 1 < Ws) ax = fabsf((P[q + 1] - p0) - (G[q + 1] - g0));
+        if (r + 1 < g.Hs[s]) ay = fabsf((P[q + Ws] - p0) - (G[q + Ws] - g0));
+#pragma unroll
+        for (int u = 1; u < kScales; ++u)
+            if (u == s) { v[3 + 2 * u] += ax; v[4 + 2 * u] += ay; }
+    }
+    block_sum<kPB>(v, red);
+    if (threadIdx.x == 0)
+        for (int q = 0; q < kPB; ++q) partB[((int64_t)b * nb + blockIdx.x) * kPB + q] = v[q];
+}
+
+// single block: pass-B partials -> smoothness sums, S_b, gradient-matching sums, the five losses
+__global__ __launch_bounds__(kTPB) void k_lossR2(const double* partB, int nb, Geo g, double* dsc, float w0, float w1,
+                                                 float w2, float w3, float* out5) {
+    __shared__ double red[4 * (2 + 2 * kScales)];
+    double v[2 + 2 * kScales];
+#pragma unroll
+    for (int q = 0; q < 2 + 2 * kScales; ++q) v[q] = 0.0;
+    for (int i = threadIdx.x; i < g.B * nb; i += kTPB) {
+        const double* pr = partB + (int64_t)i * kPB;
+        v[0] += pr[0];
+        v[1] += pr[1];
+#pragma unroll
+        for (int q = 0; q < 2 * kScales; ++q) v[2 + q] += pr[3 + q];
+    }
+    block_sum<2 + 2 * kScales>(v, red);
+    if (threadIdx.x == 0) {
+        dsc[S_SMX] = v[0];
+        dsc[S_SMY] = v[1];
+        for (int s = 0; s < kScales; ++s) { dsc[S_GX0 + s] = v[2 + 2 * s]; dsc[S_GY0 + s] = v[3 + 2 * s]; }
+    }
     for (int b = 0; b < g.B; ++b) {
         double u[1] = {0.0};
-        for (int i = threadIdx.x; i < nb; i += kTPB) u[0] += partS[((int64_t)b * nb + i) * 3 + 2];
+        for (int i = threadIdx.x; i < nb; i += kTPB) u[0] += partB[((int64_t)b * nb + i) * kPB + 2];
         block_sum<1>(u, red);
         if (threadIdx.x == 0) dsc[S_PB + g.B + b] = u[0];
     }
@@ -270,79 +346,16 @@ __global__ __launch_bounds__(kTPB) void k_reduce2(const double* partS, int nb, G
     }
 }
 
-// dL/dP_s at pooled pixel li of scale s (sign terms of both neighbours), before the 1/4 factor
-__device__ float dgrad_scale(const float* pred, const float* gt, const float* logP, const float* logG,
-                             const Geo& g, int s, int64_t li, int r, int j) {
-    const int Hs = g.Hs[s], Ws = g.Ws[s];
-    auto P = [&](int64_t q) { return s == 0 ? logf(clampf(pred[q])) : logP[g.off[s] + q]; };
-    auto G = [&](int64_t q) { return s == 0 ? logf(clampf(gt[q])) : logG[g.off[s] + q]; };
-    const float p0 = P(li), g0 = G(li);
-    float ax = 0.f, ay = 0.f;
-    if (j > 0) ax += sgnf((p0 - P(li - 1)) - (g0 - G(li - 1)));
-    if (j + 1 < Ws) ax -= sgnf((P(li + 1) - p0) - (G(li + 1) - g0));
-    if (r > 0) ay += sgnf((p0 - P(li - Ws)) - (g0 - G(li - Ws)));
-    if (r + 1 < Hs) ay -= sgnf((P(li + Ws) - p0) - (G(li + Ws) - g0));
-    const float nx = (float)g.B * Hs * (Ws - 1), ny = (float)g.B * (Hs - 1) * Ws;
-    return ax / nx + ay / ny;
-}
-
-__global__ void k_dpred(const float* __restrict__ pred, const float* __restrict__ gt, const float* __restrict__ rgb,
-                        const float* __restrict__ K, const uint8_t* __restrict__ mask, const float* __restrict__ avgP,
-                        const float* __restrict__ logP,
-                        const float* __restrict__ logG, Geo g, const double* dsc, float w0, float w1, float w2,
-                        float w3, SmoothCtx c, float* __restrict__ dpred) {
-    const int64_t HW = (int64_t)g.H * g.W, n = (int64_t)g.B * HW;
-    const double cnt = dsc[S_N];
-    const float inv_n = cnt > 0 ? (float)(1.0 / cnt) : 0.f;
-    const float sd_term = cnt > 0 ? (float)(2.0 * kLam * dsc[S_SD] / (cnt * cnt)) : 0.f;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int b = (int)(i / HW);
-        const int64_t pi = i - (int64_t)b * HW;
-        const int x = (int)(pi % g.W), y = (int)(pi / g.W);
-        const float p = pred[i], t = gt[i];
-        float grad = 0.f;
-        if ((mask ? mask[i] != 0 : t > kEps) && cnt > 0) {
-            // SI
-            const float d = logf(clampf(p)) - logf(clampf(t));
-            const float dd = 2.f * d * inv_n - sd_term;
-            grad += w0 * (dd / clampf(p)) * clampgrad(p);
-            // reprojection
-            const float* kk = K + b * 9;
-            const float fx = kk[0], cx = kk[2], fy = kk[4], cy = kk[5];
-            const float gu = (float)x - cx, gv = (float)y - cy;
-            const float a = gu / (fx + kEps), bb = gv / (fy + kEps);
-            const float dX = (gu * p) / (fx + kEps) - (gu * t) / (fx + kEps);
-            const float dY = (gv * p) / (fy + kEps) - (gv * t) / (fy + kEps);
-            const float dZ = p - t;
-            const float e = sqrtf(dX * dX + dY * dY + dZ * dZ + kEps);
-            grad += w3 * inv_n * (dX * a + dY * bb + dZ) / e;
-        }
-        // gradient matching, every scale whose pooled cell covers this pixel
-        float gg = 0.f;
-        {
-            const float dP = dgrad_scale(pred, gt, logP, logG, g, 0, i, y, x);
-            gg += dP * clampgrad(p) / clampf(p);
-        }
-        for (int s = 1; s < kScales; ++s) {
-            const int r = y >> s, j = x >> s;
-            if (r >= g.Hs[s] || j >= g.Ws[s]) continue;
-            const int64_t li = ((int64_t)b * g.Hs[s] + r) * g.Ws[s] + j;
-            const float ap = avgP[g.off[s] + li];
-            const float dP = dgrad_scale(pred, gt, logP, logG, g, s, li, r, j);
-            gg += (dP * clampgrad(ap) / clampf(ap)) / (float)(1 << (2 * s));
-        }
-        grad += w1 * gg / (float)kScales;
-        // smoothness
-        {
-            const float mean = (float)(dsc[S_PB + b] / (double)HW);
-            const float denom = mean + kEps;
-            const float gn = smooth_gn(pred + (int64_t)b * HW, rgb + (int64_t)b * 3 * HW, HW, g.W, g.H, x, y, pi,
-                                       denom, c);
-            const float Sb = (float)dsc[S_PB + g.B + b];
-            grad += w2 * (gn / denom - Sb / (denom * denom * (float)HW));
-        }
-        dpred[i] = grad;
-    }
+// the smoothness term's per-sample coupling: dpred -= w2 S_b / (denom^2 HW) (w2 != 0 only)
+__global__ void k_lossC(Geo g, const double* dsc, float w2, float* __restrict__ dpred) {
+    const int b = blockIdx.y;
+    const int HW = g.H * g.W;
+    const float mean = (float)(dsc[S_PB + b] / (double)HW);
+    const float denom = mean + kEps;
+    const float Sb = (float)dsc[S_PB + g.B + b];
+    const float cb = w2 * (Sb / (denom * denom * (float)HW));
+    float* d = dpred + (int64_t)b * HW;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < HW; i += gridDim.x * blockDim.x) d[i] -= cb;
 }
 
 Geo make_geo(int B, int H, int W) {
@@ -353,56 +366,67 @@ Geo make_geo(int B, int H, int W) {
         g.Hs[s] = H >> s;
         g.Ws[s] = W >> s;
         g.off[s] = s == 0 ? 0 : off;
-        if (s > 0) off += (int64_t)B * g.Hs[s] * g.Ws[s];
+        if (s > 0) {
+            off += (int64_t)B * g.Hs[s] * g.Ws[s];
+            g.cells += g.Hs[s] * g.Ws[s];
+        }
+        g.dWs[s] = make_fastdiv((uint32_t)std::max(1, g.Ws[s]));
+        g.dHs[s] = make_fastdiv((uint32_t)std::max(1, g.Hs[s]));
     }
+    g.dW = make_fastdiv((uint32_t)W);
     g.pyr_n = off;
     return g;
 }
 int nb_per_sample(int B, int64_t HW) {
-    return std::max(1, std::min(cdiv(1024, B), cdiv(HW, kTPB)));
+    return std::max(1, std::min(cdiv(2048, B), cdiv(HW, kTPB)));
 }
-int ng_blocks(int64_t total) { return std::max(1, std::min(1024, cdiv(total, kTPB))); }
 }  // namespace
 
-int64_t loss_workspace_floats(int B, int H, int W) { return 3 * make_geo(B, H, W).pyr_n + 64; }
+int64_t loss_workspace_floats(int B, int H, int W) {
+    // pyramid (avgP, logP, logG for scales 1..3), then scale-0 logs and edge weights (lp, lg, wx, wy)
+    return 3 * make_geo(B, H, W).pyr_n + 4 * (int64_t)B * H * W + 64;
+}
 int64_t loss_part_doubles(int B, int H, int W) {
     const int nb = nb_per_sample(B, (int64_t)H * W);
-    return (int64_t)B * nb * 5 + 1024 * 2 * kScales + (int64_t)B * nb * 3 + S_PB + 2 * B + 64;
+    return (int64_t)B * nb * (kPA + kPB) + S_PB + 2 * B + 64;
 }
 
 void loss_fwd_bwd(const float* pred, const float* gt, const float* rgb, const float* K, const uint8_t* mask, int B,
                   int H, int W, const float w[4], float* out5, float* dpred, LossWorkspace ws, hipStream_t st) {
+    if ((int64_t)B * H * W >= ((int64_t)1 << 31) || H < 2 || W < 2)
+        throw std::runtime_error("loss: B*H*W must stay below 2^31 and H, W >= 2");
     Geo g = make_geo(B, H, W);
-    const int64_t HW = (int64_t)H * W;
+    const int64_t HW = (int64_t)H * W, n = (int64_t)B * HW;
     const int nb = nb_per_sample(B, HW);
-    int64_t total = 0;
-    for (int s = 0; s < kScales; ++s) total += (int64_t)B * g.Hs[s] * g.Ws[s];
-    const int ng = ng_blocks(total);
     double* dsc = ws.part;
     double* partA = dsc + S_PB + 2 * B + 16;
-    double* partG = partA + (int64_t)B * nb * 5;
-    double* partS = partG + (int64_t)ng * 2 * kScales;
+    double* partB = partA + (int64_t)B * nb * kPA;
     float* avgP = ws.pyr;
     float* logP = avgP + g.pyr_n;
     float* logG = logP + g.pyr_n;
+    float* lp0 = logG + g.pyr_n;
+    float* lg0 = lp0 + n;
+    float* wx = lg0 + n;
+    float* wy = wx + n;
     SmoothCtx c;
     c.inv_nx = 1.f / ((float)B * H * (W - 1));
     c.inv_ny = 1.f / ((float)B * (H - 1) * W);
+    CAD_NO_ALIAS("loss_fwd_bwd", {aview(dpred, n, 1, 0, 1, 4, "dpred"), aview(ws.pyr, 1, 1, 0, 3 * g.pyr_n + 4 * n, 4, "workspace")},
+                 {aview(pred, n, 1, 0, 1, 4, "pred"), aview(gt, n, 1, 0, 1, 4, "gt"), aview(rgb, 3 * n, 1, 0, 1, 4, "rgb"),
+                  aview(mask, n, 1, 0, 1, 1, "mask")});
 
-    hipLaunchKernelGGL(k_passA, dim3(nb, B), dim3(kTPB), 0, st, pred, gt, K, mask, g, partA, nb);
-    for (int s = 1; s < kScales; ++s) {
-        const int64_t n = (int64_t)B * g.Hs[s] * g.Ws[s];
-        if (n > 0)
-            hipLaunchKernelGGL(k_pyramid, dim3(std::max(1, std::min(4096, cdiv(n, 256)))), dim3(256), 0, st, pred, gt, g, s,
-                               avgP, logP, logG);
-    }
-    hipLaunchKernelGGL(k_gradsum, dim3(ng), dim3(kTPB), 0, st, pred, gt, logP, logG, g, partG, total);
-    hipLaunchKernelGGL(k_reduce1, dim3(1), dim3(kTPB), 0, st, partA, nb, partG, ng, g, dsc);
-    hipLaunchKernelGGL(k_smooth, dim3(nb, B), dim3(kTPB), 0, st, pred, rgb, g, dsc, partS, nb, c);
-    hipLaunchKernelGGL(k_reduce2, dim3(1), dim3(kTPB), 0, st, partS, nb, g, dsc, w[0], w[1], w[2], w[3], out5);
-    const int64_t n = (int64_t)B * HW;
-    hipLaunchKernelGGL(k_dpred, dim3(std::max(1, std::min(8192, cdiv(n, 256)))), dim3(256), 0, st, pred, gt, rgb, K,
-                       mask, avgP, logP, logG, g, dsc, w[0], w[1], w[2], w[3], c, dpred);
+    hipLaunchKernelGGL(k_lossA, dim3(nb, B), dim3(kTPB), 0, st, pred, gt, rgb, K, mask, g, lp0, lg0, wx, wy, partA, nb);
+    const int64_t total = g.pyr_n;
+    if (total > 0)
+        hipLaunchKernelGGL(k_lossPyr, dim3(std::max(1, std::min(8192, cdiv(total, 256)))), dim3(256), 0, st, pred, gt, g,
+                           (int)total, avgP, logP, logG);
+    hipLaunchKernelGGL(k_lossR1, dim3(1), dim3(kTPB), 0, st, partA, nb, g, dsc);
+    hipLaunchKernelGGL(k_lossB, dim3(nb, B), dim3(kTPB), 0, st, pred, gt, K, mask, lp0, lg0, wx, wy, avgP, logP, logG, g,
+                       dsc, w[0], w[1], w[2], w[3], c, dpred, partB, nb);
+    hipLaunchKernelGGL(k_lossR2, dim3(1), dim3(kTPB), 0, st, partB, nb, g, dsc, w[0], w[1], w[2], w[3], out5);
+    if (w[2] != 0.f)
+        hipLaunchKernelGGL(k_lossC, dim3(std::max(1, std::min(256, cdiv(HW, 256 * 4))), B), dim3(256), 0, st, g, dsc, w[2],
+                           dpred);
 }
 
 }  // namespace cad

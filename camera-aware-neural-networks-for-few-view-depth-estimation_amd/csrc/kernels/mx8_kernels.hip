@@ -149,6 +149,8 @@ void mx8_quantize(const void* src, bool src_bf16, int64_t lds, int scoff, int C,
     const int nblk = C / 32;
     const int64_t n = M * nblk;
     if (n == 0) return;
+    CAD_NO_ALIAS("mx8_quantize", {aview(dst.q, M, dst.ld, dst.coff, C, 1, "q"), aview(dst.s, M, dst.ld / 32, dst.coff / 32, nblk, 1, "scales")},
+                 {aview(src, M, lds, scoff, C, src_bf16 ? 2 : 4, "src")});
     auto* q = static_cast<uint8_t*>(const_cast<void*>(dst.q));
     auto* s = static_cast<uint8_t*>(const_cast<void*>(dst.s));
     const dim3 grid((unsigned)((n + 255) / 256));
@@ -167,6 +169,9 @@ void dense_fwd_x8(Mx8 x, int K, Mx8 w, int N, float* y, int64_t ldy, int ycoff, 
     check_view(w, "dense w");
     if (!dense_x8_ok(K, N)) throw std::runtime_error("dense MX-fp8 GEMM: K % 128 and N % 64 required");
     if (M > INT32_MAX) throw std::runtime_error("dense GEMM: too many rows");
+    CAD_NO_ALIAS("dense_fwd_x8", {aview(y, M, ldy, ycoff, N, y_bf16 ? 2 : 4, "y")},
+                 {aview(x.q, M, x.ld, x.coff, K, 1, "x"), aview(x.s, M, x.ld / 32, x.coff / 32, K / 32, 1, "x scales"),
+                  aview(w.q, N, w.ld, w.coff, K, 1, "w"), aview(w.s, N, w.ld / 32, w.coff / 32, K / 32, 1, "w scales")});
     GemmArgs a{};
     a.M = (int)M; a.N = N; a.K = K;
     a.B = 1; a.H = 1; a.W = (int)M;
@@ -194,6 +199,10 @@ void conv3x3_fwd_x8(Mx8 x, int cin, Mx8 w, int cout, float* y, int64_t ldy, int 
     const WinX8 p = pick_win_x8(cin, W, cout);
     if (!p.R) throw std::runtime_error("MX-fp8 window conv: cin % 64, N % 64 and a block width dividing W required");
     if (w.ld < 9 * (int64_t)cin) throw std::runtime_error("MX-fp8 window conv: weight rows shorter than 9 cin");
+    CAD_NO_ALIAS("conv3x3_fwd_x8", {aview(y, (int64_t)B * H * W, ldy, ycoff, cout, y_bf16 ? 2 : 4, "y")},
+                 {aview(x.q, (int64_t)B * H * W, x.ld, x.coff, cin, 1, "x"),
+                  aview(x.s, (int64_t)B * H * W, x.ld / 32, x.coff / 32, cin / 32, 1, "x scales"),
+                  aview(w.q, cout, w.ld, w.coff, 9 * cin, 1, "w")});
     GemmArgs a{};
     a.M = B * H * W; a.N = cout; a.K = 9 * cin;
     a.B = B; a.H = H; a.W = W;

@@ -537,6 +537,8 @@ void bn_relu_fwd(const float* y, int C, const float* scale, const float* shift, 
     const int np = os ? split_planes() : 0;
     char* o = static_cast<char*>(os);
     const RowGrid g = row_grid(M, C);
+    CAD_NO_ALIAS("bn_relu_fwd", {aview(out, M, ldo, ocoff, C, 4, "out"), aview(os, M, ldos, oscoff, C, 2, "out twin")},
+                 {aview(y, M, C, 0, C, y_bf16 ? 2 : 4, "y")}, true);
     if (qx) {
         if (np != 1 || C % 32 || qx->ld % 128 || qx->coff || !qx->q || !qx->s)
             throw std::runtime_error("bn_relu_fwd: MX-fp8 copy layout");
@@ -571,15 +573,6 @@ __global__ void k_bn_bwd_coef(const double* tot, int C, int64_t M, const float* 
     coef[c] = k1;
     coef[C + c] = (float)(k1 * sdz / (double)M);
     coef[2 * C + c] = (float)(k1 * sdzx / (double)M);
-}
-void bn_bwd_from_tiles(const double* part, int tiles, int C, int64_t M, const float* gamma, const float* invstd,
-                       float* coef, float* dgamma, float* dbeta, double* scratch, hipStream_t st) {
-    double* tot = scratch;
-    double* p2 = scratch + 2 * C;
-    // columns [0, C): sum dz, [C, 2C): sum dz xhat — tot as bn_relu_bwd's colreduce leaves it
-    const int S = launch_colreduce<1>(OpSumD{part, 2 * C}, tiles, 2 * C, p2, st);
-    launch_colfinal(p2, S, 2 * C, tot, nullptr, 1.f, st);
-    hipLaunchKernelGGL(k_bn_bwd_coef, dim3(cdiv(C, 64)), dim3(64), 0, st, tot, C, M, gamma, invstd, coef, dgamma, dbeta);
 }
 template <int NP, bool YB, bool HG, bool GB = false, bool PA = false>
 __global__ __launch_bounds__(256) void k_bn_relu_bwd_rows(const float* __restrict__ g, int64_t ldg, int gcoff,
@@ -710,7 +703,12 @@ void bn_relu_bwd(const float* g, int64_t ldg, int gcoff, const float* y, int C, 
     double* tot = scratch;
     double* part = scratch + 2 * C;
     if (tile_part && (film_dgam || tiles <= 0)) throw std::runtime_error("bn_relu_bwd: tile partials");
-    if (gmul && (M >= ((int64_t)1 << 32) || HW < 2)) throw std::runtime_error("bn_relu_bwd: FiLM gradient layout");
+    // the reduction pass reads g and y, then the apply pass rewrites each element it reads: dy may be
+    // exactly g (in place), but no other overlap
+    CAD_NO_ALIAS("bn_relu_bwd", {aview(dy, M, C, 0, C, 4, "dy"), aview(dy_split, M, C, 0, C, 2, "dy twin")},
+                 {aview(head || pool ? nullptr : g, M, ldg, gcoff, C, g_bf16 ? 2 : 4, "g"),
+                  aview(y, M, C, 0, C, y_bf16 ? 2 : 4, "y")}, true);
+    if (gmul && (M >= ((int64_t)1 << 32) || HW < 1)) throw std::runtime_error("bn_relu_bwd: FiLM gradient layout");
     const FastDiv dHW = make_fastdiv(gmul ? (uint32_t)HW : 2u);
     if (film_dgam) {
         // a FiLM block's bn1: the BN sums and the FiLM affine's per-(sample, channel) sums in one pass,

@@ -171,6 +171,8 @@ void col2im(const float* dcol, int Kc, int C, int B, int H, int W, int KH, int K
     const int Ho = (H + 2 * P - KH) / S + 1, Wo = (W + 2 * P - KW) / S + 1;
     if (C % 4 || Kc % 4 || lddx % 4) throw std::runtime_error("col2im: alignment");
     const int64_t n4 = (int64_t)B * H * W * C / 4;
+    CAD_NO_ALIAS("col2im", {aview(dx, (int64_t)B * H * W, lddx, 0, C, 4, "dx")},
+                 {aview(dcol, (int64_t)B * Ho * Wo, Kc, 0, Kc, 4, "dcol")});
     hipLaunchKernelGGL(k_col2im, dim3(ew_blocks(n4)), dim3(256), 0, st, dcol, Kc, C, B, H, W, KH, KW, S, P, Ho, Wo, dx,
                        lddx, n4);
 }
@@ -266,6 +268,9 @@ void maxpool3s2_bwd(const float* dout, const uint8_t* idx, int C, int B, int H, 
     if (add && (ldadd < C || ldadd % 4)) throw std::runtime_error("maxpool3s2_bwd: added matrix layout");
     const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
     const int64_t n4 = (int64_t)B * H * W * C / 4;
+    CAD_NO_ALIAS("maxpool3s2_bwd", {aview(dx, (int64_t)B * H * W, C, 0, C, 4, "dx")},
+                 {aview(dout, (int64_t)B * Ho * Wo, C, 0, C, 4, "dout"), aview(idx, (int64_t)B * Ho * Wo, C, 0, C, 1, "argmax"),
+                  aview(add, (int64_t)B * H * W, ldadd, 0, C, 4, "add")});
     if (n4 < ((int64_t)1 << 31))
         hipLaunchKernelGGL(k_maxpool3s2_bwd<uint32_t>, dim3(cdiv(n4, 256)), dim3(256), 0, st, dout, idx, C, B, H, W, Ho, Wo,
                            dx, n4, add, ldadd);
@@ -316,6 +321,9 @@ void bn_add_relu(const float* y, const float* scale, const float* shift, const f
                  const float* dshift, const float* x, int64_t ldx, int C, int64_t M, float* out, void* out_split,
                  hipStream_t st, bool y_bf16, const Mx8* qx) {
     const int64_t n4 = M * C / 4;
+    CAD_NO_ALIAS("bn_add_relu", {aview(out, M, C, 0, C, 4, "out"), aview(out_split, M, C, 0, C, 2, "out twin")},
+                 {aview(y, M, C, 0, C, y_bf16 ? 2 : 4, "y"), aview(yd, M, C, 0, C, y_bf16 ? 2 : 4, "projection y"),
+                  aview(yd ? nullptr : x, M, ldx, 0, C, 4, "shortcut x")}, true);
     if (qx) {
         if (C % 32 || qx->ld % 128 || qx->coff || !qx->q || !qx->s) throw std::runtime_error("bn_add_relu: MX-fp8 copy layout");
         auto* q = static_cast<uint8_t*>(const_cast<void*>(qx->q));
@@ -350,6 +358,8 @@ __global__ void k_relu_mask(const float* __restrict__ g, int64_t ldg, int gcoff,
 }
 void relu_mask(const float* g, int64_t ldg, int gcoff, const float* out, int C, int64_t M, float* gs, hipStream_t st) {
     const int64_t n4 = M * C / 4;
+    CAD_NO_ALIAS("relu_mask", {aview(gs, M, C, 0, C, 4, "gs")},
+                 {aview(g, M, ldg, gcoff, C, 4, "g"), aview(out, M, C, 0, C, 4, "out")}, true);
     hipLaunchKernelGGL(k_relu_mask, dim3(ew_blocks(n4)), dim3(256), 0, st, g, ldg, gcoff, out, C, gs, n4);
 }
 
@@ -366,6 +376,7 @@ __global__ void k_mask_inplace(float* y, int64_t ldy, int ycoff, const float* ma
 }
 void mask_inplace(float* y, int64_t ldy, int ycoff, const float* mask, int C, int64_t M, hipStream_t st) {
     if (C % 4 || ldy % 4 || ycoff % 4) throw std::runtime_error("mask_inplace: alignment");
+    CAD_NO_ALIAS("mask_inplace", {aview(y, M, ldy, ycoff, C, 4, "y (in place)")}, {aview(mask, M, ldy, ycoff, C, 4, "mask")});
     const int64_t n4 = M * C / 4;
     hipLaunchKernelGGL(k_mask_inplace, dim3(ew_blocks(n4)), dim3(256), 0, st, y, ldy, ycoff, mask, C, n4);
 }
@@ -393,6 +404,9 @@ void add_strided(float* dst, int64_t lddst, const float* src, int64_t ldsrc, int
                  int S, hipStream_t st) {
     const int Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
     const int64_t n4 = (int64_t)B * Ho * Wo * C / 4;
+    // dst is accumulated in place (declared); src must be another buffer
+    CAD_NO_ALIAS("add_strided", {aview(dst, (int64_t)B * H * W, lddst, 0, C, 4, "dst")},
+                 {aview(src, (int64_t)B * Ho * Wo, ldsrc, scoff, C, 4, "src")});
     hipLaunchKernelGGL(k_add_strided, dim3(ew_blocks(n4)), dim3(256), 0, st, dst, lddst, src, ldsrc, scoff, C, H, W,
                        Ho, Wo, S, n4);
 }
@@ -416,6 +430,8 @@ void copy_twin(Split src, int C, int B, int H, int W, int S, void* dst, int64_t 
     if (C % 8 || src.ld % 8 || src.coff % 8 || ldd % 8 || dcoff % 8) throw std::runtime_error("copy_twin: alignment");
     const int Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
     const int64_t n8 = (int64_t)B * Ho * Wo * C / 8;
+    CAD_NO_ALIAS("copy_twin", {aview(dst, (int64_t)B * Ho * Wo, ldd, dcoff, C, 2, "dst")},
+                 {aview(src.p, (int64_t)B * H * W, src.ld, src.coff, C, 2, "src")});
     hipLaunchKernelGGL(k_copy_twin, dim3(ew_blocks(n8)), dim3(256), 0, st, (const uint16_t*)src.p, src.ld, src.coff,
                        (uint16_t*)dst, ldd, dcoff, C, H, W, Ho, Wo, S, n8);
 }

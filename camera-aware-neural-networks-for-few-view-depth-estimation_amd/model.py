@@ -704,6 +704,19 @@ class ResNetUNet:
         """Device address of the flat gradient slab (n_flat floats): the data-parallel all-reduce buffer."""
         return self._flat_g
 
+    def debug_buffer(self, name: str) -> torch.Tensor:
+        """Test hook: a buffer of the last train-mode forward as fp32 NHWC rows (cad_resunet_debug_buffer:
+        "y:<conv>" stored pre-BN outputs, "scale:<bn>" / "shift:<bn>" BN-apply coefficients, "out:<block>"
+        block outputs)."""
+        n = int(self._f("debug_buffer")(self.h, name.encode(), None, 0))
+        if n < 0:
+            raise KeyError(name)
+        out = np.empty(n, np.float32)
+        check(0 if self._f("debug_buffer")(self.h, name.encode(), out.ctypes.data_as(_abi.FP), n) == n else 1, name)
+        if name.startswith(("amax", "sidx")):
+            out = out.view(np.int32)
+        return torch.from_numpy(out)
+
     def forward(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
         B, Cc, H, W = x.shape
         assert Cc == 3 and H == self.height and W == self.width and B <= self.batch, "input shape mismatch"
@@ -846,7 +859,7 @@ class GeometryAwareNetwork(ResNetUNet):
         """Test hook: a buffer of the last step as NHWC rows ("cat<l>", "dcat<l>", "x<l>", "u<l>", "z<l>",
         the pre-BN conv outputs "y1<e|d><l>", "y2<e|d><l>"; int32: the CBAM decisions "amax<e|d><l>",
         "sidx<e|d><l>")."""
-        n = int(self._f("debug_buffer")(self.h, name.encode(), None, 0))
+        return ResNetUNet.debug_buffer(self, name)
         if n < 0:
             raise KeyError(name)
         out = np.empty(n, np.float32)

@@ -115,6 +115,16 @@ int cad_abi_version(void);
 cad_status cad_set_gemm_engine(int engine);
 int cad_get_gemm_engine(void);
 const char* cad_last_error(void);
+/* Launch-level aliasing guard (csrc/host/alias.cpp): with mode 1 every instrumented launcher (the conv /
+ * ConvT / dense GEMMs on every engine, the MX-fp8 GEMMs and quantiser, the BN / residual / pool / twin
+ * passes) refuses a launch whose output byte range overlaps one of its inputs — CAD_ERR_INVALID, the
+ * operands named in cad_last_error() — unless that pair is declared in place.  Default: the environment
+ * (CAD_ALIAS_CHECK=1; tests/conftest.py sets it), else off.  Returns the previous mode. */
+int cad_set_alias_check(int mode);
+/* The guard's overlap rule on two row views (rows of ld elements of es bytes, columns [coff, coff+cols)):
+ * 1 when they share a byte.  Host arithmetic only (no device). */
+int cad_alias_views_overlap(const void* a, int64_t arows, int64_t ald, int64_t acoff, int64_t acols, int aes,
+                            const void* b, int64_t brows, int64_t bld, int64_t bcoff, int64_t bcols, int bes);
 cad_status cad_device_count(int* n);
 cad_status cad_set_device(int device);
 cad_status cad_stream_synchronize(void* stream);
@@ -505,6 +515,10 @@ cad_status cad_resunet_backward(cad_resunet* h, const float* ddepth, void* strea
 /* staged backward (decoder first; stage s writes only the gradients in its flat-slab range, ranges
  * decreasing with s) and the overlapped data-parallel exchange over it (cad_unet_backward_allreduce's
  * semantics: SUM buckets of >= bucket_elems floats on the communicator's stream) */
+/* Test hook: a buffer of the last train-mode forward as fp32 rows — "y:<conv>" (stored pre-BN output,
+   bf16 widened), "scale:<bn>" / "shift:<bn>" (BN-apply coefficients), "out:<block>" (block output:
+   "encoder.layer<L>.<i>", "encoder.stem", "dec<l>").  Returns the element count, -1 if unknown. */
+int64_t cad_resunet_debug_buffer(cad_resunet* h, const char* name, float* host, int64_t numel);
 int cad_resunet_num_stages(const cad_resunet* h);
 /* host only (no device): the stage count (23) and each stage's [offset, offset+count), as
  * cad_resunet_stage_grad_range reports them, and the slab size */

@@ -151,14 +151,28 @@ def _rnd(x):
     return O._RoundOperand.apply(x) if O._GEMM["operands"] in ("bf16", "mx8") else x
 
 
-def _conv(x, w, stride, pad):
+def _conv(x, w, stride, pad, name=None):
     mode = O._GEMM["operands"]
     if mode == "mx8" and x8_eligible(w.shape[2], stride, x.shape[1], w.shape[0], x.shape[3]):
         y = _X8Conv.apply(x, w, stride, pad)
     else:
         y = F.conv2d(_rnd(x), _rnd(w), None, stride, pad)
     # bf16 / mx8: the dy operand of dgrad / wgrad rounded, and the pre-BN output stored as bf16
-    return O._RoundOperand.apply(O._RoundGradOperand.apply(y)) if mode in ("bf16", "mx8") else y
+    y = O._RoundOperand.apply(O._RoundGradOperand.apply(y)) if mode in ("bf16", "mx8") else y
+    # test hook (cad_oracle.Y_FORCE): the full-size test imposes the GPU's stored pre-BN outputs, keyed
+    # by the convolution's parameter name without ".weight"; Y_OWN records this restatement's own
+    forced = O.Y_FORCE.get(name) if name else None
+    if forced is None:
+        return y
+    O.Y_OWN[name] = y.detach().clone()
+    return y + (forced.to(y.device, y.dtype) - y).detach()
+
+
+def _relu(z, name):
+    """ReLU with the test hook cad_oracle.RELU_FORCE (the GPU run's decisions, keyed by the BN prefix or
+    "<block>.out" for a bottleneck's relu(bn3 + shortcut))."""
+    m = O.RELU_FORCE.get(name)
+    return F.relu(z) if m is None else z * m.to(z.device, z.dtype)
 
 
 def _rgrad(x):
@@ -168,16 +182,18 @@ def _rgrad(x):
 
 
 def _bottleneck(x, p, bufs, pre, stride, down, train):
-    t = F.relu(O._bn(_conv(x, p[pre + "conv1.weight"], 1, 0), p, bufs, pre + "bn1", train))
-    t = F.relu(O._bn(_conv(_rgrad(t) if stride == 1 else t, p[pre + "conv2.weight"], stride, 1), p, bufs, pre + "bn2",
-                     train))
-    t = O._bn(_conv(_rgrad(t), p[pre + "conv3.weight"], 1, 0), p, bufs, pre + "bn3", train)
-    sc = O._bn(_conv(x, p[pre + "downsample.0.weight"], stride, 0), p, bufs, pre + "downsample.1", train) if down else x
-    return F.relu(t + sc)
+    t = _relu(O._bn(_conv(x, p[pre + "conv1.weight"], 1, 0, pre + "conv1"), p, bufs, pre + "bn1", train), pre + "bn1")
+    t = _relu(O._bn(_conv(_rgrad(t) if stride == 1 else t, p[pre + "conv2.weight"], stride, 1, pre + "conv2"), p, bufs,
+                    pre + "bn2", train), pre + "bn2")
+    t = O._bn(_conv(_rgrad(t), p[pre + "conv3.weight"], 1, 0, pre + "conv3"), p, bufs, pre + "bn3", train)
+    sc = (O._bn(_conv(x, p[pre + "downsample.0.weight"], stride, 0, pre + "downsample.0"), p, bufs,
+                pre + "downsample.1", train) if down else x)
+    return _relu(t + sc, pre + "out")
 
 
 def forward(x, p, bufs, train=True, max_depth=10.0):
-    x1 = F.relu(O._bn(_conv(x, p["encoder.conv1.weight"], 2, 3), p, bufs, "encoder.bn1", train))
+    x1 = _relu(O._bn(_conv(x, p["encoder.conv1.weight"], 2, 3, "encoder.conv1"), p, bufs, "encoder.bn1", train),
+               "encoder.bn1")
     y = F.max_pool2d(x1, 3, 2, 1)
     feats = []
     for L, n in enumerate(NBLOCKS):
@@ -190,8 +206,10 @@ def forward(x, p, bufs, train=True, max_depth=10.0):
         # (bias_bf16: the bias gradient sums the bf16 up-half gradient the ConvT GEMMs read, as resunet.cpp)
         up = O._convT2x2(y, p[pre + "up.weight"], p[pre + "up.bias"], bias_bf16=True)
         y = torch.cat([skips[l], up], 1) if sk else up
-        y = F.relu(O._bn(_conv(y, p[pre + "conv.conv1.weight"], 1, 1), p, bufs, pre + "conv.bn1", train))
-        y = F.relu(O._bn(_conv(_rgrad(y), p[pre + "conv.conv2.weight"], 1, 1), p, bufs, pre + "conv.bn2", train))
+        y = _relu(O._bn(_conv(y, p[pre + "conv.conv1.weight"], 1, 1, pre + "conv.conv1"), p, bufs, pre + "conv.bn1",
+                        train), pre + "conv.bn1")
+        y = _relu(O._bn(_conv(_rgrad(y), p[pre + "conv.conv2.weight"], 1, 1, pre + "conv.conv2"), p, bufs,
+                        pre + "conv.bn2", train), pre + "conv.bn2")
     z = F.conv2d(y, p["out_conv.weight"], p["out_conv.bias"])
     return torch.sigmoid(z) * max_depth
 

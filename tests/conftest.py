@@ -4,6 +4,10 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# every GPU test runs with the launch-level aliasing guard on (csrc/host/alias.cpp; include/cad/cad.h
+# cad_set_alias_check): a launch whose output overlaps one of its inputs fails with CAD_ERR_INVALID
+# instead of racing (an environment value set by the caller, e.g. log:<path>, wins)
+os.environ.setdefault("CAD_ALIAS_CHECK", "1")
 sys.path.insert(0, ROOT)
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 

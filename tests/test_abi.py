@@ -83,3 +83,24 @@ def test_cpp_dropin_header_links(tmp_path):
                     os.path.join(root, "tests", "hpp_probe.cpp"), "-L", pkg, "-lcad_hip",
                     "-Wl,-rpath," + pkg, "-Wl,--allow-shlib-undefined"], check=True)
     assert exe.exists()
+
+
+def test_alias_overlap_rule(cad):
+    """The aliasing guard's overlap rule (host arithmetic, no device): distinct buffers, the skip / up
+    halves of one concat buffer (same pitch, disjoint columns: no overlap), an output written over its
+    input, a bf16 twin whose rows straddle fp32 columns, a weight block inside a slab."""
+    lib = cad.load_library()
+    base = 1 << 20
+
+    def ov(a, b):
+        return lib.cad_alias_views_overlap(C.c_void_p(a[0]), *a[1:], C.c_void_p(b[0]), *b[1:])
+    M = 1000
+    assert ov((base, M, 64, 0, 64, 4), (base + 4 * 64 * M, M, 64, 0, 64, 4)) == 0     # back to back
+    assert ov((base, M, 64, 0, 64, 4), (base + 4 * 64 * M - 4, M, 64, 0, 64, 4)) == 1
+    assert ov((base, M, 128, 0, 64, 4), (base, M, 128, 64, 64, 4)) == 0              # concat halves
+    assert ov((base, M, 128, 0, 65, 4), (base, M, 128, 64, 64, 4)) == 1
+    assert ov((base, M, 128, 0, 64, 2), (base, M, 128, 64, 64, 2)) == 0              # bf16 concat halves
+    assert ov((base, M, 128, 0, 64, 4), (base, M, 64, 0, 64, 2)) == 1                # twin over fp32 rows
+    assert ov((base, 1, 4096, 0, 4096, 4), (base + 4 * 1000, 3, 8, 0, 8, 4)) == 1     # weights in a slab
+    assert ov((0, M, 64, 0, 64, 4), (base, M, 64, 0, 64, 4)) == 0                    # absent operand
+    assert ov((base, 0, 64, 0, 64, 4), (base, M, 64, 0, 64, 4)) == 0                 # empty view

@@ -142,7 +142,9 @@ def test_rayfilm_input_pack(cad, dev, oracle):
     assert torch.equal(camn, ref)
 
 
-@pytest.mark.parametrize("model,f,B,H,W", [("film", 16, 2, 64, 96), ("rayfilm", 32, 4, 48, 64)])
+# (16 x 16: a 1 x 1 bottleneck, whose FiLM apply / gradient maps row -> sample with HW = 1)
+@pytest.mark.parametrize("model,f,B,H,W", [("film", 16, 2, 64, 96), ("rayfilm", 32, 4, 48, 64), ("film", 8, 3, 16, 16),
+                                           ("rayfilm", 8, 3, 16, 16)])
 def test_film_train_step_vs_oracle(cad, dev, oracle, model, f, B, H, W):
     """Wider FiLM nets against the oracle; same fp64-yardstick criteria as the baseline test
     (test_gpu_model.py::test_train_step_vs_oracle)."""

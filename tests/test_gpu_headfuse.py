@@ -17,8 +17,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _run(tmp_path, fuse, args, var="CAD_HEADFUSE"):
-    if var == "CAD_RC1" and fuse:
-        fuse = 2   # (CAD_RC1=2: both engines; 1 recomputes on the bf16 engine only, 0 — the default — stores y1)
     out = tmp_path / f"{var}{fuse}.pt"
     env = dict(os.environ, **{var: str(fuse)})
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "headfuse_ab.py"), *map(str, args), str(out)],
@@ -42,9 +40,6 @@ def test_head_fusion_bit_identical(tmp_path, kind, eng, f, B, H, W):
                                                   ("CAD_DCATSPLIT", "baseline", 1, 64, 2, 64, 64),
                                                   ("CAD_DCATSPLIT", "rayfilm", 1, 32, 2, 48, 64),
                                                   ("CAD_DCATSPLIT", "film", 1, 16, 2, 64, 96),
-                                                  ("CAD_RC1", "baseline", 2, 16, 2, 64, 96),
-                                                  ("CAD_RC1", "baseline", 1, 32, 2, 48, 64),
-                                                  ("CAD_RC1", "baseline", 2, 64, 2, 64, 64),
                                                   ("CAD_BNPOOL", "baseline", 2, 16, 2, 64, 96),
                                                   ("CAD_BNPOOL", "rayfilm", 2, 32, 2, 48, 64),
                                                   ("CAD_BNPOOL", "baseline", 1, 64, 2, 64, 64),
@@ -60,10 +55,7 @@ def test_backward_fusions_bit_identical(tmp_path, var, kind, eng, f, B, H, W):
     """CAD_POOLFOLD (fp32 engines; the bf16 engine always folds): the max-pool backward folded into the
     encoder's bn2 backward (nn_kernels.hip pool_add) makes the scatter's fp32 add per element.
     CAD_DCATSPLIT (bf16 engine): the decoder conv1 dgrad writes dcat's two halves straight into their
-    bf16 buffers (EpiStoreSplit2B16) with the rounding split_rows applies.  CAD_RC1: enc1.conv1 recomputed
-    instead of stored (epilogues.hpp "Recomputed convolution"; both engines) — the same accumulators, and
-    the BN-backward sums in fp64 from per-tile partials instead of row slices (a reordering of fp64 sums
-    that would have to land within 1e-16 of an fp32 rounding boundary to show).  CAD_BNPOOL (all engines):
+    bf16 buffers (EpiStoreSplit2B16) with the rounding split_rows applies.  CAD_BNPOOL (all engines):
     each encoder block's bn2 + ReLU pass also writes the next level's max-pool (nn_kernels.hip
     bn_relu_pool_fwd: the same affine, rounding and comparison).  CAD_BNSUMS (S3 engine): bn1's
     backward sums come from conv2's input-gradient window epilogue (EpiStoreBnSums: fp64 sums of the

@@ -477,3 +477,29 @@ def test_conv3x3_bf16_window_kernels(cad, dev, B, H, W, cin, cout):
         assert max_rel_err(nchw(dx.cpu()), xd.grad) < TOL
     finally:
         lib.cad_set_gemm_engine(prev)
+
+
+def test_alias_guard_refuses_overlapping_launch(cad, dev):
+    """The launch-level aliasing guard (cad.h cad_set_alias_check; on for every GPU test through
+    tests/conftest.py): a bf16 window dgrad asked to write its input gradient into the buffer it reads
+    as dZ — round 5's config-5 race in miniature — is refused with CAD_ERR_INVALID naming both operands,
+    and nothing is launched; the same call on separate buffers runs."""
+    lib = cad.load_library()
+    prev_engine = lib.cad_get_gemm_engine()
+    prev = lib.cad_set_alias_check(1)
+    assert lib.cad_set_gemm_engine(2) == 0
+    try:
+        B, H, W, c = 2, 16, 64, 64
+        dz = torch.randn(B, H, W, c, device=dev).bfloat16()
+        w = torch.randn(c, c, 3, 3, device=dev) * 0.05
+        st = lib.cad_op_conv3x3_dgrad_bf16(_p(dz), c, c, _p(w), c, _p(dz), c, 1, B, H, W, _s())
+        msg = lib.cad_last_error().decode()
+        assert st == 1, (st, msg)
+        assert "alias" in msg and "dx" in msg and "dz" in msg, msg
+        dx = torch.empty(B, H, W, c, device=dev).bfloat16()
+        assert lib.cad_op_conv3x3_dgrad_bf16(_p(dz), c, c, _p(w), c, _p(dx), c, 1, B, H, W, _s()) == 0, \
+            lib.cad_last_error()
+        torch.cuda.synchronize()
+    finally:
+        lib.cad_set_gemm_engine(prev_engine)
+        lib.cad_set_alias_check(prev)

@@ -1,0 +1,72 @@
+"""The config-5 network's fused and alternative paths (resunet.cpp, conv_kernels.hip) against their
+unfused / plain forms: two training steps with a switch at 0 and at its default (tools/resunet_ab.py,
+one process each: the switches are read once per process), bf16 and MXFP8 networks, B = 2 at 64 x 128
+(every layer, the 32-channel dec0 strip, the stride-2 projections).
+
+Bit-identical by construction (the same products and adds in the same order), so compared with
+torch.equal — predictions, losses, first-step gradients, parameters after the second step:
+  CAD_MASKFUSE   the bottleneck's ReLU backward mask inside the conv1 dgrad epilogue of the block above
+                 (EpiStoreAddMask) instead of the k_relu_mask pass;
+  CAD_UPSPLIT    a decoder conv1's input gradient split-stored (up half bf16 straight into the ConvT
+                 operand, EpiStoreSplitB16) instead of a split pass;
+  CAD_MXPREQ     (fp8) the BN-apply / residual-join passes writing the MX-fp8 copy of their output
+                 (mx8_store_group) instead of each contraction quantising its operand;
+  CAD_WPREPBATCH the per-step weight conversions batched into k_weight_prep launches.
+Reordered fp32 sums (not bit-identical; bounded):
+  CAD_SKIPFUSE   the decoder skip gradients added in the projection block's conv1 dgrad epilogue, so the
+                 skip add precedes the projection's scatter add (fp32 rounding of that one add);
+  CAD_WGSTRIP2   strip weight gradients two output rows per step: K-slices split at row pairs;
+  CAD_WGPAIR     dec0's 32-channel weight gradients as the 64-channel strip kernel on pixel pairs (a
+                 different summation order than the im2col kernel's).
+For these: the first step's forward is identical (the switches act on the backward only), every
+gradient at 1 - cos <= 1e-6 and normalised max error <= 1e-3 (a reordered fp32 sum that lands on the
+other side of a bf16 rounding boundary of a stored gradient moves one element by 2^-8 of itself)."""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SHAPE = (2, 64, 128)
+
+
+def _run(tmp_path, var, val, fp8):
+    out = tmp_path / f"{var}{val}_{fp8}.pt"
+    env = dict(os.environ)
+    env.pop(var, None)
+    if val is not None:
+        env[var] = str(val)
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "resunet_ab.py"), str(fp8), *map(str, SHAPE), str(out)],
+                   check=True, env=env, timeout=300)
+    return torch.load(out, weights_only=True)
+
+
+@pytest.mark.parametrize("var,fp8", [("CAD_MASKFUSE", 0), ("CAD_MASKFUSE", 1), ("CAD_UPSPLIT", 0), ("CAD_UPSPLIT", 1),
+                                     ("CAD_MXPREQ", 1), ("CAD_WPREPBATCH", 0), ("CAD_WPREPBATCH", 1)])
+def test_resunet_switch_bit_identical(tmp_path, var, fp8):
+    a = _run(tmp_path, var, 0, fp8)
+    b = _run(tmp_path, var, None, fp8)
+    assert a.keys() == b.keys()
+    bad = [k for k in a if not torch.equal(a[k], b[k])]
+    assert not bad, bad[:8]
+
+
+@pytest.mark.parametrize("var,fp8", [("CAD_SKIPFUSE", 0), ("CAD_WGSTRIP2", 0), ("CAD_WGPAIR", 0), ("CAD_WGPAIR", 1)])
+def test_resunet_switch_reordered(tmp_path, var, fp8):
+    a = _run(tmp_path, var, 0, fp8)
+    b = _run(tmp_path, var, None, fp8)
+    assert torch.equal(a["pred0"], b["pred0"]) and torch.equal(a["loss0"], b["loss0"])
+    worst = []
+    for k in a:
+        if not k.startswith("grad."):
+            continue
+        x, y = a[k].double().flatten(), b[k].double().flatten()
+        cos = torch.nn.functional.cosine_similarity(x[None], y[None]).item() if y.norm() > 0 else 1.0
+        err = (x - y).abs().max().item() / (y.abs().max().item() or 1.0)
+        worst.append((1 - cos, err, k))
+    worst.sort(reverse=True)
+    print(f"{var} fp8={fp8}: worst (1-cos, max err, tensor): {worst[:3]}")
+    assert worst[0][0] <= 1e-6 and max(w[1] for w in worst) <= 1e-3, worst[:4]
