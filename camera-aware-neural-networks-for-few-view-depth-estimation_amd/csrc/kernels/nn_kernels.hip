@@ -60,6 +60,9 @@ __global__ void k_colreduce(Op op, int64_t R, int C, int64_t rows_per_slice, dou
         for (int e = 0; e < 4; ++e) acc[o][e] = 0.0;
     if (c4 < C4) {
         const auto pc = prep_of(op, c4, r0, r1);   // per-thread channel coefficients, loaded once
+        // unrolled: the loads of four rows in flight together (one per iteration left the pass
+        // latency-bound: 0.90 of wave-cycles parked); the adds stay in row order (the same sums)
+#pragma unroll 4
         for (int64_t r = r0 + threadIdx.y; r < r1; r += RY) op(r, c4, acc, pc);
     }
     extern __shared__ double red[];   // [RY][CX][NOUT*4]
@@ -515,8 +518,18 @@ __global__ __launch_bounds__(256) void k_bn_relu_fwd_rows(const float* __restric
     const float4 s = *reinterpret_cast<const float4*>(scale + c);
     const float4 t = *reinterpret_cast<const float4*>(shift + c);
     const int64_t r1 = min(M, (int64_t)(blockIdx.y + 1) * rps);
-    for (int64_t r = (int64_t)blockIdx.y * rps + threadIdx.y; r < r1; r += blockDim.y) {
-        const float4 v = load4<YB>(y, r * C + c);
+    const int RY = blockDim.y;
+    // four rows per pass of the loop, their loads issued together (memory-level parallelism)
+    for (int64_t rb = (int64_t)blockIdx.y * rps + threadIdx.y; rb < r1; rb += 4 * RY) {
+      float4 vb[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+          if (rb + u * RY < r1) vb[u] = load4<YB>(y, (rb + u * RY) * C + c);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t r = rb + u * RY;
+        if (r >= r1) break;
+        const float4 v = vb[u];
         float4 o;
         o.x = bn_relu1(v.x, s.x, t.x);
         o.y = bn_relu1(v.y, s.y, t.y);
@@ -530,6 +543,7 @@ __global__ __launch_bounds__(256) void k_bn_relu_fwd_rows(const float* __restric
                                         __uint_as_float(t.y << 16), __uint_as_float(t.y & 0xFFFF0000u)),
                             q, qs, ldq, r, c);
         }
+      }
     }
 }
 void bn_relu_fwd(const float* y, int C, const float* scale, const float* shift, float* out, int64_t ldo,
@@ -604,22 +618,37 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_rows(const float* __restric
         gm_row = s0 != s1;
         if (!gm_row) gm = *reinterpret_cast<const float4*>(gmul + (int64_t)s0 * C + c0);
     }
-    for (int64_t r = r0 + threadIdx.y; r < r1; r += blockDim.y) {
+    const int RY = blockDim.y;
+    // four rows per pass of the loop: their g / y loads issued together (one row per iteration left
+    // the pass latency-bound, 0.90 of wave-cycles parked); rows keep their per-thread order
+    for (int64_t rb = r0 + threadIdx.y; rb < r1; rb += 4 * RY) {
+      float4 gb[4], yb[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t r = rb + u * RY;
+        if (r >= r1) break;
+        if constexpr (!HG && !PA) gb[u] = load4<GB>(g, r * ldg + gcoff + c0);
+        yb[u] = load4<YB>(y, r * C + c0);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t r = rb + u * RY;
+        if (r >= r1) break;
         float4 gv;
         if constexpr (HG) {
             const float s = hg.sig[r];
             const float dp = hg.dpred[r] * hg.md * ((1.f - s) * s);
             gv = make_float4(dp * hw[0], dp * hw[1], dp * hw[2], dp * hw[3]);
         } else {
-            gv = load4<GB>(g, r * ldg + gcoff + c0);
-            if constexpr (PA) gv = pool_add(pa, C, r, c0, gv);
+            if constexpr (PA) gv = pool_add(pa, C, r, c0, load4<GB>(g, r * ldg + gcoff + c0));
+            else gv = gb[u];
             if (gmul) {
                 const float4 m = gm_row ? *reinterpret_cast<const float4*>(gmul + (int64_t)fdiv(dHW, (uint32_t)r) * C + c0)
                                         : gm;
                 gv.x *= m.x; gv.y *= m.y; gv.z *= m.z; gv.w *= m.w;
             }
         }
-        const float4 yv = load4<YB>(y, r * C + c0);
+        const float4 yv = yb[u];
         const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, ya[4] = {yv.x, yv.y, yv.z, yv.w};
         float o[4];
 #pragma unroll
@@ -632,6 +661,7 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_rows(const float* __restric
         const float4 ov = make_float4(o[0], o[1], o[2], o[3]);
         if (dy) *reinterpret_cast<float4*>(dy + r * C + c0) = ov;
         if constexpr (NP > 0) split4_store<NP>(os, C, 0, r, c0, ov);
+      }
     }
 }
 // k_bn_relu_bwd_rows<NP, YB, false, GB, true> walked over pooled pixels (OpBnBwdPoolQ's order): the

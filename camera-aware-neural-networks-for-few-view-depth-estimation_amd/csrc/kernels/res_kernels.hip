@@ -293,6 +293,7 @@ __global__ void k_bn_add_relu(const float* __restrict__ y, const float* __restri
                               uint16_t* __restrict__ os, int64_t n4, uint8_t* __restrict__ mq = nullptr,
                               uint8_t* __restrict__ ms = nullptr, int64_t ldq = 0) {
     const int C4 = C >> 2;
+#pragma unroll 4
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = i / C4;
         const int c = (int)(i - r * C4) * 4;

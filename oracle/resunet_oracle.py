@@ -168,6 +168,17 @@ def _conv(x, w, stride, pad, name=None):
     return y + (forced.to(y.device, y.dtype) - y).detach()
 
 
+# Test hook: when a dict, the forward records each block's output here ("encoder.stem", "encoder.layer<L>.<i>",
+# "dec<l>"), for the full-size test's layer-by-layer comparison with cad_resunet_debug_buffer "out:<block>"
+TRACE = None
+
+
+def _trace(name, y):
+    if TRACE is not None:
+        TRACE[name] = y.detach().clone()
+    return y
+
+
 def _relu(z, name):
     """ReLU with the test hook cad_oracle.RELU_FORCE (the GPU run's decisions, keyed by the BN prefix or
     "<block>.out" for a bottleneck's relu(bn3 + shortcut))."""
@@ -188,12 +199,12 @@ def _bottleneck(x, p, bufs, pre, stride, down, train):
     t = O._bn(_conv(_rgrad(t), p[pre + "conv3.weight"], 1, 0, pre + "conv3"), p, bufs, pre + "bn3", train)
     sc = (O._bn(_conv(x, p[pre + "downsample.0.weight"], stride, 0, pre + "downsample.0"), p, bufs,
                 pre + "downsample.1", train) if down else x)
-    return _relu(t + sc, pre + "out")
+    return _trace(pre[:-1], _relu(t + sc, pre + "out"))
 
 
 def forward(x, p, bufs, train=True, max_depth=10.0):
-    x1 = _relu(O._bn(_conv(x, p["encoder.conv1.weight"], 2, 3, "encoder.conv1"), p, bufs, "encoder.bn1", train),
-               "encoder.bn1")
+    x1 = _trace("encoder.stem", _relu(O._bn(_conv(x, p["encoder.conv1.weight"], 2, 3, "encoder.conv1"), p, bufs,
+                                            "encoder.bn1", train), "encoder.bn1"))
     y = F.max_pool2d(x1, 3, 2, 1)
     feats = []
     for L, n in enumerate(NBLOCKS):
@@ -208,8 +219,8 @@ def forward(x, p, bufs, train=True, max_depth=10.0):
         y = torch.cat([skips[l], up], 1) if sk else up
         y = _relu(O._bn(_conv(y, p[pre + "conv.conv1.weight"], 1, 1, pre + "conv.conv1"), p, bufs, pre + "conv.bn1",
                         train), pre + "conv.bn1")
-        y = _relu(O._bn(_conv(_rgrad(y), p[pre + "conv.conv2.weight"], 1, 1, pre + "conv.conv2"), p, bufs,
-                        pre + "conv.bn2", train), pre + "conv.bn2")
+        y = _trace(f"dec{l}", _relu(O._bn(_conv(_rgrad(y), p[pre + "conv.conv2.weight"], 1, 1, pre + "conv.conv2"), p,
+                                          bufs, pre + "conv.bn2", train), pre + "conv.bn2"))
     z = F.conv2d(y, p["out_conv.weight"], p["out_conv.bias"])
     return torch.sigmoid(z) * max_depth
 

@@ -170,7 +170,10 @@ def test_film_train_step_vs_oracle(cad, dev, oracle, model, f, B, H, W):
     assert abs(loss5[0].item() - r["loss"]) <= 1e-4 * abs(r["loss"])
     grads = net.grads()
     for (n, _), g32, g64 in zip(oracle.param_spec(f, model=model), r["grads"], r64["grads"]):
-        if _zero_grad_bias(n, B):   # true gradient is 0: noise well below the weight-gradient scale
+        # true gradient is 0: noise well below the weight-gradient scale.  Also the bottleneck FiLM's
+        # beta bias when the bottleneck is 1 x 1 (16 x 16 inputs): conv2 then reduces to its centre tap,
+        # so sum_b dL/dA1[b] = W_c^T sum_b dL/dY2[b] = 0 (BN2's backward sums to zero over the batch)
+        if _zero_grad_bias(n, B) or (n == "bottleneck.conv.film.fc_beta.bias" and (H >> 4) * (W >> 4) == 1):
             w = grads[n[: -len("bias")] + "weight"]
             assert grads[n].abs().max().item() <= 1e-2 * w.abs().max().item() + 1e-12, n
             continue

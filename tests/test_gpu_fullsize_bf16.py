@@ -295,30 +295,38 @@ def resunet_units(B, H, W):
     return units, blocks
 
 
-def resunet_gpu_forcing(m, B, H, W, dev):
+def resunet_gpu_forcing(m, B, H, W, dev, params=None):
     """The GPU run's stored pre-BN outputs (bf16 values, NCHW on the host) and ReLU decisions of every
     ReLU of the config-5 network, keyed for cad_oracle.Y_FORCE / RELU_FORCE as resunet_oracle names them.
     A BN-ReLU decides fma(y, scale, shift) > 0 with the GPU's own coefficients (k_bn_relu_fwd / _bwd;
     the fp64 evaluation of that product and sum has the same sign), a bottleneck's relu(bn3 + shortcut)
     by its stored fp32 output (the backward's k_relu_mask / EpiStoreAddMask test the same)."""
     units, blocks = resunet_units(B, H, W)
-    yf, relu = {}, {}
+    yf, relu, coef = {}, {}, []
     for conv, bn, h, w, C, has_relu in units:
         y = m.debug_buffer("y:" + conv).reshape(B, h, w, C)
         yf[conv] = y.permute(0, 3, 1, 2).contiguous()
+        yd = y.to(dev).double()
+        sc = m.debug_buffer("scale:" + bn).to(dev).double()
+        sh = m.debug_buffer("shift:" + bn).to(dev).double()
         if has_relu:
-            yd = y.to(dev).double()
-            sc = m.debug_buffer("scale:" + bn).to(dev).double()
-            sh = m.debug_buffer("shift:" + bn).to(dev).double()
             relu[bn] = (yd * sc + sh > 0).permute(0, 3, 1, 2).contiguous().cpu()
-            del yd
-        del y
+        if params is not None:   # the GPU's BN coefficients against the batch statistics of its own stored y
+            flat = yd.reshape(-1, C)
+            inv = 1.0 / torch.sqrt(flat.var(0, unbiased=False) + 1e-5)
+            g_ = params[bn + ".weight"].to(dev).double()
+            scr = g_ * inv
+            shr = params[bn + ".bias"].to(dev).double() - flat.mean(0) * scr
+            coef.append((max(((sc - scr).abs().max() / scr.abs().max()).item(),
+                             ((sh - shr).abs().max() / shr.abs().max()).item()), bn))
+        del yd, y
     for blk, h, w, C in blocks:
         o = m.debug_buffer("out:" + blk).reshape(B, h, w, C)
         relu[blk + ".out"] = (o > 0).permute(0, 3, 1, 2).contiguous()
         del o
     torch.cuda.empty_cache()
-    return yf, relu
+    coef.sort(reverse=True)
+    return yf, relu, coef
 
 
 def conv_output_rows(yf, own, dev, skip=()):
@@ -376,7 +384,15 @@ def test_bs32_480x640_resunet_step_vs_oracle(cad, dev, oracle, beat, fp8):
     torch.cuda.synchronize()
     g = {"pred": pred.cpu(), "dpred": dpred.cpu(), "loss5": loss5.cpu().tolist()}
     g_grads = m.grads()
-    yf, relu = resunet_gpu_forcing(m, B, H, W, dev)
+    yf, relu, coef = resunet_gpu_forcing(m, B, H, W, dev, p)
+    # every block output of the GPU's forward, for the layer-by-layer comparison below
+    units_, blocks_ = resunet_units(B, H, W)
+    outs = {"encoder.stem": (m.debug_buffer("out:encoder.stem"), (H - 1) // 2 + 1, (W - 1) // 2 + 1, 64)}
+    for blk, h_, w_, C_ in blocks_:
+        outs[blk] = (m.debug_buffer("out:" + blk), h_, w_, C_)
+    for l, C_ in ((4, 512), (3, 256), (2, 128), (1, 64), (0, 32)):
+        outs[f"dec{l}"] = (m.debug_buffer(f"out:dec{l}"), H >> l, W >> l, C_)
+    beat(f"{tag}: GPU BN coefficients vs the statistics of its own stored outputs (max rel err, BN), worst: {coef[:4]}")
     m.clip_grad_norm_(1.0)
     m.adam_step(lr=LR, weight_decay=1e-5)
     torch.cuda.synchronize()
@@ -388,12 +404,21 @@ def test_bs32_480x640_resunet_step_vs_oracle(cad, dev, oracle, beat, fp8):
     ref = R.Trainer(p, b, WEIGHTS, operands="mx8" if fp8 else "bf16")
     oracle.Y_FORCE.update(yf)
     oracle.RELU_FORCE.update(relu)
+    R.TRACE = {}
     try:
         r = ref.step(rgb, gt, K)
     finally:
         oracle.Y_FORCE.clear()
         oracle.RELU_FORCE.clear()
+        trace, R.TRACE = R.TRACE, None
     del relu
+    lay = []
+    for n_, (buf, h_, w_, C_) in outs.items():
+        g_ = buf[: B * h_ * w_ * C_].reshape(B, h_, w_, C_).permute(0, 3, 1, 2)
+        lay.append((max_rel_err(g_, trace[n_]), n_))
+    del outs, trace
+    beat(f"{tag}: block outputs vs the oracle's under the imposed decisions (max rel err, block) in network order: "
+         f"{[(f'{e:.1e}', n_) for e, n_ in lay]}")
     beat(f"{tag}: oracle done (loss {r['loss']:.6f}, ours {g['loss5'][0]:.6f})")
     own = dict(oracle.Y_OWN)
     oracle.Y_OWN.clear()
@@ -416,8 +441,9 @@ def test_bs32_480x640_resunet_step_vs_oracle(cad, dev, oracle, beat, fp8):
          f"cosine {cos_all:.7f}")
     beat(f"{tag}: per-tensor gradients (1-cos, bulk, name), worst: {per[:6]}")
     worst_move = max((v - ref.p[n]).abs().max().item() for n, v in g_params.items())
-    e_bufs = max(max_rel_err(v, ref.bufs[n]) for n, v in g_bufs.items())
-    beat(f"{tag}: params after Adam max |diff| {worst_move:.3e}; BN running statistics {e_bufs:.2e}")
+    rbufs = sorted(((max_rel_err(v, ref.bufs[n]), n) for n, v in g_bufs.items()), reverse=True)
+    e_bufs = rbufs[0][0]
+    beat(f"{tag}: params after Adam max |diff| {worst_move:.3e}; BN running statistics, worst: {rbufs[:4]}")
     checks = [("conv outputs", not off, off[:6]),
               ("pred", b_pred < 1e-4 and e_pred < 1e-3, (b_pred, e_pred)),
               ("loss", e_loss < 1e-4, e_loss),

