@@ -1210,6 +1210,7 @@ int64_t cad_resunet_debug_buffer(cad_resunet* h, const char* name, float* host, 
             unit(d.u1, h->M(B, d.H, d.W));
             unit(d.u2, h->M(B, d.H, d.W));
             if (n == "out:dec" + std::to_string(d.l)) { p = d.out; cnt = h->M(B, d.H, d.W) * d.C; }
+            if (n == "cat:dec" + std::to_string(d.l)) { p = d.cats; bf16 = true; cnt = h->M(B, d.H, d.W) * (d.skipC + d.cout_up); }
         }
         need(p != nullptr, "unknown debug buffer '" + n + "'");
         if (!host) return;

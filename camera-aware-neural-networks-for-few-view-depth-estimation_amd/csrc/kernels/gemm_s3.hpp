@@ -183,35 +183,6 @@ __device__ __forceinline__ void s3_mfma(floatx16 (&acc)[MI][NJ], const bf16x8 (&
     }
 }
 
-// B1 (one product per k): the first k step of a tile, C = 0 as the MFMA's inline constant — no
-// accumulator zeroing (MI x NJ x 16 v_mov per lane and tile) ahead of the main loop
-template <int MI, int NJ>
-__device__ __forceinline__ void b1_mfma_first(floatx16 (&acc)[MI][NJ], const bf16x8 (&fa)[MI][1], const bf16x8 (&fb)[NJ][1]) {
-    const floatx16 zero = {};
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], zero, 0, 0, 0);
-}
-
-// ... with the operands swapped: block (i, j) accumulates C^T (rows = the B operand's columns), the
-// layout of the transposed-accumulator window epilogue (gemm_win.hpp win_epilogue_ta)
-template <int MI, int NJ>
-__device__ __forceinline__ void b1_mfma_first_t(floatx16 (&acc)[MI][NJ], const bf16x8 (&fa)[MI][1], const bf16x8 (&fb)[NJ][1]) {
-    const floatx16 zero = {};
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][0], fa[i][0], zero, 0, 0, 0);
-}
-template <int MI, int NJ>
-__device__ __forceinline__ void b1_mfma_t(floatx16 (&acc)[MI][NJ], const bf16x8 (&fa)[MI][1], const bf16x8 (&fb)[NJ][1]) {
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][0], fa[i][0], acc[i][j], 0, 0, 0);
-}
-
 // The S3/B1 engine for Kc x Kc operands (conv3x3 fwd/dgrad, ConvT fwd/dgrad).  Same tiling,
 // loaders, pipeline and epilogue as gemm_body (gemm_mfma.hpp); only the LDS image and the MFMA
 // differ.  AF32: A staged fp32 and split at fragment read (see s3_frag_f32); S3 with WN == 1 only.

@@ -371,180 +371,6 @@ __device__ __forceinline__ void win_epilogue16(const GemmArgs& a, const floatx4 
     if constexpr (BNS) bns.template finish<WM, WN>(a, lds, tile_lin, n0);
 }
 
-// ------------------------------------------------------------------------------------------------
-// Transposed-accumulator window epilogue (round 6, CAD_WIN_TA): the bf16 window body issues its MFMAs
-// with the operands swapped (weights as the matrix A, the pixel window as B), so each 32 x 32 block
-// holds C^T: register 4g + q of lane l is channel 8g + 4(l >> 5) + q of the block's 32, pixel l & 31.
-// A lane then holds four CONSECUTIVE channels of one pixel per g: bf16 outputs pack to 8 B, and one
-// v_permlane32_swap per dword pair (g, g + 1) gives each lane 16 contiguous bytes (lanes 0-31 channels
-// 8g .. 8g + 7, lanes 32-63 8g + 8 .. 8g + 15 of the same pixel): one dwordx4 store per 8 outputs
-// instead of one 2-byte store per output (cdna_hip_programming.md T21).  fp32 outputs: one dwordx4 per
-// 4 channels.  BN partials: per channel a wave-common shift (lane 0's / 32's value of pixel block 0),
-// shifted sums over the lane's pixels, summed over the half-wave's 32 lanes (xor butterfly), then the
-// waves merged in Chan form as BnTilePartials::finish does — the same per-tile (sum, M2, n) rows.
-// ------------------------------------------------------------------------------------------------
-#ifndef CAD_WIN_TA
-#define CAD_WIN_TA 0
-#endif
-template <class Epi>
-constexpr bool win_ta_ok() {
-    if constexpr (is_bnsums<Epi>::value) return false;
-    else return CAD_WIN_TA != 0;
-}
-typedef unsigned int ta_u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
-    return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)lo) | ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)hi) << 16);
-}
-template <int WM, int WN, int MI, int NJ, int CW, class Epi>
-__device__ __forceinline__ void win_epilogue_ta(const GemmArgs& a, const floatx16 (&acc)[MI][NJ], int tile_lin, int n0,
-                                                int b, int y0, int x0, float* lds) {
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hh = lane >> 5, t = lane & 31;
-    const int wm = wave / WN, wn = wave % WN;
-    constexpr int ES = Epi::BF16 ? 2 : 4;
-    const int64_t ldcb = a.ldc * ES;
-    const int64_t pix0 = ((int64_t)b * a.H + y0) * a.W + x0;
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const float*>(
-        reinterpret_cast<const char*>(a.C) + (pix0 * a.ldc + a.c_coff) * ES));
-    [[maybe_unused]] __amdgpu_buffer_rsrc_t rs2;
-    [[maybe_unused]] int64_t ldc2b = 0;
-    if constexpr (Epi::SPLIT) {
-        ldc2b = a.ldc2 * 2;
-        rs2 = make_rsrc(reinterpret_cast<const float*>(static_cast<const char*>(a.C2) + pix0 * ldc2b));
-    }
-    const int nw = n0 + wn * 32 * NJ;   // the wave's first output column
-    // BN partials
-    [[maybe_unused]] float shv[NJ][16], d1[NJ][16], d2[NJ][16];
-    [[maybe_unused]] float cnt = 0.f;
-    if constexpr (Epi::STATS) {
-        // the common shift of each channel: its value at lane 0 (channels 4q of the lower half) or lane
-        // 32 (upper half) in pixel block 0 — any value of the channel keeps the shifted sums well scaled
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float v0 = Epi::BF16 ? (float)(__bf16)acc[0][j][r] : acc[0][j][r];
-                const float lo = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v0), 0));
-                const float up = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v0), 32));
-                shv[j][r] = hh ? up : lo;
-                d1[j][r] = 0.f;
-                d2[j][r] = 0.f;
-            }
-    }
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-        const int mr = wm * 32 * MI + i * 32 + t;
-        const int r = mr / CW, c = mr - r * CW;
-        const bool ok = y0 + r < a.H;
-        const int64_t prow = r * (int64_t)a.W + c;
-        if constexpr (Epi::STATS) cnt += ok ? 1.f : 0.f;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int nb = nw + j * 32;   // block's first column (uniform)
-            float v[16];
-#pragma unroll
-            for (int r2 = 0; r2 < 16; ++r2) v[r2] = Epi::BF16 ? (float)(__bf16)acc[i][j][r2] : acc[i][j][r2];
-            if constexpr (Epi::STATS) {
-#pragma unroll
-                for (int r2 = 0; r2 < 16; ++r2) {
-                    const float d = ok ? v[r2] - shv[j][r2] : 0.f;
-                    d1[j][r2] += d;
-                    d2[j][r2] = fmaf(d, d, d2[j][r2]);
-                }
-            }
-            if (nb >= a.N) continue;
-            const bool to2 = Epi::SPLIT && nb >= a.split_n;   // uniform per 32-column block
-            if (Epi::BF16 || to2) {
-                uint2 u[4];
-#pragma unroll
-                for (int g = 0; g < 4; ++g) u[g] = make_uint2(pack_bf16x2(v[4 * g], v[4 * g + 1]), pack_bf16x2(v[4 * g + 2], v[4 * g + 3]));
-#pragma unroll
-                for (int g = 0; g < 4; g += 2) {
-                    const auto sx = __builtin_amdgcn_permlane32_swap(u[g].x, u[g + 1].x, false, false);
-                    const auto sy = __builtin_amdgcn_permlane32_swap(u[g].y, u[g + 1].y, false, false);
-                    const ta_u32x4 q4 = {sx[0], sy[0], sx[1], sy[1]};
-                    const int col = nb + 8 * g + 8 * hh;
-                    if (to2) {
-                        const uint32_t off = ok ? (uint32_t)(prow * ldc2b + (int64_t)(col - a.split_n) * 2) : kOOB;
-                        __builtin_amdgcn_raw_buffer_store_b128(q4, rs2, off, 0, 0);
-                    } else {
-                        const uint32_t off = ok ? (uint32_t)(prow * ldcb + (int64_t)col * 2) : kOOB;
-                        __builtin_amdgcn_raw_buffer_store_b128(q4, rs, off, 0, 0);
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const int col = nb + 8 * g + 4 * hh;
-                    const uint32_t off = ok ? (uint32_t)(prow * ldcb + (int64_t)col * 4) : kOOB;
-                    const ta_u32x4 q4 = {__float_as_uint(v[4 * g]), __float_as_uint(v[4 * g + 1]), __float_as_uint(v[4 * g + 2]),
-                                         __float_as_uint(v[4 * g + 3])};
-                    __builtin_amdgcn_raw_buffer_store_b128(q4, rs, off, 0, 0);
-                }
-            }
-        }
-    }
-    if constexpr (Epi::STATS) {
-        constexpr int BN = 32 * NJ * WN;
-        // the half-wave's 32 lanes summed by a transposing butterfly per block column j: at each level a
-        // lane keeps half of its values and adds its partner's copy of that half (16 + 8 + 4 + 2 + 1
-        // shuffles for the 32 values (sum, sum of squares) x 16 channels); lane t then holds value
-        // rev5(t), i.e. the sum (t < 16) or the sum of squares (t >= 16) of channel rev4(t & 15)
-#pragma unroll
-        for (int x = 1; x < 32; x *= 2) cnt += __shfl_xor(cnt, x);
-        const int rv = (int)(__builtin_bitreverse32((uint32_t)t) >> 27);   // rev5(t)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            float x[32];
-#pragma unroll
-            for (int r2 = 0; r2 < 16; ++r2) { x[2 * r2] = d1[j][r2]; x[2 * r2 + 1] = d2[j][r2]; }
-#pragma unroll
-            for (int lvl = 0; lvl < 5; ++lvl) {
-                const int sx = 1 << lvl, half = 16 >> lvl;
-                const bool upper = (t & sx) != 0;
-#pragma unroll
-                for (int k = 0; k < half; ++k) {
-                    const float send = upper ? x[k] : x[k + half];
-                    const float keep = upper ? x[k + half] : x[k];
-                    x[k] = keep + __shfl_xor(send, sx);
-                }
-            }
-            const float other = __shfl_xor(x[0], 16);
-            if (t < 16) {
-                const int r2 = rv >> 1;   // channel 8 (r2 >> 2) + 4 hh + (r2 & 3) of block j
-                const float s1 = x[0], s2 = other;
-                // the lane's shift for channel r2 (uniform over the half: lane 0's / 32's value)
-                float shift = 0.f;
-#pragma unroll
-                for (int k = 0; k < 16; ++k) shift = k == r2 ? shv[j][k] : shift;
-                float n = cnt, mean = 0.f, m2 = 0.f;
-                if (n > 0.f) {
-                    const float qd = s1 / n;
-                    mean = shift + qd;
-                    m2 = fmaxf(s2 - s1 * qd, 0.f);
-                }
-                const int col = wn * 32 * NJ + j * 32 + 8 * (r2 >> 2) + 4 * hh + (r2 & 3);
-                float* rr = lds + (wm * BN + col) * 3;
-                rr[0] = n; rr[1] = mean; rr[2] = m2;
-            }
-        }
-        __syncthreads();
-        for (int c = tid; c < BN; c += 256) {
-            float n = 0.f, mean = 0.f, m2 = 0.f;
-#pragma unroll
-            for (int w = 0; w < WM; ++w) {
-                const float* rr = lds + (w * BN + c) * 3;
-                chan_merge(n, mean, m2, rr[0], rr[1], rr[2]);
-            }
-            const int nn = n0 + c;
-            if (nn < a.N) {
-                a.stats[(int64_t)tile_lin * 2 * a.N + nn] = n * mean;
-                a.stats[(int64_t)tile_lin * 2 * a.N + a.N + nn] = m2;
-            }
-            if (n0 == 0 && c == 0) a.stats[(int64_t)gridDim.x * 2 * a.N + tile_lin] = n;
-        }
-    }
-}
-
 // blocks: gridDim.x = B * ceil(H / R) * (W / CW) output blocks (XCD-aware order), gridDim.y = N tiles
 template <int NP, int R, int CW, int WM, int WN, class Epi>
 __device__ __forceinline__ void conv3x3_win_body(const GemmArgs& a) {
@@ -677,7 +503,6 @@ __device__ __forceinline__ void conv3x3_win_ps_body(const GemmArgs& a) {
     constexpr int BM = 32 * MI * WM, BN = 32 * NJ * WN;
     static_assert(BM == R * CW, "tile");
     using G = WinPsGeo<R, CW, BN>;
-    constexpr bool TA = !M16 && win_ta_ok<Epi>();
     __shared__ __attribute__((aligned(16))) uint16_t lds[G::SA + 3 * G::SBT];
 
     const int tid = threadIdx.x;
@@ -742,8 +567,8 @@ __device__ __forceinline__ void conv3x3_win_ps_body(const GemmArgs& a) {
         for (int i = 0; i < 2 * MI; ++i)
 #pragma unroll
             for (int j = 0; j < 2 * NJ; ++j) acc4[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    } else if (S == 0) {
-        acc_zero(acc);   // (never on the host's shapes: cin >= 32; the main loop's first step writes acc)
+    } else {
+        acc_zero(acc);
     }
     uint4 ra[G::NVA], rb[3 * G::JB];
     int cb = 0, ky = 0;
@@ -775,8 +600,7 @@ __device__ __forceinline__ void conv3x3_win_ps_body(const GemmArgs& a) {
             for (int jj = 0; jj < G::JB; ++jj)
                 if (bact(jj)) *reinterpret_cast<uint4*>(lds + G::SA + t * G::SBT + blds0 + 64 * jj * G::LDK) = rb[t * G::JB + jj];
     };
-    auto compute = [&](auto first_stage) {
-        constexpr bool FIRST = decltype(first_stage)::value;
+    auto compute = [&]() {
         if constexpr (M16) {
 #pragma unroll
             for (int kx = 0; kx < 3; ++kx) {
@@ -812,13 +636,7 @@ __device__ __forceinline__ void conv3x3_win_ps_body(const GemmArgs& a) {
             for (int t = 0; t < 6; ++t) {
                 if (t + 1 < 6) rd(t + 1, (t + 1) & 1);
                 __builtin_amdgcn_sched_barrier(0);
-                if constexpr (TA) {   // C^T blocks: weights as the matrix A (win_epilogue_ta)
-                    if (FIRST && t == 0) b1_mfma_first_t(acc, fa[0], fb[0]);
-                    else b1_mfma_t(acc, fa[t & 1], fb[t & 1]);
-                } else {
-                    if (FIRST && t == 0) b1_mfma_first(acc, fa[0], fb[0]);
-                    else s3_mfma<1>(acc, fa[t & 1], fb[t & 1]);
-                }
+                s3_mfma<1>(acc, fa[t & 1], fb[t & 1]);
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -832,8 +650,7 @@ __device__ __forceinline__ void conv3x3_win_ps_body(const GemmArgs& a) {
     for (int s = 0; s < S; ++s) {
         const bool more = s + 1 < S;
         if (more) load();
-        if (M16 || s > 0) compute(std::false_type{});
-        else compute(std::true_type{});
+        compute();
         __syncthreads();
         if (more) {
             store();
@@ -842,8 +659,6 @@ __device__ __forceinline__ void conv3x3_win_ps_body(const GemmArgs& a) {
     }
     if constexpr (M16)
         win_epilogue16<WM, WN, 2 * MI, 2 * NJ, CW, Epi>(a, acc4, tile.x, n0, b, y0, x0, reinterpret_cast<float*>(lds));
-    else if constexpr (TA)
-        win_epilogue_ta<WM, WN, MI, NJ, CW, Epi>(a, acc, tile.x, n0, b, y0, x0, reinterpret_cast<float*>(lds));
     else
         win_epilogue<WM, WN, MI, NJ, CW, Epi>(a, acc, tile.x, n0, b, y0, x0, reinterpret_cast<float*>(lds));
 }

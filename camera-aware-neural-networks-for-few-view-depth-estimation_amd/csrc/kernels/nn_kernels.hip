@@ -60,9 +60,6 @@ __global__ void k_colreduce(Op op, int64_t R, int C, int64_t rows_per_slice, dou
         for (int e = 0; e < 4; ++e) acc[o][e] = 0.0;
     if (c4 < C4) {
         const auto pc = prep_of(op, c4, r0, r1);   // per-thread channel coefficients, loaded once
-        // unrolled: the loads of four rows in flight together (one per iteration left the pass
-        // latency-bound: 0.90 of wave-cycles parked); the adds stay in row order (the same sums)
-#pragma unroll 4
         for (int64_t r = r0 + threadIdx.y; r < r1; r += RY) op(r, c4, acc, pc);
     }
     extern __shared__ double red[];   // [RY][CX][NOUT*4]
@@ -619,19 +616,21 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_rows(const float* __restric
         if (!gm_row) gm = *reinterpret_cast<const float4*>(gmul + (int64_t)s0 * C + c0);
     }
     const int RY = blockDim.y;
-    // four rows per pass of the loop: their g / y loads issued together (one row per iteration left
-    // the pass latency-bound, 0.90 of wave-cycles parked); rows keep their per-thread order
-    for (int64_t rb = r0 + threadIdx.y; rb < r1; rb += 4 * RY) {
-      float4 gb[4], yb[4];
+    // U rows per pass of the loop: their g / y loads issued together (one row per iteration left the
+    // pass latency-bound, 0.90 of wave-cycles parked; round 6: -6 % on the plain form, +18 % on the
+    // head-gradient form, which loads y only); rows keep their per-thread order
+    constexpr int U = HG ? 1 : 4;
+    for (int64_t rb = r0 + threadIdx.y; rb < r1; rb += U * RY) {
+      float4 gb[U], yb[U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int64_t r = rb + u * RY;
         if (r >= r1) break;
         if constexpr (!HG && !PA) gb[u] = load4<GB>(g, r * ldg + gcoff + c0);
         yb[u] = load4<YB>(y, r * C + c0);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int64_t r = rb + u * RY;
         if (r >= r1) break;
         float4 gv;

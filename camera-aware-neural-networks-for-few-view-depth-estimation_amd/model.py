@@ -707,7 +707,7 @@ class ResNetUNet:
     def debug_buffer(self, name: str) -> torch.Tensor:
         """Test hook: a buffer of the last train-mode forward as fp32 NHWC rows (cad_resunet_debug_buffer:
         "y:<conv>" stored pre-BN outputs, "scale:<bn>" / "shift:<bn>" BN-apply coefficients, "out:<block>"
-        block outputs)."""
+        block outputs, "cat:dec<l>" a decoder's bf16 input [skip, up])."""
         n = int(self._f("debug_buffer")(self.h, name.encode(), None, 0))
         if n < 0:
             raise KeyError(name)

@@ -517,7 +517,8 @@ cad_status cad_resunet_backward(cad_resunet* h, const float* ddepth, void* strea
  * semantics: SUM buckets of >= bucket_elems floats on the communicator's stream) */
 /* Test hook: a buffer of the last train-mode forward as fp32 rows — "y:<conv>" (stored pre-BN output,
    bf16 widened), "scale:<bn>" / "shift:<bn>" (BN-apply coefficients), "out:<block>" (block output:
-   "encoder.layer<L>.<i>", "encoder.stem", "dec<l>").  Returns the element count, -1 if unknown. */
+   "encoder.layer<L>.<i>", "encoder.stem", "dec<l>"), "cat:dec<l>" (a decoder's bf16 input [skip, up]).
+   Returns the element count, -1 if unknown. */
 int64_t cad_resunet_debug_buffer(cad_resunet* h, const char* name, float* host, int64_t numel);
 int cad_resunet_num_stages(const cad_resunet* h);
 /* host only (no device): the stage count (23) and each stage's [offset, offset+count), as

@@ -165,18 +165,36 @@ def _conv(x, w, stride, pad, name=None):
     if forced is None:
         return y
     O.Y_OWN[name] = y.detach().clone()
-    return y + (forced.to(y.device, y.dtype) - y).detach()
+    return _impose(y, forced)
 
 
-# Test hook: when a dict, the forward records each block's output here ("encoder.stem", "encoder.layer<L>.<i>",
-# "dec<l>"), for the full-size test's layer-by-layer comparison with cad_resunet_debug_buffer "out:<block>"
+# Test hooks of the full-size test, which imposes the GPU run's forward values so that every convolution
+# of this restatement reads operands bit-identical to the GPU's (an fp32 ulp of a BN coefficient or of an
+# accumulation order flips the bf16 rounding of ~1e-4 of an activation, and behind the MX-fp8 quantiser
+# such a flip moves a product by 2^-4..2^-3 of itself: round 6 measured up to 481 bf16 ulps on 2-5% of a
+# decoder convolution's outputs without these hooks).  The backward still runs through this
+# restatement's own graph (straight-through, as cad_oracle.Y_FORCE).
+#   TRACE      when a dict, records each block's own output ("encoder.stem", "encoder.layer<L>.<i>", "dec<l>")
+#   OUT_FORCE  {block name: the GPU's fp32 block output (NCHW)} (cad_resunet_debug_buffer "out:<block>")
+#   COEF_FORCE {BN prefix: (scale, shift)} of a BN-ReLU: z = fma(y, scale, shift) rounded once to fp32
+#              (k_bn_relu_fwd), "scale:/shift:<bn>"
+#   CAT_FORCE  {"dec<l>": the decoder's bf16 input [skip, up] (NCHW)} ("cat:dec<l>": the ConvT output
+#              as the GPU stored it)
 TRACE = None
+OUT_FORCE = {}
+COEF_FORCE = {}
+CAT_FORCE = {}
+
+
+def _impose(y, forced):
+    # forced + (y - y) carries y's gradient and the forced value exactly (y + (forced - y) rounds twice)
+    return y if forced is None else forced.to(y.device, y.dtype) + (y - y.detach())
 
 
 def _trace(name, y):
-    if TRACE is not None:
+    if TRACE is not None:   # this restatement's own value, before OUT_FORCE
         TRACE[name] = y.detach().clone()
-    return y
+    return _impose(y, OUT_FORCE.get(name))
 
 
 def _relu(z, name):
@@ -186,6 +204,16 @@ def _relu(z, name):
     return F.relu(z) if m is None else z * m.to(z.device, z.dtype)
 
 
+def _bn_relu(y, p, bufs, name, train):
+    """BatchNorm2d + ReLU with the test hooks COEF_FORCE and cad_oracle.RELU_FORCE"""
+    z = O._bn(y, p, bufs, name, train)
+    cf = COEF_FORCE.get(name)
+    if cf is not None:
+        sc, sh = (t.to(y.device, torch.float64).view(1, -1, 1, 1) for t in cf)
+        z = _impose(z, (y.detach().double() * sc + sh).to(y.dtype))
+    return _relu(z, name)
+
+
 def _rgrad(x):
     """bf16 / mx8: the input gradient of this convolution stored as bf16 (resunet.cpp unit_bwd dx_bf16:
     a bottleneck's conv3 and stride-1 conv2, a decoder's conv2 — read only by the BN backward below)"""
@@ -193,9 +221,9 @@ def _rgrad(x):
 
 
 def _bottleneck(x, p, bufs, pre, stride, down, train):
-    t = _relu(O._bn(_conv(x, p[pre + "conv1.weight"], 1, 0, pre + "conv1"), p, bufs, pre + "bn1", train), pre + "bn1")
-    t = _relu(O._bn(_conv(_rgrad(t) if stride == 1 else t, p[pre + "conv2.weight"], stride, 1, pre + "conv2"), p, bufs,
-                    pre + "bn2", train), pre + "bn2")
+    t = _bn_relu(_conv(x, p[pre + "conv1.weight"], 1, 0, pre + "conv1"), p, bufs, pre + "bn1", train)
+    t = _bn_relu(_conv(_rgrad(t) if stride == 1 else t, p[pre + "conv2.weight"], stride, 1, pre + "conv2"), p, bufs,
+                 pre + "bn2", train)
     t = O._bn(_conv(_rgrad(t), p[pre + "conv3.weight"], 1, 0, pre + "conv3"), p, bufs, pre + "bn3", train)
     sc = (O._bn(_conv(x, p[pre + "downsample.0.weight"], stride, 0, pre + "downsample.0"), p, bufs,
                 pre + "downsample.1", train) if down else x)
@@ -203,8 +231,8 @@ def _bottleneck(x, p, bufs, pre, stride, down, train):
 
 
 def forward(x, p, bufs, train=True, max_depth=10.0):
-    x1 = _trace("encoder.stem", _relu(O._bn(_conv(x, p["encoder.conv1.weight"], 2, 3, "encoder.conv1"), p, bufs,
-                                            "encoder.bn1", train), "encoder.bn1"))
+    x1 = _trace("encoder.stem", _bn_relu(_conv(x, p["encoder.conv1.weight"], 2, 3, "encoder.conv1"), p, bufs,
+                                         "encoder.bn1", train))
     y = F.max_pool2d(x1, 3, 2, 1)
     feats = []
     for L, n in enumerate(NBLOCKS):
@@ -216,11 +244,10 @@ def forward(x, p, bufs, train=True, max_depth=10.0):
         pre = f"dec{l}."
         # (bias_bf16: the bias gradient sums the bf16 up-half gradient the ConvT GEMMs read, as resunet.cpp)
         up = O._convT2x2(y, p[pre + "up.weight"], p[pre + "up.bias"], bias_bf16=True)
-        y = torch.cat([skips[l], up], 1) if sk else up
-        y = _relu(O._bn(_conv(y, p[pre + "conv.conv1.weight"], 1, 1, pre + "conv.conv1"), p, bufs, pre + "conv.bn1",
-                        train), pre + "conv.bn1")
-        y = _trace(f"dec{l}", _relu(O._bn(_conv(_rgrad(y), p[pre + "conv.conv2.weight"], 1, 1, pre + "conv.conv2"), p,
-                                          bufs, pre + "conv.bn2", train), pre + "conv.bn2"))
+        y = _impose(torch.cat([skips[l], up], 1) if sk else up, CAT_FORCE.get(f"dec{l}"))
+        y = _bn_relu(_conv(y, p[pre + "conv.conv1.weight"], 1, 1, pre + "conv.conv1"), p, bufs, pre + "conv.bn1", train)
+        y = _trace(f"dec{l}", _bn_relu(_conv(_rgrad(y), p[pre + "conv.conv2.weight"], 1, 1, pre + "conv.conv2"), p,
+                                       bufs, pre + "conv.bn2", train))
     z = F.conv2d(y, p["out_conv.weight"], p["out_conv.bias"])
     return torch.sigmoid(z) * max_depth
 

@@ -62,3 +62,64 @@ def test_mx8_emulation_and_eligibility():
     t8 = R.Trainer(p, b, operands="mx8").predict_eval(x)
     e = ((t8 - t16).abs().max() / t16.abs().max()).item()
     assert 1e-6 < e < 0.2, e   # fp8 changes the result, boundedly
+
+
+def test_convT_bias_gradient_from_bf16_operand():
+    """The U-Net family's ConvT bias gradient sums the bf16-rounded up-half gradient the ConvT GEMMs read
+    (resunet.cpp colsum_bf16 over dup; cad_oracle._convT2x2 bias_bf16).  Against the fp64 sum of the
+    unrounded gradient the error per channel is at most 2^-9 * sum |g| (round-to-nearest-even to bf16,
+    relative error <= 2^-9 per term), and this records how large it is relative to the bias gradient
+    itself on a random-sign gradient (where the sum cancels)."""
+    from oracle import cad_oracle as O
+    gen = torch.Generator().manual_seed(7)
+    x = torch.randn(2, 16, 12, 10, generator=gen, dtype=torch.float64)
+    w = torch.randn(16, 8, 2, 2, generator=gen, dtype=torch.float64) * 0.1
+    g = torch.randn(2, 8, 24, 20, generator=gen, dtype=torch.float64)
+    prev, O._GEMM["operands"] = O._GEMM["operands"], "bf16"
+    try:
+        grads = []
+        for flag in (True, False):
+            b = torch.zeros(8, dtype=torch.float64, requires_grad=True)
+            (O._convT2x2(x, w, b, bias_bf16=flag) * g).sum().backward()
+            grads.append(b.grad)
+    finally:
+        O._GEMM["operands"] = prev
+    g16, g64 = grads
+    assert torch.equal(g64, g.sum((0, 2, 3)))
+    bound = 2.0 ** -9 * g.abs().sum((0, 2, 3))
+    assert bool(((g16 - g64).abs() <= bound).all()), ((g16 - g64).abs() / bound).max()
+    # recorded: relative to |sum g| the error is ~2^-9 * sqrt(n) / |mean-free sum| — at most a few 1e-3
+    # here (960 terms per channel), the size of the per-tensor 1-cos the full-size tests see on up.bias
+    rel = ((g16 - g64).abs() / g64.abs()).max().item()
+    assert rel < 2e-2, rel
+
+
+def test_forcing_hooks_with_own_values_are_identity():
+    """The full-size test's hooks (OUT_FORCE, COEF_FORCE, CAT_FORCE, cad_oracle.Y_FORCE / RELU_FORCE):
+    imposing this restatement's own forward values reproduces its step bit for bit (the straight-through
+    form forced + (y - y) carries the value exactly and the gradient unchanged)."""
+    from oracle import cad_oracle as O
+    p, b = R.init(seed=3)
+    B, H, W = 1, 64, 64
+    rgb, gt, K = [torch.from_numpy(a) for a in O.synth_batch(B, H, W)]
+    r0 = R.Trainer(p, b, operands="bf16").step(rgb, gt, K)
+    R.TRACE = {}
+    try:
+        R.Trainer(p, b, operands="bf16").step(rgb, gt, K)
+        own = R.TRACE
+    finally:
+        R.TRACE = None
+    R.CAT_FORCE.update({"dec0": torch.zeros(B, 32, H, W)})   # a forced decoder input must change the step
+    try:
+        r1 = R.Trainer(p, b, operands="bf16").step(rgb, gt, K)
+    finally:
+        R.CAT_FORCE.clear()
+    assert not torch.equal(r0["pred"], r1["pred"])
+    R.OUT_FORCE.update(own)
+    try:
+        r2 = R.Trainer(p, b, operands="bf16").step(rgb, gt, K)
+    finally:
+        R.OUT_FORCE.clear()
+    assert torch.equal(r0["pred"], r2["pred"]) and r0["loss"] == r2["loss"]
+    for g0, g2 in zip(r0["grads"], r2["grads"]):
+        assert torch.equal(g0, g2)
