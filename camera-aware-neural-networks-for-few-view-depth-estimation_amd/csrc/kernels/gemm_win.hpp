@@ -197,9 +197,6 @@ constexpr bool epi_y_bf16() {
     else return false;
 }
 
-#ifndef CAD_WIN_FASTEPI
-#define CAD_WIN_FASTEPI 1
-#endif
 template <int WM, int WN, int MI, int NJ, int CW, class Epi>
 __device__ __forceinline__ void win_epilogue(const GemmArgs& a, const floatx16 (&acc)[MI][NJ], int tile_lin, int n0,
                                              int b, int y0, int x0, float* lds) {
@@ -239,140 +236,6 @@ __device__ __forceinline__ void win_epilogue(const GemmArgs& a, const floatx16 (
         ldc2b = a.ldc2 * 2;
         rs2 = make_rsrc(reinterpret_cast<const float*>(static_cast<const char*>(a.C2) +
                                                        (((int64_t)b * a.H + y0) * a.W + x0) * ldc2b));
-    }
-    // Whole tiles (every row inside the image; N % BN == 0 is a host requirement): two outputs per bf16
-    // conversion, the wave-uniform row step q ldc in the store's scalar offset, and the statistics of
-    // the column pairs (j, j + 1) of a lane accumulated as fp32 pairs (v_pk_add / v_pk_fma: the same
-    // IEEE operations on each component, in the same (i, g, q) order per column, so the same sums) with
-    // the row count the constant 16 MI instead of a per-element select.  The epilogue outweighs the
-    // level-0 tiles' 6-stage main loop (round 6 ISA count, <4,128,Stats>: 1132 VALU after the loop
-    // against 48 per stage; this path 639)
-    if constexpr (CAD_WIN_FASTEPI && !BNS && !Epi::STATS && (CAD_XP_WIN & 2) == 0) {
-        if (y0 + (32 * MI * WM) / CW <= a.H) {
-            // no statistics: column block j outermost, its destination (C, or C2 past split_n) chosen once
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                const int nb = n0 + wn * 32 * NJ + j * 32;   // uniform
-                // (byte offsets inside the tile's descriptor window: 32-bit arithmetic, the values the
-                // 64-bit form truncates to)
-                bool b16 = Epi::BF16;
-                __amdgpu_buffer_rsrc_t rse = rs;
-                uint32_t step = (uint32_t)ldc4, col = (uint32_t)(nb + (lane & 31)) * ES;
-                if constexpr (Epi::SPLIT) {
-                    if (nb >= a.split_n) {
-                        b16 = true;
-                        rse = rs2;
-                        step = (uint32_t)ldc2b;
-                        col = (uint32_t)(nb - a.split_n + (lane & 31)) * 2;
-                    }
-                }
-#pragma unroll
-                for (int i = 0; i < MI; ++i)
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        const int mr = wm * 32 * MI + i * 32 + 4 * (lane >> 5) + 8 * g;
-                        const int r = mr / CW, c = mr - r * CW;
-                        const uint32_t lo = (uint32_t)(r * a.W + c) * step + col;
-                        if (b16) {
-#pragma unroll
-                            for (int q = 0; q < 4; q += 2) {
-                                const uint32_t u = __builtin_bit_cast(uint32_t, __builtin_convertvector(
-                                    (f32x2_t){acc[i][j][4 * g + q], acc[i][j][4 * g + q + 1]}, bf16x2_t));
-                                if constexpr ((CAD_XP_WIN & 1) == 0) {
-                                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)u, rse, lo + (uint32_t)(q * step), 0, 0);
-                                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(u >> 16), rse,
-                                                                          lo + (uint32_t)((q + 1) * step), 0, 0);
-                                }
-                            }
-                        } else {
-#pragma unroll
-                            for (int q = 0; q < 4; ++q) {
-                                // (through a scalar: __builtin_bit_cast of the vector-element lvalue itself
-                                // read element 0 for every q — hipcc 7.2 codegen, seen in the ISA)
-                                const float vq = acc[i][j][4 * g + q];
-                                if constexpr ((CAD_XP_WIN & 1) == 0)
-                                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vq), rse,
-                                                                          lo + (uint32_t)(q * step), 0, 0);
-                            }
-                        }
-                    }
-            }
-            return;
-        }
-    }
-    if constexpr (CAD_WIN_FASTEPI && !BNS && Epi::STATS && !Epi::SPLIT && NJ % 2 == 0 && (CAD_XP_WIN & 2) == 0) {
-        if (y0 + (32 * MI * WM) / CW <= a.H) {
-            typedef float f2 __attribute__((ext_vector_type(2)));
-            [[maybe_unused]] f2 sh2[NJ / 2], s1[NJ / 2], s2[NJ / 2];
-            if constexpr (Epi::STATS) {
-#pragma unroll
-                for (int jp = 0; jp < NJ / 2; ++jp) {
-                    sh2[jp] = f2{bnp.sh[2 * jp], bnp.sh[2 * jp + 1]};
-                    s1[jp] = f2{0.f, 0.f};
-                    s2[jp] = f2{0.f, 0.f};
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < MI; ++i)
-#pragma unroll
-                for (int jp = 0; jp < NJ / 2; ++jp)
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        const int mr = wm * 32 * MI + i * 32 + 4 * (lane >> 5) + 8 * g;
-                        const int r = mr / CW, c = mr - r * CW;
-                        [[maybe_unused]] float v[2][4];
-#pragma unroll
-                        for (int e = 0; e < 2; ++e) {
-                            const int nb = n0 + wn * 32 * NJ + (2 * jp + e) * 32;   // uniform per 32-column block
-                            const bool b16 = Epi::BF16;
-                            const __amdgpu_buffer_rsrc_t rse = rs;
-                            const uint32_t step = (uint32_t)ldc4;
-                            const uint32_t lo = (uint32_t)(r * a.W + c) * step + (uint32_t)(nb + (lane & 31)) * ES;
-                            if (b16) {
-#pragma unroll
-                                for (int q = 0; q < 4; q += 2) {
-                                    const uint32_t u = __builtin_bit_cast(uint32_t, __builtin_convertvector(
-                                        (f32x2_t){acc[i][2 * jp + e][4 * g + q], acc[i][2 * jp + e][4 * g + q + 1]}, bf16x2_t));
-                                    v[e][q] = __uint_as_float(u << 16);   // the stored values, which BN normalises
-                                    v[e][q + 1] = __uint_as_float(u & 0xFFFF0000u);
-                                    if constexpr ((CAD_XP_WIN & 1) == 0) {
-                                        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)u, rse, lo + (uint32_t)(q * step), 0, 0);
-                                        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(u >> 16), rse,
-                                                                              lo + (uint32_t)((q + 1) * step), 0, 0);
-                                    }
-                                }
-                            } else {
-#pragma unroll
-                                for (int q = 0; q < 4; ++q) {
-                                    v[e][q] = acc[i][2 * jp + e][4 * g + q];
-                                    if constexpr ((CAD_XP_WIN & 1) == 0)
-                                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[e][q]), rse,
-                                                                              lo + (uint32_t)(q * step), 0, 0);
-                                }
-                            }
-                        }
-                        if constexpr (Epi::STATS) {
-#pragma unroll
-                            for (int q = 0; q < 4; ++q) {
-                                const f2 d = f2{v[0][q], v[1][q]} - sh2[jp];
-                                s1[jp] += d;
-                                s2[jp] = __builtin_elementwise_fma(d, d, s2[jp]);
-                            }
-                        }
-                    }
-            if constexpr (Epi::STATS) {
-#pragma unroll
-                for (int jp = 0; jp < NJ / 2; ++jp) {
-                    bnp.d1[2 * jp] = s1[jp].x;
-                    bnp.d1[2 * jp + 1] = s1[jp].y;
-                    bnp.d2[2 * jp] = s2[jp].x;
-                    bnp.d2[2 * jp + 1] = s2[jp].y;
-                }
-                bnp.cnt = (float)(16 * MI);
-                bnp.template finish<WM, WN>(a, lds, tile_lin, n0);
-            }
-            return;
-        }
     }
 #pragma unroll
     for (int i = 0; i < MI; ++i)
