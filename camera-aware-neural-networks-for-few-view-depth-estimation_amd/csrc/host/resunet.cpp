@@ -649,12 +649,16 @@ struct PrepBatch {
 
 void prep_weights_fwd(cad_resunet* h, hipStream_t st) {
     PrepBatch pb(st);
+    cad::Mx8WList xl;   // the fp8 weights, quantised from the fp32 parameters in one launch
     auto sw = [&](RConv& c) {   // bf16 twin of [cout][Kp] (split_rows' rounding)
         pb.add(cad::WPREP_SPLIT, h->P(c.pidx), nullptr, c.ws, c.cout, c.Kp, (int64_t)c.cout * c.Kp);
         if (h->fp8 && c.x8) {
-            cad::Mx8 d;
-            d.q = c.wq; d.s = c.wsc; d.ld = c.ldq;
-            cad::mx8_quantize(h->P(c.pidx), false, c.Kp, 0, c.Kp, c.cout, d, st);
+            if (xl.njobs == cad::kMx8WMaxJobs) {
+                cad::mx8_quantize_weights(xl, st);
+                xl.njobs = 0;
+            }
+            cad::Mx8WJob& j = xl.job[xl.njobs++];
+            j.src = h->P(c.pidx); j.q = c.wq; j.s = c.wsc; j.ldq = c.ldq; j.rows = c.cout; j.C = c.Kp; j.blk0 = 0;
         }
     };
     sw(h->stem.c);
@@ -668,6 +672,7 @@ void prep_weights_fwd(cad_resunet* h, hipStream_t st) {
         pb.add(cad::WPREP_CONVT, h->P(d.up_w), d.wf, d.wfs, d.cout_up, d.cin_up, (int64_t)4 * d.cout_up * d.cin_up);
     }
     pb.flush();
+    cad::mx8_quantize_weights(xl, st);
 }
 
 void forward(cad_resunet* h, const float* rgb, float* depth, int B, hipStream_t st) {

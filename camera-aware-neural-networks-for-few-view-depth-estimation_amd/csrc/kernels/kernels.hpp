@@ -132,6 +132,22 @@ struct Mx8 {
 // dst rows [coff, coff + C) = MX(src rows [scoff, scoff + C)), src fp32 (src_bf16 = false) or bf16
 // rows of lds elements; C % 32 == 0
 void mx8_quantize(const void* src, bool src_bf16, int64_t lds, int scoff, int C, int64_t M, Mx8 dst, hipStream_t st);
+// fp32 weights [rows][C] -> MX (q rows of ldq bytes, coff 0; one e8m0 byte per 32), several tensors
+// in one launch (the bits mx8_quantize writes for each)
+struct Mx8WJob {
+    const float* src;
+    uint8_t* q;
+    uint8_t* s;
+    int64_t ldq;
+    int rows, C;
+    int blk0;   // first block of this job (filled by mx8_quantize_weights)
+};
+constexpr int kMx8WMaxJobs = 56;
+struct Mx8WList {
+    Mx8WJob job[kMx8WMaxJobs];
+    int njobs = 0;
+};
+void mx8_quantize_weights(Mx8WList& list, hipStream_t st);
 // y[m][ycoff + n] = sum_k x[m][k] w[n][k] on MX operands (+ BN partials when stats); K % 128 == 0
 bool dense_x8_ok(int K, int N);
 void dense_fwd_x8(Mx8 x, int K, Mx8 w, int N, float* y, int64_t ldy, int ycoff, int64_t M, float* stats, hipStream_t st,

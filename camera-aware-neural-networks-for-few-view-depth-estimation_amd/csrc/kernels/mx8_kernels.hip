@@ -48,6 +48,33 @@ __global__ void k_mx8_quantize(const void* __restrict__ src, int64_t lds, int sc
     s[row * (ldq >> 5) + (qcoff >> 5) + blk] = (uint8_t)sc;
 }
 
+// a list of fp32 weight tensors [rows][C] (row stride C) in one launch: the per-step quantisation of
+// config 5's ~50 fp8 weights was ~50 launches of ~4 us of which most is launch latency; job j owns
+// blocks [blk0, next blk0), the same per-(row, 32-block) work as k_mx8_quantize<false>
+__global__ __launch_bounds__(256) void k_mx8_quantize_list(Mx8WList list) {
+    int j = 0;
+    while (j + 1 < list.njobs && (int)blockIdx.x >= list.job[j + 1].blk0) ++j;
+    const Mx8WJob& jb = list.job[j];
+    const int nblk = jb.C >> 5;
+    const int64_t i = (int64_t)(blockIdx.x - jb.blk0) * 256 + threadIdx.x;
+    if (i >= (int64_t)jb.rows * nblk) return;
+    const int64_t row = i / nblk;
+    const int blk = (int)(i - row * nblk);
+    float v[32];
+    const float4* p = reinterpret_cast<const float4*>(jb.src + row * jb.C + 32 * blk);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const float4 f = p[e];
+        v[4 * e] = f.x; v[4 * e + 1] = f.y; v[4 * e + 2] = f.z; v[4 * e + 3] = f.w;
+    }
+    uint32_t w[8];
+    const uint32_t sc = mx8_quant_block(v, w);
+    uint4* d = reinterpret_cast<uint4*>(jb.q + row * jb.ldq + 32 * blk);
+    d[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    d[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    jb.s[row * (jb.ldq >> 5) + blk] = (uint8_t)sc;
+}
+
 template <int WM, int WN, class Epi>
 __global__ __launch_bounds__(256, 2) void k_dense_x8(GemmArgs a, Mx8 x, Mx8 w) {
     dense_body_x8<WM, WN, 2, 2, Epi>(a, x, w);
@@ -158,6 +185,23 @@ void mx8_quantize(const void* src, bool src_bf16, int64_t lds, int scoff, int C,
         hipLaunchKernelGGL(k_mx8_quantize<true>, grid, dim3(256), 0, st, src, lds, scoff, nblk, n, q, dst.ld, dst.coff, s);
     else
         hipLaunchKernelGGL(k_mx8_quantize<false>, grid, dim3(256), 0, st, src, lds, scoff, nblk, n, q, dst.ld, dst.coff, s);
+}
+
+void mx8_quantize_weights(Mx8WList& list, hipStream_t st) {
+    if (list.njobs <= 0) return;
+    if (list.njobs > kMx8WMaxJobs) throw std::runtime_error("mx8_quantize_weights: too many jobs");
+    int blocks = 0;
+    for (int j = 0; j < list.njobs; ++j) {
+        Mx8WJob& jb = list.job[j];
+        if (jb.C % 32 || jb.ldq % 128 || jb.ldq < jb.C || jb.rows <= 0)
+            throw std::runtime_error("mx8_quantize_weights: layout");
+        CAD_NO_ALIAS("mx8_quantize_weights",
+                     {aview(jb.q, jb.rows, jb.ldq, 0, jb.C, 1, "q"), aview(jb.s, jb.rows, jb.ldq / 32, 0, jb.C / 32, 1, "scales")},
+                     {aview(jb.src, jb.rows, jb.C, 0, jb.C, 4, "w")});
+        jb.blk0 = blocks;
+        blocks += cdiv((int64_t)jb.rows * (jb.C / 32), 256);
+    }
+    hipLaunchKernelGGL(k_mx8_quantize_list, dim3(blocks), dim3(256), 0, st, list);
 }
 
 bool dense_x8_ok(int K, int N) { return K > 0 && K % 128 == 0 && N % 64 == 0; }
