@@ -630,8 +630,10 @@ void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth
     if (h->model != CAD_MODEL_BASELINE) {
         // a14 normalisation, then every block's FiLM MLP (gamma/beta depend on the camera only)
         cad::camera_normalize(cam4, B, h->H, h->W, h->camn, st);
-        for (int l = 0; l < 5; ++l) cad::film_mlp_fwd(film_view(h, h->enc[l]), h->camn, B, h->train, st);
-        for (int l = 3; l >= 0; --l) cad::film_mlp_fwd(film_view(h, h->dec[l]), h->camn, B, h->train, st);
+        cad::FilmList fl;   // (one launch per MLP step for all nine layers)
+        for (int l = 0; l < 5; ++l) fl.l[fl.n++] = film_view(h, h->enc[l]);
+        for (int l = 3; l >= 0; --l) fl.l[fl.n++] = film_view(h, h->dec[l]);
+        cad::film_mlp_fwd_all(fl, h->camn, B, h->train, st);
     }
     if (h->model == CAD_MODEL_RAY_FILM)
         cad::rgb_rays_to_nhwc8(rgb, cam4, B, h->H, h->W, h->x0, st);

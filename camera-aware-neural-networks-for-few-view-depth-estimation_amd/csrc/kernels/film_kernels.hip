@@ -101,6 +101,7 @@ __device__ void bn1d_relu_col(float* zx, float* h, int ldz, int j, int B, bool b
     float mean, is;
     if (train) {
         double s = 0.0, s2 = 0.0;
+#pragma unroll 8
         for (int b = 0; b < B; ++b) {
             const double z = zx[b * ldz + j];
             s += z;
@@ -118,6 +119,7 @@ __device__ void bn1d_relu_col(float* zx, float* h, int ldz, int j, int B, bool b
         is = 1.f / sqrtf(rv[j] + 1e-5f);
     }
     is_out[j] = is;
+#pragma unroll 8
     for (int b = 0; b < B; ++b) {
         const float xh = (zx[b * ldz + j] - mean) * is;
         zx[b * ldz + j] = xh;
@@ -168,6 +170,58 @@ __global__ __launch_bounds__(256) void k_film_linear(const float* __restrict__ X
 // BN1d + ReLU over the fc2 outputs (already in xh2): one thread per feature column
 __global__ __launch_bounds__(H2) void k_film_l2_bn(FilmLayer L, int B, int train) {
     bn1d_relu_col(L.xh2, L.h2, H2, threadIdx.x, B, B > 1, train, L.g2, L.be2, L.rm2, L.rv2, L.is2);
+}
+
+// the list forms: blockIdx.x (l1 / l2 BN) or blockIdx.z (the Linears) selects the layer
+__global__ __launch_bounds__(H1) void k_film_l1_fwd_all(FilmList list, const float* __restrict__ camn, int B, int train) {
+    const FilmLayer& L = list.l[blockIdx.x];
+    const int j = threadIdx.x;
+    for (int b = 0; b < B; ++b) {
+        float z = L.b1[j];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) z += camn[b * 4 + k] * L.w1[j * 4 + k];
+        L.xh1[b * H1 + j] = z;
+    }
+    bn1d_relu_col(L.xh1, L.h1, H1, j, B, B > 1, train, L.g1, L.be1, L.rm1, L.rv1, L.is1);
+}
+__global__ __launch_bounds__(H2) void k_film_l2_bn_all(FilmList list, int B, int train) {
+    const FilmLayer& L = list.l[blockIdx.x];
+    bn1d_relu_col(L.xh2, L.h2, H2, threadIdx.x, B, B > 1, train, L.g2, L.be2, L.rm2, L.rv2, L.is2);
+}
+// HEADS = false: fc2 (h1 -> xh2, O = H2); true: the gamma / beta heads (h2 -> gam, bet; O = C, blockIdx.y)
+template <int K, bool HEADS>
+__global__ __launch_bounds__(256) void k_film_linear_all(FilmList list, int B) {
+    const FilmLayer& L = list.l[blockIdx.z];
+    const int O = HEADS ? L.C : H2;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)B * O) return;
+    const int b = (int)(t / O), o = (int)(t - (int64_t)b * O);
+    const float* X = HEADS ? L.h2 : L.h1;
+    const float* W = (HEADS ? (blockIdx.y ? L.wb : L.wg) : L.w2) + (int64_t)o * K;
+    const float* x = X + (int64_t)b * K;
+    float z = (HEADS ? (blockIdx.y ? L.bb : L.bg) : L.b2)[o];
+#pragma unroll 8
+    for (int k = 0; k < K; k += 4) {   // (k_film_linear's order)
+        const float4 w = *reinterpret_cast<const float4*>(W + k);
+        const float4 v = *reinterpret_cast<const float4*>(x + k);
+        z += v.x * w.x;
+        z += v.y * w.y;
+        z += v.z * w.z;
+        z += v.w * w.w;
+    }
+    (HEADS ? (blockIdx.y ? L.bet : L.gam) : L.xh2)[t] = z;
+}
+void film_mlp_fwd_all(const FilmList& list, const float* camn, int B, bool train, hipStream_t st) {
+    if (list.n <= 0) return;
+    if (list.n > kFilmMaxLayers) throw std::runtime_error("film_mlp_fwd_all: too many layers");
+    int cmax = 0;
+    for (int i = 0; i < list.n; ++i) cmax = std::max(cmax, list.l[i].C);
+    hipLaunchKernelGGL(k_film_l1_fwd_all, dim3(list.n), dim3(H1), 0, st, list, camn, B, (int)train);
+    hipLaunchKernelGGL((k_film_linear_all<H1, false>), dim3(cdiv((int64_t)B * H2, 256), 1, list.n), dim3(256), 0, st, list,
+                       B);
+    hipLaunchKernelGGL(k_film_l2_bn_all, dim3(list.n), dim3(H2), 0, st, list, B, (int)train);
+    hipLaunchKernelGGL((k_film_linear_all<H2, true>), dim3(cdiv((int64_t)B * cmax, 256), 2, list.n), dim3(256), 0, st, list,
+                       B);
 }
 
 void film_mlp_fwd(const FilmLayer& L, const float* camn, int B, bool train, hipStream_t st) {
@@ -323,11 +377,77 @@ int64_t film_reduce_doubles(int B, int64_t HW, int C) { return (int64_t)B * film
 // a16 FiLM MLP backward (train mode)
 // ------------------------------------------------------------------------------------------
 // heads: dW[o][k] = Σ_b d[b][o] h2[b][k], db[o] = Σ_b d[b][o]; column k == H2 is the bias
-__global__ __launch_bounds__(256) void k_film_head_bwd_w(FilmLayer L, int B) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// dh2[b][k] = Σ_c dgam[b][c] Wg[c][k] + Σ_c dbet[b][c] Wb[c][k], summed in that order: one thread per
+// (b, k), k fastest (coalesced weight rows, dgam / dbet broadcast); loads run 8 terms ahead of the
+// dependent FMA chain
+
+// BatchNorm1d(+ReLU) backward for feature column j: in: dh (grad of h = relu(n)), out: dz (grad of
+// the Linear output) into dh's slot; writes the BN affine grads
+__device__ void bn1d_relu_bwd_col(float* dh, const float* h, const float* xh, int ldz, int j, int B, bool bn,
+                                  const float* g, const float* is, float* dg, float* dbe) {
+    if (!bn) {
+        for (int b = 0; b < B; ++b) dh[b * ldz + j] = h[b * ldz + j] > 0.f ? dh[b * ldz + j] : 0.f;
+        dg[j] = 0.f;
+        dbe[j] = 0.f;
+        return;
+    }
+    double s = 0.0, sx = 0.0;
+#pragma unroll 8
+    for (int b = 0; b < B; ++b) {
+        const float dn = h[b * ldz + j] > 0.f ? dh[b * ldz + j] : 0.f;
+        dh[b * ldz + j] = dn;
+        s += dn;
+        sx += (double)dn * xh[b * ldz + j];
+    }
+    dg[j] = (float)sx;
+    dbe[j] = (float)s;
+    const float k1 = g[j] * is[j];
+    const float k2 = (float)(k1 * s / B), k3 = (float)(k1 * sx / B);
+#pragma unroll 8
+    for (int b = 0; b < B; ++b) dh[b * ldz + j] = k1 * dh[b * ldz + j] - k2 - k3 * xh[b * ldz + j];
+}
+
+// layer 2: dh2 -> dz2 (in place) through BN1d + ReLU, fc2 bias gradient
+__global__ __launch_bounds__(H2) void k_film_l2_bwd(FilmLayer L, int B) {
+    const int j = threadIdx.x;
+    bn1d_relu_bwd_col(L.dh2, L.h2, L.xh2, H2, j, B, B > 1, L.g2, L.is2, L.gg2, L.gbe2);
+    float db = 0.f;
+    for (int b = 0; b < B; ++b) db += L.dh2[b * H2 + j];
+    L.gb2[j] = db;
+}
+
+// fc2 weight gradient gw2[j][k] = Σ_b dz2[b][j] h1[b][k]: one thread per weight (k fastest)
+
+// layer 1: dh1[b][j] = Σ_jj dz2[b][jj] W2[jj][j], one thread per (b, j) (j fastest: coalesced weight
+// rows, dz2 broadcast), loads 8 terms ahead of the dependent FMA chain (jj ascending)
+// then BN1d + ReLU backward and the fc1 gradients per column
+__global__ __launch_bounds__(H1) void k_film_l1_bwd(FilmLayer L, const float* __restrict__ camn, int B) {
+    const int j = threadIdx.x;
+    bn1d_relu_bwd_col(L.dh1, L.h1, L.xh1, H1, j, B, B > 1, L.g1, L.is1, L.gg1, L.gbe1);
+    float db = 0.f;
+    float dw[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < B; ++b) {
+        const float d = L.dh1[b * H1 + j];
+        db += d;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dw[k] += d * camn[b * 4 + k];
+    }
+    L.gb1[j] = db;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) L.gw1[j * 4 + k] = dw[k];
+}
+
+// two independent steps in one launch: blocks [0, nb0) run the first kernel's body, the rest the
+// second's (each thread's work and order exactly the separate kernels')
+template <void (*A)(const FilmLayer&, int, int), void (*Bf)(const FilmLayer&, int, int)>
+__global__ __launch_bounds__(256) void k_film_pair(FilmLayer L, int B, int nb0) {
+    if ((int)blockIdx.x < nb0) A(L, B, blockIdx.x * 256 + threadIdx.x);
+    else Bf(L, B, ((int)blockIdx.x - nb0) * 256 + threadIdx.x);
+}
+__device__ void film_head_bwd_w_at(const FilmLayer& L, int B, int t) {
     const int C = L.C;
-    if (t >= (int64_t)2 * C * (H2 + 1)) return;
-    const int o = (int)(t / (H2 + 1)), k = (int)(t - (int64_t)o * (H2 + 1));
+    if (t >= 2 * C * (H2 + 1)) return;
+    const int o = t / (H2 + 1), k = t - o * (H2 + 1);
     const bool isg = o < C;
     const int c = isg ? o : o - C;
     const float* d = isg ? L.dgam : L.dbet;
@@ -339,11 +459,7 @@ __global__ __launch_bounds__(256) void k_film_head_bwd_w(FilmLayer L, int B) {
     if (k < H2) (isg ? L.gwg : L.gwb)[(int64_t)c * H2 + k] = acc;
     else (isg ? L.gbg : L.gbb)[c] = acc;
 }
-// dh2[b][k] = Σ_c dgam[b][c] Wg[c][k] + Σ_c dbet[b][c] Wb[c][k], summed in that order: one thread per
-// (b, k), k fastest (coalesced weight rows, dgam / dbet broadcast); loads run 8 terms ahead of the
-// dependent FMA chain
-__global__ __launch_bounds__(256) void k_film_dh2(FilmLayer L, int B) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ void film_dh2_at(const FilmLayer& L, int B, int t) {
     if (t >= B * H2) return;
     const int b = t / H2, k = t - b * H2;
     const int C = L.C;
@@ -363,54 +479,14 @@ __global__ __launch_bounds__(256) void k_film_dh2(FilmLayer L, int B) {
     }
     L.dh2[t] = acc;
 }
-
-// BatchNorm1d(+ReLU) backward for feature column j: in: dh (grad of h = relu(n)), out: dz (grad of
-// the Linear output) into dh's slot; writes the BN affine grads
-__device__ void bn1d_relu_bwd_col(float* dh, const float* h, const float* xh, int ldz, int j, int B, bool bn,
-                                  const float* g, const float* is, float* dg, float* dbe) {
-    if (!bn) {
-        for (int b = 0; b < B; ++b) dh[b * ldz + j] = h[b * ldz + j] > 0.f ? dh[b * ldz + j] : 0.f;
-        dg[j] = 0.f;
-        dbe[j] = 0.f;
-        return;
-    }
-    double s = 0.0, sx = 0.0;
-    for (int b = 0; b < B; ++b) {
-        const float dn = h[b * ldz + j] > 0.f ? dh[b * ldz + j] : 0.f;
-        dh[b * ldz + j] = dn;
-        s += dn;
-        sx += (double)dn * xh[b * ldz + j];
-    }
-    dg[j] = (float)sx;
-    dbe[j] = (float)s;
-    const float k1 = g[j] * is[j];
-    const float k2 = (float)(k1 * s / B), k3 = (float)(k1 * sx / B);
-    for (int b = 0; b < B; ++b) dh[b * ldz + j] = k1 * dh[b * ldz + j] - k2 - k3 * xh[b * ldz + j];
-}
-
-// layer 2: dh2 -> dz2 (in place) through BN1d + ReLU, fc2 bias gradient
-__global__ __launch_bounds__(H2) void k_film_l2_bwd(FilmLayer L, int B) {
-    const int j = threadIdx.x;
-    bn1d_relu_bwd_col(L.dh2, L.h2, L.xh2, H2, j, B, B > 1, L.g2, L.is2, L.gg2, L.gbe2);
-    float db = 0.f;
-    for (int b = 0; b < B; ++b) db += L.dh2[b * H2 + j];
-    L.gb2[j] = db;
-}
-
-// fc2 weight gradient gw2[j][k] = Σ_b dz2[b][j] h1[b][k]: one thread per weight (k fastest)
-__global__ __launch_bounds__(256) void k_film_gw2(FilmLayer L, int B) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ void film_gw2_at(const FilmLayer& L, int B, int t) {
     if (t >= H2 * H1) return;
     const int j = t / H1, k = t - j * H1;
     float acc = 0.f;
     for (int b = 0; b < B; ++b) acc += L.dh2[b * H2 + j] * L.h1[b * H1 + k];
     L.gw2[t] = acc;
 }
-
-// layer 1: dh1[b][j] = Σ_jj dz2[b][jj] W2[jj][j], one thread per (b, j) (j fastest: coalesced weight
-// rows, dz2 broadcast), loads 8 terms ahead of the dependent FMA chain (jj ascending)
-__global__ __launch_bounds__(256) void k_film_dh1(FilmLayer L, int B) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ void film_dh1_at(const FilmLayer& L, int B, int t) {
     if (t >= B * H1) return;
     const int b = t / H1, j = t - b * H1;
     const float* d = L.dh2 + (int64_t)b * H2;
@@ -425,30 +501,15 @@ __global__ __launch_bounds__(256) void k_film_dh1(FilmLayer L, int B) {
     }
     L.dh1[t] = acc;
 }
-// then BN1d + ReLU backward and the fc1 gradients per column
-__global__ __launch_bounds__(H1) void k_film_l1_bwd(FilmLayer L, const float* __restrict__ camn, int B) {
-    const int j = threadIdx.x;
-    bn1d_relu_bwd_col(L.dh1, L.h1, L.xh1, H1, j, B, B > 1, L.g1, L.is1, L.gg1, L.gbe1);
-    float db = 0.f;
-    float dw[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int b = 0; b < B; ++b) {
-        const float d = L.dh1[b * H1 + j];
-        db += d;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) dw[k] += d * camn[b * 4 + k];
-    }
-    L.gb1[j] = db;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) L.gw1[j * 4 + k] = dw[k];
-}
 
+// six steps in four launches: {heads' weight gradients, dh2} -> layer-2 BN backward -> {fc2 weight
+// gradient, dh1} -> layer-1 BN backward and fc1 gradients
 void film_mlp_bwd(const FilmLayer& L, const float* camn, int B, hipStream_t st) {
-    const int64_t nw = (int64_t)2 * L.C * (H2 + 1);
-    hipLaunchKernelGGL(k_film_head_bwd_w, dim3(cdiv(nw, 256)), dim3(256), 0, st, L, B);
-    hipLaunchKernelGGL(k_film_dh2, dim3(cdiv((int64_t)B * H2, 256)), dim3(256), 0, st, L, B);
+    const int nb_w = cdiv((int64_t)2 * L.C * (H2 + 1), 256), nb_dh2 = cdiv((int64_t)B * H2, 256);
+    hipLaunchKernelGGL((k_film_pair<film_head_bwd_w_at, film_dh2_at>), dim3(nb_w + nb_dh2), dim3(256), 0, st, L, B, nb_w);
     hipLaunchKernelGGL(k_film_l2_bwd, dim3(1), dim3(H2), 0, st, L, B);
-    hipLaunchKernelGGL(k_film_gw2, dim3(cdiv(H2 * H1, 256)), dim3(256), 0, st, L, B);
-    hipLaunchKernelGGL(k_film_dh1, dim3(cdiv((int64_t)B * H1, 256)), dim3(256), 0, st, L, B);
+    const int nb_gw2 = cdiv(H2 * H1, 256), nb_dh1 = cdiv((int64_t)B * H1, 256);
+    hipLaunchKernelGGL((k_film_pair<film_gw2_at, film_dh1_at>), dim3(nb_gw2 + nb_dh1), dim3(256), 0, st, L, B, nb_gw2);
     hipLaunchKernelGGL(k_film_l1_bwd, dim3(1), dim3(H1), 0, st, L, camn, B);
 }
 

@@ -386,6 +386,14 @@ struct FilmLayer {
     float *gw1, *gb1, *gw2, *gb2, *gwg, *gbg, *gwb, *gbb, *gg1, *gbe1, *gg2, *gbe2;   // gradients
 };
 void film_mlp_fwd(const FilmLayer& L, const float* camn, int B, bool train, hipStream_t st);
+// every layer's MLP forward in four launches (they depend on the camera only): the same per-layer
+// arithmetic as film_mlp_fwd
+constexpr int kFilmMaxLayers = 10;
+struct FilmList {
+    FilmLayer l[kFilmMaxLayers];
+    int n = 0;
+};
+void film_mlp_fwd_all(const FilmList& list, const float* camn, int B, bool train, hipStream_t st);
 void film_mlp_bwd(const FilmLayer& L, const float* camn, int B, hipStream_t st);
 // a1 = gam[b,c] * relu(y*scale[c] + shift[c]) + bet[b,c]   (NHWC [B*HW][C]); out (fp32, may be null)
 // and / or os (its bf16 twin, rows of C; the B1 engine's operand)
