@@ -188,9 +188,12 @@ def cpu_baseline(args, over_batch=4):
         t0 = time.perf_counter()
         ref.step(rgb, gt, K)                      # warm-up
         warm = time.perf_counter() - t0
+        # (a progress line per step: a bs32 CPU step takes ~50 s, and a run silent for minutes reads as hung)
+        log(f"cpu baseline: warm-up step {warm:.1f} s")
         t0 = time.perf_counter()
-        for _ in range(args.cpu_sample_steps):
+        for i in range(args.cpu_sample_steps):
             ref.step(rgb, gt, K)
+            log(f"cpu baseline: step {i + 1}/{args.cpu_sample_steps} at {time.perf_counter() - t0:.1f} s")
         dt = time.perf_counter() - t0
         log(f"cpu baseline: warm-up {warm:.1f} s, {args.cpu_sample_steps} steps {dt:.1f} s at {threads} threads")
         phys = host["physical_cores"] or 0
@@ -265,6 +268,7 @@ def parity_steps(args, cad, dev, steps=10, B=2):
             gl = tr.train_step(rg, gg, kg)[0].item()
             r = ref.step(rgb, gt, K)
             r64 = ref64.step(rgb, gt, K)
+            log(f"parity: step {k}/{steps}")
             if k in (1, steps):
                 model.eval()
                 g_eval = (model(hrg, cad.camera_from_K(hkg)) if model.conditioned else model(hrg))
