@@ -170,6 +170,11 @@ struct cad_unet {
     float *flat_p = nullptr, *flat_g = nullptr;
     float* norm_coef = nullptr;   // [norm, coef]
     void* arena_base = nullptr;
+    // FiLM models: the MLP backward of a block runs on `side`, forked after its bn1 backward and joined
+    // at the end of the block, beside conv1's weight gradient and dgrad (it writes only the MLP's own
+    // parameter gradients)
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // model structure
     DoubleConv enc[5];   // enc1..enc4 = levels 0..3, bottleneck = level 4
     DoubleConv dec[4];   // dec1..dec4 at levels 0..3 (index = level)
@@ -756,7 +761,15 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
                          nullptr, ff ? dc.film.dgam : nullptr, ff ? dc.film.dbet : nullptr,
                          bn1_tiles ? h->rc_part : nullptr, bn1_tiles);
     }
-    if (dc.has_film()) cad::film_mlp_bwd(film_view(h, dc), h->camn, B, st);
+    const bool film_side = dc.has_film() && h->side;
+    if (film_side) {   // fork: the MLP backward beside conv1's GEMMs (joined below)
+        HIPCHK(hipEventRecord(h->ev_fork, st));
+        HIPCHK(hipStreamWaitEvent(h->side, h->ev_fork, 0));
+        cad::film_mlp_bwd(film_view(h, dc), h->camn, B, h->side);
+        HIPCHK(hipEventRecord(h->ev_join, h->side));
+    } else if (dc.has_film()) {
+        cad::film_mlp_bwd(film_view(h, dc), h->camn, B, st);
+    }
     // conv1: wgrad, dgrad
     if (ps1)
         cad::conv3x3_wgrad_ps(sv(dYs, C), C, in_s, dc.c1.cin, h->G(dc.c1.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
@@ -771,6 +784,7 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
         } else
             cad::conv3x3_dgrad(dY, C, dc.c1.wd, dc.c1.cin, din, lddin, B, Hh, Ww, st);
     }
+    if (film_side) HIPCHK(hipStreamWaitEvent(st, h->ev_join, 0));   // join: the block's gradients complete on st
 }
 
 void repack_dgrad_weights(cad_unet* h, hipStream_t st) {   // one launch (prep_fwd_weights)
@@ -1054,6 +1068,11 @@ cad_status cad_unet_create_model(const cad_unet_desc* d, int model, int device, 
         require(real.off == sz.off, "internal: arena layout differs between the sizing and the real pass", CAD_ERR_STATE);
         compute_stage_ranges(h.get());
         default_init(h.get());
+        if (model != CAD_MODEL_BASELINE) {
+            HIPCHK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+            HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+        }
         HIPCHK(hipDeviceSynchronize());
         *out = h.release();
     });
@@ -1062,6 +1081,10 @@ cad_status cad_unet_create_model(const cad_unet_desc* d, int model, int device, 
 void cad_unet_destroy(cad_unet* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
+    if (h->side) (void)hipStreamSynchronize(h->side);
+    if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+    if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+    if (h->side) (void)hipStreamDestroy(h->side);
     (void)hipFree(h->arena_base);
     delete h;
 }
