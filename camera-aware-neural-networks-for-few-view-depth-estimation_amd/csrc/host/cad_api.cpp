@@ -170,11 +170,19 @@ struct cad_unet {
     float *flat_p = nullptr, *flat_g = nullptr;
     float* norm_coef = nullptr;   // [norm, coef]
     void* arena_base = nullptr;
-    // FiLM models: the MLP backward of a block runs on `side`, forked after its bn1 backward and joined
-    // at the end of the block, beside conv1's weight gradient and dgrad (it writes only the MLP's own
-    // parameter gradients)
+    // The backward's parameter-gradient work — FiLM MLP backwards always, conv2 / conv1 / ConvT weight
+    // gradients and the ConvT bias sums on the S3 engine (wgrad_stream) — runs on `side`, forked from the
+    // step's stream as soon as its operands exist, beside the chain dgrad -> BN backward -> dgrad that the
+    // next stage waits on (it writes only parameter gradients and its own scratch: slab, dscr2).  bn2 / bn1 of a block write their dL/dz into
+    // two buffer pairs (Sb / dYs, Sb2 / dYs2); before rewriting a pair the step's stream waits for the
+    // side's last reader of it (evA, evB).  Joined at the end of every stage, or once at the end of a
+    // whole backward (cad_unet_backward; the staged API and the DP exchange need each stage complete).
     hipStream_t side = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipEvent_t ev_fork = nullptr, evA = nullptr, evB = nullptr, ev_tail = nullptr;
+    bool defer_join = false;
+    float* Sb2 = nullptr;
+    void* dYs2 = nullptr;
+    double* dscr2 = nullptr;
     // model structure
     DoubleConv enc[5];   // enc1..enc4 = levels 0..3, bottleneck = level 4
     DoubleConv dec[4];   // dec1..dec4 at levels 0..3 (index = level)
@@ -407,6 +415,8 @@ void layout(cad_unet* h, Arena& a) {
     const int64_t M0C0 = h->Ml(0, B) * h->Cl(0);
     h->Sa = a.f(M0C0);
     h->Sb = a.f(M0C0);
+    h->Sb2 = a.f(M0C0);
+    h->dYs2 = sp(h->Ml(0, B) * h->Cl(0));
     h->Sc = a.f(h->Ml(1, B) * h->Cl(0));
     // BN tile partials: rows x (2C + 1) (S, M2 per channel + the row's count), max over layers
     int64_t st = 0, colmax = 0;
@@ -420,6 +430,7 @@ void layout(cad_unet* h, Arena& a) {
     for (int l = 0; l < 5 && film; ++l)
         dscr = std::max(dscr, cad::film_reduce_doubles(B, (int64_t)h->Hl(l) * h->Wl(l), h->Cl(l)) + 8192);
     h->dscr = a.d(dscr);
+    h->dscr2 = a.d(dscr);
     // wgrad split-K slab: enough for the largest-benefit layers, capped at 64M floats (256 MB)
     int64_t sl = 0;
     for (int l = 0; l < 5; ++l) {
@@ -704,6 +715,27 @@ void unet_forward(cad_unet* h, const float* rgb, const float* cam4, float* depth
 // g: grad wrt the DoubleConv output (ld ldg, channel offset gcoff); in: the block input (ld ldin,
 // cin channels; in_s its split twin); din: where conv1's dgrad goes (nullptr = not needed), ld lddin.
 // head != nullptr (level-0 fusion): g is null and bn2's upstream gradient is the head's, rebuilt per row.
+// fork: the side stream continues after everything issued on st so far
+void side_fork(cad_unet* h, hipStream_t st) {
+    HIPCHK(hipEventRecord(h->ev_fork, st));
+    HIPCHK(hipStreamWaitEvent(h->side, h->ev_fork, 0));
+}
+// join: st continues after everything issued on the side stream so far
+void side_join(cad_unet* h, hipStream_t st) {
+    HIPCHK(hipEventRecord(h->ev_tail, h->side));
+    HIPCHK(hipStreamWaitEvent(st, h->ev_tail, 0));
+}
+// the stream the weight gradients run on: the side stream on the S3 engine (configs[1] -1.9 %); on the
+// bf16 engine they stay on the step's stream — there the GEMMs beside each other measured neutral to
+// +0.7 % (profiles/r06_lab/README.md).  CAD_SIDE_WGRAD=1 / 0 forces either
+hipStream_t wgrad_stream(cad_unet* h, bool ps, hipStream_t st) {
+    static const int f = env_flag("CAD_SIDE_WGRAD", -1);
+    const bool side = f < 0 ? !ps : f != 0;
+    if (!side) return st;
+    side_fork(h, st);
+    return h->side;
+}
+
 void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, int gcoff, const float* in,
                      int64_t ldin, cad::Split in_s, int B, float* din, int64_t lddin, hipStream_t st,
                      const cad::HeadGrad* head = nullptr, const cad::PoolAdd* pool = nullptr, void* din_hi = nullptr,
@@ -711,12 +743,18 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     const int l = dc.level, Hh = h->Hl(l), Ww = h->Wl(l), C = dc.c1.cout;
     const int64_t M = h->Ml(l, B);
     const bool ps = h->fwd_np > 0 && h->fwd_np == cad::split_planes();
+    hipStream_t sd = h->side;
+    // bn2's dL/dz in (Sb, dYs), bn1's in (Sb2, dYs2): the weight gradients on the side stream read them
+    // while this stream goes on
     float* dY = h->Sb;
     void* dYs = h->dYs;
+    float* dY1 = h->Sb2;
+    void* dYs1 = h->dYs2;
     // conv2's input gradient; the bf16 engine stores it as bf16 (read by FiLM's and bn1's backward)
     float* dA1 = h->Sa;
     // bn2 + relu
     // with pre-split GEMMs both consumers of dY2 read its twin: the fp32 dY2 is not written
+    HIPCHK(hipStreamWaitEvent(st, h->evA, 0));   // the previous block's conv2 weight gradient has read them
     cad::bn_relu_bwd(g, ldg, gcoff, dc.y2, C, dc.b2.mean, dc.b2.invstd, dc.b2.scale, dc.b2.shift, h->P(dc.b2.widx), M,
                      h->dscr, dc.b2.coef, h->G(dc.b2.widx), h->G(dc.b2.bidx), ps ? nullptr : dY, st, nullptr, 1,
                      ps ? dYs : nullptr, true, dc.y2b, head, g_bf16, pool);
@@ -732,11 +770,14 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
         bs.mean = dc.b1.mean; bs.invstd = dc.b1.invstd; bs.scale = dc.b1.scale; bs.shift = dc.b1.shift;
         bs.part = h->rc_part; bs.part_cap = h->part_cap;
     }
+    hipStream_t wg = wgrad_stream(h, ps, st);
     if (ps) {
-        cad::conv3x3_wgrad_ps(sv(dYs, C), C, sv(dc.a1s, C), C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
+        cad::conv3x3_wgrad_ps(sv(dYs, C), C, sv(dc.a1s, C), C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, wg);
+        HIPCHK(hipEventRecord(h->evA, wg));
         cad::conv3x3_dgrad_ps(sv(dYs, C), C, sv(dc.c2.wds, 9 * C), C, dA1, C, B, Hh, Ww, st, true);
     } else {
-        cad::conv3x3_wgrad(dY, C, dc.a1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
+        cad::conv3x3_wgrad(dY, C, dc.a1, C, 0, C, h->G(dc.c2.pidx), B, Hh, Ww, h->slab, h->slab_cap, wg);
+        HIPCHK(hipEventRecord(h->evA, wg));
         if (bs.part) bn1_tiles = cad::conv3x3_dgrad_bnsums(dY, C, dc.c2.wd, C, dA1, C, B, Hh, Ww, bs, st);
         if (!bn1_tiles) cad::conv3x3_dgrad(dY, C, dc.c2.wd, C, dA1, C, B, Hh, Ww, st);
     }
@@ -753,38 +794,37 @@ void double_conv_bwd(cad_unet* h, DoubleConv& dc, const float* g, int64_t ldg, i
     // in-loader weight gradient)
     const bool ps1 = conv1_presplit(h, dc, ps, in_s);
     const bool dy1_f32 = !ps1 || (din && !(ps && dc.c1.wds));
+    HIPCHK(hipStreamWaitEvent(st, h->evB, 0));   // the previous block's conv1 weight gradient has read them
     {
         const bool ff = dc.has_film() && !film_sep;
         cad::bn_relu_bwd(dA1, C, 0, dc.y1, C, dc.b1.mean, dc.b1.invstd, dc.b1.scale, dc.b1.shift, h->P(dc.b1.widx), M,
-                         h->dscr, dc.b1.coef, h->G(dc.b1.widx), h->G(dc.b1.bidx), dy1_f32 ? dY : nullptr, st,
-                         dc.has_film() ? dc.film.gam : nullptr, HW, ps ? dYs : nullptr, true, dc.y1b, nullptr, ps,
+                         h->dscr, dc.b1.coef, h->G(dc.b1.widx), h->G(dc.b1.bidx), dy1_f32 ? dY1 : nullptr, st,
+                         dc.has_film() ? dc.film.gam : nullptr, HW, ps ? dYs1 : nullptr, true, dc.y1b, nullptr, ps,
                          nullptr, ff ? dc.film.dgam : nullptr, ff ? dc.film.dbet : nullptr,
                          bn1_tiles ? h->rc_part : nullptr, bn1_tiles);
     }
-    const bool film_side = dc.has_film() && h->side;
-    if (film_side) {   // fork: the MLP backward beside conv1's GEMMs (joined below)
-        HIPCHK(hipEventRecord(h->ev_fork, st));
-        HIPCHK(hipStreamWaitEvent(h->side, h->ev_fork, 0));
-        cad::film_mlp_bwd(film_view(h, dc), h->camn, B, h->side);
-        HIPCHK(hipEventRecord(h->ev_join, h->side));
-    } else if (dc.has_film()) {
-        cad::film_mlp_bwd(film_view(h, dc), h->camn, B, st);
+    // side: the FiLM MLP backward (needs this bn1's dgamma / dbeta: ~1.2 ms/step of small latency-bound
+    // kernels beside the block's GEMMs), then conv1's weight gradient on wgrad_stream's choice
+    if (dc.has_film()) {
+        side_fork(h, st);
+        cad::film_mlp_bwd(film_view(h, dc), h->camn, B, sd);
     }
-    // conv1: wgrad, dgrad
+    hipStream_t wg1 = wgrad_stream(h, ps, st);
     if (ps1)
-        cad::conv3x3_wgrad_ps(sv(dYs, C), C, in_s, dc.c1.cin, h->G(dc.c1.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
+        cad::conv3x3_wgrad_ps(sv(dYs1, C), C, in_s, dc.c1.cin, h->G(dc.c1.pidx), B, Hh, Ww, h->slab, h->slab_cap, wg1);
     else
-        cad::conv3x3_wgrad(dY, C, in, ldin, 0, dc.c1.cin, h->G(dc.c1.pidx), B, Hh, Ww, h->slab, h->slab_cap, st);
+        cad::conv3x3_wgrad(dY1, C, in, ldin, 0, dc.c1.cin, h->G(dc.c1.pidx), B, Hh, Ww, h->slab, h->slab_cap, wg1);
+    HIPCHK(hipEventRecord(h->evB, wg1));
+    // conv1 dgrad
     if (din) {
         // din_hi: the upper half of din's columns goes straight into that bf16 twin (decoder concat)
         if (ps && dc.c1.wds) {
-            const bool done = cad::conv3x3_dgrad_ps(sv(dYs, C), C, sv(dc.c1.wds, 9 * C), dc.c1.cin, din, lddin, B, Hh, Ww,
-                                                    st, din_bf16, din_hi, dc.c1.cin / 2, dc.c1.cin / 2);
+            const bool done = cad::conv3x3_dgrad_ps(sv(dYs1, C), C, sv(dc.c1.wds, 9 * C), dc.c1.cin, din, lddin, B, Hh,
+                                                    Ww, st, din_bf16, din_hi, dc.c1.cin / 2, dc.c1.cin / 2);
             if (din_hi_done) *din_hi_done = done && din_hi;
         } else
-            cad::conv3x3_dgrad(dY, C, dc.c1.wd, dc.c1.cin, din, lddin, B, Hh, Ww, st);
+            cad::conv3x3_dgrad(dY1, C, dc.c1.wd, dc.c1.cin, din, lddin, B, Hh, Ww, st);
     }
-    if (film_side) HIPCHK(hipStreamWaitEvent(st, h->ev_join, 0));   // join: the block's gradients complete on st
 }
 
 void repack_dgrad_weights(cad_unet* h, hipStream_t st) {   // one launch (prep_fwd_weights)
@@ -809,11 +849,19 @@ void repack_dgrad_weights(cad_unet* h, hipStream_t st) {   // one launch (prep_f
 // stages: 0 head, 1..4 dec1..dec4, 5 bottleneck, 6..9 enc4..enc1
 constexpr int kStages = 10;
 
+void backward_stage_body(cad_unet* h, int stage, const float* dpred, hipStream_t st);
 void backward_stage(cad_unet* h, int stage, const float* dpred, hipStream_t st) {
+    backward_stage_body(h, stage, dpred, st);
+    if (!h->defer_join) side_join(h, st);   // the stage's gradients complete on st
+}
+void backward_stage_body(cad_unet* h, int stage, const float* dpred, hipStream_t st) {
     const int B = h->fwd_B;
     const int f = h->f;
     const bool ps = h->fwd_np > 0 && h->fwd_np == cad::split_planes();
     if (stage == 0) {
+        // the buffer-pair events start on this stream (so a captured step never waits on a prior step)
+        HIPCHK(hipEventRecord(h->evA, st));
+        HIPCHK(hipEventRecord(h->evB, st));
         repack_dgrad_weights(h, st);
         if (h->head_fused) {   // head weight / bias gradient from dec1's bn2 input; its input gradient: stage 1
             const DoubleConv& d = h->dec[0];
@@ -850,17 +898,19 @@ void backward_stage(cad_unet* h, int stage, const float* dpred, hipStream_t st) 
             cad::split_rows(h->dcat[l], 2 * C, C, C, h->Ml(l, B), h->dcats[l], C, 0, st);
             cad::split_rows(h->dcat[l], 2 * C, 0, C, h->Ml(l, B), h->dskips[l], C, 0, st);
         }
+        // the ConvT's weight and bias gradients on the side stream (its own column-sum scratch)
+        hipStream_t sd = wgrad_stream(h, ps, st);
         if (ps) {
             cad::convT_wgrad_ps(sv(upins, u.cin), u.cin, sv(h->dcats[l], C), u.cout, h->G(u.widx), B, h->Hl(l + 1),
-                                h->Wl(l + 1), h->slab, h->slab_cap, st);
+                                h->Wl(l + 1), h->slab, h->slab_cap, sd);
         } else {
             cad::convT_wgrad(upin, u.cin, h->dcat[l], 2 * C, C, u.cout, h->G(u.widx), B, h->Hl(l + 1), h->Wl(l + 1),
-                             h->slab, h->slab_cap, st);
+                             h->slab, h->slab_cap, sd);
         }
         // ConvT bias gradient: on the bf16 engine the sum of the (bf16) gradient the ConvT GEMMs read
-        if (ps) cad::colsum_bf16(h->dcats[l], C, 0, h->Ml(l, B), C, h->dscr, st);
-        else cad::colsum(h->dcat[l], 2 * C, C, h->Ml(l, B), C, h->dscr, st);
-        cad::colsum_finalize(h->dscr, cad::colsum_slices(h->Ml(l, B)), C, h->G(u.bidx), 1.f, st);
+        if (ps) cad::colsum_bf16(h->dcats[l], C, 0, h->Ml(l, B), C, h->dscr2, sd);
+        else cad::colsum(h->dcat[l], 2 * C, C, h->Ml(l, B), C, h->dscr2, sd);
+        cad::colsum_finalize(h->dscr2, cad::colsum_slices(h->Ml(l, B)), C, h->G(u.bidx), 1.f, sd);
         if (ps)
             cad::convT_dgrad_ps(sv(h->dcats[l], C), u.cout, sv(u.wms, 4 * u.cout), u.cin, h->Sa, B, h->Hl(l + 1),
                                 h->Wl(l + 1), st, true);
@@ -1068,11 +1118,9 @@ cad_status cad_unet_create_model(const cad_unet_desc* d, int model, int device, 
         require(real.off == sz.off, "internal: arena layout differs between the sizing and the real pass", CAD_ERR_STATE);
         compute_stage_ranges(h.get());
         default_init(h.get());
-        if (model != CAD_MODEL_BASELINE) {
-            HIPCHK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
-            HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
-            HIPCHK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
-        }
+        HIPCHK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+        for (hipEvent_t* e : {&h->ev_fork, &h->evA, &h->evB, &h->ev_tail})
+            HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
         HIPCHK(hipDeviceSynchronize());
         *out = h.release();
     });
@@ -1082,8 +1130,8 @@ void cad_unet_destroy(cad_unet* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
     if (h->side) (void)hipStreamSynchronize(h->side);
-    if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
-    if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+    for (hipEvent_t e : {h->ev_fork, h->evA, h->evB, h->ev_tail})
+        if (e) (void)hipEventDestroy(e);
     if (h->side) (void)hipStreamDestroy(h->side);
     (void)hipFree(h->arena_base);
     delete h;
@@ -1492,7 +1540,16 @@ cad_status cad_unet_backward(cad_unet* h, const float* ddepth, void* stream) {
                 "GEMM engine changed between forward and backward", CAD_ERR_STATE);
         require(ddepth, "null ddepth");
         HIPCHK(hipSetDevice(h->device));
-        for (int s = 0; s < kStages; ++s) backward_stage(h, s, ddepth, S(stream));
+        // one join at the end: the side stream's weight gradients overlap across stages too
+        h->defer_join = true;
+        try {
+            for (int s = 0; s < kStages; ++s) backward_stage(h, s, ddepth, S(stream));
+        } catch (...) {
+            h->defer_join = false;
+            throw;
+        }
+        h->defer_join = false;
+        side_join(h, S(stream));
         HIPCHK(hipGetLastError());
     });
 }
