@@ -329,10 +329,20 @@ def gemm_census(lib, step, dev, steps=1):
     largest total time) whose launches the timed region then brackets, and gives the per-step GEMM
     summary (all_gemm_kernels)."""
     import torch
-    with profiled(lib) as prof:
-        for _ in range(steps):
-            step()
-        torch.cuda.synchronize(dev)
+    # every GEMM alone: the S3 engine's weight gradients otherwise run on a second stream beside the
+    # dgrad chain (cad_api.cpp wgrad_stream), where a launch's duration includes sharing the CUs
+    prev = os.environ.get("CAD_SIDE_WGRAD")
+    os.environ["CAD_SIDE_WGRAD"] = "0"
+    try:
+        with profiled(lib) as prof:
+            for _ in range(steps):
+                step()
+            torch.cuda.synchronize(dev)
+    finally:
+        if prev is None:
+            del os.environ["CAD_SIDE_WGRAD"]
+        else:
+            os.environ["CAD_SIDE_WGRAD"] = prev
     return prof()
 
 
@@ -358,6 +368,7 @@ def roofline_of(prof, steps, ms_per_step, show=False, table="pmc_traffic.json", 
     dom = max(gemm, key=lambda r: r["ms"])
     timed = [r for r in prof if r["name"] == dom["name"] and r["ms"] > 0]
     from_timed = census is None or bool(timed)
+    solo = dom if census is not None else None
     if census is not None and timed:
         dom = timed[0]   # the timed region's own launches of that kernel
     dsteps = steps if from_timed else esteps
@@ -383,6 +394,15 @@ def roofline_of(prof, steps, ms_per_step, show=False, table="pmc_traffic.json", 
             "gflop_per_launch": round(dom["gflop"] / dom["launches"], 3)}
     roof["timed_in"] = ("the timed region (HIP events around this kernel's launches only)" if from_timed
                         else "the census step")
+    if solo is not None and solo is not dom and solo["ms"] > 0:
+        sa = solo["gflop"] / solo["ms"]
+        roof["solo"] = {"achieved": round(sa, 3), "frac": round(sa / peak, 4),
+                        "avg_launch_ms": round(solo["ms"] / solo["launches"], 4),
+                        "from": "the untimed census step, every GEMM launch alone on the step's stream"}
+        if sa > 1.2 * achieved:
+            roof["co_running"] = ("in the timed region this kernel runs on a second stream beside the dgrad "
+                                  "chain (the step is ~2 % faster for it): its launches share the CUs, so "
+                                  "their durations exceed the solo ones; frac above is per launch as timed")
     tot_ms = sum(r["ms"] for r in gemm)
     tot_gf = sum(r["gflop"] for r in gemm)
     roof["all_gemm_kernels"] = {"tflops": round(tot_gf / tot_ms, 3), "ms_per_step": round(tot_ms / esteps, 3),

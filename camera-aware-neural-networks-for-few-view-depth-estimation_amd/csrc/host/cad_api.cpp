@@ -727,9 +727,10 @@ void side_join(cad_unet* h, hipStream_t st) {
 }
 // the stream the weight gradients run on: the side stream on the S3 engine (configs[1] -1.9 %); on the
 // bf16 engine they stay on the step's stream — there the GEMMs beside each other measured neutral to
-// +0.7 % (profiles/r06_lab/README.md).  CAD_SIDE_WGRAD=1 / 0 forces either
+// +0.7 % (profiles/r06_lab/README.md).  CAD_SIDE_WGRAD=1 / 0 forces either; read per call, so bench.py's
+// untimed census step can time every GEMM alone (a kernel beside another one takes longer per launch)
 hipStream_t wgrad_stream(cad_unet* h, bool ps, hipStream_t st) {
-    static const int f = env_flag("CAD_SIDE_WGRAD", -1);
+    const int f = env_flag("CAD_SIDE_WGRAD", -1);
     const bool side = f < 0 ? !ps : f != 0;
     if (!side) return st;
     side_fork(h, st);
